@@ -1,0 +1,112 @@
+/*
+ * hipcycles.h — C ABI of the MI355X (gfx950) Cycles path-tracing device.
+ *
+ * This is the drop-in boundary: a Cycles `Device` subclass (see
+ * integration/device_hip.cpp and INTEGRATION.md) forwards the reference device
+ * plugin calls to these entry points.  Plain pointers, sizes and 64-bit device
+ * handles only.  Every call returns 0 on success and a negative value on error;
+ * the first error is sticky and readable with hipcy_error(), mirroring
+ * Device::set_error / error_message (device/device.h:341-348).
+ *
+ * Reference interface each entry point replaces (blender/intern/cycles/...):
+ *   hipcy_device_count / hipcy_device_info   device/device_cuda.cpp:90 device_cuda_info,
+ *                                            device/device.cpp:475-550 available_devices
+ *   hipcy_create / hipcy_destroy             device/device.cpp:367-418 Device::create,
+ *                                            device/cuda/device_cuda_impl.cpp (CUDADevice ctor/dtor)
+ *   hipcy_error                              device/device.h:341-348 error_message
+ *   hipcy_mem_alloc / _free / _copy_to /
+ *   _copy_from / _zero                       device/device.h:484-488 mem_alloc/mem_copy_to/
+ *                                            mem_copy_from/mem_zero/mem_free
+ *   hipcy_const_copy_to                      device/device.h:366 const_copy_to("__data", ..)
+ *                                            (called from render/scene.cpp:307)
+ *   hipcy_bind_global                        device_cuda_impl.cpp:1088-1096 global_alloc ->
+ *                                            const_copy_to(mem.name, &ptr, 8) for the arrays of
+ *                                            kernel/kernel_textures.h:21-87
+ *   hipcy_load_kernels                       device/device.h:375 load_kernels(DeviceRequestedFeatures)
+ *   hipcy_path_trace                         device_cuda_impl.cpp:1853-1952 CUDADevice::render
+ *                                            (one RenderTile, samples [start, start+num))
+ *   hipcy_synchronize                        device_cuda_impl.cpp:1933 cuCtxSynchronize
+ *   hipcy_get_bvh_layout_mask                device/device.h:353 get_bvh_layout_mask
+ *   hipcy_intersect / hipcy_camera_rays      test entry points (scene_intersect, bvh/bvh.h:154;
+ *                                            kernel_path_trace_setup, kernel_path_common.h:21)
+ */
+#ifndef HIPCYCLES_H
+#define HIPCYCLES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HIPCY_ABI_VERSION 1
+
+typedef struct hipcy_device hipcy_device;
+
+/* RenderTile slice handed to the device (kernel_types.h:1690-1700 WorkTile). */
+typedef struct hipcy_work_tile {
+  int32_t x, y, w, h;
+  int32_t start_sample;
+  int32_t num_samples;
+  int32_t offset;
+  int32_t stride;
+  uint64_t buffer; /* device pointer to w*h*pass_stride floats (render buffer) */
+} hipcy_work_tile;
+
+/* Traversal statistics of the last hipcy_path_trace (for the HBM roofline). */
+typedef struct hipcy_stats {
+  uint64_t closest_rays;
+  uint64_t shadow_rays;
+  uint64_t inner_nodes; /* BVH2 inner nodes visited, both ray kinds */
+  uint64_t leaves;
+  uint64_t triangles;   /* ray-triangle tests */
+  uint64_t iterations;  /* wavefront iterations */
+  double intersect_ms;  /* summed HIP-event time of the traversal kernels */
+  double shade_ms;
+  double total_ms;      /* first launch to last completion of the tile */
+  double closest_ms;    /* closest-hit traversal kernel only */
+  uint64_t closest_launches;
+} hipcy_stats;
+
+int hipcy_abi_version(void);
+int hipcy_device_count(int *count);
+int hipcy_device_info(int ordinal, char *name, size_t name_len, uint64_t *total_mem);
+
+hipcy_device *hipcy_create(int ordinal);
+void hipcy_destroy(hipcy_device *dev);
+const char *hipcy_error(const hipcy_device *dev); /* "" when no error */
+const char *hipcy_global_error(void);             /* errors of hipcy_create */
+
+int hipcy_mem_alloc(hipcy_device *dev, size_t bytes, uint64_t *device_pointer);
+int hipcy_mem_free(hipcy_device *dev, uint64_t device_pointer);
+int hipcy_mem_copy_to(hipcy_device *dev, uint64_t dst, const void *src, size_t bytes);
+int hipcy_mem_copy_from(hipcy_device *dev, void *dst, uint64_t src, size_t bytes);
+int hipcy_mem_zero(hipcy_device *dev, uint64_t device_pointer, size_t bytes);
+
+int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, size_t size);
+int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_pointer, size_t bytes);
+
+/* Validate that the scene uploaded so far only uses features the HIP kernels
+ * implement; returns 0 or a negative code with a readable hipcy_error(). */
+int hipcy_load_kernels(hipcy_device *dev);
+uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *dev); /* BVH_LAYOUT_BVH2 = 1 */
+
+int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
+int hipcy_synchronize(hipcy_device *dev);
+int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
+/* 1: collect traversal counters and per-kernel HIP-event timings. */
+int hipcy_set_profiling(hipcy_device *dev, int enable);
+
+/* rays: n x 8 floats (P.xyz, D.xyz, t, visibility bits) in device memory;
+ * out_f: n x 3 (t, u, v); out_i: n x 4 (hit, prim, object, type).
+ * any_hit != 0 runs the opaque-shadow traversal. */
+int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t out_i, int n, int any_hit);
+/* xys: n x 3 ints (x, y, sample); out: n x 8 floats (P.xyz, D.xyz, t, rng_hash bits). */
+int hipcy_camera_rays(hipcy_device *dev, uint64_t xys, uint64_t out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIPCYCLES_H */

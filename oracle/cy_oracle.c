@@ -1,0 +1,207 @@
+/*
+ * cy_oracle.c — TEST INFRASTRUCTURE ONLY (see cy_oracle.h).  Never linked into
+ * the product.  Each function restates the reference at the cited lines:
+ *   cyo_hash_uint2          util/util_hash.h:28-93
+ *   cyo_cmj_hash_simple     kernel/kernel_jitter.h:122-129
+ *   cyo_path_rng_1d         kernel/kernel_random.h:40-90 (Sobol branch)
+ *   cyo_ray_offset          kernel/bvh/bvh.h:541-586
+ *   cyo_ray_triangle_intersect util/util_math_intersect.h:88-195 (scalar branch)
+ *   cyo_intersect_brute     closest hit = minimum t over all visible triangles,
+ *                           later primitive wins ties (geom_triangle_intersect.h:25-72
+ *                           accepts t <= current); any-hit = first hit.
+ * Compiled with -ffp-contract=off like the reference generic CPU kernel.
+ */
+#include "cy_oracle.h"
+
+#include <math.h>
+#include <string.h>
+
+static float u2f(uint32_t u)
+{
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+static uint32_t f2u(float f)
+{
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+
+#define ROT(x, k) (((x) << (k)) | ((x) >> (32 - (k))))
+
+uint32_t cyo_hash_uint2(uint32_t kx, uint32_t ky)
+{
+  uint32_t a, b, c;
+  a = b = c = 0xdeadbeef + (2 << 2) + 13;
+  b += ky;
+  a += kx;
+  c ^= b; c -= ROT(b, 14);
+  a ^= c; a -= ROT(c, 11);
+  b ^= a; b -= ROT(a, 25);
+  c ^= b; c -= ROT(b, 16);
+  a ^= c; a -= ROT(c, 4);
+  b ^= a; b -= ROT(a, 14);
+  c ^= b; c -= ROT(b, 24);
+  return c;
+}
+
+uint32_t cyo_cmj_hash_simple(uint32_t i, uint32_t p)
+{
+  i = (i ^ 61) ^ p;
+  i += i << 3;
+  i ^= i >> 4;
+  i *= 0x27d4eb2d;
+  return i;
+}
+
+float cyo_path_rng_1d(const uint32_t *lut, uint32_t rng_hash, int sample, int dimension)
+{
+  uint32_t result = 0;
+  uint32_t i = (uint32_t)sample + 64u; /* SOBOL_SKIP */
+  int j = 0;
+  while (i) {
+    int x = __builtin_ffs((int)i);
+    j += x;
+    result ^= lut[32 * dimension + j - 1];
+    i >>= x;
+  }
+  float r = (float)result * (1.0f / (float)0xFFFFFFFF);
+  uint32_t tmp_rng = cyo_cmj_hash_simple((uint32_t)dimension, rng_hash);
+  float shift = (float)tmp_rng * (1.0f / (float)0xFFFFFFFF);
+  return r + shift - floorf(r + shift);
+}
+
+static float offset1(float p, float n)
+{
+  if (fabsf(p) < 1.0f) {
+    return p + n * 1e-5f;
+  }
+  uint32_t ip = f2u(p);
+  ip += ((ip ^ f2u(n)) >> 31) ? (uint32_t)-32 : 32u;
+  return u2f(ip);
+}
+
+void cyo_ray_offset(const float P[3], const float Ng[3], float out[3])
+{
+  for (int k = 0; k < 3; k++) {
+    out[k] = offset1(P[k], Ng[k]);
+  }
+}
+
+static void sub(const float *a, const float *b, float *r)
+{
+  r[0] = a[0] - b[0];
+  r[1] = a[1] - b[1];
+  r[2] = a[2] - b[2];
+}
+static void add(const float *a, const float *b, float *r)
+{
+  r[0] = a[0] + b[0];
+  r[1] = a[1] + b[1];
+  r[2] = a[2] + b[2];
+}
+static void cross(const float *a, const float *b, float *r)
+{
+  r[0] = a[1] * b[2] - a[2] * b[1];
+  r[1] = a[2] * b[0] - a[0] * b[2];
+  r[2] = a[0] * b[1] - a[1] * b[0];
+}
+static float dot(const float *a, const float *b)
+{
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+static float fmin_c(float a, float b)
+{
+  return (a < b) ? a : b;
+}
+static float fmax_c(float a, float b)
+{
+  return (a > b) ? a : b;
+}
+
+int cyo_ray_triangle_intersect(const float P[3], const float D[3], float ray_t,
+                               const float a[3], const float b[3], const float c[3],
+                               float *u, float *v, float *t)
+{
+  float v0[3], v1[3], v2[3], e0[3], e1[3], e2[3], s[3], cr[3];
+  sub(c, P, v0);
+  sub(a, P, v1);
+  sub(b, P, v2);
+  sub(v2, v0, e0);
+  sub(v0, v1, e1);
+  sub(v1, v2, e2);
+  add(v2, v0, s);
+  cross(s, e0, cr);
+  const float U = dot(cr, D);
+  add(v0, v1, s);
+  cross(s, e1, cr);
+  const float V = dot(cr, D);
+  add(v1, v2, s);
+  cross(s, e2, cr);
+  const float W = dot(cr, D);
+  const float minUVW = fmin_c(U, fmin_c(V, W));
+  const float maxUVW = fmax_c(U, fmax_c(V, W));
+  if (minUVW < 0.0f && maxUVW > 0.0f) {
+    return 0;
+  }
+  float Ng1[3], Ng[3];
+  cross(e1, e0, Ng1);
+  add(Ng1, Ng1, Ng);
+  const float den = dot(Ng, D);
+  if (den == 0.0f) {
+    return 0;
+  }
+  const float T = dot(v0, Ng);
+  const uint32_t sign_den = f2u(den) & 0x80000000u;
+  const float sign_T = u2f(f2u(T) ^ sign_den);
+  if ((sign_T < 0.0f) || (sign_T > ray_t * u2f(f2u(den) ^ sign_den))) {
+    return 0;
+  }
+  const float inv_den = 1.0f / den;
+  *u = U * inv_den;
+  *v = V * inv_den;
+  *t = T * inv_den;
+  return 1;
+}
+
+void cyo_intersect_brute(const float *prim_tri_verts, const uint32_t *prim_visibility, int n_prims,
+                         const float *rays, int n, int any_hit, float *out_f, int32_t *out_i)
+{
+  const float ooeps = 8.271806E-25f;
+  for (int r = 0; r < n; r++) {
+    const float *ray = rays + 8 * r;
+    float P[3] = {ray[0], ray[1], ray[2]};
+    float D[3];
+    for (int k = 0; k < 3; k++) {
+      float d = ray[3 + k];
+      D[k] = (fabsf(d) > ooeps) ? d : copysignf(ooeps, d);
+    }
+    const uint32_t vis = f2u(ray[7]) & (any_hit ? ((1u << 7) | (1u << 8)) : 0xFFFFFFFFu);
+    float best_t = ray[6], bu = 0.0f, bv = 0.0f;
+    int best = -1;
+    for (int p = 0; p < n_prims; p++) {
+      const float *tv = prim_tri_verts + 12 * (size_t)p;
+      float u, v, t;
+      if (cyo_ray_triangle_intersect(P, D, best_t, tv, tv + 4, tv + 8, &u, &v, &t)) {
+        if (prim_visibility[p] & vis) {
+          best = p;
+          best_t = t;
+          bu = u;
+          bv = v;
+          if (any_hit) {
+            break;
+          }
+        }
+      }
+    }
+    out_f[3 * r + 0] = best_t;
+    out_f[3 * r + 1] = bu;
+    out_f[3 * r + 2] = bv;
+    out_i[4 * r + 0] = best >= 0;
+    out_i[4 * r + 1] = best;
+    out_i[4 * r + 2] = -1;
+    out_i[4 * r + 3] = best >= 0 ? 1 : 0;
+  }
+}

@@ -1,0 +1,27 @@
+/*
+ * cy_oracle.h — TEST INFRASTRUCTURE ONLY: plain-C restatement of the primitive
+ * operations of the Cycles path-tracing hot path, used as an independent CPU
+ * checker of the HIP device on the GPU box (where the reference tree is absent).
+ * Pinned against the reference CPU kernel (oracle/_ref) and the committed golden
+ * vectors in tests/golden/ (tests/test_oracle.py).
+ */
+#ifndef CY_ORACLE_H
+#define CY_ORACLE_H
+
+#include <stdint.h>
+
+uint32_t cyo_hash_uint2(uint32_t kx, uint32_t ky);
+uint32_t cyo_cmj_hash_simple(uint32_t i, uint32_t p);
+/* lut: 32 * dims uints; returns path_rng_1D(rng_hash, sample, dimension) */
+float cyo_path_rng_1d(const uint32_t *lut, uint32_t rng_hash, int sample, int dimension);
+void cyo_ray_offset(const float P[3], const float Ng[3], float out[3]);
+int cyo_ray_triangle_intersect(const float P[3], const float D[3], float ray_t,
+                               const float a[3], const float b[3], const float c[3],
+                               float *u, float *v, float *t);
+/* Brute-force closest hit over n_prims triangles of prim_tri_verts (3 float4 per
+ * prim, in BVH slot order) with per-prim visibility: independent of any BVH.
+ * rays: n x 8 floats (P, D, t, visibility bits); out_f n x 3, out_i n x 4. */
+void cyo_intersect_brute(const float *prim_tri_verts, const uint32_t *prim_visibility, int n_prims,
+                         const float *rays, int n, int any_hit, float *out_f, int32_t *out_i);
+
+#endif

@@ -1,0 +1,94 @@
+"""In-tree build of the native libraries (no cmake; plain hipcc / g++ / make).
+
+    python -m raytracingproject_amd.build [--no-ref]
+
+Products (git-ignored, but they travel to the GPU box with the snapshot):
+  raytracingproject_amd/libhipcycles.so       HIP device for gfx950
+  raytracingproject_amd/libhipcycles_host.so  host BVH2 builder
+Test infrastructure (oracle/, never imported by the product):
+  oracle/_build/libcy_oracle.so               plain-C restatement
+  oracle/_ref/libcycles_ref.so                reference CPU kernel (only when
+                                              /root/reference is present)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# Parity-critical flags: no contraction, IEEE div/sqrt (see cy_math.h header).
+HIP_FLAGS = [
+    "-O3",
+    "--offload-arch=gfx950",
+    "-ffp-contract=off",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-gpu-rdc",
+    "-fPIC",
+    "-shared",
+    "-std=c++17",
+    "-Wno-unused-result",
+    "-Wno-unused-value",
+]
+
+
+def _run(cmd, **kw):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, **kw)
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _sources(*dirs, exts=(".h", ".hip", ".cpp")):
+    out = []
+    for d in dirs:
+        for root, _, files in os.walk(d):
+            out += [os.path.join(root, f) for f in files if f.endswith(exts)]
+    return out
+
+
+def build_device(force=False):
+    src = os.path.join(HERE, "csrc", "device", "hipcycles.hip")
+    out = os.path.join(HERE, "libhipcycles.so")
+    deps = _sources(os.path.join(HERE, "csrc", "kernel"), os.path.join(HERE, "csrc", "device"),
+                    os.path.join(REPO, "include"))
+    if force or _stale(out, deps):
+        _run([HIPCC, *HIP_FLAGS, "-I" + os.path.join(REPO, "include"), "-o", out, src])
+    return out
+
+
+def build_host(force=False):
+    src = os.path.join(HERE, "csrc", "host", "bvh2_build.cpp")
+    out = os.path.join(HERE, "libhipcycles_host.so")
+    if force or _stale(out, [src]):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", out, src])
+    return out
+
+
+def build_oracle(ref=True):
+    oracle = os.path.join(REPO, "oracle")
+    _run(["make", "-C", oracle, "oracle", "-j4"])
+    if ref and os.path.isdir("/root/reference/blender/intern/cycles"):
+        _run(["make", "-C", oracle, "ref", "-j4"])
+
+
+def build_all(ref=True, force=False):
+    build_host(force)
+    if shutil.which(HIPCC) or os.path.exists(HIPCC):
+        build_device(force)
+    else:
+        raise RuntimeError("hipcc not found: the HIP device library cannot be built")
+    build_oracle(ref)
+
+
+if __name__ == "__main__":
+    build_all(ref="--no-ref" not in sys.argv, force="--force" in sys.argv)

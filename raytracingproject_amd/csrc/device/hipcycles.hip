@@ -1,0 +1,820 @@
+/*
+ * hipcycles.hip — MI355X (gfx950) Cycles path-tracing device: kernels + C ABI.
+ *
+ * Host side mirrors CUDADevice (device/cuda/device_cuda_impl.cpp): memory ops,
+ * const_copy_to("__data"), named-array binding (global_alloc), render of one
+ * RenderTile (CUDADevice::render :1853-1952).  The kernel side is the wavefront
+ * integrator of kernel/cy_integrator.h; see DESIGN.md for the data layout.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hipcycles.h"
+#include "../kernel/cy_integrator.h"
+
+#define CY_BLOCK 256
+
+/* ------------------------------------------------------------------------- */
+/* Kernels                                                                     */
+
+__device__ __forceinline__ void queue_push(int *queue, uint *counter, int slot, bool active)
+{
+  /* wave-aggregated append: one atomic per wave */
+  const unsigned long long mask = __ballot(active);
+  if (mask == 0) {
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  uint base = 0;
+  if (lane == leader) {
+    base = atomicAdd(counter, (uint)__popcll(mask));
+  }
+  base = __shfl(base, leader);
+  if (active) {
+    const unsigned long long lower = mask & ((1ull << lane) - 1ull);
+    queue[base + __popcll(lower)] = slot;
+  }
+}
+
+__device__ __forceinline__ void stats_add(unsigned long long *dst, uint v)
+{
+  /* wave reduce then one atomic */
+  unsigned long long x = v;
+  for (int off = 32; off > 0; off >>= 1) {
+    x += __shfl_xor(x, off);
+  }
+  if ((threadIdx.x & 63) == 0 && x) {
+    atomicAdd(dst, x);
+  }
+}
+
+__global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
+                                                          CyPathBuffers b,
+                                                          CyTile tile,
+                                                          int *queue,
+                                                          uint *counter)
+{
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  bool active = false;
+  if (slot < tile.w * tile.h) {
+    active = slot_regenerate(&kg, &b, &tile, slot, tile.start_sample);
+  }
+  queue_push(queue, counter, slot, active);
+}
+
+template<bool STATS>
+__global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
+                                                                 CyPathBuffers b,
+                                                                 const int *queue,
+                                                                 const uint *counter,
+                                                                 uint *err,
+                                                                 CyStats *stats)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  if (i < (int)*counter) {
+    const int slot = queue[i];
+    const hc_float4 rp = b.ray_P[slot];
+    const hc_float4 rd = b.ray_D[slot];
+    CyRay ray;
+    ray.P = mk3(rp.x, rp.y, rp.z);
+    ray.t = rp.w;
+    ray.D = mk3(rd.x, rd.y, rd.z);
+    const uint flag = b.state0[slot].x;
+    CyPathState s;
+    s.flag = (int)flag;
+    const uint visibility = path_state_ray_visibility(&s);
+    CyIsect isect;
+    bool hit = false;
+    if (scene_intersect_valid(&ray)) {
+      hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err,
+                                  STATS ? &n_nodes : nullptr, &n_leaves, &n_tris);
+    }
+    if (hit) {
+      b.isect[slot] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
+      b.isect_type[slot] = isect.type;
+    }
+    else {
+      b.isect_type[slot] = 0;
+    }
+  }
+  if (STATS) {
+    stats_add(&stats->nodes, n_nodes);
+    stats_add(&stats->leaves, n_leaves);
+    stats_add(&stats->tris, n_tris);
+  }
+}
+
+__global__ void __launch_bounds__(CY_BLOCK) k_shade(CyGlobals kg,
+                                                     CyPathBuffers b,
+                                                     CyTile tile,
+                                                     const int *queue_in,
+                                                     const uint *count_in,
+                                                     int *queue_out,
+                                                     uint *count_out,
+                                                     int *shadow_queue,
+                                                     uint *shadow_count,
+                                                     uint *err)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool cont = false, shadow = false;
+  int slot = 0;
+  if (i < (int)*count_in) {
+    slot = queue_in[i];
+    cont = shade_path(&kg, &b, &tile, slot, &shadow, err);
+  }
+  queue_push(queue_out, count_out, slot, cont);
+  queue_push(shadow_queue, shadow_count, slot, shadow);
+}
+
+template<bool STATS>
+__global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
+                                                                CyPathBuffers b,
+                                                                CyTile tile,
+                                                                const int *shadow_queue,
+                                                                const uint *shadow_count,
+                                                                int *queue_out,
+                                                                uint *count_out,
+                                                                uint *err,
+                                                                CyStats *stats)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool regen = false;
+  int slot = 0;
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  if (i < (int)*shadow_count) {
+    slot = shadow_queue[i];
+    const hc_float4 sp = b.shadow_P[slot];
+    const hc_float4 sdr = b.shadow_D[slot];
+    CyRay ray;
+    ray.P = mk3(sp.x, sp.y, sp.z);
+    ray.t = sp.w;
+    ray.D = mk3(sdr.x, sdr.y, sdr.z);
+    bool blocked = false;
+    if (scene_intersect_valid(&ray)) {
+      CyIsect isect;
+      blocked = bvh2_intersect<true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
+                                     STATS ? &n_nodes : nullptr, &n_leaves, &n_tris);
+    }
+    const hc_float4 sl = b.shadow_L[slot];
+    hc_float4 L4 = b.L[slot];
+    if (!blocked) {
+      L4.x = L4.x + sl.x;
+      L4.y = L4.y + sl.y;
+      L4.z = L4.z + sl.z;
+    }
+    if (sl.w != 0.0f) {
+      const int sample = (int)b.state0[slot].w;
+      const float L_transparent = b.throughput[slot].w;
+      regen = slot_finish(&kg, &b, &tile, slot, sample, mk3(L4.x, L4.y, L4.z), L_transparent);
+    }
+    else {
+      b.L[slot] = L4;
+    }
+  }
+  queue_push(queue_out, count_out, slot, regen);
+  if (STATS) {
+    stats_add(&stats->nodes, n_nodes);
+    stats_add(&stats->leaves, n_leaves);
+    stats_add(&stats->tris, n_tris);
+  }
+}
+
+__global__ void k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) {
+    return;
+  }
+  const float *r = rays + 8 * i;
+  CyRay ray;
+  ray.P = mk3(r[0], r[1], r[2]);
+  ray.D = mk3(r[3], r[4], r[5]);
+  ray.t = r[6];
+  const uint visibility = as_uint(r[7]);
+  CyIsect isect;
+  isect.t = ray.t;
+  isect.u = 0.0f;
+  isect.v = 0.0f;
+  isect.prim = PRIM_NONE;
+  isect.object = OBJECT_NONE;
+  isect.type = 0;
+  bool hit = false;
+  if (scene_intersect_valid(&ray)) {
+    if (any_hit) {
+      hit = bvh2_intersect<true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr);
+    }
+    else {
+      hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr);
+    }
+  }
+  out_f[3 * i + 0] = isect.t;
+  out_f[3 * i + 1] = isect.u;
+  out_f[3 * i + 2] = isect.v;
+  out_i[4 * i + 0] = hit ? 1 : 0;
+  out_i[4 * i + 1] = isect.prim;
+  out_i[4 * i + 2] = isect.object;
+  out_i[4 * i + 3] = isect.type;
+}
+
+__global__ void k_test_camera(CyGlobals kg, const int *xys, float *out, int n)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) {
+    return;
+  }
+  uint rng_hash;
+  CyRay ray;
+  camera_sample_ray(&kg, xys[3 * i + 0], xys[3 * i + 1], xys[3 * i + 2], &rng_hash, &ray);
+  float *o = out + 8 * i;
+  o[0] = ray.P.x;
+  o[1] = ray.P.y;
+  o[2] = ray.P.z;
+  o[3] = ray.D.x;
+  o[4] = ray.D.y;
+  o[5] = ray.D.z;
+  o[6] = ray.t;
+  o[7] = as_float(rng_hash);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Host side                                                                   */
+
+namespace {
+
+std::mutex g_error_mutex;
+std::string g_global_error;
+
+struct GlobalBinding {
+  uint64_t ptr = 0;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct hipcy_device {
+  int ordinal = 0;
+  hipStream_t stream = nullptr;
+  std::string error;
+  hc_KernelData data_host;
+  bool have_data = false;
+  hc_KernelData *data_dev = nullptr;
+  std::map<std::string, GlobalBinding> globals;
+  std::map<uint64_t, size_t> allocations;
+
+  /* wavefront buffers */
+  size_t capacity = 0;
+  char *pool = nullptr;
+  CyPathBuffers bufs;
+  int *queue[3] = {nullptr, nullptr, nullptr};
+  uint *counters = nullptr; /* [0..2] queue counts, [3] error word */
+  CyStats *stats_dev = nullptr;
+  uint *host_counters = nullptr; /* pinned */
+
+  bool profiling = false;
+  hipcy_stats stats;
+  std::vector<hipEvent_t> events;
+};
+
+static int set_error(hipcy_device *dev, const std::string &msg)
+{
+  if (dev) {
+    if (dev->error.empty()) {
+      dev->error = msg;
+      fprintf(stderr, "hipcycles: %s\n", msg.c_str());
+    }
+  }
+  else {
+    std::lock_guard<std::mutex> lock(g_error_mutex);
+    g_global_error = msg;
+  }
+  return -1;
+}
+
+#define HIP_CHECK(dev, call) \
+  do { \
+    hipError_t _e = (call); \
+    if (_e != hipSuccess) { \
+      return set_error((dev), std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } \
+  } while (0)
+
+static bool build_globals(hipcy_device *dev, CyGlobals *kg)
+{
+  memset(kg, 0, sizeof(*kg));
+  kg->data = dev->data_dev;
+#define CY_BIND(type, name) \
+  { \
+    auto it = dev->globals.find(#name); \
+    kg->name = (it != dev->globals.end()) ? (const type *)it->second.ptr : nullptr; \
+  }
+  CY_GLOBAL_ARRAYS(CY_BIND)
+#undef CY_BIND
+  return true;
+}
+
+static int ensure_capacity(hipcy_device *dev, size_t slots)
+{
+  if (slots <= dev->capacity) {
+    return 0;
+  }
+  if (dev->pool) {
+    hipFree(dev->pool);
+    dev->pool = nullptr;
+  }
+  /* 12 float4 records + 1 int per slot + 3 queues */
+  const size_t rec = 16 * slots;
+  const size_t ints = 4 * slots;
+  const size_t total = 12 * rec + ints + 3 * ints + 256;
+  HIP_CHECK(dev, hipMalloc((void **)&dev->pool, total));
+  char *p = dev->pool;
+  auto take = [&](size_t n) {
+    char *r = p;
+    p += (n + 255) & ~(size_t)255;
+    return r;
+  };
+  dev->bufs.ray_P = (hc_float4 *)take(rec);
+  dev->bufs.ray_D = (hc_float4 *)take(rec);
+  dev->bufs.isect = (hc_float4 *)take(rec);
+  dev->bufs.isect_type = (int *)take(ints);
+  dev->bufs.state0 = (hc_uint4 *)take(rec);
+  dev->bufs.state1 = (hc_uint4 *)take(rec);
+  dev->bufs.state2 = (hc_float4 *)take(rec);
+  dev->bufs.throughput = (hc_float4 *)take(rec);
+  dev->bufs.L = (hc_float4 *)take(rec);
+  dev->bufs.shadow_P = (hc_float4 *)take(rec);
+  dev->bufs.shadow_D = (hc_float4 *)take(rec);
+  dev->bufs.shadow_L = (hc_float4 *)take(rec);
+  dev->capacity = slots;
+  /* queues live in their own allocation (3 x slots ints) */
+  for (int q = 0; q < 3; q++) {
+    if (dev->queue[q]) {
+      hipFree(dev->queue[q]);
+    }
+    HIP_CHECK(dev, hipMalloc((void **)&dev->queue[q], ints));
+  }
+  return 0;
+}
+
+extern "C" {
+
+int hipcy_abi_version(void)
+{
+  return HIPCY_ABI_VERSION;
+}
+
+int hipcy_device_count(int *count)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    n = 0;
+  }
+  *count = n;
+  return 0;
+}
+
+int hipcy_device_info(int ordinal, char *name, size_t name_len, uint64_t *total_mem)
+{
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, ordinal) != hipSuccess) {
+    return -1;
+  }
+  if (name && name_len) {
+    snprintf(name, name_len, "%s (%s)", prop.name, prop.gcnArchName);
+  }
+  if (total_mem) {
+    *total_mem = prop.totalGlobalMem;
+  }
+  return 0;
+}
+
+const char *hipcy_global_error(void)
+{
+  std::lock_guard<std::mutex> lock(g_error_mutex);
+  return g_global_error.c_str();
+}
+
+hipcy_device *hipcy_create(int ordinal)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || ordinal < 0 || ordinal >= n) {
+    set_error(nullptr, "no HIP device with ordinal " + std::to_string(ordinal));
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, ordinal) != hipSuccess) {
+    set_error(nullptr, "hipGetDeviceProperties failed");
+    return nullptr;
+  }
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error(nullptr, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+    return nullptr;
+  }
+  hipcy_device *dev = new hipcy_device();
+  dev->ordinal = ordinal;
+  memset(&dev->data_host, 0, sizeof(dev->data_host));
+  memset(&dev->stats, 0, sizeof(dev->stats));
+  if (hipSetDevice(ordinal) != hipSuccess ||
+      hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&dev->data_dev, sizeof(hc_KernelData)) != hipSuccess ||
+      hipMalloc((void **)&dev->counters, 64) != hipSuccess ||
+      hipMalloc((void **)&dev->stats_dev, sizeof(CyStats)) != hipSuccess ||
+      hipHostMalloc((void **)&dev->host_counters, 64, hipHostMallocDefault) != hipSuccess) {
+    set_error(nullptr, "device context creation failed");
+    delete dev;
+    return nullptr;
+  }
+  return dev;
+}
+
+void hipcy_destroy(hipcy_device *dev)
+{
+  if (!dev) {
+    return;
+  }
+  hipSetDevice(dev->ordinal);
+  hipStreamSynchronize(dev->stream);
+  for (auto &a : dev->allocations) {
+    hipFree((void *)a.first);
+  }
+  for (auto e : dev->events) {
+    hipEventDestroy(e);
+  }
+  if (dev->pool) hipFree(dev->pool);
+  for (int q = 0; q < 3; q++) {
+    if (dev->queue[q]) hipFree(dev->queue[q]);
+  }
+  if (dev->counters) hipFree(dev->counters);
+  if (dev->stats_dev) hipFree(dev->stats_dev);
+  if (dev->data_dev) hipFree(dev->data_dev);
+  if (dev->host_counters) hipHostFree(dev->host_counters);
+  if (dev->stream) hipStreamDestroy(dev->stream);
+  delete dev;
+}
+
+const char *hipcy_error(const hipcy_device *dev)
+{
+  return dev ? dev->error.c_str() : hipcy_global_error();
+}
+
+int hipcy_mem_alloc(hipcy_device *dev, size_t bytes, uint64_t *device_pointer)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  void *p = nullptr;
+  HIP_CHECK(dev, hipMalloc(&p, bytes ? bytes : 16));
+  dev->allocations[(uint64_t)p] = bytes;
+  *device_pointer = (uint64_t)p;
+  return 0;
+}
+
+int hipcy_mem_free(hipcy_device *dev, uint64_t device_pointer)
+{
+  auto it = dev->allocations.find(device_pointer);
+  if (it == dev->allocations.end()) {
+    return set_error(dev, "mem_free of unknown pointer");
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  HIP_CHECK(dev, hipFree((void *)device_pointer));
+  dev->allocations.erase(it);
+  for (auto g = dev->globals.begin(); g != dev->globals.end();) {
+    if (g->second.ptr == device_pointer) {
+      g = dev->globals.erase(g);
+    }
+    else {
+      ++g;
+    }
+  }
+  return 0;
+}
+
+int hipcy_mem_copy_to(hipcy_device *dev, uint64_t dst, const void *src, size_t bytes)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipMemcpyAsync((void *)dst, src, bytes, hipMemcpyHostToDevice, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return 0;
+}
+
+int hipcy_mem_copy_from(hipcy_device *dev, void *dst, uint64_t src, size_t bytes)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipMemcpyAsync(dst, (const void *)src, bytes, hipMemcpyDeviceToHost, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return 0;
+}
+
+int hipcy_mem_zero(hipcy_device *dev, uint64_t device_pointer, size_t bytes)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipMemsetAsync((void *)device_pointer, 0, bytes, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return 0;
+}
+
+int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, size_t size)
+{
+  if (strcmp(name, "__data") != 0) {
+    return set_error(dev, std::string("const_copy_to: unknown constant ") + name);
+  }
+  if (size != sizeof(hc_KernelData)) {
+    return set_error(dev, "const_copy_to: KernelData size " + std::to_string(size) +
+                              " != " + std::to_string(sizeof(hc_KernelData)));
+  }
+  memcpy(&dev->data_host, host, size);
+  dev->have_data = true;
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipMemcpyAsync(dev->data_dev, host, size, hipMemcpyHostToDevice, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return 0;
+}
+
+int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_pointer, size_t bytes)
+{
+  static const char *known[] = {
+#define CY_NAME(type, n) #n,
+      CY_GLOBAL_ARRAYS(CY_NAME)
+#undef CY_NAME
+  };
+  bool ok = false;
+  for (const char *k : known) {
+    if (strcmp(k, name) == 0) {
+      ok = true;
+    }
+  }
+  if (!ok) {
+    /* Arrays of features this device rejects (curves, motion, attributes...)
+     * are accepted but must be empty; hipcy_load_kernels checks features. */
+    if (bytes == 0) {
+      return 0;
+    }
+  }
+  GlobalBinding b;
+  b.ptr = device_pointer;
+  b.bytes = bytes;
+  dev->globals[name] = b;
+  return 0;
+}
+
+uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
+{
+  return 1u; /* BVH_LAYOUT_BVH2 (kernel_types.h:1396-1406) */
+}
+
+int hipcy_load_kernels(hipcy_device *dev)
+{
+  if (!dev->have_data) {
+    return set_error(dev, "load_kernels: KernelData not uploaded");
+  }
+  const hc_KernelData &d = dev->data_host;
+  std::string why;
+  if (d.cam.type != 0) why = "only perspective cameras";
+  else if (d.cam.aperturesize > 0.0f) why = "depth of field";
+  else if (d.cam.shuttertime != -1.0f || d.cam.num_motion_steps) why = "motion blur";
+  else if (d.cam.interocular_offset != 0.0f) why = "stereo";
+  else if (d.integrator.sampling_pattern != 0) why = "only the Sobol pattern";
+  else if (d.integrator.branched) why = "branched path tracing";
+  else if (d.integrator.use_volumes) why = "volumes";
+  else if (d.integrator.transparent_shadows) why = "transparent shadows";
+  else if (d.integrator.use_ambient_occlusion) why = "ambient occlusion";
+  else if (d.integrator.use_lamp_mis || d.integrator.num_all_lights) why = "lamps (use mesh lights)";
+  else if (d.integrator.max_closures > CY_MAX_CLOSURE) why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
+  else if (d.bvh.have_motion || d.bvh.have_curves) why = "motion / curves";
+  else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
+  else if (d.film.use_light_pass) why = "light passes";
+  else if (d.film.pass_flag != 2) why = "only the combined pass";
+  else if (d.film.pass_denoising_data || d.film.pass_adaptive_aux_buffer || d.film.pass_sample_count ||
+           d.film.cryptomatte_passes)
+    why = "denoising / adaptive / cryptomatte passes";
+  else if (d.background.use_mis) why = "background MIS";
+  if (!why.empty()) {
+    return set_error(dev, "load_kernels: unsupported scene feature: " + why);
+  }
+  const char *required[] = {"__bvh_nodes", "__bvh_leaf_nodes", "__prim_tri_verts", "__prim_tri_index",
+                            "__prim_visibility", "__prim_index", "__prim_object", "__object_flag",
+                            "__tri_shader", "__tri_vindex", "__svm_nodes", "__shaders",
+                            "__lookup_table", "__sample_pattern_lut"};
+  for (const char *r : required) {
+    if (dev->globals.find(r) == dev->globals.end()) {
+      return set_error(dev, std::string("load_kernels: array not bound: ") + r);
+    }
+  }
+  return 0;
+}
+
+int hipcy_set_profiling(hipcy_device *dev, int enable)
+{
+  dev->profiling = enable != 0;
+  return 0;
+}
+
+int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out)
+{
+  *out = dev->stats;
+  return 0;
+}
+
+int hipcy_synchronize(hipcy_device *dev)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return dev->error.empty() ? 0 : -1;
+}
+
+static hipEvent_t get_event(hipcy_device *dev, size_t i)
+{
+  while (dev->events.size() <= i) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    dev->events.push_back(e);
+  }
+  return dev->events[i];
+}
+
+static int check_device_error(hipcy_device *dev)
+{
+  uint err = dev->host_counters[3];
+  if (err) {
+    const uint code = err >> 24, detail = err & 0xFFFFFF;
+    static const char *names[] = {"none", "unsupported SVM node", "unsupported closure",
+                                  "SVM stack offset beyond HIP stack", "BVH stack overflow",
+                                  "unsupported primitive", "unsupported scene feature"};
+    return set_error(dev, std::string("kernel error: ") + (code < 7 ? names[code] : "?") + " (" +
+                              std::to_string(detail) + ")");
+  }
+  return 0;
+}
+
+int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
+{
+  if (!dev->error.empty()) {
+    return -1;
+  }
+  if (hipcy_load_kernels(dev) != 0) {
+    return -1;
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  const size_t slots = (size_t)t->w * (size_t)t->h;
+  if (slots == 0 || t->num_samples <= 0) {
+    return 0;
+  }
+  if (ensure_capacity(dev, slots) != 0) {
+    return -1;
+  }
+  CyGlobals kg;
+  build_globals(dev, &kg);
+  CyTile tile;
+  tile.x = t->x;
+  tile.y = t->y;
+  tile.w = t->w;
+  tile.h = t->h;
+  tile.start_sample = t->start_sample;
+  tile.end_sample = t->start_sample + t->num_samples;
+  tile.offset = t->offset;
+  tile.stride = t->stride;
+  tile.buffer = (float *)t->buffer;
+  tile.pass_stride = dev->data_host.film.pass_stride;
+
+  memset(&dev->stats, 0, sizeof(dev->stats));
+  const bool prof = dev->profiling;
+  hipStream_t s = dev->stream;
+  uint *err = dev->counters + 3;
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, s));
+  HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, sizeof(CyStats), s));
+
+  size_t ev = 0;
+  hipEvent_t t_begin = get_event(dev, ev++);
+  HIP_CHECK(dev, hipEventRecord(t_begin, s));
+
+  int qa = 0, qb = 1;
+  const int qs = 2;
+  dim3 block(CY_BLOCK);
+  {
+    dim3 grid((unsigned)((slots + CY_BLOCK - 1) / CY_BLOCK));
+    hipLaunchKernelGGL(k_init_slots, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa],
+                       dev->counters + qa);
+  }
+  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipStreamSynchronize(s));
+  uint n_active = dev->host_counters[qa];
+
+  struct EvPair {
+    hipEvent_t a, b, c, d, e;
+  };
+  std::vector<EvPair> pairs;
+  uint64_t iterations = 0;
+  while (n_active > 0) {
+    iterations++;
+    dev->stats.closest_rays += n_active;
+    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qb, 0, 4, s));
+    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qs, 0, 4, s));
+    dim3 grid((n_active + CY_BLOCK - 1) / CY_BLOCK);
+    EvPair p;
+    if (prof) {
+      p.a = get_event(dev, ev++);
+      p.b = get_event(dev, ev++);
+      p.c = get_event(dev, ev++);
+      p.d = get_event(dev, ev++);
+      HIP_CHECK(dev, hipEventRecord(p.a, s));
+      hipLaunchKernelGGL(k_intersect_closest<true>, grid, block, 0, s, kg, dev->bufs,
+                         dev->queue[qa], dev->counters + qa, err, dev->stats_dev);
+      HIP_CHECK(dev, hipEventRecord(p.b, s));
+    }
+    else {
+      hipLaunchKernelGGL(k_intersect_closest<false>, grid, block, 0, s, kg, dev->bufs,
+                         dev->queue[qa], dev->counters + qa, err, dev->stats_dev);
+    }
+    hipLaunchKernelGGL(k_shade, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa],
+                       dev->counters + qa, dev->queue[qb], dev->counters + qb, dev->queue[qs],
+                       dev->counters + qs, err);
+    if (prof) {
+      HIP_CHECK(dev, hipEventRecord(p.c, s));
+      hipLaunchKernelGGL(k_intersect_shadow<true>, grid, block, 0, s, kg, dev->bufs, tile,
+                         dev->queue[qs], dev->counters + qs, dev->queue[qb], dev->counters + qb,
+                         err, dev->stats_dev);
+      HIP_CHECK(dev, hipEventRecord(p.d, s));
+      pairs.push_back(p);
+    }
+    else {
+      hipLaunchKernelGGL(k_intersect_shadow<false>, grid, block, 0, s, kg, dev->bufs, tile,
+                         dev->queue[qs], dev->counters + qs, dev->queue[qb], dev->counters + qb,
+                         err, dev->stats_dev);
+    }
+    HIP_CHECK(dev, hipGetLastError());
+    HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(dev, hipStreamSynchronize(s));
+    dev->stats.shadow_rays += dev->host_counters[qs];
+    n_active = dev->host_counters[qb];
+    if (dev->host_counters[3]) {
+      break;
+    }
+    int tmp = qa;
+    qa = qb;
+    qb = tmp;
+  }
+  hipEvent_t t_end = get_event(dev, ev++);
+  HIP_CHECK(dev, hipEventRecord(t_end, s));
+  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipStreamSynchronize(s));
+  float ms = 0.0f;
+  hipEventElapsedTime(&ms, t_begin, t_end);
+  dev->stats.total_ms = ms;
+  dev->stats.iterations = iterations;
+  if (prof) {
+    double closest = 0.0, shadow = 0.0, shade = 0.0;
+    for (auto &p : pairs) {
+      float a = 0, b = 0, c = 0;
+      hipEventElapsedTime(&a, p.a, p.b);
+      hipEventElapsedTime(&b, p.b, p.c);
+      hipEventElapsedTime(&c, p.c, p.d);
+      closest += a;
+      shade += b;
+      shadow += c;
+    }
+    CyStats st;
+    HIP_CHECK(dev, hipMemcpy(&st, dev->stats_dev, sizeof(st), hipMemcpyDeviceToHost));
+    dev->stats.inner_nodes = st.nodes;
+    dev->stats.leaves = st.leaves;
+    dev->stats.triangles = st.tris;
+    dev->stats.intersect_ms = closest + shadow;
+    dev->stats.closest_ms = closest;
+    dev->stats.shade_ms = shade;
+    dev->stats.closest_launches = pairs.size();
+  }
+  return check_device_error(dev);
+}
+
+int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t out_i, int n, int any_hit)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  CyGlobals kg;
+  build_globals(dev, &kg);
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
+  hipLaunchKernelGGL(k_test_intersect, dim3((n + 255) / 256), dim3(256), 0, dev->stream, kg,
+                     (const float *)rays, (float *)out_f, (int *)out_i, n, any_hit, dev->counters + 3);
+  HIP_CHECK(dev, hipGetLastError());
+  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return check_device_error(dev);
+}
+
+int hipcy_camera_rays(hipcy_device *dev, uint64_t xys, uint64_t out, int n)
+{
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  CyGlobals kg;
+  build_globals(dev, &kg);
+  hipLaunchKernelGGL(k_test_camera, dim3((n + 255) / 256), dim3(256), 0, dev->stream, kg,
+                     (const int *)xys, (float *)out, n);
+  HIP_CHECK(dev, hipGetLastError());
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return 0;
+}
+
+}  // extern "C"

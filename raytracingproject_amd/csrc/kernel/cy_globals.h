@@ -1,0 +1,46 @@
+/*
+ * cy_globals.h — device-side view of the scene the Cycles host uploads.
+ *
+ * CyGlobals is the HIP analogue of the reference's KernelGlobals
+ * (kernel/kernel_globals.h:131-137 for CUDA: one __constant__ pointer per named
+ * array of kernel/kernel_textures.h:21-87 plus the KernelData block).  It is
+ * passed by value as a kernel argument, so every pointer lives in SGPRs and every
+ * KernelData field is a scalar (s_load) read.
+ */
+#ifndef CY_GLOBALS_H
+#define CY_GLOBALS_H
+
+#include "hipcycles_kernel_types.h"
+#include "cy_math.h"
+
+/* Names of the kernel_textures.h arrays the HIP path binds (bind_global). */
+#define CY_GLOBAL_ARRAYS(X) \
+  X(hc_float4, __bvh_nodes) \
+  X(hc_float4, __bvh_leaf_nodes) \
+  X(hc_float4, __prim_tri_verts) \
+  X(uint32_t, __prim_tri_index) \
+  X(uint32_t, __prim_type) \
+  X(uint32_t, __prim_visibility) \
+  X(uint32_t, __prim_index) \
+  X(uint32_t, __prim_object) \
+  X(uint32_t, __object_node) \
+  X(hc_KernelObject, __objects) \
+  X(uint32_t, __object_flag) \
+  X(uint32_t, __tri_shader) \
+  X(hc_float4, __tri_vnormal) \
+  X(hc_uint4, __tri_vindex) \
+  X(hc_KernelLightDistribution, __light_distribution) \
+  X(hc_KernelLight, __lights) \
+  X(hc_uint4, __svm_nodes) \
+  X(hc_KernelShader, __shaders) \
+  X(float, __lookup_table) \
+  X(uint32_t, __sample_pattern_lut)
+
+typedef struct CyGlobals {
+  const hc_KernelData *data;
+#define CY_DECL_PTR(type, name) const type *name;
+  CY_GLOBAL_ARRAYS(CY_DECL_PTR)
+#undef CY_DECL_PTR
+} CyGlobals;
+
+#endif /* CY_GLOBALS_H */

@@ -1,0 +1,571 @@
+/*
+ * cy_integrator.h — the wavefront form of kernel_path_trace (kernel_path.h:509-695).
+ *
+ * The reference runs one camera sample per thread from camera ray to
+ * kernel_write_result.  The HIP device keeps one *slot* per pixel of the tile
+ * resident in HBM and advances all slots one bounce per iteration through three
+ * kernels: intersect_closest (bvh), shade (everything between two traversals),
+ * intersect_shadow (occlusion of the light sample + deferred light accumulation).
+ * A slot finishing sample s immediately regenerates sample s+1 of the same pixel,
+ * so each pixel has exactly one path in flight and its samples are added to the
+ * render buffer in sample order: the buffer is bit-identical to the CPU kernel's
+ * sample-major loop (device_cpu.cpp:906-921) with no float atomics.
+ *
+ * Radiance accumulation order per path is preserved: the deferred light
+ * contribution of bounce k is added after shade(k) and before shade(k+1), exactly
+ * where path_radiance_accum_light runs in kernel_branched_path_surface_connect_light.
+ */
+#ifndef CY_INTEGRATOR_H
+#define CY_INTEGRATOR_H
+
+#include "cy_path.h"
+
+/* Per-slot state, SoA of 16-byte records so every access is one dwordx4. */
+typedef struct CyPathBuffers {
+  hc_float4 *ray_P;      /* P.xyz, ray t */
+  hc_float4 *ray_D;      /* D.xyz, (unused) */
+  hc_float4 *isect;      /* t, u, v, prim (bits) */
+  int *isect_type;       /* primitive type, 0 = miss */
+  hc_uint4 *state0;      /* flag, rng_hash, rng_offset, sample */
+  hc_uint4 *state1;      /* bounce, diffuse_bounce, glossy_bounce, transmission_bounce */
+  hc_float4 *state2;     /* transparent_bounce (bits), min_ray_pdf, ray_pdf, ray_t */
+  hc_float4 *throughput; /* throughput.xyz, L.transparent */
+  hc_float4 *L;          /* L.emission.xyz, (unused) */
+  hc_float4 *shadow_P;   /* shadow ray P.xyz, t */
+  hc_float4 *shadow_D;   /* shadow ray D.xyz, (unused) */
+  hc_float4 *shadow_L;   /* pending light contribution xyz, w: 1 = finish path after */
+} CyPathBuffers;
+
+typedef struct CyTile {
+  int x, y, w, h;
+  int start_sample, end_sample;
+  int offset, stride;
+  float *buffer;
+  int pass_stride;
+} CyTile;
+
+typedef struct CyStats {
+  unsigned long long nodes, leaves, tris, rays;
+} CyStats;
+
+CY_FN hc_float4 mkf4(float x, float y, float z, float w)
+{
+  hc_float4 r;
+  r.x = x;
+  r.y = y;
+  r.z = z;
+  r.w = w;
+  return r;
+}
+
+CY_FN void load_state(const CyPathBuffers *b, int slot, CyPathState *s, const CyGlobals *kg)
+{
+  hc_uint4 s0 = b->state0[slot];
+  hc_uint4 s1 = b->state1[slot];
+  hc_float4 s2 = b->state2[slot];
+  s->flag = (int)s0.x;
+  s->rng_hash = s0.y;
+  s->rng_offset = (int)s0.z;
+  s->sample = (int)s0.w;
+  s->num_samples = KD->integrator.aa_samples;
+  s->bounce = (int)s1.x;
+  s->diffuse_bounce = (int)s1.y;
+  s->glossy_bounce = (int)s1.z;
+  s->transmission_bounce = (int)s1.w;
+  s->transparent_bounce = as_int(s2.x);
+  s->min_ray_pdf = s2.y;
+  s->ray_pdf = s2.z;
+  s->ray_t = s2.w;
+}
+
+CY_FN void store_state(const CyPathBuffers *b, int slot, const CyPathState *s)
+{
+  hc_uint4 s0, s1;
+  s0.x = (uint)s->flag;
+  s0.y = s->rng_hash;
+  s0.z = (uint)s->rng_offset;
+  s0.w = (uint)s->sample;
+  s1.x = (uint)s->bounce;
+  s1.y = (uint)s->diffuse_bounce;
+  s1.z = (uint)s->glossy_bounce;
+  s1.w = (uint)s->transmission_bounce;
+  b->state0[slot] = s0;
+  b->state1[slot] = s1;
+  b->state2[slot] = mkf4(int_as_float(s->transparent_bounce), s->min_ray_pdf, s->ray_pdf, s->ray_t);
+}
+
+/* kernel_path_state.h:19-71 (no volumes, no denoising features). */
+CY_FN void path_state_init(const CyGlobals *kg, CyPathState *s, uint rng_hash, int sample)
+{
+  s->flag = PATH_RAY_CAMERA | PATH_RAY_MIS_SKIP | PATH_RAY_TRANSPARENT_BACKGROUND;
+  s->rng_hash = rng_hash;
+  s->rng_offset = PRNG_BASE_NUM;
+  s->sample = sample;
+  s->num_samples = KD->integrator.aa_samples;
+  s->bounce = 0;
+  s->diffuse_bounce = 0;
+  s->glossy_bounce = 0;
+  s->transmission_bounce = 0;
+  s->transparent_bounce = 0;
+  s->min_ray_pdf = CY_FLT_MAX;
+  s->ray_pdf = 0.0f;
+  s->ray_t = 0.0f;
+}
+
+/* kernel_path_state.h:72-178 */
+CY_FN void path_state_next(const CyGlobals *kg, CyPathState *s, int label)
+{
+  if (label & LABEL_TRANSPARENT) {
+    s->flag |= PATH_RAY_TRANSPARENT;
+    s->transparent_bounce++;
+    if (s->transparent_bounce >= KD->integrator.transparent_max_bounce) {
+      s->flag |= PATH_RAY_TERMINATE_IMMEDIATE;
+    }
+    if (!KD->integrator.transparent_shadows) {
+      s->flag |= PATH_RAY_MIS_SKIP;
+    }
+    s->rng_offset += PRNG_BOUNCE_NUM;
+    return;
+  }
+  s->bounce++;
+  if (s->bounce >= KD->integrator.max_bounce) {
+    s->flag |= PATH_RAY_TERMINATE_AFTER_TRANSPARENT;
+  }
+  s->flag &= ~(PATH_RAY_ALL_VISIBILITY | PATH_RAY_MIS_SKIP);
+  if (label & LABEL_REFLECT) {
+    s->flag |= PATH_RAY_REFLECT;
+    s->flag &= ~PATH_RAY_TRANSPARENT_BACKGROUND;
+    if (label & LABEL_DIFFUSE) {
+      s->diffuse_bounce++;
+      if (s->diffuse_bounce >= KD->integrator.max_diffuse_bounce) {
+        s->flag |= PATH_RAY_TERMINATE_AFTER_TRANSPARENT;
+      }
+    }
+    else {
+      s->glossy_bounce++;
+      if (s->glossy_bounce >= KD->integrator.max_glossy_bounce) {
+        s->flag |= PATH_RAY_TERMINATE_AFTER_TRANSPARENT;
+      }
+    }
+  }
+  else {
+    s->flag |= PATH_RAY_TRANSMIT;
+    if (!(label & LABEL_TRANSMIT_TRANSPARENT)) {
+      s->flag &= ~PATH_RAY_TRANSPARENT_BACKGROUND;
+    }
+    s->transmission_bounce++;
+    if (s->transmission_bounce >= KD->integrator.max_transmission_bounce) {
+      s->flag |= PATH_RAY_TERMINATE_AFTER_TRANSPARENT;
+    }
+  }
+  if (label & LABEL_DIFFUSE) {
+    s->flag |= PATH_RAY_DIFFUSE | PATH_RAY_DIFFUSE_ANCESTOR;
+  }
+  else if (label & LABEL_GLOSSY) {
+    s->flag |= PATH_RAY_GLOSSY;
+  }
+  else {
+    s->flag |= PATH_RAY_GLOSSY | PATH_RAY_SINGULAR | PATH_RAY_MIS_SKIP;
+  }
+  s->rng_offset += PRNG_BOUNCE_NUM;
+}
+
+/* kernel_path_state.h:197-206 */
+CY_FN uint path_state_ray_visibility(const CyPathState *s)
+{
+  uint flag = (uint)s->flag & PATH_RAY_ALL_VISIBILITY;
+  if (flag & PATH_RAY_TRANSMIT) {
+    flag &= ~(PATH_RAY_DIFFUSE | PATH_RAY_GLOSSY);
+  }
+  if (s->flag & PATH_RAY_VOLUME_SCATTER) {
+    flag |= PATH_RAY_DIFFUSE;
+  }
+  return flag;
+}
+
+/* kernel_path_state.h:208-244 */
+CY_FN float path_state_continuation_probability(const CyGlobals *kg,
+                                                const CyPathState *s,
+                                                cfloat3 throughput)
+{
+  if (s->flag & PATH_RAY_TERMINATE_IMMEDIATE) {
+    return 0.0f;
+  }
+  else if (s->flag & PATH_RAY_TRANSPARENT) {
+    if (s->transparent_bounce <= KD->integrator.transparent_min_bounce) {
+      return 1.0f;
+    }
+  }
+  else {
+    if (s->bounce <= KD->integrator.min_bounce) {
+      return 1.0f;
+    }
+  }
+  /* branch_factor is 1.0 outside branched path tracing */
+  return cmin(sqrtf(max3f(fabs3(throughput)) * 1.0f), 1.0f);
+}
+
+CY_FN bool path_state_ao_bounce(const CyGlobals *kg, const CyPathState *s)
+{
+  if (s->bounce <= KD->integrator.ao_bounces) {
+    return false;
+  }
+  int bounce = s->bounce - s->transmission_bounce - (s->glossy_bounce > 0);
+  return (bounce > KD->integrator.ao_bounces);
+}
+
+/* kernel_accumulate.h:276-284 */
+CY_FN cfloat3 path_radiance_clamp(const CyGlobals *kg, cfloat3 L, int bounce)
+{
+  float limit = (bounce > 0) ? KD->integrator.sample_clamp_indirect :
+                               KD->integrator.sample_clamp_direct;
+  float sum = reduce_add3(fabs3(L));
+  if (sum > limit) {
+    L = mul3f(L, limit / sum);
+  }
+  return L;
+}
+
+/* Write the finished sample: kernel_passes.h:338-433 with only the combined pass
+ * (kernel_accumulate.h:622-688, use_light_pass == 0, no shadow catcher). */
+CY_FN void write_result(const CyTile *tile, int x, int y, cfloat3 L_emission, float L_transparent)
+{
+  cfloat3 L_sum = L_emission;
+  float sum = fabsf(L_sum.x) + fabsf(L_sum.y) + fabsf(L_sum.z);
+  if (!isfinite_safe(sum)) {
+    L_sum = mk3(0.0f, 0.0f, 0.0f);
+  }
+  float alpha = 1.0f - L_transparent;
+  float *buf = tile->buffer + (size_t)(tile->offset + x + y * tile->stride) * tile->pass_stride;
+  buf[0] += L_sum.x;
+  buf[1] += L_sum.y;
+  buf[2] += L_sum.z;
+  buf[3] += alpha;
+}
+
+/* Start the next valid sample of the slot; returns false when the slot is done.
+ * A camera ray with t == 0 produces no write (kernel_path.h:660-662). */
+CY_FN bool slot_regenerate(const CyGlobals *kg,
+                           const CyPathBuffers *b,
+                           const CyTile *tile,
+                           int slot,
+                           int sample)
+{
+  int x = tile->x + slot % tile->w;
+  int y = tile->y + slot / tile->w;
+  for (; sample < tile->end_sample; sample++) {
+    uint rng_hash;
+    CyRay ray;
+    camera_sample_ray(kg, x, y, sample, &rng_hash, &ray);
+    if (ray.t == 0.0f) {
+      continue;
+    }
+    CyPathState s;
+    path_state_init(kg, &s, rng_hash, sample);
+    store_state(b, slot, &s);
+    b->ray_P[slot] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
+    b->ray_D[slot] = mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f);
+    b->throughput[slot] = mkf4(1.0f, 1.0f, 1.0f, 0.0f);
+    b->L[slot] = mkf4(0.0f, 0.0f, 0.0f, 0.0f);
+    return true;
+  }
+  return false;
+}
+
+/* Finish the current sample of a slot: write it, regenerate the next one. */
+CY_FN bool slot_finish(const CyGlobals *kg,
+                       const CyPathBuffers *b,
+                       const CyTile *tile,
+                       int slot,
+                       int sample,
+                       cfloat3 L_emission,
+                       float L_transparent)
+{
+  int x = tile->x + slot % tile->w;
+  int y = tile->y + slot / tile->w;
+  write_result(tile, x, y, L_emission, L_transparent);
+  return slot_regenerate(kg, b, tile, slot, sample + 1);
+}
+
+/* ---------------------------------------------------------------------------
+ * Stage 2: shade one path at one bounce.  Returns true when the slot must be
+ * enqueued for the next closest-hit traversal.  *shadow is set when a shadow ray
+ * was emitted (the slot then goes to the shadow queue; if the path ends at this
+ * bounce the shadow stage finishes it).
+ */
+CY_FN bool shade_path(const CyGlobals *kg,
+                      const CyPathBuffers *b,
+                      const CyTile *tile,
+                      int slot,
+                      bool *shadow,
+                      uint *err)
+{
+  *shadow = false;
+  CyPathState state;
+  load_state(b, slot, &state, kg);
+  const hc_float4 rp = b->ray_P[slot];
+  const hc_float4 rd = b->ray_D[slot];
+  CyRay ray;
+  ray.P = mk3(rp.x, rp.y, rp.z);
+  ray.t = rp.w;
+  ray.D = mk3(rd.x, rd.y, rd.z);
+  const hc_float4 tp4 = b->throughput[slot];
+  cfloat3 throughput = mk3(tp4.x, tp4.y, tp4.z);
+  float L_transparent = tp4.w;
+  const hc_float4 L4 = b->L[slot];
+  cfloat3 L = mk3(L4.x, L4.y, L4.z);
+
+  const int type = b->isect_type[slot];
+  const bool hit = type != 0;
+  bool cont = false;      /* path continues with a new ray */
+  bool finish_now = true; /* write result in this stage */
+
+  if (!hit) {
+    /* kernel_path_background (kernel_path.h:115-144) */
+    bool skip = false;
+    if (KD->background.transparent && (state.flag & PATH_RAY_TRANSPARENT_BACKGROUND)) {
+      L_transparent += average3(throughput);
+      if (!(KD->film.light_pass_flag & (1 << 2))) { /* PASSMASK(BACKGROUND) */
+        skip = true;
+      }
+    }
+    if (!skip) {
+      if (path_state_ao_bounce(kg, &state)) {
+        throughput = mul3f(throughput, KD->background.ao_bounces_factor);
+      }
+      /* indirect_background (kernel_emission.h:288-345) */
+      uint shader = (uint)KD->background.surface_shader;
+      bool excluded = false;
+      if (shader & SHADER_EXCLUDE_ANY) {
+        if (((shader & SHADER_EXCLUDE_DIFFUSE) && (state.flag & PATH_RAY_DIFFUSE)) ||
+            ((shader & SHADER_EXCLUDE_GLOSSY) &&
+             ((state.flag & (PATH_RAY_GLOSSY | PATH_RAY_REFLECT)) ==
+              (PATH_RAY_GLOSSY | PATH_RAY_REFLECT))) ||
+            ((shader & SHADER_EXCLUDE_TRANSMIT) && (state.flag & PATH_RAY_TRANSMIT)) ||
+            ((shader & SHADER_EXCLUDE_CAMERA) && (state.flag & PATH_RAY_CAMERA)) ||
+            ((shader & SHADER_EXCLUDE_SCATTER) && (state.flag & PATH_RAY_VOLUME_SCATTER))) {
+          excluded = true;
+        }
+      }
+      cfloat3 L_background = mk3(0.0f, 0.0f, 0.0f);
+      if (!excluded) {
+        if (!shader_constant_emission_eval(kg, (int)shader, &L_background)) {
+          cy_set_error(err, CY_ERR_FEATURE, 3); /* non-constant world shader */
+        }
+        if (!(state.flag & PATH_RAY_MIS_SKIP) && KD->background.use_mis) {
+          cy_set_error(err, CY_ERR_FEATURE, 4); /* background MIS */
+        }
+      }
+      /* path_radiance_accum_background (kernel_accumulate.h:478-520) */
+      cfloat3 contribution = mul3(throughput, L_background);
+      contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
+      L = add3(L, contribution);
+    }
+  }
+  else if (!path_state_ao_bounce(kg, &state)) {
+    CyIsect isect;
+    const hc_float4 is4 = b->isect[slot];
+    isect.t = is4.x;
+    isect.u = is4.y;
+    isect.v = is4.z;
+    isect.prim = as_int(is4.w);
+    isect.object = OBJECT_NONE;
+    isect.type = type;
+
+    CySD sd;
+    shader_setup_from_ray(kg, &sd, &isect, &ray);
+    shader_eval_surface(kg, &sd, state.flag, err);
+    shader_prepare_closures(&sd, &state);
+
+    /* kernel_path_shader_apply (kernel_path.h:254-321) */
+    if ((sd.object_flag & SD_OBJECT_SHADOW_CATCHER) || (sd.flag & SD_HOLDOUT) ||
+        (sd.object_flag & SD_OBJECT_HOLDOUT_MASK)) {
+      cy_set_error(err, CY_ERR_FEATURE, 5);
+    }
+    if ((state.flag & PATH_RAY_CAMERA) && !(state.flag & PATH_RAY_SINGLE_PASS_DONE)) {
+      /* kernel_write_data_passes: no data passes, only the single-pass flag */
+      if (!(sd.flag & SD_TRANSPARENT) || KD->film.pass_alpha_threshold == 0.0f) {
+        state.flag |= PATH_RAY_SINGLE_PASS_DONE;
+      }
+    }
+    if (KD->integrator.filter_glossy != CY_FLT_MAX) {
+      float blur_pdf = KD->integrator.filter_glossy * state.min_ray_pdf;
+      if (blur_pdf < 1.0f) {
+        float blur_roughness = sqrtf(1.0f - blur_pdf) * 0.5f;
+        for (int i = 0; i < sd.num_closure; i++) {
+          CyClosure *sc = &sd.closure[i];
+          if (sc->type == CLOSURE_BSDF_MICROFACET_GGX_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID) {
+            sc->alpha_x = fmaxf(blur_roughness, sc->alpha_x);
+            sc->alpha_y = fmaxf(blur_roughness, sc->alpha_y);
+          }
+        }
+      }
+    }
+    if (sd.flag & SD_EMISSION) {
+      /* indirect_primitive_emission (kernel_emission.h:209-233) */
+      float res = (fabsf(dot3(sd.Ng, sd.I)) > 0.0f) ? 1.0f : 0.0f;
+      cfloat3 emission = mul3(mk3(res, res, res), sd.closure_emission_background);
+      if (!(state.flag & PATH_RAY_MIS_SKIP) && (sd.flag & SD_USE_MIS) &&
+          (sd.type & PRIMITIVE_ALL_TRIANGLE)) {
+        float pdf = triangle_light_pdf(kg, &sd, sd.ray_length);
+        float mis_weight = power_heuristic(state.ray_pdf, pdf);
+        emission = mul3f(emission, mis_weight);
+      }
+      /* path_radiance_accum_emission (kernel_accumulate.h:304-335) */
+      cfloat3 contribution = mul3(throughput, emission);
+      contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
+      L = add3(L, contribution);
+    }
+
+    /* Russian roulette (kernel_path.h:587-599) */
+    float probability = path_state_continuation_probability(kg, &state, throughput);
+    bool terminated = false;
+    if (probability == 0.0f) {
+      terminated = true;
+    }
+    else if (probability != 1.0f) {
+      float terminate = path_state_rng_1D(kg, &state, PRNG_TERMINATE);
+      if (terminate >= probability) {
+        terminated = true;
+      }
+      else {
+        throughput = div3f(throughput, probability);
+      }
+    }
+
+    if (!terminated) {
+      if (KD->integrator.use_ambient_occlusion || (sd.flag & SD_BSSRDF)) {
+        cy_set_error(err, CY_ERR_FEATURE, 6);
+      }
+      /* Direct light: kernel_branched_path_surface_connect_light with one sample
+       * (kernel_path_surface.h:23-140), light_sample + direct_emission
+       * (kernel_emission.h:101-205). */
+      if (KD->integrator.use_direct_light && (sd.flag & SD_BSDF_HAS_EVAL)) {
+        float light_u, light_v;
+        path_state_rng_2D(kg, &state, PRNG_LIGHT_U, &light_u, &light_v);
+        float terminate = (KD->integrator.light_inv_rr_threshold > 0.0f) ?
+                              path_state_rng_1D(kg, &state, PRNG_LIGHT_TERMINATE) :
+                              0.0f;
+        CyLightSample ls;
+        if (light_sample(kg, light_u, light_v, sd.P, &ls, err) && ls.pdf != 0.0f) {
+          cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
+          cfloat3 I = neg3(ls.D);
+          if (shader_constant_emission_eval(kg, ls.shader, &light_eval)) {
+            if ((ls.prim != PRIM_NONE) && dot3(ls.Ng, I) < 0.0f) {
+              ls.Ng = neg3(ls.Ng);
+            }
+          }
+          else {
+            cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
+          }
+          light_eval = mul3f(light_eval, ls.eval_fac);
+          if (!is_zero3(light_eval)) {
+            /* shader_bsdf_eval (kernel_shader.h:606-636) */
+            cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
+            float bpdf;
+            shader_bsdf_multi_eval(&sd, ls.D, &bpdf, -1, &eval, 0.0f, 0.0f);
+            if ((uint)ls.shader & SHADER_USE_MIS) {
+              float weight = power_heuristic(ls.pdf, bpdf);
+              eval = mul3f(eval, weight);
+            }
+            eval = mul3(eval, div3f(light_eval, ls.pdf));
+            if (((uint)ls.shader & SHADER_EXCLUDE_ANY) &&
+                ((uint)ls.shader & SHADER_EXCLUDE_DIFFUSE)) {
+              eval = mk3(0.0f, 0.0f, 0.0f);
+            }
+            bool has_emission = !is_zero3(eval);
+            if (has_emission && KD->integrator.light_inv_rr_threshold > 0.0f) {
+              float lprob = max3f(fabs3(eval)) * KD->integrator.light_inv_rr_threshold;
+              if (lprob < 1.0f) {
+                if (terminate >= lprob) {
+                  has_emission = false;
+                }
+                else {
+                  eval = mul3f(eval, 1.0f / lprob);
+                }
+              }
+            }
+            if (has_emission) {
+              /* path_radiance_accum_light, contribution precomputed */
+              cfloat3 shaded_throughput = mul3(mul3f(throughput, 1.0f), mk3(1.0f, 1.0f, 1.0f));
+              cfloat3 contribution = mul3(shaded_throughput, eval);
+              contribution = path_radiance_clamp(kg, contribution, state.bounce);
+              if ((uint)ls.shader & SHADER_CAST_SHADOW) {
+                bool transmit = (dot3(sd.Ng, ls.D) < 0.0f);
+                cfloat3 sP = ray_offset(sd.P, transmit ? neg3(sd.Ng) : sd.Ng);
+                cfloat3 sD = sub3(ray_offset(ls.P, ls.Ng), sP);
+                float st;
+                sD = normalize_len3(sD, &st);
+                b->shadow_P[slot] = mkf4(sP.x, sP.y, sP.z, st);
+                b->shadow_D[slot] = mkf4(sD.x, sD.y, sD.z, 0.0f);
+                b->shadow_L[slot] = mkf4(contribution.x, contribution.y, contribution.z, 0.0f);
+                *shadow = (st != 0.0f);
+                if (!*shadow) {
+                  L = add3(L, contribution);
+                }
+              }
+              else {
+                L = add3(L, contribution);
+              }
+            }
+          }
+        }
+      }
+
+      /* kernel_path_surface_bounce (kernel_path_surface.h:270-358) */
+      if (sd.flag & SD_BSDF) {
+        float bsdf_u, bsdf_v;
+        path_state_rng_2D(kg, &state, PRNG_BSDF_U, &bsdf_u, &bsdf_v);
+        cfloat3 bsdf_eval_v = mk3(0.0f, 0.0f, 0.0f);
+        cfloat3 omega_in = mk3(0.0f, 0.0f, 0.0f);
+        float bsdf_pdf = 0.0f;
+        int label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err);
+        if (!(bsdf_pdf == 0.0f || is_zero3(bsdf_eval_v))) {
+          float inverse_pdf = 1.0f / bsdf_pdf;
+          throughput = mul3(throughput, mul3f(bsdf_eval_v, inverse_pdf));
+          if (!(label & LABEL_TRANSPARENT)) {
+            state.ray_pdf = bsdf_pdf;
+            state.ray_t = 0.0f;
+            state.min_ray_pdf = fminf(bsdf_pdf, state.min_ray_pdf);
+          }
+          path_state_next(kg, &state, label);
+          ray.P = ray_offset(sd.P, (label & LABEL_TRANSMIT) ? neg3(sd.Ng) : sd.Ng);
+          ray.D = normalize3(omega_in);
+          if (state.bounce == 0) {
+            ray.t -= sd.ray_length;
+          }
+          else {
+            ray.t = CY_FLT_MAX;
+          }
+          cont = true;
+        }
+      }
+    }
+  }
+
+  if (cont) {
+    finish_now = false;
+    store_state(b, slot, &state);
+    b->ray_P[slot] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
+    b->ray_D[slot] = mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f);
+    b->throughput[slot] = mkf4(throughput.x, throughput.y, throughput.z, L_transparent);
+    b->L[slot] = mkf4(L.x, L.y, L.z, 0.0f);
+    return true;
+  }
+  if (*shadow) {
+    /* the path ends after its pending light contribution: the shadow stage
+     * adds it, writes the sample and regenerates the slot */
+    b->throughput[slot] = mkf4(throughput.x, throughput.y, throughput.z, L_transparent);
+    b->L[slot] = mkf4(L.x, L.y, L.z, 0.0f);
+    hc_float4 sl = b->shadow_L[slot];
+    sl.w = 1.0f;
+    b->shadow_L[slot] = sl;
+    store_state(b, slot, &state);
+    return false;
+  }
+  (void)finish_now;
+  return slot_finish(kg, b, tile, slot, state.sample, L, L_transparent);
+}
+
+#endif /* CY_INTEGRATOR_H */

@@ -1,0 +1,442 @@
+/*
+ * cy_math.h — scalar float math of the path-tracing hot path, restated for gfx950.
+ *
+ * Every operation keeps the exact operand order and rounding steps of the
+ * reference's *scalar* (non-SSE) code path, which is what the reference CPU
+ * kernel compiles on x86-64 without __KERNEL_SSE__ and what CUDA compiles:
+ *   util/util_math.h            min/max/clamp/saturate/safe_sqrtf/make_orthonormals (112-130, 283-318, 477-499, 586)
+ *   util/util_math_float3.h     float3 operators, dot, cross, normalize, len (90-480)
+ *   util/util_math_float4.h:243 dot(float4) = (x*x + y*y) + (z*z + w*w)
+ *   util/util_math_fast.h       madd, fast_rint, fast_sinf/cosf/sincosf, fast_acosf (50-293)
+ *   util/util_transform.h:56-110, util/util_projection.h:48-55 transforms
+ *   util/util_hash.h:28-93      rot / final / hash_uint2
+ *   kernel/kernel_jitter.h:106-129 cmj_hash / cmj_hash_simple
+ * The HIP build uses -ffp-contract=off and correctly rounded f32 div/sqrt so that
+ * every value is bit-identical to the reference CPU kernel.  Transcendentals that
+ * the reference takes from libm (sinf/cosf in to_unit_disk, kernel_montecarlo.h:39-46)
+ * are evaluated in double and rounded once (cy_sinf/cy_cosf): glibc's sinf/cosf are
+ * correctly rounded on all but rare inputs, so this matches them except at those.
+ */
+#ifndef CY_MATH_H
+#define CY_MATH_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP_DEVICE_COMPILE__)
+#  include <hip/hip_runtime.h>
+#  define CY_FN __device__ __forceinline__
+#  define CY_CONST __constant__
+#else
+#  include <math.h>
+#  include <string.h>
+#  define CY_FN static inline
+#  define CY_CONST static const
+#endif
+
+#define CY_PI_F 3.14159265358979323846f
+#define CY_PI_2_F 1.57079632679489661923f
+#define CY_2PI_F 6.2831853071795864f
+#define CY_1_PI_F 0.318309886183790671538f
+#define CY_FLT_MAX 3.402823466e+38f
+
+typedef unsigned int uint;
+
+struct float3c {
+  float x, y, z;
+};
+typedef struct float3c cfloat3;
+
+CY_FN cfloat3 mk3(float x, float y, float z)
+{
+  cfloat3 r;
+  r.x = x;
+  r.y = y;
+  r.z = z;
+  return r;
+}
+
+CY_FN float as_float(uint i)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __uint_as_float(i);
+#else
+  float f;
+  memcpy(&f, &i, 4);
+  return f;
+#endif
+}
+CY_FN uint as_uint(float f)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __float_as_uint(f);
+#else
+  uint i;
+  memcpy(&i, &f, 4);
+  return i;
+#endif
+}
+CY_FN int as_int(float f)
+{
+  return (int)as_uint(f);
+}
+CY_FN float int_as_float(int i)
+{
+  return as_float((uint)i);
+}
+
+/* util_math.h:112-130 (ternary forms: NaN handling matches the reference). */
+CY_FN float cmin(float a, float b)
+{
+  return (a < b) ? a : b;
+}
+CY_FN float cmax(float a, float b)
+{
+  return (a > b) ? a : b;
+}
+CY_FN int imin(int a, int b)
+{
+  return (a < b) ? a : b;
+}
+CY_FN int imax(int a, int b)
+{
+  return (a > b) ? a : b;
+}
+CY_FN float cclamp(float a, float mn, float mx)
+{
+  return cmin(cmax(a, mn), mx);
+}
+CY_FN int iclamp(int a, int mn, int mx)
+{
+  return imin(imax(a, mn), mx);
+}
+CY_FN float saturate(float a)
+{
+  return cclamp(a, 0.0f, 1.0f);
+}
+CY_FN float min4(float a, float b, float c, float d)
+{
+  return cmin(cmin(a, b), cmin(c, d));
+}
+CY_FN float max4(float a, float b, float c, float d)
+{
+  return cmax(cmax(a, b), cmax(c, d));
+}
+CY_FN float sqr(float a)
+{
+  return a * a;
+}
+CY_FN float safe_sqrtf(float f)
+{
+  return sqrtf(cmax(f, 0.0f));
+}
+CY_FN float xor_signmask(float x, int y)
+{
+  return int_as_float(as_int(x) ^ y);
+}
+CY_FN float power_heuristic(float a, float b)
+{
+  return (a * a) / (a * a + b * b);
+}
+
+/* float3 operators (util_math_float3.h, scalar branch). */
+CY_FN cfloat3 neg3(cfloat3 a)
+{
+  return mk3(-a.x, -a.y, -a.z);
+}
+CY_FN cfloat3 add3(cfloat3 a, cfloat3 b)
+{
+  return mk3(a.x + b.x, a.y + b.y, a.z + b.z);
+}
+CY_FN cfloat3 sub3(cfloat3 a, cfloat3 b)
+{
+  return mk3(a.x - b.x, a.y - b.y, a.z - b.z);
+}
+CY_FN cfloat3 mul3(cfloat3 a, cfloat3 b)
+{
+  return mk3(a.x * b.x, a.y * b.y, a.z * b.z);
+}
+/* float3 * float and float * float3 both compute a.x * f (operand order kept). */
+CY_FN cfloat3 mul3f(cfloat3 a, float f)
+{
+  return mk3(a.x * f, a.y * f, a.z * f);
+}
+CY_FN cfloat3 div3(cfloat3 a, cfloat3 b)
+{
+  return mk3(a.x / b.x, a.y / b.y, a.z / b.z);
+}
+/* operator/(float3, float): multiplies by the reciprocal. */
+CY_FN cfloat3 div3f(cfloat3 a, float f)
+{
+  float invf = 1.0f / f;
+  return mul3f(a, invf);
+}
+CY_FN float dot3(cfloat3 a, cfloat3 b)
+{
+  return a.x * b.x + a.y * b.y + a.z * b.z;
+}
+CY_FN cfloat3 cross3(cfloat3 a, cfloat3 b)
+{
+  return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+CY_FN float len3(cfloat3 a)
+{
+  return sqrtf(dot3(a, a));
+}
+CY_FN float len_squared3(cfloat3 a)
+{
+  return dot3(a, a);
+}
+CY_FN cfloat3 normalize3(cfloat3 a)
+{
+  return div3f(a, len3(a));
+}
+CY_FN cfloat3 normalize_len3(cfloat3 a, float *t)
+{
+  *t = len3(a);
+  float x = 1.0f / *t;
+  return mul3f(a, x);
+}
+CY_FN cfloat3 safe_normalize3(cfloat3 a)
+{
+  float t = len3(a);
+  return (t != 0.0f) ? mul3f(a, 1.0f / t) : a;
+}
+CY_FN cfloat3 safe_normalize_len3(cfloat3 a, float *t)
+{
+  *t = len3(a);
+  return (*t != 0.0f) ? div3f(a, *t) : a;
+}
+CY_FN cfloat3 fabs3(cfloat3 a)
+{
+  return mk3(fabsf(a.x), fabsf(a.y), fabsf(a.z));
+}
+CY_FN cfloat3 rcp3(cfloat3 a)
+{
+  return mk3(1.0f / a.x, 1.0f / a.y, 1.0f / a.z);
+}
+CY_FN float reduce_add3(cfloat3 a)
+{
+  return (a.x + a.y + a.z);
+}
+CY_FN float average3(cfloat3 a)
+{
+  return reduce_add3(a) * (1.0f / 3.0f);
+}
+CY_FN float max3f(cfloat3 a)
+{
+  return cmax(cmax(a.x, a.y), a.z);
+}
+CY_FN bool is_zero3(cfloat3 a)
+{
+  return (a.x == 0.0f && a.y == 0.0f && a.z == 0.0f);
+}
+CY_FN bool isequal3(cfloat3 a, cfloat3 b)
+{
+  return (a.x == b.x && a.y == b.y && a.z == b.z);
+}
+CY_FN bool isfinite_safe(float f)
+{
+  /* util_math.h:isfinite_safe — exponent bits test, immune to fast-math. */
+  uint x = as_uint(f);
+  return (f == f) && (x == 0 || x == (1u << 31) || (f != 2.0f * f)) && !((x << 1) > 0xff000000u);
+}
+
+/* util_math.h:477-499 */
+CY_FN void make_orthonormals(cfloat3 N, cfloat3 *a, cfloat3 *b)
+{
+  if (N.x != N.y || N.x != N.z) {
+    *a = mk3(N.z - N.y, N.x - N.z, N.y - N.x);
+  }
+  else {
+    *a = mk3(N.z - N.y, N.x + N.z, -N.y - N.x);
+  }
+  *a = normalize3(*a);
+  *b = cross3(N, *a);
+}
+
+/* util_math_fast.h */
+CY_FN float madd(float a, float b, float c)
+{
+  return a * b + c;
+}
+CY_FN int fast_rint(float x)
+{
+  return (int)(x + copysignf(0.5f, x));
+}
+CY_FN float fast_sinf(float x)
+{
+  int q = fast_rint(x * CY_1_PI_F);
+  float qf = (float)q;
+  x = madd(qf, -0.78515625f * 4, x);
+  x = madd(qf, -0.00024187564849853515625f * 4, x);
+  x = madd(qf, -3.7747668102383613586e-08f * 4, x);
+  x = madd(qf, -1.2816720341285448015e-12f * 4, x);
+  x = CY_PI_2_F - (CY_PI_2_F - x);
+  float s = x * x;
+  if ((q & 1) != 0) {
+    x = -x;
+  }
+  float u = 2.6083159809786593541503e-06f;
+  u = madd(u, s, -0.0001981069071916863322258f);
+  u = madd(u, s, +0.00833307858556509017944336f);
+  u = madd(u, s, -0.166666597127914428710938f);
+  u = madd(s, u * x, x);
+  if (fabsf(u) > 1.0f) {
+    u = 0.0f;
+  }
+  return u;
+}
+CY_FN void fast_sincosf(float x, float *sine, float *cosine)
+{
+  int q = fast_rint(x * CY_1_PI_F);
+  float qf = (float)q;
+  x = madd(qf, -0.78515625f * 4, x);
+  x = madd(qf, -0.00024187564849853515625f * 4, x);
+  x = madd(qf, -3.7747668102383613586e-08f * 4, x);
+  x = madd(qf, -1.2816720341285448015e-12f * 4, x);
+  x = CY_PI_2_F - (CY_PI_2_F - x);
+  float s = x * x;
+  if ((q & 1) != 0) {
+    x = -x;
+  }
+  float su = 2.6083159809786593541503e-06f;
+  su = madd(su, s, -0.0001981069071916863322258f);
+  su = madd(su, s, +0.00833307858556509017944336f);
+  su = madd(su, s, -0.166666597127914428710938f);
+  su = madd(s, su * x, x);
+  float cu = -2.71811842367242206819355e-07f;
+  cu = madd(cu, s, +2.47990446951007470488548e-05f);
+  cu = madd(cu, s, -0.00138888787478208541870117f);
+  cu = madd(cu, s, +0.0416666641831398010253906f);
+  cu = madd(cu, s, -0.5f);
+  cu = madd(cu, s, +1.0f);
+  if ((q & 1) != 0) {
+    cu = -cu;
+  }
+  if (fabsf(su) > 1.0f) {
+    su = 0.0f;
+  }
+  if (fabsf(cu) > 1.0f) {
+    cu = 0.0f;
+  }
+  *sine = su;
+  *cosine = cu;
+}
+CY_FN float fast_acosf(float x)
+{
+  const float f = fabsf(x);
+  const float m = (f < 1.0f) ? 1.0f - (1.0f - f) : 1.0f;
+  const float a = sqrtf(1.0f - m) *
+                  (1.5707963267f + m * (-0.213300989f + m * (0.077980478f + m * -0.02164095f)));
+  return x < 0 ? CY_PI_F - a : a;
+}
+
+/* libm sinf/cosf as the reference CPU kernel calls them (glibc): correctly rounded
+ * double evaluation. */
+CY_FN float cy_sinf(float x)
+{
+  return (float)sin((double)x);
+}
+CY_FN float cy_cosf(float x)
+{
+  return (float)cos((double)x);
+}
+
+/* Transform = 3 rows of float4, ProjectionTransform = 4 rows. */
+struct cy_f4 {
+  float x, y, z, w;
+};
+struct cy_tfm {
+  struct cy_f4 x, y, z;
+};
+struct cy_ptfm {
+  struct cy_f4 x, y, z, w;
+};
+
+CY_FN cfloat3 transform_point(const struct cy_tfm *t, cfloat3 a)
+{
+  return mk3(a.x * t->x.x + a.y * t->x.y + a.z * t->x.z + t->x.w,
+             a.x * t->y.x + a.y * t->y.y + a.z * t->y.z + t->y.w,
+             a.x * t->z.x + a.y * t->z.y + a.z * t->z.z + t->z.w);
+}
+CY_FN cfloat3 transform_direction(const struct cy_tfm *t, cfloat3 a)
+{
+  return mk3(a.x * t->x.x + a.y * t->x.y + a.z * t->x.z,
+             a.x * t->y.x + a.y * t->y.y + a.z * t->y.z,
+             a.x * t->z.x + a.y * t->z.y + a.z * t->z.z);
+}
+CY_FN float dot4(struct cy_f4 a, struct cy_f4 b)
+{
+  return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);
+}
+CY_FN cfloat3 transform_perspective(const struct cy_ptfm *t, cfloat3 a)
+{
+  struct cy_f4 b;
+  b.x = a.x;
+  b.y = a.y;
+  b.z = a.z;
+  b.w = 1.0f;
+  cfloat3 c = mk3(dot4(t->x, b), dot4(t->y, b), dot4(t->z, b));
+  float w = dot4(t->w, b);
+  return (w != 0.0f) ? div3f(c, w) : mk3(0.0f, 0.0f, 0.0f);
+}
+
+/* util_hash.h */
+#define CY_ROT(x, k) (((x) << (k)) | ((x) >> (32 - (k))))
+CY_FN uint hash_uint2(uint kx, uint ky)
+{
+  uint a, b, c;
+  a = b = c = 0xdeadbeef + (2 << 2) + 13;
+  b += ky;
+  a += kx;
+  c ^= b;
+  c -= CY_ROT(b, 14);
+  a ^= c;
+  a -= CY_ROT(c, 11);
+  b ^= a;
+  b -= CY_ROT(a, 25);
+  c ^= b;
+  c -= CY_ROT(b, 16);
+  a ^= c;
+  a -= CY_ROT(c, 4);
+  b ^= a;
+  b -= CY_ROT(a, 14);
+  c ^= b;
+  c -= CY_ROT(b, 24);
+  return c;
+}
+
+/* kernel_jitter.h:106-129 */
+CY_FN uint cmj_hash(uint i, uint p)
+{
+  i ^= p;
+  i ^= i >> 17;
+  i ^= i >> 10;
+  i *= 0xb36534e5;
+  i ^= i >> 12;
+  i ^= i >> 21;
+  i *= 0x93fc4795;
+  i ^= 0xdf6e307f;
+  i ^= i >> 17;
+  i *= 1 | p >> 18;
+  return i;
+}
+CY_FN uint cmj_hash_simple(uint i, uint p)
+{
+  i = (i ^ 61) ^ p;
+  i += i << 3;
+  i ^= i >> 4;
+  i *= 0x27d4eb2d;
+  return i;
+}
+
+CY_FN uint find_first_set(uint x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint)__ffs(x);
+#else
+  return (uint)__builtin_ffs((int)x);
+#endif
+}
+
+#endif /* CY_MATH_H */

@@ -1,0 +1,1586 @@
+/*
+ * cy_path.h — device functions of the Cycles path-tracing hot path for gfx950.
+ *
+ * A restatement (not a translation) of the reference megakernel's per-sample
+ * logic, regrouped into the three wavefront stages the HIP device runs
+ * (intersect_closest -> shade -> intersect_shadow).  The per-sample arithmetic is
+ * kept operation-for-operation identical to the reference scalar code so that the
+ * render buffer matches the reference CPU kernel; each function cites the
+ * reference it follows.
+ */
+#ifndef CY_PATH_H
+#define CY_PATH_H
+
+#include "cy_globals.h"
+#include "cy_types.h"
+
+#define KD (kg->data)
+
+CY_FN cfloat3 f4to3(hc_float4 a)
+{
+  return mk3(a.x, a.y, a.z);
+}
+
+CY_FN void cy_set_error(uint *err, uint code, uint detail)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (err) {
+    atomicCAS(err, 0u, (code << 24) | (detail & 0xFFFFFFu));
+  }
+#else
+  (void)err;
+  (void)code;
+  (void)detail;
+#endif
+}
+
+/* ---------------------------------------------------------------------------
+ * Random numbers: kernel_random.h:40-153 (Sobol + Cranley-Patterson rotation).
+ */
+CY_FN uint sobol_dimension(const CyGlobals *kg, int index, int dimension)
+{
+  uint result = 0;
+  uint i = (uint)index + SOBOL_SKIP;
+  for (int j = 0, x; (x = (int)find_first_set(i)); i >>= x) {
+    j += x;
+    result ^= kg->__sample_pattern_lut[32 * dimension + j - 1];
+  }
+  return result;
+}
+
+CY_FN float path_rng_1D(const CyGlobals *kg, uint rng_hash, int sample, int dimension)
+{
+  uint result = sobol_dimension(kg, sample, dimension);
+  float r = (float)result * (1.0f / (float)0xFFFFFFFF);
+  uint tmp_rng = cmj_hash_simple((uint)dimension, rng_hash);
+  float shift = (float)tmp_rng * (1.0f / (float)0xFFFFFFFF);
+  return r + shift - floorf(r + shift);
+}
+
+CY_FN void path_rng_2D(
+    const CyGlobals *kg, uint rng_hash, int sample, int dimension, float *fx, float *fy)
+{
+  *fx = path_rng_1D(kg, rng_hash, sample, dimension);
+  *fy = path_rng_1D(kg, rng_hash, sample, dimension + 1);
+}
+
+CY_FN float path_state_rng_1D(const CyGlobals *kg, const CyPathState *s, int dimension)
+{
+  return path_rng_1D(kg, s->rng_hash, s->sample, s->rng_offset + dimension);
+}
+
+CY_FN void path_state_rng_2D(
+    const CyGlobals *kg, const CyPathState *s, int dimension, float *fx, float *fy)
+{
+  path_rng_2D(kg, s->rng_hash, s->sample, s->rng_offset + dimension, fx, fy);
+}
+
+/* kernel_globals.h:213-227 */
+CY_FN float lookup_table_read(const CyGlobals *kg, float x, int offset, int size)
+{
+  x = saturate(x) * (size - 1);
+  int index = imin((int)x, size - 1);
+  int nindex = imin(index + 1, size - 1);
+  float t = x - index;
+  float data0 = kg->__lookup_table[index + offset];
+  if (t == 0.0f) {
+    return data0;
+  }
+  float data1 = kg->__lookup_table[nindex + offset];
+  return (1.0f - t) * data0 + t * data1;
+}
+
+/* ---------------------------------------------------------------------------
+ * Camera: kernel_path_common.h:21-46 + kernel_camera.h:42-171 (perspective,
+ * no DOF, no motion, no stereo — rejected at load otherwise).
+ */
+CY_FN void camera_sample_ray(
+    const CyGlobals *kg, int x, int y, int sample, uint *rng_hash_out, CyRay *ray)
+{
+  uint rng_hash = hash_uint2((uint)x, (uint)y);
+  rng_hash ^= (uint)KD->integrator.seed;
+  float filter_u, filter_v;
+  if (sample == 0) {
+    filter_u = 0.5f;
+    filter_v = 0.5f;
+  }
+  else {
+    path_rng_2D(kg, rng_hash, sample, PRNG_FILTER_U, &filter_u, &filter_v);
+  }
+  *rng_hash_out = rng_hash;
+
+  int filter_table_offset = KD->film.filter_table_offset;
+  float raster_x = x + lookup_table_read(kg, filter_u, filter_table_offset, FILTER_TABLE_SIZE);
+  float raster_y = y + lookup_table_read(kg, filter_v, filter_table_offset, FILTER_TABLE_SIZE);
+
+  const struct cy_ptfm *rastertocamera = (const struct cy_ptfm *)&KD->cam.rastertocamera;
+  cfloat3 Pcamera = transform_perspective(rastertocamera, mk3(raster_x, raster_y, 0.0f));
+  cfloat3 P = mk3(0.0f, 0.0f, 0.0f);
+  cfloat3 D = Pcamera;
+  const struct cy_tfm *cameratoworld = (const struct cy_tfm *)&KD->cam.cameratoworld;
+  P = transform_point(cameratoworld, P);
+  D = normalize3(transform_direction(cameratoworld, D));
+  ray->P = P;
+  ray->D = D;
+  /* camera clipping (__CAMERA_CLIPPING__) */
+  float z_inv = 1.0f / normalize3(Pcamera).z;
+  float nearclip = KD->cam.nearclip * z_inv;
+  ray->P = add3(ray->P, mul3f(ray->D, nearclip));
+  ray->t = KD->cam.cliplength * z_inv;
+}
+
+/* ---------------------------------------------------------------------------
+ * BVH2 traversal over the packed Cycles layout (bvh/bvh_traversal.h:34-227,
+ * bvh_nodes.h:31-77, geom_triangle_intersect.h:25-72, util_math_intersect.h:88-195).
+ * Single-level BVH with transforms applied (instancing rejected at load).
+ */
+CY_FN cfloat3 bvh_clamp_direction(cfloat3 dir)
+{
+  const float ooeps = 8.271806E-25f;
+  return mk3((fabsf(dir.x) > ooeps) ? dir.x : copysignf(ooeps, dir.x),
+             (fabsf(dir.y) > ooeps) ? dir.y : copysignf(ooeps, dir.y),
+             (fabsf(dir.z) > ooeps) ? dir.z : copysignf(ooeps, dir.z));
+}
+
+CY_FN bool ray_triangle_intersect(cfloat3 P,
+                                  cfloat3 dir,
+                                  float ray_t,
+                                  cfloat3 tri_a,
+                                  cfloat3 tri_b,
+                                  cfloat3 tri_c,
+                                  float *isect_u,
+                                  float *isect_v,
+                                  float *isect_t)
+{
+  const cfloat3 v0 = sub3(tri_c, P);
+  const cfloat3 v1 = sub3(tri_a, P);
+  const cfloat3 v2 = sub3(tri_b, P);
+  const cfloat3 e0 = sub3(v2, v0);
+  const cfloat3 e1 = sub3(v0, v1);
+  const cfloat3 e2 = sub3(v1, v2);
+  const float U = dot3(cross3(add3(v2, v0), e0), dir);
+  const float V = dot3(cross3(add3(v0, v1), e1), dir);
+  const float W = dot3(cross3(add3(v1, v2), e2), dir);
+  const float minUVW = cmin(U, cmin(V, W));
+  const float maxUVW = cmax(U, cmax(V, W));
+  if (minUVW < 0.0f && maxUVW > 0.0f) {
+    return false;
+  }
+  const cfloat3 Ng1 = cross3(e1, e0);
+  const cfloat3 Ng = add3(Ng1, Ng1);
+  const float den = dot3(Ng, dir);
+  if (den == 0.0f) {
+    return false;
+  }
+  const float T = dot3(v0, Ng);
+  const int sign_den = (as_int(den) & 0x80000000);
+  const float sign_T = xor_signmask(T, sign_den);
+  if ((sign_T < 0.0f) || (sign_T > ray_t * xor_signmask(den, sign_den))) {
+    return false;
+  }
+  const float inv_den = 1.0f / den;
+  *isect_u = U * inv_den;
+  *isect_v = V * inv_den;
+  *isect_t = T * inv_den;
+  return true;
+}
+
+CY_FN bool scene_intersect_valid(const CyRay *ray)
+{
+  return isfinite_safe(ray->P.x) && isfinite_safe(ray->D.x) && len_squared3(ray->D) != 0.0f;
+}
+
+/* Closest hit (any_hit == false) or opaque-shadow any hit (any_hit == true).
+ * Returns true on hit; counters (when non-null) gather traversal statistics for
+ * the algorithmic-bytes roofline (inner nodes, leaves, triangle tests). */
+template<bool any_hit>
+CY_FN bool bvh2_intersect(const CyGlobals *kg,
+                          const CyRay *ray,
+                          uint visibility,
+                          CyIsect *isect,
+                          uint *err,
+                          uint *cnt_nodes,
+                          uint *cnt_leaves,
+                          uint *cnt_tris)
+{
+  int traversal_stack[BVH_STACK_SIZE];
+  traversal_stack[0] = ENTRYPOINT_SENTINEL;
+  int stack_ptr = 0;
+  int node_addr = KD->bvh.root;
+  const cfloat3 P = ray->P;
+  const cfloat3 dir = bvh_clamp_direction(ray->D);
+  const cfloat3 idir = rcp3(dir);
+
+  isect->t = ray->t;
+  isect->u = 0.0f;
+  isect->v = 0.0f;
+  isect->prim = PRIM_NONE;
+  isect->object = OBJECT_NONE;
+  isect->type = 0;
+
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  const hc_float4 *nodes = kg->__bvh_nodes;
+
+  do {
+    while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
+      n_nodes++;
+      const hc_float4 cnodes = nodes[node_addr + 0];
+      const hc_float4 node0 = nodes[node_addr + 1];
+      const hc_float4 node1 = nodes[node_addr + 2];
+      const hc_float4 node2 = nodes[node_addr + 3];
+      const float t = isect->t;
+      float c0lox = (node0.x - P.x) * idir.x;
+      float c0hix = (node0.z - P.x) * idir.x;
+      float c0loy = (node1.x - P.y) * idir.y;
+      float c0hiy = (node1.z - P.y) * idir.y;
+      float c0loz = (node2.x - P.z) * idir.z;
+      float c0hiz = (node2.z - P.z) * idir.z;
+      float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
+      float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
+      float c1lox = (node0.y - P.x) * idir.x;
+      float c1hix = (node0.w - P.x) * idir.x;
+      float c1loy = (node1.y - P.y) * idir.y;
+      float c1hiy = (node1.w - P.y) * idir.y;
+      float c1loz = (node2.y - P.z) * idir.z;
+      float c1hiz = (node2.w - P.z) * idir.z;
+      float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
+      float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
+      int traverse_mask = (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
+                          (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
+
+      node_addr = as_int(cnodes.z);
+      int node_addr_child1 = as_int(cnodes.w);
+
+      if (traverse_mask == 3) {
+        bool is_closest_child1 = (c1min < c0min);
+        if (is_closest_child1) {
+          int tmp = node_addr;
+          node_addr = node_addr_child1;
+          node_addr_child1 = tmp;
+        }
+        ++stack_ptr;
+        if (stack_ptr >= BVH_STACK_SIZE) {
+          cy_set_error(err, CY_ERR_BVH_STACK, 0);
+          return false;
+        }
+        traversal_stack[stack_ptr] = node_addr_child1;
+      }
+      else {
+        if (traverse_mask == 2) {
+          node_addr = node_addr_child1;
+        }
+        else if (traverse_mask == 0) {
+          node_addr = traversal_stack[stack_ptr];
+          --stack_ptr;
+        }
+      }
+    }
+
+    if (node_addr < 0) {
+      n_leaves++;
+      const hc_float4 leaf = kg->__bvh_leaf_nodes[-node_addr - 1];
+      int prim_addr = as_int(leaf.x);
+      if (prim_addr >= 0) {
+        const int prim_addr2 = as_int(leaf.y);
+        const uint type = as_uint(leaf.w);
+        node_addr = traversal_stack[stack_ptr];
+        --stack_ptr;
+        if ((type & PRIMITIVE_ALL) == PRIMITIVE_TRIANGLE) {
+          for (; prim_addr < prim_addr2; prim_addr++) {
+            n_tris++;
+            const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+            const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+            float tt, uu, vv;
+            if (ray_triangle_intersect(
+                    P, dir, isect->t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt)) {
+              if (kg->__prim_visibility[prim_addr] & visibility) {
+                isect->prim = prim_addr;
+                isect->object = OBJECT_NONE;
+                isect->type = PRIMITIVE_TRIANGLE;
+                isect->u = uu;
+                isect->v = vv;
+                isect->t = tt;
+                if (any_hit) {
+                  if (cnt_nodes) {
+                    *cnt_nodes += n_nodes;
+                    *cnt_leaves += n_leaves;
+                    *cnt_tris += n_tris;
+                  }
+                  return true;
+                }
+              }
+            }
+          }
+        }
+        else {
+          cy_set_error(err, CY_ERR_PRIMITIVE, type);
+        }
+      }
+      else {
+        /* instance push — instancing is rejected at scene load */
+        cy_set_error(err, CY_ERR_FEATURE, 1);
+        node_addr = ENTRYPOINT_SENTINEL;
+      }
+    }
+  } while (node_addr != ENTRYPOINT_SENTINEL);
+
+  if (cnt_nodes) {
+    *cnt_nodes += n_nodes;
+    *cnt_leaves += n_leaves;
+    *cnt_tris += n_tris;
+  }
+  return (isect->prim != PRIM_NONE);
+}
+
+/* ---------------------------------------------------------------------------
+ * Ray offset (bvh/bvh.h:541-586, __INTERSECTION_REFINE__ branch).
+ */
+CY_FN cfloat3 ray_offset(cfloat3 P, cfloat3 Ng)
+{
+  const float epsilon_f = 1e-5f;
+  const float epsilon_test = 1.0f;
+  const int epsilon_i = 32;
+  cfloat3 res;
+  if (fabsf(P.x) < epsilon_test) {
+    res.x = P.x + Ng.x * epsilon_f;
+  }
+  else {
+    uint ix = as_uint(P.x);
+    ix += ((ix ^ as_uint(Ng.x)) >> 31) ? -epsilon_i : epsilon_i;
+    res.x = as_float(ix);
+  }
+  if (fabsf(P.y) < epsilon_test) {
+    res.y = P.y + Ng.y * epsilon_f;
+  }
+  else {
+    uint iy = as_uint(P.y);
+    iy += ((iy ^ as_uint(Ng.y)) >> 31) ? -epsilon_i : epsilon_i;
+    res.y = as_float(iy);
+  }
+  if (fabsf(P.z) < epsilon_test) {
+    res.z = P.z + Ng.z * epsilon_f;
+  }
+  else {
+    uint iz = as_uint(P.z);
+    iz += ((iz ^ as_uint(Ng.z)) >> 31) ? -epsilon_i : epsilon_i;
+    res.z = as_float(iz);
+  }
+  return res;
+}
+
+/* ---------------------------------------------------------------------------
+ * Triangle geometry: geom_triangle.h:26-110, geom_triangle_intersect.h:195-250.
+ */
+CY_FN void triangle_verts(const CyGlobals *kg, int prim, cfloat3 V[3])
+{
+  const hc_uint4 tri_vindex = kg->__tri_vindex[prim];
+  V[0] = f4to3(kg->__prim_tri_verts[tri_vindex.w + 0]);
+  V[1] = f4to3(kg->__prim_tri_verts[tri_vindex.w + 1]);
+  V[2] = f4to3(kg->__prim_tri_verts[tri_vindex.w + 2]);
+}
+
+CY_FN cfloat3 triangle_normal(const CyGlobals *kg, const CySD *sd)
+{
+  cfloat3 V[3];
+  triangle_verts(kg, sd->prim, V);
+  if (sd->object_flag & SD_OBJECT_NEGATIVE_SCALE_APPLIED) {
+    return normalize3(cross3(sub3(V[2], V[0]), sub3(V[1], V[0])));
+  }
+  return normalize3(cross3(sub3(V[1], V[0]), sub3(V[2], V[0])));
+}
+
+CY_FN cfloat3 triangle_smooth_normal(const CyGlobals *kg, cfloat3 Ng, int prim, float u, float v)
+{
+  const hc_uint4 tri_vindex = kg->__tri_vindex[prim];
+  cfloat3 n0 = f4to3(kg->__tri_vnormal[tri_vindex.x]);
+  cfloat3 n1 = f4to3(kg->__tri_vnormal[tri_vindex.y]);
+  cfloat3 n2 = f4to3(kg->__tri_vnormal[tri_vindex.z]);
+  cfloat3 N = safe_normalize3(add3(add3(mul3f(n2, (1.0f - u - v)), mul3f(n0, u)), mul3f(n1, v)));
+  return is_zero3(N) ? Ng : N;
+}
+
+CY_FN cfloat3 triangle_refine(const CyGlobals *kg, const CyIsect *isect, const CyRay *ray)
+{
+  cfloat3 P = ray->P;
+  cfloat3 D = ray->D;
+  float t = isect->t;
+  P = add3(P, mul3f(D, t));
+  const uint tri_vindex = kg->__prim_tri_index[isect->prim];
+  const hc_float4 tri_a = kg->__prim_tri_verts[tri_vindex + 0];
+  const hc_float4 tri_b = kg->__prim_tri_verts[tri_vindex + 1];
+  const hc_float4 tri_c = kg->__prim_tri_verts[tri_vindex + 2];
+  cfloat3 edge1 = mk3(tri_a.x - tri_c.x, tri_a.y - tri_c.y, tri_a.z - tri_c.z);
+  cfloat3 edge2 = mk3(tri_b.x - tri_c.x, tri_b.y - tri_c.y, tri_b.z - tri_c.z);
+  cfloat3 tvec = mk3(P.x - tri_c.x, P.y - tri_c.y, P.z - tri_c.z);
+  cfloat3 qvec = cross3(tvec, edge1);
+  cfloat3 pvec = cross3(D, edge2);
+  float det = dot3(edge1, pvec);
+  if (det != 0.0f) {
+    float rt = dot3(edge2, qvec) / det;
+    P = add3(P, mul3f(D, rt));
+  }
+  return P;
+}
+
+/* kernel_shader.h:54-153 (static triangles, no instancing, no differentials:
+ * the differentials only feed texture filtering, which this node subset lacks). */
+CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *isect, const CyRay *ray)
+{
+  sd->object = (isect->object == OBJECT_NONE) ? (int)kg->__prim_object[isect->prim] : isect->object;
+  sd->type = isect->type;
+  sd->flag = 0;
+  sd->object_flag = (int)kg->__object_flag[sd->object];
+  sd->prim = (int)kg->__prim_index[isect->prim];
+  sd->ray_length = isect->t;
+  sd->u = isect->u;
+  sd->v = isect->v;
+
+  cfloat3 Ng = triangle_normal(kg, sd);
+  sd->shader = (int)kg->__tri_shader[sd->prim];
+  sd->P = triangle_refine(kg, isect, ray);
+  sd->Ng = Ng;
+  sd->N = Ng;
+  if ((uint)sd->shader & SHADER_SMOOTH_NORMAL) {
+    sd->N = triangle_smooth_normal(kg, Ng, sd->prim, sd->u, sd->v);
+  }
+  sd->I = neg3(ray->D);
+  sd->flag |= kg->__shaders[(uint)sd->shader & SHADER_MASK].flags;
+
+  bool backfacing = (dot3(sd->Ng, sd->I) < 0.0f);
+  if (backfacing) {
+    sd->flag |= SD_BACKFACING;
+    sd->Ng = neg3(sd->Ng);
+    sd->N = neg3(sd->N);
+  }
+}
+
+/* ---------------------------------------------------------------------------
+ * Closures (closure/alloc.h, bsdf_diffuse.h, bsdf_microfacet.h GGX,
+ * bsdf_reflection.h, bsdf_refraction.h, bsdf_util.h).
+ */
+CY_FN CyClosure *closure_alloc(CySD *sd, int type, cfloat3 weight)
+{
+  if (sd->num_closure_left == 0) {
+    return 0;
+  }
+  CyClosure *sc = &sd->closure[sd->num_closure];
+  sc->type = type;
+  sc->weight = weight;
+  sd->num_closure++;
+  sd->num_closure_left--;
+  return sc;
+}
+
+CY_FN CyClosure *bsdf_alloc(CySD *sd, cfloat3 weight)
+{
+  CyClosure *sc = closure_alloc(sd, CLOSURE_NONE_ID, weight);
+  if (sc == 0) {
+    return 0;
+  }
+  float sample_weight = fabsf(average3(weight));
+  sc->sample_weight = sample_weight;
+  return (sample_weight >= CLOSURE_WEIGHT_CUTOFF) ? sc : 0;
+}
+
+CY_FN float fresnel_dielectric(
+    float eta, const cfloat3 N, const cfloat3 I, cfloat3 *R, cfloat3 *T, bool *is_inside)
+{
+  float cos = dot3(N, I), neta;
+  cfloat3 Nn;
+  if (cos > 0) {
+    neta = 1 / eta;
+    Nn = N;
+    *is_inside = false;
+  }
+  else {
+    cos = -cos;
+    neta = eta;
+    Nn = neg3(N);
+    *is_inside = true;
+  }
+  *R = sub3(mul3f(Nn, (2 * cos)), I);
+  float arg = 1 - (neta * neta * (1 - (cos * cos)));
+  if (arg < 0) {
+    *T = mk3(0.0f, 0.0f, 0.0f);
+    return 1;
+  }
+  float dnp = cmax(sqrtf(arg), 1e-7f);
+  float nK = (neta * cos) - dnp;
+  *T = add3(neg3(mul3f(I, neta)), mul3f(Nn, nK));
+  float cosTheta1 = cos;
+  float cosTheta2 = -dot3(Nn, *T);
+  float pPara = (cosTheta1 - eta * cosTheta2) / (cosTheta1 + eta * cosTheta2);
+  float pPerp = (eta * cosTheta1 - cosTheta2) / (eta * cosTheta1 + cosTheta2);
+  return 0.5f * (pPara * pPara + pPerp * pPerp);
+}
+
+CY_FN float fresnel_dielectric_cos(float cosi, float eta)
+{
+  float c = fabsf(cosi);
+  float g = eta * eta - 1 + c * c;
+  if (g > 0) {
+    g = sqrtf(g);
+    float A = (g - c) / (g + c);
+    float B = (c * (g + c) - 1) / (c * (g - c) + 1);
+    return 0.5f * A * A * (1 + B * B);
+  }
+  return 1.0f;
+}
+
+/* bsdf_microfacet.h:307-317, 370-380 */
+CY_FN int bsdf_microfacet_ggx_setup(CyClosure *b)
+{
+  b->alpha_x = saturate(b->alpha_x);
+  b->alpha_y = saturate(b->alpha_y);
+  b->type = CLOSURE_BSDF_MICROFACET_GGX_ID;
+  return SD_BSDF | SD_BSDF_HAS_EVAL;
+}
+CY_FN int bsdf_microfacet_ggx_refraction_setup(CyClosure *b)
+{
+  b->alpha_x = saturate(b->alpha_x);
+  b->alpha_y = b->alpha_x;
+  b->type = CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
+  return SD_BSDF | SD_BSDF_HAS_EVAL;
+}
+
+/* cosine hemisphere: kernel_montecarlo.h:39-66 */
+CY_FN void sample_cos_hemisphere(cfloat3 N, float randu, float randv, cfloat3 *omega_in, float *pdf)
+{
+  float phi = CY_2PI_F * randu;
+  float r = sqrtf(randv);
+  randu = r * cy_cosf(phi);
+  randv = r * cy_sinf(phi);
+  float costheta = sqrtf(cmax(1.0f - randu * randu - randv * randv, 0.0f));
+  cfloat3 T, B;
+  make_orthonormals(N, &T, &B);
+  *omega_in = add3(add3(mul3f(T, randu), mul3f(B, randv)), mul3f(N, costheta));
+  *pdf = costheta * CY_1_PI_F;
+}
+
+CY_FN cfloat3 bsdf_diffuse_eval_reflect(const CyClosure *sc, cfloat3 omega_in, float *pdf)
+{
+  float cos_pi = fmaxf(dot3(sc->N, omega_in), 0.0f) * CY_1_PI_F;
+  *pdf = cos_pi;
+  return mk3(cos_pi, cos_pi, cos_pi);
+}
+
+CY_FN int bsdf_diffuse_sample(const CyClosure *sc,
+                              cfloat3 Ng,
+                              float randu,
+                              float randv,
+                              cfloat3 *eval,
+                              cfloat3 *omega_in,
+                              float *pdf)
+{
+  sample_cos_hemisphere(sc->N, randu, randv, omega_in, pdf);
+  if (dot3(Ng, *omega_in) > 0.0f) {
+    *eval = mk3(*pdf, *pdf, *pdf);
+  }
+  else {
+    *pdf = 0.0f;
+  }
+  return LABEL_REFLECT | LABEL_DIFFUSE;
+}
+
+/* bsdf_microfacet.h:390-501 (isotropic GGX, no fresnel/clearcoat variants). */
+CY_FN cfloat3 bsdf_ggx_eval_reflect(const CyClosure *sc, cfloat3 I, cfloat3 omega_in, float *pdf)
+{
+  float alpha_x = sc->alpha_x;
+  float alpha_y = sc->alpha_y;
+  bool m_refractive = sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
+  cfloat3 N = sc->N;
+  if (m_refractive || alpha_x * alpha_y <= 1e-7f) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float cosNO = dot3(N, I);
+  float cosNI = dot3(N, omega_in);
+  if (cosNI > 0 && cosNO > 0) {
+    cfloat3 m = normalize3(add3(omega_in, I));
+    float alpha2 = alpha_x * alpha_y;
+    float cosThetaM = dot3(N, m);
+    float cosThetaM2 = cosThetaM * cosThetaM;
+    float cosThetaM4 = cosThetaM2 * cosThetaM2;
+    float tanThetaM2 = (1 - cosThetaM2) / cosThetaM2;
+    float D = alpha2 / (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
+    float G1o = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNO * cosNO) / (cosNO * cosNO)));
+    float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
+    float G = G1o * G1i;
+    float common = D * 0.25f / cosNO;
+    cfloat3 F = mk3(1.0f, 1.0f, 1.0f);
+    cfloat3 out = mul3f(mul3f(F, G), common);
+    *pdf = G1o * common;
+    return out;
+  }
+  return mk3(0.0f, 0.0f, 0.0f);
+}
+
+/* bsdf_microfacet.h:503-559 */
+CY_FN cfloat3 bsdf_ggx_eval_transmit(const CyClosure *sc, cfloat3 I, cfloat3 omega_in, float *pdf)
+{
+  float alpha_x = sc->alpha_x;
+  float alpha_y = sc->alpha_y;
+  float m_eta = sc->ior;
+  bool m_refractive = sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
+  cfloat3 N = sc->N;
+  if (!m_refractive || alpha_x * alpha_y <= 1e-7f) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float cosNO = dot3(N, I);
+  float cosNI = dot3(N, omega_in);
+  if (cosNO <= 0 || cosNI >= 0) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  cfloat3 ht = neg3(add3(mul3f(omega_in, m_eta), I));
+  cfloat3 Ht = normalize3(ht);
+  float cosHO = dot3(Ht, I);
+  float cosHI = dot3(Ht, omega_in);
+  float alpha2 = alpha_x * alpha_y;
+  float cosThetaM = dot3(N, Ht);
+  float cosThetaM2 = cosThetaM * cosThetaM;
+  float tanThetaM2 = (1 - cosThetaM2) / cosThetaM2;
+  float cosThetaM4 = cosThetaM2 * cosThetaM2;
+  float D = alpha2 / (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
+  float G1o = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNO * cosNO) / (cosNO * cosNO)));
+  float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
+  float G = G1o * G1i;
+  float Ht2 = dot3(ht, ht);
+  float common = D * (m_eta * m_eta) / (cosNO * Ht2);
+  float out = G * fabsf(cosHI * cosHO) * common;
+  *pdf = G1o * fabsf(cosHO * cosHI) * common;
+  return mk3(out, out, out);
+}
+
+/* bsdf_microfacet.h:143-253 (GGX visible-normal sampling). */
+CY_FN void microfacet_ggx_sample_slopes(const float cos_theta_i,
+                                        const float sin_theta_i,
+                                        float randu,
+                                        float randv,
+                                        float *slope_x,
+                                        float *slope_y,
+                                        float *G1i)
+{
+  if (cos_theta_i >= 0.99999f) {
+    const float r = sqrtf(randu / (1.0f - randu));
+    const float phi = CY_2PI_F * randv;
+    *slope_x = r * cy_cosf(phi);
+    *slope_y = r * cy_sinf(phi);
+    *G1i = 1.0f;
+    return;
+  }
+  const float tan_theta_i = sin_theta_i / cos_theta_i;
+  const float G1_inv = 0.5f * (1.0f + safe_sqrtf(1.0f + tan_theta_i * tan_theta_i));
+  *G1i = 1.0f / G1_inv;
+  const float A = 2.0f * randu * G1_inv - 1.0f;
+  const float AA = A * A;
+  const float tmp = 1.0f / (AA - 1.0f);
+  const float B = tan_theta_i;
+  const float BB = B * B;
+  const float D = safe_sqrtf(BB * (tmp * tmp) - (AA - BB) * tmp);
+  const float slope_x_1 = B * tmp - D;
+  const float slope_x_2 = B * tmp + D;
+  *slope_x = (A < 0.0f || slope_x_2 * tan_theta_i > 1.0f) ? slope_x_1 : slope_x_2;
+  float S;
+  if (randv > 0.5f) {
+    S = 1.0f;
+    randv = 2.0f * (randv - 0.5f);
+  }
+  else {
+    S = -1.0f;
+    randv = 2.0f * (0.5f - randv);
+  }
+  const float z = (randv * (randv * (randv * 0.27385f - 0.73369f) + 0.46341f)) /
+                  (randv * (randv * (randv * 0.093073f + 0.309420f) - 1.000000f) + 0.597999f);
+  *slope_y = S * z * safe_sqrtf(1.0f + (*slope_x) * (*slope_x));
+}
+
+CY_FN cfloat3 microfacet_sample_stretched(const cfloat3 omega_i,
+                                          const float alpha_x,
+                                          const float alpha_y,
+                                          const float randu,
+                                          const float randv,
+                                          float *G1i)
+{
+  cfloat3 omega_i_ = mk3(alpha_x * omega_i.x, alpha_y * omega_i.y, omega_i.z);
+  omega_i_ = normalize3(omega_i_);
+  float costheta_ = 1.0f;
+  float sintheta_ = 0.0f;
+  float cosphi_ = 1.0f;
+  float sinphi_ = 0.0f;
+  if (omega_i_.z < 0.99999f) {
+    costheta_ = omega_i_.z;
+    sintheta_ = safe_sqrtf(1.0f - costheta_ * costheta_);
+    float invlen = 1.0f / sintheta_;
+    cosphi_ = omega_i_.x * invlen;
+    sinphi_ = omega_i_.y * invlen;
+  }
+  float slope_x, slope_y;
+  microfacet_ggx_sample_slopes(costheta_, sintheta_, randu, randv, &slope_x, &slope_y, G1i);
+  float tmp = cosphi_ * slope_x - sinphi_ * slope_y;
+  slope_y = sinphi_ * slope_x + cosphi_ * slope_y;
+  slope_x = tmp;
+  slope_x = alpha_x * slope_x;
+  slope_y = alpha_y * slope_y;
+  return normalize3(mk3(-slope_x, -slope_y, 1.0f));
+}
+
+/* bsdf_microfacet.h:561-788 (isotropic GGX reflection / refraction). */
+CY_FN int bsdf_ggx_sample(const CyClosure *sc,
+                          cfloat3 Ng,
+                          cfloat3 I,
+                          float randu,
+                          float randv,
+                          cfloat3 *eval,
+                          cfloat3 *omega_in,
+                          float *pdf)
+{
+  float alpha_x = sc->alpha_x;
+  float alpha_y = sc->alpha_y;
+  bool m_refractive = sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
+  cfloat3 N = sc->N;
+  int label;
+  float cosNO = dot3(N, I);
+  if (cosNO > 0) {
+    cfloat3 X, Y, Z = N;
+    make_orthonormals(Z, &X, &Y);
+    cfloat3 local_I = mk3(dot3(X, I), dot3(Y, I), cosNO);
+    cfloat3 local_m;
+    float G1o;
+    local_m = microfacet_sample_stretched(local_I, alpha_x, alpha_y, randu, randv, &G1o);
+    cfloat3 m = add3(add3(mul3f(X, local_m.x), mul3f(Y, local_m.y)), mul3f(Z, local_m.z));
+    float cosThetaM = local_m.z;
+    if (!m_refractive) {
+      float cosMO = dot3(m, I);
+      label = LABEL_REFLECT | LABEL_GLOSSY;
+      if (cosMO > 0) {
+        *omega_in = sub3(mul3f(m, 2 * cosMO), I);
+        if (dot3(Ng, *omega_in) > 0) {
+          if (alpha_x * alpha_y <= 1e-7f) {
+            *pdf = 1e6f;
+            *eval = mk3(1e6f, 1e6f, 1e6f);
+            label = LABEL_REFLECT | LABEL_SINGULAR;
+          }
+          else {
+            float alpha2 = alpha_x * alpha_y;
+            float cosThetaM2 = cosThetaM * cosThetaM;
+            float cosThetaM4 = cosThetaM2 * cosThetaM2;
+            float tanThetaM2 = 1 / (cosThetaM2)-1;
+            float cosNI = dot3(N, *omega_in);
+            float D = alpha2 /
+                      (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
+            float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
+            float common = (G1o * D) * 0.25f / cosNO;
+            *pdf = common;
+            cfloat3 F = mk3(1.0f, 1.0f, 1.0f);
+            /* G1i * common * F: scalar * scalar first, then the float3 product. */
+            *eval = mul3f(F, G1i * common);
+          }
+        }
+      }
+    }
+    else {
+      label = LABEL_TRANSMIT | LABEL_GLOSSY;
+      cfloat3 R, T;
+      float m_eta = sc->ior, fresnel;
+      bool inside;
+      fresnel = fresnel_dielectric(m_eta, m, I, &R, &T, &inside);
+      if (!inside && fresnel != 1.0f) {
+        *omega_in = T;
+        if (alpha_x * alpha_y <= 1e-7f || fabsf(m_eta - 1.0f) < 1e-4f) {
+          *pdf = 1e6f;
+          *eval = mk3(1e6f, 1e6f, 1e6f);
+          label = LABEL_TRANSMIT | LABEL_SINGULAR;
+        }
+        else {
+          float alpha2 = alpha_x * alpha_y;
+          float cosThetaM2 = cosThetaM * cosThetaM;
+          float cosThetaM4 = cosThetaM2 * cosThetaM2;
+          float tanThetaM2 = 1 / (cosThetaM2)-1;
+          float D = alpha2 /
+                    (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
+          float cosNI = dot3(N, *omega_in);
+          float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
+          float cosHI = dot3(m, *omega_in);
+          float cosHO = dot3(m, I);
+          float Ht2 = m_eta * cosHI + cosHO;
+          Ht2 *= Ht2;
+          float common = (G1o * D) * (m_eta * m_eta) / (cosNO * Ht2);
+          float out = G1i * fabsf(cosHI * cosHO) * common;
+          *pdf = cosHO * fabsf(cosHI) * common;
+          *eval = mk3(out, out, out);
+        }
+      }
+    }
+  }
+  else {
+    label = (m_refractive) ? LABEL_TRANSMIT | LABEL_GLOSSY : LABEL_REFLECT | LABEL_GLOSSY;
+  }
+  return label;
+}
+
+/* bsdf_reflection.h:60-95, bsdf_refraction.h:62-111 */
+CY_FN int bsdf_reflection_sample(
+    const CyClosure *sc, cfloat3 Ng, cfloat3 I, cfloat3 *eval, cfloat3 *omega_in, float *pdf)
+{
+  cfloat3 N = sc->N;
+  float cosNO = dot3(N, I);
+  if (cosNO > 0) {
+    *omega_in = sub3(mul3f(N, (2 * cosNO)), I);
+    if (dot3(Ng, *omega_in) > 0) {
+      *pdf = 1e6f;
+      *eval = mk3(1e6f, 1e6f, 1e6f);
+    }
+  }
+  return LABEL_REFLECT | LABEL_SINGULAR;
+}
+
+CY_FN int bsdf_refraction_sample(
+    const CyClosure *sc, cfloat3 I, cfloat3 *eval, cfloat3 *omega_in, float *pdf)
+{
+  float m_eta = sc->ior;
+  cfloat3 R, T;
+  bool inside;
+  float fresnel = fresnel_dielectric(m_eta, sc->N, I, &R, &T, &inside);
+  if (!inside && fresnel != 1.0f) {
+    *pdf = 1e6f;
+    *eval = mk3(1e6f, 1e6f, 1e6f);
+    *omega_in = T;
+  }
+  return LABEL_TRANSMIT | LABEL_SINGULAR;
+}
+
+CY_FN float bsdf_get_specular_roughness_squared(const CyClosure *sc)
+{
+  if (CLOSURE_IS_BSDF_SINGULAR(sc->type)) {
+    return 0.0f;
+  }
+  if (CLOSURE_IS_BSDF_MICROFACET(sc->type)) {
+    return sc->alpha_x * sc->alpha_y;
+  }
+  return 1.0f;
+}
+
+/* bsdf.h:113-489 dispatch (subset).  Shadow-terminator offset and bump
+ * shadowing apply only when object.shadow_terminator_offset > 1 or N != sd->N,
+ * both rejected at load / not produced by this node subset. */
+CY_FN int bsdf_sample(const CyGlobals *kg,
+                      const CySD *sd,
+                      const CyClosure *sc,
+                      float randu,
+                      float randv,
+                      cfloat3 *eval,
+                      cfloat3 *omega_in,
+                      float *pdf,
+                      uint *err)
+{
+  int label;
+  const cfloat3 Ng = sd->Ng;
+  switch (sc->type) {
+    case CLOSURE_BSDF_DIFFUSE_ID:
+      label = bsdf_diffuse_sample(sc, Ng, randu, randv, eval, omega_in, pdf);
+      break;
+    case CLOSURE_BSDF_REFLECTION_ID:
+      label = bsdf_reflection_sample(sc, Ng, sd->I, eval, omega_in, pdf);
+      break;
+    case CLOSURE_BSDF_REFRACTION_ID:
+      label = bsdf_refraction_sample(sc, sd->I, eval, omega_in, pdf);
+      break;
+    case CLOSURE_BSDF_MICROFACET_GGX_ID:
+    case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+      label = bsdf_ggx_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
+      break;
+    case CLOSURE_NONE_ID:
+      label = LABEL_NONE;
+      break;
+    default:
+      cy_set_error(err, CY_ERR_CLOSURE, (uint)sc->type);
+      label = LABEL_NONE;
+      break;
+  }
+  if (label & LABEL_TRANSMIT) {
+    float threshold_squared = KD->background.transparent_roughness_squared_threshold;
+    if (threshold_squared >= 0.0f) {
+      if (bsdf_get_specular_roughness_squared(sc) <= threshold_squared) {
+        label |= LABEL_TRANSMIT_TRANSPARENT;
+      }
+    }
+  }
+  return label;
+}
+
+/* bsdf.h:495-700 (subset). */
+CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, float *pdf)
+{
+  cfloat3 eval;
+  if (dot3(sd->Ng, omega_in) >= 0.0f) {
+    switch (sc->type) {
+      case CLOSURE_BSDF_DIFFUSE_ID:
+        eval = bsdf_diffuse_eval_reflect(sc, omega_in, pdf);
+        break;
+      case CLOSURE_BSDF_MICROFACET_GGX_ID:
+      case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+        eval = bsdf_ggx_eval_reflect(sc, sd->I, omega_in, pdf);
+        break;
+      default: /* reflection/refraction are singular: zero; NONE: zero */
+        eval = mk3(0.0f, 0.0f, 0.0f);
+        break;
+    }
+  }
+  else {
+    switch (sc->type) {
+      case CLOSURE_BSDF_MICROFACET_GGX_ID:
+      case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+        eval = bsdf_ggx_eval_transmit(sc, sd->I, omega_in, pdf);
+        break;
+      default:
+        eval = mk3(0.0f, 0.0f, 0.0f);
+        break;
+    }
+  }
+  return eval;
+}
+
+/* ---------------------------------------------------------------------------
+ * SVM interpreter subset (svm/svm.h:220-549, svm_closure.h, svm_value.h,
+ * svm_fresnel.h).  Unknown nodes set CY_ERR_SVM_NODE and stop the shader.
+ */
+CY_FN float svm_load(const float *stack, uint a, uint *err)
+{
+  if (a >= CY_SVM_STACK) {
+    cy_set_error(err, CY_ERR_SVM_STACK, a);
+    return 0.0f;
+  }
+  return stack[a];
+}
+CY_FN void svm_store(float *stack, uint a, float f, uint *err)
+{
+  if (a >= CY_SVM_STACK) {
+    cy_set_error(err, CY_ERR_SVM_STACK, a);
+    return;
+  }
+  stack[a] = f;
+}
+CY_FN cfloat3 svm_load3(const float *stack, uint a, uint *err)
+{
+  return mk3(svm_load(stack, a, err), svm_load(stack, a + 1, err), svm_load(stack, a + 2, err));
+}
+CY_FN void svm_store3(float *stack, uint a, cfloat3 f, uint *err)
+{
+  svm_store(stack, a, f.x, err);
+  svm_store(stack, a + 1, f.y, err);
+  svm_store(stack, a + 2, f.z, err);
+}
+
+CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, float roughness, bool refract)
+{
+  if (type == CLOSURE_BSDF_SHARP_GLASS_ID) {
+    if (refract) {
+      b->alpha_y = 0.0f;
+      b->alpha_x = 0.0f;
+      b->ior = eta;
+      b->type = CLOSURE_BSDF_REFRACTION_ID;
+      sd->flag |= SD_BSDF;
+    }
+    else {
+      b->alpha_y = 0.0f;
+      b->alpha_x = 0.0f;
+      b->ior = 0.0f;
+      b->type = CLOSURE_BSDF_REFLECTION_ID;
+      sd->flag |= SD_BSDF;
+    }
+  }
+  else {
+    b->alpha_x = roughness;
+    b->alpha_y = roughness;
+    b->ior = eta;
+    if (refract) {
+      sd->flag |= bsdf_microfacet_ggx_refraction_setup(b);
+    }
+    else {
+      sd->flag |= bsdf_microfacet_ggx_setup(b);
+    }
+  }
+}
+
+CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
+                                 CySD *sd,
+                                 float *stack,
+                                 hc_uint4 node,
+                                 int path_flag,
+                                 int *offset,
+                                 uint *err)
+{
+  uint type = node.y & 0xFF, param1_offset = (node.y >> 8) & 0xFF;
+  uint param2_offset = (node.y >> 16) & 0xFF, mix_weight_offset = (node.y >> 24) & 0xFF;
+  float mix_weight = (mix_weight_offset != SVM_STACK_INVALID) ?
+                         svm_load(stack, mix_weight_offset, err) :
+                         1.0f;
+  hc_uint4 data_node = kg->__svm_nodes[*offset];
+  (*offset)++;
+  if (mix_weight == 0.0f) {
+    return;
+  }
+  cfloat3 N = (data_node.x != SVM_STACK_INVALID) ? svm_load3(stack, data_node.x, err) : sd->N;
+  float param1 = (param1_offset != SVM_STACK_INVALID) ? svm_load(stack, param1_offset, err) :
+                                                        as_float(node.z);
+  float param2 = (param2_offset != SVM_STACK_INVALID) ? svm_load(stack, param2_offset, err) :
+                                                        as_float(node.w);
+  switch (type) {
+    case CLOSURE_BSDF_DIFFUSE_ID: {
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (b) {
+        b->N = N;
+        float roughness = param1;
+        if (roughness == 0.0f) {
+          b->type = CLOSURE_BSDF_DIFFUSE_ID;
+          sd->flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
+        }
+        else {
+          cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_OREN_NAYAR_ID);
+        }
+      }
+      break;
+    }
+    case CLOSURE_BSDF_REFLECTION_ID:
+    case CLOSURE_BSDF_MICROFACET_GGX_ID: {
+      if (!KD->integrator.caustics_reflective && (path_flag & PATH_RAY_DIFFUSE)) {
+        break;
+      }
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (!b) {
+        break;
+      }
+      float roughness = sqr(param1);
+      b->N = N;
+      b->ior = 0.0f;
+      if (data_node.y == SVM_STACK_INVALID) {
+        b->alpha_x = roughness;
+        b->alpha_y = roughness;
+      }
+      else {
+        cy_set_error(err, CY_ERR_CLOSURE, 1000 + type); /* anisotropic tangent */
+      }
+      if (type == CLOSURE_BSDF_REFLECTION_ID) {
+        b->type = CLOSURE_BSDF_REFLECTION_ID;
+        sd->flag |= SD_BSDF;
+      }
+      else {
+        sd->flag |= bsdf_microfacet_ggx_setup(b);
+      }
+      break;
+    }
+    case CLOSURE_BSDF_REFRACTION_ID:
+    case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID: {
+      if (!KD->integrator.caustics_refractive && (path_flag & PATH_RAY_DIFFUSE)) {
+        break;
+      }
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (b) {
+        b->N = N;
+        float eta = fmaxf(param2, 1e-5f);
+        eta = (sd->flag & SD_BACKFACING) ? 1.0f / eta : eta;
+        if (type == CLOSURE_BSDF_REFRACTION_ID) {
+          b->alpha_x = 0.0f;
+          b->alpha_y = 0.0f;
+          b->ior = eta;
+          b->type = CLOSURE_BSDF_REFRACTION_ID;
+          sd->flag |= SD_BSDF;
+        }
+        else {
+          float roughness = sqr(param1);
+          b->alpha_x = roughness;
+          b->alpha_y = roughness;
+          b->ior = eta;
+          sd->flag |= bsdf_microfacet_ggx_refraction_setup(b);
+        }
+      }
+      break;
+    }
+    case CLOSURE_BSDF_SHARP_GLASS_ID:
+    case CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID: {
+      if (!KD->integrator.caustics_reflective && !KD->integrator.caustics_refractive &&
+          (path_flag & PATH_RAY_DIFFUSE)) {
+        break;
+      }
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      float eta = fmaxf(param2, 1e-5f);
+      eta = (sd->flag & SD_BACKFACING) ? 1.0f / eta : eta;
+      float cosNO = dot3(N, sd->I);
+      float fresnel = fresnel_dielectric_cos(cosNO, eta);
+      float roughness = sqr(param1);
+      if (KD->integrator.caustics_reflective || (path_flag & PATH_RAY_DIFFUSE) == 0) {
+        CyClosure *b = bsdf_alloc(sd, mul3f(weight, fresnel));
+        if (b) {
+          b->N = N;
+          svm_node_glass_setup(sd, b, (int)type, eta, roughness, false);
+        }
+      }
+      if (KD->integrator.caustics_refractive || (path_flag & PATH_RAY_DIFFUSE) == 0) {
+        CyClosure *b = bsdf_alloc(sd, mul3f(weight, (1.0f - fresnel)));
+        if (b) {
+          b->N = N;
+          svm_node_glass_setup(sd, b, (int)type, eta, roughness, true);
+        }
+      }
+      break;
+    }
+    default:
+      cy_set_error(err, CY_ERR_CLOSURE, type);
+      break;
+  }
+}
+
+CY_FN void emission_setup(CySD *sd, cfloat3 weight)
+{
+  if (sd->flag & SD_EMISSION) {
+    sd->closure_emission_background = add3(sd->closure_emission_background, weight);
+  }
+  else {
+    sd->flag |= SD_EMISSION;
+    sd->closure_emission_background = weight;
+  }
+}
+
+CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, int path_flag, uint *err)
+{
+  float stack[CY_SVM_STACK];
+  int offset = (int)((uint)sd->shader & SHADER_MASK);
+  for (int guard = 0; guard < 4096; guard++) {
+    hc_uint4 node = kg->__svm_nodes[offset];
+    offset++;
+    switch (node.x) {
+      case NODE_END:
+        return;
+      case NODE_SHADER_JUMP:
+        offset = (int)node.y; /* SHADER_TYPE_SURFACE */
+        break;
+      case NODE_CLOSURE_BSDF:
+        svm_node_closure_bsdf(kg, sd, stack, node, path_flag, &offset, err);
+        break;
+      case NODE_CLOSURE_EMISSION:
+      case NODE_CLOSURE_BACKGROUND: {
+        uint mix_weight_offset = node.y;
+        cfloat3 weight = sd->svm_closure_weight;
+        if (mix_weight_offset != SVM_STACK_INVALID) {
+          float mix_weight = svm_load(stack, mix_weight_offset, err);
+          if (mix_weight == 0.0f) {
+            break;
+          }
+          weight = mul3f(weight, mix_weight);
+        }
+        emission_setup(sd, weight);
+        break;
+      }
+      case NODE_CLOSURE_SET_WEIGHT:
+        sd->svm_closure_weight = mk3(as_float(node.y), as_float(node.z), as_float(node.w));
+        break;
+      case NODE_CLOSURE_WEIGHT:
+        sd->svm_closure_weight = svm_load3(stack, node.y, err);
+        break;
+      case NODE_EMISSION_WEIGHT: {
+        float strength = svm_load(stack, node.z, err);
+        sd->svm_closure_weight = mul3f(svm_load3(stack, node.y, err), strength);
+        break;
+      }
+      case NODE_MIX_CLOSURE: {
+        uint weight_offset = node.y & 0xFF, in_weight_offset = (node.y >> 8) & 0xFF;
+        uint weight1_offset = (node.y >> 16) & 0xFF, weight2_offset = (node.y >> 24) & 0xFF;
+        float weight = saturate(svm_load(stack, weight_offset, err));
+        float in_weight = (in_weight_offset != SVM_STACK_INVALID) ?
+                              svm_load(stack, in_weight_offset, err) :
+                              1.0f;
+        if (weight1_offset != SVM_STACK_INVALID) {
+          svm_store(stack, weight1_offset, in_weight * (1.0f - weight), err);
+        }
+        if (weight2_offset != SVM_STACK_INVALID) {
+          svm_store(stack, weight2_offset, in_weight * weight, err);
+        }
+        break;
+      }
+      case NODE_JUMP_IF_ZERO:
+        if (svm_load(stack, node.z, err) == 0.0f) {
+          offset += (int)node.y;
+        }
+        break;
+      case NODE_JUMP_IF_ONE:
+        if (svm_load(stack, node.z, err) == 1.0f) {
+          offset += (int)node.y;
+        }
+        break;
+      case NODE_VALUE_F:
+        svm_store(stack, node.z, as_float(node.y), err);
+        break;
+      case NODE_VALUE_V: {
+        hc_uint4 node1 = kg->__svm_nodes[offset];
+        offset++;
+        svm_store3(stack, node.y, mk3(as_float(node1.y), as_float(node1.z), as_float(node1.w)), err);
+        break;
+      }
+      case NODE_FRESNEL: {
+        uint normal_offset = node.w & 0xFF, out_offset = (node.w >> 8) & 0xFF;
+        float eta = (node.y != SVM_STACK_INVALID) ? svm_load(stack, node.y, err) : as_float(node.z);
+        cfloat3 normal_in = (normal_offset != SVM_STACK_INVALID) ?
+                                svm_load3(stack, normal_offset, err) :
+                                sd->N;
+        eta = fmaxf(eta, 1e-5f);
+        eta = (sd->flag & SD_BACKFACING) ? 1.0f / eta : eta;
+        svm_store(stack, out_offset, fresnel_dielectric_cos(dot3(sd->I, normal_in), eta), err);
+        break;
+      }
+      case NODE_LAYER_WEIGHT: {
+        uint ltype = node.w & 0xFF, normal_offset = (node.w >> 8) & 0xFF;
+        uint out_offset = (node.w >> 16) & 0xFF;
+        float blend = (node.y != SVM_STACK_INVALID) ? svm_load(stack, node.y, err) :
+                                                      as_float(node.z);
+        cfloat3 normal_in = (normal_offset != SVM_STACK_INVALID) ?
+                                svm_load3(stack, normal_offset, err) :
+                                sd->N;
+        float f;
+        if (ltype == NODE_LAYER_WEIGHT_FRESNEL) {
+          float eta = fmaxf(1.0f - blend, 1e-5f);
+          eta = (sd->flag & SD_BACKFACING) ? eta : 1.0f / eta;
+          f = fresnel_dielectric_cos(dot3(sd->I, normal_in), eta);
+        }
+        else {
+          f = fabsf(dot3(sd->I, normal_in));
+          if (blend != 0.5f) {
+            /* powf path: not bit-exact vs libm; reject */
+            cy_set_error(err, CY_ERR_SVM_NODE, 1000 + NODE_LAYER_WEIGHT);
+          }
+          f = 1.0f - f;
+        }
+        svm_store(stack, out_offset, f, err);
+        break;
+      }
+      default:
+        cy_set_error(err, CY_ERR_SVM_NODE, node.x);
+        return;
+    }
+  }
+}
+
+/* kernel_shader.h:1057-1112 */
+CY_FN void shader_eval_surface(const CyGlobals *kg, CySD *sd, int path_flag, uint *err)
+{
+  int max_closures;
+  if (path_flag & (PATH_RAY_TERMINATE | PATH_RAY_SHADOW | PATH_RAY_EMISSION)) {
+    max_closures = 0;
+  }
+  else {
+    max_closures = KD->integrator.max_closures;
+  }
+  sd->num_closure = 0;
+  sd->num_closure_left = max_closures;
+  svm_eval_nodes(kg, sd, path_flag, err);
+}
+
+/* kernel_shader.h:527-551 */
+CY_FN void shader_prepare_closures(CySD *sd, const CyPathState *state)
+{
+  if (state->bounce + state->transparent_bounce == 0 && sd->num_closure > 1) {
+    float sum = 0.0f;
+    for (int i = 0; i < sd->num_closure; i++) {
+      CyClosure *sc = &sd->closure[i];
+      if (CLOSURE_IS_BSDF_OR_BSSRDF(sc->type)) {
+        sum += sc->sample_weight;
+      }
+    }
+    for (int i = 0; i < sd->num_closure; i++) {
+      CyClosure *sc = &sd->closure[i];
+      if (CLOSURE_IS_BSDF_OR_BSSRDF(sc->type)) {
+        sc->sample_weight = cmax(sc->sample_weight, 0.125f * sum);
+      }
+    }
+  }
+}
+
+/* kernel_shader.h:553-582 (use_light_pass == 0: only eval->diffuse accumulates). */
+CY_FN void shader_bsdf_multi_eval(const CySD *sd,
+                                  const cfloat3 omega_in,
+                                  float *pdf,
+                                  int skip_sc,
+                                  cfloat3 *result_eval,
+                                  float sum_pdf,
+                                  float sum_sample_weight)
+{
+  for (int i = 0; i < sd->num_closure; i++) {
+    const CyClosure *sc = &sd->closure[i];
+    if (i != skip_sc && CLOSURE_IS_BSDF(sc->type)) {
+      float bsdf_pdf = 0.0f;
+      cfloat3 eval = bsdf_eval(sd, sc, omega_in, &bsdf_pdf);
+      if (bsdf_pdf != 0.0f) {
+        /* bsdf_eval_accum(..., mis_weight 1.0): value *= 1.0f, then diffuse += */
+        cfloat3 value = mul3(eval, sc->weight);
+        value = mul3f(value, 1.0f);
+        *result_eval = add3(*result_eval, value);
+        sum_pdf += bsdf_pdf * sc->sample_weight;
+      }
+      sum_sample_weight += sc->sample_weight;
+    }
+  }
+  *pdf = (sum_sample_weight > 0.0f) ? sum_pdf / sum_sample_weight : 0.0f;
+}
+
+/* kernel_shader.h:638-680 */
+CY_FN int shader_bsdf_pick(const CySD *sd, float *randu)
+{
+  int sampled = 0;
+  if (sd->num_closure > 1) {
+    float sum = 0.0f;
+    for (int i = 0; i < sd->num_closure; i++) {
+      const CyClosure *sc = &sd->closure[i];
+      if (CLOSURE_IS_BSDF_OR_BSSRDF(sc->type)) {
+        sum += sc->sample_weight;
+      }
+    }
+    float r = (*randu) * sum;
+    float partial_sum = 0.0f;
+    for (int i = 0; i < sd->num_closure; i++) {
+      const CyClosure *sc = &sd->closure[i];
+      if (CLOSURE_IS_BSDF_OR_BSSRDF(sc->type)) {
+        float next_sum = partial_sum + sc->sample_weight;
+        if (r < next_sum) {
+          sampled = i;
+          *randu = (r - partial_sum) / sc->sample_weight;
+          break;
+        }
+        partial_sum = next_sum;
+      }
+    }
+  }
+  return CLOSURE_IS_BSDF(sd->closure[sampled].type) ? sampled : -1;
+}
+
+/* kernel_shader.h:739-775 */
+CY_FN int shader_bsdf_sample(const CyGlobals *kg,
+                             const CySD *sd,
+                             float randu,
+                             float randv,
+                             cfloat3 *bsdf_eval_out,
+                             cfloat3 *omega_in,
+                             float *pdf,
+                             uint *err)
+{
+  int sci = shader_bsdf_pick(sd, &randu);
+  if (sci < 0) {
+    *pdf = 0.0f;
+    return LABEL_NONE;
+  }
+  const CyClosure *sc = &sd->closure[sci];
+  int label;
+  cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
+  *pdf = 0.0f;
+  label = bsdf_sample(kg, sd, sc, randu, randv, &eval, omega_in, pdf, err);
+  if (*pdf != 0.0f) {
+    *bsdf_eval_out = mul3(eval, sc->weight);
+    if (sd->num_closure > 1) {
+      float sweight = sc->sample_weight;
+      shader_bsdf_multi_eval(sd, *omega_in, pdf, sci, bsdf_eval_out, *pdf * sweight, sweight);
+    }
+  }
+  return label;
+}
+
+/* ---------------------------------------------------------------------------
+ * Lights: kernel_light.h:331-617 (mesh lights with constant emission).
+ */
+typedef struct CyLightSample {
+  cfloat3 P, Ng, D;
+  float t, u, v, pdf, eval_fac;
+  int object, prim, shader, lamp, type;
+} CyLightSample;
+
+CY_FN float triangle_light_pdf_area(const CyGlobals *kg, cfloat3 Ng, cfloat3 I, float t)
+{
+  float pdf = KD->integrator.pdf_triangles;
+  float cos_pi = fabsf(dot3(Ng, I));
+  if (cos_pi == 0.0f) {
+    return 0.0f;
+  }
+  return t * t * pdf / cos_pi;
+}
+
+CY_FN float triangle_light_pdf(const CyGlobals *kg, const CySD *sd, float t)
+{
+  cfloat3 V[3];
+  triangle_verts(kg, sd->prim, V);
+  const cfloat3 e0 = sub3(V[1], V[0]);
+  const cfloat3 e1 = sub3(V[2], V[0]);
+  const cfloat3 e2 = sub3(V[2], V[1]);
+  const float longest_edge_squared = cmax(len_squared3(e0), cmax(len_squared3(e1), len_squared3(e2)));
+  const cfloat3 N = cross3(e0, e1);
+  const float distance_to_plane = fabsf(dot3(N, mul3f(sd->I, t))) / dot3(N, N);
+  if (longest_edge_squared > distance_to_plane * distance_to_plane) {
+    const cfloat3 Px = add3(sd->P, mul3f(sd->I, t));
+    const cfloat3 v0_p = sub3(V[0], Px);
+    const cfloat3 v1_p = sub3(V[1], Px);
+    const cfloat3 v2_p = sub3(V[2], Px);
+    const cfloat3 u01 = safe_normalize3(cross3(v0_p, v1_p));
+    const cfloat3 u02 = safe_normalize3(cross3(v0_p, v2_p));
+    const cfloat3 u12 = safe_normalize3(cross3(v1_p, v2_p));
+    const float alpha = fast_acosf(dot3(u02, u01));
+    const float beta = fast_acosf(-dot3(u01, u12));
+    const float gamma = fast_acosf(dot3(u02, u12));
+    const float solid_angle = alpha + beta + gamma - CY_PI_F;
+    if (solid_angle == 0.0f) {
+      return 0.0f;
+    }
+    float area = 0.5f * len3(N);
+    const float pdf = area * KD->integrator.pdf_triangles;
+    return pdf / solid_angle;
+  }
+  return triangle_light_pdf_area(kg, sd->Ng, sd->I, t);
+}
+
+CY_FN void triangle_light_sample(const CyGlobals *kg,
+                                 int prim,
+                                 int object,
+                                 float randu,
+                                 float randv,
+                                 CyLightSample *ls,
+                                 const cfloat3 P)
+{
+  cfloat3 V[3];
+  triangle_verts(kg, prim, V);
+  const cfloat3 e0 = sub3(V[1], V[0]);
+  const cfloat3 e1 = sub3(V[2], V[0]);
+  const cfloat3 e2 = sub3(V[2], V[1]);
+  const float longest_edge_squared = cmax(len_squared3(e0), cmax(len_squared3(e1), len_squared3(e2)));
+  const cfloat3 N0 = cross3(e0, e1);
+  float Nl = 0.0f;
+  ls->Ng = safe_normalize_len3(N0, &Nl);
+  float area = 0.5f * Nl;
+  const int object_flag = (int)kg->__object_flag[object];
+  if (object_flag & SD_OBJECT_NEGATIVE_SCALE_APPLIED) {
+    ls->Ng = neg3(ls->Ng);
+  }
+  ls->eval_fac = 1.0f;
+  ls->shader = (int)kg->__tri_shader[prim];
+  ls->object = object;
+  ls->prim = prim;
+  ls->lamp = LAMP_NONE;
+  ls->shader |= (int)SHADER_USE_MIS;
+  ls->type = 5; /* LIGHT_TRIANGLE */
+
+  float distance_to_plane = fabsf(dot3(N0, sub3(V[0], P)) / dot3(N0, N0));
+  if (longest_edge_squared > distance_to_plane * distance_to_plane) {
+    const cfloat3 v0_p = sub3(V[0], P);
+    const cfloat3 v1_p = sub3(V[1], P);
+    const cfloat3 v2_p = sub3(V[2], P);
+    const cfloat3 u01 = safe_normalize3(cross3(v0_p, v1_p));
+    const cfloat3 u02 = safe_normalize3(cross3(v0_p, v2_p));
+    const cfloat3 u12 = safe_normalize3(cross3(v1_p, v2_p));
+    const cfloat3 A = safe_normalize3(v0_p);
+    const cfloat3 B = safe_normalize3(v1_p);
+    const cfloat3 C = safe_normalize3(v2_p);
+    const float cos_alpha = dot3(u02, u01);
+    const float cos_beta = -dot3(u01, u12);
+    const float cos_gamma = dot3(u02, u12);
+    const float alpha = fast_acosf(cos_alpha);
+    const float beta = fast_acosf(cos_beta);
+    const float gamma = fast_acosf(cos_gamma);
+    const float solid_angle = alpha + beta + gamma - CY_PI_F;
+    const float cos_c = dot3(A, B);
+    const float sin_alpha = fast_sinf(alpha);
+    const float product = sin_alpha * cos_c;
+    const float phi = randu * solid_angle - alpha;
+    float s, t;
+    fast_sincosf(phi, &s, &t);
+    const float u = t - cos_alpha;
+    const float v = s + product;
+    const cfloat3 U = safe_normalize3(sub3(C, mul3f(A, dot3(C, A))));
+    float q = 1.0f;
+    const float det = ((v * s + u * t) * sin_alpha);
+    if (det != 0.0f) {
+      q = ((v * t - u * s) * cos_alpha - v) / det;
+    }
+    const float temp = cmax(1.0f - q * q, 0.0f);
+    const cfloat3 C_ = safe_normalize3(add3(mul3f(A, q), mul3f(U, sqrtf(temp))));
+    const float z = 1.0f - randv * (1.0f - dot3(C_, B));
+    ls->D = add3(mul3f(B, z), mul3f(safe_normalize3(sub3(C_, mul3f(B, dot3(C_, B)))),
+                                    safe_sqrtf(1.0f - z * z)));
+    if (!ray_triangle_intersect(P, ls->D, CY_FLT_MAX, V[0], V[1], V[2], &ls->u, &ls->v, &ls->t)) {
+      ls->pdf = 0.0f;
+      return;
+    }
+    ls->P = add3(P, mul3f(ls->D, ls->t));
+    if (solid_angle == 0.0f) {
+      ls->pdf = 0.0f;
+      return;
+    }
+    const float pdf = area * KD->integrator.pdf_triangles;
+    ls->pdf = pdf / solid_angle;
+  }
+  else {
+    float u = randu;
+    float v = randv;
+    if (v > u) {
+      u *= 0.5f;
+      v -= u;
+    }
+    else {
+      v *= 0.5f;
+      u -= v;
+    }
+    const float t = 1.0f - u - v;
+    ls->P = add3(add3(mul3f(V[0], u), mul3f(V[1], v)), mul3f(V[2], t));
+    ls->D = normalize_len3(sub3(ls->P, P), &ls->t);
+    ls->pdf = triangle_light_pdf_area(kg, ls->Ng, neg3(ls->D), ls->t);
+    ls->u = u;
+    ls->v = v;
+  }
+}
+
+CY_FN int light_distribution_sample(const CyGlobals *kg, float *randu)
+{
+  int first = 0;
+  int len = KD->integrator.num_distribution + 1;
+  float r = *randu;
+  do {
+    int half_len = len >> 1;
+    int middle = first + half_len;
+    if (r < kg->__light_distribution[middle].totarea) {
+      len = half_len;
+    }
+    else {
+      first = middle + 1;
+      len = len - half_len - 1;
+    }
+  } while (len > 0);
+  int index = iclamp(first - 1, 0, KD->integrator.num_distribution - 1);
+  float distr_min = kg->__light_distribution[index].totarea;
+  float distr_max = kg->__light_distribution[index + 1].totarea;
+  *randu = (r - distr_min) / (distr_max - distr_min);
+  return index;
+}
+
+CY_FN bool light_sample(
+    const CyGlobals *kg, float randu, float randv, cfloat3 P, CyLightSample *ls, uint *err)
+{
+  int index = light_distribution_sample(kg, &randu);
+  const hc_KernelLightDistribution *kd = &kg->__light_distribution[index];
+  int prim = kd->prim;
+  if (prim >= 0) {
+    triangle_light_sample(kg, prim, kd->object_id, randu, randv, ls, P);
+    ls->shader |= kd->shader_flag;
+    return (ls->pdf > 0.0f);
+  }
+  cy_set_error(err, CY_ERR_FEATURE, 2); /* lamps: rejected at load */
+  return false;
+}
+
+/* kernel_shader.h:978-992 */
+CY_FN bool shader_constant_emission_eval(const CyGlobals *kg, int shader, cfloat3 *eval)
+{
+  int shader_index = (int)((uint)shader & SHADER_MASK);
+  const hc_KernelShader *ks = &kg->__shaders[shader_index];
+  if (ks->flags & SD_HAS_CONSTANT_EMISSION) {
+    *eval = mk3(ks->constant_emission[0], ks->constant_emission[1], ks->constant_emission[2]);
+    return true;
+  }
+  return false;
+}
+
+#endif /* CY_PATH_H */

@@ -1,0 +1,117 @@
+"""Loaders for the in-tree native libraries.
+
+- libhipcycles.so       : the HIP device (kernels + C ABI of include/hipcycles.h)
+- libhipcycles_host.so  : host-only helpers (BVH2 builder/packer stand-in)
+
+Both are built in-tree by __graft_entry__.build() / tools/build.py.  A missing
+device library is a hard error: there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+DEVICE_LIB = os.path.join(_HERE, "libhipcycles.so")
+HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
+
+_host = None
+_dev = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_LIB):
+            raise NativeLibraryMissing(f"{HOST_LIB} not built; run python __graft_entry__.py build")
+        lib = ctypes.CDLL(HOST_LIB)
+        lib.hcb_build.restype = ctypes.c_void_p
+        lib.hcb_build.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        lib.hcb_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        lib.hcb_free.argtypes = [ctypes.c_void_p]
+        _host = lib
+    return _host
+
+
+class WorkTile(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_int32), ("y", ctypes.c_int32), ("w", ctypes.c_int32), ("h", ctypes.c_int32),
+        ("start_sample", ctypes.c_int32), ("num_samples", ctypes.c_int32),
+        ("offset", ctypes.c_int32), ("stride", ctypes.c_int32), ("buffer", ctypes.c_uint64),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("closest_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
+        ("inner_nodes", ctypes.c_uint64), ("leaves", ctypes.c_uint64), ("triangles", ctypes.c_uint64),
+        ("iterations", ctypes.c_uint64), ("intersect_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double), ("closest_ms", ctypes.c_double), ("closest_launches", ctypes.c_uint64),
+    ]
+
+
+# exported symbols of include/hipcycles.h (checked by tests/test_native_build.py)
+DEVICE_SYMBOLS = {
+    "hipcy_abi_version": (ctypes.c_int, []),
+    "hipcy_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "hipcy_device_info": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]),
+    "hipcy_create": (ctypes.c_void_p, [ctypes.c_int]),
+    "hipcy_destroy": (None, [ctypes.c_void_p]),
+    "hipcy_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "hipcy_global_error": (ctypes.c_char_p, []),
+    "hipcy_mem_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]),
+    "hipcy_mem_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "hipcy_mem_copy_to": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]),
+    "hipcy_mem_copy_from": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t]),
+    "hipcy_mem_zero": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t]),
+    "hipcy_const_copy_to": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "hipcy_bind_global": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_size_t]),
+    "hipcy_load_kernels": (ctypes.c_int, [ctypes.c_void_p]),
+    "hipcy_get_bvh_layout_mask": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "hipcy_path_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile)]),
+    "hipcy_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "hipcy_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
+    "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hipcy_intersect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),
+    "hipcy_camera_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+}
+
+
+def device_lib():
+    global _dev
+    if _dev is None:
+        if not os.path.exists(DEVICE_LIB):
+            raise NativeLibraryMissing(
+                f"{DEVICE_LIB} not built (the HIP device library is required; no CPU fallback)"
+            )
+        lib = ctypes.CDLL(DEVICE_LIB)
+        for name, (res, args) in DEVICE_SYMBOLS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _dev = lib
+    return _dev
+
+
+def hash_uint2(kx: int, ky: int) -> int:
+    """util/util_hash.h:83-93 (host side, for KernelIntegrator.seed)."""
+    M = 0xFFFFFFFF
+
+    def rot(x, k):
+        return ((x << k) | (x >> (32 - k))) & M
+
+    a = b = c = (0xDEADBEEF + (2 << 2) + 13) & M
+    b = (b + ky) & M
+    a = (a + kx) & M
+    c ^= b; c = (c - rot(b, 14)) & M
+    a ^= c; a = (a - rot(c, 11)) & M
+    b ^= a; b = (b - rot(a, 25)) & M
+    c ^= b; c = (c - rot(b, 16)) & M
+    a ^= c; a = (a - rot(c, 4)) & M
+    b ^= a; b = (b - rot(a, 14)) & M
+    c ^= b; c = (c - rot(b, 24)) & M
+    return c if c < 2**31 else c - 2**32

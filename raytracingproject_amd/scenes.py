@@ -1,0 +1,196 @@
+"""Procedural stand-in scenes for BASELINE.json's configs.
+
+The named .blend benchmarks are not available offline, so each config is a
+procedural scene with the config's resolution and sample count:
+  cornell_box()   CB : 256x256, 32 spp, diffuse + one emissive quad
+  bmw27_standin() BMW: 1280x720, 128 spp, a tessellated car-like assembly with
+                       car paint (diffuse/glossy mix), chrome, glass, tyres,
+                       a studio floor and two emissive panels
+Generator seeds are fixed (0x5EED + config index).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import scene as sc
+
+
+def _quad(p0, p1, p2, p3):
+    v = np.array([p0, p1, p2, p3], dtype=np.float32)
+    t = np.array([[0, 1, 2], [0, 2, 3]], dtype=np.int64)
+    return v, t
+
+
+def _box(center, size, rot_y=0.0):
+    cx, cy, cz = center
+    sx, sy, sz = (s * 0.5 for s in size)
+    corners = np.array(
+        [[-sx, -sy, -sz], [sx, -sy, -sz], [sx, sy, -sz], [-sx, sy, -sz],
+         [-sx, -sy, sz], [sx, -sy, sz], [sx, sy, sz], [-sx, sy, sz]], dtype=np.float64)
+    c, s = math.cos(rot_y), math.sin(rot_y)
+    R = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    corners = corners @ R.T + np.array([cx, cy, cz])
+    faces = [[0, 3, 2, 1], [4, 5, 6, 7], [0, 1, 5, 4], [3, 7, 6, 2], [0, 4, 7, 3], [1, 2, 6, 5]]
+    v, t = [], []
+    for f in faces:
+        base = len(v)
+        v.extend(corners[f])
+        t.extend([[base, base + 1, base + 2], [base, base + 2, base + 3]])
+    return np.array(v, dtype=np.float32), np.array(t, dtype=np.int64)
+
+
+def _grid_tris(nu, nv, wrap_u=True):
+    """Triangles of a (nu x nv) vertex grid, u optionally wrapping."""
+    t = []
+    uu = nu if wrap_u else nu - 1
+    for j in range(nv - 1):
+        for i in range(uu):
+            i1 = (i + 1) % nu
+            a, b, c, d = j * nu + i, j * nu + i1, (j + 1) * nu + i1, (j + 1) * nu + i
+            t.append([a, b, c])
+            t.append([a, c, d])
+    return np.array(t, dtype=np.int64)
+
+
+def _ellipsoid(center, radii, nu, nv, exponent=1.0):
+    """Superellipsoid-ish body: exponent < 1 makes it boxier."""
+    u = np.linspace(0, 2 * math.pi, nu, endpoint=False)
+    v = np.linspace(-math.pi / 2, math.pi / 2, nv)
+    U, V = np.meshgrid(u, v)
+
+    def sgnpow(x, e):
+        return np.sign(x) * np.abs(x) ** e
+
+    x = radii[0] * sgnpow(np.cos(V), exponent) * sgnpow(np.cos(U), exponent)
+    y = radii[1] * sgnpow(np.sin(V), exponent)
+    z = radii[2] * sgnpow(np.cos(V), exponent) * sgnpow(np.sin(U), exponent)
+    verts = np.stack([x, y, z], axis=-1).reshape(-1, 3) + np.asarray(center)
+    return verts.astype(np.float32), _grid_tris(nu, nv)
+
+
+def _torus(center, R, r, nu, nv, axis="z"):
+    u = np.linspace(0, 2 * math.pi, nu, endpoint=False)
+    v = np.linspace(0, 2 * math.pi, nv, endpoint=False)
+    U, V = np.meshgrid(u, v)
+    x = (R + r * np.cos(V)) * np.cos(U)
+    y = (R + r * np.cos(V)) * np.sin(U)
+    z = r * np.sin(V)
+    p = np.stack([x, y, z], axis=-1).reshape(-1, 3)
+    if axis == "z":
+        p = p[:, [0, 1, 2]]
+    verts = p + np.asarray(center)
+    t = []
+    for j in range(nv):
+        j1 = (j + 1) % nv
+        for i in range(nu):
+            i1 = (i + 1) % nu
+            a, b, c, d = j * nu + i, j * nu + i1, j1 * nu + i1, j1 * nu + i
+            t.append([a, b, c])
+            t.append([a, c, d])
+    return verts.astype(np.float32), np.array(t, dtype=np.int64)
+
+
+def _disk(center, radius, n, axis="z"):
+    ang = np.linspace(0, 2 * math.pi, n, endpoint=False)
+    ring = np.stack([radius * np.cos(ang), radius * np.sin(ang), np.zeros(n)], axis=-1)
+    verts = np.concatenate([[[0, 0, 0]], ring]) + np.asarray(center)
+    t = np.array([[0, 1 + i, 1 + (i + 1) % n] for i in range(n)], dtype=np.int64)
+    return verts.astype(np.float32), t
+
+
+def cornell_box(width=256, height=256, samples=32) -> sc.Scene:
+    """Classic Cornell box (555 units), SURVEY.md §8(d) config CB."""
+    white = sc.diffuse((0.73, 0.73, 0.73))
+    red = sc.diffuse((0.65, 0.05, 0.05))
+    green = sc.diffuse((0.12, 0.45, 0.15))
+    light = sc.emission((1.0, 0.85, 0.6), 40.0)
+    materials = [white, red, green, light]
+    meshes = []
+    L = 555.0
+    meshes.append(sc.Mesh(*_quad((0, 0, 0), (L, 0, 0), (L, 0, L), (0, 0, L)), shader=0))  # floor
+    meshes.append(sc.Mesh(*_quad((0, L, 0), (0, L, L), (L, L, L), (L, L, 0)), shader=0))  # ceiling
+    meshes.append(sc.Mesh(*_quad((0, 0, L), (L, 0, L), (L, L, L), (0, L, L)), shader=0))  # back
+    meshes.append(sc.Mesh(*_quad((L, 0, 0), (L, L, 0), (L, L, L), (L, 0, L)), shader=1))  # left (red)
+    meshes.append(sc.Mesh(*_quad((0, 0, 0), (0, 0, L), (0, L, L), (0, L, 0)), shader=2))  # right (green)
+    meshes.append(sc.Mesh(*_box((185.0, 82.5, 169.0), (165, 165, 165), -0.314), shader=0))
+    meshes.append(sc.Mesh(*_box((368.0, 165.0, 351.0), (165, 330, 165), 0.3), shader=0))
+    meshes.append(sc.Mesh(*_quad((213, L - 1, 227), (343, L - 1, 227), (343, L - 1, 332), (213, L - 1, 332)),
+                          shader=3))
+    cam = sc.Camera(eye=(278.0, 273.0, -800.0), target=(278.0, 273.0, 0.0), up=(0.0, 1.0, 0.0),
+                    fov=math.radians(39.3), nearclip=0.1, farclip=1e5)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.0, 0.0, 0.0),
+                    world_strength=0.0, samples=samples, name="cornell_box")
+
+
+def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
+    """BMW27-class stand-in (SURVEY.md §8(d) config BMW): ~0.7M triangles at
+    detail=1.0, glossy / glass / diffuse materials, two emissive studio panels,
+    dim constant world."""
+    rng = np.random.default_rng(0x5EED + 1)
+    paint = sc.mix(0.25, sc.diffuse((0.55, 0.06, 0.04)), sc.glossy((0.9, 0.9, 0.9), 0.15))
+    chrome = sc.glossy((0.85, 0.85, 0.88), 0.08)
+    glass_m = sc.glass((0.95, 0.97, 1.0), 0.0, 1.45)
+    tyre = sc.diffuse((0.03, 0.03, 0.03))
+    rim = sc.glossy((0.7, 0.7, 0.72), 0.3)
+    floor = sc.diffuse((0.45, 0.45, 0.45))
+    panel = sc.emission((1.0, 0.97, 0.92), 6.0)
+    plastic = sc.mix(0.5, sc.diffuse((0.08, 0.08, 0.09)), sc.glossy((0.5, 0.5, 0.5), 0.35))
+    materials = [paint, chrome, glass_m, tyre, rim, floor, panel, plastic]
+    d = detail
+    meshes = []
+    # car body: boxy superellipsoid hull + cabin
+    meshes.append(sc.Mesh(*_ellipsoid((0, 0.62, 0), (2.2, 0.45, 0.95), int(768 * d), int(320 * d), 0.55),
+                          shader=0, smooth=True))
+    meshes.append(sc.Mesh(*_ellipsoid((-0.25, 1.05, 0), (1.15, 0.42, 0.8), int(384 * d), int(160 * d), 0.7),
+                          shader=2, smooth=True))
+    # wheels: tyre tori + rim disks + spokes
+    for wx in (-1.35, 1.35):
+        for wz in (-0.92, 0.92):
+            v, t = _torus((0, 0, 0), 0.33, 0.13, int(192 * d), int(64 * d))
+            v = v.copy()
+            v += np.array([wx, 0.42, wz], dtype=np.float32)
+            meshes.append(sc.Mesh(v, t, shader=3, smooth=True))
+            zs = wz + (0.06 if wz > 0 else -0.06)
+            v, t = _disk((wx, 0.42, zs), 0.27, int(96 * d))
+            meshes.append(sc.Mesh(v, t, shader=4))
+            for k in range(10):
+                a = 2 * math.pi * k / 10
+                bv, bt = _box((wx + 0.13 * math.cos(a), 0.42 + 0.13 * math.sin(a), zs), (0.2, 0.03, 0.03), 0.0)
+                meshes.append(sc.Mesh(bv, bt, shader=1))
+    # grille / detail: many small chrome and plastic boxes (instancing-free detail)
+    n_detail = int(2500 * d)
+    for k in range(n_detail):
+        x = -2.35 + 0.02 * rng.standard_normal()
+        y = 0.35 + 0.35 * rng.random()
+        z = -0.7 + 1.4 * rng.random()
+        bv, bt = _box((x, y, z), (0.05, 0.02 + 0.02 * rng.random(), 0.02), float(rng.random()))
+        meshes.append(sc.Mesh(bv, bt, shader=1 if k % 3 else 7))
+    # mirrors, spoiler, bumpers
+    meshes.append(sc.Mesh(*_box((2.15, 0.38, 0), (0.2, 0.18, 1.7)), shader=7))
+    meshes.append(sc.Mesh(*_box((-2.15, 0.38, 0), (0.2, 0.18, 1.7)), shader=7))
+    meshes.append(sc.Mesh(*_box((1.9, 1.05, 0), (0.12, 0.05, 1.5), 0.0), shader=0))
+    for z in (-0.95, 0.95):
+        meshes.append(sc.Mesh(*_ellipsoid((0.35, 1.0, z), (0.1, 0.06, 0.05), int(64 * d), int(32 * d)), shader=1,
+                              smooth=True))
+    # studio floor (tessellated) and two emissive panels
+    n = int(64 * d) + 2
+    xs = np.linspace(-12, 12, n)
+    zs = np.linspace(-12, 12, n)
+    X, Z = np.meshgrid(xs, zs)
+    fv = np.stack([X, np.zeros_like(X), Z], axis=-1).reshape(-1, 3).astype(np.float32)
+    meshes.append(sc.Mesh(fv, _grid_tris(n, n, wrap_u=False)[:, [0, 2, 1]], shader=5))
+    meshes.append(sc.Mesh(*_quad((-3, 4.5, -2.5), (3, 4.5, -2.5), (3, 4.5, 2.5), (-3, 4.5, 2.5)), shader=6))
+    meshes.append(sc.Mesh(*_quad((5.5, 0.5, -3), (5.5, 4.0, -3), (5.5, 4.0, 3), (5.5, 0.5, 3)), shader=6))
+    cam = sc.Camera(eye=(5.2, 2.3, 4.6), target=(0.0, 0.6, 0.0), up=(0.0, 1.0, 0.0),
+                    fov=math.radians(38.0), nearclip=0.1, farclip=1000.0)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.18, 0.2, 0.24),
+                    world_strength=0.6, samples=samples, filter_type="blackman_harris",
+                    filter_width=1.5, name="bmw27_standin")
+
+
+CONFIGS = {
+    "cornell_box": cornell_box,
+    "bmw27_standin": bmw27_standin,
+}
