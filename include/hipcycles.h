@@ -67,6 +67,9 @@ typedef struct hipcy_stats {
   double total_ms;      /* first launch to last completion of the tile */
   double closest_ms;    /* closest-hit traversal kernel only */
   uint64_t closest_launches;
+  uint64_t closest_nodes; /* closest-hit traversal only (the roofline kernel) */
+  uint64_t closest_leaves;
+  uint64_t closest_tris;
 } hipcy_stats;
 
 int hipcy_abi_version(void);
@@ -93,10 +96,13 @@ int hipcy_load_kernels(hipcy_device *dev);
 uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *dev); /* BVH_LAYOUT_BVH2 = 1 */
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
+/* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)
+ * and stored contiguously in the buffer: interleaved row sharding across GPUs. */
+int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *tile, int y_step);
 int hipcy_synchronize(hipcy_device *dev);
 int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
-/* 1: collect traversal counters and per-kernel HIP-event timings. */
-int hipcy_set_profiling(hipcy_device *dev, int enable);
+/* flags: bit 0 = per-kernel HIP-event timings, bit 1 = traversal counters. */
+int hipcy_set_profiling(hipcy_device *dev, int flags);
 
 /* rays: n x 8 floats (P.xyz, D.xyz, t, visibility bits) in device memory;
  * out_f: n x 3 (t, u, v); out_i: n x 4 (hit, prim, object, type).

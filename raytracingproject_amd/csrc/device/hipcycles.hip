@@ -106,9 +106,9 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     }
   }
   if (STATS) {
-    stats_add(&stats->nodes, n_nodes);
-    stats_add(&stats->leaves, n_leaves);
-    stats_add(&stats->tris, n_tris);
+    stats_add(&stats[0].nodes, n_nodes);
+    stats_add(&stats[0].leaves, n_leaves);
+    stats_add(&stats[0].tris, n_tris);
   }
 }
 
@@ -181,9 +181,9 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
   }
   queue_push(queue_out, count_out, slot, regen);
   if (STATS) {
-    stats_add(&stats->nodes, n_nodes);
-    stats_add(&stats->leaves, n_leaves);
-    stats_add(&stats->tris, n_tris);
+    stats_add(&stats[1].nodes, n_nodes);
+    stats_add(&stats[1].leaves, n_leaves);
+    stats_add(&stats[1].tris, n_tris);
   }
 }
 
@@ -278,7 +278,7 @@ struct hipcy_device {
   CyStats *stats_dev = nullptr;
   uint *host_counters = nullptr; /* pinned */
 
-  bool profiling = false;
+  int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
 };
@@ -425,7 +425,7 @@ hipcy_device *hipcy_create(int ordinal)
       hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&dev->data_dev, sizeof(hc_KernelData)) != hipSuccess ||
       hipMalloc((void **)&dev->counters, 64) != hipSuccess ||
-      hipMalloc((void **)&dev->stats_dev, sizeof(CyStats)) != hipSuccess ||
+      hipMalloc((void **)&dev->stats_dev, 2 * sizeof(CyStats)) != hipSuccess ||
       hipHostMalloc((void **)&dev->host_counters, 64, hipHostMallocDefault) != hipSuccess) {
     set_error(nullptr, "device context creation failed");
     delete dev;
@@ -609,9 +609,9 @@ int hipcy_load_kernels(hipcy_device *dev)
   return 0;
 }
 
-int hipcy_set_profiling(hipcy_device *dev, int enable)
+int hipcy_set_profiling(hipcy_device *dev, int flags)
 {
-  dev->profiling = enable != 0;
+  dev->profiling = flags;
   return 0;
 }
 
@@ -652,7 +652,19 @@ static int check_device_error(hipcy_device *dev)
   return 0;
 }
 
+static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step);
+
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
+{
+  return path_trace(dev, t, 1);
+}
+
+int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
+{
+  return path_trace(dev, t, y_step < 1 ? 1 : y_step);
+}
+
+static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
 {
   if (!dev->error.empty()) {
     return -1;
@@ -675,6 +687,7 @@ int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
   tile.y = t->y;
   tile.w = t->w;
   tile.h = t->h;
+  tile.y_step = y_step;
   tile.start_sample = t->start_sample;
   tile.end_sample = t->start_sample + t->num_samples;
   tile.offset = t->offset;
@@ -683,11 +696,12 @@ int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
   tile.pass_stride = dev->data_host.film.pass_stride;
 
   memset(&dev->stats, 0, sizeof(dev->stats));
-  const bool prof = dev->profiling;
+  const bool prof = (dev->profiling & 1) != 0;
+  const bool counters = (dev->profiling & 2) != 0;
   hipStream_t s = dev->stream;
   uint *err = dev->counters + 3;
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, s));
-  HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, sizeof(CyStats), s));
+  HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, 2 * sizeof(CyStats), s));
 
   size_t ev = 0;
   hipEvent_t t_begin = get_event(dev, ev++);
@@ -723,29 +737,37 @@ int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
       p.c = get_event(dev, ev++);
       p.d = get_event(dev, ev++);
       HIP_CHECK(dev, hipEventRecord(p.a, s));
+    }
+    if (counters) {
       hipLaunchKernelGGL(k_intersect_closest<true>, grid, block, 0, s, kg, dev->bufs,
                          dev->queue[qa], dev->counters + qa, err, dev->stats_dev);
-      HIP_CHECK(dev, hipEventRecord(p.b, s));
     }
     else {
       hipLaunchKernelGGL(k_intersect_closest<false>, grid, block, 0, s, kg, dev->bufs,
                          dev->queue[qa], dev->counters + qa, err, dev->stats_dev);
+    }
+    if (prof) {
+      HIP_CHECK(dev, hipEventRecord(p.b, s));
     }
     hipLaunchKernelGGL(k_shade, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa],
                        dev->counters + qa, dev->queue[qb], dev->counters + qb, dev->queue[qs],
                        dev->counters + qs, err);
     if (prof) {
       HIP_CHECK(dev, hipEventRecord(p.c, s));
+    }
+    if (counters) {
       hipLaunchKernelGGL(k_intersect_shadow<true>, grid, block, 0, s, kg, dev->bufs, tile,
                          dev->queue[qs], dev->counters + qs, dev->queue[qb], dev->counters + qb,
                          err, dev->stats_dev);
-      HIP_CHECK(dev, hipEventRecord(p.d, s));
-      pairs.push_back(p);
     }
     else {
       hipLaunchKernelGGL(k_intersect_shadow<false>, grid, block, 0, s, kg, dev->bufs, tile,
                          dev->queue[qs], dev->counters + qs, dev->queue[qb], dev->counters + qb,
                          err, dev->stats_dev);
+    }
+    if (prof) {
+      HIP_CHECK(dev, hipEventRecord(p.d, s));
+      pairs.push_back(p);
     }
     HIP_CHECK(dev, hipGetLastError());
     HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
@@ -778,15 +800,20 @@ int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
       shade += b;
       shadow += c;
     }
-    CyStats st;
-    HIP_CHECK(dev, hipMemcpy(&st, dev->stats_dev, sizeof(st), hipMemcpyDeviceToHost));
-    dev->stats.inner_nodes = st.nodes;
-    dev->stats.leaves = st.leaves;
-    dev->stats.triangles = st.tris;
     dev->stats.intersect_ms = closest + shadow;
     dev->stats.closest_ms = closest;
     dev->stats.shade_ms = shade;
     dev->stats.closest_launches = pairs.size();
+  }
+  if (counters) {
+    CyStats st[2];
+    HIP_CHECK(dev, hipMemcpy(st, dev->stats_dev, sizeof(st), hipMemcpyDeviceToHost));
+    dev->stats.inner_nodes = st[0].nodes + st[1].nodes;
+    dev->stats.leaves = st[0].leaves + st[1].leaves;
+    dev->stats.triangles = st[0].tris + st[1].tris;
+    dev->stats.closest_nodes = st[0].nodes;
+    dev->stats.closest_leaves = st[0].leaves;
+    dev->stats.closest_tris = st[0].tris;
   }
   return check_device_error(dev);
 }

@@ -38,6 +38,7 @@ typedef struct CyPathBuffers {
 
 typedef struct CyTile {
   int x, y, w, h;
+  int y_step; /* rows of the tile are image rows y, y+y_step, ... (1 = contiguous) */
   int start_sample, end_sample;
   int offset, stride;
   float *buffer;
@@ -46,7 +47,7 @@ typedef struct CyTile {
 
 typedef struct CyStats {
   unsigned long long nodes, leaves, tris, rays;
-} CyStats;
+} CyStats; /* [0] closest-hit traversal, [1] shadow traversal */
 
 CY_FN hc_float4 mkf4(float x, float y, float z, float w)
 {
@@ -228,7 +229,7 @@ CY_FN cfloat3 path_radiance_clamp(const CyGlobals *kg, cfloat3 L, int bounce)
 
 /* Write the finished sample: kernel_passes.h:338-433 with only the combined pass
  * (kernel_accumulate.h:622-688, use_light_pass == 0, no shadow catcher). */
-CY_FN void write_result(const CyTile *tile, int x, int y, cfloat3 L_emission, float L_transparent)
+CY_FN void write_result(const CyTile *tile, int x, int ybuf, cfloat3 L_emission, float L_transparent)
 {
   cfloat3 L_sum = L_emission;
   float sum = fabsf(L_sum.x) + fabsf(L_sum.y) + fabsf(L_sum.z);
@@ -236,7 +237,7 @@ CY_FN void write_result(const CyTile *tile, int x, int y, cfloat3 L_emission, fl
     L_sum = mk3(0.0f, 0.0f, 0.0f);
   }
   float alpha = 1.0f - L_transparent;
-  float *buf = tile->buffer + (size_t)(tile->offset + x + y * tile->stride) * tile->pass_stride;
+  float *buf = tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
   buf[0] += L_sum.x;
   buf[1] += L_sum.y;
   buf[2] += L_sum.z;
@@ -252,7 +253,7 @@ CY_FN bool slot_regenerate(const CyGlobals *kg,
                            int sample)
 {
   int x = tile->x + slot % tile->w;
-  int y = tile->y + slot / tile->w;
+  int y = tile->y + (slot / tile->w) * tile->y_step;
   for (; sample < tile->end_sample; sample++) {
     uint rng_hash;
     CyRay ray;
@@ -281,9 +282,10 @@ CY_FN bool slot_finish(const CyGlobals *kg,
                        cfloat3 L_emission,
                        float L_transparent)
 {
+  /* buffer row: the tile's rows are stored contiguously (y_step == 1: image row) */
   int x = tile->x + slot % tile->w;
-  int y = tile->y + slot / tile->w;
-  write_result(tile, x, y, L_emission, L_transparent);
+  int ybuf = tile->y + slot / tile->w;
+  write_result(tile, x, ybuf, L_emission, L_transparent);
   return slot_regenerate(kg, b, tile, slot, sample + 1);
 }
 

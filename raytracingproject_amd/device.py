@@ -1,0 +1,205 @@
+"""Python mirror of the Cycles device plugin surface over the HIP C ABI.
+
+``HIPDevice`` follows the method set of ccl::Device (device/device.h:288-500):
+mem_alloc / mem_copy_to / mem_copy_from / mem_zero / mem_free, const_copy_to,
+load_kernels, get_bvh_layout_mask, error_message, and a RENDER task over
+RenderTiles (``render_tile`` = CUDADevice::render, device_cuda_impl.cpp:1853-1952).
+``DeviceScene`` upload mirrors Scene::device_update's copy_to_device of every
+named array (stack B of SURVEY.md §3).
+
+Errors are sticky and raise ``DeviceError`` (Device::set_error semantics).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import native
+from .scene import ELEMENT_BYTES, DeviceScene
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+class DeviceBuffer:
+    """device_memory analogue: a device allocation owned by the device."""
+
+    def __init__(self, device: "HIPDevice", nbytes: int):
+        self.device = device
+        self.nbytes = nbytes
+        self.ptr = device._alloc(nbytes)
+
+    def copy_to_device(self, host: np.ndarray):
+        host = np.ascontiguousarray(host)
+        if host.nbytes > self.nbytes:
+            raise ValueError("copy_to_device overflows the allocation")
+        self.device._check(self.device.lib.hipcy_mem_copy_to(self.device.h, self.ptr, host.ctypes.data, host.nbytes))
+
+    def copy_from_device(self, out: np.ndarray) -> np.ndarray:
+        if not out.flags.c_contiguous or out.nbytes > self.nbytes:
+            raise ValueError("bad host buffer")
+        self.device._check(self.device.lib.hipcy_mem_copy_from(self.device.h, out.ctypes.data, self.ptr, out.nbytes))
+        return out
+
+    def zero(self):
+        self.device._check(self.device.lib.hipcy_mem_zero(self.device.h, self.ptr, self.nbytes))
+
+    def free(self):
+        if self.ptr:
+            self.device._check(self.device.lib.hipcy_mem_free(self.device.h, self.ptr))
+            self.ptr = 0
+
+
+class HIPDevice:
+    def __init__(self, ordinal: int = 0):
+        self.lib = native.device_lib()
+        self.ordinal = ordinal
+        h = self.lib.hipcy_create(ordinal)
+        if not h:
+            raise DeviceError(self.lib.hipcy_global_error().decode())
+        self.h = h
+        self._arrays: dict[str, DeviceBuffer] = {}
+        self.scene: DeviceScene | None = None
+
+    # ---- Device API -------------------------------------------------------
+    @staticmethod
+    def available_devices() -> list[dict]:
+        lib = native.device_lib()
+        n = ctypes.c_int(0)
+        lib.hipcy_device_count(ctypes.byref(n))
+        out = []
+        for i in range(n.value):
+            name = ctypes.create_string_buffer(256)
+            mem = ctypes.c_uint64(0)
+            if lib.hipcy_device_info(i, name, 256, ctypes.byref(mem)) == 0:
+                out.append({"ordinal": i, "name": name.value.decode(), "mem": mem.value, "type": "HIP"})
+        return out
+
+    def error_message(self) -> str:
+        return self.lib.hipcy_error(self.h).decode()
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise DeviceError(self.error_message() or "HIP device error %d" % rc)
+
+    def _alloc(self, nbytes: int) -> int:
+        p = ctypes.c_uint64(0)
+        self._check(self.lib.hipcy_mem_alloc(self.h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def mem_alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def const_copy_to(self, name: str, data) -> None:
+        raw = bytes(data)
+        buf = (ctypes.c_char * len(raw)).from_buffer_copy(raw)
+        self._check(self.lib.hipcy_const_copy_to(self.h, name.encode(), ctypes.addressof(buf), len(raw)))
+
+    def global_alloc(self, name: str, host: np.ndarray) -> DeviceBuffer:
+        """device_vector<T> GLOBAL memory: allocate, copy, bind to the kernel name."""
+        host = np.ascontiguousarray(host)
+        old = self._arrays.pop(name, None)
+        if old is not None:
+            old.free()
+        buf = DeviceBuffer(self, max(host.nbytes, 16))
+        buf.copy_to_device(host)
+        self._check(self.lib.hipcy_bind_global(self.h, name.encode(), buf.ptr, host.nbytes))
+        self._arrays[name] = buf
+        return buf
+
+    def get_bvh_layout_mask(self) -> int:
+        return int(self.lib.hipcy_get_bvh_layout_mask(self.h))
+
+    def load_kernels(self) -> None:
+        self._check(self.lib.hipcy_load_kernels(self.h))
+
+    def set_profiling(self, enable: bool) -> None:
+        self.lib.hipcy_set_profiling(self.h, int(enable))
+
+    def stats(self) -> dict:
+        st = native.Stats()
+        self.lib.hipcy_get_stats(self.h, ctypes.byref(st))
+        return {name: getattr(st, name) for name, _ in native.Stats._fields_}
+
+    # ---- scene upload (Scene::device_update) -------------------------------
+    def upload_scene(self, ds: DeviceScene) -> None:
+        for name, arr in ds.arrays.items():
+            if name not in ELEMENT_BYTES:
+                raise KeyError(name)
+            self.global_alloc(name, arr)
+        self.const_copy_to("__data", ds.data)
+        self.load_kernels()
+        self.scene = ds
+
+    # ---- RENDER task ------------------------------------------------------
+    def render_tile(self, buffer: DeviceBuffer, tile, start_sample: int, num_samples: int,
+                    offset: int, stride: int, y_step: int = 1) -> None:
+        x, y, w, h = tile
+        wt = native.WorkTile(x, y, w, h, start_sample, num_samples, offset, stride, buffer.ptr)
+        if y_step == 1:
+            self._check(self.lib.hipcy_path_trace(self.h, ctypes.byref(wt)))
+        else:
+            self._check(self.lib.hipcy_path_trace_rows(self.h, ctypes.byref(wt), y_step))
+
+    def render(self, samples: int | None = None, start_sample: int = 0, tile=None) -> np.ndarray:
+        """Render (a tile of) the uploaded scene; returns the float render buffer
+        [h, w, pass_stride] of the tile (buffer offset/stride as CPUDevice)."""
+        ds = self.scene
+        samples = ds.samples if samples is None else samples
+        x, y, w, h = tile if tile is not None else (0, 0, ds.width, ds.height)
+        nbytes = w * h * ds.pass_stride * 4
+        buf = self.mem_alloc(nbytes)
+        try:
+            buf.zero()
+            self.render_tile(buf, (x, y, w, h), start_sample, samples, -(x + y * w), w)
+            out = np.zeros((h, w, ds.pass_stride), dtype=np.float32)
+            buf.copy_from_device(out)
+        finally:
+            buf.free()
+        return out
+
+    # ---- test entry points ------------------------------------------------
+    def intersect(self, rays: np.ndarray, any_hit: bool = False):
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        n = rays.shape[0]
+        d_rays = self.mem_alloc(rays.nbytes)
+        d_f = self.mem_alloc(n * 12)
+        d_i = self.mem_alloc(n * 16)
+        try:
+            d_rays.copy_to_device(rays)
+            self._check(self.lib.hipcy_intersect(self.h, d_rays.ptr, d_f.ptr, d_i.ptr, n, int(any_hit)))
+            of = d_f.copy_from_device(np.zeros((n, 3), dtype=np.float32))
+            oi = d_i.copy_from_device(np.zeros((n, 4), dtype=np.int32))
+        finally:
+            for b in (d_rays, d_f, d_i):
+                b.free()
+        return of, oi
+
+    def camera_rays(self, xys: np.ndarray) -> np.ndarray:
+        xys = np.ascontiguousarray(xys, dtype=np.int32)
+        n = xys.shape[0]
+        d_x = self.mem_alloc(xys.nbytes)
+        d_o = self.mem_alloc(n * 32)
+        try:
+            d_x.copy_to_device(xys)
+            self._check(self.lib.hipcy_camera_rays(self.h, d_x.ptr, d_o.ptr, n))
+            out = d_o.copy_from_device(np.zeros((n, 8), dtype=np.float32))
+        finally:
+            d_x.free()
+            d_o.free()
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            for b in self._arrays.values():
+                b.ptr = 0  # freed by hipcy_destroy
+            self.lib.hipcy_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

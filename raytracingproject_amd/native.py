@@ -51,6 +51,7 @@ class Stats(ctypes.Structure):
         ("inner_nodes", ctypes.c_uint64), ("leaves", ctypes.c_uint64), ("triangles", ctypes.c_uint64),
         ("iterations", ctypes.c_uint64), ("intersect_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double), ("closest_ms", ctypes.c_double), ("closest_launches", ctypes.c_uint64),
+        ("closest_nodes", ctypes.c_uint64), ("closest_leaves", ctypes.c_uint64), ("closest_tris", ctypes.c_uint64),
     ]
 
 
@@ -73,6 +74,7 @@ DEVICE_SYMBOLS = {
     "hipcy_load_kernels": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_bvh_layout_mask": (ctypes.c_uint32, [ctypes.c_void_p]),
     "hipcy_path_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile)]),
+    "hipcy_path_trace_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.c_int]),
     "hipcy_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
