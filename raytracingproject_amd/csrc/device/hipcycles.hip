@@ -18,7 +18,7 @@
 #include "hipcycles.h"
 #include "../kernel/cy_integrator.h"
 
-#define CY_BLOCK 256
+
 
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                                                  CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int lds_stack[CY_LDS_STACK * CY_BLOCK];
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*counter) {
     const int slot = queue[i];
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     bool hit = false;
     if (scene_intersect_valid(&ray)) {
       hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err,
-                                  STATS ? &n_nodes : nullptr, &n_leaves, &n_tris);
+                                  STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     if (hit) {
       b.isect[slot] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
@@ -146,6 +147,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
                                                                 CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int lds_stack[CY_LDS_STACK * CY_BLOCK];
   bool regen = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
@@ -161,7 +163,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
       blocked = bvh2_intersect<true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
-                                     STATS ? &n_nodes : nullptr, &n_leaves, &n_tris);
+                                     STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     const hc_float4 sl = b.shadow_L[slot];
     hc_float4 L4 = b.L[slot];
@@ -187,9 +189,10 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
   }
 }
 
-__global__ void k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
+__global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int lds_stack[CY_LDS_STACK * CY_BLOCK];
   if (i >= n) {
     return;
   }
@@ -208,11 +211,13 @@ __global__ void k_test_intersect(CyGlobals kg, const float *rays, float *out_f, 
   isect.type = 0;
   bool hit = false;
   if (scene_intersect_valid(&ray)) {
-    if (any_hit) {
-      hit = bvh2_intersect<true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr);
+    /* scene_intersect: shadow visibility means early exit at the first hit
+     * (bvh_traversal.h:144-146) */
+    if (any_hit || (visibility & PATH_RAY_SHADOW_OPAQUE)) {
+      hit = bvh2_intersect<true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
     }
     else {
-      hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr);
+      hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
     }
   }
   out_f[3 * i + 0] = isect.t;
@@ -824,7 +829,7 @@ int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t o
   CyGlobals kg;
   build_globals(dev, &kg);
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
-  hipLaunchKernelGGL(k_test_intersect, dim3((n + 255) / 256), dim3(256), 0, dev->stream, kg,
+  hipLaunchKernelGGL(k_test_intersect, dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
                      (const float *)rays, (float *)out_f, (int *)out_i, n, any_hit, dev->counters + 3);
   HIP_CHECK(dev, hipGetLastError());
   HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, dev->stream));

@@ -193,6 +193,29 @@ CY_FN bool scene_intersect_valid(const CyRay *ray)
 /* Closest hit (any_hit == false) or opaque-shadow any hit (any_hit == true).
  * Returns true on hit; counters (when non-null) gather traversal statistics for
  * the algorithmic-bytes roofline (inner nodes, leaves, triangle tests). */
+/* Traversal stack (bvh_types.h:30-33: 192 entries).  On the device the first
+ * CY_LDS_STACK entries live in LDS, one column per thread (entry i of thread t
+ * at lds_base[i * CY_BLOCK + t]: 64 consecutive lanes hit 64 consecutive dwords,
+ * conflict-free); deeper entries spill to a private array that is only touched
+ * by rays descending more than CY_LDS_STACK levels below their stack bottom. */
+struct CyStack {
+  int *lds; /* &lds_base[threadIdx.x] or nullptr */
+  int spill[BVH_STACK_SIZE];
+  CY_FN void set(int i, int v)
+  {
+    if (lds && i < CY_LDS_STACK) {
+      lds[i * CY_BLOCK] = v;
+    }
+    else {
+      spill[i] = v;
+    }
+  }
+  CY_FN int get(int i) const
+  {
+    return (lds && i < CY_LDS_STACK) ? lds[i * CY_BLOCK] : spill[i];
+  }
+};
+
 template<bool any_hit>
 CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           const CyRay *ray,
@@ -201,10 +224,12 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           uint *err,
                           uint *cnt_nodes,
                           uint *cnt_leaves,
-                          uint *cnt_tris)
+                          uint *cnt_tris,
+                          int *lds_stack = nullptr)
 {
-  int traversal_stack[BVH_STACK_SIZE];
-  traversal_stack[0] = ENTRYPOINT_SENTINEL;
+  CyStack traversal_stack;
+  traversal_stack.lds = lds_stack;
+  traversal_stack.set(0, ENTRYPOINT_SENTINEL);
   int stack_ptr = 0;
   int node_addr = KD->bvh.root;
   const cfloat3 P = ray->P;
@@ -263,14 +288,14 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
           cy_set_error(err, CY_ERR_BVH_STACK, 0);
           return false;
         }
-        traversal_stack[stack_ptr] = node_addr_child1;
+        traversal_stack.set(stack_ptr, node_addr_child1);
       }
       else {
         if (traverse_mask == 2) {
           node_addr = node_addr_child1;
         }
         else if (traverse_mask == 0) {
-          node_addr = traversal_stack[stack_ptr];
+          node_addr = traversal_stack.get(stack_ptr);
           --stack_ptr;
         }
       }
@@ -283,7 +308,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
       if (prim_addr >= 0) {
         const int prim_addr2 = as_int(leaf.y);
         const uint type = as_uint(leaf.w);
-        node_addr = traversal_stack[stack_ptr];
+        node_addr = traversal_stack.get(stack_ptr);
         --stack_ptr;
         if ((type & PRIMITIVE_ALL) == PRIMITIVE_TRIANGLE) {
           for (; prim_addr < prim_addr2; prim_addr++) {

@@ -215,6 +215,10 @@ enum {
 
 #define CY_MAX_CLOSURE 8
 #define CY_SVM_STACK 32
+/* threads per workgroup of every wavefront kernel, and LDS-resident traversal
+ * stack depth (CY_LDS_STACK * CY_BLOCK * 4 B = 32 KiB per workgroup) */
+#define CY_BLOCK 256
+#define CY_LDS_STACK 32
 
 typedef struct CyRay {
   cfloat3 P;
