@@ -132,7 +132,10 @@ def main():
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        traffic = pmc.get("k_intersect_closest", {}).get("hbm_bytes_per_launch")
+        from raytracingproject_amd.build import kernel_source_digest
+
+        if pmc.get("source_digest") == kernel_source_digest():
+            traffic = pmc.get("k_intersect_closest", {}).get("hbm_bytes_per_launch")
     roofline = {
         "bound": "hbm",
         "kernel": "k_intersect_closest",

@@ -56,6 +56,20 @@ def _sources(*dirs, exts=(".h", ".hip", ".cpp")):
     return out
 
 
+def kernel_source_digest():
+    """sha256 over the device sources: ties a committed profile to the code it measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    deps = _sources(os.path.join(HERE, "csrc", "kernel"), os.path.join(HERE, "csrc", "device"),
+                    os.path.join(REPO, "include"))
+    for path in sorted(deps, key=lambda p: os.path.relpath(p, REPO)):
+        h.update(os.path.relpath(path, REPO).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def build_device(force=False):
     src = os.path.join(HERE, "csrc", "device", "hipcycles.hip")
     out = os.path.join(HERE, "libhipcycles.so")
