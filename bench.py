@@ -77,13 +77,16 @@ def main():
     dev.upload_scene(ds)
     t_upload = time.time() - t0
 
+    from raytracingproject_amd.shard import RowShard
+
     W, H, S = ds.width, ds.height, ds.samples
-    rows = len(range(rank, H, world))
+    shard = RowShard(rank, world, W, H)
+    rows = shard.rows
     buf = dev.mem_alloc(W * rows * ds.pass_stride * 4)
 
     def step():
         buf.zero()
-        dev.render_tile(buf, (0, rank, W, rows), 0, S, -(rank * W), W, y_step=world)
+        dev.render_tile(buf, shard.tile(), 0, S, shard.offset, shard.stride, y_step=shard.y_step)
 
     def barrier():
         if dist is not None:

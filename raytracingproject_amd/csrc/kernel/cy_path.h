@@ -201,7 +201,7 @@ CY_FN bool scene_intersect_valid(const CyRay *ray)
 struct CyStack {
   int *lds; /* &lds_base[threadIdx.x] or nullptr */
   int spill[BVH_STACK_SIZE];
-  CY_FN void set(int i, int v)
+  CY_MFN void set(int i, int v)
   {
     if (lds && i < CY_LDS_STACK) {
       lds[i * CY_BLOCK] = v;
@@ -210,7 +210,7 @@ struct CyStack {
       spill[i] = v;
     }
   }
-  CY_FN int get(int i) const
+  CY_MFN int get(int i) const
   {
     return (lds && i < CY_LDS_STACK) ? lds[i * CY_BLOCK] : spill[i];
   }

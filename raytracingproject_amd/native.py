@@ -14,6 +14,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 DEVICE_LIB = os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
+ABI_VERSION = 1  # HIPCY_ABI_VERSION in include/hipcycles.h
+
+
+def device_lib_path() -> str:
+    return DEVICE_LIB
 
 _host = None
 _dev = None
@@ -95,12 +100,15 @@ def device_lib():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.hipcy_abi_version() != ABI_VERSION:
+            raise NativeLibraryMissing(f"{DEVICE_LIB}: ABI {lib.hipcy_abi_version()} != {ABI_VERSION}; rebuild")
         _dev = lib
     return _dev
 
 
 def hash_uint2(kx: int, ky: int) -> int:
-    """util/util_hash.h:83-93 (host side, for KernelIntegrator.seed)."""
+    """util/util_hash.h:83-93 (host side, for KernelIntegrator.seed); returned as
+    the int32 the seed field holds."""
     M = 0xFFFFFFFF
 
     def rot(x, k):

@@ -21,7 +21,11 @@ CASES = {
 }
 
 PATH_RAY_ALL_VISIBILITY = (1 << 14) - 1
+PATH_RAY_SHADOW_OPAQUE = (1 << 7) | (1 << 8)
 PATH_RAY_SHADOW = (1 << 7) | (1 << 8) | (1 << 9) | (1 << 10)
+# every visibility bit except the opaque-shadow pair, whose presence turns
+# scene_intersect into an any-hit query (bvh/bvh_traversal.h:144-146)
+PATH_RAY_CLOSEST_VISIBILITY = PATH_RAY_ALL_VISIBILITY & ~PATH_RAY_SHADOW_OPAQUE
 
 
 def compile_case(name: str) -> sc.DeviceScene:
@@ -49,7 +53,7 @@ def make_rays(ds: sc.DeviceScene, n: int, seed: int = 7) -> np.ndarray:
     rays[:, :3] = P
     rays[:, 3:6] = D
     rays[:, 6] = np.float32(np.finfo(np.float32).max)
-    vis = np.full(n, PATH_RAY_ALL_VISIBILITY, dtype=np.uint32)
+    vis = np.full(n, PATH_RAY_CLOSEST_VISIBILITY, dtype=np.uint32)
     rays[:, 7] = vis.view(np.float32)
     # a quarter of the rays are finite-length shadow-style segments
     k = n // 4

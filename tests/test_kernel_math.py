@@ -1,0 +1,44 @@
+"""Host checks of the device math that parity depends on (no GPU).
+
+cy_sinf/cy_cosf restate glibc 2.35's sinf/cosf (sysdeps/ieee754/flt-32/s_sinf.c
+algorithm, which the reference CPU kernel calls through util/util_math.h) for
+|x| < 120; the path tracer only takes sines of angles in [-2*pi, 2*pi].
+"""
+import numpy as np
+import pytest
+
+import native_build as nb
+
+
+def _eval(x):
+    lib = nb.sincos()
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = [np.zeros_like(x) for _ in range(4)]
+    lib.sincos_eval(x.ctypes.data, len(x), *[a.ctypes.data for a in out])
+    return out
+
+
+def test_sincos_bit_exact_vs_libm_random():
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-119.0, 119.0, 1 << 20).astype(np.float32)
+    s, c, s_ref, c_ref = _eval(x)
+    assert np.array_equal(s.view(np.uint32), s_ref.view(np.uint32))
+    assert np.array_equal(c.view(np.uint32), c_ref.view(np.uint32))
+
+
+def test_sincos_bit_exact_vs_libm_path_tracer_range():
+    # every float in a slice of [0, 2*pi] (the integrator's angle range), strided
+    lo = np.float32(0.0).view(np.uint32)
+    hi = np.float32(2 * np.pi).view(np.uint32)
+    x = np.arange(lo, hi, 997, dtype=np.uint32).view(np.float32)
+    x = np.concatenate([x, -x])
+    s, c, s_ref, c_ref = _eval(x)
+    assert np.array_equal(s.view(np.uint32), s_ref.view(np.uint32))
+    assert np.array_equal(c.view(np.uint32), c_ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("v", [0.0, -0.0, 1e-45, 1e-30, 3.1415927, -3.1415927, 1.5707964, 6.2831855, 119.9])
+def test_sincos_special_values(v):
+    s, c, s_ref, c_ref = _eval(np.array([v], dtype=np.float32))
+    assert s.view(np.uint32)[0] == s_ref.view(np.uint32)[0]
+    assert c.view(np.uint32)[0] == c_ref.view(np.uint32)[0]
