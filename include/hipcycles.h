@@ -27,6 +27,9 @@
  *                                            (one RenderTile, samples [start, start+num))
  *   hipcy_synchronize                        device_cuda_impl.cpp:1933 cuCtxSynchronize
  *   hipcy_get_bvh_layout_mask                device/device.h:353 get_bvh_layout_mask
+ *   hipcy_set_bvh_width                      (device option) traverse the bound BVH2 as is, or
+ *                                            the 8-wide BVH the device widens it into, like
+ *                                            BVH::pack_nodes/widen_children_nodes bvh/bvh.cpp:149-176
  *   hipcy_intersect / hipcy_camera_rays      test entry points (scene_intersect, bvh/bvh.h:154;
  *                                            kernel_path_trace_setup, kernel_path_common.h:21)
  */
@@ -40,7 +43,7 @@
 extern "C" {
 #endif
 
-#define HIPCY_ABI_VERSION 1
+#define HIPCY_ABI_VERSION 2
 
 typedef struct hipcy_device hipcy_device;
 
@@ -70,6 +73,9 @@ typedef struct hipcy_stats {
   uint64_t closest_nodes; /* closest-hit traversal only (the roofline kernel) */
   uint64_t closest_leaves;
   uint64_t closest_tris;
+  int32_t bvh_width;      /* 2: BVH2 as bound; 8: device-widened 8-wide BVH */
+  int32_t bvh_depth;      /* levels of the 8-wide BVH (0 for BVH2) */
+  uint64_t bvh_bytes;     /* bytes of the traversed node array */
 } hipcy_stats;
 
 int hipcy_abi_version(void);
@@ -94,6 +100,10 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
  * implement; returns 0 or a negative code with a readable hipcy_error(). */
 int hipcy_load_kernels(hipcy_device *dev);
 uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *dev); /* BVH_LAYOUT_BVH2 = 1 */
+/* Traversal structure: 8 (default) widens the bound BVH2 into the device's
+ * 8-wide quantized BVH before the next path_trace/intersect; 2 traverses the
+ * BVH2 exactly as bound (bit-identical visiting order to the reference). */
+int hipcy_set_bvh_width(hipcy_device *dev, int width);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

@@ -17,6 +17,25 @@
 
 #include "hipcycles.h"
 #include "../kernel/cy_integrator.h"
+#include "../kernel/cy_bvh8.h"
+#include "../host/cy_bvh8_collapse.h"
+
+/* Traversal stack in LDS: BVH2 keeps CY_LDS_STACK node addresses per thread,
+ * the 8-wide BVH CY_LDS_STACK8 (node, entry distance) pairs. */
+template<bool WIDE> struct LdsStack {
+  static constexpr int ints = WIDE ? 2 * CY_LDS_STACK8 * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
+};
+
+template<bool WIDE, bool any_hit>
+__device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
+                                               CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
+                                               uint *n_tris, int *lds)
+{
+  if (WIDE) {
+    return bvh8_intersect<any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+  }
+  return bvh2_intersect<any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+}
 
 
 
@@ -69,7 +88,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
   queue_push(queue, counter, slot, active);
 }
 
-template<bool STATS>
+template<bool STATS, bool WIDE>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  const int *queue,
@@ -78,7 +97,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                                                  CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[CY_LDS_STACK * CY_BLOCK];
+  __shared__ int lds_stack[LdsStack<WIDE>::ints];
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*counter) {
     const int slot = queue[i];
@@ -95,8 +114,8 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     CyIsect isect;
     bool hit = false;
     if (scene_intersect_valid(&ray)) {
-      hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err,
-                                  STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
+      hit = scene_traverse<WIDE, false>(&kg, &ray, visibility, &isect, err,
+                                        STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     if (hit) {
       b.isect[slot] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
@@ -135,7 +154,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_shade(CyGlobals kg,
   queue_push(shadow_queue, shadow_count, slot, shadow);
 }
 
-template<bool STATS>
+template<bool STATS, bool WIDE>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
@@ -147,7 +166,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
                                                                 CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[CY_LDS_STACK * CY_BLOCK];
+  __shared__ int lds_stack[LdsStack<WIDE>::ints];
   bool regen = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
@@ -162,8 +181,8 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
     bool blocked = false;
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
-      blocked = bvh2_intersect<true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
-                                     STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
+      blocked = scene_traverse<WIDE, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
+                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     const hc_float4 sl = b.shadow_L[slot];
     hc_float4 L4 = b.L[slot];
@@ -189,10 +208,11 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
   }
 }
 
+template<bool WIDE>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[CY_LDS_STACK * CY_BLOCK];
+  __shared__ int lds_stack[LdsStack<WIDE>::ints];
   if (i >= n) {
     return;
   }
@@ -214,10 +234,10 @@ __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const
     /* scene_intersect: shadow visibility means early exit at the first hit
      * (bvh_traversal.h:144-146) */
     if (any_hit || (visibility & PATH_RAY_SHADOW_OPAQUE)) {
-      hit = bvh2_intersect<true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
+      hit = scene_traverse<WIDE, true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
     }
     else {
-      hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
+      hit = scene_traverse<WIDE, false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
     }
   }
   out_f[3 * i + 0] = isect.t;
@@ -284,6 +304,14 @@ struct hipcy_device {
   uint *host_counters = nullptr; /* pinned */
 
   int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
+
+  /* 8-wide BVH widened from the bound BVH2 (rebuilt when either BVH2 array or
+   * KernelData is re-bound) */
+  int bvh_width = 8;
+  bool bvh8_dirty = true;
+  hc_uint4 *bvh8 = nullptr;
+  size_t bvh8_bytes = 0;
+  int bvh8_depth = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
 };
@@ -322,7 +350,52 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   }
   CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
+  kg->bvh8_nodes = (dev->bvh_width == 8) ? dev->bvh8 : nullptr;
   return true;
+}
+
+/* Widen the bound BVH2 into the 8-wide layout (host collapse of a D2H copy;
+ * the arrays are a few tens of MB even for BMW27-class scenes). */
+static int ensure_bvh8(hipcy_device *dev)
+{
+  if (dev->bvh_width != 8 || !dev->bvh8_dirty) {
+    return 0;
+  }
+  auto nodes = dev->globals.find("__bvh_nodes");
+  auto leaves = dev->globals.find("__bvh_leaf_nodes");
+  if (leaves == dev->globals.end()) {
+    return set_error(dev, "BVH8 collapse: __bvh_leaf_nodes not bound");
+  }
+  std::vector<float> n2, l2;
+  if (nodes != dev->globals.end() && nodes->second.bytes) {
+    n2.resize(nodes->second.bytes / 4);
+    HIP_CHECK(dev, hipMemcpy(n2.data(), (const void *)nodes->second.ptr, nodes->second.bytes,
+                             hipMemcpyDeviceToHost));
+  }
+  l2.resize(leaves->second.bytes / 4);
+  HIP_CHECK(dev, hipMemcpy(l2.data(), (const void *)leaves->second.ptr, leaves->second.bytes,
+                           hipMemcpyDeviceToHost));
+  cybvh8::Collapser col;
+  col.nodes2 = n2.data();
+  col.n_nodes2 = n2.size() / 4;
+  col.leaves2 = l2.data();
+  col.n_leaves2 = l2.size() / 4;
+  if (!col.run(dev->data_host.bvh.root)) {
+    return set_error(dev, "BVH8 collapse: " + col.error);
+  }
+  const size_t bytes = col.out.size() * 4;
+  if (bytes > dev->bvh8_bytes) {
+    if (dev->bvh8) {
+      HIP_CHECK(dev, hipFree(dev->bvh8));
+      dev->bvh8 = nullptr;
+    }
+    HIP_CHECK(dev, hipMalloc((void **)&dev->bvh8, bytes));
+    dev->bvh8_bytes = bytes;
+  }
+  HIP_CHECK(dev, hipMemcpy(dev->bvh8, col.out.data(), bytes, hipMemcpyHostToDevice));
+  dev->bvh8_depth = col.max_depth;
+  dev->bvh8_dirty = false;
+  return 0;
 }
 
 static int ensure_capacity(hipcy_device *dev, size_t slots)
@@ -453,6 +526,7 @@ void hipcy_destroy(hipcy_device *dev)
     hipEventDestroy(e);
   }
   if (dev->pool) hipFree(dev->pool);
+  if (dev->bvh8) hipFree(dev->bvh8);
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
@@ -533,6 +607,9 @@ int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, s
     return set_error(dev, "const_copy_to: KernelData size " + std::to_string(size) +
                               " != " + std::to_string(sizeof(hc_KernelData)));
   }
+  if (!dev->have_data || dev->data_host.bvh.root != ((const hc_KernelData *)host)->bvh.root) {
+    dev->bvh8_dirty = true;
+  }
   memcpy(&dev->data_host, host, size);
   dev->have_data = true;
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
@@ -565,6 +642,18 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
   b.ptr = device_pointer;
   b.bytes = bytes;
   dev->globals[name] = b;
+  if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0) {
+    dev->bvh8_dirty = true;
+  }
+  return 0;
+}
+
+int hipcy_set_bvh_width(hipcy_device *dev, int width)
+{
+  if (width != 2 && width != 8) {
+    return set_error(dev, "set_bvh_width: width must be 2 or 8");
+  }
+  dev->bvh_width = width;
   return 0;
 }
 
@@ -682,11 +771,12 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
   if (slots == 0 || t->num_samples <= 0) {
     return 0;
   }
-  if (ensure_capacity(dev, slots) != 0) {
+  if (ensure_capacity(dev, slots) != 0 || ensure_bvh8(dev) != 0) {
     return -1;
   }
   CyGlobals kg;
   build_globals(dev, &kg);
+  const bool wide = kg.bvh8_nodes != nullptr;
   CyTile tile;
   tile.x = t->x;
   tile.y = t->y;
@@ -701,6 +791,12 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
   tile.pass_stride = dev->data_host.film.pass_stride;
 
   memset(&dev->stats, 0, sizeof(dev->stats));
+  dev->stats.bvh_width = wide ? 8 : 2;
+  dev->stats.bvh_depth = wide ? dev->bvh8_depth : 0;
+  {
+    auto it = dev->globals.find("__bvh_nodes");
+    dev->stats.bvh_bytes = wide ? dev->bvh8_bytes : (it != dev->globals.end() ? it->second.bytes : 0);
+  }
   const bool prof = (dev->profiling & 1) != 0;
   const bool counters = (dev->profiling & 2) != 0;
   hipStream_t s = dev->stream;
@@ -743,13 +839,11 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
       p.d = get_event(dev, ev++);
       HIP_CHECK(dev, hipEventRecord(p.a, s));
     }
-    if (counters) {
-      hipLaunchKernelGGL(k_intersect_closest<true>, grid, block, 0, s, kg, dev->bufs,
-                         dev->queue[qa], dev->counters + qa, err, dev->stats_dev);
-    }
-    else {
-      hipLaunchKernelGGL(k_intersect_closest<false>, grid, block, 0, s, kg, dev->bufs,
-                         dev->queue[qa], dev->counters + qa, err, dev->stats_dev);
+    {
+      auto kfn = counters ? (wide ? k_intersect_closest<true, true> : k_intersect_closest<true, false>)
+                          : (wide ? k_intersect_closest<false, true> : k_intersect_closest<false, false>);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, dev->queue[qa], dev->counters + qa, err,
+                         dev->stats_dev);
     }
     if (prof) {
       HIP_CHECK(dev, hipEventRecord(p.b, s));
@@ -760,15 +854,11 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
     if (prof) {
       HIP_CHECK(dev, hipEventRecord(p.c, s));
     }
-    if (counters) {
-      hipLaunchKernelGGL(k_intersect_shadow<true>, grid, block, 0, s, kg, dev->bufs, tile,
-                         dev->queue[qs], dev->counters + qs, dev->queue[qb], dev->counters + qb,
-                         err, dev->stats_dev);
-    }
-    else {
-      hipLaunchKernelGGL(k_intersect_shadow<false>, grid, block, 0, s, kg, dev->bufs, tile,
-                         dev->queue[qs], dev->counters + qs, dev->queue[qb], dev->counters + qb,
-                         err, dev->stats_dev);
+    {
+      auto kfn = counters ? (wide ? k_intersect_shadow<true, true> : k_intersect_shadow<true, false>)
+                          : (wide ? k_intersect_shadow<false, true> : k_intersect_shadow<false, false>);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qs], dev->counters + qs,
+                         dev->queue[qb], dev->counters + qb, err, dev->stats_dev);
     }
     if (prof) {
       HIP_CHECK(dev, hipEventRecord(p.d, s));
@@ -826,10 +916,14 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
 int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t out_i, int n, int any_hit)
 {
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  if (ensure_bvh8(dev) != 0) {
+    return -1;
+  }
   CyGlobals kg;
   build_globals(dev, &kg);
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
-  hipLaunchKernelGGL(k_test_intersect, dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
+  hipLaunchKernelGGL(kg.bvh8_nodes ? k_test_intersect<true> : k_test_intersect<false>,
+                     dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
                      (const float *)rays, (float *)out_f, (int *)out_i, n, any_hit, dev->counters + 3);
   HIP_CHECK(dev, hipGetLastError());
   HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, dev->stream));

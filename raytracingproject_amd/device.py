@@ -115,8 +115,13 @@ class HIPDevice:
     def load_kernels(self) -> None:
         self._check(self.lib.hipcy_load_kernels(self.h))
 
-    def set_profiling(self, enable: bool) -> None:
-        self.lib.hipcy_set_profiling(self.h, int(enable))
+    def set_profiling(self, flags: int) -> None:
+        """bit 0: HIP-event timing of every kernel launch; bit 1: traversal counters."""
+        self.lib.hipcy_set_profiling(self.h, int(flags))
+
+    def set_bvh_width(self, width: int) -> None:
+        """8 (default): traverse the device-widened 8-wide BVH; 2: the bound BVH2."""
+        self._check(self.lib.hipcy_set_bvh_width(self.h, int(width)))
 
     def stats(self) -> dict:
         st = native.Stats()

@@ -14,7 +14,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 DEVICE_LIB = os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
-ABI_VERSION = 1  # HIPCY_ABI_VERSION in include/hipcycles.h
+ABI_VERSION = 2  # HIPCY_ABI_VERSION in include/hipcycles.h
 
 
 def device_lib_path() -> str:
@@ -57,6 +57,7 @@ class Stats(ctypes.Structure):
         ("iterations", ctypes.c_uint64), ("intersect_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double), ("closest_ms", ctypes.c_double), ("closest_launches", ctypes.c_uint64),
         ("closest_nodes", ctypes.c_uint64), ("closest_leaves", ctypes.c_uint64), ("closest_tris", ctypes.c_uint64),
+        ("bvh_width", ctypes.c_int32), ("bvh_depth", ctypes.c_int32), ("bvh_bytes", ctypes.c_uint64),
     ]
 
 
@@ -83,6 +84,7 @@ DEVICE_SYMBOLS = {
     "hipcy_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hipcy_set_bvh_width": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_intersect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),
     "hipcy_camera_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
 }

@@ -41,9 +41,78 @@ def host_emu(libm_sincos: bool = True):
     else:
         so = build("tools/host_emu.cpp", "libhost_emu_dsin.so")
     lib = ctypes.CDLL(so)
-    vp, ci = ctypes.c_void_p, ctypes.c_int
-    lib.emu_render.argtypes = [vp, ci, vp, vp, vp] + [ci] * 9
+    vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+    lib.emu_render.argtypes = [vp, ci, vp, vp, vp, vp] + [ci] * 9
+    lib.emu_intersect.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, vp, vp, vp]
+    lib.emu_bvh8_build.restype = cl
+    lib.emu_bvh8_build.argtypes = [vp, cl, vp, cl, ci, vp, cl, vp, ctypes.c_char_p, ci]
     return lib
+
+
+class EmuScene:
+    """A DeviceScene bound for the host emulator (pointers kept alive)."""
+
+    def __init__(self, lib, ds, bvh_width=2):
+        import numpy as np
+
+        self.lib, self.ds = lib, ds
+        self.names = list(ds.arrays)
+        self.arrs = [np.ascontiguousarray(ds.arrays[n]) for n in self.names]
+        self.c_names = (ctypes.c_char_p * len(self.names))(*[n.encode() for n in self.names])
+        self.c_ptrs = (ctypes.c_void_p * len(self.names))(*[a.ctypes.data for a in self.arrs])
+        self.data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
+        self.bvh8 = bvh8_build(lib, ds)[0] if bvh_width == 8 else None
+
+    @property
+    def bvh8_ptr(self):
+        return None if self.bvh8 is None else self.bvh8.ctypes.data
+
+    def args(self):
+        return (ctypes.addressof(self.data), len(self.names), self.c_names, self.c_ptrs, self.bvh8_ptr)
+
+    def intersect(self, rays, any_hit=False):
+        import numpy as np
+
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        n = len(rays)
+        of = np.zeros((n, 3), dtype=np.float32)
+        oi = np.zeros((n, 4), dtype=np.int32)
+        cnt = np.zeros(3, dtype=np.uint64)
+        err = self.lib.emu_intersect(*self.args(), rays.ctypes.data, n, int(any_hit), of.ctypes.data,
+                                     oi.ctypes.data, cnt.ctypes.data)
+        assert err == 0, hex(err)
+        return of, oi, cnt
+
+    def render(self, tile=None, start_sample=0, samples=None, offset=None, out=None):
+        import numpy as np
+
+        ds = self.ds
+        samples = ds.samples if samples is None else samples
+        x, y, w, h = tile if tile is not None else (0, 0, ds.width, ds.height)
+        buf = out if out is not None else np.zeros((h, w, ds.pass_stride), dtype=np.float32)
+        off = -(x + y * w) if offset is None else offset
+        err = self.lib.emu_render(*self.args(), buf.ctypes.data, x, y, w, h, start_sample, samples, off, w,
+                                  ds.pass_stride)
+        assert err == 0, hex(err)
+        return buf
+
+
+def bvh8_build(lib, ds):
+    """Widen the scene's BVH2 exactly like the device library; returns
+    (uint32 array of 32 words per node, depth)."""
+    import numpy as np
+
+    nodes = np.ascontiguousarray(ds.arrays["__bvh_nodes"], dtype=np.float32).reshape(-1)
+    leaves = np.ascontiguousarray(ds.arrays["__bvh_leaf_nodes"], dtype=np.float32).reshape(-1)
+    cap = 32 * (len(leaves) // 4 + 2)
+    out = np.zeros(cap, dtype=np.uint32)
+    depth = ctypes.c_int(0)
+    err = ctypes.create_string_buffer(256)
+    n = lib.emu_bvh8_build(nodes.ctypes.data, len(nodes) // 4, leaves.ctypes.data, len(leaves) // 4,
+                           int(ds.data.bvh.root), out.ctypes.data, cap, ctypes.byref(depth), err, 256)
+    if n < 0:
+        raise RuntimeError(err.value.decode())
+    return out[:n].copy(), depth.value
 
 
 def sincos():

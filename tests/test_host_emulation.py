@@ -2,8 +2,6 @@
 compiled for the host and driven path by path (tools/host_emu.cpp) renders
 bit-identically to the reference CPU kernel's golden buffers.  This pins the
 device LOGIC on CPU; tests/test_gpu_parity.py pins the GPU arithmetic."""
-import ctypes
-
 import numpy as np
 import pytest
 
@@ -11,20 +9,8 @@ import native_build as nb
 from parity_cases import CASES, compile_case, load_golden
 
 
-def emu_render(lib, ds, tile=None, start_sample=0, samples=None, offset=None, out=None):
-    samples = ds.samples if samples is None else samples
-    x, y, w, h = tile if tile is not None else (0, 0, ds.width, ds.height)
-    names = list(ds.arrays)
-    arrs = [np.ascontiguousarray(ds.arrays[n]) for n in names]
-    c_names = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
-    c_ptrs = (ctypes.c_void_p * len(names))(*[a.ctypes.data for a in arrs])
-    data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
-    buf = out if out is not None else np.zeros((h, w, ds.pass_stride), dtype=np.float32)
-    off = -(x + y * w) if offset is None else offset
-    err = lib.emu_render(ctypes.addressof(data), len(names), c_names, c_ptrs, buf.ctypes.data,
-                         x, y, w, h, start_sample, samples, off, w, ds.pass_stride)
-    assert err == 0, hex(err)
-    return buf
+def emu_render(lib, ds, tile=None, start_sample=0, samples=None, offset=None, out=None, bvh_width=2):
+    return nb.EmuScene(lib, ds, bvh_width).render(tile, start_sample, samples, offset, out)
 
 
 @pytest.fixture(scope="module")

@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 def load(variant="libhost_emu.so"):
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", variant))
     vp, ci = ctypes.c_void_p, ctypes.c_int
-    lib.emu_render.argtypes = [vp, ci, vp, vp, vp] + [ci] * 9
+    lib.emu_render.argtypes = [vp, ci, vp, vp, vp, vp] + [ci] * 9
     return lib
 
 
@@ -28,7 +28,7 @@ def render(ds, lib=None, samples=None, start_sample=0, tile=None):
     c_ptrs = (ctypes.c_void_p * len(names))(*[a.ctypes.data for a in arrs])
     data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
     buf = np.zeros((h, w, ds.pass_stride), dtype=np.float32)
-    err = lib.emu_render(ctypes.addressof(data), len(names), c_names, c_ptrs, buf.ctypes.data,
+    err = lib.emu_render(ctypes.addressof(data), len(names), c_names, c_ptrs, None, buf.ctypes.data,
                          x, y, w, h, start_sample, samples, -(x + y * w), w, ds.pass_stride)
     if err:
         raise RuntimeError("emulator device error %x" % err)

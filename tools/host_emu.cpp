@@ -7,16 +7,131 @@
  * reference kernel, so any difference against oracle/_ref isolates a logic
  * difference of the restatement from GPU arithmetic.  Not part of the product.
  */
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "../raytracingproject_amd/csrc/kernel/cy_integrator.h"
+#include "../raytracingproject_amd/csrc/kernel/cy_bvh8.h"
+#include "../raytracingproject_amd/csrc/host/cy_bvh8_collapse.h"
+
+/* Widen a packed BVH2 like the device library does (hipcycles.hip ensure_bvh8).
+ * Returns the number of uint32 written (32 per node), or -1 with the reason
+ * copied to err_out. */
+extern "C" long emu_bvh8_build(const float *nodes2,
+                               long n_nodes2,
+                               const float *leaves2,
+                               long n_leaves2,
+                               int root,
+                               uint32_t *out,
+                               long out_cap,
+                               int *depth,
+                               char *err_out,
+                               int err_len)
+{
+  cybvh8::Collapser col;
+  col.nodes2 = nodes2;
+  col.n_nodes2 = (size_t)n_nodes2;
+  col.leaves2 = leaves2;
+  col.n_leaves2 = (size_t)n_leaves2;
+  if (!col.run(root)) {
+    snprintf(err_out, err_len, "%s", col.error.c_str());
+    return -1;
+  }
+  if ((long)col.out.size() > out_cap) {
+    snprintf(err_out, err_len, "output capacity %ld < %zu", out_cap, col.out.size());
+    return -1;
+  }
+  memcpy(out, col.out.data(), col.out.size() * 4);
+  *depth = col.max_depth;
+  return (long)col.out.size();
+}
+
+static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char **names, const void **ptrs,
+                     const void *bvh8)
+{
+  memset(kg, 0, sizeof(*kg));
+  kg->data = (const hc_KernelData *)data;
+  for (int i = 0; i < n_arrays; i++) {
+#define CY_BIND(type, name) \
+  if (strcmp(names[i], #name) == 0) \
+    kg->name = (const type *)ptrs[i];
+    CY_GLOBAL_ARRAYS(CY_BIND)
+#undef CY_BIND
+  }
+  kg->bvh8_nodes = (const hc_uint4 *)bvh8;
+}
+
+template<bool any_hit>
+static bool emu_traverse(const CyGlobals *kg, const CyRay *ray, uint vis, CyIsect *isect, uint *err,
+                         uint *nn, uint *nl, uint *nt)
+{
+  if (kg->bvh8_nodes) {
+    return bvh8_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+  }
+  return bvh2_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+}
+
+/* scene_intersect on host: rays n x 8 (P, D, t, visibility bits) like
+ * k_test_intersect; counters[3] = inner nodes, leaves, triangle tests. */
+extern "C" int emu_intersect(const void *data,
+                             int n_arrays,
+                             const char **names,
+                             const void **ptrs,
+                             const void *bvh8,
+                             const float *rays,
+                             int n,
+                             int any_hit,
+                             float *out_f,
+                             int *out_i,
+                             unsigned long long *counters)
+{
+  CyGlobals kg;
+  emu_bind(&kg, data, n_arrays, names, ptrs, bvh8);
+  uint err = 0;
+  for (int i = 0; i < n; i++) {
+    const float *r = rays + 8 * i;
+    CyRay ray;
+    ray.P = mk3(r[0], r[1], r[2]);
+    ray.D = mk3(r[3], r[4], r[5]);
+    ray.t = r[6];
+    const uint visibility = as_uint(r[7]);
+    CyIsect isect;
+    isect.t = ray.t;
+    isect.u = isect.v = 0.0f;
+    isect.prim = PRIM_NONE;
+    isect.object = OBJECT_NONE;
+    isect.type = 0;
+    bool hit = false;
+    uint nn = 0, nl = 0, nt = 0;
+    if (scene_intersect_valid(&ray)) {
+      if (any_hit || (visibility & PATH_RAY_SHADOW_OPAQUE)) {
+        hit = emu_traverse<true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, &err, &nn, &nl, &nt);
+      }
+      else {
+        hit = emu_traverse<false>(&kg, &ray, visibility, &isect, &err, &nn, &nl, &nt);
+      }
+    }
+    counters[0] += nn;
+    counters[1] += nl;
+    counters[2] += nt;
+    out_f[3 * i + 0] = isect.t;
+    out_f[3 * i + 1] = isect.u;
+    out_f[3 * i + 2] = isect.v;
+    out_i[4 * i + 0] = hit ? 1 : 0;
+    out_i[4 * i + 1] = isect.prim;
+    out_i[4 * i + 2] = isect.object;
+    out_i[4 * i + 3] = isect.type;
+  }
+  return (int)err;
+}
 
 extern "C" int emu_render(const void *data,
                           int n_arrays,
                           const char **names,
                           const void **ptrs,
+                          const void *bvh8,
                           float *buffer,
                           int tx,
                           int ty,
@@ -29,15 +144,7 @@ extern "C" int emu_render(const void *data,
                           int pass_stride)
 {
   CyGlobals kg;
-  memset(&kg, 0, sizeof(kg));
-  kg.data = (const hc_KernelData *)data;
-  for (int i = 0; i < n_arrays; i++) {
-#define CY_BIND(type, name) \
-  if (strcmp(names[i], #name) == 0) \
-    kg.name = (const type *)ptrs[i];
-    CY_GLOBAL_ARRAYS(CY_BIND)
-#undef CY_BIND
-  }
+  emu_bind(&kg, data, n_arrays, names, ptrs, bvh8);
   hc_float4 rec[12];
   int isect_type = 0;
   hc_uint4 s0, s1;
@@ -83,7 +190,7 @@ extern "C" int emu_render(const void *data,
           CyIsect isect;
           bool hit = false;
           if (scene_intersect_valid(&ray)) {
-            hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, &err, nullptr, nullptr, nullptr);
+            hit = emu_traverse<false>(&kg, &ray, visibility, &isect, &err, nullptr, nullptr, nullptr);
           }
           if (hit) {
             rec[2] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
@@ -105,7 +212,7 @@ extern "C" int emu_render(const void *data,
             bool blocked = false;
             if (scene_intersect_valid(&sr)) {
               CyIsect si;
-              blocked = bvh2_intersect<true>(&kg, &sr, PATH_RAY_SHADOW_OPAQUE, &si, &err, nullptr, nullptr, nullptr);
+              blocked = emu_traverse<true>(&kg, &sr, PATH_RAY_SHADOW_OPAQUE, &si, &err, nullptr, nullptr, nullptr);
             }
             hc_float4 sl = rec[8];
             hc_float4 L4 = rec[5];
