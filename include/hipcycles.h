@@ -27,8 +27,8 @@
  *                                            (one RenderTile, samples [start, start+num))
  *   hipcy_synchronize                        device_cuda_impl.cpp:1933 cuCtxSynchronize
  *   hipcy_get_bvh_layout_mask                device/device.h:353 get_bvh_layout_mask
- *   hipcy_set_bvh_width                      (device option) traverse the bound BVH2 as is, or
- *                                            the 8-wide BVH the device widens it into, like
+ *   hipcy_set_bvh_width / _leaf_merge        (device options) traverse the bound BVH2 as is, or
+ *                                            the 4/8-wide BVH the device widens it into, like
  *                                            BVH::pack_nodes/widen_children_nodes bvh/bvh.cpp:149-176
  *   hipcy_intersect / hipcy_camera_rays      test entry points (scene_intersect, bvh/bvh.h:154;
  *                                            kernel_path_trace_setup, kernel_path_common.h:21)
@@ -73,8 +73,8 @@ typedef struct hipcy_stats {
   uint64_t closest_nodes; /* closest-hit traversal only (the roofline kernel) */
   uint64_t closest_leaves;
   uint64_t closest_tris;
-  int32_t bvh_width;      /* 2: BVH2 as bound; 8: device-widened 8-wide BVH */
-  int32_t bvh_depth;      /* levels of the 8-wide BVH (0 for BVH2) */
+  int32_t bvh_width;      /* 2: BVH2 as bound; 4/8: device-widened wide BVH */
+  int32_t bvh_depth;      /* levels of the wide BVH (0 for BVH2) */
   uint64_t bvh_bytes;     /* bytes of the traversed node array */
 } hipcy_stats;
 
@@ -100,10 +100,17 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
  * implement; returns 0 or a negative code with a readable hipcy_error(). */
 int hipcy_load_kernels(hipcy_device *dev);
 uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *dev); /* BVH_LAYOUT_BVH2 = 1 */
-/* Traversal structure: 8 (default) widens the bound BVH2 into the device's
- * 8-wide quantized BVH before the next path_trace/intersect; 2 traverses the
- * BVH2 exactly as bound (bit-identical visiting order to the reference). */
+/* Traversal structure: 4 (default) or 8 widens the bound BVH2 into the
+ * device's 4- or 8-wide BVH before the next path_trace/intersect; 2 traverses
+ * the BVH2 exactly as bound (bit-identical visiting order to the reference). */
 int hipcy_set_bvh_width(hipcy_device *dev, int width);
+/* Wide BVH only: BVH2 subtrees holding at most max_prims (0..15) primitives in
+ * one contiguous range become a single leaf child (0 = keep BVH2 leaves). */
+int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims);
+/* Path slots kept in flight (default 2^20) and the byte budget of the
+ * per-sample record buffer of one pass (default 4 GiB; a tile whose samples do
+ * not fit is rendered in several sample passes).  0 keeps a value. */
+int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

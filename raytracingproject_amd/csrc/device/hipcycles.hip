@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -17,24 +18,26 @@
 
 #include "hipcycles.h"
 #include "../kernel/cy_integrator.h"
-#include "../kernel/cy_bvh8.h"
-#include "../host/cy_bvh8_collapse.h"
+#include "../kernel/cy_bvhw.h"
+#include "../host/cy_bvhw_collapse.h"
 
 /* Traversal stack in LDS: BVH2 keeps CY_LDS_STACK node addresses per thread,
- * the 8-wide BVH CY_LDS_STACK8 (node, entry distance) pairs. */
-template<bool WIDE> struct LdsStack {
-  static constexpr int ints = WIDE ? 2 * CY_LDS_STACK8 * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
+ * the wide BVHs CY_LDS_STACKW (node, entry distance) pairs. */
+template<int W> struct LdsStack {
+  static constexpr int ints = W > 2 ? 2 * CY_LDS_STACKW * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
 };
 
-template<bool WIDE, bool any_hit>
+template<int W, bool any_hit>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
                                                uint *n_tris, int *lds)
 {
-  if (WIDE) {
-    return bvh8_intersect<any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+  if constexpr (W > 2) {
+    return bvhw_intersect<W, any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
   }
-  return bvh2_intersect<any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+  else {
+    return bvh2_intersect<any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+  }
 }
 
 
@@ -74,21 +77,57 @@ __device__ __forceinline__ void stats_add(unsigned long long *dst, uint v)
   }
 }
 
+/* Claim the next work item for every lane with need set (one atomic per wave)
+ * and start it; samples without a camera ray are recorded as such and the lane
+ * claims again.  Returns true when the slot holds a new path. */
+__device__ __forceinline__ bool slot_refill(const CyGlobals &kg, const CyPathBuffers &b, const CyTile &tile,
+                                            int slot, bool need)
+{
+  const unsigned long long mask = __ballot(need);
+  if (mask == 0) {
+    return false;
+  }
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  uint base = 0;
+  if (lane == leader) {
+    base = atomicAdd(tile.work_next, (uint)__popcll(mask));
+  }
+  base = __shfl(base, leader);
+  uint item = base + (uint)__popcll(mask & ((1ull << lane) - 1ull));
+  while (need) {
+    if (item >= tile.n_items) {
+      return false;
+    }
+    if (slot_start(&kg, &b, &tile, slot, item)) {
+      return true;
+    }
+    item = atomicAdd(tile.work_next, 1u);
+  }
+  return false;
+}
+
 __global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
                                                           CyPathBuffers b,
                                                           CyTile tile,
+                                                          int n_slots,
                                                           int *queue,
                                                           uint *counter)
 {
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  bool active = false;
-  if (slot < tile.w * tile.h) {
-    active = slot_regenerate(&kg, &b, &tile, slot, tile.start_sample);
-  }
+  const bool active = slot_refill(kg, b, tile, slot, slot < n_slots);
   queue_push(queue, counter, slot, active);
 }
 
-template<bool STATS, bool WIDE>
+__global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
+{
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < tile.w * tile.h) {
+    accumulate_pixel(&tile, p);
+  }
+}
+
+template<bool STATS, int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  const int *queue,
@@ -97,7 +136,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                                                  CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[LdsStack<WIDE>::ints];
+  __shared__ int lds_stack[LdsStack<W>::ints];
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*counter) {
     const int slot = queue[i];
@@ -114,7 +153,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     CyIsect isect;
     bool hit = false;
     if (scene_intersect_valid(&ray)) {
-      hit = scene_traverse<WIDE, false>(&kg, &ray, visibility, &isect, err,
+      hit = scene_traverse<W, false>(&kg, &ray, visibility, &isect, err,
                                         STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     if (hit) {
@@ -144,17 +183,18 @@ __global__ void __launch_bounds__(CY_BLOCK) k_shade(CyGlobals kg,
                                                      uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool cont = false, shadow = false;
+  bool cont = false, shadow = false, finished = false;
   int slot = 0;
   if (i < (int)*count_in) {
     slot = queue_in[i];
-    cont = shade_path(&kg, &b, &tile, slot, &shadow, err);
+    cont = shade_path(&kg, &b, &tile, slot, &shadow, &finished, err);
   }
+  cont |= slot_refill(kg, b, tile, slot, finished);
   queue_push(queue_out, count_out, slot, cont);
   queue_push(shadow_queue, shadow_count, slot, shadow);
 }
 
-template<bool STATS, bool WIDE>
+template<bool STATS, int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
@@ -166,8 +206,8 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
                                                                 CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[LdsStack<WIDE>::ints];
-  bool regen = false;
+  __shared__ int lds_stack[LdsStack<W>::ints];
+  bool finished = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*shadow_count) {
@@ -181,7 +221,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
     bool blocked = false;
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
-      blocked = scene_traverse<WIDE, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
+      blocked = scene_traverse<W, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
                                            STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     const hc_float4 sl = b.shadow_L[slot];
@@ -192,14 +232,14 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
       L4.z = L4.z + sl.z;
     }
     if (sl.w != 0.0f) {
-      const int sample = (int)b.state0[slot].w;
-      const float L_transparent = b.throughput[slot].w;
-      regen = slot_finish(&kg, &b, &tile, slot, sample, mk3(L4.x, L4.y, L4.z), L_transparent);
+      slot_finish(&b, &tile, slot, mk3(L4.x, L4.y, L4.z), b.throughput[slot].w);
+      finished = true;
     }
     else {
       b.L[slot] = L4;
     }
   }
+  const bool regen = slot_refill(kg, b, tile, slot, finished);
   queue_push(queue_out, count_out, slot, regen);
   if (STATS) {
     stats_add(&stats[1].nodes, n_nodes);
@@ -208,11 +248,11 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
   }
 }
 
-template<bool WIDE>
+template<int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[LdsStack<WIDE>::ints];
+  __shared__ int lds_stack[LdsStack<W>::ints];
   if (i >= n) {
     return;
   }
@@ -234,10 +274,10 @@ __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const
     /* scene_intersect: shadow visibility means early exit at the first hit
      * (bvh_traversal.h:144-146) */
     if (any_hit || (visibility & PATH_RAY_SHADOW_OPAQUE)) {
-      hit = scene_traverse<WIDE, true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
+      hit = scene_traverse<W, true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
     }
     else {
-      hit = scene_traverse<WIDE, false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
+      hit = scene_traverse<W, false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
     }
   }
   out_f[3 * i + 0] = isect.t;
@@ -305,13 +345,21 @@ struct hipcy_device {
 
   int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
 
-  /* 8-wide BVH widened from the bound BVH2 (rebuilt when either BVH2 array or
-   * KernelData is re-bound) */
-  int bvh_width = 8;
-  bool bvh8_dirty = true;
-  hc_uint4 *bvh8 = nullptr;
-  size_t bvh8_bytes = 0;
-  int bvh8_depth = 0;
+  /* path slots in flight and the per-sample record buffer of one pass */
+  size_t slots_wanted = (size_t)1 << 20;
+  size_t record_budget = (size_t)4 << 30; /* bytes of sample records per pass */
+  hc_float4 *records = nullptr;
+  size_t records_capacity = 0;
+
+  /* W-wide BVH widened from the bound BVH2 (rebuilt when either BVH2 array,
+   * the root or the width changes) */
+  int bvh_width = 4;
+  int bvh_merge_prims = 0;
+  bool bvhw_dirty = true;
+  void *bvhw = nullptr;
+  size_t bvhw_bytes = 0;
+  size_t bvhw_capacity = 0;
+  int bvhw_depth = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
 };
@@ -350,21 +398,21 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   }
   CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
-  kg->bvh8_nodes = (dev->bvh_width == 8) ? dev->bvh8 : nullptr;
+  kg->bvhw_nodes = (dev->bvh_width > 2) ? dev->bvhw : nullptr;
   return true;
 }
 
-/* Widen the bound BVH2 into the 8-wide layout (host collapse of a D2H copy;
+/* Widen the bound BVH2 into the W-wide layout (host collapse of a D2H copy;
  * the arrays are a few tens of MB even for BMW27-class scenes). */
-static int ensure_bvh8(hipcy_device *dev)
+static int ensure_bvhw(hipcy_device *dev)
 {
-  if (dev->bvh_width != 8 || !dev->bvh8_dirty) {
+  if (dev->bvh_width == 2 || !dev->bvhw_dirty) {
     return 0;
   }
   auto nodes = dev->globals.find("__bvh_nodes");
   auto leaves = dev->globals.find("__bvh_leaf_nodes");
   if (leaves == dev->globals.end()) {
-    return set_error(dev, "BVH8 collapse: __bvh_leaf_nodes not bound");
+    return set_error(dev, "BVH widening: __bvh_leaf_nodes not bound");
   }
   std::vector<float> n2, l2;
   if (nodes != dev->globals.end() && nodes->second.bytes) {
@@ -375,26 +423,29 @@ static int ensure_bvh8(hipcy_device *dev)
   l2.resize(leaves->second.bytes / 4);
   HIP_CHECK(dev, hipMemcpy(l2.data(), (const void *)leaves->second.ptr, leaves->second.bytes,
                            hipMemcpyDeviceToHost));
-  cybvh8::Collapser col;
+  cybvhw::Collapser col;
+  col.width = dev->bvh_width;
+  col.merge_prims = dev->bvh_merge_prims;
   col.nodes2 = n2.data();
   col.n_nodes2 = n2.size() / 4;
   col.leaves2 = l2.data();
   col.n_leaves2 = l2.size() / 4;
   if (!col.run(dev->data_host.bvh.root)) {
-    return set_error(dev, "BVH8 collapse: " + col.error);
+    return set_error(dev, "BVH widening: " + col.error);
   }
   const size_t bytes = col.out.size() * 4;
-  if (bytes > dev->bvh8_bytes) {
-    if (dev->bvh8) {
-      HIP_CHECK(dev, hipFree(dev->bvh8));
-      dev->bvh8 = nullptr;
+  if (bytes > dev->bvhw_capacity) {
+    if (dev->bvhw) {
+      HIP_CHECK(dev, hipFree(dev->bvhw));
+      dev->bvhw = nullptr;
     }
-    HIP_CHECK(dev, hipMalloc((void **)&dev->bvh8, bytes));
-    dev->bvh8_bytes = bytes;
+    HIP_CHECK(dev, hipMalloc(&dev->bvhw, bytes));
+    dev->bvhw_capacity = bytes;
   }
-  HIP_CHECK(dev, hipMemcpy(dev->bvh8, col.out.data(), bytes, hipMemcpyHostToDevice));
-  dev->bvh8_depth = col.max_depth;
-  dev->bvh8_dirty = false;
+  HIP_CHECK(dev, hipMemcpy(dev->bvhw, col.out.data(), bytes, hipMemcpyHostToDevice));
+  dev->bvhw_bytes = bytes;
+  dev->bvhw_depth = col.max_depth;
+  dev->bvhw_dirty = false;
   return 0;
 }
 
@@ -407,10 +458,10 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     hipFree(dev->pool);
     dev->pool = nullptr;
   }
-  /* 12 float4 records + 1 int per slot + 3 queues */
+  /* 12 float4 records + 2 ints per slot (queues are separate) */
   const size_t rec = 16 * slots;
   const size_t ints = 4 * slots;
-  const size_t total = 12 * rec + ints + 3 * ints + 256;
+  const size_t total = 12 * rec + 2 * ints + 14 * 256;
   HIP_CHECK(dev, hipMalloc((void **)&dev->pool, total));
   char *p = dev->pool;
   auto take = [&](size_t n) {
@@ -430,6 +481,7 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   dev->bufs.shadow_P = (hc_float4 *)take(rec);
   dev->bufs.shadow_D = (hc_float4 *)take(rec);
   dev->bufs.shadow_L = (hc_float4 *)take(rec);
+  dev->bufs.item = (uint *)take(ints);
   dev->capacity = slots;
   /* queues live in their own allocation (3 x slots ints) */
   for (int q = 0; q < 3; q++) {
@@ -526,7 +578,8 @@ void hipcy_destroy(hipcy_device *dev)
     hipEventDestroy(e);
   }
   if (dev->pool) hipFree(dev->pool);
-  if (dev->bvh8) hipFree(dev->bvh8);
+  if (dev->bvhw) hipFree(dev->bvhw);
+  if (dev->records) hipFree(dev->records);
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
@@ -608,7 +661,7 @@ int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, s
                               " != " + std::to_string(sizeof(hc_KernelData)));
   }
   if (!dev->have_data || dev->data_host.bvh.root != ((const hc_KernelData *)host)->bvh.root) {
-    dev->bvh8_dirty = true;
+    dev->bvhw_dirty = true;
   }
   memcpy(&dev->data_host, host, size);
   dev->have_data = true;
@@ -643,17 +696,32 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
   b.bytes = bytes;
   dev->globals[name] = b;
   if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0) {
-    dev->bvh8_dirty = true;
+    dev->bvhw_dirty = true;
   }
   return 0;
 }
 
 int hipcy_set_bvh_width(hipcy_device *dev, int width)
 {
-  if (width != 2 && width != 8) {
-    return set_error(dev, "set_bvh_width: width must be 2 or 8");
+  if (width != 2 && width != 4 && width != 8) {
+    return set_error(dev, "set_bvh_width: width must be 2, 4 or 8");
+  }
+  if (width != dev->bvh_width) {
+    dev->bvhw_dirty = true;
   }
   dev->bvh_width = width;
+  return 0;
+}
+
+int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims)
+{
+  if (max_prims < 0 || max_prims > 15) {
+    return set_error(dev, "set_bvh_leaf_merge: max_prims must be in [0, 15]");
+  }
+  if (max_prims != dev->bvh_merge_prims) {
+    dev->bvhw_dirty = true;
+  }
+  dev->bvh_merge_prims = max_prims;
   return 0;
 }
 
@@ -758,6 +826,105 @@ int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *t, int y_ste
   return path_trace(dev, t, y_step < 1 ? 1 : y_step);
 }
 
+static int ensure_records(hipcy_device *dev, size_t n)
+{
+  if (n <= dev->records_capacity) {
+    return 0;
+  }
+  if (dev->records) {
+    HIP_CHECK(dev, hipFree(dev->records));
+    dev->records = nullptr;
+  }
+  HIP_CHECK(dev, hipMalloc((void **)&dev->records, n * sizeof(hc_float4)));
+  dev->records_capacity = n;
+  return 0;
+}
+
+struct EvQuad {
+  hipEvent_t a, b, c, d;
+};
+
+/* One pass over samples [tile.start_sample, tile.end_sample) of the tile. */
+static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, int W, size_t *ev,
+                           std::vector<EvQuad> *quads)
+{
+  const bool prof = (dev->profiling & 1) != 0;
+  const bool counters = (dev->profiling & 2) != 0;
+  hipStream_t s = dev->stream;
+  uint *err = dev->counters + 3;
+  const size_t n_slots = std::min<size_t>(tile.n_items, dev->capacity);
+  tile.work_next = dev->counters + 4;
+  tile.samples_out = dev->records;
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 12, s));
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters + 4, 0, 4, s));
+
+  int qa = 0, qb = 1;
+  const int qs = 2;
+  dim3 block(CY_BLOCK);
+  hipLaunchKernelGGL(k_init_slots, dim3((unsigned)((n_slots + CY_BLOCK - 1) / CY_BLOCK)), block, 0, s, kg,
+                     dev->bufs, tile, (int)n_slots, dev->queue[qa], dev->counters + qa);
+  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipStreamSynchronize(s));
+  uint n_active = dev->host_counters[qa];
+
+  while (n_active > 0) {
+    dev->stats.iterations++;
+    dev->stats.closest_rays += n_active;
+    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qb, 0, 4, s));
+    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qs, 0, 4, s));
+    dim3 grid((n_active + CY_BLOCK - 1) / CY_BLOCK);
+    EvQuad p;
+    if (prof) {
+      p.a = get_event(dev, (*ev)++);
+      p.b = get_event(dev, (*ev)++);
+      p.c = get_event(dev, (*ev)++);
+      p.d = get_event(dev, (*ev)++);
+      HIP_CHECK(dev, hipEventRecord(p.a, s));
+    }
+    {
+      auto kfn = counters ? (W == 8 ? k_intersect_closest<true, 8> : W == 4 ? k_intersect_closest<true, 4>
+                                                                     : k_intersect_closest<true, 2>)
+                          : (W == 8 ? k_intersect_closest<false, 8> : W == 4 ? k_intersect_closest<false, 4>
+                                                                     : k_intersect_closest<false, 2>);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, dev->queue[qa], dev->counters + qa, err,
+                         dev->stats_dev);
+    }
+    if (prof) {
+      HIP_CHECK(dev, hipEventRecord(p.b, s));
+    }
+    hipLaunchKernelGGL(k_shade, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa], dev->counters + qa,
+                       dev->queue[qb], dev->counters + qb, dev->queue[qs], dev->counters + qs, err);
+    if (prof) {
+      HIP_CHECK(dev, hipEventRecord(p.c, s));
+    }
+    {
+      auto kfn = counters ? (W == 8 ? k_intersect_shadow<true, 8> : W == 4 ? k_intersect_shadow<true, 4>
+                                                                    : k_intersect_shadow<true, 2>)
+                          : (W == 8 ? k_intersect_shadow<false, 8> : W == 4 ? k_intersect_shadow<false, 4>
+                                                                    : k_intersect_shadow<false, 2>);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qs], dev->counters + qs,
+                         dev->queue[qb], dev->counters + qb, err, dev->stats_dev);
+    }
+    if (prof) {
+      HIP_CHECK(dev, hipEventRecord(p.d, s));
+      quads->push_back(p);
+    }
+    HIP_CHECK(dev, hipGetLastError());
+    HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(dev, hipStreamSynchronize(s));
+    dev->stats.shadow_rays += dev->host_counters[qs];
+    n_active = dev->host_counters[qb];
+    if (dev->host_counters[3]) {
+      return 0;
+    }
+    std::swap(qa, qb);
+  }
+  const int npix = tile.w * tile.h;
+  hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npix + CY_BLOCK - 1) / CY_BLOCK)), block, 0, s, tile);
+  HIP_CHECK(dev, hipGetLastError());
+  return 0;
+}
+
 static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
 {
   if (!dev->error.empty()) {
@@ -767,114 +934,60 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
     return -1;
   }
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
-  const size_t slots = (size_t)t->w * (size_t)t->h;
-  if (slots == 0 || t->num_samples <= 0) {
+  const size_t npix = (size_t)t->w * (size_t)t->h;
+  if (npix == 0 || t->num_samples <= 0) {
     return 0;
   }
-  if (ensure_capacity(dev, slots) != 0 || ensure_bvh8(dev) != 0) {
+  /* samples per pass: as many as the record budget holds for this tile */
+  const size_t per_pass = std::max<size_t>(
+      1, std::min<size_t>((size_t)t->num_samples, dev->record_budget / (npix * sizeof(hc_float4))));
+  if (npix * per_pass > 0xFFFFFFFFull) {
+    return set_error(dev, "path_trace: tile too large for 32-bit work items");
+  }
+  const size_t items = npix * per_pass;
+  if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_records(dev, items) != 0 ||
+      ensure_bvhw(dev) != 0) {
     return -1;
   }
   CyGlobals kg;
   build_globals(dev, &kg);
-  const bool wide = kg.bvh8_nodes != nullptr;
-  CyTile tile;
-  tile.x = t->x;
-  tile.y = t->y;
-  tile.w = t->w;
-  tile.h = t->h;
-  tile.y_step = y_step;
-  tile.start_sample = t->start_sample;
-  tile.end_sample = t->start_sample + t->num_samples;
-  tile.offset = t->offset;
-  tile.stride = t->stride;
-  tile.buffer = (float *)t->buffer;
-  tile.pass_stride = dev->data_host.film.pass_stride;
+  const int W = kg.bvhw_nodes ? dev->bvh_width : 2;
 
   memset(&dev->stats, 0, sizeof(dev->stats));
-  dev->stats.bvh_width = wide ? 8 : 2;
-  dev->stats.bvh_depth = wide ? dev->bvh8_depth : 0;
+  dev->stats.bvh_width = W;
+  dev->stats.bvh_depth = W > 2 ? dev->bvhw_depth : 0;
   {
     auto it = dev->globals.find("__bvh_nodes");
-    dev->stats.bvh_bytes = wide ? dev->bvh8_bytes : (it != dev->globals.end() ? it->second.bytes : 0);
+    dev->stats.bvh_bytes = W > 2 ? dev->bvhw_bytes : (it != dev->globals.end() ? it->second.bytes : 0);
   }
-  const bool prof = (dev->profiling & 1) != 0;
-  const bool counters = (dev->profiling & 2) != 0;
   hipStream_t s = dev->stream;
-  uint *err = dev->counters + 3;
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, s));
   HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, 2 * sizeof(CyStats), s));
-
   size_t ev = 0;
   hipEvent_t t_begin = get_event(dev, ev++);
   HIP_CHECK(dev, hipEventRecord(t_begin, s));
+  std::vector<EvQuad> quads;
 
-  int qa = 0, qb = 1;
-  const int qs = 2;
-  dim3 block(CY_BLOCK);
-  {
-    dim3 grid((unsigned)((slots + CY_BLOCK - 1) / CY_BLOCK));
-    hipLaunchKernelGGL(k_init_slots, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa],
-                       dev->counters + qa);
-  }
-  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(dev, hipStreamSynchronize(s));
-  uint n_active = dev->host_counters[qa];
-
-  struct EvPair {
-    hipEvent_t a, b, c, d, e;
-  };
-  std::vector<EvPair> pairs;
-  uint64_t iterations = 0;
-  while (n_active > 0) {
-    iterations++;
-    dev->stats.closest_rays += n_active;
-    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qb, 0, 4, s));
-    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qs, 0, 4, s));
-    dim3 grid((n_active + CY_BLOCK - 1) / CY_BLOCK);
-    EvPair p;
-    if (prof) {
-      p.a = get_event(dev, ev++);
-      p.b = get_event(dev, ev++);
-      p.c = get_event(dev, ev++);
-      p.d = get_event(dev, ev++);
-      HIP_CHECK(dev, hipEventRecord(p.a, s));
+  for (int s0 = t->start_sample; s0 < t->start_sample + t->num_samples; s0 += (int)per_pass) {
+    CyTile tile;
+    tile.x = t->x;
+    tile.y = t->y;
+    tile.w = t->w;
+    tile.h = t->h;
+    tile.y_step = y_step;
+    tile.start_sample = s0;
+    tile.end_sample = std::min(s0 + (int)per_pass, t->start_sample + t->num_samples);
+    tile.offset = t->offset;
+    tile.stride = t->stride;
+    tile.buffer = (float *)t->buffer;
+    tile.pass_stride = dev->data_host.film.pass_stride;
+    tile.n_items = (uint)(npix * (size_t)(tile.end_sample - tile.start_sample));
+    if (path_trace_pass(dev, kg, tile, W, &ev, &quads) != 0) {
+      return -1;
     }
-    {
-      auto kfn = counters ? (wide ? k_intersect_closest<true, true> : k_intersect_closest<true, false>)
-                          : (wide ? k_intersect_closest<false, true> : k_intersect_closest<false, false>);
-      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, dev->queue[qa], dev->counters + qa, err,
-                         dev->stats_dev);
-    }
-    if (prof) {
-      HIP_CHECK(dev, hipEventRecord(p.b, s));
-    }
-    hipLaunchKernelGGL(k_shade, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa],
-                       dev->counters + qa, dev->queue[qb], dev->counters + qb, dev->queue[qs],
-                       dev->counters + qs, err);
-    if (prof) {
-      HIP_CHECK(dev, hipEventRecord(p.c, s));
-    }
-    {
-      auto kfn = counters ? (wide ? k_intersect_shadow<true, true> : k_intersect_shadow<true, false>)
-                          : (wide ? k_intersect_shadow<false, true> : k_intersect_shadow<false, false>);
-      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qs], dev->counters + qs,
-                         dev->queue[qb], dev->counters + qb, err, dev->stats_dev);
-    }
-    if (prof) {
-      HIP_CHECK(dev, hipEventRecord(p.d, s));
-      pairs.push_back(p);
-    }
-    HIP_CHECK(dev, hipGetLastError());
-    HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(dev, hipStreamSynchronize(s));
-    dev->stats.shadow_rays += dev->host_counters[qs];
-    n_active = dev->host_counters[qb];
     if (dev->host_counters[3]) {
       break;
     }
-    int tmp = qa;
-    qa = qb;
-    qb = tmp;
   }
   hipEvent_t t_end = get_event(dev, ev++);
   HIP_CHECK(dev, hipEventRecord(t_end, s));
@@ -883,10 +996,9 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
   float ms = 0.0f;
   hipEventElapsedTime(&ms, t_begin, t_end);
   dev->stats.total_ms = ms;
-  dev->stats.iterations = iterations;
-  if (prof) {
+  if (dev->profiling & 1) {
     double closest = 0.0, shadow = 0.0, shade = 0.0;
-    for (auto &p : pairs) {
+    for (auto &p : quads) {
       float a = 0, b = 0, c = 0;
       hipEventElapsedTime(&a, p.a, p.b);
       hipEventElapsedTime(&b, p.b, p.c);
@@ -898,9 +1010,9 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
     dev->stats.intersect_ms = closest + shadow;
     dev->stats.closest_ms = closest;
     dev->stats.shade_ms = shade;
-    dev->stats.closest_launches = pairs.size();
+    dev->stats.closest_launches = quads.size();
   }
-  if (counters) {
+  if (dev->profiling & 2) {
     CyStats st[2];
     HIP_CHECK(dev, hipMemcpy(st, dev->stats_dev, sizeof(st), hipMemcpyDeviceToHost));
     dev->stats.inner_nodes = st[0].nodes + st[1].nodes;
@@ -913,16 +1025,28 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
   return check_device_error(dev);
 }
 
+int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes)
+{
+  if (slots) {
+    dev->slots_wanted = (size_t)slots;
+  }
+  if (record_bytes) {
+    dev->record_budget = (size_t)record_bytes;
+  }
+  return 0;
+}
+
 int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t out_i, int n, int any_hit)
 {
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
-  if (ensure_bvh8(dev) != 0) {
+  if (ensure_bvhw(dev) != 0) {
     return -1;
   }
   CyGlobals kg;
   build_globals(dev, &kg);
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
-  hipLaunchKernelGGL(kg.bvh8_nodes ? k_test_intersect<true> : k_test_intersect<false>,
+  const int W = kg.bvhw_nodes ? dev->bvh_width : 2;
+  hipLaunchKernelGGL(W == 8 ? k_test_intersect<8> : W == 4 ? k_test_intersect<4> : k_test_intersect<2>,
                      dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
                      (const float *)rays, (float *)out_f, (int *)out_i, n, any_hit, dev->counters + 3);
   HIP_CHECK(dev, hipGetLastError());

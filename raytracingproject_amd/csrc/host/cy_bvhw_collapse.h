@@ -1,0 +1,305 @@
+/*
+ * cy_bvhw_collapse.h — widen the host's packed BVH2 into the device's W-wide
+ * BVH (W = 4 or 8; host C++, header-only; used by the device library when the
+ * BVH arrays are bound, and by the CPU tests through tools/host_emu.cpp).
+ *
+ * The host keeps building Cycles' BVH2 (bvh/bvh2.cpp pack_aligned_node /
+ * pack_leaf: 4 float4 per inner node, 1 float4 per leaf, leaf address ~i) and
+ * binds it as __bvh_nodes / __bvh_leaf_nodes; get_bvh_layout_mask() stays
+ * BVH_LAYOUT_BVH2.  This is the widening step the reference does for its
+ * 4/8-wide CPU layouts in BVH::pack_nodes / widen_children_nodes
+ * (bvh/bvh.cpp:149-176), done on the BVH2 the device was handed, so the
+ * primitive arrays and primitive indices are untouched.
+ *
+ * Collapse: a wide node starts from the two children of a BVH2 node and
+ * repeatedly opens the inner child of largest surface area until it holds W
+ * children or only leaves.  A BVH2 leaf becomes a leaf child (its primitive
+ * range); an inner BVH2 subtree whose leaves hold at most `merge_prims`
+ * primitives in one contiguous range also becomes a single leaf child.
+ *
+ * Node (32*W bytes: 128 B for W = 4, one L2 line; 256 B for W = 8), arrays of
+ * W 32-bit words:  lo.x  hi.x  lo.y  hi.y  lo.z  hi.z  child  meta
+ *   bounds : the exact BVH2 child boxes (float), so the slab test of a wide
+ *            child is bit-for-bit the reference's test of that BVH2 child
+ *            (bvh/bvh_nodes.h:31-80);
+ *   child  : >= 0 inner child node index, < 0 leaf ~first_primitive;
+ *   meta   : child visibility (low 28 bits, as the BVH2 node stored it) |
+ *            primitive count << 28 for leaves; 0 = empty slot.
+ */
+#ifndef CY_BVHW_COLLAPSE_H
+#define CY_BVHW_COLLAPSE_H
+
+#include <cfloat>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace cybvhw {
+
+struct Ref {
+  int addr; /* BVH2 address: >= 0 inner node (float4 units), < 0 leaf ~index */
+  float lo[3], hi[3];
+  uint32_t vis;
+};
+
+static inline float area(const Ref &b)
+{
+  const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+struct Collapser {
+  int width = 4;
+  int merge_prims = 0; /* subtrees with <= this many contiguous primitives become one leaf */
+  const float *nodes2 = nullptr; /* __bvh_nodes as floats (4 per float4) */
+  size_t n_nodes2 = 0;           /* float4 count */
+  const float *leaves2 = nullptr;
+  size_t n_leaves2 = 0;
+  std::vector<uint32_t> out; /* 8 * width words per wide node */
+  std::string error;
+  int max_depth = 0;
+  std::vector<int> sub_start, sub_count; /* per BVH2 inner node (index addr/4): contiguous range or -1 */
+
+  size_t words() const
+  {
+    return 8 * (size_t)width;
+  }
+
+  void children(int addr, Ref c[2]) const
+  {
+    const float *n = nodes2 + 4 * (size_t)addr;
+    uint32_t w[4];
+    memcpy(w, n, 16);
+    for (int k = 0; k < 2; k++) {
+      c[k].vis = w[k];
+      c[k].addr = (int)w[2 + k];
+      c[k].lo[0] = n[4 + k];
+      c[k].hi[0] = n[4 + 2 + k];
+      c[k].lo[1] = n[8 + k];
+      c[k].hi[1] = n[8 + 2 + k];
+      c[k].lo[2] = n[12 + k];
+      c[k].hi[2] = n[12 + 2 + k];
+    }
+  }
+
+  bool leaf_range(int addr, int *start, int *count)
+  {
+    const size_t li = (size_t)(-addr - 1);
+    if (li >= n_leaves2) {
+      error = "leaf index out of range";
+      return false;
+    }
+    uint32_t w[4];
+    memcpy(w, leaves2 + 4 * li, 16);
+    const int s = (int)w[0], e = (int)w[1];
+    if (s < 0) {
+      error = "instanced BVH leaves are not supported";
+      return false;
+    }
+    if ((w[3] & 1u) == 0u) { /* PRIMITIVE_TRIANGLE = 1 */
+      error = "only triangle leaves are supported";
+      return false;
+    }
+    if (e - s < 1 || e - s > 15) {
+      error = "leaf with " + std::to_string(e - s) + " primitives";
+      return false;
+    }
+    *start = s;
+    *count = e - s;
+    return true;
+  }
+
+  /* contiguous primitive range of a BVH2 subtree (memoised), or count -1 */
+  bool subtree_range(int addr, int *start, int *count)
+  {
+    if (addr < 0) {
+      return leaf_range(addr, start, count);
+    }
+    const size_t i = (size_t)addr / 4;
+    if (sub_count[i] != -2) {
+      *start = sub_start[i];
+      *count = sub_count[i];
+      return true;
+    }
+    Ref c[2];
+    children(addr, c);
+    int s0, n0, s1, n1;
+    if (!subtree_range(c[0].addr, &s0, &n0) || !subtree_range(c[1].addr, &s1, &n1)) {
+      return false;
+    }
+    int s = -1, n = -1;
+    if (n0 >= 0 && n1 >= 0 && (c[0].vis & 0x0FFFFFFFu) == (c[1].vis & 0x0FFFFFFFu)) {
+      if (s0 + n0 == s1) {
+        s = s0;
+        n = n0 + n1;
+      }
+      else if (s1 + n1 == s0) {
+        s = s1;
+        n = n0 + n1;
+      }
+    }
+    if (n > 15) {
+      n = -1;
+    }
+    sub_start[i] = s;
+    sub_count[i] = n;
+    *start = s;
+    *count = n;
+    return true;
+  }
+
+  bool mergeable(const Ref &r, int *start, int *count)
+  {
+    if (r.addr < 0) {
+      return leaf_range(r.addr, start, count);
+    }
+    if (merge_prims <= 0) {
+      return false;
+    }
+    int s, n;
+    if (!subtree_range(r.addr, &s, &n)) {
+      return false;
+    }
+    if (n >= 0 && n <= merge_prims) {
+      *start = s;
+      *count = n;
+      return true;
+    }
+    return false;
+  }
+
+  bool open(const Ref &r, Ref *ch, int *n)
+  {
+    children(r.addr, ch);
+    *n = 2;
+    while (*n < width) {
+      int best = -1;
+      float ba = -1.0f;
+      for (int i = 0; i < *n; i++) {
+        int s, c;
+        if (ch[i].addr < 0 || (ch[i].vis & 0x0FFFFFFFu) == 0u) {
+          continue;
+        }
+        if (mergeable(ch[i], &s, &c)) {
+          continue;
+        }
+        if (!error.empty()) {
+          return false;
+        }
+        if (area(ch[i]) > ba) {
+          ba = area(ch[i]);
+          best = i;
+        }
+      }
+      if (best < 0) {
+        break;
+      }
+      Ref two[2];
+      children(ch[best].addr, two);
+      ch[best] = two[0];
+      ch[(*n)++] = two[1];
+    }
+    return error.empty();
+  }
+
+  bool emit(size_t idx, const Ref *ch, int n, std::vector<std::pair<size_t, Ref>> *pending)
+  {
+    const int W = width;
+    std::vector<uint32_t> w(words(), 0u);
+    float *f = reinterpret_cast<float *>(w.data());
+    for (int s = 0; s < W; s++) {
+      /* empty slot: inverted box, never hit (meta 0 also rejects it) */
+      f[0 * W + s] = FLT_MAX;
+      f[1 * W + s] = -FLT_MAX;
+      f[2 * W + s] = FLT_MAX;
+      f[3 * W + s] = -FLT_MAX;
+      f[4 * W + s] = FLT_MAX;
+      f[5 * W + s] = -FLT_MAX;
+    }
+    int s = 0;
+    for (int i = 0; i < n; i++) {
+      const uint32_t vis = ch[i].vis & 0x0FFFFFFFu;
+      if (vis == 0u) {
+        continue; /* invisible to every ray kind */
+      }
+      for (int a = 0; a < 3; a++) {
+        f[(2 * a) * W + s] = ch[i].lo[a];
+        f[(2 * a + 1) * W + s] = ch[i].hi[a];
+      }
+      int start, count;
+      if (mergeable(ch[i], &start, &count)) {
+        if (start >= (1 << 27)) {
+          error = "primitive index beyond the 2^27 leaf-code range";
+          return false;
+        }
+        w[6 * W + s] = (uint32_t)(~start);
+        w[7 * W + s] = vis | ((uint32_t)count << 28);
+      }
+      else if (!error.empty()) {
+        return false;
+      }
+      else {
+        const size_t child = out.size() / words();
+        out.resize(out.size() + words(), 0u);
+        w[6 * W + s] = (uint32_t)child;
+        w[7 * W + s] = vis;
+        pending->push_back(std::make_pair(child, ch[i]));
+      }
+      s++;
+    }
+    memcpy(&out[idx * words()], w.data(), words() * 4);
+    return true;
+  }
+
+  /* root: BVH2 root address (KernelBVH.root) */
+  bool run(int root)
+  {
+    if (width != 4 && width != 8) {
+      error = "width must be 4 or 8";
+      return false;
+    }
+    out.assign(words(), 0u);
+    sub_start.assign(n_nodes2 / 4 + 1, -1);
+    sub_count.assign(n_nodes2 / 4 + 1, -2);
+    std::vector<std::pair<size_t, Ref>> pending, next;
+    std::vector<Ref> ch(width);
+    int n = 0;
+    if (root < 0) {
+      /* single-leaf scene: one wide node holding the leaf with an unbounded box */
+      Ref r;
+      r.addr = root;
+      r.vis = 0x0FFFFFFFu;
+      for (int a = 0; a < 3; a++) {
+        r.lo[a] = -FLT_MAX;
+        r.hi[a] = FLT_MAX;
+      }
+      max_depth = 1;
+      return emit(0, &r, 1, &pending);
+    }
+    Ref r;
+    r.addr = root;
+    r.vis = 0xFFFFFFFFu;
+    if (!open(r, ch.data(), &n) || !emit(0, ch.data(), n, &pending)) {
+      return false;
+    }
+    int depth = 1;
+    while (!pending.empty()) {
+      next.clear();
+      for (auto &p : pending) {
+        if (!open(p.second, ch.data(), &n) || !emit(p.first, ch.data(), n, &next)) {
+          return false;
+        }
+      }
+      pending.swap(next);
+      depth++;
+    }
+    max_depth = depth;
+    return true;
+  }
+};
+
+}  // namespace cybvhw
+
+#endif

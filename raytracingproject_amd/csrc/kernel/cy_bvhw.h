@@ -1,0 +1,248 @@
+/*
+ * cy_bvhw.h — closest-hit and opaque any-hit traversal of the device's W-wide
+ * BVH (W = 4 or 8, layout: csrc/host/cy_bvhw_collapse.h).
+ *
+ * Same query as bvh2_intersect (bvh/bvh_traversal.h:34-227) with the same
+ * direction clamp, the same slab arithmetic on the same (exact) child boxes,
+ * the same ray_triangle_intersect on the same primitive arrays and the same
+ * visibility tests, so every primitive the BVH2 traversal accepts is also
+ * reached here; only the visiting order differs, and with it the winner
+ * between primitives whose hit distances agree to the last ulp
+ * (tests/test_bvh_wide.py bounds that).
+ *
+ * Per wide node the W child boxes are tested, the hit children sorted by entry
+ * distance with a small sorting network, the nearest visited next and the rest
+ * pushed far-to-near with their entry distance (a popped entry farther than the
+ * current hit is skipped).  Leaf children are stack entries too, so triangles
+ * are tested in near-to-far order.  The first CY_LDS_STACKW entries of the
+ * stack live in LDS, one column per thread.
+ */
+#ifndef CY_BVHW_H
+#define CY_BVHW_H
+
+#include "cy_path.h"
+
+#ifndef CY_LDS_STACKW
+#  define CY_LDS_STACKW 16
+#endif
+#define CY_BVHW_STACK 96
+
+struct CyStackW {
+  int *lds_node; /* &lds_base[threadIdx.x] or nullptr */
+  float *lds_t;
+  int spill_node[CY_BVHW_STACK];
+  float spill_t[CY_BVHW_STACK];
+  CY_MFN void set(int i, int node, float t)
+  {
+    if (lds_node && i < CY_LDS_STACKW) {
+      lds_node[i * CY_BLOCK] = node;
+      lds_t[i * CY_BLOCK] = t;
+    }
+    else {
+      spill_node[i] = node;
+      spill_t[i] = t;
+    }
+  }
+  CY_MFN void get(int i, int *node, float *t) const
+  {
+    if (lds_node && i < CY_LDS_STACKW) {
+      *node = lds_node[i * CY_BLOCK];
+      *t = lds_t[i * CY_BLOCK];
+    }
+    else {
+      *node = spill_node[i];
+      *t = spill_t[i];
+    }
+  }
+};
+
+CY_FN void bvhw_cswap(float &ta, int &ca, float &tb, int &cb)
+{
+  const bool sw = tb < ta;
+  const float t0 = sw ? tb : ta;
+  const float t1 = sw ? ta : tb;
+  const int c0 = sw ? cb : ca;
+  const int c1 = sw ? ca : cb;
+  ta = t0;
+  tb = t1;
+  ca = c0;
+  cb = c1;
+}
+
+/* ascending sort of (entry distance, child code); misses carry +inf */
+template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
+{
+  if constexpr (W == 4) {
+    bvhw_cswap(t[0], c[0], t[1], c[1]);
+    bvhw_cswap(t[2], c[2], t[3], c[3]);
+    bvhw_cswap(t[0], c[0], t[2], c[2]);
+    bvhw_cswap(t[1], c[1], t[3], c[3]);
+    bvhw_cswap(t[1], c[1], t[2], c[2]);
+  }
+  else {
+    /* Batcher odd-even merge sort, 19 comparators */
+    bvhw_cswap(t[0], c[0], t[1], c[1]);
+    bvhw_cswap(t[2], c[2], t[3], c[3]);
+    bvhw_cswap(t[4], c[4], t[5], c[5]);
+    bvhw_cswap(t[6], c[6], t[7], c[7]);
+    bvhw_cswap(t[0], c[0], t[2], c[2]);
+    bvhw_cswap(t[1], c[1], t[3], c[3]);
+    bvhw_cswap(t[4], c[4], t[6], c[6]);
+    bvhw_cswap(t[5], c[5], t[7], c[7]);
+    bvhw_cswap(t[1], c[1], t[2], c[2]);
+    bvhw_cswap(t[5], c[5], t[6], c[6]);
+    bvhw_cswap(t[0], c[0], t[4], c[4]);
+    bvhw_cswap(t[1], c[1], t[5], c[5]);
+    bvhw_cswap(t[2], c[2], t[6], c[6]);
+    bvhw_cswap(t[3], c[3], t[7], c[7]);
+    bvhw_cswap(t[2], c[2], t[4], c[4]);
+    bvhw_cswap(t[3], c[3], t[5], c[5]);
+    bvhw_cswap(t[1], c[1], t[2], c[2]);
+    bvhw_cswap(t[3], c[3], t[4], c[4]);
+    bvhw_cswap(t[5], c[5], t[6], c[6]);
+  }
+}
+
+template<int W, bool any_hit>
+CY_FN bool bvhw_intersect(const CyGlobals *kg,
+                          const CyRay *ray,
+                          uint visibility,
+                          CyIsect *isect,
+                          uint *err,
+                          uint *cnt_nodes,
+                          uint *cnt_leaves,
+                          uint *cnt_tris,
+                          int *lds_stack = nullptr)
+{
+  CyStackW stack;
+  stack.lds_node = lds_stack;
+  stack.lds_t = lds_stack ? (float *)(lds_stack + CY_LDS_STACKW * CY_BLOCK) : nullptr;
+  int sp = 0;
+
+  const cfloat3 P = ray->P;
+  const cfloat3 dir = bvh_clamp_direction(ray->D);
+  const cfloat3 idir = rcp3(dir);
+
+  isect->t = ray->t;
+  isect->u = 0.0f;
+  isect->v = 0.0f;
+  isect->prim = PRIM_NONE;
+  isect->object = OBJECT_NONE;
+  isect->type = 0;
+
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
+  constexpr int Q = W / 4; /* float4 per array */
+  int code = 0;            /* root: wide node 0 */
+
+  while (true) {
+    if (code >= 0) {
+      /* inner node: test the W child boxes */
+      n_nodes++;
+      const hc_float4 *np = nodes + (size_t)code * (8 * Q);
+      float tn[W];
+      int cc[W];
+      const float t = isect->t;
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const hc_float4 lx = np[0 * Q + q], hx = np[1 * Q + q];
+        const hc_float4 ly = np[2 * Q + q], hy = np[3 * Q + q];
+        const hc_float4 lz = np[4 * Q + q], hz = np[5 * Q + q];
+        const hc_uint4 ch = ((const hc_uint4 *)np)[6 * Q + q];
+        const hc_uint4 mt = ((const hc_uint4 *)np)[7 * Q + q];
+        const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+        const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+        const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+        const uint ach[4] = {ch.x, ch.y, ch.z, ch.w}, amt[4] = {mt.x, mt.y, mt.z, mt.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float clox = (alx[j] - P.x) * idir.x;
+          const float chix = (ahx[j] - P.x) * idir.x;
+          const float cloy = (aly[j] - P.y) * idir.y;
+          const float chiy = (ahy[j] - P.y) * idir.y;
+          const float cloz = (alz[j] - P.z) * idir.z;
+          const float chiz = (ahz[j] - P.z) * idir.z;
+          const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz));
+          const float cmx = min4(t, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
+          const bool hit = (cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility);
+          const int s = 4 * q + j;
+          /* leaf codes carry the primitive count: ~(first << 4 | count) */
+          const int child = (int)ach[j];
+          cc[s] = child >= 0 ? child : ~((~child << 4) | (int)(amt[j] >> 28));
+          tn[s] = hit ? cmn : CY_INF;
+        }
+      }
+      bvhw_sort<W>(tn, cc);
+      if (tn[0] == CY_INF) {
+        goto pop;
+      }
+#pragma unroll
+      for (int s = W - 1; s >= 1; s--) {
+        if (tn[s] != CY_INF) {
+          if (sp >= CY_BVHW_STACK) {
+            cy_set_error(err, CY_ERR_BVH_STACK, W);
+            return false;
+          }
+          stack.set(sp++, cc[s], tn[s]);
+        }
+      }
+      code = cc[0];
+      continue;
+    }
+    else {
+      /* leaf: contiguous primitive range */
+      n_leaves++;
+      const int packed = ~code;
+      int prim_addr = packed >> 4;
+      const int prim_end = prim_addr + (packed & 15);
+      for (; prim_addr < prim_end; prim_addr++) {
+        n_tris++;
+        const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+        const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+        float tt, uu, vv;
+        if (ray_triangle_intersect(P, dir, isect->t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt)) {
+          if (kg->__prim_visibility[prim_addr] & visibility) {
+            isect->prim = prim_addr;
+            isect->object = OBJECT_NONE;
+            isect->type = PRIMITIVE_TRIANGLE;
+            isect->u = uu;
+            isect->v = vv;
+            isect->t = tt;
+            if (any_hit) {
+              if (cnt_nodes) {
+                *cnt_nodes += n_nodes;
+                *cnt_leaves += n_leaves;
+                *cnt_tris += n_tris;
+              }
+              return true;
+            }
+          }
+        }
+      }
+    }
+  pop:
+    {
+      bool found = false;
+      while (sp > 0) {
+        float et;
+        stack.get(--sp, &code, &et);
+        if (et <= isect->t) {
+          found = true;
+          break;
+        }
+      }
+      if (!found) {
+        break;
+      }
+    }
+  }
+
+  if (cnt_nodes) {
+    *cnt_nodes += n_nodes;
+    *cnt_leaves += n_leaves;
+    *cnt_tris += n_tris;
+  }
+  return (isect->prim != PRIM_NONE);
+}
+
+#endif /* CY_BVHW_H */

@@ -41,9 +41,9 @@ typedef struct CyGlobals {
 #define CY_DECL_PTR(type, name) const type *name;
   CY_GLOBAL_ARRAYS(CY_DECL_PTR)
 #undef CY_DECL_PTR
-  /* device-internal 8-wide BVH widened from __bvh_nodes/__bvh_leaf_nodes
-   * (csrc/host/cy_bvh8_collapse.h); nullptr when traversing the BVH2 */
-  const hc_uint4 *bvh8_nodes;
+  /* device-internal W-wide BVH widened from __bvh_nodes/__bvh_leaf_nodes
+   * (csrc/host/cy_bvhw_collapse.h); nullptr when traversing the BVH2 */
+  const void *bvhw_nodes;
 } CyGlobals;
 
 #endif /* CY_GLOBALS_H */

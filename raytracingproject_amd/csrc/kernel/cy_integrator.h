@@ -2,14 +2,18 @@
  * cy_integrator.h — the wavefront form of kernel_path_trace (kernel_path.h:509-695).
  *
  * The reference runs one camera sample per thread from camera ray to
- * kernel_write_result.  The HIP device keeps one *slot* per pixel of the tile
- * resident in HBM and advances all slots one bounce per iteration through three
- * kernels: intersect_closest (bvh), shade (everything between two traversals),
- * intersect_shadow (occlusion of the light sample + deferred light accumulation).
- * A slot finishing sample s immediately regenerates sample s+1 of the same pixel,
- * so each pixel has exactly one path in flight and its samples are added to the
- * render buffer in sample order: the buffer is bit-identical to the CPU kernel's
- * sample-major loop (device_cpu.cpp:906-921) with no float atomics.
+ * kernel_write_result.  The HIP device keeps a fixed pool of path *slots*
+ * resident in HBM and advances all of them one bounce per iteration through
+ * three kernels: intersect_closest (bvh), shade (everything between two
+ * traversals), intersect_shadow (occlusion of the light sample + deferred light
+ * accumulation).  Work items are the tile's (pixel, sample) pairs, numbered
+ * sample-major (item = (sample - start) * w*h + pixel); a slot whose path ends
+ * takes the next unclaimed item, so the pool stays full until the items run out
+ * and the number of iterations is set by the total path length, not by the
+ * slowest pixel.  Each finished sample leaves its (L, alpha) record at its item
+ * index; k_accumulate then adds every pixel's records to the render buffer in
+ * sample order, so the buffer is bit-identical to the CPU kernel's sample-major
+ * loop (device_cpu.cpp:906-921) with no float atomics.
  *
  * Radiance accumulation order per path is preserved: the deferred light
  * contribution of bounce k is added after shade(k) and before shade(k+1), exactly
@@ -34,15 +38,19 @@ typedef struct CyPathBuffers {
   hc_float4 *shadow_P;   /* shadow ray P.xyz, t */
   hc_float4 *shadow_D;   /* shadow ray D.xyz, (unused) */
   hc_float4 *shadow_L;   /* pending light contribution xyz, w: 1 = finish path after */
+  uint *item;            /* work item of the path in the slot */
 } CyPathBuffers;
 
 typedef struct CyTile {
   int x, y, w, h;
   int y_step; /* rows of the tile are image rows y, y+y_step, ... (1 = contiguous) */
-  int start_sample, end_sample;
+  int start_sample, end_sample; /* the sample range of this pass */
   int offset, stride;
   float *buffer;
   int pass_stride;
+  uint n_items;           /* w * h * (end_sample - start_sample) */
+  uint *work_next;        /* next unclaimed item (atomic) */
+  hc_float4 *samples_out; /* per item: L.xyz, alpha; alpha NaN = no camera ray */
 } CyTile;
 
 typedef struct CyStats {
@@ -227,9 +235,10 @@ CY_FN cfloat3 path_radiance_clamp(const CyGlobals *kg, cfloat3 L, int bounce)
   return L;
 }
 
-/* Write the finished sample: kernel_passes.h:338-433 with only the combined pass
- * (kernel_accumulate.h:622-688, use_light_pass == 0, no shadow catcher). */
-CY_FN void write_result(const CyTile *tile, int x, int ybuf, cfloat3 L_emission, float L_transparent)
+/* Record the finished sample: kernel_passes.h:338-433 with only the combined
+ * pass (kernel_accumulate.h:622-688, use_light_pass == 0, no shadow catcher);
+ * the buffer addition itself happens in accumulate_pixel. */
+CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float L_transparent)
 {
   cfloat3 L_sum = L_emission;
   float sum = fabsf(L_sum.x) + fabsf(L_sum.y) + fabsf(L_sum.z);
@@ -237,72 +246,86 @@ CY_FN void write_result(const CyTile *tile, int x, int ybuf, cfloat3 L_emission,
     L_sum = mk3(0.0f, 0.0f, 0.0f);
   }
   float alpha = 1.0f - L_transparent;
-  float *buf = tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
-  buf[0] += L_sum.x;
-  buf[1] += L_sum.y;
-  buf[2] += L_sum.z;
-  buf[3] += alpha;
+  tile->samples_out[item] = mkf4(L_sum.x, L_sum.y, L_sum.z, alpha);
 }
 
-/* Start the next valid sample of the slot; returns false when the slot is done.
- * A camera ray with t == 0 produces no write (kernel_path.h:660-662). */
-CY_FN bool slot_regenerate(const CyGlobals *kg,
-                           const CyPathBuffers *b,
-                           const CyTile *tile,
-                           int slot,
-                           int sample)
+/* Start work item `item` in the slot.  Returns false when the sample has no
+ * camera ray (t == 0: no write, kernel_path.h:660-662); the caller then claims
+ * another item. */
+CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot, uint item)
 {
-  int x = tile->x + slot % tile->w;
-  int y = tile->y + (slot / tile->w) * tile->y_step;
-  for (; sample < tile->end_sample; sample++) {
-    uint rng_hash;
-    CyRay ray;
-    camera_sample_ray(kg, x, y, sample, &rng_hash, &ray);
-    if (ray.t == 0.0f) {
-      continue;
-    }
-    CyPathState s;
-    path_state_init(kg, &s, rng_hash, sample);
-    store_state(b, slot, &s);
-    b->ray_P[slot] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
-    b->ray_D[slot] = mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f);
-    b->throughput[slot] = mkf4(1.0f, 1.0f, 1.0f, 0.0f);
-    b->L[slot] = mkf4(0.0f, 0.0f, 0.0f, 0.0f);
-    return true;
+  const uint npix = (uint)(tile->w * tile->h);
+  const int p = (int)(item % npix);
+  const int sample = tile->start_sample + (int)(item / npix);
+  const int x = tile->x + p % tile->w;
+  const int y = tile->y + (p / tile->w) * tile->y_step;
+  uint rng_hash;
+  CyRay ray;
+  camera_sample_ray(kg, x, y, sample, &rng_hash, &ray);
+  if (ray.t == 0.0f) {
+    tile->samples_out[item] = mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf(""));
+    return false;
   }
-  return false;
+  CyPathState s;
+  path_state_init(kg, &s, rng_hash, sample);
+  store_state(b, slot, &s);
+  b->item[slot] = item;
+  b->ray_P[slot] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
+  b->ray_D[slot] = mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f);
+  b->throughput[slot] = mkf4(1.0f, 1.0f, 1.0f, 0.0f);
+  b->L[slot] = mkf4(0.0f, 0.0f, 0.0f, 0.0f);
+  return true;
 }
 
-/* Finish the current sample of a slot: write it, regenerate the next one. */
-CY_FN bool slot_finish(const CyGlobals *kg,
-                       const CyPathBuffers *b,
-                       const CyTile *tile,
-                       int slot,
-                       int sample,
-                       cfloat3 L_emission,
-                       float L_transparent)
+/* Finish the path in a slot: record its sample; the slot then needs new work. */
+CY_FN void slot_finish(const CyPathBuffers *b, const CyTile *tile, int slot, cfloat3 L_emission, float L_transparent)
 {
-  /* buffer row: the tile's rows are stored contiguously (y_step == 1: image row) */
-  int x = tile->x + slot % tile->w;
-  int ybuf = tile->y + slot / tile->w;
-  write_result(tile, x, ybuf, L_emission, L_transparent);
-  return slot_regenerate(kg, b, tile, slot, sample + 1);
+  write_sample(tile, b->item[slot], L_emission, L_transparent);
+}
+
+/* Add pixel p's sample records to the render buffer in sample order
+ * (kernel_write_pass_float4, kernel_write_passes.h:49-65, once per sample).
+ * The tile's rows are stored contiguously in the buffer. */
+CY_FN void accumulate_pixel(const CyTile *tile, int p)
+{
+  const int npix = tile->w * tile->h;
+  const int x = tile->x + p % tile->w;
+  const int ybuf = tile->y + p / tile->w;
+  float *buf = tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
+  float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
+  const int n = tile->end_sample - tile->start_sample;
+  for (int k = 0; k < n; k++) {
+    const hc_float4 r = tile->samples_out[(size_t)k * npix + p];
+    if (r.w == r.w) {
+      b0 += r.x;
+      b1 += r.y;
+      b2 += r.z;
+      b3 += r.w;
+    }
+  }
+  buf[0] = b0;
+  buf[1] = b1;
+  buf[2] = b2;
+  buf[3] = b3;
 }
 
 /* ---------------------------------------------------------------------------
  * Stage 2: shade one path at one bounce.  Returns true when the slot must be
  * enqueued for the next closest-hit traversal.  *shadow is set when a shadow ray
  * was emitted (the slot then goes to the shadow queue; if the path ends at this
- * bounce the shadow stage finishes it).
+ * bounce the shadow stage finishes it).  *finished is set when the path ended
+ * here and its sample was recorded.
  */
 CY_FN bool shade_path(const CyGlobals *kg,
                       const CyPathBuffers *b,
                       const CyTile *tile,
                       int slot,
                       bool *shadow,
+                      bool *finished,
                       uint *err)
 {
   *shadow = false;
+  *finished = false;
   CyPathState state;
   load_state(b, slot, &state, kg);
   const hc_float4 rp = b->ray_P[slot];
@@ -567,7 +590,9 @@ CY_FN bool shade_path(const CyGlobals *kg,
     return false;
   }
   (void)finish_now;
-  return slot_finish(kg, b, tile, slot, state.sample, L, L_transparent);
+  slot_finish(b, tile, slot, L, L_transparent);
+  *finished = true;
+  return false;
 }
 
 #endif /* CY_INTEGRATOR_H */

@@ -40,6 +40,7 @@
 #define CY_2PI_F 6.2831853071795864f
 #define CY_1_PI_F 0.318309886183790671538f
 #define CY_FLT_MAX 3.402823466e+38f
+#define CY_INF __builtin_inff()
 
 typedef unsigned int uint;
 

@@ -120,8 +120,16 @@ class HIPDevice:
         self.lib.hipcy_set_profiling(self.h, int(flags))
 
     def set_bvh_width(self, width: int) -> None:
-        """8 (default): traverse the device-widened 8-wide BVH; 2: the bound BVH2."""
+        """4 (default) / 8: traverse the device-widened wide BVH; 2: the bound BVH2."""
         self._check(self.lib.hipcy_set_bvh_width(self.h, int(width)))
+
+    def set_slots(self, slots: int = 0, record_bytes: int = 0) -> None:
+        """Path slots in flight and the per-pass sample-record budget (0 keeps a value)."""
+        self._check(self.lib.hipcy_set_slots(self.h, int(slots), int(record_bytes)))
+
+    def set_bvh_leaf_merge(self, max_prims: int) -> None:
+        """Wide BVH: merge BVH2 subtrees of <= max_prims contiguous primitives into one leaf."""
+        self._check(self.lib.hipcy_set_bvh_leaf_merge(self.h, int(max_prims)))
 
     def stats(self) -> dict:
         st = native.Stats()

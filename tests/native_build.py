@@ -44,15 +44,16 @@ def host_emu(libm_sincos: bool = True):
     vp, ci, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
     lib.emu_render.argtypes = [vp, ci, vp, vp, vp, vp] + [ci] * 9
     lib.emu_intersect.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, vp, vp, vp]
-    lib.emu_bvh8_build.restype = cl
-    lib.emu_bvh8_build.argtypes = [vp, cl, vp, cl, ci, vp, cl, vp, ctypes.c_char_p, ci]
+    lib.emu_bvhw_build.restype = cl
+    lib.emu_bvhw_build.argtypes = [ci, ci, vp, cl, vp, cl, ci, vp, cl, vp, ctypes.c_char_p, ci]
+    lib.emu_set_width.argtypes = [ci]
     return lib
 
 
 class EmuScene:
     """A DeviceScene bound for the host emulator (pointers kept alive)."""
 
-    def __init__(self, lib, ds, bvh_width=2):
+    def __init__(self, lib, ds, bvh_width=2, merge_prims=0):
         import numpy as np
 
         self.lib, self.ds = lib, ds
@@ -61,14 +62,13 @@ class EmuScene:
         self.c_names = (ctypes.c_char_p * len(self.names))(*[n.encode() for n in self.names])
         self.c_ptrs = (ctypes.c_void_p * len(self.names))(*[a.ctypes.data for a in self.arrs])
         self.data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
-        self.bvh8 = bvh8_build(lib, ds)[0] if bvh_width == 8 else None
-
-    @property
-    def bvh8_ptr(self):
-        return None if self.bvh8 is None else self.bvh8.ctypes.data
+        self.width = bvh_width
+        self.wide = bvhw_build(lib, ds, bvh_width, merge_prims)[0] if bvh_width > 2 else None
 
     def args(self):
-        return (ctypes.addressof(self.data), len(self.names), self.c_names, self.c_ptrs, self.bvh8_ptr)
+        self.lib.emu_set_width(self.width)
+        ptr = None if self.wide is None else self.wide.ctypes.data
+        return (ctypes.addressof(self.data), len(self.names), self.c_names, self.c_ptrs, ptr)
 
     def intersect(self, rays, any_hit=False):
         import numpy as np
@@ -97,18 +97,18 @@ class EmuScene:
         return buf
 
 
-def bvh8_build(lib, ds):
+def bvhw_build(lib, ds, width=4, merge_prims=0):
     """Widen the scene's BVH2 exactly like the device library; returns
-    (uint32 array of 32 words per node, depth)."""
+    (uint32 array of 8*width words per node, depth)."""
     import numpy as np
 
     nodes = np.ascontiguousarray(ds.arrays["__bvh_nodes"], dtype=np.float32).reshape(-1)
     leaves = np.ascontiguousarray(ds.arrays["__bvh_leaf_nodes"], dtype=np.float32).reshape(-1)
-    cap = 32 * (len(leaves) // 4 + 2)
+    cap = 8 * width * (len(leaves) // 4 + 2)
     out = np.zeros(cap, dtype=np.uint32)
     depth = ctypes.c_int(0)
     err = ctypes.create_string_buffer(256)
-    n = lib.emu_bvh8_build(nodes.ctypes.data, len(nodes) // 4, leaves.ctypes.data, len(leaves) // 4,
+    n = lib.emu_bvhw_build(width, merge_prims, nodes.ctypes.data, len(nodes) // 4, leaves.ctypes.data, len(leaves) // 4,
                            int(ds.data.bvh.root), out.ctypes.data, cap, ctypes.byref(depth), err, 256)
     if n < 0:
         raise RuntimeError(err.value.decode())

@@ -12,8 +12,8 @@ contraction); rendered film within 1e-4 RMSE of the reference.
 
 Every test runs twice: traversing the BVH2 exactly as bound (bvh width 2: the
 reference's visiting order, so renders are bit-identical) and the device's
-8-wide BVH (width 8, the default), whose visiting order can only change which
-of two primitives at the same distance wins (tests/test_bvh8.py).
+4-wide BVH (width 4, the default), whose visiting order can only change which
+of two primitives at the same distance wins (tests/test_bvh_wide.py).
 """
 import numpy as np
 import pytest
@@ -34,7 +34,7 @@ def device():
     dev.close()
 
 
-@pytest.fixture(scope="module", params=[(n, w) for w in (2, 8) for n in CASES], ids=lambda p: f"{p[0]}-bvh{p[1]}")
+@pytest.fixture(scope="module", params=[(n, w) for w in (2, 4, 8) for n in CASES], ids=lambda p: f"{p[0]}-bvh{p[1]}")
 def case(request, device):
     name, width = request.param
     ds = compile_case(name)
@@ -73,7 +73,7 @@ def test_closest_hit_matches_reference(case, device):
         assert np.array_equal(oi[hit, 1], ref_i[hit, 1]), name
         assert np.array_equal(of[hit].view(np.uint32), ref_f[hit].view(np.uint32)), name
         return
-    # 8-wide: closest-hit rays (any-hit rays report whichever primitive comes first)
+    # wide: closest-hit rays (any-hit rays report whichever primitive comes first)
     hit &= (g["rays"][:, 7].view(np.uint32) & PATH_RAY_SHADOW_OPAQUE) == 0
     same = oi[hit, 1] == ref_i[hit, 1]
     assert same.mean() >= 0.995, (name, same.mean())

@@ -30,6 +30,11 @@ if [[ $MODE == all || $MODE == bench ]]; then
   step bench_quick 600 python bench.py --steps 2 --warmup 1 --samples 16 --no-cpu-baseline
   step bench 900 python bench.py --steps 3 --warmup 1 --save gpurun_out/bmw.png
 fi
+if [[ $MODE == quick ]]; then
+  step pytest_gpu 900 python -m pytest tests -x -q -m gpu
+  step bench_w8 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bvh-width 8
+  step bench_w2 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bvh-width 2
+fi
 if [[ $MODE == all || $MODE == prof ]]; then
   step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 fi

@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU-box variant sweep: parity tests once, then one short bench per argument
+# set (each set is one quoted string).  Stops at the first fatal status.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
+if [[ ${SKIP_TESTS:-0} != 1 ]]; then
+  timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_gpu.log
+  if fatal $rc; then exit $rc; fi
+fi
+i=0
+for args in "$@"; do
+  i=$((i+1))
+  timeout -k 10 600 python bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline $args > gpurun_out/sweep_$i.log 2>&1
+  rc=$?
+  echo "[$args] rc=$rc"
+  grep '"metric"' gpurun_out/sweep_$i.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); r=d['roofline']
+    print('  value %.1f Msps  ms/step %.1f  closest %.1f shade %.1f shadow %.1f  frac %.4f  avg_launch %.3f ms  nodes-bytes %d' % (d['value'], d['ms_per_step'], d['kernel_ms_per_frame']['k_intersect_closest'], d['kernel_ms_per_frame']['k_shade'], d['kernel_ms_per_frame']['k_intersect_shadow'], r['frac'], r['avg_launch_ms'], r['bvh_bytes']))
+" || tail -n 5 gpurun_out/sweep_$i.log
+  if fatal $rc; then exit $rc; fi
+done

@@ -11,15 +11,18 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <vector>
 
 #include "../raytracingproject_amd/csrc/kernel/cy_integrator.h"
-#include "../raytracingproject_amd/csrc/kernel/cy_bvh8.h"
-#include "../raytracingproject_amd/csrc/host/cy_bvh8_collapse.h"
+#include "../raytracingproject_amd/csrc/kernel/cy_bvhw.h"
+#include "../raytracingproject_amd/csrc/host/cy_bvhw_collapse.h"
 
-/* Widen a packed BVH2 like the device library does (hipcycles.hip ensure_bvh8).
+/* Widen a packed BVH2 like the device library does (hipcycles.hip ensure_bvhw).
  * Returns the number of uint32 written (32 per node), or -1 with the reason
  * copied to err_out. */
-extern "C" long emu_bvh8_build(const float *nodes2,
+extern "C" long emu_bvhw_build(int width,
+                               int merge_prims,
+                               const float *nodes2,
                                long n_nodes2,
                                const float *leaves2,
                                long n_leaves2,
@@ -30,7 +33,9 @@ extern "C" long emu_bvh8_build(const float *nodes2,
                                char *err_out,
                                int err_len)
 {
-  cybvh8::Collapser col;
+  cybvhw::Collapser col;
+  col.width = width;
+  col.merge_prims = merge_prims;
   col.nodes2 = nodes2;
   col.n_nodes2 = (size_t)n_nodes2;
   col.leaves2 = leaves2;
@@ -48,8 +53,10 @@ extern "C" long emu_bvh8_build(const float *nodes2,
   return (long)col.out.size();
 }
 
+static int g_width = 2;
+
 static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char **names, const void **ptrs,
-                     const void *bvh8)
+                     const void *bvhw)
 {
   memset(kg, 0, sizeof(*kg));
   kg->data = (const hc_KernelData *)data;
@@ -60,15 +67,23 @@ static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char *
     CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
   }
-  kg->bvh8_nodes = (const hc_uint4 *)bvh8;
+  kg->bvhw_nodes = bvhw;
+}
+
+extern "C" void emu_set_width(int w)
+{
+  g_width = w;
 }
 
 template<bool any_hit>
 static bool emu_traverse(const CyGlobals *kg, const CyRay *ray, uint vis, CyIsect *isect, uint *err,
                          uint *nn, uint *nl, uint *nt)
 {
-  if (kg->bvh8_nodes) {
-    return bvh8_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+  if (kg->bvhw_nodes) {
+    if (g_width == 8) {
+      return bvhw_intersect<8, any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+    }
+    return bvhw_intersect<4, any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
   }
   return bvh2_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
 }
@@ -79,7 +94,7 @@ extern "C" int emu_intersect(const void *data,
                              int n_arrays,
                              const char **names,
                              const void **ptrs,
-                             const void *bvh8,
+                             const void *bvhw,
                              const float *rays,
                              int n,
                              int any_hit,
@@ -88,7 +103,7 @@ extern "C" int emu_intersect(const void *data,
                              unsigned long long *counters)
 {
   CyGlobals kg;
-  emu_bind(&kg, data, n_arrays, names, ptrs, bvh8);
+  emu_bind(&kg, data, n_arrays, names, ptrs, bvhw);
   uint err = 0;
   for (int i = 0; i < n; i++) {
     const float *r = rays + 8 * i;
@@ -131,7 +146,7 @@ extern "C" int emu_render(const void *data,
                           int n_arrays,
                           const char **names,
                           const void **ptrs,
-                          const void *bvh8,
+                          const void *bvhw,
                           float *buffer,
                           int tx,
                           int ty,
@@ -144,10 +159,11 @@ extern "C" int emu_render(const void *data,
                           int pass_stride)
 {
   CyGlobals kg;
-  emu_bind(&kg, data, n_arrays, names, ptrs, bvh8);
+  emu_bind(&kg, data, n_arrays, names, ptrs, bvhw);
   hc_float4 rec[12];
   int isect_type = 0;
   hc_uint4 s0, s1;
+  uint item_slot = 0;
   CyPathBuffers b;
   b.ray_P = &rec[0];
   b.ray_D = &rec[1];
@@ -161,77 +177,82 @@ extern "C" int emu_render(const void *data,
   b.shadow_P = &rec[6];
   b.shadow_D = &rec[7];
   b.shadow_L = &rec[8];
+  b.item = &item_slot;
   uint err = 0;
-  for (int sample = start_sample; sample < start_sample + num_samples; sample++) {
-    for (int y = ty; y < ty + th; y++) {
-      for (int x = tx; x < tx + tw; x++) {
-        CyTile tile;
-        tile.x = x;
-        tile.y = y;
-        tile.w = 1;
-        tile.h = 1;
-        tile.y_step = 1;
-        tile.start_sample = sample;
-        tile.end_sample = sample + 1;
-        tile.offset = offset;
-        tile.stride = stride;
-        tile.buffer = buffer;
-        tile.pass_stride = pass_stride;
-        bool active = slot_regenerate(&kg, &b, &tile, 0, sample);
-        while (active) {
-          /* k_intersect_closest */
-          CyRay ray;
-          ray.P = mk3(rec[0].x, rec[0].y, rec[0].z);
-          ray.t = rec[0].w;
-          ray.D = mk3(rec[1].x, rec[1].y, rec[1].z);
-          CyPathState s;
-          s.flag = (int)s0.x;
-          uint visibility = path_state_ray_visibility(&s);
-          CyIsect isect;
-          bool hit = false;
-          if (scene_intersect_valid(&ray)) {
-            hit = emu_traverse<false>(&kg, &ray, visibility, &isect, &err, nullptr, nullptr, nullptr);
-          }
-          if (hit) {
-            rec[2] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
-            isect_type = isect.type;
-          }
-          else {
-            isect_type = 0;
-          }
-          /* k_shade */
-          bool shadow = false;
-          bool cont = shade_path(&kg, &b, &tile, 0, &shadow, &err);
-          bool regen = false;
-          if (shadow) {
-            /* k_intersect_shadow */
-            CyRay sr;
-            sr.P = mk3(rec[6].x, rec[6].y, rec[6].z);
-            sr.t = rec[6].w;
-            sr.D = mk3(rec[7].x, rec[7].y, rec[7].z);
-            bool blocked = false;
-            if (scene_intersect_valid(&sr)) {
-              CyIsect si;
-              blocked = emu_traverse<true>(&kg, &sr, PATH_RAY_SHADOW_OPAQUE, &si, &err, nullptr, nullptr, nullptr);
-            }
-            hc_float4 sl = rec[8];
-            hc_float4 L4 = rec[5];
-            if (!blocked) {
-              L4.x = L4.x + sl.x;
-              L4.y = L4.y + sl.y;
-              L4.z = L4.z + sl.z;
-            }
-            if (sl.w != 0.0f) {
-              regen = slot_finish(&kg, &b, &tile, 0, (int)s0.w, mk3(L4.x, L4.y, L4.z), rec[4].w);
-            }
-            else {
-              rec[5] = L4;
-            }
-          }
-          active = cont || regen;
+  CyTile tile;
+  tile.x = tx;
+  tile.y = ty;
+  tile.w = tw;
+  tile.h = th;
+  tile.y_step = 1;
+  tile.start_sample = start_sample;
+  tile.end_sample = start_sample + num_samples;
+  tile.offset = offset;
+  tile.stride = stride;
+  tile.buffer = buffer;
+  tile.pass_stride = pass_stride;
+  tile.n_items = (uint)(tw * th * num_samples);
+  tile.work_next = nullptr;
+  std::vector<hc_float4> records(tile.n_items);
+  tile.samples_out = records.data();
+  /* one slot, items in order: the device runs the same per-item code with
+   * many slots in flight; the result per item does not depend on the slot */
+  for (uint item = 0; item < tile.n_items; item++) {
+    bool active = slot_start(&kg, &b, &tile, 0, item);
+    while (active) {
+      /* k_intersect_closest */
+      CyRay ray;
+      ray.P = mk3(rec[0].x, rec[0].y, rec[0].z);
+      ray.t = rec[0].w;
+      ray.D = mk3(rec[1].x, rec[1].y, rec[1].z);
+      CyPathState s;
+      s.flag = (int)s0.x;
+      uint visibility = path_state_ray_visibility(&s);
+      CyIsect isect;
+      bool hit = false;
+      if (scene_intersect_valid(&ray)) {
+        hit = emu_traverse<false>(&kg, &ray, visibility, &isect, &err, nullptr, nullptr, nullptr);
+      }
+      if (hit) {
+        rec[2] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
+        isect_type = isect.type;
+      }
+      else {
+        isect_type = 0;
+      }
+      /* k_shade */
+      bool shadow = false, finished = false;
+      bool cont = shade_path(&kg, &b, &tile, 0, &shadow, &finished, &err);
+      if (shadow) {
+        /* k_intersect_shadow */
+        CyRay sr;
+        sr.P = mk3(rec[6].x, rec[6].y, rec[6].z);
+        sr.t = rec[6].w;
+        sr.D = mk3(rec[7].x, rec[7].y, rec[7].z);
+        bool blocked = false;
+        if (scene_intersect_valid(&sr)) {
+          CyIsect si;
+          blocked = emu_traverse<true>(&kg, &sr, PATH_RAY_SHADOW_OPAQUE, &si, &err, nullptr, nullptr, nullptr);
+        }
+        hc_float4 sl = rec[8];
+        hc_float4 L4 = rec[5];
+        if (!blocked) {
+          L4.x = L4.x + sl.x;
+          L4.y = L4.y + sl.y;
+          L4.z = L4.z + sl.z;
+        }
+        if (sl.w != 0.0f) {
+          slot_finish(&b, &tile, 0, mk3(L4.x, L4.y, L4.z), rec[4].w);
+        }
+        else {
+          rec[5] = L4;
         }
       }
+      active = cont;
     }
+  }
+  for (int p = 0; p < tw * th; p++) {
+    accumulate_pixel(&tile, p);
   }
   return (int)err;
 }
