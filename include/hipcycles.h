@@ -107,7 +107,7 @@ int hipcy_set_bvh_width(hipcy_device *dev, int width);
 /* Wide BVH only: BVH2 subtrees holding at most max_prims (0..15) primitives in
  * one contiguous range become a single leaf child (0 = keep BVH2 leaves). */
 int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims);
-/* Path slots kept in flight (default 2^20) and the byte budget of the
+/* Path slots kept in flight (default 2^23) and the byte budget of the
  * per-sample record buffer of one pass (default 4 GiB; a tile whose samples do
  * not fit is rendered in several sample passes).  0 keeps a value. */
 int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);

@@ -346,7 +346,7 @@ struct hipcy_device {
   int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
 
   /* path slots in flight and the per-sample record buffer of one pass */
-  size_t slots_wanted = (size_t)1 << 20;
+  size_t slots_wanted = (size_t)1 << 23;
   size_t record_budget = (size_t)4 << 30; /* bytes of sample records per pass */
   hc_float4 *records = nullptr;
   size_t records_capacity = 0;
