@@ -78,9 +78,11 @@ def main(tag):
             if dk == k:
                 ent["rocprof_avg_ms"] = ms
         summary[k] = ent
-    # bench.py's name for the dominant kernel (template instance without counters)
-    if "k_intersect_closest<false>" in summary:
-        summary["k_intersect_closest"] = summary["k_intersect_closest<false>"]
+    # bench.py's name for the dominant kernel: the instance without counters
+    # (k_intersect_closest<false, W>) of the BVH width that was profiled
+    for k in sorted(summary):
+        if k.startswith("k_intersect_closest<false"):
+            summary["k_intersect_closest"] = dict(summary[k], instance=k)
     with open(os.path.join(prof, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps(summary.get("k_intersect_closest", {}), indent=1))
