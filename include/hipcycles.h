@@ -97,7 +97,8 @@ int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, s
 int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_pointer, size_t bytes);
 
 /* Validate that the scene uploaded so far only uses features the HIP kernels
- * implement; returns 0 or a negative code with a readable hipcy_error(). */
+ * implement and prepare it (widen the BVH); returns 0 or a negative code with a
+ * readable hipcy_error().  hipcy_path_trace calls it too. */
 int hipcy_load_kernels(hipcy_device *dev);
 uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *dev); /* BVH_LAYOUT_BVH2 = 1 */
 /* Traversal structure: 4 (default) or 8 widens the bound BVH2 into the

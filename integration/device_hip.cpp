@@ -1,0 +1,250 @@
+/*
+ * device_hip.cpp — the Cycles-side plugin a maintainer adds to
+ * intern/cycles/device/ so Blender's unchanged host drives the MI355X path
+ * tracer.  It is a ccl::Device (device/device.h:288-500) whose every method
+ * forwards to the C ABI of include/hipcycles.h; nothing here computes.
+ *
+ * Registration (INTEGRATION.md lists the exact edits):
+ *   device/device_intern.h   declare device_hipcy_init/create/info
+ *   device/device.cpp:385    case DEVICE_HIPCY: device = device_hipcy_create(info, stats, profiler, background);
+ *   device/device.cpp:500    append device_hipcy_info(...) in available_devices
+ *   device/device.h:43-60    DEVICE_HIPCY in DeviceType / DEVICE_MASK_HIPCY
+ *
+ * Semantics mirror CUDADevice (device/cuda/device_cuda_impl.cpp):
+ *   MEM_GLOBAL arrays are bound by name (global_alloc, :1088-1096);
+ *   RENDER tasks loop acquire_tile -> path trace -> update_progress ->
+ *   release_tile on one worker thread per device (thread_run, :2342-2391);
+ *   the first error is sticky and reported through error_message().
+ *
+ * Compile-checked (g++ -fsyntax-only against the reference headers) by
+ * tests/test_integration.py; it is not linked into this repository's products.
+ */
+#include "device/device.h"
+#include "device/device_intern.h"
+
+#include "render/buffers.h"
+
+#include "util/util_logging.h"
+#include "util/util_string.h"
+#include "util/util_task.h"
+#include "util/util_thread.h"
+
+#include "hipcycles.h"
+
+CCL_NAMESPACE_BEGIN
+
+class HIPCyclesDevice : public Device {
+ public:
+  HIPCyclesDevice(DeviceInfo &info, Stats &stats, Profiler &profiler, bool background)
+      : Device(info, stats, profiler, background), dev_(hipcy_create(info.num))
+  {
+    if (dev_ == nullptr) {
+      set_error(string_printf("HIP device %d: %s", info.num, hipcy_global_error()));
+    }
+  }
+
+  ~HIPCyclesDevice() noexcept(false)
+  {
+    task_pool_.cancel();
+    hipcy_destroy(dev_);
+  }
+
+  /* device.h:353 — the host keeps building Cycles' BVH2; the device widens it */
+  BVHLayoutMask get_bvh_layout_mask() const override
+  {
+    return BVH_LAYOUT_BVH2;
+  }
+
+  /* device.h:366 — KernelData ("__data"), scene.cpp:307 / light.cpp:66 */
+  void const_copy_to(const char *name, void *host, size_t size) override
+  {
+    check(hipcy_const_copy_to(dev_, name, host, size));
+  }
+
+  /* device.h:375 — features the kernels do not implement are refused here, and
+   * once more against the uploaded KernelData before the first render */
+  bool load_kernels(const DeviceRequestedFeatures &f) override
+  {
+    if (f.use_hair || f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_subsurface ||
+        f.use_volume || f.use_integrator_branched || f.use_patch_evaluation || f.use_true_displacement ||
+        f.use_shader_raytrace || f.use_denoising) {
+      set_error("HIP device: requested features are not implemented (" + f.get_build_options() + ")");
+      return false;
+    }
+    return true;
+  }
+
+  /* device.h:484-488 */
+  void mem_alloc(device_memory &mem) override
+  {
+    if (mem.type == MEM_PIXELS || mem.type == MEM_TEXTURE) {
+      set_error(string_printf("HIP device: memory kind of %s is not supported", mem.name));
+      return;
+    }
+    uint64_t ptr = 0;
+    const size_t bytes = mem.memory_size();
+    if (check(hipcy_mem_alloc(dev_, bytes, &ptr))) {
+      mem.device_pointer = (device_ptr)ptr;
+      mem.device_size = bytes;
+      stats.mem_alloc(bytes);
+    }
+  }
+
+  void mem_copy_to(device_memory &mem) override
+  {
+    if (!mem.device_pointer) {
+      mem_alloc(mem);
+    }
+    if (!mem.device_pointer) {
+      return;
+    }
+    if (mem.host_pointer && mem.memory_size()) {
+      check(hipcy_mem_copy_to(dev_, (uint64_t)mem.device_pointer, mem.host_pointer, mem.memory_size()));
+    }
+    if (mem.type == MEM_GLOBAL) {
+      /* CUDADevice::global_alloc: bind the array to its kernel_textures.h name */
+      check(hipcy_bind_global(dev_, mem.name, (uint64_t)mem.device_pointer, mem.memory_size()));
+    }
+  }
+
+  void mem_copy_from(device_memory &mem, int y, int w, int h, int elem) override
+  {
+    const size_t offset = (size_t)elem * y * w;
+    const size_t size = (size_t)elem * w * h;
+    if (mem.host_pointer && mem.device_pointer) {
+      check(hipcy_mem_copy_from(dev_, (char *)mem.host_pointer + offset, (uint64_t)mem.device_pointer + offset,
+                                size));
+    }
+  }
+
+  void mem_zero(device_memory &mem) override
+  {
+    if (!mem.device_pointer) {
+      mem_alloc(mem);
+    }
+    if (mem.host_pointer) {
+      memset(mem.host_pointer, 0, mem.memory_size());
+    }
+    if (mem.device_pointer) {
+      check(hipcy_mem_zero(dev_, (uint64_t)mem.device_pointer, mem.memory_size()));
+    }
+  }
+
+  void mem_free(device_memory &mem) override
+  {
+    if (mem.device_pointer) {
+      if (mem.type == MEM_GLOBAL) {
+        hipcy_bind_global(dev_, mem.name, 0, 0);
+      }
+      check(hipcy_mem_free(dev_, (uint64_t)mem.device_pointer));
+      stats.mem_free(mem.device_size);
+      mem.device_pointer = 0;
+      mem.device_size = 0;
+    }
+  }
+
+  /* device.h:403-405 — one worker thread per device, like CUDADevice::task_add */
+  void task_add(DeviceTask &task) override
+  {
+    if (task.type != DeviceTask::RENDER) {
+      set_error("HIP device: only RENDER tasks are implemented");
+      return;
+    }
+    task_pool_.push([=] {
+      DeviceTask task_copy = task;
+      render(task_copy);
+    });
+  }
+
+  void task_wait() override
+  {
+    task_pool_.wait();
+  }
+
+  void task_cancel() override
+  {
+    task_pool_.cancel();
+  }
+
+ private:
+  hipcy_device *dev_;
+  DedicatedTaskPool task_pool_; /* one worker thread, as CUDADevice (device_cuda.h:45) */
+
+  bool check(int rc)
+  {
+    if (rc != 0 && dev_ != nullptr) {
+      set_error(string_printf("HIP device: %s", hipcy_error(dev_)));
+    }
+    return rc == 0;
+  }
+
+  /* CUDADevice::thread_run RENDER branch (device_cuda_impl.cpp:2346-2386) */
+  void render(DeviceTask &task)
+  {
+    if (!check(hipcy_load_kernels(dev_))) {
+      return;
+    }
+    RenderTile tile;
+    while (task.acquire_tile(this, tile, task.tile_types)) {
+      if (tile.task == RenderTile::PATH_TRACE) {
+        hipcy_work_tile wt;
+        wt.x = tile.x;
+        wt.y = tile.y;
+        wt.w = tile.w;
+        wt.h = tile.h;
+        wt.start_sample = tile.start_sample;
+        wt.num_samples = tile.num_samples;
+        wt.offset = tile.offset;
+        wt.stride = tile.stride;
+        wt.buffer = (uint64_t)tile.buffer;
+        if (!check(hipcy_path_trace(dev_, &wt)) || !check(hipcy_synchronize(dev_))) {
+          task.release_tile(tile);
+          break;
+        }
+        tile.sample = tile.start_sample + tile.num_samples;
+        task.update_progress(&tile, tile.w * tile.h * tile.num_samples);
+      }
+      task.release_tile(tile);
+      if (task.get_cancel() && !task.need_finish_queue) {
+        break;
+      }
+    }
+  }
+};
+
+bool device_hipcy_init()
+{
+  int n = 0;
+  return hipcy_device_count(&n) == 0 && n > 0;
+}
+
+Device *device_hipcy_create(DeviceInfo &info, Stats &stats, Profiler &profiler, bool background)
+{
+  return new HIPCyclesDevice(info, stats, profiler, background);
+}
+
+void device_hipcy_info(vector<DeviceInfo> &devices)
+{
+  int n = 0;
+  hipcy_device_count(&n);
+  for (int i = 0; i < n; i++) {
+    char name[256];
+    uint64_t mem = 0;
+    if (hipcy_device_info(i, name, sizeof(name), &mem) != 0) {
+      continue;
+    }
+    DeviceInfo info;
+    info.type = DEVICE_CUDA; /* replace with DEVICE_HIPCY once the enum entry is added */
+    info.description = string(name);
+    info.num = i;
+    info.id = string_printf("HIPCY_%d", i);
+    info.has_half_images = false;
+    info.has_volume_decoupled = false;
+    info.has_osl = false;
+    info.has_profiling = false;
+    info.denoisers = DENOISER_NONE;
+    devices.push_back(info);
+  }
+}
+
+CCL_NAMESPACE_END

@@ -387,6 +387,8 @@ static int set_error(hipcy_device *dev, const std::string &msg)
     } \
   } while (0)
 
+static int ensure_bvhw(hipcy_device *dev);
+
 static bool build_globals(hipcy_device *dev, CyGlobals *kg)
 {
   memset(kg, 0, sizeof(*kg));
@@ -768,7 +770,8 @@ int hipcy_load_kernels(hipcy_device *dev)
       return set_error(dev, std::string("load_kernels: array not bound: ") + r);
     }
   }
-  return 0;
+  /* scene-preparation step of the device: widen the BVH now, not in the first render */
+  return ensure_bvhw(dev);
 }
 
 int hipcy_set_profiling(hipcy_device *dev, int flags)
