@@ -70,13 +70,36 @@ def kernel_source_digest():
     return h.hexdigest()[:16]
 
 
-def build_device(force=False):
-    src = os.path.join(HERE, "csrc", "device", "hipcycles.hip")
-    out = os.path.join(HERE, "libhipcycles.so")
-    deps = _sources(os.path.join(HERE, "csrc", "kernel"), os.path.join(HERE, "csrc", "device"),
+SHADE_VARIANTS = (1, 2, 4, 8)  # closure-array sizes of the shade kernel (csrc/device/k_shade.h)
+
+
+def build_device(force=False, variant=None, defines=()):
+    """The HIP device library: hipcycles.hip plus k_shade.hip compiled once per
+    closure-array size.  A named variant (tuning builds with extra -D defines)
+    goes to libhipcycles_<variant>.so next to the default one."""
+    dev_dir = os.path.join(HERE, "csrc", "device")
+    src = os.path.join(dev_dir, "hipcycles.hip")
+    out = os.path.join(HERE, f"libhipcycles_{variant}.so" if variant else "libhipcycles.so")
+    deps = _sources(os.path.join(HERE, "csrc", "kernel"), dev_dir, os.path.join(HERE, "csrc", "host"),
                     os.path.join(REPO, "include"))
-    if force or _stale(out, deps):
-        _run([HIPCC, *HIP_FLAGS, "-I" + os.path.join(REPO, "include"), "-o", out, src])
+    if not (force or variant or _stale(out, deps)):
+        return out
+    inc = "-I" + os.path.join(REPO, "include")
+    dflags = ["-D" + d for d in defines]
+    objdir = os.path.join(REPO, "build", "device", variant or "default")
+    os.makedirs(objdir, exist_ok=True)
+    from concurrent.futures import ThreadPoolExecutor
+
+    cflags = [f for f in HIP_FLAGS if f != "-shared"]
+    jobs = [([HIPCC, *cflags, *dflags, inc, "-c", "-o", os.path.join(objdir, "hipcycles.o"), src],
+             os.path.join(objdir, "hipcycles.o"))]
+    for mc in SHADE_VARIANTS:
+        obj = os.path.join(objdir, f"k_shade_mc{mc}.o")
+        jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT=mc{mc}", inc, "-c",
+                      "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
+    with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
+        list(ex.map(lambda j: _run(j[0]), jobs))
+    _run([HIPCC, "--offload-arch=gfx950", "-fno-gpu-rdc", "-shared", "-fPIC", "-o", out, *[j[1] for j in jobs]])
     return out
 
 
@@ -105,4 +128,8 @@ def build_all(ref=True, force=False):
 
 
 if __name__ == "__main__":
-    build_all(ref="--no-ref" not in sys.argv, force="--force" in sys.argv)
+    if "--variant" in sys.argv:
+        name = sys.argv[sys.argv.index("--variant") + 1]
+        build_device(variant=name, defines=[a[2:] for a in sys.argv if a.startswith("-D")])
+    else:
+        build_all(ref="--no-ref" not in sys.argv, force="--force" in sys.argv)

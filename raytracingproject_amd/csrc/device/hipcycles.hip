@@ -17,7 +17,8 @@
 #include <vector>
 
 #include "hipcycles.h"
-#include "../kernel/cy_integrator.h"
+#include "cy_device_common.h"
+#include "k_shade.h"
 #include "../kernel/cy_bvhw.h"
 #include "../host/cy_bvhw_collapse.h"
 
@@ -44,68 +45,6 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
 
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
-
-__device__ __forceinline__ void queue_push(int *queue, uint *counter, int slot, bool active)
-{
-  /* wave-aggregated append: one atomic per wave */
-  const unsigned long long mask = __ballot(active);
-  if (mask == 0) {
-    return;
-  }
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)mask) - 1;
-  uint base = 0;
-  if (lane == leader) {
-    base = atomicAdd(counter, (uint)__popcll(mask));
-  }
-  base = __shfl(base, leader);
-  if (active) {
-    const unsigned long long lower = mask & ((1ull << lane) - 1ull);
-    queue[base + __popcll(lower)] = slot;
-  }
-}
-
-__device__ __forceinline__ void stats_add(unsigned long long *dst, uint v)
-{
-  /* wave reduce then one atomic */
-  unsigned long long x = v;
-  for (int off = 32; off > 0; off >>= 1) {
-    x += __shfl_xor(x, off);
-  }
-  if ((threadIdx.x & 63) == 0 && x) {
-    atomicAdd(dst, x);
-  }
-}
-
-/* Claim the next work item for every lane with need set (one atomic per wave)
- * and start it; samples without a camera ray are recorded as such and the lane
- * claims again.  Returns true when the slot holds a new path. */
-__device__ __forceinline__ bool slot_refill(const CyGlobals &kg, const CyPathBuffers &b, const CyTile &tile,
-                                            int slot, bool need)
-{
-  const unsigned long long mask = __ballot(need);
-  if (mask == 0) {
-    return false;
-  }
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)mask) - 1;
-  uint base = 0;
-  if (lane == leader) {
-    base = atomicAdd(tile.work_next, (uint)__popcll(mask));
-  }
-  base = __shfl(base, leader);
-  uint item = base + (uint)__popcll(mask & ((1ull << lane) - 1ull));
-  while (need) {
-    if (item >= tile.n_items) {
-      return false;
-    }
-    if (slot_start(&kg, &b, &tile, slot, item)) {
-      return true;
-    }
-    item = atomicAdd(tile.work_next, 1u);
-  }
-  return false;
-}
 
 __global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
                                                           CyPathBuffers b,
@@ -169,29 +108,6 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     stats_add(&stats[0].leaves, n_leaves);
     stats_add(&stats[0].tris, n_tris);
   }
-}
-
-__global__ void __launch_bounds__(CY_BLOCK) k_shade(CyGlobals kg,
-                                                     CyPathBuffers b,
-                                                     CyTile tile,
-                                                     const int *queue_in,
-                                                     const uint *count_in,
-                                                     int *queue_out,
-                                                     uint *count_out,
-                                                     int *shadow_queue,
-                                                     uint *shadow_count,
-                                                     uint *err)
-{
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool cont = false, shadow = false, finished = false;
-  int slot = 0;
-  if (i < (int)*count_in) {
-    slot = queue_in[i];
-    cont = shade_path(&kg, &b, &tile, slot, &shadow, &finished, err);
-  }
-  cont |= slot_refill(kg, b, tile, slot, finished);
-  queue_push(queue_out, count_out, slot, cont);
-  queue_push(shadow_queue, shadow_count, slot, shadow);
 }
 
 template<bool STATS, int W>
@@ -895,8 +811,8 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     if (prof) {
       HIP_CHECK(dev, hipEventRecord(p.b, s));
     }
-    hipLaunchKernelGGL(k_shade, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qa], dev->counters + qa,
-                       dev->queue[qb], dev->counters + qb, dev->queue[qs], dev->counters + qs, err);
+    cy_launch_shade(dev->data_host.integrator.max_closures, grid, block, s, kg, dev->bufs, tile, dev->queue[qa],
+                    dev->counters + qa, dev->queue[qb], dev->counters + qb, dev->queue[qs], dev->counters + qs, err);
     if (prof) {
       HIP_CHECK(dev, hipEventRecord(p.c, s));
     }

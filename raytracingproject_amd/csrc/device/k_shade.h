@@ -1,0 +1,34 @@
+/*
+ * k_shade.h — launchers of the shade kernel, compiled once per closure-array
+ * size (k_shade.hip with CY_MAX_CLOSURE = 1, 2, 4, 8).  A scene's
+ * KernelIntegrator.max_closures (render/integrator.cpp) picks the smallest
+ * variant that holds its shaders' closures, so the per-path closure array
+ * stays small enough to live in registers instead of scratch.
+ */
+#ifndef K_SHADE_H
+#define K_SHADE_H
+
+#include <hip/hip_runtime.h>
+
+#include "../kernel/cy_integrator.h"
+
+#define CY_SHADE_LAUNCHER_ARGS \
+  dim3 grid, dim3 block, hipStream_t stream, const CyGlobals &kg, const CyPathBuffers &b, const CyTile &tile, \
+      const int *queue_in, const uint *count_in, int *queue_out, uint *count_out, int *shadow_queue, \
+      uint *shadow_count, uint *err
+
+void cy_launch_shade_mc1(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc2(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc4(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc8(CY_SHADE_LAUNCHER_ARGS);
+
+static inline void cy_launch_shade(int max_closures, CY_SHADE_LAUNCHER_ARGS)
+{
+  auto fn = max_closures <= 1 ? cy_launch_shade_mc1 :
+            max_closures <= 2 ? cy_launch_shade_mc2 :
+            max_closures <= 4 ? cy_launch_shade_mc4 :
+                                cy_launch_shade_mc8;
+  fn(grid, block, stream, kg, b, tile, queue_in, count_in, queue_out, count_out, shadow_queue, shadow_count, err);
+}
+
+#endif

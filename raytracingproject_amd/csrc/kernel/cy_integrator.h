@@ -399,7 +399,17 @@ CY_FN bool shade_path(const CyGlobals *kg,
 
     CySD sd;
     shader_setup_from_ray(kg, &sd, &isect, &ray);
+#ifdef CY_EXP_FIXED_SVM /* profiling experiment only: one diffuse closure, no SVM */
+    sd.num_closure = 1;
+    sd.num_closure_left = 0;
+    sd.closure[0].type = CLOSURE_BSDF_DIFFUSE_ID;
+    sd.closure[0].weight = mk3(0.8f, 0.8f, 0.8f);
+    sd.closure[0].sample_weight = 0.8f;
+    sd.closure[0].N = sd.N;
+    sd.flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
+#else
     shader_eval_surface(kg, &sd, state.flag, err);
+#endif
     shader_prepare_closures(&sd, &state);
 
     /* kernel_path_shader_apply (kernel_path.h:254-321) */
@@ -466,7 +476,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
       /* Direct light: kernel_branched_path_surface_connect_light with one sample
        * (kernel_path_surface.h:23-140), light_sample + direct_emission
        * (kernel_emission.h:101-205). */
+#ifdef CY_EXP_NO_LIGHT /* profiling experiment only: skip next-event estimation */
+      if (false) {
+#else
       if (KD->integrator.use_direct_light && (sd.flag & SD_BSDF_HAS_EVAL)) {
+#endif
         float light_u, light_v;
         path_state_rng_2D(kg, &state, PRNG_LIGHT_U, &light_u, &light_v);
         float terminate = (KD->integrator.light_inv_rr_threshold > 0.0f) ?

@@ -37,13 +37,26 @@ CY_FN void cy_set_error(uint *err, uint code, uint detail)
 /* ---------------------------------------------------------------------------
  * Random numbers: kernel_random.h:40-153 (Sobol + Cranley-Patterson rotation).
  */
+/* kernel_random.h sobol_dimension: XOR of the direction numbers of the set
+ * bits of index + SOBOL_SKIP.  The reference walks the set bits with a
+ * dependent loop; here each group of 8 bits reads its 8 contiguous direction
+ * numbers at once (two 16-B loads, one memory latency) and masks them.  XOR is
+ * order-independent, so the result is identical. */
 CY_FN uint sobol_dimension(const CyGlobals *kg, int index, int dimension)
 {
   uint result = 0;
-  uint i = (uint)index + SOBOL_SKIP;
-  for (int j = 0, x; (x = (int)find_first_set(i)); i >>= x) {
-    j += x;
-    result ^= kg->__sample_pattern_lut[32 * dimension + j - 1];
+  const uint i = (uint)index + SOBOL_SKIP;
+  const uint *dirs = kg->__sample_pattern_lut + 32 * dimension;
+  for (int base = 0; base < 32 && (i >> base) != 0u; base += 8) {
+    uint v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      v[k] = dirs[base + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      result ^= ((i >> (base + k)) & 1u) ? v[k] : 0u;
+    }
   }
   return result;
 }

@@ -213,7 +213,9 @@ enum {
   CY_ERR_FEATURE = 6          /* unsupported scene feature reached at run time */
 };
 
-#define CY_MAX_CLOSURE 8
+#ifndef CY_MAX_CLOSURE
+#  define CY_MAX_CLOSURE 8 /* per-kernel closure array (k_shade.hip builds 1, 2, 4, 8) */
+#endif
 #define CY_SVM_STACK 32
 /* threads per workgroup of every wavefront kernel, and LDS-resident traversal
  * stack depth (CY_LDS_STACK * CY_BLOCK * 4 B = 32 KiB per workgroup) */

@@ -12,7 +12,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-DEVICE_LIB = os.path.join(_HERE, "libhipcycles.so")
+# HIPCY_DEVICE_LIB selects an alternative in-tree build (tuning variants made
+# by `python -m raytracingproject_amd.build --variant NAME -D...`)
+DEVICE_LIB = os.environ.get("HIPCY_DEVICE_LIB") or os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
 ABI_VERSION = 2  # HIPCY_ABI_VERSION in include/hipcycles.h
 

@@ -14,7 +14,11 @@ fi
 i=0
 for args in "$@"; do
   i=$((i+1))
-  timeout -k 10 600 python bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline $args > gpurun_out/sweep_$i.log 2>&1
+  envs=(); opts=()
+  for tok in $args; do
+    if [[ $tok == *=* && $tok != --* ]]; then envs+=("$tok"); else opts+=("$tok"); fi
+  done
+  timeout -k 10 600 env "${envs[@]}" python bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline "${opts[@]}" > gpurun_out/sweep_$i.log 2>&1
   rc=$?
   echo "[$args] rc=$rc"
   grep '"metric"' gpurun_out/sweep_$i.log | python3 -c "
