@@ -76,10 +76,10 @@ SHADE_VARIANTS = (1, 2, 4, 8)  # closure-array sizes of the shade kernel (csrc/d
 def build_device(force=False, variant=None, defines=()):
     """The HIP device library: hipcycles.hip plus k_shade.hip compiled once per
     closure-array size.  A named variant (tuning builds with extra -D defines)
-    goes to libhipcycles_<variant>.so next to the default one."""
+    goes to libhipcycles-<variant>.so next to the default one."""
     dev_dir = os.path.join(HERE, "csrc", "device")
     src = os.path.join(dev_dir, "hipcycles.hip")
-    out = os.path.join(HERE, f"libhipcycles_{variant}.so" if variant else "libhipcycles.so")
+    out = os.path.join(HERE, f"libhipcycles-{variant}.so" if variant else "libhipcycles.so")
     deps = _sources(os.path.join(HERE, "csrc", "kernel"), dev_dir, os.path.join(HERE, "csrc", "host"),
                     os.path.join(REPO, "include"))
     if not (force or variant or _stale(out, deps)):

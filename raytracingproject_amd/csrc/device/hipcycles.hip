@@ -54,8 +54,9 @@ __global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
                                                           uint *counter)
 {
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = slot_refill(kg, b, tile, slot, slot < n_slots);
-  queue_push(queue, counter, slot, active);
+  __shared__ uint claim[CY_CLAIM_LDS];
+  const bool active = slot_refill(kg, b, tile, slot, slot < n_slots, claim);
+  queue_push(queue, counter, slot, active, claim);
 }
 
 __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
@@ -79,13 +80,13 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*counter) {
     const int slot = queue[i];
-    const hc_float4 rp = b.ray_P[slot];
-    const hc_float4 rd = b.ray_D[slot];
+    const hc_float4 rp = cy_ld(&b.ray_P[slot]);
+    const hc_float4 rd = cy_ld(&b.ray_D[slot]);
     CyRay ray;
     ray.P = mk3(rp.x, rp.y, rp.z);
     ray.t = rp.w;
     ray.D = mk3(rd.x, rd.y, rd.z);
-    const uint flag = b.state0[slot].x;
+    const uint flag = cy_ld(&b.state0[slot]).x;
     CyPathState s;
     s.flag = (int)flag;
     const uint visibility = path_state_ray_visibility(&s);
@@ -96,11 +97,11 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                         STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     if (hit) {
-      b.isect[slot] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
-      b.isect_type[slot] = isect.type;
+      cy_st(&b.isect[slot], mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim)));
+      cy_st(&b.isect_type[slot], isect.type);
     }
     else {
-      b.isect_type[slot] = 0;
+      cy_st(&b.isect_type[slot], 0);
     }
   }
   if (STATS) {
@@ -128,8 +129,8 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*shadow_count) {
     slot = shadow_queue[i];
-    const hc_float4 sp = b.shadow_P[slot];
-    const hc_float4 sdr = b.shadow_D[slot];
+    const hc_float4 sp = cy_ld(&b.shadow_P[slot]);
+    const hc_float4 sdr = cy_ld(&b.shadow_D[slot]);
     CyRay ray;
     ray.P = mk3(sp.x, sp.y, sp.z);
     ray.t = sp.w;
@@ -140,23 +141,24 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
       blocked = scene_traverse<W, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
                                            STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
-    const hc_float4 sl = b.shadow_L[slot];
-    hc_float4 L4 = b.L[slot];
+    const hc_float4 sl = cy_ld(&b.shadow_L[slot]);
+    hc_float4 L4 = cy_ld(&b.L[slot]);
     if (!blocked) {
       L4.x = L4.x + sl.x;
       L4.y = L4.y + sl.y;
       L4.z = L4.z + sl.z;
     }
     if (sl.w != 0.0f) {
-      slot_finish(&b, &tile, slot, mk3(L4.x, L4.y, L4.z), b.throughput[slot].w);
+      slot_finish(&b, &tile, slot, mk3(L4.x, L4.y, L4.z), cy_ld(&b.throughput[slot]).w);
       finished = true;
     }
     else {
-      b.L[slot] = L4;
+      cy_st(&b.L[slot], L4);
     }
   }
-  const bool regen = slot_refill(kg, b, tile, slot, finished);
-  queue_push(queue_out, count_out, slot, regen);
+  __shared__ uint claim[CY_CLAIM_LDS];
+  const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
+  queue_push(queue_out, count_out, slot, regen, claim);
   if (STATS) {
     stats_add(&stats[1].nodes, n_nodes);
     stats_add(&stats[1].leaves, n_leaves);

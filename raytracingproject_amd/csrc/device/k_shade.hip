@@ -9,11 +9,20 @@
 #ifndef CY_SHADE_VARIANT
 #  error "CY_SHADE_VARIANT must be defined (mc1, mc2, mc4, mc8)"
 #endif
+/* Closures and the first CY_SVM_LDS stack entries in LDS for closure arrays of
+ * up to 4 (LDS per 256-thread block: (11*MAXC + 1 + CY_SVM_LDS) KiB; MAXC 2:
+ * 39 KiB = 4 blocks per CU), private memory for 8. */
+#ifndef CY_SHADE_LDS
+#  define CY_SHADE_LDS (CY_MAX_CLOSURE <= 4)
+#endif
+#define CY_SVM_LDS 16
+#define CY_CLOSURE_DWORDS ((int)(sizeof(CyClosure) / 4) * CY_MAX_CLOSURE + 1)
+
 #define CY_CAT2(a, b) a##b
 #define CY_CAT(a, b) CY_CAT2(a, b)
 
 #ifndef CY_SHADE_MIN_WAVES
-#  define CY_SHADE_MIN_WAVES 1
+#  define CY_SHADE_MIN_WAVES (CY_MAX_CLOSURE <= 2 ? 4 : 1)
 #endif
 __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_, CY_SHADE_VARIANT)(CyGlobals kg,
                                                      CyPathBuffers b,
@@ -27,15 +36,36 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_,
                                                      uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+#if CY_SHADE_LDS
+  /* closures (odd per-thread stride: conflict-free) and SVM stack columns in LDS */
+  __shared__ float lds[CY_BLOCK * (CY_CLOSURE_DWORDS + CY_SVM_LDS)];
+  float svm_spill[CY_SVM_STACK - CY_SVM_LDS];
+  CyShadeMem mem;
+  mem.closure = (CyClosure *)(lds + threadIdx.x * CY_CLOSURE_DWORDS);
+  mem.svm_stack = lds + CY_BLOCK * CY_CLOSURE_DWORDS + threadIdx.x;
+  mem.svm_stride = CY_BLOCK;
+  mem.svm_fast = CY_SVM_LDS;
+  mem.svm_spill = svm_spill;
+#else
+  CyClosure closure[CY_MAX_CLOSURE];
+  float svm[CY_SVM_STACK];
+  CyShadeMem mem;
+  mem.closure = closure;
+  mem.svm_stack = svm;
+  mem.svm_stride = 1;
+  mem.svm_fast = CY_SVM_STACK;
+  mem.svm_spill = nullptr;
+#endif
   bool cont = false, shadow = false, finished = false;
   int slot = 0;
   if (i < (int)*count_in) {
     slot = queue_in[i];
-    cont = shade_path(&kg, &b, &tile, slot, &shadow, &finished, err);
+    cont = shade_path(&kg, &b, &tile, slot, mem, &shadow, &finished, err);
   }
-  cont |= slot_refill(kg, b, tile, slot, finished);
-  queue_push(queue_out, count_out, slot, cont);
-  queue_push(shadow_queue, shadow_count, slot, shadow);
+  __shared__ uint claim[CY_CLAIM_LDS];
+  cont |= slot_refill(kg, b, tile, slot, finished, claim);
+  queue_push(queue_out, count_out, slot, cont, claim);
+  queue_push(shadow_queue, shadow_count, slot, shadow, claim);
 }
 
 void CY_CAT(cy_launch_shade_, CY_SHADE_VARIANT)(CY_SHADE_LAUNCHER_ARGS)

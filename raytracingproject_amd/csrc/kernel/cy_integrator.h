@@ -67,11 +67,70 @@ CY_FN hc_float4 mkf4(float x, float y, float z, float w)
   return r;
 }
 
+/* Path-slot records are touched once per iteration and the whole pool is far
+ * larger than the L2 and the 256 MB Infinity Cache: read and write them with
+ * non-temporal hints so they stream past the caches and leave the scene
+ * (BVH, triangles, shaders) resident for the random accesses. */
+#if defined(__HIPCC__)
+typedef float cy_v4f __attribute__((ext_vector_type(4)));
+typedef unsigned int cy_v4u __attribute__((ext_vector_type(4)));
+CY_FN hc_float4 cy_ld(const hc_float4 *p)
+{
+  const cy_v4f v = __builtin_nontemporal_load((const cy_v4f *)p);
+  return mkf4(v.x, v.y, v.z, v.w);
+}
+CY_FN hc_uint4 cy_ld(const hc_uint4 *p)
+{
+  const cy_v4u v = __builtin_nontemporal_load((const cy_v4u *)p);
+  hc_uint4 r;
+  r.x = v.x;
+  r.y = v.y;
+  r.z = v.z;
+  r.w = v.w;
+  return r;
+}
+CY_FN int cy_ld(const int *p)
+{
+  return __builtin_nontemporal_load(p);
+}
+CY_FN uint cy_ld(const uint *p)
+{
+  return __builtin_nontemporal_load(p);
+}
+CY_FN void cy_st(hc_float4 *p, hc_float4 v)
+{
+  cy_v4f x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, (cy_v4f *)p);
+}
+CY_FN void cy_st(hc_uint4 *p, hc_uint4 v)
+{
+  cy_v4u x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, (cy_v4u *)p);
+}
+CY_FN void cy_st(int *p, int v)
+{
+  __builtin_nontemporal_store(v, p);
+}
+CY_FN void cy_st(uint *p, uint v)
+{
+  __builtin_nontemporal_store(v, p);
+}
+#else
+template<typename T> static inline T cy_ld(const T *p)
+{
+  return *p;
+}
+template<typename T> static inline void cy_st(T *p, T v)
+{
+  *p = v;
+}
+#endif
+
 CY_FN void load_state(const CyPathBuffers *b, int slot, CyPathState *s, const CyGlobals *kg)
 {
-  hc_uint4 s0 = b->state0[slot];
-  hc_uint4 s1 = b->state1[slot];
-  hc_float4 s2 = b->state2[slot];
+  hc_uint4 s0 = cy_ld(&b->state0[slot]);
+  hc_uint4 s1 = cy_ld(&b->state1[slot]);
+  hc_float4 s2 = cy_ld(&b->state2[slot]);
   s->flag = (int)s0.x;
   s->rng_hash = s0.y;
   s->rng_offset = (int)s0.z;
@@ -98,9 +157,9 @@ CY_FN void store_state(const CyPathBuffers *b, int slot, const CyPathState *s)
   s1.y = (uint)s->diffuse_bounce;
   s1.z = (uint)s->glossy_bounce;
   s1.w = (uint)s->transmission_bounce;
-  b->state0[slot] = s0;
-  b->state1[slot] = s1;
-  b->state2[slot] = mkf4(int_as_float(s->transparent_bounce), s->min_ray_pdf, s->ray_pdf, s->ray_t);
+  cy_st(&b->state0[slot], s0);
+  cy_st(&b->state1[slot], s1);
+  cy_st(&b->state2[slot], mkf4(int_as_float(s->transparent_bounce), s->min_ray_pdf, s->ray_pdf, s->ray_t));
 }
 
 /* kernel_path_state.h:19-71 (no volumes, no denoising features). */
@@ -246,7 +305,7 @@ CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float
     L_sum = mk3(0.0f, 0.0f, 0.0f);
   }
   float alpha = 1.0f - L_transparent;
-  tile->samples_out[item] = mkf4(L_sum.x, L_sum.y, L_sum.z, alpha);
+  cy_st(&tile->samples_out[item], mkf4(L_sum.x, L_sum.y, L_sum.z, alpha));
 }
 
 /* Start work item `item` in the slot.  Returns false when the sample has no
@@ -263,24 +322,24 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
   CyRay ray;
   camera_sample_ray(kg, x, y, sample, &rng_hash, &ray);
   if (ray.t == 0.0f) {
-    tile->samples_out[item] = mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf(""));
+    cy_st(&tile->samples_out[item], mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf("")));
     return false;
   }
   CyPathState s;
   path_state_init(kg, &s, rng_hash, sample);
   store_state(b, slot, &s);
-  b->item[slot] = item;
-  b->ray_P[slot] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
-  b->ray_D[slot] = mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f);
-  b->throughput[slot] = mkf4(1.0f, 1.0f, 1.0f, 0.0f);
-  b->L[slot] = mkf4(0.0f, 0.0f, 0.0f, 0.0f);
+  cy_st(&b->item[slot], item);
+  cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
+  cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f));
+  cy_st(&b->throughput[slot], mkf4(1.0f, 1.0f, 1.0f, 0.0f));
+  cy_st(&b->L[slot], mkf4(0.0f, 0.0f, 0.0f, 0.0f));
   return true;
 }
 
 /* Finish the path in a slot: record its sample; the slot then needs new work. */
 CY_FN void slot_finish(const CyPathBuffers *b, const CyTile *tile, int slot, cfloat3 L_emission, float L_transparent)
 {
-  write_sample(tile, b->item[slot], L_emission, L_transparent);
+  write_sample(tile, cy_ld(&b->item[slot]), L_emission, L_transparent);
 }
 
 /* Add pixel p's sample records to the render buffer in sample order
@@ -295,7 +354,7 @@ CY_FN void accumulate_pixel(const CyTile *tile, int p)
   float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
   const int n = tile->end_sample - tile->start_sample;
   for (int k = 0; k < n; k++) {
-    const hc_float4 r = tile->samples_out[(size_t)k * npix + p];
+    const hc_float4 r = cy_ld(&tile->samples_out[(size_t)k * npix + p]);
     if (r.w == r.w) {
       b0 += r.x;
       b1 += r.y;
@@ -320,6 +379,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
                       const CyPathBuffers *b,
                       const CyTile *tile,
                       int slot,
+                      CyShadeMem mem,
                       bool *shadow,
                       bool *finished,
                       uint *err)
@@ -328,19 +388,19 @@ CY_FN bool shade_path(const CyGlobals *kg,
   *finished = false;
   CyPathState state;
   load_state(b, slot, &state, kg);
-  const hc_float4 rp = b->ray_P[slot];
-  const hc_float4 rd = b->ray_D[slot];
+  const hc_float4 rp = cy_ld(&b->ray_P[slot]);
+  const hc_float4 rd = cy_ld(&b->ray_D[slot]);
   CyRay ray;
   ray.P = mk3(rp.x, rp.y, rp.z);
   ray.t = rp.w;
   ray.D = mk3(rd.x, rd.y, rd.z);
-  const hc_float4 tp4 = b->throughput[slot];
+  const hc_float4 tp4 = cy_ld(&b->throughput[slot]);
   cfloat3 throughput = mk3(tp4.x, tp4.y, tp4.z);
   float L_transparent = tp4.w;
-  const hc_float4 L4 = b->L[slot];
+  const hc_float4 L4 = cy_ld(&b->L[slot]);
   cfloat3 L = mk3(L4.x, L4.y, L4.z);
 
-  const int type = b->isect_type[slot];
+  const int type = cy_ld(&b->isect_type[slot]);
   const bool hit = type != 0;
   bool cont = false;      /* path continues with a new ray */
   bool finish_now = true; /* write result in this stage */
@@ -389,7 +449,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
   else if (!path_state_ao_bounce(kg, &state)) {
     CyIsect isect;
-    const hc_float4 is4 = b->isect[slot];
+    const hc_float4 is4 = cy_ld(&b->isect[slot]);
     isect.t = is4.x;
     isect.u = is4.y;
     isect.v = is4.z;
@@ -398,6 +458,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
     isect.type = type;
 
     CySD sd;
+    sd.closure = mem.closure;
+    sd.svm_stack = mem.svm_stack;
+    sd.svm_stride = mem.svm_stride;
+    sd.svm_fast = mem.svm_fast;
+    sd.svm_spill = mem.svm_spill;
     shader_setup_from_ray(kg, &sd, &isect, &ray);
 #ifdef CY_EXP_FIXED_SVM /* profiling experiment only: one diffuse closure, no SVM */
     sd.num_closure = 1;
@@ -536,9 +601,9 @@ CY_FN bool shade_path(const CyGlobals *kg,
                 cfloat3 sD = sub3(ray_offset(ls.P, ls.Ng), sP);
                 float st;
                 sD = normalize_len3(sD, &st);
-                b->shadow_P[slot] = mkf4(sP.x, sP.y, sP.z, st);
-                b->shadow_D[slot] = mkf4(sD.x, sD.y, sD.z, 0.0f);
-                b->shadow_L[slot] = mkf4(contribution.x, contribution.y, contribution.z, 0.0f);
+                cy_st(&b->shadow_P[slot], mkf4(sP.x, sP.y, sP.z, st));
+                cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
+                cy_st(&b->shadow_L[slot], mkf4(contribution.x, contribution.y, contribution.z, 0.0f));
                 *shadow = (st != 0.0f);
                 if (!*shadow) {
                   L = add3(L, contribution);
@@ -586,20 +651,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
   if (cont) {
     finish_now = false;
     store_state(b, slot, &state);
-    b->ray_P[slot] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
-    b->ray_D[slot] = mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f);
-    b->throughput[slot] = mkf4(throughput.x, throughput.y, throughput.z, L_transparent);
-    b->L[slot] = mkf4(L.x, L.y, L.z, 0.0f);
+    cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
+    cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f));
+    cy_st(&b->throughput[slot], mkf4(throughput.x, throughput.y, throughput.z, L_transparent));
+    cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, 0.0f));
     return true;
   }
   if (*shadow) {
     /* the path ends after its pending light contribution: the shadow stage
      * adds it, writes the sample and regenerates the slot */
-    b->throughput[slot] = mkf4(throughput.x, throughput.y, throughput.z, L_transparent);
-    b->L[slot] = mkf4(L.x, L.y, L.z, 0.0f);
-    hc_float4 sl = b->shadow_L[slot];
+    cy_st(&b->throughput[slot], mkf4(throughput.x, throughput.y, throughput.z, L_transparent));
+    cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, 0.0f));
+    hc_float4 sl = cy_ld(&b->shadow_L[slot]);
     sl.w = 1.0f;
-    b->shadow_L[slot] = sl;
+    cy_st(&b->shadow_L[slot], sl);
     store_state(b, slot, &state);
     return false;
   }

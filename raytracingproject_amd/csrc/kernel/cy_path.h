@@ -981,27 +981,41 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
  * SVM interpreter subset (svm/svm.h:220-549, svm_closure.h, svm_value.h,
  * svm_fresnel.h).  Unknown nodes set CY_ERR_SVM_NODE and stop the shader.
  */
-CY_FN float svm_load(const float *stack, uint a, uint *err)
+/* SVM stack view: element i < fast at p[i * stride] (an LDS column on the
+ * device), deeper elements at spill[i - fast] */
+typedef struct CySvmStack {
+  float *p;
+  int stride;
+  int fast;
+  float *spill;
+} CySvmStack;
+
+CY_FN float svm_load(CySvmStack stack, uint a, uint *err)
 {
   if (a >= CY_SVM_STACK) {
     cy_set_error(err, CY_ERR_SVM_STACK, a);
     return 0.0f;
   }
-  return stack[a];
+  return ((int)a < stack.fast) ? stack.p[(int)a * stack.stride] : stack.spill[(int)a - stack.fast];
 }
-CY_FN void svm_store(float *stack, uint a, float f, uint *err)
+CY_FN void svm_store(CySvmStack stack, uint a, float f, uint *err)
 {
   if (a >= CY_SVM_STACK) {
     cy_set_error(err, CY_ERR_SVM_STACK, a);
     return;
   }
-  stack[a] = f;
+  if ((int)a < stack.fast) {
+    stack.p[(int)a * stack.stride] = f;
+  }
+  else {
+    stack.spill[(int)a - stack.fast] = f;
+  }
 }
-CY_FN cfloat3 svm_load3(const float *stack, uint a, uint *err)
+CY_FN cfloat3 svm_load3(CySvmStack stack, uint a, uint *err)
 {
   return mk3(svm_load(stack, a, err), svm_load(stack, a + 1, err), svm_load(stack, a + 2, err));
 }
-CY_FN void svm_store3(float *stack, uint a, cfloat3 f, uint *err)
+CY_FN void svm_store3(CySvmStack stack, uint a, cfloat3 f, uint *err)
 {
   svm_store(stack, a, f.x, err);
   svm_store(stack, a + 1, f.y, err);
@@ -1041,7 +1055,7 @@ CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, flo
 
 CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
                                  CySD *sd,
-                                 float *stack,
+                                 CySvmStack stack,
                                  hc_uint4 node,
                                  int path_flag,
                                  int *offset,
@@ -1183,7 +1197,11 @@ CY_FN void emission_setup(CySD *sd, cfloat3 weight)
 
 CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, int path_flag, uint *err)
 {
-  float stack[CY_SVM_STACK];
+  CySvmStack stack;
+  stack.p = sd->svm_stack;
+  stack.stride = sd->svm_stride;
+  stack.fast = sd->svm_fast;
+  stack.spill = sd->svm_spill;
   int offset = (int)((uint)sd->shader & SHADER_MASK);
   for (int guard = 0; guard < 4096; guard++) {
     hc_uint4 node = kg->__svm_nodes[offset];

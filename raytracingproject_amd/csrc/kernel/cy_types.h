@@ -258,8 +258,25 @@ typedef struct CySD {
   cfloat3 svm_closure_weight;
   cfloat3 closure_emission_background;
   cfloat3 closure_transparent_extinction;
-  CyClosure closure[CY_MAX_CLOSURE];
+  /* working memory of the shade stage (CyShadeMem): CY_MAX_CLOSURE closures
+   * and the SVM stack, element i at svm_stack[i * svm_stride] */
+  CyClosure *closure;
+  float *svm_stack;
+  int svm_stride;
+  int svm_fast;     /* entries [0, svm_fast) at svm_stack[i * svm_stride] */
+  float *svm_spill; /* entries [svm_fast, CY_SVM_STACK) at svm_spill[i - svm_fast] */
 } CySD;
+
+/* Where a shading thread keeps its closures and SVM stack.  The device kernel
+ * points them into LDS (per-thread strided columns) with the deep end of the
+ * stack in private memory; the host uses private arrays. */
+typedef struct CyShadeMem {
+  CyClosure *closure;
+  float *svm_stack;
+  int svm_stride;
+  int svm_fast;
+  float *svm_spill;
+} CyShadeMem;
 
 typedef struct CyPathState {
   int flag;

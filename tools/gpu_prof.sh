@@ -20,7 +20,7 @@ step() {
 }
 step list_counters 120 rocprofv3 -L
 step trace 900 rocprofv3 --kernel-trace --stats -d $OUT/trace_$TAG -o run --output-format csv -- python3 bench.py $ARGS
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_FLAT SQ_INST_LEVEL_VMEM"; do
   name=pmc_$(echo $pmc | cut -d' ' -f1)
   step $name 900 rocprofv3 --pmc $pmc --kernel-trace -d $OUT/${name}_$TAG -o run --output-format csv -- python3 bench.py $ARGS
 done

@@ -222,7 +222,15 @@ extern "C" int emu_render(const void *data,
       }
       /* k_shade */
       bool shadow = false, finished = false;
-      bool cont = shade_path(&kg, &b, &tile, 0, &shadow, &finished, &err);
+      CyClosure closure[CY_MAX_CLOSURE];
+      float svm[CY_SVM_STACK];
+      CyShadeMem mem;
+      mem.closure = closure;
+      mem.svm_stack = svm;
+      mem.svm_stride = 1;
+      mem.svm_fast = CY_SVM_STACK;
+      mem.svm_spill = nullptr;
+      bool cont = shade_path(&kg, &b, &tile, 0, mem, &shadow, &finished, &err);
       if (shadow) {
         /* k_intersect_shadow */
         CyRay sr;
