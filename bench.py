@@ -166,6 +166,8 @@ def main():
         "launches_per_frame": launches,
         "bvh_width": int(counts["bvh_width"]),
         "bvh_bytes": int(counts["bvh_bytes"]),
+        "nodes_per_ray": counts["closest_nodes"] / max(counts["closest_rays"], 1),
+        "tris_per_ray": counts["closest_tris"] / max(counts["closest_rays"], 1),
     }
 
     cpu = None

@@ -278,6 +278,7 @@ struct hipcy_device {
   size_t bvhw_bytes = 0;
   size_t bvhw_capacity = 0;
   int bvhw_depth = 0;
+  int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
 };
@@ -319,6 +320,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
   kg->bvhw_nodes = (dev->bvh_width > 2) ? dev->bvhw : nullptr;
+  kg->tri_index_identity = (dev->bvh_width > 2) ? dev->tri_index_identity : 0;
   return true;
 }
 
@@ -365,6 +367,18 @@ static int ensure_bvhw(hipcy_device *dev)
   HIP_CHECK(dev, hipMemcpy(dev->bvhw, col.out.data(), bytes, hipMemcpyHostToDevice));
   dev->bvhw_bytes = bytes;
   dev->bvhw_depth = col.max_depth;
+  /* triangle-only meshes without motion pack vertices in primitive order */
+  dev->tri_index_identity = 0;
+  auto ti = dev->globals.find("__prim_tri_index");
+  if (ti != dev->globals.end() && ti->second.bytes) {
+    std::vector<uint32_t> idx(ti->second.bytes / 4);
+    HIP_CHECK(dev, hipMemcpy(idx.data(), (const void *)ti->second.ptr, ti->second.bytes, hipMemcpyDeviceToHost));
+    bool ident = true;
+    for (size_t i = 0; i < idx.size() && ident; i++) {
+      ident = idx[i] == 3u * (uint32_t)i;
+    }
+    dev->tri_index_identity = ident ? 1 : 0;
+  }
   dev->bvhw_dirty = false;
   return 0;
 }
@@ -615,7 +629,8 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
   b.ptr = device_pointer;
   b.bytes = bytes;
   dev->globals[name] = b;
-  if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0) {
+  if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0 ||
+      strcmp(name, "__prim_tri_index") == 0) {
     dev->bvhw_dirty = true;
   }
   return 0;

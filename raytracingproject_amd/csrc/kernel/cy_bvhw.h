@@ -190,17 +190,26 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       continue;
     }
     else {
-      /* leaf: contiguous primitive range */
+      /* leaf: contiguous primitive range; the next triangle's vertices are
+       * requested before the current one is tested */
       n_leaves++;
       const int packed = ~code;
       int prim_addr = packed >> 4;
       const int prim_end = prim_addr + (packed & 15);
+      const bool ident = kg->tri_index_identity != 0;
+      uint vi = ident ? 3u * (uint)prim_addr : kg->__prim_tri_index[prim_addr];
+      hc_float4 v0 = kg->__prim_tri_verts[vi], v1 = kg->__prim_tri_verts[vi + 1], v2 = kg->__prim_tri_verts[vi + 2];
       for (; prim_addr < prim_end; prim_addr++) {
         n_tris++;
-        const uint tri_vindex = kg->__prim_tri_index[prim_addr];
-        const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+        hc_float4 w0 = v0, w1 = v1, w2 = v2;
+        if (prim_addr + 1 < prim_end) {
+          vi = ident ? 3u * (uint)(prim_addr + 1) : kg->__prim_tri_index[prim_addr + 1];
+          w0 = kg->__prim_tri_verts[vi];
+          w1 = kg->__prim_tri_verts[vi + 1];
+          w2 = kg->__prim_tri_verts[vi + 2];
+        }
         float tt, uu, vv;
-        if (ray_triangle_intersect(P, dir, isect->t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt)) {
+        if (ray_triangle_intersect(P, dir, isect->t, f4to3(v0), f4to3(v1), f4to3(v2), &uu, &vv, &tt)) {
           if (kg->__prim_visibility[prim_addr] & visibility) {
             isect->prim = prim_addr;
             isect->object = OBJECT_NONE;
@@ -218,6 +227,9 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
             }
           }
         }
+        v0 = w0;
+        v1 = w1;
+        v2 = w2;
       }
     }
   pop:

@@ -25,7 +25,7 @@ for args in "$@"; do
 import json,sys
 for l in sys.stdin:
     d=json.loads(l); r=d['roofline']
-    print('  value %.1f Msps  ms/step %.1f  closest %.1f shade %.1f shadow %.1f  frac %.4f  avg_launch %.3f ms  nodes-bytes %d' % (d['value'], d['ms_per_step'], d['kernel_ms_per_frame']['k_intersect_closest'], d['kernel_ms_per_frame']['k_shade'], d['kernel_ms_per_frame']['k_intersect_shadow'], r['frac'], r['avg_launch_ms'], r['bvh_bytes']))
+    print('  value %.1f Msps  ms/step %.1f  closest %.1f shade %.1f shadow %.1f  frac %.4f  avg_launch %.3f ms  nodes/ray %.1f tris/ray %.1f' % (d['value'], d['ms_per_step'], d['kernel_ms_per_frame']['k_intersect_closest'], d['kernel_ms_per_frame']['k_shade'], d['kernel_ms_per_frame']['k_intersect_shadow'], r['frac'], r['avg_launch_ms'], r.get('nodes_per_ray', 0), r.get('tris_per_ray', 0)))
 " || tail -n 5 gpurun_out/sweep_$i.log
   if fatal $rc; then exit $rc; fi
 done

@@ -68,6 +68,7 @@ static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char *
 #undef CY_BIND
   }
   kg->bvhw_nodes = bvhw;
+  kg->tri_index_identity = 0;
 }
 
 extern "C" void emu_set_width(int w)
