@@ -108,7 +108,7 @@ int hipcy_set_bvh_width(hipcy_device *dev, int width);
 /* Wide BVH only: BVH2 subtrees holding at most max_prims (0..15) primitives in
  * one contiguous range become a single leaf child (0 = keep BVH2 leaves). */
 int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims);
-/* Path slots kept in flight (default 2^23) and the byte budget of the
+/* Path slots kept in flight (default 2^27, ~28 GB) and the byte budget of the
  * per-sample record buffer of one pass (default 4 GiB; a tile whose samples do
  * not fit is rendered in several sample passes).  0 keeps a value. */
 int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);
@@ -119,7 +119,8 @@ int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *tile, int y_step);
 int hipcy_synchronize(hipcy_device *dev);
 int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
-/* flags: bit 0 = per-kernel HIP-event timings, bit 1 = traversal counters. */
+/* flags: bit 0 = per-kernel HIP-event timings (kernels then run on one stream,
+ * without overlap, so each launch is timed alone), bit 1 = traversal counters. */
 int hipcy_set_profiling(hipcy_device *dev, int flags);
 
 /* rays: n x 8 floats (P.xyz, D.xyz, t, visibility bits) in device memory;

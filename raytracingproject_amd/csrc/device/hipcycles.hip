@@ -49,13 +49,15 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
 __global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
                                                           CyPathBuffers b,
                                                           CyTile tile,
+                                                          int slot_base,
                                                           int n_slots,
                                                           int *queue,
                                                           uint *counter)
 {
-  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int slot = slot_base + i;
   __shared__ uint claim[CY_CLAIM_LDS];
-  const bool active = slot_refill(kg, b, tile, slot, slot < n_slots, claim);
+  const bool active = slot_refill(kg, b, tile, slot, i < n_slots, claim);
   queue_push(queue, counter, slot, active, claim);
 }
 
@@ -242,6 +244,8 @@ struct GlobalBinding {
 
 }  // namespace
 
+#define CY_LANES 4
+
 struct hipcy_device {
   int ordinal = 0;
   hipStream_t stream = nullptr;
@@ -257,14 +261,17 @@ struct hipcy_device {
   char *pool = nullptr;
   CyPathBuffers bufs;
   int *queue[3] = {nullptr, nullptr, nullptr};
-  uint *counters = nullptr; /* [0..2] queue counts, [3] error word */
+  uint *counters = nullptr; /* [3] error word; lane l: [16 + 16 l ...] (see PassLane) */
+  /* the slot pool is split into CY_LANES partitions iterated on their own
+   * streams, so one partition's kernel tail overlaps the others' work */
+  hipStream_t lane_stream[CY_LANES] = {};
   CyStats *stats_dev = nullptr;
   uint *host_counters = nullptr; /* pinned */
 
   int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
 
   /* path slots in flight and the per-sample record buffer of one pass */
-  size_t slots_wanted = (size_t)1 << 23;
+  size_t slots_wanted = (size_t)1 << 27;
   size_t record_budget = (size_t)4 << 30; /* bytes of sample records per pass */
   hc_float4 *records = nullptr;
   size_t records_capacity = 0;
@@ -483,14 +490,22 @@ hipcy_device *hipcy_create(int ordinal)
   }
   hipcy_device *dev = new hipcy_device();
   dev->ordinal = ordinal;
+  hipSetDevice(ordinal);
+  for (int l = 0; l < CY_LANES; l++) {
+    if (hipStreamCreateWithFlags(&dev->lane_stream[l], hipStreamNonBlocking) != hipSuccess) {
+      set_error(nullptr, "device context creation failed (streams)");
+      delete dev;
+      return nullptr;
+    }
+  }
   memset(&dev->data_host, 0, sizeof(dev->data_host));
   memset(&dev->stats, 0, sizeof(dev->stats));
   if (hipSetDevice(ordinal) != hipSuccess ||
       hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&dev->data_dev, sizeof(hc_KernelData)) != hipSuccess ||
-      hipMalloc((void **)&dev->counters, 64) != hipSuccess ||
+      hipMalloc((void **)&dev->counters, 16 * 4 * (CY_LANES + 1)) != hipSuccess ||
       hipMalloc((void **)&dev->stats_dev, 2 * sizeof(CyStats)) != hipSuccess ||
-      hipHostMalloc((void **)&dev->host_counters, 64, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void **)&dev->host_counters, 16 * 4 * (CY_LANES + 1), hipHostMallocDefault) != hipSuccess) {
     set_error(nullptr, "device context creation failed");
     delete dev;
     return nullptr;
@@ -522,6 +537,9 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->data_dev) hipFree(dev->data_dev);
   if (dev->host_counters) hipHostFree(dev->host_counters);
   if (dev->stream) hipStreamDestroy(dev->stream);
+  for (int l = 0; l < CY_LANES; l++) {
+    if (dev->lane_stream[l]) hipStreamDestroy(dev->lane_stream[l]);
+  }
   delete dev;
 }
 
@@ -780,83 +798,155 @@ struct EvQuad {
   hipEvent_t a, b, c, d;
 };
 
-/* One pass over samples [tile.start_sample, tile.end_sample) of the tile. */
-static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, int W, size_t *ev,
-                           std::vector<EvQuad> *quads)
+/* One partition of the slot pool with its own stream, queues and counters. */
+struct PassLane {
+  hipStream_t s;
+  int slot_base, n_slots;
+  uint *cnt;  /* device: [0..2] queue counts, [4] next item */
+  uint *hcnt; /* pinned host copy */
+  int *q[3];
+  int qa, qb;
+  uint n_active;
+  CyTile tile;
+  hipEvent_t done;
+};
+
+static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, int W, size_t *ev,
+                        std::vector<EvQuad> *quads)
 {
   const bool prof = (dev->profiling & 1) != 0;
   const bool counters = (dev->profiling & 2) != 0;
-  hipStream_t s = dev->stream;
+  hipStream_t s = ln.s;
   uint *err = dev->counters + 3;
+  const int qa = ln.qa, qb = ln.qb, qs = 2;
+  dev->stats.iterations++;
+  dev->stats.closest_rays += ln.n_active;
+  HIP_CHECK(dev, hipMemsetAsync(ln.cnt + qb, 0, 4, s));
+  HIP_CHECK(dev, hipMemsetAsync(ln.cnt + qs, 0, 4, s));
+  dim3 grid((ln.n_active + CY_BLOCK - 1) / CY_BLOCK), block(CY_BLOCK);
+  EvQuad p;
+  if (prof) {
+    p.a = get_event(dev, (*ev)++);
+    p.b = get_event(dev, (*ev)++);
+    p.c = get_event(dev, (*ev)++);
+    p.d = get_event(dev, (*ev)++);
+    HIP_CHECK(dev, hipEventRecord(p.a, s));
+  }
+  {
+    auto kfn = counters ? (W == 8 ? k_intersect_closest<true, 8> : W == 4 ? k_intersect_closest<true, 4>
+                                                                   : k_intersect_closest<true, 2>)
+                        : (W == 8 ? k_intersect_closest<false, 8> : W == 4 ? k_intersect_closest<false, 4>
+                                                                   : k_intersect_closest<false, 2>);
+    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.q[qa], ln.cnt + qa, err, dev->stats_dev);
+  }
+  if (prof) {
+    HIP_CHECK(dev, hipEventRecord(p.b, s));
+  }
+  cy_launch_shade(dev->data_host.integrator.max_closures, grid, block, s, kg, dev->bufs, ln.tile, ln.q[qa],
+                  ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
+  if (prof) {
+    HIP_CHECK(dev, hipEventRecord(p.c, s));
+  }
+  {
+    auto kfn = counters ? (W == 8 ? k_intersect_shadow<true, 8> : W == 4 ? k_intersect_shadow<true, 4>
+                                                                  : k_intersect_shadow<true, 2>)
+                        : (W == 8 ? k_intersect_shadow<false, 8> : W == 4 ? k_intersect_shadow<false, 4>
+                                                                  : k_intersect_shadow<false, 2>);
+    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
+                       ln.cnt + qb, err, dev->stats_dev);
+  }
+  if (prof) {
+    HIP_CHECK(dev, hipEventRecord(p.d, s));
+    quads->push_back(p);
+  }
+  HIP_CHECK(dev, hipGetLastError());
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, 16, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipEventRecord(ln.done, s));
+  return 0;
+}
+
+/* One pass over samples [tile.start_sample, tile.end_sample) of the tile: the
+ * items are split into CY_LANES contiguous ranges, each iterated by its own
+ * slot partition on its own stream; the host enqueues one iteration of every
+ * active lane, then waits for their queue counts. */
+static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, int W, size_t *ev,
+                           std::vector<EvQuad> *quads)
+{
   const size_t n_slots = std::min<size_t>(tile.n_items, dev->capacity);
-  tile.work_next = dev->counters + 4;
+  /* per-kernel event timing (profiling bit 0) needs kernels that do not
+   * overlap: one lane then */
+  const int max_lanes = (dev->profiling & 1) ? 1 : CY_LANES;
+  const int lanes = (int)std::max<size_t>(1, std::min<size_t>(max_lanes, n_slots / (4 * CY_BLOCK)));
   tile.samples_out = dev->records;
-  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 12, s));
-  HIP_CHECK(dev, hipMemsetAsync(dev->counters + 4, 0, 4, s));
-
-  int qa = 0, qb = 1;
-  const int qs = 2;
-  dim3 block(CY_BLOCK);
-  hipLaunchKernelGGL(k_init_slots, dim3((unsigned)((n_slots + CY_BLOCK - 1) / CY_BLOCK)), block, 0, s, kg,
-                     dev->bufs, tile, (int)n_slots, dev->queue[qa], dev->counters + qa);
-  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(dev, hipStreamSynchronize(s));
-  uint n_active = dev->host_counters[qa];
-
-  while (n_active > 0) {
-    dev->stats.iterations++;
-    dev->stats.closest_rays += n_active;
-    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qb, 0, 4, s));
-    HIP_CHECK(dev, hipMemsetAsync(dev->counters + qs, 0, 4, s));
-    dim3 grid((n_active + CY_BLOCK - 1) / CY_BLOCK);
-    EvQuad p;
-    if (prof) {
-      p.a = get_event(dev, (*ev)++);
-      p.b = get_event(dev, (*ev)++);
-      p.c = get_event(dev, (*ev)++);
-      p.d = get_event(dev, (*ev)++);
-      HIP_CHECK(dev, hipEventRecord(p.a, s));
+  PassLane ln[CY_LANES];
+  /* the main stream's pending work (buffer zeroing, uploads) precedes the lanes */
+  hipEvent_t start = get_event(dev, (*ev)++);
+  HIP_CHECK(dev, hipEventRecord(start, dev->stream));
+  for (int l = 0; l < lanes; l++) {
+    PassLane &L = ln[l];
+    L.s = dev->lane_stream[l];
+    HIP_CHECK(dev, hipStreamWaitEvent(L.s, start, 0));
+    L.slot_base = (int)(n_slots * l / lanes);
+    L.n_slots = (int)(n_slots * (l + 1) / lanes) - L.slot_base;
+    L.cnt = dev->counters + 16 * (l + 1);
+    L.hcnt = dev->host_counters + 16 * (l + 1);
+    for (int q = 0; q < 3; q++) {
+      L.q[q] = dev->queue[q] + L.slot_base;
     }
-    {
-      auto kfn = counters ? (W == 8 ? k_intersect_closest<true, 8> : W == 4 ? k_intersect_closest<true, 4>
-                                                                     : k_intersect_closest<true, 2>)
-                          : (W == 8 ? k_intersect_closest<false, 8> : W == 4 ? k_intersect_closest<false, 4>
-                                                                     : k_intersect_closest<false, 2>);
-      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, dev->queue[qa], dev->counters + qa, err,
-                         dev->stats_dev);
+    L.qa = 0;
+    L.qb = 1;
+    L.done = get_event(dev, (*ev)++);
+    L.tile = tile;
+    const uint begin = (uint)((uint64_t)tile.n_items * l / lanes);
+    L.tile.n_items = (uint)((uint64_t)tile.n_items * (l + 1) / lanes);
+    L.tile.work_next = L.cnt + 4;
+    L.hcnt[4] = begin;
+    HIP_CHECK(dev, hipMemsetAsync(L.cnt, 0, 12, L.s));
+    HIP_CHECK(dev, hipMemcpyAsync(L.cnt + 4, L.hcnt + 4, 4, hipMemcpyHostToDevice, L.s));
+    hipLaunchKernelGGL(k_init_slots, dim3((unsigned)((L.n_slots + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
+                       L.s, kg, dev->bufs, L.tile, L.slot_base, L.n_slots, L.q[L.qa], L.cnt + L.qa);
+    HIP_CHECK(dev, hipMemcpyAsync(L.hcnt, L.cnt, 16, hipMemcpyDeviceToHost, L.s));
+    HIP_CHECK(dev, hipEventRecord(L.done, L.s));
+  }
+  for (int l = 0; l < lanes; l++) {
+    HIP_CHECK(dev, hipEventSynchronize(ln[l].done));
+    ln[l].n_active = ln[l].hcnt[ln[l].qa];
+  }
+  while (true) {
+    bool any = false;
+    for (int l = 0; l < lanes; l++) {
+      if (ln[l].n_active > 0) {
+        any = true;
+        if (lane_iterate(dev, kg, ln[l], W, ev, quads) != 0) {
+          return -1;
+        }
+      }
     }
-    if (prof) {
-      HIP_CHECK(dev, hipEventRecord(p.b, s));
+    if (!any) {
+      break;
     }
-    cy_launch_shade(dev->data_host.integrator.max_closures, grid, block, s, kg, dev->bufs, tile, dev->queue[qa],
-                    dev->counters + qa, dev->queue[qb], dev->counters + qb, dev->queue[qs], dev->counters + qs, err);
-    if (prof) {
-      HIP_CHECK(dev, hipEventRecord(p.c, s));
+    for (int l = 0; l < lanes; l++) {
+      PassLane &L = ln[l];
+      if (L.n_active == 0) {
+        continue;
+      }
+      HIP_CHECK(dev, hipEventSynchronize(L.done));
+      dev->stats.shadow_rays += L.hcnt[2];
+      L.n_active = L.hcnt[L.qb];
+      std::swap(L.qa, L.qb);
     }
-    {
-      auto kfn = counters ? (W == 8 ? k_intersect_shadow<true, 8> : W == 4 ? k_intersect_shadow<true, 4>
-                                                                    : k_intersect_shadow<true, 2>)
-                          : (W == 8 ? k_intersect_shadow<false, 8> : W == 4 ? k_intersect_shadow<false, 4>
-                                                                    : k_intersect_shadow<false, 2>);
-      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, tile, dev->queue[qs], dev->counters + qs,
-                         dev->queue[qb], dev->counters + qb, err, dev->stats_dev);
-    }
-    if (prof) {
-      HIP_CHECK(dev, hipEventRecord(p.d, s));
-      quads->push_back(p);
-    }
-    HIP_CHECK(dev, hipGetLastError());
-    HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters, dev->counters, 16, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(dev, hipStreamSynchronize(s));
-    dev->stats.shadow_rays += dev->host_counters[qs];
-    n_active = dev->host_counters[qb];
+    HIP_CHECK(dev, hipMemcpy(dev->host_counters + 3, dev->counters + 3, 4, hipMemcpyDeviceToHost));
     if (dev->host_counters[3]) {
-      return 0;
+      break;
     }
-    std::swap(qa, qb);
+  }
+  /* all lanes finished: accumulate on the main stream after them */
+  for (int l = 0; l < lanes; l++) {
+    HIP_CHECK(dev, hipStreamWaitEvent(dev->stream, ln[l].done, 0));
   }
   const int npix = tile.w * tile.h;
-  hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npix + CY_BLOCK - 1) / CY_BLOCK)), block, 0, s, tile);
+  hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npix + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
+                     dev->stream, tile);
   HIP_CHECK(dev, hipGetLastError());
   return 0;
 }
@@ -897,7 +987,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
     dev->stats.bvh_bytes = W > 2 ? dev->bvhw_bytes : (it != dev->globals.end() ? it->second.bytes : 0);
   }
   hipStream_t s = dev->stream;
-  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, s));
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 16 * 4 * (CY_LANES + 1), s));
   HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, 2 * sizeof(CyStats), s));
   size_t ev = 0;
   hipEvent_t t_begin = get_event(dev, ev++);
