@@ -42,6 +42,8 @@ def parse():
                    help="4 (default) / 8: device-widened wide BVH; 2: the bound BVH2 as is")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
     p.add_argument("--slots", type=int, default=0, help="path slots in flight (0: device default)")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (RCCL, one GPU per rank); gloo rehearses N ranks on fewer GPUs")
     return p.parse_args()
 
 
@@ -53,13 +55,14 @@ def main():
     import torch
 
     dist = None
+    device_index = local_rank
+    if args.dist_backend == "gloo":
+        device_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(device_index)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", init_method="env://")
-    else:
-        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=args.dist_backend, init_method="env://")
 
     from raytracingproject_amd import scene as sc
     from raytracingproject_amd import scenes
@@ -76,7 +79,7 @@ def main():
     t0 = time.time()
     ds = sc.compile_scene(scene)
     t_compile = time.time() - t0
-    dev = HIPDevice(local_rank)
+    dev = HIPDevice(device_index)
     dev.set_bvh_width(args.bvh_width)
     dev.set_bvh_leaf_merge(args.leaf_merge)
     dev.set_slots(args.slots)
@@ -111,7 +114,7 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
