@@ -699,7 +699,7 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.integrator.use_volumes) why = "volumes";
   else if (d.integrator.transparent_shadows) why = "transparent shadows";
   else if (d.integrator.use_ambient_occlusion) why = "ambient occlusion";
-  else if (d.integrator.use_lamp_mis || d.integrator.num_all_lights) why = "lamps (use mesh lights)";
+  else if (d.background.map_weight > 0.0f) why = "background light (world importance sampling)";
   else if (d.integrator.max_closures > CY_MAX_CLOSURE) why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
   else if (d.bvh.have_motion || d.bvh.have_curves) why = "motion / curves";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";

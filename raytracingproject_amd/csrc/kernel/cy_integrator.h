@@ -402,6 +402,46 @@ CY_FN bool shade_path(const CyGlobals *kg,
 
   const int type = cy_ld(&b->isect_type[slot]);
   const bool hit = type != 0;
+
+  /* kernel_path_lamp_emission (kernel_path.h:86-113): lamps hit by the ray
+   * segment since the last non-transparent bounce, MIS-weighted
+   * (indirect_lamp_emission, kernel_emission.h:235-286) */
+  if (KD->integrator.use_lamp_mis && !(state.flag & PATH_RAY_CAMERA)) {
+    const float isect_t = hit ? cy_ld(&b->isect[slot]).x : ray.t;
+    const cfloat3 light_P = sub3(ray.P, mul3f(ray.D, state.ray_t));
+    state.ray_t += isect_t;
+    for (int lamp = 0; lamp < KD->integrator.num_all_lights; lamp++) {
+      CyLightSample ls;
+      if (!lamp_light_eval(kg, lamp, light_P, ray.D, state.ray_t, &ls)) {
+        continue;
+      }
+      const uint lsh = (uint)ls.shader;
+      if (lsh & SHADER_EXCLUDE_ANY) {
+        if (((lsh & SHADER_EXCLUDE_DIFFUSE) && (state.flag & PATH_RAY_DIFFUSE)) ||
+            ((lsh & SHADER_EXCLUDE_GLOSSY) &&
+             ((state.flag & (PATH_RAY_GLOSSY | PATH_RAY_REFLECT)) == (PATH_RAY_GLOSSY | PATH_RAY_REFLECT))) ||
+            ((lsh & SHADER_EXCLUDE_TRANSMIT) && (state.flag & PATH_RAY_TRANSMIT)) ||
+            ((lsh & SHADER_EXCLUDE_SCATTER) && (state.flag & PATH_RAY_VOLUME_SCATTER))) {
+          continue;
+        }
+      }
+      /* direct_emissive_eval (kernel_emission.h:20-99), constant lamp shader */
+      cfloat3 lamp_L = mk3(0.0f, 0.0f, 0.0f);
+      if (!shader_constant_emission_eval(kg, ls.shader, &lamp_L)) {
+        cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
+      }
+      lamp_L = mul3f(lamp_L, ls.eval_fac);
+      lamp_L = mul3(lamp_L, klight_vec(kg->__lights[lamp].strength));
+      if (!(state.flag & PATH_RAY_MIS_SKIP)) {
+        lamp_L = mul3f(lamp_L, power_heuristic(state.ray_pdf, ls.pdf));
+      }
+      /* path_radiance_accum_emission (kernel_accumulate.h:304-335) */
+      cfloat3 contribution = mul3(throughput, lamp_L);
+      contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
+      L = add3(L, contribution);
+    }
+  }
+
   bool cont = false;      /* path continues with a new ray */
   bool finish_now = true; /* write result in this stage */
 
@@ -552,7 +592,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
                               path_state_rng_1D(kg, &state, PRNG_LIGHT_TERMINATE) :
                               0.0f;
         CyLightSample ls;
-        if (light_sample(kg, light_u, light_v, sd.P, &ls, err) && ls.pdf != 0.0f) {
+        if (light_sample(kg, light_u, light_v, sd.P, state.bounce, &ls, err) && ls.pdf != 0.0f) {
           cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
           cfloat3 I = neg3(ls.D);
           if (shader_constant_emission_eval(kg, ls.shader, &light_eval)) {
@@ -564,6 +604,9 @@ CY_FN bool shade_path(const CyGlobals *kg,
             cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
           }
           light_eval = mul3f(light_eval, ls.eval_fac);
+          if (ls.lamp != LAMP_NONE) {
+            light_eval = mul3(light_eval, klight_vec(kg->__lights[ls.lamp].strength));
+          }
           if (!is_zero3(light_eval)) {
             /* shader_bsdf_eval (kernel_shader.h:606-636) */
             cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
@@ -598,9 +641,16 @@ CY_FN bool shade_path(const CyGlobals *kg,
               if ((uint)ls.shader & SHADER_CAST_SHADOW) {
                 bool transmit = (dot3(sd.Ng, ls.D) < 0.0f);
                 cfloat3 sP = ray_offset(sd.P, transmit ? neg3(sd.Ng) : sd.Ng);
-                cfloat3 sD = sub3(ray_offset(ls.P, ls.Ng), sP);
+                cfloat3 sD;
                 float st;
-                sD = normalize_len3(sD, &st);
+                if (ls.t == CY_FLT_MAX) {
+                  /* distant light */
+                  sD = ls.D;
+                  st = ls.t;
+                }
+                else {
+                  sD = normalize_len3(sub3(ray_offset(ls.P, ls.Ng), sP), &st);
+                }
                 cy_st(&b->shadow_P[slot], mkf4(sP.x, sP.y, sP.z, st));
                 cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
                 cy_st(&b->shadow_L[slot], mkf4(contribution.x, contribution.y, contribution.z, 0.0f));

@@ -136,6 +136,60 @@ CY_FN float xor_signmask(float x, int y)
 {
   return int_as_float(as_int(x) ^ y);
 }
+/* glibc 2.35 acosf (sysdeps/ieee754/flt-32/e_acosf.c, the fdlibm algorithm in
+ * float arithmetic), which the reference reaches through safe_acosf
+ * (util_math.h:601).  Bit-identical to the host libm for every float in
+ * [-1, 1] (checked exhaustively, tests/test_kernel_math.py samples it). */
+CY_FN float cy_acosf(float x)
+{
+  const float one = 1.0f, pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+  const float pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f,
+              pS3 = -4.0055535734e-02f, pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f;
+  const float qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f, qS3 = -6.8828397989e-01f,
+              qS4 = 7.7038154006e-02f;
+  const int hx = as_int(x);
+  const int ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) {
+    return (hx > 0) ? 0.0f : pi + 2.0f * pio2_lo;
+  }
+  if (ix > 0x3f800000) {
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3f000000) {
+    if (ix <= 0x32800000) {
+      return pio2_hi + pio2_lo;
+    }
+    const float z = x * x;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  }
+  if (hx < 0) {
+    const float z = (one + x) * 0.5f;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float s = sqrtf(z);
+    const float r = p / q;
+    const float w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  }
+  const float z = (one - x) * 0.5f;
+  const float s = sqrtf(z);
+  const float df = int_as_float(as_int(s) & (int)0xfffff000);
+  const float c = (z - df * df) / (s + df);
+  const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  const float r = p / q;
+  const float w = r * s + c;
+  return 2.0f * (df + w);
+}
+
+CY_FN float safe_acosf(float a)
+{
+  return cy_acosf(cclamp(a, -1.0f, 1.0f));
+}
+
 CY_FN float power_heuristic(float a, float b)
 {
   return (a * a) / (a * a + b * b);

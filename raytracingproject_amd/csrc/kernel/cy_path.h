@@ -1589,6 +1589,383 @@ CY_FN void triangle_light_sample(const CyGlobals *kg,
   }
 }
 
+/* ---------------------------------------------------------------------------
+ * Lamps: kernel_light.h:38-258 (lamp_light_sample / lamp_light_eval) with the
+ * helpers of kernel_light_common.h and util_math_intersect.h.  KernelLight's
+ * union (kernel_types.h:1489-1534) is read from hc_KernelLight.uni:
+ *   spot/point: radius, invarea, spot_angle, spot_smooth, dir[3]
+ *   area:       axisu[3], invarea, axisv[3], pad, dir[3]
+ *   distant:    radius, cosangle, invarea
+ */
+#define LIGHT_POINT 0
+#define LIGHT_DISTANT 1
+#define LIGHT_BACKGROUND 2
+#define LIGHT_AREA 3
+#define LIGHT_SPOT 4
+#define LIGHT_TRIANGLE 5
+
+/* kernel_montecarlo.h:39-46 */
+CY_FN void to_unit_disk(float *x, float *y)
+{
+  float phi = CY_2PI_F * (*x);
+  float r = sqrtf(*y);
+  *x = r * cy_cosf(phi);
+  *y = r * cy_sinf(phi);
+}
+
+/* kernel_light_common.h:106-130 */
+CY_FN cfloat3 ellipse_sample(cfloat3 ru, cfloat3 rv, float randu, float randv)
+{
+  to_unit_disk(&randu, &randv);
+  return add3(mul3f(ru, randu), mul3f(rv, randv));
+}
+CY_FN cfloat3 disk_light_sample(cfloat3 v, float randu, float randv)
+{
+  cfloat3 ru, rv;
+  make_orthonormals(v, &ru, &rv);
+  return ellipse_sample(ru, rv, randu, randv);
+}
+CY_FN cfloat3 distant_light_sample(cfloat3 D, float radius, float randu, float randv)
+{
+  return normalize3(add3(D, mul3f(disk_light_sample(D, randu, randv), radius)));
+}
+CY_FN cfloat3 sphere_light_sample(cfloat3 P, cfloat3 center, float radius, float randu, float randv)
+{
+  return mul3f(disk_light_sample(normalize3(sub3(P, center)), randu, randv), radius);
+}
+
+/* kernel_light_common.h:132-157; util_math.h:399-403 */
+CY_FN float spot_light_attenuation(cfloat3 dir, float spot_angle, float spot_smooth, cfloat3 N)
+{
+  float attenuation = dot3(dir, N);
+  if (attenuation <= spot_angle) {
+    attenuation = 0.0f;
+  }
+  else {
+    float t = attenuation - spot_angle;
+    if (t < spot_smooth && spot_smooth != 0.0f) {
+      const float f = t / spot_smooth;
+      const float ff = f * f;
+      attenuation *= (3.0f * ff - 2.0f * ff * f);
+    }
+  }
+  return attenuation;
+}
+CY_FN float lamp_light_pdf(cfloat3 Ng, cfloat3 I, float t)
+{
+  float cos_pi = dot3(Ng, I);
+  if (cos_pi <= 0.0f) {
+    return 0.0f;
+  }
+  return t * t / cos_pi;
+}
+
+/* kernel_light_common.h:30-104: solid-angle sampling of a rectangle */
+CY_FN float rect_light_sample(
+    cfloat3 P, cfloat3 *light_p, cfloat3 axisu, cfloat3 axisv, float randu, float randv, bool sample_coord)
+{
+  cfloat3 corner = sub3(sub3(*light_p, mul3f(axisu, 0.5f)), mul3f(axisv, 0.5f));
+  float axisu_len, axisv_len;
+  cfloat3 x = normalize_len3(axisu, &axisu_len);
+  cfloat3 y = normalize_len3(axisv, &axisv_len);
+  cfloat3 z = cross3(x, y);
+  cfloat3 dir = sub3(corner, P);
+  float z0 = dot3(dir, z);
+  if (z0 > 0.0f) {
+    z = mul3f(z, -1.0f);
+    z0 *= -1.0f;
+  }
+  float x0 = dot3(dir, x);
+  float y0 = dot3(dir, y);
+  float x1 = x0 + axisu_len;
+  float y1 = y0 + axisv_len;
+  /* float4 diff = (x0, y1, x1, y0) - (x1, y0, x0, y1); nz = (y0, x1, y1, x0) * diff */
+  const float d0 = x0 - x1, d1 = y1 - y0, d2 = x1 - x0, d3 = y0 - y1;
+  float n0 = y0 * d0, n1 = x1 * d1, n2 = y1 * d2, n3 = x0 * d3;
+  const float zz = z0 * z0;
+  /* nz / sqrt(z0 * z0 * diff * diff + nz * nz), component-wise */
+  n0 = n0 / sqrtf(zz * d0 * d0 + n0 * n0);
+  n1 = n1 / sqrtf(zz * d1 * d1 + n1 * n1);
+  n2 = n2 / sqrtf(zz * d2 * d2 + n2 * n2);
+  n3 = n3 / sqrtf(zz * d3 * d3 + n3 * n3);
+  float g0 = safe_acosf(-n0 * n1);
+  float g1 = safe_acosf(-n1 * n2);
+  float g2 = safe_acosf(-n2 * n3);
+  float g3 = safe_acosf(-n3 * n0);
+  float b0 = n0;
+  float b1 = n2;
+  float b0sq = b0 * b0;
+  float k = CY_2PI_F - g2 - g3;
+  float S = g0 + g1 - k;
+  if (sample_coord) {
+    float au = randu * S + k;
+    float fu = (cy_cosf(au) * b0 - b1) / cy_sinf(au);
+    float cu = 1.0f / sqrtf(fu * fu + b0sq) * (fu > 0.0f ? 1.0f : -1.0f);
+    cu = cclamp(cu, -1.0f, 1.0f);
+    float xu = -(cu * z0) / cmax(sqrtf(1.0f - cu * cu), 1e-7f);
+    xu = cclamp(xu, x0, x1);
+    float z0sq = z0 * z0;
+    float y0sq = y0 * y0;
+    float y1sq = y1 * y1;
+    float d = sqrtf(xu * xu + z0sq);
+    float h0 = y0 / sqrtf(d * d + y0sq);
+    float h1 = y1 / sqrtf(d * d + y1sq);
+    float hv = h0 + randv * (h1 - h0), hv2 = hv * hv;
+    float yv = (hv2 < 1.0f - 1e-6f) ? (hv * d) / sqrtf(1.0f - hv2) : y1;
+    *light_p = add3(add3(add3(P, mul3f(x, xu)), mul3f(y, yv)), mul3f(z, z0));
+  }
+  if (S != 0.0f) {
+    return 1.0f / S;
+  }
+  return 0.0f;
+}
+
+/* util_math_intersect.h:58-86 */
+CY_FN bool ray_aligned_disk_intersect(
+    cfloat3 ray_P, cfloat3 ray_D, float ray_t, cfloat3 disk_P, float disk_radius, cfloat3 *isect_P, float *isect_t)
+{
+  float disk_t;
+  const cfloat3 disk_N = normalize_len3(sub3(ray_P, disk_P), &disk_t);
+  const float div = dot3(ray_D, disk_N);
+  if (div == 0.0f) {
+    return false;
+  }
+  const float t = -disk_t / div;
+  if (t < 0.0f || t > ray_t) {
+    return false;
+  }
+  cfloat3 P = add3(ray_P, mul3f(ray_D, t));
+  if (len_squared3(sub3(P, disk_P)) > disk_radius * disk_radius) {
+    return false;
+  }
+  *isect_P = P;
+  *isect_t = t;
+  return true;
+}
+
+/* util_math_intersect.h:202-245 */
+CY_FN bool ray_quad_intersect(cfloat3 ray_P,
+                              cfloat3 ray_D,
+                              float ray_mint,
+                              float ray_maxt,
+                              cfloat3 quad_P,
+                              cfloat3 quad_u,
+                              cfloat3 quad_v,
+                              cfloat3 quad_n,
+                              cfloat3 *isect_P,
+                              float *isect_t,
+                              float *isect_u,
+                              float *isect_v,
+                              bool ellipse)
+{
+  float t = -(dot3(ray_P, quad_n) - dot3(quad_P, quad_n)) / dot3(ray_D, quad_n);
+  if (t < ray_mint || t > ray_maxt) {
+    return false;
+  }
+  const cfloat3 hit = add3(ray_P, mul3f(ray_D, t));
+  const cfloat3 inplane = sub3(hit, quad_P);
+  const float u = dot3(inplane, quad_u) / dot3(quad_u, quad_u);
+  if (u < -0.5f || u > 0.5f) {
+    return false;
+  }
+  const float v = dot3(inplane, quad_v) / dot3(quad_v, quad_v);
+  if (v < -0.5f || v > 0.5f) {
+    return false;
+  }
+  if (ellipse && (u * u + v * v > 0.25f)) {
+    return false;
+  }
+  *isect_P = hit;
+  *isect_t = t;
+  *isect_u = u + 0.5f;
+  *isect_v = v + 0.5f;
+  return true;
+}
+
+CY_FN cfloat3 klight_vec(const float *f)
+{
+  return mk3(f[0], f[1], f[2]);
+}
+
+/* kernel_light.h:38-158.  u/v (texture coordinates of the lamp) are only read
+ * by non-constant lamp shaders, which the device rejects; they are not set. */
+CY_FN bool lamp_light_sample(const CyGlobals *kg, int lamp, float randu, float randv, cfloat3 P, CyLightSample *ls,
+                             uint *err)
+{
+  const hc_KernelLight *klight = &kg->__lights[lamp];
+  const float *uni = klight->uni;
+  const int type = klight->type;
+  ls->type = type;
+  ls->shader = klight->shader_id;
+  ls->object = PRIM_NONE;
+  ls->prim = PRIM_NONE;
+  ls->lamp = lamp;
+  ls->u = randu;
+  ls->v = randv;
+
+  if (type == LIGHT_DISTANT) {
+    cfloat3 lightD = klight_vec(klight->co);
+    cfloat3 D = lightD;
+    float radius = uni[0];
+    float invarea = uni[2];
+    if (radius > 0.0f) {
+      D = distant_light_sample(D, radius, randu, randv);
+    }
+    ls->P = D;
+    ls->Ng = D;
+    ls->D = neg3(D);
+    ls->t = CY_FLT_MAX;
+    float costheta = dot3(lightD, D);
+    ls->pdf = invarea / (costheta * costheta * costheta);
+    ls->eval_fac = ls->pdf;
+  }
+  else if (type == LIGHT_BACKGROUND) {
+    cy_set_error(err, CY_ERR_FEATURE, 8); /* background light (rejected at load) */
+    return false;
+  }
+  else {
+    ls->P = klight_vec(klight->co);
+    if (type == LIGHT_POINT || type == LIGHT_SPOT) {
+      float radius = uni[0];
+      if (radius > 0.0f) {
+        ls->P = add3(ls->P, sphere_light_sample(P, ls->P, radius, randu, randv));
+      }
+      ls->D = normalize_len3(sub3(ls->P, P), &ls->t);
+      ls->Ng = neg3(ls->D);
+      float invarea = uni[1];
+      ls->eval_fac = (0.25f * CY_1_PI_F) * invarea;
+      ls->pdf = invarea;
+      if (type == LIGHT_SPOT) {
+        ls->eval_fac *= spot_light_attenuation(klight_vec(uni + 4), uni[2], uni[3], ls->Ng);
+        if (ls->eval_fac == 0.0f) {
+          return false;
+        }
+      }
+      ls->pdf *= lamp_light_pdf(ls->Ng, neg3(ls->D), ls->t);
+    }
+    else {
+      cfloat3 axisu = klight_vec(uni + 0);
+      cfloat3 axisv = klight_vec(uni + 4);
+      cfloat3 D = klight_vec(uni + 8);
+      float invarea = fabsf(uni[3]);
+      bool is_round = (uni[3] < 0.0f);
+      if (dot3(sub3(ls->P, P), D) > 0.0f) {
+        return false;
+      }
+      if (is_round) {
+        ls->P = add3(ls->P, ellipse_sample(mul3f(axisu, 0.5f), mul3f(axisv, 0.5f), randu, randv));
+        ls->pdf = invarea;
+      }
+      else {
+        ls->pdf = rect_light_sample(P, &ls->P, axisu, axisv, randu, randv, true);
+      }
+      ls->Ng = D;
+      ls->D = normalize_len3(sub3(ls->P, P), &ls->t);
+      ls->eval_fac = 0.25f * invarea;
+      if (is_round) {
+        ls->pdf *= lamp_light_pdf(D, neg3(ls->D), ls->t);
+      }
+    }
+  }
+  ls->pdf *= KD->integrator.pdf_lights;
+  return (ls->pdf > 0.0f);
+}
+
+/* kernel_light.h:160-258 */
+CY_FN bool lamp_light_eval(const CyGlobals *kg, int lamp, cfloat3 P, cfloat3 D, float t, CyLightSample *ls)
+{
+  const hc_KernelLight *klight = &kg->__lights[lamp];
+  const float *uni = klight->uni;
+  const int type = klight->type;
+  ls->type = type;
+  ls->shader = klight->shader_id;
+  ls->object = PRIM_NONE;
+  ls->prim = PRIM_NONE;
+  ls->lamp = lamp;
+  ls->u = 0.0f;
+  ls->v = 0.0f;
+  if (!((uint)ls->shader & SHADER_USE_MIS)) {
+    return false;
+  }
+  if (type == LIGHT_DISTANT) {
+    float radius = uni[0];
+    if (radius == 0.0f) {
+      return false;
+    }
+    if (t != CY_FLT_MAX) {
+      return false;
+    }
+    cfloat3 lightD = klight_vec(klight->co);
+    float costheta = dot3(neg3(lightD), D);
+    float cosangle = uni[1];
+    if (costheta < cosangle) {
+      return false;
+    }
+    ls->P = neg3(D);
+    ls->Ng = neg3(D);
+    ls->D = D;
+    ls->t = CY_FLT_MAX;
+    float invarea = uni[2];
+    ls->pdf = invarea / (costheta * costheta * costheta);
+    ls->eval_fac = ls->pdf;
+  }
+  else if (type == LIGHT_POINT || type == LIGHT_SPOT) {
+    cfloat3 lightP = klight_vec(klight->co);
+    float radius = uni[0];
+    if (radius == 0.0f) {
+      return false;
+    }
+    if (!ray_aligned_disk_intersect(P, D, t, lightP, radius, &ls->P, &ls->t)) {
+      return false;
+    }
+    ls->Ng = neg3(D);
+    ls->D = D;
+    float invarea = uni[1];
+    ls->eval_fac = (0.25f * CY_1_PI_F) * invarea;
+    ls->pdf = invarea;
+    if (type == LIGHT_SPOT) {
+      ls->eval_fac *= spot_light_attenuation(klight_vec(uni + 4), uni[2], uni[3], ls->Ng);
+      if (ls->eval_fac == 0.0f) {
+        return false;
+      }
+    }
+    if (ls->t != CY_FLT_MAX) {
+      ls->pdf *= lamp_light_pdf(ls->Ng, neg3(ls->D), ls->t);
+    }
+  }
+  else if (type == LIGHT_AREA) {
+    float invarea = fabsf(uni[3]);
+    bool is_round = (uni[3] < 0.0f);
+    if (invarea == 0.0f) {
+      return false;
+    }
+    cfloat3 axisu = klight_vec(uni + 0);
+    cfloat3 axisv = klight_vec(uni + 4);
+    cfloat3 Ng = klight_vec(uni + 8);
+    if (dot3(D, Ng) >= 0.0f) {
+      return false;
+    }
+    cfloat3 light_P = klight_vec(klight->co);
+    if (!ray_quad_intersect(P, D, 0.0f, t, light_P, axisu, axisv, Ng, &ls->P, &ls->t, &ls->u, &ls->v, is_round)) {
+      return false;
+    }
+    ls->D = D;
+    ls->Ng = Ng;
+    if (is_round) {
+      ls->pdf = invarea * lamp_light_pdf(Ng, neg3(D), ls->t);
+    }
+    else {
+      ls->pdf = rect_light_sample(P, &light_P, axisu, axisv, 0.0f, 0.0f, false);
+    }
+    ls->eval_fac = 0.25f * invarea;
+  }
+  else {
+    return false;
+  }
+  ls->pdf *= KD->integrator.pdf_lights;
+  return true;
+}
+
 CY_FN int light_distribution_sample(const CyGlobals *kg, float *randu)
 {
   int first = 0;
@@ -1612,8 +1989,9 @@ CY_FN int light_distribution_sample(const CyGlobals *kg, float *randu)
   return index;
 }
 
+/* kernel_light.h:628-661 */
 CY_FN bool light_sample(
-    const CyGlobals *kg, float randu, float randv, cfloat3 P, CyLightSample *ls, uint *err)
+    const CyGlobals *kg, float randu, float randv, cfloat3 P, int bounce, CyLightSample *ls, uint *err)
 {
   int index = light_distribution_sample(kg, &randu);
   const hc_KernelLightDistribution *kd = &kg->__light_distribution[index];
@@ -1623,8 +2001,12 @@ CY_FN bool light_sample(
     ls->shader |= kd->shader_flag;
     return (ls->pdf > 0.0f);
   }
-  cy_set_error(err, CY_ERR_FEATURE, 2); /* lamps: rejected at load */
-  return false;
+  const int lamp = -prim - 1;
+  /* light_select_reached_max_bounces: max_bounces is stored as a float */
+  if ((float)bounce > kg->__lights[lamp].max_bounces) {
+    return false;
+  }
+  return lamp_light_sample(kg, lamp, randu, randv, P, ls, err);
 }
 
 /* kernel_shader.h:978-992 */

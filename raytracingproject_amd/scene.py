@@ -29,6 +29,7 @@ PATH_RAY_NODE_UNALIGNED = 1 << 13
 SHADER_SMOOTH_NORMAL = 1 << 31
 SHADER_CAST_SHADOW = 1 << 30
 SHADER_AREA_LIGHT = 1 << 29
+SHADER_USE_MIS = 1 << 28
 SD_USE_MIS = 1 << 16
 SD_HAS_CONSTANT_EMISSION = 1 << 27
 SD_OBJECT_TRANSFORM_APPLIED = 1 << 2
@@ -201,6 +202,29 @@ class Mesh:
 
 
 @dataclass
+class Lamp:
+    """A Cycles Light (render/light.h): point, spot, area or sun (distant)."""
+
+    kind: str  # point | spot | area | sun
+    co: tuple = (0.0, 0.0, 0.0)
+    direction: tuple = (0.0, 0.0, -1.0)  # emission direction (spot, area normal, sun)
+    size: float = 0.0  # point/spot radius, area size multiplier
+    axisu: tuple = (1.0, 0.0, 0.0)  # area: unit axes, scaled by sizeu/sizev * size
+    axisv: tuple = (0.0, 1.0, 0.0)
+    sizeu: float = 1.0
+    sizev: float = 1.0
+    round: bool = False
+    angle: float = 0.0  # sun: angular diameter
+    spot_angle: float = math.radians(45.0)
+    spot_smooth: float = 0.0
+    color: tuple = (1.0, 1.0, 1.0)
+    strength: float = 10.0
+    use_mis: bool = True
+    cast_shadow: bool = True
+    max_bounces: int = 1024
+
+
+@dataclass
 class Camera:
     eye: tuple = (0.0, 0.0, -5.0)
     target: tuple = (0.0, 0.0, 0.0)
@@ -231,6 +255,7 @@ class Scene:
     seed: int = 0
     light_sampling_threshold: float = 0.05
     filter_glossy: float = 0.0
+    lamps: list = field(default_factory=list)
     caustics_reflective: bool = True
     caustics_refractive: bool = True
     name: str = "scene"
@@ -468,8 +493,14 @@ def compile_scene(scene: Scene) -> DeviceScene:
     tri_vnormal = np.zeros((verts.shape[0], 4), dtype=np.float32)
     tri_vnormal[:, :3] = vnormals
 
-    # --- shaders (render/shader.cpp:462-475, 508-581 + svm.cpp)
+    # --- shaders (render/shader.cpp:462-475, 508-581 + svm.cpp); lamps share
+    # one emission shader (the default light shader: emission 1.0), their
+    # color and power go to KernelLight.strength
     mats = list(scene.materials)
+    lamp_shader = None
+    if scene.lamps:
+        lamp_shader = len(mats)
+        mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
     world = Closure("background", tuple(scene.world_color), strength=scene.world_strength)
     svm = SVMCompiler().compile(mats, world)
     n_shaders = len(mats) + 1
@@ -512,20 +543,50 @@ def compile_scene(scene: Scene) -> DeviceScene:
         area = f32(0.5) * f32(np.sqrt(np.sum(np.cross(p2 - p1, p3 - p1).astype(np.float32) ** 2, dtype=np.float32)))
         totarea = f32(totarea + area)
     nd = len(light_tris)
-    dist[nd].totarea = float(totarea)
-    dist[nd].prim = 0
+    trianglearea = totarea
+    lamps = list(scene.lamps)
+    num_lights = len(lamps)
+    dist_all = (abi.KernelLightDistribution * (nd + num_lights + 1))()
+    for k in range(nd):
+        dist_all[k] = dist[k]
+    dist = dist_all
+    # lamps (light.cpp:404-433): equal share of the triangle area each
+    lightarea = f32(totarea / f32(num_lights)) if (totarea > 0 and num_lights) else f32(1.0)
+    use_lamp_mis = False
+    klights = (abi.KernelLight * max(num_lights, 1))()
+    for li, lamp in enumerate(lamps):
+        e = dist[nd + li]
+        e.totarea = float(totarea)
+        e.prim = ~li
+        e.shader_flag = f32bits_signed(1.0)  # lamp.pad
+        e.object_id = f32bits_signed(lamp.size)  # lamp.size
+        totarea = f32(totarea + lightarea)
+        use_lamp_mis |= _pack_lamp(klights[li], lamp, lamp_shader)
+    ntot = nd + num_lights
+    dist[ntot].totarea = float(totarea)
+    dist[ntot].prim = 0
     if totarea > 0:
-        for k in range(nd):
+        for k in range(ntot):
             dist[k].totarea = float(f32(dist[k].totarea) / totarea)
-        dist[nd].totarea = 1.0
+        dist[ntot].totarea = 1.0
     ki = kd.integrator
     ki.use_direct_light = int(totarea > 0)
     if ki.use_direct_light:
-        ki.num_distribution = nd
-        ki.num_all_lights = 0
-        ki.pdf_triangles = float(f32(1.0) / totarea)
+        ki.num_distribution = ntot
+        ki.num_all_lights = num_lights
+        ki.pdf_triangles = 0.0
         ki.pdf_lights = 0.0
-    ki.use_lamp_mis = 0
+        if trianglearea > 0:
+            ki.pdf_triangles = float(f32(1.0) / trianglearea)
+            if num_lights:
+                ki.pdf_triangles = float(f32(ki.pdf_triangles) * f32(0.5))
+        if num_lights:
+            ki.pdf_lights = float(f32(1.0) / f32(num_lights))
+            if trianglearea > 0:
+                ki.pdf_lights = float(f32(ki.pdf_lights) * f32(0.5))
+        ki.use_lamp_mis = int(use_lamp_mis)
+    else:
+        ki.use_lamp_mis = 0
 
     # --- integrator (render/integrator.cpp:103-245)
     ki.min_bounce = scene.min_bounce + 1
@@ -618,7 +679,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "__tri_vnormal": tri_vnormal,
         "__tri_vindex": tri_vindex,
         "__light_distribution": np.frombuffer(abi.array_bytes(dist), dtype=np.uint8).copy(),
-        "__lights": np.zeros(192, dtype=np.uint8),
+        "__lights": np.frombuffer(abi.array_bytes(klights), dtype=np.uint8).copy(),
         "__svm_nodes": svm,
         "__shaders": np.frombuffer(abi.array_bytes(kshaders), dtype=np.uint8).copy(),
         "__lookup_table": lookup,
@@ -629,10 +690,99 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "bvh_inner_nodes": nodes.shape[0] // 4,
         "bvh_leaves": leaves.shape[0],
         "light_triangles": nd,
+        "lamps": num_lights,
         "shaders": n_shaders,
         "name": scene.name,
     }
     return DeviceScene(kd, arrays, scene.width, scene.height, scene.samples, info)
+
+
+def f32bits_signed(x: float) -> int:
+    return int(np.array([x], dtype=np.float32).view(np.int32)[0])
+
+
+def _f3(v) -> np.ndarray:
+    return np.asarray(v, dtype=np.float32)
+
+
+def _safe_normalize(v: np.ndarray) -> np.ndarray:
+    t = np.float32(np.sqrt(np.float32(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])))
+    return (v * (np.float32(1.0) / t)).astype(np.float32) if t != 0 else v
+
+
+LIGHT_TYPES = {"point": 0, "sun": 1, "area": 3, "spot": 4}
+
+
+def _pack_lamp(kl, lamp: Lamp, shader_index: int) -> bool:
+    """LightManager::device_update_points (render/light.cpp:722-907); returns
+    whether the lamp turns on lamp MIS (light.cpp:419-427)."""
+    f32 = np.float32
+    shader_id = shader_index | SHADER_CAST_SHADOW | SHADER_AREA_LIGHT
+    if not lamp.cast_shadow:
+        shader_id &= ~SHADER_CAST_SHADOW
+    kl.type = LIGHT_TYPES[lamp.kind]
+    kl.samples = 1
+    strength = _f3(lamp.color) * f32(lamp.strength)
+    kl.strength[:] = [float(c) for c in strength]
+    uni = [0.0] * 12
+    co = _f3(lamp.co)
+    mis = False
+    if lamp.kind in ("point", "spot"):
+        shader_id &= ~SHADER_AREA_LIGHT
+        radius = f32(lamp.size)
+        invarea = f32(1.0) / (f32(math.pi) * radius * radius) if radius > 0 else f32(1.0)
+        if lamp.use_mis and radius > 0:
+            shader_id |= SHADER_USE_MIS
+            mis = True
+        kl.co[:] = [float(c) for c in co]
+        uni[0], uni[1] = float(radius), float(invarea)
+        if lamp.kind == "spot":
+            spot_angle = f32(math.cos(f32(lamp.spot_angle) * f32(0.5)))
+            spot_smooth = (f32(1.0) - spot_angle) * f32(lamp.spot_smooth)
+            d = _safe_normalize(_f3(lamp.direction))
+            uni[2], uni[3] = float(spot_angle), float(spot_smooth)
+            uni[4:7] = [float(c) for c in d]
+    elif lamp.kind == "sun":
+        shader_id &= ~SHADER_AREA_LIGHT
+        angle = f32(lamp.angle) / f32(2.0)
+        radius = f32(math.tan(angle))
+        cosangle = f32(math.cos(angle))
+        area = f32(math.pi) * radius * radius
+        invarea = f32(1.0) / area if area > 0 else f32(1.0)
+        d = _safe_normalize(_f3(lamp.direction))
+        if lamp.use_mis and area > 0:
+            shader_id |= SHADER_USE_MIS
+            mis = True
+        kl.co[:] = [float(c) for c in d]
+        uni[0], uni[1], uni[2] = float(radius), float(cosangle), float(invarea)
+    elif lamp.kind == "area":
+        axisu = (_f3(lamp.axisu) * (f32(lamp.sizeu) * f32(lamp.size))).astype(f32)
+        axisv = (_f3(lamp.axisv) * (f32(lamp.sizev) * f32(lamp.size))).astype(f32)
+        lu = f32(np.sqrt(np.float32(np.dot(axisu, axisu))))
+        lv = f32(np.sqrt(np.float32(np.dot(axisv, axisv))))
+        area = lu * lv
+        if lamp.round:
+            area = area * f32(-math.pi / 4)
+        invarea = f32(1.0) / area if area != 0 else f32(1.0)
+        d = _safe_normalize(_f3(lamp.direction))
+        if lamp.use_mis and area != 0:
+            shader_id |= SHADER_USE_MIS
+        mis = lamp.use_mis
+        kl.co[:] = [float(c) for c in co]
+        uni[0:3] = [float(c) for c in axisu]
+        uni[3] = float(invarea)
+        uni[4:7] = [float(c) for c in axisv]
+        uni[8:11] = [float(c) for c in d]
+    else:
+        raise ValueError(f"unsupported lamp kind {lamp.kind}")
+    kl.uni[:] = uni
+    kl.shader_id = int(np.array([shader_id], dtype=np.uint32).view(np.int32)[0])
+    kl.max_bounces = float(lamp.max_bounces)
+    kl.random = 0.0
+    ident = np.eye(4)[:3]
+    abi.set_transform(kl.tfm, ident)
+    abi.set_transform(kl.itfm, ident)
+    return mis
 
 
 def _vertex_normals(v: np.ndarray, t: np.ndarray) -> np.ndarray:

@@ -124,6 +124,29 @@ def cornell_box(width=256, height=256, samples=32) -> sc.Scene:
                     world_strength=0.0, samples=samples, name="cornell_box")
 
 
+def cornell_lamps(width=64, height=64, samples=16) -> sc.Scene:
+    """Cornell box lit by every lamp kind the device implements: a sphere point
+    lamp, a spot lamp, a rectangular and a round area lamp, a sun, plus the
+    emissive ceiling quad (mesh light and lamps share the light distribution)."""
+    scene = cornell_box(width, height, samples)
+    L = 555.0
+    scene.lamps = [
+        sc.Lamp("point", co=(140.0, 420.0, 200.0), size=25.0, color=(1.0, 0.6, 0.3), strength=4.0e6),
+        sc.Lamp("spot", co=(420.0, 500.0, 120.0), direction=(-0.3, -1.0, 0.4), size=10.0,
+                spot_angle=math.radians(50.0), spot_smooth=0.3, color=(0.4, 0.7, 1.0), strength=6.0e6),
+        sc.Lamp("area", co=(278.0, L - 2.0, 470.0), direction=(0.0, -1.0, 0.0), axisu=(1.0, 0.0, 0.0),
+                axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=160.0, sizev=60.0, color=(1.0, 1.0, 1.0),
+                strength=3.0e5),
+        sc.Lamp("area", co=(30.0, 300.0, 300.0), direction=(1.0, 0.0, 0.0), axisu=(0.0, 1.0, 0.0),
+                axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=80.0, sizev=80.0, round=True, color=(0.9, 1.0, 0.8),
+                strength=2.0e5),
+        sc.Lamp("sun", direction=(0.2, -1.0, 0.6), angle=math.radians(5.0), color=(1.0, 0.95, 0.9),
+                strength=2.0),
+    ]
+    scene.name = "cornell_lamps"
+    return scene
+
+
 def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
     """BMW27-class stand-in (SURVEY.md §8(d) config BMW): ~0.7M triangles at
     detail=1.0, glossy / glass / diffuse materials, two emissive studio panels,
@@ -191,6 +214,7 @@ def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
 
 
 CONFIGS = {
+    "cornell_lamps": cornell_lamps,
     "cornell_box": cornell_box,
     "bmw27_standin": bmw27_standin,
 }

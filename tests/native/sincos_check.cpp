@@ -13,3 +13,11 @@ extern "C" void sincos_eval(const float *x, long n, float *s_dev, float *c_dev, 
     c_libm[i] = cosf(x[i]);
   }
 }
+
+extern "C" void acos_eval(const float *x, long n, float *dev, float *libm)
+{
+  for (long i = 0; i < n; i++) {
+    dev[i] = cy_acosf(x[i]);
+    libm[i] = acosf(x[i]);
+  }
+}

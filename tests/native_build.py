@@ -119,4 +119,5 @@ def sincos():
     lib = ctypes.CDLL(build("tests/native/sincos_check.cpp", "libsincos_check.so"))
     vp = ctypes.c_void_p
     lib.sincos_eval.argtypes = [vp, ctypes.c_long, vp, vp, vp, vp]
+    lib.acos_eval.argtypes = [vp, ctypes.c_long, vp, vp]
     return lib

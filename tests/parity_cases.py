@@ -18,6 +18,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = {
     "cornell_64": lambda: scenes.cornell_box(64, 64, 16),
     "bmw_small": lambda: scenes.bmw27_standin(96, 54, 8, detail=0.25),
+    "cornell_lamps": lambda: scenes.cornell_lamps(64, 64, 16),
 }
 
 PATH_RAY_ALL_VISIBILITY = (1 << 14) - 1

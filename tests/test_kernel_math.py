@@ -42,3 +42,20 @@ def test_sincos_special_values(v):
     s, c, s_ref, c_ref = _eval(np.array([v], dtype=np.float32))
     assert s.view(np.uint32)[0] == s_ref.view(np.uint32)[0]
     assert c.view(np.uint32)[0] == c_ref.view(np.uint32)[0]
+
+
+def test_acosf_bit_exact_vs_libm():
+    """cy_acosf restates glibc's acosf (fdlibm e_acosf.c); the reference reaches
+    it through safe_acosf in rect_light_sample (kernel_light_common.h:64-67).
+    Exhaustive agreement over [-1, 1] was checked during development; here a
+    strided sweep of the float range plus random values."""
+    lib = nb.sincos()
+    one = np.float32(1.0).view(np.uint32)
+    x = np.arange(0, one + 1, 251, dtype=np.uint32).view(np.float32)
+    rng = np.random.default_rng(4)
+    x = np.concatenate([x, -x, rng.uniform(-1, 1, 1 << 18).astype(np.float32),
+                        np.array([1.0, -1.0, 0.5, -0.5, 0.49999997, -0.49999997, 1e-30], dtype=np.float32)])
+    x = np.ascontiguousarray(x)
+    dev, ref = np.zeros_like(x), np.zeros_like(x)
+    lib.acos_eval(x.ctypes.data, len(x), dev.ctypes.data, ref.ctypes.data)
+    assert np.array_equal(dev.view(np.uint32), ref.view(np.uint32))
