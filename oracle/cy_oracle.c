@@ -205,3 +205,94 @@ void cyo_intersect_brute(const float *prim_tri_verts, const uint32_t *prim_visib
     out_i[4 * r + 3] = best >= 0 ? 1 : 0;
   }
 }
+
+/* transform_point / transform_direction (util_transform.h, scalar branch) */
+static void xform(const float *m, const float *a, int point, float *r)
+{
+  for (int k = 0; k < 3; k++) {
+    const float *row = m + 4 * k;
+    r[k] = a[0] * row[0] + a[1] * row[1] + a[2] * row[2];
+    if (point) {
+      r[k] = r[k] + row[3];
+    }
+  }
+}
+
+static void clamp_dir(const float *d, float *r)
+{
+  const float ooeps = 8.271806E-25f;
+  for (int k = 0; k < 3; k++) {
+    r[k] = (fabsf(d[k]) > ooeps) ? d[k] : copysignf(ooeps, d[k]);
+  }
+}
+
+void cyo_intersect_brute_instanced(const float *prim_tri_verts, const uint32_t *prim_tri_index,
+                                   const uint32_t *prim_type, const uint32_t *prim_object,
+                                   const uint32_t *prim_visibility, int n_top, const float *obj_itfm,
+                                   const int32_t *obj_first, const int32_t *obj_count, const float *rays,
+                                   int n, int any_hit, float *out_f, int32_t *out_i)
+{
+  for (int r = 0; r < n; r++) {
+    const float *ray = rays + 8 * r;
+    const float P[3] = {ray[0], ray[1], ray[2]};
+    float D[3];
+    clamp_dir(ray + 3, D);
+    const uint32_t vis = f2u(ray[7]) & (any_hit ? ((1u << 7) | (1u << 8)) : 0xFFFFFFFFu);
+    float best_t = ray[6], bu = 0.0f, bv = 0.0f;
+    int best = -1, best_obj = -1, done = 0;
+    for (int p = 0; p < n_top && !done; p++) {
+      float u, v, t;
+      if (prim_type[p] == 1u) {
+        const float *tv = prim_tri_verts + 4 * (size_t)prim_tri_index[p];
+        if (cyo_ray_triangle_intersect(P, D, best_t, tv, tv + 4, tv + 8, &u, &v, &t) &&
+            (prim_visibility[p] & vis)) {
+          best = p;
+          best_obj = -1;
+          best_t = t;
+          bu = u;
+          bv = v;
+          done = any_hit;
+        }
+        continue;
+      }
+      /* instance: bvh_instance_push / pop (geom/geom_object.h:425-470) */
+      const int ob = (int)prim_object[p];
+      const float *itfm = obj_itfm + 12 * (size_t)ob;
+      float Po[3], Dt[3], Do[3];
+      xform(itfm, P, 1, Po);
+      xform(itfm, ray + 3, 0, Dt);
+      const float len = sqrtf(dot(Dt, Dt));
+      const float inv = 1.0f / len;
+      const float Dn[3] = {Dt[0] * inv, Dt[1] * inv, Dt[2] * inv};
+      clamp_dir(Dn, Do);
+      float t_obj = (best_t != 3.402823466e+38f) ? best_t * len : best_t;
+      for (int q = obj_first[ob]; q < obj_first[ob] + obj_count[ob]; q++) {
+        const float *tv = prim_tri_verts + 4 * (size_t)prim_tri_index[q];
+        if (cyo_ray_triangle_intersect(Po, Do, t_obj, tv, tv + 4, tv + 8, &u, &v, &t) &&
+            (prim_visibility[q] & vis)) {
+          best = q;
+          best_obj = ob;
+          t_obj = t;
+          bu = u;
+          bv = v;
+          if (any_hit) {
+            done = 1;
+            break;
+          }
+        }
+      }
+      if (t_obj != 3.402823466e+38f) {
+        xform(itfm, ray + 3, 0, Dt);
+        t_obj /= sqrtf(dot(Dt, Dt));
+      }
+      best_t = t_obj;
+    }
+    out_f[3 * r + 0] = best_t;
+    out_f[3 * r + 1] = bu;
+    out_f[3 * r + 2] = bv;
+    out_i[4 * r + 0] = best >= 0;
+    out_i[4 * r + 1] = best;
+    out_i[4 * r + 2] = best_obj;
+    out_i[4 * r + 3] = best >= 0 ? 1 : 0;
+  }
+}

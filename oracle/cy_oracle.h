@@ -23,5 +23,15 @@ int cyo_ray_triangle_intersect(const float P[3], const float D[3], float ray_t,
  * rays: n x 8 floats (P, D, t, visibility bits); out_f n x 3, out_i n x 4. */
 void cyo_intersect_brute(const float *prim_tri_verts, const uint32_t *prim_visibility, int n_prims,
                          const float *rays, int n, int any_hit, float *out_f, int32_t *out_i);
+/* Same with instancing: top-level slots [0, n_top) hold world-space triangles
+ * (prim_type 1) and object instances (prim_type 0, object prim_object[slot]);
+ * an instance's triangles are slots [obj_first, +obj_count) in object space,
+ * tested with the reference's push/pop of the ray and t (obj_itfm: 12 floats
+ * per object).  out_i[2] is the instance object or -1. */
+void cyo_intersect_brute_instanced(const float *prim_tri_verts, const uint32_t *prim_tri_index,
+                                   const uint32_t *prim_type, const uint32_t *prim_object,
+                                   const uint32_t *prim_visibility, int n_top, const float *obj_itfm,
+                                   const int32_t *obj_first, const int32_t *obj_count, const float *rays,
+                                   int n, int any_hit, float *out_f, int32_t *out_i);
 
 #endif

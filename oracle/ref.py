@@ -69,6 +69,7 @@ def oracle_lib():
         lib.cyo_path_rng_1d.argtypes = [vp, u32, ci, ci]
         lib.cyo_ray_offset.argtypes = [vp, vp, vp]
         lib.cyo_intersect_brute.argtypes = [vp, vp, ci, vp, ci, ci, vp, vp]
+        lib.cyo_intersect_brute_instanced.argtypes = [vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, ci, ci, vp, vp]
         _orc = lib
     return _orc
 

@@ -101,6 +101,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     if (hit) {
       cy_st(&b.isect[slot], mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim)));
       cy_st(&b.isect_type[slot], isect.type);
+      cy_st(&b.isect_object[slot], isect.object);
     }
     else {
       cy_st(&b.isect_type[slot], 0);
@@ -285,6 +286,7 @@ struct hipcy_device {
   size_t bvhw_bytes = 0;
   size_t bvhw_capacity = 0;
   int bvhw_depth = 0;
+  int *bvhw_object_root = nullptr; /* inside bvhw, after the nodes */
   int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
@@ -327,6 +329,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
   kg->bvhw_nodes = (dev->bvh_width > 2) ? dev->bvhw : nullptr;
+  kg->bvhw_object_root = (dev->bvh_width > 2) ? dev->bvhw_object_root : nullptr;
   kg->tri_index_identity = (dev->bvh_width > 2) ? dev->tri_index_identity : 0;
   return true;
 }
@@ -359,10 +362,29 @@ static int ensure_bvhw(hipcy_device *dev)
   col.n_nodes2 = n2.size() / 4;
   col.leaves2 = l2.data();
   col.n_leaves2 = l2.size() / 4;
+  /* instance leaves: object of the leaf's primitive slot, and each object's BVH2 root */
+  std::vector<uint32_t> pobj, onode;
+  auto fetch_u32 = [&](const char *name, std::vector<uint32_t> *v) -> int {
+    auto it = dev->globals.find(name);
+    if (it != dev->globals.end() && it->second.bytes) {
+      v->resize(it->second.bytes / 4);
+      HIP_CHECK(dev, hipMemcpy(v->data(), (const void *)it->second.ptr, it->second.bytes, hipMemcpyDeviceToHost));
+    }
+    return 0;
+  };
+  if (fetch_u32("__prim_object", &pobj) || fetch_u32("__object_node", &onode)) {
+    return -1;
+  }
+  col.prim_object = pobj.data();
+  col.n_prims = pobj.size();
+  col.object_node = onode.data();
+  col.n_objects = onode.size();
   if (!col.run(dev->data_host.bvh.root)) {
     return set_error(dev, "BVH widening: " + col.error);
   }
-  const size_t bytes = col.out.size() * 4;
+  /* wide nodes, then one int per object: the wide root of its own BVH */
+  const size_t node_bytes = col.out.size() * 4;
+  const size_t bytes = node_bytes + col.object_root.size() * 4;
   if (bytes > dev->bvhw_capacity) {
     if (dev->bvhw) {
       HIP_CHECK(dev, hipFree(dev->bvhw));
@@ -371,8 +393,13 @@ static int ensure_bvhw(hipcy_device *dev)
     HIP_CHECK(dev, hipMalloc(&dev->bvhw, bytes));
     dev->bvhw_capacity = bytes;
   }
-  HIP_CHECK(dev, hipMemcpy(dev->bvhw, col.out.data(), bytes, hipMemcpyHostToDevice));
-  dev->bvhw_bytes = bytes;
+  HIP_CHECK(dev, hipMemcpy(dev->bvhw, col.out.data(), node_bytes, hipMemcpyHostToDevice));
+  if (!col.object_root.empty()) {
+    HIP_CHECK(dev, hipMemcpy((char *)dev->bvhw + node_bytes, col.object_root.data(), col.object_root.size() * 4,
+                             hipMemcpyHostToDevice));
+  }
+  dev->bvhw_bytes = node_bytes;
+  dev->bvhw_object_root = col.object_root.empty() ? nullptr : (int *)((char *)dev->bvhw + node_bytes);
   dev->bvhw_depth = col.max_depth;
   /* triangle-only meshes without motion pack vertices in primitive order */
   dev->tri_index_identity = 0;
@@ -399,10 +426,10 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     hipFree(dev->pool);
     dev->pool = nullptr;
   }
-  /* 12 float4 records + 2 ints per slot (queues are separate) */
+  /* 12 float4 records + 3 ints per slot (queues are separate) */
   const size_t rec = 16 * slots;
   const size_t ints = 4 * slots;
-  const size_t total = 12 * rec + 2 * ints + 14 * 256;
+  const size_t total = 12 * rec + 3 * ints + 15 * 256;
   HIP_CHECK(dev, hipMalloc((void **)&dev->pool, total));
   char *p = dev->pool;
   auto take = [&](size_t n) {
@@ -414,6 +441,7 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   dev->bufs.ray_D = (hc_float4 *)take(rec);
   dev->bufs.isect = (hc_float4 *)take(rec);
   dev->bufs.isect_type = (int *)take(ints);
+  dev->bufs.isect_object = (int *)take(ints);
   dev->bufs.state0 = (hc_uint4 *)take(rec);
   dev->bufs.state1 = (hc_uint4 *)take(rec);
   dev->bufs.state2 = (hc_float4 *)take(rec);
@@ -648,7 +676,8 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
   b.bytes = bytes;
   dev->globals[name] = b;
   if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0 ||
-      strcmp(name, "__prim_tri_index") == 0) {
+      strcmp(name, "__prim_tri_index") == 0 || strcmp(name, "__prim_object") == 0 ||
+      strcmp(name, "__object_node") == 0) {
     dev->bvhw_dirty = true;
   }
   return 0;

@@ -15,7 +15,7 @@
  * BVH gives the same closest hits; parity is checked against the reference
  * kernel traversing these same arrays.
  *
- * C ABI (host only, no HIP): hcb_build_bvh2().
+ * C ABI (host only, no HIP): hcb_build / hcb_build_boxes, hcb_pack, hcb_free.
  */
 #include <algorithm>
 #include <cfloat>
@@ -64,9 +64,20 @@ struct Node {
 };
 
 struct Builder {
-  const float *verts;
   const uint32_t *vis;
+  const int32_t *kind = nullptr; /* per primitive: 0 triangle, 1 object instance */
   int max_leaf;
+
+  /* Leaves hold one primitive kind; an instance is always alone in its leaf
+   * (BVHBuild::create_leaf_node keeps object references in leaves of their own,
+   * bvh/bvh_build.cpp:777-830, and BVH2::pack_leaf encodes them, bvh2.cpp:40-61). */
+  bool leaf_ok(int lo, int hi) const
+  {
+    if (!kind) return true;
+    int inst = 0;
+    for (int i = lo; i < hi; i++) inst += kind[order[i]] != 0;
+    return inst == 0 || (inst == 1 && hi - lo == 1);
+  }
   std::vector<BBox> pbox;
   std::vector<float> cent; /* 3 per prim */
   std::vector<int> order;
@@ -88,7 +99,7 @@ struct Builder {
     const int n = hi - lo;
     int idx = (int)nodes.size();
     nodes.push_back(node);
-    if (n <= 1 || depth > 60) {
+    if (n <= 1 || (depth > 60 && leaf_ok(lo, hi))) {
       nodes[idx].leaf = true;
       nodes[idx].lo = lo;
       nodes[idx].hi = hi;
@@ -144,7 +155,7 @@ struct Builder {
     float split_cost = 1.0f + (parea > 0.0f ? best_cost / parea : FLT_MAX);
     int mid;
     if (best_axis < 0) {
-      if (n <= max_leaf) {
+      if (n <= max_leaf && leaf_ok(lo, hi)) {
         nodes[idx].leaf = true;
         nodes[idx].lo = lo;
         nodes[idx].hi = hi;
@@ -153,7 +164,7 @@ struct Builder {
       mid = lo + n / 2; /* coincident centroids: split by count */
     }
     else {
-      if (n <= max_leaf && leaf_cost <= split_cost) {
+      if (n <= max_leaf && leaf_cost <= split_cost && leaf_ok(lo, hi)) {
         nodes[idx].leaf = true;
         nodes[idx].lo = lo;
         nodes[idx].hi = hi;
@@ -209,21 +220,12 @@ struct hcb_ctx {
   int n_inner = 0, n_leaf = 0;
 };
 
-void *hcb_build(int n, const float *verts, const uint32_t *vis, int max_leaf_size, int64_t *counts)
+static void *build_common(hcb_ctx *ctx, int n, int64_t *counts)
 {
-  hcb_ctx *ctx = new hcb_ctx();
   Builder &b = ctx->b;
-  b.verts = verts;
-  b.vis = vis;
-  b.max_leaf = max_leaf_size > 0 ? max_leaf_size : 8;
-  b.pbox.resize(n);
   b.cent.resize(3 * (size_t)n);
   b.order.resize(n);
   for (int i = 0; i < n; i++) {
-    b.pbox[i].reset();
-    for (int k = 0; k < 3; k++) {
-      b.pbox[i].grow(verts + 9 * (size_t)i + 3 * k);
-    }
     for (int a = 0; a < 3; a++) {
       b.cent[3 * i + a] = 0.5f * (b.pbox[i].mn[a] + b.pbox[i].mx[a]);
     }
@@ -241,6 +243,42 @@ void *hcb_build(int n, const float *verts, const uint32_t *vis, int max_leaf_siz
   counts[1] = ctx->n_leaf;
   counts[2] = b.nodes.empty() ? 0 : (b.nodes[ctx->root].leaf ? -1 : 0);
   return ctx;
+}
+
+void *hcb_build(int n, const float *verts, const uint32_t *vis, int max_leaf_size, int64_t *counts)
+{
+  hcb_ctx *ctx = new hcb_ctx();
+  Builder &b = ctx->b;
+  b.vis = vis;
+  b.max_leaf = max_leaf_size > 0 ? max_leaf_size : 8;
+  b.pbox.resize(n);
+  for (int i = 0; i < n; i++) {
+    b.pbox[i].reset();
+    for (int k = 0; k < 3; k++) {
+      b.pbox[i].grow(verts + 9 * (size_t)i + 3 * k);
+    }
+  }
+  return build_common(ctx, n, counts);
+}
+
+/* Same over explicit primitive boxes (n x 6: min xyz, max xyz) with a kind per
+ * primitive (0 triangle, 1 object instance): the top-level BVH of a scene with
+ * instanced geometry (BVHBuild::add_reference_object, bvh/bvh_build.cpp:283). */
+void *hcb_build_boxes(
+    int n, const float *boxes, const uint32_t *vis, const int32_t *kind, int max_leaf_size, int64_t *counts)
+{
+  hcb_ctx *ctx = new hcb_ctx();
+  Builder &b = ctx->b;
+  b.vis = vis;
+  b.kind = kind;
+  b.max_leaf = max_leaf_size > 0 ? max_leaf_size : 8;
+  b.pbox.resize(n);
+  for (int i = 0; i < n; i++) {
+    b.pbox[i].reset();
+    b.pbox[i].grow(boxes + 6 * (size_t)i);
+    b.pbox[i].grow(boxes + 6 * (size_t)i + 3);
+  }
+  return build_common(ctx, n, counts);
 }
 
 /* prim_type: PRIMITIVE_TRIANGLE for every slot. */
@@ -272,10 +310,19 @@ int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
     const Node &nd = b.nodes[e.node];
     if (nd.leaf) {
       float *d = leaves_out + 4 * (size_t)e.idx;
-      d[0] = bits_i(nd.lo);
-      d[1] = bits_i(nd.hi);
-      d[2] = bits_f(nd.visibility);
-      d[3] = bits_f(PRIMITIVE_TRIANGLE);
+      if (b.kind && b.kind[b.order[nd.lo]] != 0) {
+        /* object instance leaf: ~slot, 0, visibility, prim_type 0 */
+        d[0] = bits_i(~nd.lo);
+        d[1] = bits_i(0);
+        d[2] = bits_f(nd.visibility);
+        d[3] = bits_f(0u);
+      }
+      else {
+        d[0] = bits_i(nd.lo);
+        d[1] = bits_i(nd.hi);
+        d[2] = bits_f(nd.visibility);
+        d[3] = bits_f(PRIMITIVE_TRIANGLE);
+      }
     }
     else {
       int idx[2];

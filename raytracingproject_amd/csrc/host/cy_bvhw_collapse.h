@@ -22,9 +22,13 @@
  *   bounds : the exact BVH2 child boxes (float), so the slab test of a wide
  *            child is bit-for-bit the reference's test of that BVH2 child
  *            (bvh/bvh_nodes.h:31-80);
- *   child  : >= 0 inner child node index, < 0 leaf ~first_primitive;
+ *   child  : >= 0 inner child node index, < 0 leaf ~first_primitive
+ *            (instance leaf: ~object);
  *   meta   : child visibility (low 28 bits, as the BVH2 node stored it) |
- *            primitive count << 28 for leaves; 0 = empty slot.
+ *            primitive count << 28 for leaves (0 for an instance); 0 = empty slot.
+ * Instanced geometry (two-level BVH, bvh/bvh.cpp:323-520): each object BVH
+ * root __object_node[object] is collapsed once into its own wide subtree;
+ * object_root[object] is its wide root.
  */
 #ifndef CY_BVHW_COLLAPSE_H
 #define CY_BVHW_COLLAPSE_H
@@ -57,6 +61,11 @@ struct Collapser {
   size_t n_nodes2 = 0;           /* float4 count */
   const float *leaves2 = nullptr;
   size_t n_leaves2 = 0;
+  const uint32_t *prim_object = nullptr; /* __prim_object (instance leaves) */
+  size_t n_prims = 0;
+  const uint32_t *object_node = nullptr; /* __object_node: BVH2 root of each object's own BVH */
+  size_t n_objects = 0;
+  std::vector<int> object_root; /* per object: wide root of its BVH, -1 if not instanced */
   std::vector<uint32_t> out; /* 8 * width words per wide node */
   std::string error;
   int max_depth = 0;
@@ -95,8 +104,22 @@ struct Collapser {
     memcpy(w, leaves2 + 4 * li, 16);
     const int s = (int)w[0], e = (int)w[1];
     if (s < 0) {
-      error = "instanced BVH leaves are not supported";
-      return false;
+      /* object instance leaf (bvh2.cpp pack_leaf: ~slot, 0): code it as a
+       * count-0 leaf whose index is the object */
+      const size_t slot = (size_t)(~s);
+      if (!prim_object || slot >= n_prims) {
+        error = "instance leaf without __prim_object";
+        return false;
+      }
+      const uint32_t ob = prim_object[slot];
+      if (!object_node || ob >= n_objects || ob >= (1u << 27)) {
+        error = "instance leaf object out of range";
+        return false;
+      }
+      instances.push_back((int)ob);
+      *start = (int)ob;
+      *count = 0;
+      return true;
     }
     if ((w[3] & 1u) == 0u) { /* PRIMITIVE_TRIANGLE = 1 */
       error = "only triangle leaves are supported";
@@ -130,7 +153,7 @@ struct Collapser {
       return false;
     }
     int s = -1, n = -1;
-    if (n0 >= 0 && n1 >= 0 && (c[0].vis & 0x0FFFFFFFu) == (c[1].vis & 0x0FFFFFFFu)) {
+    if (n0 > 0 && n1 > 0 && (c[0].vis & 0x0FFFFFFFu) == (c[1].vis & 0x0FFFFFFFu)) {
       if (s0 + n0 == s1) {
         s = s0;
         n = n0 + n1;
@@ -162,7 +185,7 @@ struct Collapser {
     if (!subtree_range(r.addr, &s, &n)) {
       return false;
     }
-    if (n >= 0 && n <= merge_prims) {
+    if (n > 0 && n <= merge_prims) {
       *start = s;
       *count = n;
       return true;
@@ -253,21 +276,19 @@ struct Collapser {
     return true;
   }
 
-  /* root: BVH2 root address (KernelBVH.root) */
-  bool run(int root)
+  std::vector<int> instances; /* objects referenced by instance leaves (may repeat) */
+
+  /* Collapse the BVH2 subtree at `root` into wide nodes starting at a fresh
+   * node index, breadth first; returns that index or -1 on error. */
+  long collapse(int root)
   {
-    if (width != 4 && width != 8) {
-      error = "width must be 4 or 8";
-      return false;
-    }
-    out.assign(words(), 0u);
-    sub_start.assign(n_nodes2 / 4 + 1, -1);
-    sub_count.assign(n_nodes2 / 4 + 1, -2);
+    const size_t base = out.size() / words();
+    out.resize(out.size() + words(), 0u);
     std::vector<std::pair<size_t, Ref>> pending, next;
     std::vector<Ref> ch(width);
     int n = 0;
     if (root < 0) {
-      /* single-leaf scene: one wide node holding the leaf with an unbounded box */
+      /* single-leaf BVH: one wide node holding the leaf with an unbounded box */
       Ref r;
       r.addr = root;
       r.vis = 0x0FFFFFFFu;
@@ -275,27 +296,75 @@ struct Collapser {
         r.lo[a] = -FLT_MAX;
         r.hi[a] = FLT_MAX;
       }
-      max_depth = 1;
-      return emit(0, &r, 1, &pending);
+      max_depth = std::max(max_depth, 1);
+      return emit(base, &r, 1, &pending) ? (long)base : -1;
     }
     Ref r;
     r.addr = root;
     r.vis = 0xFFFFFFFFu;
-    if (!open(r, ch.data(), &n) || !emit(0, ch.data(), n, &pending)) {
-      return false;
+    if (!open(r, ch.data(), &n) || !emit(base, ch.data(), n, &pending)) {
+      return -1;
     }
     int depth = 1;
     while (!pending.empty()) {
       next.clear();
       for (auto &p : pending) {
         if (!open(p.second, ch.data(), &n) || !emit(p.first, ch.data(), n, &next)) {
-          return false;
+          return -1;
         }
       }
       pending.swap(next);
       depth++;
     }
-    max_depth = depth;
+    max_depth = std::max(max_depth, depth);
+    return (long)base;
+  }
+
+  /* root: BVH2 root address (KernelBVH.root).  The top level becomes wide
+   * node 0; each instanced object's BVH (root __object_node[object]) is
+   * collapsed once per distinct root and recorded in object_root. */
+  bool run(int root)
+  {
+    if (width != 4 && width != 8) {
+      error = "width must be 4 or 8";
+      return false;
+    }
+    out.clear();
+    sub_start.assign(n_nodes2 / 4 + 1, -1);
+    sub_count.assign(n_nodes2 / 4 + 1, -2);
+    instances.clear();
+    object_root.assign(n_objects, -1);
+    max_depth = 0;
+    if (collapse(root) != 0) {
+      return false;
+    }
+    const int top_depth = max_depth;
+    int deepest = top_depth;
+    std::vector<std::pair<int, long>> done; /* BVH2 root -> wide root */
+    for (size_t i = 0; i < instances.size(); i++) {
+      const int ob = instances[i];
+      if (object_root[ob] >= 0) {
+        continue;
+      }
+      const int r2 = (int)object_node[ob];
+      long wr = -1;
+      for (auto &d : done) {
+        if (d.first == r2) {
+          wr = d.second;
+        }
+      }
+      if (wr < 0) {
+        max_depth = 0;
+        wr = collapse(r2);
+        if (wr < 0) {
+          return false;
+        }
+        deepest = std::max(deepest, top_depth + max_depth);
+        done.push_back(std::make_pair(r2, wr));
+      }
+      object_root[ob] = (int)wr;
+    }
+    max_depth = deepest;
     return true;
   }
 };

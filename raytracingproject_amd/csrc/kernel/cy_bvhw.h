@@ -16,6 +16,15 @@
  * current hit is skipped).  Leaf children are stack entries too, so triangles
  * are tested in near-to-far order.  The first CY_LDS_STACKW entries of the
  * stack live in LDS, one column per thread.
+ *
+ * Instancing: a leaf child with primitive count 0 is an object instance; the
+ * ray moves to object space (bvh_instance_push, t scaled like the reference)
+ * and continues at the object's own wide root; an entry with distance -inf
+ * below it restores world space when popped.  Entry distances pushed inside
+ * the instance are object-space, compared with the object-space hit t.
+ * Because a different visiting order scales t through a different sequence of
+ * instances, hit distances can differ from the BVH2 traversal's in the last
+ * ulp on instanced scenes (tests bound the film difference there).
  */
 #ifndef CY_BVHW_H
 #define CY_BVHW_H
@@ -119,9 +128,10 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
   stack.lds_t = lds_stack ? (float *)(lds_stack + CY_LDS_STACKW * CY_BLOCK) : nullptr;
   int sp = 0;
 
-  const cfloat3 P = ray->P;
-  const cfloat3 dir = bvh_clamp_direction(ray->D);
-  const cfloat3 idir = rcp3(dir);
+  cfloat3 P = ray->P;
+  cfloat3 dir = bvh_clamp_direction(ray->D);
+  cfloat3 idir = rcp3(dir);
+  int object = OBJECT_NONE;
 
   isect->t = ray->t;
   isect->u = 0.0f;
@@ -195,6 +205,19 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       n_leaves++;
       const int packed = ~code;
       int prim_addr = packed >> 4;
+      if ((packed & 15) == 0) {
+        /* instance leaf (count 0, index = object): enter the object's BVH in
+         * object space (bvh_instance_push); a -inf stack entry marks the exit */
+        object = prim_addr;
+        isect->t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect->t);
+        if (sp >= CY_BVHW_STACK) {
+          cy_set_error(err, CY_ERR_BVH_STACK, W);
+          return false;
+        }
+        stack.set(sp++, 0, -CY_INF);
+        code = kg->bvhw_object_root[object];
+        continue;
+      }
       const int prim_end = prim_addr + (packed & 15);
       const bool ident = kg->tri_index_identity != 0;
       uint vi = ident ? 3u * (uint)prim_addr : kg->__prim_tri_index[prim_addr];
@@ -212,7 +235,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
         if (ray_triangle_intersect(P, dir, isect->t, f4to3(v0), f4to3(v1), f4to3(v2), &uu, &vv, &tt)) {
           if (kg->__prim_visibility[prim_addr] & visibility) {
             isect->prim = prim_addr;
-            isect->object = OBJECT_NONE;
+            isect->object = object;
             isect->type = PRIMITIVE_TRIANGLE;
             isect->u = uu;
             isect->v = vv;
@@ -238,6 +261,12 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       while (sp > 0) {
         float et;
         stack.get(--sp, &code, &et);
+        if (et == -CY_INF) {
+          /* instance exit (bvh_instance_pop) */
+          isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
+          object = OBJECT_NONE;
+          continue;
+        }
         if (et <= isect->t) {
           found = true;
           break;

@@ -44,6 +44,9 @@ typedef struct CyGlobals {
   /* device-internal W-wide BVH widened from __bvh_nodes/__bvh_leaf_nodes
    * (csrc/host/cy_bvhw_collapse.h); nullptr when traversing the BVH2 */
   const void *bvhw_nodes;
+  /* per object: wide node index of the root of its own BVH (instanced
+   * geometry; the W-wide counterpart of __object_node), or nullptr */
+  const int *bvhw_object_root;
   /* 1 when __prim_tri_index[i] == 3 * i for every primitive (checked when the
    * BVH is widened): triangle vertices are then read without the indirection */
   int tri_index_identity;

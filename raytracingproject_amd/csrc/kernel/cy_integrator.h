@@ -30,6 +30,7 @@ typedef struct CyPathBuffers {
   hc_float4 *ray_D;      /* D.xyz, (unused) */
   hc_float4 *isect;      /* t, u, v, prim (bits) */
   int *isect_type;       /* primitive type, 0 = miss */
+  int *isect_object;     /* instance object of the hit, OBJECT_NONE if not instanced */
   hc_uint4 *state0;      /* flag, rng_hash, rng_offset, sample */
   hc_uint4 *state1;      /* bounce, diffuse_bounce, glossy_bounce, transmission_bounce */
   hc_float4 *state2;     /* transparent_bounce (bits), min_ray_pdf, ray_pdf, ray_t */
@@ -494,7 +495,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     isect.u = is4.y;
     isect.v = is4.z;
     isect.prim = as_int(is4.w);
-    isect.object = OBJECT_NONE;
+    isect.object = cy_ld(&b->isect_object[slot]);
     isect.type = type;
 
     CySD sd;

@@ -535,6 +535,12 @@ CY_FN cfloat3 transform_direction(const struct cy_tfm *t, cfloat3 a)
              a.x * t->y.x + a.y * t->y.y + a.z * t->y.z,
              a.x * t->z.x + a.y * t->z.y + a.z * t->z.z);
 }
+/* util_transform.h transform_direction_transposed: dot products with the columns */
+CY_FN cfloat3 transform_direction_transposed(const struct cy_tfm *t, cfloat3 a)
+{
+  return mk3(dot3(mk3(t->x.x, t->y.x, t->z.x), a), dot3(mk3(t->x.y, t->y.y, t->z.y), a),
+             dot3(mk3(t->x.z, t->y.z, t->z.z), a));
+}
 CY_FN float dot4(struct cy_f4 a, struct cy_f4 b)
 {
   return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);

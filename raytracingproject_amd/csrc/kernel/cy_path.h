@@ -145,7 +145,7 @@ CY_FN void camera_sample_ray(
 /* ---------------------------------------------------------------------------
  * BVH2 traversal over the packed Cycles layout (bvh/bvh_traversal.h:34-227,
  * bvh_nodes.h:31-77, geom_triangle_intersect.h:25-72, util_math_intersect.h:88-195).
- * Single-level BVH with transforms applied (instancing rejected at load).
+ * Two-level: instance leaves enter an object's own BVH in object space.
  */
 CY_FN cfloat3 bvh_clamp_direction(cfloat3 dir)
 {
@@ -229,6 +229,44 @@ struct CyStack {
   }
 };
 
+/* Object transforms (geom/geom_object.h:37-48): static objects only. */
+CY_FN const struct cy_tfm *object_tfm(const CyGlobals *kg, int object)
+{
+  return (const struct cy_tfm *)&kg->__objects[object].tfm;
+}
+CY_FN const struct cy_tfm *object_itfm(const CyGlobals *kg, int object)
+{
+  return (const struct cy_tfm *)&kg->__objects[object].itfm;
+}
+
+/* bvh_instance_push / bvh_instance_pop (geom/geom_object.h:425-470): the ray
+ * enters an instance in object space, its t scaled by the direction length. */
+CY_FN float bvh_instance_push(
+    const CyGlobals *kg, int object, const CyRay *ray, cfloat3 *P, cfloat3 *dir, cfloat3 *idir, float t)
+{
+  const struct cy_tfm *tfm = object_itfm(kg, object);
+  *P = transform_point(tfm, ray->P);
+  float len;
+  *dir = bvh_clamp_direction(normalize_len3(transform_direction(tfm, ray->D), &len));
+  *idir = rcp3(*dir);
+  if (t != CY_FLT_MAX) {
+    t *= len;
+  }
+  return t;
+}
+
+CY_FN float bvh_instance_pop(
+    const CyGlobals *kg, int object, const CyRay *ray, cfloat3 *P, cfloat3 *dir, cfloat3 *idir, float t)
+{
+  if (t != CY_FLT_MAX) {
+    t /= len3(transform_direction(object_itfm(kg, object), ray->D));
+  }
+  *P = ray->P;
+  *dir = bvh_clamp_direction(ray->D);
+  *idir = rcp3(*dir);
+  return t;
+}
+
 template<bool any_hit>
 CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           const CyRay *ray,
@@ -245,9 +283,10 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
   traversal_stack.set(0, ENTRYPOINT_SENTINEL);
   int stack_ptr = 0;
   int node_addr = KD->bvh.root;
-  const cfloat3 P = ray->P;
-  const cfloat3 dir = bvh_clamp_direction(ray->D);
-  const cfloat3 idir = rcp3(dir);
+  int object = OBJECT_NONE;
+  cfloat3 P = ray->P;
+  cfloat3 dir = bvh_clamp_direction(ray->D);
+  cfloat3 idir = rcp3(dir);
 
   isect->t = ray->t;
   isect->u = 0.0f;
@@ -260,105 +299,122 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
   const hc_float4 *nodes = kg->__bvh_nodes;
 
   do {
-    while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
-      n_nodes++;
-      const hc_float4 cnodes = nodes[node_addr + 0];
-      const hc_float4 node0 = nodes[node_addr + 1];
-      const hc_float4 node1 = nodes[node_addr + 2];
-      const hc_float4 node2 = nodes[node_addr + 3];
-      const float t = isect->t;
-      float c0lox = (node0.x - P.x) * idir.x;
-      float c0hix = (node0.z - P.x) * idir.x;
-      float c0loy = (node1.x - P.y) * idir.y;
-      float c0hiy = (node1.z - P.y) * idir.y;
-      float c0loz = (node2.x - P.z) * idir.z;
-      float c0hiz = (node2.z - P.z) * idir.z;
-      float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
-      float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
-      float c1lox = (node0.y - P.x) * idir.x;
-      float c1hix = (node0.w - P.x) * idir.x;
-      float c1loy = (node1.y - P.y) * idir.y;
-      float c1hiy = (node1.w - P.y) * idir.y;
-      float c1loz = (node2.y - P.z) * idir.z;
-      float c1hiz = (node2.w - P.z) * idir.z;
-      float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
-      float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
-      int traverse_mask = (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
-                          (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
+    do {
+      while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
+        n_nodes++;
+        const hc_float4 cnodes = nodes[node_addr + 0];
+        const hc_float4 node0 = nodes[node_addr + 1];
+        const hc_float4 node1 = nodes[node_addr + 2];
+        const hc_float4 node2 = nodes[node_addr + 3];
+        const float t = isect->t;
+        float c0lox = (node0.x - P.x) * idir.x;
+        float c0hix = (node0.z - P.x) * idir.x;
+        float c0loy = (node1.x - P.y) * idir.y;
+        float c0hiy = (node1.z - P.y) * idir.y;
+        float c0loz = (node2.x - P.z) * idir.z;
+        float c0hiz = (node2.z - P.z) * idir.z;
+        float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
+        float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
+        float c1lox = (node0.y - P.x) * idir.x;
+        float c1hix = (node0.w - P.x) * idir.x;
+        float c1loy = (node1.y - P.y) * idir.y;
+        float c1hiy = (node1.w - P.y) * idir.y;
+        float c1loz = (node2.y - P.z) * idir.z;
+        float c1hiz = (node2.w - P.z) * idir.z;
+        float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
+        float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
+        int traverse_mask = (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
+                            (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
 
-      node_addr = as_int(cnodes.z);
-      int node_addr_child1 = as_int(cnodes.w);
+        node_addr = as_int(cnodes.z);
+        int node_addr_child1 = as_int(cnodes.w);
 
-      if (traverse_mask == 3) {
-        bool is_closest_child1 = (c1min < c0min);
-        if (is_closest_child1) {
-          int tmp = node_addr;
-          node_addr = node_addr_child1;
-          node_addr_child1 = tmp;
+        if (traverse_mask == 3) {
+          bool is_closest_child1 = (c1min < c0min);
+          if (is_closest_child1) {
+            int tmp = node_addr;
+            node_addr = node_addr_child1;
+            node_addr_child1 = tmp;
+          }
+          ++stack_ptr;
+          if (stack_ptr >= BVH_STACK_SIZE) {
+            cy_set_error(err, CY_ERR_BVH_STACK, 0);
+            return false;
+          }
+          traversal_stack.set(stack_ptr, node_addr_child1);
         }
-        ++stack_ptr;
-        if (stack_ptr >= BVH_STACK_SIZE) {
-          cy_set_error(err, CY_ERR_BVH_STACK, 0);
-          return false;
+        else {
+          if (traverse_mask == 2) {
+            node_addr = node_addr_child1;
+          }
+          else if (traverse_mask == 0) {
+            node_addr = traversal_stack.get(stack_ptr);
+            --stack_ptr;
+          }
         }
-        traversal_stack.set(stack_ptr, node_addr_child1);
       }
-      else {
-        if (traverse_mask == 2) {
-          node_addr = node_addr_child1;
-        }
-        else if (traverse_mask == 0) {
+
+      if (node_addr < 0) {
+        n_leaves++;
+        const hc_float4 leaf = kg->__bvh_leaf_nodes[-node_addr - 1];
+        int prim_addr = as_int(leaf.x);
+        if (prim_addr >= 0) {
+          const int prim_addr2 = as_int(leaf.y);
+          const uint type = as_uint(leaf.w);
           node_addr = traversal_stack.get(stack_ptr);
           --stack_ptr;
-        }
-      }
-    }
-
-    if (node_addr < 0) {
-      n_leaves++;
-      const hc_float4 leaf = kg->__bvh_leaf_nodes[-node_addr - 1];
-      int prim_addr = as_int(leaf.x);
-      if (prim_addr >= 0) {
-        const int prim_addr2 = as_int(leaf.y);
-        const uint type = as_uint(leaf.w);
-        node_addr = traversal_stack.get(stack_ptr);
-        --stack_ptr;
-        if ((type & PRIMITIVE_ALL) == PRIMITIVE_TRIANGLE) {
-          for (; prim_addr < prim_addr2; prim_addr++) {
-            n_tris++;
-            const uint tri_vindex = kg->__prim_tri_index[prim_addr];
-            const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
-            float tt, uu, vv;
-            if (ray_triangle_intersect(
-                    P, dir, isect->t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt)) {
-              if (kg->__prim_visibility[prim_addr] & visibility) {
-                isect->prim = prim_addr;
-                isect->object = OBJECT_NONE;
-                isect->type = PRIMITIVE_TRIANGLE;
-                isect->u = uu;
-                isect->v = vv;
-                isect->t = tt;
-                if (any_hit) {
-                  if (cnt_nodes) {
-                    *cnt_nodes += n_nodes;
-                    *cnt_leaves += n_leaves;
-                    *cnt_tris += n_tris;
+          if ((type & PRIMITIVE_ALL) == PRIMITIVE_TRIANGLE) {
+            for (; prim_addr < prim_addr2; prim_addr++) {
+              n_tris++;
+              const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+              const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+              float tt, uu, vv;
+              if (ray_triangle_intersect(
+                      P, dir, isect->t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt)) {
+                if (kg->__prim_visibility[prim_addr] & visibility) {
+                  isect->prim = prim_addr;
+                  isect->object = object;
+                  isect->type = PRIMITIVE_TRIANGLE;
+                  isect->u = uu;
+                  isect->v = vv;
+                  isect->t = tt;
+                  if (any_hit) {
+                    if (cnt_nodes) {
+                      *cnt_nodes += n_nodes;
+                      *cnt_leaves += n_leaves;
+                      *cnt_tris += n_tris;
+                    }
+                    return true;
                   }
-                  return true;
                 }
               }
             }
           }
+          else {
+            cy_set_error(err, CY_ERR_PRIMITIVE, type);
+          }
         }
         else {
-          cy_set_error(err, CY_ERR_PRIMITIVE, type);
+          /* instance push (bvh_traversal.h:190-205) */
+          object = (int)kg->__prim_object[-prim_addr - 1];
+          isect->t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect->t);
+          ++stack_ptr;
+          if (stack_ptr >= BVH_STACK_SIZE) {
+            cy_set_error(err, CY_ERR_BVH_STACK, 0);
+            return false;
+          }
+          traversal_stack.set(stack_ptr, ENTRYPOINT_SENTINEL);
+          node_addr = (int)kg->__object_node[object];
         }
       }
-      else {
-        /* instance push — instancing is rejected at scene load */
-        cy_set_error(err, CY_ERR_FEATURE, 1);
-        node_addr = ENTRYPOINT_SENTINEL;
-      }
+    } while (node_addr != ENTRYPOINT_SENTINEL);
+
+    if (stack_ptr >= 0) {
+      /* instance pop (bvh_traversal.h:209-222) */
+      isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
+      object = OBJECT_NONE;
+      node_addr = traversal_stack.get(stack_ptr);
+      --stack_ptr;
     }
   } while (node_addr != ENTRYPOINT_SENTINEL);
 
@@ -442,6 +498,16 @@ CY_FN cfloat3 triangle_refine(const CyGlobals *kg, const CyIsect *isect, const C
   cfloat3 P = ray->P;
   cfloat3 D = ray->D;
   float t = isect->t;
+  if (isect->object != OBJECT_NONE) {
+    /* instanced geometry: refine in object space */
+    if (t == 0.0f) {
+      return P;
+    }
+    const struct cy_tfm *itfm = object_itfm(kg, isect->object);
+    P = transform_point(itfm, P);
+    D = transform_direction(itfm, mul3f(D, t));
+    D = normalize_len3(D, &t);
+  }
   P = add3(P, mul3f(D, t));
   const uint tri_vindex = kg->__prim_tri_index[isect->prim];
   const hc_float4 tri_a = kg->__prim_tri_verts[tri_vindex + 0];
@@ -457,10 +523,20 @@ CY_FN cfloat3 triangle_refine(const CyGlobals *kg, const CyIsect *isect, const C
     float rt = dot3(edge2, qvec) / det;
     P = add3(P, mul3f(D, rt));
   }
+  if (isect->object != OBJECT_NONE) {
+    P = transform_point(object_tfm(kg, isect->object), P);
+  }
   return P;
 }
 
-/* kernel_shader.h:54-153 (static triangles, no instancing, no differentials:
+/* object_normal_transform (geom_object.h:168-177, __OBJECT_MOTION__ form:
+ * sd->ob_itfm is the static inverse transform) */
+CY_FN cfloat3 object_normal_transform(const CyGlobals *kg, int object, cfloat3 N)
+{
+  return normalize3(transform_direction_transposed(object_itfm(kg, object), N));
+}
+
+/* kernel_shader.h:54-153 (static triangles, instanced or not; no differentials:
  * the differentials only feed texture filtering, which this node subset lacks). */
 CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *isect, const CyRay *ray)
 {
@@ -483,6 +559,11 @@ CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *i
   }
   sd->I = neg3(ray->D);
   sd->flag |= kg->__shaders[(uint)sd->shader & SHADER_MASK].flags;
+  if (isect->object != OBJECT_NONE) {
+    /* instance transform */
+    sd->N = object_normal_transform(kg, sd->object, sd->N);
+    sd->Ng = object_normal_transform(kg, sd->object, sd->Ng);
+  }
 
   bool backfacing = (dot3(sd->Ng, sd->I) < 0.0f);
   if (backfacing) {
@@ -1458,10 +1539,31 @@ CY_FN float triangle_light_pdf_area(const CyGlobals *kg, cfloat3 Ng, cfloat3 I, 
   return t * t * pdf / cos_pi;
 }
 
+/* triangle_world_space_vertices (kernel_light.h:302-329), static objects:
+ * true when the vertices were transformed (the reference's has_motion) */
+CY_FN bool triangle_world_space_vertices(const CyGlobals *kg, int object, int prim, cfloat3 V[3])
+{
+  triangle_verts(kg, prim, V);
+  if (!(kg->__object_flag[object] & SD_OBJECT_TRANSFORM_APPLIED)) {
+    const struct cy_tfm *tfm = object_tfm(kg, object);
+    V[0] = transform_point(tfm, V[0]);
+    V[1] = transform_point(tfm, V[1]);
+    V[2] = transform_point(tfm, V[2]);
+    return true;
+  }
+  return false;
+}
+
+/* util_math.h triangle_area */
+CY_FN float triangle_area(cfloat3 v1, cfloat3 v2, cfloat3 v3)
+{
+  return len3(cross3(sub3(v3, v2), sub3(v1, v2))) * 0.5f;
+}
+
 CY_FN float triangle_light_pdf(const CyGlobals *kg, const CySD *sd, float t)
 {
   cfloat3 V[3];
-  triangle_verts(kg, sd->prim, V);
+  const bool has_motion = triangle_world_space_vertices(kg, sd->object, sd->prim, V);
   const cfloat3 e0 = sub3(V[1], V[0]);
   const cfloat3 e1 = sub3(V[2], V[0]);
   const cfloat3 e2 = sub3(V[2], V[1]);
@@ -1483,11 +1585,20 @@ CY_FN float triangle_light_pdf(const CyGlobals *kg, const CySD *sd, float t)
     if (solid_angle == 0.0f) {
       return 0.0f;
     }
-    float area = 0.5f * len3(N);
+    float area = has_motion ? triangle_area(V[0], V[1], V[2]) : 0.5f * len3(N);
     const float pdf = area * KD->integrator.pdf_triangles;
     return pdf / solid_angle;
   }
-  return triangle_light_pdf_area(kg, sd->Ng, sd->I, t);
+  float pdf = triangle_light_pdf_area(kg, sd->Ng, sd->I, t);
+  if (has_motion) {
+    const float area = 0.5f * len3(N);
+    if (area == 0.0f) {
+      return 0.0f;
+    }
+    const float area_pre = triangle_area(V[0], V[1], V[2]);
+    pdf = pdf * area_pre / area;
+  }
+  return pdf;
 }
 
 CY_FN void triangle_light_sample(const CyGlobals *kg,
@@ -1499,7 +1610,7 @@ CY_FN void triangle_light_sample(const CyGlobals *kg,
                                  const cfloat3 P)
 {
   cfloat3 V[3];
-  triangle_verts(kg, prim, V);
+  const bool has_motion = triangle_world_space_vertices(kg, object, prim, V);
   const cfloat3 e0 = sub3(V[1], V[0]);
   const cfloat3 e1 = sub3(V[2], V[0]);
   const cfloat3 e2 = sub3(V[2], V[1]);
@@ -1566,6 +1677,9 @@ CY_FN void triangle_light_sample(const CyGlobals *kg,
       ls->pdf = 0.0f;
       return;
     }
+    if (has_motion) {
+      area = triangle_area(V[0], V[1], V[2]);
+    }
     const float pdf = area * KD->integrator.pdf_triangles;
     ls->pdf = pdf / solid_angle;
   }
@@ -1584,6 +1698,10 @@ CY_FN void triangle_light_sample(const CyGlobals *kg,
     ls->P = add3(add3(mul3f(V[0], u), mul3f(V[1], v)), mul3f(V[2], t));
     ls->D = normalize_len3(sub3(ls->P, P), &ls->t);
     ls->pdf = triangle_light_pdf_area(kg, ls->Ng, neg3(ls->D), ls->t);
+    if (has_motion && area != 0.0f) {
+      const float area_pre = triangle_area(V[0], V[1], V[2]);
+      ls->pdf = ls->pdf * area_pre / area;
+    }
     ls->u = u;
     ls->v = v;
   }

@@ -38,6 +38,9 @@ def host_lib():
         lib = ctypes.CDLL(HOST_LIB)
         lib.hcb_build.restype = ctypes.c_void_p
         lib.hcb_build.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        lib.hcb_build_boxes.restype = ctypes.c_void_p
+        lib.hcb_build_boxes.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_void_p]
         lib.hcb_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.hcb_free.argtypes = [ctypes.c_void_p]
         _host = lib

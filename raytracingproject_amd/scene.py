@@ -202,6 +202,18 @@ class Mesh:
 
 
 @dataclass
+class Instance:
+    """An object placing geometry with a transform (render/object.h).  Geometry
+    used by one object has its transform applied on the host; geometry shared
+    by several objects keeps object-space vertices and its own BVH, entered
+    through an instance leaf of the top-level BVH (render/object.cpp:800-858,
+    bvh/bvh.cpp:323-520)."""
+
+    mesh: Mesh
+    tfm: np.ndarray  # (3, 4) object to world
+
+
+@dataclass
 class Lamp:
     """A Cycles Light (render/light.h): point, spot, area or sun (distant)."""
 
@@ -256,6 +268,7 @@ class Scene:
     light_sampling_threshold: float = 0.05
     filter_glossy: float = 0.0
     lamps: list = field(default_factory=list)
+    instances: list = field(default_factory=list)
     caustics_reflective: bool = True
     caustics_refractive: bool = True
     name: str = "scene"
@@ -446,52 +459,18 @@ def compile_scene(scene: Scene) -> DeviceScene:
     f32 = np.float32
     kd = abi.KernelData()
 
-    # --- geometry (render/geometry.cpp device_update_mesh + mesh.cpp pack_*)
-    verts_all, tris_all, shader_all, smooth_all, norm_all, objid_all = [], [], [], [], [], []
-    voff = 0
-    for oi, m in enumerate(scene.meshes):
-        v = np.asarray(m.verts, dtype=np.float32).reshape(-1, 3)
-        t = np.asarray(m.tris, dtype=np.int64).reshape(-1, 3)
-        sh = np.broadcast_to(np.asarray(m.shader, dtype=np.int64), (t.shape[0],))
-        verts_all.append(v)
-        tris_all.append(t + voff)
-        shader_all.append(sh)
-        smooth_all.append(np.full(t.shape[0], bool(m.smooth)))
-        if m.normals is not None:
-            norm_all.append(np.asarray(m.normals, dtype=np.float32).reshape(-1, 3))
-        else:
-            norm_all.append(_vertex_normals(v, t))
-        objid_all.append(np.full(t.shape[0], oi, dtype=np.int64))
-        voff += v.shape[0]
-    verts = np.concatenate(verts_all)
-    tris = np.concatenate(tris_all)
-    tri_shader_idx = np.concatenate(shader_all)
-    tri_smooth = np.concatenate(smooth_all)
-    vnormals = np.concatenate(norm_all)
-    tri_object = np.concatenate(objid_all)
-    ntri = tris.shape[0]
-
-    # object visibility_for_tracing (render/object.cpp): all rays, not a shadow catcher
-    vis_obj = PATH_RAY_ALL_VISIBILITY & ~(PATH_RAY_SHADOW_OPAQUE_CATCHER | PATH_RAY_SHADOW_TRANSPARENT_CATCHER)
-    tri_pos = verts[tris]  # (T, 3, 3)
-    visibility = np.full(ntri, vis_obj, dtype=np.uint32)
-    nodes, leaves, order, root = build_bvh2(tri_pos, visibility)
-
-    # pack_primitives (bvh.cpp:279-321): BVH slot i -> triangle order[i]
-    prim_index = order.astype(np.uint32)
-    prim_object = tri_object[order].astype(np.uint32)
-    prim_type = np.full(ntri, PRIMITIVE_TRIANGLE, dtype=np.uint32)
-    prim_visibility = visibility[order]
-    prim_tri_index = (3 * np.arange(ntri, dtype=np.uint32)).astype(np.uint32)
-    prim_tri_verts = np.ones((ntri * 3, 4), dtype=np.float32)
-    prim_tri_verts[:, :3] = tri_pos[order].reshape(-1, 3)
-    slot_of_tri = np.empty(ntri, dtype=np.int64)
-    slot_of_tri[order] = np.arange(ntri)
-    tri_vindex = np.zeros((ntri, 4), dtype=np.uint32)
-    tri_vindex[:, :3] = tris.astype(np.uint32)
-    tri_vindex[:, 3] = (3 * slot_of_tri).astype(np.uint32)
-    tri_vnormal = np.zeros((verts.shape[0], 4), dtype=np.float32)
-    tri_vnormal[:, :3] = vnormals
+    # --- geometry (render/geometry.cpp device_update_mesh + mesh.cpp pack_*,
+    # object.cpp apply_static_transforms, bvh/bvh.cpp pack_primitives /
+    # pack_instances)
+    g = _pack_geometry(scene)
+    ntri = g["ntri"]
+    tri_shader_idx = g["tri_shader_idx"]
+    tri_smooth = g["tri_smooth"]
+    nodes, leaves, root = g["nodes"], g["leaves"], g["root"]
+    prim_index, prim_object, prim_type = g["prim_index"], g["prim_object"], g["prim_type"]
+    prim_visibility, prim_tri_index, prim_tri_verts = g["prim_visibility"], g["prim_tri_index"], g["prim_tri_verts"]
+    tri_vindex, tri_vnormal = g["tri_vindex"], g["tri_vnormal"]
+    objects = g["objects"]
 
     # --- shaders (render/shader.cpp:462-475, 508-581 + svm.cpp); lamps share
     # one emission shader (the default light shader: emission 1.0), their
@@ -519,30 +498,42 @@ def compile_scene(scene: Scene) -> DeviceScene:
     tri_shader = tri_shader_idx.astype(np.uint32) | np.uint32(SHADER_CAST_SHADOW | SHADER_AREA_LIGHT)
     tri_shader = np.where(tri_smooth, tri_shader | np.uint32(SHADER_SMOOTH_NORMAL), tri_shader).astype(np.uint32)
 
-    # --- objects (render/object.cpp device_update_object_transform; transforms applied)
-    nobj = len(scene.meshes)
+    # --- objects (render/object.cpp:463-544 device_update_object_transform)
+    nobj = len(objects)
     kobjects = (abi.KernelObject * max(nobj, 1))()
-    ident = np.eye(4)[:3]
-    for i in range(nobj):
-        abi.set_transform(kobjects[i].tfm, ident)
-        abi.set_transform(kobjects[i].itfm, ident)
-        kobjects[i].shadow_terminator_offset = 0.0
-    object_flag = np.full(max(nobj, 1), SD_OBJECT_TRANSFORM_APPLIED, dtype=np.uint32)
+    object_flag = np.zeros(max(nobj, 1), dtype=np.uint32)
+    object_node = np.zeros(max(nobj, 1), dtype=np.uint32)
+    for i, ob in enumerate(objects):
+        tfm = ob["tfm"]
+        abi.set_transform(kobjects[i].tfm, tfm)
+        abi.set_transform(kobjects[i].itfm, np.linalg.inv(np.vstack([tfm, [0, 0, 0, 1]]))[:3])
+        kobjects[i].shadow_terminator_offset = 1.0  # 1 / (1 - 0.5 * 0)
+        kobjects[i].numverts = ob["numverts"]
+        if ob["applied"]:
+            object_flag[i] = SD_OBJECT_TRANSFORM_APPLIED
+        object_node[i] = np.uint32(ob["node"] & 0xFFFFFFFF)
 
     # --- lights (render/light.cpp:277-480, mesh lights only)
+    # light.cpp:330-400: per object using emissive triangles, in object order,
+    # world-space area (transform_point for instanced geometry)
     emissive = np.array([m.has_emission() for m in mats], dtype=bool)
-    light_tris = np.nonzero(emissive[tri_shader_idx])[0]
-    dist = (abi.KernelLightDistribution * (len(light_tris) + 1))()
+    light_list = []
+    for oi, ob in enumerate(objects):
+        tris_g = np.arange(ob["tri_offset"], ob["tri_offset"] + ob["ntri"])
+        for ti in tris_g[emissive[tri_shader_idx[tris_g]]]:
+            light_list.append((oi, int(ti)))
+    dist = (abi.KernelLightDistribution * (len(light_list) + 1))()
     totarea = f32(0.0)
-    for k, ti in enumerate(light_tris):
+    for k, (oi, ti) in enumerate(light_list):
         dist[k].totarea = float(totarea)
-        dist[k].prim = int(ti)
+        dist[k].prim = ti
         dist[k].shader_flag = 0
-        dist[k].object_id = int(tri_object[ti])
-        p1, p2, p3 = tri_pos[ti].astype(np.float32)
-        area = f32(0.5) * f32(np.sqrt(np.sum(np.cross(p2 - p1, p3 - p1).astype(np.float32) ** 2, dtype=np.float32)))
-        totarea = f32(totarea + area)
-    nd = len(light_tris)
+        dist[k].object_id = oi
+        p1, p2, p3 = g["tri_pos_object"][ti]
+        if not objects[oi]["applied"]:
+            p1, p2, p3 = (transform_point_f32(objects[oi]["tfm"], p) for p in (p1, p2, p3))
+        totarea = f32(totarea + triangle_area_f32(p1, p2, p3))
+    nd = len(light_list)
     trianglearea = totarea
     lamps = list(scene.lamps)
     num_lights = len(lamps)
@@ -672,7 +663,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "__prim_visibility": prim_visibility,
         "__prim_index": prim_index,
         "__prim_object": prim_object,
-        "__object_node": np.zeros(max(nobj, 1), dtype=np.uint32),
+        "__object_node": object_node,
         "__objects": np.frombuffer(abi.array_bytes(kobjects), dtype=np.uint8).copy(),
         "__object_flag": object_flag,
         "__tri_shader": tri_shader,
@@ -687,6 +678,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
     }
     info = {
         "triangles": ntri,
+        "objects": nobj,
+        "instanced_objects": int(sum(not ob["applied"] for ob in objects)),
         "bvh_inner_nodes": nodes.shape[0] // 4,
         "bvh_leaves": leaves.shape[0],
         "light_triangles": nd,
@@ -695,6 +688,217 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "name": scene.name,
     }
     return DeviceScene(kd, arrays, scene.width, scene.height, scene.samples, info)
+
+
+def transform_point_f32(tfm, p) -> np.ndarray:
+    """util_transform.h transform_point, float32 in the reference's order."""
+    t = np.asarray(tfm, dtype=np.float32)
+    p = np.asarray(p, dtype=np.float32)
+    f32 = np.float32
+    return np.array([f32(f32(f32(p[0] * t[r, 0]) + f32(p[1] * t[r, 1])) + f32(p[2] * t[r, 2])) + t[r, 3]
+                     for r in range(3)], dtype=np.float32)
+
+
+def triangle_area_f32(v1, v2, v3) -> np.float32:
+    """util_math.h triangle_area: len(cross(v3 - v2, v1 - v2)) * 0.5."""
+    f32 = np.float32
+    a = (np.asarray(v3, dtype=np.float32) - np.asarray(v2, dtype=np.float32)).astype(np.float32)
+    b = (np.asarray(v1, dtype=np.float32) - np.asarray(v2, dtype=np.float32)).astype(np.float32)
+    c = np.array([f32(a[1] * b[2]) - f32(a[2] * b[1]), f32(a[2] * b[0]) - f32(a[0] * b[2]),
+                  f32(a[0] * b[1]) - f32(a[1] * b[0])], dtype=np.float32)
+    d = f32(f32(f32(c[0] * c[0]) + f32(c[1] * c[1])) + f32(c[2] * c[2]))
+    return f32(f32(np.sqrt(d)) * f32(0.5))
+
+
+def _mesh_arrays(m: Mesh, tfm=None):
+    v = np.asarray(m.verts, dtype=np.float32).reshape(-1, 3)
+    t = np.asarray(m.tris, dtype=np.int64).reshape(-1, 3)
+    if tfm is not None:
+        v = np.stack([transform_point_f32(tfm, p) for p in v]).astype(np.float32) if len(v) else v
+    if m.normals is not None and tfm is None:
+        nrm = np.asarray(m.normals, dtype=np.float32).reshape(-1, 3)
+    else:
+        nrm = _vertex_normals(v, t)
+    sh = np.broadcast_to(np.asarray(m.shader, dtype=np.int64), (t.shape[0],))
+    return v, t, sh, nrm
+
+
+def _pack_geometry(scene: Scene) -> dict:
+    """Geometry, objects and the packed BVH of a scene: the device arrays of
+    GeometryManager::device_update_mesh (render/geometry.cpp:873-960) and
+    BVH::pack_primitives / pack_instances (bvh/bvh.cpp:279-520)."""
+    # objects: plain meshes (transform already applied by the caller), then instances
+    users = {}
+    for inst in scene.instances:
+        users[id(inst.mesh)] = users.get(id(inst.mesh), 0) + 1
+    ident = np.eye(4)[:3]
+    geoms, geom_of = [], {}  # geometry records in first-use order
+    objects = []
+    for m in scene.meshes:
+        v, t, sh, nrm = _mesh_arrays(m)
+        geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(m.smooth), applied=True))
+        objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True))
+    for inst in scene.instances:
+        tfm = np.asarray(inst.tfm, dtype=np.float64).reshape(3, 4)
+        if users[id(inst.mesh)] == 1:
+            v, t, sh, nrm = _mesh_arrays(inst.mesh, tfm.astype(np.float32))
+            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True))
+            objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True))  # tfm reset on apply
+            continue
+        if id(inst.mesh) not in geom_of:
+            v, t, sh, nrm = _mesh_arrays(inst.mesh)
+            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=False))
+            geom_of[id(inst.mesh)] = len(geoms) - 1
+        objects.append(dict(geom=geom_of[id(inst.mesh)], tfm=tfm, applied=False))
+
+    # global triangle / vertex arrays, geometry order (prim_offset, vert_offset)
+    toff = voff = 0
+    for gm in geoms:
+        gm["tri_offset"], gm["vert_offset"] = toff, voff
+        toff += gm["t"].shape[0]
+        voff += gm["v"].shape[0]
+    ntri, nvert = toff, voff
+    tri_shader_idx = np.concatenate([gm["sh"] for gm in geoms]) if geoms else np.zeros(0, np.int64)
+    tri_smooth = np.concatenate([np.full(gm["t"].shape[0], gm["smooth"]) for gm in geoms])
+    tri_pos = np.concatenate([gm["v"][gm["t"]] for gm in geoms]).astype(np.float32)  # (T,3,3)
+    tri_vindex = np.zeros((ntri, 4), dtype=np.uint32)
+    tri_vindex[:, :3] = np.concatenate([gm["t"] + gm["vert_offset"] for gm in geoms]).astype(np.uint32)
+    tri_vnormal = np.zeros((nvert, 4), dtype=np.float32)
+    tri_vnormal[:, :3] = np.concatenate([gm["nrm"] for gm in geoms])
+    for ob in objects:
+        gm = geoms[ob["geom"]]
+        ob["tri_offset"], ob["ntri"], ob["numverts"] = gm["tri_offset"], gm["t"].shape[0], gm["v"].shape[0]
+
+    vis_obj = PATH_RAY_ALL_VISIBILITY & ~(PATH_RAY_SHADOW_OPAQUE_CATCHER | PATH_RAY_SHADOW_TRANSPARENT_CATCHER)
+
+    # top level: triangles of objects with applied transforms + one reference per instance
+    ref_tri, ref_obj = [], []
+    for oi, ob in enumerate(objects):
+        if ob["applied"]:
+            ref_tri.append(np.arange(ob["tri_offset"], ob["tri_offset"] + ob["ntri"]))
+            ref_obj.append(np.full(ob["ntri"], oi))
+        else:
+            ref_tri.append(np.array([-1]))
+            ref_obj.append(np.array([oi]))
+    ref_tri = np.concatenate(ref_tri) if ref_tri else np.zeros(0, np.int64)
+    ref_obj = np.concatenate(ref_obj) if ref_obj else np.zeros(0, np.int64)
+    nref = len(ref_tri)
+    is_inst = ref_tri < 0
+    vis = np.full(nref, vis_obj, dtype=np.uint32)
+    if is_inst.any():
+        boxes = np.zeros((nref, 6), dtype=np.float32)
+        tp = tri_pos[np.where(is_inst, 0, ref_tri)]
+        boxes[:, :3] = tp.min(1)
+        boxes[:, 3:] = tp.max(1)
+        for k in np.nonzero(is_inst)[0]:
+            ob = objects[ref_obj[k]]
+            boxes[k] = _instance_bounds(geoms[ob["geom"]]["v"], ob["tfm"])
+        nodes, leaves, order, root = build_bvh2_boxes(boxes, vis, is_inst.astype(np.int32))
+    else:
+        nodes, leaves, order, root = build_bvh2(tri_pos[ref_tri], vis)
+
+    # pack_primitives (bvh.cpp:279-321)
+    slot_tri = ref_tri[order]
+    slot_inst = slot_tri < 0
+    prim_index = np.where(slot_inst, -1, slot_tri).astype(np.int64)
+    prim_object = ref_obj[order].astype(np.int64)
+    prim_type = np.where(slot_inst, 0, PRIMITIVE_TRIANGLE).astype(np.int64)
+    prim_visibility = np.where(slot_inst, 0, vis[order]).astype(np.int64)
+    tri_slots = np.cumsum(~slot_inst) - 1
+    prim_tri_index = np.where(slot_inst, -1, 3 * tri_slots).astype(np.int64)
+    tv = [tri_pos[slot_tri[~slot_inst]].reshape(-1, 3)]
+    n_tv = 3 * int((~slot_inst).sum())
+
+    # pack_instances (bvh.cpp:323-520): each instanced geometry's own BVH
+    # appended once; object_node = its root
+    node_parts, leaf_parts = [nodes], [leaves]
+    n_nodes, n_leaves = nodes.shape[0], leaves.shape[0]
+    p_index, p_object, p_type, p_vis, p_tri = [prim_index], [prim_object], [prim_type], [prim_visibility], [prim_tri_index]
+    n_prims = nref
+    geom_node = {}
+    for oi, ob in enumerate(objects):
+        ob["node"] = 0
+        if ob["applied"]:
+            continue
+        gi = ob["geom"]
+        if gi in geom_node:
+            ob["node"] = geom_node[gi]
+            continue
+        gm = geoms[gi]
+        gpos = gm["v"][gm["t"]].astype(np.float32)
+        gn, gl, go, groot = build_bvh2(gpos, np.full(gpos.shape[0], vis_obj, dtype=np.uint32))
+        gn = gn.copy() if groot == 0 else gn[:0].copy()
+        cz = gn[0::4].view(np.int32)  # rows of cnodes: vis0, vis1, child0, child1
+        for c in (2, 3):
+            col = cz[:, c]
+            cz[:, c] = np.where(col >= 0, col + n_nodes, col - n_leaves)
+        gn[0::4] = cz.view(np.float32)
+        gl = gl.copy()
+        li = gl.view(np.int32)
+        li[:, 0] += n_prims
+        li[:, 1] += n_prims
+        gl = li.view(np.float32)
+        ob["node"] = n_nodes if groot == 0 else -n_leaves - 1
+        geom_node[gi] = ob["node"]
+        k = gpos.shape[0]
+        p_index.append(gm["tri_offset"] + go.astype(np.int64))
+        p_object.append(np.zeros(k, np.int64))
+        p_type.append(np.full(k, PRIMITIVE_TRIANGLE, np.int64))
+        p_vis.append(np.full(k, vis_obj, np.int64))
+        p_tri.append(3 * np.arange(k, dtype=np.int64) + n_tv)
+        tv.append(gpos[go].reshape(-1, 3))
+        n_tv += 3 * k
+        node_parts.append(gn[: gn.shape[0]] if gn.shape[0] else gn)
+        leaf_parts.append(gl)
+        n_nodes += gn.shape[0]
+        n_leaves += gl.shape[0]
+        n_prims += k
+
+    def u32(parts):
+        return (np.concatenate(parts).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
+
+    prim_index, prim_object, prim_type = u32(p_index), u32(p_object), u32(p_type)
+    prim_visibility, prim_tri_index = u32(p_vis), u32(p_tri)
+    verts_all = np.concatenate(tv) if tv else np.zeros((0, 3), np.float32)
+    prim_tri_verts = np.ones((max(len(verts_all), 1), 4), dtype=np.float32)
+    prim_tri_verts[: len(verts_all), :3] = verts_all
+    # tri_vindex.w = prim_tri_index of the triangle's slot (geometry.cpp:900-905)
+    is_tri = prim_type == PRIMITIVE_TRIANGLE
+    tri_vindex[prim_index[is_tri].astype(np.int64), 3] = prim_tri_index[is_tri]
+    tri_pos_object = tri_pos
+    return dict(ntri=ntri, tri_shader_idx=tri_shader_idx, tri_smooth=tri_smooth, nodes=np.concatenate(node_parts),
+                leaves=np.concatenate(leaf_parts), root=root, prim_index=prim_index, prim_object=prim_object,
+                prim_type=prim_type, prim_visibility=prim_visibility, prim_tri_index=prim_tri_index,
+                prim_tri_verts=prim_tri_verts, tri_vindex=tri_vindex, tri_vnormal=tri_vnormal, objects=objects,
+                tri_pos_object=tri_pos_object)
+
+
+def _instance_bounds(v: np.ndarray, tfm) -> np.ndarray:
+    """Object::compute_bounds (render/object.cpp): geometry bounds transformed
+    (all 8 corners), as float32 min / max."""
+    lo, hi = v.min(0), v.max(0)
+    corners = np.array([[x, y, z] for x in (lo[0], hi[0]) for y in (lo[1], hi[1]) for z in (lo[2], hi[2])],
+                       dtype=np.float32)
+    w = np.stack([transform_point_f32(np.asarray(tfm, dtype=np.float32), c) for c in corners])
+    return np.concatenate([w.min(0), w.max(0)]).astype(np.float32)
+
+
+def build_bvh2_boxes(boxes: np.ndarray, visibility: np.ndarray, kind: np.ndarray, max_leaf: int = 8):
+    lib = native.host_lib()
+    n = boxes.shape[0]
+    bx = np.ascontiguousarray(boxes, dtype=np.float32)
+    vis = np.ascontiguousarray(visibility, dtype=np.uint32)
+    kd = np.ascontiguousarray(kind, dtype=np.int32)
+    counts = np.zeros(3, dtype=np.int64)
+    h = lib.hcb_build_boxes(n, bx.ctypes.data, vis.ctypes.data, kd.ctypes.data, max_leaf, counts.ctypes.data)
+    try:
+        nodes = np.zeros((max(int(counts[0]), 1), 4), dtype=np.float32)
+        leaves = np.zeros((max(int(counts[1]), 1), 4), dtype=np.float32)
+        order = np.zeros(n, dtype=np.int32)
+        lib.hcb_pack(h, nodes.ctypes.data, leaves.ctypes.data, order.ctypes.data)
+    finally:
+        lib.hcb_free(h)
+    return nodes[: int(counts[0])] if counts[0] else nodes[:0], leaves, order, int(counts[2])
 
 
 def f32bits_signed(x: float) -> int:

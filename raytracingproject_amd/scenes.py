@@ -147,6 +147,47 @@ def cornell_lamps(width=64, height=64, samples=16) -> sc.Scene:
     return scene
 
 
+def _tfm(translate=(0.0, 0.0, 0.0), rot_y=0.0, scale=(1.0, 1.0, 1.0), rot_x=0.0) -> np.ndarray:
+    """3x4 object-to-world transform: translate * rot_y * rot_x * scale."""
+    c, s = math.cos(rot_y), math.sin(rot_y)
+    ry = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    c, s = math.cos(rot_x), math.sin(rot_x)
+    rx = np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    m = np.zeros((3, 4))
+    m[:, :3] = ry @ rx @ np.diag(scale)
+    m[:, 3] = translate
+    return m
+
+
+def cornell_instanced(width=64, height=64, samples=16) -> sc.Scene:
+    """Cornell box whose props are instances (two-level BVH): one box geometry
+    placed three times (rotated, non-uniformly scaled), one emissive quad
+    geometry placed twice (instanced mesh lights), and a single-use instance
+    whose transform the host applies."""
+    scene = cornell_box(width, height, samples)
+    scene.meshes = scene.meshes[:5]  # walls only
+    glossy = sc.glossy((0.8, 0.75, 0.6), 0.2)
+    scene.materials = scene.materials + [glossy]
+    box_v, box_t = _box((0.0, 0.0, 0.0), (1.0, 1.0, 1.0))
+    box = sc.Mesh(box_v, box_t, shader=0)
+    scene.instances = [
+        sc.Instance(box, _tfm((185.0, 82.5, 169.0), -0.314, (165.0, 165.0, 165.0))),
+        sc.Instance(box, _tfm((368.0, 165.0, 351.0), 0.3, (165.0, 330.0, 165.0))),
+        sc.Instance(box, _tfm((420.0, 40.0, 120.0), 0.9, (60.0, 80.0, 40.0), rot_x=0.4)),
+    ]
+    lamp_v, lamp_t = _quad((-0.5, 0.0, -0.5), (-0.5, 0.0, 0.5), (0.5, 0.0, 0.5), (0.5, 0.0, -0.5))
+    lamp = sc.Mesh(lamp_v, lamp_t, shader=3)
+    scene.instances += [
+        sc.Instance(lamp, _tfm((230.0, 554.0, 280.0), 0.0, (90.0, 1.0, 90.0))),
+        sc.Instance(lamp, _tfm((340.0, 554.0, 260.0), 0.5, (60.0, 1.0, 110.0))),
+    ]
+    ev, et = _ellipsoid((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), 24, 12)
+    scene.instances.append(sc.Instance(sc.Mesh(ev, et, shader=4, smooth=True), _tfm((150.0, 300.0, 380.0), 0.2,
+                                                                                  (60.0, 45.0, 60.0))))
+    scene.name = "cornell_instanced"
+    return scene
+
+
 def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
     """BMW27-class stand-in (SURVEY.md §8(d) config BMW): ~0.7M triangles at
     detail=1.0, glossy / glass / diffuse materials, two emissive studio panels,
@@ -215,6 +256,7 @@ def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
 
 CONFIGS = {
     "cornell_lamps": cornell_lamps,
+    "cornell_instanced": cornell_instanced,
     "cornell_box": cornell_box,
     "bmw27_standin": bmw27_standin,
 }

@@ -45,7 +45,8 @@ def host_emu(libm_sincos: bool = True):
     lib.emu_render.argtypes = [vp, ci, vp, vp, vp, vp] + [ci] * 9
     lib.emu_intersect.argtypes = [vp, ci, vp, vp, vp, vp, ci, ci, vp, vp, vp]
     lib.emu_bvhw_build.restype = cl
-    lib.emu_bvhw_build.argtypes = [ci, ci, vp, cl, vp, cl, ci, vp, cl, vp, ctypes.c_char_p, ci]
+    lib.emu_bvhw_build.argtypes = [ci, ci, vp, cl, vp, cl, ci, vp, cl, vp, cl, vp, cl, vp, vp, ctypes.c_char_p, ci]
+    lib.emu_set_object_root.argtypes = [vp]
     lib.emu_set_width.argtypes = [ci]
     return lib
 
@@ -63,10 +64,13 @@ class EmuScene:
         self.c_ptrs = (ctypes.c_void_p * len(self.names))(*[a.ctypes.data for a in self.arrs])
         self.data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
         self.width = bvh_width
-        self.wide = bvhw_build(lib, ds, bvh_width, merge_prims)[0] if bvh_width > 2 else None
+        self.wide, self.object_root = None, None
+        if bvh_width > 2:
+            self.wide, _, self.object_root = bvhw_build(lib, ds, bvh_width, merge_prims, with_roots=True)
 
     def args(self):
         self.lib.emu_set_width(self.width)
+        self.lib.emu_set_object_root(None if self.object_root is None else self.object_root.ctypes.data)
         ptr = None if self.wide is None else self.wide.ctypes.data
         return (ctypes.addressof(self.data), len(self.names), self.c_names, self.c_ptrs, ptr)
 
@@ -97,21 +101,27 @@ class EmuScene:
         return buf
 
 
-def bvhw_build(lib, ds, width=4, merge_prims=0):
+def bvhw_build(lib, ds, width=4, merge_prims=0, with_roots=False):
     """Widen the scene's BVH2 exactly like the device library; returns
-    (uint32 array of 8*width words per node, depth)."""
+    (uint32 array of 8*width words per node, depth[, per-object wide roots])."""
     import numpy as np
 
     nodes = np.ascontiguousarray(ds.arrays["__bvh_nodes"], dtype=np.float32).reshape(-1)
     leaves = np.ascontiguousarray(ds.arrays["__bvh_leaf_nodes"], dtype=np.float32).reshape(-1)
-    cap = 8 * width * (len(leaves) // 4 + 2)
+    pobj = np.ascontiguousarray(ds.arrays["__prim_object"], dtype=np.uint32)
+    onode = np.ascontiguousarray(ds.arrays["__object_node"], dtype=np.uint32)
+    cap = 8 * width * (len(leaves) // 4 + 2 + len(onode))
     out = np.zeros(cap, dtype=np.uint32)
+    roots = np.zeros(max(len(onode), 1), dtype=np.int32)
     depth = ctypes.c_int(0)
     err = ctypes.create_string_buffer(256)
     n = lib.emu_bvhw_build(width, merge_prims, nodes.ctypes.data, len(nodes) // 4, leaves.ctypes.data, len(leaves) // 4,
-                           int(ds.data.bvh.root), out.ctypes.data, cap, ctypes.byref(depth), err, 256)
+                           int(ds.data.bvh.root), pobj.ctypes.data, len(pobj), onode.ctypes.data, len(onode),
+                           out.ctypes.data, cap, roots.ctypes.data, ctypes.byref(depth), err, 256)
     if n < 0:
         raise RuntimeError(err.value.decode())
+    if with_roots:
+        return out[:n].copy(), depth.value, roots
     return out[:n].copy(), depth.value
 
 

@@ -77,7 +77,12 @@ def test_closest_hit_matches_reference(case, device):
     hit &= (g["rays"][:, 7].view(np.uint32) & PATH_RAY_SHADOW_OPAQUE) == 0
     same = oi[hit, 1] == ref_i[hit, 1]
     assert same.mean() >= 0.995, (name, same.mean())
-    assert np.array_equal(of[hit][same].view(np.uint32), ref_f[hit][same].view(np.uint32)), name
+    a, b = of[hit][same], ref_f[hit][same]
+    assert np.array_equal(a[:, 1:].view(np.uint32), b[:, 1:].view(np.uint32)), name
+    if ds.info["instanced_objects"] == 0:
+        assert np.array_equal(a[:, 0].view(np.uint32), b[:, 0].view(np.uint32)), name
+    else:  # t scaled through instances in another order (tests/test_bvh_wide.py)
+        assert np.all(np.abs(a[:, 0] - b[:, 0]) <= 4e-7 * np.abs(b[:, 0])), name
     t, tr = of[hit][~same, 0], ref_f[hit][~same, 0]
     assert np.all(np.abs(t - tr) <= 1e-6 * np.abs(tr)), name
 

@@ -27,8 +27,13 @@ extern "C" long emu_bvhw_build(int width,
                                const float *leaves2,
                                long n_leaves2,
                                int root,
+                               const uint32_t *prim_object,
+                               long n_prims,
+                               const uint32_t *object_node,
+                               long n_objects,
                                uint32_t *out,
                                long out_cap,
+                               int *object_root,
                                int *depth,
                                char *err_out,
                                int err_len)
@@ -40,6 +45,10 @@ extern "C" long emu_bvhw_build(int width,
   col.n_nodes2 = (size_t)n_nodes2;
   col.leaves2 = leaves2;
   col.n_leaves2 = (size_t)n_leaves2;
+  col.prim_object = prim_object;
+  col.n_prims = (size_t)n_prims;
+  col.object_node = object_node;
+  col.n_objects = (size_t)n_objects;
   if (!col.run(root)) {
     snprintf(err_out, err_len, "%s", col.error.c_str());
     return -1;
@@ -49,11 +58,19 @@ extern "C" long emu_bvhw_build(int width,
     return -1;
   }
   memcpy(out, col.out.data(), col.out.size() * 4);
+  memcpy(object_root, col.object_root.data(), col.object_root.size() * 4);
   *depth = col.max_depth;
   return (long)col.out.size();
 }
 
 static int g_width = 2;
+
+static const int *g_object_root = nullptr;
+
+extern "C" void emu_set_object_root(const int *roots)
+{
+  g_object_root = roots;
+}
 
 static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char **names, const void **ptrs,
                      const void *bvhw)
@@ -68,6 +85,7 @@ static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char *
 #undef CY_BIND
   }
   kg->bvhw_nodes = bvhw;
+  kg->bvhw_object_root = g_object_root;
   kg->tri_index_identity = 0;
 }
 
@@ -163,6 +181,7 @@ extern "C" int emu_render(const void *data,
   emu_bind(&kg, data, n_arrays, names, ptrs, bvhw);
   hc_float4 rec[12];
   int isect_type = 0;
+  int isect_object = OBJECT_NONE;
   hc_uint4 s0, s1;
   uint item_slot = 0;
   CyPathBuffers b;
@@ -170,6 +189,7 @@ extern "C" int emu_render(const void *data,
   b.ray_D = &rec[1];
   b.isect = &rec[2];
   b.isect_type = &isect_type;
+  b.isect_object = &isect_object;
   b.state0 = &s0;
   b.state1 = &s1;
   b.state2 = &rec[3];
@@ -217,6 +237,7 @@ extern "C" int emu_render(const void *data,
       if (hit) {
         rec[2] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
         isect_type = isect.type;
+        isect_object = isect.object;
       }
       else {
         isect_type = 0;
