@@ -28,16 +28,16 @@ template<int W> struct LdsStack {
   static constexpr int ints = W > 2 ? 2 * CY_LDS_STACKW * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
 };
 
-template<int W, bool any_hit>
+template<int W, bool any_hit, bool INST = true>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
                                                uint *n_tris, int *lds)
 {
   if constexpr (W > 2) {
-    return bvhw_intersect<W, any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+    return bvhw_intersect<W, any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
   }
   else {
-    return bvh2_intersect<any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+    return bvh2_intersect<any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
   }
 }
 
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
   }
 }
 
-template<bool STATS, int W>
+template<bool STATS, int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  const int *queue,
@@ -95,13 +95,15 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
     CyIsect isect;
     bool hit = false;
     if (scene_intersect_valid(&ray)) {
-      hit = scene_traverse<W, false>(&kg, &ray, visibility, &isect, err,
+      hit = scene_traverse<W, false, INST>(&kg, &ray, visibility, &isect, err,
                                         STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     if (hit) {
       cy_st(&b.isect[slot], mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim)));
       cy_st(&b.isect_type[slot], isect.type);
-      cy_st(&b.isect_object[slot], isect.object);
+      if (INST) {
+        cy_st(&b.isect_object[slot], isect.object);
+      }
     }
     else {
       cy_st(&b.isect_type[slot], 0);
@@ -114,7 +116,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
   }
 }
 
-template<bool STATS, int W>
+template<bool STATS, int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
     bool blocked = false;
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
-      blocked = scene_traverse<W, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
+      blocked = scene_traverse<W, true, INST>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
                                            STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
     const hc_float4 sl = cy_ld(&b.shadow_L[slot]);
@@ -230,6 +232,29 @@ __global__ void k_test_camera(CyGlobals kg, const int *xys, float *out, int n)
   o[7] = as_float(rng_hash);
 }
 
+/* Kernel instance for (traversal counters, BVH width, instancing). */
+struct ClosestK {
+  template<bool S, int W, bool I> static constexpr auto fn()
+  {
+    return k_intersect_closest<S, W, I>;
+  }
+};
+struct ShadowK {
+  template<bool S, int W, bool I> static constexpr auto fn()
+  {
+    return k_intersect_shadow<S, W, I>;
+  }
+};
+template<class K, bool S, bool I> static auto pick_width(int W)
+{
+  return W == 8 ? K::template fn<S, 8, I>() : W == 4 ? K::template fn<S, 4, I>() : K::template fn<S, 2, I>();
+}
+template<class K> static auto pick_kernel(bool stats, int W, bool inst)
+{
+  return stats ? (inst ? pick_width<K, true, true>(W) : pick_width<K, true, false>(W))
+               : (inst ? pick_width<K, false, true>(W) : pick_width<K, false, false>(W));
+}
+
 /* ------------------------------------------------------------------------- */
 /* Host side                                                                   */
 
@@ -287,6 +312,7 @@ struct hipcy_device {
   size_t bvhw_capacity = 0;
   int bvhw_depth = 0;
   int *bvhw_object_root = nullptr; /* inside bvhw, after the nodes */
+  int have_instancing = 1;         /* some object without SD_OBJECT_TRANSFORM_APPLIED */
   int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
@@ -331,6 +357,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   kg->bvhw_nodes = (dev->bvh_width > 2) ? dev->bvhw : nullptr;
   kg->bvhw_object_root = (dev->bvh_width > 2) ? dev->bvhw_object_root : nullptr;
   kg->tri_index_identity = (dev->bvh_width > 2) ? dev->tri_index_identity : 0;
+  kg->have_instancing = dev->have_instancing;
   return true;
 }
 
@@ -750,6 +777,21 @@ int hipcy_load_kernels(hipcy_device *dev)
       return set_error(dev, std::string("load_kernels: array not bound: ") + r);
     }
   }
+  /* instanced geometry present? (selects the traversal kernels with instance
+   * leaves and the instance paths of shading) */
+  {
+    auto of = dev->globals.find("__object_flag");
+    std::vector<uint32_t> flags(of->second.bytes / 4);
+    if (!flags.empty()) {
+      HIP_CHECK(dev, hipMemcpy(flags.data(), (const void *)of->second.ptr, of->second.bytes, hipMemcpyDeviceToHost));
+    }
+    dev->have_instancing = 0;
+    for (uint32_t f : flags) {
+      if (!(f & SD_OBJECT_TRANSFORM_APPLIED)) {
+        dev->have_instancing = 1;
+      }
+    }
+  }
   /* scene-preparation step of the device: widen the BVH now, not in the first render */
   return ensure_bvhw(dev);
 }
@@ -862,10 +904,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     HIP_CHECK(dev, hipEventRecord(p.a, s));
   }
   {
-    auto kfn = counters ? (W == 8 ? k_intersect_closest<true, 8> : W == 4 ? k_intersect_closest<true, 4>
-                                                                   : k_intersect_closest<true, 2>)
-                        : (W == 8 ? k_intersect_closest<false, 8> : W == 4 ? k_intersect_closest<false, 4>
-                                                                   : k_intersect_closest<false, 2>);
+    auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0);
     hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.q[qa], ln.cnt + qa, err, dev->stats_dev);
   }
   if (prof) {
@@ -877,10 +916,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }
   {
-    auto kfn = counters ? (W == 8 ? k_intersect_shadow<true, 8> : W == 4 ? k_intersect_shadow<true, 4>
-                                                                  : k_intersect_shadow<true, 2>)
-                        : (W == 8 ? k_intersect_shadow<false, 8> : W == 4 ? k_intersect_shadow<false, 4>
-                                                                  : k_intersect_shadow<false, 2>);
+    auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0);
     hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
                        ln.cnt + qb, err, dev->stats_dev);
   }

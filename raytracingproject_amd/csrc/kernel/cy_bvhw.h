@@ -112,7 +112,7 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
   }
 }
 
-template<int W, bool any_hit>
+template<int W, bool any_hit, bool INST = true>
 CY_FN bool bvhw_intersect(const CyGlobals *kg,
                           const CyRay *ray,
                           uint visibility,
@@ -205,7 +205,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       n_leaves++;
       const int packed = ~code;
       int prim_addr = packed >> 4;
-      if ((packed & 15) == 0) {
+      if (INST && (packed & 15) == 0) {
         /* instance leaf (count 0, index = object): enter the object's BVH in
          * object space (bvh_instance_push); a -inf stack entry marks the exit */
         object = prim_addr;
@@ -217,6 +217,10 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
         stack.set(sp++, 0, -CY_INF);
         code = kg->bvhw_object_root[object];
         continue;
+      }
+      if (!INST && (packed & 15) == 0) {
+        cy_set_error(err, CY_ERR_FEATURE, 1); /* instance leaf in a kernel built without instancing */
+        return false;
       }
       const int prim_end = prim_addr + (packed & 15);
       const bool ident = kg->tri_index_identity != 0;
@@ -261,7 +265,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       while (sp > 0) {
         float et;
         stack.get(--sp, &code, &et);
-        if (et == -CY_INF) {
+        if (INST && et == -CY_INF) {
           /* instance exit (bvh_instance_pop) */
           isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
           object = OBJECT_NONE;

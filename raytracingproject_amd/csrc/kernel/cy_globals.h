@@ -50,6 +50,9 @@ typedef struct CyGlobals {
   /* 1 when __prim_tri_index[i] == 3 * i for every primitive (checked when the
    * BVH is widened): triangle vertices are then read without the indirection */
   int tri_index_identity;
+  /* 1 when some object keeps its own transform (instanced geometry): enables
+   * the instance paths of shading and light sampling (uniform branch) */
+  int have_instancing;
 } CyGlobals;
 
 #endif /* CY_GLOBALS_H */

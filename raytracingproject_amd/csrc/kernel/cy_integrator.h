@@ -495,7 +495,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     isect.u = is4.y;
     isect.v = is4.z;
     isect.prim = as_int(is4.w);
-    isect.object = cy_ld(&b->isect_object[slot]);
+    isect.object = kg->have_instancing ? cy_ld(&b->isect_object[slot]) : OBJECT_NONE;
     isect.type = type;
 
     CySD sd;

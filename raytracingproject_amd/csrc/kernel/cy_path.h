@@ -267,7 +267,7 @@ CY_FN float bvh_instance_pop(
   return t;
 }
 
-template<bool any_hit>
+template<bool any_hit, bool INST = true>
 CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           const CyRay *ray,
                           uint visibility,
@@ -394,6 +394,10 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
             cy_set_error(err, CY_ERR_PRIMITIVE, type);
           }
         }
+        else if (!INST) {
+          cy_set_error(err, CY_ERR_FEATURE, 1); /* instance leaf in a kernel built without instancing */
+          return false;
+        }
         else {
           /* instance push (bvh_traversal.h:190-205) */
           object = (int)kg->__prim_object[-prim_addr - 1];
@@ -409,7 +413,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
       }
     } while (node_addr != ENTRYPOINT_SENTINEL);
 
-    if (stack_ptr >= 0) {
+    if (INST && stack_ptr >= 0) {
       /* instance pop (bvh_traversal.h:209-222) */
       isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
       object = OBJECT_NONE;
@@ -1544,7 +1548,7 @@ CY_FN float triangle_light_pdf_area(const CyGlobals *kg, cfloat3 Ng, cfloat3 I, 
 CY_FN bool triangle_world_space_vertices(const CyGlobals *kg, int object, int prim, cfloat3 V[3])
 {
   triangle_verts(kg, prim, V);
-  if (!(kg->__object_flag[object] & SD_OBJECT_TRANSFORM_APPLIED)) {
+  if (kg->have_instancing && !(kg->__object_flag[object] & SD_OBJECT_TRANSFORM_APPLIED)) {
     const struct cy_tfm *tfm = object_tfm(kg, object);
     V[0] = transform_point(tfm, V[0]);
     V[1] = transform_point(tfm, V[1]);

@@ -86,6 +86,7 @@ static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char *
   }
   kg->bvhw_nodes = bvhw;
   kg->bvhw_object_root = g_object_root;
+  kg->have_instancing = 1; /* generic: the instance paths are always enabled on the host */
   kg->tri_index_identity = 0;
 }
 
