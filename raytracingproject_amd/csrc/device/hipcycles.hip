@@ -24,6 +24,12 @@
 
 /* Traversal stack in LDS: BVH2 keeps CY_LDS_STACK node addresses per thread,
  * the wide BVHs CY_LDS_STACKW (node, entry distance) pairs. */
+/* Minimum waves per SIMD the traversal kernels are register-allocated for
+ * (amdgpu_waves_per_eu); with the LDS stack it sets their occupancy. */
+#ifndef CY_TRAV_MIN_WAVES
+#  define CY_TRAV_MIN_WAVES 6
+#endif
+
 template<int W> struct LdsStack {
   static constexpr int ints = W > 2 ? 2 * CY_LDS_STACKW * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
 };
@@ -70,7 +76,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
 }
 
 template<bool STATS, int W, bool INST>
-__global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  const int *queue,
                                                                  const uint *counter,
@@ -117,7 +123,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_closest(CyGlobals kg,
 }
 
 template<bool STATS, int W, bool INST>
-__global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow(CyGlobals kg,
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
                                                                 const int *shadow_queue,

@@ -32,7 +32,7 @@
 #include "cy_path.h"
 
 #ifndef CY_LDS_STACKW
-#  define CY_LDS_STACKW 16
+#  define CY_LDS_STACKW 8
 #endif
 #define CY_BVHW_STACK 96
 
