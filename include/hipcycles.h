@@ -30,6 +30,8 @@
  *   hipcy_set_bvh_width / _leaf_merge        (device options) traverse the bound BVH2 as is, or
  *                                            the 4/8-wide BVH the device widens it into, like
  *                                            BVH::pack_nodes/widen_children_nodes bvh/bvh.cpp:149-176
+ *   hipcy_film_convert                       device_cuda_impl.cpp:1954-2017 CUDADevice::film_convert
+ *                                            (DeviceTask FILM_CONVERT; kernel/kernel_film.h)
  *   hipcy_intersect / hipcy_camera_rays      test entry points (scene_intersect, bvh/bvh.h:154;
  *                                            kernel_path_trace_setup, kernel_path_common.h:21)
  */
@@ -122,6 +124,15 @@ int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
 /* flags: bit 0 = per-kernel HIP-event timings (kernels then run on one stream,
  * without overlap, so each launch is timed alone), bit 1 = traversal counters. */
 int hipcy_set_profiling(hipcy_device *dev, int flags);
+
+/* FILM_CONVERT task: the display pass (KernelFilm.display_pass_*) of pixels
+ * (x..x+w-1, y..y+h-1) of `buffer` (pass_stride floats per pixel) is converted
+ * to sRGB uchar4 into rgba_byte, or (rgba_byte == 0) to 4 halfs into rgba_half,
+ * at pixel index offset + x + y*stride of either; sample_scale = 1 / samples
+ * rendered (the reference passes 1/(task.sample+1)).  Halfs follow the CPU
+ * device's truncating conversion (util_half.h:80-118). */
+int hipcy_film_convert(hipcy_device *dev, uint64_t buffer, uint64_t rgba_byte, uint64_t rgba_half,
+                       float sample_scale, int x, int y, int w, int h, int offset, int stride);
 
 /* rays: n x 8 floats (P.xyz, D.xyz, t, visibility bits) in device memory;
  * out_f: n x 3 (t, u, v); out_i: n x 4 (hit, prim, object, type).

@@ -146,8 +146,16 @@ class HIPCyclesDevice : public Device {
   /* device.h:403-405 — one worker thread per device, like CUDADevice::task_add */
   void task_add(DeviceTask &task) override
   {
+    if (task.type == DeviceTask::FILM_CONVERT) {
+      /* on the calling thread, like CUDADevice::task_add (device_cuda_impl.cpp:2427-2430)
+       * -> film_convert (:1954-2017) */
+      check(hipcy_film_convert(dev_, (uint64_t)task.buffer, (uint64_t)task.rgba_byte, (uint64_t)task.rgba_half,
+                               1.0f / (task.sample + 1), task.x, task.y, task.w, task.h, task.offset,
+                               task.stride));
+      return;
+    }
     if (task.type != DeviceTask::RENDER) {
-      set_error("HIP device: only RENDER tasks are implemented");
+      set_error("HIP device: only RENDER and FILM_CONVERT tasks are implemented");
       return;
     }
     task_pool_.push([=] {

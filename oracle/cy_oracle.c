@@ -296,3 +296,102 @@ void cyo_intersect_brute_instanced(const float *prim_tri_verts, const uint32_t *
     out_i[4 * r + 3] = best >= 0 ? 1 : 0;
   }
 }
+
+
+/* ---- film convert (kernel_film.h) ---------------------------------------- */
+
+static float f_min(float a, float b) { return (a < b) ? a : b; }
+static float f_max(float a, float b) { return (a > b) ? a : b; }
+static float f_saturate(float a) { return f_min(f_max(a, 0.0f), 1.0f); }
+
+/* util_color.h:77-83; powf is libm's, as in the reference */
+static float srgb(float c)
+{
+  if (c < 0.0031308f) {
+    return (c < 0.0f) ? 0.0f : c * 12.92f;
+  }
+  return 1.055f * powf(c, 1.0f / 2.4f) - 0.055f;
+}
+
+/* util_half.h:80-118 (SSE2 branch of float4_store_half): truncating conversion */
+static uint16_t to_half(float v, float scale)
+{
+  float f = v * scale;
+  f = (f > 0.0f) ? ((f < 65504.0f) ? f : 65504.0f) : 0.0f;
+  int32_t x;
+  memcpy(&x, &f, 4);
+  const int32_t absolute = x & 0x7FFFFFFF;
+  const int32_t Z = (int32_t)((uint32_t)absolute + 0xC8000000u);
+  const int32_t result = (absolute < 0x38800000) ? 0 : Z;
+  return (uint16_t)((result >> 13) & 0x7FFF);
+}
+
+void cyo_film_convert(const int32_t film[6], float exposure, const float *buffer, void *rgba, float sample_scale,
+                      int x, int y, int w, int h, int offset, int stride, int half)
+{
+  const int pass_stride = film[0], dstride = film[1], dcomp = film[2], ddiv = film[3];
+  const int use_exposure = film[4], use_alpha = film[5];
+  const int use_scale = (ddiv == -1);
+  for (int py = y; py < y + h; py++) {
+    for (int px = x; px < x + w; px++) {
+      const int index = offset + px + py * stride;
+      float r[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      /* film_get_pass_result (kernel_film.h:19-63) */
+      const float *in = buffer + dstride + (long)index * pass_stride;
+      if (dcomp == 4) {
+        const float alpha = use_scale ? (use_alpha ? in[3] : 1.0f / sample_scale) : 1.0f;
+        r[0] = in[0];
+        r[1] = in[1];
+        r[2] = in[2];
+        r[3] = alpha;
+        if (ddiv != -1) {
+          const float *dv = buffer + ddiv + (long)index * pass_stride;
+          float q[3];
+          for (int c = 0; c < 3; c++) {
+            q[c] = (dv[c] != 0.0f) ? r[c] / dv[c] : 0.0f;
+          }
+          if (dv[0] == 0.0f) {
+            if (dv[1] == 0.0f) { q[0] = q[2]; q[1] = q[2]; }
+            else if (dv[2] == 0.0f) { q[0] = q[1]; q[2] = q[1]; }
+            else q[0] = 0.5f * (q[1] + q[2]);
+          }
+          else if (dv[1] == 0.0f) {
+            if (dv[2] == 0.0f) { q[1] = q[0]; q[2] = q[0]; }
+            else q[1] = 0.5f * (q[0] + q[2]);
+          }
+          else if (dv[2] == 0.0f) {
+            q[2] = 0.5f * (q[0] + q[1]);
+          }
+          r[0] = q[0];
+          r[1] = q[1];
+          r[2] = q[2];
+        }
+        if (use_exposure) {
+          r[0] *= exposure;
+          r[1] *= exposure;
+          r[2] *= exposure;
+          r[3] *= 1.0f;
+        }
+      }
+      else if (dcomp == 1) {
+        r[0] = r[1] = r[2] = in[0];
+        r[3] = 1.0f / sample_scale;
+      }
+      const float scale = use_scale ? sample_scale : 1.0f;
+      if (half) {
+        uint16_t *o = (uint16_t *)rgba + (long)index * 4;
+        for (int c = 0; c < 4; c++) {
+          o[c] = to_half(r[c], scale);
+        }
+      }
+      else {
+        /* film_map + film_float_to_byte (kernel_film.h:65-92) */
+        const float m[4] = {srgb(r[0] * scale), srgb(r[1] * scale), srgb(r[2] * scale), f_saturate(r[3] * scale)};
+        uint8_t *o = (uint8_t *)rgba + (long)index * 4;
+        for (int c = 0; c < 4; c++) {
+          o[c] = (uint8_t)(f_saturate(m[c]) * 255.0f);
+        }
+      }
+    }
+  }
+}

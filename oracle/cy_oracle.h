@@ -34,4 +34,13 @@ void cyo_intersect_brute_instanced(const float *prim_tri_verts, const uint32_t *
                                    const int32_t *obj_first, const int32_t *obj_count, const float *rays,
                                    int n, int any_hit, float *out_f, int32_t *out_i);
 
+/* Film convert of the combined display pass (kernel/kernel_film.h:19-141,
+ * util/util_color.h:77-83, util/util_half.h:80-118 SSE2 branch): pixels
+ * (x, y, w, h) of buffer (pass_stride floats per pixel) at index
+ * offset + x + y*stride into rgba (4 bytes, or 4 half bit patterns, per pixel).
+ * film: pass_stride, display_pass_stride, display_pass_components,
+ * display_divide_pass_stride, use_display_exposure, use_display_pass_alpha. */
+void cyo_film_convert(const int32_t film[6], float exposure, const float *buffer, void *rgba, float sample_scale,
+                      int x, int y, int w, int h, int offset, int stride, int half);
+
 #endif

@@ -41,6 +41,7 @@ def ref_lib():
         lib.cref_global_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
         lib.cref_render.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci, ci]
         lib.cref_intersect.argtypes = [vp, ci, vp, vp, vp]
+        lib.cref_film_convert.argtypes = [vp, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
         lib.cref_camera_rays.argtypes = [vp, ci, vp, vp]
         lib.cref_rng_1d.argtypes = [vp, ci, vp, vp]
         lib.cref_sobol_directions.argtypes = [vp, ci]
@@ -69,6 +70,7 @@ def oracle_lib():
         lib.cyo_path_rng_1d.argtypes = [vp, u32, ci, ci]
         lib.cyo_ray_offset.argtypes = [vp, vp, vp]
         lib.cyo_intersect_brute.argtypes = [vp, vp, ci, vp, ci, ci, vp, vp]
+        lib.cyo_film_convert.argtypes = [vp, ctypes.c_float, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
         lib.cyo_intersect_brute_instanced.argtypes = [vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, ci, ci, vp, vp]
         _orc = lib
     return _orc
@@ -122,6 +124,16 @@ class RefKernel:
         oi = np.zeros((n, 4), dtype=np.int32)
         self.lib.cref_intersect(self.h, n, rays.ctypes.data, of.ctypes.data, oi.ctypes.data)
         return of, oi
+
+    def film_convert(self, buffer: np.ndarray, sample_scale: float, half: bool):
+        """Full-frame film convert of an (H, W, pass_stride) float buffer:
+        uint8 (H, W, 4) or float16 bit patterns as uint16 (H, W, 4)."""
+        buffer = np.ascontiguousarray(buffer, dtype=np.float32)
+        h, w = buffer.shape[:2]
+        out = np.zeros((h, w, 4), dtype=np.uint16 if half else np.uint8)
+        self.lib.cref_film_convert(self.h, out.ctypes.data, buffer.ctypes.data, sample_scale, 0, 0, w, h, 0, w,
+                                   1 if half else 0)
+        return out
 
     def camera_rays(self, xys: np.ndarray):
         xys = np.ascontiguousarray(xys, dtype=np.int32)

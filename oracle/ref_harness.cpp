@@ -334,4 +334,25 @@ long cref_offsetof(const char *sname, const char *fname)
   return -1;
 }
 
+/* FILM_CONVERT task on the CPU device (device/device_cpu.cpp film_convert ->
+ * kernel_cpu_convert_to_byte / _half_float, kernels/cpu/kernel_cpu_impl.h:103-132):
+ * every pixel of (x, y, w, h) at index offset + x + y*stride of a full-frame rgba. */
+void cref_film_convert(void *h, void *rgba, float *buffer, float sample_scale, int x, int y, int w,
+                       int hgt, int offset, int stride, int half)
+{
+  RefContext *ctx = (RefContext *)h;
+  KernelGlobals kg = thread_globals(ctx->kg);
+  for (int py = y; py < y + hgt; py++) {
+    for (int px = x; px < x + w; px++) {
+      if (half) {
+        kernel_cpu_convert_to_half_float(&kg, (uchar4 *)rgba, buffer, sample_scale, px, py, offset, stride);
+      }
+      else {
+        kernel_cpu_convert_to_byte(&kg, (uchar4 *)rgba, buffer, sample_scale, px, py, offset, stride);
+      }
+    }
+  }
+  thread_globals_free(kg);
+}
+
 }  // extern "C"

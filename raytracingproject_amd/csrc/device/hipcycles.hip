@@ -238,6 +238,114 @@ __global__ void k_test_camera(CyGlobals kg, const int *xys, float *out, int n)
   o[7] = as_float(rng_hash);
 }
 
+/* Film convert (kernel/kernel_film.h, kernels/cuda/kernel.cu:156-178): one
+ * thread per pixel of the (w x h) rectangle; the parity target is the CPU
+ * device, so half output uses its truncating float4_store_half (util_half.h:80-118)
+ * rather than CUDA's round-to-nearest __float2half. */
+struct CyFilm {
+  int pass_stride, display_pass_stride, display_pass_components, display_divide_pass_stride;
+  int use_display_exposure, use_display_pass_alpha;
+  float exposure;
+};
+
+__device__ __forceinline__ ushort film_half(float v, float scale)
+{
+  float f = v * scale;
+  f = (f > 0.0f) ? ((f < 65504.0f) ? f : 65504.0f) : 0.0f;
+  const int x = (int)as_uint(f);
+  const int absolute = x & 0x7FFFFFFF;
+  const int Z = (int)((uint)absolute + 0xC8000000u);
+  const int result = (absolute < 0x38800000) ? 0 : Z;
+  return (ushort)((result >> 13) & 0x7FFF);
+}
+
+template<bool HALF>
+__global__ void __launch_bounds__(CY_BLOCK) k_film_convert(CyFilm film, const float *buffer, void *rgba,
+                                                            float sample_scale, int sx, int sy, int sw, int sh,
+                                                            int offset, int stride)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= sw * sh) {
+    return;
+  }
+  const int x = sx + i % sw, y = sy + i / sw;
+  const int index = offset + x + y * stride;
+  const bool use_scale = film.display_divide_pass_stride == -1;
+  /* film_get_pass_result (kernel_film.h:19-63) */
+  float r[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const float *in = buffer + film.display_pass_stride + (size_t)index * film.pass_stride;
+  if (film.display_pass_components == 4) {
+    const hc_float4 v = *(const hc_float4 *)in;
+    r[0] = v.x;
+    r[1] = v.y;
+    r[2] = v.z;
+    r[3] = use_scale ? (film.use_display_pass_alpha ? v.w : 1.0f / sample_scale) : 1.0f;
+    if (film.display_divide_pass_stride != -1) {
+      /* safe_divide_even_color (util_math.h:525-560) */
+      const float *dv = buffer + film.display_divide_pass_stride + (size_t)index * film.pass_stride;
+      float q[3];
+      for (int c = 0; c < 3; c++) {
+        q[c] = (dv[c] != 0.0f) ? r[c] / dv[c] : 0.0f;
+      }
+      if (dv[0] == 0.0f) {
+        if (dv[1] == 0.0f) {
+          q[0] = q[2];
+          q[1] = q[2];
+        }
+        else if (dv[2] == 0.0f) {
+          q[0] = q[1];
+          q[2] = q[1];
+        }
+        else {
+          q[0] = 0.5f * (q[1] + q[2]);
+        }
+      }
+      else if (dv[1] == 0.0f) {
+        if (dv[2] == 0.0f) {
+          q[1] = q[0];
+          q[2] = q[0];
+        }
+        else {
+          q[1] = 0.5f * (q[0] + q[2]);
+        }
+      }
+      else if (dv[2] == 0.0f) {
+        q[2] = 0.5f * (q[0] + q[1]);
+      }
+      r[0] = q[0];
+      r[1] = q[1];
+      r[2] = q[2];
+    }
+    if (film.use_display_exposure) {
+      r[0] = r[0] * film.exposure;
+      r[1] = r[1] * film.exposure;
+      r[2] = r[2] * film.exposure;
+    }
+  }
+  else if (film.display_pass_components == 1) {
+    r[0] = r[1] = r[2] = in[0];
+    r[3] = 1.0f / sample_scale;
+  }
+  const float scale = use_scale ? sample_scale : 1.0f;
+  if (HALF) {
+    ushort4 o;
+    o.x = film_half(r[0], scale);
+    o.y = film_half(r[1], scale);
+    o.z = film_half(r[2], scale);
+    o.w = film_half(r[3], scale);
+    ((ushort4 *)rgba)[index] = o;
+  }
+  else {
+    /* film_map + film_float_to_byte (kernel_film.h:65-92) */
+    uchar4 o;
+    o.x = (uchar)(saturate(color_linear_to_srgb(r[0] * scale)) * 255.0f);
+    o.y = (uchar)(saturate(color_linear_to_srgb(r[1] * scale)) * 255.0f);
+    o.z = (uchar)(saturate(color_linear_to_srgb(r[2] * scale)) * 255.0f);
+    o.w = (uchar)(saturate(saturate(r[3] * scale)) * 255.0f);
+    ((uchar4 *)rgba)[index] = o;
+  }
+}
+
 /* Kernel instance for (traversal counters, BVH width, instancing). */
 struct ClosestK {
   template<bool S, int W, bool I> static constexpr auto fn()
@@ -1159,6 +1267,46 @@ int hipcy_camera_rays(hipcy_device *dev, uint64_t xys, uint64_t out, int n)
   build_globals(dev, &kg);
   hipLaunchKernelGGL(k_test_camera, dim3((n + 255) / 256), dim3(256), 0, dev->stream, kg,
                      (const int *)xys, (float *)out, n);
+  HIP_CHECK(dev, hipGetLastError());
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return 0;
+}
+
+int hipcy_film_convert(hipcy_device *dev, uint64_t buffer, uint64_t rgba_byte, uint64_t rgba_half,
+                       float sample_scale, int x, int y, int w, int h, int offset, int stride)
+{
+  if (!dev->error.empty()) {
+    return -1;
+  }
+  if (!dev->have_data) {
+    return set_error(dev, "film_convert: KernelData not uploaded");
+  }
+  if (!buffer || (!rgba_byte && !rgba_half) || w < 0 || h < 0) {
+    return set_error(dev, "film_convert: invalid arguments");
+  }
+  if (w == 0 || h == 0) {
+    return 0;
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  const hc_KernelData &d = dev->data_host;
+  CyFilm film;
+  film.pass_stride = d.film.pass_stride;
+  film.display_pass_stride = d.film.display_pass_stride;
+  film.display_pass_components = d.film.display_pass_components;
+  film.display_divide_pass_stride = d.film.display_divide_pass_stride;
+  film.use_display_exposure = d.film.use_display_exposure;
+  film.use_display_pass_alpha = d.film.use_display_pass_alpha;
+  film.exposure = d.film.exposure;
+  const long n = (long)w * h;
+  dim3 grid((unsigned)((n + CY_BLOCK - 1) / CY_BLOCK)), block(CY_BLOCK);
+  if (rgba_half) {
+    hipLaunchKernelGGL(k_film_convert<true>, grid, block, 0, dev->stream, film, (const float *)buffer,
+                       (void *)rgba_half, sample_scale, x, y, w, h, offset, stride);
+  }
+  else {
+    hipLaunchKernelGGL(k_film_convert<false>, grid, block, 0, dev->stream, film, (const float *)buffer,
+                       (void *)rgba_byte, sample_scale, x, y, w, h, offset, stride);
+  }
   HIP_CHECK(dev, hipGetLastError());
   HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
   return 0;

@@ -173,6 +173,29 @@ class HIPDevice:
             buf.free()
         return out
 
+    # ---- FILM_CONVERT task ------------------------------------------------
+    def film_convert(self, buffer: np.ndarray, sample_scale: float, half: bool = False,
+                     tile=None) -> np.ndarray:
+        """Convert a full-frame float render buffer [H, W, pass_stride] to display
+        pixels like CUDADevice::film_convert (device_cuda_impl.cpp:1954-2017):
+        uint8 sRGB [H, W, 4], or half bit patterns as uint16 [H, W, 4]."""
+        buffer = np.ascontiguousarray(buffer, dtype=np.float32)
+        H, W = buffer.shape[:2]
+        x, y, w, h = tile if tile is not None else (0, 0, W, H)
+        out = np.zeros((H, W, 4), dtype=np.uint16 if half else np.uint8)
+        d_b = self.mem_alloc(buffer.nbytes)
+        d_o = self.mem_alloc(out.nbytes)
+        try:
+            d_b.copy_to_device(buffer)
+            d_o.copy_to_device(out)
+            self._check(self.lib.hipcy_film_convert(self.h, d_b.ptr, 0 if half else d_o.ptr, d_o.ptr if half else 0,
+                                                    float(sample_scale), x, y, w, h, 0, W))
+            d_o.copy_from_device(out)
+        finally:
+            d_b.free()
+            d_o.free()
+        return out
+
     # ---- test entry points ------------------------------------------------
     def intersect(self, rays: np.ndarray, any_hit: bool = False):
         rays = np.ascontiguousarray(rays, dtype=np.float32)

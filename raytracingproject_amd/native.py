@@ -93,6 +93,9 @@ DEVICE_SYMBOLS = {
     "hipcy_set_bvh_leaf_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_slots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "hipcy_intersect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),
+    "hipcy_film_convert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int]),
     "hipcy_camera_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
 }
 

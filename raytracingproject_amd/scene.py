@@ -640,6 +640,12 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.pass_combined = 0
     kf.pass_alpha_threshold = 0.5
     kf.filter_table_offset = 0
+    # display pass = combined (film.cpp:392, 419-423, 591-598)
+    kf.display_pass_stride = 0
+    kf.display_pass_components = 4
+    kf.display_divide_pass_stride = -1
+    kf.use_display_exposure = 1 if kf.exposure != 1.0 else 0
+    kf.use_display_pass_alpha = 1
     lookup = filter_table(scene.filter_type, scene.filter_width)
 
     # --- camera

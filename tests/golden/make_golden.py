@@ -10,8 +10,10 @@ tests/parity_cases.py it stores, in tests/golden/<case>.npz:
   rays / hit_f / hit_i / shadow_i   reference scene_intersect results
   cam_xys / cam_out                 reference kernel_path_trace_setup rays
   rng_q / rng_out                   reference path_rng_1D values
+  film_byte / film_half             reference film convert of that buffer
 and, shared by all cases:
   primitives.npz    reference hash_uint2 and ray_offset on random + edge inputs
+  film.npz          reference film convert (byte, half) of synthetic edge buffers
   abi_layout.json   sizeof/offsetof of every device-data struct field in the
                     reference headers (kernel/kernel_types.h)
 The fixtures are data (inputs + expected outputs); no reference source is kept.
@@ -78,8 +80,39 @@ def make_primitives():
         json.dump(layout, f, indent=1, sort_keys=True)
 
 
+def film_buffers(seed=11, h=24, w=40):
+    """Synthetic combined-pass buffers covering the film-convert edge cases:
+    negatives, zeros, the sRGB knee (0.0031308), values above 1 and above the
+    half range, alpha above the sample count."""
+    rng = np.random.default_rng(seed)
+    b = rng.uniform(-0.5, 3.0, (h, w, 4)).astype(np.float32) * np.float32(8.0)
+    flat = b.reshape(-1, 4)
+    edge = np.array([0.0, -0.0, -1.0, 0.0031308 * 8, 0.0031307 * 8, 0.0031309 * 8, 1e-8, 8.0, 8.0000005,
+                     7.9999995, 1e5, 7e5, 1e30, 2.5, 4.0, 12.0], dtype=np.float32)
+    flat[: len(edge) * 4 // 4, 0] = edge
+    flat[: len(edge), 1] = edge[::-1]
+    flat[: len(edge), 3] = np.linspace(0, 20, len(edge), dtype=np.float32)
+    return b
+
+
+def make_film():
+    """Film convert (byte and half) of the synthetic buffers by the reference
+    kernel, with and without display exposure."""
+    ds = compile_case("cornell_64")
+    out = {"buffer": film_buffers(), "scales": np.array([1 / 8, 1.0, 1 / 3], dtype=np.float32)}
+    for tag, exposure in (("", 1.0), ("_exp", 1.75)):
+        ds.data.film.exposure = exposure
+        ds.data.film.use_display_exposure = 1 if exposure != 1.0 else 0
+        rk = RefKernel(ds)
+        out["byte" + tag] = np.stack([rk.film_convert(out["buffer"], float(s), False) for s in out["scales"]])
+        out["half" + tag] = np.stack([rk.film_convert(out["buffer"], float(s), True) for s in out["scales"]])
+        rk.close()
+    np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), "film.npz"), **out)
+
+
 def main():
     make_primitives()
+    make_film()
     if "--primitives-only" in sys.argv:
         return
     for name in CASES:
@@ -100,6 +133,8 @@ def main():
         q[:, 2] = ds.samples
         q[:, 3] = rng.integers(0, 150, 2048)
         rng_out = rk.rng_1d(q)
+        film_byte = rk.film_convert(buf, 1.0 / ds.samples, False)
+        film_half = rk.film_convert(buf, 1.0 / ds.samples, True)
         np.savez_compressed(
             golden_path(name),
             digest=np.array(scene_digest(ds)),
@@ -114,6 +149,8 @@ def main():
             rng_q=q,
             rng_out=rng_out,
             samples=np.array(ds.samples),
+            film_byte=film_byte,
+            film_half=film_half,
         )
         print(name, "hits", int(hit_i[:, 0].sum()), "/", len(rays), "buffer mean", float(buf[..., :3].mean()))
 

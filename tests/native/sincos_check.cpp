@@ -21,3 +21,26 @@ extern "C" void acos_eval(const float *x, long n, float *dev, float *libm)
     libm[i] = acosf(x[i]);
   }
 }
+
+/* cy_powf (glibc powf restatement) and libm powf over [lo, hi] bit patterns,
+ * with y = 1/2.4 (color_linear_to_srgb); returns the number of mismatches. */
+extern "C" long powf_sweep(uint32_t lo, uint32_t hi, uint32_t step)
+{
+  long bad = 0;
+  const float y = 1.0f / 2.4f;
+  for (uint64_t u = lo; u <= hi; u += step) {
+    const float x = as_float((uint32_t)u);
+    volatile float vx = x;
+    if (as_uint(cy_powf(x, y)) != as_uint(powf(vx, y))) {
+      bad++;
+    }
+  }
+  return bad;
+}
+
+extern "C" void srgb_eval(const float *x, long n, float *dev)
+{
+  for (long i = 0; i < n; i++) {
+    dev[i] = color_linear_to_srgb(x[i]);
+  }
+}

@@ -130,4 +130,7 @@ def sincos():
     vp = ctypes.c_void_p
     lib.sincos_eval.argtypes = [vp, ctypes.c_long, vp, vp, vp, vp]
     lib.acos_eval.argtypes = [vp, ctypes.c_long, vp, vp]
+    lib.powf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    lib.powf_sweep.restype = ctypes.c_long
+    lib.srgb_eval.argtypes = [vp, ctypes.c_long, vp]
     return lib

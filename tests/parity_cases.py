@@ -82,3 +82,16 @@ def golden_path(name: str) -> str:
 
 def load_golden(name: str):
     return np.load(golden_path(name), allow_pickle=False)
+
+
+def film_params(ds: sc.DeviceScene):
+    """(int32[6], exposure) film fields read by film convert, in the order of
+    cyo_film_convert / hipcy_film_convert (kernel_film.h:19-63)."""
+    f = ds.data.film
+    return (np.array([f.pass_stride, f.display_pass_stride, f.display_pass_components,
+                      f.display_divide_pass_stride, f.use_display_exposure, f.use_display_pass_alpha],
+                     dtype=np.int32), float(f.exposure))
+
+
+def load_film_golden():
+    return np.load(os.path.join(GOLDEN, "film.npz"), allow_pickle=False)

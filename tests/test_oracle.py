@@ -155,3 +155,37 @@ def test_oracle_vs_reference_kernel_random():
         p, n = np.ascontiguousarray(P[i]), np.ascontiguousarray(Ng[i])
         orc.cyo_ray_offset(p.ctypes.data, n.ctypes.data, out.ctypes.data)
         assert np.array_equal(out.view(np.uint32), want[i].view(np.uint32)), i
+
+
+def _oracle_film(ds, buf, scale, half, exposure=None):
+    from parity_cases import film_params
+
+    p, e = film_params(ds)
+    if exposure is not None:
+        p[4], e = (1 if exposure != 1.0 else 0), exposure
+    buf = np.ascontiguousarray(buf, dtype=np.float32)
+    h, w = buf.shape[:2]
+    out = np.zeros((h, w, 4), dtype=np.uint16 if half else np.uint8)
+    oracle_lib().cyo_film_convert(p.ctypes.data, e, buf.ctypes.data, out.ctypes.data, scale, 0, 0, w, h, 0, w,
+                                  1 if half else 0)
+    return out
+
+
+def test_film_convert_golden(case):
+    """C oracle film convert (byte and half) == the reference's on the golden render."""
+    _, ds, g = case
+    s = 1.0 / int(g["samples"])
+    assert np.array_equal(_oracle_film(ds, g["buffer"], s, False), g["film_byte"])
+    assert np.array_equal(_oracle_film(ds, g["buffer"], s, True), g["film_half"])
+
+
+@pytest.mark.parametrize("tag,exposure", [("", 1.0), ("_exp", 1.75)])
+def test_film_convert_edge_golden(tag, exposure):
+    """Edge buffers (negatives, sRGB knee, > half range, alpha > samples)."""
+    from parity_cases import load_film_golden
+
+    ds = compile_case("cornell_64")
+    g = load_film_golden()
+    for i, s in enumerate(g["scales"]):
+        assert np.array_equal(_oracle_film(ds, g["buffer"], float(s), False, exposure), g["byte" + tag][i])
+        assert np.array_equal(_oracle_film(ds, g["buffer"], float(s), True, exposure), g["half" + tag][i])
