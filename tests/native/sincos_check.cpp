@@ -44,3 +44,12 @@ extern "C" void srgb_eval(const float *x, long n, float *dev)
     dev[i] = color_linear_to_srgb(x[i]);
   }
 }
+
+extern "C" void atan2_eval(const float *y, const float *x, long n, float *dev, float *libm)
+{
+  for (long i = 0; i < n; i++) {
+    dev[i] = cy_atan2f(y[i], x[i]);
+    volatile float vy = y[i], vx = x[i];
+    libm[i] = atan2f(vy, vx);
+  }
+}

@@ -133,4 +133,5 @@ def sincos():
     lib.powf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     lib.powf_sweep.restype = ctypes.c_long
     lib.srgb_eval.argtypes = [vp, ctypes.c_long, vp]
+    lib.atan2_eval.argtypes = [vp, vp, ctypes.c_long, vp, vp]
     return lib

@@ -72,3 +72,22 @@ def test_powf_bit_exact_vs_libm():
     assert lib.powf_sweep(lo, hi, 7) == 0
     assert lib.powf_sweep(hi, int(np.float32(1e30).view(np.uint32)), 101) == 0
     assert lib.powf_sweep(int(np.float32(1e-30).view(np.uint32)), lo, 1009) == 0
+
+
+def test_atan2f_bit_exact_vs_libm():
+    """cy_atan2f restates glibc's fdlibm atan2f/atanf (direction_to_equirectangular,
+    kernel_projection.h:56-65): random directions, axis-aligned and special values."""
+    lib = nb.sincos()
+    rng = np.random.default_rng(8)
+    n = 1 << 20
+    y = rng.standard_normal(n).astype(np.float32)
+    x = rng.standard_normal(n).astype(np.float32)
+    x[::5] *= np.float32(1e-4)
+    y[::7] *= np.float32(1e5)
+    sp = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, 1e-38, 3e38, 1e-45], dtype=np.float32)
+    yy, xx = np.meshgrid(sp, sp)
+    y = np.ascontiguousarray(np.concatenate([y, yy.ravel()]))
+    x = np.ascontiguousarray(np.concatenate([x, xx.ravel()]))
+    dev, ref = np.zeros_like(x), np.zeros_like(x)
+    lib.atan2_eval(y.ctypes.data, x.ctypes.data, len(x), dev.ctypes.data, ref.ctypes.data)
+    assert np.array_equal(dev.view(np.uint32), ref.view(np.uint32))
