@@ -30,6 +30,9 @@
  *   hipcy_set_bvh_width / _leaf_merge        (device options) traverse the bound BVH2 as is, or
  *                                            the 4/8-wide BVH the device widens it into, like
  *                                            BVH::pack_nodes/widen_children_nodes bvh/bvh.cpp:149-176
+ *   hipcy_shader_eval                        device_cuda_impl.cpp:2019-2093 CUDADevice::shader
+ *                                            (DeviceTask SHADER, SHADER_EVAL_BACKGROUND;
+ *                                            kernel_bake.h:474-510, light.cpp:38-85)
  *   hipcy_film_convert                       device_cuda_impl.cpp:1954-2017 CUDADevice::film_convert
  *                                            (DeviceTask FILM_CONVERT; kernel/kernel_film.h)
  *   hipcy_intersect / hipcy_camera_rays      test entry points (scene_intersect, bvh/bvh.h:154;
@@ -131,6 +134,13 @@ int hipcy_set_profiling(hipcy_device *dev, int flags);
  * at pixel index offset + x + y*stride of either; sample_scale = 1 / samples
  * rendered (the reference passes 1/(task.sample+1)).  Halfs follow the CPU
  * device's truncating conversion (util_half.h:80-118). */
+/* DeviceTask SHADER: input uint4 per pixel (x, y = u, v float bits), output
+ * float4 per pixel accumulated (+=) num_samples times over
+ * [shader_x, shader_x + shader_w).  SHADER_EVAL_DISPLACE is rejected. */
+#define HIPCY_SHADER_EVAL_DISPLACE 0   /* kernel_types.h:203 */
+#define HIPCY_SHADER_EVAL_BACKGROUND 1 /* kernel_types.h:204 */
+int hipcy_shader_eval(hipcy_device *dev, int eval_type, uint64_t input, uint64_t output, int shader_x,
+                      int shader_w, int offset, int num_samples);
 int hipcy_film_convert(hipcy_device *dev, uint64_t buffer, uint64_t rgba_byte, uint64_t rgba_half,
                        float sample_scale, int x, int y, int w, int h, int offset, int stride);
 

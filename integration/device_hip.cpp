@@ -154,8 +154,20 @@ class HIPCyclesDevice : public Device {
                                task.stride));
       return;
     }
+    if (task.type == DeviceTask::SHADER) {
+      /* LightManager background map (light.cpp:38-85) -> CUDADevice::shader
+       * (device_cuda_impl.cpp:2019-2093); SHADER_EVAL_DISPLACE is rejected */
+      task_pool_.push([=] {
+        check(hipcy_shader_eval(dev_, (int)task.shader_eval_type, (uint64_t)task.shader_input,
+                                (uint64_t)task.shader_output, task.shader_x, task.shader_w, task.offset,
+                                task.num_samples));
+        DeviceTask task_copy = task;
+        task_copy.update_progress(NULL);
+      });
+      return;
+    }
     if (task.type != DeviceTask::RENDER) {
-      set_error("HIP device: only RENDER and FILM_CONVERT tasks are implemented");
+      set_error("HIP device: only RENDER, SHADER and FILM_CONVERT tasks are implemented");
       return;
     }
     task_pool_.push([=] {

@@ -42,6 +42,7 @@ def ref_lib():
         lib.cref_render.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci, ci]
         lib.cref_intersect.argtypes = [vp, ci, vp, vp, vp]
         lib.cref_film_convert.argtypes = [vp, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
+        lib.cref_shader_eval.argtypes = [vp, vp, vp, ci, ci, ci, ci]
         lib.cref_camera_rays.argtypes = [vp, ci, vp, vp]
         lib.cref_rng_1d.argtypes = [vp, ci, vp, vp]
         lib.cref_sobol_directions.argtypes = [vp, ci]
@@ -133,6 +134,18 @@ class RefKernel:
         out = np.zeros((h, w, 4), dtype=np.uint16 if half else np.uint8)
         self.lib.cref_film_convert(self.h, out.ctypes.data, buffer.ctypes.data, sample_scale, 0, 0, w, h, 0, w,
                                    1 if half else 0)
+        return out
+
+    def background_eval(self, width: int, height: int, num_samples: int = 1):
+        """SHADER_EVAL_BACKGROUND over a (width x height) equirectangular map with
+        LightManager's inputs (light.cpp:49-59): float32 (height, width, 4)."""
+        u = ((np.arange(width, dtype=np.float32) + np.float32(0.5)) / np.float32(width)).astype(np.float32)
+        v = ((np.arange(height, dtype=np.float32) + np.float32(0.5)) / np.float32(height)).astype(np.float32)
+        inp = np.zeros((height, width, 4), dtype=np.uint32)
+        inp[..., 0] = u.view(np.uint32)[None, :]
+        inp[..., 1] = v.view(np.uint32)[:, None]
+        out = np.zeros((height, width, 4), dtype=np.float32)
+        self.lib.cref_shader_eval(self.h, inp.ctypes.data, out.ctypes.data, 1, 0, width * height, num_samples)
         return out
 
     def camera_rays(self, xys: np.ndarray):

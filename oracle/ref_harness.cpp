@@ -355,4 +355,19 @@ void cref_film_convert(void *h, void *rgba, float *buffer, float sample_scale, i
   thread_globals_free(kg);
 }
 
+/* SHADER task on the CPU device (device/device_cpu.cpp shader -> kernel_cpu_shader,
+ * kernels/cpu/kernel_cpu_impl.h:152-170 -> kernel_background_evaluate,
+ * kernel_bake.h:474-510): output[i] += world colour for i in [x, x + w), per sample. */
+void cref_shader_eval(void *h, const void *input, void *output, int type, int x, int w, int num_samples)
+{
+  RefContext *ctx = (RefContext *)h;
+  KernelGlobals kg = thread_globals(ctx->kg);
+  for (int sample = 0; sample < num_samples; sample++) {
+    for (int i = x; i < x + w; i++) {
+      kernel_cpu_shader(&kg, (uint4 *)input, (float4 *)output, type, 0, i, 0, sample);
+    }
+  }
+  thread_globals_free(kg);
+}
+
 }  // extern "C"

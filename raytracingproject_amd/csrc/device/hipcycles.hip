@@ -238,6 +238,33 @@ __global__ void k_test_camera(CyGlobals kg, const int *xys, float *out, int n)
   o[7] = as_float(rng_hash);
 }
 
+/* SHADER task, SHADER_EVAL_BACKGROUND (kernels/cuda/kernel.cu:195-212
+ * kernel_cuda_background): one thread per input pixel, output[x] += world
+ * colour.  The SVM stack is private (no closures are kept for
+ * PATH_RAY_EMISSION); this task runs once per scene update. */
+__global__ void __launch_bounds__(CY_BLOCK) k_background_eval(CyGlobals kg, const hc_uint4 *input, float *output,
+                                                               int sx, int sw, uint *err)
+{
+  const int x = sx + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (x >= sx + sw) {
+    return;
+  }
+  CyClosure closure[1];
+  float svm[CY_SVM_STACK];
+  CyShadeMem mem;
+  mem.closure = closure;
+  mem.svm_stack = svm;
+  mem.svm_stride = 1;
+  mem.svm_fast = CY_SVM_STACK;
+  mem.svm_spill = nullptr;
+  const hc_uint4 in = input[x];
+  const cfloat3 c = background_evaluate(&kg, in.x, in.y, mem, err);
+  float *o = output + 4 * (size_t)x;
+  o[0] += c.x;
+  o[1] += c.y;
+  o[2] += c.z;
+}
+
 /* Film convert (kernel/kernel_film.h, kernels/cuda/kernel.cu:156-178): one
  * thread per pixel of the (w x h) rectangle; the parity target is the CPU
  * device, so half output uses its truncating float4_store_half (util_half.h:80-118)
@@ -1310,6 +1337,49 @@ int hipcy_film_convert(hipcy_device *dev, uint64_t buffer, uint64_t rgba_byte, u
   HIP_CHECK(dev, hipGetLastError());
   HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
   return 0;
+}
+
+int hipcy_shader_eval(hipcy_device *dev, int eval_type, uint64_t input, uint64_t output, int shader_x,
+                      int shader_w, int offset, int num_samples)
+{
+  (void)offset; /* passed to kernel_cuda_background, unused by kernel_background_evaluate */
+  if (!dev->error.empty()) {
+    return -1;
+  }
+  if (eval_type != HIPCY_SHADER_EVAL_BACKGROUND) {
+    return set_error(dev, "shader_eval: only SHADER_EVAL_BACKGROUND is supported (displacement is not)");
+  }
+  if (!dev->have_data) {
+    return set_error(dev, "shader_eval: KernelData not uploaded");
+  }
+  if (!input || !output || shader_x < 0 || shader_w < 0 || num_samples < 0) {
+    return set_error(dev, "shader_eval: invalid arguments");
+  }
+  if (dev->globals.find("__svm_nodes") == dev->globals.end() ||
+      dev->globals.find("__shaders") == dev->globals.end()) {
+    return set_error(dev, "shader_eval: __svm_nodes / __shaders not bound");
+  }
+  if (shader_w == 0) {
+    return 0;
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  CyGlobals kg;
+  build_globals(dev, &kg);
+  uint *err = dev->counters + 3;
+  HIP_CHECK(dev, hipMemsetAsync(err, 0, 4, dev->stream));
+  /* CUDADevice::shader (device_cuda_impl.cpp:2019-2093): chunks of 65536, once per sample */
+  const int chunk = 65536;
+  for (int sample = 0; sample < num_samples; sample++) {
+    for (int x = shader_x; x < shader_x + shader_w; x += chunk) {
+      const int w = std::min(chunk, shader_x + shader_w - x);
+      hipLaunchKernelGGL(k_background_eval, dim3((w + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
+                         (const hc_uint4 *)input, (float *)output, x, w, err);
+      HIP_CHECK(dev, hipGetLastError());
+    }
+  }
+  HIP_CHECK(dev, hipMemcpyAsync(dev->host_counters + 3, err, 4, hipMemcpyDeviceToHost, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  return check_device_error(dev);
 }
 
 }  // extern "C"

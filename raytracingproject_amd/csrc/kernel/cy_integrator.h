@@ -725,4 +725,54 @@ CY_FN bool shade_path(const CyGlobals *kg,
   return false;
 }
 
+/* ---------------------------------------------------------------------------
+ * SHADER task, SHADER_EVAL_BACKGROUND: the world shader seen along one
+ * equirectangular direction (kernel_bake.h:474-510 kernel_background_evaluate;
+ * LightManager feeds (u, v) = ((x + 0.5) / w, (y + 0.5) / h) as float bits,
+ * light.cpp:38-60, and builds the background importance map from the result).
+ */
+
+/* kernel_projection.h:67-83: equirectangular_range_to_direction with the
+ * default range (-2pi, pi, -pi, pi) */
+CY_FN cfloat3 equirectangular_to_direction(float u, float v)
+{
+  const float m_2pi = 6.2831853071795864f;
+  const float phi = -m_2pi * u + CY_PI_F;
+  const float theta = -CY_PI_F * v + CY_PI_F;
+  const float sin_theta = cy_sinf(theta);
+  return mk3(sin_theta * cy_cosf(phi), sin_theta * cy_sinf(phi), cy_cosf(theta));
+}
+
+CY_FN cfloat3 background_evaluate(const CyGlobals *kg, uint in_u, uint in_v, CyShadeMem mem, uint *err)
+{
+  const cfloat3 D = equirectangular_to_direction(as_float(in_u), as_float(in_v));
+  /* shader_setup_from_background (kernel_shader.h:397-439), ray.P = 0, ray.t = 0 */
+  CySD sd;
+  sd.closure = mem.closure;
+  sd.svm_stack = mem.svm_stack;
+  sd.svm_stride = mem.svm_stride;
+  sd.svm_fast = mem.svm_fast;
+  sd.svm_spill = mem.svm_spill;
+  sd.P = D;
+  sd.N = neg3(D);
+  sd.Ng = neg3(D);
+  sd.I = neg3(D);
+  sd.shader = KD->background.surface_shader;
+  sd.flag = kg->__shaders[sd.shader & SHADER_MASK].flags;
+  sd.object_flag = 0;
+  sd.ray_length = 0.0f;
+  sd.object = OBJECT_NONE;
+  sd.prim = PRIM_NONE;
+  sd.type = 0; /* PRIMITIVE_NONE */
+  sd.u = 0.0f;
+  sd.v = 0.0f;
+  sd.svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
+  sd.closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
+  sd.closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);
+  /* path_flag 0 | PATH_RAY_EMISSION: no BSDF closures are kept */
+  shader_eval_surface(kg, &sd, PATH_RAY_EMISSION, err);
+  /* shader_background_eval (kernel_shader.h:996-1004) */
+  return (sd.flag & SD_EMISSION) ? sd.closure_emission_background : mk3(0.0f, 0.0f, 0.0f);
+}
+
 #endif /* CY_INTEGRATOR_H */

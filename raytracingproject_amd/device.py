@@ -173,6 +173,34 @@ class HIPDevice:
             buf.free()
         return out
 
+    # ---- SHADER task -------------------------------------------------------
+    SHADER_EVAL_BACKGROUND = 1  # kernel_types.h:204
+
+    def background_eval(self, width: int, height: int, num_samples: int = 1) -> np.ndarray:
+        """World colour over a (width x height) equirectangular map, the SHADER
+        task LightManager runs for the background importance map
+        (light.cpp:38-85 shade_background_pixels -> CUDADevice::shader,
+        device_cuda_impl.cpp:2019-2093).  Returns float32 [height, width, 4]
+        (rgb accumulated num_samples times, w = 0)."""
+        u = ((np.arange(width, dtype=np.float32) + np.float32(0.5)) / np.float32(width)).astype(np.float32)
+        v = ((np.arange(height, dtype=np.float32) + np.float32(0.5)) / np.float32(height)).astype(np.float32)
+        inp = np.zeros((height, width, 4), dtype=np.uint32)
+        inp[..., 0] = u.view(np.uint32)[None, :]
+        inp[..., 1] = v.view(np.uint32)[:, None]
+        out = np.zeros((height, width, 4), dtype=np.float32)
+        d_i = self.mem_alloc(inp.nbytes)
+        d_o = self.mem_alloc(out.nbytes)
+        try:
+            d_i.copy_to_device(inp)
+            d_o.copy_to_device(out)
+            self._check(self.lib.hipcy_shader_eval(self.h, self.SHADER_EVAL_BACKGROUND, d_i.ptr, d_o.ptr, 0,
+                                                   width * height, 0, num_samples))
+            d_o.copy_from_device(out)
+        finally:
+            d_i.free()
+            d_o.free()
+        return out
+
     # ---- FILM_CONVERT task ------------------------------------------------
     def film_convert(self, buffer: np.ndarray, sample_scale: float, half: bool = False,
                      tile=None) -> np.ndarray:

@@ -96,6 +96,8 @@ DEVICE_SYMBOLS = {
     "hipcy_film_convert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int]),
+    "hipcy_shader_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "hipcy_camera_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
 }
 

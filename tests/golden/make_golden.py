@@ -14,6 +14,8 @@ tests/parity_cases.py it stores, in tests/golden/<case>.npz:
 and, shared by all cases:
   primitives.npz    reference hash_uint2 and ray_offset on random + edge inputs
   film.npz          reference film convert (byte, half) of synthetic edge buffers
+  background.npz    reference SHADER task (SHADER_EVAL_BACKGROUND) of the worlds of
+                    parity_cases.BACKGROUND_CASES (map size and sample count per case)
   abi_layout.json   sizeof/offsetof of every device-data struct field in the
                     reference headers (kernel/kernel_types.h)
 The fixtures are data (inputs + expected outputs); no reference source is kept.
@@ -33,7 +35,9 @@ import ctypes  # noqa: E402
 import json  # noqa: E402
 
 from oracle.ref import RefKernel, ref_lib  # noqa: E402
-from parity_cases import CASES, camera_queries, compile_case, golden_path, make_rays, scene_digest  # noqa: E402
+from parity_cases import (BACKGROUND_CASES, CASES, camera_queries, compile_case, golden_path, make_rays,  # noqa: E402
+                          scene_digest)
+from raytracingproject_amd import scene as sc  # noqa: E402
 
 
 def ray_offset_inputs():
@@ -110,9 +114,26 @@ def make_film():
     np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), "film.npz"), **out)
 
 
+def make_background():
+    """SHADER_EVAL_BACKGROUND by the reference kernel for every case's world,
+    with LightManager's map inputs (light.cpp:49-59)."""
+    out = {}
+    for name, (fn, w, h, samples) in BACKGROUND_CASES.items():
+        ds = sc.compile_scene(fn())
+        rk = RefKernel(ds)
+        out["digest_" + name] = np.array(scene_digest(ds))
+        out["out_" + name] = rk.background_eval(w, h, samples)
+        rk.close()
+    np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), "background.npz"), **out)
+
+
 def main():
+    if "--background-only" in sys.argv:
+        make_background()
+        return
     make_primitives()
     make_film()
+    make_background()
     if "--primitives-only" in sys.argv:
         return
     for name in CASES:

@@ -24,6 +24,22 @@ CASES = {
     "cornell_instanced": lambda: scenes.cornell_instanced(64, 64, 64),
 }
 
+
+
+def _world_case():
+    s = scenes.cornell_box(16, 16, 1)
+    s.world_color = (0.3, 0.55, 0.9)
+    s.world_strength = 1.7
+    return s
+
+
+# SHADER task (SHADER_EVAL_BACKGROUND) cases: name -> (scene, map width, height, samples)
+BACKGROUND_CASES = {
+    **{name: (fn, 64, 32, 2) for name, fn in CASES.items()},
+    "world_blue": (_world_case, 64, 32, 2),
+    "world_blue_ragged": (_world_case, 37, 19, 3),
+}
+
 PATH_RAY_ALL_VISIBILITY = (1 << 14) - 1
 PATH_RAY_SHADOW_OPAQUE = (1 << 7) | (1 << 8)
 PATH_RAY_SHADOW = (1 << 7) | (1 << 8) | (1 << 9) | (1 << 10)
@@ -95,3 +111,7 @@ def film_params(ds: sc.DeviceScene):
 
 def load_film_golden():
     return np.load(os.path.join(GOLDEN, "film.npz"), allow_pickle=False)
+
+
+def load_background_golden():
+    return np.load(os.path.join(GOLDEN, "background.npz"), allow_pickle=False)

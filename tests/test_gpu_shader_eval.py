@@ -1,0 +1,56 @@
+"""GPU parity of the SHADER task (hipcy_shader_eval, SHADER_EVAL_BACKGROUND)
+against the reference CPU kernel (kernel_background_evaluate,
+kernel_bake.h:474-510) recorded in tests/golden/background.npz.
+
+Bar: bit-exact (the direction goes through the device's glibc sinf/cosf
+restatement, cy_math.h)."""
+import numpy as np
+import pytest
+
+from parity_cases import BACKGROUND_CASES, load_background_golden
+from raytracingproject_amd import scene as sc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def device():
+    from raytracingproject_amd.device import HIPDevice
+
+    dev = HIPDevice(0)
+    yield dev
+    dev.close()
+
+
+@pytest.mark.parametrize("name", list(BACKGROUND_CASES))
+def test_background_eval_bit_exact(name, device):
+    fn, w, h, s = BACKGROUND_CASES[name]
+    g = load_background_golden()
+    device.upload_scene(sc.compile_scene(fn()))
+    out = device.background_eval(w, h, s)
+    assert np.array_equal(out.view(np.uint32), g["out_" + name].view(np.uint32))
+
+
+def test_background_eval_large_map_chunks(device):
+    """A map beyond one 65536-pixel chunk (CUDADevice::shader chunking): every
+    pixel of a constant world equals the small fixture's value."""
+    fn, w, h, s = BACKGROUND_CASES["world_blue"]
+    g = load_background_golden()["out_world_blue"]
+    device.upload_scene(sc.compile_scene(fn()))
+    out = device.background_eval(512, 256, s)
+    assert np.array_equal(out.reshape(-1, 4).view(np.uint32),
+                          np.broadcast_to(g[0, 0], (512 * 256, 4)).view(np.uint32))
+
+
+def test_shader_eval_displace_rejected():
+    from raytracingproject_amd.device import HIPDevice
+
+    dev = HIPDevice(0)
+    try:
+        dev.upload_scene(sc.compile_scene(BACKGROUND_CASES["world_blue"][0]()))
+        d = dev.mem_alloc(64)
+        rc = dev.lib.hipcy_shader_eval(dev.h, 0, d.ptr, d.ptr, 0, 1, 0, 1)
+        assert rc != 0
+        assert "SHADER_EVAL_BACKGROUND" in dev.error_message()
+    finally:
+        dev.close()

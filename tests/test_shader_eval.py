@@ -1,0 +1,46 @@
+"""SHADER task, SHADER_EVAL_BACKGROUND (hipcy_shader_eval / cy_integrator.h
+background_evaluate) on the CPU: the fixtures match the scenes compiled here,
+and the device code compiled for the host reproduces the reference kernel's
+output (kernel_bake.h:474-510 via kernel_cpu_shader) bit for bit, with libm's
+sinf/cosf and with the device's own restatement (what the GPU runs)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import native_build as nb
+from parity_cases import BACKGROUND_CASES, load_background_golden, scene_digest
+from raytracingproject_amd import scene as sc
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import emu  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return load_background_golden()
+
+
+@pytest.mark.parametrize("name", list(BACKGROUND_CASES))
+def test_background_fixture_inputs(name, golden):
+    fn, w, h, s = BACKGROUND_CASES[name]
+    assert str(golden["digest_" + name]) == scene_digest(sc.compile_scene(fn()))
+    assert golden["out_" + name].shape == (h, w, 4)
+
+
+@pytest.mark.parametrize("libm", [True, False])
+@pytest.mark.parametrize("name", list(BACKGROUND_CASES))
+def test_background_eval_host_bit_exact(name, libm, golden):
+    fn, w, h, s = BACKGROUND_CASES[name]
+    lib = nb.host_emu(libm_sincos=libm)
+    out = emu.background(sc.compile_scene(fn()), w, h, s, lib=lib)
+    assert np.array_equal(out.view(np.uint32), golden["out_" + name].view(np.uint32))
+
+
+def test_background_inputs_match_light_manager():
+    """u, v = (x + 0.5) / w, (y + 0.5) / h in float32 (light.cpp:53-54)."""
+    inp = emu.background_inputs(5, 3)
+    assert inp[2, 4, 0] == np.float32(4.5 / 5).view(np.uint32)
+    assert inp[2, 4, 1] == np.float32(2.5 / 3).view(np.uint32)
+    assert not inp[..., 2:].any()

@@ -33,3 +33,31 @@ def render(ds, lib=None, samples=None, start_sample=0, tile=None):
     if err:
         raise RuntimeError("emulator device error %x" % err)
     return buf
+
+
+def background_inputs(width, height):
+    """LightManager's map inputs (light.cpp:49-59): uint4 per pixel, u/v float bits."""
+    u = ((np.arange(width, dtype=np.float32) + np.float32(0.5)) / np.float32(width)).astype(np.float32)
+    v = ((np.arange(height, dtype=np.float32) + np.float32(0.5)) / np.float32(height)).astype(np.float32)
+    inp = np.zeros((height, width, 4), dtype=np.uint32)
+    inp[..., 0] = u.view(np.uint32)[None, :]
+    inp[..., 1] = v.view(np.uint32)[:, None]
+    return inp
+
+
+def background(ds, width, height, num_samples=1, lib=None):
+    lib = lib or load()
+    names = list(ds.arrays)
+    arrs = [np.ascontiguousarray(ds.arrays[n]) for n in names]
+    c_names = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+    c_ptrs = (ctypes.c_void_p * len(names))(*[a.ctypes.data for a in arrs])
+    data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
+    inp = background_inputs(width, height)
+    out = np.zeros((height, width, 4), dtype=np.float32)
+    vp, ci = ctypes.c_void_p, ctypes.c_int
+    lib.emu_background.argtypes = [vp, ci, vp, vp, vp, ci, ci, vp]
+    err = lib.emu_background(ctypes.addressof(data), len(names), c_names, c_ptrs, inp.ctypes.data,
+                             width * height, num_samples, out.ctypes.data)
+    if err:
+        raise RuntimeError("emulator device error %x" % err)
+    return out

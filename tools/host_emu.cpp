@@ -287,3 +287,30 @@ extern "C" int emu_render(const void *data,
   }
   return (int)err;
 }
+
+/* SHADER task, SHADER_EVAL_BACKGROUND (cy_integrator.h background_evaluate):
+ * out[i] (float4) += world colour for input i, num_samples times. */
+extern "C" int emu_background(const void *data, int n_arrays, const char **names, const void **ptrs,
+                              const unsigned *input, int n, int num_samples, float *out)
+{
+  CyGlobals kg;
+  emu_bind(&kg, data, n_arrays, names, ptrs, nullptr);
+  uint err = 0;
+  CyClosure closure[1];
+  float svm[CY_SVM_STACK];
+  CyShadeMem mem;
+  mem.closure = closure;
+  mem.svm_stack = svm;
+  mem.svm_stride = 1;
+  mem.svm_fast = CY_SVM_STACK;
+  mem.svm_spill = nullptr;
+  for (int s = 0; s < num_samples; s++) {
+    for (int i = 0; i < n; i++) {
+      const cfloat3 c = background_evaluate(&kg, input[4 * i], input[4 * i + 1], mem, &err);
+      out[4 * i] += c.x;
+      out[4 * i + 1] += c.y;
+      out[4 * i + 2] += c.z;
+    }
+  }
+  return (int)err;
+}
