@@ -4,16 +4,26 @@
 
 One step = one full frame of the configured workload (BMW27 stand-in,
 1280x720, 128 spp, BASELINE.json configs[1]) rendered by the HIP device from
-camera rays to the render buffer, with the scene already resident in HBM.
-With N ranks (torch.distributed.run, one process per GPU) the frame's rows are
-interleaved across ranks (rank r renders rows r, r+N, ...): total work per step
-is fixed, so scaling is "strong".  Rank 0 prints one JSON line.
+camera rays to the film on the host: the render buffer is zeroed, every sample
+is path traced, and the finished film is copied to host memory (with N ranks:
+gathered to rank 0 over RCCL first), as BASELINE.md's render time ("until the
+last tile's buffer is on the host") requires.  The scene is resident in HBM
+before the timed region (scene compile / upload / BVH widening are reported
+separately).
+
+With --gpus N > 1 and no torch.distributed environment, bench.py starts N ranks
+itself (torch.distributed.run, one process per GPU) before touching any GPU.
+Rank r renders image rows r, r+N, r+2N, ... (raytracingproject_amd/shard.py):
+total work per step is fixed, so scaling is "strong".  Rank 0 prints one JSON
+line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
@@ -42,13 +52,38 @@ def parse():
                    help="4 (default) / 8: device-widened wide BVH; 2: the bound BVH2 as is")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
     p.add_argument("--slots", type=int, default=0, help="path slots in flight (0: device default)")
+    p.add_argument("--tile", type=int, default=64,
+                   help="tile-mode leg: render one extra frame as TxT RenderTiles through the plugin path "
+                        "(0 disables)")
+    p.add_argument("--tile-batch", type=int, default=0,
+                   help="tiles rendered per device pass in the tile-mode leg (0: all tiles of the frame)")
+    p.add_argument("--profile-frame", action="store_true",
+                   help="only render the instrumented single-lane frame (for rocprofv3 PMC passes)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank); gloo rehearses N ranks on fewer GPUs")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """Start N ranks (one process per GPU) and return the launcher's exit code.
+    Runs before anything in this process touches a GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -67,6 +102,7 @@ def main():
     from raytracingproject_amd import scene as sc
     from raytracingproject_amd import scenes
     from raytracingproject_amd.device import HIPDevice
+    from raytracingproject_amd.shard import RowShard
 
     kw = {}
     if args.width:
@@ -88,21 +124,63 @@ def main():
     dev.load_kernels()  # validates the scene and widens the BVH (scene preparation)
     t_upload = time.time() - t0
 
-    from raytracingproject_amd.shard import RowShard
-
-    W, H, S = ds.width, ds.height, ds.samples
+    W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
     shard = RowShard(rank, world, W, H)
-    rows = shard.rows
-    buf = dev.mem_alloc(W * rows * ds.pass_stride * 4)
+    rows_pad = -(-H // world)  # every rank's buffer has the same size for the gather
+    cuda = torch.device("cuda", device_index)
+    # render buffer: a torch allocation handed to the device as a raw pointer
+    # (RenderTile.buffer), so the gather can run over RCCL without a copy
+    local = torch.zeros((rows_pad, W, PS), dtype=torch.float32, device=cuda)
+    gather_gpu = args.dist_backend == "nccl"
+    if world > 1:
+        gathered = torch.empty((world, rows_pad, W, PS), dtype=torch.float32,
+                               device=cuda if gather_gpu else "cpu")
+    film_host = torch.empty((H, W, PS), dtype=torch.float32, pin_memory=True) if rank == 0 else None
+
+    class _Buf:  # the DeviceBuffer interface render_tile needs
+        ptr = local.data_ptr()
+
+    def render_frame():
+        local.zero_()
+        torch.cuda.current_stream().synchronize()
+        dev.render_tile(_Buf, shard.tile(), 0, S, shard.offset, shard.stride, y_step=shard.y_step)
+
+    def film_to_host():
+        """Finished film to rank 0's host memory (gather of the row-interleaved parts)."""
+        if world == 1:
+            film_host.copy_(local[:H])
+            return
+        if gather_gpu:
+            dist.all_gather_into_tensor(gathered.view(-1), local.view(-1))
+            if rank == 0:
+                full = gathered.transpose(0, 1).reshape(rows_pad * world, W, PS)[:H]
+                film_host.copy_(full)
+        else:
+            dist.all_gather_into_tensor(gathered.view(-1), local.cpu().view(-1))
+            if rank == 0:
+                film_host.copy_(gathered.transpose(0, 1).reshape(rows_pad * world, W, PS)[:H])
 
     def step():
-        buf.zero()
-        dev.render_tile(buf, shard.tile(), 0, S, shard.offset, shard.stride, y_step=shard.y_step)
+        render_frame()
+        film_to_host()
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+
+    if args.profile_frame:
+        dev.set_profiling(1)
+        render_frame()
+        torch.cuda.synchronize()
+        st = dev.stats()
+        if rank == 0:
+            print(json.dumps({"profile_frame": True, "closest_ms": st["closest_ms"],
+                              "closest_launches": st["closest_launches"]}), flush=True)
+        dev.close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     for _ in range(args.warmup):
         step()
@@ -114,20 +192,22 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cuda if gather_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
     total_samples = W * H * S * args.steps
     value = total_samples / elapsed / 1e6
+    film = film_host.numpy().copy() if rank == 0 else None
 
-    # Roofline of the dominant kernel (one extra instrumented frame, outside the
-    # timed region): HIP-event durations of every launch + traversal counters.
+    # Roofline of the dominant kernel (extra instrumented frames, outside the
+    # timed region): HIP-event durations of every launch on a single lane (no
+    # overlap), then the traversal counters.
     dev.set_profiling(1)
-    step()
+    render_frame()
     timing = dev.stats()
     dev.set_profiling(2)
-    step()
+    render_frame()
     counts = dev.stats()
     dev.set_profiling(0)
     kernels = {
@@ -149,13 +229,19 @@ def main():
     avg_ms = timing["closest_ms"] / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
+    pmc_note = None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
         from raytracingproject_amd.build import kernel_source_digest
 
         if pmc.get("source_digest") == kernel_source_digest():
-            traffic = pmc.get("k_intersect_closest", {}).get("hbm_bytes_per_launch")
+            ent = pmc.get("k_intersect_closest", {})
+            traffic = ent.get("hbm_bytes_per_launch")
+            pmc_note = {k: ent.get(k) for k in ("instance", "dispatches", "rocprof_avg_ms", "l2_hit_rate",
+                                                 "hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch")}
+        else:
+            pmc_note = "profiles/pmc_summary.json was measured on other kernel sources"
     roofline = {
         "bound": "hbm",
         "kernel": "k_intersect_closest",
@@ -164,6 +250,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        "traffic_source": pmc_note,
         "bytes_per_launch": bytes_per_launch,
         "avg_launch_ms": avg_ms,
         "launches_per_frame": launches,
@@ -173,6 +260,10 @@ def main():
         "tris_per_ray": counts["closest_tris"] / max(counts["closest_rays"], 1),
     }
 
+    tile_leg = None
+    if args.tile > 0 and world == 1:
+        tile_leg = tile_mode(dev, ds, args.tile, args.tile_batch)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ds, args.cpu_seconds)
@@ -180,12 +271,10 @@ def main():
     if args.save and rank == 0:
         from raytracingproject_amd import imageio
 
-        part = np.zeros((rows, W, ds.pass_stride), dtype=np.float32)
-        step()
-        buf.copy_from_device(part)
-        imageio.write_png(args.save, imageio.film_readout(part, S)[..., :3])
+        imageio.write_png(args.save, imageio.film_readout(film, S)[..., :3])
 
     if rank == 0:
+        rays = counts["closest_rays"] + counts["shadow_rays"]
         out = {
             "metric": "Msamples/sec on BMW27 @1280x720, 128 spp",
             "value": round(value, 3),
@@ -200,7 +289,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (procedural BMW27 stand-in scene, SURVEY.md §8(d))",
             "config": {
-                "workload": f"{args.config} {W}x{H} {S} spp, one frame per step",
+                "workload": f"{args.config} {W}x{H} {S} spp, one frame per step, film copied to host",
                 "triangles": ds.info["triangles"],
                 "parallelism": f"rows interleaved over {world} GPU(s)",
                 "wavefront_iterations_per_frame": int(timing["iterations"]),
@@ -209,20 +298,59 @@ def main():
             },
             "kernel_ms_per_frame": {k: round(v, 3) for k, v in kernels.items()},
             "rays_per_frame": {"closest": counts["closest_rays"], "shadow": counts["shadow_rays"]},
+            "mrays_per_s": round(rays * world * args.steps / elapsed / 1e6, 1),
+            "film_checksum": float(np.float64(film[..., :4].sum())) if film is not None else None,
             "roofline": roofline,
+            "tile_mode": tile_leg,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    buf.free()
+    del local
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
+def tile_mode(dev, ds, tile, batch):
+    """One frame rendered the way a Cycles Session drives a device: the frame
+    split into tile x tile RenderTiles (session.h:84 default 64), each tile
+    rendered over all its samples into its own buffer (background mode), the
+    device acquiring `batch` tiles per pass (0: all).  Reported beside the
+    whole-frame number; not the headline value."""
+    import torch
+
+    W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
+    tiles = [(x, y, min(tile, W - x), min(tile, H - y)) for y in range(0, H, tile) for x in range(0, W, tile)]
+    bufs = [torch.zeros((t[3], t[2], PS), dtype=torch.float32, device="cuda") for t in tiles]
+    batch = len(tiles) if batch <= 0 else batch
+
+    def frame():
+        for b in bufs:
+            b.zero_()
+        torch.cuda.current_stream().synchronize()
+        for i in range(0, len(tiles), batch):
+            group = [(t, b.data_ptr(), -(t[0] + t[1] * t[2]), t[2]) for t, b in zip(tiles[i:i + batch],
+                                                                                    bufs[i:i + batch])]
+            dev.render_tiles(group, 0, S)
+        for b in bufs:
+            b.cpu()
+
+    frame()  # warm (per-tile pools and records are sized on first use)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    frame()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"tile": tile, "tiles": len(tiles), "tiles_per_pass": batch,
+            "value": round(W * H * S / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(1e3 * dt, 3)}
+
+
 def cpu_baseline(ds, seconds):
     """Reference Cycles CPU kernel (oracle/_ref, compiled from the reference
-    sources) on a bounded sample of the same frame: all pixels at a reduced
-    sample count, on the host cores this process may use."""
+    sources; the AVX2 build when the host has AVX2, as stock Blender selects it,
+    device/device_cpu.cpp:76-134) on a bounded sample of the same frame: all
+    pixels at a reduced sample count, on the host cores this process may use
+    (the GPU box grants 16 cores per GPU)."""
     try:
         from oracle.ref import RefKernel, ref_available
     except Exception:
@@ -234,7 +362,7 @@ def cpu_baseline(ds, seconds):
         threads = min(threads, len(os.sched_getaffinity(0)))
     except Exception:
         pass
-    rk = RefKernel(ds)
+    rk = RefKernel(ds, fast=True)
     t0 = time.perf_counter()
     rk.render(samples=1, threads=threads)
     t1 = time.perf_counter() - t0
@@ -242,13 +370,15 @@ def cpu_baseline(ds, seconds):
     t0 = time.perf_counter()
     rk.render(samples=spp, start_sample=1, threads=threads)
     dt = time.perf_counter() - t0
+    arch = rk.arch
     rk.close()
     return {
         "value": round(ds.width * ds.height * spp / dt / 1e6, 4),
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "reference",
-        "sample": f"{ds.width}x{ds.height} at {spp} spp (samples 1..{spp}) of the same scene, {dt:.1f} s",
+        "sample": f"{ds.width}x{ds.height} at {spp} spp (samples 1..{spp}) of the same scene, {dt:.1f} s, "
+                  f"reference CPU kernel ({arch})",
     }
 
 

@@ -25,6 +25,8 @@
  *   hipcy_load_kernels                       device/device.h:375 load_kernels(DeviceRequestedFeatures)
  *   hipcy_path_trace                         device_cuda_impl.cpp:1853-1952 CUDADevice::render
  *                                            (one RenderTile, samples [start, start+num))
+ *   hipcy_path_trace_tiles                   device_cuda_impl.cpp:2342-2391 the RENDER task's
+ *                                            acquire_tile loop, several tiles per device pass
  *   hipcy_synchronize                        device_cuda_impl.cpp:1933 cuCtxSynchronize
  *   hipcy_get_bvh_layout_mask                device/device.h:353 get_bvh_layout_mask
  *   hipcy_set_bvh_width / _leaf_merge        (device options) traverse the bound BVH2 as is, or
@@ -48,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HIPCY_ABI_VERSION 2
+#define HIPCY_ABI_VERSION 3
 
 typedef struct hipcy_device hipcy_device;
 
@@ -122,18 +124,17 @@ int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)
  * and stored contiguously in the buffer: interleaved row sharding across GPUs. */
 int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *tile, int y_step);
+/* Several RenderTiles in one device pass (all with the same sample range):
+ * the plugin acquires up to n tiles from the Session (DeviceTask::acquire_tile,
+ * device_task.h) and renders them together, so small tiles still fill the GPU.
+ * Each tile keeps its own buffer, offset and stride. */
+int hipcy_path_trace_tiles(hipcy_device *dev, const hipcy_work_tile *tiles, int n_tiles);
 int hipcy_synchronize(hipcy_device *dev);
 int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
 /* flags: bit 0 = per-kernel HIP-event timings (kernels then run on one stream,
  * without overlap, so each launch is timed alone), bit 1 = traversal counters. */
 int hipcy_set_profiling(hipcy_device *dev, int flags);
 
-/* FILM_CONVERT task: the display pass (KernelFilm.display_pass_*) of pixels
- * (x..x+w-1, y..y+h-1) of `buffer` (pass_stride floats per pixel) is converted
- * to sRGB uchar4 into rgba_byte, or (rgba_byte == 0) to 4 halfs into rgba_half,
- * at pixel index offset + x + y*stride of either; sample_scale = 1 / samples
- * rendered (the reference passes 1/(task.sample+1)).  Halfs follow the CPU
- * device's truncating conversion (util_half.h:80-118). */
 /* DeviceTask SHADER: input uint4 per pixel (x, y = u, v float bits), output
  * float4 per pixel accumulated (+=) num_samples times over
  * [shader_x, shader_x + shader_w).  SHADER_EVAL_DISPLACE is rejected. */
@@ -141,6 +142,12 @@ int hipcy_set_profiling(hipcy_device *dev, int flags);
 #define HIPCY_SHADER_EVAL_BACKGROUND 1 /* kernel_types.h:204 */
 int hipcy_shader_eval(hipcy_device *dev, int eval_type, uint64_t input, uint64_t output, int shader_x,
                       int shader_w, int offset, int num_samples);
+/* FILM_CONVERT task: the display pass (KernelFilm.display_pass_*) of pixels
+ * (x..x+w-1, y..y+h-1) of `buffer` (pass_stride floats per pixel) is converted
+ * to sRGB uchar4 into rgba_byte, or (rgba_byte == 0) to 4 halfs into rgba_half,
+ * at pixel index offset + x + y*stride of either; sample_scale = 1 / samples
+ * rendered (the reference passes 1/(task.sample+1)).  Halfs follow the CPU
+ * device's truncating conversion (util_half.h:80-118). */
 int hipcy_film_convert(hipcy_device *dev, uint64_t buffer, uint64_t rgba_byte, uint64_t rgba_half,
                        float sample_scale, int x, int y, int w, int h, int offset, int stride);
 

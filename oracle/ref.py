@@ -16,9 +16,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF_LIB = os.path.join(HERE, "_ref", "libcycles_ref.so")
+# CPU-baseline only: the reference AVX2 kernel (never the parity checker)
+REF_AVX2_LIB = os.path.join(HERE, "_ref", "libcycles_ref_avx2.so")
 ORACLE_LIB = os.path.join(HERE, "_build", "libcy_oracle.so")
 
 _ref = None
+_ref_avx2 = None
 _orc = None
 
 
@@ -30,31 +33,50 @@ def oracle_available() -> bool:
     return os.path.exists(ORACLE_LIB)
 
 
-def ref_lib():
-    global _ref
+def _host_has_avx2() -> bool:
+    try:
+        with open("/proc/cpuinfo") as f:
+            flags = [ln for ln in f if ln.startswith("flags")]
+        return bool(flags) and " avx2" in flags[0] and " fma" in flags[0]
+    except OSError:
+        return False
+
+
+def ref_lib(fast: bool = False):
+    """The reference kernel library; fast=True returns the AVX2 build when it
+    exists and the host supports it (CPU baseline), else the generic one."""
+    global _ref, _ref_avx2
+    if fast and os.path.exists(REF_AVX2_LIB) and _host_has_avx2():
+        if _ref_avx2 is None:
+            _ref_avx2 = _bind_ref(ctypes.CDLL(REF_AVX2_LIB))
+        return _ref_avx2
     if _ref is None:
-        lib = ctypes.CDLL(REF_LIB)
-        vp, sz, ci, cf = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float
-        lib.cref_create.restype = vp
-        lib.cref_destroy.argtypes = [vp]
-        lib.cref_const_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
-        lib.cref_global_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
-        lib.cref_render.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci, ci]
-        lib.cref_intersect.argtypes = [vp, ci, vp, vp, vp]
-        lib.cref_film_convert.argtypes = [vp, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
-        lib.cref_shader_eval.argtypes = [vp, vp, vp, ci, ci, ci, ci]
-        lib.cref_camera_rays.argtypes = [vp, ci, vp, vp]
-        lib.cref_rng_1d.argtypes = [vp, ci, vp, vp]
-        lib.cref_sobol_directions.argtypes = [vp, ci]
-        lib.cref_hash_uint2.restype = ctypes.c_uint32
-        lib.cref_hash_uint2.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
-        lib.cref_ray_offset.argtypes = [ci, vp, vp, vp]
-        lib.cref_sizeof.restype = ctypes.c_long
-        lib.cref_sizeof.argtypes = [ctypes.c_char_p]
-        lib.cref_offsetof.restype = ctypes.c_long
-        lib.cref_offsetof.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
-        _ref = lib
+        _ref = _bind_ref(ctypes.CDLL(REF_LIB))
     return _ref
+
+
+def _bind_ref(lib):
+    vp, sz, ci, cf = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float
+    lib.cref_create.restype = vp
+    lib.cref_destroy.argtypes = [vp]
+    lib.cref_const_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
+    lib.cref_global_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
+    lib.cref_render.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci, ci]
+    lib.cref_intersect.argtypes = [vp, ci, vp, vp, vp]
+    lib.cref_film_convert.argtypes = [vp, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
+    lib.cref_shader_eval.argtypes = [vp, vp, vp, ci, ci, ci, ci]
+    lib.cref_camera_rays.argtypes = [vp, ci, vp, vp]
+    lib.cref_rng_1d.argtypes = [vp, ci, vp, vp]
+    lib.cref_sobol_directions.argtypes = [vp, ci]
+    lib.cref_hash_uint2.restype = ctypes.c_uint32
+    lib.cref_hash_uint2.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    lib.cref_ray_offset.argtypes = [ci, vp, vp, vp]
+    lib.cref_sizeof.restype = ctypes.c_long
+    lib.cref_sizeof.argtypes = [ctypes.c_char_p]
+    lib.cref_offsetof.restype = ctypes.c_long
+    lib.cref_offsetof.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.cref_arch.restype = ctypes.c_char_p
+    return lib
 
 
 def oracle_lib():
@@ -80,8 +102,9 @@ def oracle_lib():
 class RefKernel:
     """Reference CPU kernel loaded with a DeviceScene's data (CPUDevice-style)."""
 
-    def __init__(self, dscene):
-        self.lib = ref_lib()
+    def __init__(self, dscene, fast: bool = False):
+        self.lib = ref_lib(fast)
+        self.arch = self.lib.cref_arch().decode()
         self.h = self.lib.cref_create()
         self.dscene = dscene
         self._keep = []

@@ -33,6 +33,14 @@
 
 using namespace ccl;
 
+/* Kernel the render entry drives: the generic x86-64 kernel (the parity
+ * oracle), or, in the CPU-baseline build (oracle/Makefile ref-avx2), the AVX2
+ * kernel stock Blender selects on such hosts (device/device_cpu.cpp:76-134). */
+#ifndef CREF_PATH_TRACE
+#  define CREF_PATH_TRACE kernel_cpu_path_trace
+#  define CREF_ARCH "cpu (generic x86-64, no FMA)"
+#endif
+
 namespace {
 
 struct RefContext {
@@ -74,6 +82,11 @@ void thread_globals_free(KernelGlobals &kg)
 }  // namespace
 
 extern "C" {
+
+const char *cref_arch(void)
+{
+  return CREF_ARCH;
+}
 
 void *cref_create(void)
 {
@@ -128,7 +141,7 @@ void cref_render(void *h,
     for (int sample = start_sample; sample < start_sample + num_samples; sample++) {
       for (int y = ty + t; y < ty + th; y += nthreads) {
         for (int x = tx; x < tx + tw; x++) {
-          kernel_cpu_path_trace(&kg, buffer, sample, x, y, offset, stride);
+          CREF_PATH_TRACE(&kg, buffer, sample, x, y, offset, stride);
         }
       }
     }

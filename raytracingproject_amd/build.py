@@ -115,7 +115,7 @@ def build_oracle(ref=True):
     oracle = os.path.join(REPO, "oracle")
     _run(["make", "-C", oracle, "oracle", "-j4"])
     if ref and os.path.isdir("/root/reference/blender/intern/cycles"):
-        _run(["make", "-C", oracle, "ref", "-j4"])
+        _run(["make", "-C", oracle, "ref", "ref-avx2", "-j4"])
 
 
 def build_all(ref=True, force=False):

@@ -30,6 +30,8 @@
 #  define CY_TRAV_MIN_WAVES 6
 #endif
 
+#define CY_STATS_SHARDS 64
+
 template<int W> struct LdsStack {
   static constexpr int ints = W > 2 ? 2 * CY_LDS_STACKW * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
 };
@@ -52,32 +54,55 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
 
-__global__ void __launch_bounds__(CY_BLOCK) k_init_slots(CyGlobals kg,
-                                                          CyPathBuffers b,
-                                                          CyTile tile,
-                                                          int slot_base,
-                                                          int n_slots,
-                                                          int *queue,
-                                                          uint *counter)
-{
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int slot = slot_base + i;
-  __shared__ uint claim[CY_CLAIM_LDS];
-  const bool active = slot_refill(kg, b, tile, slot, i < n_slots, claim);
-  queue_push(queue, counter, slot, active, claim);
-}
-
 __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
 {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < tile.w * tile.h) {
+  if (p < (int)tile.npix) {
     accumulate_pixel(&tile, p);
   }
 }
 
+/* Traversal counters: reduced over the workgroup, then one atomic per counter
+ * and workgroup into one of CY_STATS_SHARDS copies (device-scope atomics on a
+ * single word serialise at the memory side). */
+__device__ __forceinline__ void stats_block_add(CyStats *shard, uint n_nodes, uint n_leaves, uint n_tris,
+                                                uint n_over)
+{
+  __shared__ uint red[4];
+  if (threadIdx.x < 4) {
+    red[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  uint v[4] = {n_nodes, n_leaves, n_tris, n_over};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint x = v[k];
+    for (int off = 32; off > 0; off >>= 1) {
+      x += __shfl_xor(x, off);
+    }
+    if ((threadIdx.x & 63) == 0 && x) {
+      atomicAdd(&red[k], x);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    CyStats *st = shard + (blockIdx.x % CY_STATS_SHARDS);
+    if (red[0]) atomicAdd(&st->nodes, (unsigned long long)red[0]);
+    if (red[1]) atomicAdd(&st->leaves, (unsigned long long)red[1]);
+    if (red[2]) atomicAdd(&st->tris, (unsigned long long)red[2]);
+    if (red[3]) atomicAdd(&st->rays, (unsigned long long)red[3]);
+  }
+}
+
+/* Stage 1: closest hit for every queued path, or (cam_n > 0) for the camera
+ * rays of the work items item_base .. item_base + cam_n - 1 held by slots
+ * slot_base .. slot_base + cam_n - 1. */
 template<bool STATS, int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
+                                                                 CyTile tile,
+                                                                 int cam_n,
+                                                                 int slot_base,
                                                                  const int *queue,
                                                                  const uint *counter,
                                                                  uint *err,
@@ -86,42 +111,27 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ int lds_stack[LdsStack<W>::ints];
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
-  if (i < (int)*counter) {
-    const int slot = queue[i];
-    const hc_float4 rp = cy_ld(&b.ray_P[slot]);
-    const hc_float4 rd = cy_ld(&b.ray_D[slot]);
+  const bool active = cam_n > 0 ? i < cam_n : i < (int)*counter;
+  if (active) {
+    const int slot = cam_n > 0 ? slot_base + i : queue[i];
+    const uint cam_item = cam_n > 0 ? tile.item_base + (uint)i : CY_NO_ITEM;
     CyRay ray;
-    ray.P = mk3(rp.x, rp.y, rp.z);
-    ray.t = rp.w;
-    ray.D = mk3(rd.x, rd.y, rd.z);
-    const uint flag = cy_ld(&b.state0[slot]).x;
-    CyPathState s;
-    s.flag = (int)flag;
-    const uint visibility = path_state_ray_visibility(&s);
+    uint visibility;
+    const bool has_ray = closest_load(&kg, &b, &tile, slot, cam_item, &ray, &visibility);
     CyIsect isect;
     bool hit = false;
-    if (scene_intersect_valid(&ray)) {
+    if (has_ray && scene_intersect_valid(&ray)) {
       hit = scene_traverse<W, false, INST>(&kg, &ray, visibility, &isect, err,
-                                        STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
+                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
-    if (hit) {
-      cy_st(&b.isect[slot], mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim)));
-      cy_st(&b.isect_type[slot], isect.type);
-      if (INST) {
-        cy_st(&b.isect_object[slot], isect.object);
-      }
-    }
-    else {
-      cy_st(&b.isect_type[slot], 0);
-    }
+    closest_store<INST>(&b, slot, has_ray, hit, &isect);
   }
   if (STATS) {
-    stats_add(&stats[0].nodes, n_nodes);
-    stats_add(&stats[0].leaves, n_leaves);
-    stats_add(&stats[0].tris, n_tris);
+    stats_block_add(stats, n_nodes, n_leaves, n_tris, 0);
   }
 }
 
+/* Stage 3: occlusion of the light sample, deferred light add, finish + refill. */
 template<bool STATS, int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
@@ -140,40 +150,21 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   if (i < (int)*shadow_count) {
     slot = shadow_queue[i];
-    const hc_float4 sp = cy_ld(&b.shadow_P[slot]);
-    const hc_float4 sdr = cy_ld(&b.shadow_D[slot]);
     CyRay ray;
-    ray.P = mk3(sp.x, sp.y, sp.z);
-    ray.t = sp.w;
-    ray.D = mk3(sdr.x, sdr.y, sdr.z);
+    shadow_load(&b, slot, &ray);
     bool blocked = false;
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
       blocked = scene_traverse<W, true, INST>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
                                            STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
     }
-    const hc_float4 sl = cy_ld(&b.shadow_L[slot]);
-    hc_float4 L4 = cy_ld(&b.L[slot]);
-    if (!blocked) {
-      L4.x = L4.x + sl.x;
-      L4.y = L4.y + sl.y;
-      L4.z = L4.z + sl.z;
-    }
-    if (sl.w != 0.0f) {
-      slot_finish(&b, &tile, slot, mk3(L4.x, L4.y, L4.z), cy_ld(&b.throughput[slot]).w);
-      finished = true;
-    }
-    else {
-      cy_st(&b.L[slot], L4);
-    }
+    finished = shadow_finish(&b, &tile, slot, blocked);
   }
   __shared__ uint claim[CY_CLAIM_LDS];
   const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
   queue_push(queue_out, count_out, slot, regen, claim);
   if (STATS) {
-    stats_add(&stats[1].nodes, n_nodes);
-    stats_add(&stats[1].leaves, n_leaves);
-    stats_add(&stats[1].tris, n_tris);
+    stats_block_add(stats + CY_STATS_SHARDS, n_nodes, n_leaves, n_tris, 0);
   }
 }
 
@@ -442,6 +433,8 @@ struct hipcy_device {
   size_t record_budget = (size_t)4 << 30; /* bytes of sample records per pass */
   hc_float4 *records = nullptr;
   size_t records_capacity = 0;
+  CyTileDesc *tile_descs = nullptr; /* tiles of the current multi-tile pass */
+  size_t tile_descs_capacity = 0;
 
   /* W-wide BVH widened from the bound BVH2 (rebuilt when either BVH2 array,
    * the root or the width changes) */
@@ -454,6 +447,8 @@ struct hipcy_device {
   int bvhw_depth = 0;
   int *bvhw_object_root = nullptr; /* inside bvhw, after the nodes */
   int have_instancing = 1;         /* some object without SD_OBJECT_TRANSFORM_APPLIED */
+  std::vector<uint32_t> object_flags; /* host copy of __object_flag, taken at bind time */
+  bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
@@ -700,7 +695,7 @@ hipcy_device *hipcy_create(int ordinal)
       hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&dev->data_dev, sizeof(hc_KernelData)) != hipSuccess ||
       hipMalloc((void **)&dev->counters, 16 * 4 * (CY_LANES + 1)) != hipSuccess ||
-      hipMalloc((void **)&dev->stats_dev, 2 * sizeof(CyStats)) != hipSuccess ||
+      hipMalloc((void **)&dev->stats_dev, 2 * CY_STATS_SHARDS * sizeof(CyStats)) != hipSuccess ||
       hipHostMalloc((void **)&dev->host_counters, 16 * 4 * (CY_LANES + 1), hipHostMallocDefault) != hipSuccess) {
     set_error(nullptr, "device context creation failed");
     delete dev;
@@ -725,6 +720,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->pool) hipFree(dev->pool);
   if (dev->bvhw) hipFree(dev->bvhw);
   if (dev->records) hipFree(dev->records);
+  if (dev->tile_descs) hipFree(dev->tile_descs);
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
@@ -780,6 +776,19 @@ int hipcy_mem_copy_to(hipcy_device *dev, uint64_t dst, const void *src, size_t b
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
   HIP_CHECK(dev, hipMemcpyAsync((void *)dst, src, bytes, hipMemcpyHostToDevice, dev->stream));
   HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  /* a bound array rewritten in place: features must be re-checked */
+  for (auto &g : dev->globals) {
+    if (g.second.ptr == dst) {
+      dev->features_dirty = true;
+      if (g.first == "__object_flag") {
+        dev->object_flags.assign((const uint32_t *)src, (const uint32_t *)src + std::min(bytes, g.second.bytes) / 4);
+      }
+      if (g.first == "__bvh_nodes" || g.first == "__bvh_leaf_nodes" || g.first == "__prim_tri_index" ||
+          g.first == "__prim_object" || g.first == "__object_node") {
+        dev->bvhw_dirty = true;
+      }
+    }
+  }
   return 0;
 }
 
@@ -813,6 +822,7 @@ int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, s
   }
   memcpy(&dev->data_host, host, size);
   dev->have_data = true;
+  dev->features_dirty = true;
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
   HIP_CHECK(dev, hipMemcpyAsync(dev->data_dev, host, size, hipMemcpyHostToDevice, dev->stream));
   HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
@@ -843,6 +853,17 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
   b.ptr = device_pointer;
   b.bytes = bytes;
   dev->globals[name] = b;
+  dev->features_dirty = true;
+  if (strcmp(name, "__object_flag") == 0) {
+    /* the device pointer holds the uploaded array already (global_alloc copies
+     * before binding, device_cuda_impl.cpp:1088-1096): keep a host copy for the
+     * feature checks of load_kernels, so no render needs a device read-back */
+    dev->object_flags.assign(bytes / 4, 0u);
+    if (bytes) {
+      HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+      HIP_CHECK(dev, hipMemcpy(dev->object_flags.data(), (const void *)device_pointer, bytes, hipMemcpyDeviceToHost));
+    }
+  }
   if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0 ||
       strcmp(name, "__prim_tri_index") == 0 || strcmp(name, "__prim_object") == 0 ||
       strcmp(name, "__object_node") == 0) {
@@ -920,21 +941,18 @@ int hipcy_load_kernels(hipcy_device *dev)
   }
   /* instanced geometry present? (selects the traversal kernels with instance
    * leaves and the instance paths of shading) */
-  {
-    auto of = dev->globals.find("__object_flag");
-    std::vector<uint32_t> flags(of->second.bytes / 4);
-    if (!flags.empty()) {
-      HIP_CHECK(dev, hipMemcpy(flags.data(), (const void *)of->second.ptr, of->second.bytes, hipMemcpyDeviceToHost));
-    }
-    dev->have_instancing = 0;
-    for (uint32_t f : flags) {
-      if (!(f & SD_OBJECT_TRANSFORM_APPLIED)) {
-        dev->have_instancing = 1;
-      }
+  dev->have_instancing = 0;
+  for (uint32_t f : dev->object_flags) {
+    if (!(f & SD_OBJECT_TRANSFORM_APPLIED)) {
+      dev->have_instancing = 1;
     }
   }
   /* scene-preparation step of the device: widen the BVH now, not in the first render */
-  return ensure_bvhw(dev);
+  if (ensure_bvhw(dev) != 0) {
+    return -1;
+  }
+  dev->features_dirty = false;
+  return 0;
 }
 
 int hipcy_set_profiling(hipcy_device *dev, int flags)
@@ -980,16 +998,21 @@ static int check_device_error(hipcy_device *dev)
   return 0;
 }
 
-static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step);
+static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_tiles, int y_step);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *t)
 {
-  return path_trace(dev, t, 1);
+  return path_trace(dev, t, 1, 1);
 }
 
 int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
 {
-  return path_trace(dev, t, y_step < 1 ? 1 : y_step);
+  return path_trace(dev, t, 1, y_step < 1 ? 1 : y_step);
+}
+
+int hipcy_path_trace_tiles(hipcy_device *dev, const hipcy_work_tile *tiles, int n_tiles)
+{
+  return path_trace(dev, tiles, n_tiles, 1);
 }
 
 static int ensure_records(hipcy_device *dev, size_t n)
@@ -1013,7 +1036,8 @@ struct EvQuad {
 /* One partition of the slot pool with its own stream, queues and counters. */
 struct PassLane {
   hipStream_t s;
-  int slot_base, n_slots;
+  int slot_base;
+  int cam_n; /* > 0 until the lane's camera launch is enqueued */
   uint *cnt;  /* device: [0..2] queue counts, [4] next item */
   uint *hcnt; /* pinned host copy */
   int *q[3];
@@ -1023,6 +1047,10 @@ struct PassLane {
   hipEvent_t done;
 };
 
+/* One iteration of a lane: closest -> shade -> shadow.  The lane's first
+ * iteration is its camera launch (cam_n > 0): slot slot_base + i starts work
+ * item item_base + i, and the closest and shade kernels generate its camera
+ * ray themselves (no slot initialisation pass). */
 static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, int W, size_t *ev,
                         std::vector<EvQuad> *quads)
 {
@@ -1031,6 +1059,8 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   hipStream_t s = ln.s;
   uint *err = dev->counters + 3;
   const int qa = ln.qa, qb = ln.qb, qs = 2;
+  const int cam_n = ln.cam_n;
+  ln.cam_n = 0;
   dev->stats.iterations++;
   dev->stats.closest_rays += ln.n_active;
   HIP_CHECK(dev, hipMemsetAsync(ln.cnt + qb, 0, 4, s));
@@ -1046,13 +1076,14 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   }
   {
     auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0);
-    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.q[qa], ln.cnt + qa, err, dev->stats_dev);
+    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, ln.q[qa], ln.cnt + qa,
+                       err, dev->stats_dev);
   }
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));
   }
-  cy_launch_shade(dev->data_host.integrator.max_closures, grid, block, s, kg, dev->bufs, ln.tile, ln.q[qa],
-                  ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
+  cy_launch_shade(dev->data_host.integrator.max_closures, grid, block, s, kg, dev->bufs, ln.tile, cam_n,
+                  ln.slot_base, ln.q[qa], ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }
@@ -1093,12 +1124,9 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     L.s = dev->lane_stream[l];
     HIP_CHECK(dev, hipStreamWaitEvent(L.s, start, 0));
     L.slot_base = (int)(n_slots * l / lanes);
-    L.n_slots = (int)(n_slots * (l + 1) / lanes) - L.slot_base;
+    const int lane_slots = (int)(n_slots * (l + 1) / lanes) - L.slot_base;
     L.cnt = dev->counters + 16 * (l + 1);
     L.hcnt = dev->host_counters + 16 * (l + 1);
-    for (int q = 0; q < 3; q++) {
-      L.q[q] = dev->queue[q] + L.slot_base;
-    }
     L.qa = 0;
     L.qb = 1;
     L.done = get_event(dev, (*ev)++);
@@ -1106,17 +1134,16 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     const uint begin = (uint)((uint64_t)tile.n_items * l / lanes);
     L.tile.n_items = (uint)((uint64_t)tile.n_items * (l + 1) / lanes);
     L.tile.work_next = L.cnt + 4;
-    L.hcnt[4] = begin;
+    L.tile.item_base = begin;
+    /* camera launch: one item per slot of the lane */
+    L.cam_n = (int)std::min<uint>((uint)lane_slots, L.tile.n_items - begin);
+    L.n_active = (uint)L.cam_n;
+    for (int q = 0; q < 3; q++) {
+      L.q[q] = dev->queue[q] + L.slot_base;
+    }
+    L.hcnt[4] = begin + (uint)L.cam_n;
     HIP_CHECK(dev, hipMemsetAsync(L.cnt, 0, 12, L.s));
     HIP_CHECK(dev, hipMemcpyAsync(L.cnt + 4, L.hcnt + 4, 4, hipMemcpyHostToDevice, L.s));
-    hipLaunchKernelGGL(k_init_slots, dim3((unsigned)((L.n_slots + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
-                       L.s, kg, dev->bufs, L.tile, L.slot_base, L.n_slots, L.q[L.qa], L.cnt + L.qa);
-    HIP_CHECK(dev, hipMemcpyAsync(L.hcnt, L.cnt, 16, hipMemcpyDeviceToHost, L.s));
-    HIP_CHECK(dev, hipEventRecord(L.done, L.s));
-  }
-  for (int l = 0; l < lanes; l++) {
-    HIP_CHECK(dev, hipEventSynchronize(ln[l].done));
-    ln[l].n_active = ln[l].hcnt[ln[l].qa];
   }
   while (true) {
     bool any = false;
@@ -1148,29 +1175,78 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
   }
   /* all lanes finished: accumulate on the main stream after them */
   for (int l = 0; l < lanes; l++) {
+    HIP_CHECK(dev, hipEventRecord(ln[l].done, ln[l].s));
     HIP_CHECK(dev, hipStreamWaitEvent(dev->stream, ln[l].done, 0));
   }
-  const int npix = tile.w * tile.h;
+  const int npix = (int)tile.npix;
   hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((npix + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
                      dev->stream, tile);
   HIP_CHECK(dev, hipGetLastError());
   return 0;
 }
 
-static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
+static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_tiles, int y_step)
 {
   if (!dev->error.empty()) {
     return -1;
   }
-  if (hipcy_load_kernels(dev) != 0) {
+  if (n_tiles < 1 || (n_tiles > 1 && y_step != 1)) {
+    return set_error(dev, "path_trace: invalid tile set");
+  }
+  const hipcy_work_tile *t = &tiles[0];
+  for (int k = 1; k < n_tiles; k++) {
+    if (tiles[k].start_sample != t->start_sample || tiles[k].num_samples != t->num_samples) {
+      return set_error(dev, "path_trace_tiles: all tiles of a pass must render the same sample range");
+    }
+  }
+  /* re-validate only after the scene changed (Scene::device_update) */
+  if (dev->features_dirty && hipcy_load_kernels(dev) != 0) {
     return -1;
   }
   HIP_CHECK(dev, hipSetDevice(dev->ordinal));
-  const size_t npix = (size_t)t->w * (size_t)t->h;
+  /* pixels of the pass, numbered tile by tile */
+  std::vector<CyTileDesc> descs;
+  size_t npix = 0;
+  for (int k = 0; k < n_tiles; k++) {
+    const hipcy_work_tile &tk = tiles[k];
+    if (tk.w < 0 || tk.h < 0 || (tk.w * tk.h > 0 && !tk.buffer)) {
+      return set_error(dev, "path_trace: invalid tile");
+    }
+    if ((size_t)tk.w * tk.h == 0) {
+      continue;
+    }
+    CyTileDesc d;
+    d.x = tk.x;
+    d.y = tk.y;
+    d.w = tk.w;
+    d.h = tk.h;
+    d.offset = tk.offset;
+    d.stride = tk.stride;
+    d.buffer = (float *)tk.buffer;
+    d.px_begin = (uint)npix;
+    d.pad = 0;
+    descs.push_back(d);
+    npix += (size_t)tk.w * tk.h;
+  }
   if (npix == 0 || t->num_samples <= 0) {
     return 0;
   }
-  /* samples per pass: as many as the record budget holds for this tile */
+  if (npix > 0xFFFFFFFFull) {
+    return set_error(dev, "path_trace: tile set too large for 32-bit work items");
+  }
+  if (descs.size() > 1) {
+    const size_t bytes = descs.size() * sizeof(CyTileDesc);
+    if (bytes > dev->tile_descs_capacity) {
+      if (dev->tile_descs) {
+        HIP_CHECK(dev, hipFree(dev->tile_descs));
+        dev->tile_descs = nullptr;
+      }
+      HIP_CHECK(dev, hipMalloc((void **)&dev->tile_descs, bytes));
+      dev->tile_descs_capacity = bytes;
+    }
+    HIP_CHECK(dev, hipMemcpyAsync(dev->tile_descs, descs.data(), bytes, hipMemcpyHostToDevice, dev->stream));
+  }
+  /* samples per pass: as many as the record budget holds for these pixels */
   const size_t per_pass = std::max<size_t>(
       1, std::min<size_t>((size_t)t->num_samples, dev->record_budget / (npix * sizeof(hc_float4))));
   if (npix * per_pass > 0xFFFFFFFFull) {
@@ -1194,7 +1270,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
   }
   hipStream_t s = dev->stream;
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 16 * 4 * (CY_LANES + 1), s));
-  HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, 2 * sizeof(CyStats), s));
+  HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, 2 * CY_STATS_SHARDS * sizeof(CyStats), s));
   size_t ev = 0;
   hipEvent_t t_begin = get_event(dev, ev++);
   HIP_CHECK(dev, hipEventRecord(t_begin, s));
@@ -1202,17 +1278,21 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
 
   for (int s0 = t->start_sample; s0 < t->start_sample + t->num_samples; s0 += (int)per_pass) {
     CyTile tile;
-    tile.x = t->x;
-    tile.y = t->y;
-    tile.w = t->w;
-    tile.h = t->h;
+    const CyTileDesc &d0 = descs[0];
+    tile.x = d0.x;
+    tile.y = d0.y;
+    tile.w = d0.w;
+    tile.h = d0.h;
     tile.y_step = y_step;
     tile.start_sample = s0;
     tile.end_sample = std::min(s0 + (int)per_pass, t->start_sample + t->num_samples);
-    tile.offset = t->offset;
-    tile.stride = t->stride;
-    tile.buffer = (float *)t->buffer;
+    tile.offset = d0.offset;
+    tile.stride = d0.stride;
+    tile.buffer = d0.buffer;
     tile.pass_stride = dev->data_host.film.pass_stride;
+    tile.npix = (uint)npix;
+    tile.n_tiles = (int)descs.size();
+    tile.descs = descs.size() > 1 ? dev->tile_descs : nullptr;
     tile.n_items = (uint)(npix * (size_t)(tile.end_sample - tile.start_sample));
     if (path_trace_pass(dev, kg, tile, W, &ev, &quads) != 0) {
       return -1;
@@ -1245,8 +1325,18 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *t, int y_step)
     dev->stats.closest_launches = quads.size();
   }
   if (dev->profiling & 2) {
-    CyStats st[2];
-    HIP_CHECK(dev, hipMemcpy(st, dev->stats_dev, sizeof(st), hipMemcpyDeviceToHost));
+    std::vector<CyStats> shards(2 * CY_STATS_SHARDS);
+    HIP_CHECK(dev, hipMemcpy(shards.data(), dev->stats_dev, shards.size() * sizeof(CyStats), hipMemcpyDeviceToHost));
+    CyStats st[2] = {};
+    for (int k = 0; k < 2; k++) {
+      for (int j = 0; j < CY_STATS_SHARDS; j++) {
+        const CyStats &x = shards[k * CY_STATS_SHARDS + j];
+        st[k].nodes += x.nodes;
+        st[k].leaves += x.leaves;
+        st[k].tris += x.tris;
+        st[k].rays += x.rays;
+      }
+    }
     dev->stats.inner_nodes = st[0].nodes + st[1].nodes;
     dev->stats.leaves = st[0].leaves + st[1].leaves;
     dev->stats.triangles = st[0].tris + st[1].tris;

@@ -14,7 +14,7 @@
 
 #define CY_SHADE_LAUNCHER_ARGS \
   dim3 grid, dim3 block, hipStream_t stream, const CyGlobals &kg, const CyPathBuffers &b, const CyTile &tile, \
-      const int *queue_in, const uint *count_in, int *queue_out, uint *count_out, int *shadow_queue, \
+      int cam_n, int slot_base, const int *queue_in, const uint *count_in, int *queue_out, uint *count_out, int *shadow_queue, \
       uint *shadow_count, uint *err
 
 void cy_launch_shade_mc1(CY_SHADE_LAUNCHER_ARGS);
@@ -28,7 +28,7 @@ static inline void cy_launch_shade(int max_closures, CY_SHADE_LAUNCHER_ARGS)
             max_closures <= 2 ? cy_launch_shade_mc2 :
             max_closures <= 4 ? cy_launch_shade_mc4 :
                                 cy_launch_shade_mc8;
-  fn(grid, block, stream, kg, b, tile, queue_in, count_in, queue_out, count_out, shadow_queue, shadow_count, err);
+  fn(grid, block, stream, kg, b, tile, cam_n, slot_base, queue_in, count_in, queue_out, count_out, shadow_queue, shadow_count, err);
 }
 
 #endif

@@ -27,6 +27,8 @@
 __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_, CY_SHADE_VARIANT)(CyGlobals kg,
                                                      CyPathBuffers b,
                                                      CyTile tile,
+                                                     int cam_n,
+                                                     int slot_base,
                                                      const int *queue_in,
                                                      const uint *count_in,
                                                      int *queue_out,
@@ -58,9 +60,11 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_,
 #endif
   bool cont = false, shadow = false, finished = false;
   int slot = 0;
-  if (i < (int)*count_in) {
-    slot = queue_in[i];
-    cont = shade_path(&kg, &b, &tile, slot, mem, &shadow, &finished, err);
+  /* camera launch (cam_n > 0): slot slot_base + i, work item item_base + i */
+  if (cam_n > 0 ? i < cam_n : i < (int)*count_in) {
+    slot = cam_n > 0 ? slot_base + i : queue_in[i];
+    const uint cam_item = cam_n > 0 ? tile.item_base + (uint)i : CY_NO_ITEM;
+    cont = shade_path(&kg, &b, &tile, slot, cam_item, mem, &shadow, &finished, err);
   }
   __shared__ uint claim[CY_CLAIM_LDS];
   cont |= slot_refill(kg, b, tile, slot, finished, claim);
@@ -70,6 +74,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_,
 
 void CY_CAT(cy_launch_shade_, CY_SHADE_VARIANT)(CY_SHADE_LAUNCHER_ARGS)
 {
-  hipLaunchKernelGGL(CY_CAT(k_shade_, CY_SHADE_VARIANT), grid, block, 0, stream, kg, b, tile, queue_in, count_in,
+  hipLaunchKernelGGL(CY_CAT(k_shade_, CY_SHADE_VARIANT), grid, block, 0, stream, kg, b, tile, cam_n, slot_base,
+                     queue_in, count_in,
                      queue_out, count_out, shadow_queue, shadow_count, err);
 }

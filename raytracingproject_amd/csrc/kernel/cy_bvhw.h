@@ -14,8 +14,8 @@
  * distance with a small sorting network, the nearest visited next and the rest
  * pushed far-to-near with their entry distance (a popped entry farther than the
  * current hit is skipped).  Leaf children are stack entries too, so triangles
- * are tested in near-to-far order.  The first CY_LDS_STACKW entries of the
- * stack live in LDS, one column per thread.
+ * are tested in near-to-far order.  The newest CY_LDS_STACKW stack entries
+ * live in an LDS ring (CyStackW).
  *
  * Instancing: a leaf child with primitive count 0 is an object instance; the
  * ray moves to object space (bvh_instance_push, t scaled like the reference)
@@ -35,32 +35,63 @@
 #  define CY_LDS_STACKW 8
 #endif
 #define CY_BVHW_STACK 96
+/* request the next triangle's vertices before testing the current one */
+#ifndef CY_TRI_PREFETCH
+#  define CY_TRI_PREFETCH 1
+#endif
 
+/* Traversal stack of (child code, entry distance) pairs.  The newest
+ * CY_LDS_STACKW entries live in a ring in LDS (one column per thread: entry k
+ * of thread t at base[k * stride + t], conflict-free for 64 consecutive
+ * lanes); when the ring is full the oldest entry moves to a private overflow
+ * array and comes back only after the ring has drained.  Pushes and pops of the
+ * hot end of the stack therefore never touch scratch; the overflow array is
+ * used only by rays that keep more than CY_LDS_STACKW entries pending. */
 struct CyStackW {
-  int *lds_node; /* &lds_base[threadIdx.x] or nullptr */
-  float *lds_t;
-  int spill_node[CY_BVHW_STACK];
-  float spill_t[CY_BVHW_STACK];
-  CY_MFN void set(int i, int node, float t)
+  int *node;    /* ring: LDS column (device) or host array */
+  float *t;
+  int stride;   /* CY_BLOCK on the device, 1 on the host */
+  int top;      /* ring slot of the next push */
+  int n_ring;   /* valid ring entries (0 .. CY_LDS_STACKW) */
+  int n_over;   /* entries in the overflow array */
+  int over_node[CY_BVHW_STACK - CY_LDS_STACKW];
+  float over_t[CY_BVHW_STACK - CY_LDS_STACKW];
+
+  CY_MFN bool empty() const
   {
-    if (lds_node && i < CY_LDS_STACKW) {
-      lds_node[i * CY_BLOCK] = node;
-      lds_t[i * CY_BLOCK] = t;
-    }
-    else {
-      spill_node[i] = node;
-      spill_t[i] = t;
-    }
+    return n_ring == 0 && n_over == 0;
   }
-  CY_MFN void get(int i, int *node, float *t) const
+  /* returns false when the stack is full (CY_BVHW_STACK entries) */
+  CY_MFN bool push(int c, float et)
   {
-    if (lds_node && i < CY_LDS_STACKW) {
-      *node = lds_node[i * CY_BLOCK];
-      *t = lds_t[i * CY_BLOCK];
+    if (n_ring == CY_LDS_STACKW) {
+      /* the oldest ring entry sits at `top` (the ring is full) */
+      if (n_over == CY_BVHW_STACK - CY_LDS_STACKW) {
+        return false;
+      }
+      over_node[n_over] = node[top * stride];
+      over_t[n_over] = t[top * stride];
+      n_over++;
+      n_ring--;
+    }
+    node[top * stride] = c;
+    t[top * stride] = et;
+    top = (top + 1 == CY_LDS_STACKW) ? 0 : top + 1;
+    n_ring++;
+    return true;
+  }
+  CY_MFN void pop(int *c, float *et)
+  {
+    if (n_ring > 0) {
+      top = (top == 0) ? CY_LDS_STACKW - 1 : top - 1;
+      n_ring--;
+      *c = node[top * stride];
+      *et = t[top * stride];
     }
     else {
-      *node = spill_node[i];
-      *t = spill_t[i];
+      n_over--;
+      *c = over_node[n_over];
+      *et = over_t[n_over];
     }
   }
 };
@@ -124,9 +155,23 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
                           int *lds_stack = nullptr)
 {
   CyStackW stack;
-  stack.lds_node = lds_stack;
-  stack.lds_t = lds_stack ? (float *)(lds_stack + CY_LDS_STACKW * CY_BLOCK) : nullptr;
-  int sp = 0;
+#if !defined(__HIP_DEVICE_COMPILE__)
+  int host_ring[2 * CY_LDS_STACKW];
+  if (!lds_stack) {
+    stack.node = host_ring;
+    stack.t = (float *)(host_ring + CY_LDS_STACKW);
+    stack.stride = 1;
+  }
+  else
+#endif
+  {
+    stack.node = lds_stack;
+    stack.t = (float *)(lds_stack + CY_LDS_STACKW * CY_BLOCK);
+    stack.stride = CY_BLOCK;
+  }
+  stack.top = 0;
+  stack.n_ring = 0;
+  stack.n_over = 0;
 
   cfloat3 P = ray->P;
   cfloat3 dir = bvh_clamp_direction(ray->D);
@@ -189,11 +234,10 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
 #pragma unroll
       for (int s = W - 1; s >= 1; s--) {
         if (tn[s] != CY_INF) {
-          if (sp >= CY_BVHW_STACK) {
+          if (!stack.push(cc[s], tn[s])) {
             cy_set_error(err, CY_ERR_BVH_STACK, W);
             return false;
           }
-          stack.set(sp++, cc[s], tn[s]);
         }
       }
       code = cc[0];
@@ -210,11 +254,10 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
          * object space (bvh_instance_push); a -inf stack entry marks the exit */
         object = prim_addr;
         isect->t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect->t);
-        if (sp >= CY_BVHW_STACK) {
+        if (!stack.push(0, -CY_INF)) {
           cy_set_error(err, CY_ERR_BVH_STACK, W);
           return false;
         }
-        stack.set(sp++, 0, -CY_INF);
         code = kg->bvhw_object_root[object];
         continue;
       }
@@ -229,7 +272,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       for (; prim_addr < prim_end; prim_addr++) {
         n_tris++;
         hc_float4 w0 = v0, w1 = v1, w2 = v2;
-        if (prim_addr + 1 < prim_end) {
+        if (CY_TRI_PREFETCH && prim_addr + 1 < prim_end) {
           vi = ident ? 3u * (uint)(prim_addr + 1) : kg->__prim_tri_index[prim_addr + 1];
           w0 = kg->__prim_tri_verts[vi];
           w1 = kg->__prim_tri_verts[vi + 1];
@@ -254,17 +297,25 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
             }
           }
         }
-        v0 = w0;
-        v1 = w1;
-        v2 = w2;
+        if (CY_TRI_PREFETCH) {
+          v0 = w0;
+          v1 = w1;
+          v2 = w2;
+        }
+        else if (prim_addr + 1 < prim_end) {
+          vi = ident ? 3u * (uint)(prim_addr + 1) : kg->__prim_tri_index[prim_addr + 1];
+          v0 = kg->__prim_tri_verts[vi];
+          v1 = kg->__prim_tri_verts[vi + 1];
+          v2 = kg->__prim_tri_verts[vi + 2];
+        }
       }
     }
   pop:
     {
       bool found = false;
-      while (sp > 0) {
+      while (!stack.empty()) {
         float et;
-        stack.get(--sp, &code, &et);
+        stack.pop(&code, &et);
         if (INST && et == -CY_INF) {
           /* instance exit (bvh_instance_pop) */
           isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);

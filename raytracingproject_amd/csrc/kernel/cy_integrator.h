@@ -27,10 +27,10 @@
 /* Per-slot state, SoA of 16-byte records so every access is one dwordx4. */
 typedef struct CyPathBuffers {
   hc_float4 *ray_P;      /* P.xyz, ray t */
-  hc_float4 *ray_D;      /* D.xyz, (unused) */
-  hc_float4 *isect;      /* t, u, v, prim (bits) */
-  int *isect_type;       /* primitive type, 0 = miss */
-  int *isect_object;     /* instance object of the hit, OBJECT_NONE if not instanced */
+  hc_float4 *ray_D;      /* D.xyz, visibility (bits) */
+  hc_float4 *isect;      /* t, u, v, prim (bits); prim PRIM_NONE = miss, CY_PRIM_NO_RAY = no camera ray */
+  int *isect_type;       /* primitive type of a hit (written only by scenes with curves) */
+  int *isect_object;     /* instance object of the hit (written only by instanced scenes) */
   hc_uint4 *state0;      /* flag, rng_hash, rng_offset, sample */
   hc_uint4 *state1;      /* bounce, diffuse_bounce, glossy_bounce, transmission_bounce */
   hc_float4 *state2;     /* transparent_bounce (bits), min_ray_pdf, ray_pdf, ray_t */
@@ -42,6 +42,15 @@ typedef struct CyPathBuffers {
   uint *item;            /* work item of the path in the slot */
 } CyPathBuffers;
 
+/* One RenderTile of a multi-tile pass (hipcy_path_trace_tiles). */
+typedef struct CyTileDesc {
+  int x, y, w, h;
+  int offset, stride;
+  float *buffer;
+  uint px_begin; /* first pixel of the tile in the pass's pixel numbering */
+  int pad;
+} CyTileDesc;
+
 typedef struct CyTile {
   int x, y, w, h;
   int y_step; /* rows of the tile are image rows y, y+y_step, ... (1 = contiguous) */
@@ -50,8 +59,12 @@ typedef struct CyTile {
   float *buffer;
   int pass_stride;
   uint n_items;           /* w * h * (end_sample - start_sample) */
+  uint item_base;         /* first item of a camera launch: slot s holds item item_base + (s - slot_base) */
   uint *work_next;        /* next unclaimed item (atomic) */
   hc_float4 *samples_out; /* per item: L.xyz, alpha; alpha NaN = no camera ray */
+  uint npix;              /* pixels of the pass (w * h for one tile) */
+  int n_tiles;            /* > 1: the pass covers descs[0 .. n_tiles-1], pixels numbered tile by tile */
+  const CyTileDesc *descs;
 } CyTile;
 
 typedef struct CyStats {
@@ -309,21 +322,72 @@ CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float
   cy_st(&tile->samples_out[item], mkf4(L_sum.x, L_sum.y, L_sum.z, alpha));
 }
 
-/* Start work item `item` in the slot.  Returns false when the sample has no
- * camera ray (t == 0: no write, kernel_path.h:660-662); the caller then claims
- * another item. */
+#define CY_NO_ITEM 0xFFFFFFFFu
+#define CY_PRIM_NO_RAY (-2)
+
+/* Tile of pixel p in a multi-tile pass (binary search of the tiles' first pixels). */
+CY_FN int tile_of_pixel(const CyTile *tile, uint p)
+{
+  int lo = 0, hi = tile->n_tiles - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tile->descs[mid].px_begin <= p) {
+      lo = mid;
+    }
+    else {
+      hi = mid - 1;
+    }
+  }
+  return lo;
+}
+
+/* Image position of pixel p of the pass. */
+CY_FN void pass_pixel(const CyTile *tile, uint p, int *x, int *y)
+{
+  if (tile->n_tiles > 1) {
+    const CyTileDesc &d = tile->descs[tile_of_pixel(tile, p)];
+    const int local = (int)(p - d.px_begin);
+    *x = d.x + local % d.w;
+    *y = d.y + local / d.w;
+  }
+  else {
+    *x = tile->x + (int)p % tile->w;
+    *y = tile->y + ((int)p / tile->w) * tile->y_step;
+  }
+}
+
+/* Pixel and sample of a work item (items are numbered sample-major). */
+CY_FN void item_pixel(const CyTile *tile, uint item, int *x, int *y, int *sample)
+{
+  const uint p = item % tile->npix;
+  *sample = tile->start_sample + (int)(item / tile->npix);
+  pass_pixel(tile, p, x, y);
+}
+
+/* kernel_path_trace_setup (kernel_path_common.h:21-46) for a work item. */
+CY_FN void item_camera_ray(const CyGlobals *kg, const CyTile *tile, uint item, uint *rng_hash, int *sample, CyRay *ray)
+{
+  int x, y;
+  item_pixel(tile, item, &x, &y, sample);
+  camera_sample_ray(kg, x, y, *sample, rng_hash, ray);
+}
+
+CY_FN void write_no_sample(const CyTile *tile, uint item)
+{
+  cy_st(&tile->samples_out[item], mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf("")));
+}
+
+/* Start work item `item` in the slot (refills after the camera launch).
+ * Returns false when the sample has no camera ray (t == 0: no write,
+ * kernel_path.h:660-662); the caller then claims another item. */
 CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot, uint item)
 {
-  const uint npix = (uint)(tile->w * tile->h);
-  const int p = (int)(item % npix);
-  const int sample = tile->start_sample + (int)(item / npix);
-  const int x = tile->x + p % tile->w;
-  const int y = tile->y + (p / tile->w) * tile->y_step;
   uint rng_hash;
+  int sample;
   CyRay ray;
-  camera_sample_ray(kg, x, y, sample, &rng_hash, &ray);
+  item_camera_ray(kg, tile, item, &rng_hash, &sample, &ray);
   if (ray.t == 0.0f) {
-    cy_st(&tile->samples_out[item], mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf("")));
+    write_no_sample(tile, item);
     return false;
   }
   CyPathState s;
@@ -331,27 +395,106 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
   store_state(b, slot, &s);
   cy_st(&b->item[slot], item);
   cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
-  cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f));
+  cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(path_state_ray_visibility(&s))));
   cy_st(&b->throughput[slot], mkf4(1.0f, 1.0f, 1.0f, 0.0f));
   cy_st(&b->L[slot], mkf4(0.0f, 0.0f, 0.0f, 0.0f));
   return true;
 }
 
 /* Finish the path in a slot: record its sample; the slot then needs new work. */
-CY_FN void slot_finish(const CyPathBuffers *b, const CyTile *tile, int slot, cfloat3 L_emission, float L_transparent)
+CY_FN void slot_finish(const CyPathBuffers *b, const CyTile *tile, int slot, uint item, cfloat3 L_emission,
+                       float L_transparent)
 {
-  write_sample(tile, cy_ld(&b->item[slot]), L_emission, L_transparent);
+  write_sample(tile, item != CY_NO_ITEM ? item : cy_ld(&b->item[slot]), L_emission, L_transparent);
+}
+
+/* ---------------------------------------------------------------------------
+ * Stage 1 (closest hit), around the traversal.  A camera launch (cam_item !=
+ * CY_NO_ITEM) generates the work item's camera ray itself, so the first
+ * traversal of a path reads no slot state at all and nothing is written for it
+ * before its first shade.  Returns false when there is no ray to trace. */
+CY_FN bool closest_load(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot, uint cam_item,
+                        CyRay *ray, uint *visibility)
+{
+  if (cam_item != CY_NO_ITEM) {
+    uint rng_hash;
+    int sample;
+    item_camera_ray(kg, tile, cam_item, &rng_hash, &sample, ray);
+    CyPathState s;
+    path_state_init(kg, &s, rng_hash, sample);
+    *visibility = path_state_ray_visibility(&s);
+    return ray->t != 0.0f;
+  }
+  const hc_float4 rp = cy_ld(&b->ray_P[slot]);
+  const hc_float4 rd = cy_ld(&b->ray_D[slot]);
+  ray->P = mk3(rp.x, rp.y, rp.z);
+  ray->t = rp.w;
+  ray->D = mk3(rd.x, rd.y, rd.z);
+  *visibility = as_uint(rd.w);
+  return true;
+}
+
+template<bool INST>
+CY_FN void closest_store(const CyPathBuffers *b, int slot, bool has_ray, bool hit, const CyIsect *isect)
+{
+  if (hit) {
+    cy_st(&b->isect[slot], mkf4(isect->t, isect->u, isect->v, int_as_float(isect->prim)));
+    if (INST) {
+      cy_st(&b->isect_object[slot], isect->object);
+    }
+  }
+  else {
+    cy_st(&b->isect[slot], mkf4(0.0f, 0.0f, 0.0f, int_as_float(has_ray ? PRIM_NONE : CY_PRIM_NO_RAY)));
+  }
+}
+
+/* Stage 3 (shadow), around the any-hit traversal: the shadow ray of the slot. */
+CY_FN void shadow_load(const CyPathBuffers *b, int slot, CyRay *ray)
+{
+  const hc_float4 sp = cy_ld(&b->shadow_P[slot]);
+  const hc_float4 sdr = cy_ld(&b->shadow_D[slot]);
+  ray->P = mk3(sp.x, sp.y, sp.z);
+  ray->t = sp.w;
+  ray->D = mk3(sdr.x, sdr.y, sdr.z);
+}
+
+/* Deferred light add (path_radiance_accum_light) once occlusion is known;
+ * returns true when the path ended with this light sample and its sample was
+ * recorded. */
+CY_FN bool shadow_finish(const CyPathBuffers *b, const CyTile *tile, int slot, bool blocked)
+{
+  const hc_float4 sl = cy_ld(&b->shadow_L[slot]);
+  hc_float4 L4 = cy_ld(&b->L[slot]);
+  if (!blocked) {
+    L4.x = L4.x + sl.x;
+    L4.y = L4.y + sl.y;
+    L4.z = L4.z + sl.z;
+  }
+  if (sl.w != 0.0f) {
+    slot_finish(b, tile, slot, CY_NO_ITEM, mk3(L4.x, L4.y, L4.z), cy_ld(&b->throughput[slot]).w);
+    return true;
+  }
+  cy_st(&b->L[slot], L4);
+  return false;
 }
 
 /* Add pixel p's sample records to the render buffer in sample order
  * (kernel_write_pass_float4, kernel_write_passes.h:49-65, once per sample).
- * The tile's rows are stored contiguously in the buffer. */
+ * The tile's rows are stored contiguously in its buffer. */
 CY_FN void accumulate_pixel(const CyTile *tile, int p)
 {
-  const int npix = tile->w * tile->h;
-  const int x = tile->x + p % tile->w;
-  const int ybuf = tile->y + p / tile->w;
-  float *buf = tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
+  const int npix = (int)tile->npix;
+  float *buf;
+  if (tile->n_tiles > 1) {
+    const CyTileDesc &d = tile->descs[tile_of_pixel(tile, (uint)p)];
+    const int local = p - (int)d.px_begin;
+    buf = d.buffer + (size_t)(d.offset + d.x + local % d.w + (d.y + local / d.w) * d.stride) * tile->pass_stride;
+  }
+  else {
+    const int x = tile->x + p % tile->w;
+    const int ybuf = tile->y + p / tile->w;
+    buf = tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
+  }
   float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
   const int n = tile->end_sample - tile->start_sample;
   for (int k = 0; k < n; k++) {
@@ -380,6 +523,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
                       const CyPathBuffers *b,
                       const CyTile *tile,
                       int slot,
+                      uint cam_item,
                       CyShadeMem mem,
                       bool *shadow,
                       bool *finished,
@@ -387,28 +531,49 @@ CY_FN bool shade_path(const CyGlobals *kg,
 {
   *shadow = false;
   *finished = false;
+  const hc_float4 is4 = cy_ld(&b->isect[slot]);
   CyPathState state;
-  load_state(b, slot, &state, kg);
-  const hc_float4 rp = cy_ld(&b->ray_P[slot]);
-  const hc_float4 rd = cy_ld(&b->ray_D[slot]);
   CyRay ray;
-  ray.P = mk3(rp.x, rp.y, rp.z);
-  ray.t = rp.w;
-  ray.D = mk3(rd.x, rd.y, rd.z);
-  const hc_float4 tp4 = cy_ld(&b->throughput[slot]);
-  cfloat3 throughput = mk3(tp4.x, tp4.y, tp4.z);
-  float L_transparent = tp4.w;
-  const hc_float4 L4 = cy_ld(&b->L[slot]);
-  cfloat3 L = mk3(L4.x, L4.y, L4.z);
+  cfloat3 throughput, L;
+  float L_transparent;
+  if (cam_item != CY_NO_ITEM) {
+    /* first bounce of a camera launch: the path starts here (the closest
+     * stage traced the same camera ray) */
+    if (as_int(is4.w) == CY_PRIM_NO_RAY) {
+      write_no_sample(tile, cam_item);
+      *finished = true;
+      return false;
+    }
+    uint rng_hash;
+    int sample;
+    item_camera_ray(kg, tile, cam_item, &rng_hash, &sample, &ray);
+    path_state_init(kg, &state, rng_hash, sample);
+    throughput = mk3(1.0f, 1.0f, 1.0f);
+    L_transparent = 0.0f;
+    L = mk3(0.0f, 0.0f, 0.0f);
+  }
+  else {
+    load_state(b, slot, &state, kg);
+    const hc_float4 rp = cy_ld(&b->ray_P[slot]);
+    const hc_float4 rd = cy_ld(&b->ray_D[slot]);
+    ray.P = mk3(rp.x, rp.y, rp.z);
+    ray.t = rp.w;
+    ray.D = mk3(rd.x, rd.y, rd.z);
+    const hc_float4 tp4 = cy_ld(&b->throughput[slot]);
+    throughput = mk3(tp4.x, tp4.y, tp4.z);
+    L_transparent = tp4.w;
+    const hc_float4 L4 = cy_ld(&b->L[slot]);
+    L = mk3(L4.x, L4.y, L4.z);
+  }
 
-  const int type = cy_ld(&b->isect_type[slot]);
-  const bool hit = type != 0;
+  const bool hit = as_int(is4.w) != PRIM_NONE;
+  const int type = hit ? PRIMITIVE_TRIANGLE : 0;
 
   /* kernel_path_lamp_emission (kernel_path.h:86-113): lamps hit by the ray
    * segment since the last non-transparent bounce, MIS-weighted
    * (indirect_lamp_emission, kernel_emission.h:235-286) */
   if (KD->integrator.use_lamp_mis && !(state.flag & PATH_RAY_CAMERA)) {
-    const float isect_t = hit ? cy_ld(&b->isect[slot]).x : ray.t;
+    const float isect_t = hit ? is4.x : ray.t;
     const cfloat3 light_P = sub3(ray.P, mul3f(ray.D, state.ray_t));
     state.ray_t += isect_t;
     for (int lamp = 0; lamp < KD->integrator.num_all_lights; lamp++) {
@@ -443,8 +608,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     }
   }
 
-  bool cont = false;      /* path continues with a new ray */
-  bool finish_now = true; /* write result in this stage */
+  bool cont = false; /* path continues with a new ray */
 
   if (!hit) {
     /* kernel_path_background (kernel_path.h:115-144) */
@@ -490,7 +654,6 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
   else if (!path_state_ao_bounce(kg, &state)) {
     CyIsect isect;
-    const hc_float4 is4 = cy_ld(&b->isect[slot]);
     isect.t = is4.x;
     isect.u = is4.y;
     isect.v = is4.z;
@@ -700,10 +863,12 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
 
   if (cont) {
-    finish_now = false;
     store_state(b, slot, &state);
+    if (cam_item != CY_NO_ITEM) {
+      cy_st(&b->item[slot], cam_item);
+    }
     cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
-    cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, 0.0f));
+    cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(path_state_ray_visibility(&state))));
     cy_st(&b->throughput[slot], mkf4(throughput.x, throughput.y, throughput.z, L_transparent));
     cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, 0.0f));
     return true;
@@ -711,16 +876,17 @@ CY_FN bool shade_path(const CyGlobals *kg,
   if (*shadow) {
     /* the path ends after its pending light contribution: the shadow stage
      * adds it, writes the sample and regenerates the slot */
+    if (cam_item != CY_NO_ITEM) {
+      cy_st(&b->item[slot], cam_item);
+    }
     cy_st(&b->throughput[slot], mkf4(throughput.x, throughput.y, throughput.z, L_transparent));
     cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, 0.0f));
     hc_float4 sl = cy_ld(&b->shadow_L[slot]);
     sl.w = 1.0f;
     cy_st(&b->shadow_L[slot], sl);
-    store_state(b, slot, &state);
     return false;
   }
-  (void)finish_now;
-  slot_finish(b, tile, slot, L, L_transparent);
+  slot_finish(b, tile, slot, cam_item, L, L_transparent);
   *finished = true;
   return false;
 }

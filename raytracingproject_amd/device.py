@@ -156,6 +156,15 @@ class HIPDevice:
         else:
             self._check(self.lib.hipcy_path_trace_rows(self.h, ctypes.byref(wt), y_step))
 
+    def render_tiles(self, tiles, start_sample: int, num_samples: int) -> None:
+        """Several RenderTiles in one device pass (hipcy_path_trace_tiles): tiles is
+        a list of ((x, y, w, h), buffer_pointer, offset, stride)."""
+        arr = (native.WorkTile * len(tiles))()
+        for k, ((x, y, w, h), ptr, offset, stride) in enumerate(tiles):
+            arr[k] = native.WorkTile(x, y, w, h, start_sample, num_samples, offset, stride,
+                                     ptr if isinstance(ptr, int) else ptr.ptr)
+        self._check(self.lib.hipcy_path_trace_tiles(self.h, arr, len(tiles)))
+
     def render(self, samples: int | None = None, start_sample: int = 0, tile=None) -> np.ndarray:
         """Render (a tile of) the uploaded scene; returns the float render buffer
         [h, w, pass_stride] of the tile (buffer offset/stride as CPUDevice)."""

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # by `python -m raytracingproject_amd.build --variant NAME -D...`)
 DEVICE_LIB = os.environ.get("HIPCY_DEVICE_LIB") or os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
-ABI_VERSION = 2  # HIPCY_ABI_VERSION in include/hipcycles.h
+ABI_VERSION = 3  # HIPCY_ABI_VERSION in include/hipcycles.h
 
 
 def device_lib_path() -> str:
@@ -86,6 +86,7 @@ DEVICE_SYMBOLS = {
     "hipcy_get_bvh_layout_mask": (ctypes.c_uint32, [ctypes.c_void_p]),
     "hipcy_path_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile)]),
     "hipcy_path_trace_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.c_int]),
+    "hipcy_path_trace_tiles": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.c_int]),
     "hipcy_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

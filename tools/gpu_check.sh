@@ -23,7 +23,7 @@ step() {
 
 MODE=${1:-all}
 if [[ $MODE == all || $MODE == test ]]; then
-  step pytest_gpu 900 python -m pytest tests -x -q -m gpu -s
+  step pytest_gpu 900 python -u -m pytest tests -x -q -m gpu -s --timeout 300 --timeout-method thread
   step smoke 300 python __graft_entry__.py smoke
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
@@ -31,7 +31,7 @@ if [[ $MODE == all || $MODE == bench ]]; then
   step bench 900 python bench.py --steps 3 --warmup 1 --save gpurun_out/bmw.png
 fi
 if [[ $MODE == quick ]]; then
-  step pytest_gpu 900 python -m pytest tests -x -q -m gpu
+  step pytest_gpu 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
   step bench_w8 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bvh-width 8
   step bench_w2 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bvh-width 2
 fi

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
 if [[ ${SKIP_TESTS:-0} != 1 ]]; then
-  timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_gpu.log
   if fatal $rc; then exit $rc; fi
 fi

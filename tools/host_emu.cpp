@@ -206,6 +206,9 @@ extern "C" int emu_render(const void *data,
   tile.y = ty;
   tile.w = tw;
   tile.h = th;
+  tile.npix = (uint)(tw * th);
+  tile.n_tiles = 1;
+  tile.descs = nullptr;
   tile.y_step = 1;
   tile.start_sample = start_sample;
   tile.end_sample = start_sample + num_samples;
@@ -218,31 +221,23 @@ extern "C" int emu_render(const void *data,
   std::vector<hc_float4> records(tile.n_items);
   tile.samples_out = records.data();
   /* one slot, items in order: the device runs the same per-item code with
-   * many slots in flight; the result per item does not depend on the slot */
+   * many slots in flight; the result per item does not depend on the slot.
+   * Each item starts as in the device's camera launch (cam_item set for its
+   * first closest and shade stages). */
   for (uint item = 0; item < tile.n_items; item++) {
-    bool active = slot_start(&kg, &b, &tile, 0, item);
+    uint cam_item = item;
+    bool active = true;
     while (active) {
       /* k_intersect_closest */
       CyRay ray;
-      ray.P = mk3(rec[0].x, rec[0].y, rec[0].z);
-      ray.t = rec[0].w;
-      ray.D = mk3(rec[1].x, rec[1].y, rec[1].z);
-      CyPathState s;
-      s.flag = (int)s0.x;
-      uint visibility = path_state_ray_visibility(&s);
+      uint visibility;
+      const bool has_ray = closest_load(&kg, &b, &tile, 0, cam_item, &ray, &visibility);
       CyIsect isect;
       bool hit = false;
-      if (scene_intersect_valid(&ray)) {
+      if (has_ray && scene_intersect_valid(&ray)) {
         hit = emu_traverse<false>(&kg, &ray, visibility, &isect, &err, nullptr, nullptr, nullptr);
       }
-      if (hit) {
-        rec[2] = mkf4(isect.t, isect.u, isect.v, int_as_float(isect.prim));
-        isect_type = isect.type;
-        isect_object = isect.object;
-      }
-      else {
-        isect_type = 0;
-      }
+      closest_store<true>(&b, 0, has_ray, hit, &isect);
       /* k_shade */
       bool shadow = false, finished = false;
       CyClosure closure[CY_MAX_CLOSURE];
@@ -253,31 +248,18 @@ extern "C" int emu_render(const void *data,
       mem.svm_stride = 1;
       mem.svm_fast = CY_SVM_STACK;
       mem.svm_spill = nullptr;
-      bool cont = shade_path(&kg, &b, &tile, 0, mem, &shadow, &finished, &err);
+      bool cont = shade_path(&kg, &b, &tile, 0, cam_item, mem, &shadow, &finished, &err);
+      cam_item = CY_NO_ITEM;
       if (shadow) {
         /* k_intersect_shadow */
         CyRay sr;
-        sr.P = mk3(rec[6].x, rec[6].y, rec[6].z);
-        sr.t = rec[6].w;
-        sr.D = mk3(rec[7].x, rec[7].y, rec[7].z);
+        shadow_load(&b, 0, &sr);
         bool blocked = false;
         if (scene_intersect_valid(&sr)) {
           CyIsect si;
           blocked = emu_traverse<true>(&kg, &sr, PATH_RAY_SHADOW_OPAQUE, &si, &err, nullptr, nullptr, nullptr);
         }
-        hc_float4 sl = rec[8];
-        hc_float4 L4 = rec[5];
-        if (!blocked) {
-          L4.x = L4.x + sl.x;
-          L4.y = L4.y + sl.y;
-          L4.z = L4.z + sl.z;
-        }
-        if (sl.w != 0.0f) {
-          slot_finish(&b, &tile, 0, mk3(L4.x, L4.y, L4.z), rec[4].w);
-        }
-        else {
-          rec[5] = L4;
-        }
+        shadow_finish(&b, &tile, 0, blocked);
       }
       active = cont;
     }
