@@ -254,9 +254,138 @@ def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
                     filter_width=1.5, name="bmw27_standin")
 
 
+def _cylinder(radius, height, n, caps=True):
+    """Cylinder along +y from y=0 to y=height (object space)."""
+    ang = np.linspace(0, 2 * math.pi, n, endpoint=False)
+    ring = np.stack([radius * np.cos(ang), np.zeros(n), radius * np.sin(ang)], axis=-1)
+    verts = np.concatenate([ring, ring + np.array([0.0, height, 0.0])])
+    t = []
+    for i in range(n):
+        i1 = (i + 1) % n
+        t += [[i, n + i1, i1], [i, n + i, n + i1]]
+    if caps:
+        base = len(verts)
+        verts = np.concatenate([verts, [[0.0, 0.0, 0.0], [0.0, height, 0.0]]])
+        for i in range(n):
+            i1 = (i + 1) % n
+            t += [[base, i, i1], [base + 1, n + i1, n + i]]
+    return verts.astype(np.float32), np.array(t, dtype=np.int64)
+
+
+def _merge(parts, shaders):
+    """One mesh from several (verts, tris) parts with a material per part."""
+    vs, ts, sh = [], [], []
+    base = 0
+    for (v, t), s in zip(parts, shaders):
+        vs.append(v)
+        ts.append(t + base)
+        sh.append(np.full(len(t), s, dtype=np.int64))
+        base += len(v)
+    return np.concatenate(vs).astype(np.float32), np.concatenate(ts), np.concatenate(sh)
+
+
+def barbershop_standin(width=1920, height=1080, samples=512, detail=1.0) -> sc.Scene:
+    """Barbershop-class interior stand-in (SURVEY.md §8(d) config BBS): a room
+    furnished with INSTANCED props (barber chairs, bottles on shelves, ceiling
+    lamp fittings) lit by point and area lamps plus emissive strips; glossy
+    mirrors, glass bottles, chrome, tiled floor.  Generator seed 0x5EED + 3."""
+    rng = np.random.default_rng(0x5EED + 3)
+    d = detail
+    wall = sc.diffuse((0.62, 0.58, 0.5))
+    tile_a = sc.mix(0.3, sc.diffuse((0.85, 0.85, 0.82)), sc.glossy((0.9, 0.9, 0.9), 0.1))
+    tile_b = sc.mix(0.3, sc.diffuse((0.08, 0.08, 0.09)), sc.glossy((0.9, 0.9, 0.9), 0.1))
+    mirror = sc.glossy((0.92, 0.92, 0.92), 0.0)
+    chrome = sc.glossy((0.8, 0.8, 0.82), 0.12)
+    leather = sc.mix(0.2, sc.diffuse((0.45, 0.06, 0.05)), sc.glossy((0.6, 0.6, 0.6), 0.3))
+    wood = sc.mix(0.15, sc.diffuse((0.35, 0.2, 0.1)), sc.glossy((0.5, 0.5, 0.5), 0.25))
+    bottle = sc.glass((0.7, 0.9, 0.8), 0.05, 1.5)
+    strip = sc.emission((1.0, 0.9, 0.75), 3.0)
+    ceiling = sc.diffuse((0.8, 0.8, 0.78))
+    materials = [wall, tile_a, tile_b, mirror, chrome, leather, wood, bottle, strip, ceiling]
+    W_, H_, D_ = 8.0, 3.2, 6.0
+    meshes = []
+    # tiled floor: n x n checker of quads (geometry, no textures)
+    n = max(4, int(24 * d))
+    fv, ft, fs = [], [], []
+    for j in range(n):
+        for i in range(n):
+            x0, x1 = W_ * i / n, W_ * (i + 1) / n
+            z0, z1 = D_ * j / n, D_ * (j + 1) / n
+            base = len(fv)
+            fv += [(x0, 0, z0), (x0, 0, z1), (x1, 0, z1), (x1, 0, z0)]
+            ft += [[base, base + 1, base + 2], [base, base + 2, base + 3]]
+            fs += [1 + (i + j) % 2] * 2
+    meshes.append(sc.Mesh(np.array(fv, np.float32), np.array(ft), shader=np.array(fs)))
+    meshes.append(sc.Mesh(*_quad((0, H_, 0), (W_, H_, 0), (W_, H_, D_), (0, H_, D_)), shader=9))  # ceiling
+    meshes.append(sc.Mesh(*_quad((0, 0, D_), (W_, 0, D_), (W_, H_, D_), (0, H_, D_)), shader=0))  # back
+    meshes.append(sc.Mesh(*_quad((0, 0, 0), (0, 0, D_), (0, H_, D_), (0, H_, 0)), shader=0))  # left
+    meshes.append(sc.Mesh(*_quad((W_, 0, 0), (W_, H_, 0), (W_, H_, D_), (W_, 0, D_)), shader=0))  # right
+    meshes.append(sc.Mesh(*_quad((0, 0, 0), (W_, 0, 0), (W_, H_, 0), (0, H_, 0)), shader=0))  # front (behind camera)
+    # mirrors along the back wall, counter below them, emissive strips above
+    for k in range(4):
+        x = 1.0 + 1.8 * k
+        meshes.append(sc.Mesh(*_quad((x, 1.1, D_ - 0.02), (x + 1.3, 1.1, D_ - 0.02), (x + 1.3, 2.3, D_ - 0.02),
+                                     (x, 2.3, D_ - 0.02)), shader=3))
+        meshes.append(sc.Mesh(*_quad((x, 2.45, D_ - 0.05), (x + 1.3, 2.45, D_ - 0.05), (x + 1.3, 2.55, D_ - 0.05),
+                                     (x, 2.55, D_ - 0.05)), shader=8))
+    meshes.append(sc.Mesh(*_box((W_ / 2, 0.45, D_ - 0.35), (W_ - 0.6, 0.9, 0.6)), shader=6))
+    # barber chair (one geometry, instanced 4 times): base pole, seat, back, arms, footrest
+    m = max(12, int(96 * d))
+    cv, ct, cs = _merge([
+        _cylinder(0.28, 0.05, m),
+        _cylinder(0.06, 0.45, m // 2),
+        _ellipsoid((0, 0.55, 0), (0.3, 0.1, 0.28), m, m // 2),
+        _box((0, 0.95, -0.27), (0.5, 0.7, 0.1), 0.0),
+        _box((-0.3, 0.7, 0.0), (0.08, 0.06, 0.5), 0.0),
+        _box((0.3, 0.7, 0.0), (0.08, 0.06, 0.5), 0.0),
+        _torus((0, 0, 0), 0.2, 0.025, m, m // 4),
+    ], [4, 4, 5, 5, 4, 4, 4])
+    # torus lies in xy; move it to a footrest in front of the chair
+    chair = sc.Mesh(cv, ct, shader=cs, smooth=False)
+    # bottle (instanced on the shelves): body + neck
+    bv, bt, bs = _merge([_cylinder(0.04, 0.18, m // 2), _cylinder(0.015, 0.08, m // 4)], [7, 7])
+    bv = bv.copy()
+    bv[len(_cylinder(0.04, 0.18, m // 2)[0]):, 1] += 0.18
+    bottle_mesh = sc.Mesh(bv, bt, shader=bs)
+    # lamp fitting (instanced): a chrome shade
+    lv, lt = _ellipsoid((0, 0, 0), (0.18, 0.1, 0.18), m, m // 2)
+    lamp_mesh = sc.Mesh(lv, lt, shader=4, smooth=True)
+    instances = []
+    for k in range(4):
+        instances.append(sc.Instance(chair, _tfm((1.65 + 1.8 * k, 0.0, D_ - 1.6), math.pi + 0.15 * (k - 1.5))))
+    n_bottles = max(8, int(180 * d))
+    for k in range(n_bottles):
+        shelf = k % 3
+        x = 0.6 + (W_ - 1.2) * (k // 3) / max(1, n_bottles // 3) + 0.03 * rng.standard_normal()
+        y = 1.0 + 0.0 * shelf if shelf == 0 else (0.9 + 0.0)
+        y = 0.9 if shelf == 0 else (2.65 if shelf == 1 else 0.9)
+        z = D_ - 0.25 - 0.12 * shelf + 0.02 * rng.standard_normal()
+        s = 0.8 + 0.5 * rng.random()
+        instances.append(sc.Instance(bottle_mesh, _tfm((x, y, z), float(rng.random() * 6.28), (s, s * (0.8 + 0.6 * rng.random()), s))))
+    lamps = []
+    for k in range(6):
+        x = 1.0 + (W_ - 2.0) * (k % 3) / 2.0
+        z = 1.5 + 2.5 * (k // 3)
+        instances.append(sc.Instance(lamp_mesh, _tfm((x, H_ - 0.25, z), 0.0)))
+        lamps.append(sc.Lamp("point", co=(x, H_ - 0.45, z), size=0.06, color=(1.0, 0.85, 0.65), strength=25.0))
+    lamps.append(sc.Lamp("area", co=(W_ / 2, H_ - 0.01, D_ / 2), direction=(0.0, -1.0, 0.0), axisu=(1.0, 0.0, 0.0),
+                         axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=2.0, sizev=1.0, color=(0.9, 0.95, 1.0),
+                         strength=30.0))
+    lamps.append(sc.Lamp("area", co=(0.02, 1.6, 2.0), direction=(1.0, 0.0, 0.0), axisu=(0.0, 1.0, 0.0),
+                         axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=1.2, sizev=2.0, color=(1.0, 0.95, 0.85),
+                         strength=20.0))
+    cam = sc.Camera(eye=(W_ * 0.5, 1.55, 0.35), target=(W_ * 0.55, 1.2, D_), up=(0.0, 1.0, 0.0),
+                    fov=math.radians(60.0), nearclip=0.05, farclip=100.0)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.0, 0.0, 0.0), world_strength=0.0,
+                    samples=samples, filter_type="blackman_harris", filter_width=1.5, lamps=lamps,
+                    instances=instances, max_bounce=12, max_diffuse_bounce=4, max_glossy_bounce=12,
+                    max_transmission_bounce=12, name="barbershop_standin")
+
+
 CONFIGS = {
     "cornell_lamps": cornell_lamps,
     "cornell_instanced": cornell_instanced,
     "cornell_box": cornell_box,
     "bmw27_standin": bmw27_standin,
+    "barbershop_standin": barbershop_standin,
 }
