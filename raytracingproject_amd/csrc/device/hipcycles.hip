@@ -33,19 +33,27 @@
 #define CY_STATS_SHARDS 64
 
 template<int W> struct LdsStack {
-  static constexpr int ints = W > 2 ? 2 * CY_LDS_STACKW * CY_BLOCK : CY_LDS_STACK * CY_BLOCK;
+  using T = CyStackEntry; /* ring of (child code, entry distance) */
+  static constexpr int n = CY_LDS_STACKW * CY_BLOCK;
+};
+template<> struct LdsStack<2> {
+  using T = int; /* node addresses */
+  static constexpr int n = CY_LDS_STACK * CY_BLOCK;
 };
 
+/* lds: this thread's column of the workgroup's __shared__ stack array */
 template<int W, bool any_hit, bool INST = true>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
-                                               uint *n_tris, int *lds)
+                                               uint *n_tris, typename LdsStack<W>::T *lds)
 {
   if constexpr (W > 2) {
-    return bvhw_intersect<W, any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+    return bvhw_intersect<W, any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
+                                            (CY_LDS CyStackEntry *)lds);
   }
   else {
-    return bvh2_intersect<any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, lds);
+    return bvh2_intersect<any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
+                                         (CY_LDS int *)lds);
   }
 }
 
@@ -96,7 +104,11 @@ __device__ __forceinline__ void stats_block_add(CyStats *shard, uint n_nodes, ui
 
 /* Stage 1: closest hit for every queued path, or (cam_n > 0) for the camera
  * rays of the work items item_base .. item_base + cam_n - 1 held by slots
- * slot_base .. slot_base + cam_n - 1. */
+ * slot_base .. slot_base + cam_n - 1.  One ray per thread: a persistent variant
+ * whose lanes take the next ray of a per-workgroup pool when theirs finishes
+ * (ray replacement) was measured 2x slower on the BMW stand-in (the refill path
+ * with camera-ray generation inside the traversal loop spills at the 80-VGPR
+ * budget, and replacement rays break the camera rays' fetch coherence). */
 template<bool STATS, int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
@@ -109,7 +121,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
                                                                  CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[LdsStack<W>::ints];
+  __shared__ typename LdsStack<W>::T lds_stack[LdsStack<W>::n];
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   const bool active = cam_n > 0 ? i < cam_n : i < (int)*counter;
   if (active) {
@@ -144,7 +156,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
                                                                 CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[LdsStack<W>::ints];
+  __shared__ typename LdsStack<W>::T lds_stack[LdsStack<W>::n];
   bool finished = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
@@ -172,7 +184,7 @@ template<int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ int lds_stack[LdsStack<W>::ints];
+  __shared__ typename LdsStack<W>::T lds_stack[LdsStack<W>::n];
   if (i >= n) {
     return;
   }
@@ -1076,8 +1088,8 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   }
   {
     auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0);
-    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, ln.q[qa], ln.cnt + qa,
-                       err, dev->stats_dev);
+    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, ln.q[qa],
+                       ln.cnt + qa, err, dev->stats_dev);
   }
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));

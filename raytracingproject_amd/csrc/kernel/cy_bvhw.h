@@ -15,7 +15,7 @@
  * pushed far-to-near with their entry distance (a popped entry farther than the
  * current hit is skipped).  Leaf children are stack entries too, so triangles
  * are tested in near-to-far order.  The newest CY_LDS_STACKW stack entries
- * live in an LDS ring (CyStackW).
+ * live in an LDS ring (below).
  *
  * Instancing: a leaf child with primitive count 0 is an object instance; the
  * ray moves to object space (bvh_instance_push, t scaled like the reference)
@@ -24,7 +24,10 @@
  * the instance are object-space, compared with the object-space hit t.
  * Because a different visiting order scales t through a different sequence of
  * instances, hit distances can differ from the BVH2 traversal's in the last
- * ulp on instanced scenes (tests bound the film difference there).
+ * ulp on instanced scenes (about 0.1 % of camera rays on cornell_instanced;
+ * tests bound the film difference there).  Keeping the world-space t across
+ * instances that produce no hit was tried and matches the reference less often
+ * (the reference's own t carries the round trips of its visiting order).
  */
 #ifndef CY_BVHW_H
 #define CY_BVHW_H
@@ -41,60 +44,48 @@
 #endif
 
 /* Traversal stack of (child code, entry distance) pairs.  The newest
- * CY_LDS_STACKW entries live in a ring in LDS (one column per thread: entry k
- * of thread t at base[k * stride + t], conflict-free for 64 consecutive
- * lanes); when the ring is full the oldest entry moves to a private overflow
- * array and comes back only after the ring has drained.  Pushes and pops of the
- * hot end of the stack therefore never touch scratch; the overflow array is
- * used only by rays that keep more than CY_LDS_STACKW entries pending. */
-struct CyStackW {
-  int *node;    /* ring: LDS column (device) or host array */
-  float *t;
-  int stride;   /* CY_BLOCK on the device, 1 on the host */
-  int top;      /* ring slot of the next push */
-  int n_ring;   /* valid ring entries (0 .. CY_LDS_STACKW) */
-  int n_over;   /* entries in the overflow array */
-  int over_node[CY_BVHW_STACK - CY_LDS_STACKW];
-  float over_t[CY_BVHW_STACK - CY_LDS_STACKW];
+ * CY_LDS_STACKW entries live in a ring in LDS: entry k of thread t is the
+ * 8-byte CyStackEntry at ring[k * CY_BLOCK + t] (one ds_write_b64 /
+ * ds_read_b64 per push / pop, conflict-free for 64 consecutive lanes).  When
+ * the ring is full its oldest entry moves to a private overflow array and comes
+ * back only after the ring has drained, so only rays keeping more than
+ * CY_LDS_STACKW entries pending ever touch scratch.
+ *
+ * The ring position and counts are plain locals of the traversal function
+ * (never members of an object whose address is taken), and the overflow arrays
+ * are separate allocas: the compiler keeps the counters in registers and only
+ * the dynamically indexed overflow arrays live in scratch. */
+#if (CY_LDS_STACKW & (CY_LDS_STACKW - 1)) != 0
+#  error "CY_LDS_STACKW must be a power of two"
+#endif
+#define CY_OVER_STACK (CY_BVHW_STACK - CY_LDS_STACKW)
+#if defined(__HIP_DEVICE_COMPILE__)
+#  define CY_RING_STRIDE CY_BLOCK
+#else
+#  define CY_RING_STRIDE 1
+#endif
 
-  CY_MFN bool empty() const
-  {
-    return n_ring == 0 && n_over == 0;
-  }
-  /* returns false when the stack is full (CY_BVHW_STACK entries) */
-  CY_MFN bool push(int c, float et)
-  {
-    if (n_ring == CY_LDS_STACKW) {
-      /* the oldest ring entry sits at `top` (the ring is full) */
-      if (n_over == CY_BVHW_STACK - CY_LDS_STACKW) {
-        return false;
-      }
-      over_node[n_over] = node[top * stride];
-      over_t[n_over] = t[top * stride];
-      n_over++;
-      n_ring--;
-    }
-    node[top * stride] = c;
-    t[top * stride] = et;
-    top = (top + 1 == CY_LDS_STACKW) ? 0 : top + 1;
-    n_ring++;
-    return true;
-  }
-  CY_MFN void pop(int *c, float *et)
-  {
-    if (n_ring > 0) {
-      top = (top == 0) ? CY_LDS_STACKW - 1 : top - 1;
-      n_ring--;
-      *c = node[top * stride];
-      *et = t[top * stride];
-    }
-    else {
-      n_over--;
-      *c = over_node[n_over];
-      *et = over_t[n_over];
-    }
-  }
-};
+/* returns false when the stack is full (CY_BVHW_STACK entries) */
+#define CY_STACK_PUSH(c_, t_) \
+  ([&]() -> bool { \
+    if (n_ring == CY_LDS_STACKW) { \
+      if (n_over == CY_OVER_STACK) { \
+        return false; \
+      } \
+      const CyStackEntry old = ring[top * CY_RING_STRIDE]; \
+      over_node[n_over] = old.node; \
+      over_t[n_over] = old.t; \
+      n_over++; \
+      n_ring--; \
+    } \
+    CyStackEntry e_; \
+    e_.node = (c_); \
+    e_.t = (t_); \
+    ring[top * CY_RING_STRIDE] = e_; \
+    top = (top + 1) & (CY_LDS_STACKW - 1); \
+    n_ring++; \
+    return true; \
+  }())
 
 CY_FN void bvhw_cswap(float &ta, int &ca, float &tb, int &cb)
 {
@@ -152,26 +143,21 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
                           uint *cnt_nodes,
                           uint *cnt_leaves,
                           uint *cnt_tris,
-                          int *lds_stack = nullptr)
+                          CY_LDS CyStackEntry *lds_ring = nullptr)
 {
-  CyStackW stack;
-#if !defined(__HIP_DEVICE_COMPILE__)
-  int host_ring[2 * CY_LDS_STACKW];
-  if (!lds_stack) {
-    stack.node = host_ring;
-    stack.t = (float *)(host_ring + CY_LDS_STACKW);
-    stack.stride = 1;
-  }
-  else
+  /* ring column of this thread (device) or a local array (host) */
+#if defined(__HIP_DEVICE_COMPILE__)
+  CY_LDS CyStackEntry *ring = lds_ring;
+#else
+  CyStackEntry host_ring[CY_LDS_STACKW];
+  CyStackEntry *ring = host_ring;
+  (void)lds_ring;
 #endif
-  {
-    stack.node = lds_stack;
-    stack.t = (float *)(lds_stack + CY_LDS_STACKW * CY_BLOCK);
-    stack.stride = CY_BLOCK;
-  }
-  stack.top = 0;
-  stack.n_ring = 0;
-  stack.n_over = 0;
+  int top = 0;    /* ring slot of the next push */
+  int n_ring = 0; /* valid ring entries (0 .. CY_LDS_STACKW) */
+  int n_over = 0; /* entries in the overflow arrays */
+  int over_node[CY_OVER_STACK];
+  float over_t[CY_OVER_STACK];
 
   cfloat3 P = ray->P;
   cfloat3 dir = bvh_clamp_direction(ray->D);
@@ -234,7 +220,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
 #pragma unroll
       for (int s = W - 1; s >= 1; s--) {
         if (tn[s] != CY_INF) {
-          if (!stack.push(cc[s], tn[s])) {
+          if (!CY_STACK_PUSH(cc[s], tn[s])) {
             cy_set_error(err, CY_ERR_BVH_STACK, W);
             return false;
           }
@@ -254,7 +240,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
          * object space (bvh_instance_push); a -inf stack entry marks the exit */
         object = prim_addr;
         isect->t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect->t);
-        if (!stack.push(0, -CY_INF)) {
+        if (!CY_STACK_PUSH(0, -CY_INF)) {
           cy_set_error(err, CY_ERR_BVH_STACK, W);
           return false;
         }
@@ -288,12 +274,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
             isect->v = vv;
             isect->t = tt;
             if (any_hit) {
-              if (cnt_nodes) {
-                *cnt_nodes += n_nodes;
-                *cnt_leaves += n_leaves;
-                *cnt_tris += n_tris;
-              }
-              return true;
+              goto ray_done;
             }
           }
         }
@@ -313,9 +294,26 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
   pop:
     {
       bool found = false;
-      while (!stack.empty()) {
-        float et;
-        stack.pop(&code, &et);
+      while (n_ring > 0 || n_over > 0) {
+        if (n_ring == 0) {
+          /* ring drained: move the newest overflow entries back into it (rare;
+           * pops then always read LDS, never a pointer that may be private) */
+          const int k = n_over < CY_LDS_STACKW ? n_over : CY_LDS_STACKW;
+          for (int j = n_over - k; j < n_over; j++) {
+            CyStackEntry e_;
+            e_.node = over_node[j];
+            e_.t = over_t[j];
+            ring[top * CY_RING_STRIDE] = e_;
+            top = (top + 1) & (CY_LDS_STACKW - 1);
+          }
+          n_over -= k;
+          n_ring = k;
+        }
+        top = (top - 1) & (CY_LDS_STACKW - 1);
+        n_ring--;
+        const CyStackEntry e = ring[top * CY_RING_STRIDE];
+        code = e.node;
+        const float et = e.t;
         if (INST && et == -CY_INF) {
           /* instance exit (bvh_instance_pop) */
           isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
@@ -328,9 +326,12 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
         }
       }
       if (!found) {
-        break;
+        goto ray_done;
       }
     }
+    continue;
+  ray_done:
+    break;
   }
 
   if (cnt_nodes) {

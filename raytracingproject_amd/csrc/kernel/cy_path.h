@@ -211,23 +211,9 @@ CY_FN bool scene_intersect_valid(const CyRay *ray)
  * at lds_base[i * CY_BLOCK + t]: 64 consecutive lanes hit 64 consecutive dwords,
  * conflict-free); deeper entries spill to a private array that is only touched
  * by rays descending more than CY_LDS_STACK levels below their stack bottom. */
-struct CyStack {
-  int *lds; /* &lds_base[threadIdx.x] or nullptr */
-  int spill[BVH_STACK_SIZE];
-  CY_MFN void set(int i, int v)
-  {
-    if (lds && i < CY_LDS_STACK) {
-      lds[i * CY_BLOCK] = v;
-    }
-    else {
-      spill[i] = v;
-    }
-  }
-  CY_MFN int get(int i) const
-  {
-    return (lds && i < CY_LDS_STACK) ? lds[i * CY_BLOCK] : spill[i];
-  }
-};
+/* The stack is a pair of locals of bvh2_intersect (an LDS column pointer and
+ * the private spill array), never an object whose address is taken, so the
+ * compiler keeps the pointer in a register and uses ds_* for the LDS part. */
 
 /* Object transforms (geom/geom_object.h:37-48): static objects only. */
 CY_FN const struct cy_tfm *object_tfm(const CyGlobals *kg, int object)
@@ -276,11 +262,19 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           uint *cnt_nodes,
                           uint *cnt_leaves,
                           uint *cnt_tris,
-                          int *lds_stack = nullptr)
+                          CY_LDS int *lds_stack = nullptr)
 {
-  CyStack traversal_stack;
-  traversal_stack.lds = lds_stack;
-  traversal_stack.set(0, ENTRYPOINT_SENTINEL);
+  int stack_spill[BVH_STACK_SIZE];
+  auto stack_set = [&](int i, int v) {
+    if (lds_stack && i < CY_LDS_STACK) {
+      lds_stack[i * CY_BLOCK] = v;
+    }
+    else {
+      stack_spill[i] = v;
+    }
+  };
+  auto stack_get = [&](int i) -> int { return (lds_stack && i < CY_LDS_STACK) ? lds_stack[i * CY_BLOCK] : stack_spill[i]; };
+  stack_set(0, ENTRYPOINT_SENTINEL);
   int stack_ptr = 0;
   int node_addr = KD->bvh.root;
   int object = OBJECT_NONE;
@@ -341,14 +335,14 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
             cy_set_error(err, CY_ERR_BVH_STACK, 0);
             return false;
           }
-          traversal_stack.set(stack_ptr, node_addr_child1);
+          stack_set(stack_ptr, node_addr_child1);
         }
         else {
           if (traverse_mask == 2) {
             node_addr = node_addr_child1;
           }
           else if (traverse_mask == 0) {
-            node_addr = traversal_stack.get(stack_ptr);
+            node_addr = stack_get(stack_ptr);
             --stack_ptr;
           }
         }
@@ -361,7 +355,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
         if (prim_addr >= 0) {
           const int prim_addr2 = as_int(leaf.y);
           const uint type = as_uint(leaf.w);
-          node_addr = traversal_stack.get(stack_ptr);
+          node_addr = stack_get(stack_ptr);
           --stack_ptr;
           if ((type & PRIMITIVE_ALL) == PRIMITIVE_TRIANGLE) {
             for (; prim_addr < prim_addr2; prim_addr++) {
@@ -407,7 +401,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
             cy_set_error(err, CY_ERR_BVH_STACK, 0);
             return false;
           }
-          traversal_stack.set(stack_ptr, ENTRYPOINT_SENTINEL);
+          stack_set(stack_ptr, ENTRYPOINT_SENTINEL);
           node_addr = (int)kg->__object_node[object];
         }
       }
@@ -417,7 +411,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
       /* instance pop (bvh_traversal.h:209-222) */
       isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
       object = OBJECT_NONE;
-      node_addr = traversal_stack.get(stack_ptr);
+      node_addr = stack_get(stack_ptr);
       --stack_ptr;
     }
   } while (node_addr != ENTRYPOINT_SENTINEL);

@@ -222,6 +222,20 @@ enum {
 #define CY_BLOCK 256
 #define CY_LDS_STACK 32
 
+/* LDS-qualified pointers: per-thread stacks and closure arrays carved out of a
+ * __shared__ array are addressed through these so the compiler emits ds_*
+ * instructions (a generic pointer would become flat_* accesses, which wait on
+ * the vector-memory counter too).  Plain pointers on the host. */
+#if defined(__HIP_DEVICE_COMPILE__)
+#  define CY_LDS __attribute__((address_space(3)))
+#else
+#  define CY_LDS
+#endif
+typedef struct __attribute__((aligned(8))) CyStackEntry {
+  int node;
+  float t;
+} CyStackEntry;
+
 typedef struct CyRay {
   cfloat3 P;
   cfloat3 D;
