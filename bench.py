@@ -297,7 +297,8 @@ def main():
                 "scene_upload_s": round(t_upload, 3),
             },
             "kernel_ms_per_frame": {k: round(v, 3) for k, v in kernels.items()},
-            "rays_per_frame": {"closest": counts["closest_rays"], "shadow": counts["shadow_rays"]},
+            "rays_per_frame": {"closest": counts["closest_rays"], "shadow": counts["shadow_rays"],
+                               "near_tie_retraced": counts["tie_rays"]},
             "mrays_per_s": round(rays * world * args.steps / elapsed / 1e6, 1),
             "film_checksum": float(np.float64(film[..., :4].sum())) if film is not None else None,
             "roofline": roofline,

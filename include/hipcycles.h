@@ -83,6 +83,7 @@ typedef struct hipcy_stats {
   int32_t bvh_width;      /* 2: BVH2 as bound; 4/8: device-widened wide BVH */
   int32_t bvh_depth;      /* levels of the wide BVH (0 for BVH2) */
   uint64_t bvh_bytes;     /* bytes of the traversed node array */
+  uint64_t tie_rays;      /* closest rays re-traced in the reference's order (near-ties) */
 } hipcy_stats;
 
 int hipcy_abi_version(void);

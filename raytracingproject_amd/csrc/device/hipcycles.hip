@@ -27,37 +27,48 @@
 /* Minimum waves per SIMD the traversal kernels are register-allocated for
  * (amdgpu_waves_per_eu); with the LDS stack it sets their occupancy. */
 #ifndef CY_TRAV_MIN_WAVES
-#  define CY_TRAV_MIN_WAVES 6
+#  define CY_TRAV_MIN_WAVES 5
 #endif
 
 #define CY_STATS_SHARDS 64
 
-template<int W> struct LdsStack {
-  using T = CyStackEntry; /* ring of (child code, entry distance) */
-  static constexpr int n = CY_LDS_STACKW * CY_BLOCK;
+/* LDS traversal stacks of one workgroup (one column per thread):
+ *   W = 2          BVH2 node addresses, CY_LDS_STACK deep;
+ *   W > 2          the wide traversal's ring of CY_LDS_STACKW entries, plus for
+ *                  instanced scenes the reference-order top level's BVH2 stack
+ *                  (CY_LDS_STACK_TOP deep; cy_path.h bvh2_intersect WI > 2). */
+#ifndef CY_LDS_STACK_TOP
+#  define CY_LDS_STACK_TOP 8
+#endif
+template<int W, bool INST> struct LdsStack {
+  CyStackEntry ring[CY_LDS_STACKW * CY_BLOCK];
+  int top[(INST ? CY_LDS_STACK_TOP : 1) * CY_BLOCK];
 };
-template<> struct LdsStack<2> {
-  using T = int; /* node addresses */
-  static constexpr int n = CY_LDS_STACK * CY_BLOCK;
+template<bool INST> struct LdsStack<2, INST> {
+  int top[CY_LDS_STACK * CY_BLOCK];
 };
 
-/* lds: this thread's column of the workgroup's __shared__ stack array */
 template<int W, bool any_hit, bool INST = true>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
-                                               uint *n_tris, typename LdsStack<W>::T *lds)
+                                               uint *n_tris, LdsStack<W, INST> *lds, bool *tie = nullptr)
 {
-  if constexpr (W > 2) {
-    return bvhw_intersect<W, any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
-                                            (CY_LDS CyStackEntry *)lds);
+  const int t = threadIdx.x;
+  if constexpr (W == 2) {
+    return bvh2_intersect<any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
+                                         (CY_LDS int *)(lds->top + t));
+  }
+  else if constexpr (INST) {
+    /* instanced scene: reference-order top level, wide BVH inside instances */
+    return bvh2_intersect<any_hit, true, W, CY_LDS_STACK_TOP>(kg, ray, visibility, isect, err, n_nodes, n_leaves,
+                                                               n_tris, (CY_LDS int *)(lds->top + t),
+                                                               (CY_LDS CyStackEntry *)(lds->ring + t), tie);
   }
   else {
-    return bvh2_intersect<any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
-                                         (CY_LDS int *)lds);
+    return bvhw_intersect<W, any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
+                                      (CY_LDS CyStackEntry *)(lds->ring + t), tie);
   }
 }
-
-
 
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
@@ -121,8 +132,8 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
                                                                  CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ typename LdsStack<W>::T lds_stack[LdsStack<W>::n];
-  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  __shared__ LdsStack<W, INST> lds_stack;
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
   const bool active = cam_n > 0 ? i < cam_n : i < (int)*counter;
   if (active) {
     const int slot = cam_n > 0 ? slot_base + i : queue[i];
@@ -131,15 +142,31 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
     uint visibility;
     const bool has_ray = closest_load(&kg, &b, &tile, slot, cam_item, &ray, &visibility);
     CyIsect isect;
-    bool hit = false;
+    bool hit = false, tie = false;
     if (has_ray && scene_intersect_valid(&ray)) {
       hit = scene_traverse<W, false, INST>(&kg, &ray, visibility, &isect, err,
-                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
+                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack, &tie);
+    }
+    if constexpr (W > 2) {
+      if (tie) {
+        /* near-tie (cy_bvhw.h bvhw_traverse): re-trace this ray with the bound
+         * BVH2 in the reference's visiting order, so the hit is the reference's
+         * bit for bit (about 1 ray in 3000 on the bench scene).  The first
+         * CY_LDS_STACKW entries of its stack reuse this thread's own ring column
+         * (the node word of each ring entry): other waves of the workgroup may
+         * still be traversing with theirs. */
+        hit = bvh2_intersect<false, INST, 2, CY_LDS_STACKW, 2 * CY_BLOCK>(
+            &kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr,
+            (CY_LDS int *)(lds_stack.ring + threadIdx.x));
+        if (STATS) {
+          n_ties++;
+        }
+      }
     }
     closest_store<INST>(&b, slot, has_ray, hit, &isect);
   }
   if (STATS) {
-    stats_block_add(stats, n_nodes, n_leaves, n_tris, 0);
+    stats_block_add(stats, n_nodes, n_leaves, n_tris, n_ties);
   }
 }
 
@@ -156,7 +183,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
                                                                 CyStats *stats)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ typename LdsStack<W>::T lds_stack[LdsStack<W>::n];
+  __shared__ LdsStack<W, INST> lds_stack;
   bool finished = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
@@ -168,7 +195,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
       blocked = scene_traverse<W, true, INST>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
-                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, lds_stack + threadIdx.x);
+                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack);
     }
     finished = shadow_finish(&b, &tile, slot, blocked);
   }
@@ -184,7 +211,7 @@ template<int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  __shared__ typename LdsStack<W>::T lds_stack[LdsStack<W>::n];
+  __shared__ LdsStack<W, true> lds_stack;
   if (i >= n) {
     return;
   }
@@ -206,10 +233,14 @@ __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const
     /* scene_intersect: shadow visibility means early exit at the first hit
      * (bvh_traversal.h:144-146) */
     if (any_hit || (visibility & PATH_RAY_SHADOW_OPAQUE)) {
-      hit = scene_traverse<W, true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
+      hit = scene_traverse<W, true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, &lds_stack);
     }
     else {
-      hit = scene_traverse<W, false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, lds_stack + threadIdx.x);
+      bool tie = false;
+      hit = scene_traverse<W, false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, &lds_stack, &tie);
+      if (tie) {
+        hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr);
+      }
     }
   }
   out_f[3 * i + 0] = isect.t;
@@ -1355,6 +1386,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     dev->stats.closest_nodes = st[0].nodes;
     dev->stats.closest_leaves = st[0].leaves;
     dev->stats.closest_tris = st[0].tris;
+    dev->stats.tie_rays = st[0].rays;
   }
   return check_device_error(dev);
 }

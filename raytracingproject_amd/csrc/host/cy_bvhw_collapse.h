@@ -369,6 +369,7 @@ struct Collapser {
   }
 };
 
+
 }  // namespace cybvhw
 
 #endif

@@ -17,17 +17,13 @@
  * are tested in near-to-far order.  The newest CY_LDS_STACKW stack entries
  * live in an LDS ring (below).
  *
- * Instancing: a leaf child with primitive count 0 is an object instance; the
- * ray moves to object space (bvh_instance_push, t scaled like the reference)
- * and continues at the object's own wide root; an entry with distance -inf
- * below it restores world space when popped.  Entry distances pushed inside
- * the instance are object-space, compared with the object-space hit t.
- * Because a different visiting order scales t through a different sequence of
- * instances, hit distances can differ from the BVH2 traversal's in the last
- * ulp on instanced scenes (about 0.1 % of camera rays on cornell_instanced;
- * tests bound the film difference there).  Keeping the world-space t across
- * instances that produce no hit was tried and matches the reference less often
- * (the reference's own t carries the round trips of its visiting order).
+ * Instancing: instanced scenes traverse the top level as the reference does
+ * (cy_path.h bvh2_intersect with WI = W: same visiting order, so the same
+ * sequence of bvh_instance_push/pop roundings of t) and each instance with its
+ * object's wide BVH (bvhw_traverse from bvhw_object_root).  A fully wide
+ * two-level traversal (instances in the wide top level) was measured first:
+ * its other order of entering instances changes t in the last ulp for about
+ * 0.1 % of camera rays, and renders then drift from the reference.
  */
 #ifndef CY_BVHW_H
 #define CY_BVHW_H
@@ -134,16 +130,51 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
   }
 }
 
-template<int W, bool any_hit, bool INST = true>
-CY_FN bool bvhw_intersect(const CyGlobals *kg,
-                          const CyRay *ray,
-                          uint visibility,
-                          CyIsect *isect,
-                          uint *err,
-                          uint *cnt_nodes,
-                          uint *cnt_leaves,
-                          uint *cnt_tris,
-                          CY_LDS CyStackEntry *lds_ring = nullptr)
+/* Near-tie window of the exact closest hit: hits within 2^-20 (about 8 ulps)
+ * of the best distance are kept as candidates and resolved in the reference's
+ * order at the end (bvhw_traverse). */
+#define CY_TIE_EPS (1.0f / 1048576.0f)
+/* 0: no near-tie detection (visiting-order ties resolved as they fall; for
+ * measuring its cost only) */
+#ifndef CY_EXACT_TIES
+#  define CY_EXACT_TIES 1
+#endif
+
+/* Traversal of the wide BVH from node `root` with the ray already in the space
+ * of that BVH (P, dir, idir; `object` = the instance it belongs to or
+ * OBJECT_NONE) and the current hit in *isect (its t bounds the query).  Hits
+ * found update *isect.  Returns true when it found a hit (for any_hit: at the
+ * first one).  The BVH holds no instance leaves: instanced scenes traverse their
+ * top level in reference order (cy_path.h bvh2_intersect, WI > 2) and call this
+ * per instance.
+ *
+ * Exact closest hit.  The reference visits triangles in its BVH2 order and
+ * accepts each one whose distance passes T <= t * den against the current t
+ * (util_math_intersect.h:178), so when several triangles lie at (nearly) the
+ * same distance -- shared edges, fan centres, coplanar faces -- the survivor
+ * depends on that order, on rounding, and on which of their boxes the
+ * reference's current t still admits.  Here hits are collected against the best
+ * distance widened by CY_TIE_EPS (boxes and stack entries culled against the
+ * same bound, so no such hit is missed) and *tie is set when two hits, or a hit
+ * and the incoming one, fall inside one window.  Only then can the order
+ * matter: the caller re-traces that ray with the reference-order BVH2 traversal
+ * (hipcycles.hip k_resolve_ties; about 1 ray in 10^4 on the bench scene).  Hits
+ * beyond the window lose in either order. */
+template<int W, bool any_hit>
+CY_FN bool bvhw_traverse(const CyGlobals *kg,
+                         int root,
+                         cfloat3 P,
+                         cfloat3 dir,
+                         cfloat3 idir,
+                         int object,
+                         uint visibility,
+                         CyIsect *isect,
+                         uint *err,
+                         uint *cnt_nodes,
+                         uint *cnt_leaves,
+                         uint *cnt_tris,
+                         CY_LDS CyStackEntry *lds_ring,
+                         bool *tie_out)
 {
   /* ring column of this thread (device) or a local array (host) */
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -158,23 +189,17 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
   int n_over = 0; /* entries in the overflow arrays */
   int over_node[CY_OVER_STACK];
   float over_t[CY_OVER_STACK];
+  bool found_hit = false;
 
-  cfloat3 P = ray->P;
-  cfloat3 dir = bvh_clamp_direction(ray->D);
-  cfloat3 idir = rcp3(dir);
-  int object = OBJECT_NONE;
-
-  isect->t = ray->t;
-  isect->u = 0.0f;
-  isect->v = 0.0f;
-  isect->prim = PRIM_NONE;
-  isect->object = OBJECT_NONE;
-  isect->type = 0;
+  bool tie = false; /* two hits inside the window of the current best */
+  /* culling bound: the best distance widened by the tie window (recomputed
+   * where used rather than kept in a register) */
+#define CY_T_CULL ((any_hit || !CY_EXACT_TIES) ? isect->t : isect->t * (1.0f + CY_TIE_EPS))
 
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
   constexpr int Q = W / 4; /* float4 per array */
-  int code = 0;            /* root: wide node 0 */
+  int code = root;
 
   while (true) {
     if (code >= 0) {
@@ -183,7 +208,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       const hc_float4 *np = nodes + (size_t)code * (8 * Q);
       float tn[W];
       int cc[W];
-      const float t = isect->t;
+      const float t = CY_T_CULL;
 #pragma unroll
       for (int q = 0; q < Q; q++) {
         const hc_float4 lx = np[0 * Q + q], hx = np[1 * Q + q];
@@ -222,7 +247,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
         if (tn[s] != CY_INF) {
           if (!CY_STACK_PUSH(cc[s], tn[s])) {
             cy_set_error(err, CY_ERR_BVH_STACK, W);
-            return false;
+            return found_hit;
           }
         }
       }
@@ -235,21 +260,9 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
       n_leaves++;
       const int packed = ~code;
       int prim_addr = packed >> 4;
-      if (INST && (packed & 15) == 0) {
-        /* instance leaf (count 0, index = object): enter the object's BVH in
-         * object space (bvh_instance_push); a -inf stack entry marks the exit */
-        object = prim_addr;
-        isect->t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect->t);
-        if (!CY_STACK_PUSH(0, -CY_INF)) {
-          cy_set_error(err, CY_ERR_BVH_STACK, W);
-          return false;
-        }
-        code = kg->bvhw_object_root[object];
-        continue;
-      }
-      if (!INST && (packed & 15) == 0) {
-        cy_set_error(err, CY_ERR_FEATURE, 1); /* instance leaf in a kernel built without instancing */
-        return false;
+      if ((packed & 15) == 0) {
+        cy_set_error(err, CY_ERR_FEATURE, 1); /* instance leaf: traversed by bvh2_intersect<.., WI> */
+        return found_hit;
       }
       const int prim_end = prim_addr + (packed & 15);
       const bool ident = kg->tri_index_identity != 0;
@@ -265,17 +278,33 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
           w2 = kg->__prim_tri_verts[vi + 2];
         }
         float tt, uu, vv;
-        if (ray_triangle_intersect(P, dir, isect->t, f4to3(v0), f4to3(v1), f4to3(v2), &uu, &vv, &tt)) {
-          if (kg->__prim_visibility[prim_addr] & visibility) {
+        bool exact_ok;
+        if (ray_triangle_intersect2(P, dir, CY_T_CULL, isect->t, f4to3(v0), f4to3(v1), f4to3(v2), &uu, &vv, &tt,
+                                    &exact_ok) &&
+            (kg->__prim_visibility[prim_addr] & visibility)) {
+          if (any_hit) {
             isect->prim = prim_addr;
             isect->object = object;
             isect->type = PRIMITIVE_TRIANGLE;
             isect->u = uu;
             isect->v = vv;
             isect->t = tt;
-            if (any_hit) {
-              goto ray_done;
-            }
+            found_hit = true;
+            goto ray_done;
+          }
+          /* a second hit at (nearly) the distance of the current one -- of this
+           * call or the incoming hit -- makes the result depend on the visiting
+           * order: flag the ray; a hit clearly below the current one clears it */
+          tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
+          if (exact_ok) {
+            /* the reference's acceptance test at the exact bound */
+            isect->prim = prim_addr;
+            isect->object = object;
+            isect->type = PRIMITIVE_TRIANGLE;
+            isect->u = uu;
+            isect->v = vv;
+            isect->t = tt;
+            found_hit = true;
           }
         }
         if (CY_TRI_PREFETCH) {
@@ -313,14 +342,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
         n_ring--;
         const CyStackEntry e = ring[top * CY_RING_STRIDE];
         code = e.node;
-        const float et = e.t;
-        if (INST && et == -CY_INF) {
-          /* instance exit (bvh_instance_pop) */
-          isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
-          object = OBJECT_NONE;
-          continue;
-        }
-        if (et <= isect->t) {
+        if (e.t <= CY_T_CULL) {
           found = true;
           break;
         }
@@ -334,12 +356,42 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
     break;
   }
 
+#undef CY_T_CULL
+  if (tie_out && tie) {
+    *tie_out = true;
+  }
   if (cnt_nodes) {
     *cnt_nodes += n_nodes;
     *cnt_leaves += n_leaves;
     *cnt_tris += n_tris;
   }
-  return (isect->prim != PRIM_NONE);
+  return found_hit;
+}
+
+/* Closest hit (any_hit == false) or opaque-shadow any hit over a scene without
+ * instances with the wide BVH: scene_intersect (bvh/bvh.h:154-237). */
+template<int W, bool any_hit>
+CY_FN bool bvhw_intersect(const CyGlobals *kg,
+                          const CyRay *ray,
+                          uint visibility,
+                          CyIsect *isect,
+                          uint *err,
+                          uint *cnt_nodes,
+                          uint *cnt_leaves,
+                          uint *cnt_tris,
+                          CY_LDS CyStackEntry *lds_ring = nullptr,
+                          bool *tie = nullptr)
+{
+  isect->t = ray->t;
+  isect->u = 0.0f;
+  isect->v = 0.0f;
+  isect->prim = PRIM_NONE;
+  isect->object = OBJECT_NONE;
+  isect->type = 0;
+  const cfloat3 dir = bvh_clamp_direction(ray->D);
+  bvhw_traverse<W, any_hit>(kg, 0, ray->P, dir, rcp3(dir), OBJECT_NONE, visibility, isect, err, cnt_nodes,
+                            cnt_leaves, cnt_tris, lds_ring, tie);
+  return isect->prim != PRIM_NONE;
 }
 
 #endif /* CY_BVHW_H */

@@ -155,15 +155,20 @@ CY_FN cfloat3 bvh_clamp_direction(cfloat3 dir)
              (fabsf(dir.z) > ooeps) ? dir.z : copysignf(ooeps, dir.z));
 }
 
-CY_FN bool ray_triangle_intersect(cfloat3 P,
-                                  cfloat3 dir,
-                                  float ray_t,
-                                  cfloat3 tri_a,
-                                  cfloat3 tri_b,
-                                  cfloat3 tri_c,
-                                  float *isect_u,
-                                  float *isect_v,
-                                  float *isect_t)
+/* ray_triangle_intersect against the bound ray_t, also reporting whether the
+ * hit passes the same test against a second bound t_exact (cy_bvhw.h: hits
+ * are collected against a widened bound and judged at the exact one). */
+CY_FN bool ray_triangle_intersect2(cfloat3 P,
+                                   cfloat3 dir,
+                                   float ray_t,
+                                   float t_exact,
+                                   cfloat3 tri_a,
+                                   cfloat3 tri_b,
+                                   cfloat3 tri_c,
+                                   float *isect_u,
+                                   float *isect_v,
+                                   float *isect_t,
+                                   bool *exact_ok)
 {
   const cfloat3 v0 = sub3(tri_c, P);
   const cfloat3 v1 = sub3(tri_a, P);
@@ -188,14 +193,32 @@ CY_FN bool ray_triangle_intersect(cfloat3 P,
   const float T = dot3(v0, Ng);
   const int sign_den = (as_int(den) & 0x80000000);
   const float sign_T = xor_signmask(T, sign_den);
-  if ((sign_T < 0.0f) || (sign_T > ray_t * xor_signmask(den, sign_den))) {
+  const float abs_den = xor_signmask(den, sign_den);
+  if ((sign_T < 0.0f) || (sign_T > ray_t * abs_den)) {
     return false;
   }
+  *exact_ok = !(sign_T > t_exact * abs_den);
   const float inv_den = 1.0f / den;
   *isect_u = U * inv_den;
   *isect_v = V * inv_den;
   *isect_t = T * inv_den;
   return true;
+}
+
+/* util/util_math_intersect.h:88-195 (ray_triangle_intersect, the
+ * non-SSE/watertight-style path the generic x86 kernel compiles). */
+CY_FN bool ray_triangle_intersect(cfloat3 P,
+                                  cfloat3 dir,
+                                  float ray_t,
+                                  cfloat3 tri_a,
+                                  cfloat3 tri_b,
+                                  cfloat3 tri_c,
+                                  float *isect_u,
+                                  float *isect_v,
+                                  float *isect_t)
+{
+  bool exact_ok;
+  return ray_triangle_intersect2(P, dir, ray_t, ray_t, tri_a, tri_b, tri_c, isect_u, isect_v, isect_t, &exact_ok);
 }
 
 CY_FN bool scene_intersect_valid(const CyRay *ray)
@@ -253,7 +276,24 @@ CY_FN float bvh_instance_pop(
   return t;
 }
 
-template<bool any_hit, bool INST = true>
+/* Forward declaration: the wide traversal of one instance's BVH (cy_bvhw.h). */
+template<int W, bool any_hit>
+CY_FN bool bvhw_traverse(const CyGlobals *kg, int root, cfloat3 P, cfloat3 dir, cfloat3 idir, int object,
+                         uint visibility, CyIsect *isect, uint *err, uint *cnt_nodes, uint *cnt_leaves,
+                         uint *cnt_tris, CY_LDS CyStackEntry *lds_ring, bool *tie_out);
+
+/* Closest hit / opaque any hit with the bound BVH2 in the reference's order
+ * (bvh/bvh_traversal.h:34-227).  The first LDSN stack entries live in LDS,
+ * entry i of this thread at lds_stack[i * LDS_STRIDE] (ints).
+ *
+ * WI > 2 (instanced scenes with the device's wide BVH): the top level is
+ * traversed here, in the reference's order, and each instance entered is
+ * traversed with the W-wide BVH of its object (bvhw_traverse from the object's
+ * wide root, object space).  The closest hit inside one instance does not
+ * depend on the visiting order (near-ties excepted: *tie, see bvhw_traverse), so
+ * the sequence of instances entered -- and with it every bvh_instance_push/pop
+ * rounding of t -- is the reference's. */
+template<bool any_hit, bool INST = true, int WI = 2, int LDSN = CY_LDS_STACK, int LDS_STRIDE = CY_BLOCK>
 CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           const CyRay *ray,
                           uint visibility,
@@ -262,18 +302,20 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           uint *cnt_nodes,
                           uint *cnt_leaves,
                           uint *cnt_tris,
-                          CY_LDS int *lds_stack = nullptr)
+                          CY_LDS int *lds_stack = nullptr,
+                          CY_LDS CyStackEntry *lds_ring = nullptr,
+                          bool *tie = nullptr)
 {
   int stack_spill[BVH_STACK_SIZE];
   auto stack_set = [&](int i, int v) {
-    if (lds_stack && i < CY_LDS_STACK) {
-      lds_stack[i * CY_BLOCK] = v;
+    if (lds_stack && i < LDSN) {
+      lds_stack[i * LDS_STRIDE] = v;
     }
     else {
       stack_spill[i] = v;
     }
   };
-  auto stack_get = [&](int i) -> int { return (lds_stack && i < CY_LDS_STACK) ? lds_stack[i * CY_BLOCK] : stack_spill[i]; };
+  auto stack_get = [&](int i) -> int { return (lds_stack && i < LDSN) ? lds_stack[i * LDS_STRIDE] : stack_spill[i]; };
   stack_set(0, ENTRYPOINT_SENTINEL);
   int stack_ptr = 0;
   int node_addr = KD->bvh.root;
@@ -396,6 +438,26 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
           /* instance push (bvh_traversal.h:190-205) */
           object = (int)kg->__prim_object[-prim_addr - 1];
           isect->t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect->t);
+          if constexpr (WI > 2) {
+            /* the instance's own BVH, wide; then the instance pop and the
+             * top-level continuation, as the reference does at the sentinel */
+            const bool h = bvhw_traverse<WI, any_hit>(kg, kg->bvhw_object_root[object], P, dir, idir, object,
+                                                       visibility, isect, err, cnt_nodes, cnt_leaves, cnt_tris,
+                                                       lds_ring, tie);
+            if (any_hit && h) {
+              if (cnt_nodes) {
+                *cnt_nodes += n_nodes;
+                *cnt_leaves += n_leaves;
+                *cnt_tris += n_tris;
+              }
+              return true;
+            }
+            isect->t = bvh_instance_pop(kg, object, ray, &P, &dir, &idir, isect->t);
+            object = OBJECT_NONE;
+            node_addr = stack_get(stack_ptr);
+            --stack_ptr;
+            continue;
+          }
           ++stack_ptr;
           if (stack_ptr >= BVH_STACK_SIZE) {
             cy_set_error(err, CY_ERR_BVH_STACK, 0);

@@ -63,6 +63,7 @@ class Stats(ctypes.Structure):
         ("total_ms", ctypes.c_double), ("closest_ms", ctypes.c_double), ("closest_launches", ctypes.c_uint64),
         ("closest_nodes", ctypes.c_uint64), ("closest_leaves", ctypes.c_uint64), ("closest_tris", ctypes.c_uint64),
         ("bvh_width", ctypes.c_int32), ("bvh_depth", ctypes.c_int32), ("bvh_bytes", ctypes.c_uint64),
+        ("tie_rays", ctypes.c_uint64),
     ]
 
 

@@ -14,6 +14,9 @@ tests/parity_cases.py it stores, in tests/golden/<case>.npz:
 and, shared by all cases:
   primitives.npz    reference hash_uint2 and ray_offset on random + edge inputs
   film.npz          reference film convert (byte, half) of synthetic edge buffers
+  scale_<case>.npz  reference render of parity_cases.SCALE_CASES (full-size
+                    configs on a crop) and scale_full_frame.npz (the bench
+                    scene's full frame as 16x16 block means)
   background.npz    reference SHADER task (SHADER_EVAL_BACKGROUND) of the worlds of
                     parity_cases.BACKGROUND_CASES (map size and sample count per case)
   abi_layout.json   sizeof/offsetof of every device-data struct field in the
@@ -127,7 +130,35 @@ def make_background():
     np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), "background.npz"), **out)
 
 
+def make_scale():
+    """Full-size configs on a crop (parity_cases.SCALE_CASES) and the bench
+    scene's full frame reduced to block means."""
+    from parity_cases import FULL_FRAME_BLOCK, FULL_FRAME_CASE, SCALE_CASES, block_means
+    from raytracingproject_amd import scenes
+
+    for name, (fn, tile) in SCALE_CASES.items():
+        ds = sc.compile_scene(fn())
+        rk = RefKernel(ds)
+        buf = rk.render(tile=tile, threads=os.cpu_count())
+        rk.close()
+        np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), f"scale_{name}.npz"),
+                            digest=np.array(scene_digest(ds)), buffer=buf, samples=np.array(ds.samples),
+                            tile=np.array(tile if tile else (0, 0, ds.width, ds.height)))
+        print(name, buf.shape, float(buf[..., :3].mean()) / ds.samples)
+    ds = sc.compile_scene(scenes.CONFIGS[FULL_FRAME_CASE]())
+    rk = RefKernel(ds)
+    buf = rk.render(threads=os.cpu_count())
+    rk.close()
+    np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), "scale_full_frame.npz"),
+                        digest=np.array(scene_digest(ds)), block_means=block_means(buf, FULL_FRAME_BLOCK),
+                        samples=np.array(ds.samples), block=np.array(FULL_FRAME_BLOCK))
+    print("full frame", buf.shape)
+
+
 def main():
+    if "--scale-only" in sys.argv:
+        make_scale()
+        return
     if "--background-only" in sys.argv:
         make_background()
         return

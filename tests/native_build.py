@@ -48,6 +48,8 @@ def host_emu(libm_sincos: bool = True):
     lib.emu_bvhw_build.argtypes = [ci, ci, vp, cl, vp, cl, ci, vp, cl, vp, cl, vp, cl, vp, vp, ctypes.c_char_p, ci]
     lib.emu_set_object_root.argtypes = [vp]
     lib.emu_set_width.argtypes = [ci]
+    lib.emu_set_instancing.argtypes = [ci]
+
     return lib
 
 
@@ -70,6 +72,8 @@ class EmuScene:
 
     def args(self):
         self.lib.emu_set_width(self.width)
+        self.lib.emu_set_instancing(int(self.ds.info.get("instanced_objects", 0) > 0))
+
         self.lib.emu_set_object_root(None if self.object_root is None else self.object_root.ctypes.data)
         ptr = None if self.wide is None else self.wide.ctypes.data
         return (ctypes.addressof(self.data), len(self.names), self.c_names, self.c_ptrs, ptr)

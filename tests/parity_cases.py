@@ -25,6 +25,26 @@ CASES = {
 }
 
 
+# BASELINE.json configs at their full size (scene, resolution, spp), checked on a
+# crop the reference kernel renders in seconds: name -> (scene, tile or None).
+# Tiles are (x, y, w, h) in image pixels.
+SCALE_CASES = {
+    "cornell_256": (lambda: scenes.cornell_box(256, 256, 32), None),
+    "bmw_full_tile": (lambda: scenes.bmw27_standin(), (576, 328, 64, 64)),
+    "bbs_tile": (lambda: scenes.barbershop_standin(), (960, 560, 48, 48)),
+}
+
+# Full frame of the bench scene (BMW stand-in, 1280x720, 128 spp): the
+# reference's film reduced to BLOCK x BLOCK block means (fixture size).
+FULL_FRAME_CASE = "bmw27_standin"
+FULL_FRAME_BLOCK = 16
+
+
+def block_means(buf: np.ndarray, block: int) -> np.ndarray:
+    h, w = buf.shape[:2]
+    b = buf[: h - h % block, : w - w % block, :4].astype(np.float64)
+    return b.reshape(h // block, block, w // block, block, 4).mean(axis=(1, 3))
+
 
 def _world_case():
     s = scenes.cornell_box(16, 16, 1)

@@ -5,11 +5,12 @@ renders, for 4- and 8-wide nodes with and without leaf merging.
 
 The wide nodes carry the exact BVH2 child boxes and the traversal applies the
 reference's slab test to them, so it reaches every triangle the BVH2 traversal
-accepts: hit flags and any-hit (shadow) results are identical.  The closest
-primitive can differ only where two candidates' distances agree to the last
-ulp, because the visiting order decides such ties (bvh/bvh_traversal.h:34-227
-visits BVH2 children near-first; util/util_math_intersect.h:178 accepts
-T <= ray_t*den).  Renders are held to the north-star bar, film RMSE <= 1e-4.
+accepts: hit flags and any-hit (shadow) results are identical.  Where two
+candidates' distances tie, the reference's visiting order decides
+(bvh/bvh_traversal.h:34-227 visits BVH2 children near-first;
+util/util_math_intersect.h:178 accepts T <= ray_t*den); the wide traversal
+flags such rays and they are re-traced in the reference's order, so closest
+hits and renders are bit-identical to the reference.
 """
 import numpy as np
 import pytest
@@ -99,19 +100,9 @@ def test_wide_closest_hit_vs_reference(case):
     # reported is whichever the traversal meets first, only the flag is defined
     closest = (g["rays"][:, 7].view(np.uint32) & PATH_RAY_SHADOW_OPAQUE) == 0
     hit = (hi[:, 0] == 1) & closest
-    same = oi[hit, 1] == hi[hit, 1]
-    # the Cornell boxes stand on the floor: coplanar faces give exact t ties
-    assert same.mean() >= 0.995, same.mean()
-    a, b = of[hit][same], hf[hit][same]
-    assert np.array_equal(a[:, 1:].view(np.uint32), b[:, 1:].view(np.uint32))  # u, v
-    if ds.info["instanced_objects"] == 0:
-        assert np.array_equal(a[:, 0].view(np.uint32), b[:, 0].view(np.uint32))
-    else:
-        # t is scaled into and out of every instance entered on the way
-        # (bvh_instance_push/pop); another visiting order rounds differently
-        assert np.all(np.abs(a[:, 0] - b[:, 0]) <= 4e-7 * np.abs(b[:, 0]))
-    t, tr = of[hit][~same, 0], hf[hit][~same, 0]
-    assert np.all(np.abs(t - tr) <= 1e-6 * np.abs(tr))
+    # the reference's closest hit bit for bit (near-ties re-traced in its order)
+    assert np.array_equal(oi[hit, 1], hi[hit, 1])
+    assert np.array_equal(of[hit].view(np.uint32), hf[hit].view(np.uint32))
 
 
 def test_wide_shadow_any_hit_vs_reference(case):
@@ -135,4 +126,4 @@ def test_wide_render_vs_reference(case):
     film, ref = buf[..., :3] / s, g["buffer"][..., :3] / s
     rmse = float(np.sqrt(np.mean((film - ref) ** 2)))
     assert rmse <= RMSE_TOL, rmse
-    assert np.array_equal(buf[..., 3], g["buffer"][..., 3])
+    assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32))

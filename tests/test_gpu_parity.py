@@ -10,10 +10,12 @@ Bars (BASELINE.json north_star): integer results (hit flags, primitive ids,
 rng hashes) bit-exact; camera rays and hit t/u/v bit-exact (IEEE f32, no
 contraction); rendered film within 1e-4 RMSE of the reference.
 
-Every test runs twice: traversing the BVH2 exactly as bound (bvh width 2: the
-reference's visiting order, so renders are bit-identical) and the device's
-4-wide BVH (width 4, the default), whose visiting order can only change which
-of two primitives at the same distance wins (tests/test_bvh_wide.py).
+Every test runs at three widths: the BVH2 exactly as bound (width 2, the
+reference's visiting order) and the device's 4-wide (the default) and 8-wide
+BVHs.  The wide traversals visit in another order but return the reference's
+closest hit bit for bit: rays whose hits tie are re-traced in the reference's
+order (cy_bvhw.h), and instanced scenes keep the reference's top-level order
+(cy_path.h bvh2_intersect WI > 2), so renders are bit-identical at every width.
 """
 import numpy as np
 import pytest
@@ -69,22 +71,15 @@ def test_closest_hit_matches_reference(case, device):
     ref_f, ref_i = g["hit_f"], g["hit_i"]
     assert np.array_equal(oi[:, 0], ref_i[:, 0]), name
     hit = ref_i[:, 0] == 1
-    if device.bvh_width_under_test == 2:
-        assert np.array_equal(oi[hit, 1], ref_i[hit, 1]), name
-        assert np.array_equal(of[hit].view(np.uint32), ref_f[hit].view(np.uint32)), name
-        return
-    # wide: closest-hit rays (any-hit rays report whichever primitive comes first)
+    # any-hit queries (opaque-shadow visibility) report whichever primitive the
+    # traversal meets first: only their flag is defined
     hit &= (g["rays"][:, 7].view(np.uint32) & PATH_RAY_SHADOW_OPAQUE) == 0
-    same = oi[hit, 1] == ref_i[hit, 1]
-    assert same.mean() >= 0.995, (name, same.mean())
-    a, b = of[hit][same], ref_f[hit][same]
-    assert np.array_equal(a[:, 1:].view(np.uint32), b[:, 1:].view(np.uint32)), name
-    if ds.info["instanced_objects"] == 0:
-        assert np.array_equal(a[:, 0].view(np.uint32), b[:, 0].view(np.uint32)), name
-    else:  # t scaled through instances in another order (tests/test_bvh_wide.py)
-        assert np.all(np.abs(a[:, 0] - b[:, 0]) <= 4e-7 * np.abs(b[:, 0])), name
-    t, tr = of[hit][~same, 0], ref_f[hit][~same, 0]
-    assert np.all(np.abs(t - tr) <= 1e-6 * np.abs(tr)), name
+    if device.bvh_width_under_test == 2:
+        hit = ref_i[:, 0] == 1
+    # closest hits: the reference's primitive and t, u, v bit for bit at every
+    # width (the wide traversal re-traces near-ties in the reference's order)
+    assert np.array_equal(oi[hit, 1], ref_i[hit, 1]), name
+    assert np.array_equal(of[hit].view(np.uint32), ref_f[hit].view(np.uint32)), name
 
 
 def test_shadow_any_hit_matches_reference(case, device):
@@ -105,8 +100,7 @@ def test_render_matches_reference(case, device):
     exact = float(np.mean(buf.view(np.uint32) == ref.view(np.uint32)))
     print(f"{name}: film RMSE {rmse:.3e}, bit-exact fraction {exact:.4f}, max abs {np.abs(film - ref_film).max():.3e}")
     assert rmse <= RMSE_TOL, (name, rmse, exact)
-    if device.bvh_width_under_test == 2:
-        assert exact == 1.0, (name, exact)
+    assert exact == 1.0, (name, exact)
     # alpha is exactly the sample count for opaque scenes
     assert np.array_equal(buf[..., 3], ref[..., 3])
 

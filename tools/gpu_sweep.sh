@@ -9,7 +9,8 @@ fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
 if [[ ${SKIP_TESTS:-0} != 1 ]]; then
   timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_gpu.log
-  if fatal $rc; then exit $rc; fi
+  # any failure stops the sweep: a failing parity test may be a faulting kernel
+  if [[ $rc != 0 ]]; then exit $rc; fi
 fi
 i=0
 for args in "$@"; do
@@ -21,6 +22,7 @@ for args in "$@"; do
   timeout -k 10 600 env "${envs[@]}" python bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline "${opts[@]}" > gpurun_out/sweep_$i.log 2>&1
   rc=$?
   echo "[$args] rc=$rc"
+  if [[ $rc != 0 ]]; then tail -n 5 gpurun_out/sweep_$i.log; exit $rc; fi
   grep '"metric"' gpurun_out/sweep_$i.log | python3 -c "
 import json,sys
 for l in sys.stdin:

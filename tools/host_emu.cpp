@@ -7,6 +7,7 @@
  * reference kernel, so any difference against oracle/_ref isolates a logic
  * difference of the restatement from GPU arithmetic.  Not part of the product.
  */
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -95,17 +96,74 @@ extern "C" void emu_set_width(int w)
   g_width = w;
 }
 
+/* instanced scene: the device's wide kernels then traverse the top level in
+ * the reference's order and the instances wide (hipcycles.hip scene_traverse) */
+static int g_instancing = 0;
+extern "C" void emu_set_instancing(int on)
+{
+  g_instancing = on;
+}
+
+template<bool any_hit>
+static bool emu_traverse_impl(const CyGlobals *kg, const CyRay *ray, uint vis, CyIsect *isect, uint *err,
+                              uint *nn, uint *nl, uint *nt)
+{
+  if (kg->bvhw_nodes) {
+    bool tie = false, hit;
+    if (g_instancing) {
+      hit = g_width == 8 ? bvh2_intersect<any_hit, true, 8>(kg, ray, vis, isect, err, nn, nl, nt, nullptr, nullptr, &tie) :
+                           bvh2_intersect<any_hit, true, 4>(kg, ray, vis, isect, err, nn, nl, nt, nullptr, nullptr, &tie);
+    }
+    else {
+      hit = g_width == 8 ? bvhw_intersect<8, any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr, &tie) :
+                           bvhw_intersect<4, any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr, &tie);
+    }
+    if (!tie) {
+      return hit;
+    }
+    /* near-tie: re-trace in the reference's order, as k_resolve_ties does */
+    CyGlobals k2 = *kg;
+    k2.bvhw_nodes = nullptr;
+    return bvh2_intersect<any_hit>(&k2, ray, vis, isect, err, nullptr, nullptr, nullptr, nullptr);
+  }
+  return bvh2_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+}
+
+/* Debug aid: with emu_set_check(1) every closest-hit query of a wide-BVH
+ * render is repeated with the BVH2 in the reference's order and the first
+ * mismatches (ray, both hits) are kept for emu_get_mismatches. */
+static int g_check = 0;
+static std::vector<float> g_mismatch;
+extern "C" void emu_set_check(int on)
+{
+  g_check = on;
+  g_mismatch.clear();
+}
+extern "C" int emu_get_mismatches(float *out, int max_n)
+{
+  const int n = std::min<int>(max_n, (int)(g_mismatch.size() / 16));
+  memcpy(out, g_mismatch.data(), (size_t)n * 16 * 4);
+  return (int)(g_mismatch.size() / 16);
+}
+
 template<bool any_hit>
 static bool emu_traverse(const CyGlobals *kg, const CyRay *ray, uint vis, CyIsect *isect, uint *err,
                          uint *nn, uint *nl, uint *nt)
 {
-  if (kg->bvhw_nodes) {
-    if (g_width == 8) {
-      return bvhw_intersect<8, any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+  const bool hit = emu_traverse_impl<any_hit>(kg, ray, vis, isect, err, nn, nl, nt);
+  if (g_check && !any_hit && kg->bvhw_nodes) {
+    CyGlobals k2 = *kg;
+    k2.bvhw_nodes = nullptr;
+    CyIsect i2;
+    const bool h2 = bvh2_intersect<false>(&k2, ray, vis, &i2, err, nullptr, nullptr, nullptr, nullptr);
+    if (h2 != hit || (hit && (i2.prim != isect->prim || as_uint(i2.t) != as_uint(isect->t)))) {
+      const float rec[16] = {ray->P.x, ray->D.x, ray->P.y, ray->D.y, ray->P.z, ray->D.z, ray->t, as_float(vis),
+                             (float)isect->prim, isect->t, (float)i2.prim, i2.t, (float)isect->object,
+                             (float)i2.object, isect->u, i2.u};
+      g_mismatch.insert(g_mismatch.end(), rec, rec + 16);
     }
-    return bvhw_intersect<4, any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
   }
-  return bvh2_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
+  return hit;
 }
 
 /* scene_intersect on host: rays n x 8 (P, D, t, visibility bits) like
