@@ -951,8 +951,8 @@ int hipcy_load_kernels(hipcy_device *dev)
   }
   const hc_KernelData &d = dev->data_host;
   std::string why;
-  if (d.cam.type != 0) why = "only perspective cameras";
-  else if (d.cam.aperturesize > 0.0f) why = "depth of field";
+  if (d.cam.type < 0 || d.cam.type > 2) why = "unknown camera type";
+  else if (d.cam.type == 2 && (d.cam.panorama_type < 0 || d.cam.panorama_type > 3)) why = "unknown panorama type";
   else if (d.cam.shuttertime != -1.0f || d.cam.num_motion_steps) why = "motion blur";
   else if (d.cam.interocular_offset != 0.0f) why = "stereo";
   else if (d.integrator.sampling_pattern != 0) why = "only the Sobol pattern";

@@ -190,6 +190,51 @@ CY_FN float safe_acosf(float a)
   return cy_acosf(cclamp(a, -1.0f, 1.0f));
 }
 
+/* glibc 2.35 asinf (sysdeps/ieee754/flt-32/e_asinf.c: odd polynomial below
+ * 0.5, half-angle reduction above, split sqrt in the middle band), which the
+ * reference reaches through fisheye_equisolid_to_direction
+ * (kernel_projection.h:118).  Checked against the host libm over [-1, 1]
+ * (tests/test_kernel_math.py). */
+CY_FN float cy_asinf(float x)
+{
+  const float one = 1.0f, pio2_hi = 1.57079637050628662109375f, pio2_lo = -4.37113900018624283e-8f,
+              pio4_hi = 0.785398185253143310546875f;
+  const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f, p3 = 2.417951451e-2f,
+              p4 = 4.216630880e-2f;
+  const int hx = as_int(x);
+  const int ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) {
+    return x * pio2_hi + x * pio2_lo;
+  }
+  if (ix > 0x3f800000) {
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3f000000) {
+    if (ix < 0x32000000) {
+      return x;
+    }
+    const float t = x * x;
+    const float w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+    return x + x * w;
+  }
+  float w = one - fabsf(x);
+  float t = w * 0.5f;
+  float p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+  const float s = sqrtf(t);
+  if (ix >= 0x3F79999A) {
+    t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
+  }
+  else {
+    w = int_as_float(as_int(s) & (int)0xfffff000);
+    const float c = (t - w * w) / (s + w);
+    const float r = p;
+    p = 2.0f * s * r - (pio2_lo - 2.0f * c);
+    const float q = pio4_hi - 2.0f * w;
+    t = pio4_hi - (p - q);
+  }
+  return (hx > 0) ? t : -t;
+}
+
 CY_FN float power_heuristic(float a, float b)
 {
   return (a * a) / (a * a + b * b);

@@ -104,12 +104,152 @@ CY_FN float lookup_table_read(const CyGlobals *kg, float x, int offset, int size
 }
 
 /* ---------------------------------------------------------------------------
- * Camera: kernel_path_common.h:21-46 + kernel_camera.h:42-171 (perspective,
- * no DOF, no motion, no stereo — rejected at load otherwise).
+ * Camera: kernel_path_common.h:21-46 (kernel_path_trace_setup) and
+ * kernel_camera.h:19-369: perspective, orthographic and panorama cameras
+ * (equirectangular, fisheye equidistant / equisolid, mirror ball,
+ * kernel_projection.h), depth of field with disk or polygonal apertures and
+ * anamorphic ratio, near/far clipping.  Motion blur and stereo are rejected at
+ * load_kernels.
  */
+#define CY_M_PI_2_F 1.57079632679489661923f
+#define CY_M_PI_4_F 0.785398163397448309616f
+
+/* kernel_montecarlo.h:150-169 */
+CY_FN void concentric_sample_disk(float u1, float u2, float *x, float *y)
+{
+  float phi, r;
+  const float a = 2.0f * u1 - 1.0f;
+  const float b = 2.0f * u2 - 1.0f;
+  if (a == 0.0f && b == 0.0f) {
+    *x = 0.0f;
+    *y = 0.0f;
+    return;
+  }
+  else if (a * a > b * b) {
+    r = a;
+    phi = CY_M_PI_4_F * (b / a);
+  }
+  else {
+    r = b;
+    phi = CY_M_PI_2_F - CY_M_PI_4_F * (a / b);
+  }
+  *x = r * cy_cosf(phi);
+  *y = r * cy_sinf(phi);
+}
+
+/* kernel_montecarlo.h:172-194 */
+CY_FN void regular_polygon_sample(float corners, float rotation, float u, float v, float *x, float *y)
+{
+  const float corner = floorf(u * corners);
+  u = u * corners - corner;
+  u = sqrtf(u);
+  v = v * u;
+  u = 1.0f - u;
+  const float angle = CY_PI_F / corners;
+  const float px = (u + v) * cy_cosf(angle);
+  const float py = (u - v) * cy_sinf(angle);
+  rotation += corner * 2.0f * angle;
+  const float cr = cy_cosf(rotation);
+  const float sr = cy_sinf(rotation);
+  *x = cr * px - sr * py;
+  *y = sr * px + cr * py;
+}
+
+/* kernel_camera.h:21-40 camera_sample_aperture, scaled by aperturesize */
+CY_FN void camera_sample_aperture(const CyGlobals *kg, float u, float v, float *x, float *y)
+{
+  const float blades = KD->cam.blades;
+  if (blades == 0.0f) {
+    concentric_sample_disk(u, v, x, y);
+  }
+  else {
+    regular_polygon_sample(blades, KD->cam.bladesrotation, u, v, x, y);
+  }
+  *x *= KD->cam.inv_aperture_ratio;
+  const float size = KD->cam.aperturesize;
+  *x = *x * size;
+  *y = *y * size;
+}
+
+/* kernel_projection.h:64-71 equirectangular_range_to_direction */
+CY_FN cfloat3 equirectangular_range_to_direction(float u, float v, hc_float4 range)
+{
+  const float phi = range.x * u + range.y;
+  const float theta = range.z * v + range.w;
+  const float sin_theta = cy_sinf(theta);
+  return mk3(sin_theta * cy_cosf(phi), sin_theta * cy_sinf(phi), cy_cosf(theta));
+}
+
+/* kernel_projection.h:94-111 fisheye_to_direction */
+CY_FN cfloat3 fisheye_to_direction(float u, float v, float fov)
+{
+  u = (u - 0.5f) * 2.0f;
+  v = (v - 0.5f) * 2.0f;
+  const float r = sqrtf(u * u + v * v);
+  if (r > 1.0f) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float phi = safe_acosf((r != 0.0f) ? u / r : 0.0f);
+  const float theta = r * fov * 0.5f;
+  if (v < 0.0f) {
+    phi = -phi;
+  }
+  return mk3(cy_cosf(theta), -cy_cosf(phi) * cy_sinf(theta), cy_sinf(phi) * cy_sinf(theta));
+}
+
+/* kernel_projection.h:126-145 fisheye_equisolid_to_direction */
+CY_FN cfloat3 fisheye_equisolid_to_direction(float u, float v, float lens, float fov, float width, float height)
+{
+  u = (u - 0.5f) * width;
+  v = (v - 0.5f) * height;
+  const float rmax = 2.0f * lens * cy_sinf(fov * 0.25f);
+  const float r = sqrtf(u * u + v * v);
+  if (r > rmax) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float phi = safe_acosf((r != 0.0f) ? u / r : 0.0f);
+  const float theta = 2.0f * cy_asinf(r / (2.0f * lens));
+  if (v < 0.0f) {
+    phi = -phi;
+  }
+  return mk3(cy_cosf(theta), -cy_cosf(phi) * cy_sinf(theta), cy_sinf(phi) * cy_sinf(theta));
+}
+
+/* kernel_projection.h:149-166 mirrorball_to_direction */
+CY_FN cfloat3 mirrorball_to_direction(float u, float v)
+{
+  cfloat3 dir;
+  dir.x = 2.0f * u - 1.0f;
+  dir.z = 2.0f * v - 1.0f;
+  if (dir.x * dir.x + dir.z * dir.z > 1.0f) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  dir.y = -sqrtf(fmaxf(1.0f - dir.x * dir.x - dir.z * dir.z, 0.0f));
+  const cfloat3 I = mk3(0.0f, -1.0f, 0.0f);
+  return sub3(mul3f(dir, 2.0f * dot3(dir, I)), I);
+}
+
+/* kernel_projection.h:184-199 panorama_to_direction */
+CY_FN cfloat3 panorama_to_direction(const CyGlobals *kg, float u, float v)
+{
+  switch (KD->cam.panorama_type) {
+    case 0: /* PANORAMA_EQUIRECTANGULAR */
+      return equirectangular_range_to_direction(u, v, KD->cam.equirectangular_range);
+    case 3: /* PANORAMA_MIRRORBALL */
+      return mirrorball_to_direction(u, v);
+    case 1: /* PANORAMA_FISHEYE_EQUIDISTANT */
+      return fisheye_to_direction(u, v, KD->cam.fisheye_fov);
+    case 2: /* PANORAMA_FISHEYE_EQUISOLID */
+    default:
+      return fisheye_equisolid_to_direction(u, v, KD->cam.fisheye_lens, KD->cam.fisheye_fov, KD->cam.sensorwidth,
+                                            KD->cam.sensorheight);
+  }
+}
+
 CY_FN void camera_sample_ray(
     const CyGlobals *kg, int x, int y, int sample, uint *rng_hash_out, CyRay *ray)
 {
+  /* path_rng_init (kernel_random.h:129-153) */
   uint rng_hash = hash_uint2((uint)x, (uint)y);
   rng_hash ^= (uint)KD->integrator.seed;
   float filter_u, filter_v;
@@ -121,25 +261,91 @@ CY_FN void camera_sample_ray(
     path_rng_2D(kg, rng_hash, sample, PRNG_FILTER_U, &filter_u, &filter_v);
   }
   *rng_hash_out = rng_hash;
+  float lens_u = 0.0f, lens_v = 0.0f;
+  const bool dof = KD->cam.aperturesize > 0.0f;
+  if (dof) {
+    path_rng_2D(kg, rng_hash, sample, PRNG_LENS_U, &lens_u, &lens_v);
+  }
 
-  int filter_table_offset = KD->film.filter_table_offset;
-  float raster_x = x + lookup_table_read(kg, filter_u, filter_table_offset, FILTER_TABLE_SIZE);
-  float raster_y = y + lookup_table_read(kg, filter_v, filter_table_offset, FILTER_TABLE_SIZE);
+  /* camera_sample (kernel_camera.h:296-356): pixel filter */
+  const int filter_table_offset = KD->film.filter_table_offset;
+  const float raster_x = x + lookup_table_read(kg, filter_u, filter_table_offset, FILTER_TABLE_SIZE);
+  const float raster_y = y + lookup_table_read(kg, filter_v, filter_table_offset, FILTER_TABLE_SIZE);
 
   const struct cy_ptfm *rastertocamera = (const struct cy_ptfm *)&KD->cam.rastertocamera;
-  cfloat3 Pcamera = transform_perspective(rastertocamera, mk3(raster_x, raster_y, 0.0f));
-  cfloat3 P = mk3(0.0f, 0.0f, 0.0f);
-  cfloat3 D = Pcamera;
   const struct cy_tfm *cameratoworld = (const struct cy_tfm *)&KD->cam.cameratoworld;
-  P = transform_point(cameratoworld, P);
-  D = normalize3(transform_direction(cameratoworld, D));
-  ray->P = P;
-  ray->D = D;
-  /* camera clipping (__CAMERA_CLIPPING__) */
-  float z_inv = 1.0f / normalize3(Pcamera).z;
-  float nearclip = KD->cam.nearclip * z_inv;
-  ray->P = add3(ray->P, mul3f(ray->D, nearclip));
-  ray->t = KD->cam.cliplength * z_inv;
+  const cfloat3 Pcamera = transform_perspective(rastertocamera, mk3(raster_x, raster_y, 0.0f));
+  const int type = KD->cam.type;
+  if (type == 0) {
+    /* camera_sample_perspective (kernel_camera.h:42-171) */
+    cfloat3 P = mk3(0.0f, 0.0f, 0.0f);
+    cfloat3 D = Pcamera;
+    if (dof) {
+      float lx, ly;
+      camera_sample_aperture(kg, lens_u, lens_v, &lx, &ly);
+      const float ft = KD->cam.focaldistance / D.z;
+      const cfloat3 Pfocus = mul3f(D, ft);
+      P = mk3(lx, ly, 0.0f);
+      D = normalize3(sub3(Pfocus, P));
+    }
+    P = transform_point(cameratoworld, P);
+    D = normalize3(transform_direction(cameratoworld, D));
+    ray->P = P;
+    ray->D = D;
+    /* camera clipping (__CAMERA_CLIPPING__) */
+    const float z_inv = 1.0f / normalize3(Pcamera).z;
+    const float nearclip = KD->cam.nearclip * z_inv;
+    ray->P = add3(ray->P, mul3f(ray->D, nearclip));
+    ray->t = KD->cam.cliplength * z_inv;
+  }
+  else if (type == 1) {
+    /* camera_sample_orthographic (kernel_camera.h:174-233) */
+    cfloat3 P;
+    cfloat3 D = mk3(0.0f, 0.0f, 1.0f);
+    if (dof) {
+      float lx, ly;
+      camera_sample_aperture(kg, lens_u, lens_v, &lx, &ly);
+      const cfloat3 Pfocus = mul3f(D, KD->cam.focaldistance);
+      const cfloat3 lensuvw = mk3(lx, ly, 0.0f);
+      P = add3(Pcamera, lensuvw);
+      D = normalize3(sub3(Pfocus, lensuvw));
+    }
+    else {
+      P = Pcamera;
+    }
+    ray->P = transform_point(cameratoworld, P);
+    ray->D = normalize3(transform_direction(cameratoworld, D));
+    ray->t = KD->cam.cliplength;
+  }
+  else {
+    /* camera_sample_panorama (kernel_camera.h:237-291) */
+    cfloat3 P = mk3(0.0f, 0.0f, 0.0f);
+    cfloat3 D = panorama_to_direction(kg, Pcamera.x, Pcamera.y);
+    if (D.x == 0.0f && D.y == 0.0f && D.z == 0.0f) {
+      /* outside the lens: no camera ray */
+      ray->P = P;
+      ray->D = D;
+      ray->t = 0.0f;
+      return;
+    }
+    if (dof) {
+      float lx, ly;
+      camera_sample_aperture(kg, lens_u, lens_v, &lx, &ly);
+      const cfloat3 Dfocus = normalize3(D);
+      const cfloat3 Pfocus = mul3f(Dfocus, KD->cam.focaldistance);
+      const cfloat3 U = normalize3(sub3(mk3(1.0f, 0.0f, 0.0f), mul3f(Dfocus, Dfocus.x)));
+      const cfloat3 V = normalize3(cross3(Dfocus, U));
+      P = add3(mul3f(U, lx), mul3f(V, ly));
+      D = normalize3(sub3(Pfocus, P));
+    }
+    P = transform_point(cameratoworld, P);
+    D = normalize3(transform_direction(cameratoworld, D));
+    ray->P = P;
+    ray->D = D;
+    const float nearclip = KD->cam.nearclip;
+    ray->P = add3(ray->P, mul3f(ray->D, nearclip));
+    ray->t = KD->cam.cliplength;
+  }
 }
 
 /* ---------------------------------------------------------------------------

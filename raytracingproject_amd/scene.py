@@ -238,12 +238,32 @@ class Lamp:
 
 @dataclass
 class Camera:
+    """render/camera.cpp sockets (subset): type perspective | orthographic |
+    panorama; panorama_type equirectangular | fisheye_equidistant |
+    fisheye_equisolid | mirrorball; depth of field (aperture size, blades,
+    rotation, ratio, focal distance)."""
     eye: tuple = (0.0, 0.0, -5.0)
     target: tuple = (0.0, 0.0, 0.0)
     up: tuple = (0.0, 1.0, 0.0)
     fov: float = math.radians(40.0)  # full vertical-or-horizontal fov as in Cycles
     nearclip: float = 1e-5
     farclip: float = 1e5
+    type: str = "perspective"
+    ortho_scale: float = 1.0  # orthographic: the auto viewplane scaled by this (Blender's ortho_scale / 2)
+    panorama_type: str = "equirectangular"
+    fisheye_fov: float = math.pi
+    fisheye_lens: float = 10.5
+    sensorwidth: float = 36.0  # mm, in the units of fisheye_lens (Blender sync passes both in mm)
+    sensorheight: float = 24.0
+    latitude_min: float = -math.pi / 2
+    latitude_max: float = math.pi / 2
+    longitude_min: float = -math.pi
+    longitude_max: float = math.pi
+    aperturesize: float = 0.0
+    focaldistance: float = 10.0
+    blades: int = 0
+    bladesrotation: float = 0.0
+    aperture_ratio: float = 1.0
 
 
 @dataclass
@@ -307,12 +327,15 @@ def _look_at(eye, target, up) -> np.ndarray:
     return m
 
 
-def _viewplane(width, height):
-    """Camera::compute_auto_viewplane (sensor fit AUTO)."""
+def _viewplane(width, height, cam=None):
+    """Camera::compute_auto_viewplane (sensor fit AUTO; panorama: unit square)."""
+    if cam is not None and cam.type == "panorama":
+        return (0.0, 1.0, 0.0, 1.0)
     aspect = width / height
+    s = cam.ortho_scale if cam is not None and cam.type == "orthographic" else 1.0
     if width >= height:
-        return (-aspect, aspect, -1.0, 1.0)
-    return (-1.0, 1.0, -1.0 / aspect, 1.0 / aspect)
+        return (-aspect * s, aspect * s, -1.0 * s, 1.0 * s)
+    return (-1.0 * s, 1.0 * s, -1.0 / aspect * s, 1.0 / aspect * s)
 
 
 def _from_viewplane(vp):
@@ -324,18 +347,36 @@ def _from_viewplane(vp):
     return s @ tr
 
 
+def _orthographic(n, f):
+    """util_projection.h:204-210 projection_orthographic."""
+    m = np.eye(4)
+    m[2, 2] = 1.0 / (f - n)
+    m[2, 3] = -n / (f - n)
+    return m
+
+
 def _perspective(fov, n, f):
     persp = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, f / (f - n), -f * n / (f - n)], [0, 0, 1, 0]], dtype=np.float64)
     inv_angle = 1.0 / math.tan(0.5 * fov)
     return np.diag([inv_angle, inv_angle, 1.0, 1.0]) @ persp
 
 
+PANORAMA_TYPES = {"equirectangular": 0, "fisheye_equidistant": 1, "fisheye_equisolid": 2, "mirrorball": 3}
+CAMERA_TYPES = {"perspective": 0, "orthographic": 1, "panorama": 2}
+
+
 def compile_camera(kcam, cam: Camera, width: int, height: int):
-    screentondc = _from_viewplane(_viewplane(width, height))
+    """Camera::update + Camera::device_update (render/camera.cpp:220-440)."""
+    screentondc = _from_viewplane(_viewplane(width, height, cam))
     ndctoraster = np.diag([width, height, 1.0, 1.0])
     screentoraster = ndctoraster @ screentondc
     rastertoscreen = np.linalg.inv(screentoraster)
-    cameratoscreen = _perspective(cam.fov, cam.nearclip, cam.farclip)
+    if cam.type == "perspective":
+        cameratoscreen = _perspective(cam.fov, cam.nearclip, cam.farclip)
+    elif cam.type == "orthographic":
+        cameratoscreen = _orthographic(cam.nearclip, cam.farclip)
+    else:
+        cameratoscreen = np.eye(4)
     screentocamera = np.linalg.inv(cameratoscreen)
     rastertocamera = screentocamera @ rastertoscreen
     cameratoworld = _look_at(cam.eye, cam.target, cam.up)
@@ -345,13 +386,30 @@ def compile_camera(kcam, cam: Camera, width: int, height: int):
         p = m @ np.array([v[0], v[1], v[2], 1.0])
         return p[:3] / p[3]
 
-    dx = persp(rastertocamera, (1, 0, 0)) - persp(rastertocamera, (0, 0, 0))
-    dy = persp(rastertocamera, (0, 1, 0)) - persp(rastertocamera, (0, 0, 0))
+    if cam.type == "perspective":
+        dx = persp(rastertocamera, (1, 0, 0)) - persp(rastertocamera, (0, 0, 0))
+        dy = persp(rastertocamera, (0, 1, 0)) - persp(rastertocamera, (0, 0, 0))
+    elif cam.type == "orthographic":
+        dx = rastertocamera[:3, :3] @ np.array([1.0, 0.0, 0.0])
+        dy = rastertocamera[:3, :3] @ np.array([0.0, 1.0, 0.0])
+    else:
+        dx = np.zeros(3)
+        dy = np.zeros(3)
     dx = cameratoworld[:3, :3] @ dx
     dy = cameratoworld[:3, :3] @ dy
 
-    kcam.type = 0
-    kcam.panorama_type = 0
+    kcam.type = CAMERA_TYPES[cam.type]
+    kcam.panorama_type = PANORAMA_TYPES[cam.panorama_type]
+    if cam.type == "panorama":
+        # (left zero for the other types, which never read them)
+        kcam.fisheye_fov = cam.fisheye_fov
+        kcam.fisheye_lens = cam.fisheye_lens
+        er = kcam.equirectangular_range
+        f32 = np.float32
+        er.x = float(f32(cam.longitude_min) - f32(cam.longitude_max))
+        er.y = float(-f32(cam.longitude_min))
+        er.z = float(f32(cam.latitude_min) - f32(cam.latitude_max))
+        er.w = float(-f32(cam.latitude_min) + f32(math.pi / 2))
     abi.set_transform(kcam.cameratoworld, cameratoworld[:3])
     abi.set_transform(kcam.rastertocamera, rastertocamera)
     abi.set_transform(kcam.worldtocamera, worldtocamera[:3])
@@ -363,20 +421,21 @@ def compile_camera(kcam, cam: Camera, width: int, height: int):
     abi.set_transform(kcam.worldtoraster, ndctoraster @ screentondc @ cameratoscreen @ worldtocamera)
     kcam.dx.x, kcam.dx.y, kcam.dx.z, kcam.dx.w = (*dx, 0.0)
     kcam.dy.x, kcam.dy.y, kcam.dy.z, kcam.dy.w = (*dy, 0.0)
-    kcam.aperturesize = 0.0
-    kcam.blades = 0.0
-    kcam.focaldistance = 10.0
+    kcam.aperturesize = cam.aperturesize
+    kcam.blades = 0.0 if cam.blades < 3 else float(cam.blades)
+    kcam.bladesrotation = cam.bladesrotation
+    kcam.focaldistance = cam.focaldistance
     kcam.shuttertime = -1.0
     kcam.num_motion_steps = 0
     kcam.have_perspective_motion = 0
     kcam.nearclip = cam.nearclip
     kcam.cliplength = cam.farclip - cam.nearclip
-    kcam.sensorwidth = 36.0
-    kcam.sensorheight = 24.0
+    kcam.sensorwidth = cam.sensorwidth
+    kcam.sensorheight = cam.sensorheight
     kcam.width = float(width)
     kcam.height = float(height)
     kcam.resolution = 1
-    kcam.inv_aperture_ratio = 1.0
+    kcam.inv_aperture_ratio = 1.0 / cam.aperture_ratio
     kcam.interocular_offset = 0.0
     kcam.shutter_table_offset = 0
 

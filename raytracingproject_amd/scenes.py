@@ -147,6 +147,52 @@ def cornell_lamps(width=64, height=64, samples=16) -> sc.Scene:
     return scene
 
 
+def cornell_camera(kind: str, width=64, height=64, samples=16) -> sc.Scene:
+    """Cornell box through the camera models of kernel_camera.h: "dof"
+    (perspective, hexagonal anamorphic aperture), "ortho" (orthographic with a
+    disk aperture), and the panoramas "equirect", "fisheye_equidistant",
+    "fisheye_equisolid" (with depth of field) and "mirrorball" from inside the
+    box."""
+    scene = cornell_box(width, height, samples)
+    cam = scene.camera
+    inside = dict(eye=(278.0, 273.0, 200.0), target=(278.0, 273.0, 555.0), up=(0.0, 1.0, 0.0), nearclip=0.1,
+                  farclip=1e5)
+    if kind == "dof":
+        cam.aperturesize = 25.0
+        cam.focaldistance = 950.0
+        cam.blades = 6
+        cam.bladesrotation = 0.3
+        cam.aperture_ratio = 1.5
+    elif kind == "ortho":
+        cam.type = "orthographic"
+        cam.ortho_scale = 300.0
+        cam.aperturesize = 8.0
+        cam.focaldistance = 1000.0
+    else:
+        scene.camera = sc.Camera(**inside)
+        cam = scene.camera
+        cam.type = "panorama"
+        if kind == "equirect":
+            cam.panorama_type = "equirectangular"
+            cam.latitude_min, cam.latitude_max = -1.2, 1.3
+            cam.longitude_min, cam.longitude_max = -2.5, 2.8
+        elif kind == "fisheye_equidistant":
+            cam.panorama_type = "fisheye_equidistant"
+            cam.fisheye_fov = 3.0
+        elif kind == "fisheye_equisolid":
+            cam.panorama_type = "fisheye_equisolid"
+            cam.fisheye_lens = 9.0
+            cam.fisheye_fov = 3.1
+            cam.aperturesize = 3.0
+            cam.focaldistance = 300.0
+        elif kind == "mirrorball":
+            cam.panorama_type = "mirrorball"
+        else:
+            raise ValueError(kind)
+    scene.name = "cornell_camera_" + kind
+    return scene
+
+
 def _tfm(translate=(0.0, 0.0, 0.0), rot_y=0.0, scale=(1.0, 1.0, 1.0), rot_x=0.0) -> np.ndarray:
     """3x4 object-to-world transform: translate * rot_y * rot_x * scale."""
     c, s = math.cos(rot_y), math.sin(rot_y)

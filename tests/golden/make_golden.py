@@ -162,12 +162,15 @@ def main():
     if "--background-only" in sys.argv:
         make_background()
         return
-    make_primitives()
-    make_film()
-    make_background()
+    if not any(a.startswith("--cases=") for a in sys.argv):
+        make_primitives()
+        make_film()
+        make_background()
     if "--primitives-only" in sys.argv:
         return
-    for name in CASES:
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--cases=")]
+    names = only[0].split(",") if only else list(CASES)
+    for name in names:
         ds = compile_case(name)
         rk = RefKernel(ds)
         buf = rk.render(threads=os.cpu_count())

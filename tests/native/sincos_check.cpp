@@ -22,6 +22,19 @@ extern "C" void acos_eval(const float *x, long n, float *dev, float *libm)
   }
 }
 
+extern "C" long asin_sweep(uint32_t lo, uint32_t hi, uint32_t step)
+{
+  long bad = 0;
+  for (uint64_t u = lo; u <= hi; u += step) {
+    const float x = as_float((uint32_t)u);
+    volatile float vx = x;
+    if (as_uint(cy_asinf(x)) != as_uint(asinf(vx))) {
+      bad++;
+    }
+  }
+  return bad;
+}
+
 /* cy_powf (glibc powf restatement) and libm powf over [lo, hi] bit patterns,
  * with y = 1/2.4 (color_linear_to_srgb); returns the number of mismatches. */
 extern "C" long powf_sweep(uint32_t lo, uint32_t hi, uint32_t step)

@@ -136,6 +136,8 @@ def sincos():
     lib.acos_eval.argtypes = [vp, ctypes.c_long, vp, vp]
     lib.powf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     lib.powf_sweep.restype = ctypes.c_long
+    lib.asin_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    lib.asin_sweep.restype = ctypes.c_long
     lib.srgb_eval.argtypes = [vp, ctypes.c_long, vp]
     lib.atan2_eval.argtypes = [vp, vp, ctypes.c_long, vp, vp]
     return lib

@@ -22,6 +22,9 @@ CASES = {
     # 64 spp: the wide BVH scales t through instances in its own order (cy_bvhw.h),
     # so its film is compared at the RMSE bar, which needs more samples per pixel
     "cornell_instanced": lambda: scenes.cornell_instanced(64, 64, 64),
+    # camera models (kernel_camera.h): depth of field, orthographic, panoramas
+    **{f"camera_{k}": (lambda k=k: scenes.cornell_camera(k, 48, 48, 8))
+       for k in ("dof", "ortho", "equirect", "fisheye_equidistant", "fisheye_equisolid", "mirrorball")},
 }
 
 
@@ -55,7 +58,7 @@ def _world_case():
 
 # SHADER task (SHADER_EVAL_BACKGROUND) cases: name -> (scene, map width, height, samples)
 BACKGROUND_CASES = {
-    **{name: (fn, 64, 32, 2) for name, fn in CASES.items()},
+    **{name: (fn, 64, 32, 2) for name, fn in CASES.items() if not name.startswith("camera_")},
     "world_blue": (_world_case, 64, 32, 2),
     "world_blue_ragged": (_world_case, 37, 19, 3),
 }
