@@ -94,9 +94,11 @@ def build_device(force=False, variant=None, defines=()):
     jobs = [([HIPCC, *cflags, *dflags, inc, "-c", "-o", os.path.join(objdir, "hipcycles.o"), src],
              os.path.join(objdir, "hipcycles.o"))]
     for mc in SHADE_VARIANTS:
-        obj = os.path.join(objdir, f"k_shade_mc{mc}.o")
-        jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT=mc{mc}", inc, "-c",
-                      "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
+        for tex in (0, 1):
+            name = f"mc{mc}_tex" if tex else f"mc{mc}"
+            obj = os.path.join(objdir, f"k_shade_{name}.o")
+            jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
+                          f"-DCY_SVM_TEX={tex}", inc, "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
     with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
         list(ex.map(lambda j: _run(j[0]), jobs))
     _run([HIPCC, "--offload-arch=gfx950", "-fno-gpu-rdc", "-shared", "-fPIC", "-o", out, *[j[1] for j in jobs]])

@@ -491,6 +491,9 @@ struct hipcy_device {
   int *bvhw_object_root = nullptr; /* inside bvhw, after the nodes */
   int have_instancing = 1;         /* some object without SD_OBJECT_TRANSFORM_APPLIED */
   std::vector<uint32_t> object_flags; /* host copy of __object_flag, taken at bind time */
+  std::vector<hc_uint4> svm_nodes;    /* host copy of __svm_nodes, taken at bind time */
+  size_t num_shaders = 0;             /* __shaders entries */
+  bool shade_tex = false;             /* some shader uses texture / converter / input nodes */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int tri_index_identity = 0;
   hipcy_stats stats;
@@ -907,6 +910,17 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
       HIP_CHECK(dev, hipMemcpy(dev->object_flags.data(), (const void *)device_pointer, bytes, hipMemcpyDeviceToHost));
     }
   }
+  if (strcmp(name, "__svm_nodes") == 0) {
+    /* host copy for the program scan of load_kernels (node set -> kernel variant) */
+    dev->svm_nodes.assign(bytes / sizeof(hc_uint4), hc_uint4{});
+    if (bytes) {
+      HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+      HIP_CHECK(dev, hipMemcpy(dev->svm_nodes.data(), (const void *)device_pointer, bytes, hipMemcpyDeviceToHost));
+    }
+  }
+  if (strcmp(name, "__shaders") == 0) {
+    dev->num_shaders = bytes / sizeof(hc_KernelShader);
+  }
   if (strcmp(name, "__bvh_nodes") == 0 || strcmp(name, "__bvh_leaf_nodes") == 0 ||
       strcmp(name, "__prim_tri_index") == 0 || strcmp(name, "__prim_object") == 0 ||
       strcmp(name, "__object_node") == 0) {
@@ -942,6 +956,114 @@ int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims)
 uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
 {
   return 1u; /* BVH_LAYOUT_BVH2 (kernel_types.h:1396-1406) */
+}
+
+/* Walk every shader's SVM program (jump table entry -> NODE_END) with the node
+ * lengths of svm/svm.h's decoders.  Rejects nodes the HIP interpreter does not
+ * implement before any render (the reference compiles only the node groups a
+ * scene requests: DeviceRequestedFeatures max_nodes_group / nodes_features,
+ * device/device.h:130-200) and reports whether the texture / converter / input
+ * nodes are used, which selects the shading-kernel variant. */
+static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders, bool *uses_tex)
+{
+  *uses_tex = false;
+  const size_t n = prog.size();
+  if (num_shaders > n) {
+    return "jump table larger than the program";
+  }
+  for (size_t sh = 0; sh < num_shaders; sh++) {
+    if (prog[sh].x != NODE_SHADER_JUMP) {
+      return "shader " + std::to_string(sh) + ": jump table entry is not NODE_SHADER_JUMP";
+    }
+    size_t off = prog[sh].y;
+    for (size_t steps = 0;; steps++) {
+      if (off >= n || steps > n) {
+        return "shader " + std::to_string(sh) + ": program runs past __svm_nodes";
+      }
+      const hc_uint4 node = prog[off];
+      size_t len = 1;
+      bool tex = false;
+      switch (node.x) {
+        case NODE_END:
+          len = 0;
+          break;
+        case NODE_CLOSURE_BSDF:
+        case NODE_VALUE_V:
+          len = 2;
+          break;
+        case NODE_CLOSURE_EMISSION:
+        case NODE_CLOSURE_BACKGROUND:
+        case NODE_CLOSURE_SET_WEIGHT:
+        case NODE_CLOSURE_WEIGHT:
+        case NODE_EMISSION_WEIGHT:
+        case NODE_MIX_CLOSURE:
+        case NODE_JUMP_IF_ZERO:
+        case NODE_JUMP_IF_ONE:
+        case NODE_VALUE_F:
+        case NODE_FRESNEL:
+        case NODE_LAYER_WEIGHT:
+          break;
+        case NODE_MATH:
+          if (node.y == 6 || (node.y >= 29 && node.y <= 31)) {
+            return "math node: tangent / sinh / cosh / tanh are not implemented";
+          }
+          tex = true;
+          break;
+        case NODE_VECTOR_MATH:
+          if (node.y == 23) {
+            return "vector math node: tangent is not implemented";
+          }
+          len = (node.y == 20) ? 2 : 1; /* WRAP: extra node */
+          tex = true;
+          break;
+        case NODE_TEX_COORD:
+          len = (node.y == 1 && node.w != 0) ? 4 : 1; /* OBJECT with a transform */
+          tex = true;
+          break;
+        case NODE_RGB_RAMP:
+          if (off + 1 >= n) {
+            return "rgb ramp: table size node past __svm_nodes";
+          }
+          len = 2 + (size_t)prog[off + 1].x;
+          tex = true;
+          break;
+        case NODE_MIX:
+        case NODE_SEPARATE_HSV:
+        case NODE_COMBINE_HSV:
+        case NODE_CLAMP:
+          len = 2;
+          tex = true;
+          break;
+        case NODE_MAP_RANGE:
+          len = 3;
+          tex = true;
+          break;
+        case NODE_GEOMETRY:
+        case NODE_CONVERT:
+        case NODE_HSV:
+        case NODE_GAMMA:
+        case NODE_BRIGHTCONTRAST:
+        case NODE_LIGHT_PATH:
+        case NODE_MAPPING:
+        case NODE_TEX_GRADIENT:
+        case NODE_TEX_CHECKER:
+        case NODE_LIGHT_FALLOFF:
+        case NODE_INVERT:
+        case NODE_SEPARATE_VECTOR:
+        case NODE_COMBINE_VECTOR:
+          tex = true;
+          break;
+        default:
+          return "shader " + std::to_string(sh) + ": SVM node " + std::to_string(node.x) + " is not implemented";
+      }
+      *uses_tex |= tex;
+      if (len == 0) {
+        break;
+      }
+      off += len;
+    }
+  }
+  return "";
 }
 
 int hipcy_load_kernels(hipcy_device *dev)
@@ -981,6 +1103,10 @@ int hipcy_load_kernels(hipcy_device *dev)
     if (dev->globals.find(r) == dev->globals.end()) {
       return set_error(dev, std::string("load_kernels: array not bound: ") + r);
     }
+  }
+  why = svm_scan(dev->svm_nodes, dev->num_shaders, &dev->shade_tex);
+  if (!why.empty()) {
+    return set_error(dev, "load_kernels: unsupported shader: " + why);
   }
   /* instanced geometry present? (selects the traversal kernels with instance
    * leaves and the instance paths of shading) */
@@ -1125,7 +1251,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));
   }
-  cy_launch_shade(dev->data_host.integrator.max_closures, grid, block, s, kg, dev->bufs, ln.tile, cam_n,
+  cy_launch_shade(dev->data_host.integrator.max_closures, dev->shade_tex, grid, block, s, kg, dev->bufs, ln.tile, cam_n,
                   ln.slot_base, ln.q[qa], ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.c, s));

@@ -3,7 +3,10 @@
  * size (k_shade.hip with CY_MAX_CLOSURE = 1, 2, 4, 8).  A scene's
  * KernelIntegrator.max_closures (render/integrator.cpp) picks the smallest
  * variant that holds its shaders' closures, so the per-path closure array
- * stays small enough to live in registers instead of scratch.
+ * stays small enough to live in registers instead of scratch.  Each size is
+ * built twice: plain (CY_SVM_TEX=0: closure nodes only, constant world) and
+ * "_tex" with the texture / converter / input nodes and node worlds; the
+ * plain kernels keep the register allocation of scenes that need no nodes.
  */
 #ifndef K_SHADE_H
 #define K_SHADE_H
@@ -21,13 +24,21 @@ void cy_launch_shade_mc1(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc2(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc4(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc8(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc1_tex(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc2_tex(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc4_tex(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc8_tex(CY_SHADE_LAUNCHER_ARGS);
 
-static inline void cy_launch_shade(int max_closures, CY_SHADE_LAUNCHER_ARGS)
+static inline void cy_launch_shade(int max_closures, bool tex_nodes, CY_SHADE_LAUNCHER_ARGS)
 {
-  auto fn = max_closures <= 1 ? cy_launch_shade_mc1 :
-            max_closures <= 2 ? cy_launch_shade_mc2 :
-            max_closures <= 4 ? cy_launch_shade_mc4 :
-                                cy_launch_shade_mc8;
+  auto fn = tex_nodes ? (max_closures <= 1 ? cy_launch_shade_mc1_tex :
+                         max_closures <= 2 ? cy_launch_shade_mc2_tex :
+                         max_closures <= 4 ? cy_launch_shade_mc4_tex :
+                                             cy_launch_shade_mc8_tex) :
+                        (max_closures <= 1 ? cy_launch_shade_mc1 :
+                         max_closures <= 2 ? cy_launch_shade_mc2 :
+                         max_closures <= 4 ? cy_launch_shade_mc4 :
+                                             cy_launch_shade_mc8);
   fn(grid, block, stream, kg, b, tile, cam_n, slot_base, queue_in, count_in, queue_out, count_out, shadow_queue, shadow_count, err);
 }
 

@@ -512,6 +512,63 @@ CY_FN void accumulate_pixel(const CyTile *tile, int p)
   buf[3] = b3;
 }
 
+/* shader_setup_from_background (kernel_shader.h:397-439): P = D, N = Ng = I = -D */
+CY_FN void shader_setup_from_background(const CyGlobals *kg, CySD *sd, cfloat3 D, CyShadeMem mem)
+{
+  sd->closure = mem.closure;
+  sd->svm_stack = mem.svm_stack;
+  sd->svm_stride = mem.svm_stride;
+  sd->svm_fast = mem.svm_fast;
+  sd->svm_spill = mem.svm_spill;
+  sd->P = D;
+  sd->N = neg3(D);
+  sd->Ng = neg3(D);
+  sd->I = neg3(D);
+  sd->shader = KD->background.surface_shader;
+  sd->flag = kg->__shaders[sd->shader & SHADER_MASK].flags;
+  sd->object_flag = 0;
+  sd->ray_length = 0.0f;
+  sd->object = OBJECT_NONE;
+  sd->prim = PRIM_NONE;
+  sd->type = 0; /* PRIMITIVE_NONE */
+  sd->u = 0.0f;
+  sd->v = 0.0f;
+  sd->svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
+  sd->closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
+  sd->closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);
+}
+
+/* shader_background_eval (kernel_shader.h:996-1004) */
+CY_FN cfloat3 shader_background_eval(const CySD *sd)
+{
+  return (sd->flag & SD_EMISSION) ? sd->closure_emission_background : mk3(0.0f, 0.0f, 0.0f);
+}
+
+/* indirect_background's non-constant branch (kernel_emission.h:309-321): the
+ * world shader evaluated along the ray with the bounce raised for the
+ * light-path node (path_state_modify_bounce). */
+CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
+                                        const hc_uint4 *svm_nodes,
+                                        const hc_KernelShader *shaders,
+                                        const hc_KernelObject *objects,
+                                        cfloat3 D,
+                                        CyShadeMem mem,
+                                        CyPathState state,
+                                        uint *err)
+{
+  CyGlobals kgv;
+  kgv.data = data;
+  kgv.__svm_nodes = svm_nodes;
+  kgv.__shaders = shaders;
+  kgv.__objects = objects;
+  const CyGlobals *kg = &kgv;
+  CySD esd;
+  shader_setup_from_background(kg, &esd, D, mem);
+  state.bounce += 1;
+  shader_eval_surface(kg, &esd, &state, state.flag | PATH_RAY_EMISSION, err);
+  return shader_background_eval(&esd);
+}
+
 /* ---------------------------------------------------------------------------
  * Stage 2: shade one path at one bounce.  Returns true when the slot must be
  * enqueued for the next closest-hit traversal.  *shadow is set when a shadow ray
@@ -640,7 +697,14 @@ CY_FN bool shade_path(const CyGlobals *kg,
       cfloat3 L_background = mk3(0.0f, 0.0f, 0.0f);
       if (!excluded) {
         if (!shader_constant_emission_eval(kg, (int)shader, &L_background)) {
-          cy_set_error(err, CY_ERR_FEATURE, 3); /* non-constant world shader */
+          /* world shader evaluated along the ray, bounce raised for the
+           * light-path node (path_state_modify_bounce) */
+#if CY_SVM_TEX
+          L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, ray.D,
+                                             mem, state, err);
+#else
+          cy_set_error(err, CY_ERR_FEATURE, 3); /* node world in the kernel without texture nodes */
+#endif
         }
         if (!(state.flag & PATH_RAY_MIS_SKIP) && KD->background.use_mis) {
           cy_set_error(err, CY_ERR_FEATURE, 4); /* background MIS */
@@ -677,7 +741,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     sd.closure[0].N = sd.N;
     sd.flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
 #else
-    shader_eval_surface(kg, &sd, state.flag, err);
+    shader_eval_surface(kg, &sd, &state, state.flag, err);
 #endif
     shader_prepare_closures(&sd, &state);
 
@@ -912,33 +976,11 @@ CY_FN cfloat3 equirectangular_to_direction(float u, float v)
 CY_FN cfloat3 background_evaluate(const CyGlobals *kg, uint in_u, uint in_v, CyShadeMem mem, uint *err)
 {
   const cfloat3 D = equirectangular_to_direction(as_float(in_u), as_float(in_v));
-  /* shader_setup_from_background (kernel_shader.h:397-439), ray.P = 0, ray.t = 0 */
   CySD sd;
-  sd.closure = mem.closure;
-  sd.svm_stack = mem.svm_stack;
-  sd.svm_stride = mem.svm_stride;
-  sd.svm_fast = mem.svm_fast;
-  sd.svm_spill = mem.svm_spill;
-  sd.P = D;
-  sd.N = neg3(D);
-  sd.Ng = neg3(D);
-  sd.I = neg3(D);
-  sd.shader = KD->background.surface_shader;
-  sd.flag = kg->__shaders[sd.shader & SHADER_MASK].flags;
-  sd.object_flag = 0;
-  sd.ray_length = 0.0f;
-  sd.object = OBJECT_NONE;
-  sd.prim = PRIM_NONE;
-  sd.type = 0; /* PRIMITIVE_NONE */
-  sd.u = 0.0f;
-  sd.v = 0.0f;
-  sd.svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
-  sd.closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
-  sd.closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);
+  shader_setup_from_background(kg, &sd, D, mem);
   /* path_flag 0 | PATH_RAY_EMISSION: no BSDF closures are kept */
-  shader_eval_surface(kg, &sd, PATH_RAY_EMISSION, err);
-  /* shader_background_eval (kernel_shader.h:996-1004) */
-  return (sd.flag & SD_EMISSION) ? sd.closure_emission_background : mk3(0.0f, 0.0f, 0.0f);
+  shader_eval_surface(kg, &sd, nullptr, PATH_RAY_EMISSION, err);
+  return shader_background_eval(&sd);
 }
 
 #endif /* CY_INTEGRATOR_H */

@@ -509,8 +509,30 @@ CY_FN double cy_sincos_reduce(double x, const struct cy_sincos_t *p, int *np)
   *np = n;
   return fma(-(double)n, p->hpi, x);
 }
-/* |x| >= 120 never occurs on the path (arguments are 2*pi*u, u in [0,1)); the
- * large-argument branch falls back to a double evaluation. */
+/* glibc's large-argument reduction (sincosf.h reduce_large): x * 4/pi from the
+ * bits of 4/pi (__inv_pio4) in 64-bit integer arithmetic.  With it cy_sinf /
+ * cy_cosf match the container's libm on every float (checked exhaustively). */
+CY_CONST uint32_t cy_inv_pio4[24] = {
+    0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+    0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
+CY_FN double cy_sincos_reduce_large(uint xi, int *np)
+{
+  const uint32_t *arr = &cy_inv_pio4[(xi >> 26) & 15];
+  const int shift = (xi >> 23) & 7;
+  xi = (xi & 0xffffff) | 0x800000;
+  xi <<= shift;
+  uint64_t res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+  const uint64_t res1 = (uint64_t)xi * arr[4];
+  const uint64_t res2 = (uint64_t)xi * arr[8];
+  res0 = (res2 >> 32) | (res0 << 32);
+  res0 += res1;
+  const uint64_t n = (res0 + (1ull << 61)) >> 62;
+  res0 -= n << 62;
+  const double x = (double)(int64_t)res0;
+  *np = (int)n;
+  return x * 0x1.921FB54442D18p-62;
+}
 CY_FN float cy_sinf(float y)
 {
   double x = y;
@@ -531,7 +553,16 @@ CY_FN float cy_sinf(float y)
     }
     return cy_sincos_poly(x * s, x * x, p, n);
   }
-  return (float)sin((double)y);
+  else if (cy_abstop12(y) < cy_abstop12(CY_INF)) {
+    const uint sign = as_uint(y) >> 31;
+    x = cy_sincos_reduce_large(as_uint(y), &n);
+    const double s = p->sign[(n + sign) & 3];
+    if ((n + sign) & 2) {
+      p = &cy_sincosf_table[1];
+    }
+    return cy_sincos_poly(x * s, x * x, p, n);
+  }
+  return (y - y) / (y - y);
 }
 CY_FN float cy_cosf(float y)
 {
@@ -553,7 +584,16 @@ CY_FN float cy_cosf(float y)
     }
     return cy_sincos_poly(x * s, x * x, p, n ^ 1);
   }
-  return (float)cos((double)y);
+  else if (cy_abstop12(y) < cy_abstop12(CY_INF)) {
+    const uint sign = as_uint(y) >> 31;
+    x = cy_sincos_reduce_large(as_uint(y), &n);
+    const double s = p->sign[(n + sign) & 3];
+    if ((n + sign) & 2) {
+      p = &cy_sincosf_table[1];
+    }
+    return cy_sincos_poly(x * s, x * x, p, n ^ 1);
+  }
+  return (y - y) / (y - y);
 }
 #endif
 
@@ -676,6 +716,14 @@ CY_FN float cy_powf(float x, float y)
 {
   return powf(x, y);
 }
+CY_FN float cy_expf(float x)
+{
+  return expf(x);
+}
+CY_FN float cy_logf(float x)
+{
+  return logf(x);
+}
 #else
 struct cy_powf_t {
   double invc[16], logc[16];
@@ -719,12 +767,81 @@ CY_FN uint64_t cy_as_u64(double d)
   return u;
 }
 
+/* glibc powf's classification of y (e_powf.c checkint): 0 not an integer,
+ * 1 odd integer, 2 even integer */
+CY_FN int cy_powf_checkint(uint iy)
+{
+  const int e = (int)(iy >> 23 & 0xff);
+  if (e < 0x7f) {
+    return 0;
+  }
+  if (e > 0x7f + 23) {
+    return 2;
+  }
+  if (iy & ((1u << (0x7f + 23 - e)) - 1u)) {
+    return 0;
+  }
+  if (iy & (1u << (0x7f + 23 - e))) {
+    return 1;
+  }
+  return 2;
+}
+CY_FN bool cy_powf_zeroinfnan(uint ix)
+{
+  return 2u * ix - 1u >= 2u * 0x7f800000u - 1u;
+}
+
+/* glibc 2.35 powf (e_powf.c, FMA variant), every special case included:
+ * zero / inf / nan operands, negative x with integer y, subnormal x,
+ * overflow and underflow (the math node's POWER, svm_math_util.h). */
 CY_FN float cy_powf(float x, float y)
 {
   const struct cy_powf_t *T = &cy_powf_table;
-  const uint ix = as_uint(x);
-  if (!(x == x) || ix == 0x7f800000u) {
-    return x; /* NaN, +inf */
+  uint sign_bias = 0;
+  uint ix = as_uint(x);
+  const uint iy = as_uint(y);
+  if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || cy_powf_zeroinfnan(iy)) {
+    if (cy_powf_zeroinfnan(iy)) {
+      /* issignalingf_inline: a signaling NaN operand propagates */
+      if (2u * iy == 0u) {
+        return (2u * (ix ^ 0x00400000u) > 2u * 0x7fc00000u) ? x + y : 1.0f;
+      }
+      if (ix == 0x3f800000u) {
+        return (2u * (iy ^ 0x00400000u) > 2u * 0x7fc00000u) ? x + y : 1.0f;
+      }
+      if (2u * ix > 2u * 0x7f800000u || 2u * iy > 2u * 0x7f800000u) {
+        return x + y;
+      }
+      if (2u * ix == 2u * 0x3f800000u) {
+        return 1.0f;
+      }
+      if ((2u * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u)) {
+        return 0.0f;
+      }
+      return y * y;
+    }
+    if (cy_powf_zeroinfnan(ix)) {
+      float x2 = x * x;
+      if ((ix & 0x80000000u) && cy_powf_checkint(iy) == 1) {
+        x2 = -x2;
+      }
+      return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+    }
+    if (ix & 0x80000000u) {
+      const int yint = cy_powf_checkint(iy);
+      if (yint == 0) {
+        return (x - x) / (x - x);
+      }
+      if (yint == 1) {
+        sign_bias = 1u << 16;
+      }
+      ix &= 0x7fffffffu;
+    }
+    if (ix < 0x00800000u) {
+      ix = as_uint(as_float(ix) * 0x1p23f);
+      ix &= 0x7fffffffu;
+      ix -= 23u << 23;
+    }
   }
   /* log2_inline */
   const uint tmp = ix - 0x3f330000u;
@@ -742,20 +859,108 @@ CY_FN float cy_powf(float x, float y)
   double q = fma(T->A[4], r, y0);
   q = fma(p3, r2, q);
   p5 = fma(p5, r4, q);
-  /* exp2_inline */
   const double xd = (double)y * p5;
+  if (((cy_as_u64(xd) >> 47) & 0xffff) >= (cy_as_u64(126.0) >> 47)) {
+    if (xd > 0x1.fffffffd1d571p+6) {
+      return sign_bias ? -CY_INF : CY_INF;
+    }
+    if (xd <= -150.0) {
+      return sign_bias ? as_float(0x80000000u) : 0.0f; /* signed underflow */
+    }
+  }
+  /* exp2_inline */
   const double shift = 0x1.8p+47;
   double kd = xd + shift;
   const uint64_t ki = cy_as_u64(kd);
   kd -= shift;
   const double rr = xd - kd;
-  const uint64_t t = T->E[ki % 32u] + (ki << 47);
+  const uint64_t t = T->E[ki % 32u] + ((ki + sign_bias) << 47);
   const double s = cy_as_double(t);
   const double zz = fma(T->C[0], rr, T->C[1]);
   const double rr2 = rr * rr;
   double e = fma(T->C[2], rr, 1.0);
   e = fma(zz, rr2, e);
   return (float)(e * s);
+}
+
+/* glibc 2.35 expf (e_expf.c, FMA variant): 2^(k/32) from the exp2f table and
+ * a cubic in the remainder; matches the container's libm on every float. */
+CY_FN float cy_expf(float x)
+{
+  const struct cy_powf_t *T = &cy_powf_table;
+  const uint abstop = (as_uint(x) >> 20) & 0x7ff;
+  if (abstop >= ((as_uint(88.0f) >> 20) & 0x7ff)) {
+    if (as_uint(x) == as_uint(-CY_INF)) {
+      return 0.0f;
+    }
+    if (abstop >= ((as_uint(CY_INF) >> 20) & 0x7ff)) {
+      return x + x;
+    }
+    if (x > 0x1.62e42ep6f) {
+      return CY_INF;
+    }
+    if (x < -0x1.9fe368p6f) {
+      return 0.0f;
+    }
+  }
+  const double N = 32.0;
+  const double InvLn2N = 0x1.71547652b82fep+0 * N;
+  const double xd = (double)x;
+  const double z = InvLn2N * xd;
+  const double shift = 0x1.8p+52;
+  double kd = z + shift;
+  const uint64_t ki = cy_as_u64(kd);
+  kd -= shift;
+  const double r = fma(InvLn2N, xd, -kd);
+  const uint64_t t = T->E[ki % 32u] + (ki << 47);
+  const double s = cy_as_double(t);
+  const double zz = fma(T->C[0] / (N * N * N), r, T->C[1] / (N * N));
+  const double r2 = r * r;
+  double y = fma(T->C[2] / N, r, 1.0);
+  y = fma(zz, r2, y);
+  return (float)(y * s);
+}
+
+/* glibc 2.35 logf (e_logf.c): log(c) table over 16 subintervals of [0.7, 1.4]
+ * (the same 1/c as powf's log2 table) and a cubic; matches the container's
+ * libm on every float. */
+CY_CONST double cy_logf_logc[16] = {
+    -0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3,
+    -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3,   -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611ccp-4,
+    -0x1.252f438e10c1ep-5, 0x0p+0,                0x1.aa5aa5df25984p-5,  0x1.c5e53aa362eb4p-4,
+    0x1.526e57720db08p-3,  0x1.bc2860d22477p-3,   0x1.1058bc8a07ee1p-2,  0x1.4043057b6ee09p-2};
+CY_FN float cy_logf(float x)
+{
+  const struct cy_powf_t *T = &cy_powf_table;
+  uint ix = as_uint(x);
+  if (ix == 0x3f800000u) {
+    return 0.0f;
+  }
+  if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+    if (ix * 2u == 0u) {
+      return -CY_INF;
+    }
+    if (ix == 0x7f800000u) {
+      return x;
+    }
+    if ((ix & 0x80000000u) || ix * 2u >= 0xff000000u) {
+      return (x - x) / (x - x);
+    }
+    ix = as_uint(x * 0x1p23f);
+    ix -= 23u << 23;
+  }
+  const uint tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> 19) % 16u);
+  const int k = (int)tmp >> 23;
+  const uint iz = ix - (tmp & 0xff800000u);
+  const double z = (double)as_float(iz);
+  const double r = z * T->invc[i] - 1.0;
+  const double y0 = cy_logf_logc[i] + (double)k * 0x1.62e42fefa39efp-1;
+  const double r2 = r * r;
+  double y = 0x1.5575b0be00b6ap-2 * r + -0x1.ffffef20a4123p-2;
+  y = -0x1.00ea348b88334p-2 * r2 + y;
+  y = y * r2 + (y0 + r);
+  return (float)y;
 }
 #endif
 
@@ -769,6 +974,10 @@ CY_FN float cy_powf(float x, float y)
 CY_FN float cy_atan2f(float y, float x)
 {
   return atan2f(y, x);
+}
+CY_FN float cy_atanf(float x)
+{
+  return atanf(x);
 }
 #else
 struct cy_atanf_t {

@@ -1369,6 +1369,8 @@ CY_FN void svm_store3(CySvmStack stack, uint a, cfloat3 f, uint *err)
   svm_store(stack, a + 2, f.z, err);
 }
 
+#include "cy_svm_nodes.h"
+
 CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, float roughness, bool refract)
 {
   if (type == CLOSURE_BSDF_SHARP_GLASS_ID) {
@@ -1542,7 +1544,126 @@ CY_FN void emission_setup(CySD *sd, cfloat3 weight)
   }
 }
 
-CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, int path_flag, uint *err)
+/* Texture / converter / input nodes (cy_svm_nodes.h).  Compiled only into the
+ * kernels built with CY_SVM_TEX=1: the shading kernel exists in a variant
+ * without them (picked at load_kernels when no shader uses them), whose
+ * register allocation they would otherwise burden.  Returns the next node
+ * offset, or -1 for an unknown node. */
+typedef struct CySvmTexIn {
+  cfloat3 P, N, Ng, I;
+  float u, v, ray_length;
+  int object, flag;
+  int bounce, diffuse_bounce, glossy_bounce, transparent_bounce, transmission_bounce;
+} CySvmTexIn;
+
+CY_FN int svm_eval_texture_node(const hc_KernelData *data,
+                                      const hc_uint4 *svm_nodes,
+                                      const hc_KernelObject *objects,
+                                      CySvmTexIn in,
+                                      CySvmStack stack,
+                                      hc_uint4 node,
+                                      int path_flag,
+                                      int offset,
+                                      uint *err)
+{
+  /* the three arrays the nodes read, in a local CyGlobals (registers) */
+  CyGlobals kgv;
+  kgv.data = data;
+  kgv.__svm_nodes = svm_nodes;
+  kgv.__objects = objects;
+  const CyGlobals *kg = &kgv;
+  CySD sdv;
+  CySD *sd = &sdv;
+  sdv.P = in.P;
+  sdv.N = in.N;
+  sdv.Ng = in.Ng;
+  sdv.I = in.I;
+  sdv.u = in.u;
+  sdv.v = in.v;
+  sdv.ray_length = in.ray_length;
+  sdv.object = in.object;
+  sdv.flag = in.flag;
+  CyPathState stv;
+  const CyPathState *state = &stv;
+  stv.bounce = in.bounce;
+  stv.diffuse_bounce = in.diffuse_bounce;
+  stv.glossy_bounce = in.glossy_bounce;
+  stv.transparent_bounce = in.transparent_bounce;
+  stv.transmission_bounce = in.transmission_bounce;
+  switch (node.x) {
+      case NODE_GEOMETRY:
+        svm_node_geometry(sd, stack, node.y, node.z, err);
+        break;
+      case NODE_CONVERT:
+        svm_node_convert(kg, stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_TEX_COORD:
+        svm_node_tex_coord(kg, sd, path_flag, stack, node, &offset, err);
+        break;
+      case NODE_HSV:
+        svm_node_hsv(stack, node, err);
+        break;
+      case NODE_MATH:
+        svm_node_math(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_VECTOR_MATH:
+        svm_node_vector_math(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_RGB_RAMP:
+        svm_node_rgb_ramp(kg, stack, node, &offset, err);
+        break;
+      case NODE_GAMMA:
+        svm_node_gamma(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_BRIGHTCONTRAST:
+        svm_node_brightness(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_LIGHT_PATH:
+        svm_node_light_path(sd, state, stack, node.y, node.z, path_flag, err);
+        break;
+      case NODE_MAPPING:
+        svm_node_mapping(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_TEX_GRADIENT:
+        svm_node_tex_gradient(stack, node, err);
+        break;
+      case NODE_TEX_CHECKER:
+        svm_node_tex_checker(stack, node, err);
+        break;
+      case NODE_LIGHT_FALLOFF:
+        svm_node_light_falloff(sd, stack, node, err);
+        break;
+      case NODE_INVERT:
+        svm_node_invert(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_MIX:
+        svm_node_mix(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_SEPARATE_VECTOR:
+        svm_node_separate_vector(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_COMBINE_VECTOR:
+        svm_node_combine_vector(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_SEPARATE_HSV:
+        svm_node_separate_hsv(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_COMBINE_HSV:
+        svm_node_combine_hsv(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_MAP_RANGE:
+        svm_node_map_range(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_CLAMP:
+        svm_node_clamp(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      default:
+        return -1;
+  }
+  return offset;
+}
+
+CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err)
 {
   CySvmStack stack;
   stack.p = sd->svm_stack;
@@ -1658,14 +1779,41 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, int path_flag, uint *er
         break;
       }
       default:
+#if !CY_SVM_TEX
         cy_set_error(err, CY_ERR_SVM_NODE, node.x);
         return;
+#else
+      {
+        CySvmTexIn in;
+        in.P = sd->P;
+        in.N = sd->N;
+        in.Ng = sd->Ng;
+        in.I = sd->I;
+        in.u = sd->u;
+        in.v = sd->v;
+        in.ray_length = sd->ray_length;
+        in.object = sd->object;
+        in.flag = sd->flag;
+        in.bounce = state ? state->bounce : 0; /* background SHADER task: PathState {0} */
+        in.diffuse_bounce = state ? state->diffuse_bounce : 0;
+        in.glossy_bounce = state ? state->glossy_bounce : 0;
+        in.transparent_bounce = state ? state->transparent_bounce : 0;
+        in.transmission_bounce = state ? state->transmission_bounce : 0;
+        offset = svm_eval_texture_node(kg->data, kg->__svm_nodes, kg->__objects, in, stack, node, path_flag, offset, err);
+        if (offset < 0) {
+          cy_set_error(err, CY_ERR_SVM_NODE, node.x);
+          return;
+        }
+        break;
+      }
+#endif
     }
   }
 }
 
 /* kernel_shader.h:1057-1112 */
-CY_FN void shader_eval_surface(const CyGlobals *kg, CySD *sd, int path_flag, uint *err)
+CY_FN void shader_eval_surface(
+    const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err)
 {
   int max_closures;
   if (path_flag & (PATH_RAY_TERMINATE | PATH_RAY_SHADOW | PATH_RAY_EMISSION)) {
@@ -1676,7 +1824,7 @@ CY_FN void shader_eval_surface(const CyGlobals *kg, CySD *sd, int path_flag, uin
   }
   sd->num_closure = 0;
   sd->num_closure_left = max_closures;
-  svm_eval_nodes(kg, sd, path_flag, err);
+  svm_eval_nodes(kg, sd, state, path_flag, err);
 }
 
 /* kernel_shader.h:527-551 */

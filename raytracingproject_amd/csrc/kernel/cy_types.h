@@ -217,6 +217,12 @@ enum {
 #  define CY_MAX_CLOSURE 8 /* per-kernel closure array (k_shade.hip builds 1, 2, 4, 8) */
 #endif
 #define CY_SVM_STACK 32
+/* 1: the SVM interpreter includes the texture / converter / input nodes
+ * (cy_svm_nodes.h) and non-constant world shaders; the shading kernel is also
+ * built with 0 for scenes that use neither (hipcy_load_kernels picks). */
+#ifndef CY_SVM_TEX
+#  define CY_SVM_TEX 1
+#endif
 /* threads per workgroup of every wavefront kernel, and LDS-resident traversal
  * stack depth (CY_LDS_STACK * CY_BLOCK * 4 B = 32 KiB per workgroup) */
 #define CY_BLOCK 256

@@ -1,0 +1,592 @@
+"""Shader node graph: texture, converter and input nodes feeding closure inputs.
+
+The host side of the SVM nodes in csrc/kernel/cy_svm_nodes.h.  A node is built
+with one of the constructors below; indexing it by an output name gives a
+`Socket` that can be passed wherever a closure (scene.Closure) or another node
+takes an input.  Plain numbers / 3-tuples stay constants.
+
+Encodings follow the reference's ShaderNode::compile (render/nodes.cpp) and the
+kernel decoders (kernel/svm/svm_*.h):
+  * every linked or constant input gets a stack slot (SVMCompiler::stack_assign,
+    render/svm.cpp:140-200; constants through NODE_VALUE_F / NODE_VALUE_V);
+  * inputs the kernel reads with stack_load_float_default (checker scale,
+    clamp min/max, map-range bounds) pass SVM_STACK_INVALID plus the value when
+    unlinked (stack_assign_if_linked);
+  * implicit socket conversions insert NODE_CONVERT (render/graph.cpp:250-300
+    ConvertNode): float -> color/vector (FV), color -> float (CF, film rgb_to_y),
+    vector -> float (VF).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+SVM_STACK_INVALID = 255
+
+# svm_types.h node ids
+NODE_GEOMETRY = 11
+NODE_CONVERT = 12
+NODE_TEX_COORD = 13
+NODE_VALUE_F = 14
+NODE_VALUE_V = 15
+NODE_HSV = 36
+NODE_MATH = 42
+NODE_VECTOR_MATH = 43
+NODE_RGB_RAMP = 44
+NODE_GAMMA = 45
+NODE_BRIGHTCONTRAST = 46
+NODE_LIGHT_PATH = 47
+NODE_MAPPING = 52
+NODE_TEX_GRADIENT = 57
+NODE_TEX_CHECKER = 62
+NODE_LIGHT_FALLOFF = 66
+NODE_INVERT = 72
+NODE_MIX = 73
+NODE_SEPARATE_VECTOR = 74
+NODE_COMBINE_VECTOR = 75
+NODE_SEPARATE_HSV = 76
+NODE_COMBINE_HSV = 77
+NODE_MAP_RANGE = 83
+NODE_CLAMP = 84
+
+# svm_types.h enums (the names are the Blender UI's, lower-cased)
+MATH_OPS = ["add", "subtract", "multiply", "divide", "sine", "cosine", "tangent", "arcsine", "arccosine",
+            "arctangent", "power", "logarithm", "minimum", "maximum", "round", "less_than", "greater_than",
+            "modulo", "absolute", "arctan2", "floor", "ceil", "fraction", "sqrt", "inv_sqrt", "sign",
+            "exponent", "radians", "degrees", "sinh", "cosh", "tanh", "trunc", "snap", "wrap", "compare",
+            "multiply_add", "pingpong", "smooth_min", "smooth_max"]
+# restated in the HIP kernel bit-exactly; the rest (libm tan/sinh/cosh/tanh) are rejected
+MATH_OPS_SUPPORTED = [op for op in MATH_OPS if op not in ("tangent", "sinh", "cosh", "tanh")]
+VECTOR_MATH_OPS = ["add", "subtract", "multiply", "divide", "cross_product", "project", "reflect",
+                   "dot_product", "distance", "length", "scale", "normalize", "snap", "floor", "ceil",
+                   "modulo", "fraction", "absolute", "minimum", "maximum", "wrap", "sine", "cosine",
+                   "tangent"]
+VECTOR_MATH_VALUE_OPS = ("dot_product", "distance", "length")
+MIX_TYPES = ["mix", "add", "multiply", "subtract", "screen", "divide", "difference", "darken", "lighten",
+             "overlay", "dodge", "burn", "hue", "saturation", "value", "color", "soft_light", "linear_light"]
+NODE_MIX_CLAMP = 18
+GRADIENT_TYPES = ["linear", "quadratic", "easing", "diagonal", "radial", "quadratic_sphere", "spherical"]
+TEXCO_OUTPUTS = {"Normal": 0, "Object": 1, "Camera": 2, "Window": 3, "Reflection": 4}
+GEOMETRY_OUTPUTS = {"Position": 0, "Normal": 1, "Incoming": 3, "True Normal": 4, "Parametric": 5}
+LIGHT_PATH_OUTPUTS = ["Is Camera Ray", "Is Shadow Ray", "Is Diffuse Ray", "Is Glossy Ray", "Is Singular Ray",
+                      "Is Reflection Ray", "Is Transmission Ray", "Is Volume Scatter Ray", "Is Backfacing",
+                      "Ray Length", "Ray Depth", "Diffuse Depth", "Glossy Depth", "Transparent Depth",
+                      "Transmission Depth"]
+LIGHT_FALLOFF_OUTPUTS = {"Quadratic": 0, "Linear": 1, "Constant": 2}
+MAPPING_TYPES = ["point", "texture", "vector", "normal"]
+CLAMP_TYPES = ["minmax", "range"]
+MAP_RANGE_TYPES = ["linear", "stepped", "smoothstep", "smootherstep"]
+
+CONVERT_FV, CONVERT_CF, CONVERT_VF = 0, 2, 4
+
+
+def f32bits(x: float) -> int:
+    return int(np.array([x], dtype=np.float32).view(np.uint32)[0])
+
+
+def uchar4(x, y=0, z=0, w=0) -> int:
+    return (x & 0xFF) | ((y & 0xFF) << 8) | ((z & 0xFF) << 16) | ((w & 0xFF) << 24)
+
+
+@dataclass(eq=False)
+class Node:
+    kind: str
+    inputs: dict = field(default_factory=dict)
+    params: dict = field(default_factory=dict)
+
+    def __getitem__(self, name: str) -> "Socket":
+        if name not in _outputs(self):
+            raise KeyError(f"{self.kind} node has no output {name!r}; outputs: {sorted(_outputs(self))}")
+        return Socket(self, name)
+
+
+@dataclass(frozen=True, eq=False)
+class Socket:
+    node: Node
+    name: str
+
+    @property
+    def type(self) -> str:
+        return _outputs(self.node)[self.name]
+
+
+def is_linked(v) -> bool:
+    return isinstance(v, Socket)
+
+
+# ---------------------------------------------------------------------------
+# constructors (render/nodes.cpp socket names and defaults)
+
+
+def value(v: float) -> Socket:
+    return Node("value", params={"value": float(v)})["Value"]
+
+
+def rgb(c) -> Socket:
+    return Node("rgb", params={"value": tuple(float(x) for x in c)})["Color"]
+
+
+def tex_coord() -> Node:
+    return Node("tex_coord")
+
+
+def geometry() -> Node:
+    return Node("geometry")
+
+
+def light_path() -> Node:
+    return Node("light_path")
+
+
+def light_falloff(strength=100.0, smooth=0.0) -> Node:
+    return Node("light_falloff", {"Strength": strength, "Smooth": smooth})
+
+
+def math(op: str, a=0.5, b=0.5, c=0.0, clamp: bool = False) -> Socket:
+    if op not in MATH_OPS:
+        raise ValueError(f"unknown math op {op!r}")
+    return Node("math", {"Value1": a, "Value2": b, "Value3": c}, {"op": op, "clamp": clamp})["Value"]
+
+
+def vector_math(op: str, a=(0.0, 0.0, 0.0), b=(0.0, 0.0, 0.0), c=(0.0, 0.0, 0.0), scale=1.0) -> Node:
+    if op not in VECTOR_MATH_OPS:
+        raise ValueError(f"unknown vector math op {op!r}")
+    return Node("vector_math", {"Vector1": a, "Vector2": b, "Vector3": c, "Scale": scale}, {"op": op})
+
+
+def mix_rgb(blend: str, fac, color1, color2, clamp: bool = False) -> Socket:
+    if blend not in MIX_TYPES:
+        raise ValueError(f"unknown mix type {blend!r}")
+    return Node("mix", {"Fac": fac, "Color1": color1, "Color2": color2}, {"type": blend, "clamp": clamp})["Color"]
+
+
+def hsv(color, hue=0.5, saturation=1.0, value_=1.0, fac=1.0) -> Socket:
+    return Node("hsv", {"Hue": hue, "Saturation": saturation, "Value": value_, "Fac": fac, "Color": color})["Color"]
+
+
+def gamma(color, g=1.0) -> Socket:
+    return Node("gamma", {"Color": color, "Gamma": g})["Color"]
+
+
+def bright_contrast(color, bright=0.0, contrast=0.0) -> Socket:
+    return Node("brightcontrast", {"Color": color, "Bright": bright, "Contrast": contrast})["Color"]
+
+
+def invert(color, fac=1.0) -> Socket:
+    return Node("invert", {"Fac": fac, "Color": color})["Color"]
+
+
+def checker(vector, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), scale=5.0) -> Node:
+    return Node("checker", {"Vector": vector, "Color1": color1, "Color2": color2, "Scale": scale})
+
+
+def gradient(vector, kind: str = "linear") -> Node:
+    if kind not in GRADIENT_TYPES:
+        raise ValueError(f"unknown gradient type {kind!r}")
+    return Node("gradient", {"Vector": vector}, {"type": kind})
+
+
+def mapping(vector, location=(0.0, 0.0, 0.0), rotation=(0.0, 0.0, 0.0), scale=(1.0, 1.0, 1.0),
+            kind: str = "point") -> Socket:
+    if kind not in MAPPING_TYPES:
+        raise ValueError(f"unknown mapping type {kind!r}")
+    return Node("mapping", {"Vector": vector, "Location": location, "Rotation": rotation, "Scale": scale},
+                {"type": kind})["Vector"]
+
+
+def separate_xyz(vector) -> Node:
+    return Node("separate_xyz", {"Vector": vector})
+
+
+def combine_xyz(x=0.0, y=0.0, z=0.0) -> Socket:
+    return Node("combine_xyz", {"X": x, "Y": y, "Z": z})["Vector"]
+
+
+def separate_hsv(color) -> Node:
+    return Node("separate_hsv", {"Color": color})
+
+
+def combine_hsv(h=0.0, s=0.0, v=0.0) -> Socket:
+    return Node("combine_hsv", {"H": h, "S": s, "V": v})["Color"]
+
+
+def clamp(value_, min_=0.0, max_=1.0, kind: str = "minmax") -> Socket:
+    return Node("clamp", {"Value": value_, "Min": min_, "Max": max_}, {"type": kind})["Result"]
+
+
+def map_range(value_, from_min=0.0, from_max=1.0, to_min=0.0, to_max=1.0, steps=4.0,
+              kind: str = "linear") -> Socket:
+    return Node("map_range", {"Value": value_, "From Min": from_min, "From Max": from_max, "To Min": to_min,
+                              "To Max": to_max, "Steps": steps}, {"type": kind})["Result"]
+
+
+def color_ramp(fac, stops, interpolation: str = "linear", table_size: int = 256) -> Node:
+    """ColorRamp: `stops` = [(position, (r, g, b, a)), ...] baked to a table of
+    `table_size` entries the way the host does (RGBRampNode, BKE colorband
+    evaluation at i / (size - 1)); constant interpolation looks up the stop at
+    or before the position."""
+    pts = sorted(stops, key=lambda s: s[0])
+    pos = np.array([p for p, _ in pts], dtype=np.float64)
+    col = np.array([c for _, c in pts], dtype=np.float64)
+    x = np.arange(table_size, dtype=np.float64) / (table_size - 1)
+    if interpolation == "constant":
+        idx = np.clip(np.searchsorted(pos, x, side="right") - 1, 0, len(pos) - 1)
+        table = col[idx]
+    else:
+        table = np.stack([np.interp(x, pos, col[:, k]) for k in range(4)], axis=1)
+    return Node("rgb_ramp", {"Fac": fac}, {"table": table.astype(np.float32), "interpolate": interpolation != "constant"})
+
+
+# ---------------------------------------------------------------------------
+# socket types
+
+
+def _outputs(node: Node) -> dict:
+    k = node.kind
+    if k == "value":
+        return {"Value": "float"}
+    if k == "rgb":
+        return {"Color": "color"}
+    if k == "tex_coord":
+        return {n: "vector" for n in TEXCO_OUTPUTS}
+    if k == "geometry":
+        return {n: "vector" for n in GEOMETRY_OUTPUTS}
+    if k == "light_path":
+        return {n: "float" for n in LIGHT_PATH_OUTPUTS}
+    if k == "light_falloff":
+        return {n: "float" for n in LIGHT_FALLOFF_OUTPUTS}
+    if k == "math":
+        return {"Value": "float"}
+    if k == "vector_math":
+        return {"Vector": "vector", "Value": "float"}
+    if k in ("mix", "hsv", "gamma", "brightcontrast", "invert", "combine_hsv"):
+        return {"Color": "color"}
+    if k in ("checker", "gradient"):
+        return {"Color": "color", "Fac": "float"}
+    if k in ("mapping", "combine_xyz"):
+        return {"Vector": "vector"}
+    if k == "separate_xyz":
+        return {"X": "float", "Y": "float", "Z": "float"}
+    if k == "separate_hsv":
+        return {"H": "float", "S": "float", "V": "float"}
+    if k in ("clamp", "map_range"):
+        return {"Result": "float"}
+    if k == "rgb_ramp":
+        return {"Color": "color", "Alpha": "float"}
+    raise ValueError(f"unknown node kind {k!r}")
+
+
+_INPUT_TYPES = {
+    "light_falloff": {"Strength": "float", "Smooth": "float"},
+    "math": {"Value1": "float", "Value2": "float", "Value3": "float"},
+    "vector_math": {"Vector1": "vector", "Vector2": "vector", "Vector3": "vector", "Scale": "float"},
+    "mix": {"Fac": "float", "Color1": "color", "Color2": "color"},
+    "hsv": {"Hue": "float", "Saturation": "float", "Value": "float", "Fac": "float", "Color": "color"},
+    "gamma": {"Color": "color", "Gamma": "float"},
+    "brightcontrast": {"Color": "color", "Bright": "float", "Contrast": "float"},
+    "invert": {"Fac": "float", "Color": "color"},
+    "checker": {"Vector": "vector", "Color1": "color", "Color2": "color", "Scale": "float"},
+    "gradient": {"Vector": "vector"},
+    "mapping": {"Vector": "vector", "Location": "vector", "Rotation": "vector", "Scale": "vector"},
+    "separate_xyz": {"Vector": "vector"},
+    "combine_xyz": {"X": "float", "Y": "float", "Z": "float"},
+    "separate_hsv": {"Color": "color"},
+    "combine_hsv": {"H": "float", "S": "float", "V": "float"},
+    "clamp": {"Value": "float", "Min": "float", "Max": "float"},
+    "map_range": {"Value": "float", "From Min": "float", "From Max": "float", "To Min": "float",
+                  "To Max": "float", "Steps": "float"},
+    "rgb_ramp": {"Fac": "float"},
+}
+
+
+def _width(t: str) -> int:
+    return 1 if t == "float" else 3
+
+
+def upstream(v) -> list[Node]:
+    """Nodes a value depends on, dependencies first."""
+    order: list[Node] = []
+    seen: set[int] = set()
+
+    def visit(n: Node):
+        if id(n) in seen:
+            return
+        seen.add(id(n))
+        for x in n.inputs.values():
+            if is_linked(x):
+                visit(x.node)
+        order.append(n)
+
+    if is_linked(v):
+        visit(v.node)
+    return order
+
+
+# ---------------------------------------------------------------------------
+# compiler
+
+
+class NodeCompiler:
+    """Assigns stack slots and emits the node code of one shader.
+
+    `alloc(n)` / `free(off, n)` are the owning SVMCompiler's slot allocator;
+    `emit` appends to its code.  Like the reference compiler (svm.cpp
+    stack_clear_users / stack_clear_temporary), a node output's slot is
+    released once every node reading it has been emitted, and constants /
+    conversions materialised for one node's inputs right after that node;
+    outputs feeding the closures (`roots`) stay live."""
+
+    def __init__(self, alloc, emit, roots=(), free=None):
+        self.alloc = alloc
+        self.free = free or (lambda off, n: None)
+        self.emit = emit
+        self.slots: dict[tuple[int, str], int] = {}  # (id(node), output) -> slot
+        self.done: set[int] = set()
+        self.temps: list[tuple[int, int]] = []
+        # outputs some input links to: only those get a slot (stack_assign_if_linked)
+        self.used: set[tuple[int, str]] = set()
+        self.users: dict[tuple[int, str], int] = {}
+        seen: set[int] = set()
+        for v in roots:
+            for n in upstream(v):
+                if id(n) in seen:
+                    continue
+                seen.add(id(n))
+                for x in n.inputs.values():
+                    if is_linked(x):
+                        key = (id(x.node), x.name)
+                        self.used.add(key)
+                        self.users[key] = self.users.get(key, 0) + 1
+            if is_linked(v):
+                key = (id(v.node), v.name)
+                self.used.add(key)
+                self.users[key] = self.users.get(key, 0) + (1 << 30)  # pinned
+
+    # -- inputs
+    def constant(self, v, t: str) -> int:
+        if t == "float":
+            off = self.alloc(1)
+            self.emit((NODE_VALUE_F, f32bits(float(v)), off, 0))
+            return off
+        vv = (float(v),) * 3 if np.isscalar(v) else tuple(float(x) for x in v)
+        off = self.alloc(3)
+        self.emit((NODE_VALUE_V, off, 0, 0))
+        self.emit((NODE_VALUE_V, *(f32bits(x) for x in vv)))
+        return off
+
+    def link(self, s: Socket, t: str, temps: list | None = None) -> int:
+        """Stack slot of socket `s` converted to type `t`; a conversion slot is
+        appended to `temps` (or kept for the shader's lifetime when None)."""
+        self.compile_node(s.node)
+        off = self.slots[(id(s.node), s.name)]
+        st = s.type
+        if st == t or (st != "float" and t != "float"):
+            return off  # color <-> vector share the layout
+        if st == "float":
+            out = self.alloc(3)
+            self.emit((NODE_CONVERT, CONVERT_FV, off, out))
+            n = 3
+        else:
+            out = self.alloc(1)
+            self.emit((NODE_CONVERT, CONVERT_CF if st == "color" else CONVERT_VF, off, out))
+            n = 1
+        if temps is not None:
+            temps.append((out, n))
+        return out
+
+    def assign(self, v, t: str, temps: list | None = None) -> int:
+        """stack_assign: linked sockets by slot, constants materialised."""
+        if is_linked(v):
+            return self.link(v, t, temps)
+        off = self.constant(v, t)
+        if temps is not None:
+            temps.append((off, _width(t)))
+        return off
+
+    def assign_if_linked(self, v, t: str) -> int:
+        return self.link(v, t, self.temps) if is_linked(v) else SVM_STACK_INVALID
+
+    def inp(self, node: Node, name: str) -> int:
+        return self.assign(node.inputs[name], _INPUT_TYPES[node.kind][name], self.temps)
+
+    def out(self, node: Node, name: str) -> int:
+        key = (id(node), name)
+        if key not in self.used:
+            return SVM_STACK_INVALID
+        if key not in self.slots:
+            self.slots[key] = self.alloc(_width(_outputs(node)[name]))
+        return self.slots[key]
+
+    def _release(self, n: Node):
+        for off, w in self.temps:
+            self.free(off, w)
+        self.temps = []
+        for x in n.inputs.values():
+            if is_linked(x):
+                key = (id(x.node), x.name)
+                self.users[key] -= 1
+                if self.users[key] == 0:
+                    self.free(self.slots[key], _width(x.type))
+
+    # -- nodes
+    def compile_node(self, n: Node):
+        if id(n) in self.done:
+            return
+        for x in n.inputs.values():
+            if is_linked(x):
+                self.compile_node(x.node)
+        self.done.add(id(n))
+        self.temps = []
+        getattr(self, "_n_" + n.kind)(n)
+        self._release(n)
+
+    def _n_value(self, n):
+        self.emit((NODE_VALUE_F, f32bits(n.params["value"]), self.out(n, "Value"), 0))
+
+    def _n_rgb(self, n):
+        off = self.out(n, "Color")
+        self.emit((NODE_VALUE_V, off, 0, 0))
+        self.emit((NODE_VALUE_V, *(f32bits(x) for x in n.params["value"])))
+
+    def _n_tex_coord(self, n):  # nodes.cpp TextureCoordinateNode::compile
+        for name, t in TEXCO_OUTPUTS.items():
+            if (id(n), name) in self.used:
+                self.emit((NODE_TEX_COORD, t, self.out(n, name), 0))
+
+    def _n_geometry(self, n):  # nodes.cpp GeometryNode::compile
+        for name, t in GEOMETRY_OUTPUTS.items():
+            if (id(n), name) in self.used:
+                self.emit((NODE_GEOMETRY, t, self.out(n, name), 0))
+
+    def _n_light_path(self, n):  # nodes.cpp LightPathNode::compile
+        for t, name in enumerate(LIGHT_PATH_OUTPUTS):
+            if (id(n), name) in self.used:
+                self.emit((NODE_LIGHT_PATH, t, self.out(n, name), 0))
+
+    def _n_light_falloff(self, n):
+        s, sm = self.inp(n, "Strength"), self.inp(n, "Smooth")
+        for name, t in LIGHT_FALLOFF_OUTPUTS.items():
+            if (id(n), name) not in self.used:
+                continue
+            self.emit((NODE_LIGHT_FALLOFF, t, uchar4(s, sm, self.out(n, name)), 0))
+
+    def _n_math(self, n):  # nodes.cpp MathNode::compile (+ expand: use_clamp -> ClampNode 0..1)
+        a, b, c = self.inp(n, "Value1"), self.inp(n, "Value2"), self.inp(n, "Value3")
+        out = self.out(n, "Value")
+        self.emit((NODE_MATH, MATH_OPS.index(n.params["op"]), uchar4(a, b, c), out))
+        if n.params.get("clamp"):
+            self.emit((NODE_CLAMP, out, uchar4(SVM_STACK_INVALID, SVM_STACK_INVALID, 0), out))
+            self.emit((f32bits(0.0), f32bits(1.0), 0, 0))
+
+    def _n_vector_math(self, n):  # nodes.cpp VectorMathNode::compile
+        op = n.params["op"]
+        wrong = "Vector" if op in VECTOR_MATH_VALUE_OPS else "Value"
+        if (id(n), wrong) in self.used:
+            raise ValueError(f"vector math {op!r} does not write its {wrong!r} output")
+        a, b, s = self.inp(n, "Vector1"), self.inp(n, "Vector2"), self.inp(n, "Scale")
+        value_off = self.out(n, "Value") if op in VECTOR_MATH_VALUE_OPS else SVM_STACK_INVALID
+        vector_off = SVM_STACK_INVALID if op in VECTOR_MATH_VALUE_OPS else self.out(n, "Vector")
+        if op == "wrap":
+            c = self.inp(n, "Vector3")
+            self.emit((NODE_VECTOR_MATH, VECTOR_MATH_OPS.index(op), uchar4(a, b, s), uchar4(value_off, vector_off)))
+            self.emit((c, 0, 0, 0))
+        else:
+            self.emit((NODE_VECTOR_MATH, VECTOR_MATH_OPS.index(op), uchar4(a, b, s), uchar4(value_off, vector_off)))
+
+    def _n_mix(self, n):  # nodes.cpp MixNode::compile
+        fac, c1, c2 = self.inp(n, "Fac"), self.inp(n, "Color1"), self.inp(n, "Color2")
+        out = self.out(n, "Color")
+        self.emit((NODE_MIX, fac, c1, c2))
+        self.emit((NODE_MIX, MIX_TYPES.index(n.params["type"]), out, 0))
+        if n.params.get("clamp"):
+            self.emit((NODE_MIX, 0, out, 0))
+            self.emit((NODE_MIX, NODE_MIX_CLAMP, out, 0))
+
+    def _n_hsv(self, n):
+        h, s, v = self.inp(n, "Hue"), self.inp(n, "Saturation"), self.inp(n, "Value")
+        fac, col = self.inp(n, "Fac"), self.inp(n, "Color")
+        self.emit((NODE_HSV, uchar4(col, fac, self.out(n, "Color")), uchar4(h, s, v), 0))
+
+    def _n_gamma(self, n):
+        g, col = self.inp(n, "Gamma"), self.inp(n, "Color")
+        self.emit((NODE_GAMMA, g, col, self.out(n, "Color")))
+
+    def _n_brightcontrast(self, n):
+        col, br, co = self.inp(n, "Color"), self.inp(n, "Bright"), self.inp(n, "Contrast")
+        self.emit((NODE_BRIGHTCONTRAST, col, self.out(n, "Color"), uchar4(br, co)))
+
+    def _n_invert(self, n):
+        fac, col = self.inp(n, "Fac"), self.inp(n, "Color")
+        self.emit((NODE_INVERT, fac, col, self.out(n, "Color")))
+
+    def _n_checker(self, n):  # nodes.cpp CheckerTextureNode::compile (identity texture mapping)
+        vec, c1, c2 = self.inp(n, "Vector"), self.inp(n, "Color1"), self.inp(n, "Color2")
+        scale = self.assign_if_linked(n.inputs["Scale"], "float")
+        sval = 0.0 if is_linked(n.inputs["Scale"]) else float(n.inputs["Scale"])
+        self.emit((NODE_TEX_CHECKER, uchar4(vec, c1, c2, scale),
+                   uchar4(self.out(n, "Color"), self.out(n, "Fac")), f32bits(sval)))
+
+    def _n_gradient(self, n):  # nodes.cpp GradientTextureNode::compile
+        vec = self.inp(n, "Vector")
+        self.emit((NODE_TEX_GRADIENT, uchar4(GRADIENT_TYPES.index(n.params["type"]), vec, self.out(n, "Fac"),
+                                             self.out(n, "Color")), 0, 0))
+
+    def _n_mapping(self, n):  # nodes.cpp MappingNode::compile
+        v, loc = self.inp(n, "Vector"), self.inp(n, "Location")
+        rot, sc = self.inp(n, "Rotation"), self.inp(n, "Scale")
+        self.emit((NODE_MAPPING, MAPPING_TYPES.index(n.params["type"]), uchar4(v, loc, rot, sc),
+                   self.out(n, "Vector")))
+
+    def _n_separate_xyz(self, n):
+        v = self.inp(n, "Vector")
+        for i, name in enumerate("XYZ"):
+            if (id(n), name) in self.used:
+                self.emit((NODE_SEPARATE_VECTOR, v, i, self.out(n, name)))
+
+    def _n_combine_xyz(self, n):
+        out = self.out(n, "Vector")
+        for i, name in enumerate("XYZ"):
+            self.emit((NODE_COMBINE_VECTOR, self.inp(n, name), i, out))
+
+    def _n_separate_hsv(self, n):
+        col = self.inp(n, "Color")
+        self.emit((NODE_SEPARATE_HSV, col, self.out(n, "H"), self.out(n, "S")))
+        self.emit((NODE_SEPARATE_HSV, self.out(n, "V"), 0, 0))
+
+    def _n_combine_hsv(self, n):
+        h, s, v = self.inp(n, "H"), self.inp(n, "S"), self.inp(n, "V")
+        self.emit((NODE_COMBINE_HSV, h, s, v))
+        self.emit((NODE_COMBINE_HSV, self.out(n, "Color"), 0, 0))
+
+    def _defaults(self, n, names):
+        return [0.0 if is_linked(n.inputs[k]) else float(n.inputs[k]) for k in names]
+
+    def _n_clamp(self, n):  # nodes.cpp ClampNode::compile
+        v = self.inp(n, "Value")
+        mn = self.assign_if_linked(n.inputs["Min"], "float")
+        mx = self.assign_if_linked(n.inputs["Max"], "float")
+        dmin, dmax = self._defaults(n, ["Min", "Max"])
+        self.emit((NODE_CLAMP, v, uchar4(mn, mx, CLAMP_TYPES.index(n.params["type"])), self.out(n, "Result")))
+        self.emit((f32bits(dmin), f32bits(dmax), 0, 0))
+
+    def _n_map_range(self, n):  # nodes.cpp MapRangeNode::compile
+        names = ["From Min", "From Max", "To Min", "To Max"]
+        v = self.inp(n, "Value")
+        offs = [self.assign_if_linked(n.inputs[k], "float") for k in names]
+        steps = self.assign_if_linked(n.inputs["Steps"], "float")
+        d = self._defaults(n, names)
+        (dsteps,) = self._defaults(n, ["Steps"])
+        self.emit((NODE_MAP_RANGE, v, uchar4(*offs),
+                   uchar4(MAP_RANGE_TYPES.index(n.params["type"]), steps, self.out(n, "Result"))))
+        self.emit(tuple(f32bits(x) for x in d))
+        self.emit((f32bits(dsteps), 0, 0, 0))
+
+    def _n_rgb_ramp(self, n):  # nodes.cpp RGBRampNode::compile + SVMCompiler::add_node(float4 table)
+        fac = self.inp(n, "Fac")
+        table = n.params["table"]
+        self.emit((NODE_RGB_RAMP, uchar4(fac, self.out(n, "Color"), self.out(n, "Alpha")),
+                   int(n.params["interpolate"]), 0))
+        self.emit((len(table), 0, 0, 0))
+        for row in table:
+            self.emit(tuple(f32bits(float(x)) for x in row))

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import abi, native, sobol
+from . import abi, native, nodes, sobol
 
 # ---------------------------------------------------------------------------
 # constants of the device ABI (kernel_types.h / svm_types.h)
@@ -47,8 +47,10 @@ PRNG_BOUNCE_NUM = 8
 
 NODE_END, NODE_SHADER_JUMP, NODE_CLOSURE_BSDF, NODE_CLOSURE_EMISSION = 0, 1, 2, 3
 NODE_CLOSURE_BACKGROUND, NODE_CLOSURE_SET_WEIGHT = 4, 5
+NODE_CLOSURE_WEIGHT, NODE_EMISSION_WEIGHT = 6, 7
 NODE_MIX_CLOSURE, NODE_JUMP_IF_ZERO, NODE_VALUE_F = 8, 9, 14
 SVM_STACK_INVALID = 255
+SVM_STACK_SIZE = 32  # CY_SVM_STACK (cy_types.h)
 
 CLOSURE_BSDF_DIFFUSE_ID = 2
 CLOSURE_BSDF_REFLECTION_ID = 9
@@ -69,14 +71,18 @@ def f32bits(x: float) -> int:
 
 @dataclass
 class Closure:
-    kind: str  # diffuse | glossy | glass | sharp_glass | refraction | emission | mix
-    color: tuple = (0.8, 0.8, 0.8)
-    roughness: float = 0.0
-    ior: float = 1.45
-    strength: float = 1.0
-    fac: float = 0.5
+    """One closure tree node.  `color`, `roughness`, `ior`, `strength`, `fac`
+    and `normal` take constants or node sockets (nodes.py)."""
+
+    kind: str  # diffuse | glossy | glass | sharp_glass | refraction | emission | background | mix
+    color: object = (0.8, 0.8, 0.8)
+    roughness: object = 0.0
+    ior: object = 1.45
+    strength: object = 1.0
+    fac: object = 0.5
     a: "Closure | None" = None
     b: "Closure | None" = None
+    normal: object = None
 
     def num_closures(self) -> int:
         """ShaderGraph::get_num_closures (render/graph.cpp:1130-1161)."""
@@ -91,25 +97,58 @@ class Closure:
             return self.a.has_emission() or self.b.has_emission()
         return self.kind == "emission"
 
+    def sockets(self) -> list:
+        """Every linked input of the tree (nodes.Socket), with its socket type."""
+        out = []
+        for name, t in (("color", "color"), ("roughness", "float"), ("ior", "float"), ("strength", "float"),
+                        ("fac", "float"), ("normal", "vector")):
+            v = getattr(self, name)
+            if nodes.is_linked(v) and (self.kind == "mix") == (name == "fac"):
+                out.append((v, t))
+        for sub in (self.a, self.b):
+            if sub is not None:
+                out.extend(sub.sockets())
+        return out
 
-def diffuse(color, roughness=0.0):
-    return Closure("diffuse", tuple(color), roughness=roughness)
+    def constant_emission(self):
+        """ShaderManager constant emission (shader.cpp:462-475, nodes.cpp
+        EmissionNode/BackgroundNode::constant_emission): color * strength when
+        neither input is linked."""
+        if self.kind not in ("emission", "background"):
+            return None
+        if nodes.is_linked(self.color) or nodes.is_linked(self.strength):
+            return None
+        return np.array(self.color, dtype=np.float32) * np.float32(self.strength)
 
 
-def glossy(color, roughness):
-    return Closure("glossy", tuple(color), roughness=roughness)
+def diffuse(color, roughness=0.0, normal=None):
+    return Closure("diffuse", _const_or_socket(color), roughness=roughness, normal=normal)
 
 
-def glass(color, roughness, ior=1.45):
-    return Closure("glass" if roughness > 0 else "sharp_glass", tuple(color), roughness=roughness, ior=ior)
+def glossy(color, roughness, normal=None):
+    return Closure("glossy", _const_or_socket(color), roughness=roughness, normal=normal)
+
+
+def glass(color, roughness, ior=1.45, normal=None):
+    sharp = not nodes.is_linked(roughness) and roughness == 0
+    return Closure("sharp_glass" if sharp else "glass", _const_or_socket(color), roughness=roughness, ior=ior,
+                   normal=normal)
 
 
 def emission(color, strength):
-    return Closure("emission", tuple(color), strength=strength)
+    return Closure("emission", _const_or_socket(color), strength=strength)
+
+
+def background(color, strength=1.0):
+    return Closure("background", _const_or_socket(color), strength=strength)
 
 
 def mix(fac, a, b):
     return Closure("mix", fac=fac, a=a, b=b)
+
+
+def _const_or_socket(v):
+    return v if nodes.is_linked(v) else tuple(v)
 
 
 class SVMCompiler:
@@ -119,72 +158,97 @@ class SVMCompiler:
     def __init__(self):
         self.nodes: list[tuple[int, int, int, int]] = []
         self.stack_top = 0
+        self.stack_used = [False] * SVM_STACK_SIZE
+        self.nc: nodes.NodeCompiler | None = None
 
     def alloc(self, n=1) -> int:
-        off = self.stack_top
-        self.stack_top += n
-        if self.stack_top > 32:
-            raise ValueError("SVM stack exceeds the HIP device's 32 slots")
-        return off
+        """First fit over the free slots (svm.cpp stack_find_offset)."""
+        for off in range(SVM_STACK_SIZE - n + 1):
+            if not any(self.stack_used[off:off + n]):
+                self.stack_used[off:off + n] = [True] * n
+                self.stack_top = max(self.stack_top, off + n)
+                return off
+        raise ValueError(f"SVM stack exceeds the HIP device's {SVM_STACK_SIZE} slots")
+
+    def free(self, off: int, n: int = 1):
+        self.stack_used[off:off + n] = [False] * n
 
     @staticmethod
     def uchar4(x, y, z, w) -> int:
         return (x & 0xFF) | ((y & 0xFF) << 8) | ((z & 0xFF) << 16) | ((w & 0xFF) << 24)
 
+    def _float_param(self, v):
+        """(stack offset, inline value) of a BSDF float parameter."""
+        if nodes.is_linked(v):
+            return self.nc.link(v, "float"), 0.0
+        return SVM_STACK_INVALID, float(v)
+
     def emit_closure(self, c: Closure, mix_weight: int) -> list:
         out = []
+        emit = out.append
         if c.kind == "mix":
-            fac_off = self.alloc()
+            if nodes.is_linked(c.fac):
+                fac_off = self.nc.link(c.fac, "float")
+            else:
+                fac_off = self.alloc()
+                emit((NODE_VALUE_F, f32bits(c.fac), fac_off, 0))
             w1, w2 = self.alloc(), self.alloc()
-            out.append((NODE_VALUE_F, f32bits(c.fac), fac_off, 0))
-            out.append((NODE_MIX_CLOSURE, self.uchar4(fac_off, mix_weight, w1, w2), 0, 0))
+            emit((NODE_MIX_CLOSURE, self.uchar4(fac_off, mix_weight, w1, w2), 0, 0))
             for sub, w in ((c.a, w1), (c.b, w2)):
                 code = self.emit_closure(sub, w)
-                out.append((NODE_JUMP_IF_ZERO, len(code), w, 0))
+                emit((NODE_JUMP_IF_ZERO, len(code), w, 0))
                 out.extend(code)
             return out
-        if c.kind == "emission":
-            col = np.array(c.color, dtype=np.float32) * np.float32(c.strength)
-            out.append((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in col)))
-            out.append((NODE_CLOSURE_EMISSION, mix_weight, 0, 0))
+        if c.kind in ("emission", "background"):
+            # nodes.cpp EmissionNode/BackgroundNode::compile
+            const = c.constant_emission()
+            if const is None:
+                emit((NODE_EMISSION_WEIGHT, self.nc.assign(c.color, "color"), self.nc.assign(c.strength, "float"), 0))
+            else:
+                emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in const)))
+            emit((NODE_CLOSURE_EMISSION if c.kind == "emission" else NODE_CLOSURE_BACKGROUND, mix_weight, 0, 0))
             return out
+        sharp_glossy = c.kind == "glossy" and not nodes.is_linked(c.roughness) and c.roughness == 0
         ctype = {
             "diffuse": CLOSURE_BSDF_DIFFUSE_ID,
-            "glossy": CLOSURE_BSDF_MICROFACET_GGX_ID if c.roughness > 0 else CLOSURE_BSDF_REFLECTION_ID,
+            "glossy": CLOSURE_BSDF_REFLECTION_ID if sharp_glossy else CLOSURE_BSDF_MICROFACET_GGX_ID,
             "glass": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID,
             "sharp_glass": CLOSURE_BSDF_SHARP_GLASS_ID,
             "refraction": CLOSURE_BSDF_REFRACTION_ID,
         }[c.kind]
-        out.append((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in c.color)))
-        out.append(
-            (
-                NODE_CLOSURE_BSDF,
-                self.uchar4(ctype, SVM_STACK_INVALID, SVM_STACK_INVALID, mix_weight),
-                f32bits(c.roughness),
-                f32bits(c.ior),
-            )
-        )
-        # data node: normal, tangent, rotation, extra — all default
-        out.append((SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID))
+        # nodes.cpp BsdfNode::compile: linked color -> NODE_CLOSURE_WEIGHT
+        if nodes.is_linked(c.color):
+            emit((NODE_CLOSURE_WEIGHT, self.nc.link(c.color, "color"), 0, 0))
+        else:
+            emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in c.color)))
+        p1, v1 = self._float_param(c.roughness)
+        p2, v2 = self._float_param(c.ior)
+        emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))
+        # data node: normal, tangent, rotation, extra
+        normal_off = self.nc.link(c.normal, "vector") if nodes.is_linked(c.normal) else SVM_STACK_INVALID
+        emit((normal_off, SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID))
         return out
 
     def compile(self, surfaces: list[Closure], world: Closure) -> np.ndarray:
         """Shader i's code starts with the jump node at index i (svm.cpp
-        SVMShaderManager::device_update: shader ids index the jump table)."""
+        SVMShaderManager::device_update: shader ids index the jump table).
+        Node inputs are compiled ahead of the closure tree so both branches of
+        a mix closure see them (svm.cpp generate_multi_closure shared deps)."""
         shaders = list(surfaces) + [world]
         n = len(shaders)
         self.nodes = [(NODE_SHADER_JUMP, 0, 0, 0)] * n
         for i, sh in enumerate(shaders):
             self.stack_top = 0
+            self.stack_used = [False] * SVM_STACK_SIZE
             start = len(self.nodes)
             self.nodes[i] = (NODE_SHADER_JUMP, start, 0, 0)
-            if i == n - 1:  # world background
-                col = np.array(sh.color, dtype=np.float32) * np.float32(sh.strength)
-                self.nodes.append((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in col)))
-                self.nodes.append((4, SVM_STACK_INVALID, 0, 0))  # NODE_CLOSURE_BACKGROUND
-            else:
-                self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
+            socks = sh.sockets()
+            self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [v for v, _ in socks], self.free)
+            for v, t in socks:
+                self.nc.link(v, t)
+            self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
             self.nodes.append((NODE_END, 0, 0, 0))
+        self.nc = None
         return np.array(self.nodes, dtype=np.uint32).reshape(-1, 4)
 
 
@@ -539,17 +603,13 @@ def compile_scene(scene: Scene) -> DeviceScene:
     if scene.lamps:
         lamp_shader = len(mats)
         mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
-    world = Closure("background", tuple(scene.world_color), strength=scene.world_strength)
+    world = background(scene.world_color, scene.world_strength)
     svm = SVMCompiler().compile(mats, world)
     n_shaders = len(mats) + 1
     kshaders = (abi.KernelShader * n_shaders)()
     for i, m in enumerate(mats + [world]):
         flag = SD_USE_MIS
-        const = None
-        if m.kind == "emission":
-            const = np.array(m.color, dtype=np.float32) * f32(m.strength)
-        elif m.kind == "background":
-            const = np.array(m.color, dtype=np.float32) * f32(m.strength)
+        const = m.constant_emission()
         if const is not None:
             flag |= SD_HAS_CONSTANT_EMISSION
             kshaders[i].constant_emission[:] = [float(c) for c in const]
@@ -699,6 +759,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.pass_combined = 0
     kf.pass_alpha_threshold = 0.5
     kf.filter_table_offset = 0
+    # shader.cpp:387 ColorSpaceManager defaults (no OCIO): Rec.709 luminance
+    kf.rgb_to_y.x, kf.rgb_to_y.y, kf.rgb_to_y.z = 0.2126729, 0.7151522, 0.0721750
     # display pass = combined (film.cpp:392, 419-423, 591-598)
     kf.display_pass_stride = 0
     kf.display_pass_components = 4

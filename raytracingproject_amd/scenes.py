@@ -435,3 +435,180 @@ CONFIGS = {
     "bmw27_standin": bmw27_standin,
     "barbershop_standin": barbershop_standin,
 }
+
+
+# ---------------------------------------------------------------------------
+# Shader-node coverage scenes (SVM texture / converter / input nodes)
+
+
+def _node_world():
+    """Direction-dependent world: a sky ramp over the ray direction's height
+    for camera rays, a warm gradient for every other ray (light path node)."""
+    from . import nodes as nd
+
+    D = nd.geometry()["Position"]  # background: P = ray direction
+    up = nd.separate_xyz(D)["Y"]
+    sky = nd.color_ramp(nd.map_range(up, -1.0, 1.0, 0.0, 1.0),
+                        [(0.0, (0.15, 0.12, 0.1, 1.0)), (0.45, (0.6, 0.65, 0.7, 1.0)),
+                         (1.0, (0.25, 0.45, 0.95, 1.0))])["Color"]
+    radial = nd.gradient(D, "radial")["Fac"]
+    warm = nd.mix_rgb("multiply", radial, (1.0, 0.8, 0.5), (0.9, 0.9, 0.9))
+    col = nd.mix_rgb("mix", nd.light_path()["Is Camera Ray"], warm, sky)
+    return col
+
+
+def _grid_scene(colors, width, height, samples, name, glossy_every=0):
+    """One camera-facing quad per entry of `colors` (a color socket or
+    constant), on a square grid in z = 0, lit by the node world only."""
+    n = len(colors)
+    cols = int(math.ceil(math.sqrt(n)))
+    rows = int(math.ceil(n / cols))
+    meshes, materials = [], []
+    for i, c in enumerate(colors):
+        r, q = divmod(i, cols)
+        x0, y0 = q - cols / 2.0, (rows - 1 - r) - rows / 2.0
+        # split the quad along a diagonal: barycentrics differ per half
+        meshes.append(sc.Mesh(*_quad((x0 + 0.9, y0, 0.0), (x0, y0, 0.0), (x0, y0 + 0.9, 0.0),
+                                     (x0 + 0.9, y0 + 0.9, 0.0)), shader=i))
+        if glossy_every and i % glossy_every == glossy_every - 1:
+            materials.append(sc.mix(0.3, sc.diffuse(c), sc.glossy(c, 0.3)))
+        else:
+            materials.append(sc.diffuse(c))
+    # a back plane catching light bounced off the quads
+    meshes.append(sc.Mesh(*_quad((cols, -rows, 1.5), (-cols, -rows, 1.5), (-cols, rows, 1.5), (cols, rows, 1.5)),
+                          shader=n))
+    materials.append(sc.diffuse((0.5, 0.5, 0.5)))
+    ext = max(cols, rows)
+    cam = sc.Camera(eye=(-0.05, 0.0, -2.2 * ext), target=(-0.05, 0.0, 0.0), up=(0.0, 1.0, 0.0),
+                    fov=math.radians(30.0), nearclip=0.01, farclip=1e4)
+    s = sc.Scene(width, height, cam, meshes, materials, samples=samples, name=name)
+    s.world_color = _node_world()
+    s.world_strength = 1.0
+    return s
+
+
+def _uv_inputs(lo_a, hi_a, lo_b, hi_b):
+    """Two float sockets varying across each triangle (barycentric u, v)."""
+    from . import nodes as nd
+
+    uv = nd.separate_xyz(nd.geometry()["Parametric"])
+    return nd.map_range(uv["X"], 0.0, 1.0, lo_a, hi_a), nd.map_range(uv["Y"], 0.0, 1.0, lo_b, hi_b)
+
+
+def shading_math(width=64, height=64, samples=8) -> sc.Scene:
+    """Every restated Math operation (svm_math_util.h svm_math), one quad
+    each: result clamped to [0, 1] in red, the two operands in green / blue."""
+    from . import nodes as nd
+
+    colors = []
+    for op in nd.MATH_OPS_SUPPORTED:
+        a, b = _uv_inputs(-2.5, 2.5, -1.5, 2.5)
+        r = nd.math(op, a, b, 0.3, clamp=True)
+        colors.append(nd.combine_xyz(r, nd.math("multiply", a, 0.2, clamp=True),
+                                     nd.math("multiply", b, 0.2, clamp=True)))
+    return _grid_scene(colors, width, height, samples, "shading_math", glossy_every=5)
+
+
+def shading_vector(width=64, height=64, samples=8) -> sc.Scene:
+    """Vector Math operations, the four Mapping types, separate / combine XYZ."""
+    from . import nodes as nd
+
+    colors = []
+
+    def vecs():
+        a, b = _uv_inputs(-2.0, 2.0, -1.0, 3.0)
+        va = nd.combine_xyz(a, b, 0.7)
+        vb = nd.combine_xyz(nd.math("subtract", 1.3, a), b, nd.math("subtract", a, b))
+        return va, vb
+
+    for op in nd.VECTOR_MATH_OPS:
+        if op == "tangent":
+            continue
+        va, vb = vecs()
+        vc = nd.combine_xyz(2.0, -0.5, 1.25)
+        node = nd.vector_math(op, va, vb, vc, scale=0.35)
+        out = node["Value"] if op in nd.VECTOR_MATH_VALUE_OPS else node["Vector"]
+        colors.append(nd.mix_rgb("mix", 1.0, (0.0, 0.0, 0.0), out, clamp=True))
+    for kind in nd.MAPPING_TYPES:
+        va, _ = vecs()
+        m = nd.mapping(va, location=(0.2, -0.3, 0.1), rotation=(0.4, -1.1, 2.3), scale=(1.5, 0.5, -2.0),
+                       kind=kind)
+        colors.append(nd.mix_rgb("mix", 1.0, (0.0, 0.0, 0.0), m, clamp=True))
+    return _grid_scene(colors, width, height, samples, "shading_vector", glossy_every=4)
+
+
+def shading_color(width=64, height=64, samples=8) -> sc.Scene:
+    """MixRGB blend types, HSV, gamma, bright/contrast, invert, separate and
+    combine HSV, color ramps, clamp and map-range types."""
+    from . import nodes as nd
+
+    colors = []
+    for blend in nd.MIX_TYPES:
+        a, b = _uv_inputs(0.0, 1.0, 0.0, 1.0)
+        c1 = nd.combine_xyz(a, 0.35, b)
+        c2 = nd.combine_hsv(b, 0.8, nd.math("add", a, 0.2))
+        colors.append(nd.mix_rgb(blend, nd.math("multiply", a, 1.2), c1, c2, clamp=(blend == "linear_light")))
+    a, b = _uv_inputs(0.0, 1.0, 0.0, 1.0)
+    base = nd.combine_xyz(a, b, 0.4)
+    colors.append(nd.hsv(base, hue=0.3, saturation=1.4, value_=0.9, fac=0.8))
+    colors.append(nd.gamma(base, 2.2))
+    colors.append(nd.gamma(base, nd.math("add", a, 0.5)))
+    colors.append(nd.bright_contrast(base, 0.1, 0.6))
+    colors.append(nd.invert(base, 0.7))
+    sh = nd.separate_hsv(base)
+    colors.append(nd.combine_hsv(sh["S"], sh["V"], sh["H"]))
+    colors.append(nd.color_ramp(a, [(0.1, (1.0, 0.0, 0.0, 1.0)), (0.5, (0.0, 1.0, 0.2, 0.5)),
+                                    (0.9, (0.1, 0.2, 1.0, 0.0))])["Color"])
+    ramp_c = nd.color_ramp(b, [(0.0, (0.9, 0.9, 0.1, 1.0)), (0.3, (0.1, 0.5, 0.9, 0.25)),
+                               (0.7, (0.8, 0.2, 0.4, 0.75))], interpolation="constant")
+    colors.append(nd.combine_xyz(ramp_c["Alpha"], a, 0.3))
+    for kind in nd.CLAMP_TYPES:
+        v = nd.clamp(nd.math("multiply", a, 1.4), 0.8, nd.math("multiply", b, 0.6), kind=kind)
+        colors.append(nd.combine_xyz(v, 0.2, b))
+    for kind in nd.MAP_RANGE_TYPES:
+        v = nd.map_range(a, 0.8, 0.2, 0.1, 0.9, steps=nd.math("multiply", b, 6.0), kind=kind)
+        colors.append(nd.combine_xyz(v, b, 0.5))
+    # color -> float conversion (film rgb_to_y) and float -> color
+    colors.append(nd.math("power", base, 0.5))
+    return _grid_scene(colors, width, height, samples, "shading_color", glossy_every=6)
+
+
+def shading_coords(width=64, height=64, samples=8) -> sc.Scene:
+    """Texture coordinate and geometry outputs, checker and gradient
+    textures, light path and light falloff outputs."""
+    from . import nodes as nd
+
+    colors = []
+
+    def show(v):
+        return nd.mix_rgb("mix", 1.0, (0.0, 0.0, 0.0), nd.mapping(v, scale=(0.25, 0.25, 0.25),
+                                                                    location=(0.5, 0.5, 0.5)), clamp=True)
+
+    tc = nd.tex_coord()
+    for name in nd.TEXCO_OUTPUTS:
+        colors.append(show(tc[name]))
+    g = nd.geometry()
+    for name in nd.GEOMETRY_OUTPUTS:
+        colors.append(show(g[name]))
+    P = tc["Object"]
+    colors.append(nd.checker(P, (0.9, 0.2, 0.1), (0.1, 0.3, 0.9), 3.0)["Color"])
+    colors.append(nd.checker(nd.mapping(P, rotation=(0.3, 0.2, 0.7)), (0.9, 0.9, 0.9), (0.05, 0.05, 0.05),
+                             nd.math("add", nd.separate_xyz(g["Parametric"])["X"], 2.0))["Color"])
+    for kind in nd.GRADIENT_TYPES:
+        local = nd.vector_math("fraction", nd.mapping(P, scale=(1.1, 1.1, 1.1)))["Vector"]
+        centred = nd.mapping(local, location=(-0.5, -0.5, 0.0), scale=(2.0, 2.0, 2.0))
+        colors.append(nd.gradient(centred, kind)["Color"])
+    lp = nd.light_path()
+    for name in nd.LIGHT_PATH_OUTPUTS:
+        if name in ("Is Shadow Ray", "Is Volume Scatter Ray", "Is Transmission Ray", "Transmission Depth"):
+            continue  # zero on every path of this scene
+        v = lp[name]
+        if name == "Ray Length":
+            v = nd.math("multiply", v, 0.05)
+        elif name.endswith("Depth"):
+            v = nd.math("multiply", v, 0.3)
+        colors.append(nd.combine_xyz(v, 0.3, nd.math("subtract", 1.0, v)))
+    lf = nd.light_falloff(2.0, 0.5)
+    for name in nd.LIGHT_FALLOFF_OUTPUTS:
+        colors.append(nd.combine_xyz(nd.math("multiply", lf[name], 0.01, clamp=True), 0.5, 0.2))
+    return _grid_scene(colors, width, height, samples, "shading_coords", glossy_every=3)

@@ -25,6 +25,10 @@ CASES = {
     # camera models (kernel_camera.h): depth of field, orthographic, panoramas
     **{f"camera_{k}": (lambda k=k: scenes.cornell_camera(k, 48, 48, 8))
        for k in ("dof", "ortho", "equirect", "fisheye_equidistant", "fisheye_equisolid", "mirrorball")},
+    # SVM texture / converter / input nodes (svm_*.h) on a grid of quads under a
+    # direction-dependent world shader (geometry, light path, ramp, gradient)
+    **{f"shading_{k}": (lambda k=k: getattr(scenes, f"shading_{k}")(48, 48, 8))
+       for k in ("math", "vector", "color", "coords")},
 }
 
 
@@ -58,8 +62,10 @@ def _world_case():
 
 # SHADER task (SHADER_EVAL_BACKGROUND) cases: name -> (scene, map width, height, samples)
 BACKGROUND_CASES = {
-    **{name: (fn, 64, 32, 2) for name, fn in CASES.items() if not name.startswith("camera_")},
+    **{name: (fn, 64, 32, 2) for name, fn in CASES.items() if not name.startswith(("camera_", "shading_"))},
     "world_blue": (_world_case, 64, 32, 2),
+    # node-graph world (ramp over direction, radial gradient, light path)
+    "world_nodes": (lambda: scenes.shading_coords(16, 16, 1), 64, 32, 2),
     "world_blue_ragged": (_world_case, 37, 19, 3),
 }
 

@@ -39,7 +39,7 @@ def main(filters):
     extra = [a for a in filters if a.startswith("-D")]
     filters = [a for a in filters if not a.startswith("-D")]
     for src in SRC:
-        ex = extra + (["-DCY_MAX_CLOSURE=2", "-DCY_SHADE_VARIANT=mc2"] if "k_shade" in src else [])
+        ex = extra + (["-DCY_MAX_CLOSURE=2", "-DCY_SHADE_VARIANT=mc2", "-DCY_SVM_TEX=0"] if "k_shade" in src else [])
         asm = compile_asm(src, "/tmp/_isa_stats.s", ex)
         for name, body, meta in kernels(asm):
             dem = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip().split("(")[0]
