@@ -395,3 +395,58 @@ void cyo_film_convert(const int32_t film[6], float exposure, const float *buffer
     }
   }
 }
+
+/* render/light.cpp:530-565 background_cdf: per row, the luminance-times-sine
+ * function and its running sum (each step adds the previous value / res_x),
+ * normalised by the row total which the entry past the end keeps. */
+static void cyo_cdf_row(const float *pixels, int i, int res_x, int res_y, float *cond)
+{
+  const int w = res_x + 1;
+  float *c = cond + 2 * (long)i * w;
+  const float s = sinf(3.14159265358979323846f * ((float)i + 0.5f) / (float)res_y);
+  for (int j = 0; j < res_x; j++) {
+    const float *p = pixels + 4 * ((long)i * res_x + j);
+    float lum = p[0] + p[1];
+    lum = lum + p[2];
+    lum = lum * (1.0f / 3.0f);
+    c[2 * j] = lum * s;
+    if (j == 0) {
+      c[1] = 0.0f;
+    }
+    else {
+      const float step = c[2 * j - 2] / (float)res_x;
+      c[2 * j + 1] = c[2 * j - 1] + step;
+    }
+  }
+  const float last_step = c[2 * res_x - 2] / (float)res_x;
+  const float total = c[2 * res_x - 1] + last_step;
+  const float inv = 1.0f / total;
+  c[2 * res_x] = total;
+  if (total > 0.0f) {
+    for (int j = 1; j < res_x; j++) {
+      c[2 * j + 1] = c[2 * j + 1] * inv;
+    }
+  }
+  c[2 * res_x + 1] = 1.0f;
+}
+
+/* render/light.cpp:676-716 marginal CDF over the row totals */
+void cyo_background_cdf(const float *pixels, int res_x, int res_y, float *marg, float *cond)
+{
+  for (int i = 0; i < res_y; i++) {
+    cyo_cdf_row(pixels, i, res_x, res_y, cond);
+  }
+  const int w = res_x + 1;
+  for (int i = 0; i < res_y; i++) {
+    marg[2 * i] = cond[2 * ((long)i * w + res_x)];
+    marg[2 * i + 1] = (i == 0) ? 0.0f : marg[2 * i - 1] + marg[2 * i - 2] / (float)res_y;
+  }
+  const float total = marg[2 * res_y - 1] + marg[2 * res_y - 2] / (float)res_y;
+  marg[2 * res_y] = total;
+  if (total > 0.0f) {
+    for (int i = 1; i < res_y; i++) {
+      marg[2 * i + 1] = marg[2 * i + 1] / total;
+    }
+  }
+  marg[2 * res_y + 1] = 1.0f;
+}

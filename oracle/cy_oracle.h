@@ -43,4 +43,10 @@ void cyo_intersect_brute_instanced(const float *prim_tri_verts, const uint32_t *
 void cyo_film_convert(const int32_t film[6], float exposure, const float *buffer, void *rgba, float sample_scale,
                       int x, int y, int w, int h, int offset, int stride, int half);
 
+
+/* Background importance map CDFs (render/light.cpp:530-565 background_cdf and
+ * 676-716 marginal CDF): pixels res_y x res_x float4 (rgb used), marg
+ * (res_y + 1) float pairs, cond res_y x (res_x + 1) float pairs. */
+void cyo_background_cdf(const float *pixels, int res_x, int res_y, float *marg, float *cond);
+
 #endif

@@ -106,10 +106,10 @@ def build_device(force=False, variant=None, defines=()):
 
 
 def build_host(force=False):
-    src = os.path.join(HERE, "csrc", "host", "bvh2_build.cpp")
+    srcs = [os.path.join(HERE, "csrc", "host", f) for f in ("bvh2_build.cpp", "light_background.cpp")]
     out = os.path.join(HERE, "libhipcycles_host.so")
-    if force or _stale(out, [src]):
-        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", out, src])
+    if force or _stale(out, srcs):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-o", out, *srcs])
     return out
 
 

@@ -1082,7 +1082,8 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.integrator.use_volumes) why = "volumes";
   else if (d.integrator.transparent_shadows) why = "transparent shadows";
   else if (d.integrator.use_ambient_occlusion) why = "ambient occlusion";
-  else if (d.background.map_weight > 0.0f) why = "background light (world importance sampling)";
+  else if (d.background.portal_weight > 0.0f || d.background.num_portals) why = "light portals";
+  else if (d.background.sun_weight > 0.0f) why = "sky texture sun sampling";
   else if (d.integrator.max_closures > CY_MAX_CLOSURE) why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
   else if (d.bvh.have_motion || d.bvh.have_curves) why = "motion / curves";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
@@ -1091,7 +1092,14 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.film.pass_denoising_data || d.film.pass_adaptive_aux_buffer || d.film.pass_sample_count ||
            d.film.cryptomatte_passes)
     why = "denoising / adaptive / cryptomatte passes";
-  else if (d.background.use_mis) why = "background MIS";
+  else if (d.background.map_weight > 0.0f &&
+           (d.background.map_res_x <= 0 || d.background.map_res_y <= 0 ||
+            dev->globals.find("__light_background_marginal_cdf") == dev->globals.end() ||
+            dev->globals.find("__light_background_conditional_cdf") == dev->globals.end() ||
+            dev->globals["__light_background_marginal_cdf"].bytes < (size_t)(d.background.map_res_y + 1) * 8 ||
+            dev->globals["__light_background_conditional_cdf"].bytes <
+                (size_t)(d.background.map_res_x + 1) * d.background.map_res_y * 8))
+    why = "background map CDFs not bound at the map resolution";
   if (!why.empty()) {
     return set_error(dev, "load_kernels: unsupported scene feature: " + why);
   }

@@ -31,6 +31,8 @@
   X(hc_uint4, __tri_vindex) \
   X(hc_KernelLightDistribution, __light_distribution) \
   X(hc_KernelLight, __lights) \
+  X(hc_float2, __light_background_marginal_cdf) \
+  X(hc_float2, __light_background_conditional_cdf) \
   X(hc_uint4, __svm_nodes) \
   X(hc_KernelShader, __shaders) \
   X(float, __lookup_table) \

@@ -546,7 +546,8 @@ CY_FN cfloat3 shader_background_eval(const CySD *sd)
 
 /* indirect_background's non-constant branch (kernel_emission.h:309-321): the
  * world shader evaluated along the ray with the bounce raised for the
- * light-path node (path_state_modify_bounce). */
+ * light-path node (path_state_modify_bounce); also direct_emissive_eval's
+ * background-light branch (kernel_emission.h:40-51, path flag EMISSION only). */
 CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
                                         const hc_uint4 *svm_nodes,
                                         const hc_KernelShader *shaders,
@@ -554,6 +555,7 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
                                         cfloat3 D,
                                         CyShadeMem mem,
                                         CyPathState state,
+                                        int path_flag,
                                         uint *err)
 {
   CyGlobals kgv;
@@ -565,7 +567,7 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
   CySD esd;
   shader_setup_from_background(kg, &esd, D, mem);
   state.bounce += 1;
-  shader_eval_surface(kg, &esd, &state, state.flag | PATH_RAY_EMISSION, err);
+  shader_eval_surface(kg, &esd, &state, path_flag, err);
   return shader_background_eval(&esd);
 }
 
@@ -701,13 +703,16 @@ CY_FN bool shade_path(const CyGlobals *kg,
            * light-path node (path_state_modify_bounce) */
 #if CY_SVM_TEX
           L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, ray.D,
-                                             mem, state, err);
+                                             mem, state, state.flag | PATH_RAY_EMISSION, err);
 #else
           cy_set_error(err, CY_ERR_FEATURE, 3); /* node world in the kernel without texture nodes */
 #endif
         }
+        /* background MIS weight (kernel_emission.h:325-335) */
         if (!(state.flag & PATH_RAY_MIS_SKIP) && KD->background.use_mis) {
-          cy_set_error(err, CY_ERR_FEATURE, 4); /* background MIS */
+          const float pdf = background_light_pdf(kg, ray.D);
+          const float mis_weight = power_heuristic(state.ray_pdf, pdf);
+          L_background = mul3f(L_background, mis_weight);
         }
       }
       /* path_radiance_accum_background (kernel_accumulate.h:478-520) */
@@ -828,6 +833,14 @@ CY_FN bool shade_path(const CyGlobals *kg,
               ls.Ng = neg3(ls.Ng);
             }
           }
+#if CY_SVM_TEX
+          else if (ls.type == LIGHT_BACKGROUND) {
+            /* direct_emissive_eval (kernel_emission.h:37-86): the world
+             * shader toward the sampled direction */
+            light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, ls.D, mem,
+                                             state, PATH_RAY_EMISSION, err);
+          }
+#endif
           else {
             cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
           }

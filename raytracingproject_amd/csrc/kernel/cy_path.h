@@ -2319,6 +2319,176 @@ CY_FN cfloat3 klight_vec(const float *f)
   return mk3(f[0], f[1], f[2]);
 }
 
+/* ---------------------------------------------------------------------------
+ * Background light: importance sampling of the world through the
+ * equirectangular luminance map built at scene upload
+ * (kernel_light_background.h:24-131 map, 302-447 strategy mix).  Portals and
+ * the sky texture's sun strategy are rejected at load_kernels, so their
+ * weights are zero here; the weights are still normalised as the reference
+ * does. */
+
+/* kernel_projection.h:56-65 direction_to_equirectangular (default range) */
+CY_FN void direction_to_equirectangular(cfloat3 dir, float *u, float *v)
+{
+  if (dir.x == 0.0f && dir.y == 0.0f && dir.z == 0.0f) {
+    *u = 0.0f;
+    *v = 0.0f;
+    return;
+  }
+  *u = (cy_atan2f(dir.y, dir.x) - CY_PI_F) / -CY_2PI_F;
+  *v = (cy_acosf(dir.z / len3(dir)) - CY_PI_F) / -CY_PI_F;
+}
+
+/* kernel_montecarlo.h:112-121 */
+CY_FN cfloat3 sample_uniform_sphere(float u1, float u2)
+{
+  const float z = 1.0f - 2.0f * u1;
+  const float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  const float phi = CY_2PI_F * u2;
+  return mk3(r * cy_cosf(phi), r * cy_sinf(phi), z);
+}
+
+CY_FN hc_float4 mkf4_bg(float x, float y, float z, float w)
+{
+  hc_float4 r;
+  r.x = x;
+  r.y = y;
+  r.z = z;
+  r.w = w;
+  return r;
+}
+
+/* util_math.h:425-428 */
+CY_FN float inverse_lerp(float a, float b, float x)
+{
+  return (x - a) / (b - a);
+}
+
+/* kernel_light_background.h:26-100 */
+CY_FN cfloat3 background_map_sample(const CyGlobals *kg, float randu, float randv, float *pdf)
+{
+  const int res_x = KD->background.map_res_x;
+  const int res_y = KD->background.map_res_y;
+  const int cdf_width = res_x + 1;
+  const hc_float2 *marg = kg->__light_background_marginal_cdf;
+  const hc_float2 *cond = kg->__light_background_conditional_cdf;
+  /* std::lower_bound over the marginal CDF */
+  int first = 0;
+  int count = res_y;
+  while (count > 0) {
+    const int step = count >> 1;
+    const int middle = first + step;
+    if (marg[middle].y < randv) {
+      first = middle + 1;
+      count -= step + 1;
+    }
+    else {
+      count = step;
+    }
+  }
+  const int index_v = (first - 1 > 0) ? first - 1 : 0;
+  const hc_float2 cdf_v = marg[index_v];
+  const hc_float2 cdf_next_v = marg[index_v + 1];
+  const hc_float2 cdf_last_v = marg[res_y];
+  const float dv = inverse_lerp(cdf_v.y, cdf_next_v.y, randv);
+  const float v = ((float)index_v + dv) / (float)res_y;
+
+  first = 0;
+  count = res_x;
+  while (count > 0) {
+    const int step = count >> 1;
+    const int middle = first + step;
+    if (cond[index_v * cdf_width + middle].y < randu) {
+      first = middle + 1;
+      count -= step + 1;
+    }
+    else {
+      count = step;
+    }
+  }
+  const int index_u = (first - 1 > 0) ? first - 1 : 0;
+  const hc_float2 cdf_u = cond[index_v * cdf_width + index_u];
+  const hc_float2 cdf_next_u = cond[index_v * cdf_width + index_u + 1];
+  const hc_float2 cdf_last_u = cond[index_v * cdf_width + res_x];
+  const float du = inverse_lerp(cdf_u.y, cdf_next_u.y, randu);
+  const float u = ((float)index_u + du) / (float)res_x;
+
+  const float sin_theta = cy_sinf(CY_PI_F * v);
+  const float denom = (CY_2PI_F * CY_PI_F * sin_theta) * cdf_last_u.x * cdf_last_v.x;
+  if (sin_theta == 0.0f || denom == 0.0f) {
+    *pdf = 0.0f;
+  }
+  else {
+    *pdf = (cdf_u.x * cdf_v.x) / denom;
+  }
+  return equirectangular_range_to_direction(u, v, mkf4_bg(-CY_2PI_F, CY_PI_F, -CY_PI_F, CY_PI_F));
+}
+
+/* kernel_light_background.h:105-131 */
+CY_FN float background_map_pdf(const CyGlobals *kg, cfloat3 direction)
+{
+  float u, v;
+  direction_to_equirectangular(direction, &u, &v);
+  const int res_x = KD->background.map_res_x;
+  const int res_y = KD->background.map_res_y;
+  const int cdf_width = res_x + 1;
+  const float sin_theta = cy_sinf(v * CY_PI_F);
+  if (sin_theta == 0.0f) {
+    return 0.0f;
+  }
+  int index_u = (int)(u * (float)res_x);
+  index_u = index_u < 0 ? 0 : (index_u > res_x - 1 ? res_x - 1 : index_u);
+  int index_v = (int)(v * (float)res_y);
+  index_v = index_v < 0 ? 0 : (index_v > res_y - 1 ? res_y - 1 : index_v);
+  const hc_float2 cdf_last_u = kg->__light_background_conditional_cdf[index_v * cdf_width + res_x];
+  const hc_float2 cdf_last_v = kg->__light_background_marginal_cdf[res_y];
+  const float denom = (CY_2PI_F * CY_PI_F * sin_theta) * cdf_last_u.x * cdf_last_v.x;
+  if (denom == 0.0f) {
+    return 0.0f;
+  }
+  const hc_float2 cdf_u = kg->__light_background_conditional_cdf[index_v * cdf_width + index_u];
+  const hc_float2 cdf_v = kg->__light_background_marginal_cdf[index_v];
+  return (cdf_u.x * cdf_v.x) / denom;
+}
+
+/* kernel_light_background.h:302-405 with no portals and no sun */
+CY_FN cfloat3 background_light_sample(const CyGlobals *kg, float randu, float randv, float *pdf)
+{
+  float map_method_pdf = KD->background.map_weight;
+  const float pdf_fac = map_method_pdf;
+  if (pdf_fac == 0.0f) {
+    *pdf = 1.0f / (4.0f * CY_PI_F);
+    return sample_uniform_sphere(randu, randv);
+  }
+  map_method_pdf *= 1.0f / pdf_fac;
+  /* sun_method_cdf = portal + sun = 0: the map is sampled */
+  if (map_method_pdf != 1.0f) {
+    randu = (randu - 0.0f) / map_method_pdf;
+  }
+  const cfloat3 D = background_map_sample(kg, randu, randv, pdf);
+  if (map_method_pdf != 1.0f) {
+    *pdf *= map_method_pdf;
+  }
+  return D;
+}
+
+/* kernel_light_background.h:407-445 */
+CY_FN float background_light_pdf(const CyGlobals *kg, cfloat3 direction)
+{
+  float map_method_pdf = KD->background.map_weight;
+  float pdf_fac = map_method_pdf;
+  if (pdf_fac == 0.0f) {
+    return KD->integrator.pdf_lights / (4.0f * CY_PI_F);
+  }
+  pdf_fac = 1.0f / pdf_fac;
+  map_method_pdf *= pdf_fac;
+  float pdf = 0.0f * 0.0f; /* portal_pdf * portal_method_pdf */
+  if (map_method_pdf != 0.0f) {
+    pdf += background_map_pdf(kg, direction) * map_method_pdf;
+  }
+  return pdf * KD->integrator.pdf_lights;
+}
+
 /* kernel_light.h:38-158.  u/v (texture coordinates of the lamp) are only read
  * by non-constant lamp shaders, which the device rejects; they are not set. */
 CY_FN bool lamp_light_sample(const CyGlobals *kg, int lamp, float randu, float randv, cfloat3 P, CyLightSample *ls,
@@ -2352,8 +2522,13 @@ CY_FN bool lamp_light_sample(const CyGlobals *kg, int lamp, float randu, float r
     ls->eval_fac = ls->pdf;
   }
   else if (type == LIGHT_BACKGROUND) {
-    cy_set_error(err, CY_ERR_FEATURE, 8); /* background light (rejected at load) */
-    return false;
+    /* infinite area light (world importance sampling) */
+    const cfloat3 D = neg3(background_light_sample(kg, randu, randv, &ls->pdf));
+    ls->P = D;
+    ls->Ng = D;
+    ls->D = neg3(D);
+    ls->t = CY_FLT_MAX;
+    ls->eval_fac = 1.0f;
   }
   else {
     ls->P = klight_vec(klight->co);

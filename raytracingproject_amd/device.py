@@ -144,7 +144,21 @@ class HIPDevice:
             self.global_alloc(name, arr)
         self.const_copy_to("__data", ds.data)
         self.load_kernels()
+        if ds.info.get("background_map"):
+            self.update_background_map(ds)
         self.scene = ds
+
+    def update_background_map(self, ds: DeviceScene) -> None:
+        """LightManager::device_update_background (light.cpp:568-716): the world
+        shader over the equirectangular map by this device's SHADER task, its
+        CDFs built on the host, both CDF arrays re-bound."""
+        res_x, res_y = ds.info["background_map"]
+        pixels = self.background_eval(res_x, res_y, 1)
+        marg, cond = native.background_cdf(pixels, res_x, res_y)
+        self.global_alloc("__light_background_marginal_cdf", marg)
+        self.global_alloc("__light_background_conditional_cdf", cond)
+        self.background_cdfs = (marg, cond)
+        self.load_kernels()
 
     # ---- RENDER task ------------------------------------------------------
     def render_tile(self, buffer: DeviceBuffer, tile, start_sample: int, num_samples: int,

@@ -43,6 +43,8 @@ def host_lib():
                                         ctypes.c_int, ctypes.c_void_p]
         lib.hcb_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.hcb_free.argtypes = [ctypes.c_void_p]
+        lib.hcb_background_cdf.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]
         _host = lib
     return _host
 
@@ -141,3 +143,18 @@ def hash_uint2(kx: int, ky: int) -> int:
     b ^= a; b = (b - rot(a, 14)) & M
     c ^= b; c = (c - rot(b, 24)) & M
     return c if c < 2**31 else c - 2**32
+
+
+def background_cdf(pixels, res_x: int, res_y: int):
+    """Marginal ((res_y + 1) x 2) and conditional ((res_x + 1) * res_y x 2)
+    float32 CDFs of a (res_y, res_x, 4) background map
+    (csrc/host/light_background.cpp, render/light.cpp:530-716)."""
+    import numpy as np
+
+    px = np.ascontiguousarray(pixels, dtype=np.float32)
+    if px.shape != (res_y, res_x, 4):
+        raise ValueError(f"background map must be ({res_y}, {res_x}, 4), got {px.shape}")
+    marg = np.zeros((res_y + 1, 2), dtype=np.float32)
+    cond = np.zeros(((res_x + 1) * res_y, 2), dtype=np.float32)
+    host_lib().hcb_background_cdf(px.ctypes.data, res_x, res_y, marg.ctypes.data, cond.ctypes.data)
+    return marg, cond

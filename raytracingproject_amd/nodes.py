@@ -304,6 +304,16 @@ def _width(t: str) -> int:
     return 1 if t == "float" else 3
 
 
+# ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
+# the shading point or direction (texture coordinate, geometry, textures)
+SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient")
+
+
+def has_spatial_varying(values) -> bool:
+    """ShaderGraph has_surface_spatial_varying for the sockets feeding a shader."""
+    return any(n.kind in SPATIAL_KINDS for v in values for n in upstream(v))
+
+
 def upstream(v) -> list[Node]:
     """Nodes a value depends on, dependencies first."""
     order: list[Node] = []

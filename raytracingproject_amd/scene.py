@@ -19,6 +19,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import abi, native, nodes, sobol
+from . import nodes as _nodes  # compile_scene has a local "nodes" (BVH nodes)
 
 # ---------------------------------------------------------------------------
 # constants of the device ABI (kernel_types.h / svm_types.h)
@@ -356,6 +357,11 @@ class Scene:
     caustics_reflective: bool = True
     caustics_refractive: bool = True
     name: str = "scene"
+    # world importance sampling (Blender world "Sampling Method"): a background
+    # light is added when the world shader varies over directions
+    # (light.cpp:210-243 test_enabled_lights); map_resolution 0 = automatic
+    world_mis: bool = True
+    world_map_resolution: int = 0
 
 
 @dataclass
@@ -655,7 +661,10 @@ def compile_scene(scene: Scene) -> DeviceScene:
     nd = len(light_list)
     trianglearea = totarea
     lamps = list(scene.lamps)
-    num_lights = len(lamps)
+    # background light (blender_light.cpp:162-210 sync_background_light, appended
+    # after the lamps), enabled only for a spatially varying world
+    bg_light = scene.world_mis and _nodes.has_spatial_varying([v for v, _ in world.sockets()])
+    num_lights = len(lamps) + int(bg_light)
     dist_all = (abi.KernelLightDistribution * (nd + num_lights + 1))()
     for k in range(nd):
         dist_all[k] = dist[k]
@@ -672,6 +681,15 @@ def compile_scene(scene: Scene) -> DeviceScene:
         e.object_id = f32bits_signed(lamp.size)  # lamp.size
         totarea = f32(totarea + lightarea)
         use_lamp_mis |= _pack_lamp(klights[li], lamp, lamp_shader)
+    if bg_light:
+        li = len(lamps)
+        e = dist[nd + li]
+        e.totarea = float(totarea)
+        e.prim = ~li
+        e.shader_flag = f32bits_signed(1.0)  # lamp.pad
+        e.object_id = f32bits_signed(0.0)  # lamp.size of the background light
+        totarea = f32(totarea + lightarea)
+        _pack_background_light(klights[li], n_shaders - 1)
     ntot = nd + num_lights
     dist[ntot].totarea = float(totarea)
     dist[ntot].prim = 0
@@ -748,6 +766,20 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kb.ao_bounces_factor = 0.0
     kb.ao_distance = FLT_MAX
     kb.use_mis = 0
+    kb.portal_weight = 0.0
+    kb.sun_weight = 0.0
+    kb.map_weight = 0.0
+    bg_map = None
+    if bg_light and ki.use_direct_light:
+        # light.cpp:509 map_weight (light->use_mis = sample_as_light) and
+        # device_update_background (light.cpp:568-716): no environment texture or
+        # sky sun -> automatic resolution 4096 x 2048
+        kb.map_weight = 1.0
+        kb.use_mis = 1
+        res_x = scene.world_map_resolution or 4096
+        res_y = res_x // 2 if scene.world_map_resolution else 2048
+        kb.map_res_x, kb.map_res_y = res_x, res_y
+        bg_map = (res_x, res_y)
 
     # --- film (render/film.cpp device_update, combined pass only)
     kf = kd.film
@@ -803,6 +835,12 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "__lookup_table": lookup,
         "__sample_pattern_lut": lut,
     }
+    if bg_map is not None:
+        # filled at upload from the device's SHADER task (device.py upload_scene,
+        # LightManager::device_update_background)
+        arrays["__light_background_marginal_cdf"] = np.zeros((bg_map[1] + 1, 2), dtype=np.float32)
+        arrays["__light_background_conditional_cdf"] = np.zeros(((bg_map[0] + 1) * bg_map[1], 2),
+                                                                dtype=np.float32)
     info = {
         "triangles": ntri,
         "objects": nobj,
@@ -813,6 +851,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "lamps": num_lights,
         "shaders": n_shaders,
         "name": scene.name,
+        "background_map": bg_map,
     }
     return DeviceScene(kd, arrays, scene.width, scene.height, scene.samples, info)
 
@@ -1041,7 +1080,7 @@ def _safe_normalize(v: np.ndarray) -> np.ndarray:
     return (v * (np.float32(1.0) / t)).astype(np.float32) if t != 0 else v
 
 
-LIGHT_TYPES = {"point": 0, "sun": 1, "area": 3, "spot": 4}
+LIGHT_TYPES = {"point": 0, "sun": 1, "background": 2, "area": 3, "spot": 4}
 
 
 def _pack_lamp(kl, lamp: Lamp, shader_index: int) -> bool:
@@ -1116,6 +1155,24 @@ def _pack_lamp(kl, lamp: Lamp, shader_index: int) -> bool:
     return mis
 
 
+def _pack_background_light(kl, shader_index: int):
+    """device_update_points for LIGHT_BACKGROUND (light.cpp:818-839): the world
+    shader with MIS, no area-light flag; the world is visible to every ray
+    type, so no exclusion bits; strength 1, max bounces 1024 (world default)."""
+    shader_id = (shader_index | SHADER_CAST_SHADOW | SHADER_AREA_LIGHT) & ~SHADER_AREA_LIGHT
+    shader_id |= SHADER_USE_MIS
+    kl.type = LIGHT_TYPES["background"]
+    kl.samples = 1
+    kl.strength[:] = [1.0, 1.0, 1.0]
+    kl.uni[:] = [0.0] * 12
+    kl.shader_id = int(np.array([shader_id], dtype=np.uint32).view(np.int32)[0])
+    kl.max_bounces = float(1024)
+    kl.random = 0.0
+    ident = np.eye(4)[:3]
+    abi.set_transform(kl.tfm, ident)
+    abi.set_transform(kl.itfm, ident)
+
+
 def _vertex_normals(v: np.ndarray, t: np.ndarray) -> np.ndarray:
     n = np.zeros_like(v, dtype=np.float64)
     fn = np.cross(v[t[:, 1]] - v[t[:, 0]], v[t[:, 2]] - v[t[:, 0]])
@@ -1135,4 +1192,5 @@ ELEMENT_BYTES = {
     "__light_distribution": ctypes.sizeof(abi.KernelLightDistribution),
     "__lights": ctypes.sizeof(abi.KernelLight), "__svm_nodes": 16,
     "__shaders": ctypes.sizeof(abi.KernelShader), "__lookup_table": 4, "__sample_pattern_lut": 4,
+    "__light_background_marginal_cdf": 8, "__light_background_conditional_cdf": 8,
 }

@@ -484,6 +484,7 @@ def _grid_scene(colors, width, height, samples, name, glossy_every=0):
     s = sc.Scene(width, height, cam, meshes, materials, samples=samples, name=name)
     s.world_color = _node_world()
     s.world_strength = 1.0
+    s.world_map_resolution = 64  # world importance map (the spatially varying world is a light)
     return s
 
 
@@ -612,3 +613,41 @@ def shading_coords(width=64, height=64, samples=8) -> sc.Scene:
     for name in nd.LIGHT_FALLOFF_OUTPUTS:
         colors.append(nd.combine_xyz(nd.math("multiply", lf[name], 0.01, clamp=True), 0.5, 0.2))
     return _grid_scene(colors, width, height, samples, "shading_coords", glossy_every=3)
+
+
+def world_lit(width=64, height=64, samples=8, map_resolution=128, with_lamp=False) -> sc.Scene:
+    """Objects lit mainly by a world shader with a bright direction (a sun-like
+    spot over a sky gradient): the background light (world importance
+    sampling, kernel_light_background.h) carries the direct light, and escaping
+    BSDF rays are MIS-weighted against it."""
+    from . import nodes as nd
+
+    D = nd.geometry()["Position"]
+    sun_dir = (0.45, 0.8, -0.4)
+    n = math.sqrt(sum(c * c for c in sun_dir))
+    sun_dir = tuple(c / n for c in sun_dir)
+    cosang = nd.vector_math("dot_product", D, sun_dir)["Value"]
+    spot = nd.map_range(cosang, 0.97, 1.0, 0.0, 40.0, kind="smoothstep")
+    up = nd.separate_xyz(D)["Y"]
+    sky = nd.mix_rgb("mix", nd.map_range(up, -0.2, 1.0, 0.0, 1.0), (0.25, 0.2, 0.15), (0.3, 0.5, 0.9))
+    world = nd.mix_rgb("add", 1.0, sky, nd.combine_xyz(spot, nd.math("multiply", spot, 0.85),
+                                                       nd.math("multiply", spot, 0.6)))
+    meshes, materials = [], []
+    materials.append(sc.diffuse((0.6, 0.6, 0.6)))
+    meshes.append(sc.Mesh(*_quad((-6, 0, -6), (-6, 0, 6), (6, 0, 6), (6, 0, -6)), shader=0))
+    materials.append(sc.diffuse((0.7, 0.2, 0.15)))
+    meshes.append(sc.Mesh(*_box((-1.6, 0.75, 0.5), (1.5, 1.5, 1.5), 0.4), shader=1))
+    materials.append(sc.glossy((0.9, 0.9, 0.9), 0.25))
+    meshes.append(sc.Mesh(*_ellipsoid((1.2, 0.9, 0.0), (0.9, 0.9, 0.9), 24, 12), shader=2))
+    materials.append(sc.mix(0.4, sc.diffuse((0.1, 0.4, 0.8)), sc.glossy((0.8, 0.8, 0.8), 0.05)))
+    meshes.append(sc.Mesh(*_box((0.0, 0.4, -1.8), (2.5, 0.8, 0.8), -0.2), shader=3))
+    cam = sc.Camera(eye=(0.5, 3.0, -7.5), target=(0.0, 0.6, 0.0), up=(0.0, 1.0, 0.0), fov=math.radians(45.0),
+                    nearclip=0.01, farclip=1e4)
+    lamps = []
+    if with_lamp:
+        lamps.append(sc.Lamp(kind="point", co=(-2.0, 3.0, -2.0), color=(1.0, 0.9, 0.8), strength=30.0, size=0.3))
+    s = sc.Scene(width, height, cam, meshes, materials, samples=samples, name="world_lit", lamps=lamps)
+    s.world_color = world
+    s.world_strength = 1.0
+    s.world_map_resolution = map_resolution
+    return s

@@ -29,6 +29,10 @@ CASES = {
     # direction-dependent world shader (geometry, light path, ramp, gradient)
     **{f"shading_{k}": (lambda k=k: getattr(scenes, f"shading_{k}")(48, 48, 8))
        for k in ("math", "vector", "color", "coords")},
+    # world importance sampling: background light + background MIS
+    # (kernel_light_background.h), alone and sharing the distribution with a lamp
+    "world_mis": lambda: scenes.world_lit(48, 48, 8, map_resolution=128),
+    "world_mis_lamp": lambda: scenes.world_lit(48, 48, 8, map_resolution=64, with_lamp=True),
 }
 
 
@@ -62,7 +66,8 @@ def _world_case():
 
 # SHADER task (SHADER_EVAL_BACKGROUND) cases: name -> (scene, map width, height, samples)
 BACKGROUND_CASES = {
-    **{name: (fn, 64, 32, 2) for name, fn in CASES.items() if not name.startswith(("camera_", "shading_"))},
+    **{name: (fn, 64, 32, 2) for name, fn in CASES.items()
+       if not name.startswith(("camera_", "shading_", "world_mis"))},
     "world_blue": (_world_case, 64, 32, 2),
     # node-graph world (ramp over direction, radial gradient, light path)
     "world_nodes": (lambda: scenes.shading_coords(16, 16, 1), 64, 32, 2),
@@ -79,6 +84,19 @@ PATH_RAY_CLOSEST_VISIBILITY = PATH_RAY_ALL_VISIBILITY & ~PATH_RAY_SHADOW_OPAQUE
 
 def compile_case(name: str) -> sc.DeviceScene:
     return sc.compile_scene(CASES[name]())
+
+
+BG_CDF_NAMES = ("__light_background_marginal_cdf", "__light_background_conditional_cdf")
+
+
+def with_background_golden(ds: sc.DeviceScene, g) -> sc.DeviceScene:
+    """A scene with world importance sampling carries placeholder CDF arrays
+    (filled by the device at upload); for host-side renders take the
+    reference's map CDFs from the golden fixture instead."""
+    if ds.info.get("background_map") and "bg_marg" in g.files:
+        ds.arrays[BG_CDF_NAMES[0]] = g["bg_marg"]
+        ds.arrays[BG_CDF_NAMES[1]] = g["bg_cond"]
+    return ds
 
 
 def scene_digest(ds: sc.DeviceScene) -> str:

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import native_build as nb
-from parity_cases import CASES, PATH_RAY_SHADOW_OPAQUE, compile_case, load_golden
+from parity_cases import CASES, PATH_RAY_SHADOW_OPAQUE, compile_case, load_golden, with_background_golden
 
 RMSE_TOL = 1e-4
 VARIANTS = [(4, 0), (8, 0), (4, 4), (8, 8)]
@@ -31,8 +31,9 @@ def emu():
                 ids=lambda p: f"{p[0]}-w{p[1]}-m{p[2]}")
 def case(request, emu):
     name, width, merge = request.param
-    ds = compile_case(name)
-    return name, ds, load_golden(name), nb.EmuScene(emu, ds, width, merge), merge
+    g = load_golden(name)
+    ds = with_background_golden(compile_case(name), g)
+    return name, ds, g, nb.EmuScene(emu, ds, width, merge), merge
 
 
 def _decode(es):

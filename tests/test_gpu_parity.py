@@ -88,6 +88,20 @@ def test_shadow_any_hit_matches_reference(case, device):
     assert np.array_equal(oi[:, 0], g["shadow_i"][:, 0]), name
 
 
+def test_background_map_matches_reference(case, device):
+    """World importance sampling: the device's SHADER-task map and the host
+    CDFs built from it equal the reference kernel's map and the oracle's CDFs."""
+    name, ds, g = case
+    if not ds.info.get("background_map"):
+        pytest.skip("no background light")
+    res_x, res_y = ds.info["background_map"]
+    m = device.background_eval(res_x, res_y, 1)
+    assert np.array_equal(m.view(np.uint32), g["bg_map"].view(np.uint32))
+    marg, cond = device.background_cdfs
+    assert np.array_equal(marg.view(np.uint32), g["bg_marg"].view(np.uint32))
+    assert np.array_equal(cond.view(np.uint32), g["bg_cond"].view(np.uint32))
+
+
 def test_render_matches_reference(case, device):
     name, ds, g = case
     buf = device.render()

