@@ -73,10 +73,12 @@ def kernel_source_digest():
 SHADE_VARIANTS = (1, 2, 4, 8)  # closure-array sizes of the shade kernel (csrc/device/k_shade.h)
 
 
-def build_device(force=False, variant=None, defines=()):
+def build_device(force=False, variant=None, defines=(), traversal_only=False):
     """The HIP device library: hipcycles.hip plus k_shade.hip compiled once per
     closure-array size.  A named variant (tuning builds with extra -D defines)
-    goes to libhipcycles-<variant>.so next to the default one."""
+    goes to libhipcycles-<variant>.so next to the default one; with
+    traversal_only the variant recompiles hipcycles.hip alone and links the
+    default build's shading objects."""
     dev_dir = os.path.join(HERE, "csrc", "device")
     src = os.path.join(dev_dir, "hipcycles.hip")
     out = os.path.join(HERE, f"libhipcycles-{variant}.so" if variant else "libhipcycles.so")
@@ -93,15 +95,20 @@ def build_device(force=False, variant=None, defines=()):
     cflags = [f for f in HIP_FLAGS if f != "-shared"]
     jobs = [([HIPCC, *cflags, *dflags, inc, "-c", "-o", os.path.join(objdir, "hipcycles.o"), src],
              os.path.join(objdir, "hipcycles.o"))]
+    shade_objs = []
     for mc in SHADE_VARIANTS:
         for tex in (0, 1):
             name = f"mc{mc}_tex" if tex else f"mc{mc}"
+            if traversal_only:
+                shade_objs.append(os.path.join(REPO, "build", "device", "default", f"k_shade_{name}.o"))
+                continue
             obj = os.path.join(objdir, f"k_shade_{name}.o")
             jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
                           f"-DCY_SVM_TEX={tex}", inc, "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
     with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
         list(ex.map(lambda j: _run(j[0]), jobs))
-    _run([HIPCC, "--offload-arch=gfx950", "-fno-gpu-rdc", "-shared", "-fPIC", "-o", out, *[j[1] for j in jobs]])
+    _run([HIPCC, "--offload-arch=gfx950", "-fno-gpu-rdc", "-shared", "-fPIC", "-o", out, *[j[1] for j in jobs],
+          *shade_objs])
     return out
 
 

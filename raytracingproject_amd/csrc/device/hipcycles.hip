@@ -149,15 +149,12 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
     }
     if constexpr (W > 2) {
       if (tie) {
-        /* near-tie (cy_bvhw.h bvhw_traverse): re-trace this ray with the bound
-         * BVH2 in the reference's visiting order, so the hit is the reference's
-         * bit for bit (about 1 ray in 3000 on the bench scene).  The first
-         * CY_LDS_STACKW entries of its stack reuse this thread's own ring column
-         * (the node word of each ring entry): other waves of the workgroup may
-         * still be traversing with theirs. */
-        hit = bvh2_intersect<false, INST, 2, CY_LDS_STACKW, 2 * CY_BLOCK>(
-            &kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr,
-            (CY_LDS int *)(lds_stack.ring + threadIdx.x));
+        /* near-tie (cy_bvhw.h bvhw_traverse): flagged in the stored primitive;
+         * the shading stage re-traces the ray with the bound BVH2 in the
+         * reference's visiting order (cy_integrator.h shade_path), so the hit
+         * is the reference's bit for bit (about 1 ray in 3000 on the bench
+         * scene).  There the re-trace does not weigh on this loop's registers. */
+        isect.prim |= CY_PRIM_TIE;
         if (STATS) {
           n_ties++;
         }

@@ -133,11 +133,17 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
 /* Near-tie window of the exact closest hit: hits within 2^-20 (about 8 ulps)
  * of the best distance are kept as candidates and resolved in the reference's
  * order at the end (bvhw_traverse). */
-#define CY_TIE_EPS (1.0f / 1048576.0f)
 /* 0: no near-tie detection (visiting-order ties resolved as they fall; for
  * measuring its cost only) */
 #ifndef CY_EXACT_TIES
 #  define CY_EXACT_TIES 1
+#endif
+/* tuning switches of the near-tie detection (measurement builds only) */
+#ifndef CY_TIE_BOX_WIDEN
+#  define CY_TIE_BOX_WIDEN 1
+#endif
+#ifndef CY_TIE_EXACT_OK
+#  define CY_TIE_EXACT_OK 1
 #endif
 
 /* Traversal of the wide BVH from node `root` with the ray already in the space
@@ -157,8 +163,8 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
  * distance widened by CY_TIE_EPS (boxes and stack entries culled against the
  * same bound, so no such hit is missed) and *tie is set when two hits, or a hit
  * and the incoming one, fall inside one window.  Only then can the order
- * matter: the caller re-traces that ray with the reference-order BVH2 traversal
- * (hipcycles.hip k_resolve_ties; about 1 ray in 10^4 on the bench scene).  Hits
+ * matter: that ray is re-traced with the reference-order BVH2 traversal
+ * (cy_integrator.h shade_path; about 1 ray in 3000 on the bench scene).  Hits
  * beyond the window lose in either order. */
 template<int W, bool any_hit>
 CY_FN bool bvhw_traverse(const CyGlobals *kg,
@@ -195,6 +201,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   /* culling bound: the best distance widened by the tie window (recomputed
    * where used rather than kept in a register) */
 #define CY_T_CULL ((any_hit || !CY_EXACT_TIES) ? isect->t : isect->t * (1.0f + CY_TIE_EPS))
+#define CY_T_BOX ((any_hit || !CY_EXACT_TIES || !CY_TIE_BOX_WIDEN) ? isect->t : isect->t * (1.0f + CY_TIE_EPS))
 
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
@@ -208,7 +215,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
       const hc_float4 *np = nodes + (size_t)code * (8 * Q);
       float tn[W];
       int cc[W];
-      const float t = CY_T_CULL;
+      const float t = CY_T_BOX;
 #pragma unroll
       for (int q = 0; q < Q; q++) {
         const hc_float4 lx = np[0 * Q + q], hx = np[1 * Q + q];
@@ -296,7 +303,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
            * call or the incoming hit -- makes the result depend on the visiting
            * order: flag the ray; a hit clearly below the current one clears it */
           tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
-          if (exact_ok) {
+          if (exact_ok || !CY_TIE_EXACT_OK) {
             /* the reference's acceptance test at the exact bound */
             isect->prim = prim_addr;
             isect->object = object;
@@ -342,7 +349,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         n_ring--;
         const CyStackEntry e = ring[top * CY_RING_STRIDE];
         code = e.node;
-        if (e.t <= CY_T_CULL) {
+        if (e.t <= CY_T_BOX) {
           found = true;
           break;
         }
@@ -357,6 +364,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   }
 
 #undef CY_T_CULL
+#undef CY_T_BOX
   if (tie_out && tie) {
     *tie_out = true;
   }

@@ -590,11 +590,13 @@ CY_FN bool shade_path(const CyGlobals *kg,
 {
   *shadow = false;
   *finished = false;
-  const hc_float4 is4 = cy_ld(&b->isect[slot]);
+  hc_float4 is4 = cy_ld(&b->isect[slot]);
   CyPathState state;
   CyRay ray;
   cfloat3 throughput, L;
   float L_transparent;
+  uint rng_hash = 0, ray_visibility = 0;
+  int sample = 0;
   if (cam_item != CY_NO_ITEM) {
     /* first bounce of a camera launch: the path starts here (the closest
      * stage traced the same camera ray) */
@@ -603,9 +605,47 @@ CY_FN bool shade_path(const CyGlobals *kg,
       *finished = true;
       return false;
     }
-    uint rng_hash;
-    int sample;
     item_camera_ray(kg, tile, cam_item, &rng_hash, &sample, &ray);
+  }
+  else {
+    const hc_float4 rp = cy_ld(&b->ray_P[slot]);
+    const hc_float4 rd = cy_ld(&b->ray_D[slot]);
+    ray.P = mk3(rp.x, rp.y, rp.z);
+    ray.t = rp.w;
+    ray.D = mk3(rd.x, rd.y, rd.z);
+    ray_visibility = as_uint(rd.w);
+  }
+
+  int hit_object = OBJECT_NONE;
+  if (as_int(is4.w) >= 0 && (as_int(is4.w) & CY_PRIM_TIE)) {
+    /* near-tie of the wide traversal (hipcycles.hip k_intersect_closest):
+     * re-trace with the bound BVH2 in the reference's visiting order, before
+     * the path state is loaded (little is live here).  Only hits inside the
+     * tie window can change the answer, and every box holding one starts
+     * before the window's end, so the re-trace starts with t at twice the
+     * window: the reference order of those candidates, and its t at each of
+     * their tests, are unchanged while everything farther is culled at once. */
+    if (cam_item != CY_NO_ITEM) {
+      CyPathState cs;
+      cs.flag = PATH_RAY_CAMERA | PATH_RAY_MIS_SKIP | PATH_RAY_TRANSPARENT_BACKGROUND; /* path_state_init */
+      ray_visibility = path_state_ray_visibility(&cs);
+    }
+    CyRay rt = ray;
+    rt.t = fminf(ray.t, is4.x * (1.0f + 2.0f * CY_TIE_EPS));
+    CyIsect ti;
+    if (bvh2_intersect<false>(kg, &rt, ray_visibility, &ti, err, nullptr, nullptr, nullptr)) {
+      is4 = mkf4(ti.t, ti.u, ti.v, int_as_float(ti.prim));
+      hit_object = ti.object;
+    }
+    else {
+      is4.w = int_as_float(PRIM_NONE); /* unreachable: the wide traversal's hit lies inside the window */
+    }
+  }
+  else if (kg->have_instancing && as_int(is4.w) >= 0) {
+    hit_object = cy_ld(&b->isect_object[slot]);
+  }
+
+  if (cam_item != CY_NO_ITEM) {
     path_state_init(kg, &state, rng_hash, sample);
     throughput = mk3(1.0f, 1.0f, 1.0f);
     L_transparent = 0.0f;
@@ -613,11 +653,6 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
   else {
     load_state(b, slot, &state, kg);
-    const hc_float4 rp = cy_ld(&b->ray_P[slot]);
-    const hc_float4 rd = cy_ld(&b->ray_D[slot]);
-    ray.P = mk3(rp.x, rp.y, rp.z);
-    ray.t = rp.w;
-    ray.D = mk3(rd.x, rd.y, rd.z);
     const hc_float4 tp4 = cy_ld(&b->throughput[slot]);
     throughput = mk3(tp4.x, tp4.y, tp4.z);
     L_transparent = tp4.w;
@@ -727,7 +762,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     isect.u = is4.y;
     isect.v = is4.z;
     isect.prim = as_int(is4.w);
-    isect.object = kg->have_instancing ? cy_ld(&b->isect_object[slot]) : OBJECT_NONE;
+    isect.object = hit_object;
     isect.type = type;
 
     CySD sd;

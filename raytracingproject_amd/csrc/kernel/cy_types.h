@@ -217,6 +217,11 @@ enum {
 #  define CY_MAX_CLOSURE 8 /* per-kernel closure array (k_shade.hip builds 1, 2, 4, 8) */
 #endif
 #define CY_SVM_STACK 32
+/* Near-tie window of the wide BVH's exact closest hit (cy_bvhw.h), and the
+ * bit k_intersect_closest sets in a stored primitive index whose ray the
+ * shading stage re-traces in the reference's order (cy_integrator.h). */
+#define CY_TIE_EPS (1.0f / 1048576.0f)
+#define CY_PRIM_TIE (1 << 30)
 /* 1: the SVM interpreter includes the texture / converter / input nodes
  * (cy_svm_nodes.h) and non-constant world shaders; the shading kernel is also
  * built with 0 for scenes that use neither (hipcy_load_kernels picks). */
