@@ -204,6 +204,40 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
   }
 }
 
+/* Stage 3 with transparent shadows (KernelIntegrator.transparent_shadows): the
+ * record-all occlusion of the light sample with the occluders' shaders
+ * evaluated (cy_integrator.h shadow_finish_transparent), then the same finish
+ * and refill.  Only scenes with transparent-shadow shaders use it. */
+__global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow_transparent(CyGlobals kg,
+                                                                          CyPathBuffers b,
+                                                                          CyTile tile,
+                                                                          const int *shadow_queue,
+                                                                          const uint *shadow_count,
+                                                                          int *queue_out,
+                                                                          uint *count_out,
+                                                                          uint *err)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool finished = false;
+  int slot = 0;
+  if (i < (int)*shadow_count) {
+    slot = shadow_queue[i];
+    /* shading for transparency keeps no closures (PATH_RAY_SHADOW: none
+     * allocated), only the SVM stack */
+    float svm[CY_SVM_STACK];
+    CyShadeMem mem;
+    mem.closure = nullptr;
+    mem.svm_stack = svm;
+    mem.svm_stride = 1;
+    mem.svm_fast = CY_SVM_STACK;
+    mem.svm_spill = nullptr;
+    finished = shadow_finish_transparent(&kg, &b, &tile, slot, mem, err);
+  }
+  __shared__ uint claim[CY_CLAIM_LDS];
+  const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
+  queue_push(queue_out, count_out, slot, regen, claim);
+}
+
 template<int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
@@ -656,6 +690,7 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   dev->bufs.shadow_P = (hc_float4 *)take(rec);
   dev->bufs.shadow_D = (hc_float4 *)take(rec);
   dev->bufs.shadow_L = (hc_float4 *)take(rec);
+  dev->bufs.shadow_T = (hc_float4 *)take(rec);
   dev->bufs.item = (uint *)take(ints);
   dev->capacity = slots;
   /* queues live in their own allocation (3 x slots ints) */
@@ -1077,7 +1112,11 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.integrator.sampling_pattern != 0) why = "only the Sobol pattern";
   else if (d.integrator.branched) why = "branched path tracing";
   else if (d.integrator.use_volumes) why = "volumes";
-  else if (d.integrator.transparent_shadows) why = "transparent shadows";
+  else if (d.integrator.transparent_shadows && d.integrator.transparent_max_bounce > CY_SHADOW_MAX_HITS)
+    why = "transparent shadows deeper than " + std::to_string(CY_SHADOW_MAX_HITS) + " bounces";
+  else if (d.integrator.transparent_shadows &&
+           (d.integrator.max_bounce > 255 || d.integrator.transparent_max_bounce > 255))
+    why = "transparent shadows with more than 255 bounces";
   else if (d.integrator.use_ambient_occlusion) why = "ambient occlusion";
   else if (d.background.portal_weight > 0.0f || d.background.num_portals) why = "light portals";
   else if (d.background.sun_weight > 0.0f) why = "sky texture sun sampling";
@@ -1261,7 +1300,11 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }
-  {
+  if (dev->data_host.integrator.transparent_shadows) {
+    hipLaunchKernelGGL(k_intersect_shadow_transparent, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs],
+                       ln.cnt + qs, ln.q[qb], ln.cnt + qb, err);
+  }
+  else {
     auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0);
     hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
                        ln.cnt + qb, err, dev->stats_dev);

@@ -38,7 +38,10 @@ typedef struct CyPathBuffers {
   hc_float4 *L;          /* L.emission.xyz, (unused) */
   hc_float4 *shadow_P;   /* shadow ray P.xyz, t */
   hc_float4 *shadow_D;   /* shadow ray D.xyz, (unused) */
-  hc_float4 *shadow_L;   /* pending light contribution xyz, w: 1 = finish path after */
+  hc_float4 *shadow_L;   /* pending light contribution xyz, w: 1 = finish path after; with
+                          * transparent shadows the light's BSDF-weighted eval instead */
+  hc_float4 *shadow_T;   /* transparent shadows: path throughput xyz, w: bounces (8 bits each:
+                          * bounce, transparent, diffuse, glossy); shadow_D.w: transmission bounce */
   uint *item;            /* work item of the path in the slot */
 } CyPathBuffers;
 
@@ -469,6 +472,114 @@ CY_FN bool shadow_finish(const CyPathBuffers *b, const CyTile *tile, int slot, b
     L4.x = L4.x + sl.x;
     L4.y = L4.y + sl.y;
     L4.z = L4.z + sl.z;
+  }
+  if (sl.w != 0.0f) {
+    slot_finish(b, tile, slot, CY_NO_ITEM, mk3(L4.x, L4.y, L4.z), cy_ld(&b->throughput[slot]).w);
+    return true;
+  }
+  cy_st(&b->L[slot], L4);
+  return false;
+}
+
+/* kernel_shadow.h:386-462 shadow_blocked with transparent shadows, record-all
+ * (the CPU kernel's __SHADOW_RECORD_ALL__ branch, kernel_shadow.h:130-230):
+ * the occluders' shaders are evaluated in distance order, each from the ray
+ * moved to the previous one, and their transparency attenuates *shadow.
+ * Returns true when the light is blocked. */
+#ifndef CY_SHADOW_MAX_HITS
+#  define CY_SHADOW_MAX_HITS 64 /* kernel_shadow.h:127 SHADOW_STACK_MAX_HITS */
+#endif
+CY_FN bool shadow_blocked_transparent(
+    const CyGlobals *kg, CyRay ray, const CyPathState *state, CyShadeMem mem, cfloat3 *shadow, uint *err)
+{
+  *shadow = mk3(1.0f, 1.0f, 1.0f);
+  if (ray.t == 0.0f) {
+    return false;
+  }
+  const int transparent_max_bounce = KD->integrator.transparent_max_bounce;
+  if (state->transparent_bounce >= transparent_max_bounce) {
+    return true;
+  }
+  const uint max_hits = (uint)(transparent_max_bounce - state->transparent_bounce - 1);
+  CyIsect hits[CY_SHADOW_MAX_HITS];
+  uint num_hits = 0;
+  const bool blocked = bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+  if (blocked || num_hits == 0) {
+    return blocked;
+  }
+  /* sort_intersections (bvh/bvh.h:606-626): stable, by distance */
+  for (uint i = 1; i < num_hits; i++) {
+    const CyIsect h = hits[i];
+    int j = (int)i - 1;
+    while (j >= 0 && hits[j].t > h.t) {
+      hits[j + 1] = hits[j];
+      j--;
+    }
+    hits[j + 1] = h;
+  }
+  cfloat3 throughput = mk3(1.0f, 1.0f, 1.0f);
+  const cfloat3 Pend = add3(ray.P, mul3f(ray.D, ray.t));
+  float last_t = 0.0f;
+  for (uint k = 0; k < num_hits; k++) {
+    CyIsect isect = hits[k];
+    const float new_t = isect.t;
+    isect.t -= last_t;
+    if (last_t == new_t) {
+      continue;
+    }
+    last_t = new_t;
+    /* shadow_handle_transparent_isect (kernel_shadow.h:49-85) */
+    CySD sd;
+    sd.closure = mem.closure;
+    sd.svm_stack = mem.svm_stack;
+    sd.svm_stride = mem.svm_stride;
+    sd.svm_fast = mem.svm_fast;
+    sd.svm_spill = mem.svm_spill;
+    shader_setup_from_ray(kg, &sd, &isect, &ray);
+    CyPathState st = *state;
+    st.bounce += 1; /* path_state_modify_bounce */
+    shader_eval_surface(kg, &sd, &st, PATH_RAY_SHADOW, err);
+    throughput = mul3(throughput, shader_bsdf_transparency(&sd));
+    if (is_zero3(throughput)) {
+      return true;
+    }
+    ray.P = sd.P;
+    if (ray.t != CY_FLT_MAX) {
+      ray.D = normalize_len3(sub3(Pend, ray.P), &ray.t);
+    }
+  }
+  *shadow = throughput;
+  return is_zero3(throughput);
+}
+
+/* The transparent-shadow counterpart of shadow_finish: occlusion and
+ * attenuation of the pending light sample, then its contribution
+ * (path_radiance_accum_light: throughput * shadow, times the eval, clamped). */
+CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot,
+                                     CyShadeMem mem, uint *err)
+{
+  CyRay ray;
+  shadow_load(b, slot, &ray);
+  const hc_float4 sl = cy_ld(&b->shadow_L[slot]);
+  const hc_float4 st4 = cy_ld(&b->shadow_T[slot]);
+  const uint packed = as_uint(st4.w);
+  CyPathState state;
+  load_state(b, slot, &state, kg);
+  state.bounce = (int)(packed & 0xFF);
+  state.transparent_bounce = (int)((packed >> 8) & 0xFF);
+  state.diffuse_bounce = (int)((packed >> 16) & 0xFF);
+  state.glossy_bounce = (int)(packed >> 24);
+  state.transmission_bounce = as_int(cy_ld(&b->shadow_D[slot]).w);
+  cfloat3 shadow;
+  const bool blocked = shadow_blocked_transparent(kg, ray, &state, mem, &shadow, err);
+  hc_float4 L4 = cy_ld(&b->L[slot]);
+  if (!blocked) {
+    const cfloat3 shaded_throughput = mul3(mul3f(mk3(st4.x, st4.y, st4.z), 1.0f), shadow);
+    cfloat3 contribution = mul3(shaded_throughput, mk3(sl.x, sl.y, sl.z));
+    contribution = path_radiance_clamp(kg, contribution, state.bounce);
+    L4.x = L4.x + contribution.x;
+    L4.y = L4.y + contribution.y;
+    L4.z = L4.z + contribution.z;
   }
   if (sl.w != 0.0f) {
     slot_finish(b, tile, slot, CY_NO_ITEM, mk3(L4.x, L4.y, L4.z), cy_ld(&b->throughput[slot]).w);
@@ -928,8 +1039,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
                   sD = normalize_len3(sub3(ray_offset(ls.P, ls.Ng), sP), &st);
                 }
                 cy_st(&b->shadow_P[slot], mkf4(sP.x, sP.y, sP.z, st));
-                cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
-                cy_st(&b->shadow_L[slot], mkf4(contribution.x, contribution.y, contribution.z, 0.0f));
+                if (KD->integrator.transparent_shadows) {
+                  /* the shadow's attenuation multiplies the throughput before
+                   * the eval (path_radiance_accum_light): keep both, and the
+                   * bounces the occluders' shaders see (kernel_shadow.h:60-75) */
+                  cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, int_as_float(state.transmission_bounce)));
+                  cy_st(&b->shadow_L[slot], mkf4(eval.x, eval.y, eval.z, 0.0f));
+                  const uint packed = (uint)state.bounce | ((uint)state.transparent_bounce << 8) |
+                                      ((uint)state.diffuse_bounce << 16) | ((uint)state.glossy_bounce << 24);
+                  cy_st(&b->shadow_T[slot], mkf4(throughput.x, throughput.y, throughput.z, as_float(packed)));
+                }
+                else {
+                  cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
+                  cy_st(&b->shadow_L[slot], mkf4(contribution.x, contribution.y, contribution.z, 0.0f));
+                }
                 *shadow = (st != 0.0f);
                 if (!*shadow) {
                   L = add3(L, contribution);

@@ -692,6 +692,161 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
   return (isect->prim != PRIM_NONE);
 }
 
+/* Record-all shadow traversal with the bound BVH2 in the reference's order
+ * (bvh/bvh_shadow_all.h:40-258): every primitive hit within the ray is recorded
+ * (hits holds max_hits + 1 entries) until one whose shader has no transparent
+ * shadow, or more than max_hits of them, blocks the light.  Hits inside an
+ * instance get their t scaled to world space at the instance pop. */
+template<bool INST>
+CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
+                           const CyRay *ray,
+                           CyIsect *hits,
+                           uint visibility,
+                           uint max_hits,
+                           uint *num_hits,
+                           uint *err)
+{
+  int stack[BVH_STACK_SIZE];
+  stack[0] = ENTRYPOINT_SENTINEL;
+  int stack_ptr = 0;
+  int node_addr = KD->bvh.root;
+  const float tmax = ray->t;
+  cfloat3 P = ray->P;
+  cfloat3 dir = bvh_clamp_direction(ray->D);
+  cfloat3 idir = rcp3(dir);
+  int object = OBJECT_NONE;
+  float isect_t = tmax;
+  int num_hits_in_instance = 0;
+  *num_hits = 0;
+  const hc_float4 *nodes = kg->__bvh_nodes;
+  do {
+    do {
+      while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
+        const hc_float4 cnodes = nodes[node_addr + 0];
+        const hc_float4 node0 = nodes[node_addr + 1];
+        const hc_float4 node1 = nodes[node_addr + 2];
+        const hc_float4 node2 = nodes[node_addr + 3];
+        const float t = isect_t;
+        float c0lox = (node0.x - P.x) * idir.x;
+        float c0hix = (node0.z - P.x) * idir.x;
+        float c0loy = (node1.x - P.y) * idir.y;
+        float c0hiy = (node1.z - P.y) * idir.y;
+        float c0loz = (node2.x - P.z) * idir.z;
+        float c0hiz = (node2.z - P.z) * idir.z;
+        float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
+        float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
+        float c1lox = (node0.y - P.x) * idir.x;
+        float c1hix = (node0.w - P.x) * idir.x;
+        float c1loy = (node1.y - P.y) * idir.y;
+        float c1hiy = (node1.w - P.y) * idir.y;
+        float c1loz = (node2.y - P.z) * idir.z;
+        float c1hiz = (node2.w - P.z) * idir.z;
+        float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
+        float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
+        const int traverse_mask = (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
+                                  (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
+        node_addr = as_int(cnodes.z);
+        int node_addr_child1 = as_int(cnodes.w);
+        if (traverse_mask == 3) {
+          if (c1min < c0min) {
+            const int tmp = node_addr;
+            node_addr = node_addr_child1;
+            node_addr_child1 = tmp;
+          }
+          if (++stack_ptr >= BVH_STACK_SIZE) {
+            cy_set_error(err, CY_ERR_BVH_STACK, 0);
+            return true;
+          }
+          stack[stack_ptr] = node_addr_child1;
+        }
+        else if (traverse_mask == 2) {
+          node_addr = node_addr_child1;
+        }
+        else if (traverse_mask == 0) {
+          node_addr = stack[stack_ptr];
+          --stack_ptr;
+        }
+      }
+      if (node_addr < 0) {
+        const hc_float4 leaf = kg->__bvh_leaf_nodes[-node_addr - 1];
+        int prim_addr = as_int(leaf.x);
+        if (prim_addr >= 0) {
+          const int prim_addr2 = as_int(leaf.y);
+          const uint type = as_uint(leaf.w);
+          node_addr = stack[stack_ptr];
+          --stack_ptr;
+          if ((type & PRIMITIVE_ALL) != PRIMITIVE_TRIANGLE) {
+            cy_set_error(err, CY_ERR_PRIMITIVE, type);
+            return true;
+          }
+          for (; prim_addr < prim_addr2; prim_addr++) {
+            const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+            const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+            float tt, uu, vv;
+            if (ray_triangle_intersect(P, dir, isect_t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt) &&
+                (kg->__prim_visibility[prim_addr] & visibility)) {
+              CyIsect *h = &hits[*num_hits];
+              h->prim = prim_addr;
+              h->object = object;
+              h->type = PRIMITIVE_TRIANGLE;
+              h->u = uu;
+              h->v = vv;
+              h->t = tt;
+              const int prim = (int)kg->__prim_index[prim_addr];
+              const int shader = (int)kg->__tri_shader[prim];
+              const int flag = kg->__shaders[shader & SHADER_MASK].flags;
+              if (!(flag & SD_HAS_TRANSPARENT_SHADOW)) {
+                return true;
+              }
+              if (*num_hits == max_hits) {
+                return true;
+              }
+              (*num_hits)++;
+              num_hits_in_instance++;
+            }
+          }
+        }
+        else if (!INST) {
+          cy_set_error(err, CY_ERR_FEATURE, 1);
+          return true;
+        }
+        else {
+          /* instance push */
+          object = (int)kg->__prim_object[-prim_addr - 1];
+          isect_t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect_t);
+          num_hits_in_instance = 0;
+          if (++stack_ptr >= BVH_STACK_SIZE) {
+            cy_set_error(err, CY_ERR_BVH_STACK, 0);
+            return true;
+          }
+          stack[stack_ptr] = ENTRYPOINT_SENTINEL;
+          node_addr = (int)kg->__object_node[object];
+        }
+      }
+    } while (node_addr != ENTRYPOINT_SENTINEL);
+    if (INST && stack_ptr >= 0) {
+      /* instance pop: recorded t back to world space (bvh_instance_pop_factor) */
+      if (num_hits_in_instance) {
+        const float t_fac = 1.0f / len3(transform_direction(object_itfm(kg, object), ray->D));
+        for (int i = 0; i < num_hits_in_instance; i++) {
+          hits[*num_hits - 1 - i].t *= t_fac;
+        }
+        P = ray->P;
+        dir = bvh_clamp_direction(ray->D);
+        idir = rcp3(dir);
+      }
+      else {
+        bvh_instance_pop(kg, object, ray, &P, &dir, &idir, CY_FLT_MAX);
+      }
+      isect_t = tmax;
+      object = OBJECT_NONE;
+      node_addr = stack[stack_ptr];
+      --stack_ptr;
+    }
+  } while (node_addr != ENTRYPOINT_SENTINEL);
+  return false;
+}
+
 /* ---------------------------------------------------------------------------
  * Ray offset (bvh/bvh.h:541-586, __INTERSECTION_REFINE__ branch).
  */
@@ -854,6 +1009,49 @@ CY_FN CyClosure *closure_alloc(CySD *sd, int type, cfloat3 weight)
   sd->num_closure++;
   sd->num_closure_left--;
   return sc;
+}
+
+/* closure/bsdf_transparent.h:37-80: transparency accumulates in
+ * closure_transparent_extinction and in one transparent closure (allocated
+ * even on a terminated path, for its transparency). */
+CY_FN void bsdf_transparent_setup(CySD *sd, cfloat3 weight, int path_flag)
+{
+  const float sample_weight = fabsf(average3(weight));
+  if (!(sample_weight >= CLOSURE_WEIGHT_CUTOFF)) {
+    return;
+  }
+  if (sd->flag & SD_TRANSPARENT) {
+    sd->closure_transparent_extinction = add3(sd->closure_transparent_extinction, weight);
+    for (int i = 0; i < sd->num_closure; i++) {
+      CyClosure *sc = &sd->closure[i];
+      if (sc->type == CLOSURE_BSDF_TRANSPARENT_ID) {
+        sc->weight = add3(sc->weight, weight);
+        sc->sample_weight += sample_weight;
+        break;
+      }
+    }
+  }
+  else {
+    sd->flag |= SD_BSDF | SD_TRANSPARENT;
+    sd->closure_transparent_extinction = weight;
+    if (path_flag & PATH_RAY_TERMINATE) {
+      sd->num_closure_left = 1;
+    }
+    CyClosure *bsdf = closure_alloc(sd, CLOSURE_BSDF_TRANSPARENT_ID, weight);
+    if (bsdf) {
+      bsdf->sample_weight = sample_weight;
+      bsdf->N = sd->N;
+    }
+    else if (path_flag & PATH_RAY_TERMINATE) {
+      sd->num_closure_left = 0;
+    }
+  }
+}
+
+/* kernel_shader.h:736-746 shader_bsdf_transparency (no volumes) */
+CY_FN cfloat3 shader_bsdf_transparency(const CySD *sd)
+{
+  return (sd->flag & SD_TRANSPARENT) ? sd->closure_transparent_extinction : mk3(0.0f, 0.0f, 0.0f);
 }
 
 CY_FN CyClosure *bsdf_alloc(CySD *sd, cfloat3 weight)
@@ -1273,6 +1471,13 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
     case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
       label = bsdf_ggx_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
+    case CLOSURE_BSDF_TRANSPARENT_ID:
+      /* bsdf_transparent.h:89-110: straight through */
+      *omega_in = neg3(sd->I);
+      *pdf = 1.0f;
+      *eval = mk3(1.0f, 1.0f, 1.0f);
+      label = LABEL_TRANSMIT | LABEL_TRANSPARENT;
+      break;
     case CLOSURE_NONE_ID:
       label = LABEL_NONE;
       break;
@@ -1527,6 +1732,9 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
       }
       break;
     }
+    case CLOSURE_BSDF_TRANSPARENT_ID:
+      bsdf_transparent_setup(sd, mul3f(sd->svm_closure_weight, mix_weight), path_flag);
+      break;
     default:
       cy_set_error(err, CY_ERR_CLOSURE, type);
       break;

@@ -60,6 +60,8 @@ CLOSURE_BSDF_REFRACTION_ID = 22
 CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID = 24
 CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID = 27
 CLOSURE_BSDF_SHARP_GLASS_ID = 29
+CLOSURE_BSDF_TRANSPARENT_ID = 34
+SD_HAS_TRANSPARENT_SHADOW = 1 << 17
 
 
 def f32bits(x: float) -> int:
@@ -75,7 +77,7 @@ class Closure:
     """One closure tree node.  `color`, `roughness`, `ior`, `strength`, `fac`
     and `normal` take constants or node sockets (nodes.py)."""
 
-    kind: str  # diffuse | glossy | glass | sharp_glass | refraction | emission | background | mix
+    kind: str  # diffuse | glossy | glass | sharp_glass | refraction | transparent | emission | background | mix
     color: object = (0.8, 0.8, 0.8)
     roughness: object = 0.0
     ior: object = 1.45
@@ -97,6 +99,12 @@ class Closure:
         if self.kind == "mix":
             return self.a.has_emission() or self.b.has_emission()
         return self.kind == "emission"
+
+    def has_transparent(self) -> bool:
+        """Shader::has_surface_transparent (svm.cpp:515)."""
+        if self.kind == "mix":
+            return self.a.has_transparent() or self.b.has_transparent()
+        return self.kind == "transparent"
 
     def sockets(self) -> list:
         """Every linked input of the tree (nodes.Socket), with its socket type."""
@@ -134,6 +142,12 @@ def glass(color, roughness, ior=1.45, normal=None):
     sharp = not nodes.is_linked(roughness) and roughness == 0
     return Closure("sharp_glass" if sharp else "glass", _const_or_socket(color), roughness=roughness, ior=ior,
                    normal=normal)
+
+
+def transparent(color=(1.0, 1.0, 1.0)):
+    """Transparent BSDF (nodes.cpp TransparentBsdfNode): light passes straight
+    through, weighted by color; its shadows are transparent too."""
+    return Closure("transparent", _const_or_socket(color))
 
 
 def emission(color, strength):
@@ -216,6 +230,7 @@ class SVMCompiler:
             "glass": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID,
             "sharp_glass": CLOSURE_BSDF_SHARP_GLASS_ID,
             "refraction": CLOSURE_BSDF_REFRACTION_ID,
+            "transparent": CLOSURE_BSDF_TRANSPARENT_ID,
         }[c.kind]
         # nodes.cpp BsdfNode::compile: linked color -> NODE_CLOSURE_WEIGHT
         if nodes.is_linked(c.color):
@@ -613,8 +628,12 @@ def compile_scene(scene: Scene) -> DeviceScene:
     svm = SVMCompiler().compile(mats, world)
     n_shaders = len(mats) + 1
     kshaders = (abi.KernelShader * n_shaders)()
+    any_transparent_shadow = False
     for i, m in enumerate(mats + [world]):
         flag = SD_USE_MIS
+        if m.has_transparent():  # shader.cpp:527 (use_transparent_shadow defaults to true)
+            flag |= SD_HAS_TRANSPARENT_SHADOW
+            any_transparent_shadow = True
         const = m.constant_emission()
         if const is not None:
             flag |= SD_HAS_CONSTANT_EMISSION
@@ -726,7 +745,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
     ki.transparent_min_bounce = 0 + 1
     ki.transparent_max_bounce = scene.transparent_max_bounce + 1
     ki.ao_bounces = INT_MAX
-    ki.transparent_shadows = 0
+    ki.transparent_shadows = int(any_transparent_shadow)  # shader.cpp:603
     ki.volume_max_steps = 1024
     ki.volume_step_rate = 1.0
     ki.caustics_reflective = int(scene.caustics_reflective)

@@ -651,3 +651,29 @@ def world_lit(width=64, height=64, samples=8, map_resolution=128, with_lamp=Fals
     s.world_strength = 1.0
     s.world_map_resolution = map_resolution
     return s
+
+
+def transparent_shadows(width=48, height=48, samples=8) -> sc.Scene:
+    """Transparent BSDFs seen directly and casting tinted shadows: a stack of
+    three tinted transparent panes, a half-transparent leaf whose transparency
+    follows a checker texture (texture nodes evaluated for shadow rays), and a
+    point lamp plus the ceiling light (kernel_shadow.h record-all path)."""
+    from . import nodes as nd
+
+    s = cornell_box(width, height, samples)
+    mats = s.materials
+    base = len(mats)
+    mats.append(sc.transparent((0.9, 0.5, 0.3)))
+    mats.append(sc.mix(0.35, sc.transparent((0.3, 0.8, 0.9)), sc.diffuse((0.2, 0.6, 0.3))))
+    P = nd.tex_coord()["Object"]
+    fac = nd.checker(nd.mapping(P, scale=(0.02, 0.02, 0.02)), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), 1.0)["Fac"]
+    mats.append(sc.mix(fac, sc.diffuse((0.8, 0.8, 0.2)), sc.transparent((0.95, 0.95, 0.95))))
+    for k, z in enumerate((150.0, 200.0, 250.0)):
+        s.meshes.append(sc.Mesh(*_quad((120, 300, z), (320, 300, z), (320, 470, z + 40), (120, 470, z + 40)),
+                                shader=base))
+    s.meshes.append(sc.Mesh(*_quad((300, 400, 120), (480, 400, 120), (480, 400, 420), (300, 400, 420)),
+                            shader=base + 1))
+    s.meshes.append(sc.Mesh(*_quad((80, 20, 80), (250, 20, 80), (250, 250, 160), (80, 250, 160)), shader=base + 2))
+    s.lamps = [sc.Lamp(kind="point", co=(400.0, 500.0, 250.0), color=(1.0, 0.95, 0.9), strength=2.0e5, size=10.0)]
+    s.name = "transparent_shadows"
+    return s

@@ -33,6 +33,8 @@ CASES = {
     # (kernel_light_background.h), alone and sharing the distribution with a lamp
     "world_mis": lambda: scenes.world_lit(48, 48, 8, map_resolution=128),
     "world_mis_lamp": lambda: scenes.world_lit(48, 48, 8, map_resolution=64, with_lamp=True),
+    # transparent BSDF + transparent shadows (kernel_shadow.h record-all, SVM in shadows)
+    "transparent_shadows": lambda: scenes.transparent_shadows(48, 48, 8),
 }
 
 

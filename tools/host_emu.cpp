@@ -257,6 +257,7 @@ extern "C" int emu_render(const void *data,
   b.shadow_P = &rec[6];
   b.shadow_D = &rec[7];
   b.shadow_L = &rec[8];
+  b.shadow_T = &rec[9];
   b.item = &item_slot;
   uint err = 0;
   CyTile tile;
@@ -308,7 +309,11 @@ extern "C" int emu_render(const void *data,
       mem.svm_spill = nullptr;
       bool cont = shade_path(&kg, &b, &tile, 0, cam_item, mem, &shadow, &finished, &err);
       cam_item = CY_NO_ITEM;
-      if (shadow) {
+      if (shadow && kg.data->integrator.transparent_shadows) {
+        /* k_intersect_shadow_transparent */
+        shadow_finish_transparent(&kg, &b, &tile, 0, mem, &err);
+      }
+      else if (shadow) {
         /* k_intersect_shadow */
         CyRay sr;
         shadow_load(&b, 0, &sr);
