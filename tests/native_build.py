@@ -29,9 +29,12 @@ def build(src: str, name: str, defines=()) -> str:
     os.makedirs(OUT, exist_ok=True)
     so = os.path.join(OUT, name)
     if not os.path.exists(so) or any(os.path.getmtime(d) > os.path.getmtime(so) for d in _deps()):
+        # build to a private name and rename: concurrent pytest workers never see a partial file
+        tmp = f"{so}.{os.getpid()}.tmp"
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", *FPFLAGS, *["-D" + d for d in defines],
-               "-I" + os.path.join(ROOT, "include"), "-o", so, os.path.join(ROOT, src), "-lm"]
+               "-I" + os.path.join(ROOT, "include"), "-o", tmp, os.path.join(ROOT, src), "-lm"]
         subprocess.run(cmd, check=True)
+        os.replace(tmp, so)
     return so
 
 
