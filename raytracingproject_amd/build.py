@@ -113,7 +113,7 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False):
 
 
 def build_host(force=False):
-    srcs = [os.path.join(HERE, "csrc", "host", f) for f in ("bvh2_build.cpp", "light_background.cpp")]
+    srcs = [os.path.join(HERE, "csrc", "host", f) for f in ("bvh2_build.cpp", "light_background.cpp", "lookup_tables.cpp")]
     out = os.path.join(HERE, "libhipcycles_host.so")
     if force or _stale(out, srcs):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-o", out, *srcs])

@@ -1019,7 +1019,47 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
         case NODE_END:
           len = 0;
           break;
-        case NODE_CLOSURE_BSDF:
+        case NODE_CLOSURE_BSDF: {
+          len = 2;
+          if (off + 1 >= n) {
+            return "closure node: data node past __svm_nodes";
+          }
+          /* the plain shading kernels carry the basic closure set
+           * (cy_types.h CY_CLOSURE_EXT): isotropic GGX / sharp / glass /
+           * transparent / Lambert diffuse; anything else selects the full one */
+          const uint ctype = node.y & 0xFF;
+          const bool rough_diffuse = ctype == CLOSURE_BSDF_DIFFUSE_ID &&
+                                     (((node.y >> 8) & 0xFF) != SVM_STACK_INVALID || node.z != 0u);
+          const bool tangent = prog[off + 1].y != SVM_STACK_INVALID;
+          tex = rough_diffuse || tangent ||
+                !(ctype == CLOSURE_BSDF_DIFFUSE_ID || ctype == CLOSURE_BSDF_TRANSPARENT_ID ||
+                  ctype == CLOSURE_BSDF_REFLECTION_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_ID ||
+                  ctype == CLOSURE_BSDF_REFRACTION_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID ||
+                  ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID);
+          switch (ctype) {
+            case CLOSURE_BSDF_DIFFUSE_ID:
+            case CLOSURE_BSDF_TRANSLUCENT_ID:
+            case CLOSURE_BSDF_TRANSPARENT_ID:
+            case CLOSURE_BSDF_REFLECTION_ID:
+            case CLOSURE_BSDF_MICROFACET_GGX_ID:
+            case CLOSURE_BSDF_MICROFACET_BECKMANN_ID:
+            case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
+            case CLOSURE_BSDF_REFRACTION_ID:
+            case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+            case CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID:
+            case CLOSURE_BSDF_SHARP_GLASS_ID:
+            case CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID:
+            case CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID:
+            case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
+            case CLOSURE_BSDF_DIFFUSE_TOON_ID:
+            case CLOSURE_BSDF_GLOSSY_TOON_ID:
+              break;
+            default:
+              return "shader " + std::to_string(sh) + ": closure type " + std::to_string(ctype) +
+                     " is not implemented";
+          }
+          break;
+        }
         case NODE_VALUE_V:
           len = 2;
           break;

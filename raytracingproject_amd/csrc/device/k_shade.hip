@@ -4,6 +4,10 @@
  * -DCY_MAX_CLOSURE=N -DCY_SHADE_VARIANT=mcN -DCY_SVM_TEX=0, and as mcN_tex with
  * -DCY_SVM_TEX=1 (raytracingproject_amd/build.py).
  */
+/* the plain variants carry the basic closure set (cy_types.h CY_CLOSURE_EXT) */
+#ifndef CY_CLOSURE_EXT
+#  define CY_CLOSURE_EXT CY_SVM_TEX
+#endif
 #include "cy_device_common.h"
 #include "k_shade.h"
 
@@ -11,12 +15,16 @@
 #  error "CY_SHADE_VARIANT must be defined (mc1, mc2, mc4, mc8)"
 #endif
 /* Closures and the first CY_SVM_LDS stack entries in LDS for closure arrays of
- * up to 4 (LDS per 256-thread block: (11*MAXC + 1 + CY_SVM_LDS) KiB; MAXC 2:
- * 39 KiB = 4 blocks per CU), private memory for 8. */
+ * up to 4 (LDS per 256-thread block: (R*MAXC + 1 + CY_SVM_LDS) KiB of the
+ * CU's 160 KiB with R = 11 dwords per closure (basic set) or 15 (extended);
+ * MAXC 2: basic 39 KiB, extended with 8 stack entries in LDS 39 KiB = 4 blocks
+ * per CU (4 waves/SIMD; one more KiB and the LDS limit drops the occupancy
+ * target, the compiler then spends 179 VGPRs and runs 2 waves), MAXC 4:
+ * 61 / 69 KiB = 2 blocks), private memory for 8. */
 #ifndef CY_SHADE_LDS
 #  define CY_SHADE_LDS (CY_MAX_CLOSURE <= 4)
 #endif
-#define CY_SVM_LDS 16
+#define CY_SVM_LDS (CY_MAX_CLOSURE <= 1 || !CY_CLOSURE_EXT ? 16 : 8)
 #define CY_CLOSURE_DWORDS ((int)(sizeof(CyClosure) / 4) * CY_MAX_CLOSURE + 1)
 
 #define CY_CAT2(a, b) a##b

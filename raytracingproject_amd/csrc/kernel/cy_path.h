@@ -1065,469 +1065,7 @@ CY_FN CyClosure *bsdf_alloc(CySD *sd, cfloat3 weight)
   return (sample_weight >= CLOSURE_WEIGHT_CUTOFF) ? sc : 0;
 }
 
-CY_FN float fresnel_dielectric(
-    float eta, const cfloat3 N, const cfloat3 I, cfloat3 *R, cfloat3 *T, bool *is_inside)
-{
-  float cos = dot3(N, I), neta;
-  cfloat3 Nn;
-  if (cos > 0) {
-    neta = 1 / eta;
-    Nn = N;
-    *is_inside = false;
-  }
-  else {
-    cos = -cos;
-    neta = eta;
-    Nn = neg3(N);
-    *is_inside = true;
-  }
-  *R = sub3(mul3f(Nn, (2 * cos)), I);
-  float arg = 1 - (neta * neta * (1 - (cos * cos)));
-  if (arg < 0) {
-    *T = mk3(0.0f, 0.0f, 0.0f);
-    return 1;
-  }
-  float dnp = cmax(sqrtf(arg), 1e-7f);
-  float nK = (neta * cos) - dnp;
-  *T = add3(neg3(mul3f(I, neta)), mul3f(Nn, nK));
-  float cosTheta1 = cos;
-  float cosTheta2 = -dot3(Nn, *T);
-  float pPara = (cosTheta1 - eta * cosTheta2) / (cosTheta1 + eta * cosTheta2);
-  float pPerp = (eta * cosTheta1 - cosTheta2) / (eta * cosTheta1 + cosTheta2);
-  return 0.5f * (pPara * pPara + pPerp * pPerp);
-}
-
-CY_FN float fresnel_dielectric_cos(float cosi, float eta)
-{
-  float c = fabsf(cosi);
-  float g = eta * eta - 1 + c * c;
-  if (g > 0) {
-    g = sqrtf(g);
-    float A = (g - c) / (g + c);
-    float B = (c * (g + c) - 1) / (c * (g - c) + 1);
-    return 0.5f * A * A * (1 + B * B);
-  }
-  return 1.0f;
-}
-
-/* bsdf_microfacet.h:307-317, 370-380 */
-CY_FN int bsdf_microfacet_ggx_setup(CyClosure *b)
-{
-  b->alpha_x = saturate(b->alpha_x);
-  b->alpha_y = saturate(b->alpha_y);
-  b->type = CLOSURE_BSDF_MICROFACET_GGX_ID;
-  return SD_BSDF | SD_BSDF_HAS_EVAL;
-}
-CY_FN int bsdf_microfacet_ggx_refraction_setup(CyClosure *b)
-{
-  b->alpha_x = saturate(b->alpha_x);
-  b->alpha_y = b->alpha_x;
-  b->type = CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
-  return SD_BSDF | SD_BSDF_HAS_EVAL;
-}
-
-/* cosine hemisphere: kernel_montecarlo.h:39-66 */
-CY_FN void sample_cos_hemisphere(cfloat3 N, float randu, float randv, cfloat3 *omega_in, float *pdf)
-{
-  float phi = CY_2PI_F * randu;
-  float r = sqrtf(randv);
-  randu = r * cy_cosf(phi);
-  randv = r * cy_sinf(phi);
-  float costheta = sqrtf(cmax(1.0f - randu * randu - randv * randv, 0.0f));
-  cfloat3 T, B;
-  make_orthonormals(N, &T, &B);
-  *omega_in = add3(add3(mul3f(T, randu), mul3f(B, randv)), mul3f(N, costheta));
-  *pdf = costheta * CY_1_PI_F;
-}
-
-CY_FN cfloat3 bsdf_diffuse_eval_reflect(const CyClosure *sc, cfloat3 omega_in, float *pdf)
-{
-  float cos_pi = fmaxf(dot3(sc->N, omega_in), 0.0f) * CY_1_PI_F;
-  *pdf = cos_pi;
-  return mk3(cos_pi, cos_pi, cos_pi);
-}
-
-CY_FN int bsdf_diffuse_sample(const CyClosure *sc,
-                              cfloat3 Ng,
-                              float randu,
-                              float randv,
-                              cfloat3 *eval,
-                              cfloat3 *omega_in,
-                              float *pdf)
-{
-  sample_cos_hemisphere(sc->N, randu, randv, omega_in, pdf);
-  if (dot3(Ng, *omega_in) > 0.0f) {
-    *eval = mk3(*pdf, *pdf, *pdf);
-  }
-  else {
-    *pdf = 0.0f;
-  }
-  return LABEL_REFLECT | LABEL_DIFFUSE;
-}
-
-/* bsdf_microfacet.h:390-501 (isotropic GGX, no fresnel/clearcoat variants). */
-CY_FN cfloat3 bsdf_ggx_eval_reflect(const CyClosure *sc, cfloat3 I, cfloat3 omega_in, float *pdf)
-{
-  float alpha_x = sc->alpha_x;
-  float alpha_y = sc->alpha_y;
-  bool m_refractive = sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
-  cfloat3 N = sc->N;
-  if (m_refractive || alpha_x * alpha_y <= 1e-7f) {
-    return mk3(0.0f, 0.0f, 0.0f);
-  }
-  float cosNO = dot3(N, I);
-  float cosNI = dot3(N, omega_in);
-  if (cosNI > 0 && cosNO > 0) {
-    cfloat3 m = normalize3(add3(omega_in, I));
-    float alpha2 = alpha_x * alpha_y;
-    float cosThetaM = dot3(N, m);
-    float cosThetaM2 = cosThetaM * cosThetaM;
-    float cosThetaM4 = cosThetaM2 * cosThetaM2;
-    float tanThetaM2 = (1 - cosThetaM2) / cosThetaM2;
-    float D = alpha2 / (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
-    float G1o = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNO * cosNO) / (cosNO * cosNO)));
-    float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
-    float G = G1o * G1i;
-    float common = D * 0.25f / cosNO;
-    cfloat3 F = mk3(1.0f, 1.0f, 1.0f);
-    cfloat3 out = mul3f(mul3f(F, G), common);
-    *pdf = G1o * common;
-    return out;
-  }
-  return mk3(0.0f, 0.0f, 0.0f);
-}
-
-/* bsdf_microfacet.h:503-559 */
-CY_FN cfloat3 bsdf_ggx_eval_transmit(const CyClosure *sc, cfloat3 I, cfloat3 omega_in, float *pdf)
-{
-  float alpha_x = sc->alpha_x;
-  float alpha_y = sc->alpha_y;
-  float m_eta = sc->ior;
-  bool m_refractive = sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
-  cfloat3 N = sc->N;
-  if (!m_refractive || alpha_x * alpha_y <= 1e-7f) {
-    return mk3(0.0f, 0.0f, 0.0f);
-  }
-  float cosNO = dot3(N, I);
-  float cosNI = dot3(N, omega_in);
-  if (cosNO <= 0 || cosNI >= 0) {
-    return mk3(0.0f, 0.0f, 0.0f);
-  }
-  cfloat3 ht = neg3(add3(mul3f(omega_in, m_eta), I));
-  cfloat3 Ht = normalize3(ht);
-  float cosHO = dot3(Ht, I);
-  float cosHI = dot3(Ht, omega_in);
-  float alpha2 = alpha_x * alpha_y;
-  float cosThetaM = dot3(N, Ht);
-  float cosThetaM2 = cosThetaM * cosThetaM;
-  float tanThetaM2 = (1 - cosThetaM2) / cosThetaM2;
-  float cosThetaM4 = cosThetaM2 * cosThetaM2;
-  float D = alpha2 / (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
-  float G1o = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNO * cosNO) / (cosNO * cosNO)));
-  float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
-  float G = G1o * G1i;
-  float Ht2 = dot3(ht, ht);
-  float common = D * (m_eta * m_eta) / (cosNO * Ht2);
-  float out = G * fabsf(cosHI * cosHO) * common;
-  *pdf = G1o * fabsf(cosHO * cosHI) * common;
-  return mk3(out, out, out);
-}
-
-/* bsdf_microfacet.h:143-253 (GGX visible-normal sampling). */
-CY_FN void microfacet_ggx_sample_slopes(const float cos_theta_i,
-                                        const float sin_theta_i,
-                                        float randu,
-                                        float randv,
-                                        float *slope_x,
-                                        float *slope_y,
-                                        float *G1i)
-{
-  if (cos_theta_i >= 0.99999f) {
-    const float r = sqrtf(randu / (1.0f - randu));
-    const float phi = CY_2PI_F * randv;
-    *slope_x = r * cy_cosf(phi);
-    *slope_y = r * cy_sinf(phi);
-    *G1i = 1.0f;
-    return;
-  }
-  const float tan_theta_i = sin_theta_i / cos_theta_i;
-  const float G1_inv = 0.5f * (1.0f + safe_sqrtf(1.0f + tan_theta_i * tan_theta_i));
-  *G1i = 1.0f / G1_inv;
-  const float A = 2.0f * randu * G1_inv - 1.0f;
-  const float AA = A * A;
-  const float tmp = 1.0f / (AA - 1.0f);
-  const float B = tan_theta_i;
-  const float BB = B * B;
-  const float D = safe_sqrtf(BB * (tmp * tmp) - (AA - BB) * tmp);
-  const float slope_x_1 = B * tmp - D;
-  const float slope_x_2 = B * tmp + D;
-  *slope_x = (A < 0.0f || slope_x_2 * tan_theta_i > 1.0f) ? slope_x_1 : slope_x_2;
-  float S;
-  if (randv > 0.5f) {
-    S = 1.0f;
-    randv = 2.0f * (randv - 0.5f);
-  }
-  else {
-    S = -1.0f;
-    randv = 2.0f * (0.5f - randv);
-  }
-  const float z = (randv * (randv * (randv * 0.27385f - 0.73369f) + 0.46341f)) /
-                  (randv * (randv * (randv * 0.093073f + 0.309420f) - 1.000000f) + 0.597999f);
-  *slope_y = S * z * safe_sqrtf(1.0f + (*slope_x) * (*slope_x));
-}
-
-CY_FN cfloat3 microfacet_sample_stretched(const cfloat3 omega_i,
-                                          const float alpha_x,
-                                          const float alpha_y,
-                                          const float randu,
-                                          const float randv,
-                                          float *G1i)
-{
-  cfloat3 omega_i_ = mk3(alpha_x * omega_i.x, alpha_y * omega_i.y, omega_i.z);
-  omega_i_ = normalize3(omega_i_);
-  float costheta_ = 1.0f;
-  float sintheta_ = 0.0f;
-  float cosphi_ = 1.0f;
-  float sinphi_ = 0.0f;
-  if (omega_i_.z < 0.99999f) {
-    costheta_ = omega_i_.z;
-    sintheta_ = safe_sqrtf(1.0f - costheta_ * costheta_);
-    float invlen = 1.0f / sintheta_;
-    cosphi_ = omega_i_.x * invlen;
-    sinphi_ = omega_i_.y * invlen;
-  }
-  float slope_x, slope_y;
-  microfacet_ggx_sample_slopes(costheta_, sintheta_, randu, randv, &slope_x, &slope_y, G1i);
-  float tmp = cosphi_ * slope_x - sinphi_ * slope_y;
-  slope_y = sinphi_ * slope_x + cosphi_ * slope_y;
-  slope_x = tmp;
-  slope_x = alpha_x * slope_x;
-  slope_y = alpha_y * slope_y;
-  return normalize3(mk3(-slope_x, -slope_y, 1.0f));
-}
-
-/* bsdf_microfacet.h:561-788 (isotropic GGX reflection / refraction). */
-CY_FN int bsdf_ggx_sample(const CyClosure *sc,
-                          cfloat3 Ng,
-                          cfloat3 I,
-                          float randu,
-                          float randv,
-                          cfloat3 *eval,
-                          cfloat3 *omega_in,
-                          float *pdf)
-{
-  float alpha_x = sc->alpha_x;
-  float alpha_y = sc->alpha_y;
-  bool m_refractive = sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID;
-  cfloat3 N = sc->N;
-  int label;
-  float cosNO = dot3(N, I);
-  if (cosNO > 0) {
-    cfloat3 X, Y, Z = N;
-    make_orthonormals(Z, &X, &Y);
-    cfloat3 local_I = mk3(dot3(X, I), dot3(Y, I), cosNO);
-    cfloat3 local_m;
-    float G1o;
-    local_m = microfacet_sample_stretched(local_I, alpha_x, alpha_y, randu, randv, &G1o);
-    cfloat3 m = add3(add3(mul3f(X, local_m.x), mul3f(Y, local_m.y)), mul3f(Z, local_m.z));
-    float cosThetaM = local_m.z;
-    if (!m_refractive) {
-      float cosMO = dot3(m, I);
-      label = LABEL_REFLECT | LABEL_GLOSSY;
-      if (cosMO > 0) {
-        *omega_in = sub3(mul3f(m, 2 * cosMO), I);
-        if (dot3(Ng, *omega_in) > 0) {
-          if (alpha_x * alpha_y <= 1e-7f) {
-            *pdf = 1e6f;
-            *eval = mk3(1e6f, 1e6f, 1e6f);
-            label = LABEL_REFLECT | LABEL_SINGULAR;
-          }
-          else {
-            float alpha2 = alpha_x * alpha_y;
-            float cosThetaM2 = cosThetaM * cosThetaM;
-            float cosThetaM4 = cosThetaM2 * cosThetaM2;
-            float tanThetaM2 = 1 / (cosThetaM2)-1;
-            float cosNI = dot3(N, *omega_in);
-            float D = alpha2 /
-                      (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
-            float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
-            float common = (G1o * D) * 0.25f / cosNO;
-            *pdf = common;
-            cfloat3 F = mk3(1.0f, 1.0f, 1.0f);
-            /* G1i * common * F: scalar * scalar first, then the float3 product. */
-            *eval = mul3f(F, G1i * common);
-          }
-        }
-      }
-    }
-    else {
-      label = LABEL_TRANSMIT | LABEL_GLOSSY;
-      cfloat3 R, T;
-      float m_eta = sc->ior, fresnel;
-      bool inside;
-      fresnel = fresnel_dielectric(m_eta, m, I, &R, &T, &inside);
-      if (!inside && fresnel != 1.0f) {
-        *omega_in = T;
-        if (alpha_x * alpha_y <= 1e-7f || fabsf(m_eta - 1.0f) < 1e-4f) {
-          *pdf = 1e6f;
-          *eval = mk3(1e6f, 1e6f, 1e6f);
-          label = LABEL_TRANSMIT | LABEL_SINGULAR;
-        }
-        else {
-          float alpha2 = alpha_x * alpha_y;
-          float cosThetaM2 = cosThetaM * cosThetaM;
-          float cosThetaM4 = cosThetaM2 * cosThetaM2;
-          float tanThetaM2 = 1 / (cosThetaM2)-1;
-          float D = alpha2 /
-                    (CY_PI_F * cosThetaM4 * (alpha2 + tanThetaM2) * (alpha2 + tanThetaM2));
-          float cosNI = dot3(N, *omega_in);
-          float G1i = 2 / (1 + safe_sqrtf(1 + alpha2 * (1 - cosNI * cosNI) / (cosNI * cosNI)));
-          float cosHI = dot3(m, *omega_in);
-          float cosHO = dot3(m, I);
-          float Ht2 = m_eta * cosHI + cosHO;
-          Ht2 *= Ht2;
-          float common = (G1o * D) * (m_eta * m_eta) / (cosNO * Ht2);
-          float out = G1i * fabsf(cosHI * cosHO) * common;
-          *pdf = cosHO * fabsf(cosHI) * common;
-          *eval = mk3(out, out, out);
-        }
-      }
-    }
-  }
-  else {
-    label = (m_refractive) ? LABEL_TRANSMIT | LABEL_GLOSSY : LABEL_REFLECT | LABEL_GLOSSY;
-  }
-  return label;
-}
-
-/* bsdf_reflection.h:60-95, bsdf_refraction.h:62-111 */
-CY_FN int bsdf_reflection_sample(
-    const CyClosure *sc, cfloat3 Ng, cfloat3 I, cfloat3 *eval, cfloat3 *omega_in, float *pdf)
-{
-  cfloat3 N = sc->N;
-  float cosNO = dot3(N, I);
-  if (cosNO > 0) {
-    *omega_in = sub3(mul3f(N, (2 * cosNO)), I);
-    if (dot3(Ng, *omega_in) > 0) {
-      *pdf = 1e6f;
-      *eval = mk3(1e6f, 1e6f, 1e6f);
-    }
-  }
-  return LABEL_REFLECT | LABEL_SINGULAR;
-}
-
-CY_FN int bsdf_refraction_sample(
-    const CyClosure *sc, cfloat3 I, cfloat3 *eval, cfloat3 *omega_in, float *pdf)
-{
-  float m_eta = sc->ior;
-  cfloat3 R, T;
-  bool inside;
-  float fresnel = fresnel_dielectric(m_eta, sc->N, I, &R, &T, &inside);
-  if (!inside && fresnel != 1.0f) {
-    *pdf = 1e6f;
-    *eval = mk3(1e6f, 1e6f, 1e6f);
-    *omega_in = T;
-  }
-  return LABEL_TRANSMIT | LABEL_SINGULAR;
-}
-
-CY_FN float bsdf_get_specular_roughness_squared(const CyClosure *sc)
-{
-  if (CLOSURE_IS_BSDF_SINGULAR(sc->type)) {
-    return 0.0f;
-  }
-  if (CLOSURE_IS_BSDF_MICROFACET(sc->type)) {
-    return sc->alpha_x * sc->alpha_y;
-  }
-  return 1.0f;
-}
-
-/* bsdf.h:113-489 dispatch (subset).  Shadow-terminator offset and bump
- * shadowing apply only when object.shadow_terminator_offset > 1 or N != sd->N,
- * both rejected at load / not produced by this node subset. */
-CY_FN int bsdf_sample(const CyGlobals *kg,
-                      const CySD *sd,
-                      const CyClosure *sc,
-                      float randu,
-                      float randv,
-                      cfloat3 *eval,
-                      cfloat3 *omega_in,
-                      float *pdf,
-                      uint *err)
-{
-  int label;
-  const cfloat3 Ng = sd->Ng;
-  switch (sc->type) {
-    case CLOSURE_BSDF_DIFFUSE_ID:
-      label = bsdf_diffuse_sample(sc, Ng, randu, randv, eval, omega_in, pdf);
-      break;
-    case CLOSURE_BSDF_REFLECTION_ID:
-      label = bsdf_reflection_sample(sc, Ng, sd->I, eval, omega_in, pdf);
-      break;
-    case CLOSURE_BSDF_REFRACTION_ID:
-      label = bsdf_refraction_sample(sc, sd->I, eval, omega_in, pdf);
-      break;
-    case CLOSURE_BSDF_MICROFACET_GGX_ID:
-    case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
-      label = bsdf_ggx_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
-      break;
-    case CLOSURE_BSDF_TRANSPARENT_ID:
-      /* bsdf_transparent.h:89-110: straight through */
-      *omega_in = neg3(sd->I);
-      *pdf = 1.0f;
-      *eval = mk3(1.0f, 1.0f, 1.0f);
-      label = LABEL_TRANSMIT | LABEL_TRANSPARENT;
-      break;
-    case CLOSURE_NONE_ID:
-      label = LABEL_NONE;
-      break;
-    default:
-      cy_set_error(err, CY_ERR_CLOSURE, (uint)sc->type);
-      label = LABEL_NONE;
-      break;
-  }
-  if (label & LABEL_TRANSMIT) {
-    float threshold_squared = KD->background.transparent_roughness_squared_threshold;
-    if (threshold_squared >= 0.0f) {
-      if (bsdf_get_specular_roughness_squared(sc) <= threshold_squared) {
-        label |= LABEL_TRANSMIT_TRANSPARENT;
-      }
-    }
-  }
-  return label;
-}
-
-/* bsdf.h:495-700 (subset). */
-CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, float *pdf)
-{
-  cfloat3 eval;
-  if (dot3(sd->Ng, omega_in) >= 0.0f) {
-    switch (sc->type) {
-      case CLOSURE_BSDF_DIFFUSE_ID:
-        eval = bsdf_diffuse_eval_reflect(sc, omega_in, pdf);
-        break;
-      case CLOSURE_BSDF_MICROFACET_GGX_ID:
-      case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
-        eval = bsdf_ggx_eval_reflect(sc, sd->I, omega_in, pdf);
-        break;
-      default: /* reflection/refraction are singular: zero; NONE: zero */
-        eval = mk3(0.0f, 0.0f, 0.0f);
-        break;
-    }
-  }
-  else {
-    switch (sc->type) {
-      case CLOSURE_BSDF_MICROFACET_GGX_ID:
-      case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
-        eval = bsdf_ggx_eval_transmit(sc, sd->I, omega_in, pdf);
-        break;
-      default:
-        eval = mk3(0.0f, 0.0f, 0.0f);
-        break;
-    }
-  }
-  return eval;
-}
+#include "cy_closures.h"
 
 /* ---------------------------------------------------------------------------
  * SVM interpreter subset (svm/svm.h:220-549, svm_closure.h, svm_value.h,
@@ -1576,37 +1114,41 @@ CY_FN void svm_store3(CySvmStack stack, uint a, cfloat3 f, uint *err)
 
 #include "cy_svm_nodes.h"
 
+/* svm_closure.h:21-56 */
 CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, float roughness, bool refract)
 {
   if (type == CLOSURE_BSDF_SHARP_GLASS_ID) {
+    b->alpha_y = 0.0f;
+    b->alpha_x = 0.0f;
     if (refract) {
-      b->alpha_y = 0.0f;
-      b->alpha_x = 0.0f;
       b->ior = eta;
       b->type = CLOSURE_BSDF_REFRACTION_ID;
-      sd->flag |= SD_BSDF;
     }
     else {
-      b->alpha_y = 0.0f;
-      b->alpha_x = 0.0f;
       b->ior = 0.0f;
       b->type = CLOSURE_BSDF_REFLECTION_ID;
-      sd->flag |= SD_BSDF;
     }
+    sd->flag |= SD_BSDF;
   }
+#if CY_CLOSURE_EXT
+  else if (type == CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID) {
+    b->alpha_x = roughness;
+    b->alpha_y = roughness;
+    b->ior = eta;
+    sd->flag |= refract ? bsdf_microfacet_beckmann_refraction_setup(b) : bsdf_microfacet_beckmann_setup(b);
+  }
+#endif
   else {
     b->alpha_x = roughness;
     b->alpha_y = roughness;
     b->ior = eta;
-    if (refract) {
-      sd->flag |= bsdf_microfacet_ggx_refraction_setup(b);
-    }
-    else {
-      sd->flag |= bsdf_microfacet_ggx_setup(b);
-    }
+    sd->flag |= refract ? bsdf_microfacet_ggx_refraction_setup(b) : bsdf_microfacet_ggx_setup(b);
   }
 }
 
+/* svm_closure.h:58-735 svm_node_closure_bsdf (every BSDF the SVM compiler
+ * emits except Principled, multiscatter GGX and hair; those set
+ * CY_ERR_CLOSURE). */
 CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
                                  CySD *sd,
                                  CySvmStack stack,
@@ -1638,17 +1180,40 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
         b->N = N;
         float roughness = param1;
         if (roughness == 0.0f) {
-          b->type = CLOSURE_BSDF_DIFFUSE_ID;
-          sd->flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
+          sd->flag |= bsdf_diffuse_setup(b);
         }
         else {
+#if CY_CLOSURE_EXT
+          b->alpha_x = roughness;
+          sd->flag |= bsdf_oren_nayar_setup(b);
+#else
           cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_OREN_NAYAR_ID);
+#endif
         }
       }
       break;
     }
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_TRANSLUCENT_ID: {
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (b) {
+        b->N = N;
+        sd->flag |= bsdf_translucent_setup(b);
+      }
+      break;
+    }
+#endif
+    case CLOSURE_BSDF_TRANSPARENT_ID:
+      bsdf_transparent_setup(sd, mul3f(sd->svm_closure_weight, mix_weight), path_flag);
+      break;
     case CLOSURE_BSDF_REFLECTION_ID:
-    case CLOSURE_BSDF_MICROFACET_GGX_ID: {
+    case CLOSURE_BSDF_MICROFACET_GGX_ID:
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_MICROFACET_BECKMANN_ID:
+    case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
+#endif
+    {
       if (!KD->integrator.caustics_reflective && (path_flag & PATH_RAY_DIFFUSE)) {
         break;
       }
@@ -1661,23 +1226,55 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
       b->N = N;
       b->ior = 0.0f;
       if (data_node.y == SVM_STACK_INVALID) {
+#if CY_CLOSURE_EXT
+        b->T = mk3(0.0f, 0.0f, 0.0f);
+#endif
         b->alpha_x = roughness;
         b->alpha_y = roughness;
       }
       else {
-        cy_set_error(err, CY_ERR_CLOSURE, 1000 + type); /* anisotropic tangent */
+#if !CY_CLOSURE_EXT
+        cy_set_error(err, CY_ERR_CLOSURE, 1000 + type); /* anisotropic: extended closure set */
+#else
+        b->T = svm_load3(stack, data_node.y, err);
+        float rotation = svm_load(stack, data_node.z, err);
+        if (rotation != 0.0f) {
+          b->T = rotate_around_axis(b->T, b->N, rotation * CY_2PI_F);
+        }
+        float anisotropy = cclamp(param2, -0.99f, 0.99f);
+        if (anisotropy < 0.0f) {
+          b->alpha_x = roughness / (1.0f + anisotropy);
+          b->alpha_y = roughness * (1.0f + anisotropy);
+        }
+        else {
+          b->alpha_x = roughness * (1.0f - anisotropy);
+          b->alpha_y = roughness / (1.0f - anisotropy);
+        }
+#endif
       }
       if (type == CLOSURE_BSDF_REFLECTION_ID) {
         b->type = CLOSURE_BSDF_REFLECTION_ID;
         sd->flag |= SD_BSDF;
       }
+#if CY_CLOSURE_EXT
+      else if (type == CLOSURE_BSDF_MICROFACET_BECKMANN_ID) {
+        sd->flag |= bsdf_microfacet_beckmann_setup(b);
+      }
+      else if (type == CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID) {
+        sd->flag |= bsdf_ashikhmin_shirley_setup(b);
+      }
+#endif
       else {
         sd->flag |= bsdf_microfacet_ggx_setup(b);
       }
       break;
     }
     case CLOSURE_BSDF_REFRACTION_ID:
-    case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID: {
+    case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID:
+#endif
+    {
       if (!KD->integrator.caustics_refractive && (path_flag & PATH_RAY_DIFFUSE)) {
         break;
       }
@@ -1685,6 +1282,9 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
       CyClosure *b = bsdf_alloc(sd, weight);
       if (b) {
         b->N = N;
+#if CY_CLOSURE_EXT
+        b->T = mk3(0.0f, 0.0f, 0.0f);
+#endif
         float eta = fmaxf(param2, 1e-5f);
         eta = (sd->flag & SD_BACKFACING) ? 1.0f / eta : eta;
         if (type == CLOSURE_BSDF_REFRACTION_ID) {
@@ -1699,13 +1299,25 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
           b->alpha_x = roughness;
           b->alpha_y = roughness;
           b->ior = eta;
-          sd->flag |= bsdf_microfacet_ggx_refraction_setup(b);
+#if CY_CLOSURE_EXT
+          if (type == CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID) {
+            sd->flag |= bsdf_microfacet_beckmann_refraction_setup(b);
+          }
+          else
+#endif
+          {
+            sd->flag |= bsdf_microfacet_ggx_refraction_setup(b);
+          }
         }
       }
       break;
     }
     case CLOSURE_BSDF_SHARP_GLASS_ID:
-    case CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID: {
+    case CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID:
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID:
+#endif
+    {
       if (!KD->integrator.caustics_reflective && !KD->integrator.caustics_refractive &&
           (path_flag & PATH_RAY_DIFFUSE)) {
         break;
@@ -1720,6 +1332,9 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
         CyClosure *b = bsdf_alloc(sd, mul3f(weight, fresnel));
         if (b) {
           b->N = N;
+#if CY_CLOSURE_EXT
+          b->T = mk3(0.0f, 0.0f, 0.0f);
+#endif
           svm_node_glass_setup(sd, b, (int)type, eta, roughness, false);
         }
       }
@@ -1727,14 +1342,42 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
         CyClosure *b = bsdf_alloc(sd, mul3f(weight, (1.0f - fresnel)));
         if (b) {
           b->N = N;
+#if CY_CLOSURE_EXT
+          b->T = mk3(0.0f, 0.0f, 0.0f);
+#endif
           svm_node_glass_setup(sd, b, (int)type, eta, roughness, true);
         }
       }
       break;
     }
-    case CLOSURE_BSDF_TRANSPARENT_ID:
-      bsdf_transparent_setup(sd, mul3f(sd->svm_closure_weight, mix_weight), path_flag);
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID: {
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (b) {
+        b->N = N;
+        b->alpha_x = saturate(param1);
+        sd->flag |= bsdf_ashikhmin_velvet_setup(b);
+      }
       break;
+    }
+    case CLOSURE_BSDF_GLOSSY_TOON_ID:
+      if (!KD->integrator.caustics_reflective && (path_flag & PATH_RAY_DIFFUSE)) {
+        break;
+      }
+      /* fall through */
+    case CLOSURE_BSDF_DIFFUSE_TOON_ID: {
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (b) {
+        b->N = N;
+        b->alpha_x = param1;
+        b->alpha_y = param2;
+        sd->flag |= bsdf_toon_setup(b, (int)type);
+      }
+      break;
+    }
+#endif
     default:
       cy_set_error(err, CY_ERR_CLOSURE, type);
       break;

@@ -66,10 +66,7 @@ CY_FN float cy_clampf(float a, float mn, float mx)
 {
   return cy_min(cy_max(a, mn), mx);
 }
-CY_FN float safe_divide(float a, float b)
-{
-  return (b != 0.0f) ? a / b : 0.0f;
-}
+/* safe_divide: cy_closures.h */
 CY_FN float safe_modulo(float a, float b)
 {
   return (b != 0.0f) ? fmodf(a, b) : 0.0f;

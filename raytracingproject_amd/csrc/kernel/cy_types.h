@@ -140,13 +140,19 @@ enum {
   CLOSURE_BSDF_ID = 1,
   CLOSURE_BSDF_DIFFUSE_ID = 2,
   CLOSURE_BSDF_OREN_NAYAR_ID = 3,
+  CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID = 5,
+  CLOSURE_BSDF_PRINCIPLED_SHEEN_ID = 6,
+  CLOSURE_BSDF_DIFFUSE_TOON_ID = 7,
   CLOSURE_BSDF_TRANSLUCENT_ID = 8,
   CLOSURE_BSDF_REFLECTION_ID = 9,
   CLOSURE_BSDF_MICROFACET_GGX_ID = 10,
   CLOSURE_BSDF_MICROFACET_GGX_FRESNEL_ID = 11,
   CLOSURE_BSDF_MICROFACET_GGX_CLEARCOAT_ID = 12,
   CLOSURE_BSDF_MICROFACET_BECKMANN_ID = 13,
+  CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID = 14,
   CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID = 16,
+  CLOSURE_BSDF_ASHIKHMIN_VELVET_ID = 17,
+  CLOSURE_BSDF_GLOSSY_TOON_ID = 20,
   CLOSURE_BSDF_HAIR_REFLECTION_ID = 21,
   CLOSURE_BSDF_REFRACTION_ID = 22,
   CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID = 23,
@@ -162,6 +168,7 @@ enum {
   CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID = 33,
   CLOSURE_BSDF_TRANSPARENT_ID = 34,
   CLOSURE_HOLDOUT_ID = 41,
+  CLOSURE_BSDF_PRINCIPLED_ID = 45,
   NBUILTIN_CLOSURES = 46
 };
 
@@ -260,12 +267,26 @@ typedef struct CyIsect {
   int type;
 } CyIsect;
 
+/* One closure record.  CY_CLOSURE_EXT selects the closure set compiled in:
+ * 1 (default) every closure of cy_closures.h, 15 dwords per record; 0 the
+ * basic set the bench scene uses (diffuse, isotropic GGX, sharp reflection /
+ * refraction / glass, transparent), 11 dwords, built into the shade kernels
+ * without texture nodes (k_shade.hip) so their LDS and register budget stay
+ * what they were before the extended closures existed.  Per-type use of the
+ * parameter slots is listed at the top of cy_closures.h. */
+#ifndef CY_CLOSURE_EXT
+#  define CY_CLOSURE_EXT 1
+#endif
 typedef struct CyClosure {
   cfloat3 weight;
   int type;
   float sample_weight;
   cfloat3 N;
   float alpha_x, alpha_y, ior;
+#if CY_CLOSURE_EXT
+  cfloat3 T;  /* tangent of anisotropic microfacets */
+  int extra;  /* MicrofacetExtra slot in the closure array, -1 for none */
+#endif
 } CyClosure;
 
 typedef struct CySD {

@@ -45,6 +45,8 @@ def host_lib():
         lib.hcb_free.argtypes = [ctypes.c_void_p]
         lib.hcb_background_cdf.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p]
+        lib.cyh_beckmann_table.argtypes = [ctypes.c_void_p]
+        lib.cyh_beckmann_table_size.restype = ctypes.c_int
         _host = lib
     return _host
 

@@ -54,13 +54,33 @@ SVM_STACK_INVALID = 255
 SVM_STACK_SIZE = 32  # CY_SVM_STACK (cy_types.h)
 
 CLOSURE_BSDF_DIFFUSE_ID = 2
+CLOSURE_BSDF_DIFFUSE_TOON_ID = 7
+CLOSURE_BSDF_TRANSLUCENT_ID = 8
 CLOSURE_BSDF_REFLECTION_ID = 9
 CLOSURE_BSDF_MICROFACET_GGX_ID = 10
+CLOSURE_BSDF_MICROFACET_BECKMANN_ID = 13
+CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID = 16
+CLOSURE_BSDF_ASHIKHMIN_VELVET_ID = 17
+CLOSURE_BSDF_GLOSSY_TOON_ID = 20
 CLOSURE_BSDF_REFRACTION_ID = 22
+CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID = 23
 CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID = 24
+CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID = 26
 CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID = 27
 CLOSURE_BSDF_SHARP_GLASS_ID = 29
 CLOSURE_BSDF_TRANSPARENT_ID = 34
+
+# Distribution enums of the glossy / anisotropic / glass / refraction nodes
+# (nodes.cpp GlossyBsdfNode, GlassBsdfNode, RefractionBsdfNode NODE_DEFINE)
+GLOSSY_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFLECTION_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_ID,
+                        "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_ID,
+                        "ashikhmin_shirley": CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID}
+GLASS_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_SHARP_GLASS_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID,
+                       "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID}
+REFRACTION_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFRACTION_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID,
+                            "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID}
+BECKMANN_CLOSURES = (CLOSURE_BSDF_MICROFACET_BECKMANN_ID, CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID,
+                     CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)
 SD_HAS_TRANSPARENT_SHADOW = 1 << 17
 
 
@@ -77,23 +97,53 @@ class Closure:
     """One closure tree node.  `color`, `roughness`, `ior`, `strength`, `fac`
     and `normal` take constants or node sockets (nodes.py)."""
 
-    kind: str  # diffuse | glossy | glass | sharp_glass | refraction | transparent | emission | background | mix
+    # diffuse | translucent | glossy | anisotropic | glass | refraction | velvet |
+    # diffuse_toon | glossy_toon | transparent | emission | background | mix
+    kind: str
     color: object = (0.8, 0.8, 0.8)
-    roughness: object = 0.0
-    ior: object = 1.45
+    roughness: object = 0.0  # roughness; velvet: sigma; toon: size
+    ior: object = 1.45  # glass / refraction: IOR; toon: smooth
     strength: object = 1.0
     fac: object = 0.5
     a: "Closure | None" = None
     b: "Closure | None" = None
     normal: object = None
+    distribution: str = "ggx"  # glossy / anisotropic / glass / refraction
+    anisotropy: object = 0.0
+    rotation: object = 0.0
+    tangent: object = None
+
+    def closure_type(self) -> int:
+        """The ClosureType the node compiles to, after simplify_settings
+        (nodes.cpp:2373-2581: an unlinked roughness <= 1e-4 selects the sharp
+        distribution when filter_glossy is 0)."""
+        sharp = not nodes.is_linked(self.roughness) and self.roughness <= 1e-4
+        if self.kind == "glossy":
+            return GLOSSY_DISTRIBUTIONS["sharp" if sharp else self.distribution]
+        if self.kind == "anisotropic":
+            return GLOSSY_DISTRIBUTIONS[self.distribution]
+        if self.kind == "glass":
+            return GLASS_DISTRIBUTIONS["sharp" if sharp else self.distribution]
+        if self.kind == "refraction":
+            return REFRACTION_DISTRIBUTIONS["sharp" if sharp else self.distribution]
+        return {"diffuse": CLOSURE_BSDF_DIFFUSE_ID, "translucent": CLOSURE_BSDF_TRANSLUCENT_ID,
+                "velvet": CLOSURE_BSDF_ASHIKHMIN_VELVET_ID, "diffuse_toon": CLOSURE_BSDF_DIFFUSE_TOON_ID,
+                "glossy_toon": CLOSURE_BSDF_GLOSSY_TOON_ID, "transparent": CLOSURE_BSDF_TRANSPARENT_ID}[self.kind]
 
     def num_closures(self) -> int:
         """ShaderGraph::get_num_closures (render/graph.cpp:1130-1161)."""
         if self.kind == "mix":
             return self.a.num_closures() + self.b.num_closures()
-        if self.kind in ("glass", "sharp_glass"):
+        if self.kind == "glass":
             return 2
         return 1
+
+    def closure_types(self) -> set:
+        if self.kind == "mix":
+            return self.a.closure_types() | self.b.closure_types()
+        if self.kind in ("emission", "background"):
+            return set()
+        return {self.closure_type()}
 
     def has_emission(self) -> bool:
         if self.kind == "mix":
@@ -110,7 +160,8 @@ class Closure:
         """Every linked input of the tree (nodes.Socket), with its socket type."""
         out = []
         for name, t in (("color", "color"), ("roughness", "float"), ("ior", "float"), ("strength", "float"),
-                        ("fac", "float"), ("normal", "vector")):
+                        ("fac", "float"), ("normal", "vector"), ("anisotropy", "float"), ("rotation", "float"),
+                        ("tangent", "vector")):
             v = getattr(self, name)
             if nodes.is_linked(v) and (self.kind == "mix") == (name == "fac"):
                 out.append((v, t))
@@ -134,14 +185,44 @@ def diffuse(color, roughness=0.0, normal=None):
     return Closure("diffuse", _const_or_socket(color), roughness=roughness, normal=normal)
 
 
-def glossy(color, roughness, normal=None):
-    return Closure("glossy", _const_or_socket(color), roughness=roughness, normal=normal)
+def glossy(color, roughness, normal=None, distribution="ggx"):
+    """Glossy BSDF: distribution ggx | beckmann | ashikhmin_shirley | sharp."""
+    return Closure("glossy", _const_or_socket(color), roughness=roughness, normal=normal, distribution=distribution)
 
 
-def glass(color, roughness, ior=1.45, normal=None):
-    sharp = not nodes.is_linked(roughness) and roughness == 0
-    return Closure("sharp_glass" if sharp else "glass", _const_or_socket(color), roughness=roughness, ior=ior,
-                   normal=normal)
+def anisotropic(color, roughness, anisotropy, rotation, tangent, normal=None, distribution="ggx"):
+    """Anisotropic BSDF (nodes.cpp AnisotropicBsdfNode).  The tangent must be
+    a linked vector socket: the reference's default link (a generated-
+    coordinate TangentNode) needs mesh attributes this host does not emit."""
+    if not nodes.is_linked(tangent):
+        raise ValueError("anisotropic BSDF: link the tangent input to a vector socket")
+    return Closure("anisotropic", _const_or_socket(color), roughness=roughness, anisotropy=anisotropy,
+                   rotation=rotation, tangent=tangent, normal=normal, distribution=distribution)
+
+
+def glass(color, roughness, ior=1.45, normal=None, distribution="ggx"):
+    """Glass BSDF: distribution ggx | beckmann | sharp."""
+    return Closure("glass", _const_or_socket(color), roughness=roughness, ior=ior, normal=normal,
+                   distribution=distribution)
+
+
+def refraction(color, roughness, ior=1.45, normal=None, distribution="ggx"):
+    """Refraction BSDF: distribution ggx | beckmann | sharp."""
+    return Closure("refraction", _const_or_socket(color), roughness=roughness, ior=ior, normal=normal,
+                   distribution=distribution)
+
+
+def translucent(color, normal=None):
+    return Closure("translucent", _const_or_socket(color), normal=normal)
+
+
+def velvet(color, sigma=1.0, normal=None):
+    return Closure("velvet", _const_or_socket(color), roughness=sigma, normal=normal)
+
+
+def toon(color, size=0.5, smooth=0.0, glossy=False, normal=None):
+    return Closure("glossy_toon" if glossy else "diffuse_toon", _const_or_socket(color), roughness=size,
+                   ior=smooth, normal=normal)
 
 
 def transparent(color=(1.0, 1.0, 1.0)):
@@ -223,26 +304,33 @@ class SVMCompiler:
                 emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in const)))
             emit((NODE_CLOSURE_EMISSION if c.kind == "emission" else NODE_CLOSURE_BACKGROUND, mix_weight, 0, 0))
             return out
-        sharp_glossy = c.kind == "glossy" and not nodes.is_linked(c.roughness) and c.roughness == 0
-        ctype = {
-            "diffuse": CLOSURE_BSDF_DIFFUSE_ID,
-            "glossy": CLOSURE_BSDF_REFLECTION_ID if sharp_glossy else CLOSURE_BSDF_MICROFACET_GGX_ID,
-            "glass": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID,
-            "sharp_glass": CLOSURE_BSDF_SHARP_GLASS_ID,
-            "refraction": CLOSURE_BSDF_REFRACTION_ID,
-            "transparent": CLOSURE_BSDF_TRANSPARENT_ID,
-        }[c.kind]
+        ctype = c.closure_type()
         # nodes.cpp BsdfNode::compile: linked color -> NODE_CLOSURE_WEIGHT
         if nodes.is_linked(c.color):
             emit((NODE_CLOSURE_WEIGHT, self.nc.link(c.color, "color"), 0, 0))
         else:
             emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in c.color)))
-        p1, v1 = self._float_param(c.roughness)
-        p2, v2 = self._float_param(c.ior)
-        emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))
-        # data node: normal, tangent, rotation, extra
         normal_off = self.nc.link(c.normal, "vector") if nodes.is_linked(c.normal) else SVM_STACK_INVALID
-        emit((normal_off, SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID))
+        tangent_off, param3_off = SVM_STACK_INVALID, SVM_STACK_INVALID
+        # per node: (param1, param2) of BsdfNode::compile (nodes.cpp:2200-2800)
+        if c.kind in ("diffuse", "velvet"):
+            params = (c.roughness, None)
+        elif c.kind in ("translucent", "transparent") or ctype in (CLOSURE_BSDF_REFLECTION_ID,):
+            params = (None, None)
+        elif c.kind == "anisotropic":
+            params = (c.roughness, c.anisotropy)
+            tangent_off = self.nc.link(c.tangent, "vector")
+            # param3 (rotation) is always stack-assigned (BsdfNode::compile)
+            param3_off = self.nc.assign(c.rotation, "float")
+        elif c.kind == "glossy":
+            params = (c.roughness, None)
+        else:  # glass, refraction (roughness, IOR); toons (size, smooth)
+            params = (c.roughness, c.ior)
+        p1, v1 = self._float_param(params[0]) if params[0] is not None else (SVM_STACK_INVALID, 0.0)
+        p2, v2 = self._float_param(params[1]) if params[1] is not None else (SVM_STACK_INVALID, 0.0)
+        emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))
+        # data node: normal, tangent, param3, param4
+        emit((normal_off, tangent_off, param3_off, SVM_STACK_INVALID))
         return out
 
     def compile(self, surfaces: list[Closure], world: Closure) -> np.ndarray:
@@ -819,6 +907,20 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.use_display_exposure = 1 if kf.exposure != 1.0 else 0
     kf.use_display_pass_alpha = 1
     lookup = filter_table(scene.filter_type, scene.filter_width)
+    kd.tables.beckmann_offset = 0
+    if any(t in BECKMANN_CLOSURES for m in mats for t in m.closure_types()):
+        # ShaderManager::device_update_common adds the Beckmann sampling table
+        # (render/shader.cpp:52-135) through LookupTables::add_table, which
+        # places tables at TABLE_CHUNK_SIZE (256) aligned offsets
+        # (render/tables.cpp:67-103).  Only scenes that sample Beckmann
+        # closures carry it here.
+        lib = native.host_lib()
+        n = lib.cyh_beckmann_table_size()
+        table = np.zeros(n * n, dtype=np.float32)
+        lib.cyh_beckmann_table(table.ctypes.data)
+        offset = -(-len(lookup) // 256) * 256
+        lookup = np.concatenate([lookup, np.zeros(offset - len(lookup), dtype=np.float32), table])
+        kd.tables.beckmann_offset = offset
 
     # --- camera
     compile_camera(kd.cam, scene.camera, scene.width, scene.height)
@@ -830,7 +932,6 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kd.bvh.bvh_layout = BVH_LAYOUT_BVH2
     kd.bvh.use_bvh_steps = 0
     kd.bvh.curve_subdivisions = 4
-    kd.tables.beckmann_offset = 0
 
     arrays = {
         "__bvh_nodes": nodes.astype(np.float32),

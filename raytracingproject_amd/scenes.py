@@ -677,3 +677,63 @@ def transparent_shadows(width=48, height=48, samples=8) -> sc.Scene:
     s.lamps = [sc.Lamp(kind="point", co=(400.0, 500.0, 250.0), color=(1.0, 0.95, 0.9), strength=2.0e5, size=10.0)]
     s.name = "transparent_shadows"
     return s
+
+
+def _closure_gallery(width, height, samples, name, materials, with_lamp=True):
+    """A Cornell box with a 3 x 2 grid of spheres, one per material, lit by
+    the ceiling light, a sphere point lamp and an area lamp behind the
+    spheres (transmission through translucent / refractive surfaces)."""
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    s.materials.extend(materials)
+    centers = [(120.0, 330.0, 200.0), (278.0, 330.0, 200.0), (436.0, 330.0, 200.0),
+               (120.0, 140.0, 200.0), (278.0, 140.0, 200.0), (436.0, 140.0, 200.0)]
+    for i in range(len(materials)):
+        c = centers[i % len(centers)]
+        s.meshes.append(sc.Mesh(*_ellipsoid(c, (70.0, 70.0, 70.0), 20, 12), shader=base + i))
+    if with_lamp:
+        s.lamps = [
+            sc.Lamp("point", co=(140.0, 480.0, 40.0), size=20.0, color=(1.0, 0.8, 0.6), strength=3.0e6),
+            sc.Lamp("area", co=(278.0, 240.0, 420.0), direction=(0.0, 0.0, -1.0), axisu=(1.0, 0.0, 0.0),
+                    axisv=(0.0, 1.0, 0.0), size=1.0, sizeu=300.0, sizev=200.0, color=(0.7, 0.9, 1.0),
+                    strength=2.0e5),
+        ]
+    s.name = name
+    return s
+
+
+def closures_diffuse(width=48, height=48, samples=8) -> sc.Scene:
+    """Diffuse-family closures (closure/bsdf_oren_nayar.h, bsdf_diffuse.h
+    translucent, bsdf_ashikhmin_velvet.h, bsdf_toon.h), each mixed or bare."""
+    mats = [
+        sc.diffuse((0.8, 0.5, 0.3), roughness=0.6),  # Oren-Nayar
+        sc.mix(0.5, sc.translucent((0.3, 0.8, 0.4)), sc.diffuse((0.7, 0.7, 0.7), roughness=1.0)),
+        sc.velvet((0.9, 0.3, 0.5), sigma=0.4),
+        sc.toon((0.4, 0.6, 0.9), size=0.45, smooth=0.1),
+        sc.toon((0.9, 0.9, 0.6), size=0.2, smooth=0.05, glossy=True),
+        sc.mix(0.4, sc.toon((0.2, 0.8, 0.8), size=0.7, smooth=0.0), sc.velvet((0.8, 0.8, 0.2), sigma=1.0)),
+    ]
+    return _closure_gallery(width, height, samples, "closures_diffuse", mats)
+
+
+def closures_microfacet(width=48, height=48, samples=8) -> sc.Scene:
+    """Microfacet closures (closure/bsdf_microfacet.h, bsdf_ashikhmin_shirley.h):
+    Beckmann reflection / refraction / glass (table-sampled slopes), isotropic
+    Ashikhmin-Shirley, anisotropic GGX and Beckmann with a tangent and a
+    rotation from nodes, GGX refraction."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    tangent = nd.vector_math("cross_product", g["Normal"], (0.0, 1.0, 0.0))["Vector"]
+    rot = nd.math("multiply", nd.separate_xyz(g["Parametric"])["X"], 0.25)
+    mats = [
+        sc.mix(0.3, sc.diffuse((0.6, 0.2, 0.2)), sc.glossy((0.9, 0.8, 0.7), 0.35, distribution="beckmann")),
+        sc.glass((0.95, 0.95, 1.0), 0.2, ior=1.5, distribution="beckmann"),
+        sc.mix(0.5, sc.refraction((0.9, 1.0, 0.9), 0.3, ior=1.33, distribution="beckmann"),
+               sc.refraction((1.0, 0.9, 0.9), 0.25, ior=1.45, distribution="ggx")),
+        sc.mix(0.5, sc.glossy((0.8, 0.8, 0.9), 0.4, distribution="ashikhmin_shirley"),
+               sc.diffuse((0.2, 0.3, 0.6))),
+        sc.anisotropic((0.9, 0.7, 0.4), 0.4, 0.7, rot, tangent, distribution="ggx"),
+        sc.anisotropic((0.7, 0.8, 0.9), 0.3, -0.5, 0.1, tangent, distribution="beckmann"),
+    ]
+    return _closure_gallery(width, height, samples, "closures_microfacet", mats)

@@ -35,6 +35,9 @@ CASES = {
     "world_mis_lamp": lambda: scenes.world_lit(48, 48, 8, map_resolution=64, with_lamp=True),
     # transparent BSDF + transparent shadows (kernel_shadow.h record-all, SVM in shadows)
     "transparent_shadows": lambda: scenes.transparent_shadows(48, 48, 8),
+    # BSDF closure breadth (closure/bsdf_*.h): diffuse family, microfacets
+    "closures_diffuse": lambda: scenes.closures_diffuse(48, 48, 8),
+    "closures_microfacet": lambda: scenes.closures_microfacet(48, 48, 8),
 }
 
 
