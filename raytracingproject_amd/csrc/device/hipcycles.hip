@@ -1036,7 +1036,18 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
                   ctype == CLOSURE_BSDF_REFLECTION_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_ID ||
                   ctype == CLOSURE_BSDF_REFRACTION_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID ||
                   ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID);
+          if (ctype == CLOSURE_BSDF_PRINCIPLED_ID) {
+            len = 6; /* data node + 4 nodes of principled parameters */
+            if (off + 5 >= n) {
+              return "principled BSDF: parameter nodes past __svm_nodes";
+            }
+            if (prog[off + 2].y != CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID) {
+              return "shader " + std::to_string(sh) +
+                     ": principled BSDF: only the GGX distribution is implemented (multiscatter GGX is not)";
+            }
+          }
           switch (ctype) {
+            case CLOSURE_BSDF_PRINCIPLED_ID:
             case CLOSURE_BSDF_DIFFUSE_ID:
             case CLOSURE_BSDF_TRANSLUCENT_ID:
             case CLOSURE_BSDF_TRANSPARENT_ID:

@@ -7,6 +7,7 @@
  *   diffuse / glossy toon          closure/bsdf_toon.h
  *   Ashikhmin velvet               closure/bsdf_ashikhmin_velvet.h
  *   Ashikhmin-Shirley (isotropic)  closure/bsdf_ashikhmin_shirley.h
+ *   principled diffuse / sheen     closure/bsdf_principled_diffuse.h, _sheen.h
  *   sharp reflection / refraction  closure/bsdf_reflection.h, bsdf_refraction.h
  *   transparent (sample)           closure/bsdf_transparent.h
  *   GGX + Beckmann microfacets     closure/bsdf_microfacet.h: reflection and
@@ -28,6 +29,7 @@
  *   Oren-Nayar     alpha_x = roughness, alpha_y = a, ior = b
  *   velvet         alpha_x = sigma, alpha_y = 1 / sigma^2
  *   toon           alpha_x = size, alpha_y = smooth
+ *   principled     diffuse: alpha_x = roughness; sheen: alpha_x = avg_value
  * A MicrofacetExtra slot (closure_alloc_extra, svm_closure.h) holds
  * weight = color, N = cspec0, T = fresnel_color, alpha_x = clearcoat.
  */
@@ -683,6 +685,131 @@ CY_FN int bsdf_glossy_toon_sample(const CyClosure *sc,
   }
   return LABEL_GLOSSY | LABEL_REFLECT;
 }
+
+#if CY_CLOSURE_EXT
+/* bsdf_util.h:129-134 */
+CY_FN float schlick_fresnel(float u)
+{
+  float m = cclamp(1.0f - u, 0.0f, 1.0f);
+  float m2 = m * m;
+  return m2 * m2 * m;
+}
+
+/* bsdf_principled_diffuse.h:33-118 (alpha_x = roughness) */
+CY_FN cfloat3 calculate_principled_diffuse_brdf(const CyClosure *sc, cfloat3 N, cfloat3 V, cfloat3 L, cfloat3 H,
+                                                float *pdf)
+{
+  float NdotL = cmax(dot3(N, L), 0.0f);
+  float NdotV = cmax(dot3(N, V), 0.0f);
+  if (NdotL < 0 || NdotV < 0) {
+    *pdf = 0.0f;
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float LdotH = dot3(L, H);
+  float FL = schlick_fresnel(NdotL), FV = schlick_fresnel(NdotV);
+  const float Fd90 = 0.5f + 2.0f * LdotH * LdotH * sc->alpha_x;
+  float Fd = (1.0f * (1.0f - FL) + Fd90 * FL) * (1.0f * (1.0f - FV) + Fd90 * FV);
+  float value = CY_1_PI_F * NdotL * Fd;
+  return mk3(value, value, value);
+}
+
+CY_FN cfloat3 bsdf_principled_diffuse_eval_reflect(const CyClosure *sc, cfloat3 I, cfloat3 omega_in, float *pdf)
+{
+  cfloat3 N = sc->N;
+  cfloat3 H = normalize3(add3(omega_in, I));
+  if (dot3(N, omega_in) > 0.0f) {
+    *pdf = fmaxf(dot3(N, omega_in), 0.0f) * CY_1_PI_F;
+    return calculate_principled_diffuse_brdf(sc, N, I, omega_in, H, pdf);
+  }
+  *pdf = 0.0f;
+  return mk3(0.0f, 0.0f, 0.0f);
+}
+
+CY_FN int bsdf_principled_diffuse_sample(const CyClosure *sc,
+                                         cfloat3 Ng,
+                                         cfloat3 I,
+                                         float randu,
+                                         float randv,
+                                         cfloat3 *eval,
+                                         cfloat3 *omega_in,
+                                         float *pdf)
+{
+  cfloat3 N = sc->N;
+  sample_cos_hemisphere(N, randu, randv, omega_in, pdf);
+  if (dot3(Ng, *omega_in) > 0) {
+    cfloat3 H = normalize3(add3(I, *omega_in));
+    *eval = calculate_principled_diffuse_brdf(sc, N, I, *omega_in, H, pdf);
+  }
+  else {
+    *pdf = 0.0f;
+  }
+  return LABEL_REFLECT | LABEL_DIFFUSE;
+}
+
+/* bsdf_principled_sheen.h:33-137 (alpha_x = avg_value) */
+CY_FN float calculate_avg_principled_sheen_brdf(cfloat3 N, cfloat3 I)
+{
+  float NdotI = dot3(N, I);
+  if (NdotI < 0.0f) {
+    return 0.0f;
+  }
+  return schlick_fresnel(NdotI) * NdotI;
+}
+
+CY_FN cfloat3 calculate_principled_sheen_brdf(cfloat3 N, cfloat3 V, cfloat3 L, cfloat3 H, float *pdf)
+{
+  float NdotL = dot3(N, L);
+  float NdotV = dot3(N, V);
+  if (NdotL < 0 || NdotV < 0) {
+    *pdf = 0.0f;
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float LdotH = dot3(L, H);
+  float value = schlick_fresnel(LdotH) * NdotL;
+  return mk3(value, value, value);
+}
+
+CY_FN int bsdf_principled_sheen_setup(const CySD *sd, CyClosure *b)
+{
+  b->type = CLOSURE_BSDF_PRINCIPLED_SHEEN_ID;
+  b->alpha_x = calculate_avg_principled_sheen_brdf(b->N, sd->I);
+  b->sample_weight *= b->alpha_x;
+  return SD_BSDF | SD_BSDF_HAS_EVAL;
+}
+
+CY_FN cfloat3 bsdf_principled_sheen_eval_reflect(const CyClosure *sc, cfloat3 I, cfloat3 omega_in, float *pdf)
+{
+  cfloat3 N = sc->N;
+  cfloat3 H = normalize3(add3(omega_in, I));
+  if (dot3(N, omega_in) > 0.0f) {
+    *pdf = fmaxf(dot3(N, omega_in), 0.0f) * CY_1_PI_F;
+    return calculate_principled_sheen_brdf(N, I, omega_in, H, pdf);
+  }
+  *pdf = 0.0f;
+  return mk3(0.0f, 0.0f, 0.0f);
+}
+
+CY_FN int bsdf_principled_sheen_sample(const CyClosure *sc,
+                                       cfloat3 Ng,
+                                       cfloat3 I,
+                                       float randu,
+                                       float randv,
+                                       cfloat3 *eval,
+                                       cfloat3 *omega_in,
+                                       float *pdf)
+{
+  cfloat3 N = sc->N;
+  sample_cos_hemisphere(N, randu, randv, omega_in, pdf);
+  if (dot3(Ng, *omega_in) > 0) {
+    cfloat3 H = normalize3(add3(I, *omega_in));
+    *eval = calculate_principled_sheen_brdf(N, I, *omega_in, H, pdf);
+  }
+  else {
+    *pdf = 0.0f;
+  }
+  return LABEL_REFLECT | LABEL_DIFFUSE;
+}
+#endif /* CY_CLOSURE_EXT: principled diffuse / sheen */
 
 /* ---------------------------------------------------------------------------
  * Singular closures (bsdf_reflection.h:60-95, bsdf_refraction.h:62-111)
@@ -1485,6 +1612,12 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
     case CLOSURE_BSDF_TRANSLUCENT_ID:
       label = bsdf_translucent_sample(sc, Ng, randu, randv, eval, omega_in, pdf);
       break;
+    case CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID:
+      label = bsdf_principled_diffuse_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
+      break;
+    case CLOSURE_BSDF_PRINCIPLED_SHEEN_ID:
+      label = bsdf_principled_sheen_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
+      break;
 #endif
     case CLOSURE_BSDF_REFLECTION_ID:
       label = bsdf_reflection_sample(sc, Ng, sd->I, eval, omega_in, pdf);
@@ -1559,6 +1692,12 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
 #if CY_CLOSURE_EXT
       case CLOSURE_BSDF_OREN_NAYAR_ID:
         eval = bsdf_oren_nayar_eval_reflect(sc, sd->I, omega_in, pdf);
+        break;
+      case CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID:
+        eval = bsdf_principled_diffuse_eval_reflect(sc, sd->I, omega_in, pdf);
+        break;
+      case CLOSURE_BSDF_PRINCIPLED_SHEEN_ID:
+        eval = bsdf_principled_sheen_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
 #endif
       case CLOSURE_BSDF_MICROFACET_GGX_ID:

@@ -1146,6 +1146,214 @@ CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, flo
   }
 }
 
+#if CY_CLOSURE_EXT
+/* svm_closure.h:100-463: the Principled BSDF with the GGX distribution
+ * (the multiscatter distribution is rejected at load_kernels).  On the
+ * reference CPU kernel __SUBSURFACE__ is defined, so the diffuse lobe is
+ * gated by the subsurface mix; subsurface > 0 needs a BSSRDF and sets
+ * CY_ERR_CLOSURE.  The tangent input is read only when linked (the
+ * reference reads stack slot 255 otherwise). */
+CY_FN void svm_node_principled_bsdf(const CyGlobals *kg,
+                                    CySD *sd,
+                                    CySvmStack stack,
+                                    hc_uint4 data_node,
+                                    cfloat3 N,
+                                    float param1,
+                                    float param2,
+                                    float mix_weight,
+                                    int path_flag,
+                                    int *offset,
+                                    uint *err)
+{
+  hc_uint4 data_node2 = kg->__svm_nodes[(*offset)++];
+  cfloat3 T = (data_node.y != SVM_STACK_INVALID) ? svm_load3(stack, data_node.y, err) : mk3(0.0f, 0.0f, 0.0f);
+  const uint specular_offset = data_node.z & 0xFF, roughness_offset = (data_node.z >> 8) & 0xFF;
+  const uint specular_tint_offset = (data_node.z >> 16) & 0xFF, anisotropic_offset = (data_node.z >> 24) & 0xFF;
+  const uint sheen_offset = data_node.w & 0xFF, sheen_tint_offset = (data_node.w >> 8) & 0xFF;
+  const uint clearcoat_offset = (data_node.w >> 16) & 0xFF, clearcoat_roughness_offset = (data_node.w >> 24) & 0xFF;
+  const uint eta_offset = data_node2.x & 0xFF, transmission_offset = (data_node2.x >> 8) & 0xFF;
+  const uint anisotropic_rotation_offset = (data_node2.x >> 16) & 0xFF;
+  const uint transmission_roughness_offset = (data_node2.x >> 24) & 0xFF;
+  float metallic = param1;
+  float subsurface = param2;
+  float specular = svm_load(stack, specular_offset, err);
+  float roughness = svm_load(stack, roughness_offset, err);
+  float specular_tint = svm_load(stack, specular_tint_offset, err);
+  float anisotropic = svm_load(stack, anisotropic_offset, err);
+  float sheen = svm_load(stack, sheen_offset, err);
+  float sheen_tint = svm_load(stack, sheen_tint_offset, err);
+  float clearcoat = svm_load(stack, clearcoat_offset, err);
+  float clearcoat_roughness = svm_load(stack, clearcoat_roughness_offset, err);
+  float transmission = svm_load(stack, transmission_offset, err);
+  float anisotropic_rotation = svm_load(stack, anisotropic_rotation_offset, err);
+  float transmission_roughness = svm_load(stack, transmission_roughness_offset, err);
+  float eta = fmaxf(svm_load(stack, eta_offset, err), 1e-5f);
+  const uint distribution = data_node2.y;
+  if (anisotropic_rotation != 0.0f) {
+    T = rotate_around_axis(T, N, anisotropic_rotation * CY_2PI_F);
+  }
+  float ior = (sd->flag & SD_BACKFACING) ? 1.0f / eta : eta;
+  float cosNO = dot3(N, sd->I);
+  float fresnel = fresnel_dielectric_cos(cosNO, ior);
+  float diffuse_weight = (1.0f - saturate(metallic)) * (1.0f - saturate(transmission));
+  float final_transmission = saturate(transmission) * (1.0f - saturate(metallic));
+  float specular_weight = (1.0f - final_transmission);
+
+  hc_uint4 data_base_color = kg->__svm_nodes[(*offset)++];
+  cfloat3 base_color = (data_base_color.x != SVM_STACK_INVALID) ?
+                           svm_load3(stack, data_base_color.x, err) :
+                           mk3(as_float(data_base_color.y), as_float(data_base_color.z),
+                               as_float(data_base_color.w));
+  hc_uint4 data_cn_ssr = kg->__svm_nodes[(*offset)++];
+  cfloat3 clearcoat_normal = (data_cn_ssr.x != SVM_STACK_INVALID) ? svm_load3(stack, data_cn_ssr.x, err) : sd->N;
+  hc_uint4 data_subsurface_color = kg->__svm_nodes[(*offset)++];
+  cfloat3 subsurface_color = (data_subsurface_color.x != SVM_STACK_INVALID) ?
+                                 svm_load3(stack, data_subsurface_color.x, err) :
+                                 mk3(as_float(data_subsurface_color.y), as_float(data_subsurface_color.z),
+                                     as_float(data_subsurface_color.w));
+  cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+
+  /* diffuse, gated by the subsurface mix (__SUBSURFACE__ branch) */
+  cfloat3 mixed_ss_base_color = add3(mul3f(subsurface_color, subsurface), mul3f(base_color, (1.0f - subsurface)));
+  if (path_flag & PATH_RAY_DIFFUSE_ANCESTOR) {
+    subsurface = 0.0f;
+    base_color = mixed_ss_base_color;
+  }
+  if (fabsf(average3(mixed_ss_base_color)) > CLOSURE_WEIGHT_CUTOFF) {
+    if (subsurface <= CLOSURE_WEIGHT_CUTOFF && diffuse_weight > CLOSURE_WEIGHT_CUTOFF) {
+      cfloat3 diff_weight = mul3f(mul3(weight, base_color), diffuse_weight);
+      CyClosure *b = bsdf_alloc(sd, diff_weight);
+      if (b) {
+        b->N = N;
+        b->alpha_x = roughness;
+        b->type = CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID;
+        sd->flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
+      }
+    }
+    else if (subsurface > CLOSURE_WEIGHT_CUTOFF) {
+      cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID); /* subsurface scattering */
+    }
+  }
+
+  /* sheen */
+  if (diffuse_weight > CLOSURE_WEIGHT_CUTOFF && sheen > CLOSURE_WEIGHT_CUTOFF) {
+    float m_cdlum = dot3(base_color, mk3(KD->film.rgb_to_y.x, KD->film.rgb_to_y.y, KD->film.rgb_to_y.z));
+    cfloat3 m_ctint = m_cdlum > 0.0f ? div3f(base_color, m_cdlum) : mk3(1.0f, 1.0f, 1.0f);
+    cfloat3 sheen_color = add3(mul3f(mk3(1.0f, 1.0f, 1.0f), (1.0f - sheen_tint)), mul3f(m_ctint, sheen_tint));
+    cfloat3 sheen_weight = mul3f(mul3(mul3f(weight, sheen), sheen_color), diffuse_weight);
+    CyClosure *b = bsdf_alloc(sd, sheen_weight);
+    if (b) {
+      b->N = N;
+      sd->flag |= bsdf_principled_sheen_setup(sd, b);
+    }
+  }
+
+  /* specular reflection */
+  if (KD->integrator.caustics_reflective || (path_flag & PATH_RAY_DIFFUSE) == 0) {
+    if (specular_weight > CLOSURE_WEIGHT_CUTOFF &&
+        (specular > CLOSURE_WEIGHT_CUTOFF || metallic > CLOSURE_WEIGHT_CUTOFF)) {
+      cfloat3 spec_weight = mul3f(weight, specular_weight);
+      CyClosure *b = bsdf_alloc(sd, spec_weight);
+      int extra = (b != 0) ? closure_alloc_extra(sd) : -1;
+      if (b && extra >= 0) {
+        CyClosure *ex = &sd->closure[extra];
+        b->N = N;
+        b->ior = (2.0f / (1.0f - safe_sqrtf(0.08f * specular))) - 1.0f;
+        b->T = T;
+        b->extra = extra;
+        float aspect = safe_sqrtf(1.0f - anisotropic * 0.9f);
+        float r2 = roughness * roughness;
+        b->alpha_x = r2 / aspect;
+        b->alpha_y = r2 * aspect;
+        float m_cdlum = 0.3f * base_color.x + 0.6f * base_color.y + 0.1f * base_color.z;
+        cfloat3 m_ctint = m_cdlum > 0.0f ? div3f(base_color, m_cdlum) : mk3(0.0f, 0.0f, 0.0f);
+        cfloat3 tmp_col = add3(mul3f(mk3(1.0f, 1.0f, 1.0f), (1.0f - specular_tint)), mul3f(m_ctint, specular_tint));
+        ex->N = add3(mul3f(mul3f(tmp_col, specular * 0.08f), (1.0f - metallic)), mul3f(base_color, metallic));
+        ex->weight = base_color;
+        ex->alpha_x = 0.0f;
+        if (distribution == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID || roughness <= 0.075f) {
+          sd->flag |= bsdf_microfacet_ggx_fresnel_setup(b, sd);
+        }
+        else {
+          cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID);
+        }
+      }
+    }
+  }
+
+  /* glass */
+  if (KD->integrator.caustics_reflective || KD->integrator.caustics_refractive ||
+      (path_flag & PATH_RAY_DIFFUSE) == 0) {
+    if (final_transmission > CLOSURE_WEIGHT_CUTOFF) {
+      cfloat3 glass_weight = mul3f(weight, final_transmission);
+      cfloat3 cspec0 = add3(mul3f(base_color, specular_tint), mul3f(mk3(1.0f, 1.0f, 1.0f), (1.0f - specular_tint)));
+      if (roughness <= 5e-2f || distribution == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID) {
+        float refl_roughness = roughness;
+        if (KD->integrator.caustics_reflective || (path_flag & PATH_RAY_DIFFUSE) == 0) {
+          CyClosure *b = bsdf_alloc(sd, mul3f(glass_weight, fresnel));
+          int extra = (b != 0) ? closure_alloc_extra(sd) : -1;
+          if (b && extra >= 0) {
+            CyClosure *ex = &sd->closure[extra];
+            b->N = N;
+            b->T = mk3(0.0f, 0.0f, 0.0f);
+            b->extra = extra;
+            b->alpha_x = refl_roughness * refl_roughness;
+            b->alpha_y = refl_roughness * refl_roughness;
+            b->ior = ior;
+            ex->weight = base_color;
+            ex->N = cspec0;
+            ex->alpha_x = 0.0f;
+            sd->flag |= bsdf_microfacet_ggx_fresnel_setup(b, sd);
+          }
+        }
+        if (KD->integrator.caustics_refractive || (path_flag & PATH_RAY_DIFFUSE) == 0) {
+          CyClosure *b = bsdf_alloc(sd, mul3f(mul3(base_color, glass_weight), (1.0f - fresnel)));
+          if (b) {
+            b->N = N;
+            b->T = mk3(0.0f, 0.0f, 0.0f);
+            b->extra = -1;
+            if (distribution == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID) {
+              transmission_roughness = 1.0f - (1.0f - refl_roughness) * (1.0f - transmission_roughness);
+            }
+            else {
+              transmission_roughness = refl_roughness;
+            }
+            b->alpha_x = transmission_roughness * transmission_roughness;
+            b->alpha_y = transmission_roughness * transmission_roughness;
+            b->ior = ior;
+            sd->flag |= bsdf_microfacet_ggx_refraction_setup(b);
+          }
+        }
+      }
+      else {
+        cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID);
+      }
+    }
+  }
+
+  /* clearcoat */
+  if (KD->integrator.caustics_reflective || (path_flag & PATH_RAY_DIFFUSE) == 0) {
+    if (clearcoat > CLOSURE_WEIGHT_CUTOFF) {
+      CyClosure *b = bsdf_alloc(sd, weight);
+      int extra = (b != 0) ? closure_alloc_extra(sd) : -1;
+      if (b && extra >= 0) {
+        CyClosure *ex = &sd->closure[extra];
+        b->N = clearcoat_normal;
+        b->T = mk3(0.0f, 0.0f, 0.0f);
+        b->ior = 1.5f;
+        b->extra = extra;
+        b->alpha_x = clearcoat_roughness * clearcoat_roughness;
+        b->alpha_y = clearcoat_roughness * clearcoat_roughness;
+        ex->weight = mk3(0.0f, 0.0f, 0.0f);
+        ex->N = mk3(0.04f, 0.04f, 0.04f);
+        ex->alpha_x = clearcoat;
+        sd->flag |= bsdf_microfacet_ggx_clearcoat_setup(b, sd);
+      }
+    }
+  }
+}
+#endif
+
 /* svm_closure.h:58-735 svm_node_closure_bsdf (every BSDF the SVM compiler
  * emits except Principled, multiscatter GGX and hair; those set
  * CY_ERR_CLOSURE). */
@@ -1165,6 +1373,9 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
   hc_uint4 data_node = kg->__svm_nodes[*offset];
   (*offset)++;
   if (mix_weight == 0.0f) {
+    if (type == CLOSURE_BSDF_PRINCIPLED_ID) {
+      *offset += 4; /* the principled node's extra data */
+    }
     return;
   }
   cfloat3 N = (data_node.x != SVM_STACK_INVALID) ? svm_load3(stack, data_node.x, err) : sd->N;
@@ -1173,6 +1384,11 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
   float param2 = (param2_offset != SVM_STACK_INVALID) ? svm_load(stack, param2_offset, err) :
                                                         as_float(node.w);
   switch (type) {
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_PRINCIPLED_ID:
+      svm_node_principled_bsdf(kg, sd, stack, data_node, N, param1, param2, mix_weight, path_flag, offset, err);
+      break;
+#endif
     case CLOSURE_BSDF_DIFFUSE_ID: {
       cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
       CyClosure *b = bsdf_alloc(sd, weight);

@@ -79,6 +79,17 @@ GLASS_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_SHARP_GLASS_ID, "ggx": CLOSURE_BSDF
                        "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID}
 REFRACTION_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFRACTION_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID,
                             "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID}
+CLOSURE_BSDF_PRINCIPLED_ID = 45
+CLOSURE_BSSRDF_PRINCIPLED_ID = 37
+PRINCIPLED_DISTRIBUTIONS = {"ggx": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID, "multiscatter": 25}
+# PrincipledBsdfNode sockets and defaults (render/nodes.cpp:2720-2770)
+PRINCIPLED_DEFAULTS = {
+    "base_color": (0.8, 0.8, 0.8), "subsurface_color": (0.8, 0.8, 0.8), "metallic": 0.0, "subsurface": 0.0,
+    "subsurface_radius": (0.1, 0.1, 0.1), "specular": 0.0, "roughness": 0.5, "specular_tint": 0.0,
+    "anisotropic": 0.0, "sheen": 0.0, "sheen_tint": 0.0, "clearcoat": 0.0, "clearcoat_roughness": 0.03,
+    "ior": 0.0, "transmission": 0.0, "transmission_roughness": 0.0, "anisotropic_rotation": 0.0,
+}
+PRINCIPLED_VECTORS = ("normal", "clearcoat_normal", "tangent")
 BECKMANN_CLOSURES = (CLOSURE_BSDF_MICROFACET_BECKMANN_ID, CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID,
                      CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)
 SD_HAS_TRANSPARENT_SHADOW = 1 << 17
@@ -112,6 +123,7 @@ class Closure:
     anisotropy: object = 0.0
     rotation: object = 0.0
     tangent: object = None
+    params: dict | None = None  # principled: PRINCIPLED_DEFAULTS keys + normals
 
     def closure_type(self) -> int:
         """The ClosureType the node compiles to, after simplify_settings
@@ -136,6 +148,8 @@ class Closure:
             return self.a.num_closures() + self.b.num_closures()
         if self.kind == "glass":
             return 2
+        if self.kind == "principled":
+            return 8  # CLOSURE_IS_PRINCIPLED
         return 1
 
     def closure_types(self) -> set:
@@ -143,6 +157,8 @@ class Closure:
             return self.a.closure_types() | self.b.closure_types()
         if self.kind in ("emission", "background"):
             return set()
+        if self.kind == "principled":
+            return {CLOSURE_BSDF_PRINCIPLED_ID}
         return {self.closure_type()}
 
     def has_emission(self) -> bool:
@@ -165,6 +181,11 @@ class Closure:
             v = getattr(self, name)
             if nodes.is_linked(v) and (self.kind == "mix") == (name == "fac"):
                 out.append((v, t))
+        if self.kind == "principled":
+            for name, v in self.params.items():
+                if nodes.is_linked(v):
+                    vec = name in PRINCIPLED_VECTORS or name == "subsurface_radius"
+                    out.append((v, "color" if name.endswith("color") else "vector" if vec else "float"))
         for sub in (self.a, self.b):
             if sub is not None:
                 out.extend(sub.sockets())
@@ -210,6 +231,22 @@ def refraction(color, roughness, ior=1.45, normal=None, distribution="ggx"):
     """Refraction BSDF: distribution ggx | beckmann | sharp."""
     return Closure("refraction", _const_or_socket(color), roughness=roughness, ior=ior, normal=normal,
                    distribution=distribution)
+
+
+def principled(distribution="ggx", **params):
+    """Principled BSDF (nodes.cpp PrincipledBsdfNode, svm_closure.h:100-463).
+    Parameters are PRINCIPLED_DEFAULTS keys (constants or sockets) plus the
+    normal / clearcoat_normal / tangent vector sockets.  distribution is
+    "ggx" ("multiscatter" is refused at load_kernels); subsurface > 0 needs a
+    BSSRDF, which the device does not implement.  The node's Emission and
+    Alpha inputs (expanded into separate closures by the reference graph) are
+    expressed here with emission() / transparent() and mix()."""
+    unknown = set(params) - set(PRINCIPLED_DEFAULTS) - set(PRINCIPLED_VECTORS)
+    if unknown:
+        raise ValueError(f"principled: unknown parameters {sorted(unknown)}")
+    p = dict(PRINCIPLED_DEFAULTS)
+    p.update(params)
+    return Closure("principled", distribution=distribution, params=p)
 
 
 def translucent(color, normal=None):
@@ -304,6 +341,8 @@ class SVMCompiler:
                 emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in const)))
             emit((NODE_CLOSURE_EMISSION if c.kind == "emission" else NODE_CLOSURE_BACKGROUND, mix_weight, 0, 0))
             return out
+        if c.kind == "principled":
+            return self.emit_principled(c, mix_weight)
         ctype = c.closure_type()
         # nodes.cpp BsdfNode::compile: linked color -> NODE_CLOSURE_WEIGHT
         if nodes.is_linked(c.color):
@@ -331,6 +370,63 @@ class SVMCompiler:
         emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))
         # data node: normal, tangent, param3, param4
         emit((normal_off, tangent_off, param3_off, SVM_STACK_INVALID))
+        return out
+
+    def emit_principled(self, c: Closure, mix_weight: int) -> list:
+        """nodes.cpp:2839-2925 PrincipledBsdfNode::compile: weight (1,1,1), every
+        float input stack-assigned (constants materialised as temporaries,
+        released after the node like svm.cpp stack_clear_temporary), the
+        closure node, its data node and four parameter nodes."""
+        out = []
+        emit = out.append
+        p = c.params
+        nc = self.nc
+        emit((NODE_CLOSURE_SET_WEIGHT, f32bits(1.0), f32bits(1.0), f32bits(1.0)))
+        temps: list = []
+
+        def vec_if_linked(name):
+            v = p.get(name)
+            return nc.link(v, "vector") if nodes.is_linked(v) else SVM_STACK_INVALID
+
+        # NodeCompiler.assign emits through self.nc.emit (the shader's code);
+        # route it into this closure's code while the inputs are assigned
+        saved_emit, nc.emit = nc.emit, emit
+        try:
+            normal_off = vec_if_linked("normal")
+            cc_normal_off = vec_if_linked("clearcoat_normal")
+            tangent_off = vec_if_linked("tangent")
+            offs = {}
+            for name in ("specular", "roughness", "specular_tint", "anisotropic", "sheen", "sheen_tint", "clearcoat",
+                         "clearcoat_roughness", "ior", "transmission", "transmission_roughness",
+                         "anisotropic_rotation"):
+                offs[name] = nc.assign(p[name], "float", temps)
+            radius_off = nc.assign(p["subsurface_radius"], "vector", temps)
+            metallic_off = nc.assign(p["metallic"], "float", temps)
+            subsurface_off = nc.assign(p["subsurface"], "float", temps)
+            base_off = nc.link(p["base_color"], "color") if nodes.is_linked(p["base_color"]) else SVM_STACK_INVALID
+            ss_off = (nc.link(p["subsurface_color"], "color") if nodes.is_linked(p["subsurface_color"])
+                      else SVM_STACK_INVALID)
+        finally:
+            nc.emit = saved_emit
+
+        def const(v, default):
+            return default if nodes.is_linked(v) else v
+
+        emit((NODE_CLOSURE_BSDF, self.uchar4(CLOSURE_BSDF_PRINCIPLED_ID, metallic_off, subsurface_off, mix_weight),
+              f32bits(const(p["metallic"], 0.0)), f32bits(const(p["subsurface"], 0.0))))
+        emit((normal_off, tangent_off,
+              self.uchar4(offs["specular"], offs["roughness"], offs["specular_tint"], offs["anisotropic"]),
+              self.uchar4(offs["sheen"], offs["sheen_tint"], offs["clearcoat"], offs["clearcoat_roughness"])))
+        emit((self.uchar4(offs["ior"], offs["transmission"], offs["anisotropic_rotation"],
+                          offs["transmission_roughness"]),
+              PRINCIPLED_DISTRIBUTIONS[c.distribution], CLOSURE_BSSRDF_PRINCIPLED_ID, SVM_STACK_INVALID))
+        bc = const(p["base_color"], PRINCIPLED_DEFAULTS["base_color"])
+        emit((base_off, *(f32bits(x) for x in bc)))
+        emit((cc_normal_off, radius_off, SVM_STACK_INVALID, SVM_STACK_INVALID))
+        ssc = const(p["subsurface_color"], PRINCIPLED_DEFAULTS["subsurface_color"])
+        emit((ss_off, *(f32bits(x) for x in ssc)))
+        for off, w in temps:
+            self.free(off, w)
         return out
 
     def compile(self, surfaces: list[Closure], world: Closure) -> np.ndarray:

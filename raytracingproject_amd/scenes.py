@@ -737,3 +737,28 @@ def closures_microfacet(width=48, height=48, samples=8) -> sc.Scene:
         sc.anisotropic((0.7, 0.8, 0.9), 0.3, -0.5, 0.1, tangent, distribution="beckmann"),
     ]
     return _closure_gallery(width, height, samples, "closures_microfacet", mats)
+
+
+def closures_principled(width=48, height=48, samples=8) -> sc.Scene:
+    """Principled BSDF (svm_closure.h:100-463, GGX distribution): dielectric
+    with specular, anisotropic metal, rough glass (transmission), sheen,
+    clearcoat over half-metal, node-driven base colour and roughness."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    tangent = nd.vector_math("cross_product", g["Normal"], (0.0, 1.0, 0.0))["Vector"]
+    u = nd.separate_xyz(g["Parametric"])["X"]
+    checker = nd.checker(nd.tex_coord()["Object"], (0.9, 0.3, 0.1), (0.1, 0.4, 0.8), 0.02)["Color"]
+    mats = [
+        sc.principled(base_color=(0.8, 0.2, 0.1), roughness=0.4, specular=0.5),
+        sc.principled(base_color=(0.9, 0.7, 0.3), metallic=1.0, roughness=0.3, anisotropic=0.6,
+                      anisotropic_rotation=0.1, tangent=tangent, specular=0.5),
+        sc.principled(base_color=(0.9, 0.95, 1.0), transmission=1.0, roughness=0.1, ior=1.45, specular=0.5,
+                      transmission_roughness=0.2),
+        sc.principled(base_color=(0.3, 0.5, 0.8), sheen=1.0, sheen_tint=0.5, roughness=0.8, specular=0.3),
+        sc.principled(base_color=(0.1, 0.1, 0.1), clearcoat=1.0, clearcoat_roughness=0.1, roughness=0.5,
+                      specular=0.5, metallic=0.5),
+        sc.principled(base_color=checker, roughness=nd.math("multiply", u, 0.8), specular=0.5, specular_tint=0.5,
+                      ior=1.5, transmission=0.3),
+    ]
+    return _closure_gallery(width, height, samples, "closures_principled", mats)

@@ -38,6 +38,7 @@ CASES = {
     # BSDF closure breadth (closure/bsdf_*.h): diffuse family, microfacets
     "closures_diffuse": lambda: scenes.closures_diffuse(48, 48, 8),
     "closures_microfacet": lambda: scenes.closures_microfacet(48, 48, 8),
+    "closures_principled": lambda: scenes.closures_principled(48, 48, 8),
 }
 
 
