@@ -19,6 +19,7 @@
  * Compile-checked (g++ -fsyntax-only against the reference headers) by
  * tests/test_integration.py; it is not linked into this repository's products.
  */
+#include <algorithm>
 #include "device/device.h"
 #include "device/device_intern.h"
 
@@ -158,11 +159,22 @@ class HIPCyclesDevice : public Device {
       /* LightManager background map (light.cpp:38-85) -> CUDADevice::shader
        * (device_cuda_impl.cpp:2019-2093); SHADER_EVAL_DISPLACE is rejected */
       task_pool_.push([=] {
-        check(hipcy_shader_eval(dev_, (int)task.shader_eval_type, (uint64_t)task.shader_input,
-                                (uint64_t)task.shader_output, task.shader_x, task.shader_w, task.offset,
-                                task.num_samples));
+        /* per sample, 64K-pixel chunks with a cancel check between them and
+         * progress after each sample, as CUDADevice::shader does; background
+         * evaluation does not depend on the sample index (kernel_bake.h:474) */
         DeviceTask task_copy = task;
-        task_copy.update_progress(NULL);
+        const int chunk = 0x10000;
+        const int end = task.shader_x + task.shader_w;
+        for (int sample = 0; sample < task.num_samples; sample++) {
+          for (int x = task.shader_x; x < end; x += chunk) {
+            if (task_copy.get_cancel()) {
+              return;
+            }
+            check(hipcy_shader_eval(dev_, (int)task.shader_eval_type, (uint64_t)task.shader_input,
+                                    (uint64_t)task.shader_output, x, std::min(chunk, end - x), task.offset, 1));
+          }
+          task_copy.update_progress(NULL);
+        }
       });
       return;
     }

@@ -32,14 +32,15 @@ def test_background_eval_bit_exact(name, device):
 
 
 def test_background_eval_large_map_chunks(device):
-    """A map beyond one 65536-pixel chunk (CUDADevice::shader chunking): every
-    pixel of a constant world equals the small fixture's value."""
+    """A map beyond one 65536-pixel chunk with a partial last chunk (300 x 250
+    = 75000 pixels; CUDADevice::shader chunking): every pixel of a constant
+    world equals the small fixture's value."""
     fn, w, h, s = BACKGROUND_CASES["world_blue"]
     g = load_background_golden()["out_world_blue"]
     device.upload_scene(sc.compile_scene(fn()))
-    out = device.background_eval(512, 256, s)
+    out = device.background_eval(300, 250, s)
     assert np.array_equal(out.reshape(-1, 4).view(np.uint32),
-                          np.broadcast_to(g[0, 0], (512 * 256, 4)).view(np.uint32))
+                          np.broadcast_to(g[0, 0], (300 * 250, 4)).view(np.uint32))
 
 
 def test_shader_eval_displace_rejected():
