@@ -35,6 +35,10 @@
  *   hipcy_shader_eval                        device_cuda_impl.cpp:2019-2093 CUDADevice::shader
  *                                            (DeviceTask SHADER, SHADER_EVAL_BACKGROUND;
  *                                            kernel_bake.h:474-510, light.cpp:38-85)
+ *   hipcy_tex_alloc / hipcy_tex_free         device_cuda_impl.cpp:1105-1304 CUDADevice::tex_alloc /
+ *                                            tex_free + load_texture_info (device_texture of
+ *                                            render/image.cpp device_load_image; the SVM image
+ *                                            slot indexes __texture_info, kernel_textures.h:84)
  *   hipcy_film_convert                       device_cuda_impl.cpp:1954-2017 CUDADevice::film_convert
  *                                            (DeviceTask FILM_CONVERT; kernel/kernel_film.h)
  *   hipcy_intersect / hipcy_camera_rays      test entry points (scene_intersect, bvh/bvh.h:154;
@@ -50,7 +54,7 @@
 extern "C" {
 #endif
 
-#define HIPCY_ABI_VERSION 3
+#define HIPCY_ABI_VERSION 4
 
 typedef struct hipcy_device hipcy_device;
 
@@ -103,6 +107,17 @@ int hipcy_mem_zero(hipcy_device *dev, uint64_t device_pointer, size_t bytes);
 
 int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, size_t size);
 int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_pointer, size_t bytes);
+/* Image textures: a 2D image of width x height texels of ImageDataType
+ * data_type (util_texture.h: 0 float4, 1 byte4, 2 half4, 3 float, 4 byte,
+ * 5 half, 6 ushort4, 7 ushort) with interpolation (0 linear, 1 closest,
+ * 2 cubic, 3 smart) and extension (0 repeat, 1 extend, 2 clip) in SVM image
+ * slot `slot`.  The pixels are copied to device memory owned by the device;
+ * the device keeps the TextureInfo table and binds it as __texture_info.
+ * bytes must equal width * height * the texel size.  Re-allocating a slot
+ * replaces it; hipcy_tex_free releases it. */
+int hipcy_tex_alloc(hipcy_device *dev, int slot, int data_type, int interpolation, int extension, int width,
+                    int height, const void *pixels, size_t bytes);
+int hipcy_tex_free(hipcy_device *dev, int slot);
 
 /* Validate that the scene uploaded so far only uses features the HIP kernels
  * implement and prepare it (widen the BVH); returns 0 or a negative code with a

@@ -31,6 +31,16 @@ typedef struct hc_float2 { float x, y; } hc_float2;
 typedef struct __attribute__((aligned(16))) hc_float4 { float x, y, z, w; } hc_float4;
 typedef struct __attribute__((aligned(16))) hc_uint4 { uint32_t x, y, z, w; } hc_uint4;
 typedef struct __attribute__((aligned(16))) hc_Transform { hc_float4 x, y, z; } hc_Transform;
+
+/* util_texture.h:93-107 TextureInfo (96 bytes: Transform is 16-byte aligned
+ * on the reference CPU build).  One per SVM image slot in __texture_info;
+ * `data` is the image's device address (a host pointer on the CPU device). */
+typedef struct __attribute__((aligned(16))) hc_TextureInfo {
+  uint64_t data;
+  uint32_t data_type, cl_buffer, interpolation, extension;
+  uint32_t width, height, depth, use_transform_3d;
+  hc_Transform transform_3d;
+} hc_TextureInfo;
 typedef struct __attribute__((aligned(16))) hc_ProjectionTransform { hc_float4 x, y, z, w; } hc_ProjectionTransform;
 
 /* X(type, name, count) — count > 1 declares an array. */

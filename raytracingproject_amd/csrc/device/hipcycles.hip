@@ -529,6 +529,14 @@ struct hipcy_device {
   int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
+
+  /* image textures (hipcy_tex_alloc): per SVM slot the device copy of the
+   * pixels and its TextureInfo; the table is mirrored into tex_info_dev and
+   * bound as __texture_info (CUDADevice::tex_alloc + load_texture_info) */
+  std::vector<hc_TextureInfo> tex_info;
+  std::vector<void *> tex_mem;
+  hc_TextureInfo *tex_info_dev = nullptr;
+  size_t tex_info_capacity = 0;
 };
 
 static int set_error(hipcy_device *dev, const std::string &msg)
@@ -805,6 +813,10 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->counters) hipFree(dev->counters);
   if (dev->stats_dev) hipFree(dev->stats_dev);
   if (dev->data_dev) hipFree(dev->data_dev);
+  for (void *t : dev->tex_mem) {
+    if (t) hipFree(t);
+  }
+  if (dev->tex_info_dev) hipFree(dev->tex_info_dev);
   if (dev->host_counters) hipHostFree(dev->host_counters);
   if (dev->stream) hipStreamDestroy(dev->stream);
   for (int l = 0; l < CY_LANES; l++) {
@@ -905,6 +917,82 @@ int hipcy_const_copy_to(hipcy_device *dev, const char *name, const void *host, s
   HIP_CHECK(dev, hipMemcpyAsync(dev->data_dev, host, size, hipMemcpyHostToDevice, dev->stream));
   HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
   return 0;
+}
+
+/* Mirror the texture table to the device and bind it as __texture_info. */
+static int upload_texture_info(hipcy_device *dev)
+{
+  const size_t n = dev->tex_info.size();
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  if (n > dev->tex_info_capacity) {
+    if (dev->tex_info_dev) {
+      HIP_CHECK(dev, hipFree(dev->tex_info_dev));
+    }
+    HIP_CHECK(dev, hipMalloc((void **)&dev->tex_info_dev, n * sizeof(hc_TextureInfo)));
+    dev->tex_info_capacity = n;
+  }
+  if (n) {
+    HIP_CHECK(dev, hipMemcpy(dev->tex_info_dev, dev->tex_info.data(), n * sizeof(hc_TextureInfo),
+                             hipMemcpyHostToDevice));
+  }
+  GlobalBinding b;
+  b.ptr = (uint64_t)dev->tex_info_dev;
+  b.bytes = n * sizeof(hc_TextureInfo);
+  dev->globals["__texture_info"] = b;
+  dev->features_dirty = true;
+  return 0;
+}
+
+int hipcy_tex_alloc(hipcy_device *dev, int slot, int data_type, int interpolation, int extension, int width,
+                    int height, const void *pixels, size_t bytes)
+{
+  if (!dev || slot < 0 || width <= 0 || height <= 0 || data_type < 0 || data_type > 7 || interpolation < 0 ||
+      interpolation > 3 || extension < 0 || extension > 2) {
+    return set_error(dev, "tex_alloc: invalid texture description");
+  }
+  static const size_t texel_bytes[8] = {16, 4, 8, 4, 1, 2, 8, 2}; /* ImageDataType order */
+  if (bytes != texel_bytes[data_type] * (size_t)width * (size_t)height) {
+    return set_error(dev, "tex_alloc: pixel buffer size does not match the texture description");
+  }
+  if (hipcy_tex_free(dev, slot) != 0) {
+    return -1;
+  }
+  if ((size_t)slot >= dev->tex_info.size()) {
+    dev->tex_info.resize(slot + 1);
+    dev->tex_mem.resize(slot + 1, nullptr);
+    memset(&dev->tex_info[slot], 0, sizeof(hc_TextureInfo));
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  void *mem = nullptr;
+  HIP_CHECK(dev, hipMalloc(&mem, bytes));
+  HIP_CHECK(dev, hipMemcpy(mem, pixels, bytes, hipMemcpyHostToDevice));
+  dev->tex_mem[slot] = mem;
+  hc_TextureInfo &info = dev->tex_info[slot];
+  memset(&info, 0, sizeof(info));
+  info.data = (uint64_t)mem;
+  info.data_type = (uint32_t)data_type;
+  info.interpolation = (uint32_t)interpolation;
+  info.extension = (uint32_t)extension;
+  info.width = (uint32_t)width;
+  info.height = (uint32_t)height;
+  info.depth = 1;
+  return upload_texture_info(dev);
+}
+
+int hipcy_tex_free(hipcy_device *dev, int slot)
+{
+  if (!dev) {
+    return -1;
+  }
+  if (slot < 0 || (size_t)slot >= dev->tex_mem.size() || !dev->tex_mem[slot]) {
+    return 0;
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  HIP_CHECK(dev, hipDeviceSynchronize());
+  HIP_CHECK(dev, hipFree(dev->tex_mem[slot]));
+  dev->tex_mem[slot] = nullptr;
+  memset(&dev->tex_info[slot], 0, sizeof(hc_TextureInfo));
+  return upload_texture_info(dev);
 }
 
 int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_pointer, size_t bytes)
@@ -1121,6 +1209,11 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           len = 3;
           tex = true;
           break;
+        case NODE_TEX_IMAGE:
+          len = 1 + (size_t)(((int)node.y > 0) ? (int)node.y : 0); /* UDIM tile nodes */
+          tex = true;
+          break;
+        case NODE_TEX_ENVIRONMENT:
         case NODE_GEOMETRY:
         case NODE_CONVERT:
         case NODE_HSV:

@@ -36,7 +36,8 @@
   X(hc_uint4, __svm_nodes) \
   X(hc_KernelShader, __shaders) \
   X(float, __lookup_table) \
-  X(uint32_t, __sample_pattern_lut)
+  X(uint32_t, __sample_pattern_lut) \
+  X(hc_TextureInfo, __texture_info)
 
 typedef struct CyGlobals {
   const hc_KernelData *data;

@@ -663,6 +663,7 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
                                         const hc_uint4 *svm_nodes,
                                         const hc_KernelShader *shaders,
                                         const hc_KernelObject *objects,
+                                        const hc_TextureInfo *texture_info,
                                         cfloat3 D,
                                         CyShadeMem mem,
                                         CyPathState state,
@@ -674,6 +675,7 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
   kgv.__svm_nodes = svm_nodes;
   kgv.__shaders = shaders;
   kgv.__objects = objects;
+  kgv.__texture_info = texture_info;
   const CyGlobals *kg = &kgv;
   CySD esd;
   shader_setup_from_background(kg, &esd, D, mem);
@@ -848,7 +850,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
           /* world shader evaluated along the ray, bounce raised for the
            * light-path node (path_state_modify_bounce) */
 #if CY_SVM_TEX
-          L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, ray.D,
+          L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray.D,
                                              mem, state, state.flag | PATH_RAY_EMISSION, err);
 #else
           cy_set_error(err, CY_ERR_FEATURE, 3); /* node world in the kernel without texture nodes */
@@ -983,7 +985,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
           else if (ls.type == LIGHT_BACKGROUND) {
             /* direct_emissive_eval (kernel_emission.h:37-86): the world
              * shader toward the sampled direction */
-            light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, ls.D, mem,
+            light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ls.D, mem,
                                              state, PATH_RAY_EMISSION, err);
           }
 #endif

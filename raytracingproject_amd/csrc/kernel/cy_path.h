@@ -1616,6 +1616,8 @@ CY_FN void emission_setup(CySD *sd, cfloat3 weight)
  * without them (picked at load_kernels when no shader uses them), whose
  * register allocation they would otherwise burden.  Returns the next node
  * offset, or -1 for an unknown node. */
+#include "cy_svm_image.h"
+
 typedef struct CySvmTexIn {
   cfloat3 P, N, Ng, I;
   float u, v, ray_length;
@@ -1626,6 +1628,7 @@ typedef struct CySvmTexIn {
 CY_FN int svm_eval_texture_node(const hc_KernelData *data,
                                       const hc_uint4 *svm_nodes,
                                       const hc_KernelObject *objects,
+                                      const hc_TextureInfo *texture_info,
                                       CySvmTexIn in,
                                       CySvmStack stack,
                                       hc_uint4 node,
@@ -1723,6 +1726,12 @@ CY_FN int svm_eval_texture_node(const hc_KernelData *data,
         break;
       case NODE_CLAMP:
         svm_node_clamp(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_TEX_IMAGE:
+        svm_node_tex_image(kg, texture_info, stack, node, &offset, err);
+        break;
+      case NODE_TEX_ENVIRONMENT:
+        svm_node_tex_environment(texture_info, stack, node, err);
         break;
       default:
         return -1;
@@ -1866,7 +1875,8 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         in.glossy_bounce = state ? state->glossy_bounce : 0;
         in.transparent_bounce = state ? state->transparent_bounce : 0;
         in.transmission_bounce = state ? state->transmission_bounce : 0;
-        offset = svm_eval_texture_node(kg->data, kg->__svm_nodes, kg->__objects, in, stack, node, path_flag, offset, err);
+        offset = svm_eval_texture_node(kg->data, kg->__svm_nodes, kg->__objects, kg->__texture_info, in, stack, node,
+                                       path_flag, offset, err);
         if (offset < 0) {
           cy_set_error(err, CY_ERR_SVM_NODE, node.x);
           return;
@@ -2394,17 +2404,7 @@ CY_FN cfloat3 klight_vec(const float *f)
  * weights are zero here; the weights are still normalised as the reference
  * does. */
 
-/* kernel_projection.h:56-65 direction_to_equirectangular (default range) */
-CY_FN void direction_to_equirectangular(cfloat3 dir, float *u, float *v)
-{
-  if (dir.x == 0.0f && dir.y == 0.0f && dir.z == 0.0f) {
-    *u = 0.0f;
-    *v = 0.0f;
-    return;
-  }
-  *u = (cy_atan2f(dir.y, dir.x) - CY_PI_F) / -CY_2PI_F;
-  *v = (cy_acosf(dir.z / len3(dir)) - CY_PI_F) / -CY_PI_F;
-}
+/* direction_to_equirectangular: cy_svm_image.h */
 
 /* kernel_montecarlo.h:112-121 */
 CY_FN cfloat3 sample_uniform_sphere(float u1, float u2)

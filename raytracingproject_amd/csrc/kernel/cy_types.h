@@ -128,6 +128,9 @@ enum {
   NODE_JUMP_IF_ONE = 10,
   NODE_VALUE_F = 14,
   NODE_VALUE_V = 15,
+  NODE_TEX_IMAGE = 23,
+  NODE_TEX_IMAGE_BOX = 24,
+  NODE_TEX_ENVIRONMENT = 55,
   NODE_FRESNEL = 38,
   NODE_LAYER_WEIGHT = 39
 };

@@ -142,11 +142,25 @@ class HIPDevice:
             if name not in ELEMENT_BYTES:
                 raise KeyError(name)
             self.global_alloc(name, arr)
+        for slot, im in enumerate(ds.textures):
+            self.tex_alloc(slot, im)
         self.const_copy_to("__data", ds.data)
         self.load_kernels()
         if ds.info.get("background_map"):
             self.update_background_map(ds)
         self.scene = ds
+
+    def tex_alloc(self, slot: int, image) -> None:
+        """ImageManager::device_load_image -> Device::tex_alloc
+        (device_cuda_impl.cpp:1105-1304): texels to device memory, slot's
+        TextureInfo in the device's __texture_info table."""
+        from . import nodes
+
+        a = image.texel_array()
+        self._check(self.lib.hipcy_tex_alloc(self.h, slot, nodes.IMAGE_DATA_TYPES.index(image.data_type),
+                                             nodes.INTERPOLATIONS.index(image.interpolation),
+                                             nodes.EXTENSIONS.index(image.extension), a.shape[1], a.shape[0],
+                                             a.ctypes.data, a.nbytes))
 
     def update_background_map(self, ds: DeviceScene) -> None:
         """LightManager::device_update_background (light.cpp:568-716): the world

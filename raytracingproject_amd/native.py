@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # by `python -m raytracingproject_amd.build --variant NAME -D...`)
 DEVICE_LIB = os.environ.get("HIPCY_DEVICE_LIB") or os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
-ABI_VERSION = 3  # HIPCY_ABI_VERSION in include/hipcycles.h
+ABI_VERSION = 4  # HIPCY_ABI_VERSION in include/hipcycles.h
 
 
 def device_lib_path() -> str:
@@ -87,6 +87,9 @@ DEVICE_SYMBOLS = {
     "hipcy_mem_zero": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t]),
     "hipcy_const_copy_to": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t]),
     "hipcy_bind_global": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_size_t]),
+    "hipcy_tex_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]),
+    "hipcy_tex_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_load_kernels": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_bvh_layout_mask": (ctypes.c_uint32, [ctypes.c_void_p]),
     "hipcy_path_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile)]),

@@ -181,6 +181,63 @@ def checker(vector, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), scale=5.0) -
     return Node("checker", {"Vector": vector, "Color1": color1, "Color2": color2, "Scale": scale})
 
 
+IMAGE_DATA_TYPES = ("float4", "byte4", "half4", "float", "byte", "half", "ushort4", "ushort")
+INTERPOLATIONS = ("linear", "closest", "cubic", "smart")
+EXTENSIONS = ("repeat", "extend", "clip")
+IMAGE_PROJECTIONS = {"flat": 0, "sphere": 2, "tube": 3}
+ENVIRONMENT_PROJECTIONS = {"equirectangular": 0, "mirror_ball": 1}
+NODE_TEX_IMAGE, NODE_TEX_ENVIRONMENT = 23, 55
+NODE_IMAGE_COMPRESS_AS_SRGB, NODE_IMAGE_ALPHA_UNASSOCIATE = 1, 2
+
+
+@dataclass(eq=False)
+class Image:
+    """One image of the ImageManager (render/image.cpp): texels in one of the
+    ImageDataTypes (util_texture.h:51-62), uploaded to an SVM image slot by
+    the device's tex_alloc.  `pixels` is (H, W, C) with C = 4 for the
+    *4 types and 1 (or 2-D) for the single-channel ones; row 0 is v = 0.
+    `tiles` maps UDIM tile numbers (1001, 1002, ...) to Images for a tiled
+    image; then `pixels` is unused."""
+    pixels: object = None
+    data_type: str = "byte4"
+    interpolation: str = "linear"
+    extension: str = "repeat"
+    compress_as_srgb: bool = False  # byte images stored in sRGB (ImageMetaData)
+    tiles: dict | None = None
+
+    def texel_array(self) -> np.ndarray:
+        dt = {"float4": np.float32, "float": np.float32, "byte4": np.uint8, "byte": np.uint8,
+              "half4": np.uint16, "half": np.uint16, "ushort4": np.uint16, "ushort": np.uint16}[self.data_type]
+        a = np.ascontiguousarray(self.pixels, dtype=dt)
+        ch = 4 if self.data_type.endswith("4") else 1
+        if a.ndim == 2 and ch == 1:
+            a = a[:, :, None]
+        if a.ndim != 3 or a.shape[2] != ch:
+            raise ValueError(f"{self.data_type} image needs shape (H, W, {ch}), got {a.shape}")
+        return a
+
+
+def image_texture(image: Image, vector, projection: str = "flat", alpha_unassociate: bool = False) -> Node:
+    """Image Texture node (nodes.cpp ImageTextureNode, svm_image.h:43-112).
+    The vector input must be linked (the reference's default is the UV map
+    attribute, which this host does not emit); box projection is not
+    implemented.  alpha_unassociate sets NODE_IMAGE_ALPHA_UNASSOCIATE (the
+    reference sets it when the Alpha output is used on a non-data image)."""
+    if not is_linked(vector):
+        raise ValueError("image_texture: link the vector input (UV attributes are not emitted)")
+    return Node("image_texture", {"Vector": vector},
+                params={"image": image, "projection": IMAGE_PROJECTIONS[projection],
+                        "alpha_unassociate": alpha_unassociate})
+
+
+def environment_texture(image: Image, vector, projection: str = "equirectangular") -> Node:
+    """Environment Texture node (nodes.cpp EnvironmentTextureNode,
+    svm_image.h:218-245); in a world shader geometry()["Position"] is the ray
+    direction."""
+    return Node("environment_texture", {"Vector": vector},
+                params={"image": image, "projection": ENVIRONMENT_PROJECTIONS[projection]})
+
+
 def gradient(vector, kind: str = "linear") -> Node:
     if kind not in GRADIENT_TYPES:
         raise ValueError(f"unknown gradient type {kind!r}")
@@ -272,7 +329,7 @@ def _outputs(node: Node) -> dict:
         return {"H": "float", "S": "float", "V": "float"}
     if k in ("clamp", "map_range"):
         return {"Result": "float"}
-    if k == "rgb_ramp":
+    if k in ("rgb_ramp", "image_texture", "environment_texture"):
         return {"Color": "color", "Alpha": "float"}
     raise ValueError(f"unknown node kind {k!r}")
 
@@ -297,6 +354,8 @@ _INPUT_TYPES = {
     "map_range": {"Value": "float", "From Min": "float", "From Max": "float", "To Min": "float",
                   "To Max": "float", "Steps": "float"},
     "rgb_ramp": {"Fac": "float"},
+    "image_texture": {"Vector": "vector"},
+    "environment_texture": {"Vector": "vector"},
 }
 
 
@@ -306,7 +365,7 @@ def _width(t: str) -> int:
 
 # ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
 # the shading point or direction (texture coordinate, geometry, textures)
-SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient")
+SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture")
 
 
 def has_spatial_varying(values) -> bool:
@@ -347,7 +406,8 @@ class NodeCompiler:
     conversions materialised for one node's inputs right after that node;
     outputs feeding the closures (`roots`) stay live."""
 
-    def __init__(self, alloc, emit, roots=(), free=None):
+    def __init__(self, alloc, emit, roots=(), free=None, images=None):
+        self.images = images if images is not None else []  # SVM image slots (shared per scene)
         self.alloc = alloc
         self.free = free or (lambda off, n: None)
         self.emit = emit
@@ -536,6 +596,45 @@ class NodeCompiler:
         sval = 0.0 if is_linked(n.inputs["Scale"]) else float(n.inputs["Scale"])
         self.emit((NODE_TEX_CHECKER, uchar4(vec, c1, c2, scale),
                    uchar4(self.out(n, "Color"), self.out(n, "Fac")), f32bits(sval)))
+
+    def image_slot(self, image: Image) -> int:
+        """ImageManager::add_image: one slot per distinct image."""
+        for i, im in enumerate(self.images):
+            if im is image:
+                return i
+        self.images.append(image)
+        return len(self.images) - 1
+
+    def _image_flags(self, n, image: Image) -> int:
+        flags = NODE_IMAGE_COMPRESS_AS_SRGB if image.compress_as_srgb else 0
+        if n.params.get("alpha_unassociate"):
+            flags |= NODE_IMAGE_ALPHA_UNASSOCIATE
+        return flags
+
+    def _n_image_texture(self, n):  # nodes.cpp:359-426 ImageTextureNode::compile (identity mapping)
+        image = n.params["image"]
+        vec = self.inp(n, "Vector")
+        flags = self._image_flags(n, image)
+        col, alpha = self.out(n, "Color"), self.out(n, "Alpha")
+        if image.tiles:
+            tiles = sorted(image.tiles)
+            slots = [self.image_slot(image.tiles[t]) for t in tiles]
+            num_nodes = -(-len(tiles) // 2)
+            self.emit((NODE_TEX_IMAGE, num_nodes, uchar4(vec, col, alpha, flags), n.params["projection"]))
+            for i in range(num_nodes):
+                a = (tiles[2 * i], slots[2 * i])
+                b = (tiles[2 * i + 1], slots[2 * i + 1]) if 2 * i + 1 < len(tiles) else (-1, -1)
+                self.emit(tuple(int(x) & 0xFFFFFFFF for x in (*a, *b)))
+        else:
+            slot = self.image_slot(image)
+            self.emit((NODE_TEX_IMAGE, (-slot) & 0xFFFFFFFF, uchar4(vec, col, alpha, flags), n.params["projection"]))
+
+    def _n_environment_texture(self, n):  # nodes.cpp EnvironmentTextureNode::compile
+        image = n.params["image"]
+        vec = self.inp(n, "Vector")
+        flags = self._image_flags(n, image)
+        self.emit((NODE_TEX_ENVIRONMENT, self.image_slot(image),
+                   uchar4(vec, self.out(n, "Color"), self.out(n, "Alpha"), flags), n.params["projection"]))
 
     def _n_gradient(self, n):  # nodes.cpp GradientTextureNode::compile
         vec = self.inp(n, "Vector")

@@ -289,6 +289,7 @@ class SVMCompiler:
     (the reference host compiler is render/svm.cpp + nodes.cpp compile())."""
 
     def __init__(self):
+        self.images: list = []  # SVM image slots, shared by every shader of the scene
         self.nodes: list[tuple[int, int, int, int]] = []
         self.stack_top = 0
         self.stack_used = [False] * SVM_STACK_SIZE
@@ -443,7 +444,8 @@ class SVMCompiler:
             start = len(self.nodes)
             self.nodes[i] = (NODE_SHADER_JUMP, start, 0, 0)
             socks = sh.sockets()
-            self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [v for v, _ in socks], self.free)
+            self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [v for v, _ in socks], self.free,
+                                         images=self.images)
             for v, t in socks:
                 self.nc.link(v, t)
             self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
@@ -571,10 +573,29 @@ class DeviceScene:
     height: int
     samples: int
     info: dict = field(default_factory=dict)
+    # SVM image slots (ImageManager): slot i holds textures[i] (nodes.Image)
+    textures: list = field(default_factory=list)
 
     @property
     def pass_stride(self) -> int:
         return self.data.film.pass_stride
+
+    def texture_info(self) -> tuple[np.ndarray, list]:
+        """__texture_info for a host consumer (the reference CPU kernel, the
+        host emulator): util_texture.h TextureInfo records (96 bytes) whose
+        `data` are host addresses of the texel arrays; returns the array and
+        the texel arrays, which must stay alive while it is bound."""
+        info = np.zeros((len(self.textures), 24), dtype=np.uint32)
+        keep = []
+        for i, im in enumerate(self.textures):
+            a = im.texel_array()
+            keep.append(a)
+            info[i, 0:2] = np.array([a.ctypes.data], dtype=np.uint64).view(np.uint32)
+            info[i, 2] = _nodes.IMAGE_DATA_TYPES.index(im.data_type)
+            info[i, 4] = _nodes.INTERPOLATIONS.index(im.interpolation)
+            info[i, 5] = _nodes.EXTENSIONS.index(im.extension)
+            info[i, 6], info[i, 7], info[i, 8] = a.shape[1], a.shape[0], 1
+        return info.view(np.uint8).reshape(-1), keep
 
 
 # ---------------------------------------------------------------------------
@@ -809,7 +830,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
         lamp_shader = len(mats)
         mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
     world = background(scene.world_color, scene.world_strength)
-    svm = SVMCompiler().compile(mats, world)
+    svm_compiler = SVMCompiler()
+    svm = svm_compiler.compile(mats, world)
     n_shaders = len(mats) + 1
     kshaders = (abi.KernelShader * n_shaders)()
     any_transparent_shadow = False
@@ -1069,7 +1091,9 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "name": scene.name,
         "background_map": bg_map,
     }
-    return DeviceScene(kd, arrays, scene.width, scene.height, scene.samples, info)
+    info["textures"] = len(svm_compiler.images)
+    return DeviceScene(kd, arrays, scene.width, scene.height, scene.samples, info,
+                       textures=list(svm_compiler.images))
 
 
 def transform_point_f32(tfm, p) -> np.ndarray:
@@ -1408,5 +1432,6 @@ ELEMENT_BYTES = {
     "__light_distribution": ctypes.sizeof(abi.KernelLightDistribution),
     "__lights": ctypes.sizeof(abi.KernelLight), "__svm_nodes": 16,
     "__shaders": ctypes.sizeof(abi.KernelShader), "__lookup_table": 4, "__sample_pattern_lut": 4,
+    "__texture_info": 96,
     "__light_background_marginal_cdf": 8, "__light_background_conditional_cdf": 8,
 }

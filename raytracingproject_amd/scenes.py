@@ -762,3 +762,73 @@ def closures_principled(width=48, height=48, samples=8) -> sc.Scene:
                       ior=1.5, transmission=0.3),
     ]
     return _closure_gallery(width, height, samples, "closures_principled", mats)
+
+
+def _test_image(seed, h, w, data_type, **kw):
+    """A deterministic synthetic image (no image files are available): smooth
+    gradients plus noise, in the texel type's range."""
+    from . import nodes as nd
+
+    rng = np.random.default_rng(seed)
+    ch = 4 if data_type.endswith("4") else 1
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    base = np.stack([(xx / max(w - 1, 1)), (yy / max(h - 1, 1)), 0.5 + 0.5 * np.sin(xx * 0.7 + yy * 0.4),
+                     0.2 + 0.8 * rng.random((h, w))], axis=2)[:, :, :ch]
+    base = np.clip(base + 0.15 * rng.standard_normal(base.shape), 0.0, 1.0)
+    if data_type in ("byte4", "byte"):
+        px = np.round(base * 255).astype(np.uint8)
+    elif data_type in ("ushort4", "ushort"):
+        px = np.round(base * 65535).astype(np.uint16)
+    elif data_type in ("half4", "half"):
+        px = (base * 2.5).astype(np.float16).view(np.uint16)
+    else:
+        px = (base * np.array([3.0, 1.5, 0.8, 1.0])[:ch]).astype(np.float32)
+    return nd.Image(px, data_type, **kw)
+
+
+def shading_image(width=48, height=48, samples=8) -> sc.Scene:
+    """Image and environment texture nodes (kernel_cpu_image.h, svm_image.h):
+    every ImageDataType, closest / linear / cubic / smart interpolation,
+    repeat / extend / clip, flat / sphere / tube projections, UDIM tiles,
+    sRGB-compressed bytes, alpha unassociation, a mirror-ball environment
+    lookup on a surface and an equirectangular HDR world (also the world
+    light's importance map)."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    uv = nd.separate_xyz(g["Parametric"])
+
+    def uvw(su=1.0, sv=1.0, ou=0.0, ov=0.0):
+        return nd.mapping(nd.combine_xyz(uv["X"], uv["Y"], 0.0), location=(ou, ov, 0.0), scale=(su, sv, 1.0))
+
+    colors = []
+    im = _test_image(1, 23, 37, "byte4", interpolation="linear", extension="repeat", compress_as_srgb=True)
+    colors.append(nd.image_texture(im, uvw(2.3, 1.7, -0.4, -0.3))["Color"])
+    im = _test_image(2, 16, 16, "float4", interpolation="cubic", extension="extend")
+    colors.append(nd.image_texture(im, uvw(1.4, 1.4, -0.2, -0.2))["Color"])
+    im = _test_image(3, 12, 20, "byte", interpolation="closest", extension="clip")
+    colors.append(nd.image_texture(im, uvw(1.3, 1.2, -0.1, -0.1))["Color"])
+    im = _test_image(4, 9, 13, "half4", interpolation="linear", extension="repeat")
+    tex = nd.image_texture(im, uvw(1.9, 1.1), alpha_unassociate=True)
+    colors.append(nd.mix_rgb("mix", tex["Alpha"], (0.1, 0.1, 0.1), tex["Color"]))
+    im = _test_image(5, 7, 9, "float", interpolation="smart", extension="repeat")
+    colors.append(nd.image_texture(im, nd.combine_xyz(uv["X"], uv["Y"], nd.math("multiply", uv["X"], 0.7)),
+                                   projection="tube")["Color"])
+    im = _test_image(6, 8, 8, "ushort4", interpolation="closest", extension="extend")
+    colors.append(nd.image_texture(im, nd.combine_xyz(uv["X"], uv["Y"], 0.3), projection="sphere")["Color"])
+    im = _test_image(7, 6, 6, "ushort", interpolation="linear", extension="clip")
+    colors.append(nd.image_texture(im, uvw(1.2, 1.2, -0.1, -0.1))["Color"])
+    im = _test_image(8, 10, 10, "half", interpolation="cubic", extension="clip")
+    colors.append(nd.image_texture(im, uvw(1.3, 1.3, -0.15, -0.15))["Color"])
+    udim = nd.Image(tiles={1001: _test_image(9, 8, 8, "byte4", interpolation="closest"),
+                           1002: _test_image(10, 8, 8, "float4", interpolation="linear"),
+                           1011: _test_image(11, 8, 8, "byte4", interpolation="linear")})
+    colors.append(nd.image_texture(udim, uvw(2.0, 1.6))["Color"])
+    env_small = _test_image(12, 8, 16, "float4", interpolation="linear")
+    colors.append(nd.environment_texture(env_small, g["Normal"], projection="mirror_ball")["Color"])
+    s = _grid_scene(colors, width, height, samples, "shading_image", glossy_every=4)
+    hdr = _test_image(13, 16, 32, "float4", interpolation="linear")
+    s.world_color = nd.environment_texture(hdr, g["Position"])["Color"]
+    s.world_strength = 1.0
+    s.world_map_resolution = 32
+    return s

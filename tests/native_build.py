@@ -65,6 +65,11 @@ class EmuScene:
         self.lib, self.ds = lib, ds
         self.names = list(ds.arrays)
         self.arrs = [np.ascontiguousarray(ds.arrays[n]) for n in self.names]
+        self.texels = []
+        if ds.textures:
+            info, self.texels = ds.texture_info()
+            self.names.append("__texture_info")
+            self.arrs.append(info)
         self.c_names = (ctypes.c_char_p * len(self.names))(*[n.encode() for n in self.names])
         self.c_ptrs = (ctypes.c_void_p * len(self.names))(*[a.ctypes.data for a in self.arrs])
         self.data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))

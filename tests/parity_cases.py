@@ -39,6 +39,8 @@ CASES = {
     "closures_diffuse": lambda: scenes.closures_diffuse(48, 48, 8),
     "closures_microfacet": lambda: scenes.closures_microfacet(48, 48, 8),
     "closures_principled": lambda: scenes.closures_principled(48, 48, 8),
+    # image / environment textures (kernel_cpu_image.h, svm_image.h)
+    "shading_image": lambda: scenes.shading_image(48, 48, 8),
 }
 
 
@@ -111,6 +113,9 @@ def scene_digest(ds: sc.DeviceScene) -> str:
     for k in sorted(ds.arrays):
         h.update(k.encode())
         h.update(np.ascontiguousarray(ds.arrays[k]).tobytes())
+    for i, im in enumerate(ds.textures):
+        h.update(f"texture {i} {im.data_type} {im.interpolation} {im.extension}".encode())
+        h.update(im.texel_array().tobytes())
     return h.hexdigest()
 
 

@@ -26,13 +26,14 @@ def test_device_logic_bit_exact_vs_reference(emu, name):
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32))
 
 
-@pytest.mark.parametrize("name", ["cornell_64", "closures_diffuse", "closures_microfacet", "closures_principled"])
+@pytest.mark.parametrize("name", ["cornell_64", "closures_diffuse", "closures_microfacet", "closures_principled",
+                                  "shading_image"])
 def test_device_sincos_restatement_matches_on_host(name):
     """Same render with the device's own libm restatements (sinf/cosf, expf,
     logf, powf, acosf) instead of the host libm: still bit-exact."""
     lib = nb.host_emu(libm_sincos=False)
-    ds = compile_case(name)
     g = load_golden(name)
+    ds = with_background_golden(compile_case(name), g)
     assert np.array_equal(emu_render(lib, ds).view(np.uint32), g["buffer"].view(np.uint32))
 
 
