@@ -78,8 +78,14 @@ class HIPCyclesDevice : public Device {
   /* device.h:484-488 */
   void mem_alloc(device_memory &mem) override
   {
-    if (mem.type == MEM_PIXELS || mem.type == MEM_TEXTURE) {
+    if (mem.type == MEM_PIXELS) {
       set_error(string_printf("HIP device: memory kind of %s is not supported", mem.name));
+      return;
+    }
+    if (mem.type == MEM_TEXTURE) {
+      /* CUDADevice::mem_alloc asserts here too: textures are created by
+       * mem_copy_to -> tex_alloc */
+      set_error(string_printf("HIP device: mem_alloc of texture %s (use mem_copy_to)", mem.name));
       return;
     }
     uint64_t ptr = 0;
@@ -91,8 +97,40 @@ class HIPCyclesDevice : public Device {
     }
   }
 
+  /* device_cuda_impl.cpp:1105-1304 tex_alloc: the device copies the texels and
+   * keeps TextureInfo[slot] in its own __texture_info table */
+  void tex_alloc(device_texture &mem)
+  {
+    if (mem.data_depth > 1) {
+      set_error(string_printf("HIP device: 3D texture %s is not supported", mem.name));
+      return;
+    }
+    if (check(hipcy_tex_alloc(dev_, (int)mem.slot, (int)mem.info.data_type, (int)mem.info.interpolation,
+                              (int)mem.info.extension, (int)mem.data_width, (int)std::max<size_t>(mem.data_height, 1),
+                              mem.host_pointer, mem.memory_size()))) {
+      mem.device_pointer = (device_ptr)(mem.slot + 1); /* a token: the device owns the texels */
+      mem.device_size = mem.memory_size();
+      stats.mem_alloc(mem.device_size);
+    }
+  }
+
+  void tex_free(device_texture &mem)
+  {
+    if (mem.device_pointer) {
+      hipcy_tex_free(dev_, (int)mem.slot);
+      stats.mem_free(mem.device_size);
+      mem.device_pointer = 0;
+      mem.device_size = 0;
+    }
+  }
+
   void mem_copy_to(device_memory &mem) override
   {
+    if (mem.type == MEM_TEXTURE) {
+      tex_free((device_texture &)mem);
+      tex_alloc((device_texture &)mem);
+      return;
+    }
     if (!mem.device_pointer) {
       mem_alloc(mem);
     }
@@ -133,6 +171,10 @@ class HIPCyclesDevice : public Device {
 
   void mem_free(device_memory &mem) override
   {
+    if (mem.type == MEM_TEXTURE) {
+      tex_free((device_texture &)mem);
+      return;
+    }
     if (mem.device_pointer) {
       if (mem.type == MEM_GLOBAL) {
         hipcy_bind_global(dev_, mem.name, 0, 0);
