@@ -50,6 +50,8 @@ def parse(argv=None):
     p.add_argument("--save", default=None, help="write the rank-0 film as PNG")
     p.add_argument("--bvh-width", type=int, default=4, choices=(2, 4, 8),
                    help="4 (default) / 8: device-widened wide BVH; 2: the bound BVH2 as is")
+    p.add_argument("--ray-sort", type=int, default=0, choices=(0, 3, 5),
+                   help="bin the closest queue by ray direction per bounce: 0 off, 3 octant, 5 octant x axis")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
     p.add_argument("--slots", type=int, default=0, help="path slots in flight (0: device default)")
     p.add_argument("--tile", type=int, default=64,
@@ -118,6 +120,7 @@ def main():
     dev = HIPDevice(device_index)
     dev.set_bvh_width(args.bvh_width)
     dev.set_bvh_leaf_merge(args.leaf_merge)
+    dev.set_ray_sort(args.ray_sort)
     dev.set_slots(args.slots)
     t0 = time.time()
     dev.upload_scene(ds)
@@ -293,6 +296,7 @@ def main():
                 "triangles": ds.info["triangles"],
                 "parallelism": f"rows interleaved over {world} GPU(s)",
                 "wavefront_iterations_per_frame": int(timing["iterations"]),
+                "ray_sort": args.ray_sort,
                 "scene_compile_s": round(t_compile, 2),
                 "scene_upload_s": round(t_upload, 3),
             },

@@ -135,6 +135,13 @@ int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims);
  * per-sample record buffer of one pass (default 4 GiB; a tile whose samples do
  * not fit is rendered in several sample passes).  0 keeps a value. */
 int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);
+/* Wavefront ray sorting (north_star; the reference's precedent is the split
+ * kernel's kernel/split/kernel_shader_sort.h): before every bounce iteration
+ * the closest-hit queue is binned by a key of the ray direction, so the rays
+ * of a wave descend the same BVH subtrees.  mode 0 = off, 3 = octant of D
+ * (8 bins), 5 = octant x major axis (24 of 32 bins).  Results never depend on
+ * the order (every path is a function of its work item alone). */
+int hipcy_set_ray_sort(hipcy_device *dev, int mode);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

@@ -238,6 +238,98 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow_transparent(CyGlo
   queue_push(queue_out, count_out, slot, regen, claim);
 }
 
+/* ---------------------------------------------------------------------------
+ * Closest-queue sorting (hipcy_set_ray_sort).  A counting sort of the queue by
+ * a direction bin, in three launches on the lane's stream: per-block bin
+ * histograms (LDS atomics, no device-scope atomics), one exclusive scan of the
+ * bin-major histogram, and the scatter.  Within a bin the slots keep their
+ * block order up to the order of LDS atomics inside a block, so the rays of
+ * neighbouring pixels stay together and share their octant. */
+#define CY_SORT_BINS 32
+
+template<int MODE> __device__ __forceinline__ uint ray_sort_key(const hc_float4 d)
+{
+  const uint oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
+                   ((__float_as_uint(d.z) >> 31) << 2);
+  if (MODE == 3) {
+    return oct;
+  }
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  const uint major = (ax >= ay && ax >= az) ? 0u : (ay >= az ? 1u : 2u);
+  return oct * 4u + major;
+}
+
+template<int MODE>
+__global__ void __launch_bounds__(CY_BLOCK) k_sort_count(CyPathBuffers b, const int *queue, const uint *count,
+                                                         unsigned char *keys, uint *hist, int nblocks)
+{
+  constexpr int K = MODE == 3 ? 8 : CY_SORT_BINS;
+  __shared__ uint h[K];
+  if (threadIdx.x < K) {
+    h[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int)*count) {
+    const uint key = ray_sort_key<MODE>(b.ray_D[queue[i]]);
+    keys[i] = (unsigned char)key;
+    atomicAdd(&h[key], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  }
+}
+
+/* Exclusive scan of m histogram entries in place, one workgroup (m is at most
+ * bins x blocks of a lane, a few hundred thousand words). */
+__global__ void __launch_bounds__(1024) k_sort_scan(uint *hist, int m)
+{
+  __shared__ uint part[1024];
+  const int t = threadIdx.x;
+  const int per = (m + 1023) / 1024;
+  const int b0 = min(m, t * per), b1 = min(m, b0 + per);
+  uint s = 0;
+  for (int j = b0; j < b1; j++) {
+    s += hist[j];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const uint v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint run = t ? part[t - 1] : 0u;
+  for (int j = b0; j < b1; j++) {
+    const uint c = hist[j];
+    hist[j] = run;
+    run += c;
+  }
+}
+
+template<int MODE>
+__global__ void __launch_bounds__(CY_BLOCK) k_sort_scatter(const int *queue, const uint *count,
+                                                           const unsigned char *keys, const uint *offs,
+                                                           int nblocks, int *out)
+{
+  constexpr int K = MODE == 3 ? 8 : CY_SORT_BINS;
+  __shared__ uint base[K];
+  __shared__ uint h[K];
+  if (threadIdx.x < K) {
+    base[threadIdx.x] = offs[threadIdx.x * nblocks + blockIdx.x];
+    h[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int)*count) {
+    const uint key = keys[i];
+    const uint r = atomicAdd(&h[key], 1u);
+    out[base[key] + r] = queue[i];
+  }
+}
+
 template<int W>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
@@ -499,6 +591,14 @@ struct hipcy_device {
   hipStream_t lane_stream[CY_LANES] = {};
   CyStats *stats_dev = nullptr;
   uint *host_counters = nullptr; /* pinned */
+
+  /* closest-queue sorting (hipcy_set_ray_sort): sorted queue, per-ray bin and
+   * the per-lane bin x block histogram / scanned offsets */
+  int ray_sort = 0;
+  int *sort_queue = nullptr;
+  unsigned char *sort_key = nullptr;
+  uint *sort_hist = nullptr;
+  size_t sort_capacity = 0;
 
   int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
 
@@ -810,6 +910,9 @@ void hipcy_destroy(hipcy_device *dev)
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
+  if (dev->sort_queue) hipFree(dev->sort_queue);
+  if (dev->sort_key) hipFree(dev->sort_key);
+  if (dev->sort_hist) hipFree(dev->sort_hist);
   if (dev->counters) hipFree(dev->counters);
   if (dev->stats_dev) hipFree(dev->stats_dev);
   if (dev->data_dev) hipFree(dev->data_dev);
@@ -1058,6 +1161,15 @@ int hipcy_set_bvh_width(hipcy_device *dev, int width)
     dev->bvhw_dirty = true;
   }
   dev->bvh_width = width;
+  return 0;
+}
+
+int hipcy_set_ray_sort(hipcy_device *dev, int mode)
+{
+  if (mode != 0 && mode != 3 && mode != 5) {
+    return set_error(dev, "set_ray_sort: mode must be 0, 3 or 5");
+  }
+  dev->ray_sort = mode;
   return 0;
 }
 
@@ -1393,6 +1505,7 @@ struct EvQuad {
 /* One partition of the slot pool with its own stream, queues and counters. */
 struct PassLane {
   hipStream_t s;
+  int index;
   int slot_base;
   int cam_n; /* > 0 until the lane's camera launch is enqueued */
   uint *cnt;  /* device: [0..2] queue counts, [4] next item */
@@ -1423,6 +1536,22 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   HIP_CHECK(dev, hipMemsetAsync(ln.cnt + qb, 0, 4, s));
   HIP_CHECK(dev, hipMemsetAsync(ln.cnt + qs, 0, 4, s));
   dim3 grid((ln.n_active + CY_BLOCK - 1) / CY_BLOCK), block(CY_BLOCK);
+  /* bounce iterations: bin the closest queue by ray direction (counting sort
+   * into sort_queue); closest and shade then read the sorted queue */
+  const int *queue_in = ln.q[qa];
+  if (dev->ray_sort && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
+    const int nblocks = (int)grid.x;
+    const int K = dev->ray_sort == 3 ? 8 : CY_SORT_BINS;
+    uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
+    unsigned char *keys = dev->sort_key + ln.slot_base;
+    int *sorted = dev->sort_queue + ln.slot_base;
+    hipLaunchKernelGGL(dev->ray_sort == 3 ? k_sort_count<3> : k_sort_count<5>, grid, block, 0, s, dev->bufs,
+                       ln.q[qa], ln.cnt + qa, keys, hist, nblocks);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, K * nblocks);
+    hipLaunchKernelGGL(dev->ray_sort == 3 ? k_sort_scatter<3> : k_sort_scatter<5>, grid, block, 0, s, ln.q[qa],
+                       ln.cnt + qa, keys, hist, nblocks, sorted);
+    queue_in = sorted;
+  }
   EvQuad p;
   if (prof) {
     p.a = get_event(dev, (*ev)++);
@@ -1433,14 +1562,14 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   }
   {
     auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0);
-    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, ln.q[qa],
+    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, queue_in,
                        ln.cnt + qa, err, dev->stats_dev);
   }
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));
   }
   cy_launch_shade(dev->data_host.integrator.max_closures, dev->shade_tex, grid, block, s, kg, dev->bufs, ln.tile, cam_n,
-                  ln.slot_base, ln.q[qa], ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
+                  ln.slot_base, queue_in, ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }
@@ -1476,12 +1605,29 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
   const int max_lanes = (dev->profiling & 1) ? 1 : CY_LANES;
   const int lanes = (int)std::max<size_t>(1, std::min<size_t>(max_lanes, n_slots / (4 * CY_BLOCK)));
   tile.samples_out = dev->records;
+  if (dev->ray_sort && dev->sort_capacity < dev->capacity) {
+    const size_t cap = dev->capacity;
+    if (dev->sort_queue) HIP_CHECK(dev, hipFree(dev->sort_queue));
+    if (dev->sort_key) HIP_CHECK(dev, hipFree(dev->sort_key));
+    if (dev->sort_hist) HIP_CHECK(dev, hipFree(dev->sort_hist));
+    dev->sort_queue = nullptr;
+    dev->sort_key = nullptr;
+    dev->sort_hist = nullptr;
+    dev->sort_capacity = 0;
+    HIP_CHECK(dev, hipMalloc((void **)&dev->sort_queue, cap * sizeof(int)));
+    HIP_CHECK(dev, hipMalloc((void **)&dev->sort_key, cap));
+    /* lane l's histogram starts at CY_SORT_BINS * (slot_base / CY_BLOCK + l) */
+    HIP_CHECK(dev, hipMalloc((void **)&dev->sort_hist,
+                             (size_t)CY_SORT_BINS * (cap / CY_BLOCK + CY_LANES + 1) * sizeof(uint)));
+    dev->sort_capacity = cap;
+  }
   PassLane ln[CY_LANES];
   /* the main stream's pending work (buffer zeroing, uploads) precedes the lanes */
   hipEvent_t start = get_event(dev, (*ev)++);
   HIP_CHECK(dev, hipEventRecord(start, dev->stream));
   for (int l = 0; l < lanes; l++) {
     PassLane &L = ln[l];
+    L.index = l;
     L.s = dev->lane_stream[l];
     HIP_CHECK(dev, hipStreamWaitEvent(L.s, start, 0));
     L.slot_base = (int)(n_slots * l / lanes);

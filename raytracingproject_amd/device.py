@@ -123,6 +123,11 @@ class HIPDevice:
         """4 (default) / 8: traverse the device-widened wide BVH; 2: the bound BVH2."""
         self._check(self.lib.hipcy_set_bvh_width(self.h, int(width)))
 
+    def set_ray_sort(self, mode: int) -> None:
+        """Bin the closest-hit queue by ray direction before every bounce
+        iteration: 0 off, 3 octant, 5 octant x major axis (hipcy_set_ray_sort)."""
+        self._check(self.lib.hipcy_set_ray_sort(self.h, int(mode)))
+
     def set_slots(self, slots: int = 0, record_bytes: int = 0) -> None:
         """Path slots in flight and the per-pass sample-record budget (0 keeps a value)."""
         self._check(self.lib.hipcy_set_slots(self.h, int(slots), int(record_bytes)))

@@ -35,6 +35,11 @@ if [[ $MODE == quick ]]; then
   step bench_w8 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bvh-width 8
   step bench_w2 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bvh-width 2
 fi
+if [[ $MODE == all || $MODE == sort ]]; then
+  for m in 3 5; do
+    step bench_sort$m 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --tile 0 --ray-sort $m
+  done
+fi
 if [[ $MODE == all || $MODE == prof ]]; then
   step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 fi
