@@ -62,6 +62,7 @@ def _bind_ref(lib):
     lib.cref_const_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
     lib.cref_global_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
     lib.cref_render.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci, ci]
+    lib.cref_render_adaptive.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci]
     lib.cref_intersect.argtypes = [vp, ci, vp, vp, vp]
     lib.cref_film_convert.argtypes = [vp, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
     lib.cref_shader_eval.argtypes = [vp, vp, vp, ci, ci, ci, ci]
@@ -149,6 +150,17 @@ class RefKernel:
         # buffer covers the tile: offset = -(x + y*w), stride = w (device_cpu.cpp)
         self.lib.cref_render(self.h, buf.ctypes.data, start_sample, samples, x, y, w, h,
                              -(x + y * w), w, threads)
+        return buf
+
+    def render_adaptive(self, samples=None, start_sample=0, tile=None):
+        """Adaptive-sampling render of a tile (CPUDevice::render with the GPU's
+        per-step stopping, oracle/ref_harness.cpp cref_render_adaptive)."""
+        ds = self.dscene
+        samples = ds.samples if samples is None else samples
+        x, y, w, h = tile if tile is not None else (0, 0, ds.width, ds.height)
+        buf = np.zeros((h, w, ds.pass_stride), dtype=np.float32)
+        self.lib.cref_render_adaptive(self.h, buf.ctypes.data, start_sample, samples, x, y, w, h,
+                                      -(x + y * w), w)
         return buf
 
     def intersect(self, rays: np.ndarray):

@@ -160,6 +160,88 @@ void cref_render(void *h,
   }
 }
 
+/* Adaptive sampling render of one tile, single-threaded, as CPUDevice::render
+ * does it (device_cpu.cpp:886-950) with KernelIntegrator.adaptive_stop_per_sample
+ * = 0 (the GPU setting): after every sample the tile's pixels are path traced,
+ * at need_filter samples (device_task.cpp:184-192) adaptive_sampling_filter
+ * (device_cpu.cpp:832-864: stopping per pixel, then filter_x per row and
+ * filter_y per column), and at the end adaptive_sampling_post
+ * (device_cpu.cpp:866-885).  The reference functions are called as they lie
+ * in kernel_adaptive_sampling.h. */
+void cref_render_adaptive(void *h,
+                          float *buffer,
+                          int start_sample,
+                          int num_samples,
+                          int tx,
+                          int ty,
+                          int tw,
+                          int th,
+                          int offset,
+                          int stride)
+{
+  RefContext *ctx = (RefContext *)h;
+  KernelGlobals kgt = thread_globals(ctx->kg);
+  KernelGlobals *kg = &kgt;
+  const int end_sample = start_sample + num_samples;
+  const int min_samples = kernel_data.integrator.adaptive_min_samples;
+  const int step = kernel_data.integrator.adaptive_step;
+  const int ps = kernel_data.film.pass_stride;
+  int tile_sample = start_sample;
+  for (int sample = start_sample; sample < end_sample; sample++) {
+    for (int y = ty; y < ty + th; y++) {
+      for (int x = tx; x < tx + tw; x++) {
+        CREF_PATH_TRACE(kg, buffer, sample, x, y, offset, stride);
+      }
+    }
+    tile_sample = sample + 1;
+    if (sample > min_samples && (sample & (step - 1)) == (step - 1)) {
+      WorkTile wtile;
+      wtile.x = tx;
+      wtile.y = ty;
+      wtile.w = tw;
+      wtile.h = th;
+      wtile.offset = offset;
+      wtile.stride = stride;
+      wtile.buffer = buffer;
+      if (!kernel_data.integrator.adaptive_stop_per_sample) {
+        for (int y = ty; y < ty + th; y++) {
+          for (int x = tx; x < tx + tw; x++) {
+            kernel_do_adaptive_stopping(kg, buffer + (offset + x + y * stride) * ps, sample);
+          }
+        }
+      }
+      bool any = false;
+      for (int y = ty; y < ty + th; y++) {
+        any |= kernel_do_adaptive_filter_x(kg, y, &wtile);
+      }
+      for (int x = tx; x < tx + tw; x++) {
+        any |= kernel_do_adaptive_filter_y(kg, x, &wtile);
+      }
+      if (!any) {
+        tile_sample = end_sample;
+        break;
+      }
+    }
+  }
+  for (int y = ty; y < ty + th; y++) {
+    for (int x = tx; x < tx + tw; x++) {
+      float *b = buffer + (offset + x + y * stride) * ps;
+      const int sc = kernel_data.film.pass_sample_count;
+      if (b[sc] < 0.0f) {
+        b[sc] = -b[sc];
+        const float mul = tile_sample / max((float)start_sample + 1.0f, b[sc]);
+        if (mul != 1.0f) {
+          kernel_adaptive_post_adjust(kg, b, mul);
+        }
+      }
+      else {
+        kernel_adaptive_post_adjust(kg, b, tile_sample / (tile_sample - 1.0f));
+      }
+    }
+  }
+  thread_globals_free(kgt);
+}
+
 /* rays: n x 8 floats (P.xyz, D.xyz, t, visibility-as-uint-bits).
  * out_f: n x 3 (t, u, v); out_i: n x 4 (hit, prim, object, type). */
 void cref_intersect(void *h, int n, const float *rays, float *out_f, int *out_i)

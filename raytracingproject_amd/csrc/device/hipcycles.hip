@@ -239,6 +239,99 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow_transparent(CyGlo
 }
 
 /* ---------------------------------------------------------------------------
+ * Adaptive sampling (kernel_adaptive_sampling.h; launched per RenderTile as
+ * CUDADevice::adaptive_sampling_filter / _post, device_cuda_impl.cpp:1779-1851). */
+struct CyAdaptiveTile {
+  int x, y, w, h, offset, stride;
+  float *buffer;
+  int pass_stride, aux, sample_count;
+};
+
+__device__ __forceinline__ float *adaptive_pixel(const CyAdaptiveTile &t, int x, int y)
+{
+  return t.buffer + (size_t)(t.offset + x + y * t.stride) * t.pass_stride;
+}
+
+/* kernel_do_adaptive_stopping: per-pixel error of the full against the
+ * half-sample (aux) estimate; converged pixels get aux.w += 1. */
+__global__ void __launch_bounds__(CY_BLOCK) k_adaptive_stopping(CyAdaptiveTile t, int sample, float threshold)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.w * t.h) {
+    return;
+  }
+  float *buffer = adaptive_pixel(t, t.x + i % t.w, t.y + i / t.w);
+  const float ix = buffer[0], iy = buffer[1], iz = buffer[2];
+  const float *a = buffer + t.aux;
+  const float error = (fabsf(ix - a[0]) + fabsf(iy - a[1]) + fabsf(iz - a[2])) /
+                      ((float)sample * 0.0001f + sqrtf(ix + iy + iz));
+  if (error < threshold * (float)sample) {
+    buffer[t.aux + 3] += 1.0f;
+  }
+}
+
+/* kernel_do_adaptive_filter_x / _y: a pixel next to an unconverged one along
+ * the row (column) is marked unconverged too; one thread per row (column),
+ * walking it in order as the reference does. */
+template<bool ALONG_X> __global__ void __launch_bounds__(CY_BLOCK) k_adaptive_filter(CyAdaptiveTile t)
+{
+  const int line = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_lines = ALONG_X ? t.h : t.w;
+  if (line >= n_lines) {
+    return;
+  }
+  const int n = ALONG_X ? t.w : t.h;
+  bool prev = false;
+  for (int k = 0; k < n; k++) {
+    const int x = ALONG_X ? t.x + k : t.x + line;
+    const int y = ALONG_X ? t.y + line : t.y + k;
+    float *aux = adaptive_pixel(t, x, y) + t.aux;
+    if (aux[3] == 0.0f) {
+      if (k > 0 && !prev) {
+        float *prev_aux = adaptive_pixel(t, ALONG_X ? x - 1 : x, ALONG_X ? y : y - 1) + t.aux;
+        prev_aux[3] = 0.0f;
+      }
+      prev = true;
+    }
+    else {
+      if (prev) {
+        aux[3] = 0.0f;
+      }
+      prev = false;
+    }
+  }
+}
+
+/* kernel_cuda_adaptive_scale_samples + kernel_adaptive_post_adjust: pixels
+ * that stopped early are scaled as if they had taken every sample (combined
+ * and aux passes; the device supports no other scaled pass). */
+__global__ void __launch_bounds__(CY_BLOCK) k_adaptive_scale(CyAdaptiveTile t, int start_sample, int sample)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.w * t.h) {
+    return;
+  }
+  float *buffer = adaptive_pixel(t, t.x + i % t.w, t.y + i / t.w);
+  float mul;
+  float *sc = buffer + t.sample_count;
+  if (*sc < 0.0f) {
+    *sc = -*sc;
+    const float lo = (float)start_sample + 1.0f;
+    mul = (float)sample / (lo > *sc ? lo : *sc);
+    if (mul == 1.0f) {
+      return;
+    }
+  }
+  else {
+    mul = (float)sample / ((float)sample - 1.0f);
+  }
+  for (int c = 0; c < 4; c++) {
+    buffer[c] *= mul;
+    buffer[t.aux + c] *= mul;
+  }
+}
+
+/* ---------------------------------------------------------------------------
  * Closest-queue sorting (hipcy_set_ray_sort).  A counting sort of the queue by
  * a direction bin, in three launches on the lane's stream: per-block bin
  * histograms (LDS atomics, no device-scope atomics), one exclusive scan of the
@@ -1380,10 +1473,14 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.bvh.have_motion || d.bvh.have_curves) why = "motion / curves";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
   else if (d.film.use_light_pass) why = "light passes";
-  else if (d.film.pass_flag != 2) why = "only the combined pass";
-  else if (d.film.pass_denoising_data || d.film.pass_adaptive_aux_buffer || d.film.pass_sample_count ||
-           d.film.cryptomatte_passes)
-    why = "denoising / adaptive / cryptomatte passes";
+  else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | (1 << 13) | (1 << 14))) != 0 ||
+           d.film.pass_combined != 0)
+    why = "only the combined pass (+ adaptive aux buffer / sample count)";
+  else if (d.film.pass_denoising_data || d.film.cryptomatte_passes)
+    why = "denoising / cryptomatte passes";
+  else if (d.film.pass_adaptive_aux_buffer && (d.integrator.adaptive_step <= 0 ||
+                                              (d.integrator.adaptive_step & (d.integrator.adaptive_step - 1))))
+    why = "adaptive_step must be a power of two";
   else if (d.background.map_weight > 0.0f &&
            (d.background.map_res_x <= 0 || d.background.map_res_y <= 0 ||
             dev->globals.find("__light_background_marginal_cdf") == dev->globals.end() ||
@@ -1754,8 +1851,29 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     HIP_CHECK(dev, hipMemcpyAsync(dev->tile_descs, descs.data(), bytes, hipMemcpyHostToDevice, dev->stream));
   }
   /* samples per pass: as many as the record budget holds for these pixels */
-  const size_t per_pass = std::max<size_t>(
+  size_t per_pass = std::max<size_t>(
       1, std::min<size_t>((size_t)t->num_samples, dev->record_budget / (npix * sizeof(hc_float4))));
+  /* adaptive sampling: passes of adaptive_step samples (AdaptiveSampling::
+   * align_static_samples, device_task.cpp:147-163, of a step that size), so
+   * the stopping / filter kernels run at every need_filter sample, as the
+   * CPU device does them per sample */
+  const hc_KernelFilm &film = dev->data_host.film;
+  const hc_KernelIntegrator &integ = dev->data_host.integrator;
+  const bool adaptive = film.pass_adaptive_aux_buffer != 0;
+  if (adaptive) {
+    if (y_step != 1) {
+      return set_error(dev, "path_trace_rows: adaptive sampling needs whole tiles (shard by tiles)");
+    }
+    const size_t step = (size_t)integ.adaptive_step;
+    if (per_pass >= step) {
+      per_pass = step;
+    }
+    else {
+      while (step % per_pass != 0) {
+        per_pass--;
+      }
+    }
+  }
   if (npix * per_pass > 0xFFFFFFFFull) {
     return set_error(dev, "path_trace: tile too large for 32-bit work items");
   }
@@ -1801,12 +1919,41 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     tile.n_tiles = (int)descs.size();
     tile.descs = descs.size() > 1 ? dev->tile_descs : nullptr;
     tile.n_items = (uint)(npix * (size_t)(tile.end_sample - tile.start_sample));
+    tile.aux_offset = film.pass_adaptive_aux_buffer;
+    tile.sample_count_offset = film.pass_sample_count;
+    tile.write_aux = (film.pass_adaptive_aux_buffer && integ.adaptive_threshold > 0.0f) ? 1 : 0;
     if (path_trace_pass(dev, kg, tile, W, &ev, &quads) != 0) {
       return -1;
     }
     if (dev->host_counters[3]) {
       break;
     }
+    /* CUDADevice::render: filter_sample = sample + num_samples - 1, then
+     * AdaptiveSampling::need_filter (device_task.cpp:184-192) */
+    const int filter_sample = tile.end_sample - 1;
+    if (adaptive && filter_sample > integ.adaptive_min_samples &&
+        (filter_sample & (integ.adaptive_step - 1)) == (integ.adaptive_step - 1)) {
+      for (const CyTileDesc &d : descs) {
+        const CyAdaptiveTile at = {d.x, d.y, d.w, d.h, d.offset, d.stride, d.buffer,
+                                   tile.pass_stride, film.pass_adaptive_aux_buffer, film.pass_sample_count};
+        hipLaunchKernelGGL(k_adaptive_stopping, dim3((unsigned)((d.w * d.h + CY_BLOCK - 1) / CY_BLOCK)),
+                           dim3(CY_BLOCK), 0, s, at, filter_sample, integ.adaptive_threshold);
+        hipLaunchKernelGGL(k_adaptive_filter<true>, dim3((unsigned)((d.h + 63) / 64)), dim3(64), 0, s, at);
+        hipLaunchKernelGGL(k_adaptive_filter<false>, dim3((unsigned)((d.w + 63) / 64)), dim3(64), 0, s, at);
+      }
+      HIP_CHECK(dev, hipGetLastError());
+    }
+  }
+  /* CUDADevice::adaptive_sampling_post: rescale pixels that stopped early */
+  if (adaptive && film.pass_sample_count && !dev->host_counters[3]) {
+    const int end_sample = t->start_sample + t->num_samples;
+    for (const CyTileDesc &d : descs) {
+      const CyAdaptiveTile at = {d.x, d.y, d.w, d.h, d.offset, d.stride, d.buffer,
+                                 (int)film.pass_stride, film.pass_adaptive_aux_buffer, film.pass_sample_count};
+      hipLaunchKernelGGL(k_adaptive_scale, dim3((unsigned)((d.w * d.h + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK),
+                         0, s, at, t->start_sample, end_sample);
+    }
+    HIP_CHECK(dev, hipGetLastError());
   }
   hipEvent_t t_end = get_event(dev, ev++);
   HIP_CHECK(dev, hipEventRecord(t_end, s));

@@ -68,6 +68,11 @@ typedef struct CyTile {
   uint npix;              /* pixels of the pass (w * h for one tile) */
   int n_tiles;            /* > 1: the pass covers descs[0 .. n_tiles-1], pixels numbered tile by tile */
   const CyTileDesc *descs;
+  /* adaptive sampling: KernelFilm pass_adaptive_aux_buffer / pass_sample_count
+   * offsets (0 = pass absent) and pass_adaptive_aux_buffer && adaptive_threshold > 0 */
+  int aux_offset;
+  int sample_count_offset;
+  int write_aux;
 } CyTile;
 
 typedef struct CyStats {
@@ -367,11 +372,31 @@ CY_FN void item_pixel(const CyTile *tile, uint item, int *x, int *y, int *sample
   pass_pixel(tile, p, x, y);
 }
 
-/* kernel_path_trace_setup (kernel_path_common.h:21-46) for a work item. */
+/* Render-buffer pixel of pass pixel p (the tile's rows stored contiguously). */
+CY_FN float *pixel_buffer(const CyTile *tile, uint p)
+{
+  if (tile->n_tiles > 1) {
+    const CyTileDesc &d = tile->descs[tile_of_pixel(tile, p)];
+    const int local = (int)(p - d.px_begin);
+    return d.buffer + (size_t)(d.offset + d.x + local % d.w + (d.y + local / d.w) * d.stride) * tile->pass_stride;
+  }
+  const int x = tile->x + (int)(p % (uint)tile->w);
+  const int ybuf = tile->y + (int)(p / (uint)tile->w);
+  return tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
+}
+
+/* kernel_path_trace_setup (kernel_path_common.h:21-46) for a work item.  With
+ * adaptive sampling a pixel whose aux buffer marks it converged takes no
+ * sample (kernel_path.h:654-659): reported as no camera ray (t = 0). */
 CY_FN void item_camera_ray(const CyGlobals *kg, const CyTile *tile, uint item, uint *rng_hash, int *sample, CyRay *ray)
 {
   int x, y;
   item_pixel(tile, item, &x, &y, sample);
+  if (tile->aux_offset != 0 && pixel_buffer(tile, item % tile->npix)[tile->aux_offset + 3] > 0.0f) {
+    *rng_hash = 0;
+    ray->t = 0.0f;
+    return;
+  }
   camera_sample_ray(kg, x, y, *sample, rng_hash, ray);
 }
 
@@ -591,30 +616,61 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
 
 /* Add pixel p's sample records to the render buffer in sample order
  * (kernel_write_pass_float4, kernel_write_passes.h:49-65, once per sample).
- * The tile's rows are stored contiguously in its buffer. */
+ * With adaptive sampling every recorded sample also does what the rest of
+ * kernel_write_result does (kernel_passes.h:394-432): samples with
+ * sample_is_even (kernel_random.h:294-318; for Sobol `sample & 1`) add twice
+ * their radiance to the aux buffer, and the sample count pass is made
+ * negative and decremented.  The tile's rows are stored contiguously. */
 CY_FN void accumulate_pixel(const CyTile *tile, int p)
 {
   const int npix = (int)tile->npix;
-  float *buf;
-  if (tile->n_tiles > 1) {
-    const CyTileDesc &d = tile->descs[tile_of_pixel(tile, (uint)p)];
-    const int local = p - (int)d.px_begin;
-    buf = d.buffer + (size_t)(d.offset + d.x + local % d.w + (d.y + local / d.w) * d.stride) * tile->pass_stride;
-  }
-  else {
-    const int x = tile->x + p % tile->w;
-    const int ybuf = tile->y + p / tile->w;
-    buf = tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
-  }
+  float *buf = pixel_buffer(tile, (uint)p);
   float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
   const int n = tile->end_sample - tile->start_sample;
-  for (int k = 0; k < n; k++) {
-    const hc_float4 r = cy_ld(&tile->samples_out[(size_t)k * npix + p]);
-    if (r.w == r.w) {
-      b0 += r.x;
-      b1 += r.y;
-      b2 += r.z;
-      b3 += r.w;
+  if (tile->aux_offset == 0 && tile->sample_count_offset == 0) {
+    for (int k = 0; k < n; k++) {
+      const hc_float4 r = cy_ld(&tile->samples_out[(size_t)k * npix + p]);
+      if (r.w == r.w) {
+        b0 += r.x;
+        b1 += r.y;
+        b2 += r.z;
+        b3 += r.w;
+      }
+    }
+  }
+  else {
+    float *aux = buf + tile->aux_offset;
+    float a0 = aux[0], a1 = aux[1], a2 = aux[2], a3 = aux[3];
+    float sc = tile->sample_count_offset ? buf[tile->sample_count_offset] : 0.0f;
+    for (int k = 0; k < n; k++) {
+      const hc_float4 r = cy_ld(&tile->samples_out[(size_t)k * npix + p]);
+      if (r.w == r.w) {
+        b0 += r.x;
+        b1 += r.y;
+        b2 += r.z;
+        b3 += r.w;
+        if (tile->write_aux && ((tile->start_sample + k) & 1)) {
+          a0 += r.x * 2.0f;
+          a1 += r.y * 2.0f;
+          a2 += r.z * 2.0f;
+          a3 += 0.0f;
+        }
+        if (tile->sample_count_offset) {
+          if (sc > 0.0f) {
+            sc *= -1.0f;
+          }
+          sc += -1.0f;
+        }
+      }
+    }
+    if (tile->aux_offset) {
+      aux[0] = a0;
+      aux[1] = a1;
+      aux[2] = a2;
+      aux[3] = a3;
+    }
+    if (tile->sample_count_offset) {
+      buf[tile->sample_count_offset] = sc;
     }
   }
   buf[0] = b0;

@@ -563,6 +563,12 @@ class Scene:
     # (light.cpp:210-243 test_enabled_lights); map_resolution 0 = automatic
     world_mis: bool = True
     world_map_resolution: int = 0
+    # adaptive sampling (Film use_adaptive_sampling): the adaptive aux buffer and
+    # sample count passes after the combined pass (blender_sync.cpp:684-689);
+    # threshold / min samples 0 = automatic (integrator.cpp:186-207)
+    adaptive_sampling: bool = False
+    adaptive_threshold: float = 0.0
+    adaptive_min_samples: int = 0
 
 
 @dataclass
@@ -970,10 +976,18 @@ def compile_scene(scene: Scene) -> DeviceScene:
     ki.sample_all_lights_indirect = 0
     ki.sampling_pattern = 0
     ki.aa_samples = scene.samples
-    ki.adaptive_min_samples = max(4, int(math.sqrt(scene.samples)))
+    if scene.adaptive_min_samples == 0:
+        ki.adaptive_min_samples = max(4, int(math.sqrt(scene.samples)))
+    else:
+        ki.adaptive_min_samples = max(4, scene.adaptive_min_samples)
     ki.adaptive_step = 4
+    # GPU devices: info.has_adaptive_stop_per_sample = false (stopping runs per
+    # step in its own kernel, CUDADevice::adaptive_sampling_filter)
     ki.adaptive_stop_per_sample = 0
-    ki.adaptive_threshold = max(0.001, 1.0 / scene.samples)
+    if scene.adaptive_threshold == 0.0:
+        ki.adaptive_threshold = max(0.001, 1.0 / scene.samples)
+    else:
+        ki.adaptive_threshold = scene.adaptive_threshold
     ki.light_inv_rr_threshold = (1.0 / scene.light_sampling_threshold) if scene.light_sampling_threshold > 0 else 0.0
     ki.use_volumes = 0
     ki.max_closures = max([m.num_closures() for m in mats] + [1])
@@ -1024,6 +1038,14 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.display_divide_pass_stride = -1
     kf.use_display_exposure = 1 if kf.exposure != 1.0 else 0
     kf.use_display_pass_alpha = 1
+    if scene.adaptive_sampling:
+        # film.cpp:568-573 pass offsets, :621 stride aligned to 4 floats
+        kf.pass_adaptive_aux_buffer = 4
+        kf.pass_sample_count = 8
+        kf.pass_stride = 12
+        # film.cpp:447-450: 1 << type for PASS_ADAPTIVE_AUX_BUFFER (13) and
+        # PASS_SAMPLE_COUNT (14), kernel_types.h:354-376 without __KERNEL_DEBUG__
+        kf.pass_flag = PASSMASK_COMBINED | (1 << 13) | (1 << 14)
     lookup = filter_table(scene.filter_type, scene.filter_width)
     kd.tables.beckmann_offset = 0
     if any(t in BECKMANN_CLOSURES for m in mats for t in m.closure_types()):

@@ -124,6 +124,16 @@ def cornell_box(width=256, height=256, samples=32) -> sc.Scene:
                     world_strength=0.0, samples=samples, name="cornell_box")
 
 
+def cornell_adaptive(width=64, height=64, samples=64, threshold=0.02) -> sc.Scene:
+    """Cornell box with adaptive sampling (Film use_adaptive_sampling): the
+    walls converge and stop early, the penumbrae keep sampling."""
+    scene = cornell_box(width, height, samples)
+    scene.adaptive_sampling = True
+    scene.adaptive_threshold = threshold
+    scene.name = "cornell_adaptive"
+    return scene
+
+
 def cornell_lamps(width=64, height=64, samples=16) -> sc.Scene:
     """Cornell box lit by every lamp kind the device implements: a sphere point
     lamp, a spot lamp, a rectangular and a round area lamp, a sun, plus the

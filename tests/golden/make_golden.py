@@ -184,7 +184,10 @@ def main():
             rk.set_global("__light_background_marginal_cdf", marg)
             rk.set_global("__light_background_conditional_cdf", cond)
             bg = {"bg_map": bg_map, "bg_marg": marg, "bg_cond": cond}
-        buf = rk.render(threads=os.cpu_count())
+        if ds.data.film.pass_adaptive_aux_buffer:
+            buf = rk.render_adaptive()
+        else:
+            buf = rk.render(threads=os.cpu_count())
         rays = make_rays(ds, 4096)
         hit_f, hit_i = rk.intersect(rays)
         shadow = rays.copy()

@@ -41,8 +41,17 @@ CASES = {
     "closures_principled": lambda: scenes.closures_principled(48, 48, 8),
     # image / environment textures (kernel_cpu_image.h, svm_image.h)
     "shading_image": lambda: scenes.shading_image(48, 48, 8),
+    # adaptive sampling (kernel_adaptive_sampling.h): aux buffer + sample count
+    # passes, per-step stopping and the x/y dilation filters, final rescale
+    "cornell_adaptive": lambda: scenes.cornell_adaptive(64, 64, 64),
 }
 
+# Cases whose render needs the device's host-side step loop (adaptive sampling:
+# stopping / filter / rescale kernels between sample passes, hipcycles.hip
+# path_trace); the host emulation renders single passes, so these are checked
+# on the GPU only (test_gpu_parity).
+HOST_LOOP_CASES = {"cornell_adaptive"}
+EMU_CASES = [n for n in CASES if n not in HOST_LOOP_CASES]
 
 # BASELINE.json configs at their full size (scene, resolution, spp), checked on a
 # crop the reference kernel renders in seconds: name -> (scene, tile or None).

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import native_build as nb
-from parity_cases import CASES, compile_case, load_golden, with_background_golden
+from parity_cases import EMU_CASES, compile_case, load_golden, with_background_golden
 
 
 def emu_render(lib, ds, tile=None, start_sample=0, samples=None, offset=None, out=None, bvh_width=2):
@@ -18,7 +18,7 @@ def emu():
     return nb.host_emu(libm_sincos=True)
 
 
-@pytest.mark.parametrize("name", list(CASES))
+@pytest.mark.parametrize("name", list(EMU_CASES))
 def test_device_logic_bit_exact_vs_reference(emu, name):
     g = load_golden(name)
     ds = with_background_golden(compile_case(name), g)

@@ -268,6 +268,9 @@ extern "C" int emu_render(const void *data,
   tile.npix = (uint)(tw * th);
   tile.n_tiles = 1;
   tile.descs = nullptr;
+  tile.aux_offset = 0;
+  tile.sample_count_offset = 0;
+  tile.write_aux = 0;
   tile.y_step = 1;
   tile.start_sample = start_sample;
   tile.end_sample = start_sample + num_samples;
