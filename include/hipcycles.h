@@ -33,8 +33,10 @@
  *                                            the 4/8-wide BVH the device widens it into, like
  *                                            BVH::pack_nodes/widen_children_nodes bvh/bvh.cpp:149-176
  *   hipcy_shader_eval                        device_cuda_impl.cpp:2019-2093 CUDADevice::shader
- *                                            (DeviceTask SHADER, SHADER_EVAL_BACKGROUND;
- *                                            kernel_bake.h:474-510, light.cpp:38-85)
+ *                                            (DeviceTask SHADER: SHADER_EVAL_BACKGROUND,
+ *                                            kernel_bake.h:474-510, light.cpp:38-85;
+ *                                            SHADER_EVAL_DISPLACE, kernel_bake.h:446-472,
+ *                                            mesh_displace.cpp)
  *   hipcy_tex_alloc / hipcy_tex_free         device_cuda_impl.cpp:1105-1304 CUDADevice::tex_alloc /
  *                                            tex_free + load_texture_info (device_texture of
  *                                            render/image.cpp device_load_image; the SVM image
@@ -158,9 +160,13 @@ int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
  * without overlap, so each launch is timed alone), bit 1 = traversal counters. */
 int hipcy_set_profiling(hipcy_device *dev, int flags);
 
-/* DeviceTask SHADER: input uint4 per pixel (x, y = u, v float bits), output
- * float4 per pixel accumulated (+=) num_samples times over
- * [shader_x, shader_x + shader_w).  SHADER_EVAL_DISPLACE is rejected. */
+/* DeviceTask SHADER: input uint4 per element, output float4 per element
+ * accumulated (+=) num_samples times over [shader_x, shader_x + shader_w).
+ * SHADER_EVAL_BACKGROUND: input (u, v float bits) of the world map, output the
+ * background radiance (kernel_bake.h:474-510).  SHADER_EVAL_DISPLACE: input
+ * (object, prim, u float bits, v float bits) of a mesh vertex, output the
+ * object-space displacement of the shader's displacement program
+ * (kernel_bake.h:446-472; MeshManager::displace, render/mesh_displace.cpp). */
 #define HIPCY_SHADER_EVAL_DISPLACE 0   /* kernel_types.h:203 */
 #define HIPCY_SHADER_EVAL_BACKGROUND 1 /* kernel_types.h:204 */
 int hipcy_shader_eval(hipcy_device *dev, int eval_type, uint64_t input, uint64_t output, int shader_x,

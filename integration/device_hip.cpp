@@ -198,12 +198,13 @@ class HIPCyclesDevice : public Device {
       return;
     }
     if (task.type == DeviceTask::SHADER) {
-      /* LightManager background map (light.cpp:38-85) -> CUDADevice::shader
-       * (device_cuda_impl.cpp:2019-2093); SHADER_EVAL_DISPLACE is rejected */
+      /* LightManager background map (light.cpp:38-85) and MeshManager::displace
+       * (mesh_displace.cpp, SHADER_EVAL_DISPLACE) -> CUDADevice::shader
+       * (device_cuda_impl.cpp:2019-2093) */
       task_pool_.push([=] {
         /* per sample, 64K-pixel chunks with a cancel check between them and
-         * progress after each sample, as CUDADevice::shader does; background
-         * evaluation does not depend on the sample index (kernel_bake.h:474) */
+         * progress after each sample, as CUDADevice::shader does; neither
+         * evaluation depends on the sample index (kernel_bake.h:446-510) */
         DeviceTask task_copy = task;
         const int chunk = 0x10000;
         const int end = task.shader_x + task.shader_w;

@@ -193,6 +193,13 @@ class RefKernel:
         self.lib.cref_shader_eval(self.h, inp.ctypes.data, out.ctypes.data, 1, 0, width * height, num_samples)
         return out
 
+    def displace_eval(self, inp: np.ndarray):
+        """SHADER_EVAL_DISPLACE through kernel_cpu_shader (kernel_displace_evaluate)."""
+        inp = np.ascontiguousarray(inp, dtype=np.uint32).reshape(-1, 4)
+        out = np.zeros((len(inp), 4), dtype=np.float32)
+        self.lib.cref_shader_eval(self.h, inp.ctypes.data, out.ctypes.data, 0, 0, len(inp), 1)
+        return out
+
     def camera_rays(self, xys: np.ndarray):
         xys = np.ascontiguousarray(xys, dtype=np.int32)
         out = np.zeros((xys.shape[0], 8), dtype=np.float32)

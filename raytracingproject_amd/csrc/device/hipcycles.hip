@@ -515,6 +515,31 @@ __global__ void __launch_bounds__(CY_BLOCK) k_background_eval(CyGlobals kg, cons
   o[2] += c.z;
 }
 
+/* SHADER_EVAL_DISPLACE (kernel_cuda_displace, kernels/cuda/kernel.cu:196-205):
+ * one thread per input (object, prim, u, v) of the chunk, output += (D, 0). */
+__global__ void __launch_bounds__(CY_BLOCK) k_displace_eval(CyGlobals kg, const hc_uint4 *input, float *output,
+                                                              int sx, int sw, uint *err)
+{
+  const int x = sx + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (x >= sx + sw) {
+    return;
+  }
+  float svm[CY_SVM_STACK];
+  CyShadeMem mem;
+  mem.closure = nullptr;
+  mem.svm_stack = svm;
+  mem.svm_stride = 1;
+  mem.svm_fast = CY_SVM_STACK;
+  mem.svm_spill = nullptr;
+  const hc_uint4 in = input[x];
+  const cfloat3 d = displace_evaluate(&kg, (int)in.x, (int)in.y, as_float(in.z), as_float(in.w), mem, err);
+  float *o = output + 4 * (size_t)x;
+  o[0] += d.x;
+  o[1] += d.y;
+  o[2] += d.z;
+  o[3] += 0.0f;
+}
+
 /* Film convert (kernel/kernel_film.h, kernels/cuda/kernel.cu:156-178): one
  * thread per pixel of the (w x h) rectangle; the parity target is the CPU
  * device, so half output uses its truncating float4_store_half (util_half.h:80-118)
@@ -2091,8 +2116,8 @@ int hipcy_shader_eval(hipcy_device *dev, int eval_type, uint64_t input, uint64_t
   if (!dev->error.empty()) {
     return -1;
   }
-  if (eval_type != HIPCY_SHADER_EVAL_BACKGROUND) {
-    return set_error(dev, "shader_eval: only SHADER_EVAL_BACKGROUND is supported (displacement is not)");
+  if (eval_type != HIPCY_SHADER_EVAL_BACKGROUND && eval_type != HIPCY_SHADER_EVAL_DISPLACE) {
+    return set_error(dev, "shader_eval: eval_type must be SHADER_EVAL_DISPLACE or SHADER_EVAL_BACKGROUND");
   }
   if (!dev->have_data) {
     return set_error(dev, "shader_eval: KernelData not uploaded");
@@ -2117,7 +2142,8 @@ int hipcy_shader_eval(hipcy_device *dev, int eval_type, uint64_t input, uint64_t
   for (int sample = 0; sample < num_samples; sample++) {
     for (int x = shader_x; x < shader_x + shader_w; x += chunk) {
       const int w = std::min(chunk, shader_x + shader_w - x);
-      hipLaunchKernelGGL(k_background_eval, dim3((w + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
+      hipLaunchKernelGGL(eval_type == HIPCY_SHADER_EVAL_DISPLACE ? k_displace_eval : k_background_eval,
+                         dim3((w + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
                          (const hc_uint4 *)input, (float *)output, x, w, err);
       HIP_CHECK(dev, hipGetLastError());
     }

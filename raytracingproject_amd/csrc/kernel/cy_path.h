@@ -1739,7 +1739,9 @@ CY_FN int svm_eval_texture_node(const hc_KernelData *data,
   return offset;
 }
 
-CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err)
+/* type: SHADER_TYPE_SURFACE (0) or SHADER_TYPE_DISPLACEMENT (2), svm.h:236-246 */
+CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err,
+                          int type = 0)
 {
   CySvmStack stack;
   stack.p = sd->svm_stack;
@@ -1754,7 +1756,7 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
       case NODE_END:
         return;
       case NODE_SHADER_JUMP:
-        offset = (int)node.y; /* SHADER_TYPE_SURFACE */
+        offset = (int)(type == 2 ? node.w : node.y);
         break;
       case NODE_CLOSURE_BSDF:
         svm_node_closure_bsdf(kg, sd, stack, node, path_flag, &offset, err);
@@ -1854,6 +1856,53 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         svm_store(stack, out_offset, f, err);
         break;
       }
+#if CY_SVM_TEX
+      /* svm_displace.h:86-167 (displacement programs, SHADER_EVAL_DISPLACE) */
+      case NODE_SET_DISPLACEMENT:
+        sd->P = add3(sd->P, svm_load3(stack, node.y, err));
+        break;
+      case NODE_DISPLACEMENT: {
+        const uint height_off = node.y & 0xFF, mid_off = (node.y >> 8) & 0xFF;
+        const uint scale_off = (node.y >> 16) & 0xFF, normal_off = (node.y >> 24) & 0xFF;
+        const float height = svm_load(stack, height_off, err);
+        const float midlevel = svm_load(stack, mid_off, err);
+        const float scale = svm_load(stack, scale_off, err);
+        cfloat3 dP = (normal_off != SVM_STACK_INVALID) ? svm_load3(stack, normal_off, err) : sd->N;
+        if (node.w == NODE_NORMAL_MAP_OBJECT) {
+          if (sd->object != OBJECT_NONE) {
+            dP = normalize3(transform_direction_transposed(object_tfm(kg, sd->object), dP));
+          }
+          dP = mul3f(dP, (height - midlevel) * scale);
+          dP = transform_direction(object_tfm(kg, sd->object), dP);
+        }
+        else {
+          dP = mul3f(dP, (height - midlevel) * scale);
+        }
+        svm_store3(stack, node.z, dP, err);
+        break;
+      }
+      case NODE_VECTOR_DISPLACEMENT: {
+        const hc_uint4 data = kg->__svm_nodes[offset];
+        offset++;
+        const uint space = data.x;
+        const uint vector_off = node.y & 0xFF, mid_off = (node.y >> 8) & 0xFF;
+        const uint scale_off = (node.y >> 16) & 0xFF, disp_off = (node.y >> 24) & 0xFF;
+        const cfloat3 vec = svm_load3(stack, vector_off, err);
+        const float midlevel = svm_load(stack, mid_off, err);
+        const float scale = svm_load(stack, scale_off, err);
+        cfloat3 dP = mul3f(sub3(vec, mk3(midlevel, midlevel, midlevel)), scale);
+        if (space == NODE_NORMAL_MAP_TANGENT) {
+          /* tangent space needs the tangent attributes: rejected at load_kernels */
+          cy_set_error(err, CY_ERR_SVM_NODE, NODE_VECTOR_DISPLACEMENT);
+          return;
+        }
+        if (space != NODE_NORMAL_MAP_WORLD) {
+          dP = transform_direction(object_tfm(kg, sd->object), dP);
+        }
+        svm_store3(stack, disp_off, dP, err);
+        break;
+      }
+#endif
       default:
 #if !CY_SVM_TEX
         cy_set_error(err, CY_ERR_SVM_NODE, node.x);
@@ -1902,6 +1951,61 @@ CY_FN void shader_eval_surface(
   sd->num_closure = 0;
   sd->num_closure_left = max_closures;
   svm_eval_nodes(kg, sd, state, path_flag, err);
+}
+
+/* SHADER_EVAL_DISPLACE for one (object, prim, u, v): kernel_displace_evaluate
+ * (kernel_bake.h:446-472).  shader_setup_from_displace (kernel_shader.h:367-393)
+ * = triangle_point_normal (geom_triangle.h:44-66) + shader_setup_from_sample
+ * (kernel_shader.h:244-360) with I = 0, t = 0, the smooth normal forced and the
+ * object transform applied when the mesh is not pre-transformed; then the
+ * displacement program moves sd->P and D = P' - P goes to object space. */
+CY_FN cfloat3 displace_evaluate(const CyGlobals *kg, int object, int prim, float u, float v, CyShadeMem mem,
+                                uint *err)
+{
+  CySD sd;
+  sd.closure = mem.closure;
+  sd.svm_stack = mem.svm_stack;
+  sd.svm_stride = mem.svm_stride;
+  sd.svm_fast = mem.svm_fast;
+  sd.svm_spill = mem.svm_spill;
+  cfloat3 V[3];
+  triangle_verts(kg, prim, V);
+  const float t = 1.0f - u - v;
+  const cfloat3 P = add3(add3(mul3f(V[0], u), mul3f(V[1], v)), mul3f(V[2], t));
+  const int object_flag = (int)kg->__object_flag[object];
+  cfloat3 Ng = (object_flag & SD_OBJECT_NEGATIVE_SCALE_APPLIED) ?
+                   normalize3(cross3(sub3(V[2], V[0]), sub3(V[1], V[0]))) :
+                   normalize3(cross3(sub3(V[1], V[0]), sub3(V[2], V[0])));
+  sd.shader = (int)(kg->__tri_shader[prim] | SHADER_SMOOTH_NORMAL);
+  sd.P = P;
+  sd.N = Ng;
+  sd.Ng = Ng;
+  sd.I = mk3(0.0f, 0.0f, 0.0f);
+  sd.type = PRIMITIVE_TRIANGLE;
+  sd.object = object;
+  sd.prim = prim;
+  sd.u = u;
+  sd.v = v;
+  sd.ray_length = 0.0f;
+  sd.flag = kg->__shaders[(uint)sd.shader & SHADER_MASK].flags;
+  sd.object_flag = object_flag;
+  if (!(object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
+    sd.P = transform_point(object_tfm(kg, object), sd.P);
+    sd.Ng = object_normal_transform(kg, object, sd.Ng);
+    sd.N = sd.Ng;
+    sd.I = transform_direction(object_tfm(kg, object), sd.I);
+  }
+  sd.N = triangle_smooth_normal(kg, Ng, prim, u, v);
+  if (!(object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
+    sd.N = object_normal_transform(kg, object, sd.N);
+  }
+  /* backfacing test: dot(Ng, I) with I = 0 is never negative */
+  sd.num_closure = 0;
+  sd.num_closure_left = 0;
+  sd.svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
+  const cfloat3 P0 = sd.P;
+  svm_eval_nodes(kg, &sd, nullptr, 0, err, 2);
+  return transform_direction(object_itfm(kg, object), sub3(sd.P, P0));
 }
 
 /* kernel_shader.h:527-551 */

@@ -113,10 +113,20 @@ enum {
   SD_OBJECT_SHADOW_CATCHER = (1 << 7)
 };
 
+/* NodeNormalMapSpace (svm_types.h:455-461) */
+enum {
+  NODE_NORMAL_MAP_TANGENT = 0,
+  NODE_NORMAL_MAP_OBJECT = 1,
+  NODE_NORMAL_MAP_WORLD = 2,
+};
+
 /* ShaderNodeType (svm_types.h:60-162) — the subset the HIP interpreter runs. */
 enum {
   NODE_END = 0,
   NODE_SHADER_JUMP = 1,
+  NODE_SET_DISPLACEMENT = 20,
+  NODE_DISPLACEMENT = 21,
+  NODE_VECTOR_DISPLACEMENT = 22,
   NODE_CLOSURE_BSDF = 2,
   NODE_CLOSURE_EMISSION = 3,
   NODE_CLOSURE_BACKGROUND = 4,

@@ -243,6 +243,27 @@ class HIPDevice:
             d_o.free()
         return out
 
+    def displace_eval(self, inp: np.ndarray) -> np.ndarray:
+        """SHADER_EVAL_DISPLACE (MeshManager::displace, mesh_displace.cpp ->
+        CUDADevice::shader): inp uint32 [N, 4] = (object, prim, u bits, v bits);
+        returns float32 [N, 4], the object-space displacement (w = 0)."""
+        inp = np.ascontiguousarray(inp, dtype=np.uint32).reshape(-1, 4)
+        out = np.zeros((len(inp), 4), dtype=np.float32)
+        if len(inp) == 0:
+            return out
+        d_i = self.mem_alloc(inp.nbytes)
+        d_o = self.mem_alloc(out.nbytes)
+        try:
+            d_i.copy_to_device(inp)
+            d_o.copy_to_device(out)
+            self._check(self.lib.hipcy_shader_eval(self.h, self.SHADER_EVAL_DISPLACE, d_i.ptr, d_o.ptr, 0,
+                                                   len(inp), 0, 1))
+            d_o.copy_from_device(out)
+        finally:
+            d_i.free()
+            d_o.free()
+        return out
+
     # ---- FILM_CONVERT task ------------------------------------------------
     def film_convert(self, buffer: np.ndarray, sample_scale: float, half: bool = False,
                      tile=None) -> np.ndarray:

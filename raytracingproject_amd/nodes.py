@@ -299,6 +299,30 @@ def color_ramp(fac, stops, interpolation: str = "linear", table_size: int = 256)
 # socket types
 
 
+DISPLACEMENT_SPACES = {"object": 1, "world": 2}  # NodeNormalMapSpace (svm_types.h:455-461)
+NODE_DISPLACEMENT, NODE_VECTOR_DISPLACEMENT = 21, 22
+
+
+def displacement(height, midlevel=0.5, scale=1.0, normal=None, space: str = "object") -> Socket:
+    """Displacement node (nodes.cpp:6905-6952): (height - midlevel) * scale along
+    the normal (sd->N when unlinked), in object or world space."""
+    if space not in DISPLACEMENT_SPACES:
+        raise ValueError(f"displacement space {space!r}: object or world")
+    inputs = {"Height": height, "Midlevel": midlevel, "Scale": scale}
+    if normal is not None:
+        inputs["Normal"] = normal
+    return Node("displacement", inputs, {"space": space})["Displacement"]
+
+
+def vector_displacement(vector, midlevel=0.0, scale=1.0, space: str = "object") -> Socket:
+    """Vector Displacement node (nodes.cpp:6962-7043) in object or world space
+    (tangent space needs the UV tangent attributes: not supported)."""
+    if space not in DISPLACEMENT_SPACES:
+        raise ValueError(f"vector displacement space {space!r}: object or world (tangent is not supported)")
+    return Node("vector_displacement", {"Vector": vector, "Midlevel": midlevel, "Scale": scale},
+                {"space": space})["Displacement"]
+
+
 def _outputs(node: Node) -> dict:
     k = node.kind
     if k == "value":
@@ -331,6 +355,8 @@ def _outputs(node: Node) -> dict:
         return {"Result": "float"}
     if k in ("rgb_ramp", "image_texture", "environment_texture"):
         return {"Color": "color", "Alpha": "float"}
+    if k in ("displacement", "vector_displacement"):
+        return {"Displacement": "vector"}
     raise ValueError(f"unknown node kind {k!r}")
 
 
@@ -356,6 +382,8 @@ _INPUT_TYPES = {
     "rgb_ramp": {"Fac": "float"},
     "image_texture": {"Vector": "vector"},
     "environment_texture": {"Vector": "vector"},
+    "displacement": {"Height": "float", "Midlevel": "float", "Scale": "float", "Normal": "vector"},
+    "vector_displacement": {"Vector": "color", "Midlevel": "float", "Scale": "float"},
 }
 
 
@@ -640,6 +668,17 @@ class NodeCompiler:
         vec = self.inp(n, "Vector")
         self.emit((NODE_TEX_GRADIENT, uchar4(GRADIENT_TYPES.index(n.params["type"]), vec, self.out(n, "Fac"),
                                              self.out(n, "Color")), 0, 0))
+
+    def _n_displacement(self, n):  # nodes.cpp:6937-6952 DisplacementNode::compile
+        h, m, sc = self.inp(n, "Height"), self.inp(n, "Midlevel"), self.inp(n, "Scale")
+        nrm = self.assign_if_linked(n.inputs.get("Normal"), "vector")
+        self.emit((NODE_DISPLACEMENT, uchar4(h, m, sc, nrm), self.out(n, "Displacement"),
+                   DISPLACEMENT_SPACES[n.params["space"]]))
+
+    def _n_vector_displacement(self, n):  # nodes.cpp:7014-7043 VectorDisplacementNode::compile
+        v, m, sc = self.inp(n, "Vector"), self.inp(n, "Midlevel"), self.inp(n, "Scale")
+        self.emit((NODE_VECTOR_DISPLACEMENT, uchar4(v, m, sc, self.out(n, "Displacement")), 0, 0))
+        self.emit((DISPLACEMENT_SPACES[n.params["space"]], 0, 0, 0))
 
     def _n_mapping(self, n):  # nodes.cpp MappingNode::compile
         v, loc = self.inp(n, "Vector"), self.inp(n, "Location")

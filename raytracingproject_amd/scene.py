@@ -47,6 +47,7 @@ PRNG_BASE_NUM = 10
 PRNG_BOUNCE_NUM = 8
 
 NODE_END, NODE_SHADER_JUMP, NODE_CLOSURE_BSDF, NODE_CLOSURE_EMISSION = 0, 1, 2, 3
+NODE_SET_DISPLACEMENT = 20
 NODE_CLOSURE_BACKGROUND, NODE_CLOSURE_SET_WEIGHT = 4, 5
 NODE_CLOSURE_WEIGHT, NODE_EMISSION_WEIGHT = 6, 7
 NODE_MIX_CLOSURE, NODE_JUMP_IF_ZERO, NODE_VALUE_F = 8, 9, 14
@@ -93,6 +94,7 @@ PRINCIPLED_VECTORS = ("normal", "clearcoat_normal", "tangent")
 BECKMANN_CLOSURES = (CLOSURE_BSDF_MICROFACET_BECKMANN_ID, CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID,
                      CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)
 SD_HAS_TRANSPARENT_SHADOW = 1 << 17
+SD_HAS_DISPLACEMENT = 1 << 26
 
 
 def f32bits(x: float) -> int:
@@ -124,6 +126,9 @@ class Closure:
     rotation: object = 0.0
     tangent: object = None
     params: dict | None = None  # principled: PRINCIPLED_DEFAULTS keys + normals
+    # material output "Displacement" (a vector socket, e.g. nodes.displacement),
+    # displacement method "true": its own SVM program, run by SHADER_EVAL_DISPLACE
+    displacement: object = None
 
     def closure_type(self) -> int:
         """The ClosureType the node compiles to, after simplify_settings
@@ -450,6 +455,19 @@ class SVMCompiler:
                 self.nc.link(v, t)
             self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
             self.nodes.append((NODE_END, 0, 0, 0))
+            disp = getattr(sh, "displacement", None)
+            if nodes.is_linked(disp):
+                # svm.cpp SVMCompiler::compile: the displacement program's start
+                # in the jump node's w; OutputNode::compile emits
+                # NODE_SET_DISPLACEMENT of the "Displacement" input (nodes.cpp)
+                self.nodes[i] = (NODE_SHADER_JUMP, start, 0, len(self.nodes))
+                self.stack_top = 0
+                self.stack_used = [False] * SVM_STACK_SIZE
+                self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [disp], self.free,
+                                             images=self.images)
+                off = self.nc.link(disp, "vector")
+                self.nodes.append((NODE_SET_DISPLACEMENT, off, 0, 0))
+                self.nodes.append((NODE_END, 0, 0, 0))
         self.nc = None
         return np.array(self.nodes, dtype=np.uint32).reshape(-1, 4)
 
@@ -569,6 +587,10 @@ class Scene:
     adaptive_sampling: bool = False
     adaptive_threshold: float = 0.0
     adaptive_min_samples: int = 0
+
+
+def _has_displacement(m) -> bool:
+    return nodes.is_linked(getattr(m, "displacement", None))
 
 
 @dataclass
@@ -850,6 +872,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
         if const is not None:
             flag |= SD_HAS_CONSTANT_EMISSION
             kshaders[i].constant_emission[:] = [float(c) for c in const]
+        if _has_displacement(m):
+            flag |= SD_HAS_DISPLACEMENT  # shader.cpp:559-560 (displacement_method true)
         kshaders[i].flags = flag
     tri_shader = tri_shader_idx.astype(np.uint32) | np.uint32(SHADER_CAST_SHADOW | SHADER_AREA_LIGHT)
     tri_shader = np.where(tri_smooth, tri_shader | np.uint32(SHADER_SMOOTH_NORMAL), tri_shader).astype(np.uint32)

@@ -244,6 +244,32 @@ def cornell_instanced(width=64, height=64, samples=16) -> sc.Scene:
     return scene
 
 
+def cornell_displace(width=48, height=48, samples=8) -> sc.Scene:
+    """Instanced Cornell box whose materials carry true-displacement programs
+    (SHADER_EVAL_DISPLACE, MeshManager::displace): a scalar Displacement node
+    in object space on the walls and instanced boxes (instanced ones with
+    object-space transforms), a world-space Displacement along a linked normal
+    on the red wall, and a Vector Displacement node in world space on the
+    smooth glossy ellipsoid."""
+    import dataclasses
+
+    from . import nodes as nd
+
+    scene = cornell_instanced(width, height, samples)
+    pos = nd.separate_xyz(nd.geometry()["Position"])
+    h = nd.math("sine", nd.math("multiply", pos["X"], 0.05))
+    h2 = nd.math("sine", nd.math("multiply", pos["Y"], 0.03))
+    mats = list(scene.materials)
+    mats[0] = dataclasses.replace(mats[0], displacement=nd.displacement(h, 0.5, 3.0, space="object"))
+    mats[1] = dataclasses.replace(mats[1], displacement=nd.displacement(
+        h2, 0.25, 2.0, normal=nd.geometry()["Normal"], space="world"))
+    mats[4] = dataclasses.replace(mats[4], displacement=nd.vector_displacement(
+        nd.combine_xyz(h2, 0.25, h), 0.1, 2.0, space="world"))
+    scene.materials = mats
+    scene.name = "cornell_displace"
+    return scene
+
+
 def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
     """BMW27-class stand-in (SURVEY.md §8(d) config BMW): ~0.7M triangles at
     detail=1.0, glossy / glass / diffuse materials, two emissive studio panels,

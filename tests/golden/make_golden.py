@@ -130,6 +130,20 @@ def make_background():
     np.savez_compressed(os.path.join(os.path.dirname(golden_path("x")), "background.npz"), **out)
 
 
+def make_displace():
+    """SHADER_EVAL_DISPLACE by the reference kernel (kernel_displace_evaluate)
+    over parity_cases.displace_inputs of the displacement case."""
+    from parity_cases import DISPLACE_CASE, displace_inputs
+
+    ds = compile_case(DISPLACE_CASE)
+    inp = displace_inputs(ds)
+    rk = RefKernel(ds)
+    out = rk.displace_eval(inp)
+    rk.close()
+    np.savez_compressed(golden_path("displace"), digest=np.array(scene_digest(ds)), input=inp, output=out)
+    print("displace", len(inp), "queries, |D| max", float(np.abs(out).max()))
+
+
 def make_scale():
     """Full-size configs on a crop (parity_cases.SCALE_CASES) and the bench
     scene's full frame reduced to block means."""
@@ -162,10 +176,14 @@ def main():
     if "--background-only" in sys.argv:
         make_background()
         return
+    if "--displace-only" in sys.argv:
+        make_displace()
+        return
     if not any(a.startswith("--cases=") for a in sys.argv):
         make_primitives()
         make_film()
         make_background()
+        make_displace()
     if "--primitives-only" in sys.argv:
         return
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--cases=")]

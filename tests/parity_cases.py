@@ -44,6 +44,9 @@ CASES = {
     # adaptive sampling (kernel_adaptive_sampling.h): aux buffer + sample count
     # passes, per-step stopping and the x/y dilation filters, final rescale
     "cornell_adaptive": lambda: scenes.cornell_adaptive(64, 64, 64),
+    # true-displacement materials (their displacement programs are only run by
+    # SHADER_EVAL_DISPLACE, tests/golden/displace.npz; the render uses the surfaces)
+    "cornell_displace": lambda: scenes.cornell_displace(48, 48, 8),
 }
 
 # Cases whose render needs the device's host-side step loop (adaptive sampling:
@@ -52,6 +55,48 @@ CASES = {
 # on the GPU only (test_gpu_parity).
 HOST_LOOP_CASES = {"cornell_adaptive"}
 EMU_CASES = [n for n in CASES if n not in HOST_LOOP_CASES]
+
+# SHADER_EVAL_DISPLACE (tests/golden/displace.npz)
+DISPLACE_CASE = "cornell_displace"
+
+
+def displace_inputs(ds, seed=5):
+    """MeshManager::displace-style queries (mesh_displace.cpp): (object, prim,
+    u, v) for triangles whose shader has a displacement program, at the three
+    corners and two interior points; triangles of instanced geometry are
+    queried under every instanced object (object-space transforms)."""
+    arr = ds.arrays
+    shader_mask = (1 << 23) - 1  # kernel_types.h SHADER_MASK
+    # KernelShader: 8 words, flags at word 4 (hipcycles_kernel_types.h)
+    flags = np.frombuffer(np.ascontiguousarray(arr["__shaders"]).tobytes(), dtype=np.int32).reshape(-1, 8)[:, 4]
+    tri_shader = arr["__tri_shader"] & shader_mask
+    has_disp = ((flags >> 26) & 1).astype(bool)  # SD_HAS_DISPLACEMENT
+    obj_flag = arr["__object_flag"]
+    pairs = set()
+    instanced = [o for o in range(len(obj_flag)) if not (int(obj_flag[o]) & 4)]
+    for o, t, ty in zip(arr["__prim_object"], arr["__prim_index"], arr["__prim_type"]):
+        if int(ty) == 1 and has_disp[tri_shader[int(t)]] and int(obj_flag[int(o)]) & 4:
+            pairs.add((int(o), int(t)))
+    # triangles of shared (instanced) geometry: under every instanced object
+    applied = {t for _, t in pairs}
+    for t in range(len(tri_shader)):
+        if has_disp[tri_shader[t]] and t not in applied:
+            pairs.update((oi, t) for oi in instanced)
+    # every instanced object with a few displaced triangles: the object-space
+    # setup and transforms (shader_setup_from_sample object_space) are pure
+    # functions of (object, prim), whichever geometry the object places
+    for oi in instanced:
+        pairs.update((oi, t) for t in sorted(applied)[:12])
+    pairs = sorted(pairs)
+    rng = np.random.default_rng(seed)
+    uv = [(1.0, 0.0), (0.0, 1.0), (0.0, 0.0)]
+    rows = []
+    for o, t in pairs:
+        pts = uv + [tuple(x) for x in rng.dirichlet((1.0, 1.0, 1.0), 2)[:, :2]]
+        for u, v in pts:
+            rows.append((o, t, np.float32(u).view(np.uint32), np.float32(v).view(np.uint32)))
+    return np.array(rows, dtype=np.uint32).reshape(-1, 4)
+
 
 # BASELINE.json configs at their full size (scene, resolution, spp), checked on a
 # crop the reference kernel renders in seconds: name -> (scene, tile or None).

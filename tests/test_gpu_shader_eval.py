@@ -55,3 +55,19 @@ def test_shader_eval_displace_rejected():
         assert "SHADER_EVAL_BACKGROUND" in dev.error_message()
     finally:
         dev.close()
+
+
+def test_displace_eval_bit_exact(device):
+    """SHADER_EVAL_DISPLACE (kernel_displace_evaluate, kernel_bake.h:446-472):
+    object-space displacement of scalar (object / world space, linked normal)
+    and vector displacement programs, on transform-applied and instanced
+    objects, bit-exact against the reference CPU kernel."""
+    from parity_cases import DISPLACE_CASE, compile_case, golden_path, scene_digest
+
+    g = np.load(golden_path("displace"))
+    ds = compile_case(DISPLACE_CASE)
+    assert str(g["digest"]) == scene_digest(ds)
+    device.upload_scene(ds)
+    out = device.displace_eval(g["input"])
+    assert np.isfinite(out).all()
+    assert np.array_equal(out.view(np.uint32), g["output"].view(np.uint32))

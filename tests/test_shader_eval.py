@@ -44,3 +44,16 @@ def test_background_inputs_match_light_manager():
     assert inp[2, 4, 0] == np.float32(4.5 / 5).view(np.uint32)
     assert inp[2, 4, 1] == np.float32(2.5 / 3).view(np.uint32)
     assert not inp[..., 2:].any()
+
+
+def test_displace_fixture_inputs():
+    """tests/golden/displace.npz was made from today's scene compiler output and
+    queries (parity_cases.displace_inputs), and exercises every program kind."""
+    from parity_cases import DISPLACE_CASE, compile_case, displace_inputs, golden_path
+
+    g = np.load(golden_path("displace"))
+    ds = compile_case(DISPLACE_CASE)
+    assert str(g["digest"]) == scene_digest(ds)
+    assert np.array_equal(displace_inputs(ds), g["input"])
+    assert np.isfinite(g["output"]).all() and (np.abs(g["output"][:, :3]).sum(axis=1) > 0).mean() > 0.9
+    assert len(np.unique(g["input"][:, 0])) >= 8  # applied and instanced objects
