@@ -1,4 +1,5 @@
-"""GPU parity of the SHADER task (hipcy_shader_eval, SHADER_EVAL_BACKGROUND)
+"""GPU parity of the SHADER task (hipcy_shader_eval, SHADER_EVAL_BACKGROUND and
+SHADER_EVAL_DISPLACE)
 against the reference CPU kernel (kernel_background_evaluate,
 kernel_bake.h:474-510) recorded in tests/golden/background.npz.
 
@@ -43,16 +44,17 @@ def test_background_eval_large_map_chunks(device):
                           np.broadcast_to(g[0, 0], (300 * 250, 4)).view(np.uint32))
 
 
-def test_shader_eval_displace_rejected():
+def test_shader_eval_unknown_type_rejected():
+    """Eval types other than DISPLACE / BACKGROUND (the bake passes) are refused."""
     from raytracingproject_amd.device import HIPDevice
 
     dev = HIPDevice(0)
     try:
         dev.upload_scene(sc.compile_scene(BACKGROUND_CASES["world_blue"][0]()))
         d = dev.mem_alloc(64)
-        rc = dev.lib.hipcy_shader_eval(dev.h, 0, d.ptr, d.ptr, 0, 1, 0, 1)
+        rc = dev.lib.hipcy_shader_eval(dev.h, 5, d.ptr, d.ptr, 0, 1, 0, 1)
         assert rc != 0
-        assert "SHADER_EVAL_BACKGROUND" in dev.error_message()
+        assert "SHADER_EVAL_DISPLACE or SHADER_EVAL_BACKGROUND" in dev.error_message()
     finally:
         dev.close()
 
