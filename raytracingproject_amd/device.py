@@ -217,6 +217,7 @@ class HIPDevice:
 
     # ---- SHADER task -------------------------------------------------------
     SHADER_EVAL_BACKGROUND = 1  # kernel_types.h:204
+    SHADER_EVAL_DISPLACE = 0  # kernel_types.h:203
 
     def background_eval(self, width: int, height: int, num_samples: int = 1) -> np.ndarray:
         """World colour over a (width x height) equirectangular map, the SHADER
