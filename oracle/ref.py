@@ -62,7 +62,8 @@ def _bind_ref(lib):
     lib.cref_const_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
     lib.cref_global_copy.argtypes = [vp, ctypes.c_char_p, vp, sz]
     lib.cref_render.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci, ci]
-    lib.cref_render_adaptive.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci]
+    if hasattr(lib, "cref_render_adaptive"):  # absent from builds older than the adaptive harness
+        lib.cref_render_adaptive.argtypes = [vp, vp, ci, ci, ci, ci, ci, ci, ci, ci]
     lib.cref_intersect.argtypes = [vp, ci, vp, vp, vp]
     lib.cref_film_convert.argtypes = [vp, vp, vp, ctypes.c_float, ci, ci, ci, ci, ci, ci, ci]
     lib.cref_shader_eval.argtypes = [vp, vp, vp, ci, ci, ci, ci]
