@@ -52,6 +52,8 @@ def parse(argv=None):
                    help="4 (default) / 8: device-widened wide BVH; 2: the bound BVH2 as is")
     p.add_argument("--ray-sort", type=int, default=0, choices=(0, 3, 5),
                    help="bin the closest queue by ray direction per bounce: 0 off, 3 octant, 5 octant x axis")
+    p.add_argument("--trav-budget", type=int, nargs=2, default=(0, 0), metavar=("FIRST", "SECOND"),
+                   help="iteration budget of the wide traversal kernels (continuation launches); 0 0 disables")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
     p.add_argument("--slots", type=int, default=0, help="path slots in flight (0: device default)")
     p.add_argument("--tile", type=int, default=64,
@@ -121,6 +123,7 @@ def main():
     dev.set_bvh_width(args.bvh_width)
     dev.set_bvh_leaf_merge(args.leaf_merge)
     dev.set_ray_sort(args.ray_sort)
+    dev.set_traversal_budget(*args.trav_budget)
     dev.set_slots(args.slots)
     t0 = time.time()
     dev.upload_scene(ds)
@@ -216,56 +219,17 @@ def main():
     kernels = {
         "k_intersect_closest": timing["closest_ms"],
         "k_shade": timing["shade_ms"],
-        "k_intersect_shadow": timing["intersect_ms"] - timing["closest_ms"],
+        "k_intersect_shadow": timing["shadow_ms"],
     }
-    launches = max(int(timing["closest_launches"]), 1)
-    # algorithmic bytes of closest-hit traversal: 52 B per
-    # triangle test (prim_tri_index + 3 verts) plus, for the BVH2, 64 B per
-    # inner node and 16 B per leaf; for a W-wide BVH 32*W B per node (bounds,
-    # children and the leaf ranges inline, no separate leaf fetch)
-    width = int(counts["bvh_width"])
-    if width > 2:
-        closest_bytes = 32 * width * counts["closest_nodes"] + 52 * counts["closest_tris"]
-    else:
-        closest_bytes = 64 * counts["closest_nodes"] + 16 * counts["closest_leaves"] + 52 * counts["closest_tris"]
-    bytes_per_launch = closest_bytes / launches
-    avg_ms = timing["closest_ms"] / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    pmc_note = None
-    if os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
-            pmc = json.load(f)
-        from raytracingproject_amd.build import kernel_source_digest
-
-        if pmc.get("source_digest") == kernel_source_digest():
-            ent = pmc.get("k_intersect_closest", {})
-            traffic = ent.get("hbm_bytes_per_launch")
-            pmc_note = {k: ent.get(k) for k in ("instance", "dispatches", "rocprof_avg_ms", "l2_hit_rate",
-                                                 "hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch")}
-        else:
-            pmc_note = "profiles/pmc_summary.json was measured on other kernel sources"
-    roofline = {
-        "bound": "hbm",
-        "kernel": "k_intersect_closest",
-        "achieved": round(achieved, 2),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": traffic,
-        "traffic_source": pmc_note,
-        "bytes_per_launch": bytes_per_launch,
-        "avg_launch_ms": avg_ms,
-        "launches_per_frame": launches,
-        "bvh_width": int(counts["bvh_width"]),
-        "bvh_bytes": int(counts["bvh_bytes"]),
-        "nodes_per_ray": counts["closest_nodes"] / max(counts["closest_rays"], 1),
-        "tris_per_ray": counts["closest_tris"] / max(counts["closest_rays"], 1),
-    }
+    roofline = traversal_roofline(timing, counts)
 
     tile_leg = None
     if args.tile > 0 and world == 1:
-        tile_leg = tile_mode(dev, ds, args.tile, args.tile_batch)
+        # the plugin's behaviour (integration/device_hip.cpp: acquired tiles
+        # gathered up to 2^20 pixels per pass) and one tile per pass
+        tile_leg = [tile_mode(dev, ds, args.tile, args.tile_batch)]
+        if args.tile_batch != 1:
+            tile_leg.append(tile_mode(dev, ds, args.tile, 1))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -297,6 +261,7 @@ def main():
                 "parallelism": f"rows interleaved over {world} GPU(s)",
                 "wavefront_iterations_per_frame": int(timing["iterations"]),
                 "ray_sort": args.ray_sort,
+                "traversal_budget": list(args.trav_budget),
                 "scene_compile_s": round(t_compile, 2),
                 "scene_upload_s": round(t_upload, 3),
             },
@@ -314,6 +279,86 @@ def main():
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def traversal_bytes(width, nodes, leaves, tris):
+    """Algorithmic bytes of traversal: 52 B per triangle test
+    (prim_tri_index + 3 verts) plus, for the BVH2, 64 B per inner node and 16 B
+    per leaf; for a W-wide BVH 32*W B per node (bounds, children and the leaf
+    ranges inline, no separate leaf fetch)."""
+    if width > 2:
+        return 32 * width * nodes + 52 * tris
+    return 64 * nodes + 16 * leaves + 52 * tris
+
+
+def traversal_roofline(timing, counts):
+    """HBM roofline of the traversal kernels as BASELINE.md defines it: the
+    algorithmic bytes of every closest-hit and shadow ray of the instrumented
+    frame over the summed HIP-event time of both traversal kernels (each launch
+    timed alone on one lane).  Per-kernel figures beside it; the shadow kernel's
+    time also holds its finish / refill work."""
+    width = int(counts["bvh_width"])
+    launches = max(int(timing["closest_launches"]), 1)
+    c_bytes = traversal_bytes(width, counts["closest_nodes"], counts["closest_leaves"], counts["closest_tris"])
+    s_bytes = traversal_bytes(width, counts["shadow_nodes"], counts["leaves"] - counts["closest_leaves"],
+                              counts["shadow_tris"])
+    c_ms, s_ms = timing["closest_ms"], timing["shadow_ms"]
+
+    def gbs(b, ms):
+        return b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+
+    def util(lane, wave):
+        return round(lane / (64.0 * wave), 4) if wave else None
+
+    achieved = gbs(c_bytes + s_bytes, c_ms + s_ms)
+    traffic, pmc_note = None, None
+    if os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+        from raytracingproject_amd.build import kernel_source_digest
+
+        if pmc.get("source_digest") == kernel_source_digest():
+            ents = [pmc.get(k, {}) for k in ("k_intersect_closest", "k_intersect_shadow")]
+            if all(e.get("hbm_bytes_per_launch") is not None for e in ents):
+                traffic = sum(e["hbm_bytes_per_launch"] for e in ents)
+            pmc_note = {k: {f: pmc.get(k, {}).get(f) for f in ("instance", "dispatches", "rocprof_avg_ms", "l2_hit_rate",
+                                                            "hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch",
+                                                            "hbm_bytes_per_launch")}
+                        for k in ("k_intersect_closest", "k_intersect_shadow")}
+        else:
+            pmc_note = "profiles/pmc_summary.json was measured on other kernel sources"
+    return {
+        "bound": "hbm",
+        "kernel": "BVH traversal: k_intersect_closest + k_intersect_shadow (one launch of each per wavefront iteration)",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_source": pmc_note,
+        "bytes_per_launch": (c_bytes + s_bytes) / launches,
+        "avg_launch_ms": (c_ms + s_ms) / launches,
+        "launches_per_frame": launches,
+        "bvh_width": width,
+        "bvh_bytes": int(counts["bvh_bytes"]),
+        "per_kernel": {
+            "k_intersect_closest": {
+                "bytes_per_launch": c_bytes / launches, "avg_launch_ms": c_ms / launches,
+                "achieved": round(gbs(c_bytes, c_ms), 2), "frac": round(gbs(c_bytes, c_ms) / HBM_PEAK_GBS, 4),
+                "nodes_per_ray": counts["closest_nodes"] / max(counts["closest_rays"], 1),
+                "tris_per_ray": counts["closest_tris"] / max(counts["closest_rays"], 1),
+                "lane_utilisation": util(counts["closest_lane_iters"], counts["closest_wave_iters"]),
+                "iters_per_wave": counts["closest_wave_iters"] / max(counts["closest_rays"] / 64.0, 1),
+            },
+            "k_intersect_shadow": {
+                "bytes_per_launch": s_bytes / launches, "avg_launch_ms": s_ms / launches,
+                "achieved": round(gbs(s_bytes, s_ms), 2), "frac": round(gbs(s_bytes, s_ms) / HBM_PEAK_GBS, 4),
+                "nodes_per_ray": counts["shadow_nodes"] / max(counts["shadow_rays"], 1),
+                "tris_per_ray": counts["shadow_tris"] / max(counts["shadow_rays"], 1),
+                "lane_utilisation": util(counts["shadow_lane_iters"], counts["shadow_wave_iters"]),
+            },
+        },
+    }
 
 
 def tile_mode(dev, ds, tile, batch):

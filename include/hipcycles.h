@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define HIPCY_ABI_VERSION 4
+#define HIPCY_ABI_VERSION 5
 
 typedef struct hipcy_device hipcy_device;
 
@@ -90,6 +90,16 @@ typedef struct hipcy_stats {
   int32_t bvh_depth;      /* levels of the wide BVH (0 for BVH2) */
   uint64_t bvh_bytes;     /* bytes of the traversed node array */
   uint64_t tie_rays;      /* closest rays re-traced in the reference's order (near-ties) */
+  /* traversal loop iterations (nodes + leaves visited): summed over lanes, and
+   * the per-wave maximum summed over waves (lane utilisation = lane / (64 wave)) */
+  uint64_t closest_lane_iters;
+  uint64_t closest_wave_iters;
+  uint64_t shadow_nodes;  /* opaque shadow traversal only */
+  uint64_t shadow_tris;
+  uint64_t shadow_lane_iters;
+  uint64_t shadow_wave_iters;
+  double shadow_ms;       /* shadow kernel (traversal + finish / refill) */
+  uint64_t shadow_launches;
 } hipcy_stats;
 
 int hipcy_abi_version(void);
@@ -144,6 +154,13 @@ int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);
  * (8 bins), 5 = octant x major axis (24 of 32 bins).  Results never depend on
  * the order (every path is a function of its work item alone). */
 int hipcy_set_ray_sort(hipcy_device *dev, int mode);
+/* Iteration budget of the wide-BVH traversal kernels (compaction at traversal
+ * granularity): a closest-hit or shadow traversal that has run `first` loop
+ * iterations is suspended and continued by a densely packed continuation
+ * launch, which suspends again after `second` iterations into a last launch
+ * without a budget.  Results are bit-identical; 0, 0 disables (scenes with
+ * instances always run without a budget). */
+int hipcy_set_traversal_budget(hipcy_device *dev, int first, int second);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

@@ -20,6 +20,7 @@
  * tests/test_integration.py; it is not linked into this repository's products.
  */
 #include <algorithm>
+#include <vector>
 #include "device/device.h"
 #include "device/device_intern.h"
 
@@ -67,8 +68,8 @@ class HIPCyclesDevice : public Device {
   bool load_kernels(const DeviceRequestedFeatures &f) override
   {
     if (f.use_hair || f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_subsurface ||
-        f.use_volume || f.use_integrator_branched || f.use_patch_evaluation || f.use_true_displacement ||
-        f.use_shader_raytrace || f.use_denoising) {
+        f.use_volume || f.use_integrator_branched || f.use_patch_evaluation || f.use_shader_raytrace ||
+        f.use_denoising) {
       set_error("HIP device: requested features are not implemented (" + f.get_build_options() + ")");
       return false;
     }
@@ -253,37 +254,82 @@ class HIPCyclesDevice : public Device {
     return rc == 0;
   }
 
-  /* CUDADevice::thread_run RENDER branch (device_cuda_impl.cpp:2346-2386) */
+  /* Pixels of RenderTiles gathered into one device pass.  The whole BMW frame
+   * (921,600 px in 240 tiles of 64x64) fits one pass, so the slot pool stays
+   * full across tile borders instead of draining at the end of every tile. */
+  static constexpr size_t kBatchPixels = (size_t)1 << 20;
+
+  /* CUDADevice::thread_run RENDER branch (device_cuda_impl.cpp:2346-2386),
+   * with several acquired tiles rendered per hipcy_path_trace_tiles pass: the
+   * TileManager hands out tiles as MultiDevice would to concurrent devices,
+   * each is released after the pass that rendered it. */
   void render(DeviceTask &task)
   {
     if (!check(hipcy_load_kernels(dev_))) {
       return;
     }
+    std::vector<RenderTile> batch;
     RenderTile tile;
-    while (task.acquire_tile(this, tile, task.tile_types)) {
-      if (tile.task == RenderTile::PATH_TRACE) {
-        hipcy_work_tile wt;
-        wt.x = tile.x;
-        wt.y = tile.y;
-        wt.w = tile.w;
-        wt.h = tile.h;
-        wt.start_sample = tile.start_sample;
-        wt.num_samples = tile.num_samples;
-        wt.offset = tile.offset;
-        wt.stride = tile.stride;
-        wt.buffer = (uint64_t)tile.buffer;
-        if (!check(hipcy_path_trace(dev_, &wt)) || !check(hipcy_synchronize(dev_))) {
+    bool more = true;
+    while (more) {
+      batch.clear();
+      size_t pixels = 0;
+      while (pixels < kBatchPixels && (more = task.acquire_tile(this, tile, task.tile_types))) {
+        if (tile.task != RenderTile::PATH_TRACE) {
           task.release_tile(tile);
+          continue;
+        }
+        if (!batch.empty() &&
+            (tile.start_sample != batch[0].start_sample || tile.num_samples != batch[0].num_samples)) {
+          /* one pass renders one sample range: flush what is gathered */
+          if (!render_batch(task, batch)) {
+            task.release_tile(tile);
+            return;
+          }
+          batch.clear();
+          pixels = 0;
+        }
+        batch.push_back(tile);
+        pixels += (size_t)tile.w * tile.h;
+        if (task.get_cancel() && !task.need_finish_queue) {
           break;
         }
-        tile.sample = tile.start_sample + tile.num_samples;
-        task.update_progress(&tile, tile.w * tile.h * tile.num_samples);
       }
-      task.release_tile(tile);
+      if (!batch.empty() && !render_batch(task, batch)) {
+        return;
+      }
       if (task.get_cancel() && !task.need_finish_queue) {
         break;
       }
     }
+  }
+
+  /* One pass over the gathered tiles, then progress and release per tile. */
+  bool render_batch(DeviceTask &task, std::vector<RenderTile> &batch)
+  {
+    std::vector<hipcy_work_tile> wt(batch.size());
+    for (size_t i = 0; i < batch.size(); i++) {
+      const RenderTile &t = batch[i];
+      wt[i].x = t.x;
+      wt[i].y = t.y;
+      wt[i].w = t.w;
+      wt[i].h = t.h;
+      wt[i].start_sample = t.start_sample;
+      wt[i].num_samples = t.num_samples;
+      wt[i].offset = t.offset;
+      wt[i].stride = t.stride;
+      wt[i].buffer = (uint64_t)t.buffer;
+    }
+    const bool ok = check(hipcy_path_trace_tiles(dev_, wt.data(), (int)wt.size())) &&
+                    check(hipcy_synchronize(dev_));
+    for (RenderTile &t : batch) {
+      if (ok) {
+        t.sample = t.start_sample + t.num_samples;
+        task.update_progress(&t, t.w * t.h * t.num_samples);
+      }
+      task.release_tile(t);
+    }
+    return ok;
   }
 };
 

@@ -77,7 +77,8 @@ def _bind_ref(lib):
     lib.cref_sizeof.argtypes = [ctypes.c_char_p]
     lib.cref_offsetof.restype = ctypes.c_long
     lib.cref_offsetof.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
-    lib.cref_arch.restype = ctypes.c_char_p
+    if hasattr(lib, "cref_arch"):  # absent from builds older than the AVX2 baseline harness
+        lib.cref_arch.restype = ctypes.c_char_p
     return lib
 
 
@@ -107,7 +108,7 @@ class RefKernel:
 
     def __init__(self, dscene, fast: bool = False):
         self.lib = ref_lib(fast)
-        self.arch = self.lib.cref_arch().decode()
+        self.arch = self.lib.cref_arch().decode() if hasattr(self.lib, "cref_arch") else "unknown"
         self.h = self.lib.cref_create()
         self.dscene = dscene
         self._keep = []

@@ -48,15 +48,28 @@ template<bool INST> struct LdsStack<2, INST> {
   int top[CY_LDS_STACK * CY_BLOCK];
 };
 
-template<int W, bool any_hit, bool INST = true>
+/* This thread's ring column of the wide kernels' LDS stack (nullptr for BVH2). */
+template<int W, bool INST> __device__ __forceinline__ CY_LDS CyStackEntry *lds_ring_of(LdsStack<W, INST> *lds)
+{
+  if constexpr (W > 2) {
+    return (CY_LDS CyStackEntry *)(lds->ring + threadIdx.x);
+  }
+  else {
+    return nullptr;
+  }
+}
+
+/* HAIR (scenes with curves, W = 2 only): unaligned nodes and curve leaves. */
+template<int W, bool any_hit, bool INST = true, bool HAIR = false>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
                                                uint *n_tris, LdsStack<W, INST> *lds, bool *tie = nullptr)
 {
   const int t = threadIdx.x;
   if constexpr (W == 2) {
-    return bvh2_intersect<any_hit, INST>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
-                                         (CY_LDS int *)(lds->top + t));
+    return bvh2_intersect<any_hit, INST, 2, CY_LDS_STACK, CY_BLOCK, HAIR>(kg, ray, visibility, isect, err, n_nodes,
+                                                                         n_leaves, n_tris,
+                                                                         (CY_LDS int *)(lds->top + t));
   }
   else if constexpr (INST) {
     /* instanced scene: reference-order top level, wide BVH inside instances */
@@ -83,21 +96,27 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
 
 /* Traversal counters: reduced over the workgroup, then one atomic per counter
  * and workgroup into one of CY_STATS_SHARDS copies (device-scope atomics on a
- * single word serialise at the memory side). */
+ * single word serialise at the memory side).  Besides the node / leaf /
+ * triangle counts, the loop iterations (nodes + leaves visited) are summed per
+ * lane and, as the wave's maximum, per wave: a wave runs as many iterations as
+ * its longest ray, so lane_iters / (64 * wave_iters) is the traversal loop's
+ * lane utilisation. */
 __device__ __forceinline__ void stats_block_add(CyStats *shard, uint n_nodes, uint n_leaves, uint n_tris,
                                                 uint n_over)
 {
-  __shared__ uint red[4];
-  if (threadIdx.x < 4) {
+  __shared__ uint red[6];
+  if (threadIdx.x < 6) {
     red[threadIdx.x] = 0;
   }
   __syncthreads();
-  uint v[4] = {n_nodes, n_leaves, n_tris, n_over};
+  const uint iters = n_nodes + n_leaves;
+  uint v[6] = {n_nodes, n_leaves, n_tris, n_over, iters, iters};
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < 6; k++) {
     uint x = v[k];
     for (int off = 32; off > 0; off >>= 1) {
-      x += __shfl_xor(x, off);
+      const uint y = __shfl_xor(x, off);
+      x = (k == 5) ? max(x, y) : x + y;
     }
     if ((threadIdx.x & 63) == 0 && x) {
       atomicAdd(&red[k], x);
@@ -110,6 +129,123 @@ __device__ __forceinline__ void stats_block_add(CyStats *shard, uint n_nodes, ui
     if (red[1]) atomicAdd(&st->leaves, (unsigned long long)red[1]);
     if (red[2]) atomicAdd(&st->tris, (unsigned long long)red[2]);
     if (red[3]) atomicAdd(&st->rays, (unsigned long long)red[3]);
+    if (red[4]) atomicAdd(&st->lane_iters, (unsigned long long)red[4]);
+    if (red[5]) atomicAdd(&st->wave_iters, (unsigned long long)red[5]);
+  }
+}
+
+/* ---------------------------------------------------------------------------
+ * Iteration budget (hipcy_set_traversal_budget).  A wave runs as many loop
+ * iterations as its slowest ray, so a few long traversals keep a wave -- and
+ * its slot on the SIMD -- busy with most lanes idle (closest-hit lanes are 45 %
+ * utilised on the bench frame, shadow 31 %).  With a budget B a traversal stops
+ * after B iterations and is saved as a continuation record; the records are
+ * traversed by densely packed continuation launches, which may suspend again
+ * into the other buffer, and the last one runs without a budget.  A resumed
+ * traversal continues with the same stack, hit and near-tie state, so results
+ * are bit-identical.  Used by the non-instanced wide-BVH kernels.
+ *
+ * Record (SoA, CY_CONT_F4 float4 arrays of `capacity` entries):
+ *   0: ray P, t    1: ray D, visibility    2: hit t, u, v, prim
+ *   3: cursor code, top | n_ring << 8 | tie << 16, slot, 0
+ *   4..7: the LDS ring (8 x (node, entry distance)) */
+#define CY_CONT_F4 8
+#define CY_CONT_BLOCKS 1280 /* continuation grid: 256 CUs x 5 waves/SIMD x 4 SIMDs / 4 waves per block */
+struct CyCont {
+  hc_float4 *rec;
+  uint *count;
+  uint capacity;
+};
+
+template<int W>
+__device__ __forceinline__ void cont_save(const CyCont &c, uint idx, int slot, const CyRay &ray, uint vis,
+                                          const CyIsect &is, const CyTravCursor &cur,
+                                          CY_LDS const CyStackEntry *ring)
+{
+  static_assert(CY_LDS_STACKW == 8, "continuation records hold an 8-entry ring");
+  hc_float4 *r = c.rec + idx;
+  const size_t cap = c.capacity;
+  r[0] = mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t);
+  r[cap] = mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(vis));
+  r[2 * cap] = mkf4(is.t, is.u, is.v, int_as_float(is.prim));
+  r[3 * cap] = mkf4(int_as_float(cur.code), int_as_float(cur.top | (cur.n_ring << 8) | ((int)cur.tie << 16)),
+                    int_as_float(slot), 0.0f);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (cur.n_ring > 0) {
+      const CyStackEntry e0 = ring[(2 * k) * CY_BLOCK], e1 = ring[(2 * k + 1) * CY_BLOCK];
+      r[(4 + k) * cap] = mkf4(int_as_float(e0.node), e0.t, int_as_float(e1.node), e1.t);
+    }
+  }
+}
+
+template<int W>
+__device__ __forceinline__ int cont_load(const CyCont &c, uint idx, CyRay *ray, uint *vis, CyIsect *is,
+                                         CyTravCursor *cur, CY_LDS CyStackEntry *ring)
+{
+  const hc_float4 *r = c.rec + idx;
+  const size_t cap = c.capacity;
+  const hc_float4 a = r[0], d = r[cap], h = r[2 * cap], q = r[3 * cap];
+  ray->P = mk3(a.x, a.y, a.z);
+  ray->t = a.w;
+  ray->D = mk3(d.x, d.y, d.z);
+  *vis = as_uint(d.w);
+  is->t = h.x;
+  is->u = h.y;
+  is->v = h.z;
+  is->prim = as_int(h.w);
+  is->object = OBJECT_NONE;
+  is->type = is->prim != PRIM_NONE ? PRIMITIVE_TRIANGLE : 0;
+  cur->code = as_int(q.x);
+  const int packed = as_int(q.y);
+  cur->top = packed & 0xFF;
+  cur->n_ring = (packed >> 8) & 0xFF;
+  cur->tie = ((packed >> 16) & 1) != 0;
+  cur->suspended = false;
+  if (cur->n_ring > 0) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const hc_float4 e = r[(4 + k) * cap];
+      CyStackEntry e0, e1;
+      e0.node = as_int(e.x);
+      e0.t = e.y;
+      e1.node = as_int(e.z);
+      e1.t = e.w;
+      ring[(2 * k) * CY_BLOCK] = e0;
+      ring[(2 * k + 1) * CY_BLOCK] = e1;
+    }
+  }
+  return as_int(q.z);
+}
+
+/* A wide traversal of the non-instanced scene from the root (bvhw_intersect)
+ * or from a cursor, with the budget. */
+template<int W, bool any_hit>
+__device__ __forceinline__ void bvhw_run(const CyGlobals *kg, const CyRay *ray, uint visibility, CyIsect *isect,
+                                         uint *err, uint *n_nodes, uint *n_leaves, uint *n_tris,
+                                         CY_LDS CyStackEntry *ring, bool *tie, int budget, CyTravCursor *cur)
+{
+  const cfloat3 dir = bvh_clamp_direction(ray->D);
+  bvhw_traverse<W, any_hit>(kg, 0, ray->P, dir, rcp3(dir), OBJECT_NONE, visibility, isect, err, n_nodes,
+                            n_leaves, n_tris, ring, tie, budget, cur);
+}
+
+/* Suspended lanes claim continuation records (all threads of the block call
+ * this); a lane that finds the buffer full finishes its traversal now. */
+template<int W, bool any_hit>
+__device__ __forceinline__ void cont_suspend(const CyGlobals *kg, const CyCont &out, int slot, const CyRay &ray,
+                                             uint visibility, CyIsect *isect, uint *err, uint *n_nodes,
+                                             uint *n_leaves, uint *n_tris, CY_LDS CyStackEntry *ring, bool *tie,
+                                             CyTravCursor *cur, uint *claim)
+{
+  const uint idx = block_claim(out.count, cur->suspended, claim);
+  if (cur->suspended) {
+    if (idx < out.capacity) {
+      cont_save<W>(out, idx, slot, ray, visibility, *isect, *cur, ring);
+    }
+    else {
+      bvhw_run<W, any_hit>(kg, &ray, visibility, isect, err, n_nodes, n_leaves, n_tris, ring, tie, 0, cur);
+    }
   }
 }
 
@@ -120,7 +256,14 @@ __device__ __forceinline__ void stats_block_add(CyStats *shard, uint n_nodes, ui
  * (ray replacement) was measured 2x slower on the BMW stand-in (the refill path
  * with camera-ray generation inside the traversal loop spills at the 80-VGPR
  * budget, and replacement rays break the camera rays' fetch coherence). */
-template<bool STATS, int W, bool INST>
+/* Stage 1: closest hit for every queued path, or (cam_n > 0) for the camera
+ * rays of the work items item_base .. item_base + cam_n - 1 held by slots
+ * slot_base .. slot_base + cam_n - 1.  One ray per thread: a persistent variant
+ * whose lanes take the next ray of a per-workgroup pool when theirs finishes
+ * (ray replacement) was measured 2x slower on the BMW stand-in (the refill path
+ * with camera-ray generation inside the traversal loop spills at the 80-VGPR
+ * budget, and replacement rays break the camera rays' fetch coherence). */
+template<bool STATS, int W, bool INST, bool HAIR = false>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  CyTile tile,
@@ -144,8 +287,8 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
     CyIsect isect;
     bool hit = false, tie = false;
     if (has_ray && scene_intersect_valid(&ray)) {
-      hit = scene_traverse<W, false, INST>(&kg, &ray, visibility, &isect, err,
-                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack, &tie);
+      hit = scene_traverse<W, false, INST, HAIR>(&kg, &ray, visibility, &isect, err,
+                                                 STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack, &tie);
     }
     if constexpr (W > 2) {
       if (tie) {
@@ -167,8 +310,142 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
   }
 }
 
+/* Stage 1 with the iteration budget (hipcy_set_traversal_budget; non-instanced
+ * wide BVH): as k_intersect_closest, a traversal past `budget` iterations is
+ * saved as a continuation record (cont_suspend).  A kernel of its own: the
+ * suspend path's registers and barrier must not weigh on k_intersect_closest
+ * (folded into one kernel, the unbudgeted frame lost 15 %, 52 vs 45 ms of
+ * closest per frame). */
+template<bool STATS, int W, bool INST = false>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest_budget(CyGlobals kg,
+                                                                 CyPathBuffers b,
+                                                                 CyTile tile,
+                                                                 int cam_n,
+                                                                 int slot_base,
+                                                                 const int *queue,
+                                                                 const uint *counter,
+                                                                 uint *err,
+                                                                 CyStats *stats,
+                                                                 int budget,
+                                                                 CyCont cont)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ LdsStack<W, INST> lds_stack;
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
+  const bool active = cam_n > 0 ? i < cam_n : i < (int)*counter;
+  constexpr bool CAN_SUSPEND = W > 2 && !INST;
+  CyTravCursor cur;
+  cur.suspended = false;
+  CyRay ray;
+  uint visibility = 0;
+  CyIsect isect;
+  isect.prim = PRIM_NONE;
+  bool hit = false, tie = false, has_ray = false;
+  int slot = 0;
+  if (active) {
+    slot = cam_n > 0 ? slot_base + i : queue[i];
+    const uint cam_item = cam_n > 0 ? tile.item_base + (uint)i : CY_NO_ITEM;
+    has_ray = closest_load(&kg, &b, &tile, slot, cam_item, &ray, &visibility);
+    if (has_ray && scene_intersect_valid(&ray)) {
+      if (CAN_SUSPEND && budget > 0) {
+        isect.t = ray.t;
+        isect.u = 0.0f;
+        isect.v = 0.0f;
+        isect.prim = PRIM_NONE;
+        isect.object = OBJECT_NONE;
+        isect.type = 0;
+        cur.code = 0;
+        cur.top = 0;
+        cur.n_ring = 0;
+        cur.tie = false;
+        bvhw_run<W, false>(&kg, &ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves, &n_tris,
+                           lds_ring_of(&lds_stack), &tie, budget, &cur);
+        hit = isect.prim != PRIM_NONE;
+      }
+      else {
+        hit = scene_traverse<W, false, INST>(&kg, &ray, visibility, &isect, err,
+                                                   STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack, &tie);
+      }
+    }
+  }
+  if constexpr (CAN_SUSPEND) {
+    if (budget > 0) {
+      __shared__ uint claim[CY_CLAIM_LDS];
+      cont_suspend<W, false>(&kg, cont, slot, ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves,
+                             &n_tris, lds_ring_of(&lds_stack), &tie, &cur, claim);
+      hit = active && has_ray && isect.prim != PRIM_NONE;
+    }
+  }
+  if (active && !cur.suspended) {
+    if constexpr (W > 2) {
+      if (tie) {
+        /* near-tie (cy_bvhw.h bvhw_traverse): flagged in the stored primitive;
+         * the shading stage re-traces the ray with the bound BVH2 in the
+         * reference's visiting order (cy_integrator.h shade_path), so the hit
+         * is the reference's bit for bit (about 1 ray in 3000 on the bench
+         * scene).  There the re-trace does not weigh on this loop's registers. */
+        isect.prim |= CY_PRIM_TIE;
+        if (STATS) {
+          n_ties++;
+        }
+      }
+    }
+    closest_store<INST>(&b, slot, has_ray, hit, &isect);
+  }
+  if (STATS) {
+    stats_block_add(stats, n_nodes, n_leaves, n_tris, n_ties);
+  }
+}
+
+/* Stage 1 continuation: suspended closest-hit traversals from `in`, resumed
+ * with the budget (suspending again into `out`) or, budget 0, to the end.
+ * Grid-stride over the records with a fixed grid. */
+template<bool STATS, int W>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_closest_continue(CyGlobals kg, CyPathBuffers b,
+                                                                                 CyCont in, CyCont out, int budget,
+                                                                                 uint *err, CyStats *stats)
+{
+  __shared__ LdsStack<W, false> lds_stack;
+  __shared__ uint claim[CY_CLAIM_LDS];
+  CY_LDS CyStackEntry *ring = lds_ring_of(&lds_stack);
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
+  const uint n = min(*in.count, in.capacity);
+  for (uint base = blockIdx.x * CY_BLOCK; base < n; base += gridDim.x * CY_BLOCK) {
+    const uint i = base + threadIdx.x;
+    const bool active = i < n;
+    CyTravCursor cur;
+    cur.suspended = false;
+    CyRay ray;
+    uint visibility = 0;
+    CyIsect isect;
+    bool tie = false;
+    int slot = 0;
+    if (active) {
+      slot = cont_load<W>(in, i, &ray, &visibility, &isect, &cur, ring);
+      bvhw_run<W, false>(&kg, &ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, ring,
+                         &tie, budget, &cur);
+    }
+    if (budget > 0) {
+      cont_suspend<W, false>(&kg, out, slot, ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves,
+                             &n_tris, ring, &tie, &cur, claim);
+    }
+    if (active && !cur.suspended) {
+      if (tie) {
+        isect.prim |= CY_PRIM_TIE;
+        if (STATS) {
+          n_ties++;
+        }
+      }
+      closest_store<false>(&b, slot, true, isect.prim != PRIM_NONE, &isect);
+    }
+  }
+  if (STATS) {
+    stats_block_add(stats, n_nodes, n_leaves, n_tris, n_ties);
+  }
+}
+
 /* Stage 3: occlusion of the light sample, deferred light add, finish + refill. */
-template<bool STATS, int W, bool INST>
+template<bool STATS, int W, bool INST, bool HAIR = false>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
@@ -191,14 +468,130 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
     bool blocked = false;
     if (scene_intersect_valid(&ray)) {
       CyIsect isect;
-      blocked = scene_traverse<W, true, INST>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
-                                           STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack);
+      blocked = scene_traverse<W, true, INST, HAIR>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
+                                                    STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack);
     }
     finished = shadow_finish(&b, &tile, slot, blocked);
   }
   __shared__ uint claim[CY_CLAIM_LDS];
   const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
   queue_push(queue_out, count_out, slot, regen, claim);
+  if (STATS) {
+    stats_block_add(stats + CY_STATS_SHARDS, n_nodes, n_leaves, n_tris, 0);
+  }
+}
+
+
+/* Stage 3 with the iteration budget (see k_intersect_closest_budget). */
+template<bool STATS, int W, bool INST = false>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow_budget(CyGlobals kg,
+                                                                CyPathBuffers b,
+                                                                CyTile tile,
+                                                                const int *shadow_queue,
+                                                                const uint *shadow_count,
+                                                                int *queue_out,
+                                                                uint *count_out,
+                                                                uint *err,
+                                                                CyStats *stats,
+                                                                int budget,
+                                                                CyCont cont)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ LdsStack<W, INST> lds_stack;
+  __shared__ uint claim[CY_CLAIM_LDS];
+  constexpr bool CAN_SUSPEND = W > 2 && !INST;
+  bool finished = false;
+  int slot = 0;
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  const bool active = i < (int)*shadow_count;
+  CyTravCursor cur;
+  cur.suspended = false;
+  CyRay ray;
+  CyIsect isect;
+  isect.prim = PRIM_NONE;
+  bool blocked = false;
+  if (active) {
+    slot = shadow_queue[i];
+    shadow_load(&b, slot, &ray);
+    if (scene_intersect_valid(&ray)) {
+      if (CAN_SUSPEND && budget > 0) {
+        isect.t = ray.t;
+        isect.u = 0.0f;
+        isect.v = 0.0f;
+        isect.prim = PRIM_NONE;
+        isect.object = OBJECT_NONE;
+        isect.type = 0;
+        cur.code = 0;
+        cur.top = 0;
+        cur.n_ring = 0;
+        cur.tie = false;
+        bvhw_run<W, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves,
+                          &n_tris, lds_ring_of(&lds_stack), nullptr, budget, &cur);
+        blocked = isect.prim != PRIM_NONE;
+      }
+      else {
+        blocked = scene_traverse<W, true, INST>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err,
+                                                      STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack);
+      }
+    }
+  }
+  if constexpr (CAN_SUSPEND) {
+    if (budget > 0) {
+      cont_suspend<W, true>(&kg, cont, slot, ray, PATH_RAY_SHADOW_OPAQUE, &isect, err, STATS ? &n_nodes : nullptr,
+                            &n_leaves, &n_tris, lds_ring_of(&lds_stack), nullptr, &cur,
+                            claim);
+      blocked = active && isect.prim != PRIM_NONE;
+    }
+  }
+  if (active && !cur.suspended) {
+    finished = shadow_finish(&b, &tile, slot, blocked);
+  }
+  const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
+  queue_push(queue_out, count_out, slot, regen, claim);
+  if (STATS) {
+    stats_block_add(stats + CY_STATS_SHARDS, n_nodes, n_leaves, n_tris, 0);
+  }
+}
+
+/* Stage 3 continuation: suspended shadow traversals, then the same finish,
+ * refill and queue push as k_intersect_shadow. */
+template<bool STATS, int W>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_shadow_continue(CyGlobals kg, CyPathBuffers b,
+                                                                                CyTile tile, CyCont in, CyCont out,
+                                                                                int budget, int *queue_out,
+                                                                                uint *count_out, uint *err,
+                                                                                CyStats *stats)
+{
+  __shared__ LdsStack<W, false> lds_stack;
+  __shared__ uint claim[CY_CLAIM_LDS];
+  CY_LDS CyStackEntry *ring = lds_ring_of(&lds_stack);
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  const uint n = min(*in.count, in.capacity);
+  for (uint base = blockIdx.x * CY_BLOCK; base < n; base += gridDim.x * CY_BLOCK) {
+    const uint i = base + threadIdx.x;
+    const bool active = i < n;
+    CyTravCursor cur;
+    cur.suspended = false;
+    CyRay ray;
+    uint visibility = 0;
+    CyIsect isect;
+    int slot = 0;
+    bool finished = false;
+    if (active) {
+      slot = cont_load<W>(in, i, &ray, &visibility, &isect, &cur, ring);
+      bvhw_run<W, true>(&kg, &ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, ring,
+                        nullptr, budget, &cur);
+    }
+    if (budget > 0) {
+      cont_suspend<W, true>(&kg, out, slot, ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves,
+                            &n_tris, ring, nullptr, &cur, claim);
+    }
+    if (active && !cur.suspended) {
+      finished = shadow_finish(&b, &tile, slot, isect.prim != PRIM_NONE);
+    }
+    const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
+    queue_push(queue_out, count_out, slot, regen, claim);
+  }
   if (STATS) {
     stats_block_add(stats + CY_STATS_SHARDS, n_nodes, n_leaves, n_tris, 0);
   }
@@ -423,7 +816,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_sort_scatter(const int *queue, con
   }
 }
 
-template<int W>
+template<int W, bool HAIR = false>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -449,11 +842,13 @@ __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const
     /* scene_intersect: shadow visibility means early exit at the first hit
      * (bvh_traversal.h:144-146) */
     if (any_hit || (visibility & PATH_RAY_SHADOW_OPAQUE)) {
-      hit = scene_traverse<W, true>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr, nullptr, nullptr, &lds_stack);
+      hit = scene_traverse<W, true, true, HAIR>(&kg, &ray, visibility & PATH_RAY_SHADOW_OPAQUE, &isect, err, nullptr,
+                                                nullptr, nullptr, &lds_stack);
     }
     else {
       bool tie = false;
-      hit = scene_traverse<W, false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr, &lds_stack, &tie);
+      hit = scene_traverse<W, false, true, HAIR>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr,
+                                                 &lds_stack, &tie);
       if (tie) {
         hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr);
       }
@@ -650,25 +1045,38 @@ __global__ void __launch_bounds__(CY_BLOCK) k_film_convert(CyFilm film, const fl
 
 /* Kernel instance for (traversal counters, BVH width, instancing). */
 struct ClosestK {
-  template<bool S, int W, bool I> static constexpr auto fn()
+  template<bool S, int W, bool I, bool H = false> static constexpr auto fn()
   {
-    return k_intersect_closest<S, W, I>;
+    return k_intersect_closest<S, W, I, H>;
   }
 };
 struct ShadowK {
-  template<bool S, int W, bool I> static constexpr auto fn()
+  template<bool S, int W, bool I, bool H = false> static constexpr auto fn()
   {
-    return k_intersect_shadow<S, W, I>;
+    return k_intersect_shadow<S, W, I, H>;
   }
 };
-template<class K, bool S, bool I> static auto pick_width(int W)
+template<class K, bool S, bool I> static auto pick_width(int W, bool hair)
 {
-  return W == 8 ? K::template fn<S, 8, I>() : W == 4 ? K::template fn<S, 4, I>() : K::template fn<S, 2, I>();
+  /* scenes with curves traverse the BVH2 (W = 2) with the hair node tests */
+  return hair ? K::template fn<S, 2, I, true>() :
+         W == 8 ? K::template fn<S, 8, I>() :
+         W == 4 ? K::template fn<S, 4, I>() :
+                  K::template fn<S, 2, I>();
 }
-template<class K> static auto pick_kernel(bool stats, int W, bool inst)
+template<class K> static auto pick_kernel(bool stats, int W, bool inst, bool hair = false)
 {
-  return stats ? (inst ? pick_width<K, true, true>(W) : pick_width<K, true, false>(W))
-               : (inst ? pick_width<K, false, true>(W) : pick_width<K, false, false>(W));
+  return stats ? (inst ? pick_width<K, true, true>(W, hair) : pick_width<K, true, false>(W, hair))
+               : (inst ? pick_width<K, false, true>(W, hair) : pick_width<K, false, false>(W, hair));
+}
+
+template<int W> static auto pick_closest_cont(bool stats)
+{
+  return stats ? k_closest_continue<true, W> : k_closest_continue<false, W>;
+}
+template<int W> static auto pick_shadow_cont(bool stats)
+{
+  return stats ? k_shadow_continue<true, W> : k_shadow_continue<false, W>;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -719,6 +1127,14 @@ struct hipcy_device {
   size_t sort_capacity = 0;
 
   int profiling = 0; /* bit 0: HIP-event kernel timing, bit 1: traversal counters */
+
+  /* iteration budget of the wide traversal kernels (hipcy_set_traversal_budget):
+   * first launch, first continuation; 0 disables.  Per lane two continuation
+   * record buffers of cont_capacity entries. */
+  int trav_budget[2] = {0, 0};
+  hc_float4 *cont_rec = nullptr;
+  size_t cont_capacity = 0; /* records per buffer */
+  size_t cont_lanes = 0;
 
   /* path slots in flight and the per-sample record buffer of one pass */
   size_t slots_wanted = (size_t)1 << 27;
@@ -793,10 +1209,14 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   }
   CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
-  kg->bvhw_nodes = (dev->bvh_width > 2) ? dev->bvhw : nullptr;
-  kg->bvhw_object_root = (dev->bvh_width > 2) ? dev->bvhw_object_root : nullptr;
-  kg->tri_index_identity = (dev->bvh_width > 2) ? dev->tri_index_identity : 0;
+  /* scenes with curves keep the bound BVH2 (its unaligned nodes and curve
+   * leaves; the wide layout holds triangles only) */
+  const bool wide = dev->bvh_width > 2 && !dev->data_host.bvh.have_curves;
+  kg->bvhw_nodes = wide ? dev->bvhw : nullptr;
+  kg->bvhw_object_root = wide ? dev->bvhw_object_root : nullptr;
+  kg->tri_index_identity = wide ? dev->tri_index_identity : 0;
   kg->have_instancing = dev->have_instancing;
+  kg->have_curves = dev->data_host.bvh.have_curves ? 1 : 0;
   return true;
 }
 
@@ -804,7 +1224,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
  * the arrays are a few tens of MB even for BMW27-class scenes). */
 static int ensure_bvhw(hipcy_device *dev)
 {
-  if (dev->bvh_width == 2 || !dev->bvhw_dirty) {
+  if (dev->bvh_width == 2 || !dev->bvhw_dirty || dev->data_host.bvh.have_curves) {
     return 0;
   }
   auto nodes = dev->globals.find("__bvh_nodes");
@@ -1028,6 +1448,7 @@ void hipcy_destroy(hipcy_device *dev)
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
+  if (dev->cont_rec) hipFree(dev->cont_rec);
   if (dev->sort_queue) hipFree(dev->sort_queue);
   if (dev->sort_key) hipFree(dev->sort_key);
   if (dev->sort_hist) hipFree(dev->sort_hist);
@@ -1093,6 +1514,14 @@ int hipcy_mem_copy_to(hipcy_device *dev, uint64_t dst, const void *src, size_t b
       dev->features_dirty = true;
       if (g.first == "__object_flag") {
         dev->object_flags.assign((const uint32_t *)src, (const uint32_t *)src + std::min(bytes, g.second.bytes) / 4);
+      }
+      if (g.first == "__svm_nodes") {
+        /* the program scan of load_kernels reads this copy (node set -> variant) */
+        const size_t k = std::min(bytes, g.second.bytes) / sizeof(hc_uint4);
+        dev->svm_nodes.assign((const hc_uint4 *)src, (const hc_uint4 *)src + k);
+      }
+      if (g.first == "__shaders") {
+        dev->num_shaders = g.second.bytes / sizeof(hc_KernelShader);
       }
       if (g.first == "__bvh_nodes" || g.first == "__bvh_leaf_nodes" || g.first == "__prim_tri_index" ||
           g.first == "__prim_object" || g.first == "__object_node") {
@@ -1282,6 +1711,16 @@ int hipcy_set_bvh_width(hipcy_device *dev, int width)
   return 0;
 }
 
+int hipcy_set_traversal_budget(hipcy_device *dev, int first, int second)
+{
+  if (first < 0 || second < 0 || (first == 0) != (second == 0)) {
+    return set_error(dev, "set_traversal_budget: budgets must be >= 0, both zero or both positive");
+  }
+  dev->trav_budget[0] = first;
+  dev->trav_budget[1] = second;
+  return 0;
+}
+
 int hipcy_set_ray_sort(hipcy_device *dev, int mode)
 {
   if (mode != 0 && mode != 3 && mode != 5) {
@@ -1314,10 +1753,15 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
  * scene requests: DeviceRequestedFeatures max_nodes_group / nodes_features,
  * device/device.h:130-200) and reports whether the texture / converter / input
  * nodes are used, which selects the shading-kernel variant. */
-static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders, bool *uses_tex)
+static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
+                            const std::vector<void *> &tex_mem, bool *uses_tex)
 {
   *uses_tex = false;
   const size_t n = prog.size();
+  /* an image slot the kernel will read must have been allocated (hipcy_tex_alloc):
+   * kernel_tex_image_interp indexes __texture_info without a bound check; -1 is
+   * the reference's "missing image" id and is never read */
+  auto slot_ok = [&](int id) { return id == -1 || (id >= 0 && (size_t)id < tex_mem.size() && tex_mem[id]); };
   if (num_shaders > n) {
     return "jump table larger than the program";
   }
@@ -1441,9 +1885,33 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           break;
         case NODE_TEX_IMAGE:
           len = 1 + (size_t)(((int)node.y > 0) ? (int)node.y : 0); /* UDIM tile nodes */
+          if (off + len > n) {
+            return "image texture: UDIM tile nodes past __svm_nodes";
+          }
+          if ((int)node.y <= 0) {
+            if (!slot_ok(-(int)node.y)) {
+              return "shader " + std::to_string(sh) + ": image texture slot " + std::to_string(-(int)node.y) +
+                     " was never allocated (tex_alloc)";
+            }
+          }
+          else {
+            for (size_t k = 1; k < len; k++) {
+              /* tile node: (tile, slot, tile, slot); an unused pair has tile -1 */
+              const hc_uint4 tn = prog[off + k];
+              if (((int)tn.x != -1 && !slot_ok((int)tn.y)) || ((int)tn.z != -1 && !slot_ok((int)tn.w))) {
+                return "shader " + std::to_string(sh) + ": UDIM tile image slot was never allocated (tex_alloc)";
+              }
+            }
+          }
           tex = true;
           break;
         case NODE_TEX_ENVIRONMENT:
+          if (!slot_ok((int)node.y)) {
+            return "shader " + std::to_string(sh) + ": environment texture slot " + std::to_string((int)node.y) +
+                   " was never allocated (tex_alloc)";
+          }
+          tex = true;
+          break;
         case NODE_GEOMETRY:
         case NODE_CONVERT:
         case NODE_HSV:
@@ -1492,10 +1960,14 @@ int hipcy_load_kernels(hipcy_device *dev)
            (d.integrator.max_bounce > 255 || d.integrator.transparent_max_bounce > 255))
     why = "transparent shadows with more than 255 bounces";
   else if (d.integrator.use_ambient_occlusion) why = "ambient occlusion";
+  else if (d.integrator.adaptive_stop_per_sample)
+    why = "adaptive_stop_per_sample (a CPU-device setting; this device filters at adaptive_step samples)";
   else if (d.background.portal_weight > 0.0f || d.background.num_portals) why = "light portals";
   else if (d.background.sun_weight > 0.0f) why = "sky texture sun sampling";
   else if (d.integrator.max_closures > CY_MAX_CLOSURE) why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
-  else if (d.bvh.have_motion || d.bvh.have_curves) why = "motion / curves";
+  else if (d.bvh.have_motion || d.bvh.use_bvh_steps) why = "motion blur (motion triangles / curves)";
+  else if (d.bvh.have_curves && (d.bvh.curve_subdivisions < 1 || d.bvh.curve_subdivisions > 16))
+    why = "curve_subdivisions outside 1..16";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
   else if (d.film.use_light_pass) why = "light passes";
   else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | (1 << 13) | (1 << 14))) != 0 ||
@@ -1526,7 +1998,14 @@ int hipcy_load_kernels(hipcy_device *dev)
       return set_error(dev, std::string("load_kernels: array not bound: ") + r);
     }
   }
-  why = svm_scan(dev->svm_nodes, dev->num_shaders, &dev->shade_tex);
+  if (d.bvh.have_curves) {
+    for (const char *r : {"__curves", "__curve_keys", "__prim_type"}) {
+      if (dev->globals.find(r) == dev->globals.end()) {
+        return set_error(dev, std::string("load_kernels: scene with curves, array not bound: ") + r);
+      }
+    }
+  }
+  why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, &dev->shade_tex);
   if (!why.empty()) {
     return set_error(dev, "load_kernels: unsupported shader: " + why);
   }
@@ -1682,10 +2161,55 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     p.d = get_event(dev, (*ev)++);
     HIP_CHECK(dev, hipEventRecord(p.a, s));
   }
+  /* iteration budget: non-instanced wide BVH only (the kernels' CAN_SUSPEND) */
+  const bool budget = dev->trav_budget[0] > 0 && W > 2 && !kg.have_instancing && !kg.have_curves && dev->cont_rec;
+  CyCont ca = {}, cb = {};
+  if (budget) {
+    const size_t cap = dev->cont_capacity;
+    ca.rec = dev->cont_rec + (size_t)(2 * ln.index) * CY_CONT_F4 * cap;
+    cb.rec = ca.rec + CY_CONT_F4 * cap;
+    ca.capacity = cb.capacity = (uint)cap;
+    ca.count = ln.cnt + 8;
+    cb.count = ln.cnt + 9;
+  }
+  /* closest, then (budget) the continuations: A -> B with the second budget,
+   * B to the end */
+  auto continuations = [&](bool shadow) -> int {
+    HIP_CHECK(dev, hipMemsetAsync(cb.count, 0, 4, s));
+    for (int k = 0; k < 2; k++) {
+      const CyCont &in = k == 0 ? ca : cb;
+      const CyCont &out = k == 0 ? cb : ca;
+      const int bud = k == 0 ? dev->trav_budget[1] : 0;
+      if (!shadow) {
+        auto kfn = W == 8 ? pick_closest_cont<8>(counters) : pick_closest_cont<4>(counters);
+        hipLaunchKernelGGL(kfn, dim3(CY_CONT_BLOCKS), block, 0, s, kg, dev->bufs, in, out, bud, err, dev->stats_dev);
+      }
+      else {
+        auto kfn = W == 8 ? pick_shadow_cont<8>(counters) : pick_shadow_cont<4>(counters);
+        hipLaunchKernelGGL(kfn, dim3(CY_CONT_BLOCKS), block, 0, s, kg, dev->bufs, ln.tile, in, out, bud, ln.q[qb],
+                           ln.cnt + qb, err, dev->stats_dev);
+      }
+    }
+    return 0;
+  };
   {
-    auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0);
-    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, queue_in,
-                       ln.cnt + qa, err, dev->stats_dev);
+    if (budget) {
+      HIP_CHECK(dev, hipMemsetAsync(ca.count, 0, 4, s));
+    }
+    if (budget) {
+      auto kfn = counters ? (W == 8 ? k_intersect_closest_budget<true, 8> : k_intersect_closest_budget<true, 4>)
+                          : (W == 8 ? k_intersect_closest_budget<false, 8> : k_intersect_closest_budget<false, 4>);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, queue_in,
+                         ln.cnt + qa, err, dev->stats_dev, dev->trav_budget[0], ca);
+      if (continuations(false) != 0) {
+        return -1;
+      }
+    }
+    else {
+      auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0, kg.have_curves != 0);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, queue_in,
+                         ln.cnt + qa, err, dev->stats_dev);
+    }
   }
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));
@@ -1700,9 +2224,23 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
                        ln.cnt + qs, ln.q[qb], ln.cnt + qb, err);
   }
   else {
-    auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0);
-    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
-                       ln.cnt + qb, err, dev->stats_dev);
+    if (budget) {
+      HIP_CHECK(dev, hipMemsetAsync(ca.count, 0, 4, s));
+    }
+    if (budget) {
+      auto kfn = counters ? (W == 8 ? k_intersect_shadow_budget<true, 8> : k_intersect_shadow_budget<true, 4>)
+                          : (W == 8 ? k_intersect_shadow_budget<false, 8> : k_intersect_shadow_budget<false, 4>);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
+                         ln.cnt + qb, err, dev->stats_dev, dev->trav_budget[0], ca);
+      if (continuations(true) != 0) {
+        return -1;
+      }
+    }
+    else {
+      auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0, kg.have_curves != 0);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
+                         ln.cnt + qb, err, dev->stats_dev);
+    }
   }
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.d, s));
@@ -1742,6 +2280,20 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     HIP_CHECK(dev, hipMalloc((void **)&dev->sort_hist,
                              (size_t)CY_SORT_BINS * (cap / CY_BLOCK + CY_LANES + 1) * sizeof(uint)));
     dev->sort_capacity = cap;
+  }
+  if (dev->trav_budget[0] > 0 && W > 2 && !kg.have_instancing && !kg.have_curves) {
+    /* continuation records: per lane two buffers of a quarter of the lane's slots */
+    const size_t cap = std::max<size_t>(65536, (n_slots / lanes + 3) / 4);
+    if (cap > dev->cont_capacity || lanes > (int)dev->cont_lanes) {
+      if (dev->cont_rec) {
+        HIP_CHECK(dev, hipFree(dev->cont_rec));
+        dev->cont_rec = nullptr;
+      }
+      dev->cont_capacity = 0;
+      HIP_CHECK(dev, hipMalloc((void **)&dev->cont_rec, (size_t)2 * CY_LANES * CY_CONT_F4 * cap * sizeof(hc_float4)));
+      dev->cont_capacity = cap;
+      dev->cont_lanes = CY_LANES;
+    }
   }
   PassLane ln[CY_LANES];
   /* the main stream's pending work (buffer zeroing, uploads) precedes the lanes */
@@ -2002,6 +2554,8 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     dev->stats.closest_ms = closest;
     dev->stats.shade_ms = shade;
     dev->stats.closest_launches = quads.size();
+    dev->stats.shadow_ms = shadow;
+    dev->stats.shadow_launches = quads.size();
   }
   if (dev->profiling & 2) {
     std::vector<CyStats> shards(2 * CY_STATS_SHARDS);
@@ -2014,6 +2568,8 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
         st[k].leaves += x.leaves;
         st[k].tris += x.tris;
         st[k].rays += x.rays;
+        st[k].lane_iters += x.lane_iters;
+        st[k].wave_iters += x.wave_iters;
       }
     }
     dev->stats.inner_nodes = st[0].nodes + st[1].nodes;
@@ -2023,6 +2579,12 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     dev->stats.closest_leaves = st[0].leaves;
     dev->stats.closest_tris = st[0].tris;
     dev->stats.tie_rays = st[0].rays;
+    dev->stats.closest_lane_iters = st[0].lane_iters;
+    dev->stats.closest_wave_iters = st[0].wave_iters;
+    dev->stats.shadow_nodes = st[1].nodes;
+    dev->stats.shadow_tris = st[1].tris;
+    dev->stats.shadow_lane_iters = st[1].lane_iters;
+    dev->stats.shadow_wave_iters = st[1].wave_iters;
   }
   return check_device_error(dev);
 }
@@ -2048,7 +2610,9 @@ int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t o
   build_globals(dev, &kg);
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
   const int W = kg.bvhw_nodes ? dev->bvh_width : 2;
-  hipLaunchKernelGGL(W == 8 ? k_test_intersect<8> : W == 4 ? k_test_intersect<4> : k_test_intersect<2>,
+  auto ktest = kg.have_curves ? k_test_intersect<2, true> :
+               W == 8 ? k_test_intersect<8> : W == 4 ? k_test_intersect<4> : k_test_intersect<2>;
+  hipLaunchKernelGGL(ktest,
                      dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,
                      (const float *)rays, (float *)out_f, (int *)out_i, n, any_hit, dev->counters + 3);
   HIP_CHECK(dev, hipGetLastError());

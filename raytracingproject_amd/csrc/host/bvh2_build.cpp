@@ -10,10 +10,20 @@
  *   bvh/bvh2.cpp:165-236 pack_nodes        (DFS order, leaves in their own array,
  *                                           child index ~i for leaves, root 0 or -1)
  *   bvh/bvh.cpp:279-321  pack_primitives   (prim_tri_index = 3*i, prim_tri_verts)
+ *   bvh/bvh2.cpp:133-163 pack_unaligned_node (7 x float4: vis0|UNALIGNED, vis1|UNALIGNED,
+ *                                           child0, child1 / child 0's node space /
+ *                                           child 1's node space, bvh_unaligned.cpp
+ *                                           compute_node_transform)
  * with a binned-SAH builder of its own (the reference's BVHBuild,
  * bvh/bvh_build.cpp:370+, is out of scope — SURVEY.md §2 row 25).  Any valid
  * BVH gives the same closest hits; parity is checked against the reference
  * kernel traversing these same arrays.
+ *
+ * Hair: curve segments are primitives of kind 2 with explicit boxes; leaves
+ * hold one primitive kind (BVHBuild::create_leaf_node); with unaligned nodes
+ * on (BVHParams.use_unaligned_nodes, set for scenes with curves) a subtree of
+ * curve segments only is bounded in an oriented space along its segments'
+ * mean direction, and its parent is packed as an unaligned node.
  *
  * C ABI (host only, no HIP): hcb_build / hcb_build_boxes, hcb_pack, hcb_free.
  */
@@ -61,11 +71,16 @@ struct Node {
   int lo = 0, hi = 0; /* prim range for leaves */
   uint32_t visibility = 0;
   bool leaf = false;
+  bool unaligned = false; /* curve-only subtree bounded in `space` */
+  double space[12];       /* node transform (3 rows of 4), unit box in this space */
 };
 
 struct Builder {
   const uint32_t *vis;
-  const int32_t *kind = nullptr; /* per primitive: 0 triangle, 1 object instance */
+  const int32_t *kind = nullptr; /* per primitive: 0 triangle, 1 object instance, 2 curve segment */
+  const uint32_t *ptype = nullptr; /* per primitive: packed prim type written into leaves (curves) */
+  const float *curve_cp = nullptr; /* per primitive: 4 Bezier control points + radius (16 floats) */
+  bool use_unaligned = false;
   int max_leaf;
 
   /* Leaves hold one primitive kind; an instance is always alone in its leaf
@@ -74,9 +89,76 @@ struct Builder {
   bool leaf_ok(int lo, int hi) const
   {
     if (!kind) return true;
-    int inst = 0;
-    for (int i = lo; i < hi; i++) inst += kind[order[i]] != 0;
-    return inst == 0 || (inst == 1 && hi - lo == 1);
+    int inst = 0, curve = 0;
+    for (int i = lo; i < hi; i++) {
+      inst += kind[order[i]] == 1;
+      curve += kind[order[i]] == 2;
+    }
+    if (inst) return inst == 1 && hi - lo == 1;
+    return curve == 0 || curve == hi - lo;
+  }
+
+  bool all_curves(int lo, int hi) const
+  {
+    if (!kind || !curve_cp) return false;
+    for (int i = lo; i < hi; i++) {
+      if (kind[order[i]] != 2) return false;
+    }
+    return hi > lo;
+  }
+
+  /* Oriented bounds of a curve-only range (BVHUnaligned::compute_aligned_space
+   * and compute_node_transform, bvh/bvh_unaligned.cpp:36-165, with a space of
+   * our own: z along the mean segment direction).  Writes the node transform
+   * that maps the box to the unit cube. */
+  void unaligned_space(int lo, int hi, double *out) const
+  {
+    double ax[3] = {0.0, 0.0, 0.0};
+    for (int i = lo; i < hi; i++) {
+      const float *c = curve_cp + 16 * (size_t)order[i];
+      double d[3] = {(double)c[12] - c[0], (double)c[13] - c[1], (double)c[14] - c[2]};
+      const double dot = d[0] * ax[0] + d[1] * ax[1] + d[2] * ax[2];
+      const double sgn = dot < 0.0 ? -1.0 : 1.0;
+      for (int a = 0; a < 3; a++) ax[a] += sgn * d[a];
+    }
+    double len = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+    double z[3] = {0.0, 0.0, 1.0};
+    if (len > 1e-30) {
+      for (int a = 0; a < 3; a++) z[a] = ax[a] / len;
+    }
+    double t[3] = {1.0, 0.0, 0.0};
+    if (std::fabs(z[0]) > 0.9) {
+      t[0] = 0.0;
+      t[1] = 1.0;
+    }
+    double x[3] = {t[1] * z[2] - t[2] * z[1], t[2] * z[0] - t[0] * z[2], t[0] * z[1] - t[1] * z[0]};
+    len = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    for (int a = 0; a < 3; a++) x[a] /= len;
+    double y[3] = {z[1] * x[2] - z[2] * x[1], z[2] * x[0] - z[0] * x[2], z[0] * x[1] - z[1] * x[0]};
+    const double *rows[3] = {x, y, z};
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    for (int i = lo; i < hi; i++) {
+      const float *c = curve_cp + 16 * (size_t)order[i];
+      const double r = std::max(std::max(c[3], c[7]), std::max(c[11], c[15]));
+      for (int k = 0; k < 4; k++) {
+        for (int a = 0; a < 3; a++) {
+          const double v = rows[a][0] * c[4 * k] + rows[a][1] * c[4 * k + 1] + rows[a][2] * c[4 * k + 2];
+          mn[a] = std::min(mn[a], v - r);
+          mx[a] = std::max(mx[a], v + r);
+        }
+      }
+    }
+    for (int a = 0; a < 3; a++) {
+      /* conservative: the kernel transforms in float */
+      const double pad = 1e-5 * (mx[a] - mn[a]) + 1e-6 * std::max(std::fabs(mn[a]), std::fabs(mx[a])) + 1e-12;
+      mn[a] -= pad;
+      mx[a] += pad;
+      const double inv = 1.0 / std::max(1e-18, mx[a] - mn[a]);
+      out[4 * a + 0] = rows[a][0] * inv;
+      out[4 * a + 1] = rows[a][1] * inv;
+      out[4 * a + 2] = rows[a][2] * inv;
+      out[4 * a + 3] = -mn[a] * inv;
+    }
   }
   std::vector<BBox> pbox;
   std::vector<float> cent; /* 3 per prim */
@@ -96,6 +178,10 @@ struct Builder {
       visibility |= vis[order[i]];
     }
     node.visibility = visibility;
+    if (use_unaligned && all_curves(lo, hi)) {
+      node.unaligned = true;
+      unaligned_space(lo, hi, node.space);
+    }
     const int n = hi - lo;
     int idx = (int)nodes.size();
     nodes.push_back(node);
@@ -218,7 +304,14 @@ struct hcb_ctx {
   Builder b;
   int root = 0;
   int n_inner = 0, n_leaf = 0;
+  int64_t node_rows = 0; /* float4 rows: 4 per aligned, 7 per unaligned inner node */
 };
+
+/* bvh2.cpp pack_inner: a node is packed unaligned when either child is. */
+static bool packs_unaligned(const Builder &b, const Node &nd)
+{
+  return !nd.leaf && (b.nodes[nd.child[0]].unaligned || b.nodes[nd.child[1]].unaligned);
+}
 
 static void *build_common(hcb_ctx *ctx, int n, int64_t *counts)
 {
@@ -237,9 +330,12 @@ static void *build_common(hcb_ctx *ctx, int n, int64_t *counts)
   }
   for (const Node &nd : b.nodes) {
     if (nd.leaf) ctx->n_leaf++;
-    else ctx->n_inner++;
+    else {
+      ctx->n_inner++;
+      ctx->node_rows += packs_unaligned(b, nd) ? 7 : 4;
+    }
   }
-  counts[0] = 4 * (int64_t)ctx->n_inner;
+  counts[0] = ctx->node_rows;
   counts[1] = ctx->n_leaf;
   counts[2] = b.nodes.empty() ? 0 : (b.nodes[ctx->root].leaf ? -1 : 0);
   return ctx;
@@ -261,16 +357,32 @@ void *hcb_build(int n, const float *verts, const uint32_t *vis, int max_leaf_siz
   return build_common(ctx, n, counts);
 }
 
+void *hcb_build_prims(int n, const float *boxes, const uint32_t *vis, const int32_t *kind, const uint32_t *ptype,
+                      const float *curve_cp, int use_unaligned, int max_leaf_size, int64_t *counts);
+
 /* Same over explicit primitive boxes (n x 6: min xyz, max xyz) with a kind per
  * primitive (0 triangle, 1 object instance): the top-level BVH of a scene with
  * instanced geometry (BVHBuild::add_reference_object, bvh/bvh_build.cpp:283). */
 void *hcb_build_boxes(
     int n, const float *boxes, const uint32_t *vis, const int32_t *kind, int max_leaf_size, int64_t *counts)
 {
+  return hcb_build_prims(n, boxes, vis, kind, nullptr, nullptr, 0, max_leaf_size, counts);
+}
+
+/* Same with curve segments (kind 2): ptype = packed primitive type per
+ * primitive (written into leaf.w), curve_cp = 16 floats per primitive (the
+ * segment's 4 Bezier control points, each xyz + radius; used for unaligned
+ * nodes when use_unaligned). */
+void *hcb_build_prims(int n, const float *boxes, const uint32_t *vis, const int32_t *kind, const uint32_t *ptype,
+                      const float *curve_cp, int use_unaligned, int max_leaf_size, int64_t *counts)
+{
   hcb_ctx *ctx = new hcb_ctx();
   Builder &b = ctx->b;
   b.vis = vis;
   b.kind = kind;
+  b.ptype = ptype;
+  b.curve_cp = curve_cp;
+  b.use_unaligned = use_unaligned != 0 && curve_cp != nullptr;
   b.max_leaf = max_leaf_size > 0 ? max_leaf_size : 8;
   b.pbox.resize(n);
   for (int i = 0; i < n; i++) {
@@ -281,7 +393,7 @@ void *hcb_build_boxes(
   return build_common(ctx, n, counts);
 }
 
-/* prim_type: PRIMITIVE_TRIANGLE for every slot. */
+/* Leaf prim type: PRIMITIVE_TRIANGLE, or the packed type given per primitive. */
 int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
 {
   hcb_ctx *ctx = (hcb_ctx *)h;
@@ -295,13 +407,14 @@ int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
   };
   std::vector<Entry> stack;
   int next_node = 0, next_leaf = 0;
+  auto node_rows = [&](int node) { return packs_unaligned(b, b.nodes[node]) ? 7 : 4; };
   const Node &root = b.nodes[ctx->root];
   if (root.leaf) {
     stack.push_back({ctx->root, next_leaf++});
   }
   else {
     stack.push_back({ctx->root, next_node});
-    next_node += 4;
+    next_node += node_rows(ctx->root);
   }
   auto encode = [&](int node, int idx) { return b.nodes[node].leaf ? ~idx : idx; };
   while (!stack.empty()) {
@@ -310,7 +423,7 @@ int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
     const Node &nd = b.nodes[e.node];
     if (nd.leaf) {
       float *d = leaves_out + 4 * (size_t)e.idx;
-      if (b.kind && b.kind[b.order[nd.lo]] != 0) {
+      if (b.kind && b.kind[b.order[nd.lo]] == 1) {
         /* object instance leaf: ~slot, 0, visibility, prim_type 0 */
         d[0] = bits_i(~nd.lo);
         d[1] = bits_i(0);
@@ -321,7 +434,8 @@ int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
         d[0] = bits_i(nd.lo);
         d[1] = bits_i(nd.hi);
         d[2] = bits_f(nd.visibility);
-        d[3] = bits_f(PRIMITIVE_TRIANGLE);
+        /* pack_leaf: the type of the leaf's first primitive */
+        d[3] = bits_f(b.ptype ? b.ptype[b.order[nd.lo]] : PRIMITIVE_TRIANGLE);
       }
     }
     else {
@@ -332,7 +446,7 @@ int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
         }
         else {
           idx[i] = next_node;
-          next_node += 4;
+          next_node += node_rows(nd.child[i]);
         }
       }
       stack.push_back({nd.child[0], idx[0]});
@@ -340,22 +454,49 @@ int hcb_pack(void *h, float *nodes_out, float *leaves_out, int32_t *order_out)
       const Node &c0 = b.nodes[nd.child[0]];
       const Node &c1 = b.nodes[nd.child[1]];
       float *d = nodes_out + 4 * (size_t)e.idx;
-      d[0] = bits_f(c0.visibility & ~PATH_RAY_NODE_UNALIGNED);
-      d[1] = bits_f(c1.visibility & ~PATH_RAY_NODE_UNALIGNED);
-      d[2] = bits_i(encode(nd.child[0], idx[0]));
-      d[3] = bits_i(encode(nd.child[1], idx[1]));
-      d[4] = c0.box.mn[0];
-      d[5] = c1.box.mn[0];
-      d[6] = c0.box.mx[0];
-      d[7] = c1.box.mx[0];
-      d[8] = c0.box.mn[1];
-      d[9] = c1.box.mn[1];
-      d[10] = c0.box.mx[1];
-      d[11] = c1.box.mx[1];
-      d[12] = c0.box.mn[2];
-      d[13] = c1.box.mn[2];
-      d[14] = c0.box.mx[2];
-      d[15] = c1.box.mx[2];
+      if (packs_unaligned(b, nd)) {
+        d[0] = bits_f(c0.visibility | PATH_RAY_NODE_UNALIGNED);
+        d[1] = bits_f(c1.visibility | PATH_RAY_NODE_UNALIGNED);
+        d[2] = bits_i(encode(nd.child[0], idx[0]));
+        d[3] = bits_i(encode(nd.child[1], idx[1]));
+        for (int k = 0; k < 2; k++) {
+          const Node &c = k == 0 ? c0 : c1;
+          double sp[12];
+          if (c.unaligned) {
+            memcpy(sp, c.space, sizeof(sp));
+          }
+          else {
+            /* an aligned child of an unaligned node: identity space (BVHNode::
+             * get_aligned_space), the node transform of its box */
+            for (int a = 0; a < 3; a++) {
+              const double pad = 1e-6 * std::max(std::fabs((double)c.box.mn[a]), std::fabs((double)c.box.mx[a]));
+              const double lo = (double)c.box.mn[a] - pad, hi = (double)c.box.mx[a] + pad;
+              const double inv = 1.0 / std::max(1e-18, hi - lo);
+              for (int j = 0; j < 3; j++) sp[4 * a + j] = (a == j) ? inv : 0.0;
+              sp[4 * a + 3] = -lo * inv;
+            }
+          }
+          for (int j = 0; j < 12; j++) d[4 + 12 * k + j] = (float)sp[j];
+        }
+      }
+      else {
+        d[0] = bits_f(c0.visibility & ~PATH_RAY_NODE_UNALIGNED);
+        d[1] = bits_f(c1.visibility & ~PATH_RAY_NODE_UNALIGNED);
+        d[2] = bits_i(encode(nd.child[0], idx[0]));
+        d[3] = bits_i(encode(nd.child[1], idx[1]));
+        d[4] = c0.box.mn[0];
+        d[5] = c1.box.mn[0];
+        d[6] = c0.box.mx[0];
+        d[7] = c1.box.mx[0];
+        d[8] = c0.box.mn[1];
+        d[9] = c1.box.mn[1];
+        d[10] = c0.box.mx[1];
+        d[11] = c1.box.mx[1];
+        d[12] = c0.box.mn[2];
+        d[13] = c1.box.mn[2];
+        d[14] = c0.box.mx[2];
+        d[15] = c1.box.mx[2];
+      }
     }
   }
   memcpy(order_out, b.order.data(), sizeof(int32_t) * b.order.size());

@@ -180,7 +180,9 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
                          uint *cnt_leaves,
                          uint *cnt_tris,
                          CY_LDS CyStackEntry *lds_ring,
-                         bool *tie_out)
+                         bool *tie_out,
+                         int budget,
+                         CyTravCursor *cur)
 {
   /* ring column of this thread (device) or a local array (host) */
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -190,14 +192,15 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   CyStackEntry *ring = host_ring;
   (void)lds_ring;
 #endif
-  int top = 0;    /* ring slot of the next push */
-  int n_ring = 0; /* valid ring entries (0 .. CY_LDS_STACKW) */
-  int n_over = 0; /* entries in the overflow arrays */
+  int top = cur ? cur->top : 0;       /* ring slot of the next push */
+  int n_ring = cur ? cur->n_ring : 0; /* valid ring entries (0 .. CY_LDS_STACKW) */
+  int n_over = 0;                     /* entries in the overflow arrays */
   int over_node[CY_OVER_STACK];
   float over_t[CY_OVER_STACK];
   bool found_hit = false;
 
-  bool tie = false; /* two hits inside the window of the current best */
+  bool tie = cur ? cur->tie : false; /* two hits inside the window of the current best */
+  int iters = 0;
   /* culling bound: the best distance widened by the tie window (recomputed
    * where used rather than kept in a register) */
 #define CY_T_CULL ((any_hit || !CY_EXACT_TIES) ? isect->t : isect->t * (1.0f + CY_TIE_EPS))
@@ -206,9 +209,25 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
   constexpr int Q = W / 4; /* float4 per array */
-  int code = root;
+  int code = cur ? cur->code : root;
+  if (cur) {
+    cur->suspended = false;
+  }
 
   while (true) {
+    if (cur && budget > 0) {
+      /* out of iterations: stop before processing `code` (never with entries
+       * in the private overflow arrays, which do not outlive this call) */
+      if (iters >= budget && n_over == 0) {
+        cur->code = code;
+        cur->top = top;
+        cur->n_ring = n_ring;
+        cur->tie = tie;
+        cur->suspended = true;
+        break;
+      }
+      iters++;
+    }
     if (code >= 0) {
       /* inner node: test the W child boxes */
       n_nodes++;

@@ -1600,7 +1600,8 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
                       uint *err)
 {
   int label;
-  const cfloat3 Ng = sd->Ng;
+  /* bsdf.h:124-126: curves sample against the closure's smooth normal */
+  const cfloat3 Ng = (sd->type & PRIMITIVE_ALL_CURVE) ? sc->N : sd->Ng;
   switch (sc->type) {
     case CLOSURE_BSDF_DIFFUSE_ID:
       label = bsdf_diffuse_sample(sc, Ng, randu, randv, eval, omega_in, pdf);
@@ -1684,7 +1685,9 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
 CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, float *pdf)
 {
   cfloat3 eval;
-  if (dot3(sd->Ng, omega_in) >= 0.0f) {
+  /* bsdf.h:506-508: curves evaluate against the smooth normal */
+  const cfloat3 Ng_eval = (sd->type & PRIMITIVE_ALL_CURVE) ? sd->N : sd->Ng;
+  if (dot3(Ng_eval, omega_in) >= 0.0f) {
     switch (sc->type) {
       case CLOSURE_BSDF_DIFFUSE_ID:
         eval = bsdf_diffuse_eval_reflect(sc, omega_in, pdf);

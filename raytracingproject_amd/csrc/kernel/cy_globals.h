@@ -37,7 +37,9 @@
   X(hc_KernelShader, __shaders) \
   X(float, __lookup_table) \
   X(uint32_t, __sample_pattern_lut) \
-  X(hc_TextureInfo, __texture_info)
+  X(hc_TextureInfo, __texture_info) \
+  X(hc_float4, __curves) \
+  X(hc_float4, __curve_keys)
 
 typedef struct CyGlobals {
   const hc_KernelData *data;
@@ -56,6 +58,9 @@ typedef struct CyGlobals {
   /* 1 when some object keeps its own transform (instanced geometry): enables
    * the instance paths of shading and light sampling (uniform branch) */
   int have_instancing;
+  /* KernelBVH.have_curves: hair segments in the BVH (BVH2 traversal with
+   * unaligned nodes and curve leaves; shading reads __prim_type) */
+  int have_curves;
 } CyGlobals;
 
 #endif /* CY_GLOBALS_H */

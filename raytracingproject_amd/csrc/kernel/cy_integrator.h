@@ -77,6 +77,7 @@ typedef struct CyTile {
 
 typedef struct CyStats {
   unsigned long long nodes, leaves, tris, rays;
+  unsigned long long lane_iters, wave_iters; /* loop iterations: per lane summed, per wave max summed */
 } CyStats; /* [0] closest-hit traversal, [1] shadow traversal */
 
 CY_FN hc_float4 mkf4(float x, float y, float z, float w)
@@ -528,7 +529,9 @@ CY_FN bool shadow_blocked_transparent(
   const uint max_hits = (uint)(transparent_max_bounce - state->transparent_bounce - 1);
   CyIsect hits[CY_SHADOW_MAX_HITS];
   uint num_hits = 0;
-  const bool blocked = bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+  const bool blocked = kg->have_curves ?
+                           bvh2_shadow_all<true, true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
+                           bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
   if (blocked || num_hits == 0) {
     return blocked;
   }
@@ -830,7 +833,8 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
 
   const bool hit = as_int(is4.w) != PRIM_NONE;
-  const int type = hit ? PRIMITIVE_TRIANGLE : 0;
+  /* isect->type: the primitive's packed type (a curve's carries its segment) */
+  const int type = hit ? (kg->have_curves ? (int)kg->__prim_type[as_int(is4.w)] : PRIMITIVE_TRIANGLE) : 0;
 
   /* kernel_path_lamp_emission (kernel_path.h:86-113): lamps hit by the ray
    * segment since the last non-transparent bounce, MIS-weighted

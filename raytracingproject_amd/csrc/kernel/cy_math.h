@@ -132,6 +132,11 @@ CY_FN float safe_sqrtf(float f)
 {
   return sqrtf(cmax(f, 0.0f));
 }
+/* util_math.h:591 */
+CY_FN float inversesqrtf(float f)
+{
+  return (f > 0.0f) ? 1.0f / sqrtf(f) : 0.0f;
+}
 CY_FN float xor_signmask(float x, int y)
 {
   return int_as_float(as_int(x) ^ y);

@@ -482,11 +482,104 @@ CY_FN float bvh_instance_pop(
   return t;
 }
 
+#include "cy_curve.h"
+
+/* One BVH2 inner node (bvh_nodes.h): the aligned two-child slab test
+ * (bvh_aligned_node_intersect :31-77) or, in scenes with curves, the
+ * oriented-box test of a node whose first word carries PATH_RAY_NODE_UNALIGNED
+ * (bvh_unaligned_node_intersect :79-135: each child's box is the unit cube in
+ * the affine space stored for it, 7 float4 per node).  Returns the traverse
+ * mask; dist = entry distances. */
+CY_FN bool bvh_unaligned_node_intersect_child(const hc_float4 *nodes, int node_addr, int child, cfloat3 P,
+                                              cfloat3 dir, float t, float *dist)
+{
+  const int child_addr = node_addr + child * 3;
+  const hc_float4 sx = nodes[child_addr + 1], sy = nodes[child_addr + 2], sz = nodes[child_addr + 3];
+  struct cy_tfm space;
+  space.x.x = sx.x, space.x.y = sx.y, space.x.z = sx.z, space.x.w = sx.w;
+  space.y.x = sy.x, space.y.y = sy.y, space.y.z = sy.z, space.y.w = sy.w;
+  space.z.x = sz.x, space.z.y = sz.y, space.z.z = sz.z, space.z.w = sz.w;
+  const cfloat3 aligned_dir = transform_direction(&space, dir);
+  const cfloat3 aligned_P = transform_point(&space, P);
+  const cfloat3 nrdir = neg3(rcp3(aligned_dir));
+  const cfloat3 lower_xyz = mul3(aligned_P, nrdir);
+  const cfloat3 upper_xyz = sub3(lower_xyz, nrdir);
+  const float near_x = cmin(lower_xyz.x, upper_xyz.x);
+  const float near_y = cmin(lower_xyz.y, upper_xyz.y);
+  const float near_z = cmin(lower_xyz.z, upper_xyz.z);
+  const float far_x = cmax(lower_xyz.x, upper_xyz.x);
+  const float far_y = cmax(lower_xyz.y, upper_xyz.y);
+  const float far_z = cmax(lower_xyz.z, upper_xyz.z);
+  const float tnear = max4(0.0f, near_x, near_y, near_z);
+  const float tfar = min4(t, far_x, far_y, far_z);
+  *dist = tnear;
+  return tnear <= tfar;
+}
+
+template<bool HAIR>
+CY_FN int bvh2_node_intersect(const hc_float4 *nodes, int node_addr, hc_float4 cnodes, cfloat3 P, cfloat3 dir,
+                              cfloat3 idir, float t, uint visibility, float *c0min_o, float *c1min_o)
+{
+  if (HAIR && (as_uint(cnodes.x) & PATH_RAY_NODE_UNALIGNED)) {
+    int mask = 0;
+    if (bvh_unaligned_node_intersect_child(nodes, node_addr, 0, P, dir, t, c0min_o)) {
+      if (as_uint(cnodes.x) & visibility) {
+        mask |= 1;
+      }
+    }
+    if (bvh_unaligned_node_intersect_child(nodes, node_addr, 1, P, dir, t, c1min_o)) {
+      if (as_uint(cnodes.y) & visibility) {
+        mask |= 2;
+      }
+    }
+    return mask;
+  }
+  const hc_float4 node0 = nodes[node_addr + 1];
+  const hc_float4 node1 = nodes[node_addr + 2];
+  const hc_float4 node2 = nodes[node_addr + 3];
+  float c0lox = (node0.x - P.x) * idir.x;
+  float c0hix = (node0.z - P.x) * idir.x;
+  float c0loy = (node1.x - P.y) * idir.y;
+  float c0hiy = (node1.z - P.y) * idir.y;
+  float c0loz = (node2.x - P.z) * idir.z;
+  float c0hiz = (node2.z - P.z) * idir.z;
+  float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
+  float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
+  float c1lox = (node0.y - P.x) * idir.x;
+  float c1hix = (node0.w - P.x) * idir.x;
+  float c1loy = (node1.y - P.y) * idir.y;
+  float c1hiy = (node1.w - P.y) * idir.y;
+  float c1loz = (node2.y - P.z) * idir.z;
+  float c1hiz = (node2.w - P.z) * idir.z;
+  float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
+  float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
+  *c0min_o = c0min;
+  *c1min_o = c1min;
+  return (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
+         (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
+}
+
+/* Resumable traversal (iteration budget, hipcy_set_traversal_budget): the
+ * position of a traversal that ran out of iterations -- the next stack code to
+ * process, the LDS ring's top and fill, the near-tie flag -- so that it can
+ * continue in a later launch, bit for bit as if it had not stopped.  The ring
+ * entries themselves are saved and restored by the caller (hipcycles.hip
+ * cont_save / cont_load).  A traversal with entries in the private overflow
+ * arrays never suspends. */
+struct CyTravCursor {
+  int code;
+  int top;
+  int n_ring;
+  bool tie;
+  bool suspended;
+};
+
 /* Forward declaration: the wide traversal of one instance's BVH (cy_bvhw.h). */
 template<int W, bool any_hit>
 CY_FN bool bvhw_traverse(const CyGlobals *kg, int root, cfloat3 P, cfloat3 dir, cfloat3 idir, int object,
                          uint visibility, CyIsect *isect, uint *err, uint *cnt_nodes, uint *cnt_leaves,
-                         uint *cnt_tris, CY_LDS CyStackEntry *lds_ring, bool *tie_out);
+                         uint *cnt_tris, CY_LDS CyStackEntry *lds_ring, bool *tie_out, int budget = 0,
+                         CyTravCursor *cur = nullptr);
 
 /* Closest hit / opaque any hit with the bound BVH2 in the reference's order
  * (bvh/bvh_traversal.h:34-227).  The first LDSN stack entries live in LDS,
@@ -499,7 +592,8 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg, int root, cfloat3 P, cfloat3 dir, 
  * depend on the visiting order (near-ties excepted: *tie, see bvhw_traverse), so
  * the sequence of instances entered -- and with it every bvh_instance_push/pop
  * rounding of t -- is the reference's. */
-template<bool any_hit, bool INST = true, int WI = 2, int LDSN = CY_LDS_STACK, int LDS_STRIDE = CY_BLOCK>
+template<bool any_hit, bool INST = true, int WI = 2, int LDSN = CY_LDS_STACK, int LDS_STRIDE = CY_BLOCK,
+         bool HAIR = false>
 CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           const CyRay *ray,
                           uint visibility,
@@ -545,28 +639,9 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
       while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
         n_nodes++;
         const hc_float4 cnodes = nodes[node_addr + 0];
-        const hc_float4 node0 = nodes[node_addr + 1];
-        const hc_float4 node1 = nodes[node_addr + 2];
-        const hc_float4 node2 = nodes[node_addr + 3];
-        const float t = isect->t;
-        float c0lox = (node0.x - P.x) * idir.x;
-        float c0hix = (node0.z - P.x) * idir.x;
-        float c0loy = (node1.x - P.y) * idir.y;
-        float c0hiy = (node1.z - P.y) * idir.y;
-        float c0loz = (node2.x - P.z) * idir.z;
-        float c0hiz = (node2.z - P.z) * idir.z;
-        float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
-        float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
-        float c1lox = (node0.y - P.x) * idir.x;
-        float c1hix = (node0.w - P.x) * idir.x;
-        float c1loy = (node1.y - P.y) * idir.y;
-        float c1hiy = (node1.w - P.y) * idir.y;
-        float c1loz = (node2.y - P.z) * idir.z;
-        float c1hiz = (node2.w - P.z) * idir.z;
-        float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
-        float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
-        int traverse_mask = (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
-                            (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
+        float c0min, c1min;
+        const int traverse_mask = bvh2_node_intersect<HAIR>(nodes, node_addr, cnodes, P, dir, idir, isect->t,
+                                                            visibility, &c0min, &c1min);
 
         node_addr = as_int(cnodes.z);
         int node_addr_child1 = as_int(cnodes.w);
@@ -629,6 +704,21 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
                     return true;
                   }
                 }
+              }
+            }
+          }
+          else if (HAIR && (type & PRIMITIVE_ALL_CURVE)) {
+            /* curve segments (bvh_traversal.h:166-184) */
+            for (; prim_addr < prim_addr2; prim_addr++) {
+              n_tris++;
+              const uint curve_type = kg->__prim_type[prim_addr];
+              if (curve_intersect(kg, isect, P, dir, visibility, object, prim_addr, curve_type) && any_hit) {
+                if (cnt_nodes) {
+                  *cnt_nodes += n_nodes;
+                  *cnt_leaves += n_leaves;
+                  *cnt_tris += n_tris;
+                }
+                return true;
               }
             }
           }
@@ -697,7 +787,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
  * (hits holds max_hits + 1 entries) until one whose shader has no transparent
  * shadow, or more than max_hits of them, blocks the light.  Hits inside an
  * instance get their t scaled to world space at the instance pop. */
-template<bool INST>
+template<bool INST, bool HAIR = false>
 CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
                            const CyRay *ray,
                            CyIsect *hits,
@@ -723,28 +813,9 @@ CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
     do {
       while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
         const hc_float4 cnodes = nodes[node_addr + 0];
-        const hc_float4 node0 = nodes[node_addr + 1];
-        const hc_float4 node1 = nodes[node_addr + 2];
-        const hc_float4 node2 = nodes[node_addr + 3];
-        const float t = isect_t;
-        float c0lox = (node0.x - P.x) * idir.x;
-        float c0hix = (node0.z - P.x) * idir.x;
-        float c0loy = (node1.x - P.y) * idir.y;
-        float c0hiy = (node1.z - P.y) * idir.y;
-        float c0loz = (node2.x - P.z) * idir.z;
-        float c0hiz = (node2.z - P.z) * idir.z;
-        float c0min = max4(0.0f, cmin(c0lox, c0hix), cmin(c0loy, c0hiy), cmin(c0loz, c0hiz));
-        float c0max = min4(t, cmax(c0lox, c0hix), cmax(c0loy, c0hiy), cmax(c0loz, c0hiz));
-        float c1lox = (node0.y - P.x) * idir.x;
-        float c1hix = (node0.w - P.x) * idir.x;
-        float c1loy = (node1.y - P.y) * idir.y;
-        float c1hiy = (node1.w - P.y) * idir.y;
-        float c1loz = (node2.y - P.z) * idir.z;
-        float c1hiz = (node2.w - P.z) * idir.z;
-        float c1min = max4(0.0f, cmin(c1lox, c1hix), cmin(c1loy, c1hiy), cmin(c1loz, c1hiz));
-        float c1max = min4(t, cmax(c1lox, c1hix), cmax(c1loy, c1hiy), cmax(c1loz, c1hiz));
-        const int traverse_mask = (((c0max >= c0min) && (as_uint(cnodes.x) & visibility)) ? 1 : 0) |
-                                  (((c1max >= c1min) && (as_uint(cnodes.y) & visibility)) ? 2 : 0);
+        float c0min, c1min;
+        const int traverse_mask = bvh2_node_intersect<HAIR>(nodes, node_addr, cnodes, P, dir, idir, isect_t,
+                                                            visibility, &c0min, &c1min);
         node_addr = as_int(cnodes.z);
         int node_addr_child1 = as_int(cnodes.w);
         if (traverse_mask == 3) {
@@ -775,25 +846,39 @@ CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
           const uint type = as_uint(leaf.w);
           node_addr = stack[stack_ptr];
           --stack_ptr;
-          if ((type & PRIMITIVE_ALL) != PRIMITIVE_TRIANGLE) {
+          const bool curves = HAIR && (type & PRIMITIVE_ALL_CURVE);
+          if ((type & PRIMITIVE_ALL) != PRIMITIVE_TRIANGLE && !curves) {
             cy_set_error(err, CY_ERR_PRIMITIVE, type);
             return true;
           }
           for (; prim_addr < prim_addr2; prim_addr++) {
-            const uint tri_vindex = kg->__prim_tri_index[prim_addr];
-            const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
-            float tt, uu, vv;
-            if (ray_triangle_intersect(P, dir, isect_t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt) &&
-                (kg->__prim_visibility[prim_addr] & visibility)) {
-              CyIsect *h = &hits[*num_hits];
-              h->prim = prim_addr;
-              h->object = object;
-              h->type = PRIMITIVE_TRIANGLE;
-              h->u = uu;
-              h->v = vv;
-              h->t = tt;
-              const int prim = (int)kg->__prim_index[prim_addr];
-              const int shader = (int)kg->__tri_shader[prim];
+            CyIsect *h = &hits[*num_hits];
+            bool hit;
+            int shader;
+            if (curves) {
+              /* bvh_shadow_all.h:161-169: the record's t bounds the curve test */
+              h->t = isect_t;
+              hit = curve_intersect(kg, h, P, dir, visibility, object, prim_addr, kg->__prim_type[prim_addr]);
+              shader = hit ? as_int(kg->__curves[kg->__prim_index[prim_addr]].z) : 0;
+            }
+            else {
+              const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+              const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+              float tt, uu, vv;
+              hit = ray_triangle_intersect(P, dir, isect_t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv,
+                                           &tt) &&
+                    (kg->__prim_visibility[prim_addr] & visibility);
+              if (hit) {
+                h->prim = prim_addr;
+                h->object = object;
+                h->type = PRIMITIVE_TRIANGLE;
+                h->u = uu;
+                h->v = vv;
+                h->t = tt;
+              }
+              shader = hit ? (int)kg->__tri_shader[kg->__prim_index[prim_addr]] : 0;
+            }
+            if (hit) {
               const int flag = kg->__shaders[shader & SHADER_MASK].flags;
               if (!(flag & SD_HAS_TRANSPARENT_SHADOW)) {
                 return true;
@@ -957,8 +1042,9 @@ CY_FN cfloat3 object_normal_transform(const CyGlobals *kg, int object, cfloat3 N
   return normalize3(transform_direction_transposed(object_itfm(kg, object), N));
 }
 
-/* kernel_shader.h:54-153 (static triangles, instanced or not; no differentials:
- * the differentials only feed texture filtering, which this node subset lacks). */
+/* kernel_shader.h:54-153 (static triangles and curves, instanced or not; no
+ * differentials: the differentials only feed texture filtering, which this
+ * node subset lacks). */
 CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *isect, const CyRay *ray)
 {
   sd->object = (isect->object == OBJECT_NONE) ? (int)kg->__prim_object[isect->prim] : isect->object;
@@ -970,13 +1056,18 @@ CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *i
   sd->u = isect->u;
   sd->v = isect->v;
 
-  cfloat3 Ng = triangle_normal(kg, sd);
-  sd->shader = (int)kg->__tri_shader[sd->prim];
-  sd->P = triangle_refine(kg, isect, ray);
-  sd->Ng = Ng;
-  sd->N = Ng;
-  if ((uint)sd->shader & SHADER_SMOOTH_NORMAL) {
-    sd->N = triangle_smooth_normal(kg, Ng, sd->prim, sd->u, sd->v);
+  if (kg->have_curves && (sd->type & PRIMITIVE_ALL_CURVE)) {
+    curve_shader_setup(kg, sd, isect, ray);
+  }
+  else {
+    cfloat3 Ng = triangle_normal(kg, sd);
+    sd->shader = (int)kg->__tri_shader[sd->prim];
+    sd->P = triangle_refine(kg, isect, ray);
+    sd->Ng = Ng;
+    sd->N = Ng;
+    if ((uint)sd->shader & SHADER_SMOOTH_NORMAL) {
+      sd->N = triangle_smooth_normal(kg, Ng, sd->prim, sd->u, sd->v);
+    }
   }
   sd->I = neg3(ray->D);
   sd->flag |= kg->__shaders[(uint)sd->shader & SHADER_MASK].flags;

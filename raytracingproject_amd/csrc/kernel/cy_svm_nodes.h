@@ -114,10 +114,6 @@ CY_FN float safe_logf(float a, float b)
   }
   return safe_divide(cy_logf(a), cy_logf(b));
 }
-CY_FN float inversesqrtf(float f)
-{
-  return (f > 0.0f) ? 1.0f / sqrtf(f) : 0.0f;
-}
 CY_FN float safe_asinf(float a)
 {
   return cy_asinf(cy_clampf(a, -1.0f, 1.0f));

@@ -128,6 +128,13 @@ class HIPDevice:
         iteration: 0 off, 3 octant, 5 octant x major axis (hipcy_set_ray_sort)."""
         self._check(self.lib.hipcy_set_ray_sort(self.h, int(mode)))
 
+    def set_traversal_budget(self, first: int, second: int | None = None) -> None:
+        """Iteration budget of the wide traversal kernels (hipcy_set_traversal_budget):
+        traversals longer than `first` iterations continue in packed continuation
+        launches (then `second`, then unbounded).  0 disables."""
+        second = 2 * first if second is None else second
+        self._check(self.lib.hipcy_set_traversal_budget(self.h, int(first), int(second)))
+
     def set_slots(self, slots: int = 0, record_bytes: int = 0) -> None:
         """Path slots in flight and the per-pass sample-record budget (0 keeps a value)."""
         self._check(self.lib.hipcy_set_slots(self.h, int(slots), int(record_bytes)))

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # by `python -m raytracingproject_amd.build --variant NAME -D...`)
 DEVICE_LIB = os.environ.get("HIPCY_DEVICE_LIB") or os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
-ABI_VERSION = 4  # HIPCY_ABI_VERSION in include/hipcycles.h
+ABI_VERSION = 5  # HIPCY_ABI_VERSION in include/hipcycles.h
 
 
 def device_lib_path() -> str:
@@ -41,6 +41,10 @@ def host_lib():
         lib.hcb_build_boxes.restype = ctypes.c_void_p
         lib.hcb_build_boxes.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p]
+        lib.hcb_build_prims.restype = ctypes.c_void_p
+        lib.hcb_build_prims.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p]
         lib.hcb_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.hcb_free.argtypes = [ctypes.c_void_p]
         lib.hcb_background_cdf.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -68,6 +72,10 @@ class Stats(ctypes.Structure):
         ("closest_nodes", ctypes.c_uint64), ("closest_leaves", ctypes.c_uint64), ("closest_tris", ctypes.c_uint64),
         ("bvh_width", ctypes.c_int32), ("bvh_depth", ctypes.c_int32), ("bvh_bytes", ctypes.c_uint64),
         ("tie_rays", ctypes.c_uint64),
+        ("closest_lane_iters", ctypes.c_uint64), ("closest_wave_iters", ctypes.c_uint64),
+        ("shadow_nodes", ctypes.c_uint64), ("shadow_tris", ctypes.c_uint64),
+        ("shadow_lane_iters", ctypes.c_uint64), ("shadow_wave_iters", ctypes.c_uint64),
+        ("shadow_ms", ctypes.c_double), ("shadow_launches", ctypes.c_uint64),
     ]
 
 
@@ -100,6 +108,7 @@ DEVICE_SYMBOLS = {
     "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_bvh_width": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_ray_sort": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hipcy_set_traversal_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "hipcy_set_bvh_leaf_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_slots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "hipcy_intersect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),

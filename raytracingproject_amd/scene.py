@@ -36,6 +36,10 @@ SD_HAS_CONSTANT_EMISSION = 1 << 27
 SD_OBJECT_TRANSFORM_APPLIED = 1 << 2
 SD_OBJECT_NEGATIVE_SCALE_APPLIED = 1 << 3
 PRIMITIVE_TRIANGLE = 1
+PRIMITIVE_CURVE_THICK = 1 << 2
+PRIMITIVE_CURVE_RIBBON = 1 << 4
+PRIMITIVE_ALL_CURVE = (1 << 2) | (1 << 3) | (1 << 4) | (1 << 5)
+PRIMITIVE_NUM_TOTAL = 6  # kernel_types.h:713: the segment index is packed above the type bits
 PASSMASK_COMBINED = 1 << 1
 BVH_LAYOUT_BVH2 = 1
 FILTER_TABLE_SIZE = 1024
@@ -486,6 +490,20 @@ class Mesh:
 
 
 @dataclass
+class Hair:
+    """A curves object (render/hair.h Hair): Catmull-Rom curves through keys
+    (K, 3, world space) with a radius per key; curve c uses keys
+    curve_first[c] .. curve_first[c] + curve_nkeys[c] - 1 and has
+    curve_nkeys[c] - 1 segments (Hair::Curve::num_segments)."""
+
+    keys: np.ndarray
+    radius: np.ndarray
+    curve_first: np.ndarray
+    curve_nkeys: np.ndarray
+    shader: np.ndarray | int = 0  # per curve, or one material index
+
+
+@dataclass
 class Instance:
     """An object placing geometry with a transform (render/object.h).  Geometry
     used by one object has its transform applied on the host; geometry shared
@@ -587,6 +605,11 @@ class Scene:
     adaptive_sampling: bool = False
     adaptive_threshold: float = 0.0
     adaptive_min_samples: int = 0
+    # hair (SceneParams hair_shape / hair_subdivisions, render/scene.h:173-210):
+    # curves render as "ribbon" or "thick"; curve_subdivisions = 1 << hair_subdivisions
+    hairs: list = field(default_factory=list)
+    hair_shape: str = "ribbon"
+    hair_subdivisions: int = 3
 
 
 def _has_displacement(m) -> bool:
@@ -889,6 +912,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         abi.set_transform(kobjects[i].itfm, np.linalg.inv(np.vstack([tfm, [0, 0, 0, 1]]))[:3])
         kobjects[i].shadow_terminator_offset = 1.0  # 1 / (1 - 0.5 * 0)
         kobjects[i].numverts = ob["numverts"]
+        kobjects[i].numkeys = ob.get("numkeys", 0)
         if ob["applied"]:
             object_flag[i] = SD_OBJECT_TRANSFORM_APPLIED
         object_node[i] = np.uint32(ob["node"] & 0xFFFFFFFF)
@@ -1092,10 +1116,12 @@ def compile_scene(scene: Scene) -> DeviceScene:
     # --- bvh
     kd.bvh.root = root
     kd.bvh.have_motion = 0
-    kd.bvh.have_curves = 0
+    kd.bvh.have_curves = int(g["ncurves"] > 0)  # object.cpp:553-628
     kd.bvh.bvh_layout = BVH_LAYOUT_BVH2
     kd.bvh.use_bvh_steps = 0
-    kd.bvh.curve_subdivisions = 4
+    # geometry.cpp:1096 scene->params.curve_subdivisions() (Embree's tessellation
+    # limit); scenes without curves keep the value this builder always wrote
+    kd.bvh.curve_subdivisions = min(max(1 << scene.hair_subdivisions, 1), 16) if g["ncurves"] else 4
 
     arrays = {
         "__bvh_nodes": nodes.astype(np.float32),
@@ -1119,6 +1145,15 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "__lookup_table": lookup,
         "__sample_pattern_lut": lut,
     }
+    if g["ncurves"]:
+        # Hair::pack_curves (render/hair.cpp): keys with radius, per curve the
+        # first key, key count and shader id (get_shader_id(shader, false))
+        curves = np.zeros((g["ncurves"], 4), dtype=np.uint32)
+        curves[:, 0] = g["curve_first"]
+        curves[:, 1] = g["curve_nkeys"]
+        curves[:, 2] = g["curve_shader"].astype(np.uint32) | np.uint32(SHADER_CAST_SHADOW | SHADER_AREA_LIGHT)
+        arrays["__curves"] = curves.view(np.float32)
+        arrays["__curve_keys"] = g["curve_keys"]
     if bg_map is not None:
         # filled at upload from the device's SHADER task (device.py upload_scene,
         # LightManager::device_update_background)
@@ -1127,6 +1162,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
                                                                 dtype=np.float32)
     info = {
         "triangles": ntri,
+        "curves": g["ncurves"],
+        "curve_segments": g["nsegments"],
         "objects": nobj,
         "instanced_objects": int(sum(not ob["applied"] for ob in objects)),
         "bvh_inner_nodes": nodes.shape[0] // 4,
@@ -1202,6 +1239,9 @@ def _pack_geometry(scene: Scene) -> dict:
             geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=False))
             geom_of[id(inst.mesh)] = len(geoms) - 1
         objects.append(dict(geom=geom_of[id(inst.mesh)], tfm=tfm, applied=False))
+    # hair objects: transforms applied, after the meshes (object order)
+    for hr in scene.hairs:
+        objects.append(dict(geom=None, hair=hr, tfm=ident, applied=True))
 
     # global triangle / vertex arrays, geometry order (prim_offset, vert_offset)
     toff = voff = 0
@@ -1218,8 +1258,12 @@ def _pack_geometry(scene: Scene) -> dict:
     tri_vnormal = np.zeros((nvert, 4), dtype=np.float32)
     tri_vnormal[:, :3] = np.concatenate([gm["nrm"] for gm in geoms])
     for ob in objects:
+        if ob["geom"] is None:
+            ob["tri_offset"], ob["ntri"], ob["numverts"] = 0, 0, 0
+            continue
         gm = geoms[ob["geom"]]
         ob["tri_offset"], ob["ntri"], ob["numverts"] = gm["tri_offset"], gm["t"].shape[0], gm["v"].shape[0]
+    hair = _pack_hair(objects, scene.hair_shape)
 
     vis_obj = PATH_RAY_ALL_VISIBILITY & ~(PATH_RAY_SHADOW_OPAQUE_CATCHER | PATH_RAY_SHADOW_TRANSPARENT_CATCHER)
 
@@ -1234,6 +1278,9 @@ def _pack_geometry(scene: Scene) -> dict:
             ref_obj.append(np.array([oi]))
     ref_tri = np.concatenate(ref_tri) if ref_tri else np.zeros(0, np.int64)
     ref_obj = np.concatenate(ref_obj) if ref_obj else np.zeros(0, np.int64)
+    if hair["nseg"]:
+        return _pack_geometry_with_curves(objects, geoms, ref_tri, ref_obj, tri_pos, ntri, nvert, tri_shader_idx,
+                                          tri_smooth, tri_vindex, tri_vnormal, vis_obj, hair)
     nref = len(ref_tri)
     is_inst = ref_tri < 0
     vis = np.full(nref, vis_obj, dtype=np.uint32)
@@ -1322,7 +1369,127 @@ def _pack_geometry(scene: Scene) -> dict:
                 leaves=np.concatenate(leaf_parts), root=root, prim_index=prim_index, prim_object=prim_object,
                 prim_type=prim_type, prim_visibility=prim_visibility, prim_tri_index=prim_tri_index,
                 prim_tri_verts=prim_tri_verts, tri_vindex=tri_vindex, tri_vnormal=tri_vnormal, objects=objects,
-                tri_pos_object=tri_pos_object)
+                tri_pos_object=tri_pos_object, ncurves=0, nsegments=0)
+
+
+def _pack_hair(objects: list, shape: str) -> dict:
+    """Hair::pack_curves (render/hair.cpp) over the hair objects in object
+    order, and one BVH reference per curve segment (BVHBuild::add_reference_curves,
+    bvh/bvh_build.cpp): packed type PRIMITIVE_PACK_SEGMENT(type, segment),
+    the segment's box and its Catmull-Rom span as 4 Bezier control points
+    (the box of which contains the segment; BoundBox of Hair::Curve::bounds_grow)."""
+    ptype0 = {"ribbon": PRIMITIVE_CURVE_RIBBON, "thick": PRIMITIVE_CURVE_THICK}[shape]
+    keys_l, first_l, nk_l, sh_l, seg_curve, seg_index, seg_obj = [], [], [], [], [], [], []
+    koff = coff = 0
+    for oi, ob in enumerate(objects):
+        hr = ob.get("hair")
+        if hr is None:
+            continue
+        k = np.asarray(hr.keys, dtype=np.float32).reshape(-1, 3)
+        r = np.asarray(hr.radius, dtype=np.float32).reshape(-1)
+        first = np.asarray(hr.curve_first, dtype=np.int64).reshape(-1)
+        nk = np.asarray(hr.curve_nkeys, dtype=np.int64).reshape(-1)
+        if len(r) != len(k) or (nk < 2).any() or (first + nk > len(k)).any():
+            raise ValueError("hair: curves need >= 2 keys inside the key array, one radius per key")
+        keys_l.append(np.concatenate([k, r[:, None]], axis=1))
+        first_l.append(first + koff)
+        nk_l.append(nk)
+        sh_l.append(np.broadcast_to(np.asarray(hr.shader, dtype=np.int64), first.shape))
+        nseg = nk - 1
+        seg_curve.append(np.repeat(np.arange(len(first)) + coff, nseg))
+        seg_index.append(np.concatenate([np.arange(n) for n in nseg]) if len(nseg) else np.zeros(0, np.int64))
+        seg_obj.append(np.full(int(nseg.sum()), oi))
+        ob["numkeys"] = len(k)
+        koff += len(k)
+        coff += len(first)
+    if not coff:
+        return dict(nseg=0, ncurves=0)
+    keys = np.concatenate(keys_l).astype(np.float32)
+    first = np.concatenate(first_l)
+    nk = np.concatenate(nk_l)
+    curve = np.concatenate(seg_curve)
+    seg = np.concatenate(seg_index).astype(np.int64)
+    k0 = first[curve] + seg
+    k1 = k0 + 1
+    ka = np.maximum(k0 - 1, first[curve])
+    kb = np.minimum(k1 + 1, first[curve] + nk[curve] - 1)
+    P = keys.astype(np.float64)
+    cp = np.stack([P[k0], P[k0] + (P[k1] - P[ka]) / 6.0, P[k1] - (P[kb] - P[k0]) / 6.0, P[k1]], axis=1)  # (S,4,4)
+    rmax = cp[:, :, 3].max(axis=1)
+    lo = cp[:, :, :3].min(axis=1) - rmax[:, None]
+    hi = cp[:, :, :3].max(axis=1) + rmax[:, None]
+    pad = 1e-6 * np.maximum(np.abs(lo), np.abs(hi)) + 1e-7 * (hi - lo)
+    boxes = np.concatenate([np.nextafter((lo - pad).astype(np.float32), -np.inf),
+                            np.nextafter((hi + pad).astype(np.float32), np.inf)], axis=1).astype(np.float32)
+    ptype = ((seg << PRIMITIVE_NUM_TOTAL) | ptype0).astype(np.uint32)
+    return dict(nseg=len(seg), ncurves=coff, keys=keys, first=first, nkeys=nk, shader=np.concatenate(sh_l),
+                seg_curve=curve, seg_obj=np.concatenate(seg_obj), ptype=ptype, boxes=boxes,
+                cp=cp.astype(np.float32).reshape(-1, 16))
+
+
+def _pack_geometry_with_curves(objects, geoms, ref_tri, ref_obj, tri_pos, ntri, nvert, tri_shader_idx, tri_smooth,
+                               tri_vindex, tri_vnormal, vis_obj, hair):
+    """The top-level BVH over triangles, instances and curve segments with
+    unaligned nodes for curve-only subtrees (BVHParams.use_unaligned_nodes,
+    geometry.cpp:1024-1025), and the primitive arrays (bvh.cpp:279-321:
+    curves get prim_index = curve, prim_tri_index = -1)."""
+    if (ref_tri < 0).any():
+        raise ValueError("scenes with curves: instanced geometry is not supported by this stand-in host")
+    nt = len(ref_tri)
+    ns = hair["nseg"]
+    kind = np.concatenate([np.zeros(nt, np.int32), np.full(ns, 2, np.int32)])
+    boxes = np.zeros((nt + ns, 6), dtype=np.float32)
+    tp = tri_pos[ref_tri] if nt else np.zeros((0, 3, 3), np.float32)
+    boxes[:nt, :3] = tp.min(1) if nt else boxes[:0, :3]
+    boxes[:nt, 3:] = tp.max(1) if nt else boxes[:0, 3:]
+    boxes[nt:] = hair["boxes"]
+    vis = np.full(nt + ns, vis_obj, dtype=np.uint32)
+    ptype = np.concatenate([np.full(nt, PRIMITIVE_TRIANGLE, np.uint32), hair["ptype"]])
+    cp = np.zeros((nt + ns, 16), dtype=np.float32)
+    cp[nt:] = hair["cp"]
+    lib = native.host_lib()
+    counts = np.zeros(3, dtype=np.int64)
+    bx, vs, kd, pt, cpc = (np.ascontiguousarray(a) for a in (boxes, vis, kind, ptype, cp))
+    h = lib.hcb_build_prims(nt + ns, bx.ctypes.data, vs.ctypes.data, kd.ctypes.data, pt.ctypes.data, cpc.ctypes.data,
+                            1, 8, counts.ctypes.data)
+    try:
+        nodes = np.zeros((max(int(counts[0]), 1), 4), dtype=np.float32)
+        leaves = np.zeros((max(int(counts[1]), 1), 4), dtype=np.float32)
+        order = np.zeros(nt + ns, dtype=np.int32)
+        lib.hcb_pack(h, nodes.ctypes.data, leaves.ctypes.data, order.ctypes.data)
+    finally:
+        lib.hcb_free(h)
+    nodes = nodes[: int(counts[0])] if counts[0] else nodes[:0]
+    root = int(counts[2])
+    is_curve = order >= nt
+    tri_of = np.where(is_curve, 0, order)
+    seg_of = np.where(is_curve, order - nt, 0)
+    prim_index = np.where(is_curve, hair["seg_curve"][seg_of], ref_tri[tri_of]).astype(np.int64)
+    prim_object = np.where(is_curve, hair["seg_obj"][seg_of], ref_obj[tri_of]).astype(np.int64)
+    prim_type = ptype[order].astype(np.int64)
+    prim_visibility = vis[order].astype(np.int64)
+    tri_slots = np.cumsum(~is_curve) - 1
+    prim_tri_index = np.where(is_curve, -1, 3 * tri_slots).astype(np.int64)
+    verts_all = tri_pos[ref_tri[order[~is_curve]]].reshape(-1, 3) if nt else np.zeros((0, 3), np.float32)
+    prim_tri_verts = np.ones((max(len(verts_all), 1), 4), dtype=np.float32)
+    prim_tri_verts[: len(verts_all), :3] = verts_all
+
+    def u32(a):
+        return (a.astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
+
+    prim_index, prim_object, prim_type = u32(prim_index), u32(prim_object), u32(prim_type)
+    prim_visibility, prim_tri_index = u32(prim_visibility), u32(prim_tri_index)
+    is_tri = prim_type == PRIMITIVE_TRIANGLE
+    tri_vindex[prim_index[is_tri].astype(np.int64), 3] = prim_tri_index[is_tri]
+    for ob in objects:
+        ob["node"] = 0
+    return dict(ntri=ntri, tri_shader_idx=tri_shader_idx, tri_smooth=tri_smooth, nodes=nodes, leaves=leaves,
+                root=root, prim_index=prim_index, prim_object=prim_object, prim_type=prim_type,
+                prim_visibility=prim_visibility, prim_tri_index=prim_tri_index, prim_tri_verts=prim_tri_verts,
+                tri_vindex=tri_vindex, tri_vnormal=tri_vnormal, objects=objects, tri_pos_object=tri_pos,
+                ncurves=hair["ncurves"], nsegments=ns, curve_first=hair["first"].astype(np.uint32),
+                curve_nkeys=hair["nkeys"].astype(np.uint32), curve_shader=hair["shader"],
+                curve_keys=hair["keys"])
 
 
 def _instance_bounds(v: np.ndarray, tfm) -> np.ndarray:
@@ -1480,4 +1647,5 @@ ELEMENT_BYTES = {
     "__shaders": ctypes.sizeof(abi.KernelShader), "__lookup_table": 4, "__sample_pattern_lut": 4,
     "__texture_info": 96,
     "__light_background_marginal_cdf": 8, "__light_background_conditional_cdf": 8,
+    "__curves": 16, "__curve_keys": 16,
 }

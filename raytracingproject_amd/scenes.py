@@ -464,12 +464,142 @@ def barbershop_standin(width=1920, height=1080, samples=512, detail=1.0) -> sc.S
                     max_transmission_bounce=12, name="barbershop_standin")
 
 
+# ---------------------------------------------------------------------------
+# Hair (curves): SURVEY.md §8(a8), §8(d) config JNK
+
+
+def _strands(rng, roots, normals, n_keys, length, radius_root, radius_tip, kink, gravity=0.0):
+    """Hair strands growing from `roots` along `normals`: n_keys keys per
+    strand, radius tapering root to tip, a random kink per key and an optional
+    droop along -y.  Returns (keys, radius, curve_first, curve_nkeys)."""
+    n = len(roots)
+    t = np.linspace(0.0, 1.0, n_keys)
+    keys = np.zeros((n, n_keys, 3), dtype=np.float64)
+    tang = normals / np.linalg.norm(normals, axis=1, keepdims=True)
+    side = np.cross(tang, rng.standard_normal((n, 3)))
+    side /= np.maximum(np.linalg.norm(side, axis=1, keepdims=True), 1e-9)
+    for k in range(n_keys):
+        wob = kink * np.sin(7.0 * t[k] + rng.random((n, 1)) * 6.28) * t[k]
+        droop = np.array([0.0, -gravity * length * t[k] ** 2, 0.0])
+        keys[:, k] = roots + tang * (length * t[k]) + side * wob * length + droop
+    radius = np.broadcast_to(radius_root + (radius_tip - radius_root) * t, (n, n_keys))
+    first = np.arange(n) * n_keys
+    return (keys.reshape(-1, 3).astype(np.float32), radius.reshape(-1).astype(np.float32), first,
+            np.full(n, n_keys))
+
+
+def _sphere_fur(rng, center, radius, n, n_keys, length, r_root, r_tip, kink, gravity=0.0):
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    roots = np.asarray(center) + d * radius
+    return _strands(rng, roots, d, n_keys, length, r_root, r_tip, kink, gravity)
+
+
+def hair_ball(width=48, height=48, samples=8, shape="ribbon", strands=300, name=None) -> sc.Scene:
+    """A furry ball on a floor (golden parity case for curves): strands with 5
+    keys (4 Catmull-Rom segments each) of two hair materials around a diffuse
+    core, lit by an area lamp and an emissive panel; unaligned BVH nodes bound
+    the curve-only subtrees."""
+    rng = np.random.default_rng(0x5EED + 40)
+    white = sc.diffuse((0.7, 0.7, 0.7))
+    core = sc.diffuse((0.5, 0.3, 0.2))
+    fur_a = sc.diffuse((0.8, 0.5, 0.25))
+    fur_b = sc.mix(0.3, sc.glossy((0.9, 0.8, 0.7), 0.25), sc.diffuse((0.3, 0.2, 0.1)))
+    light = sc.emission((1.0, 0.9, 0.8), 6.0)
+    materials = [white, core, fur_a, fur_b, light]
+    meshes = [sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0),
+              sc.Mesh(*_ellipsoid((0.0, 0.0, 0.0), (0.6, 0.6, 0.6), 24, 14), shader=1, smooth=True),
+              sc.Mesh(*_quad((-1.5, 2.5, -1.0), (-0.5, 2.5, -1.0), (-0.5, 2.5, 0.0), (-1.5, 2.5, 0.0)), shader=4)]
+    keys, rad, first, nk = _sphere_fur(rng, (0.0, 0.0, 0.0), 0.6, strands, 5, 0.55, 0.02, 0.004, 0.25, 0.3)
+    shader = np.where(np.arange(strands) % 3 == 0, 3, 2)
+    hairs = [sc.Hair(keys, rad, first, nk, shader=shader)]
+    lamps = [sc.Lamp("area", co=(1.5, 2.0, -1.5), direction=(-0.5, -0.7, 0.5), axisu=(1.0, 0.0, 0.0),
+                     axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=1.0, sizev=1.0, color=(1.0, 0.95, 0.9), strength=40.0)]
+    cam = sc.Camera(eye=(0.0, 0.6, -3.2), target=(0.0, 0.0, 0.0), fov=math.radians(45.0), nearclip=0.01,
+                    farclip=100.0)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.15, 0.17, 0.2), world_strength=1.0,
+                    samples=samples, lamps=lamps, hairs=hairs, hair_shape=shape,
+                    name=name or f"hair_ball_{shape}")
+
+
+def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="ribbon") -> sc.Scene:
+    """Junk Shop-class stand-in (SURVEY.md §8(d) config JNK): a cluttered shop
+    interior (shelves of boxes, a counter, barrels) with furry props -- a rug,
+    brushes and fur balls -- about 1.3M curve segments at detail 1, lit by
+    area lamps and a window panel.  (The JNK volume is not part of this
+    stand-in yet: volumes are not implemented.)"""
+    rng = np.random.default_rng(0x5EED + 4)
+    wall = sc.diffuse((0.55, 0.5, 0.45))
+    wood = sc.mix(0.2, sc.glossy((0.6, 0.45, 0.3), 0.3), sc.diffuse((0.45, 0.3, 0.18)))
+    metal = sc.glossy((0.8, 0.8, 0.85), 0.15)
+    cardboard = sc.diffuse((0.6, 0.48, 0.32))
+    fur1 = sc.diffuse((0.75, 0.6, 0.4))
+    fur2 = sc.mix(0.25, sc.glossy((0.9, 0.85, 0.8), 0.3), sc.diffuse((0.25, 0.2, 0.15)))
+    rug = sc.diffuse((0.5, 0.12, 0.1))
+    window = sc.emission((1.0, 0.97, 0.9), 8.0)
+    materials = [wall, wood, metal, cardboard, fur1, fur2, rug, window]
+    meshes = []
+    W, D, H = 10.0, 8.0, 4.0
+    meshes.append(sc.Mesh(*_quad((-W, 0, -D), (W, 0, -D), (W, 0, D), (-W, 0, D)), shader=1))
+    meshes.append(sc.Mesh(*_quad((-W, H, -D), (-W, H, D), (W, H, D), (W, H, -D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((-W, 0, D), (W, 0, D), (W, H, D), (-W, H, D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((-W, 0, -D), (-W, 0, D), (-W, H, D), (-W, H, -D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((W, 0, -D), (W, H, -D), (W, H, D), (W, 0, D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((-3, 1.2, D - 0.01), (3, 1.2, D - 0.01), (3, 3.5, D - 0.01),
+                                 (-3, 3.5, D - 0.01)), shader=7))
+    # shelves with boxes along the walls
+    for side in (-1, 1):
+        x = side * (W - 0.6)
+        for level in range(4):
+            y = 0.5 + level * 0.9
+            meshes.append(sc.Mesh(*_box((x, y, 0.0), (1.0, 0.06, 12.0)), shader=1))
+            nb = int(10 * detail) + 4
+            for b in range(nb):
+                sz = 0.25 + 0.3 * rng.random()
+                meshes.append(sc.Mesh(*_box((x, y + sz / 2 + 0.03, -5.5 + 11.0 * (b + rng.random() * 0.5) / nb),
+                                            (sz, sz, sz), rng.random() * 3.0), shader=3))
+    # counter and barrels
+    meshes.append(sc.Mesh(*_box((0.0, 0.55, 2.5), (5.0, 1.1, 1.0)), shader=1))
+    for k in range(6):
+        cx, cz = -4.0 + 1.6 * k, -4.5 + (k % 2)
+        v, t = _cylinder(0.45, 1.1, 32)
+        meshes.append(sc.Mesh(v + np.array([cx, 0.0, cz], dtype=np.float32), t, shader=2))
+    # fur: a rug, fur balls on the counter, brushes
+    n_rug = int(220000 * detail)
+    roots = np.stack([rng.uniform(-2.5, 2.5, n_rug), np.full(n_rug, 0.0), rng.uniform(-2.0, 1.5, n_rug)], axis=1)
+    normals = np.tile([0.0, 1.0, 0.0], (n_rug, 1)) + 0.25 * rng.standard_normal((n_rug, 3))
+    k1, r1, f1, n1 = _strands(rng, roots, normals, 4, 0.09, 0.004, 0.001, 0.3)
+    hairs = [sc.Hair(k1, r1, f1, n1, shader=6)]
+    for b in range(5):
+        c = (-1.8 + 0.9 * b, 1.1 + 0.35, 2.5)
+        meshes.append(sc.Mesh(*_ellipsoid(c, (0.3, 0.3, 0.3), 20, 12), shader=4))
+        kb, rb, fb, nb_ = _sphere_fur(rng, c, 0.3, int(40000 * detail), 5, 0.25, 0.006, 0.001, 0.3, 0.4)
+        hairs.append(sc.Hair(kb, rb, fb, nb_, shader=4 + (b % 2)))
+    for b in range(3):
+        x = 6.0 - 1.2 * b
+        roots = np.stack([x + rng.uniform(-0.3, 0.3, int(20000 * detail)), np.full(int(20000 * detail), 0.9),
+                          -2.0 + rng.uniform(-0.1, 0.1, int(20000 * detail))], axis=1)
+        meshes.append(sc.Mesh(*_box((x, 0.45, -2.0), (0.7, 0.9, 0.25)), shader=1))
+        kk, rr, ff, nn = _strands(rng, roots, np.tile([0.0, 1.0, 0.0], (len(roots), 1)), 4, 0.4, 0.003, 0.002, 0.1)
+        hairs.append(sc.Hair(kk, rr, ff, nn, shader=5))
+    lamps = [sc.Lamp("area", co=(0.0, H - 0.05, 0.0), direction=(0.0, -1.0, 0.0), axisu=(1.0, 0.0, 0.0),
+                     axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=3.0, sizev=2.0, color=(1.0, 0.9, 0.75), strength=600.0),
+             sc.Lamp("area", co=(-6.0, H - 0.05, -4.0), direction=(0.0, -1.0, 0.0), axisu=(1.0, 0.0, 0.0),
+                     axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=1.5, sizev=1.5, color=(0.9, 0.95, 1.0), strength=200.0)]
+    cam = sc.Camera(eye=(0.0, 2.2, -7.2), target=(0.0, 0.9, 2.0), fov=math.radians(55.0), nearclip=0.05,
+                    farclip=100.0)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.0, 0.0, 0.0), world_strength=0.0,
+                    samples=samples, filter_type="blackman_harris", filter_width=1.5, lamps=lamps, hairs=hairs,
+                    hair_shape=shape, max_bounce=8, name="junkshop_standin")
+
+
 CONFIGS = {
     "cornell_lamps": cornell_lamps,
     "cornell_instanced": cornell_instanced,
     "cornell_box": cornell_box,
     "bmw27_standin": bmw27_standin,
     "barbershop_standin": barbershop_standin,
+    "junkshop_standin": junkshop_standin,
 }
 
 

@@ -47,6 +47,10 @@ CASES = {
     # true-displacement materials (their displacement programs are only run by
     # SHADER_EVAL_DISPLACE, tests/golden/displace.npz; the render uses the surfaces)
     "cornell_displace": lambda: scenes.cornell_displace(48, 48, 8),
+    # hair curves (geom_curve_intersect.h): Catmull-Rom ribbons and thick
+    # curves in a BVH with unaligned nodes (bvh_nodes.h:79-153)
+    "hair_ribbon": lambda: scenes.hair_ball(48, 48, 8, shape="ribbon"),
+    "hair_thick": lambda: scenes.hair_ball(48, 48, 8, shape="thick"),
 }
 
 # Cases whose render needs the device's host-side step loop (adaptive sampling:
@@ -54,6 +58,9 @@ CASES = {
 # path_trace); the host emulation renders single passes, so these are checked
 # on the GPU only (test_gpu_parity).
 HOST_LOOP_CASES = {"cornell_adaptive"}
+# Scenes with curves: the device traverses the bound BVH2 (unaligned nodes,
+# curve leaves) at every requested width; the wide layout holds triangles only.
+CURVE_CASES = {"hair_ribbon", "hair_thick"}
 EMU_CASES = [n for n in CASES if n not in HOST_LOOP_CASES]
 
 # SHADER_EVAL_DISPLACE (tests/golden/displace.npz)

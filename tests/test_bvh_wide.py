@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import native_build as nb
-from parity_cases import EMU_CASES, PATH_RAY_SHADOW_OPAQUE, compile_case, load_golden, with_background_golden
+from parity_cases import CURVE_CASES, EMU_CASES, PATH_RAY_SHADOW_OPAQUE, compile_case, load_golden, with_background_golden
 
 RMSE_TOL = 1e-4
 VARIANTS = [(4, 0), (8, 0), (4, 4), (8, 8)]
@@ -27,7 +27,7 @@ def emu():
     return nb.host_emu(libm_sincos=True)
 
 
-@pytest.fixture(scope="module", params=[(n, w, m) for n in EMU_CASES for w, m in VARIANTS],
+@pytest.fixture(scope="module", params=[(n, w, m) for n in EMU_CASES if n not in CURVE_CASES for w, m in VARIANTS],
                 ids=lambda p: f"{p[0]}-w{p[1]}-m{p[2]}")
 def case(request, emu):
     name, width, merge = request.param

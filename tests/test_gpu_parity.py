@@ -202,3 +202,29 @@ def test_render_with_ray_sort_matches_reference(name, mode, device):
     finally:
         device.set_ray_sort(0)
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), name
+
+
+@pytest.mark.parametrize("budget", [(1, 2), (3, 5), (12, 24)])
+@pytest.mark.parametrize("width", [4, 8])
+@pytest.mark.parametrize("name", ["cornell_64", "bmw_small", "cornell_lamps", "world_mis", "closures_principled"])
+def test_render_with_traversal_budget_matches_reference(name, width, budget, device):
+    """Iteration budget (hipcy_set_traversal_budget): closest and shadow
+    traversals stop after `budget[0]` iterations, are saved as continuation
+    records and resumed in packed launches (again suspended after budget[1]).
+    A resumed traversal continues with the same stack, hit and near-tie state,
+    so the film is bit-identical to the reference; (1, 2) suspends almost every
+    ray twice."""
+    if name not in CASES:
+        pytest.skip(f"{name} not a parity case")
+    ds = compile_case(name)
+    g = load_golden(name)
+    device.upload_scene(ds)
+    device.set_bvh_width(width)
+    device.set_traversal_budget(*budget)
+    try:
+        buf = device.render()
+        st = device.stats()
+    finally:
+        device.set_traversal_budget(0, 0)
+    assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), (name, budget)
+    assert st["closest_rays"] > 0

@@ -89,6 +89,10 @@ static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char *
   kg->bvhw_object_root = g_object_root;
   kg->have_instancing = 1; /* generic: the instance paths are always enabled on the host */
   kg->tri_index_identity = 0;
+  kg->have_curves = kg->data->bvh.have_curves ? 1 : 0;
+  if (kg->have_curves) {
+    kg->bvhw_nodes = nullptr; /* scenes with curves keep the BVH2 (hipcycles.hip build_globals) */
+  }
 }
 
 extern "C" void emu_set_width(int w)
@@ -125,6 +129,10 @@ static bool emu_traverse_impl(const CyGlobals *kg, const CyRay *ray, uint vis, C
     CyGlobals k2 = *kg;
     k2.bvhw_nodes = nullptr;
     return bvh2_intersect<any_hit>(&k2, ray, vis, isect, err, nullptr, nullptr, nullptr, nullptr);
+  }
+  if (kg->have_curves) {
+    return bvh2_intersect<any_hit, true, 2, CY_LDS_STACK, CY_BLOCK, true>(kg, ray, vis, isect, err, nn, nl, nt,
+                                                                         nullptr);
   }
   return bvh2_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
 }
