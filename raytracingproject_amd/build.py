@@ -139,6 +139,7 @@ def build_all(ref=True, force=False):
 if __name__ == "__main__":
     if "--variant" in sys.argv:
         name = sys.argv[sys.argv.index("--variant") + 1]
-        build_device(variant=name, defines=[a[2:] for a in sys.argv if a.startswith("-D")])
+        build_device(variant=name, defines=[a[2:] for a in sys.argv if a.startswith("-D")],
+                     traversal_only="--traversal-only" in sys.argv)
     else:
         build_all(ref="--no-ref" not in sys.argv, force="--force" in sys.argv)

@@ -59,8 +59,9 @@ template<int W, bool INST> __device__ __forceinline__ CY_LDS CyStackEntry *lds_r
   }
 }
 
-/* HAIR (scenes with curves, W = 2 only): unaligned nodes and curve leaves. */
-template<int W, bool any_hit, bool INST = true, bool HAIR = false>
+/* HAIR (scenes with curves, W = 2 only): unaligned nodes and curve leaves of
+ * the shapes HAIR selects (1 ribbons, 2 thick curves, 3 both). */
+template<int W, bool any_hit, bool INST = true, int HAIR = 0>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
                                                uint *n_tris, LdsStack<W, INST> *lds, bool *tie = nullptr)
@@ -263,7 +264,7 @@ __device__ __forceinline__ void cont_suspend(const CyGlobals *kg, const CyCont &
  * (ray replacement) was measured 2x slower on the BMW stand-in (the refill path
  * with camera-ray generation inside the traversal loop spills at the 80-VGPR
  * budget, and replacement rays break the camera rays' fetch coherence). */
-template<bool STATS, int W, bool INST, bool HAIR = false>
+template<bool STATS, int W, bool INST, int HAIR = 0>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  CyTile tile,
@@ -445,7 +446,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_closest_continu
 }
 
 /* Stage 3: occlusion of the light sample, deferred light add, finish + refill. */
-template<bool STATS, int W, bool INST, bool HAIR = false>
+template<bool STATS, int W, bool INST, int HAIR = 0>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
@@ -816,7 +817,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_sort_scatter(const int *queue, con
   }
 }
 
-template<int W, bool HAIR = false>
+template<int W, int HAIR = 0>
 __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const float *rays, float *out_f, int *out_i, int n, int any_hit, uint *err)
 {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1045,26 +1046,28 @@ __global__ void __launch_bounds__(CY_BLOCK) k_film_convert(CyFilm film, const fl
 
 /* Kernel instance for (traversal counters, BVH width, instancing). */
 struct ClosestK {
-  template<bool S, int W, bool I, bool H = false> static constexpr auto fn()
+  template<bool S, int W, bool I, int H = 0> static constexpr auto fn()
   {
     return k_intersect_closest<S, W, I, H>;
   }
 };
 struct ShadowK {
-  template<bool S, int W, bool I, bool H = false> static constexpr auto fn()
+  template<bool S, int W, bool I, int H = 0> static constexpr auto fn()
   {
     return k_intersect_shadow<S, W, I, H>;
   }
 };
-template<class K, bool S, bool I> static auto pick_width(int W, bool hair)
+template<class K, bool S, bool I> static auto pick_width(int W, int hair)
 {
   /* scenes with curves traverse the BVH2 (W = 2) with the hair node tests */
-  return hair ? K::template fn<S, 2, I, true>() :
+  return hair == 1 ? K::template fn<S, 2, I, 1>() :
+         hair == 2 ? K::template fn<S, 2, I, 2>() :
+         hair == 3 ? K::template fn<S, 2, I, 3>() :
          W == 8 ? K::template fn<S, 8, I>() :
          W == 4 ? K::template fn<S, 4, I>() :
                   K::template fn<S, 2, I>();
 }
-template<class K> static auto pick_kernel(bool stats, int W, bool inst, bool hair = false)
+template<class K> static auto pick_kernel(bool stats, int W, bool inst, int hair = 0)
 {
   return stats ? (inst ? pick_width<K, true, true>(W, hair) : pick_width<K, true, false>(W, hair))
                : (inst ? pick_width<K, false, true>(W, hair) : pick_width<K, false, false>(W, hair));
@@ -1160,6 +1163,7 @@ struct hipcy_device {
   size_t num_shaders = 0;             /* __shaders entries */
   bool shade_tex = false;             /* some shader uses texture / converter / input nodes */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
+  int curve_shapes = 0;               /* curve primitive shapes in __prim_type: 1 ribbon, 2 thick, 3 both */
   int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
@@ -1826,7 +1830,13 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
             case CLOSURE_BSDF_DIFFUSE_TOON_ID:
             case CLOSURE_BSDF_GLOSSY_TOON_ID:
+            case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node, random walk */
               break;
+            case CLOSURE_BSSRDF_CUBIC_ID:
+            case CLOSURE_BSSRDF_GAUSSIAN_ID:
+            case CLOSURE_BSSRDF_BURLEY_ID:
+              return "shader " + std::to_string(sh) +
+                     ": disk BSSRDF falloffs (cubic / gaussian / burley) are not implemented, random walk is";
             default:
               return "shader " + std::to_string(sh) + ": closure type " + std::to_string(ctype) +
                      " is not implemented";
@@ -1998,11 +2008,31 @@ int hipcy_load_kernels(hipcy_device *dev)
       return set_error(dev, std::string("load_kernels: array not bound: ") + r);
     }
   }
+  dev->curve_shapes = 0;
   if (d.bvh.have_curves) {
     for (const char *r : {"__curves", "__curve_keys", "__prim_type"}) {
       if (dev->globals.find(r) == dev->globals.end()) {
         return set_error(dev, std::string("load_kernels: scene with curves, array not bound: ") + r);
       }
+    }
+    /* which curve shapes occur (selects the hair kernels: the thick
+     * intersector alone sets their register budget) */
+    const GlobalBinding &pt = dev->globals["__prim_type"];
+    std::vector<uint32_t> types(pt.bytes / 4);
+    if (!types.empty()) {
+      HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+      HIP_CHECK(dev, hipMemcpy(types.data(), (const void *)pt.ptr, pt.bytes, hipMemcpyDeviceToHost));
+    }
+    for (uint32_t t : types) {
+      if (t & (CY_PRIMITIVE_CURVE_RIBBON | CY_PRIMITIVE_MOTION_CURVE_RIBBON)) {
+        dev->curve_shapes |= 1;
+      }
+      else if (t & (CY_PRIMITIVE_CURVE_THICK | CY_PRIMITIVE_MOTION_CURVE_THICK)) {
+        dev->curve_shapes |= 2;
+      }
+    }
+    if (dev->curve_shapes == 0) {
+      dev->curve_shapes = 3;
     }
   }
   why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, &dev->shade_tex);
@@ -2206,7 +2236,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
       }
     }
     else {
-      auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0, kg.have_curves != 0);
+      auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0, dev->curve_shapes);
       hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, cam_n, ln.slot_base, queue_in,
                          ln.cnt + qa, err, dev->stats_dev);
     }
@@ -2237,7 +2267,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
       }
     }
     else {
-      auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0, kg.have_curves != 0);
+      auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0, dev->curve_shapes);
       hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
                          ln.cnt + qb, err, dev->stats_dev);
     }
@@ -2610,7 +2640,7 @@ int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t o
   build_globals(dev, &kg);
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
   const int W = kg.bvhw_nodes ? dev->bvh_width : 2;
-  auto ktest = kg.have_curves ? k_test_intersect<2, true> :
+  auto ktest = kg.have_curves ? k_test_intersect<2, 3> :
                W == 8 ? k_test_intersect<8> : W == 4 ? k_test_intersect<4> : k_test_intersect<2>;
   hipLaunchKernelGGL(ktest,
                      dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,

@@ -1604,6 +1604,9 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
   const cfloat3 Ng = (sd->type & PRIMITIVE_ALL_CURVE) ? sc->N : sd->Ng;
   switch (sc->type) {
     case CLOSURE_BSDF_DIFFUSE_ID:
+#if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_BSSRDF_ID: /* the diffuse closure replacing a BSSRDF after its scatter step */
+#endif
       label = bsdf_diffuse_sample(sc, Ng, randu, randv, eval, omega_in, pdf);
       break;
 #if CY_CLOSURE_EXT
@@ -1614,6 +1617,7 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
       label = bsdf_translucent_sample(sc, Ng, randu, randv, eval, omega_in, pdf);
       break;
     case CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID:
+    case CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID:
       label = bsdf_principled_diffuse_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
     case CLOSURE_BSDF_PRINCIPLED_SHEEN_ID:
@@ -1690,6 +1694,9 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
   if (dot3(Ng_eval, omega_in) >= 0.0f) {
     switch (sc->type) {
       case CLOSURE_BSDF_DIFFUSE_ID:
+#if CY_CLOSURE_EXT
+      case CLOSURE_BSDF_BSSRDF_ID:
+#endif
         eval = bsdf_diffuse_eval_reflect(sc, omega_in, pdf);
         break;
 #if CY_CLOSURE_EXT
@@ -1697,6 +1704,7 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
         eval = bsdf_oren_nayar_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
       case CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID:
+      case CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID:
         eval = bsdf_principled_diffuse_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
       case CLOSURE_BSDF_PRINCIPLED_SHEEN_ID:

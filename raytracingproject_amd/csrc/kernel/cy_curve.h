@@ -587,7 +587,12 @@ CY_FN void curve_segment_keys(const CyGlobals *kg, int prim, int segment, cy_c4 
 }
 
 /* curve_intersect (:620-692), static curves: the segment of primitive slot
- * curveAddr against the ray (P, dir in the space of its BVH). */
+ * curveAddr against the ray (P, dir in the space of its BVH).  SHAPES selects
+ * the intersectors compiled in (bit 0 ribbon, bit 1 thick): the thick one
+ * alone sizes a traversal kernel's registers (an any-hit kernel with both
+ * needs 188 VGPRs, with ribbons only 128), so kernels are instantiated for
+ * the shapes a scene holds (hipcycles.hip curve_shapes). */
+template<int SHAPES = 3>
 CY_FN bool curve_intersect(const CyGlobals *kg, CyIsect *isect, cfloat3 P, cfloat3 dir, uint visibility, int object,
                            int curveAddr, uint type)
 {
@@ -599,6 +604,9 @@ CY_FN bool curve_intersect(const CyGlobals *kg, CyIsect *isect, cfloat3 P, cfloa
     return false;
   }
   if (type & (CY_PRIMITIVE_CURVE_RIBBON | CY_PRIMITIVE_MOTION_CURVE_RIBBON)) {
+    if (!(SHAPES & 1)) {
+      return false;
+    }
     const int subdivisions = KD->bvh.curve_subdivisions;
     if (ribbon_intersect(P, dir, subdivisions, curve, isect)) {
       isect->prim = curveAddr;
@@ -608,7 +616,7 @@ CY_FN bool curve_intersect(const CyGlobals *kg, CyIsect *isect, cfloat3 P, cfloa
     }
     return false;
   }
-  if (curve_intersect_recursive(P, dir, curve, isect)) {
+  if ((SHAPES & 2) && curve_intersect_recursive(P, dir, curve, isect)) {
     isect->prim = curveAddr;
     isect->object = object;
     isect->type = (int)type;

@@ -23,6 +23,7 @@
 #define CY_INTEGRATOR_H
 
 #include "cy_path.h"
+#include "cy_subsurface.h"
 
 /* Per-slot state, SoA of 16-byte records so every access is one dwordx4. */
 typedef struct CyPathBuffers {
@@ -530,7 +531,7 @@ CY_FN bool shadow_blocked_transparent(
   CyIsect hits[CY_SHADOW_MAX_HITS];
   uint num_hits = 0;
   const bool blocked = kg->have_curves ?
-                           bvh2_shadow_all<true, true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
+                           bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
                            bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
   if (blocked || num_hits == 0) {
     return blocked;
@@ -1015,10 +1016,50 @@ CY_FN bool shade_path(const CyGlobals *kg,
       }
     }
 
+    /* kernel_path_subsurface_scatter (kernel_path_subsurface.h:26-110): a
+     * picked BSSRDF moves the shading point to where the random walk leaves
+     * the object, with a diffuse closure carrying the walk's weight; light is
+     * connected there with the path's state, the bounce uses rng_offset +
+     * PRNG_BOUNCE_NUM (the indirect ray's state), and a walk that never leaves
+     * ends the path */
+    bool sss_bounce = false;
     if (!terminated) {
-      if (KD->integrator.use_ambient_occlusion || (sd.flag & SD_BSSRDF)) {
+      if (KD->integrator.use_ambient_occlusion) {
         cy_set_error(err, CY_ERR_FEATURE, 6);
       }
+#if CY_CLOSURE_EXT
+      if (sd.flag & SD_BSSRDF) {
+        float bssrdf_u, bssrdf_v;
+        path_state_rng_2D(kg, &state, PRNG_BSDF_U, &bssrdf_u, &bssrdf_v);
+        const CyClosure *sc = shader_bssrdf_pick(&sd, &throughput, &bssrdf_u);
+        if (sc) {
+          const int bssrdf_type = sc->type;
+          const float bssrdf_rough = bssrdf_roughness(sc);
+          CyIsect ss_hit;
+          cfloat3 ss_weight;
+          CyRay ss_ray;
+          if (CLOSURE_IS_DISK_BSSRDF(bssrdf_type)) {
+            cy_set_error(err, CY_ERR_CLOSURE, (uint)bssrdf_type); /* disk BSSRDF: up to 4 exit points */
+            terminated = true;
+          }
+          else if (subsurface_random_walk(kg, &sd, &state, sc, bssrdf_u, bssrdf_v, &ss_hit, &ss_weight, &ss_ray,
+                                          err)) {
+            shader_setup_from_subsurface(kg, &sd, &ss_hit, &ss_ray);
+            subsurface_scatter_setup_diffuse_bsdf(kg, &sd, bssrdf_type, bssrdf_rough, ss_weight, sd.N);
+            sss_bounce = true;
+          }
+          else {
+            terminated = true;
+          }
+        }
+      }
+#else
+      if (sd.flag & SD_BSSRDF) {
+        cy_set_error(err, CY_ERR_FEATURE, 6);
+      }
+#endif
+    }
+    if (!terminated) {
       /* Direct light: kernel_branched_path_surface_connect_light with one sample
        * (kernel_path_surface.h:23-140), light_sample + direct_emission
        * (kernel_emission.h:101-205). */
@@ -1129,6 +1170,9 @@ CY_FN bool shade_path(const CyGlobals *kg,
       }
 
       /* kernel_path_surface_bounce (kernel_path_surface.h:270-358) */
+      if (sss_bounce) {
+        state.rng_offset += PRNG_BOUNCE_NUM; /* hit_state of the subsurface indirect ray */
+      }
       if (sd.flag & SD_BSDF) {
         float bsdf_u, bsdf_v;
         path_state_rng_2D(kg, &state, PRNG_BSDF_U, &bsdf_u, &bsdf_v);

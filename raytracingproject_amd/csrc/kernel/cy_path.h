@@ -516,11 +516,11 @@ CY_FN bool bvh_unaligned_node_intersect_child(const hc_float4 *nodes, int node_a
   return tnear <= tfar;
 }
 
-template<bool HAIR>
+template<int HAIR>
 CY_FN int bvh2_node_intersect(const hc_float4 *nodes, int node_addr, hc_float4 cnodes, cfloat3 P, cfloat3 dir,
                               cfloat3 idir, float t, uint visibility, float *c0min_o, float *c1min_o)
 {
-  if (HAIR && (as_uint(cnodes.x) & PATH_RAY_NODE_UNALIGNED)) {
+  if (HAIR != 0 && (as_uint(cnodes.x) & PATH_RAY_NODE_UNALIGNED)) {
     int mask = 0;
     if (bvh_unaligned_node_intersect_child(nodes, node_addr, 0, P, dir, t, c0min_o)) {
       if (as_uint(cnodes.x) & visibility) {
@@ -592,8 +592,9 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg, int root, cfloat3 P, cfloat3 dir, 
  * depend on the visiting order (near-ties excepted: *tie, see bvhw_traverse), so
  * the sequence of instances entered -- and with it every bvh_instance_push/pop
  * rounding of t -- is the reference's. */
+/* HAIR: 0 triangles only, else the curve shapes compiled in (curve_intersect). */
 template<bool any_hit, bool INST = true, int WI = 2, int LDSN = CY_LDS_STACK, int LDS_STRIDE = CY_BLOCK,
-         bool HAIR = false>
+         int HAIR = 0>
 CY_FN bool bvh2_intersect(const CyGlobals *kg,
                           const CyRay *ray,
                           uint visibility,
@@ -707,12 +708,12 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
               }
             }
           }
-          else if (HAIR && (type & PRIMITIVE_ALL_CURVE)) {
+          else if (HAIR != 0 && (type & PRIMITIVE_ALL_CURVE)) {
             /* curve segments (bvh_traversal.h:166-184) */
             for (; prim_addr < prim_addr2; prim_addr++) {
               n_tris++;
               const uint curve_type = kg->__prim_type[prim_addr];
-              if (curve_intersect(kg, isect, P, dir, visibility, object, prim_addr, curve_type) && any_hit) {
+              if (curve_intersect<HAIR>(kg, isect, P, dir, visibility, object, prim_addr, curve_type) && any_hit) {
                 if (cnt_nodes) {
                   *cnt_nodes += n_nodes;
                   *cnt_leaves += n_leaves;
@@ -787,7 +788,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
  * (hits holds max_hits + 1 entries) until one whose shader has no transparent
  * shadow, or more than max_hits of them, blocks the light.  Hits inside an
  * instance get their t scaled to world space at the instance pop. */
-template<bool INST, bool HAIR = false>
+template<bool INST, int HAIR = 0>
 CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
                            const CyRay *ray,
                            CyIsect *hits,
@@ -846,7 +847,7 @@ CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
           const uint type = as_uint(leaf.w);
           node_addr = stack[stack_ptr];
           --stack_ptr;
-          const bool curves = HAIR && (type & PRIMITIVE_ALL_CURVE);
+          const bool curves = HAIR != 0 && (type & PRIMITIVE_ALL_CURVE);
           if ((type & PRIMITIVE_ALL) != PRIMITIVE_TRIANGLE && !curves) {
             cy_set_error(err, CY_ERR_PRIMITIVE, type);
             return true;
@@ -858,7 +859,7 @@ CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
             if (curves) {
               /* bvh_shadow_all.h:161-169: the record's t bounds the curve test */
               h->t = isect_t;
-              hit = curve_intersect(kg, h, P, dir, visibility, object, prim_addr, kg->__prim_type[prim_addr]);
+              hit = curve_intersect<HAIR>(kg, h, P, dir, visibility, object, prim_addr, kg->__prim_type[prim_addr]);
               shader = hit ? as_int(kg->__curves[kg->__prim_index[prim_addr]].z) : 0;
             }
             else {
@@ -1159,6 +1160,115 @@ CY_FN CyClosure *bsdf_alloc(CySD *sd, cfloat3 weight)
 #include "cy_closures.h"
 
 /* ---------------------------------------------------------------------------
+ * BSSRDF closures (closure/bssrdf.h:330-425).  A BSSRDF keeps its radius in
+ * the closure's T, its albedo in (alpha_x, alpha_y, ior) and the principled
+ * roughness in `extra` (float bits): the random-walk scatter step
+ * (cy_subsurface.h) reads only these.  Texture blur (which needs a second
+ * shader evaluation at the entry point, kernel_subsurface.h:141-172) is
+ * rejected when set. */
+#if CY_CLOSURE_EXT
+CY_FN cfloat3 bssrdf_radius(const CyClosure *sc)
+{
+  return sc->T;
+}
+CY_FN cfloat3 bssrdf_albedo(const CyClosure *sc)
+{
+  return mk3(sc->alpha_x, sc->alpha_y, sc->ior);
+}
+CY_FN float bssrdf_roughness(const CyClosure *sc)
+{
+  return int_as_float(sc->extra);
+}
+
+/* bssrdf_alloc (bssrdf.h:332-343) */
+CY_FN CyClosure *bssrdf_alloc(CySD *sd, cfloat3 weight)
+{
+  CyClosure *sc = closure_alloc(sd, CLOSURE_NONE_ID, weight);
+  if (sc == 0) {
+    return 0;
+  }
+  const float sample_weight = fabsf(average3(weight));
+  sc->sample_weight = sample_weight;
+  return (sample_weight >= CLOSURE_WEIGHT_CUTOFF) ? sc : 0;
+}
+
+/* bssrdf_burley_fitting / _compatible_mfp / _setup (bssrdf.h:196-220) */
+CY_FN float bssrdf_burley_fitting(float A)
+{
+  return 1.9f - A + 3.5f * (A - 0.8f) * (A - 0.8f);
+}
+
+/* bssrdf_setup (bssrdf.h:345-423): radii below BSSRDF_MIN_RADIUS move their
+ * channel's weight to a diffuse closure; the BSSRDF's sample weight counts its
+ * channels; burley-type profiles (and the random walk) remap the radius to the
+ * mean free path. */
+CY_FN int bssrdf_setup(CySD *sd, CyClosure *bssrdf, int type, cfloat3 radius, cfloat3 albedo, float roughness)
+{
+  int flag = 0;
+  int bssrdf_channels = 3;
+  cfloat3 diffuse_weight = mk3(0.0f, 0.0f, 0.0f);
+  if (radius.x < BSSRDF_MIN_RADIUS) {
+    diffuse_weight.x = bssrdf->weight.x;
+    bssrdf->weight.x = 0.0f;
+    radius.x = 0.0f;
+    bssrdf_channels--;
+  }
+  if (radius.y < BSSRDF_MIN_RADIUS) {
+    diffuse_weight.y = bssrdf->weight.y;
+    bssrdf->weight.y = 0.0f;
+    radius.y = 0.0f;
+    bssrdf_channels--;
+  }
+  if (radius.z < BSSRDF_MIN_RADIUS) {
+    diffuse_weight.z = bssrdf->weight.z;
+    bssrdf->weight.z = 0.0f;
+    radius.z = 0.0f;
+    bssrdf_channels--;
+  }
+  const cfloat3 bssrdf_N = bssrdf->N;
+  if (bssrdf_channels < 3) {
+    /* the type set before the diffuse setup is overwritten by it, as in the
+     * reference: these are plain (principled) diffuse closures */
+    CyClosure *bsdf = bsdf_alloc(sd, diffuse_weight);
+    if (type == CLOSURE_BSSRDF_PRINCIPLED_ID || type == CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) {
+      if (bsdf) {
+        bsdf->N = bssrdf_N;
+        bsdf->alpha_x = roughness;
+        bsdf->type = CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID;
+        flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
+      }
+    }
+    else if (bsdf) {
+      bsdf->N = bssrdf_N;
+      flag |= bsdf_diffuse_setup(bsdf);
+    }
+  }
+  if (bssrdf_channels > 0) {
+    bssrdf->type = type;
+    bssrdf->sample_weight = fabsf(average3(bssrdf->weight)) * (float)bssrdf_channels;
+    if (type == CLOSURE_BSSRDF_BURLEY_ID || type == CLOSURE_BSSRDF_PRINCIPLED_ID ||
+        type == CLOSURE_BSSRDF_RANDOM_WALK_ID || type == CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) {
+      const cfloat3 l = mul3f(radius, 0.25f * CY_1_PI_F);
+      const cfloat3 sfit = mk3(bssrdf_burley_fitting(albedo.x), bssrdf_burley_fitting(albedo.y),
+                               bssrdf_burley_fitting(albedo.z));
+      radius = div3(l, sfit);
+    }
+    flag |= SD_BSSRDF;
+  }
+  else {
+    bssrdf->type = type;
+    bssrdf->sample_weight = 0.0f;
+  }
+  bssrdf->T = radius;
+  bssrdf->alpha_x = albedo.x;
+  bssrdf->alpha_y = albedo.y;
+  bssrdf->ior = albedo.z;
+  bssrdf->extra = as_int(roughness);
+  return flag;
+}
+#endif
+
+/* ---------------------------------------------------------------------------
  * SVM interpreter subset (svm/svm.h:220-549, svm_closure.h, svm_value.h,
  * svm_fresnel.h).  Unknown nodes set CY_ERR_SVM_NODE and stop the shader.
  */
@@ -1322,7 +1432,19 @@ CY_FN void svm_node_principled_bsdf(const CyGlobals *kg,
       }
     }
     else if (subsurface > CLOSURE_WEIGHT_CUTOFF) {
-      cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID); /* subsurface scattering */
+      /* svm_closure.h:220-236 */
+      const cfloat3 subsurf_weight = mul3f(mul3(weight, mixed_ss_base_color), diffuse_weight);
+      CyClosure *bssrdf = bssrdf_alloc(sd, subsurf_weight);
+      if (bssrdf) {
+        const int subsurface_method = (int)data_node2.z;
+        const cfloat3 subsurface_radius = (data_cn_ssr.y != SVM_STACK_INVALID) ? svm_load3(stack, data_cn_ssr.y, err) :
+                                                                                 mk3(1.0f, 1.0f, 1.0f);
+        bssrdf->N = N;
+        sd->flag |= bssrdf_setup(sd, bssrdf, subsurface_method, mul3f(subsurface_radius, subsurface),
+                                 (subsurface_method == CLOSURE_BSSRDF_PRINCIPLED_ID) ? subsurface_color :
+                                                                                     mixed_ss_base_color,
+                                 roughness);
+      }
     }
   }
 
@@ -1681,6 +1803,26 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
         b->alpha_x = param1;
         b->alpha_y = param2;
         sd->flag |= bsdf_toon_setup(b, (int)type);
+      }
+      break;
+    }
+    case CLOSURE_BSSRDF_CUBIC_ID:
+    case CLOSURE_BSSRDF_GAUSSIAN_ID:
+    case CLOSURE_BSSRDF_BURLEY_ID:
+    case CLOSURE_BSSRDF_RANDOM_WALK_ID: {
+      /* svm_closure.h:880-905 (Subsurface Scattering node) */
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *bssrdf = bssrdf_alloc(sd, weight);
+      if (bssrdf) {
+        if (path_flag & PATH_RAY_DIFFUSE_ANCESTOR) {
+          param1 = 0.0f;
+        }
+        if (saturate(param2) > 0.0f) {
+          cy_set_error(err, CY_ERR_CLOSURE, 1000 + type); /* texture blur */
+        }
+        bssrdf->N = N;
+        sd->flag |= bssrdf_setup(sd, bssrdf, (int)type, mul3f(svm_load3(stack, data_node.z, err), param1),
+                                 sd->svm_closure_weight, 0.0f);
       }
       break;
     }

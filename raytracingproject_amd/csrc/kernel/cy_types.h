@@ -180,6 +180,12 @@ enum {
   CLOSURE_BSDF_BSSRDF_ID = 32,
   CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID = 33,
   CLOSURE_BSDF_TRANSPARENT_ID = 34,
+  CLOSURE_BSSRDF_CUBIC_ID = 35,
+  CLOSURE_BSSRDF_GAUSSIAN_ID = 36,
+  CLOSURE_BSSRDF_PRINCIPLED_ID = 37,
+  CLOSURE_BSSRDF_BURLEY_ID = 38,
+  CLOSURE_BSSRDF_RANDOM_WALK_ID = 39,
+  CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID = 40,
   CLOSURE_HOLDOUT_ID = 41,
   CLOSURE_BSDF_PRINCIPLED_ID = 45,
   NBUILTIN_CLOSURES = 46
@@ -198,6 +204,10 @@ enum {
     (type) <= CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID) || \
    ((type) == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID))
 #define CLOSURE_IS_HOLDOUT(type) ((type) == CLOSURE_HOLDOUT_ID)
+#define CLOSURE_IS_BSSRDF(type) ((type) >= CLOSURE_BSSRDF_CUBIC_ID && (type) <= CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID)
+#define CLOSURE_IS_DISK_BSSRDF(type) ((type) >= CLOSURE_BSSRDF_CUBIC_ID && (type) <= CLOSURE_BSSRDF_BURLEY_ID)
+#define BSSRDF_MIN_RADIUS 1e-8f   /* kernel_types.h:49-51 */
+#define BSSRDF_MAX_BOUNCES 256
 
 #define CLOSURE_WEIGHT_CUTOFF 1e-5f
 #define SVM_STACK_INVALID 255
@@ -214,6 +224,8 @@ enum {
   PRNG_LIGHT_V = 3,
   PRNG_LIGHT_TERMINATE = 4,
   PRNG_TERMINATE = 5,
+  PRNG_PHASE_CHANNEL = 6,
+  PRNG_SCATTER_DISTANCE = 7,
   PRNG_BOUNCE_NUM = 8
 };
 

@@ -74,6 +74,9 @@ CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID = 26
 CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID = 27
 CLOSURE_BSDF_SHARP_GLASS_ID = 29
 CLOSURE_BSDF_TRANSPARENT_ID = 34
+# Subsurface Scattering node falloffs (nodes.cpp SubsurfaceScatteringNode)
+SUBSURFACE_FALLOFFS = {"cubic": 35, "gaussian": 36, "burley": 38, "random_walk": 39}
+CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID = 40
 
 # Distribution enums of the glossy / anisotropic / glass / refraction nodes
 # (nodes.cpp GlossyBsdfNode, GlassBsdfNode, RefractionBsdfNode NODE_DEFINE)
@@ -86,6 +89,8 @@ REFRACTION_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFRACTION_ID, "ggx": CLOSURE_
                             "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID}
 CLOSURE_BSDF_PRINCIPLED_ID = 45
 CLOSURE_BSSRDF_PRINCIPLED_ID = 37
+# PrincipledBsdfNode subsurface_method (nodes.cpp:2706-2711)
+PRINCIPLED_SUBSURFACE_METHODS = {"burley": 37, "random_walk": 40}
 PRINCIPLED_DISTRIBUTIONS = {"ggx": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID, "multiscatter": 25}
 # PrincipledBsdfNode sockets and defaults (render/nodes.cpp:2720-2770)
 PRINCIPLED_DEFAULTS = {
@@ -130,6 +135,11 @@ class Closure:
     rotation: object = 0.0
     tangent: object = None
     params: dict | None = None  # principled: PRINCIPLED_DEFAULTS keys + normals
+    # subsurface: radius (vector), sharpness, texture blur (strength = scale)
+    radius: object = (0.1, 0.1, 0.1)
+    sharpness: object = 0.0
+    texture_blur: object = 0.0
+    subsurface_method: str = "burley"  # principled
     # material output "Displacement" (a vector socket, e.g. nodes.displacement),
     # displacement method "true": its own SVM program, run by SHADER_EVAL_DISPLACE
     displacement: object = None
@@ -147,6 +157,8 @@ class Closure:
             return GLASS_DISTRIBUTIONS["sharp" if sharp else self.distribution]
         if self.kind == "refraction":
             return REFRACTION_DISTRIBUTIONS["sharp" if sharp else self.distribution]
+        if self.kind == "subsurface":
+            return SUBSURFACE_FALLOFFS[self.distribution]
         return {"diffuse": CLOSURE_BSDF_DIFFUSE_ID, "translucent": CLOSURE_BSDF_TRANSLUCENT_ID,
                 "velvet": CLOSURE_BSDF_ASHIKHMIN_VELVET_ID, "diffuse_toon": CLOSURE_BSDF_DIFFUSE_TOON_ID,
                 "glossy_toon": CLOSURE_BSDF_GLOSSY_TOON_ID, "transparent": CLOSURE_BSDF_TRANSPARENT_ID}[self.kind]
@@ -159,6 +171,8 @@ class Closure:
             return 2
         if self.kind == "principled":
             return 8  # CLOSURE_IS_PRINCIPLED
+        if self.kind == "subsurface":
+            return 3  # CLOSURE_IS_BSSRDF
         return 1
 
     def closure_types(self) -> set:
@@ -186,7 +200,8 @@ class Closure:
         out = []
         for name, t in (("color", "color"), ("roughness", "float"), ("ior", "float"), ("strength", "float"),
                         ("fac", "float"), ("normal", "vector"), ("anisotropy", "float"), ("rotation", "float"),
-                        ("tangent", "vector")):
+                        ("tangent", "vector"), ("radius", "vector"), ("sharpness", "float"),
+                        ("texture_blur", "float")):
             v = getattr(self, name)
             if nodes.is_linked(v) and (self.kind == "mix") == (name == "fac"):
                 out.append((v, t))
@@ -242,7 +257,7 @@ def refraction(color, roughness, ior=1.45, normal=None, distribution="ggx"):
                    distribution=distribution)
 
 
-def principled(distribution="ggx", **params):
+def principled(distribution="ggx", subsurface_method="burley", **params):
     """Principled BSDF (nodes.cpp PrincipledBsdfNode, svm_closure.h:100-463).
     Parameters are PRINCIPLED_DEFAULTS keys (constants or sockets) plus the
     normal / clearcoat_normal / tangent vector sockets.  distribution is
@@ -255,7 +270,22 @@ def principled(distribution="ggx", **params):
         raise ValueError(f"principled: unknown parameters {sorted(unknown)}")
     p = dict(PRINCIPLED_DEFAULTS)
     p.update(params)
-    return Closure("principled", distribution=distribution, params=p)
+    if subsurface_method not in PRINCIPLED_SUBSURFACE_METHODS:
+        raise ValueError(f"principled: unknown subsurface_method {subsurface_method}")
+    return Closure("principled", distribution=distribution, params=p, subsurface_method=subsurface_method)
+
+
+def subsurface(color, scale=0.01, radius=(0.1, 0.1, 0.1), falloff="random_walk", texture_blur=0.0, sharpness=0.0,
+               normal=None):
+    """Subsurface Scattering node (nodes.cpp SubsurfaceScatteringNode, a
+    BSSRDF closure, svm_closure.h:880-905): falloff random_walk | burley |
+    cubic | gaussian (the device implements the random walk; disk falloffs
+    are refused at load_kernels).  texture_blur must be 0 (the reference's
+    node default is 1, which re-evaluates the shader at the entry point)."""
+    if falloff not in SUBSURFACE_FALLOFFS:
+        raise ValueError(f"subsurface: unknown falloff {falloff}")
+    return Closure("subsurface", _const_or_socket(color), strength=scale, radius=radius, distribution=falloff,
+                   texture_blur=texture_blur, sharpness=sharpness, normal=normal)
 
 
 def translucent(color, normal=None):
@@ -360,7 +390,7 @@ class SVMCompiler:
         else:
             emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in c.color)))
         normal_off = self.nc.link(c.normal, "vector") if nodes.is_linked(c.normal) else SVM_STACK_INVALID
-        tangent_off, param3_off = SVM_STACK_INVALID, SVM_STACK_INVALID
+        tangent_off, param3_off, param4_off = SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID
         # per node: (param1, param2) of BsdfNode::compile (nodes.cpp:2200-2800)
         if c.kind in ("diffuse", "velvet"):
             params = (c.roughness, None)
@@ -373,13 +403,19 @@ class SVMCompiler:
             param3_off = self.nc.assign(c.rotation, "float")
         elif c.kind == "glossy":
             params = (c.roughness, None)
+        elif c.kind == "subsurface":
+            # BsdfNode::compile(Scale, Texture Blur, Radius, Sharpness): radius and
+            # sharpness always stack-assigned
+            params = (c.strength, c.texture_blur)
+            param3_off = self.nc.assign(c.radius, "vector")
+            param4_off = self.nc.assign(c.sharpness, "float")
         else:  # glass, refraction (roughness, IOR); toons (size, smooth)
             params = (c.roughness, c.ior)
         p1, v1 = self._float_param(params[0]) if params[0] is not None else (SVM_STACK_INVALID, 0.0)
         p2, v2 = self._float_param(params[1]) if params[1] is not None else (SVM_STACK_INVALID, 0.0)
         emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))
         # data node: normal, tangent, param3, param4
-        emit((normal_off, tangent_off, param3_off, SVM_STACK_INVALID))
+        emit((normal_off, tangent_off, param3_off, param4_off))
         return out
 
     def emit_principled(self, c: Closure, mix_weight: int) -> list:
@@ -429,7 +465,8 @@ class SVMCompiler:
               self.uchar4(offs["sheen"], offs["sheen_tint"], offs["clearcoat"], offs["clearcoat_roughness"])))
         emit((self.uchar4(offs["ior"], offs["transmission"], offs["anisotropic_rotation"],
                           offs["transmission_roughness"]),
-              PRINCIPLED_DISTRIBUTIONS[c.distribution], CLOSURE_BSSRDF_PRINCIPLED_ID, SVM_STACK_INVALID))
+              PRINCIPLED_DISTRIBUTIONS[c.distribution], PRINCIPLED_SUBSURFACE_METHODS[c.subsurface_method],
+              SVM_STACK_INVALID))
         bc = const(p["base_color"], PRINCIPLED_DEFAULTS["base_color"])
         emit((base_off, *(f32bits(x) for x in bc)))
         emit((cc_normal_off, radius_off, SVM_STACK_INVALID, SVM_STACK_INVALID))

@@ -593,6 +593,128 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
                     hair_shape=shape, max_bounce=8, name="junkshop_standin")
 
 
+# ---------------------------------------------------------------------------
+# Subsurface scattering: SURVEY.md §8(a18), §8(d) config CLS
+
+
+def sss_cornell(width=48, height=48, samples=8, instanced=False) -> sc.Scene:
+    """Cornell box with random-walk subsurface scattering (golden parity case):
+    a Subsurface Scattering node sphere, a principled random-walk sphere
+    mixing subsurface with specular and sheen, a node mixing SSS with a
+    glossy layer, and (instanced=True) the same materials on instanced
+    geometry (local intersections through bvh_instance_push)."""
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    skin = sc.subsurface((0.9, 0.6, 0.5), scale=60.0, radius=(1.0, 0.4, 0.2))
+    wax = sc.principled(subsurface_method="random_walk", base_color=(0.9, 0.85, 0.7), subsurface=0.6,
+                        subsurface_color=(0.9, 0.7, 0.4), subsurface_radius=(40.0, 25.0, 15.0), specular=0.4,
+                        roughness=0.35, sheen=0.3)
+    jade = sc.mix(0.25, sc.glossy((0.9, 0.9, 0.9), 0.15),
+                  sc.subsurface((0.3, 0.8, 0.5), scale=35.0, radius=(0.5, 1.0, 0.6)))
+    thin = sc.subsurface((0.8, 0.8, 0.9), scale=1e-9, radius=(1.0, 1.0, 1.0))  # radii below BSSRDF_MIN_RADIUS: diffuse
+    s.materials.extend([skin, wax, jade, thin])
+    centers = [(140.0, 120.0, 220.0), (300.0, 120.0, 260.0), (430.0, 300.0, 300.0), (200.0, 380.0, 380.0)]
+    if instanced:
+        ev, et = _ellipsoid((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), 20, 12)
+        for i, c in enumerate(centers):
+            geo = sc.Mesh(ev, et, shader=base + i, smooth=True)
+            s.instances.append(sc.Instance(geo, _tfm(c, 0.3 * i, (70.0, 60.0 + 5 * i, 70.0))))
+            s.instances.append(sc.Instance(geo, _tfm((c[0] * 0.7 + 60.0, 40.0, 120.0 + 50 * i), 0.0,
+                                                     (30.0, 30.0, 30.0))))
+    else:
+        for i, c in enumerate(centers):
+            s.meshes.append(sc.Mesh(*_ellipsoid(c, (70.0, 65.0, 70.0), 20, 12), shader=base + i, smooth=i % 2 == 0))
+    s.lamps = [sc.Lamp("point", co=(140.0, 480.0, 40.0), size=20.0, color=(1.0, 0.8, 0.6), strength=3.0e6)]
+    s.name = "sss_instanced" if instanced else "sss_cornell"
+    return s
+
+
+def classroom_standin(width=1920, height=1080, samples=256, detail=1.0) -> sc.Scene:
+    """Classroom-class stand-in (SURVEY.md §8(d) config CLS): a classroom with
+    rows of desks and chairs, a blackboard, windows, 60 area lights in the
+    ceiling grid and subsurface (random walk) objects -- skin-like busts,
+    wax candles and a jade vase on the desks -- at 1920x1080, 256 spp."""
+    rng = np.random.default_rng(0x5EED + 2)
+    wall = sc.diffuse((0.7, 0.68, 0.62))
+    floor = sc.mix(0.15, sc.glossy((0.7, 0.6, 0.5), 0.2), sc.diffuse((0.45, 0.3, 0.2)))
+    wood = sc.principled(base_color=(0.5, 0.33, 0.2), roughness=0.45, specular=0.4)
+    metal = sc.glossy((0.75, 0.75, 0.78), 0.25)
+    board = sc.diffuse((0.08, 0.15, 0.1))
+    glass = sc.glass((0.95, 0.97, 1.0), 0.0, ior=1.45)
+    skin = sc.principled(subsurface_method="random_walk", base_color=(0.85, 0.62, 0.52), subsurface=0.8,
+                         subsurface_color=(0.9, 0.5, 0.4), subsurface_radius=(0.12, 0.05, 0.03), roughness=0.45,
+                         specular=0.35)
+    wax = sc.subsurface((0.95, 0.9, 0.75), scale=0.05, radius=(1.0, 0.8, 0.5))
+    jade = sc.mix(0.2, sc.glossy((0.9, 0.9, 0.9), 0.1), sc.subsurface((0.3, 0.75, 0.5), scale=0.04,
+                                                                       radius=(0.4, 1.0, 0.6)))
+    window = sc.emission((1.0, 0.98, 0.92), 1.5)
+    materials = [wall, floor, wood, metal, board, glass, skin, wax, jade, window]
+    meshes = []
+    W, D, H = 6.0, 8.0, 3.2
+    meshes.append(sc.Mesh(*_quad((-W, 0, -D), (W, 0, -D), (W, 0, D), (-W, 0, D)), shader=1))
+    meshes.append(sc.Mesh(*_quad((-W, H, -D), (-W, H, D), (W, H, D), (W, H, -D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((-W, 0, D), (W, 0, D), (W, H, D), (-W, H, D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((-W, 0, -D), (-W, H, -D), (W, H, -D), (W, 0, -D)), shader=0))
+    meshes.append(sc.Mesh(*_quad((W, 0, -D), (W, H, -D), (W, H, D), (W, 0, D)), shader=0))
+    # window wall: panes of emissive sky behind glass
+    meshes.append(sc.Mesh(*_quad((-W, 0, -D), (-W, 0, D), (-W, H, D), (-W, H, -D)), shader=0))
+    for k in range(4):
+        z0 = -6.0 + 3.2 * k
+        meshes.append(sc.Mesh(*_quad((-W + 0.01, 1.0, z0), (-W + 0.01, 1.0, z0 + 2.2), (-W + 0.01, 2.6, z0 + 2.2),
+                                     (-W + 0.01, 2.6, z0)), shader=9))
+        meshes.append(sc.Mesh(*_box((-W + 0.15, 1.8, z0 + 1.1), (0.02, 1.6, 2.2)), shader=5))
+    meshes.append(sc.Mesh(*_quad((-3.0, 0.9, D - 0.02), (3.0, 0.9, D - 0.02), (3.0, 2.4, D - 0.02),
+                                 (-3.0, 2.4, D - 0.02)), shader=4))
+    # desks and chairs
+    ncols, nrows = 4, int(5 * detail) + 1
+    for r in range(nrows):
+        for c in range(ncols):
+            x = -4.2 + c * 2.8
+            z = -5.5 + r * 2.0
+            meshes.append(sc.Mesh(*_box((x, 0.75, z), (1.4, 0.05, 0.7)), shader=2))
+            for lx in (-0.65, 0.65):
+                for lz in (-0.3, 0.3):
+                    v, t = _cylinder(0.025, 0.75, 10, caps=False)
+                    meshes.append(sc.Mesh(v + np.array([x + lx, 0.0, z + lz], dtype=np.float32), t, shader=3))
+            meshes.append(sc.Mesh(*_box((x, 0.45, z - 0.65), (0.45, 0.04, 0.45)), shader=2))
+            meshes.append(sc.Mesh(*_box((x, 0.75, z - 0.88), (0.45, 0.6, 0.04)), shader=2))
+            # subsurface props on every desk
+            kind = (r + c) % 3
+            nu, nv = int(40 * detail) + 8, int(28 * detail) + 6
+            if kind == 0:
+                meshes.append(sc.Mesh(*_ellipsoid((x - 0.3, 0.93, z), (0.09, 0.13, 0.09), nu, nv), shader=6,
+                                      smooth=True))
+            elif kind == 1:
+                v, t = _cylinder(0.04, 0.22 + 0.1 * rng.random(), nu)
+                meshes.append(sc.Mesh(v + np.array([x + 0.3, 0.775, z + 0.1], dtype=np.float32), t, shader=7,
+                                      smooth=True))
+            else:
+                meshes.append(sc.Mesh(*_ellipsoid((x, 0.9, z + 0.15), (0.08, 0.14, 0.08), nu, nv, exponent=0.8),
+                                      shader=8, smooth=True))
+    # bookshelves along the back wall
+    for shelf in range(5):
+        y = 0.3 + 0.45 * shelf
+        meshes.append(sc.Mesh(*_box((3.5, y, D - 0.25), (4.0, 0.03, 0.4)), shader=2))
+        nbooks = int(70 * detail) + 10
+        for b in range(nbooks):
+            bw = 0.03 + 0.03 * rng.random()
+            bh = 0.25 + 0.15 * rng.random()
+            meshes.append(sc.Mesh(*_box((1.6 + 3.8 * (b + 0.5) / nbooks, y + 0.015 + bh / 2, D - 0.25),
+                                        (bw, bh, 0.28), 0.05 * rng.standard_normal()), shader=2 + (b % 3 == 0) * 2))
+    # 60 ceiling area lights (6 x 10 grid)
+    lamps = []
+    for i in range(6):
+        for j in range(10):
+            lamps.append(sc.Lamp("area", co=(-5.0 + 2.0 * i, H - 0.02, -7.2 + 1.6 * j), direction=(0.0, -1.0, 0.0),
+                                 axisu=(1.0, 0.0, 0.0), axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=0.6, sizev=0.3,
+                                 color=(1.0, 0.95, 0.88), strength=5.0))
+    cam = sc.Camera(eye=(4.5, 1.7, -7.4), target=(-1.0, 0.8, 2.0), fov=math.radians(62.0), nearclip=0.05,
+                    farclip=100.0)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.0, 0.0, 0.0), world_strength=0.0,
+                    samples=samples, filter_type="blackman_harris", filter_width=1.5, lamps=lamps, max_bounce=8,
+                    name="classroom_standin")
+
+
 CONFIGS = {
     "cornell_lamps": cornell_lamps,
     "cornell_instanced": cornell_instanced,
@@ -600,6 +722,7 @@ CONFIGS = {
     "bmw27_standin": bmw27_standin,
     "barbershop_standin": barbershop_standin,
     "junkshop_standin": junkshop_standin,
+    "classroom_standin": classroom_standin,
 }
 
 

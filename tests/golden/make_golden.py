@@ -150,7 +150,10 @@ def make_scale():
     from parity_cases import FULL_FRAME_BLOCK, FULL_FRAME_CASE, SCALE_CASES, block_means
     from raytracingproject_amd import scenes
 
+    only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--scale-cases=")]
     for name, (fn, tile) in SCALE_CASES.items():
+        if only and name not in only[0]:
+            continue
         ds = sc.compile_scene(fn())
         rk = RefKernel(ds)
         buf = rk.render(tile=tile, threads=os.cpu_count())
@@ -159,6 +162,8 @@ def make_scale():
                             digest=np.array(scene_digest(ds)), buffer=buf, samples=np.array(ds.samples),
                             tile=np.array(tile if tile else (0, 0, ds.width, ds.height)))
         print(name, buf.shape, float(buf[..., :3].mean()) / ds.samples)
+    if only:
+        return
     ds = sc.compile_scene(scenes.CONFIGS[FULL_FRAME_CASE]())
     rk = RefKernel(ds)
     buf = rk.render(threads=os.cpu_count())
@@ -169,7 +174,24 @@ def make_scale():
     print("full frame", buf.shape)
 
 
+def make_sobol():
+    """The reference host's Sobol direction table (render/sobol.cpp
+    sobol_generate_direction_vectors, 32 words per dimension) for as many
+    dimensions as the integrator allocates for the parity scenes
+    (integrator.cpp:230-238 with the default bounces)."""
+    from parity_cases import JOE_KUO_CASES
+
+    dims = max(sc.compile_scene(CASES[n]()).arrays["__sample_pattern_lut"].size // 32 for n in JOE_KUO_CASES)
+    lut = np.zeros(dims * 32, dtype=np.uint32)
+    ref_lib().cref_sobol_directions(lut.ctypes.data, dims)
+    np.savez_compressed(golden_path("sobol_joe_kuo"), lut=lut, dimensions=np.array(dims))
+    print("sobol_joe_kuo", dims, "dimensions")
+
+
 def main():
+    if "--sobol-only" in sys.argv:
+        make_sobol()
+        return
     if "--scale-only" in sys.argv:
         make_scale()
         return

@@ -51,7 +51,17 @@ CASES = {
     # curves in a BVH with unaligned nodes (bvh_nodes.h:79-153)
     "hair_ribbon": lambda: scenes.hair_ball(48, 48, 8, shape="ribbon"),
     "hair_thick": lambda: scenes.hair_ball(48, 48, 8, shape="thick"),
+    # the reference host's own Sobol directions (render/sobol.cpp, Joe-Kuo
+    # new-joe-kuo-6.21201, uploaded by integrator.cpp:235-243) instead of this
+    # repository's stand-in table: tests/golden/sobol_joe_kuo.npz
+    "cornell_joe_kuo": lambda: scenes.cornell_box(64, 64, 16),
+    # random-walk subsurface scattering (kernel_subsurface.h), applied and
+    # instanced geometry (scene_intersect_local through bvh_instance_push)
+    "sss_cornell": lambda: scenes.sss_cornell(48, 48, 8),
+    "sss_instanced": lambda: scenes.sss_cornell(48, 48, 8, instanced=True),
 }
+# Cases whose __sample_pattern_lut is the reference host's table (fixture)
+JOE_KUO_CASES = {"cornell_joe_kuo"}
 
 # Cases whose render needs the device's host-side step loop (adaptive sampling:
 # stopping / filter / rescale kernels between sample passes, hipcycles.hip
@@ -112,6 +122,10 @@ SCALE_CASES = {
     "cornell_256": (lambda: scenes.cornell_box(256, 256, 32), None),
     "bmw_full_tile": (lambda: scenes.bmw27_standin(), (576, 328, 64, 64)),
     "bbs_tile": (lambda: scenes.barbershop_standin(), (960, 560, 48, 48)),
+    # CLS: 60 area lights, random-walk SSS props (1920x1080, 256 spp)
+    "cls_tile": (lambda: scenes.classroom_standin(), (1130, 200, 40, 40)),
+    # JNK: fur balls / rug ribbons, 1.6M curve segments (3840x2160, 1024 spp)
+    "jnk_tile": (lambda: scenes.junkshop_standin(), (1660, 520, 32, 32)),
 }
 
 # Full frame of the bench scene (BMW stand-in, 1280x720, 128 spp): the
@@ -152,7 +166,14 @@ PATH_RAY_CLOSEST_VISIBILITY = PATH_RAY_ALL_VISIBILITY & ~PATH_RAY_SHADOW_OPAQUE
 
 
 def compile_case(name: str) -> sc.DeviceScene:
-    return sc.compile_scene(CASES[name]())
+    ds = sc.compile_scene(CASES[name]())
+    if name in JOE_KUO_CASES:
+        lut = np.load(golden_path("sobol_joe_kuo"), allow_pickle=False)["lut"]
+        n = ds.arrays["__sample_pattern_lut"].size
+        assert lut.size >= n, "sobol_joe_kuo.npz holds fewer dimensions than the integrator allocates"
+        ds.arrays["__sample_pattern_lut"] = np.ascontiguousarray(lut[:n])
+        ds.info["sobol"] = "joe-kuo (reference render/sobol.cpp)"
+    return ds
 
 
 BG_CDF_NAMES = ("__light_background_marginal_cdf", "__light_background_conditional_cdf")

@@ -131,7 +131,7 @@ static bool emu_traverse_impl(const CyGlobals *kg, const CyRay *ray, uint vis, C
     return bvh2_intersect<any_hit>(&k2, ray, vis, isect, err, nullptr, nullptr, nullptr, nullptr);
   }
   if (kg->have_curves) {
-    return bvh2_intersect<any_hit, true, 2, CY_LDS_STACK, CY_BLOCK, true>(kg, ray, vis, isect, err, nn, nl, nt,
+    return bvh2_intersect<any_hit, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(kg, ray, vis, isect, err, nn, nl, nt,
                                                                          nullptr);
   }
   return bvh2_intersect<any_hit>(kg, ray, vis, isect, err, nn, nl, nt, nullptr);
