@@ -97,14 +97,17 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False):
              os.path.join(objdir, "hipcycles.o"))]
     shade_objs = []
     for mc in SHADE_VARIANTS:
-        for tex in (0, 1):
-            name = f"mc{mc}_tex" if tex else f"mc{mc}"
+        # plain (closure nodes only), _tex (texture nodes, extended closures),
+        # _vol (_tex with volumes)
+        for kind in ("", "_tex", "_vol"):
+            name = f"mc{mc}{kind}"
             if traversal_only:
                 shade_objs.append(os.path.join(REPO, "build", "device", "default", f"k_shade_{name}.o"))
                 continue
             obj = os.path.join(objdir, f"k_shade_{name}.o")
             jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
-                          f"-DCY_SVM_TEX={tex}", inc, "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
+                          f"-DCY_SVM_TEX={0 if kind == '' else 1}", f"-DCY_VOLUME={1 if kind == '_vol' else 0}", inc,
+                          "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
     with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
         list(ex.map(lambda j: _run(j[0]), jobs))
     _run([HIPCC, "--offload-arch=gfx950", "-fno-gpu-rdc", "-shared", "-fPIC", "-o", out, *[j[1] for j in jobs],

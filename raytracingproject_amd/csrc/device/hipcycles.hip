@@ -602,6 +602,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_shadow_continue
  * record-all occlusion of the light sample with the occluders' shaders
  * evaluated (cy_integrator.h shadow_finish_transparent), then the same finish
  * and refill.  Only scenes with transparent-shadow shaders use it. */
+template<bool VOL>
 __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow_transparent(CyGlobals kg,
                                                                           CyPathBuffers b,
                                                                           CyTile tile,
@@ -625,7 +626,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_intersect_shadow_transparent(CyGlo
     mem.svm_stride = 1;
     mem.svm_fast = CY_SVM_STACK;
     mem.svm_spill = nullptr;
-    finished = shadow_finish_transparent(&kg, &b, &tile, slot, mem, err);
+    finished = shadow_finish_transparent<VOL>(&kg, &b, &tile, slot, mem, err);
   }
   __shared__ uint claim[CY_CLAIM_LDS];
   const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
@@ -1162,6 +1163,8 @@ struct hipcy_device {
   std::vector<hc_uint4> svm_nodes;    /* host copy of __svm_nodes, taken at bind time */
   size_t num_shaders = 0;             /* __shaders entries */
   bool shade_tex = false;             /* some shader uses texture / converter / input nodes */
+  bool use_volumes = false;           /* KernelIntegrator.use_volumes: the volume shading / shadow kernels */
+  int shade_closures = 1;             /* closure array of the shading kernel (variant by size) */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int curve_shapes = 0;               /* curve primitive shapes in __prim_type: 1 ribbon, 2 thick, 3 both */
   int tri_index_identity = 0;
@@ -1316,10 +1319,11 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     hipFree(dev->pool);
     dev->pool = nullptr;
   }
-  /* 12 float4 records + 3 ints per slot (queues are separate) */
+  /* 12 float4 records + 3 ints per slot (queues are separate), and the volume
+   * stack (CY_VOLUME_STACK / 2 records) and 2 volume records per slot */
   const size_t rec = 16 * slots;
   const size_t ints = 4 * slots;
-  const size_t total = 12 * rec + 3 * ints + 15 * 256;
+  const size_t total = (12 + CY_VOLUME_STACK / 2 + 2) * rec + 3 * ints + 17 * 256;
   HIP_CHECK(dev, hipMalloc((void **)&dev->pool, total));
   char *p = dev->pool;
   auto take = [&](size_t n) {
@@ -1342,6 +1346,8 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   dev->bufs.shadow_L = (hc_float4 *)take(rec);
   dev->bufs.shadow_T = (hc_float4 *)take(rec);
   dev->bufs.item = (uint *)take(ints);
+  dev->bufs.vol_stack = (hc_uint4 *)take((CY_VOLUME_STACK / 2) * rec);
+  dev->bufs.vol_rec = (hc_uint4 *)take(2 * rec);
   dev->capacity = slots;
   /* queues live in their own allocation (3 x slots ints) */
   for (int q = 0; q < 3; q++) {
@@ -1758,9 +1764,16 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
  * device/device.h:130-200) and reports whether the texture / converter / input
  * nodes are used, which selects the shading-kernel variant. */
 static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
-                            const std::vector<void *> &tex_mem, bool *uses_tex)
+                            const std::vector<void *> &tex_mem, const std::vector<uint32_t> &shader_flags,
+                            bool *uses_tex, bool *uses_bssrdf, int *surface_closures, int *volume_closures)
 {
   *uses_tex = false;
+  *uses_bssrdf = false;
+  /* closures one program can allocate, counted as ShaderGraph::get_num_closures
+   * (render/graph.cpp:1130-1161) counts them, except that a phase closure
+   * allocates one per evaluation (the reference reserves VOLUME_STACK_SIZE) */
+  *surface_closures = 0;
+  *volume_closures = 0;
   const size_t n = prog.size();
   /* an image slot the kernel will read must have been allocated (hipcy_tex_alloc):
    * kernel_tex_image_interp indexes __texture_info without a bound check; -1 is
@@ -1769,11 +1782,18 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
   if (num_shaders > n) {
     return "jump table larger than the program";
   }
-  for (size_t sh = 0; sh < num_shaders; sh++) {
+  /* every shader's surface program, and the volume program of shaders with a volume */
+  for (size_t pi = 0; pi < 2 * num_shaders; pi++) {
+    const size_t sh = pi % num_shaders;
+    const bool volume = pi >= num_shaders;
     if (prog[sh].x != NODE_SHADER_JUMP) {
       return "shader " + std::to_string(sh) + ": jump table entry is not NODE_SHADER_JUMP";
     }
-    size_t off = prog[sh].y;
+    if (volume && !(sh < shader_flags.size() && (shader_flags[sh] & SD_HAS_VOLUME))) {
+      continue;
+    }
+    size_t off = volume ? prog[sh].z : prog[sh].y;
+    int closures = 0;
     for (size_t steps = 0;; steps++) {
       if (off >= n || steps > n) {
         return "shader " + std::to_string(sh) + ": program runs past __svm_nodes";
@@ -1794,6 +1814,11 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
            * (cy_types.h CY_CLOSURE_EXT): isotropic GGX / sharp / glass /
            * transparent / Lambert diffuse; anything else selects the full one */
           const uint ctype = node.y & 0xFF;
+          closures += (ctype == CLOSURE_BSDF_PRINCIPLED_ID)                                 ? 8 :
+                      (ctype >= CLOSURE_BSSRDF_CUBIC_ID && ctype <= CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) ? 3 :
+                      (ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID ||
+                       ctype == CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)                  ? 2 :
+                                                                                            1;
           const bool rough_diffuse = ctype == CLOSURE_BSDF_DIFFUSE_ID &&
                                      (((node.y >> 8) & 0xFF) != SVM_STACK_INVALID || node.z != 0u);
           const bool tangent = prog[off + 1].y != SVM_STACK_INVALID;
@@ -1831,6 +1856,10 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             case CLOSURE_BSDF_DIFFUSE_TOON_ID:
             case CLOSURE_BSDF_GLOSSY_TOON_ID:
             case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node, random walk */
+              /* a random-walk BSSRDF, or a principled BSDF with subsurface (param2: linked or > 0) */
+              *uses_bssrdf |= ctype == CLOSURE_BSSRDF_RANDOM_WALK_ID ||
+                              (ctype == CLOSURE_BSDF_PRINCIPLED_ID &&
+                               (((node.y >> 16) & 0xFF) != SVM_STACK_INVALID || node.w != 0u));
               break;
             case CLOSURE_BSSRDF_CUBIC_ID:
             case CLOSURE_BSSRDF_GAUSSIAN_ID:
@@ -1845,6 +1874,21 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
         }
         case NODE_VALUE_V:
           len = 2;
+          break;
+        case NODE_CLOSURE_VOLUME:
+          closures += ((node.y & 0xFF) == CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID) ? 1 : 0;
+          tex = true; /* volumes run in the extended shading kernels */
+          break;
+        case NODE_PRINCIPLED_VOLUME:
+          len = 3; /* value node, attribute node */
+          if (off + 2 >= n) {
+            return "principled volume: parameter nodes past __svm_nodes";
+          }
+          if (((node.z >> 16) & 0xFF) != SVM_STACK_INVALID || __builtin_bit_cast(float, prog[off + 1].w) > 0.0f) {
+            return "shader " + std::to_string(sh) + ": principled volume blackbody emission is not implemented";
+          }
+          closures += 1;
+          tex = true;
           break;
         case NODE_CLOSURE_EMISSION:
         case NODE_CLOSURE_BACKGROUND:
@@ -1942,6 +1986,8 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
       }
       *uses_tex |= tex;
       if (len == 0) {
+        int *m = volume ? volume_closures : surface_closures;
+        *m = std::max(*m, closures);
         break;
       }
       off += len;
@@ -1963,7 +2009,11 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.cam.interocular_offset != 0.0f) why = "stereo";
   else if (d.integrator.sampling_pattern != 0) why = "only the Sobol pattern";
   else if (d.integrator.branched) why = "branched path tracing";
-  else if (d.integrator.use_volumes) why = "volumes";
+  else if (d.integrator.use_volumes && d.integrator.volume_decoupled)
+    why = "decoupled volume ray marching (a CPU-device setting: GPU devices set volume_decoupled 0)";
+  else if (d.integrator.use_volumes && d.cam.is_inside_volume) why = "camera inside a volume object";
+  else if (d.integrator.use_volumes && !d.integrator.transparent_shadows)
+    why = "volumes without transparent shadows (shader.cpp:529-536 sets them for every volume shader)";
   else if (d.integrator.transparent_shadows && d.integrator.transparent_max_bounce > CY_SHADOW_MAX_HITS)
     why = "transparent shadows deeper than " + std::to_string(CY_SHADOW_MAX_HITS) + " bounces";
   else if (d.integrator.transparent_shadows &&
@@ -1974,7 +2024,8 @@ int hipcy_load_kernels(hipcy_device *dev)
     why = "adaptive_stop_per_sample (a CPU-device setting; this device filters at adaptive_step samples)";
   else if (d.background.portal_weight > 0.0f || d.background.num_portals) why = "light portals";
   else if (d.background.sun_weight > 0.0f) why = "sky texture sun sampling";
-  else if (d.integrator.max_closures > CY_MAX_CLOSURE) why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
+  else if (d.integrator.max_closures > CY_MAX_CLOSURE && !d.integrator.use_volumes)
+    why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
   else if (d.bvh.have_motion || d.bvh.use_bvh_steps) why = "motion blur (motion triangles / curves)";
   else if (d.bvh.have_curves && (d.bvh.curve_subdivisions < 1 || d.bvh.curve_subdivisions > 16))
     why = "curve_subdivisions outside 1..16";
@@ -2035,9 +2086,61 @@ int hipcy_load_kernels(hipcy_device *dev)
       dev->curve_shapes = 3;
     }
   }
-  why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, &dev->shade_tex);
+  std::vector<uint32_t> shader_flags(dev->num_shaders, 0u);
+  if (dev->num_shaders) {
+    std::vector<hc_KernelShader> ks(dev->num_shaders);
+    HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+    HIP_CHECK(dev, hipMemcpy(ks.data(), (const void *)dev->globals["__shaders"].ptr,
+                             dev->num_shaders * sizeof(hc_KernelShader), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ks.size(); i++) {
+      shader_flags[i] = (uint32_t)ks[i].flags;
+    }
+  }
+  bool uses_bssrdf = false;
+  int surface_closures = 0, volume_closures = 0;
+  why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, shader_flags, &dev->shade_tex, &uses_bssrdf,
+                 &surface_closures, &volume_closures);
   if (!why.empty()) {
     return set_error(dev, "load_kernels: unsupported shader: " + why);
+  }
+  dev->use_volumes = d.integrator.use_volumes != 0;
+  dev->shade_closures = d.integrator.max_closures;
+  if (dev->use_volumes) {
+    /* the volume stack of a path holds the world and every volume object it
+     * is inside of (plus the terminator) */
+    size_t volume_objects = 0;
+    bool intersects_volume = false, volume_attributes = false;
+    for (uint32_t f : dev->object_flags) {
+      volume_objects += (f & SD_OBJECT_HAS_VOLUME) ? 1 : 0;
+      intersects_volume |= (f & SD_OBJECT_INTERSECTS_VOLUME) != 0;
+      volume_attributes |= (f & SD_OBJECT_HAS_VOLUME_ATTRIBUTES) != 0;
+    }
+    /* the volume stack's shaders evaluate into one closure array (merged
+     * when their phase closures are equal): a bound on what a shading
+     * point allocates selects the array (the reference's max_closures
+     * reserves VOLUME_STACK_SIZE per volume closure, never reached here) */
+    const int bound = std::max(std::min(surface_closures, (int)d.integrator.max_closures),
+                               (int)(volume_objects + 1) * volume_closures);
+    dev->shade_closures = std::max(bound, 1);
+    if (bound > CY_MAX_CLOSURE) {
+      why = "volume scene needing " + std::to_string(bound) + " closures > " + std::to_string(CY_MAX_CLOSURE);
+    }
+    else if (volume_objects + 2 > CY_VOLUME_STACK) {
+      why = "more than " + std::to_string(CY_VOLUME_STACK - 2) + " volume objects (the device's volume stack)";
+    }
+    else if (volume_attributes) {
+      why = "volume attributes (voxel grids)";
+    }
+    else if (uses_bssrdf && intersects_volume) {
+      why = "subsurface scattering on objects that intersect volume objects (volume stack update of the walk)";
+    }
+    else if (volume_objects && dev->globals.find("__object_volume_step") == dev->globals.end()) {
+      why = "volume objects without __object_volume_step";
+    }
+    if (!why.empty()) {
+      return set_error(dev, "load_kernels: unsupported scene feature: " + why);
+    }
+    dev->shade_tex = true;
   }
   /* instanced geometry present? (selects the traversal kernels with instance
    * leaves and the instance paths of shading) */
@@ -2244,14 +2347,16 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));
   }
-  cy_launch_shade(dev->data_host.integrator.max_closures, dev->shade_tex, grid, block, s, kg, dev->bufs, ln.tile, cam_n,
+  cy_launch_shade(dev->shade_closures, dev->shade_tex, dev->use_volumes, grid, block, s, kg,
+                  dev->bufs, ln.tile, cam_n,
                   ln.slot_base, queue_in, ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }
   if (dev->data_host.integrator.transparent_shadows) {
-    hipLaunchKernelGGL(k_intersect_shadow_transparent, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs],
-                       ln.cnt + qs, ln.q[qb], ln.cnt + qb, err);
+    auto kfn = dev->use_volumes ? k_intersect_shadow_transparent<true> : k_intersect_shadow_transparent<false>;
+    hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb], ln.cnt + qb,
+                       err);
   }
   else {
     if (budget) {

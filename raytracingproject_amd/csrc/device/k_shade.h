@@ -7,6 +7,8 @@
  * built twice: plain (CY_SVM_TEX=0: closure nodes only, constant world) and
  * "_tex" with the texture / converter / input nodes and node worlds; the
  * plain kernels keep the register allocation of scenes that need no nodes.
+ * Scenes with volumes use a third build, "_vol" (CY_VOLUME=1: the "_tex"
+ * kernel with the volume stack, segment integration and phase closures).
  */
 #ifndef K_SHADE_H
 #define K_SHADE_H
@@ -28,10 +30,18 @@ void cy_launch_shade_mc1_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc2_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc4_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc8_tex(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc1_vol(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc2_vol(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc4_vol(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc8_vol(CY_SHADE_LAUNCHER_ARGS);
 
-static inline void cy_launch_shade(int max_closures, bool tex_nodes, CY_SHADE_LAUNCHER_ARGS)
+static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, CY_SHADE_LAUNCHER_ARGS)
 {
-  auto fn = tex_nodes ? (max_closures <= 1 ? cy_launch_shade_mc1_tex :
+  auto fn = volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :
+                       max_closures <= 2 ? cy_launch_shade_mc2_vol :
+                       max_closures <= 4 ? cy_launch_shade_mc4_vol :
+                                           cy_launch_shade_mc8_vol) :
+            tex_nodes ? (max_closures <= 1 ? cy_launch_shade_mc1_tex :
                          max_closures <= 2 ? cy_launch_shade_mc2_tex :
                          max_closures <= 4 ? cy_launch_shade_mc4_tex :
                                              cy_launch_shade_mc8_tex) :

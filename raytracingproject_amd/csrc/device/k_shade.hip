@@ -4,7 +4,11 @@
  * -DCY_MAX_CLOSURE=N -DCY_SHADE_VARIANT=mcN -DCY_SVM_TEX=0, and as mcN_tex with
  * -DCY_SVM_TEX=1 (raytracingproject_amd/build.py).
  */
-/* the plain variants carry the basic closure set (cy_types.h CY_CLOSURE_EXT) */
+/* the plain variants carry the basic closure set (cy_types.h CY_CLOSURE_EXT);
+ * the volume variants (-DCY_VOLUME=1) are "_tex" builds with volumes */
+#ifndef CY_VOLUME
+#  define CY_VOLUME 0
+#endif
 #ifndef CY_CLOSURE_EXT
 #  define CY_CLOSURE_EXT CY_SVM_TEX
 #endif
@@ -73,7 +77,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_,
   if (cam_n > 0 ? i < cam_n : i < (int)*count_in) {
     slot = cam_n > 0 ? slot_base + i : queue_in[i];
     const uint cam_item = cam_n > 0 ? tile.item_base + (uint)i : CY_NO_ITEM;
-    cont = shade_path(&kg, &b, &tile, slot, cam_item, mem, &shadow, &finished, err);
+    cont = shade_path<CY_VOLUME != 0>(&kg, &b, &tile, slot, cam_item, mem, &shadow, &finished, err);
   }
   __shared__ uint claim[CY_CLAIM_LDS];
   cont |= slot_refill(kg, b, tile, slot, finished, claim);

@@ -39,7 +39,8 @@
   X(uint32_t, __sample_pattern_lut) \
   X(hc_TextureInfo, __texture_info) \
   X(hc_float4, __curves) \
-  X(hc_float4, __curve_keys)
+  X(hc_float4, __curve_keys) \
+  X(float, __object_volume_step)
 
 typedef struct CyGlobals {
   const hc_KernelData *data;

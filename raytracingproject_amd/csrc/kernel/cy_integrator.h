@@ -24,6 +24,7 @@
 
 #include "cy_path.h"
 #include "cy_subsurface.h"
+#include "cy_volume.h"
 
 /* Per-slot state, SoA of 16-byte records so every access is one dwordx4. */
 typedef struct CyPathBuffers {
@@ -44,7 +45,23 @@ typedef struct CyPathBuffers {
   hc_float4 *shadow_T;   /* transparent shadows: path throughput xyz, w: bounces (8 bits each:
                           * bounce, transparent, diffuse, glossy); shadow_D.w: transmission bounce */
   uint *item;            /* work item of the path in the slot */
+  /* volume scenes (KernelIntegrator.use_volumes): the path's volume stack,
+   * CY_VOLUME_STACK / 2 records per slot of two (object, shader) entries, and
+   * two records per slot: [0] object, shader, pending stack update flags
+   * (CY_VOP_*), volume_bounce; [1] volume_bounds_bounce, the rng_offset the
+   * pending shadow ray sees */
+  hc_uint4 *vol_stack;
+  hc_uint4 *vol_rec;
 } CyPathBuffers;
+
+/* Pending volume stack update of a slot (cy_volume.h volume_stack_enter_exit
+ * of the surface in vol_rec[0].xy): the reference updates the stack when the
+ * path bounces through the surface, after the surface's light sample was
+ * traced with the old stack; the wavefront traces that shadow ray in the next
+ * stage, so the update is recorded and applied by the next shade. */
+#define CY_VOP_PATH 1u       /* apply to the path's stack at its next shade */
+#define CY_VOP_SHADOW 2u     /* apply to the shadow ray's copy (kernel_shadow.h:22-45) */
+#define CY_VOP_BACKFACING 4u /* the surface was hit from behind (SD_BACKFACING) */
 
 /* One RenderTile of a multi-tile pass (hipcy_path_trace_tiles). */
 typedef struct CyTileDesc {
@@ -186,7 +203,70 @@ CY_FN void store_state(const CyPathBuffers *b, int slot, const CyPathState *s)
   cy_st(&b->state2[slot], mkf4(int_as_float(s->transparent_bounce), s->min_ray_pdf, s->ray_pdf, s->ray_t));
 }
 
-/* kernel_path_state.h:19-71 (no volumes, no denoising features). */
+#if CY_CLOSURE_EXT
+/* The slot's volume stack and pending update records (CyPathBuffers.vol_*). */
+CY_FN void vol_stack_load(const CyPathBuffers *b, int slot, CyVolumeStack *st)
+{
+  const hc_uint4 *src = b->vol_stack + (size_t)slot * (CY_VOLUME_STACK / 2);
+  for (int k = 0; k < CY_VOLUME_STACK / 2; k++) {
+    const hc_uint4 r = cy_ld(&src[k]);
+    st->e[2 * k].object = (int)r.x;
+    st->e[2 * k].shader = (int)r.y;
+    st->e[2 * k + 1].object = (int)r.z;
+    st->e[2 * k + 1].shader = (int)r.w;
+    if ((int)r.y == SHADER_NONE || (int)r.w == SHADER_NONE) {
+      break;
+    }
+  }
+}
+
+CY_FN void vol_stack_store(const CyPathBuffers *b, int slot, const CyVolumeStack *st)
+{
+  hc_uint4 *dst = b->vol_stack + (size_t)slot * (CY_VOLUME_STACK / 2);
+  for (int k = 0; k < CY_VOLUME_STACK / 2; k++) {
+    hc_uint4 r;
+    r.x = (uint)st->e[2 * k].object;
+    r.y = (uint)st->e[2 * k].shader;
+    r.z = (uint)st->e[2 * k + 1].object;
+    r.w = (uint)st->e[2 * k + 1].shader;
+    cy_st(&dst[k], r);
+    if ((int)r.y == SHADER_NONE || (int)r.w == SHADER_NONE) {
+      break;
+    }
+  }
+}
+
+CY_FN void vol_rec_store(const CyPathBuffers *b, int slot, uint object, uint shader, uint flags,
+                         const CyPathState *state, int shadow_rng_offset)
+{
+  hc_uint4 r0, r1;
+  r0.x = object;
+  r0.y = shader;
+  r0.z = flags;
+  r0.w = (uint)state->volume_bounce;
+  r1.x = (uint)state->volume_bounds_bounce;
+  r1.y = (uint)shadow_rng_offset;
+  r1.z = 0u;
+  r1.w = 0u;
+  cy_st(&b->vol_rec[2 * (size_t)slot], r0);
+  cy_st(&b->vol_rec[2 * (size_t)slot + 1], r1);
+}
+
+/* A new path in the slot: the stack of a camera ray (kernel_path_state.h:62-68) */
+CY_FN void vol_slot_init(const CyGlobals *kg, const CyPathBuffers *b, int slot)
+{
+  CyVolumeStack st;
+  volume_stack_init(kg, &st);
+  vol_stack_store(b, slot, &st);
+  CyPathState s;
+  s.volume_bounce = 0;
+  s.volume_bounds_bounce = 0;
+  vol_rec_store(b, slot, 0u, 0u, 0u, &s, 0);
+}
+
+#endif
+
+/* kernel_path_state.h:19-71 (the volume stack: vol_slot_init / shade_path). */
 CY_FN void path_state_init(const CyGlobals *kg, CyPathState *s, uint rng_hash, int sample)
 {
   s->flag = PATH_RAY_CAMERA | PATH_RAY_MIS_SKIP | PATH_RAY_TRANSPARENT_BACKGROUND;
@@ -202,10 +282,12 @@ CY_FN void path_state_init(const CyGlobals *kg, CyPathState *s, uint rng_hash, i
   s->min_ray_pdf = CY_FLT_MAX;
   s->ray_pdf = 0.0f;
   s->ray_t = 0.0f;
+  s->volume_bounce = 0;
+  s->volume_bounds_bounce = 0;
 }
 
 /* kernel_path_state.h:72-178 */
-CY_FN void path_state_next(const CyGlobals *kg, CyPathState *s, int label)
+template<bool VOL = false> CY_FN void path_state_next(const CyGlobals *kg, CyPathState *s, int label)
 {
   if (label & LABEL_TRANSPARENT) {
     s->flag |= PATH_RAY_TRANSPARENT;
@@ -224,6 +306,16 @@ CY_FN void path_state_next(const CyGlobals *kg, CyPathState *s, int label)
     s->flag |= PATH_RAY_TERMINATE_AFTER_TRANSPARENT;
   }
   s->flag &= ~(PATH_RAY_ALL_VISIBILITY | PATH_RAY_MIS_SKIP);
+  if (VOL && (label & LABEL_VOLUME_SCATTER)) {
+    s->flag |= PATH_RAY_VOLUME_SCATTER;
+    s->flag &= ~PATH_RAY_TRANSPARENT_BACKGROUND;
+    s->volume_bounce++;
+    if (s->volume_bounce >= KD->integrator.max_volume_bounce) {
+      s->flag |= PATH_RAY_TERMINATE_AFTER_TRANSPARENT;
+    }
+    s->rng_offset += PRNG_BOUNCE_NUM;
+    return;
+  }
   if (label & LABEL_REFLECT) {
     s->flag |= PATH_RAY_REFLECT;
     s->flag &= ~PATH_RAY_TRANSPARENT_BACKGROUND;
@@ -423,6 +515,11 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
   CyPathState s;
   path_state_init(kg, &s, rng_hash, sample);
   store_state(b, slot, &s);
+#if CY_CLOSURE_EXT
+  if (KD->integrator.use_volumes) {
+    vol_slot_init(kg, b, slot);
+  }
+#endif
   cy_st(&b->item[slot], item);
   cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
   cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(path_state_ray_visibility(&s))));
@@ -516,9 +613,16 @@ CY_FN bool shadow_finish(const CyPathBuffers *b, const CyTile *tile, int slot, b
 #ifndef CY_SHADOW_MAX_HITS
 #  define CY_SHADOW_MAX_HITS 64 /* kernel_shadow.h:127 SHADOW_STACK_MAX_HITS */
 #endif
-CY_FN bool shadow_blocked_transparent(
-    const CyGlobals *kg, CyRay ray, const CyPathState *state, CyShadeMem mem, cfloat3 *shadow, uint *err)
+template<bool VOL = false>
+CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPathState *state, CyShadeMem mem,
+                                      cfloat3 *shadow, uint *err, void *volume_stack = nullptr)
 {
+#if CY_CLOSURE_EXT
+  /* volume scenes: the shadow ray's copy of the path's volume stack, crossed
+   * at every transparent surface (kernel_shadow.h:49-85), and the volumes'
+   * attenuation of each segment between surfaces */
+  CyVolumeStack *vstack = (CyVolumeStack *)volume_stack;
+#endif
   *shadow = mk3(1.0f, 1.0f, 1.0f);
   if (ray.t == 0.0f) {
     return false;
@@ -534,6 +638,12 @@ CY_FN bool shadow_blocked_transparent(
                            bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
                            bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
   if (blocked || num_hits == 0) {
+#if CY_CLOSURE_EXT
+    if (VOL && !blocked && vstack->e[0].shader != SHADER_NONE) {
+      CySD vsd;
+      volume_shadow(kg, &vsd, state, vstack, &ray, shadow, mem, err);
+    }
+#endif
     return blocked;
   }
   /* sort_intersections (bvh/bvh.h:606-626): stable, by distance */
@@ -558,6 +668,14 @@ CY_FN bool shadow_blocked_transparent(
     }
     last_t = new_t;
     /* shadow_handle_transparent_isect (kernel_shadow.h:49-85) */
+#if CY_CLOSURE_EXT
+    if (VOL && vstack->e[0].shader != SHADER_NONE) {
+      CyRay segment_ray = ray;
+      segment_ray.t = isect.t;
+      CySD vsd;
+      volume_shadow(kg, &vsd, state, vstack, &segment_ray, &throughput, mem, err);
+    }
+#endif
     CySD sd;
     sd.closure = mem.closure;
     sd.svm_stack = mem.svm_stack;
@@ -565,18 +683,32 @@ CY_FN bool shadow_blocked_transparent(
     sd.svm_fast = mem.svm_fast;
     sd.svm_spill = mem.svm_spill;
     shader_setup_from_ray(kg, &sd, &isect, &ray);
-    CyPathState st = *state;
-    st.bounce += 1; /* path_state_modify_bounce */
-    shader_eval_surface(kg, &sd, &st, PATH_RAY_SHADOW, err);
-    throughput = mul3(throughput, shader_bsdf_transparency(&sd));
+    if (!VOL || !(sd.flag & SD_HAS_ONLY_VOLUME)) {
+      CyPathState st = *state;
+      st.bounce += 1; /* path_state_modify_bounce */
+      shader_eval_surface(kg, &sd, &st, PATH_RAY_SHADOW, err);
+      throughput = mul3(throughput, shader_bsdf_transparency(&sd));
+    }
     if (is_zero3(throughput)) {
       return true;
     }
+#if CY_CLOSURE_EXT
+    if (VOL) {
+      volume_stack_enter_exit(sd.flag, sd.object, sd.shader, vstack);
+    }
+#endif
     ray.P = sd.P;
     if (ray.t != CY_FLT_MAX) {
       ray.D = normalize_len3(sub3(Pend, ray.P), &ray.t);
     }
   }
+#if CY_CLOSURE_EXT
+  if (VOL && vstack->e[0].shader != SHADER_NONE) {
+    /* the last segment, towards the light */
+    CySD vsd;
+    volume_shadow(kg, &vsd, state, vstack, &ray, &throughput, mem, err);
+  }
+#endif
   *shadow = throughput;
   return is_zero3(throughput);
 }
@@ -584,6 +716,7 @@ CY_FN bool shadow_blocked_transparent(
 /* The transparent-shadow counterpart of shadow_finish: occlusion and
  * attenuation of the pending light sample, then its contribution
  * (path_radiance_accum_light: throughput * shadow, times the eval, clamped). */
+template<bool VOL = false>
 CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot,
                                      CyShadeMem mem, uint *err)
 {
@@ -600,7 +733,27 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
   state.glossy_bounce = (int)(packed >> 24);
   state.transmission_bounce = as_int(cy_ld(&b->shadow_D[slot]).w);
   cfloat3 shadow;
-  const bool blocked = shadow_blocked_transparent(kg, ray, &state, mem, &shadow, err);
+  bool blocked;
+#if CY_CLOSURE_EXT
+  if (VOL) {
+    /* the stack the light sample saw, crossing the surface when the ray
+     * leaves through it, and the rng offset of the sample's bounce */
+    CyVolumeStack vstack;
+    vol_stack_load(b, slot, &vstack);
+    const hc_uint4 r0 = cy_ld(&b->vol_rec[2 * (size_t)slot]);
+    const hc_uint4 r1 = cy_ld(&b->vol_rec[2 * (size_t)slot + 1]);
+    if (r0.z & CY_VOP_SHADOW) {
+      volume_stack_enter_exit(SD_HAS_VOLUME | ((r0.z & CY_VOP_BACKFACING) ? SD_BACKFACING : 0), (int)r0.x,
+                              (int)r0.y, &vstack);
+    }
+    state.rng_offset = (int)r1.y;
+    blocked = shadow_blocked_transparent<true>(kg, ray, &state, mem, &shadow, err, &vstack);
+  }
+  else
+#endif
+  {
+    blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err);
+  }
   hc_float4 L4 = cy_ld(&b->L[slot]);
   if (!blocked) {
     const cfloat3 shaded_throughput = mul3(mul3f(mk3(st4.x, st4.y, st4.z), 1.0f), shadow);
@@ -744,6 +897,133 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
   return shader_background_eval(&esd);
 }
 
+/* Direct light at a shading point, one light sample (kernel_path_surface.h:23-140
+ * kernel_branched_path_surface_connect_light with one sample, or
+ * kernel_path_volume_connect_light, kernel_path_volume.h:21-61, when PHASE: a
+ * volume scatter point lit through its phase closures): light_sample +
+ * direct_emission (kernel_emission.h:101-205).  An occluded-or-not light
+ * sample is left in the slot's shadow records and *shadow set; *shadow_D is
+ * the shadow ray's direction then. */
+template<bool PHASE>
+CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, const CySD *sd,
+                         const CyPathState *state, cfloat3 throughput, cfloat3 *L, bool *shadow, cfloat3 *shadow_D,
+                         CyShadeMem mem, uint *err)
+{
+  float light_u, light_v;
+  path_state_rng_2D(kg, state, PRNG_LIGHT_U, &light_u, &light_v);
+  float terminate = (KD->integrator.light_inv_rr_threshold > 0.0f) ?
+                        path_state_rng_1D(kg, state, PRNG_LIGHT_TERMINATE) :
+                        0.0f;
+  CyLightSample ls;
+  if (light_sample(kg, light_u, light_v, sd->P, state->bounce, &ls, err) && ls.pdf != 0.0f) {
+    cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
+    cfloat3 I = neg3(ls.D);
+    if (shader_constant_emission_eval(kg, ls.shader, &light_eval)) {
+      if ((ls.prim != PRIM_NONE) && dot3(ls.Ng, I) < 0.0f) {
+        ls.Ng = neg3(ls.Ng);
+      }
+    }
+#if CY_SVM_TEX
+    else if (ls.type == LIGHT_BACKGROUND) {
+      /* direct_emissive_eval (kernel_emission.h:37-86): the world
+       * shader toward the sampled direction */
+      light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ls.D, mem,
+                                       *state, PATH_RAY_EMISSION, err);
+    }
+#endif
+    else {
+      cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
+    }
+    light_eval = mul3f(light_eval, ls.eval_fac);
+    if (ls.lamp != LAMP_NONE) {
+      light_eval = mul3(light_eval, klight_vec(kg->__lights[ls.lamp].strength));
+    }
+    if (!is_zero3(light_eval)) {
+      cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
+      float bpdf;
+#if CY_CLOSURE_EXT
+      if (PHASE) {
+        /* direct_emission at a volume point (kernel_emission.h:127-138): the
+         * phase functions, the MIS weight on the light's eval */
+        eval = shader_volume_phase_eval(sd, ls.D, &bpdf);
+        if ((uint)ls.shader & SHADER_USE_MIS) {
+          light_eval = mul3f(light_eval, power_heuristic(ls.pdf, bpdf));
+        }
+      }
+      else
+#endif
+      {
+        /* shader_bsdf_eval (kernel_shader.h:606-636) */
+        shader_bsdf_multi_eval(sd, ls.D, &bpdf, -1, &eval, 0.0f, 0.0f);
+        if ((uint)ls.shader & SHADER_USE_MIS) {
+          float weight = power_heuristic(ls.pdf, bpdf);
+          eval = mul3f(eval, weight);
+        }
+      }
+      eval = mul3(eval, div3f(light_eval, ls.pdf));
+      if (((uint)ls.shader & SHADER_EXCLUDE_ANY) &&
+          ((uint)ls.shader & SHADER_EXCLUDE_DIFFUSE)) {
+        eval = mk3(0.0f, 0.0f, 0.0f);
+      }
+      bool has_emission = !is_zero3(eval);
+      if (has_emission && KD->integrator.light_inv_rr_threshold > 0.0f) {
+        float lprob = max3f(fabs3(eval)) * KD->integrator.light_inv_rr_threshold;
+        if (lprob < 1.0f) {
+          if (terminate >= lprob) {
+            has_emission = false;
+          }
+          else {
+            eval = mul3f(eval, 1.0f / lprob);
+          }
+        }
+      }
+      if (has_emission) {
+        /* path_radiance_accum_light, contribution precomputed */
+        cfloat3 shaded_throughput = mul3(mul3f(throughput, 1.0f), mk3(1.0f, 1.0f, 1.0f));
+        cfloat3 contribution = mul3(shaded_throughput, eval);
+        contribution = path_radiance_clamp(kg, contribution, state->bounce);
+        if ((uint)ls.shader & SHADER_CAST_SHADOW) {
+          bool transmit = (dot3(sd->Ng, ls.D) < 0.0f);
+          cfloat3 sP = ray_offset(sd->P, transmit ? neg3(sd->Ng) : sd->Ng);
+          cfloat3 sD;
+          float st;
+          if (ls.t == CY_FLT_MAX) {
+            /* distant light */
+            sD = ls.D;
+            st = ls.t;
+          }
+          else {
+            sD = normalize_len3(sub3(ray_offset(ls.P, ls.Ng), sP), &st);
+          }
+          *shadow_D = sD;
+          cy_st(&b->shadow_P[slot], mkf4(sP.x, sP.y, sP.z, st));
+          if (KD->integrator.transparent_shadows) {
+            /* the shadow's attenuation multiplies the throughput before
+             * the eval (path_radiance_accum_light): keep both, and the
+             * bounces the occluders' shaders see (kernel_shadow.h:60-75) */
+            cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, int_as_float(state->transmission_bounce)));
+            cy_st(&b->shadow_L[slot], mkf4(eval.x, eval.y, eval.z, 0.0f));
+            const uint packed = (uint)state->bounce | ((uint)state->transparent_bounce << 8) |
+                                ((uint)state->diffuse_bounce << 16) | ((uint)state->glossy_bounce << 24);
+            cy_st(&b->shadow_T[slot], mkf4(throughput.x, throughput.y, throughput.z, as_float(packed)));
+          }
+          else {
+            cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
+            cy_st(&b->shadow_L[slot], mkf4(contribution.x, contribution.y, contribution.z, 0.0f));
+          }
+          *shadow = (st != 0.0f);
+          if (!*shadow) {
+            *L = add3(*L, contribution);
+          }
+        }
+        else {
+          *L = add3(*L, contribution);
+        }
+      }
+    }
+  }
+}
+
 /* ---------------------------------------------------------------------------
  * Stage 2: shade one path at one bounce.  Returns true when the slot must be
  * enqueued for the next closest-hit traversal.  *shadow is set when a shadow ray
@@ -751,6 +1031,45 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
  * bounce the shadow stage finishes it).  *finished is set when the path ended
  * here and its sample was recorded.
  */
+#if CY_CLOSURE_EXT
+/* kernel_path_volume_bounce: a new direction from the phase closures */
+CY_FN bool volume_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *throughput, CyPathState *state, CyRay *ray)
+{
+  float phase_u, phase_v;
+  path_state_rng_2D(kg, state, PRNG_BSDF_U, &phase_u, &phase_v);
+  cfloat3 phase_eval = mk3(0.0f, 0.0f, 0.0f);
+  cfloat3 omega_in = mk3(0.0f, 0.0f, 0.0f);
+  float phase_pdf = 0.0f;
+  const int label = shader_volume_phase_sample(sd, phase_u, phase_v, &phase_eval, &omega_in, &phase_pdf);
+  if (phase_pdf == 0.0f || is_zero3(phase_eval)) {
+    return false;
+  }
+  /* path_radiance_bsdf_bounce */
+  const float inverse_pdf = 1.0f / phase_pdf;
+  *throughput = mul3(*throughput, mul3f(phase_eval, inverse_pdf));
+  state->ray_pdf = phase_pdf;
+  state->ray_t = 0.0f;
+  state->min_ray_pdf = fminf(phase_pdf, state->min_ray_pdf);
+  path_state_next<true>(kg, state, label);
+  const float probability = path_state_continuation_probability(kg, state, *throughput);
+  if (probability == 0.0f) {
+    return false;
+  }
+  else if (probability != 1.0f) {
+    const float terminate = path_state_rng_1D(kg, state, PRNG_TERMINATE - PRNG_BOUNCE_NUM);
+    if (terminate >= probability) {
+      return false;
+    }
+    *throughput = div3f(*throughput, probability);
+  }
+  ray->P = sd->P;
+  ray->D = omega_in;
+  ray->t = CY_FLT_MAX;
+  return true;
+}
+#endif
+
+template<bool VOL = false>
 CY_FN bool shade_path(const CyGlobals *kg,
                       const CyPathBuffers *b,
                       const CyTile *tile,
@@ -833,6 +1152,29 @@ CY_FN bool shade_path(const CyGlobals *kg,
     L = mk3(L4.x, L4.y, L4.z);
   }
 
+#if CY_CLOSURE_EXT
+  /* the path's volume stack, with the update its last surface left pending */
+  CyVolumeStack vstack;
+  uint vop_object = 0u, vop_shader = 0u, vop_flags = 0u; /* this bounce's pending update */
+  int shadow_rng_offset = 0;
+  if (VOL) {
+    if (cam_item != CY_NO_ITEM) {
+      volume_stack_init(kg, &vstack);
+    }
+    else {
+      vol_stack_load(b, slot, &vstack);
+      const hc_uint4 r0 = cy_ld(&b->vol_rec[2 * (size_t)slot]);
+      const hc_uint4 r1 = cy_ld(&b->vol_rec[2 * (size_t)slot + 1]);
+      state.volume_bounce = (int)r0.w;
+      state.volume_bounds_bounce = (int)r1.x;
+      if (r0.z & CY_VOP_PATH) {
+        volume_stack_enter_exit(SD_HAS_VOLUME | ((r0.z & CY_VOP_BACKFACING) ? SD_BACKFACING : 0), (int)r0.x,
+                                (int)r0.y, &vstack);
+      }
+    }
+  }
+#endif
+
   const bool hit = as_int(is4.w) != PRIM_NONE;
   /* isect->type: the primitive's packed type (a curve's carries its segment) */
   const int type = hit ? (kg->have_curves ? (int)kg->__prim_type[as_int(is4.w)] : PRIMITIVE_TRIANGLE) : 0;
@@ -866,6 +1208,19 @@ CY_FN bool shade_path(const CyGlobals *kg,
       }
       lamp_L = mul3f(lamp_L, ls.eval_fac);
       lamp_L = mul3(lamp_L, klight_vec(kg->__lights[lamp].strength));
+#if CY_CLOSURE_EXT
+      if (VOL && vstack.e[0].shader != SHADER_NONE) {
+        /* shadow attenuation by the volumes along the segment (kernel_emission.h:264-272) */
+        CyRay volume_ray;
+        volume_ray.P = light_P;
+        volume_ray.D = ray.D;
+        volume_ray.t = ls.t;
+        cfloat3 volume_tp = mk3(1.0f, 1.0f, 1.0f);
+        CySD esd;
+        volume_shadow(kg, &esd, &state, &vstack, &volume_ray, &volume_tp, mem, err);
+        lamp_L = mul3(lamp_L, volume_tp);
+      }
+#endif
       if (!(state.flag & PATH_RAY_MIS_SKIP)) {
         lamp_L = mul3f(lamp_L, power_heuristic(state.ray_pdf, ls.pdf));
       }
@@ -877,8 +1232,38 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
 
   bool cont = false; /* path continues with a new ray */
+  cfloat3 shadow_D = mk3(0.0f, 0.0f, 0.0f);
+  bool vol_scattered = false;
 
-  if (!hit) {
+#if CY_CLOSURE_EXT
+  if (VOL) {
+    /* kernel_path_volume (kernel_path.h:149-247), distance sampling */
+    if (!hit) {
+      volume_stack_clean(kg, &vstack);
+    }
+    if (vstack.e[0].shader != SHADER_NONE) {
+      CyRay volume_ray = ray;
+      volume_ray.t = hit ? is4.x : CY_FLT_MAX;
+      const float step_size = volume_stack_step_size(kg, &vstack);
+      CySD vsd;
+      const int result = volume_integrate(kg, &state, &vsd, &vstack, &volume_ray, &L, &throughput, step_size, mem,
+                                          err);
+      if (result == VOLUME_PATH_SCATTERED) {
+        vol_scattered = true;
+        connect_light<true>(kg, b, slot, &vsd, &state, throughput, &L, shadow, &shadow_D, mem, err);
+        shadow_rng_offset = state.rng_offset;
+        if (volume_bounce(kg, &vsd, &throughput, &state, &ray)) {
+          cont = true;
+        }
+      }
+    }
+  }
+#endif
+
+  if (vol_scattered) {
+    /* the segment scattered: no surface or background at its end */
+  }
+  else if (!hit) {
     /* kernel_path_background (kernel_path.h:115-144) */
     bool skip = false;
     if (KD->background.transparent && (state.flag & PATH_RAY_TRANSPARENT_BACKGROUND)) {
@@ -946,6 +1331,31 @@ CY_FN bool shade_path(const CyGlobals *kg,
     sd.svm_fast = mem.svm_fast;
     sd.svm_spill = mem.svm_spill;
     shader_setup_from_ray(kg, &sd, &isect, &ray);
+#if CY_CLOSURE_EXT
+    if (VOL && (sd.flag & SD_HAS_ONLY_VOLUME)) {
+      /* volume bounding surface: pass through without a bounce
+       * (kernel_path_surface.h:332-352, path_state_volume_next) */
+      state.volume_bounds_bounce++;
+      if (state.volume_bounds_bounce <= VOLUME_BOUNDS_MAX) {
+        if (state.volume_bounds_bounce > 1) {
+          state.rng_offset += PRNG_BOUNCE_NUM;
+        }
+        if (state.bounce == 0) {
+          ray.t -= sd.ray_length;
+        }
+        else {
+          ray.t = CY_FLT_MAX;
+        }
+        ray.P = ray_offset(sd.P, neg3(sd.Ng));
+        vop_object = (uint)sd.object;
+        vop_shader = (uint)sd.shader;
+        vop_flags = CY_VOP_PATH | ((sd.flag & SD_BACKFACING) ? CY_VOP_BACKFACING : 0u);
+        cont = true;
+      }
+    }
+    else
+#endif
+    {
 #ifdef CY_EXP_FIXED_SVM /* profiling experiment only: one diffuse closure, no SVM */
     sd.num_closure = 1;
     sd.num_closure_left = 0;
@@ -1068,106 +1478,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
 #else
       if (KD->integrator.use_direct_light && (sd.flag & SD_BSDF_HAS_EVAL)) {
 #endif
-        float light_u, light_v;
-        path_state_rng_2D(kg, &state, PRNG_LIGHT_U, &light_u, &light_v);
-        float terminate = (KD->integrator.light_inv_rr_threshold > 0.0f) ?
-                              path_state_rng_1D(kg, &state, PRNG_LIGHT_TERMINATE) :
-                              0.0f;
-        CyLightSample ls;
-        if (light_sample(kg, light_u, light_v, sd.P, state.bounce, &ls, err) && ls.pdf != 0.0f) {
-          cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
-          cfloat3 I = neg3(ls.D);
-          if (shader_constant_emission_eval(kg, ls.shader, &light_eval)) {
-            if ((ls.prim != PRIM_NONE) && dot3(ls.Ng, I) < 0.0f) {
-              ls.Ng = neg3(ls.Ng);
-            }
-          }
-#if CY_SVM_TEX
-          else if (ls.type == LIGHT_BACKGROUND) {
-            /* direct_emissive_eval (kernel_emission.h:37-86): the world
-             * shader toward the sampled direction */
-            light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ls.D, mem,
-                                             state, PATH_RAY_EMISSION, err);
-          }
-#endif
-          else {
-            cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
-          }
-          light_eval = mul3f(light_eval, ls.eval_fac);
-          if (ls.lamp != LAMP_NONE) {
-            light_eval = mul3(light_eval, klight_vec(kg->__lights[ls.lamp].strength));
-          }
-          if (!is_zero3(light_eval)) {
-            /* shader_bsdf_eval (kernel_shader.h:606-636) */
-            cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
-            float bpdf;
-            shader_bsdf_multi_eval(&sd, ls.D, &bpdf, -1, &eval, 0.0f, 0.0f);
-            if ((uint)ls.shader & SHADER_USE_MIS) {
-              float weight = power_heuristic(ls.pdf, bpdf);
-              eval = mul3f(eval, weight);
-            }
-            eval = mul3(eval, div3f(light_eval, ls.pdf));
-            if (((uint)ls.shader & SHADER_EXCLUDE_ANY) &&
-                ((uint)ls.shader & SHADER_EXCLUDE_DIFFUSE)) {
-              eval = mk3(0.0f, 0.0f, 0.0f);
-            }
-            bool has_emission = !is_zero3(eval);
-            if (has_emission && KD->integrator.light_inv_rr_threshold > 0.0f) {
-              float lprob = max3f(fabs3(eval)) * KD->integrator.light_inv_rr_threshold;
-              if (lprob < 1.0f) {
-                if (terminate >= lprob) {
-                  has_emission = false;
-                }
-                else {
-                  eval = mul3f(eval, 1.0f / lprob);
-                }
-              }
-            }
-            if (has_emission) {
-              /* path_radiance_accum_light, contribution precomputed */
-              cfloat3 shaded_throughput = mul3(mul3f(throughput, 1.0f), mk3(1.0f, 1.0f, 1.0f));
-              cfloat3 contribution = mul3(shaded_throughput, eval);
-              contribution = path_radiance_clamp(kg, contribution, state.bounce);
-              if ((uint)ls.shader & SHADER_CAST_SHADOW) {
-                bool transmit = (dot3(sd.Ng, ls.D) < 0.0f);
-                cfloat3 sP = ray_offset(sd.P, transmit ? neg3(sd.Ng) : sd.Ng);
-                cfloat3 sD;
-                float st;
-                if (ls.t == CY_FLT_MAX) {
-                  /* distant light */
-                  sD = ls.D;
-                  st = ls.t;
-                }
-                else {
-                  sD = normalize_len3(sub3(ray_offset(ls.P, ls.Ng), sP), &st);
-                }
-                cy_st(&b->shadow_P[slot], mkf4(sP.x, sP.y, sP.z, st));
-                if (KD->integrator.transparent_shadows) {
-                  /* the shadow's attenuation multiplies the throughput before
-                   * the eval (path_radiance_accum_light): keep both, and the
-                   * bounces the occluders' shaders see (kernel_shadow.h:60-75) */
-                  cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, int_as_float(state.transmission_bounce)));
-                  cy_st(&b->shadow_L[slot], mkf4(eval.x, eval.y, eval.z, 0.0f));
-                  const uint packed = (uint)state.bounce | ((uint)state.transparent_bounce << 8) |
-                                      ((uint)state.diffuse_bounce << 16) | ((uint)state.glossy_bounce << 24);
-                  cy_st(&b->shadow_T[slot], mkf4(throughput.x, throughput.y, throughput.z, as_float(packed)));
-                }
-                else {
-                  cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
-                  cy_st(&b->shadow_L[slot], mkf4(contribution.x, contribution.y, contribution.z, 0.0f));
-                }
-                *shadow = (st != 0.0f);
-                if (!*shadow) {
-                  L = add3(L, contribution);
-                }
-              }
-              else {
-                L = add3(L, contribution);
-              }
-            }
-          }
+        connect_light<false>(kg, b, slot, &sd, &state, throughput, &L, shadow, &shadow_D, mem, err);
+      }
+#if CY_CLOSURE_EXT
+      if (VOL && *shadow) {
+        /* the shadow ray leaves through the surface: its copy of the stack
+         * crosses it (shadow_blocked_volume_path_state) */
+        shadow_rng_offset = state.rng_offset;
+        if ((sd.flag & SD_HAS_VOLUME) && dot3(sd.Ng, shadow_D) < 0.0f) {
+          vop_object = (uint)sd.object;
+          vop_shader = (uint)sd.shader;
+          vop_flags |= CY_VOP_SHADOW | ((sd.flag & SD_BACKFACING) ? CY_VOP_BACKFACING : 0u);
         }
       }
+#endif
 
       /* kernel_path_surface_bounce (kernel_path_surface.h:270-358) */
       if (sss_bounce) {
@@ -1198,10 +1522,26 @@ CY_FN bool shade_path(const CyGlobals *kg,
             ray.t = CY_FLT_MAX;
           }
           cont = true;
+#if CY_CLOSURE_EXT
+          if (VOL && (label & LABEL_TRANSMIT) && (sd.flag & SD_HAS_VOLUME)) {
+            /* enter/exit the surface's volume (kernel_path_surface.h:325-329) */
+            vop_object = (uint)sd.object;
+            vop_shader = (uint)sd.shader;
+            vop_flags |= CY_VOP_PATH | ((sd.flag & SD_BACKFACING) ? CY_VOP_BACKFACING : 0u);
+          }
+#endif
         }
       }
     }
+    }
   }
+
+#if CY_CLOSURE_EXT
+  if (VOL && (cont || *shadow)) {
+    vol_stack_store(b, slot, &vstack);
+    vol_rec_store(b, slot, vop_object, vop_shader, vop_flags, &state, shadow_rng_offset);
+  }
+#endif
 
   if (cont) {
     store_state(b, slot, &state);

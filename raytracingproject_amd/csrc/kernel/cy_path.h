@@ -1972,7 +1972,107 @@ CY_FN int svm_eval_texture_node(const hc_KernelData *data,
   return offset;
 }
 
-/* type: SHADER_TYPE_SURFACE (0) or SHADER_TYPE_DISPLACEMENT (2), svm.h:236-246 */
+#if CY_CLOSURE_EXT
+/* svm_closure.h:912-962 svm_node_closure_volume: absorption (extinction of
+ * 1 - color) or Henyey-Greenstein scattering (a phase closure with its g in
+ * alpha_x) times density; both add to the extinction. */
+CY_FN void svm_node_closure_volume(CySD *sd, CySvmStack stack, hc_uint4 node, int shader_type, uint *err)
+{
+  if (shader_type != 1) {
+    return;
+  }
+  const uint type = node.y & 0xFF, density_offset = (node.y >> 8) & 0xFF;
+  const uint anisotropy_offset = (node.y >> 16) & 0xFF, mix_weight_offset = (node.y >> 24) & 0xFF;
+  const float mix_weight = (mix_weight_offset != SVM_STACK_INVALID) ? svm_load(stack, mix_weight_offset, err) : 1.0f;
+  if (mix_weight == 0.0f) {
+    return;
+  }
+  float density = (density_offset != SVM_STACK_INVALID) ? svm_load(stack, density_offset, err) : as_float(node.z);
+  density = mix_weight * fmaxf(density, 0.0f);
+  cfloat3 weight = sd->svm_closure_weight;
+  if (type == CLOSURE_VOLUME_ABSORPTION_ID) {
+    weight = sub3(mk3(1.0f, 1.0f, 1.0f), weight);
+  }
+  weight = mul3f(weight, density);
+  if (type == CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID) {
+    CyClosure *volume = bsdf_alloc(sd, weight);
+    if (volume) {
+      const float g = (anisotropy_offset != SVM_STACK_INVALID) ? svm_load(stack, anisotropy_offset, err) :
+                                                                 as_float(node.w);
+      /* volume_henyey_greenstein_setup (closure/volume.h:54-62) */
+      volume->type = CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID;
+      volume->alpha_x = ((g < 0.0f) ? -1.0f : 1.0f) * fminf(fabsf(g), 1.0f - 1e-3f);
+      sd->flag |= SD_SCATTER;
+    }
+  }
+  /* volume_extinction_setup (closure/volume.h:24-34) */
+  if (sd->flag & SD_EXTINCTION) {
+    sd->closure_transparent_extinction = add3(sd->closure_transparent_extinction, weight);
+  }
+  else {
+    sd->flag |= SD_EXTINCTION;
+    sd->closure_transparent_extinction = weight;
+  }
+}
+
+/* svm_closure.h:964-1075 svm_node_principled_volume without volume attributes
+ * (the host packs none: find_attribute finds nothing) and without blackbody
+ * (hipcy_load_kernels refuses a blackbody intensity). */
+CY_FN void svm_node_principled_volume(const CyGlobals *kg, CySD *sd, CySvmStack stack, hc_uint4 node, int shader_type,
+                                      int path_flag, int *offset, uint *err)
+{
+  const hc_uint4 value_node = kg->__svm_nodes[*offset];
+  *offset += 2; /* value node, attribute node */
+  if (shader_type != 1) {
+    return;
+  }
+  const uint density_offset = node.y & 0xFF, anisotropy_offset = (node.y >> 8) & 0xFF;
+  const uint absorption_color_offset = (node.y >> 16) & 0xFF, mix_weight_offset = (node.y >> 24) & 0xFF;
+  const float mix_weight = (mix_weight_offset != SVM_STACK_INVALID) ? svm_load(stack, mix_weight_offset, err) : 1.0f;
+  if (mix_weight == 0.0f) {
+    return;
+  }
+  float density = (density_offset != SVM_STACK_INVALID) ? svm_load(stack, density_offset, err) :
+                                                         as_float(value_node.x);
+  density = mix_weight * fmaxf(density, 0.0f);
+  if (density > CLOSURE_WEIGHT_CUTOFF) {
+    const cfloat3 color = sd->svm_closure_weight;
+    CyClosure *volume = bsdf_alloc(sd, mul3f(color, density));
+    if (volume) {
+      const float g = (anisotropy_offset != SVM_STACK_INVALID) ? svm_load(stack, anisotropy_offset, err) :
+                                                                 as_float(value_node.y);
+      volume->type = CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID;
+      volume->alpha_x = ((g < 0.0f) ? -1.0f : 1.0f) * fminf(fabsf(g), 1.0f - 1e-3f);
+      sd->flag |= SD_SCATTER;
+    }
+    const cfloat3 zero = mk3(0.0f, 0.0f, 0.0f);
+    const cfloat3 one = mk3(1.0f, 1.0f, 1.0f);
+    const cfloat3 ac = svm_load3(stack, absorption_color_offset, err);
+    const cfloat3 absorption_color = max3v(mk3(sqrtf(ac.x), sqrtf(ac.y), sqrtf(ac.z)), zero);
+    const cfloat3 absorption = mul3(max3v(sub3(one, color), zero), max3v(sub3(one, absorption_color), zero));
+    const cfloat3 weight = mul3f(add3(color, absorption), density);
+    if (sd->flag & SD_EXTINCTION) {
+      sd->closure_transparent_extinction = add3(sd->closure_transparent_extinction, weight);
+    }
+    else {
+      sd->flag |= SD_EXTINCTION;
+      sd->closure_transparent_extinction = weight;
+    }
+  }
+  if (path_flag & PATH_RAY_SHADOW) {
+    return;
+  }
+  const uint emission_offset = node.z & 0xFF, emission_color_offset = (node.z >> 8) & 0xFF;
+  const float emission = (emission_offset != SVM_STACK_INVALID) ? svm_load(stack, emission_offset, err) :
+                                                                 as_float(value_node.z);
+  if (emission > CLOSURE_WEIGHT_CUTOFF) {
+    const cfloat3 emission_color = svm_load3(stack, emission_color_offset, err);
+    emission_setup(sd, mul3f(emission_color, emission));
+  }
+}
+#endif
+
+/* type: SHADER_TYPE_SURFACE (0), SHADER_TYPE_VOLUME (1) or SHADER_TYPE_DISPLACEMENT (2), svm.h:236-246 */
 CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err,
                           int type = 0)
 {
@@ -1989,8 +2089,16 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
       case NODE_END:
         return;
       case NODE_SHADER_JUMP:
-        offset = (int)(type == 2 ? node.w : node.y);
+        offset = (int)(type == 2 ? node.w : type == 1 ? node.z : node.y);
         break;
+#if CY_CLOSURE_EXT
+      case NODE_CLOSURE_VOLUME:
+        svm_node_closure_volume(sd, stack, node, type, err);
+        break;
+      case NODE_PRINCIPLED_VOLUME:
+        svm_node_principled_volume(kg, sd, stack, node, type, path_flag, &offset, err);
+        break;
+#endif
       case NODE_CLOSURE_BSDF:
         svm_node_closure_bsdf(kg, sd, stack, node, path_flag, &offset, err);
         break;

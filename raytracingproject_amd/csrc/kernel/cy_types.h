@@ -101,7 +101,19 @@ enum {
   SD_HAS_TRANSPARENT_SHADOW = (1 << 17),
   SD_HAS_VOLUME = (1 << 18),
   SD_HAS_ONLY_VOLUME = (1 << 19),
-  SD_HAS_CONSTANT_EMISSION = (1 << 27)
+  SD_HETEROGENEOUS_VOLUME = (1 << 20),
+  SD_HAS_BSSRDF_BUMP = (1 << 21),
+  SD_VOLUME_EQUIANGULAR = (1 << 22),
+  SD_VOLUME_MIS = (1 << 23),
+  SD_VOLUME_CUBIC = (1 << 24),
+  SD_HAS_BUMP = (1 << 25),
+  SD_HAS_DISPLACEMENT = (1 << 26),
+  SD_HAS_CONSTANT_EMISSION = (1 << 27),
+  SD_NEED_VOLUME_ATTRIBUTES = (1 << 28),
+  SD_SHADER_FLAGS = (SD_USE_MIS | SD_HAS_TRANSPARENT_SHADOW | SD_HAS_VOLUME | SD_HAS_ONLY_VOLUME |
+                     SD_HETEROGENEOUS_VOLUME | SD_HAS_BSSRDF_BUMP | SD_VOLUME_EQUIANGULAR | SD_VOLUME_MIS |
+                     SD_VOLUME_CUBIC | SD_HAS_BUMP | SD_HAS_DISPLACEMENT | SD_HAS_CONSTANT_EMISSION |
+                     SD_NEED_VOLUME_ATTRIBUTES)
 };
 
 enum {
@@ -109,8 +121,14 @@ enum {
   SD_OBJECT_MOTION = (1 << 1),
   SD_OBJECT_TRANSFORM_APPLIED = (1 << 2),
   SD_OBJECT_NEGATIVE_SCALE_APPLIED = (1 << 3),
+  SD_OBJECT_HAS_VOLUME = (1 << 4),
+  SD_OBJECT_INTERSECTS_VOLUME = (1 << 5),
   SD_OBJECT_HAS_VERTEX_MOTION = (1 << 6),
-  SD_OBJECT_SHADOW_CATCHER = (1 << 7)
+  SD_OBJECT_SHADOW_CATCHER = (1 << 7),
+  SD_OBJECT_HAS_VOLUME_ATTRIBUTES = (1 << 8),
+  SD_OBJECT_FLAGS = (SD_OBJECT_HOLDOUT_MASK | SD_OBJECT_MOTION | SD_OBJECT_TRANSFORM_APPLIED |
+                     SD_OBJECT_NEGATIVE_SCALE_APPLIED | SD_OBJECT_HAS_VOLUME | SD_OBJECT_INTERSECTS_VOLUME |
+                     SD_OBJECT_SHADOW_CATCHER | SD_OBJECT_HAS_VOLUME_ATTRIBUTES)
 };
 
 /* NodeNormalMapSpace (svm_types.h:455-461) */
@@ -142,7 +160,9 @@ enum {
   NODE_TEX_IMAGE_BOX = 24,
   NODE_TEX_ENVIRONMENT = 55,
   NODE_FRESNEL = 38,
-  NODE_LAYER_WEIGHT = 39
+  NODE_LAYER_WEIGHT = 39,
+  NODE_CLOSURE_VOLUME = 40,
+  NODE_PRINCIPLED_VOLUME = 41
 };
 
 #define NODE_LAYER_WEIGHT_FRESNEL 0
@@ -187,6 +207,9 @@ enum {
   CLOSURE_BSSRDF_RANDOM_WALK_ID = 39,
   CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID = 40,
   CLOSURE_HOLDOUT_ID = 41,
+  CLOSURE_VOLUME_ID = 42,
+  CLOSURE_VOLUME_ABSORPTION_ID = 43,
+  CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID = 44,
   CLOSURE_BSDF_PRINCIPLED_ID = 45,
   NBUILTIN_CLOSURES = 46
 };
@@ -205,9 +228,12 @@ enum {
    ((type) == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID))
 #define CLOSURE_IS_HOLDOUT(type) ((type) == CLOSURE_HOLDOUT_ID)
 #define CLOSURE_IS_BSSRDF(type) ((type) >= CLOSURE_BSSRDF_CUBIC_ID && (type) <= CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID)
+#define CLOSURE_IS_VOLUME(type) ((type) >= CLOSURE_VOLUME_ID && (type) <= CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID)
+#define CLOSURE_IS_PHASE(type) ((type) == CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID)
 #define CLOSURE_IS_DISK_BSSRDF(type) ((type) >= CLOSURE_BSSRDF_CUBIC_ID && (type) <= CLOSURE_BSSRDF_BURLEY_ID)
 #define BSSRDF_MIN_RADIUS 1e-8f   /* kernel_types.h:49-51 */
 #define BSSRDF_MAX_BOUNCES 256
+#define VOLUME_BOUNDS_MAX 1024    /* kernel_types.h:54 */
 
 #define CLOSURE_WEIGHT_CUTOFF 1e-5f
 #define SVM_STACK_INVALID 255
@@ -363,6 +389,8 @@ typedef struct CyPathState {
   float min_ray_pdf;
   float ray_pdf;
   float ray_t;
+  int volume_bounce;        /* volume scenes only (cy_volume.h) */
+  int volume_bounds_bounce;
 } CyPathState;
 
 #endif /* CY_TYPES_H */

@@ -104,6 +104,21 @@ BECKMANN_CLOSURES = (CLOSURE_BSDF_MICROFACET_BECKMANN_ID, CLOSURE_BSDF_MICROFACE
                      CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)
 SD_HAS_TRANSPARENT_SHADOW = 1 << 17
 SD_HAS_DISPLACEMENT = 1 << 26
+# volumes (kernel_types.h:832-931, svm_types.h:577-579, 105-106)
+SD_HAS_VOLUME = 1 << 18
+SD_HAS_ONLY_VOLUME = 1 << 19
+SD_HETEROGENEOUS_VOLUME = 1 << 20
+SD_NEED_VOLUME_ATTRIBUTES = 1 << 28
+SD_OBJECT_HAS_VOLUME = 1 << 4
+SD_OBJECT_INTERSECTS_VOLUME = 1 << 5
+CLOSURE_VOLUME_ABSORPTION_ID = 43
+CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID = 44
+NODE_CLOSURE_VOLUME, NODE_PRINCIPLED_VOLUME = 40, 41
+VOLUME_STACK_SIZE = 32  # kernel_types.h:64
+ATTR_STD_VOLUME_DENSITY, ATTR_STD_VOLUME_TEMPERATURE, ATTR_STD_NUM = 18, 22, 26
+# PrincipledVolumeNode sockets and defaults (render/nodes.cpp:3376-3410)
+PRINCIPLED_VOLUME_DEFAULTS = {"absorption_color": (0.0, 0.0, 0.0), "emission_strength": 0.0,
+                              "emission_color": (1.0, 1.0, 1.0)}
 
 
 def f32bits(x: float) -> int:
@@ -143,6 +158,10 @@ class Closure:
     # material output "Displacement" (a vector socket, e.g. nodes.displacement),
     # displacement method "true": its own SVM program, run by SHADER_EVAL_DISPLACE
     displacement: object = None
+    # material output "Volume": a tree of volume closures (volume_absorption,
+    # volume_scatter, principled_volume, emission, mix), its own SVM program
+    volume: "Closure | None" = None
+    density: object = 1.0  # volume closures
 
     def closure_type(self) -> int:
         """The ClosureType the node compiles to, after simplify_settings
@@ -173,12 +192,20 @@ class Closure:
             return 8  # CLOSURE_IS_PRINCIPLED
         if self.kind == "subsurface":
             return 3  # CLOSURE_IS_BSSRDF
+        if self.kind in VOLUME_KINDS:
+            return VOLUME_STACK_SIZE  # CLOSURE_IS_VOLUME
+        if self.kind in ("none", "emission", "background"):
+            return 0 if self.kind == "none" else 1
         return 1
+
+    def material_closures(self) -> int:
+        """ShaderGraph::get_num_closures over both outputs of a material."""
+        return self.num_closures() + (self.volume.num_closures() if self.volume is not None else 0)
 
     def closure_types(self) -> set:
         if self.kind == "mix":
             return self.a.closure_types() | self.b.closure_types()
-        if self.kind in ("emission", "background"):
+        if self.kind in ("emission", "background", "none") or self.kind in VOLUME_KINDS:
             return set()
         if self.kind == "principled":
             return {CLOSURE_BSDF_PRINCIPLED_ID}
@@ -201,11 +228,11 @@ class Closure:
         for name, t in (("color", "color"), ("roughness", "float"), ("ior", "float"), ("strength", "float"),
                         ("fac", "float"), ("normal", "vector"), ("anisotropy", "float"), ("rotation", "float"),
                         ("tangent", "vector"), ("radius", "vector"), ("sharpness", "float"),
-                        ("texture_blur", "float")):
+                        ("texture_blur", "float"), ("density", "float")):
             v = getattr(self, name)
             if nodes.is_linked(v) and (self.kind == "mix") == (name == "fac"):
                 out.append((v, t))
-        if self.kind == "principled":
+        if self.kind in ("principled", "principled_volume"):
             for name, v in self.params.items():
                 if nodes.is_linked(v):
                     vec = name in PRINCIPLED_VECTORS or name == "subsurface_radius"
@@ -286,6 +313,40 @@ def subsurface(color, scale=0.01, radius=(0.1, 0.1, 0.1), falloff="random_walk",
         raise ValueError(f"subsurface: unknown falloff {falloff}")
     return Closure("subsurface", _const_or_socket(color), strength=scale, radius=radius, distribution=falloff,
                    texture_blur=texture_blur, sharpness=sharpness, normal=normal)
+
+
+VOLUME_KINDS = ("volume_absorption", "volume_scatter", "principled_volume")
+
+
+def volume_absorption(color=(0.8, 0.8, 0.8), density=1.0):
+    """Volume Absorption node (nodes.cpp AbsorptionVolumeNode)."""
+    return Closure("volume_absorption", _const_or_socket(color), density=density)
+
+
+def volume_scatter(color=(0.8, 0.8, 0.8), density=1.0, anisotropy=0.0):
+    """Volume Scatter node (nodes.cpp ScatterVolumeNode): Henyey-Greenstein."""
+    return Closure("volume_scatter", _const_or_socket(color), density=density, anisotropy=anisotropy)
+
+
+def principled_volume(color=(0.5, 0.5, 0.5), density=1.0, anisotropy=0.0, **params):
+    """Principled Volume node (nodes.cpp PrincipledVolumeNode) without volume
+    attributes (no voxel grids: the density and color attributes are never
+    found) and without blackbody emission.  params: absorption_color,
+    emission_strength, emission_color."""
+    unknown = set(params) - set(PRINCIPLED_VOLUME_DEFAULTS)
+    if unknown:
+        raise ValueError(f"principled_volume: unknown parameters {sorted(unknown)}")
+    p = dict(PRINCIPLED_VOLUME_DEFAULTS)
+    p.update(params)
+    return Closure("principled_volume", _const_or_socket(color), density=density, anisotropy=anisotropy, params=p)
+
+
+def material(surface=None, volume=None):
+    """A material with a Surface and / or a Volume output.  Without a surface
+    the mesh only bounds its volume (SD_HAS_ONLY_VOLUME: rays pass through)."""
+    m = surface if surface is not None else Closure("none")
+    m.volume = volume
+    return m
 
 
 def translucent(color, normal=None):
@@ -383,6 +444,10 @@ class SVMCompiler:
             return out
         if c.kind == "principled":
             return self.emit_principled(c, mix_weight)
+        if c.kind == "none":
+            return out
+        if c.kind in VOLUME_KINDS:
+            return self.emit_volume(c, mix_weight)
         ctype = c.closure_type()
         # nodes.cpp BsdfNode::compile: linked color -> NODE_CLOSURE_WEIGHT
         if nodes.is_linked(c.color):
@@ -416,6 +481,50 @@ class SVMCompiler:
         emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))
         # data node: normal, tangent, param3, param4
         emit((normal_off, tangent_off, param3_off, param4_off))
+        return out
+
+    def emit_volume(self, c: Closure, mix_weight: int) -> list:
+        """nodes.cpp:3273-3290 VolumeNode::compile (absorption: density;
+        scatter: density, anisotropy) and 3417-3455 PrincipledVolumeNode::compile
+        (closure node, value node, attribute node)."""
+        out = []
+        emit = out.append
+        if nodes.is_linked(c.color):
+            emit((NODE_CLOSURE_WEIGHT, self.nc.link(c.color, "color"), 0, 0))
+        else:
+            emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in c.color)))
+        if c.kind in ("volume_absorption", "volume_scatter"):
+            ctype = CLOSURE_VOLUME_ABSORPTION_ID if c.kind == "volume_absorption" else \
+                CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID
+            d_off, d_val = self._float_param(c.density)
+            a_off, a_val = (self._float_param(c.anisotropy) if c.kind == "volume_scatter"
+                            else (SVM_STACK_INVALID, 0.0))
+            emit((NODE_CLOSURE_VOLUME, self.uchar4(ctype, d_off, a_off, mix_weight), f32bits(d_val), f32bits(a_val)))
+            return out
+        p = c.params
+        nc = self.nc
+        temps: list = []
+        saved_emit, nc.emit = nc.emit, emit
+        try:
+            d_off = nc.link(c.density, "float") if nodes.is_linked(c.density) else SVM_STACK_INVALID
+            a_off = nc.link(c.anisotropy, "float") if nodes.is_linked(c.anisotropy) else SVM_STACK_INVALID
+            ac_off = nc.assign(p["absorption_color"], "color", temps)
+            e_off = (nc.link(p["emission_strength"], "float") if nodes.is_linked(p["emission_strength"])
+                     else SVM_STACK_INVALID)
+            ec_off = nc.assign(p["emission_color"], "color", temps)
+        finally:
+            nc.emit = saved_emit
+
+        def const(v):
+            return 0.0 if nodes.is_linked(v) else float(v)
+
+        emit((NODE_PRINCIPLED_VOLUME, self.uchar4(d_off, a_off, ac_off, mix_weight),
+              self.uchar4(e_off, ec_off, SVM_STACK_INVALID, SVM_STACK_INVALID), SVM_STACK_INVALID))
+        emit((f32bits(const(c.density)), f32bits(const(c.anisotropy)), f32bits(const(p["emission_strength"])),
+              f32bits(0.0)))
+        emit((ATTR_STD_VOLUME_DENSITY, ATTR_STD_NUM, ATTR_STD_VOLUME_TEMPERATURE, 0))
+        for off, w in temps:
+            self.free(off, w)
         return out
 
     def emit_principled(self, c: Closure, mix_weight: int) -> list:
@@ -496,12 +605,28 @@ class SVMCompiler:
                 self.nc.link(v, t)
             self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
             self.nodes.append((NODE_END, 0, 0, 0))
+            vol = getattr(sh, "volume", None)
+            vol_start = 0
+            if vol is not None:
+                # svm.cpp SVMCompiler::compile: the volume program's start in
+                # the jump node's z
+                vol_start = len(self.nodes)
+                self.nodes[i] = (NODE_SHADER_JUMP, start, vol_start, 0)
+                self.stack_top = 0
+                self.stack_used = [False] * SVM_STACK_SIZE
+                vsocks = vol.sockets()
+                self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [v for v, _ in vsocks], self.free,
+                                             images=self.images)
+                for v, t in vsocks:
+                    self.nc.link(v, t)
+                self.nodes.extend(self.emit_closure(vol, SVM_STACK_INVALID))
+                self.nodes.append((NODE_END, 0, 0, 0))
             disp = getattr(sh, "displacement", None)
             if nodes.is_linked(disp):
                 # svm.cpp SVMCompiler::compile: the displacement program's start
                 # in the jump node's w; OutputNode::compile emits
                 # NODE_SET_DISPLACEMENT of the "Displacement" input (nodes.cpp)
-                self.nodes[i] = (NODE_SHADER_JUMP, start, 0, len(self.nodes))
+                self.nodes[i] = (NODE_SHADER_JUMP, start, vol_start, len(self.nodes))
                 self.stack_top = 0
                 self.stack_used = [False] * SVM_STACK_SIZE
                 self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [disp], self.free,
@@ -647,6 +772,8 @@ class Scene:
     hairs: list = field(default_factory=list)
     hair_shape: str = "ribbon"
     hair_subdivisions: int = 3
+    # world "Volume" output (a volume closure tree, e.g. a homogeneous fog)
+    world_volume: "Closure | None" = None
 
 
 def _has_displacement(m) -> bool:
@@ -918,6 +1045,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         lamp_shader = len(mats)
         mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
     world = background(scene.world_color, scene.world_strength)
+    world.volume = scene.world_volume
     svm_compiler = SVMCompiler()
     svm = svm_compiler.compile(mats, world)
     n_shaders = len(mats) + 1
@@ -934,6 +1062,19 @@ def compile_scene(scene: Scene) -> DeviceScene:
             kshaders[i].constant_emission[:] = [float(c) for c in const]
         if _has_displacement(m):
             flag |= SD_HAS_DISPLACEMENT  # shader.cpp:559-560 (displacement_method true)
+        if m.volume is not None:
+            # shader.cpp:529-553: a volume shader has transparent shadows; one
+            # without a surface only bounds its volume; heterogeneous_volume
+            # (default true) with spatially varying inputs steps the volume
+            flag |= SD_HAS_VOLUME | SD_HAS_TRANSPARENT_SHADOW
+            any_transparent_shadow = True
+            if m.kind == "none":
+                flag |= SD_HAS_ONLY_VOLUME
+            vsocks = [v for v, _ in m.volume.sockets()]
+            if _nodes.has_spatial_varying(vsocks):
+                flag |= SD_HETEROGENEOUS_VOLUME
+            if _volume_attribute_dependency(m.volume):
+                flag |= SD_NEED_VOLUME_ATTRIBUTES
         kshaders[i].flags = flag
     tri_shader = tri_shader_idx.astype(np.uint32) | np.uint32(SHADER_CAST_SHADOW | SHADER_AREA_LIGHT)
     tri_shader = np.where(tri_smooth, tri_shader | np.uint32(SHADER_SMOOTH_NORMAL), tri_shader).astype(np.uint32)
@@ -953,6 +1094,36 @@ def compile_scene(scene: Scene) -> DeviceScene:
         if ob["applied"]:
             object_flag[i] = SD_OBJECT_TRANSFORM_APPLIED
         object_node[i] = np.uint32(ob["node"] & 0xFFFFFFFF)
+
+    # --- volume objects (object.cpp:678-736 device_update_flags,
+    # object.cpp:270-349 compute_volume_step_size, :378-389 volume density)
+    use_volumes = any(m.volume is not None for m in mats) or world.volume is not None
+    object_volume_step = np.full(max(nobj, 1), FLT_MAX, dtype=np.float32)
+    vol_bounds = []
+    for i, ob in enumerate(objects):
+        used = _object_shaders(ob, tri_shader_idx)
+        vmats = [mats[k] for k in used if mats[k].volume is not None]
+        if not vmats:
+            continue
+        object_flag[i] |= SD_OBJECT_HAS_VOLUME
+        kobjects[i].surface_area = 1.0
+        lo, hi = _object_bounds(ob, g)
+        vol_bounds.append((i, lo, hi))
+        step_rate = FLT_MAX
+        for m in vmats:
+            if _nodes.has_spatial_varying([v for v, _ in m.volume.sockets()]) or \
+                    _volume_attribute_dependency(m.volume):
+                step_rate = min(step_rate, 1.0)  # Shader::volume_step_rate default
+        if step_rate != FLT_MAX:
+            size = (hi - lo).astype(np.float32)
+            avg = np.float32(np.float32(np.float32(size[0] + size[1]) + size[2]) * np.float32(1.0 / 3.0))
+            object_volume_step[i] = np.float32(np.float32(0.1) * avg) * np.float32(step_rate)
+    for i, ob in enumerate(objects):
+        lo, hi = _object_bounds(ob, g)
+        for j, vlo, vhi in vol_bounds:
+            if j != i and np.all(lo <= vhi) and np.all(vlo <= hi):
+                object_flag[i] |= SD_OBJECT_INTERSECTS_VOLUME
+                break
 
     # --- lights (render/light.cpp:277-480, mesh lights only)
     # light.cpp:330-400: per object using emissive triangles, in object order,
@@ -1074,8 +1245,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
     else:
         ki.adaptive_threshold = scene.adaptive_threshold
     ki.light_inv_rr_threshold = (1.0 / scene.light_sampling_threshold) if scene.light_sampling_threshold > 0 else 0.0
-    ki.use_volumes = 0
-    ki.max_closures = max([m.num_closures() for m in mats] + [1])
+    ki.use_volumes = int(use_volumes)  # shader.cpp:601
+    ki.max_closures = max([m.material_closures() for m in mats + [world]] + [1])
     total_bounces = scene.max_bounce + scene.transparent_max_bounce + 3 + VOLUME_BOUNDS_MAX + BSSRDF_MAX_BOUNCES
     dims = min(PRNG_BASE_NUM + total_bounces * PRNG_BOUNCE_NUM, sobol.SOBOL_MAX_DIMENSIONS)
     lut = sobol.sample_pattern_lut(dims)
@@ -1083,7 +1254,15 @@ def compile_scene(scene: Scene) -> DeviceScene:
     # --- background (render/background.cpp:63-118)
     kb = kd.background
     kb.surface_shader = n_shaders - 1
-    kb.volume_shader = -1
+    # background.cpp:92-97: the world's volume (get_shader_id: default flags)
+    kb.volume_shader = ((n_shaders - 1) | SHADER_CAST_SHADOW | SHADER_AREA_LIGHT) if world.volume is not None else -1
+    if kb.volume_shader != -1:
+        kb.volume_shader = kb.volume_shader - (1 << 32) if kb.volume_shader >= (1 << 31) else kb.volume_shader
+    if use_volumes:
+        # volume_step_size * volume_step_rate (the reference writes it for every
+        # scene; it is read only through a world volume, so scenes without
+        # volumes keep 0 and their golden digests)
+        kb.volume_step_size = float(np.float32(0.1) * np.float32(1.0))
     kb.transparent = 0
     kb.transparent_roughness_squared_threshold = -1.0
     kb.ao_factor = 0.0
@@ -1149,6 +1328,14 @@ def compile_scene(scene: Scene) -> DeviceScene:
 
     # --- camera
     compile_camera(kd.cam, scene.camera, scene.width, scene.height)
+    # camera.cpp:495-527 device_update_volume: a volume object whose bounds
+    # hold the view plane (at the near clip: the eye) puts the camera inside
+    kd.cam.is_inside_volume = 0
+    if use_volumes:
+        eye = np.asarray(scene.camera.eye, dtype=np.float32)
+        for _, vlo, vhi in vol_bounds:
+            if np.all(eye >= vlo - 1e-3) and np.all(eye <= vhi + 1e-3):
+                kd.cam.is_inside_volume = 1
 
     # --- bvh
     kd.bvh.root = root
@@ -1182,6 +1369,11 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "__lookup_table": lookup,
         "__sample_pattern_lut": lut,
     }
+    if use_volumes:
+        arrays["__object_volume_step"] = object_volume_step
+        # geometry.cpp device_update_attributes: no attributes are packed, every
+        # object's map is the ATTR_STD_NONE terminator (ATTR_PRIM_TYPES rows)
+        arrays["__attributes_map"] = np.zeros((2, 4), dtype=np.uint32)
     if g["ncurves"]:
         # Hair::pack_curves (render/hair.cpp): keys with radius, per curve the
         # first key, key count and shader id (get_shader_id(shader, false))
@@ -1214,6 +1406,36 @@ def compile_scene(scene: Scene) -> DeviceScene:
     info["textures"] = len(svm_compiler.images)
     return DeviceScene(kd, arrays, scene.width, scene.height, scene.samples, info,
                        textures=list(svm_compiler.images))
+
+
+def _volume_attribute_dependency(v) -> bool:
+    """Shader::has_volume_attribute_dependency (svm.cpp:443-448): a principled
+    volume, or an attribute-reading node, in the volume graph."""
+    if v is None:
+        return False
+    if v.kind == "mix":
+        return _volume_attribute_dependency(v.a) or _volume_attribute_dependency(v.b)
+    if v.kind == "principled_volume":
+        return True
+    return any(n.kind in ("tex_coord", "geometry", "image_texture", "environment_texture")
+               for s, _ in v.sockets() for n in _nodes.upstream(s))
+
+
+def _object_shaders(ob, tri_shader_idx) -> list:
+    """Material indices the object's triangles use (Mesh::used_shaders)."""
+    lo, n = ob["tri_offset"], ob["ntri"]
+    return sorted(set(int(k) for k in np.unique(tri_shader_idx[lo:lo + n]))) if n else []
+
+
+def _object_bounds(ob, g):
+    """World-space bounds of an object's triangles (Object::bounds)."""
+    lo, n = ob["tri_offset"], ob["ntri"]
+    if n == 0:
+        return np.zeros(3, np.float32), np.zeros(3, np.float32)
+    p = g["tri_pos_object"][lo:lo + n].reshape(-1, 3).astype(np.float32)
+    if not ob["applied"]:
+        p = np.array([transform_point_f32(ob["tfm"], q) for q in p], dtype=np.float32)
+    return p.min(axis=0), p.max(axis=0)
 
 
 def transform_point_f32(tfm, p) -> np.ndarray:
@@ -1685,4 +1907,5 @@ ELEMENT_BYTES = {
     "__texture_info": 96,
     "__light_background_marginal_cdf": 8, "__light_background_conditional_cdf": 8,
     "__curves": 16, "__curve_keys": 16,
+    "__object_volume_step": 4, "__attributes_map": 16,
 }

@@ -526,8 +526,9 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
     """Junk Shop-class stand-in (SURVEY.md §8(d) config JNK): a cluttered shop
     interior (shelves of boxes, a counter, barrels) with furry props -- a rug,
     brushes and fur balls -- about 1.3M curve segments at detail 1, lit by
-    area lamps and a window panel.  (The JNK volume is not part of this
-    stand-in yet: volumes are not implemented.)"""
+    area lamps and a window panel -- and volumes: a dusty (homogeneous,
+    forward-scattering) atmosphere in the world and a smoke volume in the
+    window light (a volume-only box with a principled volume)."""
     rng = np.random.default_rng(0x5EED + 4)
     wall = sc.diffuse((0.55, 0.5, 0.45))
     wood = sc.mix(0.2, sc.glossy((0.6, 0.45, 0.3), 0.3), sc.diffuse((0.45, 0.3, 0.18)))
@@ -537,7 +538,9 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
     fur2 = sc.mix(0.25, sc.glossy((0.9, 0.85, 0.8), 0.3), sc.diffuse((0.25, 0.2, 0.15)))
     rug = sc.diffuse((0.5, 0.12, 0.1))
     window = sc.emission((1.0, 0.97, 0.9), 8.0)
-    materials = [wall, wood, metal, cardboard, fur1, fur2, rug, window]
+    smoke = sc.material(volume=sc.principled_volume((0.7, 0.7, 0.72), density=0.35, anisotropy=0.3,
+                                                    absorption_color=(0.4, 0.4, 0.45)))
+    materials = [wall, wood, metal, cardboard, fur1, fur2, rug, window, smoke]
     meshes = []
     W, D, H = 10.0, 8.0, 4.0
     meshes.append(sc.Mesh(*_quad((-W, 0, -D), (W, 0, -D), (W, 0, D), (-W, 0, D)), shader=1))
@@ -582,6 +585,7 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
         meshes.append(sc.Mesh(*_box((x, 0.45, -2.0), (0.7, 0.9, 0.25)), shader=1))
         kk, rr, ff, nn = _strands(rng, roots, np.tile([0.0, 1.0, 0.0], (len(roots), 1)), 4, 0.4, 0.003, 0.002, 0.1)
         hairs.append(sc.Hair(kk, rr, ff, nn, shader=5))
+    meshes.append(sc.Mesh(*_box((0.0, 2.3, D - 1.2), (5.0, 2.4, 1.6)), shader=8))
     lamps = [sc.Lamp("area", co=(0.0, H - 0.05, 0.0), direction=(0.0, -1.0, 0.0), axisu=(1.0, 0.0, 0.0),
                      axisv=(0.0, 0.0, 1.0), size=1.0, sizeu=3.0, sizev=2.0, color=(1.0, 0.9, 0.75), strength=600.0),
              sc.Lamp("area", co=(-6.0, H - 0.05, -4.0), direction=(0.0, -1.0, 0.0), axisu=(1.0, 0.0, 0.0),
@@ -590,7 +594,8 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
                     farclip=100.0)
     return sc.Scene(width, height, cam, meshes, materials, world_color=(0.0, 0.0, 0.0), world_strength=0.0,
                     samples=samples, filter_type="blackman_harris", filter_width=1.5, lamps=lamps, hairs=hairs,
-                    hair_shape=shape, max_bounce=8, name="junkshop_standin")
+                    hair_shape=shape, max_bounce=8, name="junkshop_standin",
+                    world_volume=sc.volume_scatter((0.9, 0.88, 0.85), density=0.012, anisotropy=0.5))
 
 
 # ---------------------------------------------------------------------------
@@ -626,6 +631,47 @@ def sss_cornell(width=48, height=48, samples=8, instanced=False) -> sc.Scene:
             s.meshes.append(sc.Mesh(*_ellipsoid(c, (70.0, 65.0, 70.0), 20, 12), shader=base + i, smooth=i % 2 == 0))
     s.lamps = [sc.Lamp("point", co=(140.0, 480.0, 40.0), size=20.0, color=(1.0, 0.8, 0.6), strength=3.0e6)]
     s.name = "sss_instanced" if instanced else "sss_cornell"
+    return s
+
+
+def volume_cornell(width=48, height=48, samples=8, heterogeneous=False) -> sc.Scene:
+    """Cornell box with volumes (golden parity case): homogeneous fog in the
+    world (Henyey-Greenstein, forward scattering), a volume-only box with a
+    principled volume, a glass sphere filled with an absorbing medium, a
+    glowing principled-volume box and a point lamp whose MIS hits are
+    attenuated by the fog.  heterogeneous=True drives the density of a
+    scattering box and the world fog by textures of the position (ray
+    marching with the jittered step of kernel_volume_step_init)."""
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    smoke = sc.material(volume=sc.principled_volume((0.8, 0.5, 0.35), density=0.012, anisotropy=-0.3,
+                                                    absorption_color=(0.3, 0.6, 0.2)))
+    tinted_glass = sc.material(sc.glass((1.0, 1.0, 1.0), 0.0, ior=1.33),
+                               volume=sc.volume_absorption((0.1, 0.5, 0.9), density=0.02))
+    glow = sc.material(volume=sc.principled_volume((0.6, 0.6, 0.6), density=0.004,
+                                                   emission_strength=0.02, emission_color=(1.0, 0.5, 0.2)))
+    mats = [smoke, tinted_glass, glow]
+    fog = sc.volume_scatter((0.9, 0.9, 0.95), density=0.0006, anisotropy=0.4)
+    if heterogeneous:
+        from . import nodes
+
+        co = nodes.tex_coord()["Object"]
+        dens = nodes.math("multiply", nodes.checker(co, (1.0, 1.0, 1.0), (0.1, 0.1, 0.1), scale=0.02)["Fac"],
+                          0.03)
+        mats.append(sc.material(volume=sc.mix(0.3, sc.volume_scatter((0.7, 0.8, 0.9), density=dens, anisotropy=0.2),
+                                              sc.volume_absorption((0.5, 0.2, 0.2), density=dens))))
+        px = nodes.separate_xyz(nodes.tex_coord()["Object"])["X"]
+        fog = sc.volume_scatter((0.9, 0.9, 0.95), density=nodes.math("multiply", px, 0.000002), anisotropy=0.0)
+    s.materials.extend(mats)
+    s.meshes.append(sc.Mesh(*_box((150.0, 300.0, 300.0), (140, 160, 140), 0.4), shader=base))
+    s.meshes.append(sc.Mesh(*_ellipsoid((400.0, 110.0, 140.0), (90.0, 90.0, 90.0), 24, 14), shader=base + 1,
+                            smooth=True))
+    s.meshes.append(sc.Mesh(*_box((420.0, 420.0, 380.0), (110, 90, 110), -0.2), shader=base + 2))
+    if heterogeneous:
+        s.meshes.append(sc.Mesh(*_box((260.0, 120.0, 330.0), (160, 200, 160), 0.2), shader=base + 3))
+    s.world_volume = fog
+    s.lamps = [sc.Lamp("point", co=(100.0, 450.0, 100.0), size=25.0, color=(1.0, 0.9, 0.8), strength=2.0e6)]
+    s.name = "volume_hetero" if heterogeneous else "volume_cornell"
     return s
 
 

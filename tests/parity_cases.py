@@ -59,6 +59,11 @@ CASES = {
     # instanced geometry (scene_intersect_local through bvh_instance_push)
     "sss_cornell": lambda: scenes.sss_cornell(48, 48, 8),
     "sss_instanced": lambda: scenes.sss_cornell(48, 48, 8, instanced=True),
+    # volumes (kernel_volume.h, distance sampling as on GPU devices): world fog,
+    # volume-only boxes, a glass sphere with an absorbing interior, emission;
+    # heterogeneous: texture-driven densities, ray marching
+    "volume_cornell": lambda: scenes.volume_cornell(48, 48, 8),
+    "volume_hetero": lambda: scenes.volume_cornell(32, 32, 4, heterogeneous=True),
 }
 # Cases whose __sample_pattern_lut is the reference host's table (fixture)
 JOE_KUO_CASES = {"cornell_joe_kuo"}

@@ -267,6 +267,11 @@ extern "C" int emu_render(const void *data,
   b.shadow_L = &rec[8];
   b.shadow_T = &rec[9];
   b.item = &item_slot;
+  hc_uint4 vol_stack[CY_VOLUME_STACK / 2];
+  hc_uint4 vol_rec[2];
+  b.vol_stack = vol_stack;
+  b.vol_rec = vol_rec;
+  const bool vol = ((const hc_KernelData *)data)->integrator.use_volumes != 0;
   uint err = 0;
   CyTile tile;
   tile.x = tx;
@@ -318,11 +323,17 @@ extern "C" int emu_render(const void *data,
       mem.svm_stride = 1;
       mem.svm_fast = CY_SVM_STACK;
       mem.svm_spill = nullptr;
-      bool cont = shade_path(&kg, &b, &tile, 0, cam_item, mem, &shadow, &finished, &err);
+      bool cont = vol ? shade_path<true>(&kg, &b, &tile, 0, cam_item, mem, &shadow, &finished, &err) :
+                        shade_path<false>(&kg, &b, &tile, 0, cam_item, mem, &shadow, &finished, &err);
       cam_item = CY_NO_ITEM;
       if (shadow && kg.data->integrator.transparent_shadows) {
         /* k_intersect_shadow_transparent */
-        shadow_finish_transparent(&kg, &b, &tile, 0, mem, &err);
+        if (vol) {
+          shadow_finish_transparent<true>(&kg, &b, &tile, 0, mem, &err);
+        }
+        else {
+          shadow_finish_transparent<false>(&kg, &b, &tile, 0, mem, &err);
+        }
       }
       else if (shadow) {
         /* k_intersect_shadow */
