@@ -1966,6 +1966,22 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           }
           tex = true;
           break;
+        case NODE_TEX_NOISE:
+        case NODE_TEX_WAVE:
+        case NODE_TEX_MUSGRAVE:
+        case NODE_TEX_VORONOI:
+          len = 3; /* two parameter nodes */
+          tex = true;
+          break;
+        case NODE_TEX_MAGIC:
+          len = 2;
+          tex = true;
+          break;
+        case NODE_TEX_BRICK:
+          len = 4;
+          tex = true;
+          break;
+        case NODE_TEX_WHITE_NOISE:
         case NODE_GEOMETRY:
         case NODE_CONVERT:
         case NODE_HSV:

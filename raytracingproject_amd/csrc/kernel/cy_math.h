@@ -25,12 +25,14 @@
 #if defined(__HIPCC__) || defined(__HIP_DEVICE_COMPILE__)
 #  include <hip/hip_runtime.h>
 #  define CY_FN __device__ __forceinline__
+#  define CY_NOINLINE __device__ __noinline__ /* a real call: large, rarely used code */
 #  define CY_MFN __device__ __forceinline__
 #  define CY_CONST __constant__
 #else
 #  include <math.h>
 #  include <string.h>
 #  define CY_FN static inline
+#  define CY_NOINLINE static
 #  define CY_MFN inline
 #  define CY_CONST static const
 #endif

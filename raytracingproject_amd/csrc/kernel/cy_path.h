@@ -1314,6 +1314,7 @@ CY_FN void svm_store3(CySvmStack stack, uint a, cfloat3 f, uint *err)
 }
 
 #include "cy_svm_nodes.h"
+#include "cy_svm_noise.h"
 
 /* svm_closure.h:21-56 */
 CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, float roughness, bool refract)
@@ -1858,7 +1859,7 @@ typedef struct CySvmTexIn {
   int bounce, diffuse_bounce, glossy_bounce, transparent_bounce, transmission_bounce;
 } CySvmTexIn;
 
-CY_FN int svm_eval_texture_node(const hc_KernelData *data,
+CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
                                       const hc_uint4 *svm_nodes,
                                       const hc_KernelObject *objects,
                                       const hc_TextureInfo *texture_info,
@@ -1965,6 +1966,27 @@ CY_FN int svm_eval_texture_node(const hc_KernelData *data,
         break;
       case NODE_TEX_ENVIRONMENT:
         svm_node_tex_environment(texture_info, stack, node, err);
+        break;
+      case NODE_TEX_NOISE:
+        svm_node_tex_noise(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_TEX_WAVE:
+        svm_node_tex_wave(kg, stack, node, &offset, err);
+        break;
+      case NODE_TEX_MAGIC:
+        svm_node_tex_magic(kg, stack, node, &offset, err);
+        break;
+      case NODE_TEX_BRICK:
+        svm_node_tex_brick(kg, stack, node, &offset, err);
+        break;
+      case NODE_TEX_WHITE_NOISE:
+        svm_node_tex_white_noise(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_TEX_MUSGRAVE:
+        svm_node_tex_musgrave(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_TEX_VORONOI:
+        svm_node_tex_voronoi(kg, stack, node.y, node.z, node.w, &offset, err);
         break;
       default:
         return -1;

@@ -31,6 +31,10 @@
  * so find_attribute never finds one and the principled volume's density and
  * colour come from its sockets alone.
  *
+ * shader_eval_volume, volume_shadow and volume_integrate are out-of-line
+ * calls (CY_NOINLINE): each runs the SVM interpreter, and a shading or shadow
+ * kernel reaches them from several places.
+ *
  * The volume stack of a path lives in HBM next to the other slot records
  * (CyPathBuffers.vol_stack, CY_VOLUME_STACK entries per slot); the device
  * refuses scenes whose volume objects could overflow it.
@@ -173,7 +177,7 @@ CY_FN void shader_merge_volume_closures(CySD *sd)
 
 /* shader_eval_volume: the closures of every volume on the stack, accumulated
  * into one array (merged after the second). */
-CY_FN void shader_eval_volume(
+CY_NOINLINE void shader_eval_volume(
     const CyGlobals *kg, CySD *sd, const CyPathState *state, const CyVolumeStack *stack, int path_flag, uint *err)
 {
   const int max_closures = (path_flag & (PATH_RAY_TERMINATE | PATH_RAY_SHADOW | PATH_RAY_EMISSION)) ?
@@ -295,7 +299,7 @@ CY_FN void volume_step_init(const CyGlobals *kg, const CyPathState *state, float
 }
 
 /* kernel_volume_shadow: attenuation of a segment with no surface inside it. */
-CY_FN void volume_shadow(const CyGlobals *kg, CySD *sd, const CyPathState *state, const CyVolumeStack *stack,
+CY_NOINLINE void volume_shadow(const CyGlobals *kg, CySD *sd, const CyPathState *state, const CyVolumeStack *stack,
                          const CyRay *ray, cfloat3 *throughput, CyShadeMem mem, uint *err)
 {
   shader_setup_from_volume(sd, ray, mem);
@@ -531,7 +535,7 @@ CY_FN int volume_integrate_heterogeneous(const CyGlobals *kg, CyPathState *state
 }
 
 /* kernel_volume_integrate: the ray segment through the volumes on the stack */
-CY_FN int volume_integrate(const CyGlobals *kg, CyPathState *state, CySD *sd, const CyVolumeStack *stack,
+CY_NOINLINE int volume_integrate(const CyGlobals *kg, CyPathState *state, CySD *sd, const CyVolumeStack *stack,
                            const CyRay *ray, cfloat3 *L, cfloat3 *throughput, float step_size, CyShadeMem mem,
                            uint *err)
 {

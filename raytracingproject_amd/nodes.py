@@ -40,6 +40,16 @@ NODE_LIGHT_PATH = 47
 NODE_MAPPING = 52
 NODE_TEX_GRADIENT = 57
 NODE_TEX_CHECKER = 62
+# procedural noise textures (svm_types.h:89-128)
+NODE_TEX_NOISE, NODE_TEX_MUSGRAVE, NODE_TEX_WAVE, NODE_TEX_MAGIC = 25, 59, 60, 61
+NODE_TEX_BRICK, NODE_TEX_WHITE_NOISE, NODE_TEX_VORONOI = 63, 64, 58
+VORONOI_FEATURES = {"f1": 0, "f2": 1, "smooth_f1": 2, "distance_to_edge": 3, "n_sphere_radius": 4}
+VORONOI_METRICS = {"euclidean": 0, "manhattan": 1, "chebychev": 2, "minkowski": 3}
+MUSGRAVE_TYPES = {"multifractal": 0, "fBm": 1, "hybrid_multifractal": 2, "ridged_multifractal": 3,
+                  "hetero_terrain": 4}
+WAVE_TYPES = {"bands": 0, "rings": 1}
+WAVE_DIRECTIONS = {"x": 0, "y": 1, "z": 2, "diagonal": 3, "spherical": 3}
+WAVE_PROFILES = {"sin": 0, "saw": 1, "tri": 2}
 NODE_LIGHT_FALLOFF = 66
 NODE_INVERT = 72
 NODE_MIX = 73
@@ -238,6 +248,76 @@ def environment_texture(image: Image, vector, projection: str = "equirectangular
                 params={"image": image, "projection": ENVIRONMENT_PROJECTIONS[projection]})
 
 
+def noise_texture(vector, w=0.0, scale=5.0, detail=2.0, roughness=0.5, distortion=0.0, dimensions=3) -> Node:
+    """Noise Texture (nodes.cpp NoiseTextureNode): fractal Perlin noise in 1-4
+    dimensions (1D uses W, 4D the vector and W); outputs Fac, Color.  The
+    vector must be linked (the reference's default is generated coordinates,
+    an attribute this host does not pack)."""
+    if dimensions not in (1, 2, 3, 4):
+        raise ValueError("noise dimensions: 1..4")
+    return Node("noise_texture", {"Vector": vector, "W": w, "Scale": scale, "Detail": detail,
+                                  "Roughness": roughness, "Distortion": distortion}, {"dimensions": dimensions})
+
+
+def musgrave_texture(vector, kind="fBm", w=0.0, scale=5.0, detail=2.0, dimension=2.0, lacunarity=2.0, offset=0.0,
+                     gain=1.0, dimensions=3) -> Node:
+    """Musgrave Texture (nodes.cpp MusgraveTextureNode): multifractal / fBm /
+    hybrid multifractal / ridged multifractal / hetero terrain, 1-4 D."""
+    if kind not in MUSGRAVE_TYPES or dimensions not in (1, 2, 3, 4):
+        raise ValueError(f"musgrave: type one of {sorted(MUSGRAVE_TYPES)}, dimensions 1..4")
+    return Node("musgrave_texture", {"Vector": vector, "W": w, "Scale": scale, "Detail": detail,
+                                     "Dimension": dimension, "Lacunarity": lacunarity, "Offset": offset, "Gain": gain},
+                {"type": kind, "dimensions": dimensions})
+
+
+def wave_texture(vector, kind="bands", direction="x", profile="sin", scale=5.0, distortion=0.0, detail=2.0,
+                 detail_scale=1.0, detail_roughness=0.5, phase=0.0) -> Node:
+    """Wave Texture (nodes.cpp WaveTextureNode): bands or rings, sine / saw /
+    triangle profile, optional noise distortion."""
+    if kind not in WAVE_TYPES or direction not in WAVE_DIRECTIONS or profile not in WAVE_PROFILES:
+        raise ValueError("wave: unknown type / direction / profile")
+    return Node("wave_texture", {"Vector": vector, "Scale": scale, "Distortion": distortion, "Detail": detail,
+                                 "Detail Scale": detail_scale, "Detail Roughness": detail_roughness,
+                                 "Phase Offset": phase}, {"type": kind, "direction": direction, "profile": profile})
+
+
+def magic_texture(vector, depth=2, scale=5.0, distortion=1.0) -> Node:
+    """Magic Texture (nodes.cpp MagicTextureNode)."""
+    return Node("magic_texture", {"Vector": vector, "Scale": scale, "Distortion": distortion}, {"depth": int(depth)})
+
+
+def brick_texture(vector, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), mortar=(0.0, 0.0, 0.0), scale=5.0,
+                  mortar_size=0.02, mortar_smooth=0.1, bias=0.0, brick_width=0.5, row_height=0.25, offset=0.5,
+                  offset_frequency=2, squash=1.0, squash_frequency=2) -> Node:
+    """Brick Texture (nodes.cpp BrickTextureNode)."""
+    return Node("brick_texture", {"Vector": vector, "Color1": color1, "Color2": color2, "Mortar": mortar,
+                                  "Scale": scale, "Mortar Size": mortar_size, "Mortar Smooth": mortar_smooth,
+                                  "Bias": bias, "Brick Width": brick_width, "Row Height": row_height},
+                {"offset": float(offset), "offset_frequency": int(offset_frequency), "squash": float(squash),
+                 "squash_frequency": int(squash_frequency)})
+
+
+def voronoi_texture(vector, feature="f1", metric="euclidean", w=0.0, scale=5.0, smoothness=1.0, exponent=0.5,
+                    randomness=1.0, dimensions=3) -> Node:
+    """Voronoi Texture (nodes.cpp VoronoiTextureNode): F1 / F2 / smooth F1 /
+    distance to edge / n-sphere radius in 1-4 D with euclidean, manhattan,
+    chebychev or minkowski distances; outputs Distance, Color, Position, W,
+    Radius."""
+    if feature not in VORONOI_FEATURES or metric not in VORONOI_METRICS or dimensions not in (1, 2, 3, 4):
+        raise ValueError("voronoi: unknown feature / metric / dimensions")
+    return Node("voronoi_texture", {"Vector": vector, "W": w, "Scale": scale, "Smoothness": smoothness,
+                                    "Exponent": exponent, "Randomness": randomness},
+                {"feature": feature, "metric": metric, "dimensions": dimensions})
+
+
+def white_noise_texture(vector, w=0.0, dimensions=3) -> Node:
+    """White Noise Texture (nodes.cpp WhiteNoiseTextureNode): hashes of the
+    coordinates; outputs Value, Color."""
+    if dimensions not in (1, 2, 3, 4):
+        raise ValueError("white noise dimensions: 1..4")
+    return Node("white_noise_texture", {"Vector": vector, "W": w}, {"dimensions": dimensions})
+
+
 def gradient(vector, kind: str = "linear") -> Node:
     if kind not in GRADIENT_TYPES:
         raise ValueError(f"unknown gradient type {kind!r}")
@@ -343,8 +423,14 @@ def _outputs(node: Node) -> dict:
         return {"Vector": "vector", "Value": "float"}
     if k in ("mix", "hsv", "gamma", "brightcontrast", "invert", "combine_hsv"):
         return {"Color": "color"}
-    if k in ("checker", "gradient"):
+    if k in ("checker", "gradient", "noise_texture", "wave_texture", "magic_texture", "brick_texture"):
         return {"Color": "color", "Fac": "float"}
+    if k == "musgrave_texture":
+        return {"Fac": "float"}
+    if k == "white_noise_texture":
+        return {"Value": "float", "Color": "color"}
+    if k == "voronoi_texture":
+        return {"Distance": "float", "Color": "color", "Position": "vector", "W": "float", "Radius": "float"}
     if k in ("mapping", "combine_xyz"):
         return {"Vector": "vector"}
     if k == "separate_xyz":
@@ -371,6 +457,19 @@ _INPUT_TYPES = {
     "invert": {"Fac": "float", "Color": "color"},
     "checker": {"Vector": "vector", "Color1": "color", "Color2": "color", "Scale": "float"},
     "gradient": {"Vector": "vector"},
+    "noise_texture": {"Vector": "vector", "W": "float", "Scale": "float", "Detail": "float", "Roughness": "float",
+                      "Distortion": "float"},
+    "musgrave_texture": {"Vector": "vector", "W": "float", "Scale": "float", "Detail": "float", "Dimension": "float",
+                         "Lacunarity": "float", "Offset": "float", "Gain": "float"},
+    "wave_texture": {"Vector": "vector", "Scale": "float", "Distortion": "float", "Detail": "float",
+                     "Detail Scale": "float", "Detail Roughness": "float", "Phase Offset": "float"},
+    "magic_texture": {"Vector": "vector", "Scale": "float", "Distortion": "float"},
+    "brick_texture": {"Vector": "vector", "Color1": "color", "Color2": "color", "Mortar": "color", "Scale": "float",
+                      "Mortar Size": "float", "Mortar Smooth": "float", "Bias": "float", "Brick Width": "float",
+                      "Row Height": "float"},
+    "white_noise_texture": {"Vector": "vector", "W": "float"},
+    "voronoi_texture": {"Vector": "vector", "W": "float", "Scale": "float", "Smoothness": "float",
+                        "Exponent": "float", "Randomness": "float"},
     "mapping": {"Vector": "vector", "Location": "vector", "Rotation": "vector", "Scale": "vector"},
     "separate_xyz": {"Vector": "vector"},
     "combine_xyz": {"X": "float", "Y": "float", "Z": "float"},
@@ -663,6 +762,96 @@ class NodeCompiler:
         flags = self._image_flags(n, image)
         self.emit((NODE_TEX_ENVIRONMENT, self.image_slot(image),
                    uchar4(vec, self.out(n, "Color"), self.out(n, "Alpha"), flags), n.params["projection"]))
+
+    # -- procedural noise textures (nodes.cpp *TextureNode::compile, identity
+    # texture mapping: tex_mapping.compile_begin = stack_assign(vector))
+    def _lin(self, n, name):
+        return self.assign_if_linked(n.inputs[name], _INPUT_TYPES[n.kind][name])
+
+    def _val(self, n, name):
+        v = n.inputs[name]
+        return f32bits(0.0 if is_linked(v) else float(v))
+
+    def _vector(self, n):
+        if not is_linked(n.inputs["Vector"]):
+            raise ValueError(f"{n.kind}: link the Vector input (generated coordinates are not packed)")
+        return self.inp(n, "Vector")
+
+    def _n_noise_texture(self, n):  # nodes.cpp:1061-1095
+        vec = self._vector(n)
+        offs = [self._lin(n, k) for k in ("W", "Scale", "Detail", "Roughness", "Distortion")]
+        self.emit((NODE_TEX_NOISE, n.params["dimensions"], uchar4(vec, offs[0], offs[1], offs[2]),
+                   uchar4(offs[3], offs[4], self.out(n, "Fac"), self.out(n, "Color"))))
+        self.emit(tuple(self._val(n, k) for k in ("W", "Scale", "Detail", "Roughness")))
+        self.emit((self._val(n, "Distortion"), SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID))
+
+    def _n_musgrave_texture(self, n):  # nodes.cpp:1393-1428 (Fac always stack-assigned)
+        vec = self._vector(n)
+        offs = [self._lin(n, k) for k in ("W", "Scale", "Detail", "Dimension", "Lacunarity", "Offset", "Gain")]
+        fac = self.out(n, "Fac")
+        if fac == SVM_STACK_INVALID:
+            fac = self.alloc(1)
+            self.temps.append((fac, 1))
+        self.emit((NODE_TEX_MUSGRAVE, uchar4(MUSGRAVE_TYPES[n.params["type"]], n.params["dimensions"], vec, offs[0]),
+                   uchar4(offs[1], offs[2], offs[3], offs[4]), uchar4(offs[5], offs[6], fac)))
+        self.emit(tuple(self._val(n, k) for k in ("W", "Scale", "Detail", "Dimension")))
+        self.emit((self._val(n, "Lacunarity"), self._val(n, "Offset"), self._val(n, "Gain"), 0))
+
+    def _n_wave_texture(self, n):  # nodes.cpp:1492-1528
+        vec = self._vector(n)
+        d = WAVE_DIRECTIONS[n.params["direction"]]
+        self.emit((NODE_TEX_WAVE, uchar4(WAVE_TYPES[n.params["type"]], d, d, WAVE_PROFILES[n.params["profile"]]),
+                   uchar4(vec, self._lin(n, "Scale"), self._lin(n, "Distortion")),
+                   uchar4(self._lin(n, "Detail"), self._lin(n, "Detail Scale"), self._lin(n, "Detail Roughness"),
+                          self._lin(n, "Phase Offset"))))
+        self.emit((uchar4(self.out(n, "Color"), self.out(n, "Fac")), self._val(n, "Scale"),
+                   self._val(n, "Distortion"), self._val(n, "Detail")))
+        self.emit((self._val(n, "Detail Scale"), self._val(n, "Detail Roughness"), self._val(n, "Phase Offset"),
+                   SVM_STACK_INVALID))
+
+    def _n_magic_texture(self, n):  # nodes.cpp:1567-1587
+        vec = self._vector(n)
+        self.emit((NODE_TEX_MAGIC, uchar4(n.params["depth"], self.out(n, "Color"), self.out(n, "Fac")),
+                   uchar4(vec, self._lin(n, "Scale"), self._lin(n, "Distortion")), 0))
+        self.emit((self._val(n, "Scale"), self._val(n, "Distortion"), 0, 0))
+
+    def _n_brick_texture(self, n):  # nodes.cpp:1688-1734
+        vec = self._vector(n)
+        c1, c2, mortar = self.inp(n, "Color1"), self.inp(n, "Color2"), self.inp(n, "Mortar")
+        p = n.params
+        self.emit((NODE_TEX_BRICK, uchar4(vec, c1, c2, mortar),
+                   uchar4(self._lin(n, "Scale"), self._lin(n, "Mortar Size"), self._lin(n, "Bias"),
+                          self._lin(n, "Brick Width")),
+                   uchar4(self._lin(n, "Row Height"), self.out(n, "Color"), self.out(n, "Fac"),
+                          self._lin(n, "Mortar Smooth"))))
+        self.emit((uchar4(p["offset_frequency"], p["squash_frequency"]), self._val(n, "Scale"),
+                   self._val(n, "Mortar Size"), self._val(n, "Bias")))
+        self.emit((self._val(n, "Brick Width"), self._val(n, "Row Height"), f32bits(p["offset"]),
+                   f32bits(p["squash"])))
+        self.emit((self._val(n, "Mortar Smooth"), SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID))
+
+    def _n_voronoi_texture(self, n):  # nodes.cpp:1155-1199
+        vec = self._vector(n)
+        offs = [self._lin(n, k) for k in ("W", "Scale", "Smoothness", "Exponent", "Randomness")]
+        p = n.params
+        self.emit((NODE_TEX_VORONOI, p["dimensions"], VORONOI_FEATURES[p["feature"]], VORONOI_METRICS[p["metric"]]))
+        self.emit((uchar4(vec, offs[0], offs[1], offs[2]),
+                   uchar4(offs[3], offs[4], self.out(n, "Distance"), self.out(n, "Color")),
+                   uchar4(self.out(n, "Position"), self.out(n, "W"), self.out(n, "Radius")), self._val(n, "W")))
+        self.emit(tuple(self._val(n, k) for k in ("Scale", "Smoothness", "Exponent", "Randomness")))
+
+    def _n_white_noise_texture(self, n):  # nodes.cpp:1327-1343 (every socket stack-assigned)
+        vec = self._vector(n)
+        w = self.inp(n, "W")
+        outs = []
+        for name in ("Value", "Color"):
+            off = self.out(n, name)
+            if off == SVM_STACK_INVALID:
+                width = 1 if name == "Value" else 3
+                off = self.alloc(width)
+                self.temps.append((off, width))
+            outs.append(off)
+        self.emit((NODE_TEX_WHITE_NOISE, n.params["dimensions"], uchar4(vec, w), uchar4(outs[0], outs[1])))
 
     def _n_gradient(self, n):  # nodes.cpp GradientTextureNode::compile
         vec = self.inp(n, "Vector")

@@ -909,6 +909,78 @@ def shading_color(width=64, height=64, samples=8) -> sc.Scene:
     return _grid_scene(colors, width, height, samples, "shading_color", glossy_every=6)
 
 
+def shading_noise(width=64, height=64, samples=8) -> sc.Scene:
+    """The procedural noise textures (svm_noise.h and its users): Noise in
+    1-4 D with and without distortion, every Musgrave type in 3 D plus 1/2/4 D
+    fBm, Wave bands / rings with each profile and direction, Magic at three
+    depths, Brick with offset / squash, White Noise in 1-4 D."""
+    from . import nodes as nd
+
+    tc = nd.tex_coord()
+    P = nd.mapping(tc["Object"], scale=(1.7, 1.7, 1.7), location=(0.3, -0.2, 0.1))
+    W = nd.separate_xyz(tc["Object"])["Y"]
+    colors = []
+    for dims in (1, 2, 3, 4):
+        colors.append(nd.noise_texture(P, w=W, scale=2.5, detail=3.5, roughness=0.6, dimensions=dims)["Color"])
+    colors.append(nd.noise_texture(P, w=W, scale=4.0, detail=1.0, distortion=2.5, dimensions=3)["Color"])
+    colors.append(nd.noise_texture(P, w=W, scale=3.0, detail=0.0, distortion=1.0, dimensions=2)["Color"])
+    colors.append(nd.noise_texture(P, w=W, scale=1.5, detail=6.7, roughness=0.45, distortion=0.7,
+                                   dimensions=4)["Color"])
+    for kind in nd.MUSGRAVE_TYPES:
+        fac = nd.musgrave_texture(P, kind, scale=2.0, detail=4.3, dimension=1.2, lacunarity=2.1, offset=0.8,
+                                  gain=1.3)["Fac"]
+        colors.append(nd.mix_rgb("mix", nd.math("multiply", fac, 0.4), (0.1, 0.1, 0.3), (1.0, 0.8, 0.2),
+                                 clamp=True))
+    for dims in (1, 2, 4):
+        fac = nd.musgrave_texture(P, "fBm", w=W, scale=3.0, detail=2.5, dimensions=dims)["Fac"]
+        colors.append(nd.mix_rgb("mix", nd.math("add", nd.math("multiply", fac, 0.5), 0.5), (0.0, 0.2, 0.1),
+                                 (0.9, 0.9, 0.6), clamp=True))
+    for kind, direction, profile in (("bands", "x", "sin"), ("bands", "diagonal", "saw"), ("rings", "spherical",
+                                     "tri"), ("rings", "z", "sin"), ("bands", "y", "tri")):
+        colors.append(nd.wave_texture(P, kind, direction, profile, scale=1.5, distortion=3.0 if profile == "sin"
+                                      else 0.0, detail=2.0, detail_scale=1.5, phase=0.7)["Color"])
+    for depth in (0, 2, 7):
+        colors.append(nd.magic_texture(P, depth=depth, scale=1.2, distortion=1.4 if depth else 0.0)["Color"])
+    colors.append(nd.brick_texture(P, (0.7, 0.2, 0.1), (0.5, 0.4, 0.3), (0.9, 0.9, 0.85), scale=2.0,
+                                   mortar_size=0.03, mortar_smooth=0.4, bias=0.1, brick_width=0.45, row_height=0.2,
+                                   offset=0.4, squash=0.8)["Color"])
+    for dims in (1, 2, 3, 4):
+        colors.append(nd.white_noise_texture(nd.mapping(tc["Object"], scale=(9.0, 9.0, 9.0)), w=W,
+                                             dimensions=dims)["Color"])
+    return _grid_scene(colors, width, height, samples, "shading_noise")
+
+
+def shading_voronoi(width=64, height=64, samples=8) -> sc.Scene:
+    """Voronoi Texture (svm_voronoi.h): every feature in 1-4 D with the four
+    distance metrics, its Distance / Color / Position / W / Radius outputs."""
+    from . import nodes as nd
+
+    tc = nd.tex_coord()
+    P = nd.mapping(tc["Object"], scale=(1.3, 1.3, 1.3), location=(0.2, 0.1, -0.3))
+    W = nd.math("multiply", nd.separate_xyz(tc["Object"])["X"], 0.7)
+    colors = []
+
+    def shade(v, lo=(0.05, 0.1, 0.3), hi=(1.0, 0.9, 0.6)):
+        return nd.mix_rgb("mix", v, lo, hi, clamp=True)
+
+    metrics = ("euclidean", "manhattan", "chebychev", "minkowski")
+    for dims in (1, 2, 3, 4):
+        for feature in ("f1", "f2", "smooth_f1"):
+            m = metrics[(dims + len(feature)) % 4]
+            v = nd.voronoi_texture(P, feature, m, w=W, scale=3.0, smoothness=0.6, exponent=0.7, randomness=0.9,
+                                   dimensions=dims)
+            colors.append(nd.mix_rgb("mix", 0.5, v["Color"], shade(v["Distance"]), clamp=True))
+            if feature == "f1":
+                pos = v["W"] if dims == 1 else v["Position"]
+                colors.append(nd.vector_math("fraction", pos)["Vector"] if dims > 1 else shade(
+                    nd.math("fraction", pos)))
+        e = nd.voronoi_texture(P, "distance_to_edge", w=W, scale=2.5, randomness=0.8, dimensions=dims)
+        colors.append(shade(nd.math("multiply", e["Distance"], 4.0)))
+        r = nd.voronoi_texture(P, "n_sphere_radius", w=W, scale=2.5, randomness=1.0, dimensions=dims)
+        colors.append(shade(nd.math("multiply", r["Radius"], 2.0), (0.3, 0.05, 0.05), (0.9, 1.0, 0.8)))
+    return _grid_scene(colors, width, height, samples, "shading_voronoi")
+
+
 def shading_coords(width=64, height=64, samples=8) -> sc.Scene:
     """Texture coordinate and geometry outputs, checker and gradient
     textures, light path and light falloff outputs."""
