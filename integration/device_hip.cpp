@@ -64,12 +64,14 @@ class HIPCyclesDevice : public Device {
   }
 
   /* device.h:375 — features the kernels do not implement are refused here, and
-   * once more against the uploaded KernelData before the first render */
+   * once more against the uploaded KernelData before the first render (hair
+   * curves, random-walk subsurface scattering and volumes are implemented;
+   * hipcy_load_kernels checks their variants: curve shapes, BSSRDF falloffs,
+   * volume_decoupled, camera in volume) */
   bool load_kernels(const DeviceRequestedFeatures &f) override
   {
-    if (f.use_hair || f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_subsurface ||
-        f.use_volume || f.use_integrator_branched || f.use_patch_evaluation || f.use_shader_raytrace ||
-        f.use_denoising) {
+    if (f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_integrator_branched ||
+        f.use_patch_evaluation || f.use_shader_raytrace || f.use_denoising) {
       set_error("HIP device: requested features are not implemented (" + f.get_build_options() + ")");
       return false;
     }
