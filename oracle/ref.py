@@ -123,6 +123,12 @@ class RefKernel:
             self._keep.append(a)
             nelem = a.nbytes // ELEMENT_BYTES[name]
             self.lib.cref_global_copy(self.h, name.encode(), a.ctypes.data, nelem)
+        if dscene.textures:
+            # ImageManager::device_update: TextureInfo records whose data are
+            # host addresses of the texel arrays (kept alive with the kernel)
+            info, texels = dscene.texture_info()
+            self._keep += [info, *texels]
+            self.lib.cref_global_copy(self.h, b"__texture_info", info.ctypes.data, len(dscene.textures))
 
     def set_global(self, name: str, arr: np.ndarray):
         """Re-bind one global array (e.g. the background CDFs built after the map)."""

@@ -1765,10 +1765,12 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
  * nodes are used, which selects the shading-kernel variant. */
 static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
                             const std::vector<void *> &tex_mem, const std::vector<uint32_t> &shader_flags,
-                            bool *uses_tex, bool *uses_bssrdf, int *surface_closures, int *volume_closures)
+                            bool *uses_tex, bool *uses_bssrdf, bool *uses_attr, int *surface_closures,
+                            int *volume_closures)
 {
   *uses_tex = false;
   *uses_bssrdf = false;
+  *uses_attr = false;
   /* closures one program can allocate, counted as ShaderGraph::get_num_closures
    * (render/graph.cpp:1130-1161) counts them, except that a phase closure
    * allocates one per evaluation (the reference reserves VOLUME_STACK_SIZE) */
@@ -1981,6 +1983,11 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           len = 4;
           tex = true;
           break;
+        case NODE_ATTR:
+        case NODE_VERTEX_COLOR:
+          *uses_attr = true;
+          tex = true;
+          break;
         case NODE_TEX_WHITE_NOISE:
         case NODE_GEOMETRY:
         case NODE_CONVERT:
@@ -2112,10 +2119,15 @@ int hipcy_load_kernels(hipcy_device *dev)
       shader_flags[i] = (uint32_t)ks[i].flags;
     }
   }
-  bool uses_bssrdf = false;
+  bool uses_bssrdf = false, uses_attr = false;
   int surface_closures = 0, volume_closures = 0;
   why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, shader_flags, &dev->shade_tex, &uses_bssrdf,
-                 &surface_closures, &volume_closures);
+                 &uses_attr, &surface_closures, &volume_closures);
+  if (why.empty() && uses_attr && dev->globals.find("__attributes_map") == dev->globals.end()) {
+    /* the attribute nodes look attributes up through the objects' maps
+     * (GeometryManager::device_update_attributes, geometry.cpp:379-474) */
+    why = "attribute / texture coordinate (UV, Generated) / vertex color nodes without __attributes_map";
+  }
   if (!why.empty()) {
     return set_error(dev, "load_kernels: unsupported shader: " + why);
   }

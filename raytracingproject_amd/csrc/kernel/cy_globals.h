@@ -40,7 +40,12 @@
   X(hc_TextureInfo, __texture_info) \
   X(hc_float4, __curves) \
   X(hc_float4, __curve_keys) \
-  X(float, __object_volume_step)
+  X(float, __object_volume_step) \
+  X(hc_uint4, __attributes_map) \
+  X(float, __attributes_float) \
+  X(hc_float2, __attributes_float2) \
+  X(hc_float4, __attributes_float3) \
+  X(uint32_t, __attributes_uchar4)
 
 typedef struct CyGlobals {
   const hc_KernelData *data;

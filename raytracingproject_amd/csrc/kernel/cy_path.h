@@ -1315,6 +1315,7 @@ CY_FN void svm_store3(CySvmStack stack, uint a, cfloat3 f, uint *err)
 
 #include "cy_svm_nodes.h"
 #include "cy_svm_noise.h"
+#include "cy_attribute.h"
 
 /* svm_closure.h:21-56 */
 CY_FN void svm_node_glass_setup(CySD *sd, CyClosure *b, int type, float eta, float roughness, bool refract)
@@ -2272,6 +2273,12 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         return;
 #else
       {
+        if (node.x == NODE_ATTR || node.x == NODE_VERTEX_COLOR) {
+          svm_eval_attribute_node(kg->__objects, kg->__attributes_map, kg->__attributes_float,
+                                  kg->__attributes_float2, kg->__attributes_float3, kg->__attributes_uchar4,
+                                  kg->__tri_vindex, sd->object, sd->prim, sd->type, sd->u, sd->v, stack, node, err);
+          break;
+        }
         CySvmTexIn in;
         in.P = sd->P;
         in.N = sd->N;

@@ -59,6 +59,13 @@ NODE_SEPARATE_HSV = 76
 NODE_COMBINE_HSV = 77
 NODE_MAP_RANGE = 83
 NODE_CLAMP = 84
+NODE_ATTR, NODE_VERTEX_COLOR = 16, 17
+# NodeAttributeType (svm_types.h:160-166)
+NODE_ATTR_FLOAT, NODE_ATTR_FLOAT2, NODE_ATTR_FLOAT3, NODE_ATTR_RGBA = 0, 1, 2, 3
+# AttributeStandard (kernel_types.h:750-779) of the attributes this host packs;
+# Attribute::standard_name (render/attribute.cpp:279-330) for the name lookup
+ATTR_STD_UV, ATTR_STD_VERTEX_COLOR, ATTR_STD_GENERATED, ATTR_STD_NUM = 3, 6, 7, 26
+ATTR_STD_NAMES = {"uv": ATTR_STD_UV, "vertex_color": ATTR_STD_VERTEX_COLOR, "generated": ATTR_STD_GENERATED}
 
 # svm_types.h enums (the names are the Blender UI's, lower-cased)
 MATH_OPS = ["add", "subtract", "multiply", "divide", "sine", "cosine", "tangent", "arcsine", "arccosine",
@@ -138,7 +145,31 @@ def rgb(c) -> Socket:
 
 
 def tex_coord() -> Node:
+    """Texture Coordinate node (nodes.cpp:3818-3923): Generated and UV read the
+    mesh attributes (render/attribute.cpp: generated = vertex float3, uv =
+    corner float2), the others NODE_TEX_COORD."""
     return Node("tex_coord")
+
+
+def attribute(name: str) -> Node:
+    """Attribute node (nodes.cpp:5394-5436): the named (or standard: "uv",
+    "generated", "vertex_color") geometry attribute as Color / Vector / Fac."""
+    return Node("attribute", params={"name": str(name)})
+
+
+def vertex_color(layer: str = "") -> Node:
+    """Vertex Color node (nodes.cpp:4532-4568): a byte-colour corner attribute
+    (the active layer when `layer` is empty) as Color and Alpha."""
+    return Node("vertex_color", params={"layer": str(layer)})
+
+
+def _default_vector(vector, kind: str = "generated"):
+    """ShaderGraph::default_inputs (render/graph.cpp:830-880): an unlinked
+    texture vector reads the generated coordinates (LINK_TEXTURE_GENERATED) or
+    the UV map (LINK_TEXTURE_UV)."""
+    if vector is not None:
+        return vector
+    return tex_coord()["UV" if kind == "uv" else "Generated"]
 
 
 def geometry() -> Node:
@@ -187,8 +218,8 @@ def invert(color, fac=1.0) -> Socket:
     return Node("invert", {"Fac": fac, "Color": color})["Color"]
 
 
-def checker(vector, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), scale=5.0) -> Node:
-    return Node("checker", {"Vector": vector, "Color1": color1, "Color2": color2, "Scale": scale})
+def checker(vector=None, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), scale=5.0) -> Node:
+    return Node("checker", {"Vector": _default_vector(vector), "Color1": color1, "Color2": color2, "Scale": scale})
 
 
 IMAGE_DATA_TYPES = ("float4", "byte4", "half4", "float", "byte", "half", "ushort4", "ushort")
@@ -227,15 +258,12 @@ class Image:
         return a
 
 
-def image_texture(image: Image, vector, projection: str = "flat", alpha_unassociate: bool = False) -> Node:
+def image_texture(image: Image, vector=None, projection: str = "flat", alpha_unassociate: bool = False) -> Node:
     """Image Texture node (nodes.cpp ImageTextureNode, svm_image.h:43-112).
-    The vector input must be linked (the reference's default is the UV map
-    attribute, which this host does not emit); box projection is not
-    implemented.  alpha_unassociate sets NODE_IMAGE_ALPHA_UNASSOCIATE (the
+    An unlinked vector reads the UV map (LINK_TEXTURE_UV); box projection is
+    not implemented.  alpha_unassociate sets NODE_IMAGE_ALPHA_UNASSOCIATE (the
     reference sets it when the Alpha output is used on a non-data image)."""
-    if not is_linked(vector):
-        raise ValueError("image_texture: link the vector input (UV attributes are not emitted)")
-    return Node("image_texture", {"Vector": vector},
+    return Node("image_texture", {"Vector": _default_vector(vector, "uv")},
                 params={"image": image, "projection": IMAGE_PROJECTIONS[projection],
                         "alpha_unassociate": alpha_unassociate})
 
@@ -248,56 +276,55 @@ def environment_texture(image: Image, vector, projection: str = "equirectangular
                 params={"image": image, "projection": ENVIRONMENT_PROJECTIONS[projection]})
 
 
-def noise_texture(vector, w=0.0, scale=5.0, detail=2.0, roughness=0.5, distortion=0.0, dimensions=3) -> Node:
+def noise_texture(vector=None, w=0.0, scale=5.0, detail=2.0, roughness=0.5, distortion=0.0, dimensions=3) -> Node:
     """Noise Texture (nodes.cpp NoiseTextureNode): fractal Perlin noise in 1-4
-    dimensions (1D uses W, 4D the vector and W); outputs Fac, Color.  The
-    vector must be linked (the reference's default is generated coordinates,
-    an attribute this host does not pack)."""
+    dimensions (1D uses W, 4D the vector and W); outputs Fac, Color.  An
+    unlinked vector reads the generated coordinates."""
     if dimensions not in (1, 2, 3, 4):
         raise ValueError("noise dimensions: 1..4")
-    return Node("noise_texture", {"Vector": vector, "W": w, "Scale": scale, "Detail": detail,
+    return Node("noise_texture", {"Vector": _default_vector(vector), "W": w, "Scale": scale, "Detail": detail,
                                   "Roughness": roughness, "Distortion": distortion}, {"dimensions": dimensions})
 
 
-def musgrave_texture(vector, kind="fBm", w=0.0, scale=5.0, detail=2.0, dimension=2.0, lacunarity=2.0, offset=0.0,
+def musgrave_texture(vector=None, kind="fBm", w=0.0, scale=5.0, detail=2.0, dimension=2.0, lacunarity=2.0, offset=0.0,
                      gain=1.0, dimensions=3) -> Node:
     """Musgrave Texture (nodes.cpp MusgraveTextureNode): multifractal / fBm /
     hybrid multifractal / ridged multifractal / hetero terrain, 1-4 D."""
     if kind not in MUSGRAVE_TYPES or dimensions not in (1, 2, 3, 4):
         raise ValueError(f"musgrave: type one of {sorted(MUSGRAVE_TYPES)}, dimensions 1..4")
-    return Node("musgrave_texture", {"Vector": vector, "W": w, "Scale": scale, "Detail": detail,
+    return Node("musgrave_texture", {"Vector": _default_vector(vector), "W": w, "Scale": scale, "Detail": detail,
                                      "Dimension": dimension, "Lacunarity": lacunarity, "Offset": offset, "Gain": gain},
                 {"type": kind, "dimensions": dimensions})
 
 
-def wave_texture(vector, kind="bands", direction="x", profile="sin", scale=5.0, distortion=0.0, detail=2.0,
+def wave_texture(vector=None, kind="bands", direction="x", profile="sin", scale=5.0, distortion=0.0, detail=2.0,
                  detail_scale=1.0, detail_roughness=0.5, phase=0.0) -> Node:
     """Wave Texture (nodes.cpp WaveTextureNode): bands or rings, sine / saw /
     triangle profile, optional noise distortion."""
     if kind not in WAVE_TYPES or direction not in WAVE_DIRECTIONS or profile not in WAVE_PROFILES:
         raise ValueError("wave: unknown type / direction / profile")
-    return Node("wave_texture", {"Vector": vector, "Scale": scale, "Distortion": distortion, "Detail": detail,
+    return Node("wave_texture", {"Vector": _default_vector(vector), "Scale": scale, "Distortion": distortion, "Detail": detail,
                                  "Detail Scale": detail_scale, "Detail Roughness": detail_roughness,
                                  "Phase Offset": phase}, {"type": kind, "direction": direction, "profile": profile})
 
 
-def magic_texture(vector, depth=2, scale=5.0, distortion=1.0) -> Node:
+def magic_texture(vector=None, depth=2, scale=5.0, distortion=1.0) -> Node:
     """Magic Texture (nodes.cpp MagicTextureNode)."""
-    return Node("magic_texture", {"Vector": vector, "Scale": scale, "Distortion": distortion}, {"depth": int(depth)})
+    return Node("magic_texture", {"Vector": _default_vector(vector), "Scale": scale, "Distortion": distortion}, {"depth": int(depth)})
 
 
-def brick_texture(vector, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), mortar=(0.0, 0.0, 0.0), scale=5.0,
+def brick_texture(vector=None, color1=(0.8, 0.8, 0.8), color2=(0.2, 0.2, 0.2), mortar=(0.0, 0.0, 0.0), scale=5.0,
                   mortar_size=0.02, mortar_smooth=0.1, bias=0.0, brick_width=0.5, row_height=0.25, offset=0.5,
                   offset_frequency=2, squash=1.0, squash_frequency=2) -> Node:
     """Brick Texture (nodes.cpp BrickTextureNode)."""
-    return Node("brick_texture", {"Vector": vector, "Color1": color1, "Color2": color2, "Mortar": mortar,
+    return Node("brick_texture", {"Vector": _default_vector(vector), "Color1": color1, "Color2": color2, "Mortar": mortar,
                                   "Scale": scale, "Mortar Size": mortar_size, "Mortar Smooth": mortar_smooth,
                                   "Bias": bias, "Brick Width": brick_width, "Row Height": row_height},
                 {"offset": float(offset), "offset_frequency": int(offset_frequency), "squash": float(squash),
                  "squash_frequency": int(squash_frequency)})
 
 
-def voronoi_texture(vector, feature="f1", metric="euclidean", w=0.0, scale=5.0, smoothness=1.0, exponent=0.5,
+def voronoi_texture(vector=None, feature="f1", metric="euclidean", w=0.0, scale=5.0, smoothness=1.0, exponent=0.5,
                     randomness=1.0, dimensions=3) -> Node:
     """Voronoi Texture (nodes.cpp VoronoiTextureNode): F1 / F2 / smooth F1 /
     distance to edge / n-sphere radius in 1-4 D with euclidean, manhattan,
@@ -305,23 +332,23 @@ def voronoi_texture(vector, feature="f1", metric="euclidean", w=0.0, scale=5.0, 
     Radius."""
     if feature not in VORONOI_FEATURES or metric not in VORONOI_METRICS or dimensions not in (1, 2, 3, 4):
         raise ValueError("voronoi: unknown feature / metric / dimensions")
-    return Node("voronoi_texture", {"Vector": vector, "W": w, "Scale": scale, "Smoothness": smoothness,
+    return Node("voronoi_texture", {"Vector": _default_vector(vector), "W": w, "Scale": scale, "Smoothness": smoothness,
                                     "Exponent": exponent, "Randomness": randomness},
                 {"feature": feature, "metric": metric, "dimensions": dimensions})
 
 
-def white_noise_texture(vector, w=0.0, dimensions=3) -> Node:
+def white_noise_texture(vector=None, w=0.0, dimensions=3) -> Node:
     """White Noise Texture (nodes.cpp WhiteNoiseTextureNode): hashes of the
     coordinates; outputs Value, Color."""
     if dimensions not in (1, 2, 3, 4):
         raise ValueError("white noise dimensions: 1..4")
-    return Node("white_noise_texture", {"Vector": vector, "W": w}, {"dimensions": dimensions})
+    return Node("white_noise_texture", {"Vector": _default_vector(vector), "W": w}, {"dimensions": dimensions})
 
 
-def gradient(vector, kind: str = "linear") -> Node:
+def gradient(vector=None, kind: str = "linear") -> Node:
     if kind not in GRADIENT_TYPES:
         raise ValueError(f"unknown gradient type {kind!r}")
-    return Node("gradient", {"Vector": vector}, {"type": kind})
+    return Node("gradient", {"Vector": _default_vector(vector)}, {"type": kind})
 
 
 def mapping(vector, location=(0.0, 0.0, 0.0), rotation=(0.0, 0.0, 0.0), scale=(1.0, 1.0, 1.0),
@@ -410,7 +437,11 @@ def _outputs(node: Node) -> dict:
     if k == "rgb":
         return {"Color": "color"}
     if k == "tex_coord":
-        return {n: "vector" for n in TEXCO_OUTPUTS}
+        return {n: "vector" for n in ("Generated", *TEXCO_OUTPUTS, "UV")}
+    if k == "attribute":
+        return {"Color": "color", "Vector": "vector", "Fac": "float"}
+    if k == "vertex_color":
+        return {"Color": "color", "Alpha": "float"}
     if k == "geometry":
         return {n: "vector" for n in GEOMETRY_OUTPUTS}
     if k == "light_path":
@@ -492,7 +523,8 @@ def _width(t: str) -> int:
 
 # ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
 # the shading point or direction (texture coordinate, geometry, textures)
-SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture")
+SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture",
+                 "attribute", "vertex_color")
 
 
 def has_spatial_varying(values) -> bool:
@@ -533,8 +565,15 @@ class NodeCompiler:
     conversions materialised for one node's inputs right after that node;
     outputs feeding the closures (`roots`) stay live."""
 
-    def __init__(self, alloc, emit, roots=(), free=None, images=None):
+    def __init__(self, alloc, emit, roots=(), free=None, images=None, attribute=None, background=False,
+                 volume=False):
         self.images = images if images is not None else []  # SVM image slots (shared per scene)
+        # SVMCompiler::attribute (svm.cpp): attribute id of a standard id or a
+        # name, recording the shader's attribute request
+        self.attribute = attribute or (lambda key: (_ for _ in ()).throw(
+            ValueError("attribute nodes need the scene's SVM compiler")))
+        self.background = background  # compiler.background: the world shader
+        self.volume = volume  # compiler.output_type() == SHADER_TYPE_VOLUME
         self.alloc = alloc
         self.free = free or (lambda off, n: None)
         self.emit = emit
@@ -646,10 +685,50 @@ class NodeCompiler:
         self.emit((NODE_VALUE_V, off, 0, 0))
         self.emit((NODE_VALUE_V, *(f32bits(x) for x in n.params["value"])))
 
-    def _n_tex_coord(self, n):  # nodes.cpp TextureCoordinateNode::compile
-        for name, t in TEXCO_OUTPUTS.items():
+    def _n_tex_coord(self, n):  # nodes.cpp:3840-3923 TextureCoordinateNode::compile
+        used = lambda name: (id(n), name) in self.used  # noqa: E731
+        if used("Generated"):
+            if self.background:
+                self.emit((NODE_GEOMETRY, GEOMETRY_OUTPUTS["Position"], self.out(n, "Generated"), 0))
+            elif self.volume:
+                raise ValueError("tex_coord Generated in a volume shader (NODE_TEXCO_VOLUME_GENERATED needs the "
+                                 "generated-transform attribute) is not supported")
+            else:
+                self.emit((NODE_ATTR, self.attribute(ATTR_STD_GENERATED), self.out(n, "Generated"), NODE_ATTR_FLOAT3))
+        if used("Normal"):
+            self.emit((NODE_TEX_COORD, TEXCO_OUTPUTS["Normal"], self.out(n, "Normal"), 0))
+        if used("UV"):
+            self.emit((NODE_ATTR, self.attribute(ATTR_STD_UV), self.out(n, "UV"), NODE_ATTR_FLOAT3))
+        for name in ("Object", "Camera", "Window"):
+            if used(name):
+                self.emit((NODE_TEX_COORD, TEXCO_OUTPUTS[name], self.out(n, name), 0))
+        if used("Reflection"):
+            if self.background:
+                self.emit((NODE_GEOMETRY, GEOMETRY_OUTPUTS["Incoming"], self.out(n, "Reflection"), 0))
+            else:
+                self.emit((NODE_TEX_COORD, TEXCO_OUTPUTS["Reflection"], self.out(n, "Reflection"), 0))
+
+    def _n_attribute(self, n):  # nodes.cpp:5411-5436 AttributeNode::compile
+        attr = self.attribute(ATTR_STD_NAMES.get(n.params["name"], n.params["name"]))
+        for name in ("Color", "Vector"):
             if (id(n), name) in self.used:
-                self.emit((NODE_TEX_COORD, t, self.out(n, name), 0))
+                self.emit((NODE_ATTR, attr, self.out(n, name), NODE_ATTR_FLOAT3))
+        if (id(n), "Fac") in self.used:
+            self.emit((NODE_ATTR, attr, self.out(n, "Fac"), NODE_ATTR_FLOAT))
+
+    def _n_vertex_color(self, n):  # nodes.cpp:4543-4568 VertexColorNode::compile
+        layer = n.params["layer"]
+        attr = self.attribute(ATTR_STD_NAMES.get(layer, layer) if layer else ATTR_STD_VERTEX_COLOR)
+        # both outputs are stack-assigned (stack_assign): an unread one gets a
+        # slot released after the node
+        offs = []
+        for name, w in (("Color", 3), ("Alpha", 1)):
+            off = self.out(n, name)
+            if off == SVM_STACK_INVALID:
+                off = self.alloc(w)
+                self.temps.append((off, w))
+            offs.append(off)
+        self.emit((NODE_VERTEX_COLOR, attr, offs[0], offs[1]))
 
     def _n_geometry(self, n):  # nodes.cpp GeometryNode::compile
         for name, t in GEOMETRY_OUTPUTS.items():
@@ -773,8 +852,6 @@ class NodeCompiler:
         return f32bits(0.0 if is_linked(v) else float(v))
 
     def _vector(self, n):
-        if not is_linked(n.inputs["Vector"]):
-            raise ValueError(f"{n.kind}: link the Vector input (generated coordinates are not packed)")
         return self.inp(n, "Vector")
 
     def _n_noise_texture(self, n):  # nodes.cpp:1061-1095

@@ -394,6 +394,31 @@ class SVMCompiler:
         self.stack_top = 0
         self.stack_used = [False] * SVM_STACK_SIZE
         self.nc: nodes.NodeCompiler | None = None
+        # ShaderManager::get_attribute_id (shader.cpp:442-460): standard
+        # attributes by their id, names from ATTR_STD_NUM in first-use order
+        self.attribute_ids: dict[str, int] = {}
+        # per shader: the attribute requests of its nodes (ShaderNode::attributes),
+        # as standard ids or names, in first-use order
+        self.requests: list[list] = []
+        self._shader = 0
+
+    def attribute(self, key) -> int:
+        """SVMCompiler::attribute: the kernel's id for a standard attribute
+        (int) or a name, recorded as a request of the shader being compiled."""
+        if isinstance(key, str):
+            if key not in self.attribute_ids:
+                self.attribute_ids[key] = nodes.ATTR_STD_NUM + len(self.attribute_ids)
+            aid = self.attribute_ids[key]
+        else:
+            aid = int(key)
+        reqs = self.requests[self._shader]
+        if key not in reqs:
+            reqs.append(key)
+        return aid
+
+    def _node_compiler(self, roots, background=False, volume=False):
+        return nodes.NodeCompiler(self.alloc, self.nodes.append, roots, self.free, images=self.images,
+                                  attribute=self.attribute, background=background, volume=volume)
 
     def alloc(self, n=1) -> int:
         """First fit over the free slots (svm.cpp stack_find_offset)."""
@@ -593,14 +618,15 @@ class SVMCompiler:
         shaders = list(surfaces) + [world]
         n = len(shaders)
         self.nodes = [(NODE_SHADER_JUMP, 0, 0, 0)] * n
+        self.requests = [[] for _ in shaders]
         for i, sh in enumerate(shaders):
+            self._shader = i
             self.stack_top = 0
             self.stack_used = [False] * SVM_STACK_SIZE
             start = len(self.nodes)
             self.nodes[i] = (NODE_SHADER_JUMP, start, 0, 0)
             socks = sh.sockets()
-            self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [v for v, _ in socks], self.free,
-                                         images=self.images)
+            self.nc = self._node_compiler([v for v, _ in socks], background=sh is world)
             for v, t in socks:
                 self.nc.link(v, t)
             self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
@@ -615,8 +641,7 @@ class SVMCompiler:
                 self.stack_top = 0
                 self.stack_used = [False] * SVM_STACK_SIZE
                 vsocks = vol.sockets()
-                self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [v for v, _ in vsocks], self.free,
-                                             images=self.images)
+                self.nc = self._node_compiler([v for v, _ in vsocks], background=sh is world, volume=True)
                 for v, t in vsocks:
                     self.nc.link(v, t)
                 self.nodes.extend(self.emit_closure(vol, SVM_STACK_INVALID))
@@ -629,8 +654,7 @@ class SVMCompiler:
                 self.nodes[i] = (NODE_SHADER_JUMP, start, vol_start, len(self.nodes))
                 self.stack_top = 0
                 self.stack_used = [False] * SVM_STACK_SIZE
-                self.nc = nodes.NodeCompiler(self.alloc, self.nodes.append, [disp], self.free,
-                                             images=self.images)
+                self.nc = self._node_compiler([disp], background=sh is world)
                 off = self.nc.link(disp, "vector")
                 self.nodes.append((NODE_SET_DISPLACEMENT, off, 0, 0))
                 self.nodes.append((NODE_END, 0, 0, 0))
@@ -649,6 +673,15 @@ class Mesh:
     shader: np.ndarray | int = 0  # per-triangle material index, or one index
     smooth: bool = False
     normals: np.ndarray | None = None  # (V, 3) vertex normals for smooth shading
+    # geometry attributes (render/attribute.h AttributeSet), read by the
+    # Attribute, Texture Coordinate (UV, Generated) and Vertex Color nodes:
+    uv: np.ndarray | None = None  # (T, 3, 2) per-corner UV map "UVMap" (ATTR_STD_UV)
+    # name -> (T, 3, 4) per-corner RGBA in [0, 1], stored as bytes
+    # (ATTR_ELEMENT_CORNER_BYTE); the first layer is the active one (ATTR_STD_VERTEX_COLOR)
+    vertex_colors: dict | None = None
+    # name -> (element, data): element "vertex" (V rows), "face" (T rows) or
+    # "corner" (3T rows), data (N,) float, (N, 2) float2 or (N, 3) float3
+    attributes: dict | None = None
 
 
 @dataclass
@@ -1125,6 +1158,12 @@ def compile_scene(scene: Scene) -> DeviceScene:
                 object_flag[i] |= SD_OBJECT_INTERSECTS_VOLUME
                 break
 
+    # --- geometry attributes (geometry.cpp:379-474 device_update_attributes
+    # + :508-620 update_attribute_element_offset)
+    attr_arrays = None
+    if any(svm_compiler.requests):
+        attr_arrays = _pack_attributes(g, objects, tri_shader_idx, svm_compiler, kobjects)
+
     # --- lights (render/light.cpp:277-480, mesh lights only)
     # light.cpp:330-400: per object using emissive triangles, in object order,
     # world-space area (transform_point for instanced geometry)
@@ -1374,6 +1413,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
         # geometry.cpp device_update_attributes: no attributes are packed, every
         # object's map is the ATTR_STD_NONE terminator (ATTR_PRIM_TYPES rows)
         arrays["__attributes_map"] = np.zeros((2, 4), dtype=np.uint32)
+    if attr_arrays is not None:
+        arrays.update(attr_arrays)
     if g["ncurves"]:
         # Hair::pack_curves (render/hair.cpp): keys with radius, per curve the
         # first key, key count and shader id (get_shader_id(shader, false))
@@ -1419,6 +1460,135 @@ def _volume_attribute_dependency(v) -> bool:
         return True
     return any(n.kind in ("tex_coord", "geometry", "image_texture", "environment_texture")
                for s, _ in v.sockets() for n in _nodes.upstream(s))
+
+
+_ATTR_TYPES = {"float": 0, "float2": 1, "float3": 2, "rgba": 3}  # NodeAttributeType
+_ATTR_ELEMENTS = {"object": 1, "mesh": 2, "face": 3, "vertex": 4, "corner": 6, "corner_byte": 7}
+
+
+def _generated_coordinates(m: Mesh) -> np.ndarray:
+    """ATTR_STD_GENERATED as Blender syncs it (blender/blender_mesh.cpp
+    create_mesh: undeformed co * size - loc, blender_util.h:470-483
+    mesh_texture_space) with the automatic texture space of the mesh's
+    untransformed vertices: location the bounds' centre, size their half
+    extents (a zero extent kept as 1)."""
+    f32 = np.float32
+    v = np.asarray(m.verts, dtype=f32).reshape(-1, 3)
+    lo, hi = v.min(axis=0), v.max(axis=0)
+    loc = ((lo + hi) * f32(0.5)).astype(f32)
+    size = ((hi - lo) * f32(0.5)).astype(f32)
+    size = np.where(size == 0, f32(1.0), size).astype(f32)
+    size = (f32(0.5) / size).astype(f32)
+    loc = (loc * size - f32(0.5)).astype(f32)
+    return (v * size - loc).astype(f32)
+
+
+def _mesh_attribute(gm: dict, key):
+    """AttributeSet::find(AttributeRequest) on one mesh (render/attribute.cpp):
+    (element, type, rows) of the attribute a request names, or None."""
+    from . import nodes as _nodes_mod
+    m = gm.get("mesh")
+    if m is None:
+        return None
+    T = gm["t"].shape[0]
+    if key == _nodes_mod.ATTR_STD_UV or key == "UVMap":
+        if m.uv is None:
+            return None
+        return "corner", "float2", np.asarray(m.uv, dtype=np.float32).reshape(3 * T, 2)
+    if key == _nodes_mod.ATTR_STD_GENERATED:
+        return "vertex", "float3", _generated_coordinates(m)
+    colors = dict(m.vertex_colors or {})
+    if key == _nodes_mod.ATTR_STD_VERTEX_COLOR:
+        if not colors:
+            return None
+        key = next(iter(colors))
+    if not isinstance(key, str):
+        return None
+    if key in colors:
+        c = np.asarray(colors[key], dtype=np.float64).reshape(3 * T, 4)
+        b = np.clip(np.rint(c * 255.0), 0, 255).astype(np.uint32)
+        return "corner_byte", "rgba", (b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16) | (b[:, 3] << 24)).astype(np.uint32)
+    attrs = m.attributes or {}
+    if key not in attrs:
+        return None
+    element, data = attrs[key]
+    if element not in ("vertex", "face", "corner"):
+        raise ValueError(f"attribute {key!r}: element must be vertex, face or corner, not {element!r}")
+    rows = {"vertex": gm["v"].shape[0], "face": T, "corner": 3 * T}[element]
+    a = np.asarray(data, dtype=np.float32)
+    a = a.reshape(rows) if a.size == rows else a.reshape(rows, -1)
+    kind = "float" if a.ndim == 1 else {2: "float2", 3: "float3"}.get(a.shape[1])
+    if kind is None:
+        raise ValueError(f"attribute {key!r}: rows of 1, 2 or 3 floats")
+    return element, kind, a
+
+
+def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobjects) -> dict:
+    """GeometryManager::device_update_attributes (render/geometry.cpp:379-474)
+    and update_attribute_element_offset (:508-620): per geometry one map row
+    pair (geometry, subdivision) per attribute its shaders request, closed by
+    the ATTR_STD_NONE pair; the data appended to the float / float2 / float3 /
+    uchar4 arrays in geometry and request order, offsets corrected by the
+    geometry's vert / prim offsets so the kernel indexes them with global
+    vertex and triangle numbers.  Curves objects get an empty map."""
+    geoms = g["geoms"]
+    data = {"float": [], "float2": [], "float3": [], "uchar4": []}
+    size = {"float": 0, "float2": 0, "float3": 0, "uchar4": 0}
+    rows = []
+    geom_offset = {}
+    for gi, gm in enumerate(geoms):
+        used = sorted(set(int(k) for k in np.unique(gm["sh"]))) if len(gm["sh"]) else []
+        reqs = []
+        for k in used:
+            for key in svm_compiler.requests[k]:
+                if key not in reqs:
+                    reqs.append(key)
+        geom_offset[gi] = len(rows)
+        for key in reqs:
+            aid = svm_compiler.attribute_ids[key] if isinstance(key, str) else int(key)
+            found = _mesh_attribute(gm, key)
+            if found is None:
+                # AttributeRequest defaults: element NONE, offset 0, TypeFloat
+                rows.append((aid, 0, 0, 0))
+            else:
+                element, kind, a = found
+                store = "uchar4" if kind == "rgba" else "float3" if kind == "float3" else kind
+                if kind == "float3":
+                    a4 = np.zeros((a.shape[0], 4), dtype=np.float32)
+                    a4[:, :3] = a
+                    a = a4
+                offset = size[store]
+                data[store].append(a)
+                size[store] += a.shape[0]
+                if element == "vertex":
+                    offset -= gm["vert_offset"]
+                elif element == "face":
+                    offset -= gm["tri_offset"]
+                elif element in ("corner", "corner_byte"):
+                    offset -= 3 * gm["tri_offset"]
+                rows.append((aid, _ATTR_ELEMENTS[element], offset & 0xFFFFFFFF, _ATTR_TYPES[kind]))
+            rows.append((0, 0, 0, 0))  # no subdivision surface
+        rows.extend([(0, 0, 0, 0)] * 2)
+    empty = len(rows)
+    rows.extend([(0, 0, 0, 0)] * 2)
+    for i, ob in enumerate(objects):
+        kobjects[i].attribute_map_offset = geom_offset[ob["geom"]] if ob.get("geom") is not None else empty
+
+    def cat(store, shape, dtype):
+        if not data[store]:
+            return np.zeros(shape, dtype=dtype)
+        return np.concatenate(data[store]).astype(dtype)
+
+    ntri = max(g["ntri"], 1)
+    return {
+        "__attributes_map": np.array(rows, dtype=np.uint32).reshape(-1, 4),
+        "__attributes_float": cat("float", (1,), np.float32),
+        "__attributes_float2": cat("float2", (1, 2), np.float32),
+        "__attributes_float3": cat("float3", (1, 4), np.float32),
+        "__attributes_uchar4": cat("uchar4", (1,), np.uint32),
+        # Mesh::pack_patches (mesh.cpp): no subdivision patches, every triangle ~0
+        "__tri_patch": np.full(ntri, 0xFFFFFFFF, dtype=np.uint32),
+    }
 
 
 def _object_shaders(ob, tri_shader_idx) -> list:
@@ -1484,18 +1654,18 @@ def _pack_geometry(scene: Scene) -> dict:
     objects = []
     for m in scene.meshes:
         v, t, sh, nrm = _mesh_arrays(m)
-        geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(m.smooth), applied=True))
+        geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(m.smooth), applied=True, mesh=m))
         objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True))
     for inst in scene.instances:
         tfm = np.asarray(inst.tfm, dtype=np.float64).reshape(3, 4)
         if users[id(inst.mesh)] == 1:
             v, t, sh, nrm = _mesh_arrays(inst.mesh, tfm.astype(np.float32))
-            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True))
+            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True, mesh=inst.mesh))
             objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True))  # tfm reset on apply
             continue
         if id(inst.mesh) not in geom_of:
             v, t, sh, nrm = _mesh_arrays(inst.mesh)
-            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=False))
+            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=False, mesh=inst.mesh))
             geom_of[id(inst.mesh)] = len(geoms) - 1
         objects.append(dict(geom=geom_of[id(inst.mesh)], tfm=tfm, applied=False))
     # hair objects: transforms applied, after the meshes (object order)
@@ -1628,7 +1798,7 @@ def _pack_geometry(scene: Scene) -> dict:
                 leaves=np.concatenate(leaf_parts), root=root, prim_index=prim_index, prim_object=prim_object,
                 prim_type=prim_type, prim_visibility=prim_visibility, prim_tri_index=prim_tri_index,
                 prim_tri_verts=prim_tri_verts, tri_vindex=tri_vindex, tri_vnormal=tri_vnormal, objects=objects,
-                tri_pos_object=tri_pos_object, ncurves=0, nsegments=0)
+                tri_pos_object=tri_pos_object, ncurves=0, nsegments=0, geoms=geoms)
 
 
 def _pack_hair(objects: list, shape: str) -> dict:
@@ -1748,7 +1918,7 @@ def _pack_geometry_with_curves(objects, geoms, ref_tri, ref_obj, tri_pos, ntri, 
                 tri_vindex=tri_vindex, tri_vnormal=tri_vnormal, objects=objects, tri_pos_object=tri_pos,
                 ncurves=hair["ncurves"], nsegments=ns, curve_first=hair["first"].astype(np.uint32),
                 curve_nkeys=hair["nkeys"].astype(np.uint32), curve_shader=hair["shader"],
-                curve_keys=hair["keys"])
+                curve_keys=hair["keys"], geoms=geoms)
 
 
 def _instance_bounds(v: np.ndarray, tfm) -> np.ndarray:
@@ -1908,4 +2078,6 @@ ELEMENT_BYTES = {
     "__light_background_marginal_cdf": 8, "__light_background_conditional_cdf": 8,
     "__curves": 16, "__curve_keys": 16,
     "__object_volume_step": 4, "__attributes_map": 16,
+    "__attributes_float": 4, "__attributes_float2": 8, "__attributes_float3": 16, "__attributes_uchar4": 4,
+    "__tri_patch": 4,
 }

@@ -1239,3 +1239,59 @@ def shading_image(width=48, height=48, samples=8) -> sc.Scene:
     s.world_strength = 1.0
     s.world_map_resolution = 32
     return s
+
+
+def shading_attributes(width=48, height=48, samples=8) -> sc.Scene:
+    """Geometry attributes (geom_attribute.h, geom_triangle.h:114-356,
+    svm_attribute.h, svm_vertex_color.h): the UV map through an image
+    texture's default vector and the Texture Coordinate node, generated
+    coordinates (a checker and a noise texture with default vectors), byte
+    vertex colours (active and named layers, colour and alpha), named float /
+    float2 / float3 attributes per vertex, face and corner read as Color,
+    Vector and Fac, a missing attribute (zero), and a shared (instanced) mesh
+    whose attributes are indexed through corrected offsets; the world reads
+    Generated (the ray direction in a background shader)."""
+    from . import nodes as nd
+
+    im = _test_image(21, 13, 17, "byte4", interpolation="linear", extension="repeat")
+    tc = nd.tex_coord()
+    wear = nd.attribute("wear")
+    colors = [
+        nd.image_texture(im)["Color"],
+        tc["UV"],
+        tc["Generated"],
+        nd.checker(scale=3.0)["Color"],
+        nd.noise_texture(scale=4.0, detail=1.0)["Color"],
+        nd.vertex_color()["Color"],
+        nd.mix_rgb("mix", nd.vertex_color("Tint")["Alpha"], (0.1, 0.3, 0.1), nd.vertex_color("Tint")["Color"]),
+        nd.color_ramp(wear["Fac"], [(0.0, (0.9, 0.2, 0.1, 1.0)), (1.0, (0.1, 0.3, 0.9, 1.0))])["Color"],
+        nd.attribute("facecol")["Color"],
+        nd.attribute("cornerf2")["Vector"],
+        nd.mix_rgb("add", 0.5, nd.attribute("missing")["Color"], (0.2, 0.2, 0.6)),
+        nd.mix_rgb("mix", nd.attribute("Col")["Fac"], nd.attribute("Col")["Color"], (0.9, 0.9, 0.2)),
+        nd.combine_xyz(nd.attribute("uv")["Fac"], 0.3, 0.5),
+        wear["Vector"],
+    ]
+    s = _grid_scene(colors, width, height, samples, "shading_attributes", glossy_every=5)
+    rng = np.random.default_rng(77)
+    for i, m in enumerate(s.meshes[:len(colors)]):
+        nv, nt = len(m.verts), len(m.tris)
+        m.uv = rng.uniform(-0.2, 1.3, (nt, 3, 2)).astype(np.float32)
+        m.vertex_colors = {"Col": rng.uniform(0.0, 1.0, (nt, 3, 4)), "Tint": rng.uniform(0.0, 1.0, (nt, 3, 4))}
+        m.attributes = {"wear": ("vertex", rng.uniform(0.0, 1.0, nv).astype(np.float32)),
+                        "facecol": ("face", rng.uniform(0.0, 1.0, (nt, 3)).astype(np.float32)),
+                        "cornerf2": ("corner", rng.uniform(0.0, 1.0, (3 * nt, 2)).astype(np.float32))}
+    # a box shared by two objects (instanced: object-space vertices, own BVH)
+    # whose generated coordinates and per-vertex attribute colour it
+    bv, bt = _box((0.0, 0.0, 0.0), (0.5, 0.5, 0.5))
+    n = len(s.materials)
+    s.materials.append(sc.diffuse(nd.mix_rgb("mix", nd.attribute("wear")["Fac"], tc["Generated"], (0.8, 0.1, 0.1))))
+    box = sc.Mesh(bv, bt, shader=n)
+    box.attributes = {"wear": ("vertex", rng.uniform(0.0, 1.0, len(bv)).astype(np.float32))}
+    box.uv = rng.uniform(0.0, 1.0, (len(bt), 3, 2)).astype(np.float32)
+    s.instances = [sc.Instance(box, _tfm((-1.6, -1.2, -0.6), rot_y=0.5)),
+                   sc.Instance(box, _tfm((1.5, 1.1, -0.5), rot_y=-0.3, scale=(0.8, 1.2, 0.8)))]
+    gen = nd.separate_xyz(nd.tex_coord()["Generated"])
+    s.world_color = nd.combine_xyz(nd.map_range(gen["Y"], -1.0, 1.0, 0.1, 0.6), 0.35,
+                                   nd.map_range(gen["X"], -1.0, 1.0, 0.2, 0.7))
+    return s
