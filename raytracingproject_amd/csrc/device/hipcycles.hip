@@ -1819,7 +1819,8 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           closures += (ctype == CLOSURE_BSDF_PRINCIPLED_ID)                                 ? 8 :
                       (ctype >= CLOSURE_BSSRDF_CUBIC_ID && ctype <= CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) ? 3 :
                       (ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID ||
-                       ctype == CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)                  ? 2 :
+                       ctype == CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID ||
+                       ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID)                       ? 2 :
                                                                                             1;
           const bool rough_diffuse = ctype == CLOSURE_BSDF_DIFFUSE_ID &&
                                      (((node.y >> 8) & 0xFF) != SVM_STACK_INVALID || node.z != 0u);
@@ -1834,9 +1835,12 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             if (off + 5 >= n) {
               return "principled BSDF: parameter nodes past __svm_nodes";
             }
-            if (prog[off + 2].y != CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID) {
-              return "shader " + std::to_string(sh) +
-                     ": principled BSDF: only the GGX distribution is implemented (multiscatter GGX is not)";
+            /* GGX or multiscatter GGX: the multiscatter glass lobe of rough
+             * transmission raises CY_ERR_CLOSURE when reached (lgammaf) */
+            if (prog[off + 2].y != CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID &&
+                prog[off + 2].y != CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID) {
+              return "shader " + std::to_string(sh) + ": principled BSDF: unknown distribution " +
+                     std::to_string(prog[off + 2].y);
             }
           }
           switch (ctype) {
@@ -1857,6 +1861,7 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
             case CLOSURE_BSDF_DIFFUSE_TOON_ID:
             case CLOSURE_BSDF_GLOSSY_TOON_ID:
+            case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
             case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node, random walk */
               /* a random-walk BSSRDF, or a principled BSDF with subsurface (param2: linked or > 0) */
               *uses_bssrdf |= ctype == CLOSURE_BSSRDF_RANDOM_WALK_ID ||

@@ -1559,6 +1559,10 @@ CY_FN int bsdf_ashikhmin_shirley_sample(const CyClosure *sc,
 
 #endif /* CY_CLOSURE_EXT: Beckmann, Ashikhmin-Shirley */
 
+#if CY_CLOSURE_EXT
+#  include "cy_microfacet_multi.h"
+#endif
+
 /* ---------------------------------------------------------------------------
  * Dispatch (bsdf.h)
  */
@@ -1651,6 +1655,10 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
     case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
       label = bsdf_ashikhmin_shirley_sample(sc, sd->I, randu, randv, eval, omega_in, pdf, err);
       break;
+    case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+    case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
+      label = bsdf_microfacet_multi_ggx_sample(sd, sc, sd->I, eval, omega_in, pdf);
+      break;
     case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
       label = bsdf_ashikhmin_velvet_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
@@ -1725,6 +1733,10 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
       case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
         eval = bsdf_ashikhmin_shirley_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
+        eval = bsdf_microfacet_multi_ggx_eval_reflect(sd, sc, sd->I, omega_in, pdf);
+        break;
       case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
         eval = bsdf_ashikhmin_velvet_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
@@ -1762,6 +1774,11 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
       case CLOSURE_BSDF_MICROFACET_BECKMANN_ID:
       case CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID:
         eval = bsdf_beckmann_eval_transmit(sc, sd->I, omega_in, pdf);
+        break;
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID: /* bsdf_microfacet_multi.h:418-426 */
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
+        *pdf = 0.0f;
+        eval = mk3(0.0f, 0.0f, 0.0f);
         break;
 #endif
       default:

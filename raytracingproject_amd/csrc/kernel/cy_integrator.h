@@ -1386,8 +1386,18 @@ CY_FN bool shade_path(const CyGlobals *kg,
         float blur_roughness = sqrtf(1.0f - blur_pdf) * 0.5f;
         for (int i = 0; i < sd.num_closure; i++) {
           CyClosure *sc = &sd.closure[i];
-          if (sc->type == CLOSURE_BSDF_MICROFACET_GGX_ID ||
-              sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID) {
+          /* bsdf.h:706-735 bsdf_blur: GGX (all variants), multiscatter GGX,
+           * Beckmann and Ashikhmin-Shirley raise their roughness alike */
+          if (sc->type == CLOSURE_BSDF_MICROFACET_GGX_ID || sc->type == CLOSURE_BSDF_MICROFACET_GGX_FRESNEL_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_GGX_CLEARCOAT_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_BECKMANN_ID ||
+              sc->type == CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID ||
+              sc->type == CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID) {
             sc->alpha_x = fmaxf(blur_roughness, sc->alpha_x);
             sc->alpha_y = fmaxf(blur_roughness, sc->alpha_y);
           }

@@ -1490,7 +1490,8 @@ CY_FN void svm_node_principled_bsdf(const CyGlobals *kg,
           sd->flag |= bsdf_microfacet_ggx_fresnel_setup(b, sd);
         }
         else {
-          cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID);
+          /* multi-scatter GGX (svm_closure.h:281-283) */
+          sd->flag |= bsdf_microfacet_multi_ggx_fresnel_setup(sd, b);
         }
       }
     }
@@ -1643,6 +1644,7 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
 #if CY_CLOSURE_EXT
     case CLOSURE_BSDF_MICROFACET_BECKMANN_ID:
     case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
+    case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
 #endif
     {
       if (!KD->integrator.caustics_reflective && (path_flag & PATH_RAY_DIFFUSE)) {
@@ -1693,6 +1695,18 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
       }
       else if (type == CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID) {
         sd->flag |= bsdf_ashikhmin_shirley_setup(b);
+      }
+      else if (type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID) {
+        /* svm_closure.h:345-356: the color (param4) in a MicrofacetExtra */
+        const int extra = closure_alloc_extra(sd);
+        if (extra >= 0) {
+          CyClosure *ex = &sd->closure[extra];
+          b->extra = extra;
+          ex->weight = svm_load3(stack, data_node.w, err);
+          ex->N = mk3(0.0f, 0.0f, 0.0f);
+          ex->alpha_x = 0.0f;
+          sd->flag |= bsdf_microfacet_multi_ggx_setup(sd, b);
+        }
       }
 #endif
       else {
@@ -2321,6 +2335,12 @@ CY_FN void shader_eval_surface(
   sd->num_closure = 0;
   sd->num_closure_left = max_closures;
   svm_eval_nodes(kg, sd, state, path_flag, err);
+#if CY_CLOSURE_EXT
+  if ((sd->flag & SD_BSDF_NEEDS_LCG) && state) {
+    /* kernel_shader.h:1109-1111: lcg_state_init_addrspace(state, 0xb4bc3953) */
+    sd->lcg_state = lcg_init(state->rng_hash + (uint)state->rng_offset + (uint)state->sample * 0xb4bc3953u);
+  }
+#endif
 }
 
 /* SHADER_EVAL_DISPLACE for one (object, prim, u, v): kernel_displace_evaluate

@@ -183,6 +183,7 @@ enum {
   CLOSURE_BSDF_MICROFACET_GGX_CLEARCOAT_ID = 12,
   CLOSURE_BSDF_MICROFACET_BECKMANN_ID = 13,
   CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID = 14,
+  CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID = 15,
   CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID = 16,
   CLOSURE_BSDF_ASHIKHMIN_VELVET_ID = 17,
   CLOSURE_BSDF_GLOSSY_TOON_ID = 20,
@@ -362,6 +363,13 @@ typedef struct CySD {
   int svm_stride;
   int svm_fast;     /* entries [0, svm_fast) at svm_stack[i * svm_stride] */
   float *svm_spill; /* entries [svm_fast, CY_SVM_STACK) at svm_spill[i - svm_fast] */
+#if CY_CLOSURE_EXT
+  /* sd->lcg_state of closures with SD_BSDF_NEEDS_LCG (multiscatter GGX): set
+   * after shader evaluation, stepped by every evaluation and sample of such a
+   * closure; mutable because evaluation otherwise reads the shading point
+   * only (the reference passes ShaderData by non-const pointer for it) */
+  mutable uint lcg_state;
+#endif
 } CySD;
 
 /* Where a shading thread keeps its closures and SVM stack.  The device kernel

@@ -80,9 +80,11 @@ CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID = 40
 
 # Distribution enums of the glossy / anisotropic / glass / refraction nodes
 # (nodes.cpp GlossyBsdfNode, GlassBsdfNode, RefractionBsdfNode NODE_DEFINE)
+CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID = 14
 GLOSSY_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFLECTION_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_ID,
                         "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_ID,
-                        "ashikhmin_shirley": CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID}
+                        "ashikhmin_shirley": CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID,
+                        "multi_ggx": CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID}
 GLASS_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_SHARP_GLASS_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID,
                        "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID}
 REFRACTION_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFRACTION_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID,
@@ -188,6 +190,8 @@ class Closure:
             return self.a.num_closures() + self.b.num_closures()
         if self.kind == "glass":
             return 2
+        if self.kind in ("glossy", "anisotropic") and self.closure_type() == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+            return 2  # CLOSURE_IS_BSDF_MULTISCATTER
         if self.kind == "principled":
             return 8  # CLOSURE_IS_PRINCIPLED
         if self.kind == "subsurface":
@@ -258,7 +262,8 @@ def diffuse(color, roughness=0.0, normal=None):
 
 
 def glossy(color, roughness, normal=None, distribution="ggx"):
-    """Glossy BSDF: distribution ggx | beckmann | ashikhmin_shirley | sharp."""
+    """Glossy BSDF: distribution ggx | beckmann | ashikhmin_shirley | sharp |
+    multi_ggx (multiple-scattering GGX, bsdf_microfacet_multi.h)."""
     return Closure("glossy", _const_or_socket(color), roughness=roughness, normal=normal, distribution=distribution)
 
 
@@ -288,10 +293,12 @@ def principled(distribution="ggx", subsurface_method="burley", **params):
     """Principled BSDF (nodes.cpp PrincipledBsdfNode, svm_closure.h:100-463).
     Parameters are PRINCIPLED_DEFAULTS keys (constants or sockets) plus the
     normal / clearcoat_normal / tangent vector sockets.  distribution is
-    "ggx" ("multiscatter" is refused at load_kernels); subsurface > 0 needs a
-    BSSRDF, which the device does not implement.  The node's Emission and
-    Alpha inputs (expanded into separate closures by the reference graph) are
-    expressed here with emission() / transparent() and mix()."""
+    "ggx" or "multiscatter" (Blender's default: multiple-scattering GGX for the
+    specular layer; its rough-transmission glass lobe is not implemented, so a
+    multiscatter principled with transmission is refused); subsurface > 0 adds
+    a BSSRDF (random walk).  The node's Emission and Alpha inputs (expanded
+    into separate closures by the reference graph) are expressed here with
+    emission() / transparent() and mix()."""
     unknown = set(params) - set(PRINCIPLED_DEFAULTS) - set(PRINCIPLED_VECTORS)
     if unknown:
         raise ValueError(f"principled: unknown parameters {sorted(unknown)}")
@@ -299,6 +306,11 @@ def principled(distribution="ggx", subsurface_method="burley", **params):
     p.update(params)
     if subsurface_method not in PRINCIPLED_SUBSURFACE_METHODS:
         raise ValueError(f"principled: unknown subsurface_method {subsurface_method}")
+    if distribution not in PRINCIPLED_DISTRIBUTIONS:
+        raise ValueError(f"principled: distribution one of {sorted(PRINCIPLED_DISTRIBUTIONS)}")
+    if distribution == "multiscatter" and (_nodes.is_linked(p["transmission"]) or float(p["transmission"]) > 0.0):
+        raise ValueError("principled: multiscatter GGX glass (transmission > 0) is not implemented "
+                         "(bsdf_microfacet_multi.h glass walk needs glibc's lgammaf)")
     return Closure("principled", distribution=distribution, params=p, subsurface_method=subsurface_method)
 
 
@@ -491,8 +503,14 @@ class SVMCompiler:
             tangent_off = self.nc.link(c.tangent, "vector")
             # param3 (rotation) is always stack-assigned (BsdfNode::compile)
             param3_off = self.nc.assign(c.rotation, "float")
+            if ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+                param4_off = self.nc.assign(c.color, "color")  # nodes.cpp:2330-2332
         elif c.kind == "glossy":
             params = (c.roughness, None)
+            if ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+                # GlossyBsdfNode::compile (nodes.cpp:2423-2424): the colour
+                # goes to the multiscatter walk as param4 (stack-assigned)
+                param4_off = self.nc.assign(c.color, "color")
         elif c.kind == "subsurface":
             # BsdfNode::compile(Scale, Texture Blur, Radius, Sharpness): radius and
             # sharpness always stack-assigned

@@ -1295,3 +1295,33 @@ def shading_attributes(width=48, height=48, samples=8) -> sc.Scene:
     s.world_color = nd.combine_xyz(nd.map_range(gen["Y"], -1.0, 1.0, 0.1, 0.6), 0.35,
                                    nd.map_range(gen["X"], -1.0, 1.0, 0.2, 0.7))
     return s
+
+
+def closures_multiscatter(width=48, height=48, samples=8, filter_glossy=0.0) -> sc.Scene:
+    """Multiple-scattering GGX (closure/bsdf_microfacet_multi.h, the
+    MF_MULTI_GLOSSY walk of bsdf_microfacet_multi_impl.h): the Glossy BSDF's
+    Multiscatter GGX distribution with a node-driven colour, the anisotropic
+    variant with a tangent frame, and Principled BSDFs with the multiscatter
+    distribution (Blender's default) as dielectric, tinted metal, anisotropic
+    metal and clearcoat over a rough base; the walk steps each shading point's
+    LCG.  filter_glossy > 0 also blurs the closures (bsdf_blur)."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    tangent = nd.vector_math("cross_product", g["Normal"], (0.0, 1.0, 0.0))["Vector"]
+    u = nd.separate_xyz(g["Parametric"])["X"]
+    tint = nd.mix_rgb("mix", u, (0.9, 0.5, 0.2), (0.3, 0.7, 0.9))
+    mats = [
+        sc.mix(0.3, sc.diffuse((0.2, 0.5, 0.2)), sc.glossy(tint, 0.45, distribution="multi_ggx")),
+        sc.anisotropic((0.9, 0.8, 0.6), 0.5, 0.6, 0.1, tangent, distribution="multi_ggx"),
+        sc.principled("multiscatter", base_color=(0.8, 0.25, 0.1), roughness=0.5, specular=0.5),
+        sc.principled("multiscatter", base_color=(0.95, 0.7, 0.35), metallic=1.0, roughness=0.35,
+                      specular_tint=0.4),
+        sc.principled("multiscatter", base_color=(0.7, 0.75, 0.8), metallic=1.0, roughness=0.6, anisotropic=0.5,
+                      anisotropic_rotation=0.2, tangent=tangent),
+        sc.principled("multiscatter", base_color=(0.1, 0.2, 0.6), roughness=0.9, clearcoat=0.8,
+                      clearcoat_roughness=0.2, specular=0.6, metallic=0.3),
+    ]
+    s = _closure_gallery(width, height, samples, "closures_multiscatter", mats)
+    s.filter_glossy = filter_glossy
+    return s

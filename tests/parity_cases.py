@@ -39,6 +39,11 @@ CASES = {
     "closures_diffuse": lambda: scenes.closures_diffuse(48, 48, 8),
     "closures_microfacet": lambda: scenes.closures_microfacet(48, 48, 8),
     "closures_principled": lambda: scenes.closures_principled(48, 48, 8),
+    # multiple-scattering GGX (bsdf_microfacet_multi.h): glossy / anisotropic
+    # nodes and the Principled default distribution; the blurred variant sets
+    # Filter Glossy (bsdf_blur of every microfacet closure)
+    "closures_multiscatter": lambda: scenes.closures_multiscatter(48, 48, 8),
+    "closures_multiscatter_blur": lambda: scenes.closures_multiscatter(48, 48, 8, filter_glossy=1.0),
     # image / environment textures (kernel_cpu_image.h, svm_image.h)
     "shading_image": lambda: scenes.shading_image(48, 48, 8),
     # adaptive sampling (kernel_adaptive_sampling.h): aux buffer + sample count

@@ -244,6 +244,10 @@ extern "C" int emu_render(const void *data,
                           int stride,
                           int pass_stride)
 {
+  const hc_KernelData *kd = (const hc_KernelData *)data;
+  if (kd->integrator.max_closures > CY_MAX_CLOSURE && !kd->integrator.use_volumes) {
+    return -1; /* the device refuses these scenes too (hipcy_load_kernels) */
+  }
   CyGlobals kg;
   emu_bind(&kg, data, n_arrays, names, ptrs, bvhw);
   hc_float4 rec[12];
