@@ -71,6 +71,7 @@ def kernel_source_digest():
 
 
 SHADE_VARIANTS = (1, 2, 4, 8)  # closure-array sizes of the shade kernel (csrc/device/k_shade.h)
+LARGE_SHADE_VARIANTS = (16, 64)  # texture / volume builds only (extended closure set)
 
 
 def build_device(force=False, variant=None, defines=(), traversal_only=False):
@@ -96,10 +97,10 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False):
     jobs = [([HIPCC, *cflags, *dflags, inc, "-c", "-o", os.path.join(objdir, "hipcycles.o"), src],
              os.path.join(objdir, "hipcycles.o"))]
     shade_objs = []
-    for mc in SHADE_VARIANTS:
+    for mc in SHADE_VARIANTS + LARGE_SHADE_VARIANTS:
         # plain (closure nodes only), _tex (texture nodes, extended closures),
         # _vol (_tex with volumes)
-        for kind in ("", "_tex", "_vol"):
+        for kind in ("", "_tex", "_vol") if mc in SHADE_VARIANTS else ("_tex", "_vol"):
             name = f"mc{mc}{kind}"
             if traversal_only:
                 shade_objs.append(os.path.join(REPO, "build", "device", "default", f"k_shade_{name}.o"))

@@ -2052,8 +2052,8 @@ int hipcy_load_kernels(hipcy_device *dev)
     why = "adaptive_stop_per_sample (a CPU-device setting; this device filters at adaptive_step samples)";
   else if (d.background.portal_weight > 0.0f || d.background.num_portals) why = "light portals";
   else if (d.background.sun_weight > 0.0f) why = "sky texture sun sampling";
-  else if (d.integrator.max_closures > CY_MAX_CLOSURE && !d.integrator.use_volumes)
-    why = "max_closures > " + std::to_string(CY_MAX_CLOSURE);
+  else if (d.integrator.max_closures > CY_DEVICE_MAX_CLOSURE && !d.integrator.use_volumes)
+    why = "max_closures > " + std::to_string(CY_DEVICE_MAX_CLOSURE);
   else if (d.bvh.have_motion || d.bvh.use_bvh_steps) why = "motion blur (motion triangles / curves)";
   else if (d.bvh.have_curves && (d.bvh.curve_subdivisions < 1 || d.bvh.curve_subdivisions > 16))
     why = "curve_subdivisions outside 1..16";
@@ -2155,8 +2155,8 @@ int hipcy_load_kernels(hipcy_device *dev)
     const int bound = std::max(std::min(surface_closures, (int)d.integrator.max_closures),
                                (int)(volume_objects + 1) * volume_closures);
     dev->shade_closures = std::max(bound, 1);
-    if (bound > CY_MAX_CLOSURE) {
-      why = "volume scene needing " + std::to_string(bound) + " closures > " + std::to_string(CY_MAX_CLOSURE);
+    if (bound > CY_DEVICE_MAX_CLOSURE) {
+      why = "volume scene needing " + std::to_string(bound) + " closures > " + std::to_string(CY_DEVICE_MAX_CLOSURE);
     }
     else if (volume_objects + 2 > CY_VOLUME_STACK) {
       why = "more than " + std::to_string(CY_VOLUME_STACK - 2) + " volume objects (the device's volume stack)";

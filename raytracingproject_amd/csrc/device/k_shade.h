@@ -1,6 +1,7 @@
 /*
  * k_shade.h — launchers of the shade kernel, compiled once per closure-array
- * size (k_shade.hip with CY_MAX_CLOSURE = 1, 2, 4, 8).  A scene's
+ * size (k_shade.hip with CY_MAX_CLOSURE = 1, 2, 4, 8; 16 and 64 for the
+ * texture / volume builds).  A scene's
  * KernelIntegrator.max_closures (render/integrator.cpp) picks the smallest
  * variant that holds its shaders' closures, so the per-path closure array
  * stays small enough to live in registers instead of scratch.  Each size is
@@ -34,13 +35,24 @@ void cy_launch_shade_mc1_vol(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc2_vol(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc4_vol(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc8_vol(CY_SHADE_LAUNCHER_ARGS);
+/* large closure arrays (mixed Principled BSDFs and the like; the reference
+ * CPU kernel's MAX_CLOSURE is 64): extended closure set only, in private
+ * memory */
+void cy_launch_shade_mc16_tex(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc64_tex(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc16_vol(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc64_vol(CY_SHADE_LAUNCHER_ARGS);
+#define CY_DEVICE_MAX_CLOSURE 64
 
 static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, CY_SHADE_LAUNCHER_ARGS)
 {
   auto fn = volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :
                        max_closures <= 2 ? cy_launch_shade_mc2_vol :
                        max_closures <= 4 ? cy_launch_shade_mc4_vol :
-                                           cy_launch_shade_mc8_vol) :
+                       max_closures <= 8 ? cy_launch_shade_mc8_vol :
+                       max_closures <= 16 ? cy_launch_shade_mc16_vol :
+                                            cy_launch_shade_mc64_vol) :
+            max_closures > 8 ? (max_closures <= 16 ? cy_launch_shade_mc16_tex : cy_launch_shade_mc64_tex) :
             tex_nodes ? (max_closures <= 1 ? cy_launch_shade_mc1_tex :
                          max_closures <= 2 ? cy_launch_shade_mc2_tex :
                          max_closures <= 4 ? cy_launch_shade_mc4_tex :

@@ -16,7 +16,7 @@
 #include "k_shade.h"
 
 #ifndef CY_SHADE_VARIANT
-#  error "CY_SHADE_VARIANT must be defined (mc1, mc2, mc4, mc8)"
+#  error "CY_SHADE_VARIANT must be defined (mc1, mc2, mc4, mc8, mc16, mc64)"
 #endif
 /* Closures and the first CY_SVM_LDS stack entries in LDS for closure arrays of
  * up to 4 (LDS per 256-thread block: (R*MAXC + 1 + CY_SVM_LDS) KiB of the

@@ -2333,7 +2333,10 @@ CY_FN void shader_eval_surface(
     max_closures = KD->integrator.max_closures;
   }
   sd->num_closure = 0;
-  sd->num_closure_left = max_closures;
+  /* the closure array holds CY_MAX_CLOSURE (the variant load_kernels picked
+   * holds every closure the shaders allocate, so allocations succeed exactly
+   * as with the reference's budget; the clamp keeps extras in the array) */
+  sd->num_closure_left = (max_closures < CY_MAX_CLOSURE) ? max_closures : CY_MAX_CLOSURE;
   svm_eval_nodes(kg, sd, state, path_flag, err);
 #if CY_CLOSURE_EXT
   if ((sd->flag & SD_BSDF_NEEDS_LCG) && state) {

@@ -184,7 +184,7 @@ CY_NOINLINE void shader_eval_volume(
                                0 :
                                KD->integrator.max_closures;
   sd->num_closure = 0;
-  sd->num_closure_left = max_closures;
+  sd->num_closure_left = (max_closures < CY_MAX_CLOSURE) ? max_closures : CY_MAX_CLOSURE; /* see shader_eval_surface */
   sd->flag = 0;
   sd->object_flag = 0;
   for (int i = 0; stack->e[i].shader != SHADER_NONE; i++) {

@@ -1325,3 +1325,33 @@ def closures_multiscatter(width=48, height=48, samples=8, filter_glossy=0.0) -> 
     s = _closure_gallery(width, height, samples, "closures_multiscatter", mats)
     s.filter_glossy = filter_glossy
     return s
+
+
+def closures_layered(width=48, height=48, samples=8, triple=False) -> sc.Scene:
+    """Materials needing more than 8 closures (the device's 16- and 64-closure
+    shading variants): two Principled BSDFs mixed by a node-driven factor
+    (16), a Principled BSDF over a multiscatter glossy and a translucent
+    layer (11), and a deep mix tree of nine lobes; `triple` adds a mix of
+    three Principled BSDFs (24: the 64-closure variant)."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    u = nd.separate_xyz(g["Parametric"])["X"]
+    p1 = sc.principled(base_color=(0.8, 0.3, 0.2), roughness=0.4, specular=0.5, clearcoat=0.5, sheen=0.3)
+    p2 = sc.principled("multiscatter", base_color=(0.3, 0.6, 0.8), metallic=0.7, roughness=0.5, specular=0.4)
+    deep = sc.diffuse((0.5, 0.5, 0.5))
+    for i, c in enumerate([(0.9, 0.2, 0.2), (0.2, 0.9, 0.2), (0.2, 0.2, 0.9), (0.9, 0.9, 0.2)]):
+        deep = sc.mix(0.5, deep, sc.mix(0.4, sc.glossy(c, 0.2 + 0.15 * i), sc.diffuse(c, roughness=0.3 * i)))
+    mats = [
+        sc.mix(u, p1, p2),
+        sc.mix(0.5, sc.principled(base_color=(0.9, 0.8, 0.4), roughness=0.3, specular=0.5, clearcoat=1.0),
+               sc.mix(0.5, sc.glossy((0.8, 0.8, 0.8), 0.5, distribution="multi_ggx"),
+                      sc.translucent((0.4, 0.8, 0.4)))),
+        deep,
+        sc.mix(0.3, p1, sc.mix(0.5, p2, sc.principled(base_color=(0.4, 0.9, 0.4), roughness=0.2, specular=0.5)))
+        if triple else sc.diffuse((0.6, 0.6, 0.6)),
+        sc.mix(0.5, p2, sc.glossy((0.9, 0.6, 0.3), 0.3)),
+        sc.principled(base_color=(0.2, 0.2, 0.2), roughness=0.6, specular=0.5),
+    ]
+    return _closure_gallery(width, height, samples, "closures_layered_triple" if triple else "closures_layered",
+                            mats)

@@ -44,6 +44,9 @@ CASES = {
     # Filter Glossy (bsdf_blur of every microfacet closure)
     "closures_multiscatter": lambda: scenes.closures_multiscatter(48, 48, 8),
     "closures_multiscatter_blur": lambda: scenes.closures_multiscatter(48, 48, 8, filter_glossy=1.0),
+    # more than 8 closures per shading point (16- / 64-closure shading variants)
+    "closures_layered": lambda: scenes.closures_layered(48, 48, 8),
+    "closures_layered_triple": lambda: scenes.closures_layered(48, 48, 8, triple=True),
     # image / environment textures (kernel_cpu_image.h, svm_image.h)
     "shading_image": lambda: scenes.shading_image(48, 48, 8),
     # adaptive sampling (kernel_adaptive_sampling.h): aux buffer + sample count

@@ -14,6 +14,8 @@
 #include <vector>
 #include <vector>
 
+/* the device's largest shading variant (csrc/device/k_shade.h CY_DEVICE_MAX_CLOSURE) */
+#define CY_MAX_CLOSURE 64
 #include "../raytracingproject_amd/csrc/kernel/cy_integrator.h"
 #include "../raytracingproject_amd/csrc/kernel/cy_bvhw.h"
 #include "../raytracingproject_amd/csrc/host/cy_bvhw_collapse.h"
