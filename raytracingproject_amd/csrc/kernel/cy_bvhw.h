@@ -130,6 +130,18 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
   }
 }
 
+/* Slab test in FMA form (measurement switch): (lo - P) * idir as
+ * fma(lo, idir, -P * idir) with P * idir hoisted per ray, one operation per
+ * plane instead of two.  Its rounding differs from the reference's form by at
+ * most 2^-24 |P idir| (the hoisted product) plus 3 ulp of the result, so the
+ * interval is widened by 2^-21 (|P.x idir.x| + |P.y idir.y| + |P.z idir.z|)
+ * and 2^-20 relative: every box the exact test accepts is still accepted
+ * (boxes only decide which triangles are tested; the triangle test and the
+ * near-tie re-trace decide the hit). */
+#ifndef CY_SLAB_FMA
+#  define CY_SLAB_FMA 0
+#endif
+
 /* Near-tie window of the exact closest hit: hits within 2^-20 (about 8 ulps)
  * of the best distance are kept as candidates and resolved in the reference's
  * order at the end (bvhw_traverse). */
@@ -208,6 +220,10 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
 
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
   const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
+#if CY_SLAB_FMA
+  const float pix = P.x * idir.x, piy = P.y * idir.y, piz = P.z * idir.z;
+  const float ewide = (fabsf(pix) + fabsf(piy) + fabsf(piz)) * 0x1p-21f;
+#endif
   constexpr int Q = W / 4; /* float4 per array */
   int code = cur ? cur->code : root;
   if (cur) {
@@ -248,6 +264,18 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         const uint ach[4] = {ch.x, ch.y, ch.z, ch.w}, amt[4] = {mt.x, mt.y, mt.z, mt.w};
 #pragma unroll
         for (int j = 0; j < 4; j++) {
+#if CY_SLAB_FMA
+          const float clox = __builtin_fmaf(alx[j], idir.x, -pix);
+          const float chix = __builtin_fmaf(ahx[j], idir.x, -pix);
+          const float cloy = __builtin_fmaf(aly[j], idir.y, -piy);
+          const float chiy = __builtin_fmaf(ahy[j], idir.y, -piy);
+          const float cloz = __builtin_fmaf(alz[j], idir.z, -piz);
+          const float chiz = __builtin_fmaf(ahz[j], idir.z, -piz);
+          const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz)) * (1.0f - 0x1p-20f) -
+                            ewide;
+          const float cmx = (min4(t, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz)) + ewide) *
+                            (1.0f + 0x1p-20f);
+#else
           const float clox = (alx[j] - P.x) * idir.x;
           const float chix = (ahx[j] - P.x) * idir.x;
           const float cloy = (aly[j] - P.y) * idir.y;
@@ -256,6 +284,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
           const float chiz = (ahz[j] - P.z) * idir.z;
           const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz));
           const float cmx = min4(t, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
+#endif
           const bool hit = (cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility);
           const int s = 4 * q + j;
           /* leaf codes carry the primitive count: ~(first << 4 | count) */
