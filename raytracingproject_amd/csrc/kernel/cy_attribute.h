@@ -8,6 +8,9 @@
  *   primitive_surface_attribute_* (meshes) kernel/geom/geom_primitive.h:57-241
  *   svm_node_attr                          kernel/svm/svm_attribute.h:21-95
  *   svm_node_vertex_color                  kernel/svm/svm_vertex_color.h:19-36
+ *   svm_node_normal_map, svm_node_tangent  kernel/svm/svm_tex_coord.h:255-392
+ *   ensure_valid_reflection                kernel/kernel_montecarlo.h:196-298
+ *   svm_node_object_info                   kernel/svm/svm_geometry.h:104-139
  * The host packs attributes only for triangle meshes without subdivision
  * (`__tri_patch` is all ~0, so attribute_primitive_type is always
  * ATTR_PRIM_GEOMETRY); an attribute found on a curve raises
@@ -20,8 +23,13 @@
 
 enum {
   NODE_ATTR = 16,
-  NODE_VERTEX_COLOR = 17
+  NODE_VERTEX_COLOR = 17,
+  NODE_OBJECT_INFO = 48,
+  NODE_TANGENT = 70,
+  NODE_NORMAL_MAP = 71
 };
+/* AttributeStandard ids read by the kernel itself (kernel_types.h:750-779) */
+#define ATTR_STD_VERTEX_NORMAL 1u
 
 /* AttributeElement (kernel_types.h:735-748) and NodeAttributeType (svm_types.h:160-166) */
 enum {
@@ -258,26 +266,281 @@ CY_FN void svm_node_vertex_color(const CyGlobals *kg, int object, int prim, int 
   }
 }
 
-/* NODE_ATTR / NODE_VERTEX_COLOR out of line: the arrays they read in a local
- * CyGlobals, so the shading kernels' register allocation does not carry them */
+/* the shading point as the geometry-aware nodes read it */
+typedef struct CyAttrIn {
+  cfloat3 P, N, Ng, I;
+  float u, v;
+  int object, prim, type, flag, shader;
+} CyAttrIn;
+
+/* primitive_surface_attribute_float / float2 / float3 (geom_primitive.h:57-241):
+ * triangles interpolate, curves carry no packed attributes (error when one is
+ * found), anything else reads 0 */
+CY_FN void surface_attribute(const CyGlobals *kg, const CyAttrIn &in, const CyAttr &desc, int n, float f[4],
+                             uint *err)
+{
+  f[0] = f[1] = f[2] = f[3] = 0.0f;
+  if (in.type & PRIMITIVE_ALL_TRIANGLE) {
+    triangle_attribute(kg, desc, in.prim, in.u, in.v, n, f);
+  }
+  else if ((in.type & PRIMITIVE_ALL_CURVE) && desc.element != ATTR_ELEMENT_NONE) {
+    cy_set_error(err, CY_ERR_FEATURE, 11);
+  }
+}
+
+/* kernel_montecarlo.h:196-298: N tilted towards Ng just enough that the
+ * reflection of I stays above the surface */
+CY_FN cfloat3 ensure_valid_reflection(cfloat3 Ng, cfloat3 I, cfloat3 N)
+{
+  const cfloat3 R = sub3(mul3f(N, 2.0f * dot3(N, I)), I);
+  const float threshold = cmin(0.9f * dot3(Ng, I), 0.01f);
+  if (dot3(Ng, R) >= threshold) {
+    return N;
+  }
+  const float NdotNg = dot3(N, Ng);
+  const cfloat3 X = normalize3(sub3(N, mul3f(Ng, NdotNg)));
+  const float Ix = dot3(I, X), Iz = dot3(I, Ng);
+  const float Ix2 = sqr(Ix), Iz2 = sqr(Iz);
+  const float a = Ix2 + Iz2;
+  const float b = safe_sqrtf(Ix2 * (a - sqr(threshold)));
+  const float c = Iz * threshold + a;
+  const float fac = 0.5f / a;
+  const float N1_z2 = fac * (b + c), N2_z2 = fac * (-b + c);
+  bool valid1 = (N1_z2 > 1e-5f) && (N1_z2 <= (1.0f + 1e-5f));
+  bool valid2 = (N2_z2 > 1e-5f) && (N2_z2 <= (1.0f + 1e-5f));
+  float nx, nz;
+  if (valid1 && valid2) {
+    const float N1x = safe_sqrtf(1.0f - N1_z2), N1y = safe_sqrtf(N1_z2);
+    const float N2x = safe_sqrtf(1.0f - N2_z2), N2y = safe_sqrtf(N2_z2);
+    const float R1 = 2.0f * (N1x * Ix + N1y * Iz) * N1y - Iz;
+    const float R2 = 2.0f * (N2x * Ix + N2y * Iz) * N2y - Iz;
+    valid1 = (R1 >= 1e-5f);
+    valid2 = (R2 >= 1e-5f);
+    const bool first = (valid1 && valid2) ? (R1 < R2) : (R1 > R2);
+    nx = first ? N1x : N2x;
+    nz = first ? N1y : N2y;
+  }
+  else if (valid1 || valid2) {
+    const float Nz2 = valid1 ? N1_z2 : N2_z2;
+    nx = safe_sqrtf(1.0f - Nz2);
+    nz = safe_sqrtf(Nz2);
+  }
+  else {
+    return Ng;
+  }
+  return add3(mul3f(X, nx), mul3f(Ng, nz));
+}
+
+/* object_normal_transform / object_inverse_normal_transform (geom_object.h,
+ * __OBJECT_MOTION__ form: the object's static transforms) */
+CY_FN cfloat3 attr_object_normal_transform(const CyGlobals *kg, int object, cfloat3 N)
+{
+  return normalize3(transform_direction_transposed(object_itfm(kg, object), N));
+}
+CY_FN cfloat3 attr_object_inverse_normal_transform(const CyGlobals *kg, int object, cfloat3 N)
+{
+  return (object != OBJECT_NONE) ? normalize3(transform_direction_transposed(object_tfm(kg, object), N)) : N;
+}
+
+/* svm_tex_coord.h:255-345 */
+CY_FN void svm_node_normal_map(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, hc_uint4 node, uint *err)
+{
+  uint color_offset, strength_offset, normal_offset, space;
+  svm_unpack4(node.y, &color_offset, &strength_offset, &normal_offset, &space);
+  cfloat3 color = svm_load3(stack, color_offset, err);
+  color = mul3f(mk3(color.x - 0.5f, color.y - 0.5f, color.z - 0.5f), 2.0f);
+  const bool is_backfacing = (in.flag & SD_BACKFACING) != 0;
+  cfloat3 N;
+  if (space == 0) { /* NODE_NORMAL_MAP_TANGENT */
+    if (in.object == OBJECT_NONE) {
+      svm_store3(stack, normal_offset, mk3(0.0f, 0.0f, 0.0f), err);
+      return;
+    }
+    const CyAttr attr = find_attribute(kg, in.object, in.prim, node.z);
+    const CyAttr attr_sign = find_attribute(kg, in.object, in.prim, node.w);
+    const CyAttr attr_normal = find_attribute(kg, in.object, in.prim, ATTR_STD_VERTEX_NORMAL);
+    if (attr.offset == (int)ATTR_STD_NOT_FOUND || attr_sign.offset == (int)ATTR_STD_NOT_FOUND ||
+        attr_normal.offset == (int)ATTR_STD_NOT_FOUND) {
+      svm_store3(stack, normal_offset, mk3(0.0f, 0.0f, 0.0f), err);
+      return;
+    }
+    float f[4];
+    surface_attribute(kg, in, attr, 3, f, err);
+    const cfloat3 tangent = mk3(f[0], f[1], f[2]);
+    surface_attribute(kg, in, attr_sign, 1, f, err);
+    const float sign = f[0];
+    cfloat3 normal;
+    if ((uint)in.shader & SHADER_SMOOTH_NORMAL) {
+      surface_attribute(kg, in, attr_normal, 3, f, err);
+      normal = mk3(f[0], f[1], f[2]);
+    }
+    else {
+      normal = is_backfacing ? neg3(in.Ng) : in.Ng;
+      normal = attr_object_inverse_normal_transform(kg, in.object, normal);
+    }
+    const cfloat3 B = mul3f(cross3(normal, tangent), sign);
+    N = safe_normalize3(add3(add3(mul3f(tangent, color.x), mul3f(B, color.y)), mul3f(normal, color.z)));
+    N = attr_object_normal_transform(kg, in.object, N);
+  }
+  else {
+    if (space == 3 || space == 4) { /* BLENDER_OBJECT / BLENDER_WORLD */
+      color.y = -color.y;
+      color.z = -color.z;
+    }
+    N = color;
+    if (space == 1 || space == 3) { /* OBJECT / BLENDER_OBJECT */
+      if (in.object == OBJECT_NONE) {
+        cy_set_error(err, CY_ERR_SVM_NODE, 1000 + NODE_NORMAL_MAP); /* no object transform to apply */
+      }
+      else {
+        N = attr_object_normal_transform(kg, in.object, N);
+      }
+    }
+    else {
+      N = safe_normalize3(N);
+    }
+  }
+  if (is_backfacing) {
+    N = neg3(N);
+  }
+  float strength = svm_load(stack, strength_offset, err);
+  if (strength != 1.0f) {
+    strength = cmax(strength, 0.0f);
+    N = safe_normalize3(add3(in.N, mul3f(sub3(N, in.N), strength)));
+  }
+  N = ensure_valid_reflection(in.Ng, in.I, N);
+  if (is_zero3(N)) {
+    N = in.N;
+  }
+  svm_store3(stack, normal_offset, N, err);
+}
+
+/* svm_tex_coord.h:347-390 */
+CY_FN void svm_node_tangent(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, hc_uint4 node, uint *err)
+{
+  uint tangent_offset, direction_type, axis;
+  svm_unpack3(node.y, &tangent_offset, &direction_type, &axis);
+  cfloat3 tangent;
+  cfloat3 attribute_value = mk3(0.0f, 0.0f, 0.0f);
+  const CyAttr desc = find_attribute(kg, in.object, in.prim, node.z);
+  if (desc.offset != (int)ATTR_STD_NOT_FOUND) {
+    float f[4];
+    if (desc.type == NODE_ATTR_FLOAT2) {
+      surface_attribute(kg, in, desc, 2, f, err);
+      attribute_value = mk3(f[0], f[1], 0.0f);
+    }
+    else {
+      surface_attribute(kg, in, desc, 3, f, err);
+      attribute_value = mk3(f[0], f[1], f[2]);
+    }
+  }
+  if (direction_type == 1) { /* NODE_TANGENT_UVMAP */
+    tangent = (desc.offset == (int)ATTR_STD_NOT_FOUND) ? mk3(0.0f, 0.0f, 0.0f) : attribute_value;
+  }
+  else { /* radial */
+    const cfloat3 generated = (desc.offset == (int)ATTR_STD_NOT_FOUND) ? in.P : attribute_value;
+    if (axis == 0) {
+      tangent = mk3(0.0f, -(generated.z - 0.5f), (generated.y - 0.5f));
+    }
+    else if (axis == 1) {
+      tangent = mk3(-(generated.z - 0.5f), 0.0f, (generated.x - 0.5f));
+    }
+    else {
+      tangent = mk3(-(generated.y - 0.5f), (generated.x - 0.5f), 0.0f);
+    }
+  }
+  if (in.object == OBJECT_NONE) {
+    cy_set_error(err, CY_ERR_SVM_NODE, 1000 + NODE_TANGENT); /* no object transform to apply */
+  }
+  else {
+    tangent = attr_object_normal_transform(kg, in.object, tangent);
+  }
+  tangent = cross3(in.N, normalize3(cross3(tangent, in.N)));
+  svm_store3(stack, tangent_offset, tangent, err);
+}
+
+/* svm_geometry.h:104-139 (surfaces: sd->lamp is LAMP_NONE) */
+CY_FN void svm_node_object_info(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, uint type, uint out_offset,
+                                uint *err)
+{
+  const int object = in.object;
+  float data;
+  switch (type) {
+    case 0: { /* NODE_INFO_OB_LOCATION: object_location (ob_tfm translation) */
+      cfloat3 loc = mk3(0.0f, 0.0f, 0.0f);
+      if (object != OBJECT_NONE) {
+        const struct cy_tfm *t = object_tfm(kg, object);
+        loc = mk3(t->x.w, t->y.w, t->z.w);
+      }
+      svm_store3(stack, out_offset, loc, err);
+      return;
+    }
+    case 1: { /* NODE_INFO_OB_COLOR */
+      cfloat3 col = mk3(0.0f, 0.0f, 0.0f);
+      if (object != OBJECT_NONE) {
+        const hc_KernelObject &ko = kg->__objects[object];
+        col = mk3(ko.color[0], ko.color[1], ko.color[2]);
+      }
+      svm_store3(stack, out_offset, col, err);
+      return;
+    }
+    case 2: /* NODE_INFO_OB_INDEX */
+      data = (object != OBJECT_NONE) ? kg->__objects[object].pass_id : 0.0f;
+      break;
+    case 3: /* NODE_INFO_MAT_INDEX: shader_pass_id */
+      data = (float)kg->__shaders[(uint)in.shader & SHADER_MASK].pass_id;
+      break;
+    case 4: /* NODE_INFO_OB_RANDOM */
+      data = (object != OBJECT_NONE) ? kg->__objects[object].random_number : 0.0f;
+      break;
+    default:
+      data = 0.0f;
+      break;
+  }
+  svm_store(stack, out_offset, data, err);
+}
+
+/* svm_geometry.h NODE_GEOM_T: primitive_tangent (geom_primitive.h:292-320),
+ * the spherical tangent of the generated coordinates around Z; the surface
+ * derivative fallback (sd->dPdu) and curves are not carried */
+CY_FN void svm_node_geometry_tangent(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, uint out_offset,
+                                     uint *err)
+{
+  cfloat3 T = mk3(0.0f, 0.0f, 0.0f);
+  const CyAttr desc = (in.type & PRIMITIVE_ALL_CURVE) ? attribute_not_found() :
+                                                        find_attribute(kg, in.object, in.prim, 7u /* GENERATED */);
+  if (desc.offset != (int)ATTR_STD_NOT_FOUND) {
+    float f[4];
+    surface_attribute(kg, in, desc, 3, f, err);
+    cfloat3 data = mk3(-(f[1] - 0.5f), (f[0] - 0.5f), 0.0f);
+    data = attr_object_normal_transform(kg, in.object, data);
+    T = cross3(in.N, normalize3(cross3(data, in.N)));
+  }
+  else {
+    cy_set_error(err, CY_ERR_SVM_NODE, 2000 + 2); /* tangent from surface derivatives (sd->dPdu) */
+  }
+  svm_store3(stack, out_offset, T, err);
+}
+
+/* NODE_ATTR / NODE_VERTEX_COLOR / NODE_NORMAL_MAP / NODE_TANGENT /
+ * NODE_OBJECT_INFO out of line: the arrays they read in a local CyGlobals, so
+ * the shading kernels' register allocation does not carry them */
 CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
+                                         const hc_KernelShader *shaders,
                                          const hc_uint4 *attributes_map,
                                          const float *attributes_float,
                                          const hc_float2 *attributes_float2,
                                          const hc_float4 *attributes_float3,
                                          const uint32_t *attributes_uchar4,
                                          const hc_uint4 *tri_vindex,
-                                         int object,
-                                         int prim,
-                                         int type,
-                                         float u,
-                                         float v,
+                                         CyAttrIn in,
                                          CySvmStack stack,
                                          hc_uint4 node,
                                          uint *err)
 {
   CyGlobals kgv;
   kgv.__objects = objects;
+  kgv.__shaders = shaders;
   kgv.__attributes_map = attributes_map;
   kgv.__attributes_float = attributes_float;
   kgv.__attributes_float2 = attributes_float2;
@@ -285,11 +548,25 @@ CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
   kgv.__attributes_uchar4 = attributes_uchar4;
   kgv.__tri_vindex = tri_vindex;
   const CyGlobals *kg = &kgv;
-  if (node.x == NODE_ATTR) {
-    svm_node_attr(kg, object, prim, type, u, v, stack, node, err);
-  }
-  else {
-    svm_node_vertex_color(kg, object, prim, type, u, v, stack, node.y, node.z, node.w, err);
+  switch (node.x) {
+    case NODE_ATTR:
+      svm_node_attr(kg, in.object, in.prim, in.type, in.u, in.v, stack, node, err);
+      break;
+    case NODE_VERTEX_COLOR:
+      svm_node_vertex_color(kg, in.object, in.prim, in.type, in.u, in.v, stack, node.y, node.z, node.w, err);
+      break;
+    case NODE_NORMAL_MAP:
+      svm_node_normal_map(kg, in, stack, node, err);
+      break;
+    case NODE_TANGENT:
+      svm_node_tangent(kg, in, stack, node, err);
+      break;
+    case NODE_OBJECT_INFO:
+      svm_node_object_info(kg, in, stack, node.y, node.z, err);
+      break;
+    case NODE_GEOMETRY: /* NODE_GEOM_T only */
+      svm_node_geometry_tangent(kg, in, stack, node.z, err);
+      break;
   }
 }
 

@@ -2226,8 +2226,9 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         else {
           f = fabsf(dot3(sd->I, normal_in));
           if (blend != 0.5f) {
-            /* powf path: not bit-exact vs libm; reject */
-            cy_set_error(err, CY_ERR_SVM_NODE, 1000 + NODE_LAYER_WEIGHT);
+            blend = cclamp(blend, 0.0f, 1.0f - 1e-5f);
+            blend = (blend < 0.5f) ? 2.0f * blend : 0.5f / (1.0f - blend);
+            f = cy_powf(f, blend); /* glibc powf, restated (cy_math.h) */
           }
           f = 1.0f - f;
         }
@@ -2287,10 +2288,23 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         return;
 #else
       {
-        if (node.x == NODE_ATTR || node.x == NODE_VERTEX_COLOR) {
-          svm_eval_attribute_node(kg->__objects, kg->__attributes_map, kg->__attributes_float,
+        if (node.x == NODE_ATTR || node.x == NODE_VERTEX_COLOR || node.x == NODE_NORMAL_MAP ||
+            node.x == NODE_TANGENT || node.x == NODE_OBJECT_INFO || (node.x == NODE_GEOMETRY && node.y == 2u)) {
+          CyAttrIn ain;
+          ain.P = sd->P;
+          ain.N = sd->N;
+          ain.Ng = sd->Ng;
+          ain.I = sd->I;
+          ain.u = sd->u;
+          ain.v = sd->v;
+          ain.object = sd->object;
+          ain.prim = sd->prim;
+          ain.type = sd->type;
+          ain.flag = sd->flag;
+          ain.shader = sd->shader;
+          svm_eval_attribute_node(kg->__objects, kg->__shaders, kg->__attributes_map, kg->__attributes_float,
                                   kg->__attributes_float2, kg->__attributes_float3, kg->__attributes_uchar4,
-                                  kg->__tri_vindex, sd->object, sd->prim, sd->type, sd->u, sd->v, stack, node, err);
+                                  kg->__tri_vindex, ain, stack, node, err);
           break;
         }
         CySvmTexIn in;

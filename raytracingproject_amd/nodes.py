@@ -60,12 +60,21 @@ NODE_COMBINE_HSV = 77
 NODE_MAP_RANGE = 83
 NODE_CLAMP = 84
 NODE_ATTR, NODE_VERTEX_COLOR = 16, 17
+NODE_OBJECT_INFO, NODE_TANGENT, NODE_NORMAL_MAP = 48, 70, 71
+NODE_FRESNEL, NODE_LAYER_WEIGHT = 38, 39
+NORMAL_MAP_SPACES = {"tangent": 0, "object": 1, "world": 2, "blender_object": 3, "blender_world": 4}
+TANGENT_DIRECTIONS = {"radial": 0, "uv_map": 1}
+TANGENT_AXES = {"x": 0, "y": 1, "z": 2}
+OBJECT_INFO_OUTPUTS = {"Location": ("vector", 0), "Color": ("color", 1), "Object Index": ("float", 2),
+                       "Material Index": ("float", 3), "Random": ("float", 4)}
 # NodeAttributeType (svm_types.h:160-166)
 NODE_ATTR_FLOAT, NODE_ATTR_FLOAT2, NODE_ATTR_FLOAT3, NODE_ATTR_RGBA = 0, 1, 2, 3
 # AttributeStandard (kernel_types.h:750-779) of the attributes this host packs;
 # Attribute::standard_name (render/attribute.cpp:279-330) for the name lookup
 ATTR_STD_UV, ATTR_STD_VERTEX_COLOR, ATTR_STD_GENERATED, ATTR_STD_NUM = 3, 6, 7, 26
-ATTR_STD_NAMES = {"uv": ATTR_STD_UV, "vertex_color": ATTR_STD_VERTEX_COLOR, "generated": ATTR_STD_GENERATED}
+ATTR_STD_VERTEX_NORMAL, ATTR_STD_UV_TANGENT, ATTR_STD_UV_TANGENT_SIGN = 1, 4, 5
+ATTR_STD_NAMES = {"uv": ATTR_STD_UV, "vertex_color": ATTR_STD_VERTEX_COLOR, "generated": ATTR_STD_GENERATED,
+                  "N": ATTR_STD_VERTEX_NORMAL, "tangent": ATTR_STD_UV_TANGENT, "tangent_sign": ATTR_STD_UV_TANGENT_SIGN}
 
 # svm_types.h enums (the names are the Blender UI's, lower-cased)
 MATH_OPS = ["add", "subtract", "multiply", "divide", "sine", "cosine", "tangent", "arcsine", "arccosine",
@@ -85,7 +94,7 @@ MIX_TYPES = ["mix", "add", "multiply", "subtract", "screen", "divide", "differen
 NODE_MIX_CLAMP = 18
 GRADIENT_TYPES = ["linear", "quadratic", "easing", "diagonal", "radial", "quadratic_sphere", "spherical"]
 TEXCO_OUTPUTS = {"Normal": 0, "Object": 1, "Camera": 2, "Window": 3, "Reflection": 4}
-GEOMETRY_OUTPUTS = {"Position": 0, "Normal": 1, "Incoming": 3, "True Normal": 4, "Parametric": 5}
+GEOMETRY_OUTPUTS = {"Position": 0, "Normal": 1, "Tangent": 2, "Incoming": 3, "True Normal": 4, "Parametric": 5}
 LIGHT_PATH_OUTPUTS = ["Is Camera Ray", "Is Shadow Ray", "Is Diffuse Ray", "Is Glossy Ray", "Is Singular Ray",
                       "Is Reflection Ray", "Is Transmission Ray", "Is Volume Scatter Ray", "Is Backfacing",
                       "Ray Length", "Ray Depth", "Diffuse Depth", "Glossy Depth", "Transparent Depth",
@@ -161,6 +170,41 @@ def vertex_color(layer: str = "") -> Node:
     """Vertex Color node (nodes.cpp:4532-4568): a byte-colour corner attribute
     (the active layer when `layer` is empty) as Color and Alpha."""
     return Node("vertex_color", params={"layer": str(layer)})
+
+
+def normal_map(color=(0.5, 0.5, 1.0), strength=1.0, space: str = "tangent", uv_map: str = "") -> Socket:
+    """Normal Map node (nodes.cpp:6717-6761, svm_tex_coord.h:255-345): a
+    tangent-space map reads the UV tangent, its sign and the vertex normal
+    (attributes `uv_map`.tangent / .tangent_sign, or the standard ones when
+    `uv_map` is empty); object / world spaces transform the colour directly."""
+    if space not in NORMAL_MAP_SPACES:
+        raise ValueError(f"normal_map space one of {sorted(NORMAL_MAP_SPACES)}")
+    return Node("normal_map", {"Color": color, "Strength": strength}, {"space": space, "uv_map": uv_map})["Normal"]
+
+
+def tangent(direction: str = "radial", axis: str = "z", uv_map: str = "") -> Socket:
+    """Tangent node (nodes.cpp:6813-6847, svm_tex_coord.h:347-390): radial
+    around an axis of the generated coordinates, or the UV map's tangent."""
+    if direction not in TANGENT_DIRECTIONS or axis not in TANGENT_AXES:
+        raise ValueError("tangent: direction radial | uv_map, axis x | y | z")
+    return Node("tangent", params={"direction": direction, "axis": axis, "uv_map": uv_map})["Tangent"]
+
+
+def fresnel(ior=1.45, normal=None) -> Socket:
+    """Fresnel node (nodes.cpp FresnelNode, svm_fresnel.h:21-38): Fac."""
+    return Node("fresnel", {"IOR": ior, "Normal": normal})["Fac"]
+
+
+def layer_weight(blend=0.5, normal=None) -> Node:
+    """Layer Weight node (nodes.cpp LayerWeightNode, svm_fresnel.h:40-75):
+    Fresnel and Facing (blend != 0.5 bends Facing through powf)."""
+    return Node("layer_weight", {"Blend": blend, "Normal": normal})
+
+
+def object_info() -> Node:
+    """Object Info node (nodes.cpp:4211-4237, svm_geometry.h:104-139): Location,
+    Color, Object Index, Material Index, Random."""
+    return Node("object_info")
 
 
 def _default_vector(vector, kind: str = "generated"):
@@ -442,6 +486,16 @@ def _outputs(node: Node) -> dict:
         return {"Color": "color", "Vector": "vector", "Fac": "float"}
     if k == "vertex_color":
         return {"Color": "color", "Alpha": "float"}
+    if k == "normal_map":
+        return {"Normal": "vector"}
+    if k == "fresnel":
+        return {"Fac": "float"}
+    if k == "layer_weight":
+        return {"Fresnel": "float", "Facing": "float"}
+    if k == "tangent":
+        return {"Tangent": "vector"}
+    if k == "object_info":
+        return {n: t for n, (t, _) in OBJECT_INFO_OUTPUTS.items()}
     if k == "geometry":
         return {n: "vector" for n in GEOMETRY_OUTPUTS}
     if k == "light_path":
@@ -513,6 +567,9 @@ _INPUT_TYPES = {
     "image_texture": {"Vector": "vector"},
     "environment_texture": {"Vector": "vector"},
     "displacement": {"Height": "float", "Midlevel": "float", "Scale": "float", "Normal": "vector"},
+    "normal_map": {"Color": "color", "Strength": "float"},
+    "fresnel": {"IOR": "float", "Normal": "vector"},
+    "layer_weight": {"Blend": "float", "Normal": "vector"},
     "vector_displacement": {"Vector": "color", "Midlevel": "float", "Scale": "float"},
 }
 
@@ -524,7 +581,7 @@ def _width(t: str) -> int:
 # ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
 # the shading point or direction (texture coordinate, geometry, textures)
 SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture",
-                 "attribute", "vertex_color")
+                 "attribute", "vertex_color", "normal_map", "tangent", "object_info")
 
 
 def has_spatial_varying(values) -> bool:
@@ -716,6 +773,46 @@ class NodeCompiler:
         if (id(n), "Fac") in self.used:
             self.emit((NODE_ATTR, attr, self.out(n, "Fac"), NODE_ATTR_FLOAT))
 
+    def _n_normal_map(self, n):  # nodes.cpp:6717-6761 NormalMapNode::attributes / compile
+        space = NORMAL_MAP_SPACES[n.params["space"]]
+        attr = attr_sign = 0
+        if space == 0 and not self.volume:
+            uvm = n.params["uv_map"]
+            attr = self.attribute(f"{uvm}.tangent" if uvm else ATTR_STD_UV_TANGENT)
+            attr_sign = self.attribute(f"{uvm}.tangent_sign" if uvm else ATTR_STD_UV_TANGENT_SIGN)
+            self.attribute(ATTR_STD_VERTEX_NORMAL)  # requested by attributes(), looked up by id
+        col, strength = self.inp(n, "Color"), self.inp(n, "Strength")
+        out = self.out(n, "Normal")
+        self.emit((NODE_NORMAL_MAP, uchar4(col, strength, out, space), attr, attr_sign))
+
+    def _n_tangent(self, n):  # nodes.cpp:6813-6847 TangentNode::attributes / compile
+        uvm = n.params["uv_map"]
+        if n.params["direction"] == "uv_map":
+            attr = self.attribute(f"{uvm}.tangent" if uvm else ATTR_STD_UV_TANGENT)
+        else:
+            attr = self.attribute(ATTR_STD_GENERATED)
+        self.emit((NODE_TANGENT, uchar4(self.out(n, "Tangent"), TANGENT_DIRECTIONS[n.params["direction"]],
+                                        TANGENT_AXES[n.params["axis"]]), attr, 0))
+
+    def _n_fresnel(self, n):  # nodes.cpp FresnelNode::compile
+        ior = self.assign_if_linked(n.inputs["IOR"], "float")
+        nrm = self.assign_if_linked(n.inputs["Normal"], "vector")
+        val = 0.0 if is_linked(n.inputs["IOR"]) else float(n.inputs["IOR"])
+        self.emit((NODE_FRESNEL, ior, f32bits(val), uchar4(nrm, self.out(n, "Fac"))))
+
+    def _n_layer_weight(self, n):  # nodes.cpp LayerWeightNode::compile
+        blend = self.assign_if_linked(n.inputs["Blend"], "float")
+        nrm = self.assign_if_linked(n.inputs["Normal"], "vector")
+        val = 0.0 if is_linked(n.inputs["Blend"]) else float(n.inputs["Blend"])
+        for t, name in enumerate(("Fresnel", "Facing")):
+            if (id(n), name) in self.used:
+                self.emit((NODE_LAYER_WEIGHT, blend, f32bits(val), uchar4(t, nrm, self.out(n, name))))
+
+    def _n_object_info(self, n):  # nodes.cpp:4211-4237 ObjectInfoNode::compile
+        for name, (_, t) in OBJECT_INFO_OUTPUTS.items():
+            if (id(n), name) in self.used:
+                self.emit((NODE_OBJECT_INFO, t, self.out(n, name), 0))
+
     def _n_vertex_color(self, n):  # nodes.cpp:4543-4568 VertexColorNode::compile
         layer = n.params["layer"]
         attr = self.attribute(ATTR_STD_NAMES.get(layer, layer) if layer else ATTR_STD_VERTEX_COLOR)
@@ -730,7 +827,9 @@ class NodeCompiler:
             offs.append(off)
         self.emit((NODE_VERTEX_COLOR, attr, offs[0], offs[1]))
 
-    def _n_geometry(self, n):  # nodes.cpp GeometryNode::compile
+    def _n_geometry(self, n):  # nodes.cpp GeometryNode::attributes / compile
+        if (id(n), "Tangent") in self.used and not self.background:
+            self.attribute(ATTR_STD_GENERATED)  # primitive_tangent reads the generated coordinates
         for name, t in GEOMETRY_OUTPUTS.items():
             if (id(n), name) in self.used:
                 self.emit((NODE_GEOMETRY, t, self.out(n, name), 0))

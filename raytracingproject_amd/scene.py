@@ -163,6 +163,7 @@ class Closure:
     # material output "Volume": a tree of volume closures (volume_absorption,
     # volume_scatter, principled_volume, emission, mix), its own SVM program
     volume: "Closure | None" = None
+    pass_index: int = 0  # Material pass index (KernelShader.pass_id, Object Info "Material Index")
     density: object = 1.0  # volume closures
 
     def closure_type(self) -> int:
@@ -267,10 +268,12 @@ def glossy(color, roughness, normal=None, distribution="ggx"):
     return Closure("glossy", _const_or_socket(color), roughness=roughness, normal=normal, distribution=distribution)
 
 
-def anisotropic(color, roughness, anisotropy, rotation, tangent, normal=None, distribution="ggx"):
-    """Anisotropic BSDF (nodes.cpp AnisotropicBsdfNode).  The tangent must be
-    a linked vector socket: the reference's default link (a generated-
-    coordinate TangentNode) needs mesh attributes this host does not emit."""
+def anisotropic(color, roughness, anisotropy, rotation, tangent=None, normal=None, distribution="ggx"):
+    """Anisotropic BSDF (nodes.cpp AnisotropicBsdfNode).  An unset tangent is
+    the reference's default link (graph.cpp:885-889): the Geometry node's
+    Tangent, the radial tangent of the generated coordinates."""
+    if tangent is None:
+        tangent = nodes.geometry()["Tangent"]
     if not nodes.is_linked(tangent):
         raise ValueError("anisotropic BSDF: link the tangent input to a vector socket")
     return Closure("anisotropic", _const_or_socket(color), roughness=roughness, anisotropy=anisotropy,
@@ -306,6 +309,10 @@ def principled(distribution="ggx", subsurface_method="burley", **params):
     p.update(params)
     if subsurface_method not in PRINCIPLED_SUBSURFACE_METHODS:
         raise ValueError(f"principled: unknown subsurface_method {subsurface_method}")
+    if "tangent" not in params and (_nodes.is_linked(p["anisotropic"]) or float(p["anisotropic"]) != 0.0):
+        # graph.cpp:885-889 default link of the Tangent input (only read when
+        # the roughness is anisotropic)
+        p["tangent"] = _nodes.geometry()["Tangent"]
     if distribution not in PRINCIPLED_DISTRIBUTIONS:
         raise ValueError(f"principled: distribution one of {sorted(PRINCIPLED_DISTRIBUTIONS)}")
     if distribution == "multiscatter" and (_nodes.is_linked(p["transmission"]) or float(p["transmission"]) > 0.0):
@@ -700,6 +707,11 @@ class Mesh:
     # name -> (element, data): element "vertex" (V rows), "face" (T rows) or
     # "corner" (3T rows), data (N,) float, (N, 2) float2 or (N, 3) float3
     attributes: dict | None = None
+    # object properties (render/object.h Object: color, pass_id, random_id;
+    # Object Info node); unset ones pack as 0
+    object_color: tuple | None = None
+    pass_index: int = 0
+    object_random: float | None = None  # Object::random_id / 0xFFFFFFFF
 
 
 @dataclass
@@ -726,6 +738,9 @@ class Instance:
 
     mesh: Mesh
     tfm: np.ndarray  # (3, 4) object to world
+    object_color: tuple | None = None  # None: the mesh's
+    pass_index: int | None = None
+    object_random: float | None = None
 
 
 @dataclass
@@ -1127,6 +1142,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
             if _volume_attribute_dependency(m.volume):
                 flag |= SD_NEED_VOLUME_ATTRIBUTES
         kshaders[i].flags = flag
+        kshaders[i].pass_id = int(getattr(m, "pass_index", 0))
     tri_shader = tri_shader_idx.astype(np.uint32) | np.uint32(SHADER_CAST_SHADOW | SHADER_AREA_LIGHT)
     tri_shader = np.where(tri_smooth, tri_shader | np.uint32(SHADER_SMOOTH_NORMAL), tri_shader).astype(np.uint32)
 
@@ -1140,6 +1156,12 @@ def compile_scene(scene: Scene) -> DeviceScene:
         abi.set_transform(kobjects[i].tfm, tfm)
         abi.set_transform(kobjects[i].itfm, np.linalg.inv(np.vstack([tfm, [0, 0, 0, 1]]))[:3])
         kobjects[i].shadow_terminator_offset = 1.0  # 1 / (1 - 0.5 * 0)
+        # object.cpp:454-461: color, pass_id, random_number
+        if ob.get("color") is not None:
+            kobjects[i].color[:] = [float(c) for c in ob["color"]]
+        kobjects[i].pass_id = float(ob.get("pass_index") or 0)
+        if ob.get("random") is not None:
+            kobjects[i].random_number = float(ob["random"])
         kobjects[i].numverts = ob["numverts"]
         kobjects[i].numkeys = ob.get("numkeys", 0)
         if ob["applied"]:
@@ -1515,6 +1537,17 @@ def _mesh_attribute(gm: dict, key):
         return "corner", "float2", np.asarray(m.uv, dtype=np.float32).reshape(3 * T, 2)
     if key == _nodes_mod.ATTR_STD_GENERATED:
         return "vertex", "float3", _generated_coordinates(m)
+    if key == _nodes_mod.ATTR_STD_VERTEX_NORMAL or key == "N":
+        # Mesh::add_vertex_normals: the normals __tri_vnormal holds
+        return "vertex", "float3", np.asarray(gm["nrm"], dtype=np.float32)
+    if key in (_nodes_mod.ATTR_STD_UV_TANGENT, _nodes_mod.ATTR_STD_UV_TANGENT_SIGN, "UVMap.tangent",
+               "UVMap.tangent_sign"):
+        if m.uv is None:
+            return None
+        tan, sign = _uv_tangents(gm, np.asarray(m.uv, dtype=np.float32).reshape(T, 3, 2))
+        if key in (_nodes_mod.ATTR_STD_UV_TANGENT, "UVMap.tangent"):
+            return "corner", "float3", tan
+        return "corner", "float", sign
     colors = dict(m.vertex_colors or {})
     if key == _nodes_mod.ATTR_STD_VERTEX_COLOR:
         if not colors:
@@ -1539,6 +1572,28 @@ def _mesh_attribute(gm: dict, key):
     if kind is None:
         raise ValueError(f"attribute {key!r}: rows of 1, 2 or 3 floats")
     return element, kind, a
+
+
+def _uv_tangents(gm: dict, uv: np.ndarray):
+    """Per-corner UV tangents and their bitangent sign (the data Blender's
+    mikktspace pass stores as ATTR_STD_UV_TANGENT / _SIGN, mesh_tangents in
+    blender/blender_mesh.cpp): the triangle's dP/du, orthogonalised against
+    each corner's vertex normal; sign +1 or -1 from the dP/dv handedness."""
+    f32 = np.float32
+    v, t, nrm = gm["v"].astype(np.float64), gm["t"], gm["nrm"].astype(np.float64)
+    p = v[t]  # (T, 3, 3)
+    e1, e2 = p[:, 1] - p[:, 0], p[:, 2] - p[:, 0]
+    d1, d2 = (uv[:, 1] - uv[:, 0]).astype(np.float64), (uv[:, 2] - uv[:, 0]).astype(np.float64)
+    det = d1[:, 0] * d2[:, 1] - d2[:, 0] * d1[:, 1]
+    r = np.where(np.abs(det) > 1e-12, 1.0 / np.where(det == 0, 1.0, det), 0.0)[:, None]
+    dpdu = (e1 * d2[:, 1:2] - e2 * d1[:, 1:2]) * r
+    dpdv = (e2 * d1[:, 0:1] - e1 * d2[:, 0:1]) * r
+    n = nrm[t]  # (T, 3, 3)
+    tc = dpdu[:, None, :] - n * np.sum(n * dpdu[:, None, :], axis=2, keepdims=True)
+    ln = np.linalg.norm(tc, axis=2, keepdims=True)
+    tc = np.where(ln > 1e-12, tc / np.where(ln == 0, 1.0, ln), np.array([1.0, 0.0, 0.0]))
+    sign = np.where(np.sum(np.cross(n, tc) * dpdv[:, None, :], axis=2) < 0.0, -1.0, 1.0)
+    return tc.reshape(-1, 3).astype(f32), sign.reshape(-1).astype(f32)
 
 
 def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobjects) -> dict:
@@ -1659,6 +1714,15 @@ def _mesh_arrays(m: Mesh, tfm=None):
     return v, t, sh, nrm
 
 
+def _instance_props(inst) -> dict:
+    def pick(a, b):
+        return a if a is not None else b
+
+    return dict(color=pick(inst.object_color, inst.mesh.object_color),
+                pass_index=pick(inst.pass_index, inst.mesh.pass_index),
+                random=pick(inst.object_random, inst.mesh.object_random))
+
+
 def _pack_geometry(scene: Scene) -> dict:
     """Geometry, objects and the packed BVH of a scene: the device arrays of
     GeometryManager::device_update_mesh (render/geometry.cpp:873-960) and
@@ -1673,19 +1737,21 @@ def _pack_geometry(scene: Scene) -> dict:
     for m in scene.meshes:
         v, t, sh, nrm = _mesh_arrays(m)
         geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(m.smooth), applied=True, mesh=m))
-        objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True))
+        objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True, color=m.object_color,
+                            pass_index=m.pass_index, random=m.object_random))
     for inst in scene.instances:
         tfm = np.asarray(inst.tfm, dtype=np.float64).reshape(3, 4)
         if users[id(inst.mesh)] == 1:
             v, t, sh, nrm = _mesh_arrays(inst.mesh, tfm.astype(np.float32))
             geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True, mesh=inst.mesh))
-            objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True))  # tfm reset on apply
+            objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True,  # tfm reset on apply
+                                **_instance_props(inst)))
             continue
         if id(inst.mesh) not in geom_of:
             v, t, sh, nrm = _mesh_arrays(inst.mesh)
             geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=False, mesh=inst.mesh))
             geom_of[id(inst.mesh)] = len(geoms) - 1
-        objects.append(dict(geom=geom_of[id(inst.mesh)], tfm=tfm, applied=False))
+        objects.append(dict(geom=geom_of[id(inst.mesh)], tfm=tfm, applied=False, **_instance_props(inst)))
     # hair objects: transforms applied, after the meshes (object order)
     for hr in scene.hairs:
         objects.append(dict(geom=None, hair=hr, tfm=ident, applied=True))

@@ -996,7 +996,7 @@ def shading_coords(width=64, height=64, samples=8) -> sc.Scene:
     for name in nd.TEXCO_OUTPUTS:
         colors.append(show(tc[name]))
     g = nd.geometry()
-    for name in nd.GEOMETRY_OUTPUTS:
+    for name in ("Position", "Normal", "Incoming", "True Normal", "Parametric"):
         colors.append(show(g[name]))
     P = tc["Object"]
     colors.append(nd.checker(P, (0.9, 0.2, 0.1), (0.1, 0.3, 0.9), 3.0)["Color"])
@@ -1355,3 +1355,69 @@ def closures_layered(width=48, height=48, samples=8, triple=False) -> sc.Scene:
     ]
     return _closure_gallery(width, height, samples, "closures_layered_triple" if triple else "closures_layered",
                             mats)
+
+
+def shading_normals(width=48, height=48, samples=8) -> sc.Scene:
+    """Normal perturbation and object data (svm_tex_coord.h:255-390,
+    kernel_montecarlo.h ensure_valid_reflection, svm_geometry.h): tangent-space
+    normal maps (UV tangents, their sign and the vertex normals, smooth and
+    flat shading, strength above and below one), object / world / Blender
+    object-space maps, the Tangent node (radial about each axis, UV map) and
+    the Geometry node's Tangent feeding anisotropic BSDFs, Object Info (location,
+    colour, pass index, random, material index) and an instanced, rotated mesh
+    whose maps go through its object transform."""
+    from . import nodes as nd
+
+    def bumpy(seed):
+        n = nd.noise_texture(scale=3.0 + seed, detail=1.0)["Color"]
+        return nd.mix_rgb("mix", 0.6, (0.5, 0.5, 1.0), n)
+
+    oi = nd.object_info()
+    mats = [
+        sc.diffuse((0.7, 0.6, 0.5), normal=nd.normal_map(bumpy(0))),
+        sc.glossy((0.8, 0.8, 0.8), 0.3, normal=nd.normal_map(bumpy(1), strength=0.5)),
+        sc.diffuse((0.5, 0.7, 0.6), normal=nd.normal_map(bumpy(2), strength=2.5)),
+        sc.diffuse((0.6, 0.5, 0.7), normal=nd.normal_map(bumpy(3), space="object")),
+        sc.glossy((0.7, 0.7, 0.6), 0.2, normal=nd.normal_map(bumpy(4), space="world")),
+        sc.diffuse((0.6, 0.6, 0.6), normal=nd.normal_map(bumpy(5), space="blender_object", strength=0.8)),
+        sc.anisotropic((0.9, 0.7, 0.5), 0.4, 0.7, 0.0, nd.tangent("radial", "x")),
+        sc.anisotropic((0.5, 0.7, 0.9), 0.4, -0.6, 0.1, nd.tangent("radial", "y")),
+        sc.anisotropic((0.7, 0.9, 0.5), 0.3, 0.5, 0.0, nd.tangent("uv_map")),
+        sc.anisotropic((0.8, 0.8, 0.5), 0.35, 0.8, 0.0),  # default: geometry Tangent (radial z)
+        sc.principled(base_color=(0.9, 0.6, 0.3), metallic=1.0, roughness=0.4, anisotropic=0.7),
+        sc.diffuse(nd.combine_xyz(oi["Random"], nd.math("multiply", oi["Object Index"], 0.1),
+                                  nd.math("multiply", oi["Material Index"], 0.2))),
+        sc.diffuse(nd.mix_rgb("mix", 0.5, oi["Color"], nd.vector_math("fraction", oi["Location"])["Vector"])),
+        # Fresnel / Layer Weight (svm_fresnel.h), facing bent through powf
+        sc.mix(nd.layer_weight(0.3)["Facing"], sc.diffuse((0.2, 0.3, 0.8)), sc.glossy((0.9, 0.9, 0.9), 0.2)),
+        sc.mix(nd.layer_weight(0.85, normal=nd.normal_map(bumpy(8)))["Facing"], sc.diffuse((0.8, 0.3, 0.2)),
+               sc.glossy((0.9, 0.9, 0.9), 0.3)),
+        sc.mix(nd.fresnel(nd.math("add", 1.2, nd.separate_xyz(nd.geometry()["Parametric"])["X"])),
+               sc.diffuse((0.3, 0.7, 0.3)), sc.glossy((0.9, 0.9, 0.9), 0.1)),
+        sc.mix(nd.layer_weight(0.4)["Fresnel"], sc.diffuse((0.6, 0.6, 0.2)), sc.glossy((0.8, 0.8, 0.9), 0.25)),
+    ]
+    s = _grid_scene([(0.5, 0.5, 0.5)] * len(mats), width, height, samples, "shading_normals")
+    rng = np.random.default_rng(5)
+    for i, m in enumerate(mats):
+        s.materials[i] = m
+        mesh = s.meshes[i]
+        nt = len(mesh.tris)
+        mesh.uv = rng.uniform(-0.3, 1.4, (nt, 3, 2)).astype(np.float32)
+        mesh.smooth = (i % 2 == 0)
+        mesh.object_color = tuple(float(x) for x in rng.uniform(0.0, 1.0, 3))
+        mesh.pass_index = i
+        mesh.object_random = float(np.float32(rng.uniform(0.0, 1.0)))
+    s.materials[11].pass_index = 3
+    s.materials[12].pass_index = 5
+    # a sphere shared by two rotated objects: object-space maps and tangents
+    # go through each object's transform
+    sv, st = _ellipsoid((0.0, 0.0, 0.0), (0.45, 0.45, 0.45), 16, 10)
+    n = len(s.materials)
+    s.materials.append(sc.glossy((0.8, 0.7, 0.6), 0.35, normal=nd.normal_map(bumpy(6), strength=1.5)))
+    s.materials.append(sc.diffuse((0.6, 0.7, 0.8), normal=nd.normal_map(bumpy(7), space="object")))
+    ball = sc.Mesh(sv, st, shader=np.array([n + (k % 2) for k in range(len(st))]), smooth=True)
+    ball.uv = rng.uniform(0.0, 1.0, (len(st), 3, 2)).astype(np.float32)
+    ball.object_color = (0.9, 0.2, 0.3)
+    s.instances = [sc.Instance(ball, _tfm((-1.5, 1.2, -0.7), rot_y=0.7, rot_x=0.4), pass_index=7, object_random=0.3),
+                   sc.Instance(ball, _tfm((1.4, -1.1, -0.6), rot_y=-1.1, scale=(1.2, 0.8, 1.0)))]
+    return s

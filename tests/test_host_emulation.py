@@ -27,7 +27,7 @@ def test_device_logic_bit_exact_vs_reference(emu, name):
 
 
 @pytest.mark.parametrize("name", ["cornell_64", "closures_diffuse", "closures_microfacet", "closures_principled",
-                                  "shading_image", "shading_noise", "shading_voronoi", "shading_attributes", "closures_multiscatter",
+                                  "shading_image", "shading_noise", "shading_voronoi", "shading_attributes", "shading_normals", "closures_multiscatter",
                                   "volume_cornell"])
 def test_device_sincos_restatement_matches_on_host(name):
     """Same render with the device's own libm restatements (sinf/cosf, expf,
