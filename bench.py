@@ -63,6 +63,9 @@ def parse(argv=None):
                    help="tiles rendered per device pass in the tile-mode leg (0: all tiles of the frame)")
     p.add_argument("--profile-frame", action="store_true",
                    help="only render the instrumented single-lane frame (for rocprofv3 PMC passes)")
+    p.add_argument("--other-configs", default="barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
+                   help="BASELINE.json's other configs, one frame each after the headline measurement (rank 0, "
+                        "N=1): name or name@XxY+WxH for a full-spp crop; empty disables")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank); gloo rehearses N ranks on fewer GPUs")
     return p.parse_args(argv)
@@ -235,6 +238,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ds, args.cpu_seconds)
 
+    others = None
+    if rank == 0 and world == 1 and args.other_configs:
+        del local
+        dev.close()
+        local, dev = None, None
+        others = [other_config(spec, device_index, args) for spec in args.other_configs.split(",") if spec]
+
     if args.save and rank == 0:
         from raytracingproject_amd import imageio
 
@@ -272,11 +282,13 @@ def main():
             "film_checksum": float(np.float64(film[..., :4].sum())) if film is not None else None,
             "roofline": roofline,
             "tile_mode": tile_leg,
+            "other_configs": others,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     del local
-    dev.close()
+    if dev is not None:
+        dev.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -393,6 +405,60 @@ def tile_mode(dev, ds, tile, batch):
     dt = time.perf_counter() - t0
     return {"tile": tile, "tiles": len(tiles), "tiles_per_pass": batch,
             "value": round(W * H * S / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(1e3 * dt, 3)}
+
+
+def other_config(spec, device_index, args):
+    """One frame of another BASELINE.json config (its procedural stand-in,
+    SURVEY.md §8(d)) on this GPU: `name` renders the whole frame at its full
+    sample count, `name@XxY+WxH` the crop (x, y, w, h) at the full sample
+    count (configs whose frame takes minutes).  A 1-sample frame first sizes
+    the device; then one timed frame.  Failures are reported, not raised."""
+    import torch
+
+    from raytracingproject_amd import scene as sc
+    from raytracingproject_amd import scenes
+    from raytracingproject_amd.device import HIPDevice
+
+    name, _, region = spec.partition("@")
+    res = {"config": name}
+    dev = None
+    try:
+        t0 = time.time()
+        ds = sc.compile_scene(scenes.CONFIGS[name]())
+        res["scene_compile_s"] = round(time.time() - t0, 2)
+        W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
+        x, y, w, h = 0, 0, W, H
+        if region:
+            pos, _, size = region.partition("+")
+            x, y = (int(v) for v in pos.split("x"))
+            w, h = (int(v) for v in size.split("x"))
+        dev = HIPDevice(device_index)
+        dev.set_bvh_width(args.bvh_width)
+        dev.upload_scene(ds)
+        dev.load_kernels()
+        buf = torch.zeros((h, w, PS), dtype=torch.float32, device=torch.device("cuda", device_index))
+
+        class _Buf:
+            ptr = buf.data_ptr()
+
+        dev.render_tile(_Buf, (x, y, w, h), 0, 1, -(x + y * w), w)
+        torch.cuda.synchronize()
+        buf.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.render_tile(_Buf, (x, y, w, h), 0, S, -(x + y * w), w)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res.update({"frame": f"{W}x{H} {S} spp", "region": [x, y, w, h],
+                    "value": round(w * h * S / dt / 1e6, 3), "unit": "Msamples/s", "ms": round(1e3 * dt, 1),
+                    "film_checksum": float(buf[..., :4].double().sum().item())})
+        del buf
+    except Exception as e:  # reported beside the headline, never fatal
+        res["error"] = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        if dev is not None:
+            dev.close()
+    return res
 
 
 def cpu_baseline(ds, seconds):
