@@ -1990,11 +1990,22 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           break;
         case NODE_ATTR:
         case NODE_VERTEX_COLOR:
+        case NODE_TANGENT:
           *uses_attr = true;
           tex = true;
           break;
-        case NODE_TEX_WHITE_NOISE:
+        case NODE_NORMAL_MAP:
+          *uses_attr |= (node.y >> 24) == 0u; /* tangent space reads the UV tangent attributes */
+          tex = true;
+          break;
+        case NODE_OBJECT_INFO:
+          tex = true;
+          break;
         case NODE_GEOMETRY:
+          *uses_attr |= node.y == 2u; /* Tangent: primitive_tangent reads the generated coordinates */
+          tex = true;
+          break;
+        case NODE_TEX_WHITE_NOISE:
         case NODE_CONVERT:
         case NODE_HSV:
         case NODE_GAMMA:
