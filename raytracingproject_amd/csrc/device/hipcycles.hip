@@ -1999,6 +1999,21 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           tex = true;
           break;
         case NODE_OBJECT_INFO:
+        case NODE_CAMERA:
+        case NODE_VECTOR_ROTATE:
+        case NODE_VECTOR_TRANSFORM:
+          tex = true;
+          break;
+        case NODE_NORMAL:
+          len = 2; /* direction node */
+          tex = true;
+          break;
+        case NODE_RGB_CURVES:
+        case NODE_VECTOR_CURVES:
+          if (off + 1 >= n) {
+            return "curves: table size node past __svm_nodes";
+          }
+          len = 2 + (size_t)prog[off + 1].x;
           tex = true;
           break;
         case NODE_GEOMETRY:

@@ -1315,6 +1315,7 @@ CY_FN void svm_store3(CySvmStack stack, uint a, cfloat3 f, uint *err)
 
 #include "cy_svm_nodes.h"
 #include "cy_svm_noise.h"
+#include "cy_svm_extra.h"
 #include "cy_attribute.h"
 
 /* svm_closure.h:21-56 */
@@ -1942,6 +1943,22 @@ CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
         break;
       case NODE_MAPPING:
         svm_node_mapping(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_CAMERA:
+        svm_node_camera(kg, sd, stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_NORMAL:
+        svm_node_normal(kg, stack, node.y, node.z, node.w, &offset, err);
+        break;
+      case NODE_RGB_CURVES:
+      case NODE_VECTOR_CURVES:
+        svm_node_curves(kg, stack, node, &offset, err);
+        break;
+      case NODE_VECTOR_ROTATE:
+        svm_node_vector_rotate(stack, node.y, node.z, node.w, err);
+        break;
+      case NODE_VECTOR_TRANSFORM:
+        svm_node_vector_transform(kg, sd, stack, node, err);
         break;
       case NODE_TEX_GRADIENT:
         svm_node_tex_gradient(stack, node, err);

@@ -62,6 +62,12 @@ NODE_CLAMP = 84
 NODE_ATTR, NODE_VERTEX_COLOR = 16, 17
 NODE_OBJECT_INFO, NODE_TANGENT, NODE_NORMAL_MAP = 48, 70, 71
 NODE_FRESNEL, NODE_LAYER_WEIGHT = 38, 39
+NODE_CAMERA, NODE_NORMAL, NODE_RGB_CURVES, NODE_VECTOR_CURVES = 54, 65, 68, 69
+NODE_VECTOR_ROTATE, NODE_VECTOR_TRANSFORM = 78, 79
+VECTOR_ROTATE_TYPES = {"axis": 0, "x": 1, "y": 2, "z": 3, "euler_xyz": 4}
+VECTOR_TRANSFORM_TYPES = {"vector": 0, "point": 1, "normal": 2}
+VECTOR_TRANSFORM_SPACES = {"world": 0, "object": 1, "camera": 2}
+CAMERA_OUTPUTS = {"View Vector": "vector", "View Z Depth": "float", "View Distance": "float"}
 NORMAL_MAP_SPACES = {"tangent": 0, "object": 1, "world": 2, "blender_object": 3, "blender_world": 4}
 TANGENT_DIRECTIONS = {"radial": 0, "uv_map": 1}
 TANGENT_AXES = {"x": 0, "y": 1, "z": 2}
@@ -199,6 +205,64 @@ def layer_weight(blend=0.5, normal=None) -> Node:
     """Layer Weight node (nodes.cpp LayerWeightNode, svm_fresnel.h:40-75):
     Fresnel and Facing (blend != 0.5 bends Facing through powf)."""
     return Node("layer_weight", {"Blend": blend, "Normal": normal})
+
+
+def camera_data() -> Node:
+    """Camera Data node (nodes.cpp CameraNode, svm_camera.h): View Vector,
+    View Z Depth, View Distance."""
+    return Node("camera_data")
+
+
+def normal(direction=(0.0, 0.0, 1.0), normal_in=(0.0, 0.0, 1.0)) -> Node:
+    """Normal node (nodes.cpp NormalNode, svm_normal.h): the node's direction
+    and its Dot with the normalised input."""
+    return Node("normal", {"Normal": normal_in}, {"direction": tuple(float(x) for x in direction)})
+
+
+def _curve_table(points, table_size, min_x, max_x):
+    """Piecewise-linear curve through (x, y) control points sampled at
+    table_size positions over [min_x, max_x] (the host bakes Blender's curve
+    mapping to such a table, CurvesNode / curvemapping_table_RGBA)."""
+    pts = sorted((float(x), float(y)) for x, y in points)
+    xs = np.array([p for p, _ in pts]), np.array([q for _, q in pts])
+    x = min_x + (max_x - min_x) * np.arange(table_size, dtype=np.float64) / (table_size - 1)
+    return np.interp(x, xs[0], xs[1])
+
+
+def rgb_curves(color, r=((0, 0), (1, 1)), g=((0, 0), (1, 1)), b=((0, 0), (1, 1)), fac=1.0,
+               table_size: int = 257, min_x: float = 0.0, max_x: float = 1.0) -> Socket:
+    """RGB Curves node (nodes.cpp RGBCurvesNode / CurvesNode::compile,
+    svm_ramp.h svm_node_curves): per-channel curves with linear extrapolation
+    outside [min_x, max_x]."""
+    table = np.stack([_curve_table(c, table_size, min_x, max_x) for c in (r, g, b)], axis=1)
+    return Node("rgb_curves", {"Fac": fac, "Color": color},
+                {"table": table, "min_x": float(min_x), "max_x": float(max_x)})["Color"]
+
+
+def vector_curves(vector, x=((-1, -1), (1, 1)), y=((-1, -1), (1, 1)), z=((-1, -1), (1, 1)), fac=1.0,
+                  table_size: int = 257, min_x: float = -1.0, max_x: float = 1.0) -> Socket:
+    """Vector Curves node (nodes.cpp VectorCurvesNode): per-component curves."""
+    table = np.stack([_curve_table(c, table_size, min_x, max_x) for c in (x, y, z)], axis=1)
+    return Node("vector_curves", {"Fac": fac, "Vector": vector},
+                {"table": table, "min_x": float(min_x), "max_x": float(max_x)})["Vector"]
+
+
+def vector_rotate(vector, kind: str = "axis", center=(0.0, 0.0, 0.0), axis=(0.0, 0.0, 1.0), angle=0.0,
+                  rotation=(0.0, 0.0, 0.0), invert: bool = False) -> Socket:
+    """Vector Rotate node (nodes.cpp VectorRotateNode, svm_vector_rotate.h)."""
+    if kind not in VECTOR_ROTATE_TYPES:
+        raise ValueError(f"vector_rotate type one of {sorted(VECTOR_ROTATE_TYPES)}")
+    return Node("vector_rotate", {"Vector": vector, "Rotation": rotation, "Center": center, "Axis": axis,
+                                  "Angle": angle}, {"type": kind, "invert": bool(invert)})["Vector"]
+
+
+def vector_transform(vector, kind: str = "vector", convert_from: str = "world", convert_to: str = "object") -> Socket:
+    """Vector Transform node (nodes.cpp VectorTransformNode, svm_vector_transform.h)."""
+    if kind not in VECTOR_TRANSFORM_TYPES or convert_from not in VECTOR_TRANSFORM_SPACES or \
+            convert_to not in VECTOR_TRANSFORM_SPACES:
+        raise ValueError("vector_transform: type vector | point | normal, spaces world | object | camera")
+    return Node("vector_transform", {"Vector": vector}, {"type": kind, "from": convert_from,
+                                                         "to": convert_to})["Vector"]
 
 
 def object_info() -> Node:
@@ -490,6 +554,14 @@ def _outputs(node: Node) -> dict:
         return {"Normal": "vector"}
     if k == "fresnel":
         return {"Fac": "float"}
+    if k == "camera_data":
+        return dict(CAMERA_OUTPUTS)
+    if k == "normal":
+        return {"Normal": "vector", "Dot": "float"}
+    if k == "rgb_curves":
+        return {"Color": "color"}
+    if k in ("vector_curves", "vector_rotate", "vector_transform"):
+        return {"Vector": "vector"}
     if k == "layer_weight":
         return {"Fresnel": "float", "Facing": "float"}
     if k == "tangent":
@@ -569,6 +641,12 @@ _INPUT_TYPES = {
     "displacement": {"Height": "float", "Midlevel": "float", "Scale": "float", "Normal": "vector"},
     "normal_map": {"Color": "color", "Strength": "float"},
     "fresnel": {"IOR": "float", "Normal": "vector"},
+    "normal": {"Normal": "vector"},
+    "rgb_curves": {"Fac": "float", "Color": "color"},
+    "vector_curves": {"Fac": "float", "Vector": "vector"},
+    "vector_rotate": {"Vector": "vector", "Rotation": "vector", "Center": "vector", "Axis": "vector",
+                      "Angle": "float"},
+    "vector_transform": {"Vector": "vector"},
     "layer_weight": {"Blend": "float", "Normal": "vector"},
     "vector_displacement": {"Vector": "color", "Midlevel": "float", "Scale": "float"},
 }
@@ -581,7 +659,7 @@ def _width(t: str) -> int:
 # ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
 # the shading point or direction (texture coordinate, geometry, textures)
 SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture",
-                 "attribute", "vertex_color", "normal_map", "tangent", "object_info")
+                 "attribute", "vertex_color", "normal_map", "tangent", "object_info", "camera_data")
 
 
 def has_spatial_varying(values) -> bool:
@@ -793,6 +871,42 @@ class NodeCompiler:
             attr = self.attribute(ATTR_STD_GENERATED)
         self.emit((NODE_TANGENT, uchar4(self.out(n, "Tangent"), TANGENT_DIRECTIONS[n.params["direction"]],
                                         TANGENT_AXES[n.params["axis"]]), attr, 0))
+
+    def _n_camera_data(self, n):  # nodes.cpp CameraNode::compile
+        self.emit((NODE_CAMERA, *(self.out(n, k) for k in CAMERA_OUTPUTS)))
+
+    def _n_normal(self, n):  # nodes.cpp NormalNode::compile
+        nin = self.inp(n, "Normal")
+        self.emit((NODE_NORMAL, nin, self.out(n, "Normal"), self.out(n, "Dot")))
+        self.emit(tuple(f32bits(x) for x in n.params["direction"]) + (0,))
+
+    def _curves(self, n, ntype, value):  # nodes.cpp CurvesNode::compile
+        fac, val = self.inp(n, "Fac"), self.inp(n, value)
+        table = n.params["table"]
+        self.emit((ntype, uchar4(fac, val, self.out(n, value)), f32bits(n.params["min_x"]),
+                   f32bits(n.params["max_x"])))
+        self.emit((len(table), 0, 0, 0))
+        for row in table:
+            self.emit((f32bits(row[0]), f32bits(row[1]), f32bits(row[2]), 0))
+
+    def _n_rgb_curves(self, n):
+        self._curves(n, NODE_RGB_CURVES, "Color")
+
+    def _n_vector_curves(self, n):
+        self._curves(n, NODE_VECTOR_CURVES, "Vector")
+
+    def _n_vector_rotate(self, n):  # nodes.cpp VectorRotateNode::compile
+        v, rot, c, ax, ang = (self.inp(n, k) for k in ("Vector", "Rotation", "Center", "Axis", "Angle"))
+        self.emit((NODE_VECTOR_ROTATE, uchar4(VECTOR_ROTATE_TYPES[n.params["type"]], v, rot,
+                                              int(n.params["invert"])),
+                   uchar4(c, ax, ang), self.out(n, "Vector")))
+
+    def _n_vector_transform(self, n):  # nodes.cpp VectorTransformNode::compile
+        v = self.inp(n, "Vector")
+        self.emit((NODE_VECTOR_TRANSFORM, uchar4(VECTOR_TRANSFORM_TYPES[n.params["type"]],
+                                                 VECTOR_TRANSFORM_SPACES[n.params["from"]],
+                                                 VECTOR_TRANSFORM_SPACES[n.params["to"]]),
+                   uchar4(v, self.out(n, "Vector")), 0))
 
     def _n_fresnel(self, n):  # nodes.cpp FresnelNode::compile
         ior = self.assign_if_linked(n.inputs["IOR"], "float")

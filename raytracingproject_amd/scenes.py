@@ -1421,3 +1421,55 @@ def shading_normals(width=48, height=48, samples=8) -> sc.Scene:
     s.instances = [sc.Instance(ball, _tfm((-1.5, 1.2, -0.7), rot_y=0.7, rot_x=0.4), pass_index=7, object_random=0.3),
                    sc.Instance(ball, _tfm((1.4, -1.1, -0.6), rot_y=-1.1, scale=(1.2, 0.8, 1.0)))]
     return s
+
+
+def shading_converters(width=48, height=48, samples=8) -> sc.Scene:
+    """Input / vector / converter nodes (svm_camera.h, svm_normal.h,
+    svm_ramp.h curves, svm_vector_rotate.h, svm_vector_transform.h): Camera
+    Data outputs, the Normal node's dot product, RGB and Vector Curves with
+    values beyond the curve range (linear extrapolation), Vector Rotate about an
+    axis / X / Y / Z / Euler (inverted too) and Vector Transform between world,
+    object and camera spaces on a rotated, scaled instance."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    P, N = g["Position"], g["Normal"]
+    cam = nd.camera_data()
+
+    def show(v, s=0.25):
+        return nd.mix_rgb("mix", 1.0, (0.0, 0.0, 0.0), nd.mapping(v, scale=(s, s, s), location=(0.5, 0.5, 0.5)),
+                          clamp=True)
+
+    wave = nd.noise_texture(scale=2.0, detail=1.0)["Color"]
+    wide = nd.mapping(wave, scale=(2.0, 2.0, 2.0), location=(-0.5, -0.5, -0.5))  # reaches below 0 and above 1
+    colors = [
+        show(cam["View Vector"], 0.5),
+        nd.combine_xyz(nd.math("multiply", cam["View Z Depth"], 0.05), nd.math("multiply", cam["View Distance"], 0.04),
+                       0.3),
+        nd.combine_xyz(nd.normal((0.3, 0.5, -0.8), N)["Dot"], 0.4, nd.normal((0.0, 1.0, 0.0), N)["Dot"]),
+        nd.rgb_curves(wide, r=((0.0, 0.1), (0.4, 0.7), (1.0, 0.9)), g=((0.0, 0.0), (1.0, 1.0)),
+                      b=((0.0, 1.0), (0.5, 0.2), (1.0, 0.5))),
+        nd.rgb_curves(wave, r=((0.0, 0.0), (1.0, 1.0)), g=((0.0, 0.3), (1.0, 0.6)), fac=0.6),
+        show(nd.vector_curves(nd.mapping(P, scale=(0.7, 0.7, 0.7)), x=((-1, 0.5), (1, -0.5)),
+                              y=((-1, -1), (0, 0.3), (1, 1)))),
+        show(nd.vector_rotate(P, "axis", center=(0.2, 0.1, 0.0), axis=(0.3, 1.0, 0.2), angle=0.9)),
+        show(nd.vector_rotate(P, "x", angle=1.2, invert=True)),
+        show(nd.vector_rotate(P, "y", angle=-0.7)),
+        show(nd.vector_rotate(P, "z", center=(0.5, 0.5, 0.0), angle=2.0)),
+        show(nd.vector_rotate(P, "euler_xyz", rotation=(0.3, 0.6, 0.9))),
+        show(nd.vector_rotate(P, "euler_xyz", rotation=(0.3, -0.4, 1.1), invert=True)),
+        show(nd.vector_transform(P, "point", "world", "camera"), 0.1),
+        show(nd.vector_transform(N, "normal", "world", "camera"), 0.5),
+        show(nd.vector_transform(nd.geometry()["Incoming"], "vector", "camera", "world"), 0.5),
+    ]
+    s = _grid_scene(colors, width, height, samples, "shading_converters", glossy_every=4)
+    # object-space transforms on a rotated, scaled instance shared by two objects
+    bv, bt = _box((0.0, 0.0, 0.0), (0.6, 0.6, 0.6))
+    n = len(s.materials)
+    s.materials.append(sc.diffuse(show(nd.vector_transform(P, "point", "world", "object"), 0.8)))
+    s.materials.append(sc.diffuse(show(nd.vector_transform(N, "normal", "object", "world"), 0.5)))
+    s.materials.append(sc.diffuse(show(nd.vector_transform(P, "point", "camera", "object"), 0.2)))
+    box = sc.Mesh(bv, bt, shader=np.array([n + (k % 3) for k in range(len(bt))]))
+    s.instances = [sc.Instance(box, _tfm((-1.7, 1.3, -0.7), rot_y=0.6, rot_x=0.3, scale=(1.0, 0.7, 1.2))),
+                   sc.Instance(box, _tfm((1.6, -1.2, -0.6), rot_y=-0.8))]
+    return s
