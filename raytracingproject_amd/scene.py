@@ -764,6 +764,9 @@ class Lamp:
     use_mis: bool = True
     cast_shadow: bool = True
     max_bounces: int = 1024
+    # the light's shader (Light::shader; None: the shared default emission
+    # shader of strength 1, color and strength then go to KernelLight.strength)
+    shader: "Closure | None" = None
 
 
 @dataclass
@@ -794,6 +797,8 @@ class Camera:
     blades: int = 0
     bladesrotation: float = 0.0
     aperture_ratio: float = 1.0
+    # camera-to-world (4x4, Camera::matrix) instead of eye / target / up
+    matrix: np.ndarray | None = None
 
 
 @dataclass
@@ -840,6 +845,8 @@ class Scene:
     hair_subdivisions: int = 3
     # world "Volume" output (a volume closure tree, e.g. a homogeneous fog)
     world_volume: "Closure | None" = None
+    # Film exposure (film.cpp:363; applied by film convert)
+    exposure: float = 1.0
 
 
 def _has_displacement(m) -> bool:
@@ -950,7 +957,11 @@ def compile_camera(kcam, cam: Camera, width: int, height: int):
         cameratoscreen = np.eye(4)
     screentocamera = np.linalg.inv(cameratoscreen)
     rastertocamera = screentocamera @ rastertoscreen
-    cameratoworld = _look_at(cam.eye, cam.target, cam.up)
+    if cam.matrix is not None:
+        cameratoworld = np.eye(4)
+        cameratoworld[:3] = np.asarray(cam.matrix, dtype=np.float64)[:3]
+    else:
+        cameratoworld = _look_at(cam.eye, cam.target, cam.up)
     worldtocamera = np.linalg.inv(cameratoworld)
 
     def persp(m, v):
@@ -1107,9 +1118,23 @@ def compile_scene(scene: Scene) -> DeviceScene:
     # color and power go to KernelLight.strength
     mats = list(scene.materials)
     lamp_shader = None
-    if scene.lamps:
-        lamp_shader = len(mats)
-        mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
+    lamp_shaders = []  # per lamp: its shader index
+    for lamp in scene.lamps:
+        if lamp.shader is None:
+            if lamp_shader is None:
+                lamp_shader = len(mats)
+                mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
+            lamp_shaders.append(lamp_shader)
+        else:
+            if lamp.shader.constant_emission() is None:
+                # lamp emission is evaluated from the shader's constant
+                # (cy_integrator.h direct_emissive_eval)
+                raise ValueError("lamp shader: only constant emission is supported")
+            ids = [i for i, m in enumerate(mats) if m is lamp.shader]
+            if not ids:
+                mats.append(lamp.shader)
+                ids = [len(mats) - 1]
+            lamp_shaders.append(ids[0])
     world = background(scene.world_color, scene.world_strength)
     world.volume = scene.world_volume
     svm_compiler = SVMCompiler()
@@ -1246,7 +1271,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         e.shader_flag = f32bits_signed(1.0)  # lamp.pad
         e.object_id = f32bits_signed(lamp.size)  # lamp.size
         totarea = f32(totarea + lightarea)
-        use_lamp_mis |= _pack_lamp(klights[li], lamp, lamp_shader)
+        use_lamp_mis |= _pack_lamp(klights[li], lamp, lamp_shaders[li])
     if bg_light:
         li = len(lamps)
         e = dist[nd + li]
@@ -1365,7 +1390,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
 
     # --- film (render/film.cpp device_update, combined pass only)
     kf = kd.film
-    kf.exposure = 1.0
+    kf.exposure = float(scene.exposure)
     kf.pass_flag = PASSMASK_COMBINED
     kf.light_pass_flag = 0
     kf.pass_stride = 4
