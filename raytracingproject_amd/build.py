@@ -129,6 +129,9 @@ def build_oracle(ref=True):
     _run(["make", "-C", oracle, "oracle", "-j4"])
     if ref and os.path.isdir("/root/reference/blender/intern/cycles"):
         _run(["make", "-C", oracle, "ref", "ref-avx2", "-j4"])
+        # the Device plugin linked with the reference host's device layer
+        # (tests/test_plugin_harness.py; needs libhipcycles.so)
+        _run(["bash", os.path.join(REPO, "tools", "plugin_harness.sh")])
 
 
 def build_all(ref=True, force=False):
