@@ -424,6 +424,225 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   return found_hit;
 }
 
+/* While-while traversal with postponed leaves (Aila & Laine, "Understanding
+ * the Efficiency of Ray Traversal on GPUs", HPG 2009), measurement switch.
+ * bvhw_traverse handles one node OR one leaf per iteration, so a wave whose
+ * lanes are split between inner nodes and leaves runs both bodies every
+ * iteration.  Here a lane that meets a leaf parks it and keeps descending
+ * inner nodes until every lane of the wave holds a leaf (or has run out of
+ * nodes); then the parked leaves are tested together.  Same boxes, culling
+ * bounds, triangle test and near-tie bookkeeping as bvhw_traverse; only the
+ * order in which leaves are tested changes, which the near-tie window already
+ * makes irrelevant to the result. */
+#ifndef CY_WHILE_WHILE
+#  define CY_WHILE_WHILE 0
+#endif
+
+CY_FN bool cy_wave_all(bool p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __all(p ? 1 : 0) != 0;
+#else
+  return p;
+#endif
+}
+
+template<int W, bool any_hit>
+CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
+                            cfloat3 P,
+                            cfloat3 dir,
+                            cfloat3 idir,
+                            uint visibility,
+                            CyIsect *isect,
+                            uint *err,
+                            uint *cnt_nodes,
+                            uint *cnt_leaves,
+                            uint *cnt_tris,
+                            CY_LDS CyStackEntry *lds_ring,
+                            bool *tie_out)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  CY_LDS CyStackEntry *ring = lds_ring;
+#else
+  CyStackEntry host_ring[CY_LDS_STACKW];
+  CyStackEntry *ring = host_ring;
+  (void)lds_ring;
+#endif
+  int top = 0, n_ring = 0, n_over = 0;
+  int over_node[CY_OVER_STACK];
+  float over_t[CY_OVER_STACK];
+  bool found_hit = false, tie = false;
+#define CY_T_CULL ((any_hit || !CY_EXACT_TIES) ? isect->t : isect->t * (1.0f + CY_TIE_EPS))
+#define CY_T_BOX ((any_hit || !CY_EXACT_TIES || !CY_TIE_BOX_WIDEN) ? isect->t : isect->t * (1.0f + CY_TIE_EPS))
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
+  constexpr int Q = W / 4;
+
+  int code = 0; /* next node or leaf to visit (root) */
+  bool have_code = true;
+  int leaf = 0; /* parked leaf */
+  bool have_leaf = false;
+
+  /* pops the nearest pending entry that the current hit does not cull */
+  auto pop = [&]() -> bool {
+    while (n_ring > 0 || n_over > 0) {
+      if (n_ring == 0) {
+        const int k = n_over < CY_LDS_STACKW ? n_over : CY_LDS_STACKW;
+        for (int j = n_over - k; j < n_over; j++) {
+          CyStackEntry e_;
+          e_.node = over_node[j];
+          e_.t = over_t[j];
+          ring[top * CY_RING_STRIDE] = e_;
+          top = (top + 1) & (CY_LDS_STACKW - 1);
+        }
+        n_over -= k;
+        n_ring = k;
+      }
+      top = (top - 1) & (CY_LDS_STACKW - 1);
+      n_ring--;
+      const CyStackEntry e = ring[top * CY_RING_STRIDE];
+      if (e.t <= CY_T_BOX) {
+        code = e.node;
+        return true;
+      }
+    }
+    return false;
+  };
+
+  while (have_code || have_leaf) {
+    /* inner phase: descend until every lane holds a leaf or has no nodes left */
+    while (!cy_wave_all(have_leaf || !have_code)) {
+      if (!have_code || (code < 0 && have_leaf)) {
+        continue; /* waits for the wave */
+      }
+      if (code < 0) {
+        leaf = code;
+        have_leaf = true;
+        have_code = pop();
+        continue;
+      }
+      n_nodes++;
+      const hc_float4 *np = nodes + (size_t)code * (8 * Q);
+      float tn[W];
+      int cc[W];
+      const float t = CY_T_BOX;
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const hc_float4 lx = np[0 * Q + q], hx = np[1 * Q + q];
+        const hc_float4 ly = np[2 * Q + q], hy = np[3 * Q + q];
+        const hc_float4 lz = np[4 * Q + q], hz = np[5 * Q + q];
+        const hc_uint4 ch = ((const hc_uint4 *)np)[6 * Q + q];
+        const hc_uint4 mt = ((const hc_uint4 *)np)[7 * Q + q];
+        const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+        const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+        const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+        const uint ach[4] = {ch.x, ch.y, ch.z, ch.w}, amt[4] = {mt.x, mt.y, mt.z, mt.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float clox = (alx[j] - P.x) * idir.x;
+          const float chix = (ahx[j] - P.x) * idir.x;
+          const float cloy = (aly[j] - P.y) * idir.y;
+          const float chiy = (ahy[j] - P.y) * idir.y;
+          const float cloz = (alz[j] - P.z) * idir.z;
+          const float chiz = (ahz[j] - P.z) * idir.z;
+          const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz));
+          const float cmx = min4(t, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
+          const bool hit = (cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility);
+          const int s = 4 * q + j;
+          const int child = (int)ach[j];
+          cc[s] = child >= 0 ? child : ~((~child << 4) | (int)(amt[j] >> 28));
+          tn[s] = hit ? cmn : CY_INF;
+        }
+      }
+      bvhw_sort<W>(tn, cc);
+      if (tn[0] == CY_INF) {
+        have_code = pop();
+        continue;
+      }
+#pragma unroll
+      for (int s = W - 1; s >= 1; s--) {
+        if (tn[s] != CY_INF) {
+          if (!CY_STACK_PUSH(cc[s], tn[s])) {
+            cy_set_error(err, CY_ERR_BVH_STACK, W);
+            have_code = false;
+            have_leaf = false;
+            goto out;
+          }
+        }
+      }
+      code = cc[0];
+    }
+
+    /* leaf phase: the parked leaves of the wave together */
+    if (have_leaf) {
+      have_leaf = false;
+      n_leaves++;
+      const int packed = ~leaf;
+      int prim_addr = packed >> 4;
+      if ((packed & 15) == 0) {
+        cy_set_error(err, CY_ERR_FEATURE, 1);
+        goto out;
+      }
+      const int prim_end = prim_addr + (packed & 15);
+      const bool ident = kg->tri_index_identity != 0;
+      uint vi = ident ? 3u * (uint)prim_addr : kg->__prim_tri_index[prim_addr];
+      hc_float4 v0 = kg->__prim_tri_verts[vi], v1 = kg->__prim_tri_verts[vi + 1], v2 = kg->__prim_tri_verts[vi + 2];
+      for (; prim_addr < prim_end; prim_addr++) {
+        n_tris++;
+        hc_float4 w0 = v0, w1 = v1, w2 = v2;
+        if (prim_addr + 1 < prim_end) {
+          vi = ident ? 3u * (uint)(prim_addr + 1) : kg->__prim_tri_index[prim_addr + 1];
+          w0 = kg->__prim_tri_verts[vi];
+          w1 = kg->__prim_tri_verts[vi + 1];
+          w2 = kg->__prim_tri_verts[vi + 2];
+        }
+        float tt, uu, vv;
+        bool exact_ok;
+        if (ray_triangle_intersect2(P, dir, CY_T_CULL, isect->t, f4to3(v0), f4to3(v1), f4to3(v2), &uu, &vv, &tt,
+                                    &exact_ok) &&
+            (kg->__prim_visibility[prim_addr] & visibility)) {
+          if (any_hit) {
+            isect->prim = prim_addr;
+            isect->object = OBJECT_NONE;
+            isect->type = PRIMITIVE_TRIANGLE;
+            isect->u = uu;
+            isect->v = vv;
+            isect->t = tt;
+            found_hit = true;
+            have_code = false;
+            break;
+          }
+          tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
+          if (exact_ok || !CY_TIE_EXACT_OK) {
+            isect->prim = prim_addr;
+            isect->object = OBJECT_NONE;
+            isect->type = PRIMITIVE_TRIANGLE;
+            isect->u = uu;
+            isect->v = vv;
+            isect->t = tt;
+            found_hit = true;
+          }
+        }
+        v0 = w0;
+        v1 = w1;
+        v2 = w2;
+      }
+    }
+  }
+out:
+#undef CY_T_CULL
+#undef CY_T_BOX
+  if (tie_out && tie) {
+    *tie_out = true;
+  }
+  if (cnt_nodes) {
+    *cnt_nodes += n_nodes;
+    *cnt_leaves += n_leaves;
+    *cnt_tris += n_tris;
+  }
+  return found_hit;
+}
+
 /* Closest hit (any_hit == false) or opaque-shadow any hit over a scene without
  * instances with the wide BVH: scene_intersect (bvh/bvh.h:154-237). */
 template<int W, bool any_hit>
@@ -445,8 +664,13 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
   isect->object = OBJECT_NONE;
   isect->type = 0;
   const cfloat3 dir = bvh_clamp_direction(ray->D);
+#if CY_WHILE_WHILE
+  bvhw_traverse_ww<W, any_hit>(kg, ray->P, dir, rcp3(dir), visibility, isect, err, cnt_nodes, cnt_leaves, cnt_tris,
+                               lds_ring, tie);
+#else
   bvhw_traverse<W, any_hit>(kg, 0, ray->P, dir, rcp3(dir), OBJECT_NONE, visibility, isect, err, cnt_nodes,
                             cnt_leaves, cnt_tris, lds_ring, tie);
+#endif
   return isect->prim != PRIM_NONE;
 }
 

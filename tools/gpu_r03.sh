@@ -29,4 +29,12 @@ fi
 if [[ $MODE == benchq ]]; then
   step bench 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --tile 0 "$@"
 fi
+if [[ $MODE == variants ]]; then
+  # traversal variants (python -m raytracingproject_amd.build --variant NAME -D... --traversal-only)
+  Q="--steps 5 --warmup 1 --no-cpu-baseline --tile 0 --other-configs="
+  step bench_default 600 python bench.py $Q "$@"
+  for v in ${VARIANTS:-slabfma ww}; do
+    step bench_$v 600 env HIPCY_DEVICE_LIB=$PWD/raytracingproject_amd/libhipcycles-$v.so python bench.py $Q "$@"
+  done
+fi
 echo done
