@@ -66,6 +66,9 @@ def parse(argv=None):
     p.add_argument("--other-configs", default="barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
                    help="BASELINE.json's other configs, one frame each after the headline measurement (rank 0, "
                         "N=1): name or name@XxY+WxH for a full-spp crop; empty disables")
+    p.add_argument("--shard", default="auto", choices=("auto", "rows", "tiles"),
+                   help="multi-GPU split: interleaved rows, or whole tiles per rank (auto: tiles for "
+                        "adaptive-sampling scenes, whose filters run per RenderTile)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (RCCL, one GPU per rank); gloo rehearses N ranks on fewer GPUs")
     return p.parse_args(argv)
@@ -109,7 +112,7 @@ def main():
     from raytracingproject_amd import scene as sc
     from raytracingproject_amd import scenes
     from raytracingproject_amd.device import HIPDevice
-    from raytracingproject_amd.shard import RowShard
+    from raytracingproject_amd.shard import RowShard, TileShard, assemble_tiles
 
     kw = {}
     if args.width:
@@ -136,6 +139,13 @@ def main():
     W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
     shard = RowShard(rank, world, W, H)
     rows_pad = -(-H // world)  # every rank's buffer has the same size for the gather
+    use_tiles = args.shard == "tiles" or (args.shard == "auto" and world > 1 and
+                                           bool(ds.data.film.pass_adaptive_aux_buffer))
+    if use_tiles:
+        # whole tiles per rank, full-frame buffers (shard.TileShard)
+        tile_size = args.tile if args.tile > 0 else 64
+        tshards = [TileShard(r, world, W, H, tile_size) for r in range(world)]
+        rows_pad = H
     cuda = torch.device("cuda", device_index)
     # render buffer: a torch allocation handed to the device as a raw pointer
     # (RenderTile.buffer), so the gather can run over RCCL without a copy
@@ -152,12 +162,22 @@ def main():
     def render_frame():
         local.zero_()
         torch.cuda.current_stream().synchronize()
-        dev.render_tile(_Buf, shard.tile(), 0, S, shard.offset, shard.stride, y_step=shard.y_step)
+        if use_tiles:
+            ts = tshards[rank]
+            dev.render_tiles([(t, _Buf.ptr, ts.offset, ts.stride) for t in ts.tiles()], 0, S)
+        else:
+            dev.render_tile(_Buf, shard.tile(), 0, S, shard.offset, shard.stride, y_step=shard.y_step)
 
     def film_to_host():
         """Finished film to rank 0's host memory (gather of the row-interleaved parts)."""
         if world == 1:
             film_host.copy_(local[:H])
+            return
+        if use_tiles:
+            dist.all_gather_into_tensor(gathered.view(-1), (local if gather_gpu else local.cpu()).view(-1))
+            if rank == 0:
+                parts = [gathered[r].cpu().numpy() for r in range(world)]
+                film_host.copy_(torch.from_numpy(assemble_tiles(parts, tshards)))
             return
         if gather_gpu:
             dist.all_gather_into_tensor(gathered.view(-1), local.view(-1))
@@ -268,7 +288,8 @@ def main():
             "config": {
                 "workload": f"{args.config} {W}x{H} {S} spp, one frame per step, film copied to host",
                 "triangles": ds.info["triangles"],
-                "parallelism": f"rows interleaved over {world} GPU(s)",
+                "parallelism": (f"{tile_size}x{tile_size} tiles dealt over {world} GPU(s)" if use_tiles
+                                else f"rows interleaved over {world} GPU(s)"),
                 "wavefront_iterations_per_frame": int(timing["iterations"]),
                 "ray_sort": args.ray_sort,
                 "traversal_budget": list(args.trav_budget),

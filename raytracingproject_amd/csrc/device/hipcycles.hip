@@ -275,10 +275,11 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
                                                                  uint *err,
                                                                  CyStats *stats)
 {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_active = cam_n > 0 ? cam_n : (int)*counter;
+  const int i = cy_queue_index(n_active);
   __shared__ LdsStack<W, INST> lds_stack;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
-  const bool active = cam_n > 0 ? i < cam_n : i < (int)*counter;
+  const bool active = i < n_active;
   if (active) {
     const int slot = cam_n > 0 ? slot_base + i : queue[i];
     const uint cam_item = cam_n > 0 ? tile.item_base + (uint)i : CY_NO_ITEM;
@@ -457,12 +458,13 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
                                                                 uint *err,
                                                                 CyStats *stats)
 {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_active = (int)*shadow_count;
+  const int i = cy_queue_index(n_active);
   __shared__ LdsStack<W, INST> lds_stack;
   bool finished = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
-  if (i < (int)*shadow_count) {
+  if (i < n_active) {
     slot = shadow_queue[i];
     CyRay ray;
     shadow_load(&b, slot, &ray);

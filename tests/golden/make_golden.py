@@ -188,7 +188,30 @@ def make_sobol():
     print("sobol_joe_kuo", dims, "dimensions")
 
 
+def make_adaptive_tiles(tile=24):
+    """Adaptive sampling rendered tile by tile by the reference CPU device's
+    adaptive loop (per-RenderTile stopping and filters): the golden of the
+    tile-sharded multi-GPU path (shard.TileShard)."""
+    from parity_cases import HOST_LOOP_CASES
+
+    name = sorted(HOST_LOOP_CASES)[0]
+    ds = compile_case(name)
+    rk = RefKernel(ds)
+    from raytracingproject_amd.shard import TileShard
+
+    full = np.zeros((ds.height, ds.width, ds.pass_stride), dtype=np.float32)
+    for x, y, w, h in TileShard(0, 1, ds.width, ds.height, tile).all_tiles():
+        full[y:y + h, x:x + w] = rk.render_adaptive(tile=(x, y, w, h))
+    rk.close()
+    np.savez_compressed(golden_path(f"{name}_tiles{tile}"), digest=np.array(scene_digest(ds)), buffer=full,
+                        samples=np.array(ds.samples), tile=np.array(tile))
+    print(name, "tiles", tile, "buffer mean", float(full[..., :3].mean()))
+
+
 def main():
+    if "--adaptive-tiles-only" in sys.argv:
+        make_adaptive_tiles()
+        return
     if "--sobol-only" in sys.argv:
         make_sobol()
         return

@@ -75,3 +75,27 @@ def test_shard_plan_partitions_rows():
             # last local row lands inside the compact buffer
             j = sh.rows - 1
             assert sh.offset + (y + j) * sh.stride == j * 1280
+
+
+@pytest.mark.parametrize("world, tile, size", [(1, 64, (64, 64)), (2, 24, (64, 64)), (3, 16, (37, 19)),
+                                               (8, 64, (1280, 720))])
+def test_tile_shards_cover_every_pixel_once(world, tile, size):
+    from raytracingproject_amd.shard import TileShard, assemble_tiles
+
+    w, h = size
+    shards = [TileShard(r, world, w, h, tile) for r in range(world)]
+    cover = np.zeros((h, w), dtype=np.int32)
+    for sh in shards:
+        for x, y, tw, th in sh.tiles():
+            assert 0 < tw <= tile and 0 < th <= tile
+            cover[y:y + th, x:x + tw] += 1
+    assert (cover == 1).all()
+    # every rank's tiles come back from that rank's buffer
+    parts = [np.full((h, w, 1), r + 1, dtype=np.float32) for r in range(world)]
+    out = assemble_tiles(parts, shards)
+    for r, sh in enumerate(shards):
+        for x, y, tw, th in sh.tiles():
+            assert (out[y:y + th, x:x + tw] == r + 1).all()
+    # ranks get tile counts within one of each other
+    counts = [len(sh.tiles()) for sh in shards]
+    assert max(counts) - min(counts) <= 1
