@@ -142,6 +142,11 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
 #  define CY_SLAB_FMA 0
 #endif
 
+/* opaque any-hit without the child sort (measurement switch) */
+#ifndef CY_ANYHIT_NOSORT
+#  define CY_ANYHIT_NOSORT 0
+#endif
+
 /* Near-tie window of the exact closest hit: hits within 2^-20 (about 8 ulps)
  * of the best distance are kept as candidates and resolved in the reference's
  * order at the end (bvhw_traverse). */
@@ -292,6 +297,30 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
           cc[s] = child >= 0 ? child : ~((~child << 4) | (int)(amt[j] >> 28));
           tn[s] = hit ? cmn : CY_INF;
         }
+      }
+      if (any_hit && CY_ANYHIT_NOSORT) {
+        /* any hit ends the query, so the children need no distance order:
+         * the first hit child is visited next, the others pushed as found */
+        int next = 0;
+        bool have_next = false;
+#pragma unroll
+        for (int s = 0; s < W; s++) {
+          if (tn[s] != CY_INF) {
+            if (!have_next) {
+              next = cc[s];
+              have_next = true;
+            }
+            else if (!CY_STACK_PUSH(cc[s], tn[s])) {
+              cy_set_error(err, CY_ERR_BVH_STACK, W);
+              return found_hit;
+            }
+          }
+        }
+        if (!have_next) {
+          goto pop;
+        }
+        code = next;
+        continue;
       }
       bvhw_sort<W>(tn, cc);
       if (tn[0] == CY_INF) {
