@@ -123,10 +123,13 @@ def main(tag):
         summary[k] = ent
     # bench.py's name for the dominant kernel: the instance without counters
     # (k_intersect_closest<false, W, I>); the profiled frame runs exactly one
-    inst = sorted(k for k in summary if k.startswith("k_intersect_closest<false"))
-    if len(inst) != 1:
-        raise SystemExit(f"expected one timed closest-hit instance, found {inst}")
-    summary["k_intersect_closest"] = dict(summary[inst[0]], instance=inst[0])
+    # and the same for the opaque-shadow traversal (BASELINE.md's roofline
+    # covers both traversal kernels)
+    for base in ("k_intersect_closest", "k_intersect_shadow"):
+        inst = sorted(k for k in summary if k.startswith(base + "<false"))
+        if len(inst) != 1:
+            raise SystemExit(f"expected one timed {base} instance, found {inst}")
+        summary[base] = dict(summary[inst[0]], instance=inst[0])
     with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps(summary["k_intersect_closest"], indent=1))
