@@ -897,6 +897,63 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
   return shader_background_eval(&esd);
 }
 
+#if CY_SVM_TEX
+/* direct_emissive_eval's non-constant branch for a mesh-light or lamp sample
+ * (kernel_emission.h:54-88): shader_setup_from_sample (kernel_shader.h:244-360;
+ * world space, no differentials; a lamp's transform is the identity the host
+ * packs) and the emitter's SVM program with PATH_RAY_EMISSION, which stores no
+ * closures (shader_eval_surface: max_closures 0), so the shading point's
+ * closure array in `mem` is left intact; then shader_emissive_eval
+ * (kernel_shader.h, emissive_simple_eval).  ls->Ng takes the emitter's
+ * (backfacing-flipped) normal as the reference's does.  Out of line: it is
+ * reached from the light sample and from lamp MIS hits. */
+CY_NOINLINE cfloat3 emissive_eval_svm(const CyGlobals *kg, CyLightSample *ls, cfloat3 I, float t, CyShadeMem mem,
+                                      CyPathState state, uint *err)
+{
+  CySD esd;
+  esd.closure = mem.closure;
+  esd.svm_stack = mem.svm_stack;
+  esd.svm_stride = mem.svm_stride;
+  esd.svm_fast = mem.svm_fast;
+  esd.svm_spill = mem.svm_spill;
+  esd.P = ls->P;
+  esd.N = ls->Ng;
+  esd.Ng = ls->Ng;
+  esd.I = I;
+  esd.shader = ls->shader;
+  esd.type = (ls->prim != PRIM_NONE) ? PRIMITIVE_TRIANGLE : ((ls->lamp != LAMP_NONE) ? (1 << 6) /* PRIMITIVE_LAMP */ : 0);
+  esd.object = ls->object;
+  esd.prim = ls->prim;
+  esd.u = ls->u;
+  esd.v = ls->v;
+  esd.ray_length = t;
+  esd.flag = kg->__shaders[(uint)esd.shader & SHADER_MASK].flags;
+  esd.object_flag = (esd.object != OBJECT_NONE) ? (int)kg->__object_flag[esd.object] : 0;
+  if ((esd.type & PRIMITIVE_TRIANGLE) && ((uint)esd.shader & SHADER_SMOOTH_NORMAL)) {
+    esd.N = triangle_smooth_normal(kg, ls->Ng, esd.prim, esd.u, esd.v);
+    if (!(esd.object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
+      esd.N = object_normal_transform(kg, esd.object, esd.N);
+    }
+  }
+  if (esd.prim != PRIM_NONE && dot3(esd.Ng, esd.I) < 0.0f) {
+    esd.flag |= SD_BACKFACING;
+    esd.Ng = neg3(esd.Ng);
+    esd.N = neg3(esd.N);
+  }
+  ls->Ng = esd.Ng;
+  esd.closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
+  esd.closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);
+  esd.svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
+  state.bounce += 1; /* path_state_modify_bounce(state, true) */
+  shader_eval_surface(kg, &esd, &state, PATH_RAY_EMISSION, err);
+  if (!(esd.flag & SD_EMISSION)) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  const float res = (fabsf(dot3(esd.Ng, esd.I)) > 0.0f) ? 1.0f : 0.0f;
+  return mul3(mk3(res, res, res), esd.closure_emission_background);
+}
+#endif
+
 /* Direct light at a shading point, one light sample (kernel_path_surface.h:23-140
  * kernel_branched_path_surface_connect_light with one sample, or
  * kernel_path_volume_connect_light, kernel_path_volume.h:21-61, when PHASE: a
@@ -930,10 +987,15 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
       light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ls.D, mem,
                                        *state, PATH_RAY_EMISSION, err);
     }
-#endif
     else {
-      cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
+      /* a mesh light or lamp whose emission depends on its shader's nodes */
+      light_eval = emissive_eval_svm(kg, &ls, I, ls.t, mem, *state, err);
     }
+#else
+    else {
+      cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter: a _tex variant scans it */
+    }
+#endif
     light_eval = mul3f(light_eval, ls.eval_fac);
     if (ls.lamp != LAMP_NONE) {
       light_eval = mul3(light_eval, klight_vec(kg->__lights[ls.lamp].strength));
@@ -1201,10 +1263,14 @@ CY_FN bool shade_path(const CyGlobals *kg,
           continue;
         }
       }
-      /* direct_emissive_eval (kernel_emission.h:20-99), constant lamp shader */
+      /* direct_emissive_eval (kernel_emission.h:20-99) */
       cfloat3 lamp_L = mk3(0.0f, 0.0f, 0.0f);
       if (!shader_constant_emission_eval(kg, ls.shader, &lamp_L)) {
-        cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter */
+#if CY_SVM_TEX
+        lamp_L = emissive_eval_svm(kg, &ls, neg3(ray.D), ls.t, mem, state, err);
+#else
+        cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter: a _tex variant scans it */
+#endif
       }
       lamp_L = mul3f(lamp_L, ls.eval_fac);
       lamp_L = mul3(lamp_L, klight_vec(kg->__lights[lamp].strength));

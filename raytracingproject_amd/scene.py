@@ -1126,10 +1126,6 @@ def compile_scene(scene: Scene) -> DeviceScene:
                 mats.append(Closure("emission", (1.0, 1.0, 1.0), strength=1.0))
             lamp_shaders.append(lamp_shader)
         else:
-            if lamp.shader.constant_emission() is None:
-                # lamp emission is evaluated from the shader's constant
-                # (cy_integrator.h direct_emissive_eval)
-                raise ValueError("lamp shader: only constant emission is supported")
             ids = [i for i, m in enumerate(mats) if m is lamp.shader]
             if not ids:
                 mats.append(lamp.shader)

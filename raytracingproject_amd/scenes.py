@@ -157,6 +157,33 @@ def cornell_lamps(width=64, height=64, samples=16) -> sc.Scene:
     return scene
 
 
+def emission_nodes(width=48, height=48, samples=8) -> sc.Scene:
+    """Emitters whose emission comes from shader nodes (direct_emissive_eval's
+    non-constant branch, kernel_emission.h:54-88): a ceiling mesh light with a
+    checker-textured colour on its generated coordinates, a point lamp (with
+    lamp MIS) whose strength is a Light Falloff node's Linear output (it reads
+    the sample distance), a spot lamp with a Light Path-dependent strength, and
+    a constant sun for contrast."""
+    from . import nodes
+
+    scene = cornell_box(width, height, samples)
+    ck = nodes.checker(color1=(1.0, 0.85, 0.6), color2=(0.3, 0.3, 0.9), scale=3.0)["Color"]
+    scene.materials[3] = sc.emission(ck, 40.0)
+    falloff = nodes.light_falloff(strength=1.0, smooth=50.0)["Linear"]
+    diffuse_ray = nodes.light_path()["Is Diffuse Ray"]
+    spot_strength = nodes.math("add", diffuse_ray, 0.5)
+    scene.lamps = [
+        sc.Lamp("point", co=(140.0, 420.0, 200.0), size=25.0, color=(1.0, 0.6, 0.3), strength=1.0e4,
+                shader=sc.emission((1.0, 1.0, 1.0), falloff)),
+        sc.Lamp("spot", co=(420.0, 500.0, 120.0), direction=(-0.3, -1.0, 0.4), size=10.0, use_mis=False,
+                spot_angle=math.radians(50.0), spot_smooth=0.3, color=(0.4, 0.7, 1.0), strength=6.0e6,
+                shader=sc.emission((1.0, 1.0, 1.0), spot_strength)),
+        sc.Lamp("sun", direction=(0.2, -1.0, 0.6), angle=math.radians(5.0), color=(1.0, 0.95, 0.9), strength=2.0),
+    ]
+    scene.name = "emission_nodes"
+    return scene
+
+
 def cornell_camera(kind: str, width=64, height=64, samples=16) -> sc.Scene:
     """Cornell box through the camera models of kernel_camera.h: "dof"
     (perspective, hexagonal anamorphic aperture), "ortho" (orthographic with a

@@ -577,10 +577,6 @@ class XMLReader:
             surf, _ = self.shaders[st.shader]
             if surf is None:
                 raise ValueError(f"light shader {st.shader!r} has no surface")
-            if surf.constant_emission() is None:
-                # the device evaluates lamp emission from the shader's constant
-                # (SD_HAS_CONSTANT_EMISSION); node-driven lamp shaders are refused
-                raise ValueError(f"light shader {st.shader!r}: only constant emission is supported")
             lamp.shader = surf
         self.lamps.append(lamp)
 

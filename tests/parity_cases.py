@@ -74,6 +74,9 @@ CASES = {
     # heterogeneous: texture-driven densities, ray marching
     "volume_cornell": lambda: scenes.volume_cornell(48, 48, 8),
     "volume_hetero": lambda: scenes.volume_cornell(32, 32, 4, heterogeneous=True),
+    # emitters with node-driven emission (direct_emissive_eval non-constant
+    # branch): textured mesh light, Light Falloff / Light Path lamp shaders
+    "emission_nodes": lambda: scenes.emission_nodes(48, 48, 8),
     # scene ingestion: a Cornell box written in the Cycles standalone XML format
     # (app/cycles_xml.cpp: transforms, state shaders, polygon meshes with UVs,
     # shader graphs with connects, lights with their own shaders, an include)

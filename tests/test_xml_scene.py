@@ -112,9 +112,6 @@ def test_background_graph_and_background_light():
     ('<mesh P="0 0 0 1 0 0 0 1 0" nverts="3" verts="0 1 5" />', "out of range"),
     ('<teapot />', "unknown node"),
     ('<integrator method="branched_path" />', "not supported"),
-    ('<shader name="l"><light_path name="lp" /><emission name="e" />'
-     '<connect from="lp is_camera_ray" to="e strength" /><connect from="e emission" to="output surface" />'
-     '</shader><state shader="l"><light type="point" /></state>', "constant emission"),
 ])
 def test_refusals_name_the_problem(body, msg):
     with pytest.raises(ValueError, match=msg):
