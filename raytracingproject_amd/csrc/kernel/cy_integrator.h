@@ -904,11 +904,15 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
  * packs) and the emitter's SVM program with PATH_RAY_EMISSION, which stores no
  * closures (shader_eval_surface: max_closures 0), so the shading point's
  * closure array in `mem` is left intact; then shader_emissive_eval
- * (kernel_shader.h, emissive_simple_eval).  ls->Ng takes the emitter's
- * (backfacing-flipped) normal as the reference's does.  Out of line: it is
- * reached from the light sample and from lamp MIS hits. */
-CY_NOINLINE cfloat3 emissive_eval_svm(const CyGlobals *kg, CyLightSample *ls, cfloat3 I, float t, CyShadeMem mem,
-                                      CyPathState state, uint *err)
+ * (kernel_shader.h, emissive_simple_eval).  The caller flips ls.Ng to the
+ * emitter's backfacing-corrected normal (ls->Ng = emission_sd->Ng), which is
+ * the same flip the constant branch makes.  Inlined: as an out-of-line call
+ * it raised the _tex shading kernels' scratch from 1.7 to 2.9 KB per lane and
+ * their renders went wrong on the GPU (non-finite films) while the host
+ * build stayed exact. */
+CY_FN cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I, int shader, int object,
+                                      int prim, int lamp, float u, float v, float t, CyShadeMem mem, CyPathState state,
+                                      uint *err)
 {
   CySD esd;
   esd.closure = mem.closure;
@@ -916,21 +920,21 @@ CY_NOINLINE cfloat3 emissive_eval_svm(const CyGlobals *kg, CyLightSample *ls, cf
   esd.svm_stride = mem.svm_stride;
   esd.svm_fast = mem.svm_fast;
   esd.svm_spill = mem.svm_spill;
-  esd.P = ls->P;
-  esd.N = ls->Ng;
-  esd.Ng = ls->Ng;
+  esd.P = P;
+  esd.N = Ng;
+  esd.Ng = Ng;
   esd.I = I;
-  esd.shader = ls->shader;
-  esd.type = (ls->prim != PRIM_NONE) ? PRIMITIVE_TRIANGLE : ((ls->lamp != LAMP_NONE) ? (1 << 6) /* PRIMITIVE_LAMP */ : 0);
-  esd.object = ls->object;
-  esd.prim = ls->prim;
-  esd.u = ls->u;
-  esd.v = ls->v;
+  esd.shader = shader;
+  esd.type = (prim != PRIM_NONE) ? PRIMITIVE_TRIANGLE : ((lamp != LAMP_NONE) ? (1 << 6) /* PRIMITIVE_LAMP */ : 0);
+  esd.object = object;
+  esd.prim = prim;
+  esd.u = u;
+  esd.v = v;
   esd.ray_length = t;
   esd.flag = kg->__shaders[(uint)esd.shader & SHADER_MASK].flags;
   esd.object_flag = (esd.object != OBJECT_NONE) ? (int)kg->__object_flag[esd.object] : 0;
   if ((esd.type & PRIMITIVE_TRIANGLE) && ((uint)esd.shader & SHADER_SMOOTH_NORMAL)) {
-    esd.N = triangle_smooth_normal(kg, ls->Ng, esd.prim, esd.u, esd.v);
+    esd.N = triangle_smooth_normal(kg, Ng, esd.prim, esd.u, esd.v);
     if (!(esd.object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
       esd.N = object_normal_transform(kg, esd.object, esd.N);
     }
@@ -940,7 +944,6 @@ CY_NOINLINE cfloat3 emissive_eval_svm(const CyGlobals *kg, CyLightSample *ls, cf
     esd.Ng = neg3(esd.Ng);
     esd.N = neg3(esd.N);
   }
-  ls->Ng = esd.Ng;
   esd.closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
   esd.closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);
   esd.svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
@@ -989,7 +992,11 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
     }
     else {
       /* a mesh light or lamp whose emission depends on its shader's nodes */
-      light_eval = emissive_eval_svm(kg, &ls, I, ls.t, mem, *state, err);
+      light_eval = emissive_eval_svm(kg, ls.P, ls.Ng, I, ls.shader, ls.object, ls.prim, ls.lamp, ls.u, ls.v, ls.t, mem,
+                                     *state, err);
+      if ((ls.prim != PRIM_NONE) && dot3(ls.Ng, I) < 0.0f) {
+        ls.Ng = neg3(ls.Ng);
+      }
     }
 #else
     else {
@@ -1267,7 +1274,8 @@ CY_FN bool shade_path(const CyGlobals *kg,
       cfloat3 lamp_L = mk3(0.0f, 0.0f, 0.0f);
       if (!shader_constant_emission_eval(kg, ls.shader, &lamp_L)) {
 #if CY_SVM_TEX
-        lamp_L = emissive_eval_svm(kg, &ls, neg3(ray.D), ls.t, mem, state, err);
+        lamp_L = emissive_eval_svm(kg, ls.P, ls.Ng, neg3(ray.D), ls.shader, ls.object, ls.prim, ls.lamp, ls.u, ls.v,
+                                   ls.t, mem, state, err);
 #else
         cy_set_error(err, CY_ERR_FEATURE, 7); /* non-constant emitter: a _tex variant scans it */
 #endif
