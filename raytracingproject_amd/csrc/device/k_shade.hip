@@ -50,10 +50,6 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_,
                                                      uint *shadow_count,
                                                      uint *err)
 {
-  /* identity block mapping: the XCD remap of the traversal kernels
-   * (cy_device_common.h) made this kernel slower, 27.6 -> 29.2 ms per frame
-   * (profiles/r03/traversal_variants_r03.jsonl) */
-  const int n_active = cam_n > 0 ? cam_n : (int)*count_in;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
 #if CY_SHADE_LDS
   /* closures (odd per-thread stride: conflict-free) and SVM stack columns in LDS */
@@ -78,7 +74,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_,
   bool cont = false, shadow = false, finished = false;
   int slot = 0;
   /* camera launch (cam_n > 0): slot slot_base + i, work item item_base + i */
-  if (i < n_active) {
+  if (cam_n > 0 ? i < cam_n : i < (int)*count_in) {
     slot = cam_n > 0 ? slot_base + i : queue_in[i];
     const uint cam_item = cam_n > 0 ? tile.item_base + (uint)i : CY_NO_ITEM;
     cont = shade_path<CY_VOLUME != 0>(&kg, &b, &tile, slot, cam_item, mem, &shadow, &finished, err);
