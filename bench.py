@@ -60,7 +60,12 @@ def parse(argv=None):
                    help="tile-mode leg: render one extra frame as TxT RenderTiles through the plugin path "
                         "(0 disables)")
     p.add_argument("--tile-batch", type=int, default=0,
-                   help="tiles rendered per device pass in the tile-mode leg (0: all tiles of the frame)")
+                   help="tile-mode leg: 0 streams the tiles into one running wavefront (hipcy_render_feed, the "
+                        "plugin's path); N > 0 renders N acquired tiles per device pass")
+    p.add_argument("--stream-hold", type=int, default=0,
+                   help="tile stream: pixel-samples the device may hold (0: device default)")
+    p.add_argument("--stream-hold-sweep", default="",
+                   help="comma-separated extra holds for more tile-stream legs (measurement)")
     p.add_argument("--profile-frame", action="store_true",
                    help="only render the instrumented single-lane frame (for rocprofv3 PMC passes)")
     p.add_argument("--other-configs", default="barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
@@ -248,11 +253,15 @@ def main():
 
     tile_leg = None
     if args.tile > 0 and world == 1:
-        # the plugin's behaviour (integration/device_hip.cpp: acquired tiles
-        # gathered up to 2^20 pixels per pass) and one tile per pass
-        tile_leg = [tile_mode(dev, ds, args.tile, args.tile_batch)]
+        # the plugin's behaviour (integration/device_hip.cpp: the session's tiles
+        # streamed into one running wavefront, at most `hold` pixel-samples held)
+        # and, for comparison, one tile per device pass
+        tile_leg = [tile_mode(dev, ds, args.tile, args.tile_batch, args.stream_hold, film)]
+        for extra in (args.stream_hold_sweep or "").split(","):
+            if extra:
+                tile_leg.append(tile_mode(dev, ds, args.tile, 0, int(extra), film))
         if args.tile_batch != 1:
-            tile_leg.append(tile_mode(dev, ds, args.tile, 1))
+            tile_leg.append(tile_mode(dev, ds, args.tile, 1, 0, film))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -394,38 +403,75 @@ def traversal_roofline(timing, counts):
     }
 
 
-def tile_mode(dev, ds, tile, batch):
+def tile_mode(dev, ds, tile, batch, hold=0, film=None):
     """One frame rendered the way a Cycles Session drives a device: the frame
-    split into tile x tile RenderTiles (session.h:84 default 64), each tile
-    rendered over all its samples into its own buffer (background mode), the
-    device acquiring `batch` tiles per pass (0: all).  Reported beside the
-    whole-frame number; not the headline value."""
+    split into tile x tile RenderTiles (session.h:84 default 64) acquired in
+    row order, each rendered over all its samples into its own buffer
+    (background mode) and copied to the host when the device releases it.
+    batch 0: the tiles are streamed into one running wavefront that never holds
+    more than `hold` pixel-samples (hipcy_render_feed, what the plugin does);
+    batch N: N acquired tiles per device pass.  Reported beside the whole-frame
+    number (with whether the tiles reassemble to its film bit for bit); not
+    the headline value."""
     import torch
 
     W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
     tiles = [(x, y, min(tile, W - x), min(tile, H - y)) for y in range(0, H, tile) for x in range(0, W, tile)]
     bufs = [torch.zeros((t[3], t[2], PS), dtype=torch.float32, device="cuda") for t in tiles]
-    batch = len(tiles) if batch <= 0 else batch
+    # each released tile goes to pinned host memory on a copy stream, without
+    # blocking the device's render thread (Session::release_tile's buffer copy)
+    host = [torch.empty((t[3], t[2], PS), dtype=torch.float32, pin_memory=True) for t in tiles]
+    copy_stream = torch.cuda.Stream()
+    batch = max(batch, 0)
 
     def frame():
         for b in bufs:
             b.zero_()
         torch.cuda.current_stream().synchronize()
-        for i in range(0, len(tiles), batch):
-            group = [(t, b.data_ptr(), -(t[0] + t[1] * t[2]), t[2]) for t, b in zip(tiles[i:i + batch],
-                                                                                    bufs[i:i + batch])]
-            dev.render_tiles(group, 0, S)
-        for b in bufs:
-            b.cpu()
+        if batch == 0:
+            nxt = [0]
 
-    frame()  # warm (per-tile pools and records are sized on first use)
+            def acquire():
+                k = nxt[0]
+                if k >= len(tiles):
+                    return None
+                nxt[0] += 1
+                t = tiles[k]
+                return t, 0, S, bufs[k].data_ptr(), -(t[0] + t[1] * t[2]), t[2], k
+
+            def release(k, _):
+                with torch.cuda.stream(copy_stream):
+                    host[k].copy_(bufs[k], non_blocking=True)
+
+            dev.render_feed(acquire, release, hold=hold)
+        else:
+            for i in range(0, len(tiles), batch):
+                group = [(t, b.data_ptr(), -(t[0] + t[1] * t[2]), t[2]) for t, b in zip(tiles[i:i + batch],
+                                                                                        bufs[i:i + batch])]
+                dev.render_tiles(group, 0, S)
+                with torch.cuda.stream(copy_stream):
+                    for k in range(i, min(i + batch, len(tiles))):
+                        host[k].copy_(bufs[k], non_blocking=True)
+        copy_stream.synchronize()
+
+    frame()  # warm (pools and records are sized on first use)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     frame()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"tile": tile, "tiles": len(tiles), "tiles_per_pass": batch,
-            "value": round(W * H * S / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(1e3 * dt, 3)}
+    res = {"tile": tile, "tiles": len(tiles), "mode": "stream" if batch == 0 else f"{batch} tile(s) per pass",
+           "value": round(W * H * S / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(1e3 * dt, 3)}
+    if batch == 0:
+        res["hold_pixel_samples"] = hold or (1 << 25)
+        st = dev.stats()
+        res["wavefront_iterations"] = int(st["iterations"])
+    if film is not None:
+        full = np.zeros((H, W, PS), dtype=np.float32)
+        for (x, y, w, h), b in zip(tiles, host):
+            full[y:y + h, x:x + w] = b.numpy()
+        res["film_bit_exact_vs_whole_frame"] = bool(np.array_equal(full.view(np.uint32), film.view(np.uint32)))
+    return res
 
 
 def other_config(spec, device_index, args):

@@ -27,6 +27,10 @@
  *                                            (one RenderTile, samples [start, start+num))
  *   hipcy_path_trace_tiles                   device_cuda_impl.cpp:2342-2391 the RENDER task's
  *                                            acquire_tile loop, several tiles per device pass
+ *   hipcy_render_feed / hipcy_set_stream_hold device_cuda_impl.cpp:2342-2391 the RENDER task's
+ *                                            acquire_tile / release_tile loop (device_task.h:157-160
+ *                                            callbacks; render/tile.cpp:498-557 next_tile shared by
+ *                                            the devices of device/device_multi.cpp:689-737)
  *   hipcy_synchronize                        device_cuda_impl.cpp:1933 cuCtxSynchronize
  *   hipcy_get_bvh_layout_mask                device/device.h:353 get_bvh_layout_mask
  *   hipcy_set_bvh_width / _leaf_merge        (device options) traverse the bound BVH2 as is, or
@@ -56,7 +60,7 @@
 extern "C" {
 #endif
 
-#define HIPCY_ABI_VERSION 5
+#define HIPCY_ABI_VERSION 6
 
 typedef struct hipcy_device hipcy_device;
 
@@ -171,6 +175,25 @@ int hipcy_path_trace_rows(hipcy_device *dev, const hipcy_work_tile *tile, int y_
  * device_task.h) and renders them together, so small tiles still fill the GPU.
  * Each tile keeps its own buffer, offset and stride. */
 int hipcy_path_trace_tiles(hipcy_device *dev, const hipcy_work_tile *tiles, int n_tiles);
+/* Tile stream: the RENDER task's acquire_tile / release_tile loop with the
+ * tiles fed to one running wavefront (hipcy_render_feed).  acquire fills
+ * *tile (and an opaque tag) and returns 1, or 0 when the queue is empty;
+ * release is called once every sample of the tile is in its buffer, from the
+ * thread that called hipcy_render_feed.  cancelled (may be NULL) stops the
+ * acquisition; tiles already acquired are finished.  hold bounds the
+ * pixel-samples the device has acquired but not finished (0: the device's
+ * hipcy_set_stream_hold value), so devices sharing one queue each take tiles
+ * only as fast as they finish them. */
+typedef struct hipcy_tile_feed {
+  void *user;
+  int (*acquire)(void *user, hipcy_work_tile *tile, uint64_t *tag);
+  void (*release)(void *user, const hipcy_work_tile *tile, uint64_t tag);
+  int (*cancelled)(void *user);
+  uint64_t hold;
+} hipcy_tile_feed;
+int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed);
+/* Default hold of tile streams, in pixel-samples (2^25). */
+int hipcy_set_stream_hold(hipcy_device *dev, uint64_t pixel_samples);
 int hipcy_synchronize(hipcy_device *dev);
 int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);
 /* flags: bit 0 = per-kernel HIP-event timings (kernels then run on one stream,

@@ -13,13 +13,18 @@
  * Semantics mirror CUDADevice (device/cuda/device_cuda_impl.cpp):
  *   MEM_GLOBAL arrays are bound by name (global_alloc, :1088-1096);
  *   RENDER tasks loop acquire_tile -> path trace -> update_progress ->
- *   release_tile on one worker thread per device (thread_run, :2342-2391);
+ *   release_tile on one worker thread per device (thread_run, :2342-2391),
+ *   the tiles streamed into one running device pass (hipcy_render_feed);
  *   the first error is sticky and reported through error_message().
  *
- * Compile-checked (g++ -fsyntax-only against the reference headers) by
- * tests/test_integration.py; it is not linked into this repository's products.
+ * Built and linked with the reference host's own device layer by
+ * tools/plugin_harness.sh and driven through DeviceTask RENDER, one or two
+ * devices on one tile queue (tests/test_plugin_harness.py); compile-checked
+ * against the reference headers by tests/test_integration.py.
  */
 #include <algorithm>
+#include <cstdlib>
+#include <deque>
 #include <vector>
 #include "device/device.h"
 #include "device/device_intern.h"
@@ -35,6 +40,12 @@
 
 CCL_NAMESPACE_BEGIN
 
+/* DEVICE_HIPCY: the DeviceType entry INTEGRATION.md adds after DEVICE_OPTIX
+ * (device/device.h:42-50).  Spelled by value so the plugin also builds against
+ * an unedited device.h (the harness); never DEVICE_CUDA, whose type checks
+ * (device_multi.cpp:112-113, device.cpp:688) would treat this device as CUDA. */
+static const DeviceType kDeviceTypeHIPCY = (DeviceType)(DEVICE_OPTIX + 1);
+
 class HIPCyclesDevice : public Device {
  public:
   HIPCyclesDevice(DeviceInfo &info, Stats &stats, Profiler &profiler, bool background)
@@ -42,6 +53,9 @@ class HIPCyclesDevice : public Device {
   {
     if (dev_ == nullptr) {
       set_error(string_printf("HIP device %d: %s", info.num, hipcy_global_error()));
+    }
+    if (const char *env = getenv("CYCLES_HIPCY_STREAM_HOLD")) {
+      hold_ = strtoull(env, nullptr, 10);
     }
   }
 
@@ -247,6 +261,9 @@ class HIPCyclesDevice : public Device {
  private:
   hipcy_device *dev_;
   DedicatedTaskPool task_pool_; /* one worker thread, as CUDADevice (device_cuda.h:45) */
+  /* pixel-samples a RENDER task may hold (0: the device default, 2^25);
+   * CYCLES_HIPCY_STREAM_HOLD overrides it */
+  uint64_t hold_ = 0;
 
   bool check(int rc)
   {
@@ -256,82 +273,76 @@ class HIPCyclesDevice : public Device {
     return rc == 0;
   }
 
-  /* Pixels of RenderTiles gathered into one device pass.  The whole BMW frame
-   * (921,600 px in 240 tiles of 64x64) fits one pass, so the slot pool stays
-   * full across tile borders instead of draining at the end of every tile. */
-  static constexpr size_t kBatchPixels = (size_t)1 << 20;
+  /* CUDADevice::thread_run RENDER branch (device_cuda_impl.cpp:2346-2386):
+   * acquire_tile -> render -> update_progress -> release_tile, with the tiles
+   * streamed into one running device pass (hipcy_render_feed).  The device
+   * asks for a tile only when its unclaimed work runs low and never holds more
+   * than `hold` pixel-samples, so devices sharing the session's TileManager
+   * queue (MultiDevice::task_add, device_multi.cpp:689-737, one cloned task per
+   * device) each take tiles as fast as they finish them; every tile is
+   * released as soon as all of its samples are in its buffer. */
+  struct Feed {
+    HIPCyclesDevice *self;
+    DeviceTask *task;
+    std::deque<RenderTile> tiles; /* acquired, indexed by the feed tag */
+  };
 
-  /* CUDADevice::thread_run RENDER branch (device_cuda_impl.cpp:2346-2386),
-   * with several acquired tiles rendered per hipcy_path_trace_tiles pass: the
-   * TileManager hands out tiles as MultiDevice would to concurrent devices,
-   * each is released after the pass that rendered it. */
+  static int feed_acquire(void *user, hipcy_work_tile *wt, uint64_t *tag)
+  {
+    Feed *f = (Feed *)user;
+    DeviceTask &task = *f->task;
+    RenderTile tile;
+    while (task.acquire_tile(f->self, tile, task.tile_types)) {
+      if (tile.task != RenderTile::PATH_TRACE) {
+        task.release_tile(tile);
+        continue;
+      }
+      wt->x = tile.x;
+      wt->y = tile.y;
+      wt->w = tile.w;
+      wt->h = tile.h;
+      wt->start_sample = tile.start_sample;
+      wt->num_samples = tile.num_samples;
+      wt->offset = tile.offset;
+      wt->stride = tile.stride;
+      wt->buffer = (uint64_t)tile.buffer;
+      *tag = f->tiles.size();
+      f->tiles.push_back(tile);
+      return 1;
+    }
+    return 0;
+  }
+
+  static void feed_release(void *user, const hipcy_work_tile *, uint64_t tag)
+  {
+    Feed *f = (Feed *)user;
+    RenderTile &t = f->tiles[tag];
+    t.sample = t.start_sample + t.num_samples;
+    f->task->update_progress(&t, t.w * t.h * t.num_samples);
+    f->task->release_tile(t);
+  }
+
+  static int feed_cancelled(void *user)
+  {
+    Feed *f = (Feed *)user;
+    return f->task->get_cancel() && !f->task->need_finish_queue;
+  }
+
   void render(DeviceTask &task)
   {
     if (!check(hipcy_load_kernels(dev_))) {
       return;
     }
-    std::vector<RenderTile> batch;
-    RenderTile tile;
-    bool more = true;
-    while (more) {
-      batch.clear();
-      size_t pixels = 0;
-      while (pixels < kBatchPixels && (more = task.acquire_tile(this, tile, task.tile_types))) {
-        if (tile.task != RenderTile::PATH_TRACE) {
-          task.release_tile(tile);
-          continue;
-        }
-        if (!batch.empty() &&
-            (tile.start_sample != batch[0].start_sample || tile.num_samples != batch[0].num_samples)) {
-          /* one pass renders one sample range: flush what is gathered */
-          if (!render_batch(task, batch)) {
-            task.release_tile(tile);
-            return;
-          }
-          batch.clear();
-          pixels = 0;
-        }
-        batch.push_back(tile);
-        pixels += (size_t)tile.w * tile.h;
-        if (task.get_cancel() && !task.need_finish_queue) {
-          break;
-        }
-      }
-      if (!batch.empty() && !render_batch(task, batch)) {
-        return;
-      }
-      if (task.get_cancel() && !task.need_finish_queue) {
-        break;
-      }
-    }
-  }
-
-  /* One pass over the gathered tiles, then progress and release per tile. */
-  bool render_batch(DeviceTask &task, std::vector<RenderTile> &batch)
-  {
-    std::vector<hipcy_work_tile> wt(batch.size());
-    for (size_t i = 0; i < batch.size(); i++) {
-      const RenderTile &t = batch[i];
-      wt[i].x = t.x;
-      wt[i].y = t.y;
-      wt[i].w = t.w;
-      wt[i].h = t.h;
-      wt[i].start_sample = t.start_sample;
-      wt[i].num_samples = t.num_samples;
-      wt[i].offset = t.offset;
-      wt[i].stride = t.stride;
-      wt[i].buffer = (uint64_t)t.buffer;
-    }
-    const bool ok = check(hipcy_path_trace_tiles(dev_, wt.data(), (int)wt.size())) &&
-                    check(hipcy_synchronize(dev_));
-    for (RenderTile &t : batch) {
-      if (ok) {
-        t.sample = t.start_sample + t.num_samples;
-        task.update_progress(&t, t.w * t.h * t.num_samples);
-      }
-      task.release_tile(t);
-    }
-    return ok;
+    Feed f;
+    f.self = this;
+    f.task = &task;
+    hipcy_tile_feed feed;
+    feed.user = &f;
+    feed.acquire = feed_acquire;
+    feed.release = feed_release;
+    feed.cancelled = feed_cancelled;
+    feed.hold = hold_;
+    check(hipcy_render_feed(dev_, &feed));
   }
 };
 
@@ -357,7 +368,7 @@ void device_hipcy_info(vector<DeviceInfo> &devices)
       continue;
     }
     DeviceInfo info;
-    info.type = DEVICE_CUDA; /* replace with DEVICE_HIPCY once the enum entry is added */
+    info.type = kDeviceTypeHIPCY;
     info.description = string(name);
     info.num = i;
     info.id = string_printf("HIPCY_%d", i);

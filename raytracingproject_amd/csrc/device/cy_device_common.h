@@ -109,6 +109,11 @@ __device__ __forceinline__ bool slot_refill(const CyGlobals &kg, const CyPathBuf
   uint item = block_claim(tile.work_next, need, lds);
   while (need) {
     if (item >= tile.n_items) {
+      if (tile.stream) {
+        /* the slot goes idle; k_stream_restart hands it work once the host
+         * has appended tiles to the lane */
+        cy_st(&b.item[slot], CY_NO_ITEM);
+      }
       return false;
     }
     if (slot_start(&kg, &b, &tile, slot, item)) {

@@ -95,6 +95,64 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
   }
 }
 
+/* ---------------------------------------------------------------------------
+ * Tile streams (hipcy_render_feed).  A lane's work items are numbered over
+ * the tiles appended to it; see stream_render for the host side. */
+
+/* One stream tile's records added to its render buffer (sample order per
+ * pixel, as k_accumulate). */
+__global__ void __launch_bounds__(CY_BLOCK) k_accumulate_stream(CyTileDesc d, const hc_float4 *ring, uint ring_mask,
+                                                                int pass_stride)
+{
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < d.w * d.h) {
+    accumulate_stream_pixel(d, ring, ring_mask, pass_stride, p);
+  }
+}
+
+/* Smallest work item held by a live path of the lane (the slots of its next
+ * queue): every item below min(this, next unclaimed item) has its record. */
+__global__ void __launch_bounds__(CY_BLOCK) k_stream_min_live(const int *queue, const uint *count, const uint *items,
+                                                              uint *out)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint v = 0xFFFFFFFFu;
+  if (i < (int)*count) {
+    v = cy_ld(&items[queue[i]]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    v = min(v, (uint)__shfl_xor(v, off));
+  }
+  __shared__ uint red[CY_BLOCK / 64];
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint m = red[0];
+    for (int w = 1; w < CY_BLOCK / 64; w++) {
+      m = min(m, red[w]);
+    }
+    if (m != 0xFFFFFFFFu) {
+      atomicMin(out, m);
+    }
+  }
+}
+
+/* Idle slots of a lane (item CY_NO_ITEM: never started, or no item was left
+ * when their path ended) claim the items the host appended since and join
+ * the lane's next closest queue. */
+__global__ void __launch_bounds__(CY_BLOCK) k_stream_restart(CyGlobals kg, CyPathBuffers b, CyTile tile, int slot_base,
+                                                             int n_slots, int *queue_out, uint *count_out)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int slot = slot_base + i;
+  const bool idle = i < n_slots && cy_ld(&b.item[slot]) == CY_NO_ITEM;
+  __shared__ uint claim[CY_CLAIM_LDS];
+  const bool started = slot_refill(kg, b, tile, slot, idle, claim);
+  queue_push(queue_out, count_out, slot, started, claim);
+}
+
 /* Traversal counters: reduced over the workgroup, then one atomic per counter
  * and workgroup into one of CY_STATS_SHARDS copies (device-scope atomics on a
  * single word serialise at the memory side).  Besides the node / leaf /
@@ -1115,6 +1173,7 @@ struct hipcy_device {
   /* wavefront buffers */
   size_t capacity = 0;
   char *pool = nullptr;
+  char *vol_pool = nullptr; /* volume stacks of the slots (volume scenes only) */
   CyPathBuffers bufs;
   int *queue[3] = {nullptr, nullptr, nullptr};
   uint *counters = nullptr; /* [3] error word; lane l: [16 + 16 l ...] (see PassLane) */
@@ -1149,6 +1208,12 @@ struct hipcy_device {
   size_t records_capacity = 0;
   CyTileDesc *tile_descs = nullptr; /* tiles of the current multi-tile pass */
   size_t tile_descs_capacity = 0;
+  /* tile streams (hipcy_render_feed): pixel-samples one device holds at most
+   * (in flight + unclaimed), and the lanes' appended tile chunks */
+  size_t stream_hold = (size_t)1 << 25;
+  CyTileDesc *stream_desc_dev = nullptr;
+  CyTileDesc *stream_desc_host = nullptr; /* pinned */
+  CyGlobals kg_stream;
 
   /* W-wide BVH widened from the bound BVH2 (rebuilt when either BVH2 array,
    * the root or the width changes) */
@@ -1321,11 +1386,12 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     hipFree(dev->pool);
     dev->pool = nullptr;
   }
-  /* 12 float4 records + 3 ints per slot (queues are separate), and the volume
-   * stack (CY_VOLUME_STACK / 2 records) and 2 volume records per slot */
+  /* 12 float4 records + 3 ints per slot (queues are separate); the volume
+   * stack and records are allocated by ensure_volume_capacity for volume
+   * scenes only */
   const size_t rec = 16 * slots;
   const size_t ints = 4 * slots;
-  const size_t total = (12 + CY_VOLUME_STACK / 2 + 2) * rec + 3 * ints + 17 * 256;
+  const size_t total = 12 * rec + 3 * ints + 15 * 256;
   HIP_CHECK(dev, hipMalloc((void **)&dev->pool, total));
   char *p = dev->pool;
   auto take = [&](size_t n) {
@@ -1348,9 +1414,13 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   dev->bufs.shadow_L = (hc_float4 *)take(rec);
   dev->bufs.shadow_T = (hc_float4 *)take(rec);
   dev->bufs.item = (uint *)take(ints);
-  dev->bufs.vol_stack = (hc_uint4 *)take((CY_VOLUME_STACK / 2) * rec);
-  dev->bufs.vol_rec = (hc_uint4 *)take(2 * rec);
   dev->capacity = slots;
+  if (dev->vol_pool) {
+    hipFree(dev->vol_pool);
+    dev->vol_pool = nullptr;
+  }
+  dev->bufs.vol_stack = nullptr;
+  dev->bufs.vol_rec = nullptr;
   /* queues live in their own allocation (3 x slots ints) */
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) {
@@ -1358,6 +1428,21 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     }
     HIP_CHECK(dev, hipMalloc((void **)&dev->queue[q], ints));
   }
+  return 0;
+}
+
+/* The per-slot volume stack (CY_VOLUME_STACK / 2 records) and 2 volume
+ * records (cy_integrator.h CyPathBuffers.vol_*), for scenes with volumes:
+ * 160 B per slot that other scenes do not pay for. */
+static int ensure_volume_capacity(hipcy_device *dev)
+{
+  if (!dev->use_volumes || dev->vol_pool) {
+    return 0;
+  }
+  const size_t rec = 16 * dev->capacity;
+  HIP_CHECK(dev, hipMalloc((void **)&dev->vol_pool, (CY_VOLUME_STACK / 2 + 2) * rec));
+  dev->bufs.vol_stack = (hc_uint4 *)dev->vol_pool;
+  dev->bufs.vol_rec = (hc_uint4 *)(dev->vol_pool + (CY_VOLUME_STACK / 2) * rec);
   return 0;
 }
 
@@ -1454,9 +1539,12 @@ void hipcy_destroy(hipcy_device *dev)
     hipEventDestroy(e);
   }
   if (dev->pool) hipFree(dev->pool);
+  if (dev->vol_pool) hipFree(dev->vol_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
   if (dev->records) hipFree(dev->records);
   if (dev->tile_descs) hipFree(dev->tile_descs);
+  if (dev->stream_desc_dev) hipFree(dev->stream_desc_dev);
+  if (dev->stream_desc_host) hipHostFree(dev->stream_desc_host);
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
@@ -2310,6 +2398,7 @@ struct PassLane {
   uint n_active;
   CyTile tile;
   hipEvent_t done;
+  bool stream = false; /* tile stream lane: also reduce the live paths' smallest item */
 };
 
 /* One iteration of a lane: closest -> shade -> shadow.  The lane's first
@@ -2442,8 +2531,16 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     HIP_CHECK(dev, hipEventRecord(p.d, s));
     quads->push_back(p);
   }
+  if (ln.stream) {
+    /* tile streams: the smallest item still held by a live path (cnt[5]) and
+     * the next unclaimed item (cnt[4]) tell the host which tiles are done */
+    HIP_CHECK(dev, hipMemsetAsync(ln.cnt + 5, 0xFF, 4, s));
+    hipLaunchKernelGGL(k_stream_min_live, grid, block, 0, s, ln.q[qb], ln.cnt + qb, dev->bufs.item, ln.cnt + 5);
+  }
   HIP_CHECK(dev, hipGetLastError());
-  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, 16, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, ln.stream ? 24 : 16, hipMemcpyDeviceToHost, s));
+  /* the kernels' error word, read with the lane's counts */
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt + 6, err, 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(dev, hipEventRecord(ln.done, s));
   return 0;
 }
@@ -2478,9 +2575,14 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     dev->sort_capacity = cap;
   }
   if (dev->trav_budget[0] > 0 && W > 2 && !kg.have_instancing && !kg.have_curves) {
-    /* continuation records: per lane two buffers of a quarter of the lane's slots */
-    const size_t cap = std::max<size_t>(65536, (n_slots / lanes + 3) / 4);
-    if (cap > dev->cont_capacity || lanes > (int)dev->cont_lanes) {
+    /* continuation records: per lane two buffers of a quarter of the lane's
+     * slots; HIPCY_CONT_CAPACITY overrides the size (tests force the
+     * buffer-full path, where a suspended traversal finishes in place) */
+    size_t cap = std::max<size_t>(65536, (n_slots / lanes + 3) / 4);
+    if (const char *env = getenv("HIPCY_CONT_CAPACITY")) {
+      cap = std::max<size_t>(1, (size_t)strtoull(env, nullptr, 10));
+    }
+    if (cap != dev->cont_capacity || lanes > (int)dev->cont_lanes) {
       if (dev->cont_rec) {
         HIP_CHECK(dev, hipFree(dev->cont_rec));
         dev->cont_rec = nullptr;
@@ -2522,32 +2624,36 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     HIP_CHECK(dev, hipMemsetAsync(L.cnt, 0, 12, L.s));
     HIP_CHECK(dev, hipMemcpyAsync(L.cnt + 4, L.hcnt + 4, 4, hipMemcpyHostToDevice, L.s));
   }
-  while (true) {
-    bool any = false;
-    for (int l = 0; l < lanes; l++) {
-      if (ln[l].n_active > 0) {
-        any = true;
-        if (lane_iterate(dev, kg, ln[l], W, ev, quads) != 0) {
-          return -1;
-        }
+  /* lanes in submission order: the oldest lane's iteration is waited for,
+   * and its next one enqueued at once, while the other lanes run */
+  int fifo[CY_LANES];
+  int head = 0, n_fifo = 0;
+  for (int l = 0; l < lanes; l++) {
+    if (ln[l].n_active > 0) {
+      if (lane_iterate(dev, kg, ln[l], W, ev, quads) != 0) {
+        return -1;
       }
+      fifo[(head + n_fifo++) % CY_LANES] = l;
     }
-    if (!any) {
+  }
+  dev->host_counters[3] = 0;
+  while (n_fifo > 0) {
+    PassLane &L = ln[fifo[head]];
+    head = (head + 1) % CY_LANES;
+    n_fifo--;
+    HIP_CHECK(dev, hipEventSynchronize(L.done));
+    dev->stats.shadow_rays += L.hcnt[2];
+    L.n_active = L.hcnt[L.qb];
+    std::swap(L.qa, L.qb);
+    if (L.hcnt[6]) {
+      dev->host_counters[3] = L.hcnt[6];
       break;
     }
-    for (int l = 0; l < lanes; l++) {
-      PassLane &L = ln[l];
-      if (L.n_active == 0) {
-        continue;
+    if (L.n_active > 0) {
+      if (lane_iterate(dev, kg, L, W, ev, quads) != 0) {
+        return -1;
       }
-      HIP_CHECK(dev, hipEventSynchronize(L.done));
-      dev->stats.shadow_rays += L.hcnt[2];
-      L.n_active = L.hcnt[L.qb];
-      std::swap(L.qa, L.qb);
-    }
-    HIP_CHECK(dev, hipMemcpy(dev->host_counters + 3, dev->counters + 3, 4, hipMemcpyDeviceToHost));
-    if (dev->host_counters[3]) {
-      break;
+      fifo[(head + n_fifo++) % CY_LANES] = L.index;
     }
   }
   /* all lanes finished: accumulate on the main stream after them */
@@ -2601,7 +2707,9 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     d.stride = tk.stride;
     d.buffer = (float *)tk.buffer;
     d.px_begin = (uint)npix;
-    d.pad = 0;
+    d.start_sample = tk.start_sample;
+    d.item_begin = 0;
+    d.num_samples = tk.num_samples;
     descs.push_back(d);
     npix += (size_t)tk.w * tk.h;
   }
@@ -2651,8 +2759,8 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     return set_error(dev, "path_trace: tile too large for 32-bit work items");
   }
   const size_t items = npix * per_pass;
-  if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_records(dev, items) != 0 ||
-      ensure_bvhw(dev) != 0) {
+  if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
+      ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }
   CyGlobals kg;
@@ -2782,6 +2890,475 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     dev->stats.shadow_lane_iters = st[1].lane_iters;
     dev->stats.shadow_wave_iters = st[1].wave_iters;
   }
+  return check_device_error(dev);
+}
+
+/* ---------------------------------------------------------------------------
+ * Tile streams: hipcy_render_feed (the RENDER task's acquire_tile loop of
+ * CUDADevice::thread_run, device_cuda_impl.cpp:2342-2391, with tiles fed to a
+ * running wavefront instead of one render per tile).
+ *
+ * Each lane keeps its own list of appended tile chunks (a RenderTile, or a
+ * sample range of one when the tile alone would overflow the lane's record
+ * ring) and numbers their work items consecutively.  After every lane
+ * iteration the host knows the lane's next unclaimed item and the smallest
+ * item a live path still holds (k_stream_min_live); every chunk below both is
+ * complete, so its records are added to its buffer (k_accumulate_stream, on the
+ * lane's stream, in chunk order) and the RenderTile is released once that has
+ * run.  The host appends tiles whenever a lane's unclaimed items fall below
+ * its slot count, so the pool stays full across tile borders and no device
+ * holds more than `hold` pixel-samples of the shared queue: with several
+ * devices on one TileManager each keeps taking tiles as fast as it finishes
+ * them.  Slots whose path ended while the lane had no item left go idle and
+ * are restarted (k_stream_restart) once tiles arrive.
+ * ------------------------------------------------------------------------- */
+struct FeedTile {
+  hipcy_work_tile t;
+  uint64_t tag;
+  int next_sample; /* first sample not yet appended to a lane */
+};
+
+struct StreamChunk {
+  CyTileDesc d;
+  uint item_end;
+  int feed;  /* FeedTile index */
+  bool last; /* the RenderTile's last chunk */
+};
+
+struct StreamLane {
+  PassLane ln;
+  int lane_slots = 0;
+  hc_float4 *ring = nullptr;
+  uint ring_cap = 0;
+  CyTileDesc *desc_dev = nullptr;
+  CyTileDesc *desc_host = nullptr; /* pinned, append-only within a session */
+  int desc_cap = 0;
+  std::vector<StreamChunk> chunks;
+  size_t done_chunks = 0; /* chunks whose accumulation is enqueued */
+  size_t lo_chunk = 0;    /* first chunk that can still hand out items */
+  uint n_items = 0;
+  uint work_next = 0;
+  uint ring_head = 0;
+  int cur_feed = -1; /* RenderTile partly appended to this lane */
+  bool closed = false;
+  std::vector<int> release; /* RenderTiles whose last accumulation is enqueued */
+};
+
+#define CY_STREAM_DESCS 16384
+#define CY_STREAM_ITEM_CAP 0xE0000000u /* 32-bit items; claims past the end overshoot by < 2^28 */
+
+struct StreamState {
+  hipcy_device *dev;
+  const hipcy_tile_feed *feed;
+  std::vector<FeedTile> tiles;
+  size_t released = 0;
+  bool feed_empty = false;
+  std::vector<int> carry; /* RenderTiles left partly appended by closed lanes */
+};
+
+static bool feed_cancelled(const StreamState &st)
+{
+  return st.feed->cancelled && st.feed->cancelled(st.feed->user);
+}
+
+/* Append chunks to the lane until it holds `target` unclaimed items (or the
+ * queue, the ring or the lane's numbering runs out). */
+static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chunk)
+{
+  hipcy_device *dev = st.dev;
+  uint unclaimed = S.n_items - std::min(S.work_next, S.n_items);
+  while (!S.closed && unclaimed < target) {
+    if (S.cur_feed < 0) {
+      if (!st.carry.empty()) {
+        S.cur_feed = st.carry.front();
+        st.carry.erase(st.carry.begin());
+      }
+      else {
+        if (st.feed_empty || feed_cancelled(st)) {
+          st.feed_empty = true;
+          break;
+        }
+        FeedTile f;
+        memset(&f.t, 0, sizeof(f.t));
+        f.tag = 0;
+        if (!st.feed->acquire(st.feed->user, &f.t, &f.tag)) {
+          st.feed_empty = true;
+          break;
+        }
+        if (f.t.w < 0 || f.t.h < 0 || (f.t.w * f.t.h > 0 && f.t.num_samples > 0 && !f.t.buffer)) {
+          return set_error(dev, "render_feed: invalid tile");
+        }
+        f.next_sample = f.t.start_sample;
+        st.tiles.push_back(f);
+        if ((size_t)f.t.w * f.t.h == 0 || f.t.num_samples <= 0) {
+          /* nothing to render: released at once */
+          st.feed->release(st.feed->user, &st.tiles.back().t, f.tag);
+          st.released++;
+          continue;
+        }
+        S.cur_feed = (int)st.tiles.size() - 1;
+      }
+    }
+    FeedTile &F = st.tiles[S.cur_feed];
+    const uint npix = (uint)(F.t.w * F.t.h);
+    if ((size_t)npix * 2 > S.ring_cap) {
+      return set_error(dev, "render_feed: tile of " + std::to_string(npix) +
+                                " pixels does not fit the record ring (raise hipcy_set_slots record_bytes)");
+    }
+    const int remaining = F.t.start_sample + F.t.num_samples - F.next_sample;
+    const int chunk_s = std::min(remaining, (int)std::max<uint>(1u, (S.ring_cap / 4) / npix));
+    const uint items = npix * (uint)chunk_s;
+    if ((uint64_t)S.n_items + items > CY_STREAM_ITEM_CAP || (int)S.chunks.size() >= S.desc_cap) {
+      S.closed = true;
+      break;
+    }
+    if ((uint64_t)S.n_items + items - S.ring_head > S.ring_cap) {
+      break; /* ring full until older tiles complete */
+    }
+    CyTileDesc d;
+    d.x = F.t.x;
+    d.y = F.t.y;
+    d.w = F.t.w;
+    d.h = F.t.h;
+    d.offset = F.t.offset;
+    d.stride = F.t.stride;
+    d.buffer = (float *)F.t.buffer;
+    d.px_begin = 0;
+    d.start_sample = F.next_sample;
+    d.item_begin = S.n_items;
+    d.num_samples = chunk_s;
+    const size_t k = S.chunks.size();
+    S.desc_host[k] = d;
+    HIP_CHECK(dev, hipMemcpyAsync(S.desc_dev + k, S.desc_host + k, sizeof(CyTileDesc), hipMemcpyHostToDevice,
+                                  S.ln.s));
+    StreamChunk c;
+    c.d = d;
+    c.item_end = S.n_items + items;
+    c.feed = S.cur_feed;
+    c.last = chunk_s == remaining;
+    S.chunks.push_back(c);
+    S.n_items += items;
+    unclaimed += items;
+    F.next_sample += chunk_s;
+    if (c.last) {
+      S.cur_feed = -1;
+    }
+    if (one_chunk) {
+      break;
+    }
+  }
+  return 0;
+}
+
+/* The lane's chunks below `bound` are complete: enqueue their accumulation. */
+static int stream_complete(StreamState &st, StreamLane &S, uint bound)
+{
+  hipcy_device *dev = st.dev;
+  const int pass_stride = dev->data_host.film.pass_stride;
+  while (S.done_chunks < S.chunks.size() && S.chunks[S.done_chunks].item_end <= bound) {
+    const StreamChunk &c = S.chunks[S.done_chunks];
+    const int npix = c.d.w * c.d.h;
+    hipLaunchKernelGGL(k_accumulate_stream, dim3((unsigned)((npix + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
+                       S.ln.s, c.d, (const hc_float4 *)S.ring, S.ring_cap - 1, pass_stride);
+    if (c.last) {
+      S.release.push_back(c.feed);
+    }
+    S.done_chunks++;
+  }
+  HIP_CHECK(dev, hipGetLastError());
+  S.ring_head = S.done_chunks < S.chunks.size() ? S.chunks[S.done_chunks].d.item_begin : S.n_items;
+  return 0;
+}
+
+static void stream_release(StreamState &st, StreamLane &S)
+{
+  for (int f : S.release) {
+    FeedTile &F = st.tiles[f];
+    st.feed->release(st.feed->user, &F.t, F.tag);
+    st.released++;
+  }
+  S.release.clear();
+}
+
+/* Hand the lane's new items to its idle slots and refresh the tile view the
+ * kernels get; n_live = the lane's live paths after its last iteration. */
+static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
+{
+  hipcy_device *dev = st.dev;
+  PassLane &L = S.ln;
+  while (S.lo_chunk < S.chunks.size() && S.chunks[S.lo_chunk].item_end <= S.work_next) {
+    S.lo_chunk++;
+  }
+  L.tile.n_items = S.n_items;
+  L.tile.n_tiles = (int)S.chunks.size();
+  L.tile.desc_lo = (uint)std::min(S.lo_chunk, S.chunks.empty() ? 0 : S.chunks.size() - 1);
+  const uint avail = S.n_items - S.work_next;
+  uint n_active = n_live;
+  if (n_live < (uint)S.lane_slots && avail > 0) {
+    hipLaunchKernelGGL(k_stream_restart, dim3((unsigned)((S.lane_slots + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
+                       L.s, st.dev->kg_stream, dev->bufs, L.tile, L.slot_base, S.lane_slots, L.q[L.qa], L.cnt + L.qa);
+    HIP_CHECK(dev, hipGetLastError());
+    n_active = (uint)std::min<uint64_t>((uint64_t)S.lane_slots, (uint64_t)n_live + avail);
+  }
+  L.n_active = n_active;
+  return 0;
+}
+
+static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t lane_slots, uint ring_cap,
+                          size_t *ev)
+{
+  hipcy_device *dev = st.dev;
+  const int lanes = CY_LANES;
+  StreamLane lane[CY_LANES];
+  /* idle marks: every slot of the pool starts without an item */
+  HIP_CHECK(dev, hipMemsetAsync(dev->bufs.item, 0xFF, lane_slots * lanes * sizeof(uint), dev->stream));
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 16 * 4 * (CY_LANES + 1), dev->stream));
+  hipEvent_t start = get_event(dev, (*ev)++);
+  HIP_CHECK(dev, hipEventRecord(start, dev->stream));
+  for (int l = 0; l < lanes; l++) {
+    StreamLane &S = lane[l];
+    PassLane &L = S.ln;
+    L.index = l;
+    L.s = dev->lane_stream[l];
+    HIP_CHECK(dev, hipStreamWaitEvent(L.s, start, 0));
+    L.slot_base = (int)(lane_slots * l);
+    L.cnt = dev->counters + 16 * (l + 1);
+    L.hcnt = dev->host_counters + 16 * (l + 1);
+    L.qa = 0;
+    L.qb = 1;
+    L.done = get_event(dev, (*ev)++);
+    L.stream = true;
+    for (int q = 0; q < 3; q++) {
+      L.q[q] = dev->queue[q] + L.slot_base;
+    }
+    S.lane_slots = (int)lane_slots;
+    S.ring = dev->records + (size_t)ring_cap * l;
+    S.ring_cap = ring_cap;
+    S.desc_dev = dev->stream_desc_dev + (size_t)CY_STREAM_DESCS * l;
+    S.desc_host = dev->stream_desc_host + (size_t)CY_STREAM_DESCS * l;
+    S.desc_cap = CY_STREAM_DESCS;
+    CyTile &t = L.tile;
+    t = CyTile();
+    t.y_step = 1;
+    t.pass_stride = dev->data_host.film.pass_stride;
+    t.stream = 1;
+    t.ring_mask = ring_cap - 1;
+    t.samples_out = S.ring;
+    t.descs = S.desc_dev;
+    t.work_next = L.cnt + 4;
+    t.item_base = 0;
+    t.aux_offset = 0;
+    t.sample_count_offset = 0;
+    t.write_aux = 0;
+    t.npix = 1;
+  }
+  /* initial fill, round robin one chunk at a time: each lane wants its slots'
+   * worth of camera rays plus as many in reserve */
+  for (bool more = true; more;) {
+    more = false;
+    for (int l = 0; l < lanes; l++) {
+      StreamLane &S = lane[l];
+      const size_t before = S.chunks.size();
+      if (stream_fill(st, S, 2 * (uint)lane_slots, true) != 0) {
+        return -1;
+      }
+      more |= S.chunks.size() > before;
+    }
+  }
+  for (int l = 0; l < lanes; l++) {
+    StreamLane &S = lane[l];
+    PassLane &L = S.ln;
+    L.cam_n = (int)std::min<uint>((uint)lane_slots, S.n_items);
+    L.n_active = (uint)L.cam_n;
+    S.work_next = (uint)L.cam_n;
+    L.tile.n_items = S.n_items;
+    L.tile.n_tiles = (int)S.chunks.size();
+    L.tile.desc_lo = 0;
+    L.hcnt[4] = S.work_next;
+    HIP_CHECK(dev, hipMemcpyAsync(L.cnt + 4, L.hcnt + 4, 4, hipMemcpyHostToDevice, L.s));
+  }
+  /* lanes in submission order (as path_trace_pass): the oldest lane is
+   * waited for, its finished tiles accumulated, tiles appended and idle slots
+   * restarted, and its next iteration enqueued while the others run */
+  int fifo[CY_LANES];
+  int head = 0, n_fifo = 0;
+  bool queued[CY_LANES] = {};
+  auto submit = [&](int l) -> int {
+    if (lane_iterate(dev, kg, lane[l].ln, W, ev, nullptr) != 0) {
+      return -1;
+    }
+    fifo[(head + n_fifo++) % CY_LANES] = l;
+    queued[l] = true;
+    return 0;
+  };
+  for (int l = 0; l < lanes; l++) {
+    if (lane[l].ln.n_active > 0 && submit(l) != 0) {
+      return -1;
+    }
+  }
+  dev->host_counters[3] = 0;
+  while (n_fifo > 0) {
+    const int l = fifo[head];
+    head = (head + 1) % CY_LANES;
+    n_fifo--;
+    queued[l] = false;
+    StreamLane &S = lane[l];
+    PassLane &L = S.ln;
+    HIP_CHECK(dev, hipEventSynchronize(L.done));
+    if (L.hcnt[6]) {
+      dev->host_counters[3] = L.hcnt[6];
+      break;
+    }
+    /* the accumulations enqueued before this iteration have run */
+    stream_release(st, S);
+    dev->stats.shadow_rays += L.hcnt[2];
+    const uint n_live = L.hcnt[L.qb];
+    uint wn = L.hcnt[4];
+    const uint live_min = L.hcnt[5];
+    if (wn > S.n_items) {
+      /* claims past the end: put the counter back so appended items are
+       * handed out from the first one */
+      wn = S.n_items;
+      L.hcnt[12] = wn;
+      HIP_CHECK(dev, hipMemcpyAsync(L.cnt + 4, L.hcnt + 12, 4, hipMemcpyHostToDevice, L.s));
+    }
+    S.work_next = wn;
+    if (stream_complete(st, S, std::min(live_min, wn)) != 0) {
+      return -1;
+    }
+    std::swap(L.qa, L.qb);
+    if (stream_fill(st, S, (uint)lane_slots, false) != 0 || stream_restart(st, S, n_live) != 0) {
+      return -1;
+    }
+    if (L.n_active > 0 && submit(l) != 0) {
+      return -1;
+    }
+    /* an idle lane takes tiles again while the queue has some */
+    for (int k = 0; k < lanes; k++) {
+      StreamLane &I = lane[k];
+      if (queued[k] || I.ln.n_active > 0 || I.closed || (st.feed_empty && st.carry.empty())) {
+        continue;
+      }
+      if (stream_fill(st, I, (uint)lane_slots, false) != 0 || stream_restart(st, I, 0) != 0) {
+        return -1;
+      }
+      if (I.ln.n_active > 0 && submit(k) != 0) {
+        return -1;
+      }
+    }
+  }
+  /* drained: every chunk is complete; run the last accumulations, then release */
+  for (int l = 0; l < lanes; l++) {
+    StreamLane &S = lane[l];
+    if (!dev->host_counters[3] && stream_complete(st, S, S.n_items) != 0) {
+      return -1;
+    }
+    HIP_CHECK(dev, hipStreamSynchronize(S.ln.s));
+    if (dev->host_counters[3]) {
+      S.release.clear();
+      continue;
+    }
+    stream_release(st, S);
+    if (S.cur_feed >= 0) {
+      st.carry.push_back(S.cur_feed); /* closed lane: the rest of this RenderTile goes on in the next session */
+    }
+  }
+  return 0;
+}
+
+/* Adaptive sampling filters each RenderTile between sample steps: those
+ * scenes are rendered one acquired tile per device pass, as CUDADevice does. */
+static int feed_per_tile(StreamState &st)
+{
+  hipcy_device *dev = st.dev;
+  while (!feed_cancelled(st)) {
+    FeedTile f;
+    memset(&f.t, 0, sizeof(f.t));
+    f.tag = 0;
+    if (!st.feed->acquire(st.feed->user, &f.t, &f.tag)) {
+      break;
+    }
+    if (path_trace(dev, &f.t, 1, 1) != 0 || hipcy_synchronize(dev) != 0) {
+      return -1;
+    }
+    st.feed->release(st.feed->user, &f.t, f.tag);
+    st.released++;
+  }
+  return 0;
+}
+
+int hipcy_set_stream_hold(hipcy_device *dev, uint64_t pixel_samples)
+{
+  dev->stream_hold = pixel_samples ? (size_t)pixel_samples : dev->stream_hold;
+  return 0;
+}
+
+int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
+{
+  if (!dev->error.empty()) {
+    return -1;
+  }
+  if (!feed || !feed->acquire || !feed->release) {
+    return set_error(dev, "render_feed: acquire and release callbacks are required");
+  }
+  if (dev->features_dirty && hipcy_load_kernels(dev) != 0) {
+    return -1;
+  }
+  HIP_CHECK(dev, hipSetDevice(dev->ordinal));
+  StreamState st;
+  st.dev = dev;
+  st.feed = feed;
+  if (dev->data_host.film.pass_adaptive_aux_buffer) {
+    return feed_per_tile(st);
+  }
+  const int lanes = CY_LANES;
+  const size_t hold = feed->hold ? (size_t)feed->hold : dev->stream_hold;
+  /* half of a lane's share in flight, half in reserve */
+  size_t lane_slots = std::min(dev->slots_wanted / lanes, std::max<size_t>(hold / (2 * lanes), 4 * CY_BLOCK));
+  lane_slots = (lane_slots + CY_BLOCK - 1) / CY_BLOCK * CY_BLOCK;
+  /* per-lane record ring: the largest power of two the record budget holds */
+  uint ring_cap = 1u << 12;
+  while ((size_t)ring_cap * 2 * sizeof(hc_float4) * lanes <= dev->record_budget && ring_cap < (1u << 30)) {
+    ring_cap <<= 1;
+  }
+  if (ensure_capacity(dev, lane_slots * lanes) != 0 || ensure_volume_capacity(dev) != 0 ||
+      ensure_records(dev, (size_t)ring_cap * lanes) != 0 || ensure_bvhw(dev) != 0) {
+    return -1;
+  }
+  if (!dev->stream_desc_dev) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->stream_desc_dev, sizeof(CyTileDesc) * CY_STREAM_DESCS * CY_LANES));
+    HIP_CHECK(dev, hipHostMalloc((void **)&dev->stream_desc_host, sizeof(CyTileDesc) * CY_STREAM_DESCS * CY_LANES,
+                                 hipHostMallocDefault));
+  }
+  CyGlobals kg;
+  build_globals(dev, &kg);
+  dev->kg_stream = kg;
+  const int W = kg.bvhw_nodes ? dev->bvh_width : 2;
+  memset(&dev->stats, 0, sizeof(dev->stats));
+  dev->stats.bvh_width = W;
+  HIP_CHECK(dev, hipMemsetAsync(dev->stats_dev, 0, 2 * CY_STATS_SHARDS * sizeof(CyStats), dev->stream));
+  /* per-kernel event timing needs one lane without overlap: not in streams */
+  const int prof = dev->profiling;
+  dev->profiling &= ~1;
+  size_t ev = 0;
+  hipEvent_t t_begin = get_event(dev, ev++);
+  HIP_CHECK(dev, hipEventRecord(t_begin, dev->stream));
+  int rc = 0;
+  do {
+    /* a session ends when every lane drained; another starts only when a lane
+     * ran out of item numbers or tile slots while the queue still had tiles */
+    rc = stream_session(st, kg, W, lane_slots, ring_cap, &ev);
+  } while (rc == 0 && !dev->host_counters[3] && (!st.feed_empty || !st.carry.empty()));
+  dev->profiling = prof;
+  if (rc != 0) {
+    return -1;
+  }
+  hipEvent_t t_end = get_event(dev, ev++);
+  HIP_CHECK(dev, hipEventRecord(t_end, dev->stream));
+  HIP_CHECK(dev, hipStreamSynchronize(dev->stream));
+  float ms = 0.0f;
+  hipEventElapsedTime(&ms, t_begin, t_end);
+  dev->stats.total_ms = ms;
   return check_device_error(dev);
 }
 

@@ -63,13 +63,16 @@ typedef struct CyPathBuffers {
 #define CY_VOP_SHADOW 2u     /* apply to the shadow ray's copy (kernel_shadow.h:22-45) */
 #define CY_VOP_BACKFACING 4u /* the surface was hit from behind (SD_BACKFACING) */
 
-/* One RenderTile of a multi-tile pass (hipcy_path_trace_tiles). */
+/* One RenderTile of a multi-tile pass (hipcy_path_trace_tiles), or of a lane's
+ * tile stream (hipcy_render_feed). */
 typedef struct CyTileDesc {
   int x, y, w, h;
   int offset, stride;
   float *buffer;
-  uint px_begin; /* first pixel of the tile in the pass's pixel numbering */
-  int pad;
+  uint px_begin;    /* first pixel of the tile in the pass's pixel numbering */
+  int start_sample; /* tile streams: the tile's first sample */
+  uint item_begin;  /* tile streams: first work item of the tile in the lane's item numbering */
+  int num_samples;  /* tile streams: samples of the tile */
 } CyTileDesc;
 
 typedef struct CyTile {
@@ -91,6 +94,13 @@ typedef struct CyTile {
   int aux_offset;
   int sample_count_offset;
   int write_aux;
+  /* Tile streams (hipcy_render_feed): work items are numbered tile by tile,
+   * each tile's samples sample-major inside it (descs[k].item_begin), and
+   * only tiles desc_lo .. n_tiles-1 can still hand out items; records live in
+   * a ring indexed by item & ring_mask (all ones for ordinary passes). */
+  int stream = 0;
+  uint desc_lo = 0;
+  uint ring_mask = 0xFFFFFFFFu;
 } CyTile;
 
 typedef struct CyStats {
@@ -421,7 +431,7 @@ CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float
     L_sum = mk3(0.0f, 0.0f, 0.0f);
   }
   float alpha = 1.0f - L_transparent;
-  cy_st(&tile->samples_out[item], mkf4(L_sum.x, L_sum.y, L_sum.z, alpha));
+  cy_st(&tile->samples_out[item & tile->ring_mask], mkf4(L_sum.x, L_sum.y, L_sum.z, alpha));
 }
 
 #define CY_NO_ITEM 0xFFFFFFFFu
@@ -458,9 +468,37 @@ CY_FN void pass_pixel(const CyTile *tile, uint p, int *x, int *y)
   }
 }
 
-/* Pixel and sample of a work item (items are numbered sample-major). */
+/* Tile of a tile stream's work item (binary search of the tiles' first items
+ * over the tiles that can still hand out items). */
+CY_FN int tile_of_item(const CyTile *tile, uint item)
+{
+  int lo = (int)tile->desc_lo, hi = tile->n_tiles - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tile->descs[mid].item_begin <= item) {
+      lo = mid;
+    }
+    else {
+      hi = mid - 1;
+    }
+  }
+  return lo;
+}
+
+/* Pixel and sample of a work item (items are numbered sample-major; in a tile
+ * stream, sample-major inside each tile). */
 CY_FN void item_pixel(const CyTile *tile, uint item, int *x, int *y, int *sample)
 {
+  if (tile->stream) {
+    const CyTileDesc &d = tile->descs[tile_of_item(tile, item)];
+    const uint local = item - d.item_begin;
+    const uint npix = (uint)(d.w * d.h);
+    const uint p = local % npix;
+    *sample = d.start_sample + (int)(local / npix);
+    *x = d.x + (int)(p % (uint)d.w);
+    *y = d.y + (int)(p / (uint)d.w);
+    return;
+  }
   const uint p = item % tile->npix;
   *sample = tile->start_sample + (int)(item / tile->npix);
   pass_pixel(tile, p, x, y);
@@ -496,7 +534,7 @@ CY_FN void item_camera_ray(const CyGlobals *kg, const CyTile *tile, uint item, u
 
 CY_FN void write_no_sample(const CyTile *tile, uint item)
 {
-  cy_st(&tile->samples_out[item], mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf("")));
+  cy_st(&tile->samples_out[item & tile->ring_mask], mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf("")));
 }
 
 /* Start work item `item` in the slot (refills after the camera launch).
@@ -828,6 +866,29 @@ CY_FN void accumulate_pixel(const CyTile *tile, int p)
     }
     if (tile->sample_count_offset) {
       buf[tile->sample_count_offset] = sc;
+    }
+  }
+  buf[0] = b0;
+  buf[1] = b1;
+  buf[2] = b2;
+  buf[3] = b3;
+}
+
+/* accumulate_pixel for pixel p of tile d of a tile stream: the tile's records
+ * of sample k sit at item d.item_begin + k * w*h + p of the lane's ring. */
+CY_FN void accumulate_stream_pixel(const CyTileDesc &d, const hc_float4 *ring, uint ring_mask, int pass_stride,
+                                   int p)
+{
+  float *buf = d.buffer + (size_t)(d.offset + d.x + p % d.w + (d.y + p / d.w) * d.stride) * pass_stride;
+  float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
+  const uint npix = (uint)(d.w * d.h);
+  for (int k = 0; k < d.num_samples; k++) {
+    const hc_float4 r = cy_ld(&ring[(d.item_begin + (uint)k * npix + (uint)p) & ring_mask]);
+    if (r.w == r.w) {
+      b0 += r.x;
+      b1 += r.y;
+      b2 += r.z;
+      b3 += r.w;
     }
   }
   buf[0] = b0;
@@ -1181,18 +1242,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
   if (as_int(is4.w) >= 0 && (as_int(is4.w) & CY_PRIM_TIE)) {
     /* near-tie of the wide traversal (hipcycles.hip k_intersect_closest):
      * re-trace with the bound BVH2 in the reference's visiting order, before
-     * the path state is loaded (little is live here).  Only hits inside the
-     * tie window can change the answer, and every box holding one starts
-     * before the window's end, so the re-trace starts with t at twice the
-     * window: the reference order of those candidates, and its t at each of
-     * their tests, are unchanged while everything farther is culled at once. */
+     * the path state is loaded (little is live here).  The re-trace starts
+     * from the ray's own t, as the reference does: a t shortened to the tie
+     * window would be rescaled by every instance push / pop on the way
+     * (bvh_instance_push leaves FLT_MAX unscaled, any other t is multiplied
+     * and divided again), so the t each candidate is tested against would
+     * drift from the reference's by a rounding -- enough to flip exactly the
+     * near-equal comparisons a tie is about (measured: 364 pixels of the BBS
+     * stand-in's instanced frame). */
     if (cam_item != CY_NO_ITEM) {
       CyPathState cs;
       cs.flag = PATH_RAY_CAMERA | PATH_RAY_MIS_SKIP | PATH_RAY_TRANSPARENT_BACKGROUND; /* path_state_init */
       ray_visibility = path_state_ray_visibility(&cs);
     }
     CyRay rt = ray;
-    rt.t = fminf(ray.t, is4.x * (1.0f + 2.0f * CY_TIE_EPS));
     CyIsect ti;
     if (bvh2_intersect<false>(kg, &rt, ray_visibility, &ti, err, nullptr, nullptr, nullptr)) {
       is4 = mkf4(ti.t, ti.u, ti.v, int_as_float(ti.prim));

@@ -205,6 +205,49 @@ class HIPDevice:
                                      ptr if isinstance(ptr, int) else ptr.ptr)
         self._check(self.lib.hipcy_path_trace_tiles(self.h, arr, len(tiles)))
 
+    def set_stream_hold(self, pixel_samples: int) -> None:
+        """Default bound on the pixel-samples a tile stream holds (hipcy_set_stream_hold)."""
+        self._check(self.lib.hipcy_set_stream_hold(self.h, int(pixel_samples)))
+
+    def render_feed(self, acquire, release, hold: int = 0, cancelled=None) -> None:
+        """The RENDER task's acquire_tile / release_tile loop over a tile stream
+        (hipcy_render_feed; device_cuda_impl.cpp:2342-2391 thread_run).
+        acquire() returns None or a tuple ((x, y, w, h), start_sample,
+        num_samples, buffer_pointer, offset, stride[, tag]); release(tag, tile)
+        is called once the tile's samples are in its buffer.  Exceptions raised
+        by the callbacks end the stream's acquisition and are re-raised."""
+        errors = []
+
+        def _acquire(user, tile_p, tag_p):
+            try:
+                t = None if errors else acquire()
+            except BaseException as e:  # noqa: BLE001 - re-raised after the stream drained
+                errors.append(e)
+                t = None
+            if t is None:
+                return 0
+            (x, y, w, h), s0, ns, ptr, offset, stride = t[:6]
+            tile_p[0] = native.WorkTile(x, y, w, h, s0, ns, offset, stride, ptr if isinstance(ptr, int) else ptr.ptr)
+            tag_p[0] = int(t[6]) if len(t) > 6 else 0
+            return 1
+
+        def _release(user, tile_p, tag):
+            t = tile_p[0]
+            try:
+                release(int(tag), (t.x, t.y, t.w, t.h, t.start_sample, t.num_samples))
+            except BaseException as e:  # noqa: BLE001
+                errors.append(e)
+
+        def _cancelled(user):
+            return 1 if (errors or (cancelled is not None and cancelled())) else 0
+
+        feed = native.TileFeed(None, native.FEED_ACQUIRE(_acquire), native.FEED_RELEASE(_release),
+                               native.FEED_CANCELLED(_cancelled), int(hold))
+        rc = self.lib.hipcy_render_feed(self.h, ctypes.byref(feed))
+        if errors:
+            raise errors[0]
+        self._check(rc)
+
     def render(self, samples: int | None = None, start_sample: int = 0, tile=None) -> np.ndarray:
         """Render (a tile of) the uploaded scene; returns the float render buffer
         [h, w, pass_stride] of the tile (buffer offset/stride as CPUDevice)."""

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # by `python -m raytracingproject_amd.build --variant NAME -D...`)
 DEVICE_LIB = os.environ.get("HIPCY_DEVICE_LIB") or os.path.join(_HERE, "libhipcycles.so")
 HOST_LIB = os.path.join(_HERE, "libhipcycles_host.so")
-ABI_VERSION = 5  # HIPCY_ABI_VERSION in include/hipcycles.h
+ABI_VERSION = 6  # HIPCY_ABI_VERSION in include/hipcycles.h
 
 
 def device_lib_path() -> str:
@@ -63,6 +63,19 @@ class WorkTile(ctypes.Structure):
     ]
 
 
+# hipcy_tile_feed callbacks: acquire(user, tile*, tag*) -> int, release(user, tile*, tag), cancelled(user) -> int
+FEED_ACQUIRE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.POINTER(ctypes.c_uint64))
+FEED_RELEASE = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.c_uint64)
+FEED_CANCELLED = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+
+class TileFeed(ctypes.Structure):
+    _fields_ = [
+        ("user", ctypes.c_void_p), ("acquire", FEED_ACQUIRE), ("release", FEED_RELEASE),
+        ("cancelled", FEED_CANCELLED), ("hold", ctypes.c_uint64),
+    ]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [
         ("closest_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
@@ -103,6 +116,8 @@ DEVICE_SYMBOLS = {
     "hipcy_path_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile)]),
     "hipcy_path_trace_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.c_int]),
     "hipcy_path_trace_tiles": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorkTile), ctypes.c_int]),
+    "hipcy_render_feed": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TileFeed)]),
+    "hipcy_set_stream_hold": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "hipcy_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

@@ -471,10 +471,21 @@ class XMLReader:
 
     def read_include(self, st: _State, src: str):
         path = os.path.join(st.base, src)
+        # a file may be included several times (e.g. under different
+        # transforms), but not from inside itself
+        real = os.path.realpath(path)
+        active = self.__dict__.setdefault("_including", [])
+        if real in active:
+            chain = " -> ".join(os.path.basename(p) for p in active + [real])
+            raise ValueError(f"{src}: include cycle ({chain})")
         root = ET.parse(path).getroot()
         if root.tag != "cycles":
             raise ValueError(f"{src}: the document element must be <cycles>")
-        self.read_scene(_State(st.tfm, st.shader, st.smooth, os.path.dirname(path)), root)
+        active.append(real)
+        try:
+            self.read_scene(_State(st.tfm, st.shader, st.smooth, os.path.dirname(path)), root)
+        finally:
+            active.pop()
 
     def read_camera(self, st: _State, el):
         a = el.attrib

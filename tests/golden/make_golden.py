@@ -17,6 +17,8 @@ and, shared by all cases:
   scale_<case>.npz  reference render of parity_cases.SCALE_CASES (full-size
                     configs on a crop) and scale_full_frame.npz (the bench
                     scene's full frame as 16x16 block means)
+  full_<config>.npz sha256 of the reference's whole float32 render buffer of a
+                    BASELINE config at full resolution (parity_cases.FULL_DIGEST_CASES)
   background.npz    reference SHADER task (SHADER_EVAL_BACKGROUND) of the worlds of
                     parity_cases.BACKGROUND_CASES (map size and sample count per case)
   abi_layout.json   sizeof/offsetof of every device-data struct field in the
@@ -27,6 +29,7 @@ from __future__ import annotations
 
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -174,6 +177,33 @@ def make_scale():
     print("full frame", buf.shape)
 
 
+def make_full_digests():
+    """Whole frames of the BASELINE configs at their full resolution, rendered
+    by the reference CPU kernel: the sha256 of the float32 render buffer (the
+    exact-parity fixture) plus 16x16 block means (printed by the GPU test on a
+    mismatch).  One npz per config (parity_cases.FULL_DIGEST_CASES); pass
+    --digest-cases=a,b to regenerate a subset."""
+    from parity_cases import FULL_DIGEST_CASES, FULL_FRAME_BLOCK, block_means, buffer_sha256
+
+    only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--digest-cases=")]
+    threads = int(os.environ.get("CY_REF_THREADS", os.cpu_count()))
+    for name, fn in FULL_DIGEST_CASES.items():
+        if only and name not in only[0]:
+            continue
+        ds = sc.compile_scene(fn())
+        rk = RefKernel(ds)
+        t0 = time.time()
+        buf = rk.render(threads=threads)
+        dt = time.time() - t0
+        rk.close()
+        np.savez_compressed(golden_path(f"full_{name}"), digest=np.array(scene_digest(ds)),
+                            sha256=np.array(buffer_sha256(buf)), shape=np.array(buf.shape),
+                            samples=np.array(ds.samples), block=np.array(FULL_FRAME_BLOCK),
+                            block_means=block_means(buf, FULL_FRAME_BLOCK).astype(np.float32))
+        print(f"full {name} {ds.width}x{ds.height}x{ds.samples}: {dt:.0f} s on {threads} threads, "
+              f"sha256 {buffer_sha256(buf)[:16]}", flush=True)
+
+
 def make_sobol():
     """The reference host's Sobol direction table (render/sobol.cpp
     sobol_generate_direction_vectors, 32 words per dimension) for as many
@@ -211,6 +241,9 @@ def make_adaptive_tiles(tile=24):
 def main():
     if "--adaptive-tiles-only" in sys.argv:
         make_adaptive_tiles()
+        return
+    if "--full-digests-only" in sys.argv:
+        make_full_digests()
         return
     if "--sobol-only" in sys.argv:
         make_sobol()

@@ -155,6 +155,22 @@ SCALE_CASES = {
 FULL_FRAME_CASE = "bmw27_standin"
 FULL_FRAME_BLOCK = 16
 
+# BASELINE configs as whole frames at full resolution, pinned exactly by the
+# sha256 of the reference's float32 render buffer (tests/golden/full_<name>.npz).
+# JNK keeps its 3840x2160 resolution at 32 spp: its 1024-spp frame (8.5 G
+# samples with 1.6 M curve segments) is days of CPU time for the reference.
+FULL_DIGEST_CASES = {
+    "bmw": lambda: scenes.bmw27_standin(),
+    "bbs": lambda: scenes.barbershop_standin(),
+    "cls": lambda: scenes.classroom_standin(),
+    "jnk32": lambda: scenes.junkshop_standin(samples=32),
+}
+
+
+def buffer_sha256(buf: np.ndarray) -> str:
+    """sha256 of a render buffer's float32 bytes (C order, H x W x pass_stride)."""
+    return hashlib.sha256(np.ascontiguousarray(buf, dtype=np.float32).tobytes()).hexdigest()
+
 
 def block_means(buf: np.ndarray, block: int) -> np.ndarray:
     h, w = buf.shape[:2]

@@ -228,3 +228,24 @@ def test_render_with_traversal_budget_matches_reference(name, width, budget, dev
         device.set_traversal_budget(0, 0)
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), (name, budget)
     assert st["closest_rays"] > 0
+
+
+@pytest.mark.parametrize("capacity", [1, 97])
+@pytest.mark.parametrize("name", ["cornell_64", "bmw_small"])
+def test_traversal_budget_with_full_continuation_buffer(name, capacity, device, monkeypatch):
+    """Continuation buffers smaller than the suspended traversals
+    (HIPCY_CONT_CAPACITY): lanes that find the buffer full finish their
+    traversal in place (cont_suspend's fallback), still bit-exact."""
+    monkeypatch.setenv("HIPCY_CONT_CAPACITY", str(capacity))
+    ds = compile_case(name)
+    g = load_golden(name)
+    device.upload_scene(ds)
+    device.set_bvh_width(4)
+    device.set_traversal_budget(1, 2)
+    try:
+        buf = device.render()
+    finally:
+        device.set_traversal_budget(0, 0)
+        monkeypatch.delenv("HIPCY_CONT_CAPACITY")
+        device.render(samples=1)  # back to the default continuation buffers
+    assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), (name, capacity)

@@ -63,3 +63,36 @@ def test_plugin_renders_through_device_task_bit_exact(tmp_path, name, tile):
     assert "released" in r.stdout
     film = np.fromfile(out, dtype=np.float32).reshape(g["buffer"].shape)
     assert np.array_equal(film.view(np.uint32), g["buffer"].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_two_plugin_devices_share_the_tile_queue_on_the_bench_frame(tmp_path):
+    """MultiDevice's pattern (device_multi.cpp:689-737): two HIPCyclesDevice
+    instances, each given a clone of the RENDER task, pulling 64x64 tiles
+    from one acquire_tile queue.  Both must take part within +-2 tiles of an
+    even split of the BMW stand-in's 240 tiles, and the frame assembled from
+    the tiles each device released must be the reference CPU kernel's full
+    frame bit for bit (its sha256, tests/golden/full_bmw.npz)."""
+    import re
+
+    from parity_cases import FULL_DIGEST_CASES, buffer_sha256
+
+    if not os.path.exists(HARNESS):
+        pytest.fail("integration/_build/plugin_harness missing: run tools/plugin_harness.sh before the GPU tests")
+    from raytracingproject_amd import scene as sc
+
+    g = load_golden("full_bmw")
+    ds = sc.compile_scene(FULL_DIGEST_CASES["bmw"]())
+    assert scene_digest(ds) == str(g["digest"])
+    write_scene_dir(ds, str(tmp_path))
+    W, H, S = int(ds.data.cam.width), int(ds.data.cam.height), int(g["samples"])
+    out = tmp_path / "film.bin"
+    r = subprocess.run([HARNESS, str(tmp_path), str(W), str(H), str(S), "64", str(ds.pass_stride), str(out), "2"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    print(r.stdout)
+    counts = [int(m) for m in re.findall(r"device \d+ tiles (\d+)", r.stdout)]
+    assert len(counts) == 2 and sum(counts) == 240, r.stdout
+    assert all(abs(c - 120) <= 2 for c in counts), counts
+    film = np.fromfile(out, dtype=np.float32).reshape(tuple(int(v) for v in g["shape"]))
+    assert buffer_sha256(film) == str(g["sha256"])

@@ -130,6 +130,24 @@ def test_include_resolves_relative_to_the_including_file(tmp_path):
     assert s.lamps[0].shader.constant_emission().tolist() == pytest.approx([1.6, 1.6, 1.6])
 
 
+def test_include_cycle_is_a_scene_error(tmp_path):
+    (tmp_path / "a.xml").write_text('<cycles><include src="b.xml" /></cycles>')
+    (tmp_path / "b.xml").write_text('<cycles><include src="a.xml" /></cycles>')
+    with pytest.raises(ValueError, match="include cycle"):
+        xml_scene.read_file(str(tmp_path / "a.xml"))
+    (tmp_path / "self.xml").write_text('<cycles><include src="./self.xml" /></cycles>')
+    with pytest.raises(ValueError, match="include cycle"):
+        xml_scene.read_file(str(tmp_path / "self.xml"))
+
+
+def test_same_file_included_twice_is_not_a_cycle(tmp_path):
+    (tmp_path / "lamp.xml").write_text('<cycles><light type="point" strength="1 1 1" /></cycles>')
+    (tmp_path / "main.xml").write_text(f'<cycles>{CAM}<include src="lamp.xml" />'
+                                       '<transform translate="1 0 0"><include src="lamp.xml" /></transform></cycles>')
+    s = xml_scene.read_file(str(tmp_path / "main.xml"))
+    assert len(s.lamps) == 2
+
+
 def test_rotate_matches_reference_formula():
     r = xml_scene._rotate(math.radians(30.0), (1.0, 2.0, 2.0))
     a = np.array([1.0, 2.0, 2.0]) / 3.0

@@ -127,10 +127,17 @@ static bool emu_traverse_impl(const CyGlobals *kg, const CyRay *ray, uint vis, C
     if (!tie) {
       return hit;
     }
-    /* near-tie: re-trace in the reference's order, as k_resolve_ties does */
+    /* near-tie: re-trace in the reference's order, as shade_path does */
     CyGlobals k2 = *kg;
     k2.bvhw_nodes = nullptr;
+#ifdef CY_EMU_SHORT_RETRACE
+    /* debugging aid: the re-trace from a t shortened to twice the tie window */
+    CyRay rt = *ray;
+    rt.t = fminf(ray->t, isect->t * (1.0f + 2.0f * CY_TIE_EPS));
+    return bvh2_intersect<any_hit>(&k2, &rt, vis, isect, err, nullptr, nullptr, nullptr, nullptr);
+#else
     return bvh2_intersect<any_hit>(&k2, ray, vis, isect, err, nullptr, nullptr, nullptr, nullptr);
+#endif
   }
   if (kg->have_curves) {
     return bvh2_intersect<any_hit, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(kg, ray, vis, isect, err, nn, nl, nt,

@@ -16,9 +16,17 @@
  *   TileManager's role) until the frame is done; release_tile counts them
  *   task_add / task_wait, then mem_copy_from of the buffer
  *
- * usage: plugin_harness <scene dir> <width> <height> <samples> <tile size> <pass stride> <out.bin>
+ * usage: plugin_harness <scene dir> <width> <height> <samples> <tile size> <pass stride> <out.bin> [devices]
  * The scene dir holds kernel_data.bin, manifest.txt ("name bytes" lines) and
  * one <name>.bin per array (written by tests/test_plugin_harness.py).
+ *
+ * With devices > 1 it does what MultiDevice does (device_multi.cpp:689-737):
+ * one HIPCyclesDevice per sub-device, each with its own scene upload and
+ * render buffer, each given a clone of the RENDER task (DeviceTask::split of a
+ * RENDER task copies it), all acquiring from the one shared tile queue; a tile
+ * is rendered into the buffer of the device that acquired it, and the frame
+ * is assembled from the tiles each device released.  Prints the tiles each
+ * device rendered.  The sub-devices share GPU 0 here (one-GPU test box).
  */
 #include <cstdio>
 #include <cstring>
@@ -33,6 +41,7 @@
 #include "render/buffers.h"
 #include "util/util_profiling.h"
 #include "util/util_stats.h"
+#include "util/util_time.h"
 
 CCL_NAMESPACE_BEGIN
 bool device_hipcy_init();
@@ -49,14 +58,55 @@ static bool read_file(const std::string &path, void *dst, size_t bytes)
   return (size_t)f.gcount() == bytes;
 }
 
+struct SubDevice {
+  Device *dev = nullptr;
+  std::vector<device_vector<uchar> *> arrays;
+  device_vector<float> *buffer = nullptr;
+  std::vector<int> tiles; /* indices of the tiles it acquired */
+};
+
+static int upload_scene(SubDevice &sd, const std::string &dir, int W, int H, int stride)
+{
+  std::vector<std::string> names;
+  std::vector<size_t> sizes;
+  {
+    std::ifstream man(dir + "/manifest.txt");
+    std::string name;
+    size_t bytes;
+    while (man >> name >> bytes) {
+      names.push_back(name);
+      sizes.push_back(bytes);
+    }
+  }
+  for (size_t i = 0; i < names.size(); i++) {
+    auto *v = new device_vector<uchar>(sd.dev, names[i].c_str(), MEM_GLOBAL);
+    uchar *p = v->alloc(sizes[i]);
+    if (!read_file(dir + "/" + names[i] + ".bin", p, sizes[i])) {
+      fprintf(stderr, "short read: %s\n", names[i].c_str());
+      return 5;
+    }
+    v->copy_to_device();
+    sd.arrays.push_back(v);
+  }
+  std::vector<char> kd(1 << 16);
+  std::ifstream kf(dir + "/kernel_data.bin", std::ios::binary);
+  kf.read(kd.data(), (std::streamsize)kd.size());
+  sd.dev->const_copy_to("__data", kd.data(), (size_t)kf.gcount());
+  sd.buffer = new device_vector<float>(sd.dev, "render_buffer", MEM_READ_WRITE);
+  sd.buffer->alloc((size_t)W * H * stride);
+  sd.buffer->zero_to_device();
+  return 0;
+}
+
 int main(int argc, char **argv)
 {
-  if (argc != 8) {
-    fprintf(stderr, "usage: %s dir width height samples tile pass_stride out.bin\n", argv[0]);
+  if (argc != 8 && argc != 9) {
+    fprintf(stderr, "usage: %s dir width height samples tile pass_stride out.bin [devices]\n", argv[0]);
     return 2;
   }
   const std::string dir = argv[1];
   const int W = atoi(argv[2]), H = atoi(argv[3]), S = atoi(argv[4]), T = atoi(argv[5]), stride = atoi(argv[6]);
+  const int ndev = argc == 9 ? atoi(argv[8]) : 1;
 
   if (!device_hipcy_init()) {
     fprintf(stderr, "no HIP device\n");
@@ -66,55 +116,27 @@ int main(int argc, char **argv)
   device_hipcy_info(infos);
   Stats stats;
   Profiler profiler;
-  Device *dev = device_hipcy_create(infos[0], stats, profiler, true);
-  if (dev->have_error()) {
-    fprintf(stderr, "create: %s\n", dev->error_message().c_str());
-    return 4;
-  }
-  printf("device: %s (%s)\n", infos[0].description.c_str(), infos[0].id.c_str());
-  DeviceRequestedFeatures features;
-  if (!dev->load_kernels(features)) {
-    fprintf(stderr, "load_kernels: %s\n", dev->error_message().c_str());
-    return 4;
-  }
-
-  /* scene arrays, bound by name (MEM_GLOBAL) */
-  std::vector<device_vector<uchar> *> arrays;
-  std::vector<std::string> names;
-  {
-    std::ifstream man(dir + "/manifest.txt");
-    std::string name;
-    size_t bytes;
-    while (man >> name >> bytes) {
-      names.push_back(name);
+  std::vector<SubDevice> subs(ndev);
+  for (int d = 0; d < ndev; d++) {
+    subs[d].dev = device_hipcy_create(infos[0], stats, profiler, true);
+    if (subs[d].dev->have_error()) {
+      fprintf(stderr, "create: %s\n", subs[d].dev->error_message().c_str());
+      return 4;
+    }
+    DeviceRequestedFeatures features;
+    if (!subs[d].dev->load_kernels(features)) {
+      fprintf(stderr, "load_kernels: %s\n", subs[d].dev->error_message().c_str());
+      return 4;
+    }
+    const int rc = upload_scene(subs[d], dir, W, H, stride);
+    if (rc) {
+      return rc;
     }
   }
-  {
-    std::ifstream man(dir + "/manifest.txt");
-    std::string name;
-    size_t bytes;
-    size_t i = 0;
-    while (man >> name >> bytes) {
-      auto *v = new device_vector<uchar>(dev, names[i++].c_str(), MEM_GLOBAL);
-      uchar *p = v->alloc(bytes);
-      if (!read_file(dir + "/" + name + ".bin", p, bytes)) {
-        fprintf(stderr, "short read: %s\n", name.c_str());
-        return 5;
-      }
-      v->copy_to_device();
-      arrays.push_back(v);
-    }
-  }
-  std::vector<char> kd(1 << 16);
-  std::ifstream kf(dir + "/kernel_data.bin", std::ios::binary);
-  kf.read(kd.data(), (std::streamsize)kd.size());
-  dev->const_copy_to("__data", kd.data(), (size_t)kf.gcount());
+  printf("device: %s (%s) x %d\n", infos[0].description.c_str(), infos[0].id.c_str(), ndev);
 
-  device_vector<float> buffer(dev, "render_buffer", MEM_READ_WRITE);
-  buffer.alloc((size_t)W * H * stride);
-  buffer.zero_to_device();
-
-  /* the TileManager's role: tiles in row order, each rendered with all samples */
+  /* the TileManager's role: tiles in row order, each rendered with all
+   * samples, handed out from one queue to whichever device asks */
   std::vector<RenderTile> tiles;
   for (int y = 0; y < H; y += T) {
     for (int x = 0; x < W; x += T) {
@@ -131,30 +153,49 @@ int main(int argc, char **argv)
       t.offset = 0;
       t.stride = W;
       t.tile_index = (int)tiles.size();
-      t.buffer = buffer.device_pointer;
       tiles.push_back(t);
     }
   }
   std::mutex mtx;
   size_t next = 0, released = 0;
   long progress = 0;
+  std::vector<int> done(tiles.size(), 0);
+  std::vector<double> t_last(ndev, 0.0);
+  const double t_start = time_dt();
   DeviceTask task(DeviceTask::RENDER);
-  task.acquire_tile = [&](Device *, RenderTile &tile, uint tile_types) {
+  task.acquire_tile = [&](Device *dev, RenderTile &tile, uint tile_types) {
     std::lock_guard<std::mutex> lock(mtx);
     if (next >= tiles.size() || !(tile_types & RenderTile::PATH_TRACE)) {
       return false;
     }
-    tile = tiles[next++];
-    return true;
+    for (SubDevice &sd : subs) {
+      if (sd.dev == dev) {
+        tile = tiles[next];
+        tile.buffer = sd.buffer->device_pointer;
+        sd.tiles.push_back((int)next);
+        next++;
+        return true;
+      }
+    }
+    return false;
   };
   task.release_tile = [&](RenderTile &tile) {
     std::lock_guard<std::mutex> lock(mtx);
     if (tile.sample != tile.start_sample + tile.num_samples) {
       fprintf(stderr, "tile %d released at sample %d\n", tile.tile_index, tile.sample);
     }
+    done[tile.tile_index]++;
     released++;
+    for (size_t d = 0; d < subs.size(); d++) {
+      if (tile.buffer == subs[d].buffer->device_pointer) {
+        t_last[d] = time_dt() - t_start;
+      }
+    }
   };
-  task.update_progress_sample = [&](long pixel_samples, int) { progress += pixel_samples; };
+  task.update_progress_sample = [&](long pixel_samples, int) {
+    std::lock_guard<std::mutex> lock(mtx);
+    progress += pixel_samples;
+  };
   task.update_tile_sample = [&](RenderTile &) {};
   task.get_cancel = [] { return false; };
   task.tile_types = RenderTile::PATH_TRACE;
@@ -167,30 +208,55 @@ int main(int argc, char **argv)
   task.h = H;
   task.offset = 0;
   task.stride = W;
-  task.buffer = buffer.device_pointer;
   task.pass_stride = stride;
 
-  dev->task_add(task);
-  dev->task_wait();
-  if (dev->have_error()) {
-    fprintf(stderr, "render: %s\n", dev->error_message().c_str());
-    return 6;
+  /* MultiDevice::task_add: a clone of the task per sub-device, then task_wait */
+  for (SubDevice &sd : subs) {
+    DeviceTask subtask = task;
+    subtask.buffer = sd.buffer->device_pointer;
+    sd.dev->task_add(subtask);
   }
-  buffer.copy_from_device(0, W * stride, H);
+  for (SubDevice &sd : subs) {
+    sd.dev->task_wait();
+    if (sd.dev->have_error()) {
+      fprintf(stderr, "render: %s\n", sd.dev->error_message().c_str());
+      return 6;
+    }
+  }
+  std::vector<float> film((size_t)W * H * stride, 0.0f);
+  for (int d = 0; d < ndev; d++) {
+    SubDevice &sd = subs[d];
+    sd.buffer->copy_from_device(0, W * stride, H);
+    for (int k : sd.tiles) {
+      const RenderTile &t = tiles[k];
+      for (int y = t.y; y < t.y + t.h; y++) {
+        memcpy(&film[((size_t)y * W + t.x) * stride], &sd.buffer->data()[((size_t)y * W + t.x) * stride],
+               sizeof(float) * t.w * stride);
+      }
+    }
+    printf("device %d tiles %zu last release %.3f s\n", d, sd.tiles.size(), t_last[d]);
+  }
+  bool once = true;
+  for (int c : done) {
+    once &= c == 1;
+  }
   printf("tiles %zu released %zu progress %ld pixel-samples\n", tiles.size(), released, progress);
-  if (released != tiles.size() || progress != (long)W * H * S) {
+  if (released != tiles.size() || !once || progress != (long)W * H * S) {
     fprintf(stderr, "tile bookkeeping mismatch\n");
     return 7;
   }
   FILE *out = fopen(argv[7], "wb");
-  fwrite(buffer.data(), sizeof(float), (size_t)W * H * stride, out);
+  fwrite(film.data(), sizeof(float), film.size(), out);
   fclose(out);
 
-  for (auto *v : arrays) {
-    v->free();
-    delete v;
+  for (SubDevice &sd : subs) {
+    for (auto *v : sd.arrays) {
+      v->free();
+      delete v;
+    }
+    sd.buffer->free();
+    delete sd.buffer;
+    delete sd.dev;
   }
-  buffer.free();
-  delete dev;
   return 0;
 }
