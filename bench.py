@@ -64,6 +64,9 @@ def parse(argv=None):
                         "plugin's path); N > 0 renders N acquired tiles per device pass")
     p.add_argument("--stream-hold", type=int, default=0,
                    help="tile stream: pixel-samples the device may hold (0: device default)")
+    p.add_argument("--render", default="frame", choices=("frame", "stream"),
+                   help="frame: the whole frame as one RenderTile (headline); stream: the frame's --tile RenderTiles "
+                        "fed to hipcy_render_feed (1 GPU; for profiling the plugin's path)")
     p.add_argument("--stream-hold-sweep", default="",
                    help="comma-separated extra holds for more tile-stream legs (measurement)")
     p.add_argument("--profile-frame", action="store_true",
@@ -164,10 +167,25 @@ def main():
     class _Buf:  # the DeviceBuffer interface render_tile needs
         ptr = local.data_ptr()
 
+    stream_tiles = [(x, y, min(args.tile or 64, W - x), min(args.tile or 64, H - y))
+                    for y in range(0, H, args.tile or 64) for x in range(0, W, args.tile or 64)]
+
     def render_frame():
         local.zero_()
         torch.cuda.current_stream().synchronize()
-        if use_tiles:
+        if args.render == "stream":
+            # the frame's RenderTiles streamed into one wavefront (the plugin's path)
+            nxt = [0]
+
+            def acquire():
+                k = nxt[0]
+                if k >= len(stream_tiles):
+                    return None
+                nxt[0] += 1
+                return stream_tiles[k], 0, S, _Buf.ptr, 0, W, k
+
+            dev.render_feed(acquire, lambda k, t: None, hold=args.stream_hold)
+        elif use_tiles:
             ts = tshards[rank]
             dev.render_tiles([(t, _Buf.ptr, ts.offset, ts.stride) for t in ts.tiles()], 0, S)
         else:

@@ -99,11 +99,13 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
  * Tile streams (hipcy_render_feed).  A lane's work items are numbered over
  * the tiles appended to it; see stream_render for the host side. */
 
-/* One stream tile's records added to its render buffer (sample order per
- * pixel, as k_accumulate). */
-__global__ void __launch_bounds__(CY_BLOCK) k_accumulate_stream(CyTileDesc d, const hc_float4 *ring, uint ring_mask,
-                                                                int pass_stride)
+/* The records of the lane's completed chunks descs[0 .. gridDim.y-1] added
+ * to their render buffers (sample order per pixel, as k_accumulate); one
+ * launch per batch of chunks completed together, blockIdx.y the chunk. */
+__global__ void __launch_bounds__(CY_BLOCK) k_accumulate_stream(const CyTileDesc *descs, const hc_float4 *ring,
+                                                                uint ring_mask, int pass_stride)
 {
+  const CyTileDesc d = descs[blockIdx.y];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < d.w * d.h) {
     accumulate_stream_pixel(d, ring, ring_mask, pass_stride, p);
@@ -111,7 +113,9 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate_stream(CyTileDesc d, co
 }
 
 /* Smallest work item held by a live path of the lane (the slots of its next
- * queue): every item below min(this, next unclaimed item) has its record. */
+ * queue): every item below min(this, next unclaimed item) has its record.
+ * Reduced per workgroup into CY_MIN_SHARDS words the host takes the minimum of. */
+#define CY_MIN_SHARDS 32
 __global__ void __launch_bounds__(CY_BLOCK) k_stream_min_live(const int *queue, const uint *count, const uint *items,
                                                               uint *out)
 {
@@ -134,7 +138,8 @@ __global__ void __launch_bounds__(CY_BLOCK) k_stream_min_live(const int *queue, 
       m = min(m, red[w]);
     }
     if (m != 0xFFFFFFFFu) {
-      atomicMin(out, m);
+      /* one of CY_MIN_SHARDS words (atomics on one word serialise) */
+      atomicMin(out + (blockIdx.x % CY_MIN_SHARDS), m);
     }
   }
 }
@@ -228,7 +233,7 @@ __device__ __forceinline__ void cont_save(const CyCont &c, uint idx, int slot, c
   r[cap] = mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(vis));
   r[2 * cap] = mkf4(is.t, is.u, is.v, int_as_float(is.prim));
   r[3 * cap] = mkf4(int_as_float(cur.code), int_as_float(cur.top | (cur.n_ring << 8) | ((int)cur.tie << 16)),
-                    int_as_float(slot), 0.0f);
+                    int_as_float(slot), cur.code_t);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if (cur.n_ring > 0) {
@@ -256,6 +261,7 @@ __device__ __forceinline__ int cont_load(const CyCont &c, uint idx, CyRay *ray, 
   is->object = OBJECT_NONE;
   is->type = is->prim != PRIM_NONE ? PRIMITIVE_TRIANGLE : 0;
   cur->code = as_int(q.x);
+  cur->code_t = q.w;
   const int packed = as_int(q.y);
   cur->top = packed & 0xFF;
   cur->n_ring = (packed >> 8) & 0xFF;
@@ -415,6 +421,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
         isect.object = OBJECT_NONE;
         isect.type = 0;
         cur.code = 0;
+        cur.code_t = 0.0f;
         cur.top = 0;
         cur.n_ring = 0;
         cur.tie = false;
@@ -583,6 +590,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
         isect.object = OBJECT_NONE;
         isect.type = 0;
         cur.code = 0;
+        cur.code_t = 0.0f;
         cur.top = 0;
         cur.n_ring = 0;
         cur.tie = false;
@@ -1213,6 +1221,8 @@ struct hipcy_device {
   size_t stream_hold = (size_t)1 << 25;
   CyTileDesc *stream_desc_dev = nullptr;
   CyTileDesc *stream_desc_host = nullptr; /* pinned */
+  uint *min_live_dev = nullptr;           /* per lane CY_MIN_SHARDS words (k_stream_min_live) */
+  uint *min_live_host = nullptr;          /* pinned copy */
   CyGlobals kg_stream;
 
   /* W-wide BVH widened from the bound BVH2 (rebuilt when either BVH2 array,
@@ -1545,6 +1555,8 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->tile_descs) hipFree(dev->tile_descs);
   if (dev->stream_desc_dev) hipFree(dev->stream_desc_dev);
   if (dev->stream_desc_host) hipHostFree(dev->stream_desc_host);
+  if (dev->min_live_dev) hipFree(dev->min_live_dev);
+  if (dev->min_live_host) hipHostFree(dev->min_live_host);
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
@@ -1910,7 +1922,8 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
                       (ctype >= CLOSURE_BSSRDF_CUBIC_ID && ctype <= CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) ? 3 :
                       (ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID ||
                        ctype == CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID ||
-                       ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID)                       ? 2 :
+                       ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID ||
+                       ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID)                 ? 2 :
                                                                                             1;
           const bool rough_diffuse = ctype == CLOSURE_BSDF_DIFFUSE_ID &&
                                      (((node.y >> 8) & 0xFF) != SVM_STACK_INVALID || node.z != 0u);
@@ -1925,8 +1938,7 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             if (off + 5 >= n) {
               return "principled BSDF: parameter nodes past __svm_nodes";
             }
-            /* GGX or multiscatter GGX: the multiscatter glass lobe of rough
-             * transmission raises CY_ERR_CLOSURE when reached (lgammaf) */
+            /* GGX or multiscatter GGX (specular layer and rough transmission) */
             if (prog[off + 2].y != CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID &&
                 prog[off + 2].y != CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID) {
               return "shader " + std::to_string(sh) + ": principled BSDF: unknown distribution " +
@@ -1952,6 +1964,7 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             case CLOSURE_BSDF_DIFFUSE_TOON_ID:
             case CLOSURE_BSDF_GLOSSY_TOON_ID:
             case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+            case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
             case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node, random walk */
               /* a random-walk BSSRDF, or a principled BSDF with subsurface (param2: linked or > 0) */
               *uses_bssrdf |= ctype == CLOSURE_BSSRDF_RANDOM_WALK_ID ||
@@ -2532,13 +2545,17 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     quads->push_back(p);
   }
   if (ln.stream) {
-    /* tile streams: the smallest item still held by a live path (cnt[5]) and
-     * the next unclaimed item (cnt[4]) tell the host which tiles are done */
-    HIP_CHECK(dev, hipMemsetAsync(ln.cnt + 5, 0xFF, 4, s));
-    hipLaunchKernelGGL(k_stream_min_live, grid, block, 0, s, ln.q[qb], ln.cnt + qb, dev->bufs.item, ln.cnt + 5);
+    /* tile streams: the smallest item still held by a live path (min_live
+     * shards) and the next unclaimed item (cnt[4]) tell the host which tiles
+     * are done */
+    uint *shards = dev->min_live_dev + CY_MIN_SHARDS * ln.index;
+    HIP_CHECK(dev, hipMemsetAsync(shards, 0xFF, CY_MIN_SHARDS * 4, s));
+    hipLaunchKernelGGL(k_stream_min_live, grid, block, 0, s, ln.q[qb], ln.cnt + qb, dev->bufs.item, shards);
+    HIP_CHECK(dev, hipMemcpyAsync(dev->min_live_host + CY_MIN_SHARDS * ln.index, shards, CY_MIN_SHARDS * 4,
+                                  hipMemcpyDeviceToHost, s));
   }
   HIP_CHECK(dev, hipGetLastError());
-  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, ln.stream ? 24 : 16, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, ln.stream ? 20 : 16, hipMemcpyDeviceToHost, s));
   /* the kernels' error word, read with the lane's counts */
   HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt + 6, err, 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(dev, hipEventRecord(ln.done, s));
@@ -3055,15 +3072,22 @@ static int stream_complete(StreamState &st, StreamLane &S, uint bound)
 {
   hipcy_device *dev = st.dev;
   const int pass_stride = dev->data_host.film.pass_stride;
+  const size_t first = S.done_chunks;
+  int max_pix = 0;
   while (S.done_chunks < S.chunks.size() && S.chunks[S.done_chunks].item_end <= bound) {
     const StreamChunk &c = S.chunks[S.done_chunks];
-    const int npix = c.d.w * c.d.h;
-    hipLaunchKernelGGL(k_accumulate_stream, dim3((unsigned)((npix + CY_BLOCK - 1) / CY_BLOCK)), dim3(CY_BLOCK), 0,
-                       S.ln.s, c.d, (const hc_float4 *)S.ring, S.ring_cap - 1, pass_stride);
+    max_pix = std::max(max_pix, c.d.w * c.d.h);
     if (c.last) {
       S.release.push_back(c.feed);
     }
     S.done_chunks++;
+  }
+  if (S.done_chunks > first) {
+    /* the completed chunks are consecutive in the lane's descriptor array */
+    hipLaunchKernelGGL(k_accumulate_stream, dim3((unsigned)((max_pix + CY_BLOCK - 1) / CY_BLOCK),
+                                                 (unsigned)(S.done_chunks - first)),
+                       dim3(CY_BLOCK), 0, S.ln.s, (const CyTileDesc *)(S.desc_dev + first),
+                       (const hc_float4 *)S.ring, S.ring_cap - 1, pass_stride);
   }
   HIP_CHECK(dev, hipGetLastError());
   S.ring_head = S.done_chunks < S.chunks.size() ? S.chunks[S.done_chunks].d.item_begin : S.n_items;
@@ -3214,7 +3238,10 @@ static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t la
     dev->stats.shadow_rays += L.hcnt[2];
     const uint n_live = L.hcnt[L.qb];
     uint wn = L.hcnt[4];
-    const uint live_min = L.hcnt[5];
+    uint live_min = 0xFFFFFFFFu;
+    for (int k = 0; k < CY_MIN_SHARDS; k++) {
+      live_min = std::min(live_min, dev->min_live_host[CY_MIN_SHARDS * l + k]);
+    }
     if (wn > S.n_items) {
       /* claims past the end: put the counter back so appended items are
        * handed out from the first one */
@@ -3329,6 +3356,8 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
     HIP_CHECK(dev, hipMalloc((void **)&dev->stream_desc_dev, sizeof(CyTileDesc) * CY_STREAM_DESCS * CY_LANES));
     HIP_CHECK(dev, hipHostMalloc((void **)&dev->stream_desc_host, sizeof(CyTileDesc) * CY_STREAM_DESCS * CY_LANES,
                                  hipHostMallocDefault));
+    HIP_CHECK(dev, hipMalloc((void **)&dev->min_live_dev, CY_MIN_SHARDS * CY_LANES * 4));
+    HIP_CHECK(dev, hipHostMalloc((void **)&dev->min_live_host, CY_MIN_SHARDS * CY_LANES * 4, hipHostMallocDefault));
   }
   CyGlobals kg;
   build_globals(dev, &kg);

@@ -217,6 +217,11 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   bool found_hit = false;
 
   bool tie = cur ? cur->tie : false; /* two hits inside the window of the current best */
+  /* a hit accepted in front of its own leaf's box entry: the triangle test's
+   * rounding (sliver triangles) put it closer than the box that holds it, so
+   * the reference, whose culling bound is not widened, may never have tested
+   * it -- resolved by the reference-order re-trace like a near-tie (sticky) */
+  bool bad = cur ? cur->tie : false;
   int iters = 0;
   /* culling bound: the best distance widened by the tie window (recomputed
    * where used rather than kept in a register) */
@@ -231,6 +236,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
 #endif
   constexpr int Q = W / 4; /* float4 per array */
   int code = cur ? cur->code : root;
+  float code_t = cur ? cur->code_t : 0.0f; /* entry distance of `code`'s box */
   if (cur) {
     cur->suspended = false;
   }
@@ -241,9 +247,10 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
        * in the private overflow arrays, which do not outlive this call) */
       if (iters >= budget && n_over == 0) {
         cur->code = code;
+        cur->code_t = code_t;
         cur->top = top;
         cur->n_ring = n_ring;
-        cur->tie = tie;
+        cur->tie = tie || bad;
         cur->suspended = true;
         break;
       }
@@ -336,6 +343,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         }
       }
       code = cc[0];
+      code_t = tn[0];
       continue;
     }
     else {
@@ -380,6 +388,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
            * call or the incoming hit -- makes the result depend on the visiting
            * order: flag the ray; a hit clearly below the current one clears it */
           tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
+          bad |= CY_EXACT_TIES && exact_ok && tt < code_t;
           if (exact_ok || !CY_TIE_EXACT_OK) {
             /* the reference's acceptance test at the exact bound */
             isect->prim = prim_addr;
@@ -426,6 +435,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         n_ring--;
         const CyStackEntry e = ring[top * CY_RING_STRIDE];
         code = e.node;
+        code_t = e.t;
         if (e.t <= CY_T_BOX) {
           found = true;
           break;
@@ -442,7 +452,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
 
 #undef CY_T_CULL
 #undef CY_T_BOX
-  if (tie_out && tie) {
+  if (tie_out && (tie || bad)) {
     *tie_out = true;
   }
   if (cnt_nodes) {
@@ -508,6 +518,8 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
   constexpr int Q = W / 4;
 
   int code = 0; /* next node or leaf to visit (root) */
+  float code_t = 0.0f, leaf_t = 0.0f; /* their boxes' entry distances (see bvhw_traverse `bad`) */
+  bool bad = false;
   bool have_code = true;
   int leaf = 0; /* parked leaf */
   bool have_leaf = false;
@@ -532,6 +544,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
       const CyStackEntry e = ring[top * CY_RING_STRIDE];
       if (e.t <= CY_T_BOX) {
         code = e.node;
+        code_t = e.t;
         return true;
       }
     }
@@ -546,6 +559,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
       }
       if (code < 0) {
         leaf = code;
+        leaf_t = code_t;
         have_leaf = true;
         have_code = pop();
         continue;
@@ -600,6 +614,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
         }
       }
       code = cc[0];
+      code_t = tn[0];
     }
 
     /* leaf phase: the parked leaves of the wave together */
@@ -642,6 +657,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
             break;
           }
           tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
+          bad |= CY_EXACT_TIES && exact_ok && tt < leaf_t;
           if (exact_ok || !CY_TIE_EXACT_OK) {
             isect->prim = prim_addr;
             isect->object = OBJECT_NONE;
@@ -661,7 +677,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
 out:
 #undef CY_T_CULL
 #undef CY_T_BOX
-  if (tie_out && tie) {
+  if (tie_out && (tie || bad)) {
     *tie_out = true;
   }
   if (cnt_nodes) {

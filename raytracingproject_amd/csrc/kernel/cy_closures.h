@@ -1659,6 +1659,10 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
     case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
       label = bsdf_microfacet_multi_ggx_sample(sd, sc, sd->I, eval, omega_in, pdf);
       break;
+    case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
+    case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID:
+      label = bsdf_microfacet_multi_ggx_glass_sample(sd, sc, sd->I, randu, eval, omega_in, pdf);
+      break;
     case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
       label = bsdf_ashikhmin_velvet_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
@@ -1737,6 +1741,10 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
       case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
         eval = bsdf_microfacet_multi_ggx_eval_reflect(sd, sc, sd->I, omega_in, pdf);
         break;
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID:
+        eval = bsdf_microfacet_multi_ggx_glass_eval(sd, sc, sd->I, omega_in, pdf, true);
+        break;
       case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
         eval = bsdf_ashikhmin_velvet_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
@@ -1779,6 +1787,10 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
       case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
         *pdf = 0.0f;
         eval = mk3(0.0f, 0.0f, 0.0f);
+        break;
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID:
+        eval = bsdf_microfacet_multi_ggx_glass_eval(sd, sc, sd->I, omega_in, pdf, false);
         break;
 #endif
       default:

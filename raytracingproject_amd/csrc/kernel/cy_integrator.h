@@ -882,8 +882,30 @@ CY_FN void accumulate_stream_pixel(const CyTileDesc &d, const hc_float4 *ring, u
   float *buf = d.buffer + (size_t)(d.offset + d.x + p % d.w + (d.y + p / d.w) * d.stride) * pass_stride;
   float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
   const uint npix = (uint)(d.w * d.h);
-  for (int k = 0; k < d.num_samples; k++) {
-    const hc_float4 r = cy_ld(&ring[(d.item_begin + (uint)k * npix + (uint)p) & ring_mask]);
+  const uint first = d.item_begin + (uint)p;
+  /* the records of 8 samples are requested before they are added (in
+   * sample order): a tile has few pixels, so each thread needs several
+   * loads in flight */
+  constexpr int U = 8;
+  int k = 0;
+  for (; k + U <= d.num_samples; k += U) {
+    hc_float4 r[U];
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      r[j] = cy_ld(&ring[(first + (uint)(k + j) * npix) & ring_mask]);
+    }
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      if (r[j].w == r[j].w) {
+        b0 += r[j].x;
+        b1 += r[j].y;
+        b2 += r[j].z;
+        b3 += r[j].w;
+      }
+    }
+  }
+  for (; k < d.num_samples; k++) {
+    const hc_float4 r = cy_ld(&ring[(first + (uint)k * npix) & ring_mask]);
     if (r.w == r.w) {
       b0 += r.x;
       b1 += r.y;

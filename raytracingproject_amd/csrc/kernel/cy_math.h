@@ -971,6 +971,143 @@ CY_FN float cy_logf(float x)
 }
 #endif
 
+/* libm lgammaf as the reference reaches it through beta() (util_math.h:
+ * expf(lgammaf(x) + lgammaf(y) - lgammaf(x + y))) in the multiscatter GGX
+ * glass closure (bsdf_microfacet_multi_impl.h mf_eval, MF_MULTI_GLASS).
+ * glibc 2.35's lgammaf is fdlibm's float algorithm
+ * (sysdeps/ieee754/flt-32/e_lgammaf_r.c): rational / polynomial fits around
+ * the minimum (tc), on [0.9, 2), the recurrence lgamma(x) = log((x-1)(x-2)..)
+ * + lgamma(frac) on [2, 8) and Stirling's series above; its published
+ * coefficients are restated here in its evaluation order (float, no FMA), with
+ * logf from cy_logf.  Positive x only (beta's arguments are >= 0.9999 there);
+ * every float of [2^-40, 2^26] agrees with the container's libm
+ * (tests/test_kernel_math.py). */
+#if defined(CY_HOST_LIBM_SINCOS)
+CY_FN float cy_lgammaf(float x)
+{
+  return lgammaf(x);
+}
+#else
+CY_FN float cy_lgammaf_poly(float x, int i, float y, float r)
+{
+  if (i == 0) {
+    const float z = y * y;
+    const float p1 = 0.0772156641f +
+                     z * (0.0673523024f +
+                          z * (0.007385551f + z * (0.00119270768f + z * (0.000220862785f + z * 2.52144564e-05f))));
+    const float p2 = z * (0.322467029f +
+                          z * (0.0205808077f +
+                               z * (0.00289051374f + z * (0.000510069774f + z * (0.000108011569f + z * 4.48640967e-05f)))));
+    const float p = y * p1 + p2;
+    return r + (p - 0.5f * y);
+  }
+  if (i == 1) {
+    const float z = y * y;
+    const float w = z * y;
+    const float p1 = 0.483836114f + w * (-0.0327885412f + w * (0.00610053865f + w * (-0.0014034647f + w * 0.00031563206f)));
+    const float p2 = -0.147587717f + w * (0.0179706756f + w * (-0.00368452026f + w * (0.000881081854f + w * -0.000312754157f)));
+    const float p3 = 0.0646249428f + w * (-0.0103142243f + w * (0.00225964771f + w * (-0.000538595312f + w * 0.000335529185f)));
+    const float p = z * p1 - (6.69710065e-09f - w * (p2 + y * p3));
+    return r + (-0.121486284f + p);
+  }
+  const float p1 = y * (-0.0772156641f +
+                        y * (0.632827044f + y * (1.45492256f + y * (0.977717519f + y * (0.228963733f + y * 0.0133810919f)))));
+  const float p2 = 1.0f + y * (2.45597792f + y * (2.12848973f + y * (0.769285142f + y * (0.104222648f + y * 0.00321709248f))));
+  return r + (-0.5f * y + p1 / p2);
+}
+
+CY_FN float cy_lgammaf(float x)
+{
+  const int hx = as_int(x);
+  const int ix = hx & 0x7fffffff;
+  if (ix >= 0x7f800000) {
+    return x * x;
+  }
+  if (hx <= 0) {
+    return (x - x) / (x - x); /* x <= 0: not reached by beta() */
+  }
+  const float tc = 1.46163213f; /* 0x3fbb16c3, the minimum of gamma */
+  if (ix < 0x30800000) {
+    return -cy_logf(x); /* |x| < 2^-30 */
+  }
+  if (ix == 0x3f800000 || ix == 0x40000000) {
+    return 0.0f;
+  }
+  if (ix < 0x40000000) {
+    /* x < 2 */
+    if (ix <= 0x3f666666) {
+      /* lgamma(x) = lgamma(x+1) - log(x) */
+      const float r = -cy_logf(x);
+      if (ix >= 0x3f3b4a20) {
+        return cy_lgammaf_poly(x, 0, 1.0f - x, r);
+      }
+      if (ix >= 0x3e6d3308) {
+        return cy_lgammaf_poly(x, 1, x - (tc - 1.0f), r);
+      }
+      return cy_lgammaf_poly(x, 2, x, r);
+    }
+    if (ix >= 0x3fdda618) {
+      return cy_lgammaf_poly(x, 0, 2.0f - x, 0.0f);
+    }
+    if (ix >= 0x3f9da620) {
+      return cy_lgammaf_poly(x, 1, x - tc, 0.0f);
+    }
+    return cy_lgammaf_poly(x, 2, x - 1.0f, 0.0f);
+  }
+  if (ix < 0x41000000) {
+    /* 2 <= x < 8: lgamma(i + y) = lgamma(1 + y) + log((y+1)(y+2)..(y+i-1)) */
+    const int i = (int)x;
+    const float y = x - (float)i;
+    const float p = y * (-0.0772156641f +
+                         y * (0.21498242f +
+                              y * (0.325778782f + y * (0.146350473f + y * (0.0266422704f + y * (0.00184028456f +
+                                                                                                  y * 3.1947533e-05f))))));
+    const float q = 1.0f + y * (1.39200532f +
+                                y * (0.72193557f +
+                                     y * (0.17193386f + y * (0.0186459199f + y * (0.000777942478f + y * 7.32668423e-06f)))));
+    float r = 0.5f * y + p / q;
+    float z = 1.0f;
+    switch (i) {
+      case 7:
+        z *= (y + 6.0f);
+        /* fall through */
+      case 6:
+        z *= (y + 5.0f);
+        /* fall through */
+      case 5:
+        z *= (y + 4.0f);
+        /* fall through */
+      case 4:
+        z *= (y + 3.0f);
+        /* fall through */
+      case 3:
+        z *= (y + 2.0f);
+        r += cy_logf(z);
+        break;
+    }
+    return r;
+  }
+  if (ix < 0x4c800000) {
+    /* 8 <= x < 2^26: Stirling */
+    const float t = cy_logf(x);
+    const float z = 1.0f / x;
+    const float y = z * z;
+    const float w = 0.418938547f +
+                    z * (0.0833333358f +
+                         y * (-0.00277777785f +
+                              y * (0.000793650572f + y * (-0.000595187536f + y * (0.000836339896f + y * -0.0016309293f)))));
+    return (x - 0.5f) * (t - 1.0f) + w;
+  }
+  return x * (cy_logf(x) - 1.0f);
+}
+#endif
+
+/* util_math.h beta(): the reference's expf / lgammaf (glibc) */
+CY_FN float cy_beta(float x, float y)
+{
+  return cy_expf(cy_lgammaf(x) + cy_lgammaf(y) - cy_lgammaf(x + y));
+}
+
 /* libm atan2f as the reference calls it in direction_to_equirectangular
  * (kernel_projection.h:56-65, background MIS pdf).  glibc 2.35 atan2f/atanf are
  * fdlibm's float algorithms (sysdeps/ieee754/flt-32/e_atan2f.c, s_atanf.c),

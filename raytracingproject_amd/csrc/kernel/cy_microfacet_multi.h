@@ -12,11 +12,18 @@
  *                                                (MF_MULTI_GLOSSY instantiation)
  *   setups, eval_reflect, sample                 closure/bsdf_microfacet_multi.h:365-533
  *
- * The glass instantiation (MULTI_GGX_GLASS, used by the Glass BSDF's
- * multiscatter distribution and the Principled BSDF's rough transmission)
- * evaluates refraction through beta() = expf(lgammaf(x) + lgammaf(y) -
- * lgammaf(x + y)) (util_math.h): glibc 2.35's lgammaf is not restated here,
- * so those closures stay refused (load_kernels / CY_ERR_CLOSURE).
+ *   mf_sample_phase_glass / mf_eval_phase_glass,
+ *   mf_ggx_transmission_albedo, mf_glass_pdf     closure/bsdf_microfacet_multi.h:138-190, 278-351
+ *   mf_eval_glass / mf_sample_glass              closure/bsdf_microfacet_multi_impl.h
+ *                                                (MF_MULTI_GLASS instantiation)
+ *   glass setups, eval_reflect / _transmit,
+ *   sample                                       closure/bsdf_microfacet_multi.h:537-731
+ *
+ * The glass instantiation (the Glass BSDF's multiscatter distribution and
+ * the Principled BSDF's default rough transmission) evaluates the analytic
+ * single-scattering transmission through beta() = expf(lgammaf(x) +
+ * lgammaf(y) - lgammaf(x + y)) (util_math.h), with glibc's lgammaf restated
+ * in cy_math.h (cy_lgammaf).
  *
  * Arithmetic follows the reference's scalar float3 operators (no SSE,
  * -ffp-contract=off): every product and sum in the reference's order.
@@ -483,6 +490,363 @@ CY_FN int bsdf_microfacet_multi_ggx_sample(const CySD *sd,
   *eval = mul3f(*eval, *pdf);
   *omega_in = add3(add3(mul3f(X, localO.x), mul3f(Y, localO.y)), mul3f(Z, localO.z));
   return LABEL_REFLECT | LABEL_GLOSSY;
+}
+
+/* ---------------------------------------------------------------------------
+ * Multiscattering GGX glass */
+
+/* bsdf_microfacet_multi.h:140-153: reflection or refraction through the
+ * microfacet, by the dielectric fresnel term */
+CY_FN cfloat3 mf_sample_phase_glass(cfloat3 wi, float eta, cfloat3 wm, float randV, bool *outside)
+{
+  const float cosI = dot3(wi, wm);
+  const float f = fresnel_dielectric_cos(cosI, eta);
+  if (randV < f) {
+    *outside = true;
+    return add3(neg3(wi), mul3f(mul3f(wm, 2.0f), cosI));
+  }
+  *outside = false;
+  const float inv_eta = 1.0f / eta;
+  const float cosT = -safe_sqrtf(1.0f - (1.0f - cosI * cosI) * inv_eta * inv_eta);
+  return normalize3(sub3(mul3f(wm, cosI * inv_eta + cosT), mul3f(wi, inv_eta)));
+}
+
+/* bsdf_microfacet_multi.h:155-190 (the float3 result has three equal components) */
+CY_FN float mf_eval_phase_glass(cfloat3 w, float lambda, cfloat3 wo, bool wo_outside, float alpha, float eta)
+{
+  if (w.z > 0.9999f) {
+    return 0.0f;
+  }
+  const float pArea = (w.z < -0.9999f) ? 1.0f : lambda * w.z;
+  float v;
+  if (wo_outside) {
+    const cfloat3 wh = normalize3(sub3(wo, w));
+    if (wh.z < 0.0f) {
+      return 0.0f;
+    }
+    const float dotW_WH = dot3(neg3(w), wh);
+    v = fresnel_dielectric_cos(dotW_WH, eta) * cmax(0.0f, dotW_WH) * D_ggx(wh, alpha) * 0.25f / (pArea * dotW_WH);
+  }
+  else {
+    cfloat3 wh = normalize3(sub3(mul3f(wo, eta), w));
+    if (wh.z < 0.0f) {
+      wh = neg3(wh);
+    }
+    const float dotW_WH = dot3(neg3(w), wh), dotWO_WH = dot3(wo, wh);
+    if (dotW_WH < 0.0f) {
+      return 0.0f;
+    }
+    const float temp = dotW_WH + eta * dotWO_WH;
+    v = (1.0f - fresnel_dielectric_cos(dotW_WH, eta)) * cmax(0.0f, dotW_WH) * cmax(0.0f, -dotWO_WH) *
+        D_ggx(wh, alpha) / (pArea * temp * temp);
+  }
+  return v;
+}
+
+/* bsdf_microfacet_multi.h:278-293 */
+CY_FN float mf_ggx_transmission_albedo(float a, float ior)
+{
+  if (ior < 1.0f) {
+    ior = 1.0f / ior;
+  }
+  a = saturate(a);
+  ior = cclamp(ior, 1.0f, 3.0f);
+  const float I_1 = 0.0476898f * cy_expf(-0.978352f * (ior - 0.65657f) * (ior - 0.65657f)) - 0.033756f * ior +
+                    0.993261f;
+  const float R_1 = (((0.116991f * a - 0.270369f) * a + 0.0501366f) * a - 0.00411511f) * a + 1.00008f;
+  const float I_2 = (((-2.08704f * ior + 26.3298f) * ior - 127.906f) * ior + 292.958f) * ior - 287.946f +
+                    199.803f / (ior * ior) - 101.668f / (ior * ior * ior);
+  const float R_2 = ((((5.3725f * a - 24.9307f) * a + 22.7437f) * a - 3.40751f) * a + 0.0986325f) * a + 0.00493504f;
+  return saturate(1.0f + I_2 * R_2 * 0.0019127f - (1.0f - I_1) * (1.0f - R_1) * 9.3205f);
+}
+
+/* bsdf_microfacet_multi.h:320-351 */
+CY_FN float mf_glass_pdf(cfloat3 wi, cfloat3 wo, float alpha, float eta)
+{
+  const bool reflective = (wi.z * wo.z > 0.0f);
+  float wh_len;
+  cfloat3 wh = normalize_len3(add3(wi, reflective ? wo : mul3f(wo, eta)), &wh_len);
+  if (wh.z < 0.0f) {
+    wh = neg3(wh);
+  }
+  const cfloat3 r_wi = (wi.z < 0.0f) ? neg3(wi) : wi;
+  const float lambda = mf_lambda(r_wi, alpha, alpha);
+  const float D = D_ggx(wh, alpha);
+  const float fresnel = fresnel_dielectric_cos(dot3(r_wi, wh), eta);
+  const float multiscatter = fabsf(wo.z * CY_1_PI_F);
+  if (reflective) {
+    const float singlescatter = 0.25f * D / cmax((1.0f + lambda) * r_wi.z, 1e-7f);
+    const float albedo = mf_ggx_albedo(alpha);
+    return fresnel * (albedo * singlescatter + (1.0f - albedo) * multiscatter);
+  }
+  const float singlescatter = fabsf(dot3(r_wi, wh) * dot3(wo, wh) * D * eta * eta /
+                                    cmax((1.0f + lambda) * r_wi.z * wh_len * wh_len, 1e-7f));
+  const float albedo = mf_ggx_transmission_albedo(alpha, eta);
+  return (1.0f - fresnel) * (albedo * singlescatter + (1.0f - albedo) * multiscatter);
+}
+
+/* bsdf_microfacet_multi_impl.h:28-182, MF_MULTI_GLASS (isotropic: alpha_y ==
+ * alpha_x after the glass setups) */
+CY_FN cfloat3 mf_eval_glass(cfloat3 wi,
+                            cfloat3 wo,
+                            const bool wo_outside,
+                            const cfloat3 color,
+                            const float alpha,
+                            uint *lcg_state,
+                            const float eta,
+                            bool use_fresnel,
+                            const cfloat3 cspec0)
+{
+  bool swapped = false;
+  if (wi.z * wo.z < 0.0f) {
+    /* transmission: the directions swap hemispheres */
+    if (-wo.z < wi.z) {
+      swapped = true;
+      const cfloat3 tmp = neg3(wo);
+      wo = neg3(wi);
+      wi = tmp;
+    }
+  }
+  else if (wo.z < wi.z) {
+    swapped = true;
+    const cfloat3 tmp = wo;
+    wo = wi;
+    wi = tmp;
+  }
+  if (wi.z < 1e-5f || (wo.z < 1e-5f && wo_outside) || (wo.z > -1e-5f && !wo_outside)) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  float lambda_r = mf_lambda(neg3(wi), alpha, alpha);
+  const float shadowing_lambda = mf_lambda(wo_outside ? wo : neg3(wo), alpha, alpha);
+
+  /* single scattering, analytically */
+  cfloat3 throughput = mk3(1.0f, 1.0f, 1.0f);
+  const cfloat3 wh = normalize3(add3(wi, wo));
+  const float v0 = mf_eval_phase_glass(neg3(wi), lambda_r, wo, wo_outside, alpha, eta);
+  cfloat3 eval = mk3(v0, v0, v0);
+  if (wo_outside) {
+    eval = mul3f(eval, -lambda_r / (shadowing_lambda - lambda_r));
+  }
+  else {
+    eval = mul3f(eval, -lambda_r * cy_beta(-lambda_r, shadowing_lambda + 1.0f));
+  }
+
+  const float F0 = fresnel_dielectric_cos(1.0f, eta);
+  if (use_fresnel) {
+    throughput = interpolate_fresnel_color(wi, wh, eta, F0, cspec0);
+    eval = mul3(eval, throughput);
+  }
+
+  cfloat3 wr = neg3(wi);
+  float hr = 1.0f;
+  float C1_r = 1.0f;
+  float G1_r = 0.0f;
+  bool outside = true;
+
+  for (int order = 0; order < 10; order++) {
+    float height_rand = lcg_step_float(lcg_state);
+    if (!mf_sample_height(wr, &hr, &C1_r, &G1_r, &lambda_r, height_rand)) {
+      break;
+    }
+    float vndf_rand_y = lcg_step_float(lcg_state);
+    float vndf_rand_x = lcg_step_float(lcg_state);
+    cfloat3 wm = mf_sample_vndf(neg3(wr), alpha, alpha, vndf_rand_x, vndf_rand_y);
+
+    if (order == 0 && use_fresnel) {
+      /* with the fresnel tint the first bounce replaces the analytic term */
+      const float p = outside ? mf_eval_phase_glass(wr, lambda_r, wo, wo_outside, alpha, eta) :
+                                mf_eval_phase_glass(wr, lambda_r, neg3(wo), !wo_outside, alpha, 1.0f / eta);
+      eval = mul3f(mul3(throughput, mk3(p, p, p)),
+                   mf_G1(wo_outside ? wo : neg3(wo), mf_C1((outside == wo_outside) ? hr : -hr), shadowing_lambda));
+    }
+    if (order > 0) {
+      const float p = outside ? mf_eval_phase_glass(wr, lambda_r, wo, wo_outside, alpha, eta) :
+                                mf_eval_phase_glass(wr, lambda_r, neg3(wo), !wo_outside, alpha, 1.0f / eta);
+      eval = add3(eval, mul3f(mul3(throughput, mk3(p, p, p)),
+                              mf_G1(wo_outside ? wo : neg3(wo), mf_C1((outside == wo_outside) ? hr : -hr),
+                                    shadowing_lambda)));
+    }
+    if (order + 1 < 10) {
+      /* bounce from the microfacet */
+      bool next_outside;
+      const cfloat3 wi_prev = neg3(wr);
+      const float phase_rand = lcg_step_float(lcg_state);
+      wr = mf_sample_phase_glass(neg3(wr), outside ? eta : 1.0f / eta, wm, phase_rand, &next_outside);
+      if (!next_outside) {
+        outside = !outside;
+        wr = neg3(wr);
+        hr = -hr;
+      }
+      if (use_fresnel && !next_outside) {
+        throughput = mul3(throughput, color);
+      }
+      else if (use_fresnel && order > 0) {
+        throughput = mul3(throughput, interpolate_fresnel_color(wi_prev, wm, eta, F0, cspec0));
+      }
+      lambda_r = mf_lambda(wr, alpha, alpha);
+      if (!use_fresnel) {
+        throughput = mul3(throughput, color);
+      }
+      C1_r = mf_C1(hr);
+      G1_r = mf_G1(wr, C1_r, lambda_r);
+    }
+  }
+  if (swapped) {
+    eval = mul3f(eval, fabsf(wi.z / wo.z));
+  }
+  return eval;
+}
+
+/* bsdf_microfacet_multi_impl.h:188-274, MF_MULTI_GLASS */
+CY_FN cfloat3 mf_sample_glass(cfloat3 wi,
+                              cfloat3 *wo,
+                              const cfloat3 color,
+                              const float alpha,
+                              uint *lcg_state,
+                              const float eta,
+                              bool use_fresnel,
+                              const cfloat3 cspec0)
+{
+  cfloat3 throughput = mk3(1.0f, 1.0f, 1.0f);
+  cfloat3 wr = neg3(wi);
+  float lambda_r = mf_lambda(wr, alpha, alpha);
+  float hr = 1.0f;
+  float C1_r = 1.0f;
+  float G1_r = 0.0f;
+  bool outside = true;
+
+  const float F0 = fresnel_dielectric_cos(1.0f, eta);
+  if (use_fresnel) {
+    /* normalize(wi + wr) of opposite vectors: NaN, as in the reference */
+    throughput = interpolate_fresnel_color(wi, normalize3(add3(wi, wr)), eta, F0, cspec0);
+  }
+
+  for (int order = 0; order < 10; order++) {
+    float height_rand = lcg_step_float(lcg_state);
+    if (!mf_sample_height(wr, &hr, &C1_r, &G1_r, &lambda_r, height_rand)) {
+      /* the walk left the surface */
+      *wo = outside ? wr : neg3(wr);
+      return throughput;
+    }
+    float vndf_rand_y = lcg_step_float(lcg_state);
+    float vndf_rand_x = lcg_step_float(lcg_state);
+    cfloat3 wm = mf_sample_vndf(neg3(wr), alpha, alpha, vndf_rand_x, vndf_rand_y);
+
+    /* first-bounce color is already in the mix weight */
+    if (!use_fresnel && order > 0) {
+      throughput = mul3(throughput, color);
+    }
+    bool next_outside;
+    const cfloat3 wi_prev = neg3(wr);
+    const float phase_rand = lcg_step_float(lcg_state);
+    wr = mf_sample_phase_glass(neg3(wr), outside ? eta : 1.0f / eta, wm, phase_rand, &next_outside);
+    if (!next_outside) {
+      hr = -hr;
+      wr = neg3(wr);
+      outside = !outside;
+    }
+    if (use_fresnel) {
+      if (!next_outside) {
+        throughput = mul3(throughput, color);
+      }
+      else {
+        const cfloat3 t_color = interpolate_fresnel_color(wi_prev, wm, eta, F0, cspec0);
+        if (order == 0) {
+          throughput = t_color;
+        }
+        else {
+          throughput = mul3(throughput, t_color);
+        }
+      }
+    }
+    lambda_r = mf_lambda(wr, alpha, alpha);
+    G1_r = mf_G1(wr, C1_r, lambda_r);
+  }
+  *wo = mk3(0.0f, 0.0f, 1.0f);
+  return mk3(0.0f, 0.0f, 0.0f);
+}
+
+/* bsdf_microfacet_multi.h:537-564: extra slot weight = color, N = cspec0 */
+CY_FN int bsdf_microfacet_multi_ggx_glass_setup(CySD *sd, CyClosure *b)
+{
+  CyClosure *ex = &sd->closure[b->extra];
+  b->alpha_x = cclamp(b->alpha_x, 1e-4f, 1.0f);
+  b->alpha_y = b->alpha_x;
+  b->ior = cmax(0.0f, b->ior);
+  ex->weight = saturate3(ex->weight);
+  b->type = CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID;
+  return SD_BSDF | SD_BSDF_HAS_EVAL | SD_BSDF_NEEDS_LCG;
+}
+CY_FN int bsdf_microfacet_multi_ggx_glass_fresnel_setup(CySD *sd, CyClosure *b)
+{
+  CyClosure *ex = &sd->closure[b->extra];
+  b->alpha_x = cclamp(b->alpha_x, 1e-4f, 1.0f);
+  b->alpha_y = b->alpha_x;
+  b->ior = cmax(0.0f, b->ior);
+  ex->weight = saturate3(ex->weight);
+  ex->N = saturate3(ex->N);
+  b->type = CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID;
+  bsdf_microfacet_fresnel_color(sd, b);
+  return SD_BSDF | SD_BSDF_HAS_EVAL | SD_BSDF_NEEDS_LCG;
+}
+
+/* bsdf_microfacet_multi.h:566-626: eval_transmit (no fresnel tint) and
+ * eval_reflect */
+CY_FN cfloat3 bsdf_microfacet_multi_ggx_glass_eval(const CySD *sd, const CyClosure *b, cfloat3 I, cfloat3 omega_in,
+                                                   float *pdf, bool reflect)
+{
+  if (b->alpha_x * b->alpha_y < 1e-7f) {
+    return mk3(0.0f, 0.0f, 0.0f);
+  }
+  const CyClosure *ex = &sd->closure[b->extra];
+  const bool use_fresnel = reflect && (b->type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID);
+  cfloat3 X, Y;
+  const cfloat3 Z = b->N;
+  make_orthonormals(Z, &X, &Y);
+  const cfloat3 localI = mk3(dot3(I, X), dot3(I, Y), dot3(I, Z));
+  const cfloat3 localO = mk3(dot3(omega_in, X), dot3(omega_in, Y), dot3(omega_in, Z));
+  *pdf = mf_glass_pdf(localI, localO, b->alpha_x, b->ior);
+  return mf_eval_glass(localI, localO, reflect, ex->weight, b->alpha_x, &sd->lcg_state, b->ior, use_fresnel,
+                       reflect ? ex->N : ex->weight);
+}
+
+/* bsdf_microfacet_multi.h:628-731 */
+CY_FN int bsdf_microfacet_multi_ggx_glass_sample(const CySD *sd,
+                                                const CyClosure *b,
+                                                cfloat3 I,
+                                                float randu,
+                                                cfloat3 *eval,
+                                                cfloat3 *omega_in,
+                                                float *pdf)
+{
+  const cfloat3 Z = b->N;
+  if (b->alpha_x * b->alpha_y < 1e-7f) {
+    cfloat3 R, T;
+    bool inside;
+    const float fresnel = fresnel_dielectric(b->ior, Z, I, &R, &T, &inside);
+    *pdf = 1e6f;
+    *eval = mk3(1e6f, 1e6f, 1e6f);
+    if (randu < fresnel) {
+      *omega_in = R;
+      return LABEL_REFLECT | LABEL_SINGULAR;
+    }
+    *omega_in = T;
+    return LABEL_TRANSMIT | LABEL_SINGULAR;
+  }
+  const CyClosure *ex = &sd->closure[b->extra];
+  const bool use_fresnel = (b->type == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID);
+  cfloat3 X, Y;
+  make_orthonormals(Z, &X, &Y);
+  const cfloat3 localI = mk3(dot3(I, X), dot3(I, Y), dot3(I, Z));
+  cfloat3 localO;
+  *eval = mf_sample_glass(localI, &localO, ex->weight, b->alpha_x, &sd->lcg_state, b->ior, use_fresnel, ex->N);
+  *pdf = mf_glass_pdf(localI, localO, b->alpha_x, b->ior);
+  *eval = mul3f(*eval, *pdf);
+  *omega_in = add3(add3(mul3f(X, localO.x), mul3f(Y, localO.y)), mul3f(Z, localO.z));
+  if (localO.z * localI.z > 0.0f) {
+    return LABEL_REFLECT | LABEL_GLOSSY;
+  }
+  return LABEL_TRANSMIT | LABEL_GLOSSY;
 }
 
 #endif /* CY_MICROFACET_MULTI_H */

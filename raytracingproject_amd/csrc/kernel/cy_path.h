@@ -568,6 +568,7 @@ CY_FN int bvh2_node_intersect(const hc_float4 *nodes, int node_addr, hc_float4 c
  * arrays never suspends. */
 struct CyTravCursor {
   int code;
+  float code_t; /* entry distance of code's box */
   int top;
   int n_ring;
   bool tie;
@@ -1543,7 +1544,22 @@ CY_FN void svm_node_principled_bsdf(const CyGlobals *kg,
         }
       }
       else {
-        cy_set_error(err, CY_ERR_CLOSURE, CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID);
+        /* multi-scatter GGX (svm_closure.h:403-426) */
+        CyClosure *b = bsdf_alloc(sd, glass_weight);
+        int extra = (b != 0) ? closure_alloc_extra(sd) : -1;
+        if (b && extra >= 0) {
+          CyClosure *ex = &sd->closure[extra];
+          b->N = N;
+          b->extra = extra;
+          b->T = mk3(0.0f, 0.0f, 0.0f);
+          b->alpha_x = roughness * roughness;
+          b->alpha_y = roughness * roughness;
+          b->ior = ior;
+          ex->weight = base_color;
+          ex->N = cspec0;
+          ex->alpha_x = 0.0f;
+          sd->flag |= bsdf_microfacet_multi_ggx_glass_fresnel_setup(sd, b);
+        }
       }
     }
   }
@@ -1797,6 +1813,36 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
       break;
     }
 #if CY_CLOSURE_EXT
+    case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID: {
+      /* svm_closure.h:664-698 (Glass BSDF, Multiscatter GGX) */
+      if (!KD->integrator.caustics_reflective && !KD->integrator.caustics_refractive &&
+          (path_flag & PATH_RAY_DIFFUSE)) {
+        break;
+      }
+      cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (!b) {
+        break;
+      }
+      const int extra = closure_alloc_extra(sd);
+      if (extra < 0) {
+        break;
+      }
+      CyClosure *ex = &sd->closure[extra];
+      b->N = N;
+      b->extra = extra;
+      b->T = mk3(0.0f, 0.0f, 0.0f);
+      float roughness = sqr(param1);
+      b->alpha_x = roughness;
+      b->alpha_y = roughness;
+      float eta = fmaxf(param2, 1e-5f);
+      b->ior = (sd->flag & SD_BACKFACING) ? 1.0f / eta : eta;
+      ex->weight = svm_load3(stack, data_node.z, err);
+      ex->N = mk3(0.0f, 0.0f, 0.0f);
+      ex->alpha_x = 0.0f;
+      sd->flag |= bsdf_microfacet_multi_ggx_glass_setup(sd, b);
+      break;
+    }
     case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID: {
       cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
       CyClosure *b = bsdf_alloc(sd, weight);

@@ -85,8 +85,10 @@ GLOSSY_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFLECTION_ID, "ggx": CLOSURE_BSDF
                         "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_ID,
                         "ashikhmin_shirley": CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID,
                         "multi_ggx": CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID}
+CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID = 25
 GLASS_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_SHARP_GLASS_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID,
-                       "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID}
+                       "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID,
+                       "multi_ggx": CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID}
 REFRACTION_DISTRIBUTIONS = {"sharp": CLOSURE_BSDF_REFRACTION_ID, "ggx": CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID,
                             "beckmann": CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID}
 CLOSURE_BSDF_PRINCIPLED_ID = 45
@@ -281,7 +283,8 @@ def anisotropic(color, roughness, anisotropy, rotation, tangent=None, normal=Non
 
 
 def glass(color, roughness, ior=1.45, normal=None, distribution="ggx"):
-    """Glass BSDF: distribution ggx | beckmann | sharp."""
+    """Glass BSDF: distribution ggx | beckmann | sharp | multi_ggx
+    (multiple-scattering GGX glass, bsdf_microfacet_multi.h)."""
     return Closure("glass", _const_or_socket(color), roughness=roughness, ior=ior, normal=normal,
                    distribution=distribution)
 
@@ -297,9 +300,7 @@ def principled(distribution="ggx", subsurface_method="burley", **params):
     Parameters are PRINCIPLED_DEFAULTS keys (constants or sockets) plus the
     normal / clearcoat_normal / tangent vector sockets.  distribution is
     "ggx" or "multiscatter" (Blender's default: multiple-scattering GGX for the
-    specular layer; its rough-transmission glass lobe is not implemented, so a
-    multiscatter principled with transmission is refused); subsurface > 0 adds
-    a BSSRDF (random walk).  The node's Emission and Alpha inputs (expanded
+    specular layer and for rough transmission); subsurface > 0 adds a BSSRDF.  The node's Emission and Alpha inputs (expanded
     into separate closures by the reference graph) are expressed here with
     emission() / transparent() and mix()."""
     unknown = set(params) - set(PRINCIPLED_DEFAULTS) - set(PRINCIPLED_VECTORS)
@@ -315,9 +316,6 @@ def principled(distribution="ggx", subsurface_method="burley", **params):
         p["tangent"] = _nodes.geometry()["Tangent"]
     if distribution not in PRINCIPLED_DISTRIBUTIONS:
         raise ValueError(f"principled: distribution one of {sorted(PRINCIPLED_DISTRIBUTIONS)}")
-    if distribution == "multiscatter" and (_nodes.is_linked(p["transmission"]) or float(p["transmission"]) > 0.0):
-        raise ValueError("principled: multiscatter GGX glass (transmission > 0) is not implemented "
-                         "(bsdf_microfacet_multi.h glass walk needs glibc's lgammaf)")
     return Closure("principled", distribution=distribution, params=p, subsurface_method=subsurface_method)
 
 
@@ -526,6 +524,9 @@ class SVMCompiler:
             param4_off = self.nc.assign(c.sharpness, "float")
         else:  # glass, refraction (roughness, IOR); toons (size, smooth)
             params = (c.roughness, c.ior)
+            if ctype == CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
+                # GlassBsdfNode::compile (nodes.cpp:2516-2517): the colour as param3
+                param3_off = self.nc.assign(c.color, "color")
         p1, v1 = self._float_param(params[0]) if params[0] is not None else (SVM_STACK_INVALID, 0.0)
         p2, v2 = self._float_param(params[1]) if params[1] is not None else (SVM_STACK_INVALID, 0.0)
         emit((NODE_CLOSURE_BSDF, self.uchar4(ctype, p1, p2, mix_weight), f32bits(v1), f32bits(v2)))

@@ -1354,6 +1354,30 @@ def closures_multiscatter(width=48, height=48, samples=8, filter_glossy=0.0) -> 
     return s
 
 
+def closures_multiscatter_glass(width=48, height=48, samples=8) -> sc.Scene:
+    """Multiple-scattering GGX glass (the MF_MULTI_GLASS walk of
+    bsdf_microfacet_multi_impl.h, beta() through glibc's lgammaf): Glass BSDFs
+    with the Multiscatter GGX distribution (node-driven colour, rough and
+    nearly smooth), and default Principled BSDFs (multiscatter distribution)
+    with rough transmission -- a clear and a tinted glass, and a partly
+    transmissive dielectric."""
+    from . import nodes as nd
+
+    g = nd.geometry()
+    u = nd.separate_xyz(g["Parametric"])["X"]
+    tint = nd.mix_rgb("mix", u, (0.95, 0.85, 0.6), (0.6, 0.9, 0.95))
+    mats = [
+        sc.glass(tint, 0.35, 1.45, distribution="multi_ggx"),
+        sc.glass((0.9, 0.95, 0.9), 0.08, 1.33, distribution="multi_ggx"),
+        sc.principled("multiscatter", base_color=(0.95, 0.95, 0.95), transmission=1.0, roughness=0.3, ior=1.45),
+        sc.principled("multiscatter", base_color=(0.5, 0.8, 0.6), transmission=1.0, roughness=0.6, ior=1.5,
+                      specular_tint=0.5),
+        sc.principled("multiscatter", base_color=(0.8, 0.4, 0.2), transmission=0.5, roughness=0.45, metallic=0.2),
+        sc.mix(0.5, sc.glass((0.9, 0.9, 0.9), 0.5, 1.6, distribution="multi_ggx"), sc.diffuse((0.3, 0.3, 0.7))),
+    ]
+    return _closure_gallery(width, height, samples, "closures_multiscatter_glass", mats)
+
+
 def closures_layered(width=48, height=48, samples=8, triple=False) -> sc.Scene:
     """Materials needing more than 8 closures (the device's 16- and 64-closure
     shading variants): two Principled BSDFs mixed by a node-driven factor

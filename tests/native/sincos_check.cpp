@@ -66,3 +66,21 @@ extern "C" void atan2_eval(const float *y, const float *x, long n, float *dev, f
     libm[i] = atan2f(vy, vx);
   }
 }
+
+/* cy_lgammaf (glibc lgammaf restatement) and libm lgammaf over [lo, hi] bit
+ * patterns; returns the number of mismatches (and the first one in *first). */
+extern "C" long lgammaf_sweep(uint32_t lo, uint32_t hi, uint32_t step, uint32_t *first)
+{
+  long bad = 0;
+  for (uint64_t u = lo; u <= hi; u += step) {
+    const float x = as_float((uint32_t)u);
+    volatile float vx = x;
+    if (as_uint(cy_lgammaf(x)) != as_uint(lgammaf(vx))) {
+      if (!bad && first) {
+        *first = (uint32_t)u;
+      }
+      bad++;
+    }
+  }
+  return bad;
+}

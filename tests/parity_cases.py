@@ -46,6 +46,9 @@ CASES = {
     # Filter Glossy (bsdf_blur of every microfacet closure)
     "closures_multiscatter": lambda: scenes.closures_multiscatter(48, 48, 8),
     "closures_multiscatter_blur": lambda: scenes.closures_multiscatter(48, 48, 8, filter_glossy=1.0),
+    # multiple-scattering GGX glass: Glass BSDF multiscatter distribution and
+    # the Principled BSDF's default rough transmission (glibc lgammaf in beta())
+    "closures_multiscatter_glass": lambda: scenes.closures_multiscatter_glass(48, 48, 8),
     # more than 8 closures per shading point (16- / 64-closure shading variants)
     "closures_layered": lambda: scenes.closures_layered(48, 48, 8),
     "closures_layered_triple": lambda: scenes.closures_layered(48, 48, 8, triple=True),
