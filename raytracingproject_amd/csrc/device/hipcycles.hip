@@ -1241,6 +1241,8 @@ struct hipcy_device {
   size_t num_shaders = 0;             /* __shaders entries */
   bool shade_tex = false;             /* some shader uses texture / converter / input nodes */
   bool use_volumes = false;           /* KernelIntegrator.use_volumes: the volume shading / shadow kernels */
+  bool use_disk_bssrdf = false;       /* disk BSSRDFs: the slots' subsurface indirect-ray records */
+  char *sss_pool = nullptr;           /* those records and their depths */
   int shade_closures = 1;             /* closure array of the shading kernel (variant by size) */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int curve_shapes = 0;               /* curve primitive shapes in __prim_type: 1 ribbon, 2 thick, 3 both */
@@ -1431,6 +1433,12 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   }
   dev->bufs.vol_stack = nullptr;
   dev->bufs.vol_rec = nullptr;
+  if (dev->sss_pool) {
+    hipFree(dev->sss_pool);
+    dev->sss_pool = nullptr;
+  }
+  dev->bufs.sss_rec = nullptr;
+  dev->bufs.sss_count = nullptr;
   /* queues live in their own allocation (3 x slots ints) */
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) {
@@ -1453,6 +1461,24 @@ static int ensure_volume_capacity(hipcy_device *dev)
   HIP_CHECK(dev, hipMalloc((void **)&dev->vol_pool, (CY_VOLUME_STACK / 2 + 2) * rec));
   dev->bufs.vol_stack = (hc_uint4 *)dev->vol_pool;
   dev->bufs.vol_rec = (hc_uint4 *)(dev->vol_pool + (CY_VOLUME_STACK / 2) * rec);
+  return 0;
+}
+
+/* The slots' subsurface indirect-ray records (cy_integrator.h CY_SSS_RECS x
+ * CY_SSS_REC_F4 float4 and a depth per slot, 292 B), for scenes with disk
+ * BSSRDFs only.  Every path leaves its slot with depth 0, so the depths are
+ * cleared once, here. */
+static int ensure_sss_capacity(hipcy_device *dev)
+{
+  const size_t recs = (size_t)16 * CY_SSS_RECS * CY_SSS_REC_F4 * dev->capacity;
+  const size_t counts = 4 * dev->capacity;
+  if (dev->use_disk_bssrdf && !dev->sss_pool) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->sss_pool, recs + counts));
+    HIP_CHECK(dev, hipMemset(dev->sss_pool + recs, 0, counts));
+  }
+  /* other scenes' shading never looks at the records */
+  dev->bufs.sss_rec = dev->use_disk_bssrdf ? (hc_float4 *)dev->sss_pool : nullptr;
+  dev->bufs.sss_count = dev->use_disk_bssrdf ? (uint *)(dev->sss_pool + recs) : nullptr;
   return 0;
 }
 
@@ -1550,6 +1576,7 @@ void hipcy_destroy(hipcy_device *dev)
   }
   if (dev->pool) hipFree(dev->pool);
   if (dev->vol_pool) hipFree(dev->vol_pool);
+  if (dev->sss_pool) hipFree(dev->sss_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
   if (dev->records) hipFree(dev->records);
   if (dev->tile_descs) hipFree(dev->tile_descs);
@@ -1867,11 +1894,12 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
  * nodes are used, which selects the shading-kernel variant. */
 static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
                             const std::vector<void *> &tex_mem, const std::vector<uint32_t> &shader_flags,
-                            bool *uses_tex, bool *uses_bssrdf, bool *uses_attr, int *surface_closures,
-                            int *volume_closures)
+                            bool *uses_tex, bool *uses_bssrdf, bool *uses_disk_bssrdf, bool *uses_attr,
+                            int *surface_closures, int *volume_closures)
 {
   *uses_tex = false;
   *uses_bssrdf = false;
+  *uses_disk_bssrdf = false;
   *uses_attr = false;
   /* closures one program can allocate, counted as ShaderGraph::get_num_closures
    * (render/graph.cpp:1130-1161) counts them, except that a phase closure
@@ -1965,17 +1993,19 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             case CLOSURE_BSDF_GLOSSY_TOON_ID:
             case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
             case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
-            case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node, random walk */
-              /* a random-walk BSSRDF, or a principled BSDF with subsurface (param2: linked or > 0) */
-              *uses_bssrdf |= ctype == CLOSURE_BSSRDF_RANDOM_WALK_ID ||
-                              (ctype == CLOSURE_BSDF_PRINCIPLED_ID &&
-                               (((node.y >> 16) & 0xFF) != SVM_STACK_INVALID || node.w != 0u));
-              break;
+            case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node */
             case CLOSURE_BSSRDF_CUBIC_ID:
             case CLOSURE_BSSRDF_GAUSSIAN_ID:
-            case CLOSURE_BSSRDF_BURLEY_ID:
-              return "shader " + std::to_string(sh) +
-                     ": disk BSSRDF falloffs (cubic / gaussian / burley) are not implemented, random walk is";
+            case CLOSURE_BSSRDF_BURLEY_ID: {
+              /* a BSSRDF, or a principled BSDF with subsurface (param2: linked
+               * or > 0; the method in its second data node's z) */
+              const bool principled_sss = ctype == CLOSURE_BSDF_PRINCIPLED_ID &&
+                                          (((node.y >> 16) & 0xFF) != SVM_STACK_INVALID || node.w != 0u);
+              *uses_bssrdf |= principled_sss || (ctype >= CLOSURE_BSSRDF_CUBIC_ID && ctype <= CLOSURE_BSSRDF_RANDOM_WALK_ID);
+              *uses_disk_bssrdf |= (ctype >= CLOSURE_BSSRDF_CUBIC_ID && ctype <= CLOSURE_BSSRDF_BURLEY_ID) ||
+                                   (principled_sss && prog[off + 2].z == CLOSURE_BSSRDF_PRINCIPLED_ID);
+              break;
+            }
             default:
               return "shader " + std::to_string(sh) + ": closure type " + std::to_string(ctype) +
                      " is not implemented";
@@ -2253,10 +2283,10 @@ int hipcy_load_kernels(hipcy_device *dev)
       shader_flags[i] = (uint32_t)ks[i].flags;
     }
   }
-  bool uses_bssrdf = false, uses_attr = false;
+  bool uses_bssrdf = false, uses_disk_bssrdf = false, uses_attr = false;
   int surface_closures = 0, volume_closures = 0;
   why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, shader_flags, &dev->shade_tex, &uses_bssrdf,
-                 &uses_attr, &surface_closures, &volume_closures);
+                 &uses_disk_bssrdf, &uses_attr, &surface_closures, &volume_closures);
   if (why.empty() && uses_attr && dev->globals.find("__attributes_map") == dev->globals.end()) {
     /* the attribute nodes look attributes up through the objects' maps
      * (GeometryManager::device_update_attributes, geometry.cpp:379-474) */
@@ -2266,6 +2296,7 @@ int hipcy_load_kernels(hipcy_device *dev)
     return set_error(dev, "load_kernels: unsupported shader: " + why);
   }
   dev->use_volumes = d.integrator.use_volumes != 0;
+  dev->use_disk_bssrdf = uses_disk_bssrdf;
   dev->shade_closures = d.integrator.max_closures;
   if (dev->use_volumes) {
     /* the volume stack of a path holds the world and every volume object it
@@ -2292,6 +2323,9 @@ int hipcy_load_kernels(hipcy_device *dev)
     }
     else if (volume_attributes) {
       why = "volume attributes (voxel grids)";
+    }
+    else if (uses_disk_bssrdf) {
+      why = "disk BSSRDFs (cubic / gaussian / burley, principled burley) in a scene with volumes";
     }
     else if (uses_bssrdf && intersects_volume) {
       why = "subsurface scattering on objects that intersect volume objects (volume stack update of the walk)";
@@ -2777,6 +2811,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
   }
   const size_t items = npix * per_pass;
   if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 ||
       ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }
@@ -3349,6 +3384,7 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
     ring_cap <<= 1;
   }
   if (ensure_capacity(dev, lane_slots * lanes) != 0 || ensure_volume_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 ||
       ensure_records(dev, (size_t)ring_cap * lanes) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }

@@ -52,7 +52,15 @@ typedef struct CyPathBuffers {
    * pending shadow ray sees */
   hc_uint4 *vol_stack;
   hc_uint4 *vol_rec;
+  /* scenes with disk BSSRDFs: the path's SubsurfaceIndirectRays stack
+   * (kernel_types.h:1241-1249) beyond the ray the path continues with,
+   * CY_SSS_RECS records of CY_SSS_REC_F4 float4 per slot, and its depth */
+  hc_float4 *sss_rec;
+  uint *sss_count;
 } CyPathBuffers;
+
+#define CY_SSS_RECS (BSSRDF_MAX_HITS - 1)
+#define CY_SSS_REC_F4 6
 
 /* Pending volume stack update of a slot (cy_volume.h volume_stack_enter_exit
  * of the surface in vol_rec[0].xy): the reference updates the stack when the
@@ -214,6 +222,52 @@ CY_FN void store_state(const CyPathBuffers *b, int slot, const CyPathState *s)
 }
 
 #if CY_CLOSURE_EXT
+/* A subsurface indirect ray of the slot (state, ray, throughput). */
+CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathState *s, const CyRay *ray,
+                         cfloat3 throughput)
+{
+  hc_float4 *dst = b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4;
+  cy_st(&dst[0], mkf4(int_as_float(s->flag), as_float(s->rng_hash), int_as_float(s->rng_offset),
+                      int_as_float(s->sample)));
+  cy_st(&dst[1], mkf4(int_as_float(s->bounce), int_as_float(s->diffuse_bounce), int_as_float(s->glossy_bounce),
+                      int_as_float(s->transmission_bounce)));
+  cy_st(&dst[2], mkf4(int_as_float(s->transparent_bounce), s->min_ray_pdf, s->ray_pdf, s->ray_t));
+  cy_st(&dst[3], mkf4(ray->P.x, ray->P.y, ray->P.z, ray->t));
+  cy_st(&dst[4], mkf4(ray->D.x, ray->D.y, ray->D.z, 0.0f));
+  cy_st(&dst[5], mkf4(throughput.x, throughput.y, throughput.z, 0.0f));
+}
+
+CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals *kg, CyPathState *s, CyRay *ray,
+                        cfloat3 *throughput)
+{
+  const hc_float4 *src = b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4;
+  const hc_float4 r0 = cy_ld(&src[0]);
+  const hc_float4 r1 = cy_ld(&src[1]);
+  const hc_float4 r2 = cy_ld(&src[2]);
+  const hc_float4 r3 = cy_ld(&src[3]);
+  const hc_float4 r4 = cy_ld(&src[4]);
+  const hc_float4 r5 = cy_ld(&src[5]);
+  s->flag = as_int(r0.x);
+  s->rng_hash = as_uint(r0.y);
+  s->rng_offset = as_int(r0.z);
+  s->sample = as_int(r0.w);
+  s->num_samples = KD->integrator.aa_samples;
+  s->bounce = as_int(r1.x);
+  s->diffuse_bounce = as_int(r1.y);
+  s->glossy_bounce = as_int(r1.z);
+  s->transmission_bounce = as_int(r1.w);
+  s->transparent_bounce = as_int(r2.x);
+  s->min_ray_pdf = r2.y;
+  s->ray_pdf = r2.z;
+  s->ray_t = r2.w;
+  s->volume_bounce = 0;
+  s->volume_bounds_bounce = 0;
+  ray->P = mk3(r3.x, r3.y, r3.z);
+  ray->t = r3.w;
+  ray->D = mk3(r4.x, r4.y, r4.z);
+  *throughput = mk3(r5.x, r5.y, r5.z);
+}
+
 /* The slot's volume stack and pending update records (CyPathBuffers.vol_*). */
 CY_FN void vol_stack_load(const CyPathBuffers *b, int slot, CyVolumeStack *st)
 {
@@ -1047,7 +1101,7 @@ CY_FN cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cflo
  * direct_emission (kernel_emission.h:101-205).  An occluded-or-not light
  * sample is left in the slot's shadow records and *shadow set; *shadow_D is
  * the shadow ray's direction then. */
-template<bool PHASE>
+template<bool PHASE, bool INLINE = false>
 CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, const CySD *sd,
                          const CyPathState *state, cfloat3 throughput, cfloat3 *L, bool *shadow, cfloat3 *shadow_D,
                          CyShadeMem mem, uint *err)
@@ -1148,6 +1202,42 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
             sD = normalize_len3(sub3(ray_offset(ls.P, ls.Ng), sP), &st);
           }
           *shadow_D = sD;
+#if CY_CLOSURE_EXT
+          if (INLINE) {
+            /* a subsurface exit point: the light sample is occluded here and
+             * now (one of up to BSSRDF_MAX_HITS per shade); *shadow reports
+             * that the transparent-shadow evaluation reused sd's closure
+             * memory */
+            CyRay sray;
+            sray.P = sP;
+            sray.D = sD;
+            sray.t = st;
+            if (KD->integrator.transparent_shadows) {
+              cfloat3 attenuation;
+              const bool blocked = shadow_blocked_transparent<false>(kg, sray, state, mem, &attenuation, err);
+              *shadow = true;
+              if (!blocked) {
+                const cfloat3 shaded = mul3(mul3f(throughput, 1.0f), attenuation);
+                *L = add3(*L, path_radiance_clamp(kg, mul3(shaded, eval), state->bounce));
+              }
+            }
+            else {
+              bool blocked = false;
+              if (scene_intersect_valid(&sray)) {
+                CyIsect si;
+                blocked = kg->have_curves ?
+                              bvh2_intersect<true, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(
+                                  kg, &sray, PATH_RAY_SHADOW_OPAQUE, &si, err, nullptr, nullptr, nullptr) :
+                              bvh2_intersect<true>(kg, &sray, PATH_RAY_SHADOW_OPAQUE, &si, err, nullptr, nullptr,
+                                                   nullptr);
+              }
+              if (!blocked) {
+                *L = add3(*L, contribution);
+              }
+            }
+            return;
+          }
+#endif
           cy_st(&b->shadow_P[slot], mkf4(sP.x, sP.y, sP.z, st));
           if (KD->integrator.transparent_shadows) {
             /* the shadow's attenuation multiplies the throughput before
@@ -1175,6 +1265,116 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
     }
   }
 }
+
+#if CY_CLOSURE_EXT
+/* kernel_path_surface_bounce (kernel_path_surface.h:270-358) for the diffuse
+ * closure at a subsurface exit point (no volumes: disk BSSRDFs are refused in
+ * volume scenes). */
+CY_FN bool subsurface_exit_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *throughput, CyPathState *state,
+                                  CyRay *ray, uint *err)
+{
+  if (!(sd->flag & SD_BSDF)) {
+    return false;
+  }
+  float bsdf_u, bsdf_v;
+  path_state_rng_2D(kg, state, PRNG_BSDF_U, &bsdf_u, &bsdf_v);
+  cfloat3 bsdf_eval_v = mk3(0.0f, 0.0f, 0.0f);
+  cfloat3 omega_in = mk3(0.0f, 0.0f, 0.0f);
+  float bsdf_pdf = 0.0f;
+  const int label = shader_bsdf_sample(kg, sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err);
+  if (bsdf_pdf == 0.0f || is_zero3(bsdf_eval_v)) {
+    return false;
+  }
+  const float inverse_pdf = 1.0f / bsdf_pdf;
+  *throughput = mul3(*throughput, mul3f(bsdf_eval_v, inverse_pdf));
+  if (!(label & LABEL_TRANSPARENT)) {
+    state->ray_pdf = bsdf_pdf;
+    state->ray_t = 0.0f;
+    state->min_ray_pdf = fminf(bsdf_pdf, state->min_ray_pdf);
+  }
+  path_state_next(kg, state, label);
+  ray->P = ray_offset(sd->P, (label & LABEL_TRANSMIT) ? neg3(sd->Ng) : sd->Ng);
+  ray->D = normalize3(omega_in);
+  if (state->bounce == 0) {
+    ray->t -= sd->ray_length;
+  }
+  else {
+    ray->t = CY_FLT_MAX;
+  }
+  return true;
+}
+
+/* kernel_path_subsurface_scatter (kernel_path_subsurface.h:26-110) for a disk
+ * BSSRDF: up to BSSRDF_MAX_HITS exit points, each lit with the path's state and
+ * throughput (its shadow ray traced here), each bouncing into an indirect ray
+ * with rng_offset + PRNG_BOUNCE_NUM.  The reference ends the path there and
+ * then traces the indirect rays last to first, ray k with rng_offset +
+ * k * PRNG_BOUNCE_NUM (kernel_path_subsurface_setup_indirect): the last one
+ * replaces the path's state, ray and throughput here, the others wait in the
+ * slot's SSS records until the path before them ends (shade_path).  Returns
+ * the number of indirect rays. */
+CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int slot, uint cam_item, CySD *sd,
+                                const CyClosure *sc, float bssrdf_u, float bssrdf_v, CyPathState *state,
+                                CyRay *ray, cfloat3 *throughput, cfloat3 *L, CyShadeMem mem, uint *err)
+{
+  if (!b->sss_rec || (cam_item == CY_NO_ITEM && cy_ld(&b->sss_count[slot]) != 0u)) {
+    cy_set_error(err, CY_ERR_FEATURE, 12); /* no indirect-ray records, or a second scatter on one path */
+    return 0;
+  }
+  const int bssrdf_type = sc->type;
+  const float bssrdf_rough = bssrdf_roughness(sc);
+  uint lcg_state = lcg_init(state->rng_hash + (uint)state->rng_offset + (uint)state->sample * 0x68bc21ebu);
+  CyLocalHits li;
+  CyRay ss_ray;
+  const int num_hits = subsurface_scatter_disk(kg, &li, sd, sc, &lcg_state, bssrdf_u, bssrdf_v, &ss_ray, err);
+  int pushed = 0;
+  CyPathState top_state;
+  CyRay top_ray;
+  cfloat3 top_tp = mk3(0.0f, 0.0f, 0.0f);
+  for (int hit = 0; hit < num_hits; hit++) {
+    /* subsurface_scatter_multi_setup (kernel_subsurface.h:284-313) */
+    shader_setup_from_subsurface(kg, sd, &li.hits[hit], &ss_ray);
+    cfloat3 weight = li.weight[hit];
+    cfloat3 N = sd->N;
+    subsurface_color_bump_blur(kg, sd, state, &weight, &N, err);
+    subsurface_scatter_setup_diffuse_bsdf(kg, sd, bssrdf_type, bssrdf_rough, weight, N);
+    if (KD->integrator.use_direct_light && (sd->flag & SD_BSDF_HAS_EVAL)) {
+      bool reused = false;
+      cfloat3 shadow_D;
+      connect_light<false, true>(kg, b, slot, sd, state, *throughput, L, &reused, &shadow_D, mem, err);
+      if (reused) {
+        shader_setup_from_subsurface(kg, sd, &li.hits[hit], &ss_ray);
+        subsurface_scatter_setup_diffuse_bsdf(kg, sd, bssrdf_type, bssrdf_rough, weight, N);
+      }
+    }
+    CyPathState hit_state = *state;
+    CyRay hit_ray = *ray;
+    cfloat3 hit_tp = *throughput;
+    hit_state.rng_offset += PRNG_BOUNCE_NUM;
+    if (subsurface_exit_bounce(kg, sd, &hit_tp, &hit_state, &hit_ray, err)) {
+      hit_state.ray_t = 0.0f;
+      if (pushed > 0) {
+        top_state.rng_offset += (pushed - 1) * PRNG_BOUNCE_NUM;
+        sss_rec_store(b, slot, pushed - 1, &top_state, &top_ray, top_tp);
+      }
+      top_state = hit_state;
+      top_ray = hit_ray;
+      top_tp = hit_tp;
+      pushed++;
+    }
+  }
+  if (pushed > 0) {
+    top_state.rng_offset += (pushed - 1) * PRNG_BOUNCE_NUM;
+    *state = top_state;
+    *ray = top_ray;
+    *throughput = top_tp;
+    if (pushed > 1) {
+      cy_st(&b->sss_count[slot], (uint)(pushed - 1));
+    }
+  }
+  return pushed;
+}
+#endif
 
 /* ---------------------------------------------------------------------------
  * Stage 2: shade one path at one bounce.  Returns true when the slot must be
@@ -1393,6 +1593,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
   bool cont = false; /* path continues with a new ray */
   cfloat3 shadow_D = mk3(0.0f, 0.0f, 0.0f);
   bool vol_scattered = false;
+  int sss_disk_rays = -1; /* >= 0: a disk BSSRDF scattered at this bounce */
 
 #if CY_CLOSURE_EXT
   if (VOL) {
@@ -1618,13 +1819,23 @@ CY_FN bool shade_path(const CyGlobals *kg,
           cfloat3 ss_weight;
           CyRay ss_ray;
           if (CLOSURE_IS_DISK_BSSRDF(bssrdf_type)) {
-            cy_set_error(err, CY_ERR_CLOSURE, (uint)bssrdf_type); /* disk BSSRDF: up to 4 exit points */
+            /* the exit points' light and bounces replace the path's own */
+            if (VOL) {
+              cy_set_error(err, CY_ERR_CLOSURE, (uint)bssrdf_type); /* refused with volumes at load */
+            }
+            else {
+              sss_disk_rays = subsurface_disk_paths(kg, b, slot, cam_item, &sd, sc, bssrdf_u, bssrdf_v, &state,
+                                                    &ray, &throughput, &L, mem, err);
+            }
             terminated = true;
           }
           else if (subsurface_random_walk(kg, &sd, &state, sc, bssrdf_u, bssrdf_v, &ss_hit, &ss_weight, &ss_ray,
                                           err)) {
+            /* subsurface_scatter_multi_setup (kernel_subsurface.h:284-313) */
             shader_setup_from_subsurface(kg, &sd, &ss_hit, &ss_ray);
-            subsurface_scatter_setup_diffuse_bsdf(kg, &sd, bssrdf_type, bssrdf_rough, ss_weight, sd.N);
+            cfloat3 ss_N = sd.N;
+            subsurface_color_bump_blur(kg, &sd, &state, &ss_weight, &ss_N, err);
+            subsurface_scatter_setup_diffuse_bsdf(kg, &sd, bssrdf_type, bssrdf_rough, ss_weight, ss_N);
             sss_bounce = true;
           }
           else {
@@ -1706,6 +1917,19 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
 
 #if CY_CLOSURE_EXT
+  if (sss_disk_rays > 0) {
+    cont = true; /* the last indirect ray of the exit points */
+  }
+  else if (!cont && b->sss_rec) {
+    /* the path ended: the next subsurface indirect ray of the slot
+     * (kernel_path_subsurface_setup_indirect), if any */
+    const int pending = (sss_disk_rays == 0 || cam_item != CY_NO_ITEM) ? 0 : (int)cy_ld(&b->sss_count[slot]);
+    if (pending > 0) {
+      sss_rec_load(b, slot, pending - 1, kg, &state, &ray, &throughput);
+      cy_st(&b->sss_count[slot], (uint)(pending - 1));
+      cont = true;
+    }
+  }
   if (VOL && (cont || *shadow)) {
     vol_stack_store(b, slot, &vstack);
     vol_rec_store(b, slot, vop_object, vop_shader, vop_flags, &state, shadow_rng_offset);

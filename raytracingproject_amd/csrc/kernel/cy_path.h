@@ -1162,12 +1162,17 @@ CY_FN CyClosure *bsdf_alloc(CySD *sd, cfloat3 weight)
 
 /* ---------------------------------------------------------------------------
  * BSSRDF closures (closure/bssrdf.h:330-425).  A BSSRDF keeps its radius in
- * the closure's T, its albedo in (alpha_x, alpha_y, ior) and the principled
- * roughness in `extra` (float bits): the random-walk scatter step
- * (cy_subsurface.h) reads only these.  Texture blur (which needs a second
- * shader evaluation at the entry point, kernel_subsurface.h:141-172) is
- * rejected when set. */
+ * the closure's T.  The random walk keeps its albedo in (alpha_x, alpha_y,
+ * ior); the disk profiles (cubic / gaussian / burley / principled) need no
+ * albedo after setup and keep the cubic sharpness in alpha_x and the channel
+ * count in alpha_y.  `extra` (float bits) holds the roughness of the
+ * principled types and the texture blur of the Subsurface Scattering node's
+ * (whose roughness is 0, as the principled types' texture blur is). */
 #if CY_CLOSURE_EXT
+CY_FN bool bssrdf_is_principled(int type)
+{
+  return type == CLOSURE_BSSRDF_PRINCIPLED_ID || type == CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID;
+}
 CY_FN cfloat3 bssrdf_radius(const CyClosure *sc)
 {
   return sc->T;
@@ -1178,7 +1183,11 @@ CY_FN cfloat3 bssrdf_albedo(const CyClosure *sc)
 }
 CY_FN float bssrdf_roughness(const CyClosure *sc)
 {
-  return int_as_float(sc->extra);
+  return bssrdf_is_principled((int)sc->type) ? int_as_float(sc->extra) : 0.0f;
+}
+CY_FN float bssrdf_texture_blur(const CyClosure *sc)
+{
+  return bssrdf_is_principled((int)sc->type) ? 0.0f : int_as_float(sc->extra);
 }
 
 /* bssrdf_alloc (bssrdf.h:332-343) */
@@ -1203,7 +1212,8 @@ CY_FN float bssrdf_burley_fitting(float A)
  * channel's weight to a diffuse closure; the BSSRDF's sample weight counts its
  * channels; burley-type profiles (and the random walk) remap the radius to the
  * mean free path. */
-CY_FN int bssrdf_setup(CySD *sd, CyClosure *bssrdf, int type, cfloat3 radius, cfloat3 albedo, float roughness)
+CY_FN int bssrdf_setup(CySD *sd, CyClosure *bssrdf, int type, cfloat3 radius, cfloat3 albedo, float roughness,
+                       float sharpness, float texture_blur)
 {
   int flag = 0;
   int bssrdf_channels = 3;
@@ -1247,6 +1257,8 @@ CY_FN int bssrdf_setup(CySD *sd, CyClosure *bssrdf, int type, cfloat3 radius, cf
   if (bssrdf_channels > 0) {
     bssrdf->type = type;
     bssrdf->sample_weight = fabsf(average3(bssrdf->weight)) * (float)bssrdf_channels;
+    texture_blur = saturate(texture_blur);
+    sharpness = saturate(sharpness);
     if (type == CLOSURE_BSSRDF_BURLEY_ID || type == CLOSURE_BSSRDF_PRINCIPLED_ID ||
         type == CLOSURE_BSSRDF_RANDOM_WALK_ID || type == CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) {
       const cfloat3 l = mul3f(radius, 0.25f * CY_1_PI_F);
@@ -1261,10 +1273,16 @@ CY_FN int bssrdf_setup(CySD *sd, CyClosure *bssrdf, int type, cfloat3 radius, cf
     bssrdf->sample_weight = 0.0f;
   }
   bssrdf->T = radius;
-  bssrdf->alpha_x = albedo.x;
-  bssrdf->alpha_y = albedo.y;
-  bssrdf->ior = albedo.z;
-  bssrdf->extra = as_int(roughness);
+  if (type == CLOSURE_BSSRDF_RANDOM_WALK_ID || type == CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) {
+    bssrdf->alpha_x = albedo.x;
+    bssrdf->alpha_y = albedo.y;
+    bssrdf->ior = albedo.z;
+  }
+  else {
+    bssrdf->alpha_x = sharpness;
+    bssrdf->alpha_y = (float)bssrdf_channels;
+  }
+  bssrdf->extra = as_int(bssrdf_is_principled(type) ? roughness : texture_blur);
   return flag;
 }
 #endif
@@ -1447,7 +1465,7 @@ CY_FN void svm_node_principled_bsdf(const CyGlobals *kg,
         sd->flag |= bssrdf_setup(sd, bssrdf, subsurface_method, mul3f(subsurface_radius, subsurface),
                                  (subsurface_method == CLOSURE_BSSRDF_PRINCIPLED_ID) ? subsurface_color :
                                                                                      mixed_ss_base_color,
-                                 roughness);
+                                 roughness, 0.0f, 0.0f);
       }
     }
   }
@@ -1880,12 +1898,9 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
         if (path_flag & PATH_RAY_DIFFUSE_ANCESTOR) {
           param1 = 0.0f;
         }
-        if (saturate(param2) > 0.0f) {
-          cy_set_error(err, CY_ERR_CLOSURE, 1000 + type); /* texture blur */
-        }
         bssrdf->N = N;
         sd->flag |= bssrdf_setup(sd, bssrdf, (int)type, mul3f(svm_load3(stack, data_node.z, err), param1),
-                                 sd->svm_closure_weight, 0.0f);
+                                 sd->svm_closure_weight, 0.0f, svm_load(stack, data_node.w, err), param2);
       }
       break;
     }

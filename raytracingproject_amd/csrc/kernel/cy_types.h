@@ -234,6 +234,7 @@ enum {
 #define CLOSURE_IS_DISK_BSSRDF(type) ((type) >= CLOSURE_BSSRDF_CUBIC_ID && (type) <= CLOSURE_BSSRDF_BURLEY_ID)
 #define BSSRDF_MIN_RADIUS 1e-8f   /* kernel_types.h:49-51 */
 #define BSSRDF_MAX_BOUNCES 256
+#define BSSRDF_MAX_HITS 4 /* kernel_types.h:50 */
 #define VOLUME_BOUNDS_MAX 1024    /* kernel_types.h:54 */
 
 #define CLOSURE_WEIGHT_CUTOFF 1e-5f

@@ -108,6 +108,7 @@ BECKMANN_CLOSURES = (CLOSURE_BSDF_MICROFACET_BECKMANN_ID, CLOSURE_BSDF_MICROFACE
                      CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID)
 SD_HAS_TRANSPARENT_SHADOW = 1 << 17
 SD_HAS_DISPLACEMENT = 1 << 26
+SD_HAS_BSSRDF_BUMP = 1 << 21
 # volumes (kernel_types.h:832-931, svm_types.h:577-579, 105-106)
 SD_HAS_VOLUME = 1 << 18
 SD_HAS_ONLY_VOLUME = 1 << 19
@@ -319,13 +320,13 @@ def principled(distribution="ggx", subsurface_method="burley", **params):
     return Closure("principled", distribution=distribution, params=p, subsurface_method=subsurface_method)
 
 
-def subsurface(color, scale=0.01, radius=(0.1, 0.1, 0.1), falloff="random_walk", texture_blur=0.0, sharpness=0.0,
+def subsurface(color, scale=0.01, radius=(0.1, 0.1, 0.1), falloff="burley", texture_blur=1.0, sharpness=0.0,
                normal=None):
-    """Subsurface Scattering node (nodes.cpp SubsurfaceScatteringNode, a
-    BSSRDF closure, svm_closure.h:880-905): falloff random_walk | burley |
-    cubic | gaussian (the device implements the random walk; disk falloffs
-    are refused at load_kernels).  texture_blur must be 0 (the reference's
-    node default is 1, which re-evaluates the shader at the entry point)."""
+    """Subsurface Scattering node (nodes.cpp:3025-3045 SubsurfaceScatteringNode,
+    a BSSRDF closure, svm_closure.h:880-905), with the node's defaults:
+    falloff burley | cubic | gaussian (disk profiles, up to four exit points)
+    | random_walk; texture_blur re-evaluates the shader at the exit point and
+    blends the two points' colours (kernel_subsurface.h:132-158)."""
     if falloff not in SUBSURFACE_FALLOFFS:
         raise ValueError(f"subsurface: unknown falloff {falloff}")
     return Closure("subsurface", _const_or_socket(color), strength=scale, radius=radius, distribution=falloff,
@@ -854,6 +855,29 @@ def _has_displacement(m) -> bool:
     return nodes.is_linked(getattr(m, "displacement", None))
 
 
+def _has_bssrdf_bump(m) -> bool:
+    """Shader::has_bssrdf_bump (svm.cpp:515-521, 855): a BSSRDF node whose
+    Normal input is linked to anything but the Geometry node
+    (SubsurfaceScatteringNode / PrincipledBsdfNode::has_bssrdf_bump,
+    nodes.cpp:2960-2963, 3069-3075).  Bump displacement (the other source) is
+    not expressible here: displacement is always the "true" method."""
+    if m is None:
+        return False
+
+    def bumped(v):
+        return nodes.is_linked(v) and v.node.kind != "geometry"
+
+    if m.kind == "mix":
+        return _has_bssrdf_bump(m.a) or _has_bssrdf_bump(m.b)
+    if m.kind == "subsurface":
+        return bumped(m.normal)
+    if m.kind == "principled":
+        sss = m.params["subsurface"]
+        has_sss = nodes.is_linked(sss) or float(sss) > 1e-5  # has_surface_bssrdf, CLOSURE_WEIGHT_CUTOFF
+        return has_sss and bumped(m.params.get("normal"))
+    return False
+
+
 @dataclass
 class DeviceScene:
     data: abi.KernelData
@@ -1150,6 +1174,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
             kshaders[i].constant_emission[:] = [float(c) for c in const]
         if _has_displacement(m):
             flag |= SD_HAS_DISPLACEMENT  # shader.cpp:559-560 (displacement_method true)
+        if _has_bssrdf_bump(m):
+            flag |= SD_HAS_BSSRDF_BUMP  # shader.cpp:547-548
         if m.volume is not None:
             # shader.cpp:529-553: a volume shader has transparent shadows; one
             # without a surface only bounds its volume; heterogeneous_volume

@@ -629,21 +629,36 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
 # Subsurface scattering: SURVEY.md §8(a18), §8(d) config CLS
 
 
-def sss_cornell(width=48, height=48, samples=8, instanced=False) -> sc.Scene:
+def sss_cornell(width=48, height=48, samples=8, instanced=False, blur=False) -> sc.Scene:
     """Cornell box with random-walk subsurface scattering (golden parity case):
     a Subsurface Scattering node sphere, a principled random-walk sphere
     mixing subsurface with specular and sheen, a node mixing SSS with a
     glossy layer, and (instanced=True) the same materials on instanced
-    geometry (local intersections through bvh_instance_push)."""
+    geometry (local intersections through bvh_instance_push).  blur=True
+    gives the node sphere a checker colour with the node's default texture
+    blur and the principled sphere a bumped normal (the exit point's shader
+    evaluated again, kernel_subsurface.h:132-158)."""
+    from . import nodes
+
     s = cornell_box(width, height, samples)
     base = len(s.materials)
-    skin = sc.subsurface((0.9, 0.6, 0.5), scale=60.0, radius=(1.0, 0.4, 0.2))
+    if blur:
+        checker = nodes.checker(None, (0.9, 0.6, 0.5), (0.4, 0.7, 0.9), scale=3.0)["Color"]
+        skin = sc.subsurface(checker, scale=60.0, radius=(1.0, 0.4, 0.2), falloff="random_walk")
+    else:
+        skin = sc.subsurface((0.9, 0.6, 0.5), scale=60.0, radius=(1.0, 0.4, 0.2), falloff="random_walk",
+                              texture_blur=0.0)
     wax = sc.principled(subsurface_method="random_walk", base_color=(0.9, 0.85, 0.7), subsurface=0.6,
                         subsurface_color=(0.9, 0.7, 0.4), subsurface_radius=(40.0, 25.0, 15.0), specular=0.4,
-                        roughness=0.35, sheen=0.3)
+                        roughness=0.35, sheen=0.3,
+                        **({"normal": nodes.vector_math("normalize", nodes.vector_math(
+                            "add", nodes.geometry()["Normal"], (0.2, 0.0, 0.1))["Vector"])["Vector"]}
+                           if blur else {}))
     jade = sc.mix(0.25, sc.glossy((0.9, 0.9, 0.9), 0.15),
-                  sc.subsurface((0.3, 0.8, 0.5), scale=35.0, radius=(0.5, 1.0, 0.6)))
-    thin = sc.subsurface((0.8, 0.8, 0.9), scale=1e-9, radius=(1.0, 1.0, 1.0))  # radii below BSSRDF_MIN_RADIUS: diffuse
+                  sc.subsurface((0.3, 0.8, 0.5), scale=35.0, radius=(0.5, 1.0, 0.6), falloff="random_walk",
+                                texture_blur=0.0))
+    thin = sc.subsurface((0.8, 0.8, 0.9), scale=1e-9, radius=(1.0, 1.0, 1.0), falloff="random_walk",
+                          texture_blur=0.0)  # radii below BSSRDF_MIN_RADIUS: diffuse
     s.materials.extend([skin, wax, jade, thin])
     centers = [(140.0, 120.0, 220.0), (300.0, 120.0, 260.0), (430.0, 300.0, 300.0), (200.0, 380.0, 380.0)]
     if instanced:
@@ -657,7 +672,55 @@ def sss_cornell(width=48, height=48, samples=8, instanced=False) -> sc.Scene:
         for i, c in enumerate(centers):
             s.meshes.append(sc.Mesh(*_ellipsoid(c, (70.0, 65.0, 70.0), 20, 12), shader=base + i, smooth=i % 2 == 0))
     s.lamps = [sc.Lamp("point", co=(140.0, 480.0, 40.0), size=20.0, color=(1.0, 0.8, 0.6), strength=3.0e6)]
-    s.name = "sss_instanced" if instanced else "sss_cornell"
+    s.name = ("sss_instanced" if instanced else "sss_cornell") + ("_blur" if blur else "")
+    return s
+
+
+def sss_disk_cornell(width=48, height=48, samples=8, instanced=False, transparent=False) -> sc.Scene:
+    """Cornell box with disk BSSRDFs (golden parity case): Subsurface
+    Scattering nodes with the cubic (sharpness 0.5, blurred checker colour),
+    gaussian (bumped normal: SD_HAS_BSSRDF_BUMP) and default burley (texture
+    blur 1 over a noise colour) profiles, the cubic profile at sharpness 1
+    with one radius channel below BSSRDF_MIN_RADIUS, and the Principled BSDF's
+    default subsurface method; instanced=True puts them on instanced geometry,
+    transparent=True adds a half-transparent pane so the exit points' light
+    samples take the transparent-shadow evaluation."""
+    from . import nodes
+
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    checker = nodes.checker(None, (0.9, 0.55, 0.45), (0.5, 0.8, 0.6), scale=3.0)["Color"]
+    noise = nodes.noise_texture(None, scale=0.02, detail=1.0)["Color"]
+    bumped = nodes.vector_math("normalize", nodes.vector_math("add", nodes.geometry()["Normal"],
+                                                              nodes.vector_math("scale", noise, scale=0.4)["Vector"])
+                               ["Vector"])["Vector"]
+    cubic = sc.subsurface(checker, scale=40.0, radius=(1.0, 0.5, 0.25), falloff="cubic", sharpness=0.5,
+                          texture_blur=0.5)
+    gauss = sc.subsurface((0.3, 0.8, 0.5), scale=30.0, radius=(0.5, 1.0, 0.6), falloff="gaussian", texture_blur=0.0,
+                          normal=bumped)
+    burley = sc.subsurface(noise, scale=50.0, radius=(1.0, 0.4, 0.2))
+    skin = sc.principled(base_color=(0.85, 0.62, 0.52), subsurface=0.7, subsurface_color=(0.9, 0.5, 0.4),
+                         subsurface_radius=(30.0, 12.0, 8.0), roughness=0.45, specular=0.35)
+    sharp = sc.mix(0.3, sc.glossy((0.9, 0.9, 0.9), 0.2),
+                   sc.subsurface((0.8, 0.7, 0.9), scale=45.0, radius=(1.0, 0.0, 0.3), falloff="cubic",
+                                 sharpness=1.0, texture_blur=0.0))
+    s.materials.extend([cubic, gauss, burley, skin, sharp])
+    centers = [(140.0, 120.0, 220.0), (300.0, 120.0, 260.0), (430.0, 300.0, 300.0), (200.0, 380.0, 380.0),
+               (420.0, 110.0, 120.0)]
+    if instanced:
+        ev, et = _ellipsoid((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), 20, 12)
+        for i, c in enumerate(centers):
+            geo = sc.Mesh(ev, et, shader=base + i, smooth=True)
+            s.instances.append(sc.Instance(geo, _tfm(c, 0.3 * i, (70.0, 60.0 + 5 * i, 70.0))))
+    else:
+        for i, c in enumerate(centers):
+            s.meshes.append(sc.Mesh(*_ellipsoid(c, (70.0, 65.0, 70.0), 20, 12), shader=base + i, smooth=i % 2 == 0))
+    if transparent:
+        s.materials.append(sc.mix(0.5, sc.transparent((1.0, 1.0, 1.0)), sc.diffuse((0.7, 0.7, 0.75))))
+        s.meshes.append(sc.Mesh(*_quad((60.0, 300.0, 100.0), (260.0, 300.0, 100.0), (260.0, 300.0, 300.0),
+                                       (60.0, 300.0, 300.0)), shader=len(s.materials) - 1))
+    s.lamps = [sc.Lamp("point", co=(140.0, 480.0, 40.0), size=20.0, color=(1.0, 0.8, 0.6), strength=3.0e6)]
+    s.name = "sss_disk" + ("_instanced" if instanced else "") + ("_transparent" if transparent else "")
     return s
 
 
@@ -705,7 +768,7 @@ def volume_cornell(width=48, height=48, samples=8, heterogeneous=False) -> sc.Sc
 def classroom_standin(width=1920, height=1080, samples=256, detail=1.0) -> sc.Scene:
     """Classroom-class stand-in (SURVEY.md §8(d) config CLS): a classroom with
     rows of desks and chairs, a blackboard, windows, 60 area lights in the
-    ceiling grid and subsurface (random walk) objects -- skin-like busts,
+    ceiling grid and subsurface objects (disk BSSRDFs) -- skin-like busts,
     wax candles and a jade vase on the desks -- at 1920x1080, 256 spp."""
     rng = np.random.default_rng(0x5EED + 2)
     wall = sc.diffuse((0.7, 0.68, 0.62))
@@ -714,9 +777,11 @@ def classroom_standin(width=1920, height=1080, samples=256, detail=1.0) -> sc.Sc
     metal = sc.glossy((0.75, 0.75, 0.78), 0.25)
     board = sc.diffuse((0.08, 0.15, 0.1))
     glass = sc.glass((0.95, 0.97, 1.0), 0.0, ior=1.45)
-    skin = sc.principled(subsurface_method="random_walk", base_color=(0.85, 0.62, 0.52), subsurface=0.8,
-                         subsurface_color=(0.9, 0.5, 0.4), subsurface_radius=(0.12, 0.05, 0.03), roughness=0.45,
-                         specular=0.35)
+    # subsurface with the defaults of Blender's nodes: the Principled BSDF's
+    # "Christensen-Burley" method and the Subsurface Scattering node's burley
+    # falloff with texture blur 1 (disk BSSRDFs, up to four exit points)
+    skin = sc.principled(base_color=(0.85, 0.62, 0.52), subsurface=0.8, subsurface_color=(0.9, 0.5, 0.4),
+                         subsurface_radius=(0.12, 0.05, 0.03), roughness=0.45, specular=0.35)
     wax = sc.subsurface((0.95, 0.9, 0.75), scale=0.05, radius=(1.0, 0.8, 0.5))
     jade = sc.mix(0.2, sc.glossy((0.9, 0.9, 0.9), 0.1), sc.subsurface((0.3, 0.75, 0.5), scale=0.04,
                                                                        radius=(0.4, 1.0, 0.6)))

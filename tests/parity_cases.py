@@ -72,6 +72,10 @@ CASES = {
     # instanced geometry (scene_intersect_local through bvh_instance_push)
     "sss_cornell": lambda: scenes.sss_cornell(48, 48, 8),
     "sss_instanced": lambda: scenes.sss_cornell(48, 48, 8, instanced=True),
+    "sss_blur": lambda: scenes.sss_cornell(40, 40, 8, blur=True),
+    "sss_disk": lambda: scenes.sss_disk_cornell(48, 48, 8),
+    "sss_disk_instanced": lambda: scenes.sss_disk_cornell(48, 48, 8, instanced=True),
+    "sss_disk_transparent": lambda: scenes.sss_disk_cornell(40, 40, 8, transparent=True),
     # volumes (kernel_volume.h, distance sampling as on GPU devices): world fog,
     # volume-only boxes, a glass sphere with an absorbing interior, emission;
     # heterogeneous: texture-driven densities, ray marching
@@ -147,7 +151,7 @@ SCALE_CASES = {
     "cornell_256": (lambda: scenes.cornell_box(256, 256, 32), None),
     "bmw_full_tile": (lambda: scenes.bmw27_standin(), (576, 328, 64, 64)),
     "bbs_tile": (lambda: scenes.barbershop_standin(), (960, 560, 48, 48)),
-    # CLS: 60 area lights, random-walk SSS props (1920x1080, 256 spp)
+    # CLS: 60 area lights, disk-BSSRDF SSS props (1920x1080, 256 spp)
     "cls_tile": (lambda: scenes.classroom_standin(), (1130, 200, 40, 40)),
     # JNK: fur balls / rug ribbons, 1.6M curve segments (3840x2160, 1024 spp)
     "jnk_tile": (lambda: scenes.junkshop_standin(), (1660, 520, 32, 32)),

@@ -284,6 +284,10 @@ extern "C" int emu_render(const void *data,
   hc_uint4 vol_rec[2];
   b.vol_stack = vol_stack;
   b.vol_rec = vol_rec;
+  hc_float4 sss_rec[CY_SSS_RECS * CY_SSS_REC_F4];
+  uint sss_count = 0;
+  b.sss_rec = sss_rec;
+  b.sss_count = &sss_count;
   const bool vol = ((const hc_KernelData *)data)->integrator.use_volumes != 0;
   uint err = 0;
   CyTile tile;
