@@ -99,13 +99,36 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
  * Tile streams (hipcy_render_feed).  A lane's work items are numbered over
  * the tiles appended to it; see stream_render for the host side. */
 
+/* chunk b carries on chunk a: the next sample range of the same RenderTile,
+ * its items right after a's (stream_fill appends a tile's chunks in a row) */
+static __device__ bool stream_chunk_continues(const CyTileDesc &a, const CyTileDesc &b)
+{
+  return b.buffer == a.buffer && b.x == a.x && b.y == a.y && b.w == a.w && b.h == a.h &&
+         b.start_sample == a.start_sample + a.num_samples &&
+         b.item_begin == a.item_begin + (uint)(a.w * a.h) * (uint)a.num_samples;
+}
+
 /* The records of the lane's completed chunks descs[0 .. gridDim.y-1] added
  * to their render buffers (sample order per pixel, as k_accumulate); one
- * launch per batch of chunks completed together, blockIdx.y the chunk. */
+ * launch per batch of chunks completed together, blockIdx.y the chunk.  A
+ * tile split into several chunks of the batch is added by the block row of
+ * its first chunk, over all of them in sample order (two rows adding to the
+ * same pixels would race and lose samples). */
 __global__ void __launch_bounds__(CY_BLOCK) k_accumulate_stream(const CyTileDesc *descs, const hc_float4 *ring,
                                                                 uint ring_mask, int pass_stride)
 {
-  const CyTileDesc d = descs[blockIdx.y];
+  const int y = (int)blockIdx.y;
+  CyTileDesc d = descs[y];
+  if (y > 0 && stream_chunk_continues(descs[y - 1], d)) {
+    return;
+  }
+  for (int j = y + 1; j < (int)gridDim.y; j++) {
+    const CyTileDesc n = descs[j];
+    if (!stream_chunk_continues(descs[j - 1], n)) {
+      break;
+    }
+    d.num_samples += n.num_samples;
+  }
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < d.w * d.h) {
     accumulate_stream_pixel(d, ring, ring_mask, pass_stride, p);
@@ -1947,6 +1970,7 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
            * transparent / Lambert diffuse; anything else selects the full one */
           const uint ctype = node.y & 0xFF;
           closures += (ctype == CLOSURE_BSDF_PRINCIPLED_ID)                                 ? 8 :
+                      (ctype == CLOSURE_BSDF_HAIR_PRINCIPLED_ID)                            ? 4 :
                       (ctype >= CLOSURE_BSSRDF_CUBIC_ID && ctype <= CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID) ? 3 :
                       (ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID ||
                        ctype == CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID ||
@@ -1961,6 +1985,13 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
                   ctype == CLOSURE_BSDF_REFLECTION_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_ID ||
                   ctype == CLOSURE_BSDF_REFRACTION_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID ||
                   ctype == CLOSURE_BSDF_SHARP_GLASS_ID || ctype == CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID);
+          if (ctype == CLOSURE_BSDF_HAIR_PRINCIPLED_ID) {
+            len = 5; /* data node + 3 parameter nodes (the last: the Random attribute) */
+            if (off + 4 >= n) {
+              return "principled hair BSDF: parameter nodes past __svm_nodes";
+            }
+            *uses_attr |= prog[off + 4].y != SVM_STACK_INVALID;
+          }
           if (ctype == CLOSURE_BSDF_PRINCIPLED_ID) {
             len = 6; /* data node + 4 nodes of principled parameters */
             if (off + 5 >= n) {
@@ -1993,6 +2024,9 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             case CLOSURE_BSDF_GLOSSY_TOON_ID:
             case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
             case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
+            case CLOSURE_BSDF_HAIR_REFLECTION_ID:
+            case CLOSURE_BSDF_HAIR_TRANSMISSION_ID:
+            case CLOSURE_BSDF_HAIR_PRINCIPLED_ID:
             case CLOSURE_BSSRDF_RANDOM_WALK_ID: /* Subsurface Scattering node */
             case CLOSURE_BSSRDF_CUBIC_ID:
             case CLOSURE_BSSRDF_GAUSSIAN_ID:

@@ -1561,6 +1561,7 @@ CY_FN int bsdf_ashikhmin_shirley_sample(const CyClosure *sc,
 
 #if CY_CLOSURE_EXT
 #  include "cy_microfacet_multi.h"
+#  include "cy_hair.h"
 #endif
 
 /* ---------------------------------------------------------------------------
@@ -1672,6 +1673,13 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
     case CLOSURE_BSDF_GLOSSY_TOON_ID:
       label = bsdf_glossy_toon_sample(sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
+    case CLOSURE_BSDF_HAIR_REFLECTION_ID:
+    case CLOSURE_BSDF_HAIR_TRANSMISSION_ID:
+      label = bsdf_hair_sample(sc, sd->I, randu, randv, eval, omega_in, pdf);
+      break;
+    case CLOSURE_BSDF_HAIR_PRINCIPLED_ID:
+      label = bsdf_principled_hair_sample(sd, sc, randu, randv, eval, omega_in, pdf);
+      break;
 #endif
     case CLOSURE_NONE_ID:
       label = LABEL_NONE;
@@ -1754,6 +1762,12 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
       case CLOSURE_BSDF_GLOSSY_TOON_ID:
         eval = bsdf_glossy_toon_eval_reflect(sc, sd->I, omega_in, pdf);
         break;
+      case CLOSURE_BSDF_HAIR_PRINCIPLED_ID:
+        eval = bsdf_principled_hair_eval(sd, sc, omega_in, pdf);
+        break;
+      case CLOSURE_BSDF_HAIR_REFLECTION_ID:
+        eval = bsdf_hair_reflection_eval_reflect(sc, sd->I, omega_in, pdf);
+        break;
 #endif
       default: /* translucent, singular closures, NONE: zero */
         eval = mk3(0.0f, 0.0f, 0.0f);
@@ -1791,6 +1805,12 @@ CY_FN cfloat3 bsdf_eval(const CySD *sd, const CyClosure *sc, cfloat3 omega_in, f
       case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
       case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID:
         eval = bsdf_microfacet_multi_ggx_glass_eval(sd, sc, sd->I, omega_in, pdf, false);
+        break;
+      case CLOSURE_BSDF_HAIR_PRINCIPLED_ID:
+        eval = bsdf_principled_hair_eval(sd, sc, omega_in, pdf);
+        break;
+      case CLOSURE_BSDF_HAIR_TRANSMISSION_ID:
+        eval = bsdf_hair_transmission_eval_transmit(sc, sd->I, omega_in, pdf);
         break;
 #endif
       default:

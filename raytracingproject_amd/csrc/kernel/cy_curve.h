@@ -625,9 +625,10 @@ CY_FN bool curve_intersect(const CyGlobals *kg, CyIsect *isect, cfloat3 P, cfloa
   return false;
 }
 
-/* curve_shader_setup (:694-794) without dPdu / dPdv (no node of the HIP SVM
- * subset reads them): hit point, shading and geometric normal, u / v and the
- * curve's shader.  sd->prim is already __prim_index[isect->prim]. */
+/* curve_shader_setup (:694-794): hit point, shading and geometric normal,
+ * u / v, dPdu / dPdv (object space here, transformed with the normals by
+ * shader_setup_from_ray) and the curve's shader.  sd->prim is already
+ * __prim_index[isect->prim]. */
 CY_FN void curve_shader_setup(const CyGlobals *kg, CySD *sd, const CyIsect *isect, const CyRay *ray)
 {
   float t = isect->t;
@@ -663,6 +664,10 @@ CY_FN void curve_shader_setup(const CyGlobals *kg, CySD *sd, const CyIsect *isec
     sd->Ng = Ng;
     sd->v = 0.0f;
   }
+#if CY_CLOSURE_EXT
+  sd->dPdu = dPdu;
+  sd->dPdv = cross3(dPdu, sd->Ng);
+#endif
   if (isect->object != OBJECT_NONE) {
     P = transform_point(object_tfm(kg, isect->object), P);
   }

@@ -1761,6 +1761,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
             sc->alpha_x = fmaxf(blur_roughness, sc->alpha_x);
             sc->alpha_y = fmaxf(blur_roughness, sc->alpha_y);
           }
+#if CY_CLOSURE_EXT
+          else if (sc->type == CLOSURE_BSDF_HAIR_PRINCIPLED_ID) {
+            bsdf_principled_hair_blur(&sd, sc, blur_roughness);
+          }
+#endif
         }
       }
     }

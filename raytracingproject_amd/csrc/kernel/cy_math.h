@@ -315,6 +315,11 @@ CY_FN cfloat3 safe_normalize_len3(cfloat3 a, float *t)
   *t = len3(a);
   return (*t != 0.0f) ? div3f(a, *t) : a;
 }
+/* util_math.h:514 safe_divide_color */
+CY_FN cfloat3 safe_divide_color(cfloat3 a, cfloat3 b)
+{
+  return mk3((b.x != 0.0f) ? a.x / b.x : 0.0f, (b.y != 0.0f) ? a.y / b.y : 0.0f, (b.z != 0.0f) ? a.z / b.z : 0.0f);
+}
 CY_FN cfloat3 fabs3(cfloat3 a)
 {
   return mk3(fabsf(a.x), fabsf(a.y), fabsf(a.z));
@@ -1263,6 +1268,260 @@ CY_FN float cy_atan2f(float y, float x)
     default:
       return (z - pi_lo) - pi;
   }
+}
+#endif
+
+/* libm tanf, expm1f and sinhf as the reference's hair closures call them
+ * (closure/bsdf_hair.h sample: tanf; bsdf_hair_principled.h
+ * longitudinal_scattering: sinhf).  glibc 2.35's are fdlibm's float
+ * algorithms (sysdeps/ieee754/flt-32/k_tanf.c, s_expm1f.c, e_sinhf.c),
+ * restated with their published constants in their evaluation order (float,
+ * no FMA); tanf's range reduction is glibc's own (e_rem_pio2f.c, the sinf /
+ * cosf reduction in double) and its tiny-argument cotangent is a plain
+ * -1 / x.  Every float of both signs agrees with the container's libm for all
+ * three (tests/test_kernel_math.py samples it). */
+#if defined(CY_HOST_LIBM_SINCOS)
+CY_FN float cy_tanf(float x)
+{
+  return tanf(x);
+}
+CY_FN float cy_expm1f(float x)
+{
+  return expm1f(x);
+}
+CY_FN float cy_sinhf(float x)
+{
+  return sinhf(x);
+}
+#else
+CY_FN float cy_kernel_tanf(float x, float y, int iy)
+{
+  const float one = 1.0f, pio4 = 7.8539812565e-01f, pio4lo = 3.7748947079e-08f;
+  const float T0 = 3.3333334327e-01f, T1 = 1.3333334029e-01f, T2 = 5.3968254477e-02f, T3 = 2.1869488060e-02f,
+              T4 = 8.8632395491e-03f, T5 = 3.5920790397e-03f, T6 = 1.4562094584e-03f, T7 = 5.8804126456e-04f,
+              T8 = 2.4646313977e-04f, T9 = 7.8179444245e-05f, T10 = 7.1407252108e-05f, T11 = -1.8558637748e-05f,
+              T12 = 2.5907305826e-05f;
+  float z, r, v, w, s;
+  const int hx = as_int(x);
+  const int ix = hx & 0x7fffffff;
+  if (ix < 0x39000000) { /* |x| < 2^-13 */
+    if ((int)x == 0) {
+      if ((ix | (iy + 1)) == 0) {
+        return one / fabsf(x);
+      }
+      else if (iy == 1) {
+        return x;
+      }
+      else {
+        return -one / x;
+      }
+    }
+  }
+  if (ix >= 0x3f2ca140) { /* |x| >= 0.6744 */
+    if (hx < 0) {
+      x = -x;
+      y = -y;
+    }
+    z = pio4 - x;
+    w = pio4lo - y;
+    x = z + w;
+    y = 0.0f;
+    if (fabsf(x) < 0x1p-13f) {
+      return (float)(1 - ((hx >> 30) & 2)) * (float)iy * (1.0f - 2.0f * (float)iy * x);
+    }
+  }
+  z = x * x;
+  w = z * z;
+  r = T1 + w * (T3 + w * (T5 + w * (T7 + w * (T9 + w * T11))));
+  v = z * (T2 + w * (T4 + w * (T6 + w * (T8 + w * (T10 + w * T12)))));
+  s = z * x;
+  r = y + z * (s * (r + v) + y);
+  r += T0 * s;
+  w = x + r;
+  if (ix >= 0x3f2ca140) {
+    v = (float)iy;
+    return (float)(1 - ((hx >> 30) & 2)) * (v - 2.0f * (x - (w * w / (w + v) - r)));
+  }
+  if (iy == 1) {
+    return w;
+  }
+  /* -1.0 / (x + r) accurately */
+  z = w;
+  z = int_as_float(as_int(z) & 0xfffff000);
+  v = r - (z - x);
+  float t, a;
+  t = a = -1.0f / w;
+  t = int_as_float(as_int(t) & 0xfffff000);
+  s = 1.0f + t * z;
+  return t + a * (s + t * v);
+}
+
+/* __ieee754_rem_pio2f (glibc 2.35 e_rem_pio2f.c): the sinf / cosf range
+ * reduction (sincosf.h reduce_fast below 120, reduce_large above) in double,
+ * split into y[0] + y[1]; compiled without FMA (not a multiarch routine), so
+ * the fast step is a separate multiply and subtract. */
+CY_FN int cy_rem_pio2f(float x, float *y)
+{
+  const struct cy_sincos_t *p = &cy_sincosf_table[0];
+  double dx = x;
+  int n;
+  if (cy_abstop12(x) < cy_abstop12(120.0f)) {
+    const double r = dx * p->hpi_inv;
+    n = ((int32_t)r + 0x800000) >> 24;
+    const double nh = (double)n * p->hpi;
+    dx = dx - nh;
+  }
+  else {
+    const uint xi = as_uint(x);
+    dx = cy_sincos_reduce_large(xi, &n);
+    dx = (xi >> 31) ? -dx : dx;
+  }
+  y[0] = (float)dx;
+  y[1] = (float)(dx - (double)y[0]);
+  return n;
+}
+
+CY_FN float cy_tanf(float x)
+{
+  const int ix = as_int(x) & 0x7fffffff;
+  if (ix <= 0x3f490fda) {
+    return cy_kernel_tanf(x, 0.0f, 1);
+  }
+  if (ix >= 0x7f800000) {
+    return x - x;
+  }
+  float y[2];
+  const int n = cy_rem_pio2f(x, y);
+  return cy_kernel_tanf(y[0], y[1], 1 - ((n & 1) << 1));
+}
+
+CY_FN float cy_expm1f(float x)
+{
+  const float one = 1.0f, huge = 1.0e+30f, tiny = 1.0e-30f, o_threshold = 8.8721679688e+01f,
+              ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f, invln2 = 1.4426950216e+00f,
+              Q1 = -3.3333335072e-02f, Q2 = 1.5873016091e-03f, Q3 = -7.9365076090e-05f, Q4 = 4.0082177293e-06f,
+              Q5 = -2.0109921195e-07f;
+  float y, hi, lo, c = 0.0f, t, e, hxs, hfx, r1;
+  int k;
+  uint hx = as_uint(x);
+  const uint xsb = hx & 0x80000000u;
+  hx &= 0x7fffffffu;
+  if (hx == 0u) {
+    return x; /* +-0 */
+  }
+  if (hx >= 0x4195b844u) { /* |x| >= 27 ln2 */
+    if (hx >= 0x42b17218u) {
+      if (hx > 0x7f800000u) {
+        return x + x;
+      }
+      if (hx == 0x7f800000u) {
+        return (xsb == 0) ? x : -1.0f;
+      }
+      if (x > o_threshold) {
+        return huge * huge;
+      }
+    }
+    if (xsb != 0) {
+      return tiny - one;
+    }
+  }
+  if (hx > 0x3eb17218u) { /* |x| > 0.5 ln2 */
+    if (hx < 0x3F851592u) {
+      if (xsb == 0) {
+        hi = x - ln2_hi;
+        lo = ln2_lo;
+        k = 1;
+      }
+      else {
+        hi = x + ln2_hi;
+        lo = -ln2_lo;
+        k = -1;
+      }
+    }
+    else {
+      k = (int)(invln2 * x + ((xsb == 0) ? 0.5f : -0.5f));
+      t = (float)k;
+      hi = x - t * ln2_hi;
+      lo = t * ln2_lo;
+    }
+    x = hi - lo;
+    c = (hi - x) - lo;
+  }
+  else if (hx < 0x33000000u) { /* |x| < 2^-25 */
+    t = huge + x;
+    return x - (t - (huge + x));
+  }
+  else {
+    k = 0;
+  }
+  hfx = 0.5f * x;
+  hxs = x * hfx;
+  r1 = one + hxs * (Q1 + hxs * (Q2 + hxs * (Q3 + hxs * (Q4 + hxs * Q5))));
+  t = 3.0f - r1 * hfx;
+  e = hxs * ((r1 - t) / (6.0f - x * t));
+  if (k == 0) {
+    return x - (x * e - hxs);
+  }
+  e = (x * (e - c) - c);
+  e -= hxs;
+  if (k == -1) {
+    return 0.5f * (x - e) - 0.5f;
+  }
+  if (k == 1) {
+    if (x < -0.25f) {
+      return -2.0f * (e - (x + 0.5f));
+    }
+    return one + 2.0f * (x - e);
+  }
+  if (k <= -2 || k > 56) {
+    y = one - (e - x);
+    y = int_as_float(as_int(y) + (k << 23));
+    return y - one;
+  }
+  if (k < 23) {
+    t = int_as_float(0x3f800000 - (0x1000000 >> k)); /* 1 - 2^-k */
+    y = t - (e - x);
+    y = int_as_float(as_int(y) + (k << 23));
+  }
+  else {
+    t = int_as_float((0x7f - k) << 23); /* 2^-k */
+    y = x - (e + t);
+    y += one;
+    y = int_as_float(as_int(y) + (k << 23));
+  }
+  return y;
+}
+
+CY_FN float cy_sinhf(float x)
+{
+  const float one = 1.0f, shuge = 1.0e37f;
+  const int jx = as_int(x);
+  const int ix = jx & 0x7fffffff;
+  if (ix >= 0x7f800000) {
+    return x + x;
+  }
+  const float h = (jx < 0) ? -0.5f : 0.5f;
+  if (ix < 0x41b00000) { /* |x| < 22 */
+    if (ix < 0x31800000) { /* |x| < 2^-28 */
+      if (shuge + x > one) {
+        return x;
+      }
+    }
+    const float t = cy_expm1f(fabsf(x));
+    if (ix < 0x3f800000) {
+      return h * (2.0f * t - t * t / (t + one));
+    }
+    return h * (t + t / (t + one));
+  }
+  if (ix < 0x42b17180) {
+    return h * cy_expf(fabsf(x));
+  }
+  if (ix <= 0x42b2d4fc) {
+    const float w = cy_expf(0.5f * fabsf(x));
+    const float t = h * w;
+    return t * w;
+  }
+  return x * shuge;
 }
 #endif
 

@@ -981,6 +981,17 @@ CY_FN void triangle_verts(const CyGlobals *kg, int prim, cfloat3 V[3])
   V[2] = f4to3(kg->__prim_tri_verts[tri_vindex.w + 2]);
 }
 
+#if CY_CLOSURE_EXT
+/* triangle_dPdudv (geom_triangle.h): derivatives of P w.r.t. the barycentric u, v */
+CY_FN void triangle_dPdudv(const CyGlobals *kg, int prim, cfloat3 *dPdu, cfloat3 *dPdv)
+{
+  cfloat3 V[3];
+  triangle_verts(kg, prim, V);
+  *dPdu = sub3(V[0], V[2]);
+  *dPdv = sub3(V[1], V[2]);
+}
+#endif
+
 CY_FN cfloat3 triangle_normal(const CyGlobals *kg, const CySD *sd)
 {
   cfloat3 V[3];
@@ -1070,6 +1081,9 @@ CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *i
     if ((uint)sd->shader & SHADER_SMOOTH_NORMAL) {
       sd->N = triangle_smooth_normal(kg, Ng, sd->prim, sd->u, sd->v);
     }
+#if CY_CLOSURE_EXT
+    triangle_dPdudv(kg, sd->prim, &sd->dPdu, &sd->dPdv);
+#endif
   }
   sd->I = neg3(ray->D);
   sd->flag |= kg->__shaders[(uint)sd->shader & SHADER_MASK].flags;
@@ -1077,6 +1091,10 @@ CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *i
     /* instance transform */
     sd->N = object_normal_transform(kg, sd->object, sd->N);
     sd->Ng = object_normal_transform(kg, sd->object, sd->Ng);
+#if CY_CLOSURE_EXT
+    sd->dPdu = transform_direction(object_tfm(kg, sd->object), sd->dPdu);
+    sd->dPdv = transform_direction(object_tfm(kg, sd->object), sd->dPdv);
+#endif
   }
 
   bool backfacing = (dot3(sd->Ng, sd->I) < 0.0f);
@@ -1084,6 +1102,10 @@ CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *i
     sd->flag |= SD_BACKFACING;
     sd->Ng = neg3(sd->Ng);
     sd->N = neg3(sd->N);
+#if CY_CLOSURE_EXT
+    sd->dPdu = neg3(sd->dPdu);
+    sd->dPdv = neg3(sd->dPdv);
+#endif
   }
 }
 
@@ -1627,6 +1649,13 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
     if (type == CLOSURE_BSDF_PRINCIPLED_ID) {
       *offset += 4; /* the principled node's extra data */
     }
+#if CY_CLOSURE_EXT
+    else if (type == CLOSURE_BSDF_HAIR_PRINCIPLED_ID) {
+      /* the reference skips none of the principled hair node's three extra
+       * data nodes here and runs them as instructions (svm_closure.h:75-85) */
+      cy_set_error(err, CY_ERR_FEATURE, 13);
+    }
+#endif
     return;
   }
   cfloat3 N = (data_node.x != SVM_STACK_INVALID) ? svm_load3(stack, data_node.x, err) : sd->N;
@@ -1884,6 +1913,105 @@ CY_FN void svm_node_closure_bsdf(const CyGlobals *kg,
         b->alpha_x = param1;
         b->alpha_y = param2;
         sd->flag |= bsdf_toon_setup(b, (int)type);
+      }
+      break;
+    }
+    case CLOSURE_BSDF_HAIR_PRINCIPLED_ID: {
+      /* svm_closure.h:735-844 (Principled Hair BSDF node) */
+      const hc_uint4 data_node2 = kg->__svm_nodes[(*offset)++];
+      const hc_uint4 data_node3 = kg->__svm_nodes[(*offset)++];
+      const hc_uint4 data_node4 = kg->__svm_nodes[(*offset)++];
+      const cfloat3 weight = mul3f(sd->svm_closure_weight, mix_weight);
+      const uint offset_ofs = data_node.y & 0xFF, ior_ofs = (data_node.y >> 8) & 0xFF;
+      const uint color_ofs = (data_node.y >> 16) & 0xFF, parametrization = data_node.y >> 24;
+      const float alpha = svm_load_default(stack, offset_ofs, data_node.z, err);
+      const float ior = svm_load_default(stack, ior_ofs, data_node.w, err);
+      const uint coat_ofs = data_node2.x & 0xFF, melanin_ofs = (data_node2.x >> 8) & 0xFF;
+      const uint melanin_redness_ofs = (data_node2.x >> 16) & 0xFF, absorption_ofs = data_node2.x >> 24;
+      const uint tint_ofs = data_node3.x & 0xFF, random_ofs = (data_node3.x >> 8) & 0xFF;
+      const uint random_color_ofs = (data_node3.x >> 16) & 0xFF, random_roughness_ofs = data_node3.x >> 24;
+      float random = 0.0f;
+      const CyAttr attr_random = (data_node4.y != SVM_STACK_INVALID) ?
+                                     find_attribute(kg, sd->object, sd->prim, data_node4.y) :
+                                     attribute_not_found();
+      if (attr_random.offset != (int)ATTR_STD_NOT_FOUND) {
+        cy_set_error(err, CY_ERR_FEATURE, 11); /* curve attributes are not packed */
+      }
+      else {
+        random = svm_load_default(stack, random_ofs, data_node3.y, err);
+      }
+      CyClosure *b = bsdf_alloc(sd, weight);
+      if (b) {
+        const int extra = closure_alloc_extra(sd);
+        if (extra < 0) {
+          break;
+        }
+        CyClosure *ex = &sd->closure[extra];
+        const float random_roughness = svm_load_default(stack, random_roughness_ofs, data_node3.w, err);
+        const float factor_random_roughness = 1.0f + 2.0f * (random - 0.5f) * random_roughness;
+        const float roughness = param1 * factor_random_roughness;
+        const float radial_roughness = param2 * factor_random_roughness;
+        const float coat = svm_load_default(stack, coat_ofs, data_node2.y, err);
+        const float m0_roughness = 1.0f - cclamp(coat, 0.0f, 1.0f);
+        b->N = N;
+        b->alpha_x = roughness;
+        b->alpha_y = radial_roughness;
+        b->ior = ior;
+        b->extra = extra;
+        ex->ior = m0_roughness;
+        ex->alpha_y = alpha;
+        ex->T = mk3(KD->film.rgb_to_y.x, KD->film.rgb_to_y.y, KD->film.rgb_to_y.z);
+        switch (parametrization) {
+          case 2: /* NODE_PRINCIPLED_HAIR_DIRECT_ABSORPTION */
+            b->T = svm_load3(stack, absorption_ofs, err);
+            break;
+          case 1: { /* NODE_PRINCIPLED_HAIR_PIGMENT_CONCENTRATION */
+            float melanin = svm_load_default(stack, melanin_ofs, data_node2.z, err);
+            const float melanin_redness = svm_load_default(stack, melanin_redness_ofs, data_node2.w, err);
+            float random_color = svm_load_default(stack, random_color_ofs, data_node3.z, err);
+            random_color = cclamp(random_color, 0.0f, 1.0f);
+            const float factor_random_color = 1.0f + 2.0f * (random - 0.5f) * random_color;
+            melanin *= factor_random_color;
+            melanin = -cy_logf(fmaxf(1.0f - melanin, 0.0001f));
+            const float eumelanin = melanin * (1.0f - melanin_redness);
+            const float pheomelanin = melanin * melanin_redness;
+            const cfloat3 melanin_sigma = bsdf_principled_hair_sigma_from_concentration(eumelanin, pheomelanin);
+            const cfloat3 tint = svm_load3(stack, tint_ofs, err);
+            const cfloat3 tint_sigma = bsdf_principled_hair_sigma_from_reflectance(tint, radial_roughness);
+            b->T = add3(melanin_sigma, tint_sigma);
+            break;
+          }
+          case 0: /* NODE_PRINCIPLED_HAIR_REFLECTANCE */
+            b->T = bsdf_principled_hair_sigma_from_reflectance(svm_load3(stack, color_ofs, err), radial_roughness);
+            break;
+          default:
+            b->T = bsdf_principled_hair_sigma_from_concentration(0.0f, 0.8054375f);
+            break;
+        }
+        sd->flag |= bsdf_principled_hair_setup(sd, b, ex);
+      }
+      break;
+    }
+    case CLOSURE_BSDF_HAIR_REFLECTION_ID:
+    case CLOSURE_BSDF_HAIR_TRANSMISSION_ID: {
+      /* svm_closure.h:846-877 (Hair BSDF node) */
+      CyClosure *b = bsdf_alloc(sd, mul3f(sd->svm_closure_weight, mix_weight));
+      if (b) {
+        b->N = N;
+        b->alpha_x = param1;
+        b->alpha_y = param2;
+        b->ior = -svm_load(stack, data_node.z, err);
+        if (data_node.y != SVM_STACK_INVALID) {
+          b->T = normalize3(svm_load3(stack, data_node.y, err));
+        }
+        else if (!(sd->type & PRIMITIVE_ALL_CURVE)) {
+          b->T = normalize3(sd->dPdv);
+          b->ior = 0.0f;
+        }
+        else {
+          b->T = normalize3(sd->dPdu);
+        }
+        sd->flag |= bsdf_hair_setup(b, (int)type);
       }
       break;
     }

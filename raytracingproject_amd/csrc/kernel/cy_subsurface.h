@@ -195,12 +195,6 @@ CY_FN float volume_channel_get(cfloat3 value, int channel)
   return (channel == 0) ? value.x : ((channel == 1) ? value.y : value.z);
 }
 
-/* util_math.h:514 safe_divide_color */
-CY_FN cfloat3 safe_divide_color(cfloat3 a, cfloat3 b)
-{
-  return mk3((b.x != 0.0f) ? a.x / b.x : 0.0f, (b.y != 0.0f) ? a.y / b.y : 0.0f, (b.z != 0.0f) ? a.z / b.z : 0.0f);
-}
-
 /* volume_color_transmittance: exp3(-sigma * t) */
 CY_FN cfloat3 volume_color_transmittance(cfloat3 sigma, float t)
 {
@@ -361,15 +355,20 @@ CY_FN void shader_setup_from_subsurface(const CyGlobals *kg, CySD *sd, const CyI
   if ((uint)sd->shader & SHADER_SMOOTH_NORMAL) {
     sd->N = triangle_smooth_normal(kg, Ng, sd->prim, sd->u, sd->v);
   }
+  triangle_dPdudv(kg, sd->prim, &sd->dPdu, &sd->dPdv);
   sd->flag |= kg->__shaders[(uint)sd->shader & SHADER_MASK].flags;
   if (isect->object != OBJECT_NONE) {
     sd->N = object_normal_transform(kg, sd->object, sd->N);
     sd->Ng = object_normal_transform(kg, sd->object, sd->Ng);
+    sd->dPdu = transform_direction(object_tfm(kg, sd->object), sd->dPdu);
+    sd->dPdv = transform_direction(object_tfm(kg, sd->object), sd->dPdv);
   }
   if (backfacing) {
     sd->flag |= SD_BACKFACING;
     sd->Ng = neg3(sd->Ng);
     sd->N = neg3(sd->N);
+    sd->dPdu = neg3(sd->dPdu);
+    sd->dPdv = neg3(sd->dPdv);
   }
   sd->I = sd->N;
 }

@@ -370,6 +370,8 @@ typedef struct CySD {
    * closure; mutable because evaluation otherwise reads the shading point
    * only (the reference passes ShaderData by non-const pointer for it) */
   mutable uint lcg_state;
+  /* surface derivatives (__DPDU__): hair closures, the Tangent node fallback */
+  cfloat3 dPdu, dPdv;
 #endif
 } CySD;
 

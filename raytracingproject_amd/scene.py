@@ -74,6 +74,20 @@ CLOSURE_BSDF_MICROFACET_BECKMANN_GLASS_ID = 26
 CLOSURE_BSDF_MICROFACET_GGX_GLASS_ID = 27
 CLOSURE_BSDF_SHARP_GLASS_ID = 29
 CLOSURE_BSDF_TRANSPARENT_ID = 34
+CLOSURE_BSDF_HAIR_REFLECTION_ID = 21
+CLOSURE_BSDF_HAIR_PRINCIPLED_ID = 30
+CLOSURE_BSDF_HAIR_TRANSMISSION_ID = 31
+ATTR_STD_CURVE_RANDOM = 15  # kernel_types.h AttributeStandard
+# PrincipledHairBsdfNode (nodes.cpp:3474-3512): parametrization enum
+# (svm_types.h:509-513) and socket defaults
+PRINCIPLED_HAIR_PARAMETRIZATIONS = {"color": 0, "melanin": 1, "absorption": 2}
+PRINCIPLED_HAIR_DEFAULTS = {
+    "color": (0.017513, 0.005763, 0.002059), "melanin": 0.8, "melanin_redness": 1.0, "tint": (1.0, 1.0, 1.0),
+    "absorption_coefficient": (0.245531, 0.52, 1.365), "offset": 2.0 * 3.14159265358979 / 180.0, "roughness": 0.3,
+    "radial_roughness": 0.3, "coat": 0.0, "ior": 1.55, "random_roughness": 0.0, "random_color": 0.0,
+    "random": 0.0, "normal": None}
+# HairBsdfNode (nodes.cpp:3603-3635)
+HAIR_DEFAULTS = {"offset": 0.0, "roughness_u": 0.2, "roughness_v": 0.2}
 # Subsurface Scattering node falloffs (nodes.cpp SubsurfaceScatteringNode)
 SUBSURFACE_FALLOFFS = {"cubic": 35, "gaussian": 36, "burley": 38, "random_walk": 39}
 CLOSURE_BSSRDF_PRINCIPLED_RANDOM_WALK_ID = 40
@@ -184,6 +198,11 @@ class Closure:
             return REFRACTION_DISTRIBUTIONS["sharp" if sharp else self.distribution]
         if self.kind == "subsurface":
             return SUBSURFACE_FALLOFFS[self.distribution]
+        if self.kind == "hair":
+            return CLOSURE_BSDF_HAIR_TRANSMISSION_ID if self.distribution == "transmission" else \
+                CLOSURE_BSDF_HAIR_REFLECTION_ID
+        if self.kind == "principled_hair":
+            return CLOSURE_BSDF_HAIR_PRINCIPLED_ID
         return {"diffuse": CLOSURE_BSDF_DIFFUSE_ID, "translucent": CLOSURE_BSDF_TRANSLUCENT_ID,
                 "velvet": CLOSURE_BSDF_ASHIKHMIN_VELVET_ID, "diffuse_toon": CLOSURE_BSDF_DIFFUSE_TOON_ID,
                 "glossy_toon": CLOSURE_BSDF_GLOSSY_TOON_ID, "transparent": CLOSURE_BSDF_TRANSPARENT_ID}[self.kind]
@@ -200,6 +219,8 @@ class Closure:
             return 8  # CLOSURE_IS_PRINCIPLED
         if self.kind == "subsurface":
             return 3  # CLOSURE_IS_BSSRDF
+        if self.kind == "principled_hair":
+            return 4  # graph.cpp:1153-1155
         if self.kind in VOLUME_KINDS:
             return VOLUME_STACK_SIZE  # CLOSURE_IS_VOLUME
         if self.kind in ("none", "emission", "background"):
@@ -240,11 +261,12 @@ class Closure:
             v = getattr(self, name)
             if nodes.is_linked(v) and (self.kind == "mix") == (name == "fac"):
                 out.append((v, t))
-        if self.kind in ("principled", "principled_volume"):
+        if self.kind in ("principled", "principled_volume", "principled_hair", "hair"):
             for name, v in self.params.items():
                 if nodes.is_linked(v):
-                    vec = name in PRINCIPLED_VECTORS or name == "subsurface_radius"
-                    out.append((v, "color" if name.endswith("color") else "vector" if vec else "float"))
+                    vec = name in PRINCIPLED_VECTORS or name in ("subsurface_radius", "absorption_coefficient")
+                    col = name.endswith("color") and name != "random_color" or name == "tint"
+                    out.append((v, "color" if col else "vector" if vec else "float"))
         for sub in (self.a, self.b):
             if sub is not None:
                 out.extend(sub.sockets())
@@ -331,6 +353,39 @@ def subsurface(color, scale=0.01, radius=(0.1, 0.1, 0.1), falloff="burley", text
         raise ValueError(f"subsurface: unknown falloff {falloff}")
     return Closure("subsurface", _const_or_socket(color), strength=scale, radius=radius, distribution=falloff,
                    texture_blur=texture_blur, sharpness=sharpness, normal=normal)
+
+
+def principled_hair(parametrization="color", **params):
+    """Principled Hair BSDF node (nodes.cpp:3474-3593 PrincipledHairBsdfNode,
+    closure/bsdf_hair_principled.h): parametrization "color" (direct
+    colouring), "melanin" (pigment concentration, with tint and random
+    colour) or "absorption" (absorption coefficient); parameters are
+    PRINCIPLED_HAIR_DEFAULTS keys (constants or sockets).  Random defaults to
+    the curves' ATTR_STD_CURVE_RANDOM attribute when unlinked (absent here:
+    the node's Random value is used)."""
+    unknown = set(params) - set(PRINCIPLED_HAIR_DEFAULTS)
+    if unknown:
+        raise ValueError(f"principled_hair: unknown parameters {sorted(unknown)}")
+    if parametrization not in PRINCIPLED_HAIR_PARAMETRIZATIONS:
+        raise ValueError(f"principled_hair: parametrization one of {sorted(PRINCIPLED_HAIR_PARAMETRIZATIONS)}")
+    p = dict(PRINCIPLED_HAIR_DEFAULTS)
+    p.update(params)
+    return Closure("principled_hair", distribution=parametrization, params=p)
+
+
+def hair(color=(0.8, 0.8, 0.8), component="reflection", tangent=None, normal=None, **params):
+    """Hair BSDF node (nodes.cpp:3603-3635 HairBsdfNode, closure/bsdf_hair.h):
+    component "reflection" or "transmission"; offset, roughness_u,
+    roughness_v (HAIR_DEFAULTS keys); the tangent defaults to the curve's
+    dPdu (dPdv on meshes, offset 0)."""
+    unknown = set(params) - set(HAIR_DEFAULTS)
+    if unknown:
+        raise ValueError(f"hair: unknown parameters {sorted(unknown)}")
+    if component not in ("reflection", "transmission"):
+        raise ValueError("hair: component is reflection or transmission")
+    p = dict(HAIR_DEFAULTS)
+    p.update(params)
+    return Closure("hair", _const_or_socket(color), distribution=component, params=p, tangent=tangent, normal=normal)
 
 
 VOLUME_KINDS = ("volume_absorption", "volume_scatter", "principled_volume")
@@ -487,6 +542,8 @@ class SVMCompiler:
             return out
         if c.kind == "principled":
             return self.emit_principled(c, mix_weight)
+        if c.kind == "principled_hair":
+            return self.emit_principled_hair(c, mix_weight)
         if c.kind == "none":
             return out
         if c.kind in VOLUME_KINDS:
@@ -517,6 +574,12 @@ class SVMCompiler:
                 # GlossyBsdfNode::compile (nodes.cpp:2423-2424): the colour
                 # goes to the multiscatter walk as param4 (stack-assigned)
                 param4_off = self.nc.assign(c.color, "color")
+        elif c.kind == "hair":
+            # HairBsdfNode::compile: BsdfNode::compile(RoughnessU, RoughnessV, Offset)
+            params = (c.params["roughness_u"], c.params["roughness_v"])
+            param3_off = self.nc.assign(c.params["offset"], "float")
+            if nodes.is_linked(c.tangent):
+                tangent_off = self.nc.link(c.tangent, "vector")
         elif c.kind == "subsurface":
             # BsdfNode::compile(Scale, Texture Blur, Radius, Sharpness): radius and
             # sharpness always stack-assigned
@@ -633,6 +696,55 @@ class SVMCompiler:
         emit((cc_normal_off, radius_off, SVM_STACK_INVALID, SVM_STACK_INVALID))
         ssc = const(p["subsurface_color"], PRINCIPLED_DEFAULTS["subsurface_color"])
         emit((ss_off, *(f32bits(x) for x in ssc)))
+        for off, w in temps:
+            self.free(off, w)
+        return out
+
+    def emit_principled_hair(self, c: Closure, mix_weight: int) -> list:
+        """nodes.cpp:3529-3593 PrincipledHairBsdfNode::compile: weight (1,1,1),
+        Color / Tint / Absorption Coefficient stack-assigned (temporaries),
+        the other inputs by slot when linked and inline otherwise, the Random
+        attribute request when Random is unlinked; the closure node and four
+        data nodes."""
+        out = []
+        emit = out.append
+        p = c.params
+        nc = self.nc
+        emit((NODE_CLOSURE_SET_WEIGHT, f32bits(1.0), f32bits(1.0), f32bits(1.0)))
+        temps: list = []
+        saved_emit, nc.emit = nc.emit, emit
+        try:
+            color_off = nc.assign(p["color"], "color", temps)
+            tint_off = nc.assign(p["tint"], "color", temps)
+            absorption_off = nc.assign(p["absorption_coefficient"], "vector", temps)
+
+            def lk(name, t="float"):
+                v = p.get(name)
+                return nc.link(v, t) if nodes.is_linked(v) else SVM_STACK_INVALID
+
+            offs = {k: lk(k) for k in ("roughness", "radial_roughness", "offset", "ior", "coat", "melanin",
+                                       "melanin_redness", "random", "random_color", "random_roughness")}
+            normal_off = lk("normal", "vector")
+        finally:
+            nc.emit = saved_emit
+        attr_random = SVM_STACK_INVALID if nodes.is_linked(p["random"]) else self.attribute(ATTR_STD_CURVE_RANDOM)
+
+        def f(name):
+            v = p[name]
+            return f32bits(0.0 if nodes.is_linked(v) else float(v))
+
+        emit((NODE_CLOSURE_BSDF,
+              self.uchar4(CLOSURE_BSDF_HAIR_PRINCIPLED_ID, offs["roughness"], offs["radial_roughness"], mix_weight),
+              f("roughness"), f("radial_roughness")))
+        emit((normal_off,
+              self.uchar4(offs["offset"], offs["ior"], color_off, PRINCIPLED_HAIR_PARAMETRIZATIONS[c.distribution]),
+              f("offset"), f("ior")))
+        emit((self.uchar4(offs["coat"], offs["melanin"], offs["melanin_redness"], absorption_off),
+              f("coat"), f("melanin"), f("melanin_redness")))
+        emit((self.uchar4(tint_off, offs["random"], offs["random_color"], offs["random_roughness"]),
+              f("random"), f("random_color"), f("random_roughness")))
+        emit((self.uchar4(SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID, SVM_STACK_INVALID), attr_random,
+              SVM_STACK_INVALID, SVM_STACK_INVALID))
         for off, w in temps:
             self.free(off, w)
         return out

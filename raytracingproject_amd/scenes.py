@@ -522,16 +522,33 @@ def _sphere_fur(rng, center, radius, n, n_keys, length, r_root, r_tip, kink, gra
     return _strands(rng, roots, d, n_keys, length, r_root, r_tip, kink, gravity)
 
 
-def hair_ball(width=48, height=48, samples=8, shape="ribbon", strands=300, name=None) -> sc.Scene:
+def hair_ball(width=48, height=48, samples=8, shape="ribbon", strands=300, name=None, fur="plain") -> sc.Scene:
     """A furry ball on a floor (golden parity case for curves): strands with 5
     keys (4 Catmull-Rom segments each) of two hair materials around a diffuse
     core, lit by an area lamp and an emissive panel; unaligned BVH nodes bound
-    the curve-only subtrees."""
+    the curve-only subtrees.  fur="principled": Principled Hair BSDFs (melanin
+    with tint and random colour / roughness; a mix of the absorption and
+    direct-colour parametrizations with coat); fur="hair_bsdf": the Hair BSDF
+    node's reflection and transmission components, also on the core mesh
+    (tangent from dPdv there)."""
     rng = np.random.default_rng(0x5EED + 40)
     white = sc.diffuse((0.7, 0.7, 0.7))
     core = sc.diffuse((0.5, 0.3, 0.2))
     fur_a = sc.diffuse((0.8, 0.5, 0.25))
     fur_b = sc.mix(0.3, sc.glossy((0.9, 0.8, 0.7), 0.25), sc.diffuse((0.3, 0.2, 0.1)))
+    if fur == "principled":
+        fur_a = sc.principled_hair("melanin", melanin=0.65, melanin_redness=0.4, tint=(0.9, 0.75, 0.6),
+                                   random=0.3, random_color=0.4, random_roughness=0.3, roughness=0.35,
+                                   radial_roughness=0.5)
+        fur_b = sc.mix(0.4, sc.principled_hair("absorption", absorption_coefficient=(0.3, 0.6, 1.2), coat=0.4,
+                                               roughness=0.08, radial_roughness=0.3),
+                       sc.principled_hair("color", color=(0.45, 0.3, 0.2), ior=1.6, offset=0.06))
+    elif fur == "hair_bsdf":
+        fur_a = sc.mix(0.5, sc.hair((0.9, 0.7, 0.5), "reflection", roughness_u=0.15, roughness_v=0.4, offset=0.05),
+                       sc.hair((0.8, 0.5, 0.3), "transmission", roughness_u=0.3, roughness_v=0.6))
+        fur_b = sc.hair((0.6, 0.6, 0.65), "reflection", roughness_u=0.05, roughness_v=0.2)
+        core = sc.mix(0.5, sc.diffuse((0.5, 0.3, 0.2)), sc.hair((0.8, 0.8, 0.8), "reflection", roughness_u=0.2,
+                                                                   roughness_v=0.3, offset=0.1))
     light = sc.emission((1.0, 0.9, 0.8), 6.0)
     materials = [white, core, fur_a, fur_b, light]
     meshes = [sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0),
@@ -546,13 +563,14 @@ def hair_ball(width=48, height=48, samples=8, shape="ribbon", strands=300, name=
                     farclip=100.0)
     return sc.Scene(width, height, cam, meshes, materials, world_color=(0.15, 0.17, 0.2), world_strength=1.0,
                     samples=samples, lamps=lamps, hairs=hairs, hair_shape=shape,
-                    name=name or f"hair_ball_{shape}")
+                    name=name or f"hair_ball_{shape}" + ("" if fur == "plain" else "_" + fur))
 
 
 def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="ribbon") -> sc.Scene:
     """Junk Shop-class stand-in (SURVEY.md §8(d) config JNK): a cluttered shop
     interior (shelves of boxes, a counter, barrels) with furry props -- a rug,
-    brushes and fur balls -- about 1.3M curve segments at detail 1, lit by
+    brushes and fur balls, Principled Hair BSDF strands -- about 1.3M curve
+    segments at detail 1, lit by
     area lamps and a window panel -- and volumes: a dusty (homogeneous,
     forward-scattering) atmosphere in the world and a smoke volume in the
     window light (a volume-only box with a principled volume)."""
@@ -561,9 +579,13 @@ def junkshop_standin(width=3840, height=2160, samples=1024, detail=1.0, shape="r
     wood = sc.mix(0.2, sc.glossy((0.6, 0.45, 0.3), 0.3), sc.diffuse((0.45, 0.3, 0.18)))
     metal = sc.glossy((0.8, 0.8, 0.85), 0.15)
     cardboard = sc.diffuse((0.6, 0.48, 0.32))
-    fur1 = sc.diffuse((0.75, 0.6, 0.4))
-    fur2 = sc.mix(0.25, sc.glossy((0.9, 0.85, 0.8), 0.3), sc.diffuse((0.25, 0.2, 0.15)))
-    rug = sc.diffuse((0.5, 0.12, 0.1))
+    # fur and rug strands with the Principled Hair BSDF (the node Blender
+    # hair uses): melanin-pigmented, direct-coloured with a coat, and a
+    # red direct-coloured rug
+    fur1 = sc.principled_hair("melanin", melanin=0.55, melanin_redness=0.6, tint=(1.0, 0.9, 0.8), roughness=0.3,
+                              radial_roughness=0.4)
+    fur2 = sc.principled_hair("color", color=(0.22, 0.16, 0.1), coat=0.3, roughness=0.25, radial_roughness=0.35)
+    rug = sc.principled_hair("color", color=(0.5, 0.12, 0.1), roughness=0.5, radial_roughness=0.6)
     window = sc.emission((1.0, 0.97, 0.9), 8.0)
     smoke = sc.material(volume=sc.principled_volume((0.7, 0.7, 0.72), density=0.35, anisotropy=0.3,
                                                     absorption_color=(0.4, 0.4, 0.45)))

@@ -84,3 +84,34 @@ extern "C" long lgammaf_sweep(uint32_t lo, uint32_t hi, uint32_t step, uint32_t 
   }
   return bad;
 }
+
+/* cy_tanf / cy_expm1f / cy_sinhf (glibc restatements) against libm over [lo, hi]
+ * bit patterns: which = 0 tanf, 1 expm1f, 2 sinhf; returns the mismatches. */
+extern "C" long libm_sweep(int which, uint32_t lo, uint32_t hi, uint32_t step, uint32_t *first)
+{
+  long bad = 0;
+  for (uint64_t u = lo; u <= hi; u += step) {
+    const float x = as_float((uint32_t)u);
+    volatile float vx = x;
+    float a, b;
+    if (which == 0) {
+      a = cy_tanf(x);
+      b = tanf(vx);
+    }
+    else if (which == 1) {
+      a = cy_expm1f(x);
+      b = expm1f(vx);
+    }
+    else {
+      a = cy_sinhf(x);
+      b = sinhf(vx);
+    }
+    if (as_uint(a) != as_uint(b) && !(a != a && b != b)) {
+      if (!bad && first) {
+        *first = (uint32_t)u;
+      }
+      bad++;
+    }
+  }
+  return bad;
+}

@@ -64,6 +64,9 @@ CASES = {
     # curves in a BVH with unaligned nodes (bvh_nodes.h:79-153)
     "hair_ribbon": lambda: scenes.hair_ball(48, 48, 8, shape="ribbon"),
     "hair_thick": lambda: scenes.hair_ball(48, 48, 8, shape="thick"),
+    "hair_principled": lambda: scenes.hair_ball(48, 48, 8, shape="ribbon", fur="principled"),
+    "hair_principled_thick": lambda: scenes.hair_ball(40, 40, 8, shape="thick", fur="principled"),
+    "hair_reflection_transmission": lambda: scenes.hair_ball(48, 48, 8, shape="thick", fur="hair_bsdf"),
     # the reference host's own Sobol directions (render/sobol.cpp, Joe-Kuo
     # new-joe-kuo-6.21201, uploaded by integrator.cpp:235-243) instead of this
     # repository's stand-in table: tests/golden/sobol_joe_kuo.npz
@@ -99,7 +102,7 @@ JOE_KUO_CASES = {"cornell_joe_kuo"}
 HOST_LOOP_CASES = {"cornell_adaptive"}
 # Scenes with curves: the device traverses the bound BVH2 (unaligned nodes,
 # curve leaves) at every requested width; the wide layout holds triangles only.
-CURVE_CASES = {"hair_ribbon", "hair_thick"}
+CURVE_CASES = {"hair_ribbon", "hair_thick", "hair_principled", "hair_principled_thick", "hair_reflection_transmission"}
 EMU_CASES = [n for n in CASES if n not in HOST_LOOP_CASES]
 
 # SHADER_EVAL_DISPLACE (tests/golden/displace.npz)

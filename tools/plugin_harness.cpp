@@ -63,6 +63,8 @@ struct SubDevice {
   std::vector<device_vector<uchar> *> arrays;
   device_vector<float> *buffer = nullptr;
   std::vector<int> tiles; /* indices of the tiles it acquired */
+  int held = 0;           /* acquired and not yet released */
+  int max_held = 0;
 };
 
 static int upload_scene(SubDevice &sd, const std::string &dir, int W, int H, int stride)
@@ -174,6 +176,7 @@ int main(int argc, char **argv)
         tile.buffer = sd.buffer->device_pointer;
         sd.tiles.push_back((int)next);
         next++;
+        sd.max_held = std::max(sd.max_held, ++sd.held);
         return true;
       }
     }
@@ -189,6 +192,7 @@ int main(int argc, char **argv)
     for (size_t d = 0; d < subs.size(); d++) {
       if (tile.buffer == subs[d].buffer->device_pointer) {
         t_last[d] = time_dt() - t_start;
+        subs[d].held--;
       }
     }
   };
@@ -234,7 +238,7 @@ int main(int argc, char **argv)
                sizeof(float) * t.w * stride);
       }
     }
-    printf("device %d tiles %zu last release %.3f s\n", d, sd.tiles.size(), t_last[d]);
+    printf("device %d tiles %zu max held %d last release %.3f s\n", d, sd.tiles.size(), sd.max_held, t_last[d]);
   }
   bool once = true;
   for (int c : done) {
