@@ -271,6 +271,9 @@ typedef struct CyAttrIn {
   cfloat3 P, N, Ng, I;
   float u, v;
   int object, prim, type, flag, shader;
+#if CY_CLOSURE_EXT
+  cfloat3 dPdu;
+#endif
 } CyAttrIn;
 
 /* primitive_surface_attribute_float / float2 / float3 (geom_primitive.h:57-241):
@@ -501,8 +504,8 @@ CY_FN void svm_node_object_info(const CyGlobals *kg, const CyAttrIn &in, CySvmSt
 }
 
 /* svm_geometry.h NODE_GEOM_T: primitive_tangent (geom_primitive.h:292-320),
- * the spherical tangent of the generated coordinates around Z; the surface
- * derivative fallback (sd->dPdu) and curves are not carried */
+ * the spherical tangent of the generated coordinates around Z, else (and on
+ * curves) the normalised surface derivative dPdu */
 CY_FN void svm_node_geometry_tangent(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, uint out_offset,
                                      uint *err)
 {
@@ -517,7 +520,11 @@ CY_FN void svm_node_geometry_tangent(const CyGlobals *kg, const CyAttrIn &in, Cy
     T = cross3(in.N, normalize3(cross3(data, in.N)));
   }
   else {
+#if CY_CLOSURE_EXT
+    T = normalize3(in.dPdu);
+#else
     cy_set_error(err, CY_ERR_SVM_NODE, 2000 + 2); /* tangent from surface derivatives (sd->dPdu) */
+#endif
   }
   svm_store3(stack, out_offset, T, err);
 }

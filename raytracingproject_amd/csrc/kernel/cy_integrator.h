@@ -992,6 +992,10 @@ CY_FN void shader_setup_from_background(const CyGlobals *kg, CySD *sd, cfloat3 D
   sd->object = OBJECT_NONE;
   sd->prim = PRIM_NONE;
   sd->type = 0; /* PRIMITIVE_NONE */
+#if CY_CLOSURE_EXT
+  sd->dPdu = mk3(0.0f, 0.0f, 0.0f);
+  sd->dPdv = mk3(0.0f, 0.0f, 0.0f);
+#endif
   sd->u = 0.0f;
   sd->v = 0.0f;
   sd->svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
@@ -1047,7 +1051,12 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
  * it raised the _tex shading kernels' scratch from 1.7 to 2.9 KB per lane and
  * their renders went wrong on the GPU (non-finite films) while the host
  * build stayed exact. */
-CY_FN cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I, int shader, int object,
+#ifdef CY_EMISSIVE_OOL /* diagnostic build (build.py --variant ... -DCY_EMISSIVE_OOL): the out-of-line form */
+CY_NOINLINE
+#else
+CY_FN
+#endif
+cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I, int shader, int object,
                                       int prim, int lamp, float u, float v, float t, CyShadeMem mem, CyPathState state,
                                       uint *err)
 {
@@ -1076,10 +1085,25 @@ CY_FN cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cflo
       esd.N = object_normal_transform(kg, esd.object, esd.N);
     }
   }
+#if CY_CLOSURE_EXT
+  esd.dPdu = mk3(0.0f, 0.0f, 0.0f);
+  esd.dPdv = mk3(0.0f, 0.0f, 0.0f);
+  if (esd.type & PRIMITIVE_TRIANGLE) {
+    triangle_dPdudv(kg, esd.prim, &esd.dPdu, &esd.dPdv);
+    if (!(esd.object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
+      esd.dPdu = transform_direction(object_tfm(kg, esd.object), esd.dPdu);
+      esd.dPdv = transform_direction(object_tfm(kg, esd.object), esd.dPdv);
+    }
+  }
+#endif
   if (esd.prim != PRIM_NONE && dot3(esd.Ng, esd.I) < 0.0f) {
     esd.flag |= SD_BACKFACING;
     esd.Ng = neg3(esd.Ng);
     esd.N = neg3(esd.N);
+#if CY_CLOSURE_EXT
+    esd.dPdu = neg3(esd.dPdu);
+    esd.dPdv = neg3(esd.dPdv);
+#endif
   }
   esd.closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
   esd.closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);

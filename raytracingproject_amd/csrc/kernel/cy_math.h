@@ -1293,6 +1293,14 @@ CY_FN float cy_sinhf(float x)
 {
   return sinhf(x);
 }
+CY_FN float cy_coshf(float x)
+{
+  return coshf(x);
+}
+CY_FN float cy_tanhf(float x)
+{
+  return tanhf(x);
+}
 #else
 CY_FN float cy_kernel_tanf(float x, float y, int iy)
 {
@@ -1522,6 +1530,69 @@ CY_FN float cy_sinhf(float x)
     return t * w;
   }
   return x * shuge;
+}
+
+/* e_coshf.c */
+CY_FN float cy_coshf(float x)
+{
+  const float one = 1.0f, half = 0.5f, huge = 1.0e30f;
+  const int ix = as_int(x) & 0x7fffffff;
+  if (ix < 0x41b00000) { /* |x| < 22 */
+    if (ix < 0x3eb17218) { /* |x| < 0.5 ln2 */
+      const float t = cy_expm1f(fabsf(x));
+      const float w = one + t;
+      if (ix < 0x24000000) {
+        return w;
+      }
+      return one + (t * t) / (w + w);
+    }
+    const float t = cy_expf(fabsf(x));
+    return half * t + half / t;
+  }
+  if (ix < 0x42b17180) {
+    return half * cy_expf(fabsf(x));
+  }
+  if (ix <= 0x42b2d4fc) {
+    const float w = cy_expf(half * fabsf(x));
+    const float t = half * w;
+    return t * w;
+  }
+  if (ix >= 0x7f800000) {
+    return x * x;
+  }
+  return huge * huge;
+}
+
+/* s_tanhf.c */
+CY_FN float cy_tanhf(float x)
+{
+  const float one = 1.0f, two = 2.0f, tiny = 1.0e-30f;
+  const int jx = as_int(x);
+  const int ix = jx & 0x7fffffff;
+  float t, z;
+  if (ix >= 0x7f800000) {
+    return (jx >= 0) ? one / x + one : one / x - one;
+  }
+  if (ix < 0x41b00000) { /* |x| < 22 */
+    if (ix == 0) {
+      return x;
+    }
+    if (ix < 0x24000000) {
+      return x * (one + x);
+    }
+    if (ix >= 0x3f800000) {
+      t = cy_expm1f(two * fabsf(x));
+      z = one - two / (t + two);
+    }
+    else {
+      t = cy_expm1f(-two * fabsf(x));
+      z = -t / (t + two);
+    }
+  }
+  else {
+    z = one - tiny;
+  }
+  return (jx >= 0) ? z : -z;
 }
 #endif
 

@@ -2508,6 +2508,9 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
           ain.type = sd->type;
           ain.flag = sd->flag;
           ain.shader = sd->shader;
+#if CY_CLOSURE_EXT
+          ain.dPdu = sd->dPdu;
+#endif
           svm_eval_attribute_node(kg->__objects, kg->__shaders, kg->__attributes_map, kg->__attributes_float,
                                   kg->__attributes_float2, kg->__attributes_float3, kg->__attributes_uchar4,
                                   kg->__tri_vindex, ain, stack, node, err);
@@ -2612,6 +2615,13 @@ CY_FN cfloat3 displace_evaluate(const CyGlobals *kg, int object, int prim, float
   if (!(object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
     sd.N = object_normal_transform(kg, object, sd.N);
   }
+#if CY_CLOSURE_EXT
+  triangle_dPdudv(kg, prim, &sd.dPdu, &sd.dPdv);
+  if (!(object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
+    sd.dPdu = transform_direction(object_tfm(kg, object), sd.dPdu);
+    sd.dPdv = transform_direction(object_tfm(kg, object), sd.dPdv);
+  }
+#endif
   /* backfacing test: dot(Ng, I) with I = 0 is never negative */
   sd.num_closure = 0;
   sd.num_closure_left = 0;

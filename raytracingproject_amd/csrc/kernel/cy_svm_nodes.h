@@ -231,7 +231,15 @@ CY_FN float svm_math(uint type, float a, float b, float c, uint *err)
       return smoothminf(a, b, c);
     case 39: /* SMOOTH_MAX */
       return -smoothminf(-a, -b, c);
-    default: /* TANGENT, SINH, COSH, TANH: libm functions not restated */
+    case 6: /* TANGENT */
+      return cy_tanf(a);
+    case 29: /* SINH */
+      return cy_sinhf(a);
+    case 30: /* COSH */
+      return cy_coshf(a);
+    case 31: /* TANH */
+      return cy_tanhf(a);
+    default:
       cy_set_error(err, CY_ERR_SVM_NODE, 10000 + type);
       return 0.0f;
   }
@@ -314,7 +322,10 @@ CY_FN void svm_vector_math(
     case 22: /* COSINE */
       *vector = mk3(cy_cosf(a.x), cy_cosf(a.y), cy_cosf(a.z));
       break;
-    default: /* TANGENT */
+    case 23: /* TANGENT */
+      *vector = mk3(cy_tanf(a.x), cy_tanf(a.y), cy_tanf(a.z));
+      break;
+    default:
       cy_set_error(err, CY_ERR_SVM_NODE, 11000 + type);
       *vector = mk3(0.0f, 0.0f, 0.0f);
       *value = 0.0f;

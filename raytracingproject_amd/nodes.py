@@ -88,8 +88,9 @@ MATH_OPS = ["add", "subtract", "multiply", "divide", "sine", "cosine", "tangent"
             "modulo", "absolute", "arctan2", "floor", "ceil", "fraction", "sqrt", "inv_sqrt", "sign",
             "exponent", "radians", "degrees", "sinh", "cosh", "tanh", "trunc", "snap", "wrap", "compare",
             "multiply_add", "pingpong", "smooth_min", "smooth_max"]
-# restated in the HIP kernel bit-exactly; the rest (libm tan/sinh/cosh/tanh) are rejected
-MATH_OPS_SUPPORTED = [op for op in MATH_OPS if op not in ("tangent", "sinh", "cosh", "tanh")]
+# the shading_math golden grid: every op but the libm tan / sinh / cosh / tanh,
+# which the shading_math_libm case covers (all restated bit-exactly)
+MATH_OPS_GRID = [op for op in MATH_OPS if op not in ("tangent", "sinh", "cosh", "tanh")]
 VECTOR_MATH_OPS = ["add", "subtract", "multiply", "divide", "cross_product", "project", "reflect",
                    "dot_product", "distance", "length", "scale", "normalize", "snap", "floor", "ceil",
                    "modulo", "fraction", "absolute", "minimum", "maximum", "wrap", "sine", "cosine",

@@ -951,12 +951,29 @@ def shading_math(width=64, height=64, samples=8) -> sc.Scene:
     from . import nodes as nd
 
     colors = []
-    for op in nd.MATH_OPS_SUPPORTED:
+    for op in nd.MATH_OPS_GRID:
         a, b = _uv_inputs(-2.5, 2.5, -1.5, 2.5)
         r = nd.math(op, a, b, 0.3, clamp=True)
         colors.append(nd.combine_xyz(r, nd.math("multiply", a, 0.2, clamp=True),
                                      nd.math("multiply", b, 0.2, clamp=True)))
     return _grid_scene(colors, width, height, samples, "shading_math", glossy_every=5)
+
+
+def shading_math_libm(width=32, height=32, samples=8) -> sc.Scene:
+    """The Math operations backed by libm functions the kernel restates from
+    glibc (tan, sinh, cosh, tanh; cy_math.h) and Vector Math tangent, over
+    arguments that cross the reduction and branch boundaries."""
+    from . import nodes as nd
+
+    colors = []
+    for op in ("tangent", "sinh", "cosh", "tanh"):
+        a, b = _uv_inputs(-4.0, 4.0, -1.5, 2.5)
+        r = nd.math(op, a, b, 0.3)
+        colors.append(nd.combine_xyz(nd.math("multiply", r, 0.1), nd.math("multiply", a, 0.2, clamp=True),
+                                     nd.math("multiply", b, 0.2, clamp=True)))
+    a, b = _uv_inputs(-6.0, 6.0, -1.5, 1.5)
+    colors.append(nd.vector_math("tangent", nd.combine_xyz(a, b, 1.2))["Vector"])
+    return _grid_scene(colors, width, height, samples, "shading_math_libm")
 
 
 def shading_vector(width=64, height=64, samples=8) -> sc.Scene:

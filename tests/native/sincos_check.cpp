@@ -86,7 +86,8 @@ extern "C" long lgammaf_sweep(uint32_t lo, uint32_t hi, uint32_t step, uint32_t 
 }
 
 /* cy_tanf / cy_expm1f / cy_sinhf (glibc restatements) against libm over [lo, hi]
- * bit patterns: which = 0 tanf, 1 expm1f, 2 sinhf; returns the mismatches. */
+ * bit patterns: which = 0 tanf, 1 expm1f, 2 sinhf, 3 coshf, 4 tanhf; returns the
+ * mismatches. */
 extern "C" long libm_sweep(int which, uint32_t lo, uint32_t hi, uint32_t step, uint32_t *first)
 {
   long bad = 0;
@@ -102,9 +103,17 @@ extern "C" long libm_sweep(int which, uint32_t lo, uint32_t hi, uint32_t step, u
       a = cy_expm1f(x);
       b = expm1f(vx);
     }
-    else {
+    else if (which == 2) {
       a = cy_sinhf(x);
       b = sinhf(vx);
+    }
+    else if (which == 3) {
+      a = cy_coshf(x);
+      b = coshf(vx);
+    }
+    else {
+      a = cy_tanhf(x);
+      b = tanhf(vx);
     }
     if (as_uint(a) != as_uint(b) && !(a != a && b != b)) {
       if (!bad && first) {

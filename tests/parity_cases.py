@@ -31,6 +31,7 @@ CASES = {
     # direction-dependent world shader (geometry, light path, ramp, gradient)
     **{f"shading_{k}": (lambda k=k: getattr(scenes, f"shading_{k}")(48, 48, 8))
        for k in ("math", "vector", "color", "coords", "noise", "voronoi", "attributes", "normals", "converters")},
+    "shading_math_libm": lambda: scenes.shading_math_libm(32, 32, 8),
     # world importance sampling: background light + background MIS
     # (kernel_light_background.h), alone and sharing the distribution with a lamp
     "world_mis": lambda: scenes.world_lit(48, 48, 8, map_resolution=128),

@@ -119,10 +119,10 @@ def test_lgammaf_bit_exact_vs_libm():
     assert lib.lgammaf_sweep(lo, hi, 1, None) == 0
 
 
-def test_tanf_expm1f_sinhf_bit_exact_vs_libm():
-    """cy_tanf / cy_expm1f / cy_sinhf restate glibc 2.35 (fdlibm k_tanf.c with
-    glibc's double-precision rem_pio2f, s_expm1f.c, e_sinhf.c) for the hair
-    closures.  Every float of both signs agreed during development (0 of
+def test_tanf_expm1f_sinhf_coshf_tanhf_bit_exact_vs_libm():
+    """cy_tanf / cy_expm1f / cy_sinhf / cy_coshf / cy_tanhf restate glibc 2.35
+    (fdlibm k_tanf.c with glibc's double-precision rem_pio2f, s_expm1f.c,
+    e_sinhf.c, e_coshf.c, s_tanhf.c) for the hair closures and the Math node.  Every float of both signs agreed during development (0 of
     4.3e9 differ for each); here every 997th float of the whole range and
     every 13th of [-4, 4] (tanf) / [-12, 12] (expm1f, sinhf), both of which
     walk every exponent and branch."""
@@ -131,7 +131,7 @@ def test_tanf_expm1f_sinhf_bit_exact_vs_libm():
     lib = nb.sincos()
     lib.libm_sweep.restype = ctypes.c_long
     lib.libm_sweep.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
-    for which, dense in ((0, 4.0), (1, 12.0), (2, 12.0)):
+    for which, dense in ((0, 4.0), (1, 12.0), (2, 12.0), (3, 12.0), (4, 12.0)):
         top = int(np.float32(dense).view(np.uint32))
         assert lib.libm_sweep(which, 0, 0x7F800000, 997, None) == 0, which
         assert lib.libm_sweep(which, 0x80000000, 0xFF800000, 997, None) == 0, which
