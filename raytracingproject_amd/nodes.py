@@ -60,6 +60,12 @@ NODE_COMBINE_HSV = 77
 NODE_MAP_RANGE = 83
 NODE_CLAMP = 84
 NODE_ATTR, NODE_VERTEX_COLOR = 16, 17
+# bump evaluation (svm_types.h): the *_BUMP_DX / _DY forms of the geometry,
+# attribute, vertex colour and texture coordinate nodes, and NODE_SET_BUMP
+NODE_GEOMETRY_BUMP_DX, NODE_GEOMETRY_BUMP_DY = 18, 19
+NODE_SET_BUMP, NODE_ATTR_BUMP_DX, NODE_ATTR_BUMP_DY = 26, 27, 28
+NODE_VERTEX_COLOR_BUMP_DX, NODE_VERTEX_COLOR_BUMP_DY = 29, 30
+NODE_TEX_COORD_BUMP_DX, NODE_TEX_COORD_BUMP_DY = 31, 32
 NODE_OBJECT_INFO, NODE_TANGENT, NODE_NORMAL_MAP = 48, 70, 71
 NODE_FRESNEL, NODE_LAYER_WEIGHT = 38, 39
 NODE_CAMERA, NODE_NORMAL, NODE_RGB_CURVES, NODE_VECTOR_CURVES = 54, 65, 68, 69
@@ -519,6 +525,37 @@ DISPLACEMENT_SPACES = {"object": 1, "world": 2}  # NodeNormalMapSpace (svm_types
 NODE_DISPLACEMENT, NODE_VECTOR_DISPLACEMENT = 21, 22
 
 
+def _bump_copy(s: Socket, mode: str, memo: dict) -> Socket:
+    """A copy of the node graph feeding `s` with every node marked for the
+    bump offset `mode` ("dx" / "dy"): ShaderGraph::refine_bump_nodes
+    (graph.cpp:1003-1054) copies the Height input's dependencies twice and
+    sets node->bump to SHADER_BUMP_DX / DY."""
+    n = s.node
+    if id(n) not in memo:
+        inputs = {k: (_bump_copy(v, mode, memo) if is_linked(v) else v) for k, v in n.inputs.items()}
+        memo[id(n)] = Node(n.kind, inputs, {**n.params, "bump": mode})
+    return Socket(memo[id(n)], s.name)
+
+
+def bump(height=1.0, strength=1.0, distance=0.1, invert=False, normal=None, object_space=False) -> Socket:
+    """Bump node (nodes.cpp BumpNode, svm_displace.h svm_node_set_bump): the
+    height at the shading point and, through copies of its node graph that
+    sample one ray differential away (geometry, texture coordinate, attribute
+    and vertex colour nodes in their *_BUMP_DX / _DY forms), at the
+    neighbouring points; the perturbed normal (needs the device's ray
+    differentials).  An unlinked height leaves the three samples at 0."""
+    inputs = {"Strength": strength, "Distance": distance}
+    if normal is not None:
+        inputs["Normal"] = normal
+    if is_linked(height):
+        inputs["SampleCenter"] = height
+        inputs["SampleX"] = _bump_copy(height, "dx", {})
+        inputs["SampleY"] = _bump_copy(height, "dy", {})
+    else:
+        inputs.update({"SampleCenter": 0.0, "SampleX": 0.0, "SampleY": 0.0})
+    return Node("bump", inputs, {"invert": bool(invert), "object_space": bool(object_space)})["Normal"]
+
+
 def displacement(height, midlevel=0.5, scale=1.0, normal=None, space: str = "object") -> Socket:
     """Displacement node (nodes.cpp:6905-6952): (height - midlevel) * scale along
     the normal (sd->N when unlinked), in object or world space."""
@@ -601,6 +638,8 @@ def _outputs(node: Node) -> dict:
         return {"Color": "color", "Alpha": "float"}
     if k in ("displacement", "vector_displacement"):
         return {"Displacement": "vector"}
+    if k == "bump":
+        return {"Normal": "vector"}
     raise ValueError(f"unknown node kind {k!r}")
 
 
@@ -650,6 +689,8 @@ _INPUT_TYPES = {
     "vector_transform": {"Vector": "vector"},
     "layer_weight": {"Blend": "float", "Normal": "vector"},
     "vector_displacement": {"Vector": "color", "Midlevel": "float", "Scale": "float"},
+    "bump": {"SampleCenter": "float", "SampleX": "float", "SampleY": "float", "Normal": "vector",
+             "Strength": "float", "Distance": "float"},
 }
 
 
@@ -821,36 +862,45 @@ class NodeCompiler:
         self.emit((NODE_VALUE_V, off, 0, 0))
         self.emit((NODE_VALUE_V, *(f32bits(x) for x in n.params["value"])))
 
+    @staticmethod
+    def _bump_kind(n, center, dx, dy):
+        """The node type of `n`'s bump copy (ShaderNode::bump, nodes.cpp)."""
+        return {"dx": dx, "dy": dy}.get(n.params.get("bump"), center)
+
     def _n_tex_coord(self, n):  # nodes.cpp:3840-3923 TextureCoordinateNode::compile
         used = lambda name: (id(n), name) in self.used  # noqa: E731
+        texco = self._bump_kind(n, NODE_TEX_COORD, NODE_TEX_COORD_BUMP_DX, NODE_TEX_COORD_BUMP_DY)
+        attr = self._bump_kind(n, NODE_ATTR, NODE_ATTR_BUMP_DX, NODE_ATTR_BUMP_DY)
+        geom = self._bump_kind(n, NODE_GEOMETRY, NODE_GEOMETRY_BUMP_DX, NODE_GEOMETRY_BUMP_DY)
         if used("Generated"):
             if self.background:
-                self.emit((NODE_GEOMETRY, GEOMETRY_OUTPUTS["Position"], self.out(n, "Generated"), 0))
+                self.emit((geom, GEOMETRY_OUTPUTS["Position"], self.out(n, "Generated"), 0))
             elif self.volume:
                 raise ValueError("tex_coord Generated in a volume shader (NODE_TEXCO_VOLUME_GENERATED needs the "
                                  "generated-transform attribute) is not supported")
             else:
-                self.emit((NODE_ATTR, self.attribute(ATTR_STD_GENERATED), self.out(n, "Generated"), NODE_ATTR_FLOAT3))
+                self.emit((attr, self.attribute(ATTR_STD_GENERATED), self.out(n, "Generated"), NODE_ATTR_FLOAT3))
         if used("Normal"):
-            self.emit((NODE_TEX_COORD, TEXCO_OUTPUTS["Normal"], self.out(n, "Normal"), 0))
+            self.emit((texco, TEXCO_OUTPUTS["Normal"], self.out(n, "Normal"), 0))
         if used("UV"):
-            self.emit((NODE_ATTR, self.attribute(ATTR_STD_UV), self.out(n, "UV"), NODE_ATTR_FLOAT3))
+            self.emit((attr, self.attribute(ATTR_STD_UV), self.out(n, "UV"), NODE_ATTR_FLOAT3))
         for name in ("Object", "Camera", "Window"):
             if used(name):
-                self.emit((NODE_TEX_COORD, TEXCO_OUTPUTS[name], self.out(n, name), 0))
+                self.emit((texco, TEXCO_OUTPUTS[name], self.out(n, name), 0))
         if used("Reflection"):
             if self.background:
-                self.emit((NODE_GEOMETRY, GEOMETRY_OUTPUTS["Incoming"], self.out(n, "Reflection"), 0))
+                self.emit((geom, GEOMETRY_OUTPUTS["Incoming"], self.out(n, "Reflection"), 0))
             else:
-                self.emit((NODE_TEX_COORD, TEXCO_OUTPUTS["Reflection"], self.out(n, "Reflection"), 0))
+                self.emit((texco, TEXCO_OUTPUTS["Reflection"], self.out(n, "Reflection"), 0))
 
     def _n_attribute(self, n):  # nodes.cpp:5411-5436 AttributeNode::compile
         attr = self.attribute(ATTR_STD_NAMES.get(n.params["name"], n.params["name"]))
+        node = self._bump_kind(n, NODE_ATTR, NODE_ATTR_BUMP_DX, NODE_ATTR_BUMP_DY)
         for name in ("Color", "Vector"):
             if (id(n), name) in self.used:
-                self.emit((NODE_ATTR, attr, self.out(n, name), NODE_ATTR_FLOAT3))
+                self.emit((node, attr, self.out(n, name), NODE_ATTR_FLOAT3))
         if (id(n), "Fac") in self.used:
-            self.emit((NODE_ATTR, attr, self.out(n, "Fac"), NODE_ATTR_FLOAT))
+            self.emit((node, attr, self.out(n, "Fac"), NODE_ATTR_FLOAT))
 
     def _n_normal_map(self, n):  # nodes.cpp:6717-6761 NormalMapNode::attributes / compile
         space = NORMAL_MAP_SPACES[n.params["space"]]
@@ -940,14 +990,24 @@ class NodeCompiler:
                 off = self.alloc(w)
                 self.temps.append((off, w))
             offs.append(off)
-        self.emit((NODE_VERTEX_COLOR, attr, offs[0], offs[1]))
+        self.emit((self._bump_kind(n, NODE_VERTEX_COLOR, NODE_VERTEX_COLOR_BUMP_DX, NODE_VERTEX_COLOR_BUMP_DY), attr,
+                   offs[0], offs[1]))
 
     def _n_geometry(self, n):  # nodes.cpp GeometryNode::attributes / compile
         if (id(n), "Tangent") in self.used and not self.background:
             self.attribute(ATTR_STD_GENERATED)  # primitive_tangent reads the generated coordinates
+        geom = self._bump_kind(n, NODE_GEOMETRY, NODE_GEOMETRY_BUMP_DX, NODE_GEOMETRY_BUMP_DY)
         for name, t in GEOMETRY_OUTPUTS.items():
             if (id(n), name) in self.used:
-                self.emit((NODE_GEOMETRY, t, self.out(n, name), 0))
+                self.emit((geom, t, self.out(n, name), 0))
+
+    def _n_bump(self, n):  # nodes.cpp BumpNode::compile
+        nrm = self.assign_if_linked(n.inputs.get("Normal"), "vector")
+        dist = self.inp(n, "Distance")
+        c, x, y = self.inp(n, "SampleCenter"), self.inp(n, "SampleX"), self.inp(n, "SampleY")
+        strength = self.inp(n, "Strength")
+        self.emit((NODE_SET_BUMP, uchar4(nrm, dist, int(n.params["invert"]), int(n.params["object_space"])),
+                   uchar4(c, x, y, strength), self.out(n, "Normal")))
 
     def _n_light_path(self, n):  # nodes.cpp LightPathNode::compile
         for t, name in enumerate(LIGHT_PATH_OUTPUTS):

@@ -698,6 +698,51 @@ def sss_cornell(width=48, height=48, samples=8, instanced=False, blur=False) -> 
     return s
 
 
+def bump_cornell(width=48, height=48, samples=8, camera="perspective") -> sc.Scene:
+    """Cornell box with Bump nodes (golden parity case for ray differentials):
+    a diffuse sphere bumped by a noise texture over generated coordinates, a
+    glossy sphere bumped by a checker, an object-space bump from a position
+    ramp on the back wall, a Principled sphere with a bumped normal, a mirror
+    and a glass sphere (bounces whose reflected / refracted differentials
+    reach the bumped surfaces).  camera: "perspective", "ortho" (dP
+    differentials) or "equirect" (panorama differentials from inside)."""
+    from . import nodes
+
+    s = cornell_box(width, height, samples)
+    if camera == "ortho":
+        s.camera.type = "orthographic"
+        s.camera.ortho_scale = 560.0
+    elif camera == "equirect":
+        s.camera = sc.Camera(eye=(278.0, 273.0, 200.0), target=(278.0, 273.0, 555.0), up=(0.0, 1.0, 0.0),
+                             nearclip=0.1, farclip=1e5)
+        s.camera.type = "panorama"
+        s.camera.panorama_type = "equirectangular"
+        s.camera.latitude_min, s.camera.latitude_max = -1.2, 1.3
+        s.camera.longitude_min, s.camera.longitude_max = -2.5, 2.8
+    base = len(s.materials)
+    noise = nodes.noise_texture(None, scale=0.05, detail=2.0)["Fac"]
+    checker = nodes.checker(None, (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), scale=4.0)["Fac"]
+    ramp = nodes.math("sine", nodes.math("multiply", nodes.separate_xyz(nodes.geometry()["Position"])["X"], 0.05))
+    bumpy = sc.diffuse((0.8, 0.6, 0.4), normal=nodes.bump(noise, strength=1.0, distance=2.0))
+    tiles = sc.glossy((0.8, 0.8, 0.9), 0.3, normal=nodes.bump(checker, strength=0.6, distance=0.5, invert=True))
+    wall = sc.diffuse((0.7, 0.7, 0.7), normal=nodes.bump(ramp, strength=0.8, distance=1.0, object_space=True))
+    plastic = sc.principled(base_color=(0.2, 0.4, 0.8), roughness=0.3, specular=0.5,
+                            normal=nodes.bump(noise, strength=0.5, distance=3.0))
+    mirror = sc.glossy((0.9, 0.9, 0.9), 0.0)
+    glass = sc.glass((0.95, 0.97, 1.0), 0.0, ior=1.45)
+    s.materials.extend([bumpy, tiles, wall, plastic, mirror, glass])
+    centers = [(140.0, 110.0, 220.0), (300.0, 110.0, 260.0), None, (430.0, 300.0, 300.0), (200.0, 380.0, 380.0),
+               (420.0, 100.0, 120.0)]
+    for i, c in enumerate(centers):
+        if c is None:
+            s.meshes.append(sc.Mesh(*_quad((40.0, 20.0, 540.0), (520.0, 20.0, 540.0), (520.0, 520.0, 540.0),
+                                           (40.0, 520.0, 540.0)), shader=base + i))
+        else:
+            s.meshes.append(sc.Mesh(*_ellipsoid(c, (70.0, 65.0, 70.0), 20, 12), shader=base + i, smooth=True))
+    s.name = "bump_cornell_" + camera
+    return s
+
+
 def sss_disk_cornell(width=48, height=48, samples=8, instanced=False, transparent=False) -> sc.Scene:
     """Cornell box with disk BSSRDFs (golden parity case): Subsurface
     Scattering nodes with the cubic (sharpness 0.5, blurred checker colour),

@@ -77,6 +77,10 @@ CASES = {
     "sss_cornell": lambda: scenes.sss_cornell(48, 48, 8),
     "sss_instanced": lambda: scenes.sss_cornell(48, 48, 8, instanced=True),
     "sss_blur": lambda: scenes.sss_cornell(40, 40, 8, blur=True),
+    # Bump nodes through ray differentials (kernel_differential.h, svm_displace.h)
+    "shading_bump": lambda: scenes.bump_cornell(48, 48, 8),
+    "shading_bump_ortho": lambda: scenes.bump_cornell(40, 40, 8, camera="ortho"),
+    "shading_bump_equirect": lambda: scenes.bump_cornell(40, 40, 8, camera="equirect"),
     "sss_disk": lambda: scenes.sss_disk_cornell(48, 48, 8),
     "sss_disk_instanced": lambda: scenes.sss_disk_cornell(48, 48, 8, instanced=True),
     "sss_disk_transparent": lambda: scenes.sss_disk_cornell(40, 40, 8, transparent=True),
