@@ -52,6 +52,8 @@ def parse(argv=None):
                    help="4 (default) / 8: device-widened wide BVH; 2: the bound BVH2 as is")
     p.add_argument("--ray-sort", type=int, default=0, choices=(0, 3, 5),
                    help="bin the closest queue by ray direction per bounce: 0 off, 3 octant, 5 octant x axis")
+    p.add_argument("--refill", type=int, nargs=2, default=(0, 16), metavar=("ROUNDS", "MIN_IDLE"),
+                   help="lane refill of the closest-hit traversal (0 = off)")
     p.add_argument("--trav-budget", type=int, nargs=2, default=(0, 0), metavar=("FIRST", "SECOND"),
                    help="iteration budget of the wide traversal kernels (continuation launches); 0 0 disables")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
@@ -138,6 +140,7 @@ def main():
     dev.set_bvh_leaf_merge(args.leaf_merge)
     dev.set_ray_sort(args.ray_sort)
     dev.set_traversal_budget(*args.trav_budget)
+    dev.set_traversal_refill(*args.refill)
     dev.set_slots(args.slots)
     t0 = time.time()
     dev.upload_scene(ds)
@@ -320,6 +323,7 @@ def main():
                 "wavefront_iterations_per_frame": int(timing["iterations"]),
                 "ray_sort": args.ray_sort,
                 "traversal_budget": list(args.trav_budget),
+                "traversal_refill": list(args.refill),
                 "scene_compile_s": round(t_compile, 2),
                 "scene_upload_s": round(t_upload, 3),
             },

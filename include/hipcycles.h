@@ -165,6 +165,11 @@ int hipcy_set_ray_sort(hipcy_device *dev, int mode);
  * without a budget.  Results are bit-identical; 0, 0 disables (scenes with
  * instances always run without a budget). */
 int hipcy_set_traversal_budget(hipcy_device *dev, int first, int second);
+/* Lane refill of the closest-hit traversal (non-instanced wide BVH without
+ * curves): persistent waves whose lanes traverse `rounds` iterations at a time
+ * and, once `min_idle` lanes of a wave have finished their rays, take the next
+ * rays of the queue.  Results are bit-identical; rounds 0 disables. */
+int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

@@ -344,13 +344,6 @@ __device__ __forceinline__ void cont_suspend(const CyGlobals *kg, const CyCont &
  * (ray replacement) was measured 2x slower on the BMW stand-in (the refill path
  * with camera-ray generation inside the traversal loop spills at the 80-VGPR
  * budget, and replacement rays break the camera rays' fetch coherence). */
-/* Stage 1: closest hit for every queued path, or (cam_n > 0) for the camera
- * rays of the work items item_base .. item_base + cam_n - 1 held by slots
- * slot_base .. slot_base + cam_n - 1.  One ray per thread: a persistent variant
- * whose lanes take the next ray of a per-workgroup pool when theirs finishes
- * (ray replacement) was measured 2x slower on the BMW stand-in (the refill path
- * with camera-ray generation inside the traversal loop spills at the 80-VGPR
- * budget, and replacement rays break the camera rays' fetch coherence). */
 template<bool STATS, int W, bool INST, int HAIR = 0>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
@@ -527,6 +520,162 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_closest_continu
         }
       }
       closest_store<false>(&b, slot, true, isect.prim != PRIM_NONE, &isect);
+    }
+  }
+  if (STATS) {
+    stats_block_add(stats, n_nodes, n_leaves, n_tris, n_ties);
+  }
+}
+
+/* Lane refill (hipcy_set_traversal_refill; non-instanced wide BVH without
+ * curves).  A wave's rays end after very different numbers of iterations (18
+ * loop iterations per wave against 7.3 nodes per ray on the BMW stand-in: lane
+ * utilisation 0.45), and a one-ray-per-thread kernel keeps a lane idle from
+ * its ray's end to the wave's.  Here waves are persistent: every lane traverses
+ * for at most `rounds` iterations (the resumable cursor of the continuation
+ * kernels, its LDS ring column kept in place), then lanes whose ray ended store
+ * it and -- once at least `min_idle` lanes of the wave are idle -- take the next
+ * rays of the queue.  The queue is split into 8 contiguous parts, one per XCD
+ * (blockIdx & 7, the dispatch's round-robin; each XCD's L2 then sees one image
+ * region, as with cy_xcd_block), handed out in chunks of CY_REFILL_CHUNK by one
+ * atomic per wave; a wave whose part is drained moves on to the next part.
+ * Each ray's traversal is the same computation split into rounds, so results
+ * are bit-identical.  Camera launches first write their rays into the slots
+ * (k_camera_rays): generating them inside the loop costs the loop registers. */
+#ifndef CY_REFILL_CHUNK
+#  define CY_REFILL_CHUNK 256u
+#endif
+#define CY_REFILL_BLOCKS 1280 /* 256 CUs x 5 waves/SIMD x 4 SIMDs / 4 waves per block */
+
+__global__ void __launch_bounds__(CY_BLOCK) k_camera_rays(CyGlobals kg, CyPathBuffers b, CyTile tile, int cam_n,
+                                                          int slot_base)
+{
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= cam_n) {
+    return;
+  }
+  CyRay ray;
+  uint visibility;
+  closest_load(&kg, &b, &tile, slot_base + i, tile.item_base + (uint)i, &ray, &visibility);
+  cy_st(&b.ray_P[slot_base + i], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
+  cy_st(&b.ray_D[slot_base + i], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(visibility)));
+}
+
+/* The [lo, hi) range of part p of n queue entries. */
+__device__ __forceinline__ void refill_part(uint n, uint p, uint *lo, uint *hi)
+{
+  *lo = (uint)(((unsigned long long)n * p) >> 3);
+  *hi = (uint)(((unsigned long long)n * (p + 1)) >> 3);
+}
+
+/* Hand out the next queue indices of the wave to its idle lanes (wave-uniform
+ * control flow); returns this lane's index or 0xFFFFFFFF. */
+__device__ __forceinline__ uint refill_take(uint n, uint *claim, bool idle, uint *part, uint *parts_left,
+                                            uint *next, uint *end)
+{
+  const int lane = threadIdx.x & 63;
+  const unsigned long long mask = __ballot(idle);
+  const uint rank = (uint)__popcll(mask & ((1ull << lane) - 1ull));
+  uint want = (uint)__popcll(mask);
+  uint given = 0;
+  uint mine = 0xFFFFFFFFu;
+  while (want > 0 && *parts_left > 0) {
+    if (*next == *end) {
+      uint base = 0;
+      if (lane == 0) {
+        base = atomicAdd(&claim[*part], CY_REFILL_CHUNK);
+      }
+      base = __shfl(base, 0);
+      uint lo, hi;
+      refill_part(n, *part, &lo, &hi);
+      if (base >= hi - lo) {
+        *part = (*part + 1) & 7u;
+        (*parts_left)--;
+        continue;
+      }
+      *next = lo + base;
+      *end = min(*next + CY_REFILL_CHUNK, hi);
+    }
+    const uint take = min(*end - *next, want);
+    if (idle && rank >= given && rank < given + take) {
+      mine = *next + (rank - given);
+    }
+    given += take;
+    want -= take;
+    *next += take;
+  }
+  return mine;
+}
+
+template<bool STATS, int W>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_closest_refill(CyGlobals kg,
+                                                                 CyPathBuffers b,
+                                                                 int cam_n,
+                                                                 int slot_base,
+                                                                 const int *queue,
+                                                                 const uint *counter,
+                                                                 uint *claim,
+                                                                 uint *err,
+                                                                 CyStats *stats,
+                                                                 int rounds,
+                                                                 int min_idle)
+{
+  const uint n = cam_n > 0 ? (uint)cam_n : *counter;
+  __shared__ LdsStack<W, false> lds_stack;
+  CY_LDS CyStackEntry *ring = lds_ring_of(&lds_stack);
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
+  uint part = blockIdx.x & 7u, parts_left = 8, next = 0, end = 0;
+  bool busy = false, tie = false, has_ray = false;
+  int slot = 0;
+  CyRay ray;
+  uint visibility = 0;
+  CyIsect isect;
+  CyTravCursor cur;
+  while (true) {
+    const int n_idle = (int)__popcll(__ballot(!busy));
+    if (n_idle >= min_idle || n_idle == 64) {
+      const uint idx = refill_take(n, claim, !busy, &part, &parts_left, &next, &end);
+      if (idx != 0xFFFFFFFFu) {
+        slot = cam_n > 0 ? slot_base + (int)idx : queue[idx];
+        closest_load(&kg, &b, nullptr, slot, CY_NO_ITEM, &ray, &visibility);
+        has_ray = cam_n > 0 ? ray.t != 0.0f : true;
+        isect.t = ray.t;
+        isect.u = 0.0f;
+        isect.v = 0.0f;
+        isect.prim = PRIM_NONE;
+        isect.object = OBJECT_NONE;
+        isect.type = 0;
+        cur.code = 0;
+        cur.code_t = 0.0f;
+        cur.top = 0;
+        cur.n_ring = 0;
+        cur.tie = false;
+        cur.suspended = false;
+        tie = false;
+        busy = true;
+        if (!(has_ray && scene_intersect_valid(&ray))) {
+          closest_store<false>(&b, slot, has_ray, false, &isect);
+          busy = false;
+        }
+      }
+    }
+    if (!__any(busy)) {
+      break;
+    }
+    if (busy) {
+      bvhw_run<W, false>(&kg, &ray, visibility, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, ring,
+                         &tie, rounds, &cur);
+      if (!cur.suspended) {
+        const bool hit = isect.prim != PRIM_NONE;
+        if (tie) {
+          isect.prim |= CY_PRIM_TIE;
+          if (STATS) {
+            n_ties++;
+          }
+        }
+        closest_store<false>(&b, slot, true, hit, &isect);
+        busy = false;
+      }
     }
   }
   if (STATS) {
@@ -1228,6 +1377,8 @@ struct hipcy_device {
    * first launch, first continuation; 0 disables.  Per lane two continuation
    * record buffers of cont_capacity entries. */
   int trav_budget[2] = {0, 0};
+  int trav_refill[2] = {0, 0};     /* lane refill: iterations per round, idle lanes that trigger a refill */
+  uint *refill_claim = nullptr;    /* CY_LANES x 8 per-part chunk counters */
   hc_float4 *cont_rec = nullptr;
   size_t cont_capacity = 0; /* records per buffer */
   size_t cont_lanes = 0;
@@ -1266,6 +1417,8 @@ struct hipcy_device {
   bool use_volumes = false;           /* KernelIntegrator.use_volumes: the volume shading / shadow kernels */
   bool use_disk_bssrdf = false;       /* disk BSSRDFs: the slots' subsurface indirect-ray records */
   char *sss_pool = nullptr;           /* those records and their depths */
+  bool use_ray_diff = false;          /* a shader reads ray differentials (Bump / *_BUMP_DX / _DY nodes) */
+  char *diff_pool = nullptr;          /* the slots' ray and shadow-ray differentials */
   int shade_closures = 1;             /* closure array of the shading kernel (variant by size) */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int curve_shapes = 0;               /* curve primitive shapes in __prim_type: 1 ribbon, 2 thick, 3 both */
@@ -1326,6 +1479,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   kg->tri_index_identity = wide ? dev->tri_index_identity : 0;
   kg->have_instancing = dev->have_instancing;
   kg->have_curves = dev->data_host.bvh.have_curves ? 1 : 0;
+  kg->use_ray_diff = dev->use_ray_diff ? 1 : 0;
   return true;
 }
 
@@ -1462,6 +1616,12 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   }
   dev->bufs.sss_rec = nullptr;
   dev->bufs.sss_count = nullptr;
+  if (dev->diff_pool) {
+    hipFree(dev->diff_pool);
+    dev->diff_pool = nullptr;
+  }
+  dev->bufs.ray_diff = nullptr;
+  dev->bufs.shadow_dP = nullptr;
   /* queues live in their own allocation (3 x slots ints) */
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) {
@@ -1502,6 +1662,20 @@ static int ensure_sss_capacity(hipcy_device *dev)
   /* other scenes' shading never looks at the records */
   dev->bufs.sss_rec = dev->use_disk_bssrdf ? (hc_float4 *)dev->sss_pool : nullptr;
   dev->bufs.sss_count = dev->use_disk_bssrdf ? (uint *)(dev->sss_pool + recs) : nullptr;
+  return 0;
+}
+
+/* The slots' ray differentials (CY_RAY_DIFF_F4 float4) and the pending
+ * shadow ray's dP (2 float4), 80 B per slot, for scenes whose shaders read
+ * differentials only. */
+static int ensure_diff_capacity(hipcy_device *dev)
+{
+  const size_t rays = (size_t)16 * CY_RAY_DIFF_F4 * dev->capacity;
+  if (dev->use_ray_diff && !dev->diff_pool) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->diff_pool, rays + (size_t)32 * dev->capacity));
+  }
+  dev->bufs.ray_diff = dev->use_ray_diff ? (hc_float4 *)dev->diff_pool : nullptr;
+  dev->bufs.shadow_dP = dev->use_ray_diff ? (hc_float4 *)(dev->diff_pool + rays) : nullptr;
   return 0;
 }
 
@@ -1600,6 +1774,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->pool) hipFree(dev->pool);
   if (dev->vol_pool) hipFree(dev->vol_pool);
   if (dev->sss_pool) hipFree(dev->sss_pool);
+  if (dev->diff_pool) hipFree(dev->diff_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
   if (dev->records) hipFree(dev->records);
   if (dev->tile_descs) hipFree(dev->tile_descs);
@@ -1611,6 +1786,7 @@ void hipcy_destroy(hipcy_device *dev)
     if (dev->queue[q]) hipFree(dev->queue[q]);
   }
   if (dev->cont_rec) hipFree(dev->cont_rec);
+  if (dev->refill_claim) hipFree(dev->refill_claim);
   if (dev->sort_queue) hipFree(dev->sort_queue);
   if (dev->sort_key) hipFree(dev->sort_key);
   if (dev->sort_hist) hipFree(dev->sort_hist);
@@ -1883,6 +2059,16 @@ int hipcy_set_traversal_budget(hipcy_device *dev, int first, int second)
   return 0;
 }
 
+int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle)
+{
+  if (rounds < 0 || min_idle < 1 || min_idle > 64) {
+    return set_error(dev, "set_traversal_refill: rounds >= 0 (0 = off), 1 <= min_idle <= 64");
+  }
+  dev->trav_refill[0] = rounds;
+  dev->trav_refill[1] = min_idle;
+  return 0;
+}
+
 int hipcy_set_ray_sort(hipcy_device *dev, int mode)
 {
   if (mode != 0 && mode != 3 && mode != 5) {
@@ -1918,9 +2104,10 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
 static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
                             const std::vector<void *> &tex_mem, const std::vector<uint32_t> &shader_flags,
                             bool *uses_tex, bool *uses_bssrdf, bool *uses_disk_bssrdf, bool *uses_attr,
-                            int *surface_closures, int *volume_closures)
+                            bool *uses_ray_diff, int *surface_closures, int *volume_closures)
 {
   *uses_tex = false;
+  *uses_ray_diff = false;
   *uses_bssrdf = false;
   *uses_disk_bssrdf = false;
   *uses_attr = false;
@@ -2077,20 +2264,25 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
         case NODE_LAYER_WEIGHT:
           break;
         case NODE_MATH:
-          if (node.y == 6 || (node.y >= 29 && node.y <= 31)) {
-            return "math node: tangent / sinh / cosh / tanh are not implemented";
-          }
           tex = true;
           break;
         case NODE_VECTOR_MATH:
-          if (node.y == 23) {
-            return "vector math node: tangent is not implemented";
-          }
           len = (node.y == 20) ? 2 : 1; /* WRAP: extra node */
           tex = true;
           break;
+        case NODE_TEX_COORD_BUMP_DX:
+        case NODE_TEX_COORD_BUMP_DY:
+          *uses_ray_diff = true;
+          /* fall through */
         case NODE_TEX_COORD:
           len = (node.y == 1 && node.w != 0) ? 4 : 1; /* OBJECT with a transform */
+          tex = true;
+          break;
+        case NODE_SET_BUMP:
+          *uses_ray_diff = true;
+          tex = true;
+          break;
+        case NODE_CLOSURE_SET_NORMAL: /* the bump program of displacement method "bump" */
           tex = true;
           break;
         case NODE_RGB_RAMP:
@@ -2155,6 +2347,12 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           len = 4;
           tex = true;
           break;
+        case NODE_ATTR_BUMP_DX:
+        case NODE_ATTR_BUMP_DY:
+        case NODE_VERTEX_COLOR_BUMP_DX:
+        case NODE_VERTEX_COLOR_BUMP_DY:
+          *uses_ray_diff = true;
+          /* fall through */
         case NODE_ATTR:
         case NODE_VERTEX_COLOR:
         case NODE_TANGENT:
@@ -2183,6 +2381,10 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           len = 2 + (size_t)prog[off + 1].x;
           tex = true;
           break;
+        case NODE_GEOMETRY_BUMP_DX:
+        case NODE_GEOMETRY_BUMP_DY:
+          *uses_ray_diff = true;
+          /* fall through */
         case NODE_GEOMETRY:
           *uses_attr |= node.y == 2u; /* Tangent: primitive_tangent reads the generated coordinates */
           tex = true;
@@ -2317,10 +2519,10 @@ int hipcy_load_kernels(hipcy_device *dev)
       shader_flags[i] = (uint32_t)ks[i].flags;
     }
   }
-  bool uses_bssrdf = false, uses_disk_bssrdf = false, uses_attr = false;
+  bool uses_bssrdf = false, uses_disk_bssrdf = false, uses_attr = false, uses_ray_diff = false;
   int surface_closures = 0, volume_closures = 0;
   why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, shader_flags, &dev->shade_tex, &uses_bssrdf,
-                 &uses_disk_bssrdf, &uses_attr, &surface_closures, &volume_closures);
+                 &uses_disk_bssrdf, &uses_attr, &uses_ray_diff, &surface_closures, &volume_closures);
   if (why.empty() && uses_attr && dev->globals.find("__attributes_map") == dev->globals.end()) {
     /* the attribute nodes look attributes up through the objects' maps
      * (GeometryManager::device_update_attributes, geometry.cpp:379-474) */
@@ -2331,6 +2533,7 @@ int hipcy_load_kernels(hipcy_device *dev)
   }
   dev->use_volumes = d.integrator.use_volumes != 0;
   dev->use_disk_bssrdf = uses_disk_bssrdf;
+  dev->use_ray_diff = uses_ray_diff;
   dev->shade_closures = d.integrator.max_closures;
   if (dev->use_volumes) {
     /* the volume stack of a path holds the world and every volume object it
@@ -2568,6 +2771,23 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
       if (continuations(false) != 0) {
         return -1;
       }
+    }
+    else if (dev->trav_refill[0] > 0 && W > 2 && !kg.have_instancing && !kg.have_curves) {
+      /* persistent waves with lane refill (k_closest_refill) */
+      if (!dev->refill_claim) {
+        HIP_CHECK(dev, hipMalloc((void **)&dev->refill_claim, (size_t)CY_LANES * 8 * sizeof(uint)));
+      }
+      uint *claim = dev->refill_claim + 8 * ln.index;
+      HIP_CHECK(dev, hipMemsetAsync(claim, 0, 8 * sizeof(uint), s));
+      if (cam_n > 0) {
+        hipLaunchKernelGGL(k_camera_rays, dim3((cam_n + CY_BLOCK - 1) / CY_BLOCK), block, 0, s, kg, dev->bufs,
+                           ln.tile, cam_n, ln.slot_base);
+      }
+      auto kfn = counters ? (W == 8 ? k_closest_refill<true, 8> : k_closest_refill<true, 4>)
+                          : (W == 8 ? k_closest_refill<false, 8> : k_closest_refill<false, 4>);
+      hipLaunchKernelGGL(kfn, dim3(std::min<uint>(CY_REFILL_BLOCKS, grid.x)), block, 0, s, kg, dev->bufs, cam_n,
+                         ln.slot_base, queue_in, ln.cnt + qa, claim, err, dev->stats_dev, dev->trav_refill[0],
+                         dev->trav_refill[1]);
     }
     else {
       auto kfn = pick_kernel<ClosestK>(counters, W, kg.have_instancing != 0, dev->curve_shapes);
@@ -2845,7 +3065,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
   }
   const size_t items = npix * per_pass;
   if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
       ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }
@@ -3418,7 +3638,7 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
     ring_cap <<= 1;
   }
   if (ensure_capacity(dev, lane_slots * lanes) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
       ensure_records(dev, (size_t)ring_cap * lanes) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }

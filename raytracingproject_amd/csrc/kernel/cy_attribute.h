@@ -11,6 +11,9 @@
  *   svm_node_normal_map, svm_node_tangent  kernel/svm/svm_tex_coord.h:255-392
  *   ensure_valid_reflection                kernel/kernel_montecarlo.h:196-298
  *   svm_node_object_info                   kernel/svm/svm_geometry.h:104-139
+ *   svm_node_attr_bump_dx / _dy            kernel/svm/svm_attribute.h:92-188
+ *   svm_node_vertex_color_bump_dx / _dy    kernel/svm/svm_vertex_color.h:38-90
+ *   svm_node_set_bump                      kernel/svm/svm_displace.h:21-84
  * The host packs attributes only for triangle meshes without subdivision
  * (`__tri_patch` is all ~0, so attribute_primitive_type is always
  * ATTR_PRIM_GEOMETRY); an attribute found on a curve raises
@@ -24,6 +27,7 @@
 enum {
   NODE_ATTR = 16,
   NODE_VERTEX_COLOR = 17,
+  NODE_SET_BUMP = 26,
   NODE_OBJECT_INFO = 48,
   NODE_TANGENT = 70,
   NODE_NORMAL_MAP = 71
@@ -125,8 +129,11 @@ CY_FN void attr_fetch(const CyGlobals *kg, int n, bool bytes, int i, float f[4])
  * the triangle at (u, v): u*f0 + v*f1 + (1-u-v)*f2 per component for
  * per-vertex and per-corner elements, the stored value for per-face and
  * per-object ones, 0 for elements the reference's reader of that width
- * does not handle */
-CY_FN void triangle_attribute(const CyGlobals *kg, const CyAttr &desc, int prim, float u, float v, int n, float out[4])
+ * does not handle.  With dd = {du, dv} (one axis of the shading point's
+ * differentials) the value plus its derivative, du*f0 + dv*f1 - (du+dv)*f2
+ * for interpolated elements and 0 otherwise (the *_BUMP_DX / _DY nodes) */
+CY_FN void triangle_attribute(const CyGlobals *kg, const CyAttr &desc, int prim, float u, float v, int n, float out[4],
+                              const float *dd = nullptr)
 {
   int idx[3] = {0, 0, 0};
   int m = 0;
@@ -184,12 +191,18 @@ CY_FN void triangle_attribute(const CyGlobals *kg, const CyAttr &desc, int prim,
   for (int c = 0; c < n; c++) {
     out[c] = (m == 3) ? u * f[0][c] + v * f[1][c] + w * f[2][c] : (m == 1) ? f[0][c] : 0.0f;
   }
+  if (dd) {
+    for (int c = 0; c < n; c++) {
+      const float d = (m == 3) ? dd[0] * f[0][c] + dd[1] * f[1][c] - (dd[0] + dd[1]) * f[2][c] : 0.0f;
+      out[c] = out[c] + d;
+    }
+  }
 }
 
 /* svm_node_attr: the attribute read with the stored type, converted to the
  * node's output type (float: the average of a colour / vector) */
 CY_FN void svm_node_attr(const CyGlobals *kg, int object, int prim, int type, float u, float v, CySvmStack stack,
-                         hc_uint4 node, uint *err)
+                         hc_uint4 node, uint *err, const float *dd = nullptr)
 {
   const uint out_offset = node.z;
   const int out_type = (int)node.w;
@@ -216,7 +229,7 @@ CY_FN void svm_node_attr(const CyGlobals *kg, int object, int prim, int type, fl
                 (desc.type == NODE_ATTR_RGBA)  ? 4 :
                                                  3;
   if (tri) {
-    triangle_attribute(kg, desc, prim, u, v, n, f);
+    triangle_attribute(kg, desc, prim, u, v, n, f, dd);
   }
   if (n == 1) {
     if (out_type == NODE_ATTR_FLOAT) {
@@ -246,13 +259,14 @@ CY_FN void svm_node_attr(const CyGlobals *kg, int object, int prim, int type, fl
 }
 
 CY_FN void svm_node_vertex_color(const CyGlobals *kg, int object, int prim, int type, float u, float v,
-                                 CySvmStack stack, uint layer_id, uint color_offset, uint alpha_offset, uint *err)
+                                 CySvmStack stack, uint layer_id, uint color_offset, uint alpha_offset, uint *err,
+                                 const float *dd = nullptr)
 {
   const CyAttr desc = find_attribute(kg, object, prim, layer_id);
   if (desc.offset != (int)ATTR_STD_NOT_FOUND) {
     float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (type & PRIMITIVE_ALL_TRIANGLE) {
-      triangle_attribute(kg, desc, prim, u, v, 4, f);
+      triangle_attribute(kg, desc, prim, u, v, 4, f, dd);
     }
     else if (type & PRIMITIVE_ALL_CURVE) {
       cy_set_error(err, CY_ERR_FEATURE, 11);
@@ -273,6 +287,10 @@ typedef struct CyAttrIn {
   int object, prim, type, flag, shader;
 #if CY_CLOSURE_EXT
   cfloat3 dPdu;
+  /* the Bump node's dP.dx / dP.dy; a bump form's du, dv along its axis */
+  cfloat3 dPdx, dPdy;
+  float bump_du, bump_dv;
+  int bump;
 #endif
 } CyAttrIn;
 
@@ -529,8 +547,59 @@ CY_FN void svm_node_geometry_tangent(const CyGlobals *kg, const CyAttrIn &in, Cy
   svm_store3(stack, out_offset, T, err);
 }
 
+#if CY_CLOSURE_EXT
+/* svm_displace.h:21-84 svm_node_set_bump: the normal tilted by the height's
+ * differences across the shading point's dP.dx / dP.dy (the graph's
+ * SampleX / SampleY copies were evaluated at P + dP.dx / dy) */
+CY_FN void svm_node_set_bump(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, hc_uint4 node, uint *err)
+{
+  uint normal_offset, scale_offset, invert, use_object_space;
+  svm_unpack4(node.y, &normal_offset, &scale_offset, &invert, &use_object_space);
+  cfloat3 normal_in = (normal_offset != SVM_STACK_INVALID) ? svm_load3(stack, normal_offset, err) : in.N;
+  cfloat3 dPdx = in.dPdx;
+  cfloat3 dPdy = in.dPdy;
+  if (use_object_space) {
+    normal_in = attr_object_inverse_normal_transform(kg, in.object, normal_in);
+    if (in.object != OBJECT_NONE) {
+      dPdx = transform_direction(object_itfm(kg, in.object), dPdx);
+      dPdy = transform_direction(object_itfm(kg, in.object), dPdy);
+    }
+  }
+  /* surface tangents from the normal */
+  const cfloat3 Rx = cross3(dPdy, normal_in);
+  const cfloat3 Ry = cross3(normal_in, dPdx);
+  uint c_offset, x_offset, y_offset, strength_offset;
+  svm_unpack4(node.z, &c_offset, &x_offset, &y_offset, &strength_offset);
+  const float h_c = svm_load(stack, c_offset, err);
+  const float h_x = svm_load(stack, x_offset, err);
+  const float h_y = svm_load(stack, y_offset, err);
+  /* surface gradient and determinant */
+  const float det = dot3(dPdx, Rx);
+  const cfloat3 surfgrad = add3(mul3f(Rx, h_x - h_c), mul3f(Ry, h_y - h_c));
+  const float absdet = fabsf(det);
+  float strength = svm_load(stack, strength_offset, err);
+  float scale = svm_load(stack, scale_offset, err);
+  if (invert) {
+    scale *= -1.0f;
+  }
+  strength = cmax(strength, 0.0f);
+  cfloat3 normal_out = safe_normalize3(sub3(mul3f(normal_in, absdet), mul3f(surfgrad, scale * signf(det))));
+  if (is_zero3(normal_out)) {
+    normal_out = normal_in;
+  }
+  else {
+    normal_out = normalize3(add3(mul3f(normal_out, strength), mul3f(normal_in, 1.0f - strength)));
+  }
+  if (use_object_space) {
+    normal_out = attr_object_normal_transform(kg, in.object, normal_out);
+  }
+  normal_out = ensure_valid_reflection(in.Ng, in.I, normal_out);
+  svm_store3(stack, node.w, normal_out, err);
+}
+#endif
+
 /* NODE_ATTR / NODE_VERTEX_COLOR / NODE_NORMAL_MAP / NODE_TANGENT /
- * NODE_OBJECT_INFO out of line: the arrays they read in a local CyGlobals, so
+ * NODE_OBJECT_INFO / NODE_SET_BUMP out of line: the arrays they read in a local CyGlobals, so
  * the shading kernels' register allocation does not carry them */
 CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
                                          const hc_KernelShader *shaders,
@@ -555,13 +624,24 @@ CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
   kgv.__attributes_uchar4 = attributes_uchar4;
   kgv.__tri_vindex = tri_vindex;
   const CyGlobals *kg = &kgv;
+#if CY_CLOSURE_EXT
+  const float dd[2] = {in.bump_du, in.bump_dv};
+  const float *ddp = in.bump ? dd : nullptr;
+#else
+  const float *ddp = nullptr;
+#endif
   switch (node.x) {
     case NODE_ATTR:
-      svm_node_attr(kg, in.object, in.prim, in.type, in.u, in.v, stack, node, err);
+      svm_node_attr(kg, in.object, in.prim, in.type, in.u, in.v, stack, node, err, ddp);
       break;
     case NODE_VERTEX_COLOR:
-      svm_node_vertex_color(kg, in.object, in.prim, in.type, in.u, in.v, stack, node.y, node.z, node.w, err);
+      svm_node_vertex_color(kg, in.object, in.prim, in.type, in.u, in.v, stack, node.y, node.z, node.w, err, ddp);
       break;
+#if CY_CLOSURE_EXT
+    case NODE_SET_BUMP:
+      svm_node_set_bump(kg, in, stack, node, err);
+      break;
+#endif
     case NODE_NORMAL_MAP:
       svm_node_normal_map(kg, in, stack, node, err);
       break;

@@ -1118,7 +1118,8 @@ CY_FN int bsdf_ggx_sample(const CyGlobals *kg,
                           float randv,
                           cfloat3 *eval,
                           cfloat3 *omega_in,
-                          float *pdf)
+                          float *pdf,
+                          cfloat3 *m_out = nullptr)
 {
   float alpha_x = sc->alpha_x;
   float alpha_y = sc->alpha_y;
@@ -1143,6 +1144,9 @@ CY_FN int bsdf_ggx_sample(const CyGlobals *kg,
     float G1o;
     local_m = microfacet_sample_stretched(kg, local_I, alpha_x, alpha_y, randu, randv, false, &G1o);
     cfloat3 m = add3(add3(mul3f(X, local_m.x), mul3f(Y, local_m.y)), mul3f(Z, local_m.z));
+    if (m_out) {
+      *m_out = m;
+    }
     float cosThetaM = local_m.z;
     if (!m_refractive) {
       float cosMO = dot3(m, I);
@@ -1361,7 +1365,8 @@ CY_FN int bsdf_beckmann_sample(const CyGlobals *kg,
                                float randv,
                                cfloat3 *eval,
                                cfloat3 *omega_in,
-                               float *pdf)
+                               float *pdf,
+                          cfloat3 *m_out = nullptr)
 {
   float alpha_x = sc->alpha_x;
   float alpha_y = sc->alpha_y;
@@ -1381,6 +1386,9 @@ CY_FN int bsdf_beckmann_sample(const CyGlobals *kg,
     float G1o;
     cfloat3 local_m = microfacet_sample_stretched(kg, local_I, alpha_x, alpha_x, randu, randv, true, &G1o);
     cfloat3 m = add3(add3(mul3f(X, local_m.x), mul3f(Y, local_m.y)), mul3f(Z, local_m.z));
+    if (m_out) {
+      *m_out = m;
+    }
     float cosThetaM = local_m.z;
     if (!m_refractive) {
       label = LABEL_REFLECT | LABEL_GLOSSY;
@@ -1592,8 +1600,75 @@ CY_FN float bump_shadowing_term(cfloat3 Ng, cfloat3 N, cfloat3 I)
   return -g2 * g + g2 + g;
 }
 
+#if CY_CLOSURE_EXT
+/* The differentials of a sampled direction follow from the shading point's
+ * dI by one of a few rules (the __RAY_DIFFERENTIALS__ lines of each closure's
+ * sample function): the mirror about n (bsdf_diffuse.h:104), its negation
+ * (bsdf_diffuse.h:166), -dI (bsdf_transparent.h:117), fresnel_dielectric's
+ * refracted differential (bsdf_util.h:92) or zero (total internal reflection). */
+enum { CY_DIFF_ZERO = 0, CY_DIFF_MIRROR, CY_DIFF_NEG_MIRROR, CY_DIFF_NEG, CY_DIFF_REFRACT };
+typedef struct CyDiffRule {
+  int kind;
+  cfloat3 n;
+  float neta, k; /* refraction: -(neta * dI) + (k * dot(dI, n)) * n */
+} CyDiffRule;
+
+CY_FN cfloat3 diff_rule_apply(const CyDiffRule &r, cfloat3 dI)
+{
+  switch (r.kind) {
+    case CY_DIFF_MIRROR:
+      return sub3(mul3f(r.n, 2 * dot3(r.n, dI)), dI);
+    case CY_DIFF_NEG_MIRROR:
+      return neg3(sub3(mul3f(r.n, 2 * dot3(r.n, dI)), dI));
+    case CY_DIFF_NEG:
+      return neg3(dI);
+    case CY_DIFF_REFRACT:
+      return add3(neg3(mul3f(dI, r.neta)), mul3f(r.n, r.k * dot3(dI, r.n)));
+    default:
+      return mk3(0.0f, 0.0f, 0.0f);
+  }
+}
+
+CY_FN void diff_rule_set(CyDiffRule *r, int kind, cfloat3 n)
+{
+  r->kind = kind;
+  r->n = n;
+}
+
+/* fresnel_dielectric's dR (reflect) or dT (bsdf_util.h:53-93) */
+CY_FN void diff_rule_fresnel(CyDiffRule *r, float eta, cfloat3 N, cfloat3 I, bool reflect)
+{
+  float cos = dot3(N, I), neta;
+  cfloat3 Nn;
+  if (cos > 0) {
+    neta = 1 / eta;
+    Nn = N;
+  }
+  else {
+    cos = -cos;
+    neta = eta;
+    Nn = neg3(N);
+  }
+  r->n = Nn;
+  if (reflect) {
+    r->kind = CY_DIFF_MIRROR;
+    return;
+  }
+  const float arg = 1 - (neta * neta * (1 - (cos * cos)));
+  if (arg < 0) {
+    r->kind = CY_DIFF_ZERO;
+    return;
+  }
+  const float dnp = cmax(sqrtf(arg), 1e-7f);
+  r->kind = CY_DIFF_REFRACT;
+  r->neta = neta;
+  r->k = neta - neta * neta * cos / dnp;
+}
+#endif
+
 /* bsdf.h:113-489.  The shadow-terminator offset (object frequency multiplier
- * > 1) is rejected at load_kernels. */
+ * > 1) is rejected at load_kernels.  With ray differentials the sampled
+ * direction's rule comes out in *rule. */
 CY_FN int bsdf_sample(const CyGlobals *kg,
                       const CySD *sd,
                       const CyClosure *sc,
@@ -1602,7 +1677,12 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
                       cfloat3 *eval,
                       cfloat3 *omega_in,
                       float *pdf,
-                      uint *err)
+                      uint *err
+#if CY_CLOSURE_EXT
+                      ,
+                      CyDiffRule *rule = nullptr
+#endif
+)
 {
   int label;
   /* bsdf.h:124-126: curves sample against the closure's smooth normal */
@@ -1646,11 +1726,37 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
     case CLOSURE_BSDF_MICROFACET_GGX_FRESNEL_ID:
     case CLOSURE_BSDF_MICROFACET_GGX_CLEARCOAT_ID:
     case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+#if CY_CLOSURE_EXT
+      if (rule) {
+        cfloat3 m = mk3(0.0f, 0.0f, 0.0f);
+        label = bsdf_ggx_sample(kg, sd, sc, Ng, sd->I, randu, randv, eval, omega_in, pdf, &m);
+        /* bsdf_microfacet.h:702, 720-740 */
+        if (sc->type == CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID) {
+          diff_rule_fresnel(rule, sc->ior, m, sd->I, false);
+        }
+        else {
+          diff_rule_set(rule, CY_DIFF_MIRROR, m);
+        }
+        break;
+      }
+#endif
       label = bsdf_ggx_sample(kg, sd, sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
 #if CY_CLOSURE_EXT
     case CLOSURE_BSDF_MICROFACET_BECKMANN_ID:
     case CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID:
+      if (rule) {
+        cfloat3 m = mk3(0.0f, 0.0f, 0.0f);
+        label = bsdf_beckmann_sample(kg, sc, Ng, sd->I, randu, randv, eval, omega_in, pdf, &m);
+        /* bsdf_microfacet.h:1093, 1111-1131 */
+        if (sc->type == CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID) {
+          diff_rule_fresnel(rule, sc->ior, m, sd->I, false);
+        }
+        else {
+          diff_rule_set(rule, CY_DIFF_MIRROR, m);
+        }
+        break;
+      }
       label = bsdf_beckmann_sample(kg, sc, Ng, sd->I, randu, randv, eval, omega_in, pdf);
       break;
     case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
@@ -1689,6 +1795,77 @@ CY_FN int bsdf_sample(const CyGlobals *kg,
       label = LABEL_NONE;
       break;
   }
+#if CY_CLOSURE_EXT
+  if (rule) {
+    switch (sc->type) {
+      case CLOSURE_BSDF_DIFFUSE_ID:
+      case CLOSURE_BSDF_BSSRDF_ID:
+      case CLOSURE_BSDF_OREN_NAYAR_ID:
+      case CLOSURE_BSDF_REFLECTION_ID:
+      case CLOSURE_BSDF_ASHIKHMIN_SHIRLEY_ID:
+      case CLOSURE_BSDF_ASHIKHMIN_VELVET_ID:
+      case CLOSURE_BSDF_DIFFUSE_TOON_ID:
+      case CLOSURE_BSDF_GLOSSY_TOON_ID:
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_ID:
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_FRESNEL_ID:
+        diff_rule_set(rule, CY_DIFF_MIRROR, sc->N);
+        break;
+      case CLOSURE_BSDF_TRANSLUCENT_ID:
+      case CLOSURE_BSDF_PRINCIPLED_DIFFUSE_ID:
+      case CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID:
+      case CLOSURE_BSDF_PRINCIPLED_SHEEN_ID:
+        diff_rule_set(rule, CY_DIFF_NEG_MIRROR, sc->N);
+        break;
+      case CLOSURE_BSDF_TRANSPARENT_ID:
+        rule->kind = CY_DIFF_NEG;
+        break;
+      case CLOSURE_BSDF_REFRACTION_ID:
+        diff_rule_fresnel(rule, sc->ior, sc->N, sd->I, false);
+        break;
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_ID:
+      case CLOSURE_BSDF_MICROFACET_MULTI_GGX_GLASS_FRESNEL_ID:
+        if (sc->alpha_x * sc->alpha_y < 1e-7f) {
+          /* bsdf_microfacet_multi.h:651-690 */
+          diff_rule_fresnel(rule, sc->ior, sc->N, sd->I, (label & LABEL_REFLECT) != 0);
+        }
+        else if (label & LABEL_REFLECT) {
+          diff_rule_set(rule, CY_DIFF_MIRROR, sc->N);
+        }
+        else {
+          /* bsdf_microfacet_multi.h:720-726: the refraction with neta = ior */
+          const float ior = sc->ior;
+          const float cosI = dot3(sc->N, sd->I);
+          const float dnp = cmax(sqrtf(1.0f - (ior * ior * (1.0f - cosI * cosI))), 1e-7f);
+          rule->kind = CY_DIFF_REFRACT;
+          rule->n = sc->N;
+          rule->neta = ior;
+          rule->k = ior - ior * ior * cosI / dnp;
+        }
+        break;
+      case CLOSURE_BSDF_HAIR_REFLECTION_ID:
+      case CLOSURE_BSDF_HAIR_TRANSMISSION_ID: {
+        /* bsdf_hair.h:231-232 */
+        const float Iz = dot3(sc->T, sd->I);
+        diff_rule_set(rule, CY_DIFF_MIRROR, normalize3(sub3(sd->I, mul3f(sc->T, Iz))));
+        break;
+      }
+      case CLOSURE_BSDF_HAIR_PRINCIPLED_ID:
+        /* bsdf_hair_principled.h:477-479 */
+        diff_rule_set(rule, CY_DIFF_MIRROR, safe_normalize3(add3(sd->I, *omega_in)));
+        break;
+      case CLOSURE_BSDF_MICROFACET_GGX_ID:
+      case CLOSURE_BSDF_MICROFACET_GGX_FRESNEL_ID:
+      case CLOSURE_BSDF_MICROFACET_GGX_CLEARCOAT_ID:
+      case CLOSURE_BSDF_MICROFACET_GGX_REFRACTION_ID:
+      case CLOSURE_BSDF_MICROFACET_BECKMANN_ID:
+      case CLOSURE_BSDF_MICROFACET_BECKMANN_REFRACTION_ID:
+        break; /* set above */
+      default:
+        rule->kind = CY_DIFF_ZERO;
+        break;
+    }
+  }
+#endif
   if (label & LABEL_TRANSMIT) {
     float threshold_squared = KD->background.transparent_roughness_squared_threshold;
     if (threshold_squared >= 0.0f) {

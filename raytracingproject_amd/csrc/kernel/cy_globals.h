@@ -67,6 +67,10 @@ typedef struct CyGlobals {
   /* KernelBVH.have_curves: hair segments in the BVH (BVH2 traversal with
    * unaligned nodes and curve leaves; shading reads __prim_type) */
   int have_curves;
+  /* 1 when a shader reads ray differentials (Bump / *_BUMP_DX / _DY nodes):
+   * the paths carry dP / dD (CyPathBuffers.ray_diff) and shading points get
+   * dP, dI, du, dv; otherwise they are zero */
+  int use_ray_diff;
 } CyGlobals;
 
 #endif /* CY_GLOBALS_H */

@@ -57,10 +57,17 @@ typedef struct CyPathBuffers {
    * CY_SSS_RECS records of CY_SSS_REC_F4 float4 per slot, and its depth */
   hc_float4 *sss_rec;
   uint *sss_count;
+  /* scenes whose shaders read ray differentials (CyGlobals.use_ray_diff): the
+   * path ray's dP / dD, CY_RAY_DIFF_F4 float4 per slot (written when the ray
+   * is made; a camera launch's first shade recomputes them), and the shading
+   * point's dP the pending transparent shadow ray carries, 2 float4 per slot */
+  hc_float4 *ray_diff;
+  hc_float4 *shadow_dP;
 } CyPathBuffers;
 
 #define CY_SSS_RECS (BSSRDF_MAX_HITS - 1)
-#define CY_SSS_REC_F4 6
+#define CY_SSS_REC_F4 9 /* state (3), ray (2), throughput, ray differentials (3) */
+#define CY_RAY_DIFF_F4 3
 
 /* Pending volume stack update of a slot (cy_volume.h volume_stack_enter_exit
  * of the surface in vol_rec[0].xy): the reference updates the stack when the
@@ -222,9 +229,29 @@ CY_FN void store_state(const CyPathBuffers *b, int slot, const CyPathState *s)
 }
 
 #if CY_CLOSURE_EXT
-/* A subsurface indirect ray of the slot (state, ray, throughput). */
+/* A ray's differentials dP, dD in three float4. */
+CY_FN void diff_store(hc_float4 *dst, const CyDiff3 &dP, const CyDiff3 &dD)
+{
+  cy_st(&dst[0], mkf4(dP.dx.x, dP.dx.y, dP.dx.z, dP.dy.x));
+  cy_st(&dst[1], mkf4(dP.dy.y, dP.dy.z, dD.dx.x, dD.dx.y));
+  cy_st(&dst[2], mkf4(dD.dx.z, dD.dy.x, dD.dy.y, dD.dy.z));
+}
+
+CY_FN void diff_load(const hc_float4 *src, CyDiff3 *dP, CyDiff3 *dD)
+{
+  const hc_float4 a = cy_ld(&src[0]);
+  const hc_float4 c = cy_ld(&src[1]);
+  const hc_float4 e = cy_ld(&src[2]);
+  dP->dx = mk3(a.x, a.y, a.z);
+  dP->dy = mk3(a.w, c.x, c.y);
+  dD->dx = mk3(c.z, c.w, e.x);
+  dD->dy = mk3(e.y, e.z, e.w);
+}
+
+/* A subsurface indirect ray of the slot (state, ray, throughput; with ray
+ * differentials their dP, dD). */
 CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathState *s, const CyRay *ray,
-                         cfloat3 throughput)
+                         cfloat3 throughput, const CyDiff3 *dP = nullptr, const CyDiff3 *dD = nullptr)
 {
   hc_float4 *dst = b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4;
   cy_st(&dst[0], mkf4(int_as_float(s->flag), as_float(s->rng_hash), int_as_float(s->rng_offset),
@@ -235,10 +262,13 @@ CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathSt
   cy_st(&dst[3], mkf4(ray->P.x, ray->P.y, ray->P.z, ray->t));
   cy_st(&dst[4], mkf4(ray->D.x, ray->D.y, ray->D.z, 0.0f));
   cy_st(&dst[5], mkf4(throughput.x, throughput.y, throughput.z, 0.0f));
+  if (dP) {
+    diff_store(&dst[6], *dP, *dD);
+  }
 }
 
 CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals *kg, CyPathState *s, CyRay *ray,
-                        cfloat3 *throughput)
+                        cfloat3 *throughput, CyDiff3 *dP = nullptr, CyDiff3 *dD = nullptr)
 {
   const hc_float4 *src = b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4;
   const hc_float4 r0 = cy_ld(&src[0]);
@@ -266,6 +296,9 @@ CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals
   ray->t = r3.w;
   ray->D = mk3(r4.x, r4.y, r4.z);
   *throughput = mk3(r5.x, r5.y, r5.z);
+  if (dP) {
+    diff_load(&src[6], dP, dD);
+  }
 }
 
 /* The slot's volume stack and pending update records (CyPathBuffers.vol_*). */
@@ -586,6 +619,26 @@ CY_FN void item_camera_ray(const CyGlobals *kg, const CyTile *tile, uint item, u
   camera_sample_ray(kg, x, y, *sample, rng_hash, ray);
 }
 
+#if CY_CLOSURE_EXT
+/* The differentials of the slot's ray: a camera launch's first shade
+ * recomputes the camera ray's (camera_sample_ray), later ones read the slot's
+ * record. */
+CY_FN void ray_diff_load(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot, uint cam_item,
+                         CyDiff3 *dP, CyDiff3 *dD)
+{
+  if (cam_item != CY_NO_ITEM) {
+    int x, y, sample;
+    uint rng_hash;
+    CyRay ray;
+    item_pixel(tile, cam_item, &x, &y, &sample);
+    camera_sample_ray(kg, x, y, sample, &rng_hash, &ray, dP, dD);
+  }
+  else {
+    diff_load(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, dP, dD);
+  }
+}
+#endif
+
 CY_FN void write_no_sample(const CyTile *tile, uint item)
 {
   cy_st(&tile->samples_out[item & tile->ring_mask], mkf4(0.0f, 0.0f, 0.0f, __builtin_nanf("")));
@@ -599,6 +652,13 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
   uint rng_hash;
   int sample;
   CyRay ray;
+#if CY_CLOSURE_EXT
+  if (kg->use_ray_diff) {
+    CyDiff3 dP, dD;
+    ray_diff_load(kg, b, tile, slot, item, &dP, &dD);
+    diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, dP, dD);
+  }
+#endif
   item_camera_ray(kg, tile, item, &rng_hash, &sample, &ray);
   if (ray.t == 0.0f) {
     write_no_sample(tile, item);
@@ -707,7 +767,8 @@ CY_FN bool shadow_finish(const CyPathBuffers *b, const CyTile *tile, int slot, b
 #endif
 template<bool VOL = false>
 CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPathState *state, CyShadeMem mem,
-                                      cfloat3 *shadow, uint *err, void *volume_stack = nullptr)
+                                      cfloat3 *shadow, uint *err, void *volume_stack = nullptr,
+                                      const CyDiff3 *ray_dP = nullptr)
 {
 #if CY_CLOSURE_EXT
   /* volume scenes: the shadow ray's copy of the path's volume stack, crossed
@@ -774,7 +835,15 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
     sd.svm_stride = mem.svm_stride;
     sd.svm_fast = mem.svm_fast;
     sd.svm_spill = mem.svm_spill;
+#if CY_CLOSURE_EXT
+    /* the shadow ray carries the shading point's dP and no dD
+     * (kernel_emission.h:193-194) */
+    CyDiff3 zero_dD;
+    zero_dD.dx = zero_dD.dy = mk3(0.0f, 0.0f, 0.0f);
+    shader_setup_from_ray(kg, &sd, &isect, &ray, ray_dP, &zero_dD);
+#else
     shader_setup_from_ray(kg, &sd, &isect, &ray);
+#endif
     if (!VOL || !(sd.flag & SD_HAS_ONLY_VOLUME)) {
       CyPathState st = *state;
       st.bounce += 1; /* path_state_modify_bounce */
@@ -827,6 +896,15 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
   cfloat3 shadow;
   bool blocked;
 #if CY_CLOSURE_EXT
+  CyDiff3 sdP;
+  const CyDiff3 *sdP_ptr = nullptr;
+  if (kg->use_ray_diff) {
+    const hc_float4 a = cy_ld(&b->shadow_dP[2 * (size_t)slot]);
+    const hc_float4 c = cy_ld(&b->shadow_dP[2 * (size_t)slot + 1]);
+    sdP.dx = mk3(a.x, a.y, a.z);
+    sdP.dy = mk3(a.w, c.x, c.y);
+    sdP_ptr = &sdP;
+  }
   if (VOL) {
     /* the stack the light sample saw, crossing the surface when the ray
      * leaves through it, and the rng offset of the sample's bounce */
@@ -839,13 +917,15 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
                               (int)r0.y, &vstack);
     }
     state.rng_offset = (int)r1.y;
-    blocked = shadow_blocked_transparent<true>(kg, ray, &state, mem, &shadow, err, &vstack);
+    blocked = shadow_blocked_transparent<true>(kg, ray, &state, mem, &shadow, err, &vstack, sdP_ptr);
   }
   else
-#endif
   {
-    blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err);
+    blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err, nullptr, sdP_ptr);
   }
+#else
+  blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err);
+#endif
   hc_float4 L4 = cy_ld(&b->L[slot]);
   if (!blocked) {
     const cfloat3 shaded_throughput = mul3(mul3f(mk3(st4.x, st4.y, st4.z), 1.0f), shadow);
@@ -974,7 +1054,8 @@ CY_FN void accumulate_stream_pixel(const CyTileDesc &d, const hc_float4 *ring, u
 }
 
 /* shader_setup_from_background (kernel_shader.h:397-439): P = D, N = Ng = I = -D */
-CY_FN void shader_setup_from_background(const CyGlobals *kg, CySD *sd, cfloat3 D, CyShadeMem mem)
+CY_FN void shader_setup_from_background(const CyGlobals *kg, CySD *sd, cfloat3 D, CyShadeMem mem,
+                                        const CyDiff3 *ray_dD = nullptr)
 {
   sd->closure = mem.closure;
   sd->svm_stack = mem.svm_stack;
@@ -995,6 +1076,13 @@ CY_FN void shader_setup_from_background(const CyGlobals *kg, CySD *sd, cfloat3 D
 #if CY_CLOSURE_EXT
   sd->dPdu = mk3(0.0f, 0.0f, 0.0f);
   sd->dPdv = mk3(0.0f, 0.0f, 0.0f);
+  /* dP = the ray's dD, dI = -dD (kernel_shader.h:426-432) */
+  sd_zero_differentials(sd);
+  if (ray_dD) {
+    sd->dP = *ray_dD;
+    sd->dI.dx = neg3(ray_dD->dx);
+    sd->dI.dy = neg3(ray_dD->dy);
+  }
 #endif
   sd->u = 0.0f;
   sd->v = 0.0f;
@@ -1022,7 +1110,8 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
                                         CyShadeMem mem,
                                         CyPathState state,
                                         int path_flag,
-                                        uint *err)
+                                        uint *err,
+                                        const CyDiff3 *ray_dD = nullptr)
 {
   CyGlobals kgv;
   kgv.data = data;
@@ -1032,7 +1121,7 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
   kgv.__texture_info = texture_info;
   const CyGlobals *kg = &kgv;
   CySD esd;
-  shader_setup_from_background(kg, &esd, D, mem);
+  shader_setup_from_background(kg, &esd, D, mem, ray_dD);
   state.bounce += 1;
   shader_eval_surface(kg, &esd, &state, path_flag, err);
   return shader_background_eval(&esd);
@@ -1105,6 +1194,9 @@ cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I,
     esd.dPdv = neg3(esd.dPdv);
 #endif
   }
+#if CY_CLOSURE_EXT
+  sd_zero_differentials(&esd); /* shader_setup_from_sample: no ray differentials */
+#endif
   esd.closure_emission_background = mk3(0.0f, 0.0f, 0.0f);
   esd.closure_transparent_extinction = mk3(0.0f, 0.0f, 0.0f);
   esd.svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);
@@ -1238,7 +1330,8 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
             sray.t = st;
             if (KD->integrator.transparent_shadows) {
               cfloat3 attenuation;
-              const bool blocked = shadow_blocked_transparent<false>(kg, sray, state, mem, &attenuation, err);
+              const bool blocked = shadow_blocked_transparent<false>(kg, sray, state, mem, &attenuation, err,
+                                                                      nullptr, kg->use_ray_diff ? &sd->dP : nullptr);
               *shadow = true;
               if (!blocked) {
                 const cfloat3 shaded = mul3(mul3f(throughput, 1.0f), attenuation);
@@ -1272,6 +1365,12 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
             const uint packed = (uint)state->bounce | ((uint)state->transparent_bounce << 8) |
                                 ((uint)state->diffuse_bounce << 16) | ((uint)state->glossy_bounce << 24);
             cy_st(&b->shadow_T[slot], mkf4(throughput.x, throughput.y, throughput.z, as_float(packed)));
+#if CY_CLOSURE_EXT
+            if (kg->use_ray_diff) {
+              cy_st(&b->shadow_dP[2 * (size_t)slot], mkf4(sd->dP.dx.x, sd->dP.dx.y, sd->dP.dx.z, sd->dP.dy.x));
+              cy_st(&b->shadow_dP[2 * (size_t)slot + 1], mkf4(sd->dP.dy.y, sd->dP.dy.z, 0.0f, 0.0f));
+            }
+#endif
           }
           else {
             cy_st(&b->shadow_D[slot], mkf4(sD.x, sD.y, sD.z, 0.0f));
@@ -1295,7 +1394,7 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
  * closure at a subsurface exit point (no volumes: disk BSSRDFs are refused in
  * volume scenes). */
 CY_FN bool subsurface_exit_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *throughput, CyPathState *state,
-                                  CyRay *ray, uint *err)
+                                  CyRay *ray, uint *err, CyDiff3 *domega_in = nullptr)
 {
   if (!(sd->flag & SD_BSDF)) {
     return false;
@@ -1305,7 +1404,7 @@ CY_FN bool subsurface_exit_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *
   cfloat3 bsdf_eval_v = mk3(0.0f, 0.0f, 0.0f);
   cfloat3 omega_in = mk3(0.0f, 0.0f, 0.0f);
   float bsdf_pdf = 0.0f;
-  const int label = shader_bsdf_sample(kg, sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err);
+  const int label = shader_bsdf_sample(kg, sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err, domega_in);
   if (bsdf_pdf == 0.0f || is_zero3(bsdf_eval_v)) {
     return false;
   }
@@ -1355,6 +1454,10 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
   CyPathState top_state;
   CyRay top_ray;
   cfloat3 top_tp = mk3(0.0f, 0.0f, 0.0f);
+  /* with ray differentials each indirect ray carries the entry point's dP
+   * (shader_setup_from_subsurface keeps sd->dP, dI) and its sampled dD */
+  const bool diff = kg->use_ray_diff != 0;
+  CyDiff3 top_dD, hit_dD;
   for (int hit = 0; hit < num_hits; hit++) {
     /* subsurface_scatter_multi_setup (kernel_subsurface.h:284-313) */
     shader_setup_from_subsurface(kg, sd, &li.hits[hit], &ss_ray);
@@ -1375,15 +1478,16 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
     CyRay hit_ray = *ray;
     cfloat3 hit_tp = *throughput;
     hit_state.rng_offset += PRNG_BOUNCE_NUM;
-    if (subsurface_exit_bounce(kg, sd, &hit_tp, &hit_state, &hit_ray, err)) {
+    if (subsurface_exit_bounce(kg, sd, &hit_tp, &hit_state, &hit_ray, err, diff ? &hit_dD : nullptr)) {
       hit_state.ray_t = 0.0f;
       if (pushed > 0) {
         top_state.rng_offset += (pushed - 1) * PRNG_BOUNCE_NUM;
-        sss_rec_store(b, slot, pushed - 1, &top_state, &top_ray, top_tp);
+        sss_rec_store(b, slot, pushed - 1, &top_state, &top_ray, top_tp, diff ? &sd->dP : nullptr, &top_dD);
       }
       top_state = hit_state;
       top_ray = hit_ray;
       top_tp = hit_tp;
+      top_dD = hit_dD;
       pushed++;
     }
   }
@@ -1392,6 +1496,9 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
     *state = top_state;
     *ray = top_ray;
     *throughput = top_tp;
+    if (diff) {
+      diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, sd->dP, top_dD);
+    }
     if (pushed > 1) {
       cy_st(&b->sss_count[slot], (uint)(pushed - 1));
     }
@@ -1638,6 +1745,16 @@ CY_FN bool shade_path(const CyGlobals *kg,
         shadow_rng_offset = state.rng_offset;
         if (volume_bounce(kg, &vsd, &throughput, &state, &ray)) {
           cont = true;
+          if (kg->use_ray_diff) {
+            /* kernel_path_volume.h:123-124: dP = the volume point's dP (the
+             * segment ray's dD, shader_setup_from_volume), dD = the phase
+             * sample's (zero, volume.h:146-147) */
+            CyDiff3 rdP, rdD;
+            ray_diff_load(kg, b, tile, slot, cam_item, &rdP, &rdD);
+            CyDiff3 zero;
+            zero.dx = zero.dy = mk3(0.0f, 0.0f, 0.0f);
+            diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, rdD, zero);
+          }
         }
       }
     }
@@ -1680,8 +1797,18 @@ CY_FN bool shade_path(const CyGlobals *kg,
           /* world shader evaluated along the ray, bounce raised for the
            * light-path node (path_state_modify_bounce) */
 #if CY_SVM_TEX
+#if CY_CLOSURE_EXT
+          CyDiff3 rdP, rdD;
+          if (kg->use_ray_diff) {
+            ray_diff_load(kg, b, tile, slot, cam_item, &rdP, &rdD);
+          }
+          L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray.D,
+                                             mem, state, state.flag | PATH_RAY_EMISSION, err,
+                                             kg->use_ray_diff ? &rdD : nullptr);
+#else
           L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray.D,
                                              mem, state, state.flag | PATH_RAY_EMISSION, err);
+#endif
 #else
           cy_set_error(err, CY_ERR_FEATURE, 3); /* node world in the kernel without texture nodes */
 #endif
@@ -1714,7 +1841,15 @@ CY_FN bool shade_path(const CyGlobals *kg,
     sd.svm_stride = mem.svm_stride;
     sd.svm_fast = mem.svm_fast;
     sd.svm_spill = mem.svm_spill;
+#if CY_CLOSURE_EXT
+    CyDiff3 rdP, rdD;
+    if (kg->use_ray_diff) {
+      ray_diff_load(kg, b, tile, slot, cam_item, &rdP, &rdD);
+    }
+    shader_setup_from_ray(kg, &sd, &isect, &ray, kg->use_ray_diff ? &rdP : nullptr, &rdD);
+#else
     shader_setup_from_ray(kg, &sd, &isect, &ray);
+#endif
 #if CY_CLOSURE_EXT
     if (VOL && (sd.flag & SD_HAS_ONLY_VOLUME)) {
       /* volume bounding surface: pass through without a bounce
@@ -1731,6 +1866,10 @@ CY_FN bool shade_path(const CyGlobals *kg,
           ray.t = CY_FLT_MAX;
         }
         ray.P = ray_offset(sd.P, neg3(sd.Ng));
+        if (kg->use_ray_diff) {
+          /* kernel_path_surface.h:346: dP transferred, dD kept */
+          diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, sd.dP, rdD);
+        }
         vop_object = (uint)sd.object;
         vop_shader = (uint)sd.shader;
         vop_flags = CY_VOP_PATH | ((sd.flag & SD_BACKFACING) ? CY_VOP_BACKFACING : 0u);
@@ -1912,7 +2051,13 @@ CY_FN bool shade_path(const CyGlobals *kg,
         cfloat3 bsdf_eval_v = mk3(0.0f, 0.0f, 0.0f);
         cfloat3 omega_in = mk3(0.0f, 0.0f, 0.0f);
         float bsdf_pdf = 0.0f;
+#if CY_CLOSURE_EXT
+        CyDiff3 domega;
+        int label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err,
+                                       kg->use_ray_diff ? &domega : nullptr);
+#else
         int label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err);
+#endif
         if (!(bsdf_pdf == 0.0f || is_zero3(bsdf_eval_v))) {
           float inverse_pdf = 1.0f / bsdf_pdf;
           throughput = mul3(throughput, mul3f(bsdf_eval_v, inverse_pdf));
@@ -1932,6 +2077,10 @@ CY_FN bool shade_path(const CyGlobals *kg,
           }
           cont = true;
 #if CY_CLOSURE_EXT
+          if (kg->use_ray_diff) {
+            /* kernel_path_surface.h:321-322 */
+            diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, sd.dP, domega);
+          }
           if (VOL && (label & LABEL_TRANSMIT) && (sd.flag & SD_HAS_VOLUME)) {
             /* enter/exit the surface's volume (kernel_path_surface.h:325-329) */
             vop_object = (uint)sd.object;
@@ -1954,7 +2103,14 @@ CY_FN bool shade_path(const CyGlobals *kg,
      * (kernel_path_subsurface_setup_indirect), if any */
     const int pending = (sss_disk_rays == 0 || cam_item != CY_NO_ITEM) ? 0 : (int)cy_ld(&b->sss_count[slot]);
     if (pending > 0) {
-      sss_rec_load(b, slot, pending - 1, kg, &state, &ray, &throughput);
+      if (kg->use_ray_diff) {
+        CyDiff3 pdP, pdD;
+        sss_rec_load(b, slot, pending - 1, kg, &state, &ray, &throughput, &pdP, &pdD);
+        diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, pdP, pdD);
+      }
+      else {
+        sss_rec_load(b, slot, pending - 1, kg, &state, &ray, &throughput);
+      }
       cy_st(&b->sss_count[slot], (uint)(pending - 1));
       cont = true;
     }

@@ -246,8 +246,8 @@ CY_FN cfloat3 panorama_to_direction(const CyGlobals *kg, float u, float v)
   }
 }
 
-CY_FN void camera_sample_ray(
-    const CyGlobals *kg, int x, int y, int sample, uint *rng_hash_out, CyRay *ray)
+CY_FN void camera_sample_ray(const CyGlobals *kg, int x, int y, int sample, uint *rng_hash_out, CyRay *ray,
+                             CyDiff3 *dP = nullptr, CyDiff3 *dD = nullptr)
 {
   /* path_rng_init (kernel_random.h:129-153) */
   uint rng_hash = hash_uint2((uint)x, (uint)y);
@@ -292,10 +292,24 @@ CY_FN void camera_sample_ray(
     D = normalize3(transform_direction(cameratoworld, D));
     ray->P = P;
     ray->D = D;
+    if (dP) {
+      /* kernel_camera.h:114-120 */
+      const cfloat3 Dcenter = transform_direction(cameratoworld, Pcamera);
+      const cfloat3 cdx = mk3(KD->cam.dx.x, KD->cam.dx.y, KD->cam.dx.z);
+      const cfloat3 cdy = mk3(KD->cam.dy.x, KD->cam.dy.y, KD->cam.dy.z);
+      dP->dx = mk3(0.0f, 0.0f, 0.0f);
+      dP->dy = mk3(0.0f, 0.0f, 0.0f);
+      dD->dx = sub3(normalize3(add3(Dcenter, cdx)), normalize3(Dcenter));
+      dD->dy = sub3(normalize3(add3(Dcenter, cdy)), normalize3(Dcenter));
+    }
     /* camera clipping (__CAMERA_CLIPPING__) */
     const float z_inv = 1.0f / normalize3(Pcamera).z;
     const float nearclip = KD->cam.nearclip * z_inv;
     ray->P = add3(ray->P, mul3f(ray->D, nearclip));
+    if (dP) {
+      dP->dx = add3(dP->dx, mul3f(dD->dx, nearclip));
+      dP->dy = add3(dP->dy, mul3f(dD->dy, nearclip));
+    }
     ray->t = KD->cam.cliplength * z_inv;
   }
   else if (type == 1) {
@@ -315,6 +329,13 @@ CY_FN void camera_sample_ray(
     }
     ray->P = transform_point(cameratoworld, P);
     ray->D = normalize3(transform_direction(cameratoworld, D));
+    if (dP) {
+      /* kernel_camera.h:221-227 */
+      dP->dx = mk3(KD->cam.dx.x, KD->cam.dx.y, KD->cam.dx.z);
+      dP->dy = mk3(KD->cam.dy.x, KD->cam.dy.y, KD->cam.dy.z);
+      dD->dx = mk3(0.0f, 0.0f, 0.0f);
+      dD->dy = mk3(0.0f, 0.0f, 0.0f);
+    }
     ray->t = KD->cam.cliplength;
   }
   else {
@@ -342,8 +363,29 @@ CY_FN void camera_sample_ray(
     D = normalize3(transform_direction(cameratoworld, D));
     ray->P = P;
     ray->D = D;
+    if (dP) {
+      /* kernel_camera.h:305-339: the centre and the two neighbouring pixels'
+       * rays (without depth of field) */
+      const cfloat3 Pcenter = transform_point(cameratoworld, Pcamera);
+      const cfloat3 Dcenter =
+          normalize3(transform_direction(cameratoworld, panorama_to_direction(kg, Pcamera.x, Pcamera.y)));
+      const cfloat3 Px0 = transform_perspective(rastertocamera, mk3(raster_x + 1.0f, raster_y, 0.0f));
+      const cfloat3 Dx = normalize3(transform_direction(cameratoworld, panorama_to_direction(kg, Px0.x, Px0.y)));
+      const cfloat3 Px = transform_point(cameratoworld, Px0);
+      dP->dx = sub3(Px, Pcenter);
+      dD->dx = sub3(Dx, Dcenter);
+      const cfloat3 Py0 = transform_perspective(rastertocamera, mk3(raster_x, raster_y + 1.0f, 0.0f));
+      const cfloat3 Dy = normalize3(transform_direction(cameratoworld, panorama_to_direction(kg, Py0.x, Py0.y)));
+      const cfloat3 Py = transform_point(cameratoworld, Py0);
+      dP->dy = sub3(Py, Pcenter);
+      dD->dy = sub3(Dy, Dcenter);
+    }
     const float nearclip = KD->cam.nearclip;
     ray->P = add3(ray->P, mul3f(ray->D, nearclip));
+    if (dP) {
+      dP->dx = add3(dP->dx, mul3f(dD->dx, nearclip));
+      dP->dy = add3(dP->dy, mul3f(dD->dy, nearclip));
+    }
     ray->t = KD->cam.cliplength;
   }
 }
@@ -1058,7 +1100,54 @@ CY_FN cfloat3 object_normal_transform(const CyGlobals *kg, int object, cfloat3 N
 /* kernel_shader.h:54-153 (static triangles and curves, instanced or not; no
  * differentials: the differentials only feed texture filtering, which this
  * node subset lacks). */
-CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *isect, const CyRay *ray)
+#if CY_CLOSURE_EXT
+/* kernel_differential.h: the ray differential transferred to the hit plane,
+ * the incoming direction's, and the barycentric u / v differentials */
+CY_FN void differential_transfer(CyDiff3 *dP_, const CyDiff3 &dP, cfloat3 D, const CyDiff3 &dD, cfloat3 Ng, float t)
+{
+  const cfloat3 tmp = div3f(D, dot3(D, Ng));
+  const cfloat3 tmpx = add3(dP.dx, mul3f(dD.dx, t));
+  const cfloat3 tmpy = add3(dP.dy, mul3f(dD.dy, t));
+  dP_->dx = sub3(tmpx, mul3f(tmp, dot3(tmpx, Ng)));
+  dP_->dy = sub3(tmpy, mul3f(tmp, dot3(tmpy, Ng)));
+}
+
+CY_FN void differential_dudv(CyDiff *du, CyDiff *dv, cfloat3 dPdu, cfloat3 dPdv, CyDiff3 dP, cfloat3 Ng)
+{
+  const float xn = fabsf(Ng.x);
+  const float yn = fabsf(Ng.y);
+  const float zn = fabsf(Ng.z);
+  if (zn < xn || zn < yn) {
+    if (yn < xn || yn < zn) {
+      dPdu.x = dPdu.y;
+      dPdv.x = dPdv.y;
+      dP.dx.x = dP.dx.y;
+      dP.dy.x = dP.dy.y;
+    }
+    dPdu.y = dPdu.z;
+    dPdv.y = dPdv.z;
+    dP.dx.y = dP.dx.z;
+    dP.dy.y = dP.dy.z;
+  }
+  float det = (dPdu.x * dPdv.y - dPdv.x * dPdu.y);
+  if (det != 0.0f) {
+    det = 1.0f / det;
+  }
+  du->dx = (dP.dx.x * dPdv.y - dP.dx.y * dPdv.x) * det;
+  dv->dx = (dP.dx.y * dPdu.x - dP.dx.x * dPdu.y) * det;
+  du->dy = (dP.dy.x * dPdv.y - dP.dy.y * dPdv.x) * det;
+  dv->dy = (dP.dy.y * dPdu.x - dP.dy.x * dPdu.y) * det;
+}
+
+CY_FN void sd_zero_differentials(CySD *sd)
+{
+  sd->dP.dx = sd->dP.dy = sd->dI.dx = sd->dI.dy = mk3(0.0f, 0.0f, 0.0f);
+  sd->du.dx = sd->du.dy = sd->dv.dx = sd->dv.dy = 0.0f;
+}
+#endif
+
+CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *isect, const CyRay *ray,
+                                 const CyDiff3 *ray_dP = nullptr, const CyDiff3 *ray_dD = nullptr)
 {
   sd->object = (isect->object == OBJECT_NONE) ? (int)kg->__prim_object[isect->prim] : isect->object;
   sd->type = isect->type;
@@ -1107,6 +1196,18 @@ CY_FN void shader_setup_from_ray(const CyGlobals *kg, CySD *sd, const CyIsect *i
     sd->dPdv = neg3(sd->dPdv);
 #endif
   }
+#if CY_CLOSURE_EXT
+  if (ray_dP) {
+    /* kernel_shader.h:145-149 */
+    differential_transfer(&sd->dP, *ray_dP, ray->D, *ray_dD, sd->Ng, isect->t);
+    sd->dI.dx = neg3(ray_dD->dx);
+    sd->dI.dy = neg3(ray_dD->dy);
+    differential_dudv(&sd->du, &sd->dv, sd->dPdu, sd->dPdv, sd->dP, sd->Ng);
+  }
+  else {
+    sd_zero_differentials(sd);
+  }
+#endif
 }
 
 /* ---------------------------------------------------------------------------
@@ -2442,6 +2543,14 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         break;
       }
 #if CY_SVM_TEX
+      /* svm_closure.h:1188-1194: the bump program's normal becomes the
+       * shading normal (displacement method "bump") */
+      case NODE_CLOSURE_SET_NORMAL: {
+        const cfloat3 normal = svm_load3(stack, node.y, err);
+        sd->N = normal;
+        svm_store3(stack, node.z, normal, err);
+        break;
+      }
       /* svm_displace.h:86-167 (displacement programs, SHADER_EVAL_DISPLACE) */
       case NODE_SET_DISPLACEMENT:
         sd->P = add3(sd->P, svm_load3(stack, node.y, err));
@@ -2494,8 +2603,41 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         return;
 #else
       {
+#if CY_CLOSURE_EXT
+        /* the bump forms (svm.h:298-345) read their centre node at
+         * P + dP.dx (.dy), u + du.dx, v + dv.dx (svm_geometry.h:54-100,
+         * svm_tex_coord.h:97-255), attributes plus their derivative
+         * (svm_attribute.h:92-188, svm_vertex_color.h:38-90) */
+        int bump = 0;
+        switch (node.x) {
+          case NODE_GEOMETRY_BUMP_DX:
+          case NODE_GEOMETRY_BUMP_DY:
+            bump = (node.x == NODE_GEOMETRY_BUMP_DX) ? 1 : 2;
+            node.x = NODE_GEOMETRY;
+            break;
+          case NODE_ATTR_BUMP_DX:
+          case NODE_ATTR_BUMP_DY:
+            bump = (node.x == NODE_ATTR_BUMP_DX) ? 1 : 2;
+            node.x = NODE_ATTR;
+            break;
+          case NODE_VERTEX_COLOR_BUMP_DX:
+          case NODE_VERTEX_COLOR_BUMP_DY:
+            bump = (node.x == NODE_VERTEX_COLOR_BUMP_DX) ? 1 : 2;
+            node.x = NODE_VERTEX_COLOR;
+            break;
+          case NODE_TEX_COORD_BUMP_DX:
+          case NODE_TEX_COORD_BUMP_DY:
+            bump = (node.x == NODE_TEX_COORD_BUMP_DX) ? 1 : 2;
+            node.x = NODE_TEX_COORD;
+            break;
+        }
+#endif
         if (node.x == NODE_ATTR || node.x == NODE_VERTEX_COLOR || node.x == NODE_NORMAL_MAP ||
-            node.x == NODE_TANGENT || node.x == NODE_OBJECT_INFO || (node.x == NODE_GEOMETRY && node.y == 2u)) {
+            node.x == NODE_TANGENT || node.x == NODE_OBJECT_INFO || (node.x == NODE_GEOMETRY && node.y == 2u)
+#if CY_CLOSURE_EXT
+            || node.x == NODE_SET_BUMP
+#endif
+        ) {
           CyAttrIn ain;
           ain.P = sd->P;
           ain.N = sd->N;
@@ -2510,6 +2652,11 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
           ain.shader = sd->shader;
 #if CY_CLOSURE_EXT
           ain.dPdu = sd->dPdu;
+          ain.dPdx = sd->dP.dx;
+          ain.dPdy = sd->dP.dy;
+          ain.bump = bump;
+          ain.bump_du = (bump == 2) ? sd->du.dy : sd->du.dx;
+          ain.bump_dv = (bump == 2) ? sd->dv.dy : sd->dv.dx;
 #endif
           svm_eval_attribute_node(kg->__objects, kg->__shaders, kg->__attributes_map, kg->__attributes_float,
                                   kg->__attributes_float2, kg->__attributes_float3, kg->__attributes_uchar4,
@@ -2531,6 +2678,14 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         in.glossy_bounce = state ? state->glossy_bounce : 0;
         in.transparent_bounce = state ? state->transparent_bounce : 0;
         in.transmission_bounce = state ? state->transmission_bounce : 0;
+#if CY_CLOSURE_EXT
+        if (bump) {
+          /* only the position-based outputs read P, u, v */
+          in.P = add3(sd->P, (bump == 2) ? sd->dP.dy : sd->dP.dx);
+          in.u = sd->u + ((bump == 2) ? sd->du.dy : sd->du.dx);
+          in.v = sd->v + ((bump == 2) ? sd->dv.dy : sd->dv.dx);
+        }
+#endif
         offset = svm_eval_texture_node(kg->data, kg->__svm_nodes, kg->__objects, kg->__texture_info, in, stack, node,
                                        path_flag, offset, err);
         if (offset < 0) {
@@ -2621,6 +2776,7 @@ CY_FN cfloat3 displace_evaluate(const CyGlobals *kg, int object, int prim, float
     sd.dPdu = transform_direction(object_tfm(kg, object), sd.dPdu);
     sd.dPdv = transform_direction(object_tfm(kg, object), sd.dPdv);
   }
+  sd_zero_differentials(&sd); /* shader_setup_from_sample: no ray differentials */
 #endif
   /* backfacing test: dot(Ng, I) with I = 0 is never negative */
   sd.num_closure = 0;
@@ -2716,7 +2872,8 @@ CY_FN int shader_bsdf_sample(const CyGlobals *kg,
                              cfloat3 *bsdf_eval_out,
                              cfloat3 *omega_in,
                              float *pdf,
-                             uint *err)
+                             uint *err,
+                             CyDiff3 *domega_in = nullptr)
 {
   int sci = shader_bsdf_pick(sd, &randu);
   if (sci < 0) {
@@ -2727,7 +2884,19 @@ CY_FN int shader_bsdf_sample(const CyGlobals *kg,
   int label;
   cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
   *pdf = 0.0f;
-  label = bsdf_sample(kg, sd, sc, randu, randv, &eval, omega_in, pdf, err);
+#if CY_CLOSURE_EXT
+  if (domega_in) {
+    CyDiffRule rule;
+    rule.kind = CY_DIFF_ZERO;
+    label = bsdf_sample(kg, sd, sc, randu, randv, &eval, omega_in, pdf, err, &rule);
+    domega_in->dx = diff_rule_apply(rule, sd->dI.dx);
+    domega_in->dy = diff_rule_apply(rule, sd->dI.dy);
+  }
+  else
+#endif
+  {
+    label = bsdf_sample(kg, sd, sc, randu, randv, &eval, omega_in, pdf, err);
+  }
   if (*pdf != 0.0f) {
     *bsdf_eval_out = mul3(eval, sc->weight);
     if (sd->num_closure > 1) {

@@ -371,6 +371,10 @@ CY_FN void shader_setup_from_subsurface(const CyGlobals *kg, CySD *sd, const CyI
     sd->dPdv = neg3(sd->dPdv);
   }
   sd->I = sd->N;
+  if (kg->use_ray_diff) {
+    /* kernel_shader.h:232-236: new du / dv from the entry's dP (dP, dI kept) */
+    differential_dudv(&sd->du, &sd->dv, sd->dPdu, sd->dPdv, sd->dP, sd->Ng);
+  }
 }
 
 /* subsurface_scatter_setup_diffuse_bsdf: the closures are replaced by one

@@ -5,8 +5,7 @@
  *
  * Every libm call of these nodes is glibc's algorithm (cy_math.h: sinf, cosf,
  * powf, expf, logf, asinf, acosf, atanf, atan2f), so the device agrees with the
- * reference CPU kernel bit for bit.  Math operations that need a libm function
- * not restated here (tan, sinh, cosh, tanh) raise CY_ERR_SVM_NODE.
+ * reference CPU kernel bit for bit (tan, sinh, cosh, tanh and expm1 too).
  */
 #ifndef CY_SVM_NODES_H
 #define CY_SVM_NODES_H
@@ -16,6 +15,15 @@ enum {
   NODE_GEOMETRY = 11,
   NODE_CONVERT = 12,
   NODE_TEX_COORD = 13,
+  NODE_GEOMETRY_BUMP_DX = 18,
+  NODE_GEOMETRY_BUMP_DY = 19,
+  NODE_ATTR_BUMP_DX = 27,
+  NODE_ATTR_BUMP_DY = 28,
+  NODE_VERTEX_COLOR_BUMP_DX = 29,
+  NODE_VERTEX_COLOR_BUMP_DY = 30,
+  NODE_TEX_COORD_BUMP_DX = 31,
+  NODE_TEX_COORD_BUMP_DY = 32,
+  NODE_CLOSURE_SET_NORMAL = 33,
   NODE_HSV = 36,
   NODE_MATH = 42,
   NODE_VECTOR_MATH = 43,

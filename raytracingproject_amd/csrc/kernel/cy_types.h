@@ -313,6 +313,14 @@ typedef struct CyRay {
   float t;
 } CyRay;
 
+/* ray differentials (kernel_types.h differential3 / differential) */
+typedef struct CyDiff3 {
+  cfloat3 dx, dy;
+} CyDiff3;
+typedef struct CyDiff {
+  float dx, dy;
+} CyDiff;
+
 typedef struct CyIsect {
   float t, u, v;
   int prim;
@@ -372,6 +380,10 @@ typedef struct CySD {
   mutable uint lcg_state;
   /* surface derivatives (__DPDU__): hair closures, the Tangent node fallback */
   cfloat3 dPdu, dPdv;
+  /* ray differentials at the shading point (__RAY_DIFFERENTIALS__): the Bump
+   * node and the *_BUMP_DX / _DY nodes; zero unless CyGlobals.use_ray_diff */
+  CyDiff3 dP, dI;
+  CyDiff du, dv;
 #endif
 } CySD;
 

@@ -142,6 +142,13 @@ CY_FN void shader_setup_from_volume(CySD *sd, const CyRay *ray, CyShadeMem mem)
   sd->type = 0; /* PRIMITIVE_NONE */
   sd->u = 0.0f;
   sd->v = 0.0f;
+#if CY_CLOSURE_EXT
+  sd->dPdu = mk3(0.0f, 0.0f, 0.0f);
+  sd->dPdv = mk3(0.0f, 0.0f, 0.0f);
+  /* the reference's dP here is the segment ray's dD (kernel_shader.h:474-479),
+   * read by no node a volume program runs: zero */
+  sd_zero_differentials(sd);
+#endif
   sd->num_closure = 0;
   sd->num_closure_left = 0;
   sd->svm_closure_weight = mk3(0.0f, 0.0f, 0.0f);

@@ -135,6 +135,12 @@ class HIPDevice:
         second = 2 * first if second is None else second
         self._check(self.lib.hipcy_set_traversal_budget(self.h, int(first), int(second)))
 
+    def set_traversal_refill(self, rounds: int, min_idle: int = 16) -> None:
+        """Lane refill of the closest-hit traversal (hipcy_set_traversal_refill):
+        persistent waves traversing `rounds` iterations at a time, refilled with
+        new rays once `min_idle` lanes are idle.  0 disables."""
+        self._check(self.lib.hipcy_set_traversal_refill(self.h, int(rounds), int(min_idle)))
+
     def set_slots(self, slots: int = 0, record_bytes: int = 0) -> None:
         """Path slots in flight and the per-pass sample-record budget (0 keeps a value)."""
         self._check(self.lib.hipcy_set_slots(self.h, int(slots), int(record_bytes)))

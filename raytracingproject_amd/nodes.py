@@ -66,6 +66,7 @@ NODE_GEOMETRY_BUMP_DX, NODE_GEOMETRY_BUMP_DY = 18, 19
 NODE_SET_BUMP, NODE_ATTR_BUMP_DX, NODE_ATTR_BUMP_DY = 26, 27, 28
 NODE_VERTEX_COLOR_BUMP_DX, NODE_VERTEX_COLOR_BUMP_DY = 29, 30
 NODE_TEX_COORD_BUMP_DX, NODE_TEX_COORD_BUMP_DY = 31, 32
+NODE_CLOSURE_SET_NORMAL = 33
 NODE_OBJECT_INFO, NODE_TANGENT, NODE_NORMAL_MAP = 48, 70, 71
 NODE_FRESNEL, NODE_LAYER_WEIGHT = 38, 39
 NODE_CAMERA, NODE_NORMAL, NODE_RGB_CURVES, NODE_VECTOR_CURVES = 54, 65, 68, 69
@@ -556,6 +557,24 @@ def bump(height=1.0, strength=1.0, distance=0.1, invert=False, normal=None, obje
     return Node("bump", inputs, {"invert": bool(invert), "object_space": bool(object_space)})["Normal"]
 
 
+def bump_from_displacement(disp: Socket, object_space: bool = False) -> Socket:
+    """ShaderGraph::bump_from_displacement (graph.cpp:956-1050), the
+    displacement method "bump": three copies of the displacement graph (centre,
+    dx, dy), each projected on the Geometry normal by a dot product, feed a
+    Bump node (distance 1) whose normal a Set Normal node makes the shading
+    normal.  Compiled as the shader's bump program, which falls through into
+    its surface program (svm.cpp:864-880)."""
+    geom_n = geometry()["Normal"]
+
+    def height(v):
+        return vector_math("dot_product", v, geom_n)["Value"]
+
+    b = Node("bump", {"Strength": 1.0, "Distance": 1.0, "SampleCenter": height(disp),
+                      "SampleX": height(_bump_copy(disp, "dx", {})), "SampleY": height(_bump_copy(disp, "dy", {}))},
+             {"invert": False, "object_space": bool(object_space)})["Normal"]
+    return Node("set_normal", {"Direction": b})["Normal"]
+
+
 def displacement(height, midlevel=0.5, scale=1.0, normal=None, space: str = "object") -> Socket:
     """Displacement node (nodes.cpp:6905-6952): (height - midlevel) * scale along
     the normal (sd->N when unlinked), in object or world space."""
@@ -638,7 +657,7 @@ def _outputs(node: Node) -> dict:
         return {"Color": "color", "Alpha": "float"}
     if k in ("displacement", "vector_displacement"):
         return {"Displacement": "vector"}
-    if k == "bump":
+    if k in ("bump", "set_normal"):
         return {"Normal": "vector"}
     raise ValueError(f"unknown node kind {k!r}")
 
@@ -691,6 +710,7 @@ _INPUT_TYPES = {
     "vector_displacement": {"Vector": "color", "Midlevel": "float", "Scale": "float"},
     "bump": {"SampleCenter": "float", "SampleX": "float", "SampleY": "float", "Normal": "vector",
              "Strength": "float", "Distance": "float"},
+    "set_normal": {"Direction": "vector"},
 }
 
 
@@ -1008,6 +1028,9 @@ class NodeCompiler:
         strength = self.inp(n, "Strength")
         self.emit((NODE_SET_BUMP, uchar4(nrm, dist, int(n.params["invert"]), int(n.params["object_space"])),
                    uchar4(c, x, y, strength), self.out(n, "Normal")))
+
+    def _n_set_normal(self, n):  # nodes.cpp SetNormalNode::compile
+        self.emit((NODE_CLOSURE_SET_NORMAL, self.inp(n, "Direction"), self.out(n, "Normal"), 0))
 
     def _n_light_path(self, n):  # nodes.cpp LightPathNode::compile
         for t, name in enumerate(LIGHT_PATH_OUTPUTS):

@@ -123,6 +123,7 @@ BECKMANN_CLOSURES = (CLOSURE_BSDF_MICROFACET_BECKMANN_ID, CLOSURE_BSDF_MICROFACE
 SD_HAS_TRANSPARENT_SHADOW = 1 << 17
 SD_HAS_DISPLACEMENT = 1 << 26
 SD_HAS_BSSRDF_BUMP = 1 << 21
+SD_HAS_BUMP = 1 << 25
 # volumes (kernel_types.h:832-931, svm_types.h:577-579, 105-106)
 SD_HAS_VOLUME = 1 << 18
 SD_HAS_ONLY_VOLUME = 1 << 19
@@ -174,9 +175,14 @@ class Closure:
     sharpness: object = 0.0
     texture_blur: object = 0.0
     subsurface_method: str = "burley"  # principled
-    # material output "Displacement" (a vector socket, e.g. nodes.displacement),
-    # displacement method "true": its own SVM program, run by SHADER_EVAL_DISPLACE
+    # material output "Displacement" (a vector socket, e.g. nodes.displacement)
+    # and the material's displacement method (shader.cpp:184-188): "true" (its
+    # own SVM program, run by SHADER_EVAL_DISPLACE) or "bump" (a bump program
+    # from the displacement graph ahead of the surface program, through ray
+    # differentials; Blender's default).  "both" needs the mesh displaced with
+    # its undisplaced positions kept (ATTR_STD_POSITION_UNDISPLACED): refused.
     displacement: object = None
+    displacement_method: str = "true"
     # material output "Volume": a tree of volume closures (volume_absorption,
     # volume_scatter, principled_volume, emission, mix), its own SVM program
     volume: "Closure | None" = None
@@ -764,6 +770,15 @@ class SVMCompiler:
             self.stack_used = [False] * SVM_STACK_SIZE
             start = len(self.nodes)
             self.nodes[i] = (NODE_SHADER_JUMP, start, 0, 0)
+            if _has_bump(sh):
+                # the bump program (svm.cpp:864-868, compile_type SHADER_TYPE_BUMP:
+                # the graph feeding the output's Normal, no NODE_END) falls
+                # through into the surface program
+                setn = nodes.bump_from_displacement(sh.displacement)
+                self.nc = self._node_compiler([setn], background=False)
+                self.nc.link(setn, "vector")
+                self.stack_top = 0
+                self.stack_used = [False] * SVM_STACK_SIZE
             socks = sh.sockets()
             self.nc = self._node_compiler([v for v, _ in socks], background=sh is world)
             for v, t in socks:
@@ -967,6 +982,20 @@ def _has_displacement(m) -> bool:
     return nodes.is_linked(getattr(m, "displacement", None))
 
 
+def _displacement_method(m) -> str:
+    method = getattr(m, "displacement_method", "true")
+    if method not in ("true", "bump"):
+        raise ValueError(f"displacement_method {method!r}: true or bump ('both' needs displaced meshes)")
+    return method
+
+
+def _has_bump(m) -> bool:
+    """svm.cpp:836-837 has_bump: bump displacement with both the surface and
+    the displacement outputs linked."""
+    return (m is not None and _has_displacement(m) and _displacement_method(m) == "bump"
+            and m.kind not in ("none", "background"))
+
+
 def _has_bssrdf_bump(m) -> bool:
     """Shader::has_bssrdf_bump (svm.cpp:515-521, 855): a BSSRDF node whose
     Normal input is linked to anything but the Geometry node
@@ -975,6 +1004,8 @@ def _has_bssrdf_bump(m) -> bool:
     not expressible here: displacement is always the "true" method."""
     if m is None:
         return False
+    if _has_bump(m):
+        return True  # svm.cpp:855 has_bssrdf_bump = has_bump
 
     def bumped(v):
         return nodes.is_linked(v) and v.node.kind != "geometry"
@@ -1284,8 +1315,10 @@ def compile_scene(scene: Scene) -> DeviceScene:
         if const is not None:
             flag |= SD_HAS_CONSTANT_EMISSION
             kshaders[i].constant_emission[:] = [float(c) for c in const]
-        if _has_displacement(m):
+        if _has_displacement(m) and _displacement_method(m) != "bump":
             flag |= SD_HAS_DISPLACEMENT  # shader.cpp:559-560 (displacement_method true)
+        if _has_bump(m):
+            flag |= SD_HAS_BUMP  # shader.cpp:557-558
         if _has_bssrdf_bump(m):
             flag |= SD_HAS_BSSRDF_BUMP  # shader.cpp:547-548
         if m.volume is not None:

@@ -743,6 +743,105 @@ def bump_cornell(width=48, height=48, samples=8, camera="perspective") -> sc.Sce
     return s
 
 
+def bump_paths(width=40, height=40, samples=8) -> sc.Scene:
+    """Bump nodes on the other branches of a path (golden parity case for the
+    differentials each one carries): a burley BSSRDF with a bumped normal (its
+    exit points' indirect rays keep the entry's dP in the slot records), a
+    pane whose transparency follows the Layer Weight of a bumped normal (shadow
+    rays evaluate it with the shading point's dP), a rough multiscatter glass,
+    a translucent and a velvet sphere, a Beckmann glossy sphere bumped by a UV
+    checker, one bumped by its vertex colours and one through the Object /
+    Camera / Window texture coordinates."""
+    from . import nodes
+
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    tc = nodes.tex_coord()
+    noise = nodes.noise_texture(None, scale=0.05, detail=2.0)["Fac"]
+    uv_checker = nodes.checker(tc["UV"], (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), scale=6.0)["Fac"]
+    vcol = nodes.separate_xyz(nodes.vertex_color("Col")["Color"])["Y"]
+    coords = nodes.math("add", nodes.separate_xyz(tc["Object"])["X"],
+                        nodes.math("add", nodes.separate_xyz(tc["Camera"])["Y"],
+                                   nodes.separate_xyz(tc["Window"])["X"]))
+    wave = nodes.math("sine", nodes.math("multiply", coords, 0.4))
+    pane_bump = nodes.bump(nodes.checker(tc["Object"], (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), scale=0.05)["Fac"],
+                           strength=1.0, distance=4.0)
+    mats = [
+        sc.subsurface((0.8, 0.5, 0.4), scale=40.0, radius=(1.0, 0.5, 0.25),
+                      normal=nodes.bump(noise, strength=1.0, distance=3.0)),
+        sc.glass((0.95, 0.95, 1.0), 0.25, ior=1.4, distribution="multi_ggx",
+                 normal=nodes.bump(noise, strength=0.7, distance=2.0)),
+        sc.translucent((0.7, 0.8, 0.5), normal=nodes.bump(noise, strength=0.8, distance=2.0, invert=True)),
+        sc.velvet((0.8, 0.3, 0.5), sigma=0.6, normal=nodes.bump(vcol, strength=1.0, distance=0.5)),
+        sc.glossy((0.8, 0.8, 0.6), 0.25, distribution="beckmann",
+                  normal=nodes.bump(uv_checker, strength=0.8, distance=0.3)),
+        sc.diffuse((0.6, 0.7, 0.9), normal=nodes.bump(wave, strength=1.0, distance=1.5)),
+    ]
+    s.materials.extend(mats)
+    centers = [(130.0, 110.0, 230.0), (290.0, 100.0, 160.0), (440.0, 110.0, 280.0), (130.0, 330.0, 380.0),
+               (290.0, 320.0, 420.0), (440.0, 330.0, 380.0)]
+    rng = np.random.default_rng(91)
+    for i, c in enumerate(centers):
+        m = sc.Mesh(*_ellipsoid(c, (68.0, 64.0, 68.0), 20, 12), shader=base + i, smooth=i % 2 == 0)
+        nt = len(m.tris)
+        m.uv = rng.uniform(0.0, 1.0, (nt, 3, 2)).astype(np.float32)
+        m.vertex_colors = {"Col": rng.uniform(0.0, 1.0, (nt, 3, 4))}
+        s.meshes.append(m)
+    facing = nodes.layer_weight(0.4, normal=pane_bump)["Facing"]
+    s.materials.append(sc.mix(facing, sc.transparent((1.0, 1.0, 1.0)), sc.diffuse((0.7, 0.7, 0.75))))
+    s.meshes.append(sc.Mesh(*_quad((60.0, 420.0, 100.0), (500.0, 420.0, 100.0), (500.0, 420.0, 500.0),
+                                   (60.0, 420.0, 500.0)), shader=len(s.materials) - 1))
+    s.lamps = [sc.Lamp("point", co=(278.0, 500.0, 280.0), size=20.0, color=(1.0, 0.9, 0.8), strength=2.0e6)]
+    s.name = "bump_paths"
+    return s
+
+
+def bump_displace(width=40, height=40, samples=8) -> sc.Scene:
+    """Displacement method "bump" (Blender's default; golden parity case):
+    graph.cpp bump_from_displacement turns the material's Displacement output
+    into a bump program ahead of the surface program (svm.cpp:864-880) that
+    sets the shading normal — a scalar Displacement of a noise height in
+    object space on a diffuse sphere and on the instanced boxes, a Vector
+    Displacement in world space on a glossy sphere, a world-space Displacement
+    on a Principled BSDF with subsurface (burley: SD_HAS_BSSRDF_BUMP, the exit
+    points re-run the bump program) and a Mix of glass and diffuse."""
+    import dataclasses
+
+    from . import nodes as nd
+
+    s = cornell_instanced(width, height, samples)
+    pos = nd.separate_xyz(nd.geometry()["Position"])
+    noise = nd.noise_texture(None, scale=0.04, detail=2.0)["Fac"]
+    wave = nd.math("sine", nd.math("multiply", pos["X"], 0.09))
+    mats = list(s.materials)
+    # the walls' and instanced boxes' material (object-space transforms in the
+    # bump program) and the host-transformed glossy ellipsoid's
+    mats[0] = dataclasses.replace(mats[0], displacement=nd.displacement(noise, 0.5, 12.0, space="object"),
+                                  displacement_method="bump")
+    mats[-1] = dataclasses.replace(mats[-1], displacement=nd.displacement(wave, 0.5, 5.0, space="object"),
+                                   displacement_method="bump")
+    base = len(mats)
+    mats.extend([
+        dataclasses.replace(sc.diffuse((0.7, 0.6, 0.5)), displacement=nd.displacement(noise, 0.5, 10.0),
+                            displacement_method="bump"),
+        dataclasses.replace(sc.glossy((0.8, 0.8, 0.9), 0.2), displacement=nd.vector_displacement(
+            nd.combine_xyz(wave, nd.math("multiply", noise, 2.0), 0.0), 0.0, 6.0, space="world"),
+            displacement_method="bump"),
+        dataclasses.replace(sc.principled(base_color=(0.85, 0.6, 0.5), subsurface=0.6,
+                                          subsurface_color=(0.9, 0.5, 0.4), subsurface_radius=(20.0, 8.0, 5.0),
+                                          roughness=0.4),
+                            displacement=nd.displacement(wave, 0.5, 6.0, space="world"), displacement_method="bump"),
+        dataclasses.replace(sc.mix(0.4, sc.glass((0.95, 0.95, 1.0), 0.1, ior=1.4), sc.diffuse((0.3, 0.5, 0.8))),
+                            displacement=nd.displacement(noise, 0.3, 8.0), displacement_method="bump"),
+    ])
+    s.materials = mats
+    centers = [(90.0, 70.0, 330.0), (470.0, 70.0, 250.0), (280.0, 430.0, 300.0), (450.0, 400.0, 420.0)]
+    for i, c in enumerate(centers):
+        s.meshes.append(sc.Mesh(*_ellipsoid(c, (62.0, 60.0, 62.0), 20, 12), shader=base + i, smooth=i % 2 == 0))
+    s.name = "bump_displace"
+    return s
+
+
 def sss_disk_cornell(width=48, height=48, samples=8, instanced=False, transparent=False) -> sc.Scene:
     """Cornell box with disk BSSRDFs (golden parity case): Subsurface
     Scattering nodes with the cubic (sharpness 0.5, blurred checker colour),

@@ -81,6 +81,12 @@ CASES = {
     "shading_bump": lambda: scenes.bump_cornell(48, 48, 8),
     "shading_bump_ortho": lambda: scenes.bump_cornell(40, 40, 8, camera="ortho"),
     "shading_bump_equirect": lambda: scenes.bump_cornell(40, 40, 8, camera="equirect"),
+    # differentials on the path's other branches: disk-BSSRDF exit records,
+    # transparent-shadow evaluation, multiscatter glass / translucent / velvet /
+    # Beckmann bounces, attribute / vertex colour / texture coordinate bumps
+    "shading_bump_paths": lambda: scenes.bump_paths(40, 40, 8),
+    # displacement method "bump": the bump program from the Displacement output
+    "shading_bump_displace": lambda: scenes.bump_displace(40, 40, 8),
     "sss_disk": lambda: scenes.sss_disk_cornell(48, 48, 8),
     "sss_disk_instanced": lambda: scenes.sss_disk_cornell(48, 48, 8, instanced=True),
     "sss_disk_transparent": lambda: scenes.sss_disk_cornell(40, 40, 8, transparent=True),

@@ -230,6 +230,33 @@ def test_render_with_traversal_budget_matches_reference(name, width, budget, dev
     assert st["closest_rays"] > 0
 
 
+@pytest.mark.parametrize("refill", [(1, 1), (4, 16), (16, 64)])
+@pytest.mark.parametrize("width", [4, 8])
+@pytest.mark.parametrize("name", ["cornell_64", "bmw_small", "cornell_lamps", "closures_principled",
+                                  "shading_bump_paths", "sss_disk"])
+def test_render_with_lane_refill_matches_reference(name, width, refill, device):
+    """Lane refill (hipcy_set_traversal_refill): persistent closest-hit waves
+    traverse `refill[0]` iterations at a time and hand finished lanes the next
+    rays of the queue once `refill[1]` lanes are idle; camera launches write
+    their rays into the slots first.  Each ray's traversal is split into rounds
+    of the resumable cursor, so the film is bit-identical; (1, 1) refills after
+    every iteration."""
+    if name not in CASES:
+        pytest.skip(f"{name} not a parity case")
+    ds = compile_case(name)
+    g = load_golden(name)
+    device.upload_scene(ds)
+    device.set_bvh_width(width)
+    device.set_traversal_refill(*refill)
+    try:
+        buf = device.render()
+        st = device.stats()
+    finally:
+        device.set_traversal_refill(0, 16)
+    assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), (name, refill)
+    assert st["closest_rays"] > 0
+
+
 @pytest.mark.parametrize("capacity", [1, 97])
 @pytest.mark.parametrize("name", ["cornell_64", "bmw_small"])
 def test_traversal_budget_with_full_continuation_buffer(name, capacity, device, monkeypatch):

@@ -9,6 +9,7 @@
  */
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -288,6 +289,13 @@ extern "C" int emu_render(const void *data,
   uint sss_count = 0;
   b.sss_rec = sss_rec;
   b.sss_count = &sss_count;
+  hc_float4 ray_diff[CY_RAY_DIFF_F4];
+  hc_float4 shadow_dP[2];
+  b.ray_diff = ray_diff;
+  b.shadow_dP = shadow_dP;
+  /* generic: the differentials are always carried on the host (they change
+   * nothing unless a shader reads them) */
+  kg.use_ray_diff = getenv("EMU_NO_RAY_DIFF") ? 0 : 1; /* debugging switch */
   const bool vol = ((const hc_KernelData *)data)->integrator.use_volumes != 0;
   uint err = 0;
   CyTile tile;
