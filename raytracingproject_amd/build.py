@@ -109,8 +109,16 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False):
             jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
                           f"-DCY_SVM_TEX={0 if kind == '' else 1}", f"-DCY_VOLUME={1 if kind == '_vol' else 0}", inc,
                           "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
-    with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
-        list(ex.map(lambda j: _run(j[0]), jobs))
+    # per-object staleness: the traversal file and the shading kernels share
+    # the kernel headers but not each other's source
+    shade_src = os.path.join(dev_dir, "k_shade.hip")
+    def own_deps(obj):
+        other = shade_src if obj.endswith("hipcycles.o") else src
+        return [d for d in deps if d != other]
+
+    jobs_run = jobs if (force or variant) else [j for j in jobs if _stale(j[1], own_deps(j[1]))]
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs_run), os.cpu_count() or 1))) as ex:
+        list(ex.map(lambda j: _run(j[0]), jobs_run))
     _run([HIPCC, "--offload-arch=gfx950", "-fno-gpu-rdc", "-shared", "-fPIC", "-o", out, *[j[1] for j in jobs],
           *shade_objs])
     return out

@@ -683,6 +683,92 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_closest_refill(
   }
 }
 
+/* Stage 3 with lane refill: the opaque any-hit traversals of the shadow queue
+ * in persistent waves (as k_closest_refill); the occlusion goes to the shadow
+ * record's unused w (shadow_D.w, opaque shadows only) and k_shadow_finish then
+ * adds the light, finishes paths and refills slots (its slot claims and queue
+ * pushes synchronise whole workgroups, which a persistent loop cannot). */
+template<bool STATS, int W>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_shadow_refill(CyGlobals kg,
+                                                                CyPathBuffers b,
+                                                                const int *shadow_queue,
+                                                                const uint *shadow_count,
+                                                                uint *claim,
+                                                                uint *err,
+                                                                CyStats *stats,
+                                                                int rounds,
+                                                                int min_idle)
+{
+  const uint n = *shadow_count;
+  __shared__ LdsStack<W, false> lds_stack;
+  CY_LDS CyStackEntry *ring = lds_ring_of(&lds_stack);
+  uint n_nodes = 0, n_leaves = 0, n_tris = 0;
+  uint part = blockIdx.x & 7u, parts_left = 8, next = 0, end = 0;
+  bool busy = false;
+  int slot = 0;
+  CyRay ray;
+  CyIsect isect;
+  CyTravCursor cur;
+  while (true) {
+    const int n_idle = (int)__popcll(__ballot(!busy));
+    if (n_idle >= min_idle || n_idle == 64) {
+      const uint idx = refill_take(n, claim, !busy, &part, &parts_left, &next, &end);
+      if (idx != 0xFFFFFFFFu) {
+        slot = shadow_queue[idx];
+        shadow_load(&b, slot, &ray);
+        isect.t = ray.t;
+        isect.u = 0.0f;
+        isect.v = 0.0f;
+        isect.prim = PRIM_NONE;
+        isect.object = OBJECT_NONE;
+        isect.type = 0;
+        cur.code = 0;
+        cur.code_t = 0.0f;
+        cur.top = 0;
+        cur.n_ring = 0;
+        cur.tie = false;
+        cur.suspended = false;
+        busy = true;
+        if (!scene_intersect_valid(&ray)) {
+          ((float *)&b.shadow_D[slot])[3] = 0.0f;
+          busy = false;
+        }
+      }
+    }
+    if (!__any(busy)) {
+      break;
+    }
+    if (busy) {
+      bvhw_run<W, true>(&kg, &ray, PATH_RAY_SHADOW_OPAQUE, &isect, err, STATS ? &n_nodes : nullptr, &n_leaves,
+                        &n_tris, ring, nullptr, rounds, &cur);
+      if (!cur.suspended) {
+        ((float *)&b.shadow_D[slot])[3] = isect.prim != PRIM_NONE ? 1.0f : 0.0f;
+        busy = false;
+      }
+    }
+  }
+  if (STATS) {
+    stats_block_add(stats + CY_STATS_SHARDS, n_nodes, n_leaves, n_tris, 0);
+  }
+}
+
+__global__ void __launch_bounds__(CY_BLOCK) k_shadow_finish(CyGlobals kg, CyPathBuffers b, CyTile tile,
+                                                            const int *shadow_queue, const uint *shadow_count,
+                                                            int *queue_out, uint *count_out)
+{
+  const int n_active = (int)*shadow_count;
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  bool finished = false;
+  int slot = 0;
+  if (i < n_active) {
+    slot = shadow_queue[i];
+    finished = shadow_finish(&b, &tile, slot, cy_ld(&b.shadow_D[slot]).w != 0.0f);
+  }
+  __shared__ uint claim[CY_CLAIM_LDS];
+  const bool regen = slot_refill(kg, b, tile, slot, finished, claim);
+  queue_push(queue_out, count_out, slot, regen, claim);
+}
+
 /* Stage 3: occlusion of the light sample, deferred light add, finish + refill. */
 template<bool STATS, int W, bool INST, int HAIR = 0>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow(CyGlobals kg,
@@ -2283,6 +2369,12 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           tex = true;
           break;
         case NODE_CLOSURE_SET_NORMAL: /* the bump program of displacement method "bump" */
+        case NODE_AMBIENT_OCCLUSION:
+        case NODE_BEVEL:
+          tex = true;
+          break;
+        case NODE_WIREFRAME:
+          *uses_ray_diff |= (node.w & 0xFF) != 0 || ((node.w >> 8) & 0xFF) != 0; /* pixel size / bump forms */
           tex = true;
           break;
         case NODE_RGB_RAMP:
@@ -2821,6 +2913,16 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
       if (continuations(true) != 0) {
         return -1;
       }
+    }
+    else if (dev->trav_refill[0] > 0 && W > 2 && !kg.have_instancing && !kg.have_curves) {
+      uint *claim = dev->refill_claim + 8 * ln.index;
+      HIP_CHECK(dev, hipMemsetAsync(claim, 0, 8 * sizeof(uint), s));
+      auto kfn = counters ? (W == 8 ? k_shadow_refill<true, 8> : k_shadow_refill<true, 4>)
+                          : (W == 8 ? k_shadow_refill<false, 8> : k_shadow_refill<false, 4>);
+      hipLaunchKernelGGL(kfn, dim3(std::min<uint>(CY_REFILL_BLOCKS, grid.x)), block, 0, s, kg, dev->bufs, ln.q[qs],
+                         ln.cnt + qs, claim, err, dev->stats_dev, dev->trav_refill[0], dev->trav_refill[1]);
+      hipLaunchKernelGGL(k_shadow_finish, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs,
+                         ln.q[qb], ln.cnt + qb);
     }
     else {
       auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0, dev->curve_shapes);

@@ -25,6 +25,7 @@
 #include "cy_path.h"
 #include "cy_subsurface.h"
 #include "cy_volume.h"
+#include "cy_svm_raytrace.h"
 
 /* Per-slot state, SoA of 16-byte records so every access is one dwordx4. */
 typedef struct CyPathBuffers {

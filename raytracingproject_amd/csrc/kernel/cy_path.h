@@ -2417,6 +2417,74 @@ CY_FN void svm_node_principled_volume(const CyGlobals *kg, CySD *sd, CySvmStack 
 #endif
 
 /* type: SHADER_TYPE_SURFACE (0), SHADER_TYPE_VOLUME (1) or SHADER_TYPE_DISPLACEMENT (2), svm.h:236-246 */
+#if CY_SVM_TEX && CY_CLOSURE_EXT
+/* svm_wireframe.h:39-88: 1 when P lies within size / 2 (times the pixel's
+ * footprint from the ray differentials with use_pixel_size) of an edge of
+ * the shading point's triangle */
+CY_FN float wireframe(const CyGlobals *kg, const CySD *sd, float size, int pixel_size, cfloat3 P)
+{
+  if (sd->prim != PRIM_NONE && (sd->type & PRIMITIVE_ALL_TRIANGLE)) {
+    cfloat3 Co[3];
+    float pixelwidth = 1.0f;
+    const int np = 3;
+    triangle_verts(kg, sd->prim, Co);
+    if (!(sd->object_flag & SD_OBJECT_TRANSFORM_APPLIED)) {
+      const struct cy_tfm *tfm = object_tfm(kg, sd->object);
+      Co[0] = transform_point(tfm, Co[0]);
+      Co[1] = transform_point(tfm, Co[1]);
+      Co[2] = transform_point(tfm, Co[2]);
+    }
+    if (pixel_size) {
+      /* the differentials of P projected on the plane across I */
+      const float pixelwidth_x = len3(sub3(sd->dP.dx, mul3f(sd->I, dot3(sd->dP.dx, sd->I))));
+      const float pixelwidth_y = len3(sub3(sd->dP.dy, mul3f(sd->I, dot3(sd->dP.dy, sd->I))));
+      pixelwidth = (pixelwidth_x + pixelwidth_y) * 0.5f;
+    }
+    /* half the width (the neighbouring face renders the other half), squared */
+    pixelwidth *= 0.5f * size;
+    pixelwidth *= pixelwidth;
+    for (int i = 0; i < np; i++) {
+      const int i2 = i ? i - 1 : np - 1;
+      const cfloat3 dir = sub3(P, Co[i]);
+      const cfloat3 edge = sub3(Co[i], Co[i2]);
+      const cfloat3 crs = cross3(edge, dir);
+      /* dot(crs, crs) / dot(edge, edge): the squared distance to the edge */
+      if (dot3(crs, crs) < (dot3(edge, edge) * pixelwidth)) {
+        return 1.0f;
+      }
+    }
+  }
+  return 0.0f;
+}
+
+/* svm_wireframe.h:90-127; the bump forms add a one-sided difference */
+CY_FN void svm_node_wireframe(const CyGlobals *kg, const CySD *sd, CySvmStack stack, hc_uint4 node, uint *err)
+{
+  const uint in_size = node.y, out_fac = node.z;
+  const uint use_pixel_size = node.w & 0xFF, bump_offset = (node.w >> 8) & 0xFF;
+  const float size = svm_load(stack, in_size, err);
+  const int pixel_size = (int)use_pixel_size;
+  float f = wireframe(kg, sd, size, pixel_size, sd->P);
+  if (bump_offset == 1) { /* NODE_BUMP_OFFSET_DX */
+    const cfloat3 Px = sub3(sd->P, sd->dP.dx);
+    f += (f - wireframe(kg, sd, size, pixel_size, Px)) / len3(sd->dP.dx);
+  }
+  else if (bump_offset == 2) { /* NODE_BUMP_OFFSET_DY */
+    const cfloat3 Py = sub3(sd->P, sd->dP.dy);
+    f += (f - wireframe(kg, sd, size, pixel_size, Py)) / len3(sd->dP.dy);
+  }
+  if (out_fac != SVM_STACK_INVALID) {
+    svm_store(stack, out_fac, f, err);
+  }
+}
+
+/* the ray-tracing nodes (cy_svm_raytrace.h, after the local traversals) */
+CY_FN void svm_node_ao(const CyGlobals *kg, CySD *sd, const CyPathState *state, CySvmStack stack, hc_uint4 node,
+                       uint *err);
+CY_FN void svm_node_bevel(const CyGlobals *kg, CySD *sd, const CyPathState *state, CySvmStack stack, hc_uint4 node,
+                          uint *err);
+#endif
+
 CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err,
                           int type = 0)
 {
@@ -2543,6 +2611,18 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         break;
       }
 #if CY_SVM_TEX
+#if CY_CLOSURE_EXT
+      case NODE_WIREFRAME:
+        svm_node_wireframe(kg, sd, stack, node, err);
+        break;
+      /* svm_ao.h, svm_bevel.h: rays traced from the shader */
+      case NODE_AMBIENT_OCCLUSION:
+        svm_node_ao(kg, sd, state, stack, node, err);
+        break;
+      case NODE_BEVEL:
+        svm_node_bevel(kg, sd, state, stack, node, err);
+        break;
+#endif
       /* svm_closure.h:1188-1194: the bump program's normal becomes the
        * shading normal (displacement method "bump") */
       case NODE_CLOSURE_SET_NORMAL: {

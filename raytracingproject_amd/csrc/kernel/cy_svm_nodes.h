@@ -36,13 +36,16 @@ enum {
   NODE_TEX_CHECKER = 62,
   NODE_LIGHT_FALLOFF = 66,
   NODE_INVERT = 72,
+  NODE_WIREFRAME = 80,
   NODE_MIX = 73,
   NODE_SEPARATE_VECTOR = 74,
   NODE_COMBINE_VECTOR = 75,
   NODE_SEPARATE_HSV = 76,
   NODE_COMBINE_HSV = 77,
   NODE_MAP_RANGE = 83,
-  NODE_CLAMP = 84
+  NODE_CLAMP = 84,
+  NODE_BEVEL = 85,
+  NODE_AMBIENT_OCCLUSION = 86
 };
 
 CY_FN void svm_unpack3(uint i, uint *x, uint *y, uint *z)

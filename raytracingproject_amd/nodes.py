@@ -67,6 +67,9 @@ NODE_SET_BUMP, NODE_ATTR_BUMP_DX, NODE_ATTR_BUMP_DY = 26, 27, 28
 NODE_VERTEX_COLOR_BUMP_DX, NODE_VERTEX_COLOR_BUMP_DY = 29, 30
 NODE_TEX_COORD_BUMP_DX, NODE_TEX_COORD_BUMP_DY = 31, 32
 NODE_CLOSURE_SET_NORMAL = 33
+NODE_BEVEL, NODE_AMBIENT_OCCLUSION = 85, 86
+NODE_WIREFRAME = 80
+NODE_AO_ONLY_LOCAL, NODE_AO_INSIDE, NODE_AO_GLOBAL_RADIUS = 1, 2, 4
 NODE_OBJECT_INFO, NODE_TANGENT, NODE_NORMAL_MAP = 48, 70, 71
 NODE_FRESNEL, NODE_LAYER_WEIGHT = 38, 39
 NODE_CAMERA, NODE_NORMAL, NODE_RGB_CURVES, NODE_VECTOR_CURVES = 54, 65, 68, 69
@@ -557,6 +560,36 @@ def bump(height=1.0, strength=1.0, distance=0.1, invert=False, normal=None, obje
     return Node("bump", inputs, {"invert": bool(invert), "object_space": bool(object_space)})["Normal"]
 
 
+def ambient_occlusion(color=(1.0, 1.0, 1.0), distance=1.0, normal=None, samples=16, inside=False,
+                      only_local=False) -> Node:
+    """Ambient Occlusion node (nodes.cpp:3210-3256, svm_ao.h): the fraction of
+    `samples` cosine-distributed rays from the shading point that reach
+    `distance` (0 unlinked: the world's AO distance) without a hit -- of the
+    same object only with only_local -- as AO and times Color.  An unset Normal
+    is the Geometry normal (graph.cpp default_inputs, LINK_NORMAL)."""
+    if normal is None:
+        normal = geometry()["Normal"]
+    return Node("ambient_occlusion", {"Color": color, "Distance": distance, "Normal": normal},
+                {"samples": int(samples), "inside": bool(inside), "only_local": bool(only_local)})
+
+
+def wireframe(size=0.01, use_pixel_size=False) -> Socket:
+    """Wireframe node (nodes.cpp:5583-5613, svm_wireframe.h): Fac 1 within
+    size / 2 of the shading triangle's edges (in pixels, through the ray
+    differentials, with use_pixel_size)."""
+    return Node("wireframe", {"Size": size}, {"use_pixel_size": bool(use_pixel_size)})["Fac"]
+
+
+def bevel(radius=0.05, normal=None, samples=4) -> Socket:
+    """Bevel node (nodes.cpp:6865-6894, svm_bevel.h): the normal averaged over
+    nearby points of the same object within `radius` (local probe rays); an
+    unset Normal input is the Geometry normal (LINK_NORMAL), which the node
+    adds its change to."""
+    if normal is None:
+        normal = geometry()["Normal"]
+    return Node("bevel", {"Radius": radius, "Normal": normal}, {"samples": int(samples)})["Normal"]
+
+
 def bump_from_displacement(disp: Socket, object_space: bool = False) -> Socket:
     """ShaderGraph::bump_from_displacement (graph.cpp:956-1050), the
     displacement method "bump": three copies of the displacement graph (centre,
@@ -657,8 +690,12 @@ def _outputs(node: Node) -> dict:
         return {"Color": "color", "Alpha": "float"}
     if k in ("displacement", "vector_displacement"):
         return {"Displacement": "vector"}
-    if k in ("bump", "set_normal"):
+    if k in ("bump", "set_normal", "bevel"):
         return {"Normal": "vector"}
+    if k == "ambient_occlusion":
+        return {"Color": "color", "AO": "float"}
+    if k == "wireframe":
+        return {"Fac": "float"}
     raise ValueError(f"unknown node kind {k!r}")
 
 
@@ -711,6 +748,9 @@ _INPUT_TYPES = {
     "bump": {"SampleCenter": "float", "SampleX": "float", "SampleY": "float", "Normal": "vector",
              "Strength": "float", "Distance": "float"},
     "set_normal": {"Direction": "vector"},
+    "ambient_occlusion": {"Color": "color", "Distance": "float", "Normal": "vector"},
+    "bevel": {"Radius": "float", "Normal": "vector"},
+    "wireframe": {"Size": "float"},
 }
 
 
@@ -1028,6 +1068,27 @@ class NodeCompiler:
         strength = self.inp(n, "Strength")
         self.emit((NODE_SET_BUMP, uchar4(nrm, dist, int(n.params["invert"]), int(n.params["object_space"])),
                    uchar4(c, x, y, strength), self.out(n, "Normal")))
+
+    def _n_ambient_occlusion(self, n):  # nodes.cpp:3233-3256 AmbientOcclusionNode::compile
+        dist = n.inputs["Distance"]
+        flags = (NODE_AO_INSIDE if n.params["inside"] else 0) | (NODE_AO_ONLY_LOCAL if n.params["only_local"] else 0)
+        if not is_linked(dist) and float(dist) == 0.0:
+            flags |= NODE_AO_GLOBAL_RADIUS
+        self.emit((NODE_AMBIENT_OCCLUSION,
+                   uchar4(flags, self.assign_if_linked(dist, "float"), self.assign_if_linked(n.inputs["Normal"], "vector"),
+                          self.out(n, "AO")),
+                   uchar4(self.inp(n, "Color"), self.out(n, "Color"), n.params["samples"]),
+                   f32bits(0.0 if is_linked(dist) else float(dist))))
+
+    def _n_wireframe(self, n):  # nodes.cpp:5598-5613 WireframeNode::compile
+        offset = {"dx": 1, "dy": 2}.get(n.params.get("bump"), 0)
+        self.emit((NODE_WIREFRAME, self.inp(n, "Size"), self.out(n, "Fac"),
+                   uchar4(int(n.params["use_pixel_size"]), offset)))
+
+    def _n_bevel(self, n):  # nodes.cpp:6883-6894 BevelNode::compile
+        self.emit((NODE_BEVEL, uchar4(n.params["samples"], self.inp(n, "Radius"),
+                                      self.assign_if_linked(n.inputs["Normal"], "vector"), self.out(n, "Normal")),
+                   0, 0))
 
     def _n_set_normal(self, n):  # nodes.cpp SetNormalNode::compile
         self.emit((NODE_CLOSURE_SET_NORMAL, self.inp(n, "Direction"), self.out(n, "Normal"), 0))

@@ -842,6 +842,50 @@ def bump_displace(width=40, height=40, samples=8) -> sc.Scene:
     return s
 
 
+def shading_raytrace(width=40, height=40, samples=8) -> sc.Scene:
+    """Shader ray tracing (golden parity case, svm_ao.h / svm_bevel.h): Bevel
+    normals on a glossy box (host-applied transform) and an instanced rotated
+    box (object-space normal transforms, 4 local probe hits at most), Bevel
+    feeding a Principled BSDF on a smooth superellipsoid, an Ambient Occlusion
+    colour (8 rays of 200 units) on a diffuse sphere, AO from inside the same
+    object only (only_local + inside) driving a mix, AO with the world's
+    distance (Distance 0) on the back wall's stand-in quad, and the Wireframe
+    node in pixel size (ray differentials) and as a bump height (its
+    *_BUMP_DX / _DY one-sided differences)."""
+    from . import nodes as nd
+
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    ao = nd.ambient_occlusion((0.85, 0.7, 0.5), distance=200.0, samples=8)
+    ao_local = nd.ambient_occlusion((1.0, 1.0, 1.0), distance=90.0, samples=6, inside=True, only_local=True)
+    ao_world = nd.ambient_occlusion((0.6, 0.8, 0.6), distance=0.0, samples=4)
+    s.materials.extend([
+        sc.glossy((0.8, 0.8, 0.85), 0.25, normal=nd.bevel(8.0, samples=4)),
+        sc.principled(base_color=(0.3, 0.5, 0.8), roughness=0.35, normal=nd.bevel(12.0, samples=6)),
+        sc.diffuse(ao["Color"]),
+        sc.mix(ao_local["AO"], sc.diffuse((0.9, 0.3, 0.2)), sc.glossy((0.9, 0.9, 0.9), 0.1)),
+        sc.diffuse(ao_world["Color"]),
+        sc.mix(nd.wireframe(2.0, use_pixel_size=True), sc.diffuse((0.2, 0.3, 0.7)), sc.diffuse((0.9, 0.9, 0.9))),
+        sc.glossy((0.8, 0.6, 0.3), 0.3, normal=nd.bump(nd.wireframe(6.0), strength=1.0, distance=2.0)),
+    ])
+    s.meshes.append(sc.Mesh(*_box((150.0, 80.0, 200.0), (120.0, 160.0, 120.0), 0.4), shader=base))
+    bv, bt = _box((0.0, 0.0, 0.0), (1.0, 1.0, 1.0))
+    s.instances.append(sc.Instance(sc.Mesh(bv, bt, shader=base), _tfm((400.0, 70.0, 300.0), 0.7, (110.0, 140.0, 90.0),
+                                                                      rot_x=0.3)))
+    s.meshes.append(sc.Mesh(*_ellipsoid((420.0, 330.0, 200.0), (70.0, 60.0, 70.0), 20, 12, exponent=0.5),
+                            shader=base + 1, smooth=True))
+    s.meshes.append(sc.Mesh(*_ellipsoid((160.0, 350.0, 380.0), (65.0, 65.0, 65.0), 20, 12), shader=base + 2,
+                            smooth=True))
+    s.meshes.append(sc.Mesh(*_ellipsoid((280.0, 200.0, 420.0), (60.0, 60.0, 60.0), 16, 10), shader=base + 3))
+    s.meshes.append(sc.Mesh(*_quad((60.0, 430.0, 520.0), (500.0, 430.0, 520.0), (500.0, 540.0, 520.0),
+                                   (60.0, 540.0, 520.0)), shader=base + 4))
+    s.meshes.append(sc.Mesh(*_ellipsoid((300.0, 70.0, 150.0), (55.0, 55.0, 55.0), 12, 8), shader=base + 5))
+    s.meshes.append(sc.Mesh(*_ellipsoid((80.0, 230.0, 280.0), (50.0, 50.0, 50.0), 12, 8), shader=base + 6,
+                            smooth=True))
+    s.name = "shading_raytrace"
+    return s
+
+
 def sss_disk_cornell(width=48, height=48, samples=8, instanced=False, transparent=False) -> sc.Scene:
     """Cornell box with disk BSSRDFs (golden parity case): Subsurface
     Scattering nodes with the cubic (sharpness 0.5, blurred checker colour),

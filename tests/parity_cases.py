@@ -87,6 +87,8 @@ CASES = {
     "shading_bump_paths": lambda: scenes.bump_paths(40, 40, 8),
     # displacement method "bump": the bump program from the Displacement output
     "shading_bump_displace": lambda: scenes.bump_displace(40, 40, 8),
+    # shader ray tracing: Ambient Occlusion and Bevel nodes (svm_ao.h, svm_bevel.h)
+    "shading_raytrace": lambda: scenes.shading_raytrace(40, 40, 8),
     "sss_disk": lambda: scenes.sss_disk_cornell(48, 48, 8),
     "sss_disk_instanced": lambda: scenes.sss_disk_cornell(48, 48, 8, instanced=True),
     "sss_disk_transparent": lambda: scenes.sss_disk_cornell(40, 40, 8, transparent=True),

@@ -47,4 +47,11 @@ if [[ $MODE == variants ]]; then
     step bench_$v 600 env HIPCY_DEVICE_LIB=$PWD/raytracingproject_amd/libhipcycles-$v.so python bench.py $Q "$@"
   done
 fi
+if [[ $MODE == refill ]]; then
+  # lane-refill settings (bench.py --refill ROUNDS MIN_IDLE), "0 16" = off
+  Q="--steps 5 --warmup 1 --no-cpu-baseline --other-configs="
+  for r in ${REFILLS:-0,16 8,16 16,16 32,16 16,32}; do
+    step "bench_refill_${r/,/_}" 600 python bench.py $Q --refill ${r%,*} ${r#*,} "$@"
+  done
+fi
 echo done
