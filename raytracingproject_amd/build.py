@@ -136,7 +136,7 @@ def build_oracle(ref=True):
     oracle = os.path.join(REPO, "oracle")
     _run(["make", "-C", oracle, "oracle", "-j4"])
     if ref and os.path.isdir("/root/reference/blender/intern/cycles"):
-        _run(["make", "-C", oracle, "ref", "ref-avx2", "-j4"])
+        _run(["make", "-C", oracle, "ref", "ref-avx2", "sky", "ies", "-j4"])
         # the Device plugin linked with the reference host's device layer
         # (tests/test_plugin_harness.py; needs libhipcycles.so)
         _run(["bash", os.path.join(REPO, "tools", "plugin_harness.sh")])

@@ -2190,9 +2190,10 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
 static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
                             const std::vector<void *> &tex_mem, const std::vector<uint32_t> &shader_flags,
                             bool *uses_tex, bool *uses_bssrdf, bool *uses_disk_bssrdf, bool *uses_attr,
-                            bool *uses_ray_diff, int *surface_closures, int *volume_closures)
+                            bool *uses_ray_diff, bool *uses_ies, int *surface_closures, int *volume_closures)
 {
   *uses_tex = false;
+  *uses_ies = false;
   *uses_ray_diff = false;
   *uses_bssrdf = false;
   *uses_disk_bssrdf = false;
@@ -2368,6 +2369,11 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           *uses_ray_diff = true;
           tex = true;
           break;
+        case NODE_VECTOR_DISPLACEMENT: /* height / vector displacement inside a bump program */
+          len = 2;
+          tex = true;
+          break;
+        case NODE_DISPLACEMENT:
         case NODE_CLOSURE_SET_NORMAL: /* the bump program of displacement method "bump" */
         case NODE_AMBIENT_OCCLUSION:
         case NODE_BEVEL:
@@ -2420,6 +2426,21 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
         case NODE_TEX_ENVIRONMENT:
           if (!slot_ok((int)node.y)) {
             return "shader " + std::to_string(sh) + ": environment texture slot " + std::to_string((int)node.y) +
+                   " was never allocated (tex_alloc)";
+          }
+          tex = true;
+          break;
+        case NODE_IES:
+          *uses_ies = true;
+          tex = true;
+          break;
+        case NODE_TEX_SKY: /* 8 parameter nodes, Nishita 3 (with its texture slot) */
+          len = (node.w == 2u) ? 4 : 9;
+          if (off + len > n) {
+            return "sky texture: parameter nodes past __svm_nodes";
+          }
+          if (node.w == 2u && !slot_ok((int)prog[off + 3].z)) {
+            return "shader " + std::to_string(sh) + ": sky texture slot " + std::to_string((int)prog[off + 3].z) +
                    " was never allocated (tex_alloc)";
           }
           tex = true;
@@ -2611,10 +2632,14 @@ int hipcy_load_kernels(hipcy_device *dev)
       shader_flags[i] = (uint32_t)ks[i].flags;
     }
   }
-  bool uses_bssrdf = false, uses_disk_bssrdf = false, uses_attr = false, uses_ray_diff = false;
+  bool uses_bssrdf = false, uses_disk_bssrdf = false, uses_attr = false, uses_ray_diff = false, uses_ies = false;
   int surface_closures = 0, volume_closures = 0;
   why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, shader_flags, &dev->shade_tex, &uses_bssrdf,
-                 &uses_disk_bssrdf, &uses_attr, &uses_ray_diff, &surface_closures, &volume_closures);
+                 &uses_disk_bssrdf, &uses_attr, &uses_ray_diff, &uses_ies, &surface_closures, &volume_closures);
+  if (why.empty() && uses_ies && dev->globals.find("__ies") == dev->globals.end()) {
+    /* LightManager::device_update_ies (light.cpp:1080-1125) */
+    why = "IES texture without the __ies table bound";
+  }
   if (why.empty() && uses_attr && dev->globals.find("__attributes_map") == dev->globals.end()) {
     /* the attribute nodes look attributes up through the objects' maps
      * (GeometryManager::device_update_attributes, geometry.cpp:379-474) */

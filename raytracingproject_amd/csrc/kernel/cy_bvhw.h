@@ -217,10 +217,14 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   bool found_hit = false;
 
   bool tie = cur ? cur->tie : false; /* two hits inside the window of the current best */
-  /* a hit accepted in front of its own leaf's box entry: the triangle test's
-   * rounding (sliver triangles) put it closer than the box that holds it, so
-   * the reference, whose culling bound is not widened, may never have tested
-   * it -- resolved by the reference-order re-trace like a near-tie (sticky) */
+  /* a hit accepted in front of its own leaf's box entry by more than the tie
+   * window: the triangle test's rounding (sliver triangles) put it clearly
+   * closer than the box that holds it, so the reference, whose culling bound
+   * is not widened, may have culled that box against a hit between the two --
+   * resolved by the reference-order re-trace like a near-tie (sticky).  A hit
+   * within the window of its box entry (every hit on an axis-aligned face can
+   * round an ulp below its flat box) needs no flag: a competing hit between
+   * the two lies inside the tie window and sets `tie` */
   bool bad = cur ? cur->tie : false;
   int iters = 0;
   /* culling bound: the best distance widened by the tie window (recomputed
@@ -388,7 +392,7 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
            * call or the incoming hit -- makes the result depend on the visiting
            * order: flag the ray; a hit clearly below the current one clears it */
           tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
-          bad |= CY_EXACT_TIES && exact_ok && tt < code_t;
+          bad |= CY_EXACT_TIES && exact_ok && tt * (1.0f + CY_TIE_EPS) < code_t;
           if (exact_ok || !CY_TIE_EXACT_OK) {
             /* the reference's acceptance test at the exact bound */
             isect->prim = prim_addr;
@@ -657,7 +661,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
             break;
           }
           tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
-          bad |= CY_EXACT_TIES && exact_ok && tt < leaf_t;
+          bad |= CY_EXACT_TIES && exact_ok && tt * (1.0f + CY_TIE_EPS) < leaf_t;
           if (exact_ok || !CY_TIE_EXACT_OK) {
             isect->prim = prim_addr;
             isect->object = OBJECT_NONE;

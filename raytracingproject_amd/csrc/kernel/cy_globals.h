@@ -45,7 +45,8 @@
   X(float, __attributes_float) \
   X(hc_float2, __attributes_float2) \
   X(hc_float4, __attributes_float3) \
-  X(uint32_t, __attributes_uchar4)
+  X(uint32_t, __attributes_uchar4) \
+  X(float, __ies)
 
 typedef struct CyGlobals {
   const hc_KernelData *data;

@@ -1162,6 +1162,7 @@ cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I,
   esd.I = I;
   esd.shader = shader;
   esd.type = (prim != PRIM_NONE) ? PRIMITIVE_TRIANGLE : ((lamp != LAMP_NONE) ? (1 << 6) /* PRIMITIVE_LAMP */ : 0);
+  esd.lamp = lamp;
   esd.object = object;
   esd.prim = prim;
   esd.u = u;

@@ -2157,11 +2157,14 @@ CY_FN void emission_setup(CySD *sd, cfloat3 weight)
  * register allocation they would otherwise burden.  Returns the next node
  * offset, or -1 for an unknown node. */
 #include "cy_svm_image.h"
+#include "cy_svm_sky.h"
+#include "cy_svm_ies.h"
 
 typedef struct CySvmTexIn {
   cfloat3 P, N, Ng, I;
   float u, v, ray_length;
   int object, flag;
+  int lamp; /* light index of a PRIMITIVE_LAMP point, else -1 */
   int bounce, diffuse_bounce, glossy_bounce, transparent_bounce, transmission_bounce;
 } CySvmTexIn;
 
@@ -2169,6 +2172,8 @@ CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
                                       const hc_uint4 *svm_nodes,
                                       const hc_KernelObject *objects,
                                       const hc_TextureInfo *texture_info,
+                                      const float *ies,
+                                      const hc_KernelLight *lights,
                                       CySvmTexIn in,
                                       CySvmStack stack,
                                       hc_uint4 node,
@@ -2193,6 +2198,9 @@ CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
   sdv.ray_length = in.ray_length;
   sdv.object = in.object;
   sdv.flag = in.flag;
+  sdv.lamp = in.lamp;
+  sdv.type = (in.lamp >= 0) ? (1 << 6) /* PRIMITIVE_LAMP */ : 0;
+  kgv.__lights = lights;
   CyPathState stv;
   const CyPathState *state = &stv;
   stv.bounce = in.bounce;
@@ -2288,6 +2296,12 @@ CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
         break;
       case NODE_TEX_ENVIRONMENT:
         svm_node_tex_environment(texture_info, stack, node, err);
+        break;
+      case NODE_TEX_SKY:
+        svm_node_tex_sky(kg, texture_info, stack, node, &offset, err);
+        break;
+      case NODE_IES:
+        svm_node_ies(ies, stack, node, err);
         break;
       case NODE_TEX_NOISE:
         svm_node_tex_noise(kg, stack, node.y, node.z, node.w, &offset, err);
@@ -2753,6 +2767,7 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         in.ray_length = sd->ray_length;
         in.object = sd->object;
         in.flag = sd->flag;
+        in.lamp = (sd->type == (1 << 6) /* PRIMITIVE_LAMP */) ? sd->lamp : -1;
         in.bounce = state ? state->bounce : 0; /* background SHADER task: PathState {0} */
         in.diffuse_bounce = state ? state->diffuse_bounce : 0;
         in.glossy_bounce = state ? state->glossy_bounce : 0;
@@ -2766,8 +2781,8 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
           in.v = sd->v + ((bump == 2) ? sd->dv.dy : sd->dv.dx);
         }
 #endif
-        offset = svm_eval_texture_node(kg->data, kg->__svm_nodes, kg->__objects, kg->__texture_info, in, stack, node,
-                                       path_flag, offset, err);
+        offset = svm_eval_texture_node(kg->data, kg->__svm_nodes, kg->__objects, kg->__texture_info, kg->__ies, kg->__lights, in,
+                                       stack, node, path_flag, offset, err);
         if (offset < 0) {
           cy_set_error(err, CY_ERR_SVM_NODE, node.x);
           return;

@@ -1028,10 +1028,15 @@ CY_FN void svm_node_tex_coord(
       }
       break;
     }
-    case 0: /* NORMAL: object_inverse_normal_transform */
+    case 0: /* NORMAL: object_inverse_normal_transform (geom_object.h:144-162; the CPU
+             * kernel's __OBJECT_MOTION__ form: a lamp's shading point uses the lamp's
+             * transform, ob_tfm = lamp_fetch_transform) */
       data = sd->N;
       if (sd->object != OBJECT_NONE) {
         data = normalize3(transform_direction_transposed(object_tfm(kg, sd->object), data));
+      }
+      else if (sd->type == (1 << 6) /* PRIMITIVE_LAMP */) {
+        data = normalize3(transform_direction_transposed((const struct cy_tfm *)&kg->__lights[sd->lamp].tfm, data));
       }
       break;
     case 2: { /* CAMERA */

@@ -359,6 +359,7 @@ typedef struct CySD {
   int type;
   float u, v;
   int object;
+  int lamp; /* the light of a PRIMITIVE_LAMP shading point (read only then) */
   float ray_length;
   int num_closure;
   int num_closure_left;

@@ -395,6 +395,95 @@ def environment_texture(image: Image, vector, projection: str = "equirectangular
                 params={"image": image, "projection": ENVIRONMENT_PROJECTIONS[projection]})
 
 
+SKY_TYPES = {"preetham": 0, "hosek_wilkie": 1, "nishita_improved": 2}
+NODE_TEX_SKY = 56
+
+
+def _sky_preetham(sun_direction, turbidity):
+    """nodes.cpp:624-705 sky_texture_precompute_preetham, in float32: the sun's
+    (theta, phi), zenith Y / x / y (radiance_x/y/z) and the Perez
+    coefficients (config_x/y/z[0..4]) normalised at the zenith."""
+    f = np.float32
+    d = np.asarray(sun_direction, dtype=np.float32)
+    theta, phi = f(np.arccos(d[2])), f(np.arctan2(d[0], d[1]))
+    theta2 = f(theta * theta)
+    theta3 = f(theta2 * theta)
+    T = f(turbidity)
+    T2 = f(T * T)
+    chi = f(f(f(4.0 / 9.0) - f(T / f(120.0))) * f(f(np.pi) - f(2.0) * theta))
+    rx = f(f(f(f(4.0453) * T - f(4.9710)) * f(np.tan(chi)) - f(0.2155) * T) + f(2.4192))
+    rx = f(rx * f(0.06))
+
+    def poly(a, b, c, d_, e, g, h, i, j, k, l_):
+        t1 = f(f(f(a) * theta3 - f(b) * theta2) + f(c) * theta)
+        t2 = f(f(f(f(d_) * theta3 + f(e) * theta2) - f(g) * theta) + f(h))
+        t3 = f(f(f(f(i) * theta3 - f(j) * theta2) + f(k) * theta) + f(l_))
+        return f(f(t1 * T2 + t2 * T) + t3)
+
+    ry = poly(0.00166, 0.00375, 0.00209, -0.02903, 0.06377, 0.03202, 0.00394, 0.11693, 0.21196, 0.06052, 0.25886)
+    rz = poly(0.00275, 0.00610, 0.00317, -0.04214, 0.08970, 0.04153, 0.00516, 0.15346, 0.26756, 0.06670, 0.26688)
+    lin = lambda a, b: f(f(a) * T + f(b))  # noqa: E731
+    cx = [lin(0.1787, -1.4630), lin(-0.3554, 0.4275), lin(-0.0227, 5.3251), lin(0.1206, -2.5771),
+          lin(-0.0670, 0.3703)] + [f(0.0)] * 4
+    cy = [lin(-0.0193, -0.2592), lin(-0.0665, 0.0008), lin(-0.0004, 0.2125), lin(-0.0641, -0.8989),
+          lin(-0.0033, 0.0452)] + [f(0.0)] * 4
+    cz = [lin(-0.0167, -0.2608), lin(-0.0950, 0.0092), lin(-0.0079, 0.2102), lin(-0.0441, -1.6537),
+          lin(-0.0109, 0.0529)] + [f(0.0)] * 4
+
+    def perez(lam, th, gamma):
+        a = f(f(1.0) + f(lam[0] * f(np.exp(f(lam[1] / f(np.cos(th)))))))
+        cg = f(np.cos(gamma))
+        b = f(f(f(1.0) + f(lam[2] * f(np.exp(f(lam[3] * gamma))))) + f(f(lam[4] * cg) * cg))
+        return f(a * b)
+
+    rx = f(rx / perez(cx, f(0.0), theta))
+    ry = f(ry / perez(cy, f(0.0), theta))
+    rz = f(rz / perez(cz, f(0.0), theta))
+    return theta, phi, (rx, ry, rz), (cx, cy, cz)
+
+
+def sky_texture(vector, kind: str = "nishita_improved", sun_direction=(0.0, 0.0, 1.0), turbidity: float = 2.2,
+                ground_albedo: float = 0.3, sun_disc: bool = True, sun_size: float = 0.009512,
+                sun_intensity: float = 1.0, sun_elevation: float = 15.0 * np.pi / 180.0, sun_rotation: float = 0.0,
+                model=None) -> Node:
+    """Sky Texture node (nodes.cpp:708-914 SkyTextureNode, svm_sky.h).  The
+    Preetham parameters are computed here (nodes.cpp:645-705).  The other two
+    models take their precomputed data from Blender's intern/sky library, which
+    the host runs (outside the device path): `model` is, for hosek_wilkie,
+    {"configs": (3, 9), "radiances": (3,)} of SKY_arhosek_xyz_skymodelstate at
+    (turbidity, ground_albedo, the sun's elevation) — theta / phi of
+    `sun_direction` come from sky_spherical_coordinates here; for
+    nishita_improved, {"pixel_bottom": (3,), "pixel_top": (3,), "image": Image}
+    (SKY_nishita_skymodel_precompute_sun / _texture; the image is the 512 x 128
+    float4 SkyLoader texture, linear interpolation, extend).  In a world shader
+    geometry()["Position"] is the ray direction."""
+    if kind not in SKY_TYPES:
+        raise ValueError("sky_texture: preetham | hosek_wilkie | nishita_improved")
+    if kind != "preetham" and model is None:
+        raise ValueError(f"sky_texture {kind}: needs the host-precomputed model data")
+    return Node("sky_texture", {"Vector": vector},
+                params={"type": SKY_TYPES[kind], "sun_direction": tuple(float(c) for c in sun_direction),
+                        "turbidity": float(turbidity), "ground_albedo": float(ground_albedo),
+                        "sun_disc": bool(sun_disc), "sun_size": float(sun_size),
+                        "sun_intensity": float(sun_intensity), "sun_elevation": float(sun_elevation),
+                        "sun_rotation": float(sun_rotation), "model": model})
+
+
+NODE_IES = 67
+
+
+def ies_texture(vector, ies, strength=1.0) -> Node:
+    """IES Texture node (nodes.cpp:1213-1300 IESLightNode, svm_ies.h): the
+    light's intensity towards `vector` from an IES photometric file (its text,
+    or an ies.IESFile), times Strength; outputs Fac.  The file gets a slot of
+    the scene's __ies table (LightManager::add_ies: one slot per distinct
+    content)."""
+    from .ies import IESFile
+
+    f = ies if isinstance(ies, IESFile) else IESFile(ies)
+    return Node("ies_texture", {"Vector": vector, "Strength": strength}, params={"ies": f})
+
+
 def noise_texture(vector=None, w=0.0, scale=5.0, detail=2.0, roughness=0.5, distortion=0.0, dimensions=3) -> Node:
     """Noise Texture (nodes.cpp NoiseTextureNode): fractal Perlin noise in 1-4
     dimensions (1D uses W, 4D the vector and W); outputs Fac, Color.  An
@@ -688,6 +777,10 @@ def _outputs(node: Node) -> dict:
         return {"Result": "float"}
     if k in ("rgb_ramp", "image_texture", "environment_texture"):
         return {"Color": "color", "Alpha": "float"}
+    if k == "sky_texture":
+        return {"Color": "color"}
+    if k == "ies_texture":
+        return {"Fac": "float"}
     if k in ("displacement", "vector_displacement"):
         return {"Displacement": "vector"}
     if k in ("bump", "set_normal", "bevel"):
@@ -734,6 +827,8 @@ _INPUT_TYPES = {
     "rgb_ramp": {"Fac": "float"},
     "image_texture": {"Vector": "vector"},
     "environment_texture": {"Vector": "vector"},
+    "sky_texture": {"Vector": "vector"},
+    "ies_texture": {"Vector": "vector", "Strength": "float"},
     "displacement": {"Height": "float", "Midlevel": "float", "Scale": "float", "Normal": "vector"},
     "normal_map": {"Color": "color", "Strength": "float"},
     "fresnel": {"IOR": "float", "Normal": "vector"},
@@ -760,7 +855,7 @@ def _width(t: str) -> int:
 
 # ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
 # the shading point or direction (texture coordinate, geometry, textures)
-SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture",
+SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture", "sky_texture", "ies_texture",
                  "attribute", "vertex_color", "normal_map", "tangent", "object_info", "camera_data")
 
 
@@ -803,8 +898,11 @@ class NodeCompiler:
     outputs feeding the closures (`roots`) stay live."""
 
     def __init__(self, alloc, emit, roots=(), free=None, images=None, attribute=None, background=False,
-                 volume=False):
+                 volume=False, features=None, ies_slots=None):
         self.images = images if images is not None else []  # SVM image slots (shared per scene)
+        self.ies_slots = ies_slots if ies_slots is not None else []  # __ies slots (shared per scene)
+        # scene-wide needs of the compiled nodes (e.g. "xyz_to_rgb": film colour matrices)
+        self.features = features if features is not None else set()
         # SVMCompiler::attribute (svm.cpp): attribute id of a standard id or a
         # name, recording the shader's attribute request
         self.attribute = attribute or (lambda key: (_ for _ in ()).throw(
@@ -1199,6 +1297,57 @@ class NodeCompiler:
         flags = self._image_flags(n, image)
         self.emit((NODE_TEX_ENVIRONMENT, self.image_slot(image),
                    uchar4(vec, self.out(n, "Color"), self.out(n, "Alpha"), flags), n.params["projection"]))
+
+    def _n_sky_texture(self, n):  # nodes.cpp:837-914 SkyTextureNode::compile (identity texture mapping)
+        p = n.params
+        vec = self.inp(n, "Vector")
+        col = self.out(n, "Color")
+        if col == SVM_STACK_INVALID:
+            col = self.alloc(3)
+            self.temps.append((col, 3))
+        self.emit((NODE_TEX_SKY, vec, col, p["type"]))
+        self.features.add("xyz_to_rgb")
+        f = np.float32
+        if p["type"] != SKY_TYPES["nishita_improved"]:
+            if p["type"] == SKY_TYPES["preetham"]:
+                theta, phi, rad, cfg = _sky_preetham(p["sun_direction"], p["turbidity"])
+            else:  # sky_texture_precompute_hosek: clamped theta, the library's state cast to float
+                d = np.asarray(p["sun_direction"], dtype=np.float32)
+                theta = f(min(max(f(np.arccos(d[2])), f(0.0)), f(np.pi / 2)))
+                phi = f(np.arctan2(d[0], d[1]))
+                m = p["model"]
+                cfg = np.asarray(m["configs"], dtype=np.float32).reshape(3, 9)
+                rad = np.asarray(m["radiances"], dtype=np.float32).reshape(3)
+            vals = [phi, theta, rad[0], rad[1], rad[2], *cfg[0], *cfg[1], *cfg[2]]
+        else:  # sky_texture_precompute_nishita
+            m = p["model"]
+            rot = f(np.fmod(f(p["sun_rotation"]), f(2.0 * np.pi)))
+            if rot < 0.0:
+                rot = f(rot + f(2.0 * np.pi))
+            rot = f(f(2.0 * np.pi) - rot)
+            size = f(max(f(p["sun_size"]), f(0.0005)))  # get_sun_size
+            vals = [*np.asarray(m["pixel_bottom"], dtype=np.float32), *np.asarray(m["pixel_top"], dtype=np.float32),
+                    f(p["sun_elevation"]), rot, size if p["sun_disc"] else f(-1.0), f(p["sun_intensity"])]
+        words = [f32bits(float(v)) for v in vals]
+        if p["type"] == SKY_TYPES["nishita_improved"]:
+            words = words + [self.image_slot(p["model"]["image"]), 0]
+        for i in range(0, len(words), 4):
+            self.emit(tuple(words[i:i + 4]))
+
+    def _n_ies_texture(self, n):  # nodes.cpp:1279-1295 IESLightNode::compile (identity texture mapping)
+        f = n.params["ies"]
+        slot = next((i for i, g in enumerate(self.ies_slots) if g.content == f.content), None)
+        if slot is None:  # LightManager::add_ies: a new slot per distinct file
+            self.ies_slots.append(f)
+            slot = len(self.ies_slots) - 1
+        strength = self.assign_if_linked(n.inputs["Strength"], "float")
+        vec = self.inp(n, "Vector")
+        fac = self.out(n, "Fac")
+        if fac == SVM_STACK_INVALID:
+            fac = self.alloc(1)
+            self.temps.append((fac, 1))
+        sval = 0.0 if is_linked(n.inputs["Strength"]) else float(n.inputs["Strength"])
+        self.emit((NODE_IES, uchar4(strength, vec, fac, 0), slot, f32bits(sval)))
 
     # -- procedural noise textures (nodes.cpp *TextureNode::compile, identity
     # texture mapping: tex_mapping.compile_begin = stack_assign(vector))

@@ -469,6 +469,8 @@ class SVMCompiler:
 
     def __init__(self):
         self.images: list = []  # SVM image slots, shared by every shader of the scene
+        self.features: set = set()  # scene-wide needs of the compiled nodes (NodeCompiler.features)
+        self.ies_slots: list = []  # IES files of the IES Texture nodes (LightManager ies_slots)
         self.nodes: list[tuple[int, int, int, int]] = []
         self.stack_top = 0
         self.stack_used = [False] * SVM_STACK_SIZE
@@ -497,7 +499,8 @@ class SVMCompiler:
 
     def _node_compiler(self, roots, background=False, volume=False):
         return nodes.NodeCompiler(self.alloc, self.nodes.append, roots, self.free, images=self.images,
-                                  attribute=self.attribute, background=background, volume=volume)
+                                  attribute=self.attribute, background=background, volume=volume,
+                                  features=self.features, ies_slots=self.ies_slots)
 
     def alloc(self, n=1) -> int:
         """First fit over the free slots (svm.cpp stack_find_offset)."""
@@ -1568,6 +1571,14 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.filter_table_offset = 0
     # shader.cpp:387 ColorSpaceManager defaults (no OCIO): Rec.709 luminance
     kf.rgb_to_y.x, kf.rgb_to_y.y, kf.rgb_to_y.z = 0.2126729, 0.7151522, 0.0721750
+    if "xyz_to_rgb" in svm_compiler.features:
+        # shader.cpp:384-386 (and :608-610): the XYZ -> linear Rec.709 rows.  The
+        # reference host always uploads them; they are set here only for scenes
+        # whose nodes read them (sky texture), which keeps the KernelData bytes
+        # of every other golden case unchanged.
+        kf.xyz_to_r.x, kf.xyz_to_r.y, kf.xyz_to_r.z = 3.2404542, -1.5371385, -0.4985314
+        kf.xyz_to_g.x, kf.xyz_to_g.y, kf.xyz_to_g.z = -0.9692660, 1.8760108, 0.0415560
+        kf.xyz_to_b.x, kf.xyz_to_b.y, kf.xyz_to_b.z = 0.0556434, -0.2040259, 1.0572252
     # display pass = combined (film.cpp:392, 419-423, 591-598)
     kf.display_pass_stride = 0
     kf.display_pass_components = 4
@@ -1641,6 +1652,11 @@ def compile_scene(scene: Scene) -> DeviceScene:
         "__lookup_table": lookup,
         "__sample_pattern_lut": lut,
     }
+    if svm_compiler.ies_slots:
+        # LightManager::device_update_ies (light.cpp:1080-1125)
+        from .ies import pack_slots
+
+        arrays["__ies"] = pack_slots(svm_compiler.ies_slots)
     if use_volumes:
         arrays["__object_volume_step"] = object_volume_step
         # geometry.cpp device_update_attributes: no attributes are packed, every
@@ -2356,5 +2372,5 @@ ELEMENT_BYTES = {
     "__curves": 16, "__curve_keys": 16,
     "__object_volume_step": 4, "__attributes_map": 16,
     "__attributes_float": 4, "__attributes_float2": 8, "__attributes_float3": 16, "__attributes_uchar4": 4,
-    "__tri_patch": 4,
+    "__tri_patch": 4, "__ies": 4,
 }

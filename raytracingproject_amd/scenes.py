@@ -184,6 +184,33 @@ def emission_nodes(width=48, height=48, samples=8) -> sc.Scene:
     return scene
 
 
+def ies_lamps(width=48, height=48, samples=8, ies_files=()) -> sc.Scene:
+    """Point and spot lamps whose strength is an IES Texture node (svm_ies.h)
+    on the texture-coordinate normal (the node's default LINK_TEXTURE_NORMAL
+    input): `ies_files` are the texts of two IES photometric files (a one-
+    quadrant type C downlight, a half-plane type C file with a TILT block);
+    the second file is also used by the spot lamp, so both lamps share its
+    __ies slot."""
+    from . import nodes
+
+    scene = cornell_box(width, height, samples)
+    scene.materials[3] = sc.emission((1.0, 1.0, 1.0), 2.0)
+    normal = nodes.tex_coord()["Normal"]
+    a = nodes.ies_texture(normal, ies_files[0], strength=1.0)["Fac"]
+    b = nodes.ies_texture(normal, ies_files[1], strength=nodes.math("add", nodes.light_path()["Is Diffuse Ray"], 0.5))
+    scene.lamps = [
+        sc.Lamp("point", co=(180.0, 480.0, 250.0), size=15.0, color=(1.0, 0.8, 0.6), strength=3.0e3,
+                shader=sc.emission((1.0, 1.0, 1.0), a)),
+        sc.Lamp("point", co=(400.0, 300.0, 150.0), size=10.0, color=(0.6, 0.8, 1.0), strength=2.0e3,
+                shader=sc.emission((1.0, 1.0, 1.0), b["Fac"])),
+        sc.Lamp("spot", co=(300.0, 500.0, 400.0), direction=(-0.2, -1.0, -0.3), size=10.0,
+                spot_angle=math.radians(70.0), spot_smooth=0.2, color=(1.0, 1.0, 1.0), strength=1.0e5,
+                shader=sc.emission((1.0, 1.0, 1.0), nodes.ies_texture(normal, ies_files[1], 2.0)["Fac"])),
+    ]
+    scene.name = "ies_lamps"
+    return scene
+
+
 def cornell_camera(kind: str, width=64, height=64, samples=16) -> sc.Scene:
     """Cornell box through the camera models of kernel_camera.h: "dof"
     (perspective, hexagonal anamorphic aperture), "ortho" (orthographic with a
@@ -1374,6 +1401,37 @@ def world_lit(width=64, height=64, samples=8, map_resolution=128, with_lamp=Fals
         lamps.append(sc.Lamp(kind="point", co=(-2.0, 3.0, -2.0), color=(1.0, 0.9, 0.8), strength=30.0, size=0.3))
     s = sc.Scene(width, height, cam, meshes, materials, samples=samples, name="world_lit", lamps=lamps)
     s.world_color = world
+    s.world_strength = 1.0
+    s.world_map_resolution = map_resolution
+    return s
+
+
+def sky_lit(width=32, height=32, samples=4, kind="preetham", model=None, map_resolution=64) -> sc.Scene:
+    """Objects on a ground plane under a Sky Texture world (svm_sky.h), Z up as
+    the sky models assume: the camera sees the horizon and the sky, the world
+    importance map (background light, kernel_light_background.h) samples it.
+    `model` is the host-precomputed data of the Hosek-Wilkie / Nishita models
+    (nodes.sky_texture)."""
+    from . import nodes as nd
+
+    D = nd.geometry()["Position"]
+    sun = (0.3, 0.55, 0.78)
+    if kind == "nishita_improved":
+        sky = nd.sky_texture(D, kind, sun_disc=True, sun_size=0.05, sun_intensity=0.002,
+                             sun_elevation=math.radians(12.0), sun_rotation=math.radians(-30.0), model=model)
+    else:
+        sky = nd.sky_texture(D, kind, sun_direction=sun, turbidity=3.0, ground_albedo=0.4, model=model)
+    meshes, materials = [], []
+    materials.append(sc.diffuse((0.5, 0.5, 0.45)))
+    meshes.append(sc.Mesh(*_quad((-8, -8, 0), (8, -8, 0), (8, 8, 0), (-8, 8, 0)), shader=0))
+    materials.append(sc.diffuse((0.7, 0.25, 0.15)))
+    meshes.append(sc.Mesh(*_box((-1.4, 0.6, 0.75), (1.5, 1.5, 1.5), 0.3), shader=1))
+    materials.append(sc.glossy((0.9, 0.9, 0.9), 0.2))
+    meshes.append(sc.Mesh(*_ellipsoid((1.1, -0.2, 0.9), (0.9, 0.9, 0.9), 24, 12), shader=2))
+    cam = sc.Camera(eye=(0.0, -7.0, 1.6), target=(0.0, 0.0, 1.4), up=(0.0, 0.0, 1.0), fov=math.radians(60.0),
+                    nearclip=0.01, farclip=1e4)
+    s = sc.Scene(width, height, cam, meshes, materials, samples=samples, name=f"sky_{kind}")
+    s.world_color = sky["Color"]
     s.world_strength = 1.0
     s.world_map_resolution = map_resolution
     return s

@@ -36,6 +36,12 @@ CASES = {
     # (kernel_light_background.h), alone and sharing the distribution with a lamp
     "world_mis": lambda: scenes.world_lit(48, 48, 8, map_resolution=128),
     "world_mis_lamp": lambda: scenes.world_lit(48, 48, 8, map_resolution=64, with_lamp=True),
+    # Sky Texture worlds (svm_sky.h): Preetham, Hosek-Wilkie and Nishita (its
+    # precomputed sky image + sun disc); host model data from tests/golden/sky.npz
+    **{f"shading_sky_{k}": (lambda k=k: scenes.sky_lit(32, 32, 4, kind=k, model=sky_model(k)))
+       for k in ("preetham", "hosek_wilkie", "nishita_improved")},
+    # IES Texture lamps (svm_ies.h, util_ies.cpp parsing / processing on the host)
+    "shading_ies": lambda: scenes.ies_lamps(48, 48, 8, ies_files=ies_texts()),
     # transparent BSDF + transparent shadows (kernel_shadow.h record-all, SVM in shadows)
     "transparent_shadows": lambda: scenes.transparent_shadows(48, 48, 8),
     # BSDF closure breadth (closure/bsdf_*.h): diffuse family, microfacets
@@ -105,6 +111,25 @@ CASES = {
     # shader graphs with connects, lights with their own shaders, an include)
     "xml_cornell": lambda: xml_scene.read_file(os.path.join(SCENES, "cornell.xml"), samples=8),
 }
+def ies_texts():
+    """The two IES photometric files of the shading_ies case (tests/scenes)."""
+    return [open(os.path.join(SCENES, f)).read() for f in ("spot_c.ies", "wide_c.ies")]
+
+
+def sky_model(kind):
+    """Host-precomputed Sky Texture data (tests/golden/make_sky.py: Blender's
+    intern/sky run on the reference's sources) for the shading_sky cases."""
+    if kind == "preetham":
+        return None
+    from raytracingproject_amd import nodes as nd
+
+    g = np.load(os.path.join(GOLDEN, "sky.npz"), allow_pickle=False)
+    if kind == "hosek_wilkie":
+        return {"configs": g["hosek_configs"], "radiances": g["hosek_radiances"]}
+    image = nd.Image(pixels=g["nishita_texture"], data_type="float4", interpolation="linear", extension="extend")
+    return {"pixel_bottom": g["nishita_bottom"], "pixel_top": g["nishita_top"], "image": image}
+
+
 # Cases whose __sample_pattern_lut is the reference host's table (fixture)
 JOE_KUO_CASES = {"cornell_joe_kuo"}
 

@@ -123,15 +123,20 @@ def test_constant_emission_detection():
 
 @pytest.mark.gpu
 def test_unimplemented_node_rejected_at_load_kernels():
-    """tan has no glibc restatement in the kernel: the program scan rejects it
-    before any render, naming the node."""
+    """A node the device does not run (here NODE_IES, svm_types.h, patched over a
+    Math node of a compiled program) is rejected by the program scan before
+    any render, naming the node."""
     from raytracingproject_amd.device import DeviceError, HIPDevice
 
     s = scenes.shading_math(8, 8, 1)
-    s.materials[0] = sc.diffuse(nd.combine_xyz(nd.math("tangent", 0.3, 0.0), 0.0, 0.0))
+    s.materials[0] = sc.diffuse(nd.combine_xyz(nd.math("sine", 0.3, 0.0), 0.0, 0.0))
+    ds = sc.compile_scene(s)
+    prog = ds.arrays["__svm_nodes"]
+    k = int(np.flatnonzero(prog[:, 0] == 42)[0])  # NODE_MATH
+    prog[k, 0] = 67  # NODE_IES
     dev = HIPDevice(0)
     try:
-        with pytest.raises(DeviceError, match="tangent"):
-            dev.upload_scene(sc.compile_scene(s))
+        with pytest.raises(DeviceError, match="SVM node 67 is not implemented"):
+            dev.upload_scene(ds)
     finally:
         dev.close()

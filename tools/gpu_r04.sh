@@ -20,7 +20,7 @@ step() {
 MODE=${1:-all}
 shift || true
 if [[ $MODE == all || $MODE == test ]]; then
-  step pytest_gpu 900 python -u -m pytest tests -q -m gpu --maxfail=20 --timeout 120 --timeout-method thread
+  step pytest_gpu 900 python -u -m pytest tests -q -m gpu --maxfail=200 --timeout 120 --timeout-method thread
   step smoke 300 python __graft_entry__.py smoke
 fi
 if [[ $MODE == sel ]]; then
