@@ -73,7 +73,7 @@ def parse(argv=None):
                    help="comma-separated extra holds for more tile-stream legs (measurement)")
     p.add_argument("--profile-frame", action="store_true",
                    help="only render the instrumented single-lane frame (for rocprofv3 PMC passes)")
-    p.add_argument("--other-configs", default="barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
+    p.add_argument("--other-configs", default="bmw27_production,barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
                    help="BASELINE.json's other configs, one frame each after the headline measurement (rank 0, "
                         "N=1): name or name@XxY+WxH for a full-spp crop; empty disables")
     p.add_argument("--shard", default="auto", choices=("auto", "rows", "tiles"),

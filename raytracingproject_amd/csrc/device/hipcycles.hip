@@ -2430,6 +2430,10 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           }
           tex = true;
           break;
+        case NODE_WAVELENGTH:
+        case NODE_BLACKBODY:
+          tex = true;
+          break;
         case NODE_IES:
           *uses_ies = true;
           tex = true;

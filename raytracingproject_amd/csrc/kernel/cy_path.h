@@ -2159,6 +2159,7 @@ CY_FN void emission_setup(CySD *sd, cfloat3 weight)
 #include "cy_svm_image.h"
 #include "cy_svm_sky.h"
 #include "cy_svm_ies.h"
+#include "cy_svm_spectral.h"
 
 typedef struct CySvmTexIn {
   cfloat3 P, N, Ng, I;
@@ -2302,6 +2303,12 @@ CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
         break;
       case NODE_IES:
         svm_node_ies(ies, stack, node, err);
+        break;
+      case NODE_WAVELENGTH:
+        svm_node_wavelength(kg, stack, node.y, node.z, err);
+        break;
+      case NODE_BLACKBODY:
+        svm_node_blackbody(stack, node.y, node.z, err);
         break;
       case NODE_TEX_NOISE:
         svm_node_tex_noise(kg, stack, node.y, node.z, node.w, &offset, err);

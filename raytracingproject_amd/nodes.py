@@ -472,6 +472,24 @@ def sky_texture(vector, kind: str = "nishita_improved", sun_direction=(0.0, 0.0,
 NODE_IES = 67
 
 
+NODE_WAVELENGTH, NODE_BLACKBODY = 81, 82
+
+
+def wavelength(value=500.0) -> Socket:
+    """Wavelength node (nodes.cpp WavelengthNode, svm_wavelength.h): the CIE
+    colour of a wavelength in nm through the film's XYZ -> RGB rows."""
+    return Node("wavelength", {"Wavelength": value})["Color"]
+
+
+def blackbody(temperature=1500.0) -> Socket:
+    """Blackbody node (nodes.cpp BlackbodyNode, svm_blackbody.h): the colour of
+    a black body at `temperature` Kelvin.  (The reference host folds a
+    constant temperature to a colour; link it to keep the node.)"""
+    return Node("blackbody", {"Temperature": temperature})["Color"]
+
+
+
+
 def ies_texture(vector, ies, strength=1.0) -> Node:
     """IES Texture node (nodes.cpp:1213-1300 IESLightNode, svm_ies.h): the
     light's intensity towards `vector` from an IES photometric file (its text,
@@ -781,6 +799,8 @@ def _outputs(node: Node) -> dict:
         return {"Color": "color"}
     if k == "ies_texture":
         return {"Fac": "float"}
+    if k in ("wavelength", "blackbody"):
+        return {"Color": "color"}
     if k in ("displacement", "vector_displacement"):
         return {"Displacement": "vector"}
     if k in ("bump", "set_normal", "bevel"):
@@ -829,6 +849,8 @@ _INPUT_TYPES = {
     "environment_texture": {"Vector": "vector"},
     "sky_texture": {"Vector": "vector"},
     "ies_texture": {"Vector": "vector", "Strength": "float"},
+    "wavelength": {"Wavelength": "float"},
+    "blackbody": {"Temperature": "float"},
     "displacement": {"Height": "float", "Midlevel": "float", "Scale": "float", "Normal": "vector"},
     "normal_map": {"Color": "color", "Strength": "float"},
     "fresnel": {"IOR": "float", "Normal": "vector"},
@@ -1333,6 +1355,21 @@ class NodeCompiler:
             words = words + [self.image_slot(p["model"]["image"]), 0]
         for i in range(0, len(words), 4):
             self.emit(tuple(words[i:i + 4]))
+
+    def _n_wavelength(self, n):  # nodes.cpp:5645-5653 WavelengthNode::compile
+        self.features.add("xyz_to_rgb")
+        self.emit((NODE_WAVELENGTH, self.inp(n, "Wavelength"), self._out_assigned(n, "Color", 3), 0))
+
+    def _n_blackbody(self, n):  # nodes.cpp:5680-5690 BlackbodyNode::compile
+        self.emit((NODE_BLACKBODY, self.inp(n, "Temperature"), self._out_assigned(n, "Color", 3), 0))
+
+    def _out_assigned(self, n, name, width):
+        """compiler.stack_assign(output): a slot even when nothing reads it."""
+        off = self.out(n, name)
+        if off == SVM_STACK_INVALID:
+            off = self.alloc(width)
+            self.temps.append((off, width))
+        return off
 
     def _n_ies_texture(self, n):  # nodes.cpp:1279-1295 IESLightNode::compile (identity texture mapping)
         f = n.params["ies"]

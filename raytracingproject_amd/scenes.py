@@ -211,6 +211,29 @@ def ies_lamps(width=48, height=48, samples=8, ies_files=()) -> sc.Scene:
     return scene
 
 
+def shading_spectral(width=40, height=40, samples=8) -> sc.Scene:
+    """Wavelength and Blackbody nodes (svm_wavelength.h, svm_blackbody.h): the
+    back wall's colour sweeps 350-800 nm over its object X coordinate (both
+    ends outside the table, where the node returns black), the floor's
+    sweeps the same range through Y; a sphere emits the blackbody colour of
+    a temperature rising from 700 K to 13000 K over the sphere (every branch
+    of the piecewise fit and both clamps)."""
+    from . import nodes
+
+    scene = cornell_box(width, height, samples)
+    P = nodes.separate_xyz(nodes.tex_coord()["Object"])
+    lam_x = nodes.math("add", nodes.math("multiply", P["X"], 450.0 / 555.0), 350.0)
+    lam_z = nodes.math("add", nodes.math("multiply", P["Z"], 450.0 / 555.0), 350.0)
+    scene.materials[0] = sc.diffuse(nodes.wavelength(lam_x))
+    scene.materials[1] = sc.diffuse(nodes.wavelength(lam_z))
+    temp = nodes.math("add", nodes.math("multiply", P["Y"], 12300.0 / 140.0), 700.0 - 130.0 * 12300.0 / 140.0)
+    scene.materials.append(sc.emission(nodes.blackbody(temp), 3.0))
+    scene.meshes.append(sc.Mesh(*_ellipsoid((278.0, 200.0, 250.0), (70.0, 70.0, 70.0), 20, 12),
+                                shader=len(scene.materials) - 1))
+    scene.name = "shading_spectral"
+    return scene
+
+
 def cornell_camera(kind: str, width=64, height=64, samples=16) -> sc.Scene:
     """Cornell box through the camera models of kernel_camera.h: "dof"
     (perspective, hexagonal anamorphic aperture), "ortho" (orthographic with a
@@ -324,19 +347,41 @@ def cornell_displace(width=48, height=48, samples=8) -> sc.Scene:
     return scene
 
 
-def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
+def bmw27_standin(width=1280, height=720, samples=128, detail=1.0, materials="basic") -> sc.Scene:
     """BMW27-class stand-in (SURVEY.md §8(d) config BMW): ~0.7M triangles at
     detail=1.0, glossy / glass / diffuse materials, two emissive studio panels,
-    dim constant world."""
+    dim constant world.  materials="production" swaps in the node setups a
+    Blender user would give the same objects (the extended shading kernel):
+    Principled BSDFs with Blender's default multiscatter GGX (clear-coated
+    paint, rough glass, bump-mapped tyres from a noise height, rims with
+    noise-driven roughness) and a checker / noise floor."""
     rng = np.random.default_rng(0x5EED + 1)
-    paint = sc.mix(0.25, sc.diffuse((0.55, 0.06, 0.04)), sc.glossy((0.9, 0.9, 0.9), 0.15))
-    chrome = sc.glossy((0.85, 0.85, 0.88), 0.08)
-    glass_m = sc.glass((0.95, 0.97, 1.0), 0.0, 1.45)
-    tyre = sc.diffuse((0.03, 0.03, 0.03))
-    rim = sc.glossy((0.7, 0.7, 0.72), 0.3)
-    floor = sc.diffuse((0.45, 0.45, 0.45))
-    panel = sc.emission((1.0, 0.97, 0.92), 6.0)
-    plastic = sc.mix(0.5, sc.diffuse((0.08, 0.08, 0.09)), sc.glossy((0.5, 0.5, 0.5), 0.35))
+    if materials == "production":
+        from . import nodes as nd
+
+        grain = nd.noise_texture(scale=40.0, detail=3.0)["Fac"]
+        paint = sc.principled("multiscatter", base_color=(0.55, 0.06, 0.04), metallic=0.3, specular=0.5, roughness=0.25,
+                              clearcoat=0.8, clearcoat_roughness=0.05)
+        chrome = sc.principled("multiscatter", base_color=(0.85, 0.85, 0.88), metallic=1.0, specular=0.5, roughness=0.08)
+        glass_m = sc.principled("multiscatter", base_color=(0.95, 0.97, 1.0), transmission=1.0, roughness=0.1,
+                                ior=1.45)
+        tyre = sc.principled("multiscatter", base_color=(0.03, 0.03, 0.03), roughness=0.7, specular=0.5,
+                             normal=nd.bump(grain, strength=0.4, distance=0.02))
+        rim = sc.principled("multiscatter", base_color=(0.7, 0.7, 0.72), metallic=1.0, specular=0.5,
+                            roughness=nd.map_range(grain, 0.0, 1.0, 0.15, 0.45))
+        ck = nd.checker(nd.tex_coord()["Object"], (0.5, 0.5, 0.5), (0.35, 0.35, 0.37), 0.5)["Color"]
+        floor = sc.principled("multiscatter", base_color=ck, roughness=0.6, specular=0.5)
+        panel = sc.emission((1.0, 0.97, 0.92), 6.0)
+        plastic = sc.principled("multiscatter", base_color=(0.08, 0.08, 0.09), roughness=0.35, specular=0.5)
+    else:
+        paint = sc.mix(0.25, sc.diffuse((0.55, 0.06, 0.04)), sc.glossy((0.9, 0.9, 0.9), 0.15))
+        chrome = sc.glossy((0.85, 0.85, 0.88), 0.08)
+        glass_m = sc.glass((0.95, 0.97, 1.0), 0.0, 1.45)
+        tyre = sc.diffuse((0.03, 0.03, 0.03))
+        rim = sc.glossy((0.7, 0.7, 0.72), 0.3)
+        floor = sc.diffuse((0.45, 0.45, 0.45))
+        panel = sc.emission((1.0, 0.97, 0.92), 6.0)
+        plastic = sc.mix(0.5, sc.diffuse((0.08, 0.08, 0.09)), sc.glossy((0.5, 0.5, 0.5), 0.35))
     materials = [paint, chrome, glass_m, tyre, rim, floor, panel, plastic]
     d = detail
     meshes = []
@@ -387,7 +432,7 @@ def bmw27_standin(width=1280, height=720, samples=128, detail=1.0) -> sc.Scene:
                     fov=math.radians(38.0), nearclip=0.1, farclip=1000.0)
     return sc.Scene(width, height, cam, meshes, materials, world_color=(0.18, 0.2, 0.24),
                     world_strength=0.6, samples=samples, filter_type="blackman_harris",
-                    filter_width=1.5, name="bmw27_standin")
+                    filter_width=1.5, name="bmw27_standin" if materials == "basic" else "bmw27_production")
 
 
 def _cylinder(radius, height, n, caps=True):
@@ -1095,6 +1140,8 @@ CONFIGS = {
     "cornell_instanced": cornell_instanced,
     "cornell_box": cornell_box,
     "bmw27_standin": bmw27_standin,
+    # the bench frame with production node setups (Principled, bump, textures)
+    "bmw27_production": lambda **kw: bmw27_standin(materials="production", **kw),
     "barbershop_standin": barbershop_standin,
     "junkshop_standin": junkshop_standin,
     "classroom_standin": classroom_standin,

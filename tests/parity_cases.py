@@ -42,6 +42,8 @@ CASES = {
        for k in ("preetham", "hosek_wilkie", "nishita_improved")},
     # IES Texture lamps (svm_ies.h, util_ies.cpp parsing / processing on the host)
     "shading_ies": lambda: scenes.ies_lamps(48, 48, 8, ies_files=ies_texts()),
+    # Wavelength / Blackbody nodes (CIE table, piecewise blackbody fit)
+    "shading_spectral": lambda: scenes.shading_spectral(40, 40, 8),
     # transparent BSDF + transparent shadows (kernel_shadow.h record-all, SVM in shadows)
     "transparent_shadows": lambda: scenes.transparent_shadows(48, 48, 8),
     # BSDF closure breadth (closure/bsdf_*.h): diffuse family, microfacets
@@ -191,6 +193,8 @@ def displace_inputs(ds, seed=5):
 SCALE_CASES = {
     "cornell_256": (lambda: scenes.cornell_box(256, 256, 32), None),
     "bmw_full_tile": (lambda: scenes.bmw27_standin(), (576, 328, 64, 64)),
+    # the bench frame with production node setups (Principled multiscatter, bump, textures)
+    "bmw_production_tile": (lambda: scenes.CONFIGS["bmw27_production"](), (576, 328, 64, 64)),
     "bbs_tile": (lambda: scenes.barbershop_standin(), (960, 560, 48, 48)),
     # CLS: 60 area lights, disk-BSSRDF SSS props (1920x1080, 256 spp)
     "cls_tile": (lambda: scenes.classroom_standin(), (1130, 200, 40, 40)),

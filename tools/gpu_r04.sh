@@ -54,4 +54,14 @@ if [[ $MODE == refill ]]; then
     step "bench_refill_${r/,/_}" 600 python bench.py $Q --refill ${r%,*} ${r#*,} "$@"
   done
 fi
+if [[ $MODE == dbg ]]; then
+  # first differing pixels / samples of a parity case: tools/gpu_r04.sh dbg CASE [WIDTH]
+  step dbg 300 python tools/dbg_mismatch.py "$@"
+fi
+if [[ $MODE == configs ]]; then
+  # per-kernel breakdown of the other BASELINE configs (one frame each, whole-frame render)
+  for c in ${CONFIGS:-classroom_standin}; do
+    step "bench_$c" 600 python bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline --tile 0 --other-configs= "$@"
+  done
+fi
 echo done
