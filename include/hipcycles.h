@@ -155,8 +155,11 @@ int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);
  * kernel's kernel/split/kernel_shader_sort.h): before every bounce iteration
  * the closest-hit queue is binned by a key of the ray direction, so the rays
  * of a wave descend the same BVH subtrees.  mode 0 = off, 3 = octant of D
- * (8 bins), 5 = octant x major axis (24 of 32 bins).  Results never depend on
- * the order (every path is a function of its work item alone). */
+ * (8 bins), 5 = octant x major axis (24 of 32 bins).  Mode 8 sorts the
+ * shading queue instead, between the closest-hit and shading launches, by the
+ * shader of each path's hit (kernel_shader_sort.h's key), so a shading wave
+ * runs one material's SVM program.  Results never depend on the order (every
+ * path is a function of its work item alone). */
 int hipcy_set_ray_sort(hipcy_device *dev, int mode);
 /* Iteration budget of the wide-BVH traversal kernels (compaction at traversal
  * granularity): a closest-hit or shadow traversal that has run `first` loop

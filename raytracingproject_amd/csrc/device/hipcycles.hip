@@ -1095,6 +1095,44 @@ __global__ void __launch_bounds__(CY_BLOCK) k_sort_count(CyPathBuffers b, const 
   }
 }
 
+/* Shading-queue sort (hipcy_set_ray_sort mode 8): the same counting sort between
+ * the closest-hit and shading launches, keyed by the shader of each path's hit
+ * (bin 0: misses and paths without a ray; bin 31: curve hits; otherwise 1 +
+ * shader mod 30), so a shading wave runs one SVM program and one closure set
+ * instead of interleaving every material of the scene (instruction cache,
+ * divergence).  Results are unchanged: every path is shaded by its own slot. */
+__global__ void __launch_bounds__(CY_BLOCK) k_shade_sort_count(CyGlobals kg, CyPathBuffers b, const int *queue,
+                                                               const uint *count, unsigned char *keys, uint *hist,
+                                                               int nblocks)
+{
+  __shared__ uint h[CY_SORT_BINS];
+  if (threadIdx.x < CY_SORT_BINS) {
+    h[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int)*count) {
+    const int slot = queue[i];
+    const int pw = __float_as_int(b.isect[slot].w);
+    uint key = 0;
+    if (pw >= 0) {
+      const int prim = pw & ~CY_PRIM_TIE;
+      if (kg.have_curves && b.isect_type[slot] != PRIMITIVE_TRIANGLE) {
+        key = CY_SORT_BINS - 1;
+      }
+      else {
+        key = 1u + ((uint)kg.__tri_shader[kg.__prim_index[prim]] & SHADER_MASK) % (CY_SORT_BINS - 2);
+      }
+    }
+    keys[i] = (unsigned char)key;
+    atomicAdd(&h[key], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < CY_SORT_BINS) {
+    hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  }
+}
+
 /* Exclusive scan of m histogram entries in place, one workgroup (m is at most
  * bins x blocks of a lane, a few hundred thousand words). */
 __global__ void __launch_bounds__(1024) k_sort_scan(uint *hist, int m)
@@ -2157,8 +2195,8 @@ int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle)
 
 int hipcy_set_ray_sort(hipcy_device *dev, int mode)
 {
-  if (mode != 0 && mode != 3 && mode != 5) {
-    return set_error(dev, "set_ray_sort: mode must be 0, 3 or 5");
+  if (mode != 0 && mode != 3 && mode != 5 && mode != 8) {
+    return set_error(dev, "set_ray_sort: mode must be 0, 3, 5 or 8");
   }
   dev->ray_sort = mode;
   return 0;
@@ -2828,7 +2866,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   /* bounce iterations: bin the closest queue by ray direction (counting sort
    * into sort_queue); closest and shade then read the sorted queue */
   const int *queue_in = ln.q[qa];
-  if (dev->ray_sort && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
+  if ((dev->ray_sort == 3 || dev->ray_sort == 5) && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
     const int nblocks = (int)grid.x;
     const int K = dev->ray_sort == 3 ? 8 : CY_SORT_BINS;
     uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
@@ -2919,9 +2957,22 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.b, s));
   }
+  const int *shade_queue = queue_in;
+  if (dev->ray_sort == 8 && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
+    /* shading-queue sort by the hit's shader (k_shade_sort_count) */
+    const int nblocks = (int)grid.x;
+    uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
+    unsigned char *keys = dev->sort_key + ln.slot_base;
+    int *sorted = dev->sort_queue + ln.slot_base;
+    hipLaunchKernelGGL(k_shade_sort_count, grid, block, 0, s, kg, dev->bufs, queue_in, ln.cnt + qa, keys, hist,
+                       nblocks);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, CY_SORT_BINS * nblocks);
+    hipLaunchKernelGGL(k_sort_scatter<5>, grid, block, 0, s, queue_in, ln.cnt + qa, keys, hist, nblocks, sorted);
+    shade_queue = sorted;
+  }
   cy_launch_shade(dev->shade_closures, dev->shade_tex, dev->use_volumes, grid, block, s, kg,
                   dev->bufs, ln.tile, cam_n,
-                  ln.slot_base, queue_in, ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
+                  ln.slot_base, shade_queue, ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
   if (prof) {
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }

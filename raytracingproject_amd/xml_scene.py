@@ -186,6 +186,35 @@ NODE_SOCKETS = {
     "gradient_texture": {"type": ("e", "linear"), "vector": ("n", None)},
     "noise_texture": {"dimensions": ("e", "3D"), "vector": ("n", None), "w": ("f", 0.0), "scale": ("f", 1.0),
                       "detail": ("f", 2.0), "roughness": ("f", 0.5), "distortion": ("f", 0.0)},
+    "principled_bsdf": {"distribution": ("e", "Multiscatter GGX"), "subsurface_method": ("e", "burley"),
+                        "base_color": ("c", _C08), "subsurface_color": ("c", _C08), "metallic": ("f", 0.0),
+                        "subsurface": ("f", 0.0), "subsurface_radius": ("c", (0.1, 0.1, 0.1)),
+                        "specular": ("f", 0.0), "roughness": ("f", 0.5), "specular_tint": ("f", 0.0),
+                        "anisotropic": ("f", 0.0), "sheen": ("f", 0.0), "sheen_tint": ("f", 0.0),
+                        "clearcoat": ("f", 0.0), "clearcoat_roughness": ("f", 0.03), "ior": ("f", 0.0),
+                        "transmission": ("f", 0.0), "transmission_roughness": ("f", 0.0),
+                        "anisotropic_rotation": ("f", 0.0), "emission": ("c", _Z3), "alpha": ("f", 1.0),
+                        "normal": ("n", None), "clearcoat_normal": ("n", None), "tangent": ("n", None)},
+    "subsurface_scattering": {"color": ("c", _C08), "normal": ("n", None), "falloff": ("e", "burley"),
+                              "scale": ("f", 0.01), "radius": ("c", (0.1, 0.1, 0.1)), "sharpness": ("f", 0.0),
+                              "texture_blur": ("f", 1.0)},
+    "wavelength": {"wavelength": ("f", 500.0)},
+    "blackbody": {"temperature": ("f", 1200.0)},
+    "sky_texture": {"type": ("e", "nishita_improved"), "vector": ("n", None), "sun_direction": ("c", (0.0, 0.0, 1.0)),
+                    "turbidity": ("f", 2.2), "ground_albedo": ("f", 0.3)},
+    "ies_light": {"ies": ("s", None), "filename": ("s", None), "strength": ("f", 1.0), "vector": ("n", None)},
+    "bump": {"invert": ("b", False), "use_object_space": ("b", False), "height": ("f", 1.0),
+             "normal": ("n", None), "strength": ("f", 1.0), "distance": ("f", 0.1)},
+    "ambient_occlusion": {"samples": ("i", 16), "color": ("c", (1.0, 1.0, 1.0)), "distance": ("f", 1.0),
+                          "normal": ("n", None), "inside": ("b", False), "only_local": ("b", False)},
+    "bevel": {"samples": ("i", 4), "radius": ("f", 0.05), "normal": ("n", None)},
+    "wireframe": {"use_pixel_size": ("b", False), "size": ("f", 0.01)},
+    "clamp": {"type": ("e", "minmax"), "value": ("f", 1.0), "min": ("f", 0.0), "max": ("f", 1.0)},
+    "map_range": {"type": ("e", "linear"), "value": ("f", 1.0), "from_min": ("f", 0.0), "from_max": ("f", 1.0),
+                  "to_min": ("f", 0.0), "to_max": ("f", 1.0), "steps": ("f", 4.0)},
+    "light_falloff": {"strength": ("f", 100.0), "smooth": ("f", 0.0)},
+    "white_noise_texture": {"dimensions": ("e", "3D"), "vector": ("n", None), "w": ("f", 0.0)},
+    "object_info": {},
     "output": {"surface": ("x", None), "volume": ("x", None)},
 }
 # output socket identifier (lower case) -> builder key per node type
@@ -202,6 +231,12 @@ NODE_OUTPUTS = {
     "mix": ("color",), "invert": ("color",), "gamma": ("color",), "hsv": ("color",), "brightness_contrast": ("color",),
     "separate_xyz": ("x", "y", "z"), "combine_xyz": ("vector",),
     "checker_texture": ("color", "fac"), "gradient_texture": ("color", "fac"), "noise_texture": ("fac", "color"),
+    "principled_bsdf": ("bsdf",), "subsurface_scattering": ("bssrdf",), "wavelength": ("color",),
+    "blackbody": ("color",), "sky_texture": ("color",), "ies_light": ("fac",), "bump": ("normal",),
+    "ambient_occlusion": ("color", "ao"), "bevel": ("normal",), "wireframe": ("fac",), "clamp": ("result",),
+    "map_range": ("result",), "light_falloff": ("quadratic", "linear", "constant"),
+    "white_noise_texture": ("value", "color"),
+    "object_info": ("location", "color", "object_index", "material_index", "random"),
 }
 
 
@@ -215,8 +250,9 @@ class _GraphNode:
 class ShaderGraph:
     """One `<shader>` / `<background>` element's nodes and links."""
 
-    def __init__(self, el, where: str):
+    def __init__(self, el, where: str, base: str = "."):
         self.where = where
+        self.base = base  # directory of the XML file (ies_light filename)
         self.nodes = {"output": _GraphNode("output", {})}
         self._cache = {}
         for child in el:
@@ -274,7 +310,7 @@ class ShaderGraph:
             return _bool(raw)
         if kind == "i":
             return int(raw)
-        if kind == "e":
+        if kind in ("e", "s"):
             return raw
         raise ValueError(f"{self.where}: {node.kind}.{ident} cannot be set by value")
 
@@ -366,7 +402,91 @@ class ShaderGraph:
             node = nodes.noise_texture(g("vector"), w=g("w"), scale=g("scale"), detail=g("detail"),
                                        roughness=g("roughness"), distortion=g("distortion"), dimensions=dims)
             return node[out.capitalize()]
+        if k == "principled_bsdf":
+            return self._principled(g)
+        if k == "subsurface_scattering":
+            if g("falloff") not in sc.SUBSURFACE_FALLOFFS:
+                raise ValueError(f"{self.where}: subsurface_scattering falloff {g('falloff')!r}")
+            return sc.subsurface(g("color"), scale=g("scale"), radius=g("radius"), falloff=g("falloff"),
+                                 texture_blur=g("texture_blur"), sharpness=g("sharpness"), normal=g("normal"))
+        if k == "wavelength":
+            return nodes.wavelength(g("wavelength"))
+        if k == "blackbody":
+            return nodes.blackbody(g("temperature"))
+        if k == "sky_texture":
+            # the Hosek-Wilkie and Nishita models need intern/sky's precomputation on the host
+            if g("type") != "preetham":
+                raise ValueError(f"{self.where}: sky_texture type {g('type')!r}: only preetham is computed by the "
+                                 "XML reader's host")
+            return nodes.sky_texture(self._vector(g, "generated"), "preetham", sun_direction=g("sun_direction"),
+                                     turbidity=g("turbidity"))["Color"]
+        if k == "ies_light":
+            text = g("ies")
+            if text is None:
+                fn = g("filename")
+                if fn is None:
+                    raise ValueError(f"{self.where}: ies_light without ies or filename")
+                with open(os.path.join(self.base, fn)) as f:
+                    text = f.read()
+            return nodes.ies_texture(self._vector(g, "normal"), text, strength=g("strength"))["Fac"]
+        if k == "bump":
+            return nodes.bump(g("height"), strength=g("strength"), distance=g("distance"), invert=g("invert"),
+                              normal=g("normal"), object_space=g("use_object_space"))
+        if k == "ambient_occlusion":
+            node = nodes.ambient_occlusion(g("color"), g("distance"), normal=g("normal"), samples=g("samples"),
+                                           inside=g("inside"), only_local=g("only_local"))
+            return node["AO" if out == "ao" else "Color"]
+        if k == "bevel":
+            return nodes.bevel(g("radius"), normal=g("normal"), samples=g("samples"))
+        if k == "wireframe":
+            return nodes.wireframe(g("size"), use_pixel_size=g("use_pixel_size"))
+        if k == "clamp":
+            return nodes.clamp(g("value"), g("min"), g("max"), kind=g("type"))
+        if k == "map_range":
+            return nodes.map_range(g("value"), g("from_min"), g("from_max"), g("to_min"), g("to_max"),
+                                   g("steps"), kind=g("type"))
+        if k == "light_falloff":
+            return nodes.light_falloff(g("strength"), g("smooth"))[out.capitalize()]
+        if k == "white_noise_texture":
+            dims = {"1D": 1, "2D": 2, "3D": 3, "4D": 4}.get(g("dimensions"))
+            if dims is None:
+                raise ValueError(f"{self.where}: white_noise_texture dimensions {g('dimensions')!r}")
+            return nodes.white_noise_texture(g("vector"), w=g("w"), dimensions=dims)[out.capitalize()]
+        if k == "object_info":
+            name = {"location": "Location", "color": "Color", "object_index": "Object Index",
+                    "material_index": "Material Index", "random": "Random"}[out]
+            return nodes.object_info()[name]
         raise ValueError(f"{self.where}: node type {k!r} has no builder")
+
+    @staticmethod
+    def _vector(g, link):
+        """A texture vector input's default link (graph.cpp default_inputs:
+        LINK_TEXTURE_GENERATED / LINK_TEXTURE_NORMAL)."""
+        v = g("vector")
+        if v is not None:
+            return v
+        return nodes.tex_coord()["Generated" if link == "generated" else "Normal"]
+
+    def _principled(self, g):
+        """PrincipledBsdfNode (nodes.cpp:2665-2850) with its expand(): Alpha
+        below 1 (or linked) becomes a mix with a transparent BSDF; Emission
+        would become an add closure, which the scene model does not have."""
+        dist = {"GGX": "ggx", "Multiscatter GGX": "multiscatter"}.get(g("distribution"))
+        if dist is None:
+            raise ValueError(f"{self.where}: principled_bsdf distribution {g('distribution')!r}")
+        method = g("subsurface_method")
+        em = g("emission")
+        if nodes.is_linked(em) or tuple(em) != (0.0, 0.0, 0.0):
+            raise ValueError(f"{self.where}: principled_bsdf emission (an add closure) is not supported")
+        params = {key: g(key) for key in sc.PRINCIPLED_DEFAULTS}
+        for key in sc.PRINCIPLED_VECTORS:
+            if g(key) is not None:
+                params[key] = g(key)
+        bsdf = sc.principled(dist, subsurface_method=method, **params)
+        alpha = g("alpha")
+        if nodes.is_linked(alpha) or float(alpha) != 1.0:
+            return sc.mix(alpha, sc.transparent((1.0, 1.0, 1.0)), bsdf)
+        return bsdf
 
     def shader(self):
         """(surface closure or None, volume closure or None) at the output node."""
@@ -440,9 +560,9 @@ class XMLReader:
                 name = el.attrib.get("name")
                 if not name:
                     raise ValueError("shader without a name")
-                self.shaders[name] = ShaderGraph(el, f"shader {name!r}").shader()
+                self.shaders[name] = ShaderGraph(el, f"shader {name!r}", st.base).shader()
             elif tag == "background":
-                self.world = ShaderGraph(el, "background").shader()
+                self.world = ShaderGraph(el, "background", st.base).shader()
             elif tag == "mesh":
                 self.read_mesh(st, el)
             elif tag == "light":

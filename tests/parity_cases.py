@@ -112,6 +112,9 @@ CASES = {
     # (app/cycles_xml.cpp: transforms, state shaders, polygon meshes with UVs,
     # shader graphs with connects, lights with their own shaders, an include)
     "xml_cornell": lambda: xml_scene.read_file(os.path.join(SCENES, "cornell.xml"), samples=8),
+    # XML node breadth: Principled (alpha, bump), SSS node, wavelength / blackbody,
+    # AO, wireframe, object info, clamp / map range, an ies_light lamp, Preetham sky
+    "xml_nodes": lambda: xml_scene.read_file(os.path.join(SCENES, "nodes.xml"), samples=8),
 }
 def ies_texts():
     """The two IES photometric files of the shading_ies case (tests/scenes)."""

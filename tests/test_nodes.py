@@ -123,7 +123,7 @@ def test_constant_emission_detection():
 
 @pytest.mark.gpu
 def test_unimplemented_node_rejected_at_load_kernels():
-    """A node the device does not run (here NODE_IES, svm_types.h, patched over a
+    """A node the device does not run (here NODE_TEX_VOXEL, svm_types.h, patched over a
     Math node of a compiled program) is rejected by the program scan before
     any render, naming the node."""
     from raytracingproject_amd.device import DeviceError, HIPDevice
@@ -133,10 +133,10 @@ def test_unimplemented_node_rejected_at_load_kernels():
     ds = sc.compile_scene(s)
     prog = ds.arrays["__svm_nodes"]
     k = int(np.flatnonzero(prog[:, 0] == 42)[0])  # NODE_MATH
-    prog[k, 0] = 67  # NODE_IES
+    prog[k, 0] = 87  # NODE_TEX_VOXEL
     dev = HIPDevice(0)
     try:
-        with pytest.raises(DeviceError, match="SVM node 67 is not implemented"):
+        with pytest.raises(DeviceError, match="SVM node 87 is not implemented"):
             dev.upload_scene(ds)
     finally:
         dev.close()

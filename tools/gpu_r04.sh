@@ -64,4 +64,18 @@ if [[ $MODE == configs ]]; then
     step "bench_$c" 600 python bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline --tile 0 --other-configs= "$@"
   done
 fi
+if [[ $MODE == sortcmp ]]; then
+  # shading-queue sort (ray_sort 8) against unsorted, headline + other configs
+  step bench_sort0 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --tile 0 "$@"
+  step bench_sort8 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --tile 0 --ray-sort 8 "$@"
+fi
+if [[ $MODE == libtest ]]; then
+  # parity tests against a variant build: LIB=name tools/gpu_r04.sh libtest -k expr
+  step "pytest_lib_$LIB" 600 env HIPCY_DEVICE_LIB=$PWD/raytracingproject_amd/libhipcycles-$LIB.so \
+    python -u -m pytest -v -m gpu --maxfail=10 --timeout 300 --timeout-method thread tests/test_gpu_parity.py "$@"
+fi
+if [[ $MODE == libbench ]]; then
+  step "bench_lib_$LIB" 600 env HIPCY_DEVICE_LIB=$PWD/raytracingproject_amd/libhipcycles-$LIB.so \
+    python bench.py --steps 5 --warmup 1 --no-cpu-baseline --tile 0 --other-configs= "$@"
+fi
 echo done
