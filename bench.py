@@ -50,9 +50,10 @@ def parse(argv=None):
     p.add_argument("--save", default=None, help="write the rank-0 film as PNG")
     p.add_argument("--bvh-width", type=int, default=4, choices=(2, 4, 8),
                    help="4 (default) / 8: device-widened wide BVH; 2: the bound BVH2 as is")
-    p.add_argument("--ray-sort", type=int, default=0, choices=(0, 3, 5, 8),
+    p.add_argument("--ray-sort", type=int, default=-1, choices=(-1, 0, 3, 5, 8),
                    help="bin the closest queue by ray direction per bounce: 0 off, 3 octant, 5 octant x axis; "
-                        "8: bin the shading queue by the hit's shader")
+                        "8: bin the shading queue by the hit's shader; -1 (default): the device's automatic "
+                        "choice (8 for scenes on the extended shading kernel, else 0)")
     p.add_argument("--refill", type=int, nargs=2, default=(0, 16), metavar=("ROUNDS", "MIN_IDLE"),
                    help="lane refill of the closest-hit traversal (0 = off)")
     p.add_argument("--trav-budget", type=int, nargs=2, default=(0, 0), metavar=("FIRST", "SECOND"),

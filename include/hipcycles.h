@@ -158,8 +158,10 @@ int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes);
  * (8 bins), 5 = octant x major axis (24 of 32 bins).  Mode 8 sorts the
  * shading queue instead, between the closest-hit and shading launches, by the
  * shader of each path's hit (kernel_shader_sort.h's key), so a shading wave
- * runs one material's SVM program.  Results never depend on the order (every
- * path is a function of its work item alone). */
+ * runs one material's SVM program.  -1 (the default) picks mode 8 for scenes
+ * that run the extended shading kernel (texture / Principled / BSSRDF nodes)
+ * without curves, else 0.  Results never depend on the order (every path is a
+ * function of its work item alone). */
 int hipcy_set_ray_sort(hipcy_device *dev, int mode);
 /* Iteration budget of the wide-BVH traversal kernels (compaction at traversal
  * granularity): a closest-hit or shadow traversal that has run `first` loop

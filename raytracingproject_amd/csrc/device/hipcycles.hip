@@ -1489,7 +1489,7 @@ struct hipcy_device {
 
   /* closest-queue sorting (hipcy_set_ray_sort): sorted queue, per-ray bin and
    * the per-lane bin x block histogram / scanned offsets */
-  int ray_sort = 0;
+  int ray_sort = -1; /* -1: automatic (shading-queue sort for the extended shading kernel) */
   int *sort_queue = nullptr;
   unsigned char *sort_key = nullptr;
   uint *sort_hist = nullptr;
@@ -2195,8 +2195,8 @@ int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle)
 
 int hipcy_set_ray_sort(hipcy_device *dev, int mode)
 {
-  if (mode != 0 && mode != 3 && mode != 5 && mode != 8) {
-    return set_error(dev, "set_ray_sort: mode must be 0, 3, 5 or 8");
+  if (mode != -1 && mode != 0 && mode != 3 && mode != 5 && mode != 8) {
+    return set_error(dev, "set_ray_sort: mode must be -1, 0, 3, 5 or 8");
   }
   dev->ray_sort = mode;
   return 0;
@@ -2844,6 +2844,19 @@ struct PassLane {
   bool stream = false; /* tile stream lane: also reduce the live paths' smallest item */
 };
 
+/* The queue sort in effect: the requested mode, or (automatic, -1) the
+ * shading-queue sort when the scene runs the extended shading kernel without
+ * curves -- measured: production-material BMW 272 -> 423, CLS 93 -> 116
+ * Msamples/s, while the plain kernel's scenes lose by it (BMW 1241 -> 1207,
+ * BBS 245 -> 187) and the hair scene is flat (profiles/r04/sort_*.json). */
+static int effective_sort(const hipcy_device *dev)
+{
+  if (dev->ray_sort >= 0) {
+    return dev->ray_sort;
+  }
+  return (dev->shade_tex && !dev->data_host.bvh.have_curves) ? 8 : 0;
+}
+
 /* One iteration of a lane: closest -> shade -> shadow.  The lane's first
  * iteration is its camera launch (cam_n > 0): slot slot_base + i starts work
  * item item_base + i, and the closest and shade kernels generate its camera
@@ -2866,16 +2879,18 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   /* bounce iterations: bin the closest queue by ray direction (counting sort
    * into sort_queue); closest and shade then read the sorted queue */
   const int *queue_in = ln.q[qa];
-  if ((dev->ray_sort == 3 || dev->ray_sort == 5) && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
+  /* sort buffers exist only where a pass sized them (path_trace_pass) */
+  const int sort = (dev->sort_queue && dev->sort_capacity >= dev->capacity) ? effective_sort(dev) : 0;
+  if ((sort == 3 || sort == 5) && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
     const int nblocks = (int)grid.x;
-    const int K = dev->ray_sort == 3 ? 8 : CY_SORT_BINS;
+    const int K = sort == 3 ? 8 : CY_SORT_BINS;
     uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
     unsigned char *keys = dev->sort_key + ln.slot_base;
     int *sorted = dev->sort_queue + ln.slot_base;
-    hipLaunchKernelGGL(dev->ray_sort == 3 ? k_sort_count<3> : k_sort_count<5>, grid, block, 0, s, dev->bufs,
+    hipLaunchKernelGGL(sort == 3 ? k_sort_count<3> : k_sort_count<5>, grid, block, 0, s, dev->bufs,
                        ln.q[qa], ln.cnt + qa, keys, hist, nblocks);
     hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, K * nblocks);
-    hipLaunchKernelGGL(dev->ray_sort == 3 ? k_sort_scatter<3> : k_sort_scatter<5>, grid, block, 0, s, ln.q[qa],
+    hipLaunchKernelGGL(sort == 3 ? k_sort_scatter<3> : k_sort_scatter<5>, grid, block, 0, s, ln.q[qa],
                        ln.cnt + qa, keys, hist, nblocks, sorted);
     queue_in = sorted;
   }
@@ -2958,7 +2973,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     HIP_CHECK(dev, hipEventRecord(p.b, s));
   }
   const int *shade_queue = queue_in;
-  if (dev->ray_sort == 8 && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
+  if (sort == 8 && cam_n == 0 && ln.n_active >= 4 * CY_BLOCK) {
     /* shading-queue sort by the hit's shader (k_shade_sort_count) */
     const int nblocks = (int)grid.x;
     uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
@@ -3045,7 +3060,7 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
   const int max_lanes = (dev->profiling & 1) ? 1 : CY_LANES;
   const int lanes = (int)std::max<size_t>(1, std::min<size_t>(max_lanes, n_slots / (4 * CY_BLOCK)));
   tile.samples_out = dev->records;
-  if (dev->ray_sort && dev->sort_capacity < dev->capacity) {
+  if (effective_sort(dev) && dev->sort_capacity < dev->capacity) {
     const size_t cap = dev->capacity;
     if (dev->sort_queue) HIP_CHECK(dev, hipFree(dev->sort_queue));
     if (dev->sort_key) HIP_CHECK(dev, hipFree(dev->sort_key));

@@ -1137,10 +1137,10 @@ CY_FN cfloat3 background_eval_svm(const hc_KernelData *data,
  * closure array in `mem` is left intact; then shader_emissive_eval
  * (kernel_shader.h, emissive_simple_eval).  The caller flips ls.Ng to the
  * emitter's backfacing-corrected normal (ls->Ng = emission_sd->Ng), which is
- * the same flip the constant branch makes.  Inlined: as an out-of-line call
- * it raised the _tex shading kernels' scratch from 1.7 to 2.9 KB per lane and
- * their renders went wrong on the GPU (non-finite films) while the host
- * build stayed exact. */
+ * the same flip the constant branch makes.  Inlined by default.  This
+ * out-of-line form (CY_EMISSIVE_OOL) is bit-exact on the GPU;
+ * the r03 form that produced non-finite films wrote ls->Ng through a pointer
+ * into the caller's private frame. */
 #ifdef CY_EMISSIVE_OOL /* diagnostic build (build.py --variant ... -DCY_EMISSIVE_OOL): the out-of-line form */
 CY_NOINLINE
 #else

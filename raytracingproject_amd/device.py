@@ -126,7 +126,8 @@ class HIPDevice:
     def set_ray_sort(self, mode: int) -> None:
         """Bin the closest-hit queue by ray direction before every bounce
         iteration: 0 off, 3 octant, 5 octant x major axis; 8 sorts the shading
-        queue by the hit's shader instead (hipcy_set_ray_sort)."""
+        queue by the hit's shader instead; -1 (the device default) picks 8
+        for scenes on the extended shading kernel (hipcy_set_ray_sort)."""
         self._check(self.lib.hipcy_set_ray_sort(self.h, int(mode)))
 
     def set_traversal_budget(self, first: int, second: int | None = None) -> None:

@@ -221,7 +221,7 @@ def test_render_with_ray_sort_matches_reference(name, mode, device):
     try:
         buf = device.render()
     finally:
-        device.set_ray_sort(0)
+        device.set_ray_sort(-1)
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), name
 
 
