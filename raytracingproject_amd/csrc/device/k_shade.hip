@@ -34,8 +34,13 @@
 #define CY_CAT2(a, b) a##b
 #define CY_CAT(a, b) CY_CAT2(a, b)
 
+/* Occupancy target: the plain kernels of 1-2 closures keep 4 waves per SIMD
+ * (128 VGPRs); the extended kernels of up to 8 closures are allocated for 2
+ * waves (256 VGPRs), which removes most of their spills: production-material
+ * BMW 422 -> 456, CLS 117 -> 128 Msamples/s against the unconstrained
+ * allocation (profiles/r04/shade_waves_*.json); the plain kernels lose at 2. */
 #ifndef CY_SHADE_MIN_WAVES
-#  define CY_SHADE_MIN_WAVES (CY_MAX_CLOSURE <= 2 ? 4 : 1)
+#  define CY_SHADE_MIN_WAVES ((CY_SVM_TEX && CY_MAX_CLOSURE <= 8) ? 2 : (CY_MAX_CLOSURE <= 2 ? 4 : 1))
 #endif
 __global__ void __launch_bounds__(CY_BLOCK, CY_SHADE_MIN_WAVES) CY_CAT(k_shade_, CY_SHADE_VARIANT)(CyGlobals kg,
                                                      CyPathBuffers b,
