@@ -101,7 +101,7 @@ def test_background_graph_and_background_light():
 
 
 @pytest.mark.parametrize("body, msg", [
-    ('<shader name="a"><bump name="b" /></shader>', "not supported"),
+    ('<shader name="a"><voronoi_texture name="b" /></shader>', "not supported"),
     ('<shader name="a"><diffuse_bsdf name="d" colour="1 1 1" /></shader>', "unsupported sockets"),
     ('<shader name="a"><diffuse_bsdf name="d" /><connect from="d closure" to="output surface" /></shader>',
      "unknown output socket"),
