@@ -71,8 +71,12 @@ def parse(argv=None):
     p.add_argument("--render", default="frame", choices=("frame", "stream"),
                    help="frame: the whole frame as one RenderTile (headline); stream: the frame's --tile RenderTiles "
                         "fed to hipcy_render_feed (1 GPU; for profiling the plugin's path)")
-    p.add_argument("--stream-hold-sweep", default="",
-                   help="comma-separated extra holds for more tile-stream legs (measurement)")
+    p.add_argument("--stream-hold-sweep", default="33554432",
+                   help="comma-separated extra holds for more tile-stream legs (default: 2^25, the share the "
+                        "plugin gives each of several devices on one queue)")
+    p.add_argument("--scaling-proxy", default="2,4,8",
+                   help="single-GPU proxy of strong scaling (rank 0, N=1 only): for each N, rank 0's rows of an "
+                        "N-way row split rendered alone and timed; empty disables")
     p.add_argument("--profile-frame", action="store_true",
                    help="only render the instrumented single-lane frame (for rocprofv3 PMC passes)")
     p.add_argument("--other-configs", default="bmw27_production,barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
@@ -286,6 +290,10 @@ def main():
         if args.tile_batch != 1:
             tile_leg.append(tile_mode(dev, ds, args.tile, 1, 0, film))
 
+    proxy = None
+    if world == 1 and args.scaling_proxy:
+        proxy = scaling_proxy(dev, ds, [int(n) for n in args.scaling_proxy.split(",") if n], value)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ds, args.cpu_seconds)
@@ -336,6 +344,7 @@ def main():
             "film_checksum": float(np.float64(film[..., :4].sum())) if film is not None else None,
             "roofline": roofline,
             "tile_mode": tile_leg,
+            "scaling_proxy": proxy,
             "other_configs": others,
             "cpu_baseline": cpu,
         }
@@ -487,7 +496,7 @@ def tile_mode(dev, ds, tile, batch, hold=0, film=None):
     res = {"tile": tile, "tiles": len(tiles), "mode": "stream" if batch == 0 else f"{batch} tile(s) per pass",
            "value": round(W * H * S / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(1e3 * dt, 3)}
     if batch == 0:
-        res["hold_pixel_samples"] = hold or (1 << 25)
+        res["hold_pixel_samples"] = hold or "device default: the slot pool in flight plus as much in reserve"
         st = dev.stats()
         res["wavefront_iterations"] = int(st["iterations"])
     if film is not None:
@@ -496,6 +505,50 @@ def tile_mode(dev, ds, tile, batch, hold=0, film=None):
             full[y:y + h, x:x + w] = b.numpy()
         res["film_bit_exact_vs_whole_frame"] = bool(np.array_equal(full.view(np.uint32), film.view(np.uint32)))
     return res
+
+
+def scaling_proxy(dev, ds, ns, full_value, frames=3):
+    """Per-GPU throughput at 1/N of the frame, measured on this one GPU: rank
+    0's rows of an N-way interleaved row split (shard.RowShard, what
+    `bench.py --gpus N` gives each rank) rendered alone, `frames` timed frames
+    after a warm one, the film copied to the host as in the headline step.
+    Strong scaling at N GPUs cannot exceed N x this rate / the full-frame rate
+    (the ratio reported as `per_gpu_vs_full`); the rows of the other ranks cost
+    the same within a few per cent (every rank gets every N-th row)."""
+    import torch
+
+    from raytracingproject_amd.shard import RowShard
+
+    W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
+    out = {}
+    for n in ns:
+        if n < 2:
+            continue
+        sh = RowShard(0, n, W, H)
+        buf = torch.zeros((sh.rows, W, PS), dtype=torch.float32, device="cuda")
+        host = torch.empty((sh.rows, W, PS), dtype=torch.float32, pin_memory=True)
+
+        class _Buf:
+            ptr = buf.data_ptr()
+
+        def frame():
+            buf.zero_()
+            dev.render_tile(_Buf, sh.tile(), 0, S, sh.offset, sh.stride, y_step=sh.y_step)
+            host.copy_(buf)
+
+        frame()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            frame()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / frames
+        per_gpu = sh.rows * W * S / dt / 1e6
+        out[str(n)] = {"rows": sh.rows, "ms_per_frame": round(1e3 * dt, 3), "per_gpu_value": round(per_gpu, 3),
+                       "per_gpu_vs_full": round(per_gpu / full_value, 4),
+                       "wavefront_iterations": int(dev.stats()["iterations"])}
+        del buf, host
+    return {"unit": "Msamples/s", "method": "rank 0's rows of an N-way row split on one GPU", "legs": out}
 
 
 def other_config(spec, device_index, args):

@@ -188,12 +188,20 @@ int hipcy_path_trace_tiles(hipcy_device *dev, const hipcy_work_tile *tiles, int 
 /* Tile stream: the RENDER task's acquire_tile / release_tile loop with the
  * tiles fed to one running wavefront (hipcy_render_feed).  acquire fills
  * *tile (and an opaque tag) and returns 1, or 0 when the queue is empty;
- * release is called once every sample of the tile is in its buffer, from the
- * thread that called hipcy_render_feed.  cancelled (may be NULL) stops the
- * acquisition; tiles already acquired are finished.  hold bounds the
- * pixel-samples the device has acquired but not finished (0: the device's
- * hipcy_set_stream_hold value), so devices sharing one queue each take tiles
- * only as fast as they finish them. */
+ * release is called once for every acquired tile, from the thread that called
+ * hipcy_render_feed: when every sample of the tile is in its buffer, or, if
+ * the stream fails (a kernel error, an invalid or oversized tile), before
+ * hipcy_render_feed returns its error -- hipcy_error() is then already set, so
+ * the callback can tell an unfinished tile (CUDADevice::thread_run releases
+ * every tile it acquired, device_cuda_impl.cpp:2361-2388).  cancelled (may be
+ * NULL) stops the acquisition; tiles already acquired are finished.  hold is
+ * the device's target of acquired-but-unfinished pixel-samples (0: the
+ * hipcy_set_stream_hold value): tiles are acquired only while the unclaimed
+ * work is below it.  It is approximate: tiles are taken whole (or in sample
+ * chunks of a quarter of the record ring), and a tile stays held until its
+ * last path ends, so a device may hold up to about twice `hold` (more with
+ * holds of a few tiles).  Devices sharing one queue each take tiles only as
+ * fast as they finish them. */
 typedef struct hipcy_tile_feed {
   void *user;
   int (*acquire)(void *user, hipcy_work_tile *tile, uint64_t *tag);
@@ -202,7 +210,9 @@ typedef struct hipcy_tile_feed {
   uint64_t hold;
 } hipcy_tile_feed;
 int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed);
-/* Default hold of tile streams, in pixel-samples (2^25). */
+/* Default hold of tile streams, in pixel-samples (initially 0: twice the slot
+ * pool of hipcy_set_slots, i.e. every slot in flight and as much in reserve,
+ * what a device alone on the queue wants).  0 keeps the value. */
 int hipcy_set_stream_hold(hipcy_device *dev, uint64_t pixel_samples);
 int hipcy_synchronize(hipcy_device *dev);
 int hipcy_get_stats(const hipcy_device *dev, hipcy_stats *out);

@@ -23,6 +23,7 @@
  * against the reference headers by tests/test_integration.py.
  */
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <deque>
 #include <vector>
@@ -51,6 +52,7 @@ class HIPCyclesDevice : public Device {
   HIPCyclesDevice(DeviceInfo &info, Stats &stats, Profiler &profiler, bool background)
       : Device(info, stats, profiler, background), dev_(hipcy_create(info.num))
   {
+    live_devices_++;
     if (dev_ == nullptr) {
       set_error(string_printf("HIP device %d: %s", info.num, hipcy_global_error()));
     }
@@ -63,6 +65,7 @@ class HIPCyclesDevice : public Device {
   {
     task_pool_.cancel();
     hipcy_destroy(dev_);
+    live_devices_--;
   }
 
   /* device.h:353 — the host keeps building Cycles' BVH2; the device widens it */
@@ -78,14 +81,17 @@ class HIPCyclesDevice : public Device {
   }
 
   /* device.h:375 — features the kernels do not implement are refused here, and
-   * once more against the uploaded KernelData before the first render (hair
-   * curves, random-walk subsurface scattering and volumes are implemented;
-   * hipcy_load_kernels checks their variants: curve shapes, BSSRDF falloffs,
-   * volume_decoupled, camera in volume) */
+   * once more against the uploaded KernelData and SVM programs before the first
+   * render (hair curves, subsurface scattering, volumes and the shader
+   * ray-tracing nodes are implemented; hipcy_load_kernels checks their
+   * variants: curve shapes, BSSRDF falloffs, volume_decoupled, camera in
+   * volume, shadow catchers).  use_shader_raytrace is what
+   * ShaderManager::get_requested_features sets for any Ambient Occlusion or
+   * Bevel node (render/shader.cpp:724-725): those nodes run on the device. */
   bool load_kernels(const DeviceRequestedFeatures &f) override
   {
     if (f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_integrator_branched ||
-        f.use_patch_evaluation || f.use_shader_raytrace || f.use_denoising) {
+        f.use_patch_evaluation || f.use_denoising) {
       set_error("HIP device: requested features are not implemented (" + f.get_build_options() + ")");
       return false;
     }
@@ -261,9 +267,26 @@ class HIPCyclesDevice : public Device {
  private:
   hipcy_device *dev_;
   DedicatedTaskPool task_pool_; /* one worker thread, as CUDADevice (device_cuda.h:45) */
-  /* pixel-samples a RENDER task may hold (0: the device default, 2^25);
-   * CYCLES_HIPCY_STREAM_HOLD overrides it */
+  /* pixel-samples a RENDER task may hold; CYCLES_HIPCY_STREAM_HOLD overrides
+   * the choice of stream_hold() */
   uint64_t hold_ = 0;
+  /* HIPCyclesDevice instances alive in this process: the sub-devices of one
+   * MultiDevice (device_multi.cpp:47-105 creates them all before any task) */
+  static std::atomic<int> live_devices_;
+
+  /* The only device of the session holds as much as its slot pool keeps in
+   * flight (0: the device default, the whole pool plus as much in reserve), so
+   * a frame renders in as few wavefront iterations as a whole-frame pass.
+   * Devices sharing one TileManager queue each hold 2^25 pixel-samples (a
+   * 64x64 tile at 128 spp is 2^19), a small share of any frame they split:
+   * each takes tiles as fast as it finishes them. */
+  uint64_t stream_hold() const
+  {
+    if (hold_) {
+      return hold_;
+    }
+    return live_devices_.load() > 1 ? (uint64_t)1 << 25 : 0;
+  }
 
   bool check(int rc)
   {
@@ -313,12 +336,17 @@ class HIPCyclesDevice : public Device {
     return 0;
   }
 
+  /* every acquired tile comes back here once: finished, or (after a device
+   * error, hipcy_error non-empty) unfinished, released without progress as
+   * CUDADevice::thread_run still releases a tile whose render failed */
   static void feed_release(void *user, const hipcy_work_tile *, uint64_t tag)
   {
     Feed *f = (Feed *)user;
     RenderTile &t = f->tiles[tag];
-    t.sample = t.start_sample + t.num_samples;
-    f->task->update_progress(&t, t.w * t.h * t.num_samples);
+    if (hipcy_error(f->self->dev_)[0] == '\0') {
+      t.sample = t.start_sample + t.num_samples;
+      f->task->update_progress(&t, t.w * t.h * t.num_samples);
+    }
     f->task->release_tile(t);
   }
 
@@ -341,10 +369,12 @@ class HIPCyclesDevice : public Device {
     feed.acquire = feed_acquire;
     feed.release = feed_release;
     feed.cancelled = feed_cancelled;
-    feed.hold = hold_;
+    feed.hold = stream_hold();
     check(hipcy_render_feed(dev_, &feed));
   }
 };
+
+std::atomic<int> HIPCyclesDevice::live_devices_{0};
 
 bool device_hipcy_init()
 {

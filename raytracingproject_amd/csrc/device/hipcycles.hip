@@ -43,6 +43,8 @@
 template<int W, bool INST> struct LdsStack {
   CyStackEntry ring[CY_LDS_STACKW * CY_BLOCK];
   int top[(INST ? CY_LDS_STACK_TOP : 1) * CY_BLOCK];
+  /* the wide BVH's top CY_LDS_TOP nodes (2 W float4 each), non-instanced scenes */
+  hc_float4 top_nodes[(!INST && CY_LDS_TOP > 0) ? CY_LDS_TOP * 2 * W : 1];
 };
 template<bool INST> struct LdsStack<2, INST> {
   int top[CY_LDS_STACK * CY_BLOCK];
@@ -80,7 +82,22 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
   }
   else {
     return bvhw_intersect<W, any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
-                                      (CY_LDS CyStackEntry *)(lds->ring + t), tie);
+                                      (CY_LDS CyStackEntry *)(lds->ring + t), tie,
+                                      (CY_LDS const hc_float4 *)lds->top_nodes, kg->bvhw_top);
+  }
+}
+
+/* Copy the wide BVH's top nodes into the workgroup's LDS (CY_LDS_TOP; every
+ * thread of the block calls this before its traversal). */
+template<int W, bool INST> __device__ __forceinline__ void lds_fill_top(const CyGlobals *kg, LdsStack<W, INST> *lds)
+{
+  if constexpr (W > 2 && !INST && CY_LDS_TOP > 0) {
+    const int n = kg->bvhw_top * 2 * W;
+    const hc_float4 *src = (const hc_float4 *)kg->bvhw_nodes;
+    for (int i = threadIdx.x; i < n; i += CY_BLOCK) {
+      lds->top_nodes[i] = src[i];
+    }
+    __syncthreads();
   }
 }
 
@@ -358,6 +375,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
   const int n_active = cam_n > 0 ? cam_n : (int)*counter;
   const int i = cy_queue_index(n_active);
   __shared__ LdsStack<W, INST> lds_stack;
+  lds_fill_top<W, INST>(&kg, &lds_stack);
   uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
   const bool active = i < n_active;
   if (active) {
@@ -784,6 +802,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shado
   const int n_active = (int)*shadow_count;
   const int i = cy_queue_index(n_active);
   __shared__ LdsStack<W, INST> lds_stack;
+  lds_fill_top<W, INST>(&kg, &lds_stack);
   bool finished = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
@@ -1514,9 +1533,10 @@ struct hipcy_device {
   size_t records_capacity = 0;
   CyTileDesc *tile_descs = nullptr; /* tiles of the current multi-tile pass */
   size_t tile_descs_capacity = 0;
-  /* tile streams (hipcy_render_feed): pixel-samples one device holds at most
-   * (in flight + unclaimed), and the lanes' appended tile chunks */
-  size_t stream_hold = (size_t)1 << 25;
+  /* tile streams (hipcy_render_feed): pixel-samples one device holds (in
+   * flight + unclaimed; 0 = the slot pool plus as much in reserve), and the
+   * lanes' appended tile chunks */
+  size_t stream_hold = 0;
   CyTileDesc *stream_desc_dev = nullptr;
   CyTileDesc *stream_desc_host = nullptr; /* pinned */
   uint *min_live_dev = nullptr;           /* per lane CY_MIN_SHARDS words (k_stream_min_live) */
@@ -1604,6 +1624,10 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   kg->have_instancing = dev->have_instancing;
   kg->have_curves = dev->data_host.bvh.have_curves ? 1 : 0;
   kg->use_ray_diff = dev->use_ray_diff ? 1 : 0;
+  /* LDS copy of the top levels: non-instanced wide BVH only (instanced scenes
+   * traverse their top level as the reference's BVH2) */
+  const size_t wide_nodes = dev->bvh_width > 2 ? dev->bvhw_bytes / (32 * (size_t)dev->bvh_width) : 0;
+  kg->bvhw_top = (wide && !dev->have_instancing) ? (int)std::min<size_t>(CY_LDS_TOP, wide_nodes) : 0;
   return true;
 }
 
@@ -2690,6 +2714,14 @@ int hipcy_load_kernels(hipcy_device *dev)
   if (!why.empty()) {
     return set_error(dev, "load_kernels: unsupported shader: " + why);
   }
+  /* kernel_path_shader_apply (kernel_path.h:254-283): shadow-catcher objects
+   * need the shadow-catcher radiance terms, refused before the first launch
+   * rather than mid-frame */
+  for (uint32_t f : dev->object_flags) {
+    if (f & SD_OBJECT_SHADOW_CATCHER) {
+      return set_error(dev, "load_kernels: unsupported scene feature: shadow catcher objects");
+    }
+  }
   dev->use_volumes = d.integrator.use_volumes != 0;
   dev->use_disk_bssrdf = uses_disk_bssrdf;
   dev->use_ray_diff = uses_ray_diff;
@@ -3047,19 +3079,11 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
   return 0;
 }
 
-/* One pass over samples [tile.start_sample, tile.end_sample) of the tile: the
- * items are split into CY_LANES contiguous ranges, each iterated by its own
- * slot partition on its own stream; the host enqueues one iteration of every
- * active lane, then waits for their queue counts. */
-static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, int W, size_t *ev,
-                           std::vector<EvQuad> *quads)
+/* Queue-sort buffers (hipcy_set_ray_sort) sized to the slot pool: called after
+ * ensure_capacity by every entry that iterates lanes (path_trace_pass and the
+ * tile stream), so the automatic shading-queue sort runs on both. */
+static int ensure_sort(hipcy_device *dev)
 {
-  const size_t n_slots = std::min<size_t>(tile.n_items, dev->capacity);
-  /* per-kernel event timing (profiling bit 0) needs kernels that do not
-   * overlap: one lane then */
-  const int max_lanes = (dev->profiling & 1) ? 1 : CY_LANES;
-  const int lanes = (int)std::max<size_t>(1, std::min<size_t>(max_lanes, n_slots / (4 * CY_BLOCK)));
-  tile.samples_out = dev->records;
   if (effective_sort(dev) && dev->sort_capacity < dev->capacity) {
     const size_t cap = dev->capacity;
     if (dev->sort_queue) HIP_CHECK(dev, hipFree(dev->sort_queue));
@@ -3075,6 +3099,25 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     HIP_CHECK(dev, hipMalloc((void **)&dev->sort_hist,
                              (size_t)CY_SORT_BINS * (cap / CY_BLOCK + CY_LANES + 1) * sizeof(uint)));
     dev->sort_capacity = cap;
+  }
+  return 0;
+}
+
+/* One pass over samples [tile.start_sample, tile.end_sample) of the tile: the
+ * items are split into CY_LANES contiguous ranges, each iterated by its own
+ * slot partition on its own stream; the host enqueues one iteration of every
+ * active lane, then waits for their queue counts. */
+static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, int W, size_t *ev,
+                           std::vector<EvQuad> *quads)
+{
+  const size_t n_slots = std::min<size_t>(tile.n_items, dev->capacity);
+  /* per-kernel event timing (profiling bit 0) needs kernels that do not
+   * overlap: one lane then */
+  const int max_lanes = (dev->profiling & 1) ? 1 : CY_LANES;
+  const int lanes = (int)std::max<size_t>(1, std::min<size_t>(max_lanes, n_slots / (4 * CY_BLOCK)));
+  tile.samples_out = dev->records;
+  if (ensure_sort(dev) != 0) {
+    return -1;
   }
   if (dev->trav_budget[0] > 0 && W > 2 && !kg.have_instancing && !kg.have_curves) {
     /* continuation records: per lane two buffers of a quarter of the lane's
@@ -3418,7 +3461,8 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
 struct FeedTile {
   hipcy_work_tile t;
   uint64_t tag;
-  int next_sample; /* first sample not yet appended to a lane */
+  int next_sample;       /* first sample not yet appended to a lane */
+  bool released = false; /* handed back through feed->release */
 };
 
 struct StreamChunk {
@@ -3464,6 +3508,36 @@ static bool feed_cancelled(const StreamState &st)
   return st.feed->cancelled && st.feed->cancelled(st.feed->user);
 }
 
+static void feed_release_tile(StreamState &st, size_t f)
+{
+  FeedTile &F = st.tiles[f];
+  if (!F.released) {
+    F.released = true;
+    st.feed->release(st.feed->user, &F.t, F.tag);
+    st.released++;
+  }
+}
+
+/* Error exit of a tile stream: every acquired tile goes back to the queue's
+ * owner, as CUDADevice::thread_run releases each tile it acquired whatever its
+ * render did (device_cuda_impl.cpp:2361-2388).  The device's sticky error is
+ * set before this runs, so the caller's release callback can tell these tiles
+ * from finished ones (hipcy_error is non-empty). */
+static void feed_release_all(StreamState &st)
+{
+  hipcy_device *dev = st.dev;
+  /* no kernel may still write a buffer that is handed back */
+  for (int l = 0; l < CY_LANES; l++) {
+    if (dev->lane_stream[l]) {
+      hipStreamSynchronize(dev->lane_stream[l]);
+    }
+  }
+  hipStreamSynchronize(dev->stream);
+  for (size_t f = 0; f < st.tiles.size(); f++) {
+    feed_release_tile(st, f);
+  }
+}
+
 /* Append chunks to the lane until it holds `target` unclaimed items (or the
  * queue, the ring or the lane's numbering runs out). */
 static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chunk)
@@ -3488,15 +3562,14 @@ static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chu
           st.feed_empty = true;
           break;
         }
+        f.next_sample = f.t.start_sample;
+        st.tiles.push_back(f);
         if (f.t.w < 0 || f.t.h < 0 || (f.t.w * f.t.h > 0 && f.t.num_samples > 0 && !f.t.buffer)) {
           return set_error(dev, "render_feed: invalid tile");
         }
-        f.next_sample = f.t.start_sample;
-        st.tiles.push_back(f);
         if ((size_t)f.t.w * f.t.h == 0 || f.t.num_samples <= 0) {
           /* nothing to render: released at once */
-          st.feed->release(st.feed->user, &st.tiles.back().t, f.tag);
-          st.released++;
+          feed_release_tile(st, st.tiles.size() - 1);
           continue;
         }
         S.cur_feed = (int)st.tiles.size() - 1;
@@ -3583,9 +3656,7 @@ static int stream_complete(StreamState &st, StreamLane &S, uint bound)
 static void stream_release(StreamState &st, StreamLane &S)
 {
   for (int f : S.release) {
-    FeedTile &F = st.tiles[f];
-    st.feed->release(st.feed->user, &F.t, F.tag);
-    st.released++;
+    feed_release_tile(st, (size_t)f);
   }
   S.release.clear();
 }
@@ -3614,34 +3685,33 @@ static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
   return 0;
 }
 
+/* The slot pool of a tile stream (and the per-slot extras the scene needs). */
+static int stream_pool(hipcy_device *dev, size_t slots)
+{
+  if (ensure_capacity(dev, slots) != 0 || ensure_volume_capacity(dev) != 0 || ensure_sss_capacity(dev) != 0 ||
+      ensure_diff_capacity(dev) != 0 || ensure_sort(dev) != 0) {
+    return -1;
+  }
+  return 0;
+}
+
 static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t lane_slots, uint ring_cap,
                           size_t *ev)
 {
   hipcy_device *dev = st.dev;
   const int lanes = CY_LANES;
   StreamLane lane[CY_LANES];
-  /* idle marks: every slot of the pool starts without an item */
-  HIP_CHECK(dev, hipMemsetAsync(dev->bufs.item, 0xFF, lane_slots * lanes * sizeof(uint), dev->stream));
-  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 16 * 4 * (CY_LANES + 1), dev->stream));
-  hipEvent_t start = get_event(dev, (*ev)++);
-  HIP_CHECK(dev, hipEventRecord(start, dev->stream));
   for (int l = 0; l < lanes; l++) {
     StreamLane &S = lane[l];
     PassLane &L = S.ln;
     L.index = l;
     L.s = dev->lane_stream[l];
-    HIP_CHECK(dev, hipStreamWaitEvent(L.s, start, 0));
-    L.slot_base = (int)(lane_slots * l);
     L.cnt = dev->counters + 16 * (l + 1);
     L.hcnt = dev->host_counters + 16 * (l + 1);
     L.qa = 0;
     L.qb = 1;
     L.done = get_event(dev, (*ev)++);
     L.stream = true;
-    for (int q = 0; q < 3; q++) {
-      L.q[q] = dev->queue[q] + L.slot_base;
-    }
-    S.lane_slots = (int)lane_slots;
     S.ring = dev->records + (size_t)ring_cap * l;
     S.ring_cap = ring_cap;
     S.desc_dev = dev->stream_desc_dev + (size_t)CY_STREAM_DESCS * l;
@@ -3674,6 +3744,33 @@ static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t la
       }
       more |= S.chunks.size() > before;
     }
+  }
+  if (st.feed_empty && st.carry.empty()) {
+    /* the whole queue is in the lanes: no lane needs more slots than items */
+    size_t most = 0;
+    for (int l = 0; l < lanes; l++) {
+      most = std::max<size_t>(most, lane[l].n_items);
+    }
+    most = std::max<size_t>((most + CY_BLOCK - 1) / CY_BLOCK * CY_BLOCK, 4 * CY_BLOCK);
+    lane_slots = std::min(lane_slots, most);
+  }
+  if (stream_pool(dev, lane_slots * lanes) != 0) {
+    return -1;
+  }
+  /* idle marks: every slot of the pool starts without an item */
+  HIP_CHECK(dev, hipMemsetAsync(dev->bufs.item, 0xFF, lane_slots * lanes * sizeof(uint), dev->stream));
+  HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 16 * 4 * (CY_LANES + 1), dev->stream));
+  hipEvent_t start = get_event(dev, (*ev)++);
+  HIP_CHECK(dev, hipEventRecord(start, dev->stream));
+  for (int l = 0; l < lanes; l++) {
+    StreamLane &S = lane[l];
+    PassLane &L = S.ln;
+    HIP_CHECK(dev, hipStreamWaitEvent(L.s, start, 0));
+    L.slot_base = (int)(lane_slots * l);
+    for (int q = 0; q < 3; q++) {
+      L.q[q] = dev->queue[q] + L.slot_base;
+    }
+    S.lane_slots = (int)lane_slots;
   }
   for (int l = 0; l < lanes; l++) {
     StreamLane &S = lane[l];
@@ -3791,11 +3888,12 @@ static int feed_per_tile(StreamState &st)
     if (!st.feed->acquire(st.feed->user, &f.t, &f.tag)) {
       break;
     }
-    if (path_trace(dev, &f.t, 1, 1) != 0 || hipcy_synchronize(dev) != 0) {
+    f.next_sample = f.t.start_sample;
+    st.tiles.push_back(f);
+    if (path_trace(dev, &st.tiles.back().t, 1, 1) != 0 || hipcy_synchronize(dev) != 0) {
       return -1;
     }
-    st.feed->release(st.feed->user, &f.t, f.tag);
-    st.released++;
+    feed_release_tile(st, st.tiles.size() - 1);
   }
   return 0;
 }
@@ -3822,10 +3920,15 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
   st.dev = dev;
   st.feed = feed;
   if (dev->data_host.film.pass_adaptive_aux_buffer) {
-    return feed_per_tile(st);
+    if (feed_per_tile(st) != 0) {
+      feed_release_all(st);
+      return -1;
+    }
+    return 0;
   }
   const int lanes = CY_LANES;
-  const size_t hold = feed->hold ? (size_t)feed->hold : dev->stream_hold;
+  const size_t hold = feed->hold ? (size_t)feed->hold
+                                  : dev->stream_hold ? dev->stream_hold : 2 * dev->slots_wanted;
   /* half of a lane's share in flight, half in reserve */
   size_t lane_slots = std::min(dev->slots_wanted / lanes, std::max<size_t>(hold / (2 * lanes), 4 * CY_BLOCK));
   lane_slots = (lane_slots + CY_BLOCK - 1) / CY_BLOCK * CY_BLOCK;
@@ -3834,9 +3937,9 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
   while ((size_t)ring_cap * 2 * sizeof(hc_float4) * lanes <= dev->record_budget && ring_cap < (1u << 30)) {
     ring_cap <<= 1;
   }
-  if (ensure_capacity(dev, lane_slots * lanes) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
-      ensure_records(dev, (size_t)ring_cap * lanes) != 0 || ensure_bvhw(dev) != 0) {
+  /* the slot pool is sized by each session once its first tiles are in
+   * (stream_pool) */
+  if (ensure_records(dev, (size_t)ring_cap * lanes) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }
   if (!dev->stream_desc_dev) {
@@ -3867,6 +3970,7 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
   } while (rc == 0 && !dev->host_counters[3] && (!st.feed_empty || !st.carry.empty()));
   dev->profiling = prof;
   if (rc != 0) {
+    feed_release_all(st);
     return -1;
   }
   hipEvent_t t_end = get_event(dev, ev++);
@@ -3875,7 +3979,11 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
   float ms = 0.0f;
   hipEventElapsedTime(&ms, t_begin, t_end);
   dev->stats.total_ms = ms;
-  return check_device_error(dev);
+  if (check_device_error(dev) != 0) {
+    feed_release_all(st);
+    return -1;
+  }
+  return 0;
 }
 
 int hipcy_set_slots(hipcy_device *dev, uint64_t slots, uint64_t record_bytes)

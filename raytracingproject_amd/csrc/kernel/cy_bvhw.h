@@ -83,6 +83,16 @@
     return true; \
   }())
 
+CY_FN hc_uint4 as_uint4(hc_float4 f)
+{
+  hc_uint4 u;
+  u.x = as_uint(f.x);
+  u.y = as_uint(f.y);
+  u.z = as_uint(f.z);
+  u.w = as_uint(f.w);
+  return u;
+}
+
 CY_FN void bvhw_cswap(float &ta, int &ca, float &tb, int &cb)
 {
   const bool sw = tb < ta;
@@ -142,6 +152,16 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
 #  define CY_SLAB_FMA 0
 #endif
 
+/* Top levels of the wide BVH served from LDS: the collapse numbers wide nodes
+ * breadth first (cy_bvhw_collapse.h), so nodes 0 .. CY_LDS_TOP-1 are the root
+ * and the levels below it (W = 4: 1 + 4 + 16 = 21 nodes for two levels below
+ * the root, 85 for three).  The traversal kernels copy them into LDS once per
+ * workgroup (hipcycles.hip lds_fill_top) and every visit of one of them reads
+ * LDS instead of issuing eight 16-B global loads to a 128-B line.  0 = off. */
+#ifndef CY_LDS_TOP
+#  define CY_LDS_TOP 0
+#endif
+
 /* opaque any-hit without the child sort (measurement switch) */
 #ifndef CY_ANYHIT_NOSORT
 #  define CY_ANYHIT_NOSORT 0
@@ -199,7 +219,9 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
                          CY_LDS CyStackEntry *lds_ring,
                          bool *tie_out,
                          int budget,
-                         CyTravCursor *cur)
+                         CyTravCursor *cur,
+                         CY_LDS const hc_float4 *top_nodes,
+                         int n_top)
 {
   /* ring column of this thread (device) or a local array (host) */
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -264,16 +286,33 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
       /* inner node: test the W child boxes */
       n_nodes++;
       const hc_float4 *np = nodes + (size_t)code * (8 * Q);
+      hc_float4 nd[8 * Q];
+#if defined(__HIP_DEVICE_COMPILE__) && CY_LDS_TOP > 0
+      if (code < n_top) {
+        CY_LDS const hc_float4 *lp = top_nodes + (size_t)code * (8 * Q);
+#  pragma unroll
+        for (int k = 0; k < 8 * Q; k++) {
+          nd[k] = lp[k];
+        }
+      }
+      else
+#endif
+      {
+#pragma unroll
+        for (int k = 0; k < 8 * Q; k++) {
+          nd[k] = np[k];
+        }
+      }
       float tn[W];
       int cc[W];
       const float t = CY_T_BOX;
 #pragma unroll
       for (int q = 0; q < Q; q++) {
-        const hc_float4 lx = np[0 * Q + q], hx = np[1 * Q + q];
-        const hc_float4 ly = np[2 * Q + q], hy = np[3 * Q + q];
-        const hc_float4 lz = np[4 * Q + q], hz = np[5 * Q + q];
-        const hc_uint4 ch = ((const hc_uint4 *)np)[6 * Q + q];
-        const hc_uint4 mt = ((const hc_uint4 *)np)[7 * Q + q];
+        const hc_float4 lx = nd[0 * Q + q], hx = nd[1 * Q + q];
+        const hc_float4 ly = nd[2 * Q + q], hy = nd[3 * Q + q];
+        const hc_float4 lz = nd[4 * Q + q], hz = nd[5 * Q + q];
+        const hc_uint4 ch = as_uint4(nd[6 * Q + q]);
+        const hc_uint4 mt = as_uint4(nd[7 * Q + q]);
         const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
         const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
         const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
@@ -704,7 +743,9 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
                           uint *cnt_leaves,
                           uint *cnt_tris,
                           CY_LDS CyStackEntry *lds_ring = nullptr,
-                          bool *tie = nullptr)
+                          bool *tie = nullptr,
+                          CY_LDS const hc_float4 *top_nodes = nullptr,
+                          int n_top = 0)
 {
   isect->t = ray->t;
   isect->u = 0.0f;
@@ -718,7 +759,7 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
                                lds_ring, tie);
 #else
   bvhw_traverse<W, any_hit>(kg, 0, ray->P, dir, rcp3(dir), OBJECT_NONE, visibility, isect, err, cnt_nodes,
-                            cnt_leaves, cnt_tris, lds_ring, tie);
+                            cnt_leaves, cnt_tris, lds_ring, tie, 0, nullptr, top_nodes, n_top);
 #endif
   return isect->prim != PRIM_NONE;
 }

@@ -72,6 +72,9 @@ typedef struct CyGlobals {
    * the paths carry dP / dD (CyPathBuffers.ray_diff) and shading points get
    * dP, dI, du, dv; otherwise they are zero */
   int use_ray_diff;
+  /* wide nodes 0 .. bvhw_top-1 (the top levels, breadth first) are read from
+   * the traversal kernels' LDS copy (cy_bvhw.h CY_LDS_TOP); 0 = none */
+  int bvhw_top;
 } CyGlobals;
 
 #endif /* CY_GLOBALS_H */

@@ -622,7 +622,8 @@ template<int W, bool any_hit>
 CY_FN bool bvhw_traverse(const CyGlobals *kg, int root, cfloat3 P, cfloat3 dir, cfloat3 idir, int object,
                          uint visibility, CyIsect *isect, uint *err, uint *cnt_nodes, uint *cnt_leaves,
                          uint *cnt_tris, CY_LDS CyStackEntry *lds_ring, bool *tie_out, int budget = 0,
-                         CyTravCursor *cur = nullptr);
+                         CyTravCursor *cur = nullptr, CY_LDS const hc_float4 *top_nodes = nullptr,
+                         int n_top = 0);
 
 /* Closest hit / opaque any hit with the bound BVH2 in the reference's order
  * (bvh/bvh_traversal.h:34-227).  The first LDSN stack entries live in LDS,

@@ -9,8 +9,16 @@
  * What it does is what render/session.cpp does with a GPU device for one
  * frame (Session::run_gpu -> DeviceTask RENDER, session.cpp:381-533):
  *   device_hipcy_info / device_hipcy_create      (device.cpp:367-418 path)
+ *   load_kernels(DeviceRequestedFeatures)        (session.cpp load_kernels; features.txt
+ *                                                 sets use_shader_raytrace as shader.cpp:724-725
+ *                                                 does for AO / Bevel nodes)
  *   MEM_GLOBAL device_vector uploads by name     (scene.cpp device_update)
+ *   MEM_TEXTURE device_texture uploads           (image.cpp device_load_image: textures.txt)
  *   const_copy_to("__data", KernelData)
+ *   the background importance map: a DeviceTask SHADER with
+ *   SHADER_EVAL_BACKGROUND over the map (light.cpp:38-85 shade_background_pixels,
+ *   split in 128x128-element tasks), its CDFs built on the host
+ *   (libhipcycles_host.so, light.cpp:530-716) and re-uploaded (background.txt)
  *   a MEM_READ_WRITE render buffer, zeroed
  *   DeviceTask RENDER whose acquire_tile hands out tile_size tiles (the
  *   TileManager's role) until the frame is done; release_tile counts them
@@ -18,7 +26,10 @@
  *
  * usage: plugin_harness <scene dir> <width> <height> <samples> <tile size> <pass stride> <out.bin> [devices]
  * The scene dir holds kernel_data.bin, manifest.txt ("name bytes" lines) and
- * one <name>.bin per array (written by tests/test_plugin_harness.py).
+ * one <name>.bin per array (written by tests/test_plugin_harness.py), and
+ * optionally textures.txt ("slot data_type interpolation extension width
+ * height" lines, texels in tex_<slot>.bin), background.txt ("res_x res_y")
+ * and features.txt ("name 0|1" lines of DeviceRequestedFeatures).
  *
  * With devices > 1 it does what MultiDevice does (device_multi.cpp:689-737):
  * one HIPCyclesDevice per sub-device, each with its own scene upload and
@@ -39,6 +50,7 @@
 #include "device/device_memory.h"
 #include "device/device_task.h"
 #include "render/buffers.h"
+#include "util/util_math.h"
 #include "util/util_profiling.h"
 #include "util/util_stats.h"
 #include "util/util_time.h"
@@ -48,6 +60,10 @@ bool device_hipcy_init();
 Device *device_hipcy_create(DeviceInfo &info, Stats &stats, Profiler &profiler, bool background);
 void device_hipcy_info(vector<DeviceInfo> &devices);
 CCL_NAMESPACE_END
+
+/* the repository's host restatement of the background CDFs (render/light.cpp
+ * background_cdf), csrc/host/light_background.cpp in libhipcycles_host.so */
+extern "C" void hcb_background_cdf(const float *pixels, int res_x, int res_y, float *marg_cdf, float *cond_cdf);
 
 using namespace ccl;
 
@@ -61,11 +77,102 @@ static bool read_file(const std::string &path, void *dst, size_t bytes)
 struct SubDevice {
   Device *dev = nullptr;
   std::vector<device_vector<uchar> *> arrays;
+  std::vector<device_texture *> textures;
   device_vector<float> *buffer = nullptr;
   std::vector<int> tiles; /* indices of the tiles it acquired */
   int held = 0;           /* acquired and not yet released */
   int max_held = 0;
 };
+
+static device_vector<uchar> *find_array(SubDevice &sd, const char *name)
+{
+  for (auto *v : sd.arrays) {
+    if (strcmp(v->name, name) == 0) {
+      return v;
+    }
+  }
+  auto *v = new device_vector<uchar>(sd.dev, name, MEM_GLOBAL);
+  sd.arrays.push_back(v);
+  return v;
+}
+
+/* shade_background_pixels (light.cpp:38-85): the world shader over the map by
+ * DeviceTask SHADER, split in 128x128-element tasks (DeviceTask::split of
+ * SHADER tasks), each task_add / task_wait / copy_from_device; then the CDFs on
+ * the host and the two CDF arrays re-uploaded by name. */
+static int shade_background(SubDevice &sd, int width, int height)
+{
+  Device *device = sd.dev;
+  device_vector<uint4> d_input(device, "background_input", MEM_READ_ONLY);
+  device_vector<float4> d_output(device, "background_output", MEM_READ_WRITE);
+  uint4 *in = d_input.alloc((size_t)width * height);
+  for (int y = 0; y < height; y++) {
+    for (int x = 0; x < width; x++) {
+      const float u = (x + 0.5f) / width;
+      const float v = (y + 0.5f) / height;
+      in[x + y * width] = make_uint4(__float_as_uint(u), __float_as_uint(v), 0, 0);
+    }
+  }
+  d_output.alloc((size_t)width * height);
+  d_output.zero_to_device();
+  d_input.copy_to_device();
+  DeviceTask main_task(DeviceTask::SHADER);
+  main_task.shader_input = d_input.device_pointer;
+  main_task.shader_output = d_output.device_pointer;
+  main_task.shader_eval_type = SHADER_EVAL_BACKGROUND;
+  main_task.shader_x = 0;
+  main_task.shader_w = width * height;
+  main_task.num_samples = 1;
+  main_task.get_cancel = [] { return false; };
+  main_task.update_progress_sample = [](long, int) {};
+  list<DeviceTask> split_tasks;
+  main_task.split(split_tasks, 1, 128 * 128);
+  int n_tasks = 0;
+  for (DeviceTask &task : split_tasks) {
+    device->task_add(task);
+    device->task_wait();
+    d_output.copy_from_device(task.shader_x, 1, task.shader_w);
+    n_tasks++;
+  }
+  if (device->have_error()) {
+    fprintf(stderr, "background SHADER task: %s\n", device->error_message().c_str());
+    return 8;
+  }
+  d_input.free();
+  std::vector<float> pixels((size_t)4 * width * height);
+  memcpy(pixels.data(), d_output.data(), pixels.size() * sizeof(float));
+  d_output.free();
+  std::vector<float> marg((size_t)2 * (height + 1)), cond((size_t)2 * (width + 1) * height);
+  hcb_background_cdf(pixels.data(), width, height, marg.data(), cond.data());
+  const std::pair<const char *, std::vector<float> *> cdfs[2] = {{"__light_background_marginal_cdf", &marg},
+                                                                 {"__light_background_conditional_cdf", &cond}};
+  for (const auto &c : cdfs) {
+    device_vector<uchar> *v = find_array(sd, c.first);
+    uchar *p = v->alloc(c.second->size() * sizeof(float));
+    memcpy(p, c.second->data(), c.second->size() * sizeof(float));
+    v->copy_to_device();
+  }
+  printf("background map %dx%d by %d SHADER task(s)\n", width, height, n_tasks);
+  return 0;
+}
+
+static DeviceRequestedFeatures read_features(const std::string &dir)
+{
+  DeviceRequestedFeatures f;
+  std::ifstream ff(dir + "/features.txt");
+  std::string name;
+  int on;
+  while (ff >> name >> on) {
+    if (name == "shader_raytrace") f.use_shader_raytrace = on != 0;
+    else if (name == "hair") f.use_hair = on != 0;
+    else if (name == "volume") f.use_volume = on != 0;
+    else if (name == "subsurface") f.use_subsurface = on != 0;
+    else if (name == "transparent") f.use_transparent = on != 0;
+    else if (name == "background_light") f.use_background_light = on != 0;
+    else fprintf(stderr, "features.txt: unknown feature %s\n", name.c_str());
+  }
+  return f;
+}
 
 static int upload_scene(SubDevice &sd, const std::string &dir, int W, int H, int stride)
 {
@@ -90,10 +197,39 @@ static int upload_scene(SubDevice &sd, const std::string &dir, int W, int H, int
     v->copy_to_device();
     sd.arrays.push_back(v);
   }
+  {
+    /* ImageManager::device_load_image: a device_texture per slot, copy_to_device
+     * (-> Device::mem_copy_to -> tex_alloc) */
+    std::ifstream tx(dir + "/textures.txt");
+    int slot, type, interp, ext;
+    size_t w, h;
+    while (tx >> slot >> type >> interp >> ext >> w >> h) {
+      auto *t = new device_texture(sd.dev, "__tex_image", (uint)slot, (ImageDataType)type, (InterpolationType)interp,
+                                   (ExtensionType)ext);
+      void *p = t->alloc(w, h);
+      if (!read_file(dir + "/tex_" + std::to_string(slot) + ".bin", p, t->memory_size())) {
+        fprintf(stderr, "short read: texture %d\n", slot);
+        return 5;
+      }
+      t->copy_to_device();
+      sd.textures.push_back(t);
+    }
+  }
   std::vector<char> kd(1 << 16);
   std::ifstream kf(dir + "/kernel_data.bin", std::ios::binary);
   kf.read(kd.data(), (std::streamsize)kd.size());
   sd.dev->const_copy_to("__data", kd.data(), (size_t)kf.gcount());
+  {
+    std::ifstream bg(dir + "/background.txt");
+    int res_x = 0, res_y = 0;
+    if (bg >> res_x >> res_y) {
+      /* LightManager::device_update_background (light.cpp:568-716) */
+      const int rc = shade_background(sd, res_x, res_y);
+      if (rc) {
+        return rc;
+      }
+    }
+  }
   sd.buffer = new device_vector<float>(sd.dev, "render_buffer", MEM_READ_WRITE);
   sd.buffer->alloc((size_t)W * H * stride);
   sd.buffer->zero_to_device();
@@ -125,7 +261,7 @@ int main(int argc, char **argv)
       fprintf(stderr, "create: %s\n", subs[d].dev->error_message().c_str());
       return 4;
     }
-    DeviceRequestedFeatures features;
+    const DeviceRequestedFeatures features = read_features(dir);
     if (!subs[d].dev->load_kernels(features)) {
       fprintf(stderr, "load_kernels: %s\n", subs[d].dev->error_message().c_str());
       return 4;
@@ -257,6 +393,9 @@ int main(int argc, char **argv)
     for (auto *v : sd.arrays) {
       v->free();
       delete v;
+    }
+    for (auto *t : sd.textures) {
+      delete t;
     }
     sd.buffer->free();
     delete sd.buffer;

@@ -35,6 +35,6 @@ gcc -O1 -fPIC -DWITH_DYNLOAD -I"$REF/intern/numaapi/include" -c "$REF/intern/num
 OBJS+=("$OUT/obj/numaapi_linux.o")
 wait
 g++ -o "$OUT/plugin_harness" "$OUT/obj/plugin_harness.o" "$OUT/obj/device_hip.o" "${OBJS[@]}" \
-  -L"$ROOT/raytracingproject_amd" -lhipcycles -Wl,-rpath,'$ORIGIN/../../raytracingproject_amd' \
+  -L"$ROOT/raytracingproject_amd" -lhipcycles -lhipcycles_host -Wl,-rpath,'$ORIGIN/../../raytracingproject_amd' \
   -Wl,--unresolved-symbols=ignore-all -lpthread -ldl
 echo "built $OUT/plugin_harness"
