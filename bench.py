@@ -284,6 +284,10 @@ def main():
         # streamed into one running wavefront, at most `hold` pixel-samples held)
         # and, for comparison, one tile per device pass
         tile_leg = [tile_mode(dev, ds, args.tile, args.tile_batch, args.stream_hold, film)]
+        if args.tile_batch == 0:
+            # the same stream with the tiles in one frame buffer, released without a copy:
+            # the device side of the stream alone (no per-tile D2H in Python callbacks)
+            tile_leg.append(tile_mode(dev, ds, args.tile, 0, args.stream_hold, film, frame_buffer=True))
         for extra in (args.stream_hold_sweep or "").split(","):
             if extra:
                 tile_leg.append(tile_mode(dev, ds, args.tile, 0, int(extra), film))
@@ -436,7 +440,7 @@ def traversal_roofline(timing, counts):
     }
 
 
-def tile_mode(dev, ds, tile, batch, hold=0, film=None):
+def tile_mode(dev, ds, tile, batch, hold=0, film=None, frame_buffer=False):
     """One frame rendered the way a Cycles Session drives a device: the frame
     split into tile x tile RenderTiles (session.h:84 default 64) acquired in
     row order, each rendered over all its samples into its own buffer
@@ -445,11 +449,47 @@ def tile_mode(dev, ds, tile, batch, hold=0, film=None):
     more than `hold` pixel-samples (hipcy_render_feed, what the plugin does);
     batch N: N acquired tiles per device pass.  Reported beside the whole-frame
     number (with whether the tiles reassemble to its film bit for bit); not
-    the headline value."""
+    the headline value.  frame_buffer: every tile renders into one frame
+    buffer at its offset (a Session's single RenderBuffers) and its release
+    does nothing; the film is copied once at the end."""
     import torch
 
     W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
     tiles = [(x, y, min(tile, W - x), min(tile, H - y)) for y in range(0, H, tile) for x in range(0, W, tile)]
+    if frame_buffer:
+        fbuf = torch.zeros((H, W, PS), dtype=torch.float32, device="cuda")
+        fhost = torch.empty((H, W, PS), dtype=torch.float32, pin_memory=True)
+
+        def fb_frame():
+            fbuf.zero_()
+            torch.cuda.current_stream().synchronize()
+            nxt = [0]
+
+            def acquire():
+                k = nxt[0]
+                if k >= len(tiles):
+                    return None
+                nxt[0] += 1
+                return tiles[k], 0, S, fbuf.data_ptr(), 0, W, k
+
+            dev.render_feed(acquire, lambda k, t: None, hold=hold)
+            fhost.copy_(fbuf)
+
+        fb_frame()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fb_frame()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res = {"tile": tile, "tiles": len(tiles), "mode": "stream into one frame buffer, film copied once",
+               "value": round(W * H * S / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_frame": round(1e3 * dt, 3),
+               "hold_pixel_samples": hold or "device default: the slot pool in flight plus as much in reserve",
+               "wavefront_iterations": int(dev.stats()["iterations"])}
+        if film is not None:
+            res["film_bit_exact_vs_whole_frame"] = bool(np.array_equal(fhost.numpy().view(np.uint32),
+                                                                       film.view(np.uint32)))
+        del fbuf, fhost
+        return res
     bufs = [torch.zeros((t[3], t[2], PS), dtype=torch.float32, device="cuda") for t in tiles]
     # each released tile goes to pinned host memory on a copy stream, without
     # blocking the device's render thread (Session::release_tile's buffer copy)

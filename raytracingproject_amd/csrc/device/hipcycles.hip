@@ -95,7 +95,12 @@ template<int W, bool INST> __device__ __forceinline__ void lds_fill_top(const Cy
     const int n = kg->bvhw_top * 2 * W;
     const hc_float4 *src = (const hc_float4 *)kg->bvhw_nodes;
     for (int i = threadIdx.x; i < n; i += CY_BLOCK) {
+#  if CY_LDS_TOP_SOA
+      /* node i / 2W, float4 i % 2W */
+      lds->top_nodes[(i % (2 * W)) * CY_LDS_TOP + i / (2 * W)] = src[i];
+#  else
       lds->top_nodes[i] = src[i];
+#  endif
     }
     __syncthreads();
   }

@@ -22,8 +22,9 @@
  *   bounds : the exact BVH2 child boxes (float), so the slab test of a wide
  *            child is bit-for-bit the reference's test of that BVH2 child
  *            (bvh/bvh_nodes.h:31-80);
- *   child  : >= 0 inner child node index, < 0 leaf ~first_primitive
- *            (instance leaf: ~object);
+ *   child  : >= 0 inner child node index, < 0 leaf ~(first_primitive << 4 |
+ *            count) (instance leaf: ~(object << 4), count 0), the code the
+ *            traversal pushes as it is;
  *   meta   : child visibility (low 28 bits, as the BVH2 node stored it) |
  *            primitive count << 28 for leaves (0 for an instance); 0 = empty slot.
  * Instanced geometry (two-level BVH, bvh/bvh.cpp:323-520): each object BVH
@@ -257,7 +258,7 @@ struct Collapser {
           error = "primitive index beyond the 2^27 leaf-code range";
           return false;
         }
-        w[6 * W + s] = (uint32_t)(~start);
+        w[6 * W + s] = ~(((uint32_t)start << 4) | (uint32_t)count);
         w[7 * W + s] = vis | ((uint32_t)count << 28);
       }
       else if (!error.empty()) {

@@ -83,6 +83,39 @@
     return true; \
   }())
 
+/* Slab-test min / max.  The reference's min / max ((a < b) ? a : b,
+ * util_math.h:122-167) and the hardware's v_min_f32 / v_max_f32 (min3 / max3)
+ * agree on every operand the slab test produces except the sign of a zero
+ * result: the operands are products of finite differences and finite inverse
+ * directions (bvh_clamp_direction bounds |idir| by 1.2e24), so never NaN, and
+ * min(-0, +0) may return either zero.  Every later use of these values is a
+ * comparison (hit = tmax >= tmin, the child sort, the stack's cull against the
+ * current hit, the leaf-box entry check) or a copy into one, for which -0 and
+ * +0 are equal, so the traversal decides exactly as the reference's arithmetic
+ * does.  0 selects the reference's form (measurement switch). */
+#ifndef CY_FAST_MINMAX
+#  define CY_FAST_MINMAX 1
+#endif
+#if CY_FAST_MINMAX
+CY_FN float slab_min(float a, float b)
+{
+  return __builtin_fminf(a, b);
+}
+CY_FN float slab_max(float a, float b)
+{
+  return __builtin_fmaxf(a, b);
+}
+#else
+CY_FN float slab_min(float a, float b)
+{
+  return cmin(a, b);
+}
+CY_FN float slab_max(float a, float b)
+{
+  return cmax(a, b);
+}
+#endif
+
 CY_FN hc_uint4 as_uint4(hc_float4 f)
 {
   hc_uint4 u;
@@ -159,7 +192,13 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
  * workgroup (hipcycles.hip lds_fill_top) and every visit of one of them reads
  * LDS instead of issuing eight 16-B global loads to a 128-B line.  0 = off. */
 #ifndef CY_LDS_TOP
-#  define CY_LDS_TOP 0
+#  define CY_LDS_TOP 21
+#endif
+/* LDS image layout of the top nodes: 0 node after node (float4 k of node n at
+ * n * 2W + k), 1 float4-major (at k * CY_LDS_TOP + n), so lanes reading the
+ * same float4 of different nodes hit different banks */
+#ifndef CY_LDS_TOP_SOA
+#  define CY_LDS_TOP_SOA 0
 #endif
 
 /* opaque any-hit without the child sort (measurement switch) */
@@ -289,11 +328,19 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
       hc_float4 nd[8 * Q];
 #if defined(__HIP_DEVICE_COMPILE__) && CY_LDS_TOP > 0
       if (code < n_top) {
+#  if CY_LDS_TOP_SOA
+        CY_LDS const hc_float4 *lp = top_nodes + code;
+#    pragma unroll
+        for (int k = 0; k < 8 * Q; k++) {
+          nd[k] = lp[k * CY_LDS_TOP];
+        }
+#  else
         CY_LDS const hc_float4 *lp = top_nodes + (size_t)code * (8 * Q);
-#  pragma unroll
+#    pragma unroll
         for (int k = 0; k < 8 * Q; k++) {
           nd[k] = lp[k];
         }
+#  endif
       }
       else
 #endif
@@ -337,14 +384,15 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
           const float chiy = (ahy[j] - P.y) * idir.y;
           const float cloz = (alz[j] - P.z) * idir.z;
           const float chiz = (ahz[j] - P.z) * idir.z;
-          const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz));
-          const float cmx = min4(t, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
+          const float cmn = slab_max(slab_max(0.0f, slab_min(clox, chix)),
+                                     slab_max(slab_min(cloy, chiy), slab_min(cloz, chiz)));
+          const float cmx = slab_min(slab_min(t, slab_max(clox, chix)),
+                                     slab_min(slab_max(cloy, chiy), slab_max(cloz, chiz)));
 #endif
           const bool hit = (cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility);
           const int s = 4 * q + j;
-          /* leaf codes carry the primitive count: ~(first << 4 | count) */
-          const int child = (int)ach[j];
-          cc[s] = child >= 0 ? child : ~((~child << 4) | (int)(amt[j] >> 28));
+          /* the node stores final codes: inner >= 0, leaf ~(first << 4 | count) */
+          cc[s] = (int)ach[j];
           tn[s] = hit ? cmn : CY_INF;
         }
       }
@@ -376,14 +424,39 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
       if (tn[0] == CY_INF) {
         goto pop;
       }
+      {
+        /* push the hit children after the nearest, far to near: make room in
+         * the ring first (its oldest entries move to the overflow arrays, as
+         * one push at a time would move them; rare), then write them */
+        int npush = 0;
 #pragma unroll
-      for (int s = W - 1; s >= 1; s--) {
-        if (tn[s] != CY_INF) {
-          if (!CY_STACK_PUSH(cc[s], tn[s])) {
-            cy_set_error(err, CY_ERR_BVH_STACK, W);
-            return found_hit;
+        for (int s = 1; s < W; s++) {
+          npush += tn[s] != CY_INF ? 1 : 0;
+        }
+        if (n_ring + npush > CY_LDS_STACKW) {
+          while (n_ring + npush > CY_LDS_STACKW) {
+            if (n_over == CY_OVER_STACK) {
+              cy_set_error(err, CY_ERR_BVH_STACK, W);
+              return found_hit;
+            }
+            const CyStackEntry old = ring[((top - n_ring) & (CY_LDS_STACKW - 1)) * CY_RING_STRIDE];
+            over_node[n_over] = old.node;
+            over_t[n_over] = old.t;
+            n_over++;
+            n_ring--;
           }
         }
+#pragma unroll
+        for (int s = W - 1; s >= 1; s--) {
+          if (tn[s] != CY_INF) {
+            CyStackEntry e_;
+            e_.node = cc[s];
+            e_.t = tn[s];
+            ring[top * CY_RING_STRIDE] = e_;
+            top = (top + 1) & (CY_LDS_STACKW - 1);
+          }
+        }
+        n_ring += npush;
       }
       code = cc[0];
       code_t = tn[0];
@@ -635,8 +708,7 @@ CY_FN bool bvhw_traverse_ww(const CyGlobals *kg,
           const float cmx = min4(t, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
           const bool hit = (cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility);
           const int s = 4 * q + j;
-          const int child = (int)ach[j];
-          cc[s] = child >= 0 ? child : ~((~child << 4) | (int)(amt[j] >> 28));
+          cc[s] = (int)ach[j];
           tn[s] = hit ? cmn : CY_INF;
         }
       }

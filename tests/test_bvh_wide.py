@@ -70,9 +70,10 @@ def test_collapse_structure(case):
     assert np.all(refs[is_root] == 0) and np.all(refs[~is_root] == 1)
     # the leaf ranges tile the primitive array exactly once (instance slots,
     # prim_type 0, are entered through count-0 instance leaves instead)
-    starts, counts = ~child[leaf], meta[leaf] >> 28
+    starts, counts = (~child[leaf]) >> 4, meta[leaf] >> 28
+    assert np.array_equal((~child[leaf]) & 15, counts)
     tri_leaf = counts > 0
-    assert set((~child[leaf])[~tri_leaf].tolist()) == set(inst_objects.tolist())
+    assert set(((~child[leaf]) >> 4)[~tri_leaf].tolist()) == set(inst_objects.tolist())
     starts, counts = starts[tri_leaf], counts[tri_leaf]
     cover = np.zeros(len(ds.arrays["__prim_index"]), dtype=np.int32)
     for s, c in zip(starts.tolist(), counts.tolist()):
