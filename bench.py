@@ -74,6 +74,8 @@ def parse(argv=None):
     p.add_argument("--stream-hold-sweep", default="33554432",
                    help="comma-separated extra holds for more tile-stream legs (default: 2^25, the share the "
                         "plugin gives each of several devices on one queue)")
+    p.add_argument("--profile-shard", type=int, default=1,
+                   help="profiling only (N=1): the timed frame is rank 0's rows of an N-way row split")
     p.add_argument("--scaling-proxy", default="2,4,8",
                    help="single-GPU proxy of strong scaling (rank 0, N=1 only): for each N, rank 0's rows of an "
                         "N-way row split rendered alone and timed; empty disables")
@@ -156,6 +158,9 @@ def main():
     W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
     shard = RowShard(rank, world, W, H)
     rows_pad = -(-H // world)  # every rank's buffer has the same size for the gather
+    if args.profile_shard > 1 and world == 1:
+        shard = RowShard(0, args.profile_shard, W, H)
+        rows_pad = shard.rows
     use_tiles = args.shard == "tiles" or (args.shard == "auto" and world > 1 and
                                            bool(ds.data.film.pass_adaptive_aux_buffer))
     if use_tiles:
@@ -203,7 +208,7 @@ def main():
     def film_to_host():
         """Finished film to rank 0's host memory (gather of the row-interleaved parts)."""
         if world == 1:
-            film_host.copy_(local[:H])
+            film_host[:rows_pad].copy_(local[:H])
             return
         if use_tiles:
             dist.all_gather_into_tensor(gathered.view(-1), (local if gather_gpu else local.cpu()).view(-1))
@@ -257,7 +262,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
-    total_samples = W * H * S * args.steps
+    total_samples = W * (shard.rows if (args.profile_shard > 1 and world == 1) else H) * S * args.steps
     value = total_samples / elapsed / 1e6
     film = film_host.numpy().copy() if rank == 0 else None
 

@@ -13,6 +13,7 @@
  *
  * Field order follows kernel_types.h:1118-1572 (KernelCamera ... KernelBake),
  * 1575-1670 (KernelObject, KernelLight, KernelLightDistribution, KernelShader),
+ * 1551-1562 (KernelParticle),
  * util/util_transform.h:31 (Transform) and util/util_projection.h:26.
  *
  * Plain C, no HIP or torch types: included by host C/C++, by HIP device code
@@ -303,6 +304,17 @@ typedef struct __attribute__((aligned(16))) hc_ProjectionTransform { hc_float4 x
   X(int32_t, pad2, 1) \
   X(int32_t, pad3, 1)
 
+/* KernelParticle (kernel_types.h:1551-1562): the Particle Info node's record */
+#define HC_KERNEL_PARTICLE_FIELDS(X) \
+  X(int32_t, index, 1) \
+  X(float, age, 1) \
+  X(float, lifetime, 1) \
+  X(float, size, 1) \
+  X(hc_float4, rotation, 1) \
+  X(hc_float4, location, 1) \
+  X(hc_float4, velocity, 1) \
+  X(hc_float4, angular_velocity, 1)
+
 #define HC_FIELD_DECL(type, name, count) type name[count];
 #define HC_FIELD_DECL1(type, name, count) HC_FIELD_DECL_##count(type, name)
 #define HC_FIELD_DECL_1(type, name) type name;
@@ -324,6 +336,7 @@ HC_DECLARE_STRUCT(hc_KernelObject, HC_KERNEL_OBJECT_FIELDS)
 HC_DECLARE_STRUCT(hc_KernelLight, HC_KERNEL_LIGHT_FIELDS)
 HC_DECLARE_STRUCT(hc_KernelLightDistribution, HC_KERNEL_LIGHT_DISTRIBUTION_FIELDS)
 HC_DECLARE_STRUCT(hc_KernelShader, HC_KERNEL_SHADER_FIELDS)
+HC_DECLARE_STRUCT(hc_KernelParticle, HC_KERNEL_PARTICLE_FIELDS)
 
 typedef struct __attribute__((aligned(16))) hc_KernelData {
   hc_KernelCamera cam;

@@ -348,6 +348,7 @@ long cref_sizeof(const char *name)
   HC_SZ(KernelLight)
   HC_SZ(KernelLightDistribution)
   HC_SZ(KernelShader)
+  HC_SZ(KernelParticle)
   HC_SZ(WorkTile)
 #undef HC_SZ
   return -1;
@@ -368,6 +369,7 @@ long cref_offsetof(const char *sname, const char *fname)
 #define HC_FIELDS_KernelBake HC_KERNEL_BAKE_FIELDS
 #define HC_FIELDS_KernelObject HC_KERNEL_OBJECT_FIELDS
 #define HC_FIELDS_KernelShader HC_KERNEL_SHADER_FIELDS
+#define HC_FIELDS_KernelParticle HC_KERNEL_PARTICLE_FIELDS
 #define HC_OFF_FIELD_KernelCamera(t, f, c) \
   if (strcmp(fname, #f) == 0) \
     return (long)offsetof(KernelCamera, f);
@@ -395,6 +397,9 @@ long cref_offsetof(const char *sname, const char *fname)
 #define HC_OFF_FIELD_KernelShader(t, f, c) \
   if (strcmp(fname, #f) == 0) \
     return (long)offsetof(KernelShader, f);
+#define HC_OFF_FIELD_KernelParticle(t, f, c) \
+  if (strcmp(fname, #f) == 0) \
+    return (long)offsetof(KernelParticle, f);
   HC_OFF(KernelCamera)
   HC_OFF(KernelFilm)
   HC_OFF(KernelBackground)
@@ -404,6 +409,7 @@ long cref_offsetof(const char *sname, const char *fname)
   HC_OFF(KernelBake)
   HC_OFF(KernelObject)
   HC_OFF(KernelShader)
+  HC_OFF(KernelParticle)
   /* Structs with unions: check the named members explicitly. */
   if (strcmp(sname, "KernelLight") == 0) {
     if (strcmp(fname, "type") == 0) return (long)offsetof(KernelLight, type);

@@ -58,6 +58,7 @@ STRUCT_MACROS = {
     "KernelLight": "HC_KERNEL_LIGHT_FIELDS",
     "KernelLightDistribution": "HC_KERNEL_LIGHT_DISTRIBUTION_FIELDS",
     "KernelShader": "HC_KERNEL_SHADER_FIELDS",
+    "KernelParticle": "HC_KERNEL_PARTICLE_FIELDS",
 }
 
 
@@ -123,6 +124,7 @@ KernelObject = _make_struct("KernelObject", _FIELDS["KernelObject"])
 KernelLight = _make_struct("KernelLight", _FIELDS["KernelLight"])
 KernelLightDistribution = _make_struct("KernelLightDistribution", _FIELDS["KernelLightDistribution"])
 KernelShader = _make_struct("KernelShader", _FIELDS["KernelShader"])
+KernelParticle = _make_struct("KernelParticle", _FIELDS["KernelParticle"])
 
 
 class KernelData(ctypes.Structure):
@@ -150,6 +152,7 @@ STRUCTS = {
     "KernelLight": KernelLight,
     "KernelLightDistribution": KernelLightDistribution,
     "KernelShader": KernelShader,
+    "KernelParticle": KernelParticle,
 }
 
 SIZEOF_KERNEL_DATA = 1584

@@ -125,7 +125,9 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
  * its items right after a's (stream_fill appends a tile's chunks in a row) */
 static __device__ bool stream_chunk_continues(const CyTileDesc &a, const CyTileDesc &b)
 {
-  return b.buffer == a.buffer && b.x == a.x && b.y == a.y && b.w == a.w && b.h == a.h &&
+  /* groups of one tile only (a tile split in sample ranges is never grouped) */
+  return a.group_npix == (uint)(a.w * a.h) && b.group_npix == (uint)(b.w * b.h) && a.px_begin == 0 &&
+         b.px_begin == 0 && b.buffer == a.buffer && b.x == a.x && b.y == a.y && b.w == a.w && b.h == a.h &&
          b.start_sample == a.start_sample + a.num_samples &&
          b.item_begin == a.item_begin + (uint)(a.w * a.h) * (uint)a.num_samples;
 }
@@ -2257,9 +2259,11 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *)
 static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shaders,
                             const std::vector<void *> &tex_mem, const std::vector<uint32_t> &shader_flags,
                             bool *uses_tex, bool *uses_bssrdf, bool *uses_disk_bssrdf, bool *uses_attr,
-                            bool *uses_ray_diff, bool *uses_ies, int *surface_closures, int *volume_closures)
+                            bool *uses_ray_diff, bool *uses_ies, bool *uses_particles, int *surface_closures,
+                            int *volume_closures)
 {
   *uses_tex = false;
+  *uses_particles = false;
   *uses_ies = false;
   *uses_ray_diff = false;
   *uses_bssrdf = false;
@@ -2403,6 +2407,25 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
             return "shader " + std::to_string(sh) + ": principled volume blackbody emission is not implemented";
           }
           closures += 1;
+          tex = true;
+          break;
+        case NODE_CLOSURE_HOLDOUT: /* svm_closure.h:1043-1057 */
+          closures += 1;
+          tex = true;
+          break;
+        case NODE_TEXTURE_MAPPING: /* three matrix rows */
+          len = 4;
+          tex = true;
+          break;
+        case NODE_MIN_MAX: /* min and max rows */
+          len = 3;
+          tex = true;
+          break;
+        case NODE_PARTICLE_INFO:
+          *uses_particles = true;
+          tex = true;
+          break;
+        case NODE_HAIR_INFO:
           tex = true;
           break;
         case NODE_CLOSURE_EMISSION:
@@ -2704,9 +2727,15 @@ int hipcy_load_kernels(hipcy_device *dev)
     }
   }
   bool uses_bssrdf = false, uses_disk_bssrdf = false, uses_attr = false, uses_ray_diff = false, uses_ies = false;
+  bool uses_particles = false;
   int surface_closures = 0, volume_closures = 0;
   why = svm_scan(dev->svm_nodes, dev->num_shaders, dev->tex_mem, shader_flags, &dev->shade_tex, &uses_bssrdf,
-                 &uses_disk_bssrdf, &uses_attr, &uses_ray_diff, &uses_ies, &surface_closures, &volume_closures);
+                 &uses_disk_bssrdf, &uses_attr, &uses_ray_diff, &uses_ies, &uses_particles, &surface_closures,
+                 &volume_closures);
+  if (why.empty() && uses_particles && dev->globals.find("__particles") == dev->globals.end()) {
+    /* ParticleSystemManager::device_update_particles (particles.cpp:61-105) */
+    why = "particle info node without the __particles table bound";
+  }
   if (why.empty() && uses_ies && dev->globals.find("__ies") == dev->globals.end()) {
     /* LightManager::device_update_ies (light.cpp:1080-1125) */
     why = "IES texture without the __ies table bound";
@@ -2878,7 +2907,8 @@ struct PassLane {
   uint n_active;
   CyTile tile;
   hipEvent_t done;
-  bool stream = false; /* tile stream lane: also reduce the live paths' smallest item */
+  bool stream = false;  /* tile stream lane */
+  bool min_live = false; /* tile stream: also reduce the live paths' smallest item */
 };
 
 /* The queue sort in effect: the requested mode, or (automatic, -1) the
@@ -3066,7 +3096,7 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     HIP_CHECK(dev, hipEventRecord(p.d, s));
     quads->push_back(p);
   }
-  if (ln.stream) {
+  if (ln.stream && ln.min_live) {
     /* tile streams: the smallest item still held by a live path (min_live
      * shards) and the next unclaimed item (cnt[4]) tell the host which tiles
      * are done */
@@ -3260,6 +3290,8 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
     d.start_sample = tk.start_sample;
     d.item_begin = 0;
     d.num_samples = tk.num_samples;
+    d.group_npix = 0; /* tile streams only */
+    d.group_first = 0;
     descs.push_back(d);
     npix += (size_t)tk.w * tk.h;
   }
@@ -3470,11 +3502,21 @@ struct FeedTile {
   bool released = false; /* handed back through feed->release */
 };
 
+/* A group of tiles appended to a lane together with one sample range: its
+ * items are numbered sample-major over the group's pixels (CyTileDesc
+ * group_npix), as a whole-frame pass numbers its items, so the rays in flight
+ * spread over all of the group's tiles instead of piling onto one 64x64 tile
+ * (a single tile's samples one after the other made the camera launch 45 %
+ * slower: every CU fetched the same few BVH nodes and triangles).  A tile
+ * too large for the record ring is split in sample ranges, each a group of
+ * one. */
 struct StreamChunk {
-  CyTileDesc d;
-  uint item_end;
-  int feed;  /* FeedTile index */
-  bool last; /* the RenderTile's last chunk */
+  uint item_begin, item_end;
+  size_t desc_begin, desc_end; /* the group's tile descriptors */
+  int start_sample, num_samples;
+  uint npix;    /* pixels of the group (its items per sample) */
+  bool open;    /* still taking tiles (descriptors not yet uploaded) */
+  bool grouped; /* whole tiles: more may join */
 };
 
 struct StreamLane {
@@ -3485,6 +3527,10 @@ struct StreamLane {
   CyTileDesc *desc_dev = nullptr;
   CyTileDesc *desc_host = nullptr; /* pinned, append-only within a session */
   int desc_cap = 0;
+  size_t n_descs = 0;   /* descriptors written to desc_host */
+  size_t uploaded = 0;  /* descriptors copied to desc_dev (closed groups only) */
+  std::vector<int> desc_feed;   /* per descriptor: its FeedTile */
+  std::vector<char> desc_last;  /* per descriptor: the RenderTile's last samples */
   std::vector<StreamChunk> chunks;
   size_t done_chunks = 0; /* chunks whose accumulation is enqueued */
   size_t lo_chunk = 0;    /* first chunk that can still hand out items */
@@ -3543,9 +3589,31 @@ static void feed_release_all(StreamState &st)
   }
 }
 
-/* Append chunks to the lane until it holds `target` unclaimed items (or the
- * queue, the ring or the lane's numbering runs out). */
-static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chunk)
+/* Close the lane's open group: its descriptors get the group's pixel count and
+ * every descriptor not yet on the device is copied there in one transfer. */
+static int stream_close(hipcy_device *dev, StreamLane &S)
+{
+  if (!S.chunks.empty() && S.chunks.back().open) {
+    StreamChunk &g = S.chunks.back();
+    for (size_t k = g.desc_begin; k < g.desc_end; k++) {
+      S.desc_host[k].group_npix = g.npix;
+    }
+    g.open = false;
+  }
+  if (S.n_descs > S.uploaded) {
+    HIP_CHECK(dev, hipMemcpyAsync(S.desc_dev + S.uploaded, S.desc_host + S.uploaded,
+                                  (S.n_descs - S.uploaded) * sizeof(CyTileDesc), hipMemcpyHostToDevice, S.ln.s));
+    S.uploaded = S.n_descs;
+  }
+  return 0;
+}
+
+/* Append tiles to the lane until it holds `target` unclaimed items (or the
+ * queue, the ring or the lane's numbering runs out): whole tiles with the
+ * sample range of the lane's open group join it.  one_chunk: at most one tile
+ * (the initial round-robin fill); keep_open: leave the group open for the next
+ * call (closed otherwise, so its items can be handed out). */
+static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chunk, bool keep_open = false)
 {
   hipcy_device *dev = st.dev;
   uint unclaimed = S.n_items - std::min(S.work_next, S.n_items);
@@ -3589,13 +3657,21 @@ static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chu
     const int remaining = F.t.start_sample + F.t.num_samples - F.next_sample;
     const int chunk_s = std::min(remaining, (int)std::max<uint>(1u, (S.ring_cap / 4) / npix));
     const uint items = npix * (uint)chunk_s;
-    if ((uint64_t)S.n_items + items > CY_STREAM_ITEM_CAP || (int)S.chunks.size() >= S.desc_cap) {
+    const bool whole = chunk_s == remaining && F.next_sample == F.t.start_sample;
+    StreamChunk *g = (!S.chunks.empty() && S.chunks.back().open) ? &S.chunks.back() : nullptr;
+    const bool join = whole && g && g->grouped && g->start_sample == F.next_sample && g->num_samples == chunk_s &&
+                      (uint64_t)g->npix + npix <= S.ring_cap;
+    if ((uint64_t)S.n_items + items > CY_STREAM_ITEM_CAP || (int)S.n_descs >= S.desc_cap) {
       S.closed = true;
       break;
     }
     if ((uint64_t)S.n_items + items - S.ring_head > S.ring_cap) {
       break; /* ring full until older tiles complete */
     }
+    if (g && !join && stream_close(dev, S) != 0) {
+      return -1;
+    }
+    const size_t k = S.n_descs;
     CyTileDesc d;
     d.x = F.t.x;
     d.y = F.t.y;
@@ -3604,29 +3680,49 @@ static int stream_fill(StreamState &st, StreamLane &S, uint target, bool one_chu
     d.offset = F.t.offset;
     d.stride = F.t.stride;
     d.buffer = (float *)F.t.buffer;
-    d.px_begin = 0;
     d.start_sample = F.next_sample;
-    d.item_begin = S.n_items;
     d.num_samples = chunk_s;
-    const size_t k = S.chunks.size();
+    d.group_npix = npix; /* the group's, set when it closes */
+    if (join) {
+      d.item_begin = g->item_begin;
+      d.px_begin = g->npix;
+      d.group_first = (uint)g->desc_begin;
+      g->npix += npix;
+      g->item_end += items;
+      g->desc_end = k + 1;
+    }
+    else {
+      d.item_begin = S.n_items;
+      d.px_begin = 0;
+      d.group_first = (uint)k;
+      StreamChunk c;
+      c.item_begin = S.n_items;
+      c.item_end = S.n_items + items;
+      c.desc_begin = k;
+      c.desc_end = k + 1;
+      c.start_sample = F.next_sample;
+      c.num_samples = chunk_s;
+      c.npix = npix;
+      c.open = true;
+      c.grouped = whole;
+      S.chunks.push_back(c);
+    }
     S.desc_host[k] = d;
-    HIP_CHECK(dev, hipMemcpyAsync(S.desc_dev + k, S.desc_host + k, sizeof(CyTileDesc), hipMemcpyHostToDevice,
-                                  S.ln.s));
-    StreamChunk c;
-    c.d = d;
-    c.item_end = S.n_items + items;
-    c.feed = S.cur_feed;
-    c.last = chunk_s == remaining;
-    S.chunks.push_back(c);
+    S.n_descs = k + 1;
+    S.desc_feed.push_back(S.cur_feed);
+    S.desc_last.push_back(chunk_s == remaining ? 1 : 0);
     S.n_items += items;
     unclaimed += items;
     F.next_sample += chunk_s;
-    if (c.last) {
+    if (chunk_s == remaining) {
       S.cur_feed = -1;
     }
     if (one_chunk) {
       break;
     }
+  }
+  if (!keep_open && stream_close(dev, S) != 0) {
+    return -1;
   }
   return 0;
 }
@@ -3636,25 +3732,29 @@ static int stream_complete(StreamState &st, StreamLane &S, uint bound)
 {
   hipcy_device *dev = st.dev;
   const int pass_stride = dev->data_host.film.pass_stride;
-  const size_t first = S.done_chunks;
+  const size_t first = S.done_chunks < S.chunks.size() ? S.chunks[S.done_chunks].desc_begin : 0;
+  size_t last = first;
   int max_pix = 0;
-  while (S.done_chunks < S.chunks.size() && S.chunks[S.done_chunks].item_end <= bound) {
+  while (S.done_chunks < S.chunks.size() && !S.chunks[S.done_chunks].open &&
+         S.chunks[S.done_chunks].item_end <= bound) {
     const StreamChunk &c = S.chunks[S.done_chunks];
-    max_pix = std::max(max_pix, c.d.w * c.d.h);
-    if (c.last) {
-      S.release.push_back(c.feed);
+    for (size_t k = c.desc_begin; k < c.desc_end; k++) {
+      max_pix = std::max(max_pix, S.desc_host[k].w * S.desc_host[k].h);
+      if (S.desc_last[k]) {
+        S.release.push_back(S.desc_feed[k]);
+      }
     }
+    last = c.desc_end;
     S.done_chunks++;
   }
-  if (S.done_chunks > first) {
-    /* the completed chunks are consecutive in the lane's descriptor array */
-    hipLaunchKernelGGL(k_accumulate_stream, dim3((unsigned)((max_pix + CY_BLOCK - 1) / CY_BLOCK),
-                                                 (unsigned)(S.done_chunks - first)),
-                       dim3(CY_BLOCK), 0, S.ln.s, (const CyTileDesc *)(S.desc_dev + first),
-                       (const hc_float4 *)S.ring, S.ring_cap - 1, pass_stride);
+  if (last > first) {
+    /* the completed groups' descriptors are consecutive in the lane's array */
+    hipLaunchKernelGGL(k_accumulate_stream, dim3((unsigned)((max_pix + CY_BLOCK - 1) / CY_BLOCK), (unsigned)(last - first)),
+                       dim3(CY_BLOCK), 0, S.ln.s, (const CyTileDesc *)(S.desc_dev + first), (const hc_float4 *)S.ring,
+                       S.ring_cap - 1, pass_stride);
   }
   HIP_CHECK(dev, hipGetLastError());
-  S.ring_head = S.done_chunks < S.chunks.size() ? S.chunks[S.done_chunks].d.item_begin : S.n_items;
+  S.ring_head = S.done_chunks < S.chunks.size() ? S.chunks[S.done_chunks].item_begin : S.n_items;
   return 0;
 }
 
@@ -3676,8 +3776,9 @@ static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
     S.lo_chunk++;
   }
   L.tile.n_items = S.n_items;
-  L.tile.n_tiles = (int)S.chunks.size();
-  L.tile.desc_lo = (uint)std::min(S.lo_chunk, S.chunks.empty() ? 0 : S.chunks.size() - 1);
+  L.tile.n_tiles = (int)S.uploaded;
+  L.tile.desc_lo = S.lo_chunk < S.chunks.size() ? (uint)S.chunks[S.lo_chunk].desc_begin
+                                                : (uint)(S.uploaded ? S.uploaded - 1 : 0);
   const uint avail = S.n_items - S.work_next;
   uint n_active = n_live;
   if (n_live < (uint)S.lane_slots && avail > 0) {
@@ -3737,17 +3838,23 @@ static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t la
     t.write_aux = 0;
     t.npix = 1;
   }
-  /* initial fill, round robin one chunk at a time: each lane wants its slots'
-   * worth of camera rays plus as many in reserve */
+  /* initial fill, round robin one tile at a time: each lane wants its slots'
+   * worth of camera rays plus as many in reserve; a lane's tiles form one
+   * group (so every lane's rays in flight cover tiles all over the queue) */
   for (bool more = true; more;) {
     more = false;
     for (int l = 0; l < lanes; l++) {
       StreamLane &S = lane[l];
-      const size_t before = S.chunks.size();
-      if (stream_fill(st, S, 2 * (uint)lane_slots, true) != 0) {
+      const size_t before = S.n_descs;
+      if (stream_fill(st, S, 2 * (uint)lane_slots, true, true) != 0) {
         return -1;
       }
-      more |= S.chunks.size() > before;
+      more |= S.n_descs > before;
+    }
+  }
+  for (int l = 0; l < lanes; l++) {
+    if (stream_close(dev, lane[l]) != 0) {
+      return -1;
     }
   }
   if (st.feed_empty && st.carry.empty()) {
@@ -3784,7 +3891,7 @@ static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t la
     L.n_active = (uint)L.cam_n;
     S.work_next = (uint)L.cam_n;
     L.tile.n_items = S.n_items;
-    L.tile.n_tiles = (int)S.chunks.size();
+    L.tile.n_tiles = (int)S.uploaded;
     L.tile.desc_lo = 0;
     L.hcnt[4] = S.work_next;
     HIP_CHECK(dev, hipMemcpyAsync(L.cnt + 4, L.hcnt + 4, 4, hipMemcpyHostToDevice, L.s));
@@ -3796,6 +3903,11 @@ static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t la
   int head = 0, n_fifo = 0;
   bool queued[CY_LANES] = {};
   auto submit = [&](int l) -> int {
+    /* a group is complete only once no live path holds one of its items: with
+     * one incomplete group that is when the lane has no live path, which the
+     * counts tell; the smallest live item (k_stream_min_live, a pass over the
+     * queue) is needed only with two or more */
+    lane[l].ln.min_live = lane[l].chunks.size() > lane[l].done_chunks + 1;
     if (lane_iterate(dev, kg, lane[l].ln, W, ev, nullptr) != 0) {
       return -1;
     }
@@ -3826,9 +3938,12 @@ static int stream_session(StreamState &st, const CyGlobals &kg, int W, size_t la
     dev->stats.shadow_rays += L.hcnt[2];
     const uint n_live = L.hcnt[L.qb];
     uint wn = L.hcnt[4];
-    uint live_min = 0xFFFFFFFFu;
-    for (int k = 0; k < CY_MIN_SHARDS; k++) {
-      live_min = std::min(live_min, dev->min_live_host[CY_MIN_SHARDS * l + k]);
+    uint live_min = n_live > 0 ? 0u : 0xFFFFFFFFu;
+    if (L.min_live) {
+      live_min = 0xFFFFFFFFu;
+      for (int k = 0; k < CY_MIN_SHARDS; k++) {
+        live_min = std::min(live_min, dev->min_live_host[CY_MIN_SHARDS * l + k]);
+      }
     }
     if (wn > S.n_items) {
       /* claims past the end: put the counter back so appended items are

@@ -11,13 +11,18 @@
  *   svm_node_normal_map, svm_node_tangent  kernel/svm/svm_tex_coord.h:255-392
  *   ensure_valid_reflection                kernel/kernel_montecarlo.h:196-298
  *   svm_node_object_info                   kernel/svm/svm_geometry.h:104-139
+ *   svm_node_particle_info                 kernel/svm/svm_geometry.h:141-202
+ *   svm_node_hair_info, curve_thickness,
+ *   curve_tangent_normal                   kernel/svm/svm_geometry.h:204-243, geom/geom_curve.h:263-323
+ *   curve_attribute_float / float2 / float3 kernel/geom/geom_curve.h:28-200
  *   svm_node_attr_bump_dx / _dy            kernel/svm/svm_attribute.h:92-188
  *   svm_node_vertex_color_bump_dx / _dy    kernel/svm/svm_vertex_color.h:38-90
  *   svm_node_set_bump                      kernel/svm/svm_displace.h:21-84
- * The host packs attributes only for triangle meshes without subdivision
+ * The host packs attributes for triangle meshes without subdivision
  * (`__tri_patch` is all ~0, so attribute_primitive_type is always
- * ATTR_PRIM_GEOMETRY); an attribute found on a curve raises
- * CY_ERR_FEATURE.  Per-object maps: KernelObject.attribute_map_offset into
+ * ATTR_PRIM_GEOMETRY) and float / float2 / float3 attributes of curves (per
+ * curve or per key, e.g. the Hair Info node's intercept and random); an RGBA
+ * attribute found on a curve raises CY_ERR_FEATURE.  Per-object maps: KernelObject.attribute_map_offset into
  * `__attributes_map`, two rows (geometry, subdivision) per attribute, closed
  * by ATTR_STD_NONE.
  */
@@ -29,6 +34,8 @@ enum {
   NODE_VERTEX_COLOR = 17,
   NODE_SET_BUMP = 26,
   NODE_OBJECT_INFO = 48,
+  NODE_PARTICLE_INFO = 49,
+  NODE_HAIR_INFO = 50,
   NODE_TANGENT = 70,
   NODE_NORMAL_MAP = 71
 };
@@ -45,6 +52,9 @@ enum {
   ATTR_ELEMENT_VERTEX_MOTION = 5,
   ATTR_ELEMENT_CORNER = 6,
   ATTR_ELEMENT_CORNER_BYTE = 7,
+  ATTR_ELEMENT_CURVE = 8,
+  ATTR_ELEMENT_CURVE_KEY = 9,
+  ATTR_ELEMENT_CURVE_KEY_MOTION = 10,
   ATTR_ELEMENT_VOXEL = 11
 };
 enum { NODE_ATTR_FLOAT = 0, NODE_ATTR_FLOAT2 = 1, NODE_ATTR_FLOAT3 = 2, NODE_ATTR_RGBA = 3 };
@@ -199,10 +209,47 @@ CY_FN void triangle_attribute(const CyGlobals *kg, const CyAttr &desc, int prim,
   }
 }
 
+/* curve_attribute_float / float2 / float3 (geom_curve.h:28-200) of the curve
+ * segment at parameter u: per-key values interpolated (1 - u) * f0 + u * f1
+ * between the segment's keys, per-curve and per-object ones as stored, 0
+ * otherwise.  du_dx (the bump X form) adds du.dx * (f1 - f0) for per-key
+ * values; the Y form's derivative is 0 on curves. */
+CY_FN void curve_attribute(const CyGlobals *kg, const CyAttr &desc, int prim, int type, float u, int n, float out[4],
+                           const float *du_dx = nullptr)
+{
+  int idx[2] = {0, 0};
+  int m = 0;
+  const int e = desc.element;
+  if (e == ATTR_ELEMENT_CURVE) {
+    idx[0] = desc.offset + prim;
+    m = 1;
+  }
+  else if (e == ATTR_ELEMENT_CURVE_KEY || e == ATTR_ELEMENT_CURVE_KEY_MOTION) {
+    const int k0 = as_int(kg->__curves[prim].x) + (int)CY_PRIMITIVE_UNPACK_SEGMENT((uint)type);
+    idx[0] = desc.offset + k0;
+    idx[1] = desc.offset + k0 + 1;
+    m = 2;
+  }
+  else if (e == ATTR_ELEMENT_OBJECT || e == ATTR_ELEMENT_MESH) {
+    idx[0] = desc.offset;
+    m = 1;
+  }
+  float f[2][4] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+  for (int k = 0; k < m; k++) {
+    attr_fetch(kg, n, false, idx[k], f[k]);
+  }
+  for (int c = 0; c < n; c++) {
+    out[c] = (m == 2) ? (1.0f - u) * f[0][c] + u * f[1][c] : (m == 1) ? f[0][c] : 0.0f;
+    if (du_dx && m == 2) {
+      out[c] = out[c] + *du_dx * (f[1][c] - f[0][c]);
+    }
+  }
+}
+
 /* svm_node_attr: the attribute read with the stored type, converted to the
  * node's output type (float: the average of a colour / vector) */
 CY_FN void svm_node_attr(const CyGlobals *kg, int object, int prim, int type, float u, float v, CySvmStack stack,
-                         hc_uint4 node, uint *err, const float *dd = nullptr)
+                         hc_uint4 node, uint *err, const float *dd = nullptr, int bump_axis = 0)
 {
   const uint out_offset = node.z;
   const int out_type = (int)node.w;
@@ -221,15 +268,19 @@ CY_FN void svm_node_attr(const CyGlobals *kg, int object, int prim, int type, fl
     desc.type = out_type;
   }
   const bool tri = (type & PRIMITIVE_ALL_TRIANGLE) != 0;
-  if (!tri && (type & PRIMITIVE_ALL_CURVE) && desc.element != ATTR_ELEMENT_NONE) {
-    cy_set_error(err, CY_ERR_FEATURE, 11); /* curve attributes are not packed */
-  }
+  const bool curve = !tri && (type & PRIMITIVE_ALL_CURVE);
   float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   const int n = (desc.type == NODE_ATTR_FLOAT) ? 1 : (desc.type == NODE_ATTR_FLOAT2) ? 2 :
                 (desc.type == NODE_ATTR_RGBA)  ? 4 :
                                                  3;
+  if (curve && n == 4 && desc.element != ATTR_ELEMENT_NONE) {
+    cy_set_error(err, CY_ERR_FEATURE, 11); /* RGBA attributes of curves are not packed */
+  }
   if (tri) {
     triangle_attribute(kg, desc, prim, u, v, n, f, dd);
+  }
+  else if (curve && n < 4) {
+    curve_attribute(kg, desc, prim, type, u, n, f, (dd && bump_axis == 1) ? &dd[0] : nullptr);
   }
   if (n == 1) {
     if (out_type == NODE_ATTR_FLOAT) {
@@ -303,6 +354,9 @@ CY_FN void surface_attribute(const CyGlobals *kg, const CyAttrIn &in, const CyAt
   f[0] = f[1] = f[2] = f[3] = 0.0f;
   if (in.type & PRIMITIVE_ALL_TRIANGLE) {
     triangle_attribute(kg, desc, in.prim, in.u, in.v, n, f);
+  }
+  else if ((in.type & PRIMITIVE_ALL_CURVE) && n < 4) {
+    curve_attribute(kg, desc, in.prim, in.type, in.u, n, f);
   }
   else if ((in.type & PRIMITIVE_ALL_CURVE) && desc.element != ATTR_ELEMENT_NONE) {
     cy_set_error(err, CY_ERR_FEATURE, 11);
@@ -521,6 +575,78 @@ CY_FN void svm_node_object_info(const CyGlobals *kg, const CyAttrIn &in, CySvmSt
   svm_store(stack, out_offset, data, err);
 }
 
+/* svm_node_particle_info (svm_geometry.h:141-202): the record of the object's
+ * particle (object_particle_id, geom_object.h:267-273; particle 0 for no object) */
+CY_FN void svm_node_particle_info(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, uint type,
+                                  uint out_offset, uint *err)
+{
+  const int id = (in.object == OBJECT_NONE) ? 0 : kg->__objects[in.object].particle_index;
+  const hc_KernelParticle &p = kg->__particles[id];
+  switch (type) {
+    case 0: /* NODE_INFO_PAR_INDEX: particle_index is a uint */
+      svm_store(stack, out_offset, (float)(uint)p.index, err);
+      break;
+    case 1: /* NODE_INFO_PAR_RANDOM: hash_uint2_to_float(particle_index, 0) */
+      svm_store(stack, out_offset, (float)hash_uint2((uint)p.index, 0u) / (float)0xFFFFFFFFu, err);
+      break;
+    case 2:
+      svm_store(stack, out_offset, p.age, err);
+      break;
+    case 3:
+      svm_store(stack, out_offset, p.lifetime, err);
+      break;
+    case 4:
+      svm_store3(stack, out_offset, mk3(p.location.x, p.location.y, p.location.z), err);
+      break;
+    case 6:
+      svm_store(stack, out_offset, p.size, err);
+      break;
+    case 7:
+      svm_store3(stack, out_offset, mk3(p.velocity.x, p.velocity.y, p.velocity.z), err);
+      break;
+    case 8:
+      svm_store3(stack, out_offset, mk3(p.angular_velocity.x, p.angular_velocity.y, p.angular_velocity.z), err);
+      break;
+  }
+}
+
+#if CY_CLOSURE_EXT
+/* svm_node_hair_info (svm_geometry.h:204-243): strand flag, curve_thickness
+ * (geom_curve.h:263-286: twice the radius interpolated between the segment's
+ * keys) and curve_tangent_normal (:307-323); intercept and random are curve
+ * attributes (NODE_ATTR) */
+CY_FN void svm_node_hair_info(const CyGlobals *kg, const CyAttrIn &in, CySvmStack stack, uint type, uint out_offset,
+                              uint *err)
+{
+  const bool curve = (in.type & PRIMITIVE_ALL_CURVE) != 0;
+  switch (type) {
+    case 0: /* NODE_INFO_CURVE_IS_STRAND */
+      svm_store(stack, out_offset, curve ? 1.0f : 0.0f, err);
+      break;
+    case 2: { /* NODE_INFO_CURVE_THICKNESS */
+      float r = 0.0f;
+      if (curve) {
+        const int k0 = as_int(kg->__curves[in.prim].x) + (int)CY_PRIMITIVE_UNPACK_SEGMENT((uint)in.type);
+        const hc_float4 P0 = kg->__curve_keys[k0], P1 = kg->__curve_keys[k0 + 1];
+        r = (P1.w - P0.w) * in.u + P0.w;
+      }
+      svm_store(stack, out_offset, r * 2.0f, err);
+      break;
+    }
+    case 3: { /* NODE_INFO_CURVE_TANGENT_NORMAL */
+      cfloat3 tgN = mk3(0.0f, 0.0f, 0.0f);
+      if (curve) {
+        const cfloat3 mI = neg3(in.I);
+        tgN = neg3(sub3(mI, mul3f(in.dPdu, dot3(in.dPdu, mI) / len_squared3(in.dPdu))));
+        tgN = normalize3(tgN);
+      }
+      svm_store3(stack, out_offset, tgN, err);
+      break;
+    }
+  }
+}
+#endif
+
 /* svm_geometry.h NODE_GEOM_T: primitive_tangent (geom_primitive.h:292-320),
  * the spherical tangent of the generated coordinates around Z, else (and on
  * curves) the normalised surface derivative dPdu */
@@ -609,12 +735,18 @@ CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
                                          const hc_float4 *attributes_float3,
                                          const uint32_t *attributes_uchar4,
                                          const hc_uint4 *tri_vindex,
+                                         const hc_float4 *curves,
+                                         const hc_float4 *curve_keys,
+                                         const hc_KernelParticle *particles,
                                          CyAttrIn in,
                                          CySvmStack stack,
                                          hc_uint4 node,
                                          uint *err)
 {
   CyGlobals kgv;
+  kgv.__curves = curves;
+  kgv.__curve_keys = curve_keys;
+  kgv.__particles = particles;
   kgv.__objects = objects;
   kgv.__shaders = shaders;
   kgv.__attributes_map = attributes_map;
@@ -632,7 +764,11 @@ CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
 #endif
   switch (node.x) {
     case NODE_ATTR:
+#if CY_CLOSURE_EXT
+      svm_node_attr(kg, in.object, in.prim, in.type, in.u, in.v, stack, node, err, ddp, in.bump);
+#else
       svm_node_attr(kg, in.object, in.prim, in.type, in.u, in.v, stack, node, err, ddp);
+#endif
       break;
     case NODE_VERTEX_COLOR:
       svm_node_vertex_color(kg, in.object, in.prim, in.type, in.u, in.v, stack, node.y, node.z, node.w, err, ddp);
@@ -651,6 +787,14 @@ CY_NOINLINE void svm_eval_attribute_node(const hc_KernelObject *objects,
     case NODE_OBJECT_INFO:
       svm_node_object_info(kg, in, stack, node.y, node.z, err);
       break;
+    case NODE_PARTICLE_INFO:
+      svm_node_particle_info(kg, in, stack, node.y, node.z, err);
+      break;
+#if CY_CLOSURE_EXT
+    case NODE_HAIR_INFO:
+      svm_node_hair_info(kg, in, stack, node.y, node.z, err);
+      break;
+#endif
     case NODE_GEOMETRY: /* NODE_GEOM_T only */
       svm_node_geometry_tangent(kg, in, stack, node.z, err);
       break;

@@ -46,7 +46,8 @@
   X(hc_float2, __attributes_float2) \
   X(hc_float4, __attributes_float3) \
   X(uint32_t, __attributes_uchar4) \
-  X(float, __ies)
+  X(float, __ies) \
+  X(hc_KernelParticle, __particles)
 
 typedef struct CyGlobals {
   const hc_KernelData *data;

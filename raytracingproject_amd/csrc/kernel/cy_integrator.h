@@ -85,10 +85,18 @@ typedef struct CyTileDesc {
   int x, y, w, h;
   int offset, stride;
   float *buffer;
-  uint px_begin;    /* first pixel of the tile in the pass's pixel numbering */
+  uint px_begin;    /* first pixel of the tile in the pass's (tile streams: its group's) pixel numbering */
   int start_sample; /* tile streams: the tile's first sample */
-  uint item_begin;  /* tile streams: first work item of the tile in the lane's item numbering */
+  uint item_begin;  /* tile streams: first work item of the tile's group in the lane's item numbering */
   int num_samples;  /* tile streams: samples of the tile */
+  /* tile streams: a group of tiles with one sample range shares its items,
+   * numbered sample-major over the group's pixels (group_npix per sample,
+   * this tile's at px_begin ..), so the rays in flight at one time spread over
+   * every tile of the group as a whole-frame pass's do; group_first is the
+   * descriptor index of the group's first tile.  A tile alone (or one sample
+   * range of a tile too large for the record ring) is a group of one. */
+  uint group_npix;
+  uint group_first;
 } CyTileDesc;
 
 typedef struct CyTile {
@@ -556,8 +564,10 @@ CY_FN void pass_pixel(const CyTile *tile, uint p, int *x, int *y)
   }
 }
 
-/* Tile of a tile stream's work item (binary search of the tiles' first items
- * over the tiles that can still hand out items). */
+/* Group of a tile stream's work item: the last descriptor whose group starts
+ * at or before it (binary search over the tiles that can still hand out
+ * items; the tiles of one group share item_begin, so this is the group's last
+ * tile). */
 CY_FN int tile_of_item(const CyTile *tile, uint item)
 {
   int lo = (int)tile->desc_lo, hi = tile->n_tiles - 1;
@@ -574,15 +584,28 @@ CY_FN int tile_of_item(const CyTile *tile, uint item)
 }
 
 /* Pixel and sample of a work item (items are numbered sample-major; in a tile
- * stream, sample-major inside each tile). */
+ * stream, sample-major over each group's pixels). */
 CY_FN void item_pixel(const CyTile *tile, uint item, int *x, int *y, int *sample)
 {
   if (tile->stream) {
-    const CyTileDesc &d = tile->descs[tile_of_item(tile, item)];
-    const uint local = item - d.item_begin;
-    const uint npix = (uint)(d.w * d.h);
-    const uint p = local % npix;
-    *sample = d.start_sample + (int)(local / npix);
+    int k = tile_of_item(tile, item);
+    const CyTileDesc &g = tile->descs[k];
+    const uint local = item - g.item_begin;
+    const uint q = local % g.group_npix;
+    *sample = g.start_sample + (int)(local / g.group_npix);
+    /* the group's tile holding pixel q: the last with px_begin <= q */
+    int lo = (int)g.group_first;
+    while (lo < k) {
+      const int mid = (lo + k + 1) >> 1;
+      if (tile->descs[mid].px_begin <= q) {
+        lo = mid;
+      }
+      else {
+        k = mid - 1;
+      }
+    }
+    const CyTileDesc &d = tile->descs[lo];
+    const uint p = q - d.px_begin;
     *x = d.x + (int)(p % (uint)d.w);
     *y = d.y + (int)(p / (uint)d.w);
     return;
@@ -1010,14 +1033,15 @@ CY_FN void accumulate_pixel(const CyTile *tile, int p)
 }
 
 /* accumulate_pixel for pixel p of tile d of a tile stream: the tile's records
- * of sample k sit at item d.item_begin + k * w*h + p of the lane's ring. */
+ * of sample k sit at item d.item_begin + k * group_npix + px_begin + p of the
+ * lane's ring. */
 CY_FN void accumulate_stream_pixel(const CyTileDesc &d, const hc_float4 *ring, uint ring_mask, int pass_stride,
                                    int p)
 {
   float *buf = d.buffer + (size_t)(d.offset + d.x + p % d.w + (d.y + p / d.w) * d.stride) * pass_stride;
   float b0 = buf[0], b1 = buf[1], b2 = buf[2], b3 = buf[3];
-  const uint npix = (uint)(d.w * d.h);
-  const uint first = d.item_begin + (uint)p;
+  const uint npix = d.group_npix;
+  const uint first = d.item_begin + d.px_begin + (uint)p;
   /* the records of 8 samples are requested before they are added (in
    * sample order): a tile has few pixels, so each thread needs several
    * loads in flight */
@@ -1894,11 +1918,25 @@ CY_FN bool shade_path(const CyGlobals *kg,
 #endif
     shader_prepare_closures(&sd, &state);
 
-    /* kernel_path_shader_apply (kernel_path.h:254-321) */
-    if ((sd.object_flag & SD_OBJECT_SHADOW_CATCHER) || (sd.flag & SD_HOLDOUT) ||
-        (sd.object_flag & SD_OBJECT_HOLDOUT_MASK)) {
+    /* kernel_path_shader_apply (kernel_path.h:254-321); shadow catchers are
+     * refused by hipcy_load_kernels */
+    bool terminated = false;
+    if (sd.object_flag & SD_OBJECT_SHADOW_CATCHER) {
       cy_set_error(err, CY_ERR_FEATURE, 5);
     }
+    if (((sd.flag & SD_HOLDOUT) || (sd.object_flag & SD_OBJECT_HOLDOUT_MASK)) &&
+        (state.flag & PATH_RAY_TRANSPARENT_BACKGROUND)) {
+      /* holdout (kernel_path.h:285-296): the holdout weight makes the pixel
+       * transparent; a full holdout ends the path */
+      const cfloat3 holdout_weight = shader_holdout_apply(&sd);
+      if (KD->background.transparent) {
+        L_transparent += average3(mul3(holdout_weight, throughput));
+      }
+      if (holdout_weight.x == 1.0f && holdout_weight.y == 1.0f && holdout_weight.z == 1.0f) {
+        terminated = true;
+      }
+    }
+    if (!terminated) {
     if ((state.flag & PATH_RAY_CAMERA) && !(state.flag & PATH_RAY_SINGLE_PASS_DONE)) {
       /* kernel_write_data_passes: no data passes, only the single-pass flag */
       if (!(sd.flag & SD_TRANSPARENT) || KD->film.pass_alpha_threshold == 0.0f) {
@@ -1952,7 +1990,6 @@ CY_FN bool shade_path(const CyGlobals *kg,
 
     /* Russian roulette (kernel_path.h:587-599) */
     float probability = path_state_continuation_probability(kg, &state, throughput);
-    bool terminated = false;
     if (probability == 0.0f) {
       terminated = true;
     }
@@ -1965,6 +2002,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
         throughput = div3f(throughput, probability);
       }
     }
+    } /* !holdout end */
 
     /* kernel_path_subsurface_scatter (kernel_path_subsurface.h:26-110): a
      * picked BSSRDF moves the shading point to where the random walk leaves

@@ -1271,6 +1271,40 @@ CY_FN cfloat3 shader_bsdf_transparency(const CySD *sd)
   return (sd->flag & SD_TRANSPARENT) ? sd->closure_transparent_extinction : mk3(0.0f, 0.0f, 0.0f);
 }
 
+/* kernel_shader.h:1020-1053 shader_holdout_apply.  A holdout object keeps its
+ * transparent closure and retypes the rest to NBUILTIN_CLOSURES (sampled and
+ * evaluated by nobody); the flag mask is the reference's arithmetic
+ * SD_CLOSURE_FLAGS - (SD_TRANSPARENT | SD_BSDF), which clears SD_TRANSPARENT
+ * and keeps SD_BSDF_NEEDS_LCG. */
+CY_FN cfloat3 shader_holdout_apply(CySD *sd)
+{
+  cfloat3 weight = mk3(0.0f, 0.0f, 0.0f);
+  if (sd->object_flag & SD_OBJECT_HOLDOUT_MASK) {
+    if ((sd->flag & SD_TRANSPARENT) && !(sd->flag & SD_HAS_ONLY_VOLUME)) {
+      weight = sub3(mk3(1.0f, 1.0f, 1.0f), sd->closure_transparent_extinction);
+      for (int i = 0; i < sd->num_closure; i++) {
+        CyClosure *sc = &sd->closure[i];
+        if (sc->type != CLOSURE_BSDF_TRANSPARENT_ID) {
+          sc->type = NBUILTIN_CLOSURES;
+        }
+      }
+      sd->flag &= ~(SD_CLOSURE_FLAGS - (SD_TRANSPARENT | SD_BSDF));
+    }
+    else {
+      weight = mk3(1.0f, 1.0f, 1.0f);
+    }
+  }
+  else {
+    for (int i = 0; i < sd->num_closure; i++) {
+      const CyClosure *sc = &sd->closure[i];
+      if (sc->type == CLOSURE_HOLDOUT_ID) {
+        weight = add3(weight, sc->weight);
+      }
+    }
+  }
+  return weight;
+}
+
 CY_FN CyClosure *bsdf_alloc(CySD *sd, cfloat3 weight)
 {
   CyClosure *sc = closure_alloc(sd, CLOSURE_NONE_ID, weight);
@@ -2645,6 +2679,48 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         svm_node_bevel(kg, sd, state, stack, node, err);
         break;
 #endif
+      /* svm_closure.h:1113-1129: a holdout closure of the mix weight */
+      case NODE_CLOSURE_HOLDOUT: {
+        const uint mix_weight_offset = node.y;
+        cfloat3 weight = sd->svm_closure_weight;
+        if (mix_weight_offset != SVM_STACK_INVALID) {
+          const float mix_weight = svm_load(stack, mix_weight_offset, err);
+          if (mix_weight == 0.0f) {
+            break;
+          }
+          weight = mul3f(weight, mix_weight);
+        }
+        closure_alloc(sd, CLOSURE_HOLDOUT_ID, weight);
+        sd->flag |= SD_HOLDOUT;
+        break;
+      }
+      /* svm_mapping.h:47-59: a texture node's TextureMapping matrix */
+      case NODE_TEXTURE_MAPPING: {
+        const cfloat3 v = svm_load3(stack, node.y, err);
+        struct cy_tfm tfm;
+        struct cy_f4 *rows[3] = {&tfm.x, &tfm.y, &tfm.z};
+        for (int r = 0; r < 3; r++) {
+          const hc_uint4 row = kg->__svm_nodes[offset];
+          offset++;
+          rows[r]->x = as_float(row.x);
+          rows[r]->y = as_float(row.y);
+          rows[r]->z = as_float(row.z);
+          rows[r]->w = as_float(row.w);
+        }
+        svm_store3(stack, node.z, transform_point(&tfm, v), err);
+        break;
+      }
+      /* svm_mapping.h:61-71: min(max(mn, v), mx) per component */
+      case NODE_MIN_MAX: {
+        const cfloat3 v = svm_load3(stack, node.y, err);
+        const hc_uint4 a = kg->__svm_nodes[offset], b = kg->__svm_nodes[offset + 1];
+        offset += 2;
+        const cfloat3 r = mk3(cy_min(cy_max(as_float(a.x), v.x), as_float(b.x)),
+                              cy_min(cy_max(as_float(a.y), v.y), as_float(b.y)),
+                              cy_min(cy_max(as_float(a.z), v.z), as_float(b.z)));
+        svm_store3(stack, node.z, r, err);
+        break;
+      }
       /* svm_closure.h:1188-1194: the bump program's normal becomes the
        * shading normal (displacement method "bump") */
       case NODE_CLOSURE_SET_NORMAL: {
@@ -2735,9 +2811,10 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         }
 #endif
         if (node.x == NODE_ATTR || node.x == NODE_VERTEX_COLOR || node.x == NODE_NORMAL_MAP ||
-            node.x == NODE_TANGENT || node.x == NODE_OBJECT_INFO || (node.x == NODE_GEOMETRY && node.y == 2u)
+            node.x == NODE_TANGENT || node.x == NODE_OBJECT_INFO || node.x == NODE_PARTICLE_INFO ||
+            (node.x == NODE_GEOMETRY && node.y == 2u)
 #if CY_CLOSURE_EXT
-            || node.x == NODE_SET_BUMP
+            || node.x == NODE_SET_BUMP || node.x == NODE_HAIR_INFO
 #endif
         ) {
           CyAttrIn ain;
@@ -2762,7 +2839,8 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
 #endif
           svm_eval_attribute_node(kg->__objects, kg->__shaders, kg->__attributes_map, kg->__attributes_float,
                                   kg->__attributes_float2, kg->__attributes_float3, kg->__attributes_uchar4,
-                                  kg->__tri_vindex, ain, stack, node, err);
+                                  kg->__tri_vindex, kg->__curves, kg->__curve_keys, kg->__particles, ain, stack,
+                                  node, err);
           break;
         }
         CySvmTexIn in;

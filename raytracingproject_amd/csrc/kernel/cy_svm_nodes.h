@@ -31,7 +31,10 @@ enum {
   NODE_GAMMA = 45,
   NODE_BRIGHTCONTRAST = 46,
   NODE_LIGHT_PATH = 47,
+  NODE_CLOSURE_HOLDOUT = 37,
+  NODE_TEXTURE_MAPPING = 51,
   NODE_MAPPING = 52,
+  NODE_MIN_MAX = 53,
   NODE_TEX_GRADIENT = 57,
   NODE_TEX_CHECKER = 62,
   NODE_LIGHT_FALLOFF = 66,

@@ -110,6 +110,8 @@ enum {
   SD_HAS_DISPLACEMENT = (1 << 26),
   SD_HAS_CONSTANT_EMISSION = (1 << 27),
   SD_NEED_VOLUME_ATTRIBUTES = (1 << 28),
+  SD_CLOSURE_FLAGS = (SD_EMISSION | SD_BSDF | SD_BSDF_HAS_EVAL | SD_BSSRDF | SD_HOLDOUT | SD_EXTINCTION |
+                      SD_SCATTER | SD_BSDF_NEEDS_LCG), /* kernel_types.h:869-870 (no SD_TRANSPARENT) */
   SD_SHADER_FLAGS = (SD_USE_MIS | SD_HAS_TRANSPARENT_SHADOW | SD_HAS_VOLUME | SD_HAS_ONLY_VOLUME |
                      SD_HETEROGENEOUS_VOLUME | SD_HAS_BSSRDF_BUMP | SD_VOLUME_EQUIANGULAR | SD_VOLUME_MIS |
                      SD_VOLUME_CUBIC | SD_HAS_BUMP | SD_HAS_DISPLACEMENT | SD_HAS_CONSTANT_EMISSION |

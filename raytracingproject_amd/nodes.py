@@ -83,6 +83,15 @@ TANGENT_DIRECTIONS = {"radial": 0, "uv_map": 1}
 TANGENT_AXES = {"x": 0, "y": 1, "z": 2}
 OBJECT_INFO_OUTPUTS = {"Location": ("vector", 0), "Color": ("color", 1), "Object Index": ("float", 2),
                        "Material Index": ("float", 3), "Random": ("float", 4)}
+# Particle Info / Hair Info (svm_types.h:185-205, nodes.cpp:4247-4426)
+NODE_PARTICLE_INFO, NODE_HAIR_INFO, NODE_TEXTURE_MAPPING, NODE_MIN_MAX = 49, 50, 51, 53
+PARTICLE_INFO_OUTPUTS = {"Index": ("float", 0), "Random": ("float", 1), "Age": ("float", 2),
+                         "Lifetime": ("float", 3), "Location": ("vector", 4), "Size": ("float", 6),
+                         "Velocity": ("vector", 7), "Angular Velocity": ("vector", 8)}
+HAIR_INFO_OUTPUTS = {"Is Strand": "float", "Intercept": "float", "Thickness": "float",
+                     "Tangent Normal": "vector", "Random": "float"}
+NODE_INFO_CURVE_IS_STRAND, NODE_INFO_CURVE_THICKNESS, NODE_INFO_CURVE_TANGENT_NORMAL = 0, 2, 3
+ATTR_STD_CURVE_INTERCEPT, ATTR_STD_CURVE_RANDOM = 14, 15
 # NodeAttributeType (svm_types.h:160-166)
 NODE_ATTR_FLOAT, NODE_ATTR_FLOAT2, NODE_ATTR_FLOAT3, NODE_ATTR_RGBA = 0, 1, 2, 3
 # AttributeStandard (kernel_types.h:750-779) of the attributes this host packs;
@@ -280,6 +289,32 @@ def object_info() -> Node:
     """Object Info node (nodes.cpp:4211-4237, svm_geometry.h:104-139): Location,
     Color, Object Index, Material Index, Random."""
     return Node("object_info")
+
+
+def particle_info() -> Node:
+    """Particle Info node (nodes.cpp:4247-4347, svm_geometry.h:141-202): the
+    instancing object's particle (KernelObject.particle_index into __particles):
+    Index, Random, Age, Lifetime, Location, Size, Velocity, Angular Velocity."""
+    return Node("particle_info")
+
+
+def hair_info() -> Node:
+    """Hair Info node (nodes.cpp:4354-4426, svm_geometry.h:204-243): Is Strand,
+    Thickness and Tangent Normal from the hit curve segment; Intercept and
+    Random read the curves' ATTR_STD_CURVE_INTERCEPT / _RANDOM attributes."""
+    return Node("hair_info")
+
+
+def texture_mapping(vector, tfm, min_=None, max_=None, normalize: bool = False) -> Socket:
+    """A texture node's TextureMapping (nodes.cpp:155-176 compile, the mapping
+    Blender's legacy texture settings carry): the vector through the 3x4
+    matrix `tfm` (TextureMapping::compute_transform's result, any affine map
+    here), then clamped to [min_, max_] per component (use_minmax), then
+    normalized (type NORMAL)."""
+    t = np.asarray(tfm, dtype=np.float32).reshape(3, 4)
+    mm = None if min_ is None else (tuple(float(v) for v in min_), tuple(float(v) for v in max_))
+    return Node("texture_mapping", inputs={"Vector": vector},
+                params={"tfm": t, "minmax": mm, "normalize": bool(normalize)})["Vector"]
 
 
 def _default_vector(vector, kind: str = "generated"):
@@ -765,6 +800,12 @@ def _outputs(node: Node) -> dict:
         return {"Tangent": "vector"}
     if k == "object_info":
         return {n: t for n, (t, _) in OBJECT_INFO_OUTPUTS.items()}
+    if k == "particle_info":
+        return {n: t for n, (t, _) in PARTICLE_INFO_OUTPUTS.items()}
+    if k == "hair_info":
+        return dict(HAIR_INFO_OUTPUTS)
+    if k == "texture_mapping":
+        return {"Vector": "vector"}
     if k == "geometry":
         return {n: "vector" for n in GEOMETRY_OUTPUTS}
     if k == "light_path":
@@ -813,6 +854,7 @@ def _outputs(node: Node) -> dict:
 
 
 _INPUT_TYPES = {
+    "texture_mapping": {"Vector": "vector"},
     "light_falloff": {"Strength": "float", "Smooth": "float"},
     "math": {"Value1": "float", "Value2": "float", "Value3": "float"},
     "vector_math": {"Vector1": "vector", "Vector2": "vector", "Vector3": "vector", "Scale": "float"},
@@ -1157,6 +1199,38 @@ class NodeCompiler:
         for name, (_, t) in OBJECT_INFO_OUTPUTS.items():
             if (id(n), name) in self.used:
                 self.emit((NODE_OBJECT_INFO, t, self.out(n, name), 0))
+
+    def _n_particle_info(self, n):  # nodes.cpp:4295-4347 ParticleInfoNode::compile
+        for name, (_, t) in PARTICLE_INFO_OUTPUTS.items():
+            if (id(n), name) in self.used:
+                self.emit((NODE_PARTICLE_INFO, t, self.out(n, name), 0))
+
+    def _n_hair_info(self, n):  # nodes.cpp:4391-4426 HairInfoNode::compile
+        for name in HAIR_INFO_OUTPUTS:
+            if (id(n), name) not in self.used:
+                continue
+            if name == "Intercept":
+                self.emit((NODE_ATTR, self.attribute(ATTR_STD_CURVE_INTERCEPT), self.out(n, name), NODE_ATTR_FLOAT))
+            elif name == "Random":
+                self.emit((NODE_ATTR, self.attribute(ATTR_STD_CURVE_RANDOM), self.out(n, name), NODE_ATTR_FLOAT))
+            else:
+                t = {"Is Strand": NODE_INFO_CURVE_IS_STRAND, "Thickness": NODE_INFO_CURVE_THICKNESS,
+                     "Tangent Normal": NODE_INFO_CURVE_TANGENT_NORMAL}[name]
+                self.emit((NODE_HAIR_INFO, t, self.out(n, name), 0))
+
+    def _n_texture_mapping(self, n):  # nodes.cpp:155-176 TextureMapping::compile
+        v = self.inp(n, "Vector")
+        out = self.out(n, "Vector")
+        self.emit((NODE_TEXTURE_MAPPING, v, out, 0))
+        for row in n.params["tfm"]:
+            self.emit(tuple(f32bits(float(x)) for x in row))
+        if n.params["minmax"] is not None:
+            self.emit((NODE_MIN_MAX, out, out, 0))
+            for vec in n.params["minmax"]:
+                self.emit((*(f32bits(x) for x in vec), f32bits(0.0)))
+        if n.params["normalize"]:
+            self.emit((NODE_VECTOR_MATH, VECTOR_MATH_OPS.index("normalize"), uchar4(out, out, out),
+                       uchar4(SVM_STACK_INVALID, out)))
 
     def _n_vertex_color(self, n):  # nodes.cpp:4543-4568 VertexColorNode::compile
         layer = n.params["layer"]

@@ -53,6 +53,7 @@ PRNG_BOUNCE_NUM = 8
 NODE_END, NODE_SHADER_JUMP, NODE_CLOSURE_BSDF, NODE_CLOSURE_EMISSION = 0, 1, 2, 3
 NODE_SET_DISPLACEMENT = 20
 NODE_CLOSURE_BACKGROUND, NODE_CLOSURE_SET_WEIGHT = 4, 5
+NODE_CLOSURE_HOLDOUT = 37  # svm_types.h ShaderNodeType
 NODE_CLOSURE_WEIGHT, NODE_EMISSION_WEIGHT = 6, 7
 NODE_MIX_CLOSURE, NODE_JUMP_IF_ZERO, NODE_VALUE_F = 8, 9, 14
 SVM_STACK_INVALID = 255
@@ -77,7 +78,7 @@ CLOSURE_BSDF_TRANSPARENT_ID = 34
 CLOSURE_BSDF_HAIR_REFLECTION_ID = 21
 CLOSURE_BSDF_HAIR_PRINCIPLED_ID = 30
 CLOSURE_BSDF_HAIR_TRANSMISSION_ID = 31
-ATTR_STD_CURVE_RANDOM = 15  # kernel_types.h AttributeStandard
+ATTR_STD_CURVE_INTERCEPT, ATTR_STD_CURVE_RANDOM = 14, 15  # kernel_types.h AttributeStandard
 # PrincipledHairBsdfNode (nodes.cpp:3474-3512): parametrization enum
 # (svm_types.h:509-513) and socket defaults
 PRINCIPLED_HAIR_PARAMETRIZATIONS = {"color": 0, "melanin": 1, "absorption": 2}
@@ -131,6 +132,7 @@ SD_HETEROGENEOUS_VOLUME = 1 << 20
 SD_NEED_VOLUME_ATTRIBUTES = 1 << 28
 SD_OBJECT_HAS_VOLUME = 1 << 4
 SD_OBJECT_INTERSECTS_VOLUME = 1 << 5
+SD_OBJECT_HOLDOUT_MASK = 1 << 0  # kernel_types.h ShaderDataObjectFlag; object.cpp:547-548 use_holdout
 CLOSURE_VOLUME_ABSORPTION_ID = 43
 CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID = 44
 NODE_CLOSURE_VOLUME, NODE_PRINCIPLED_VOLUME = 40, 41
@@ -240,7 +242,7 @@ class Closure:
     def closure_types(self) -> set:
         if self.kind == "mix":
             return self.a.closure_types() | self.b.closure_types()
-        if self.kind in ("emission", "background", "none") or self.kind in VOLUME_KINDS:
+        if self.kind in ("emission", "background", "none", "holdout") or self.kind in VOLUME_KINDS:
             return set()
         if self.kind == "principled":
             return {CLOSURE_BSDF_PRINCIPLED_ID}
@@ -451,6 +453,13 @@ def emission(color, strength):
     return Closure("emission", _const_or_socket(color), strength=strength)
 
 
+def holdout():
+    """Holdout closure (nodes.cpp:3177-3201 HoldoutNode): with a transparent
+    film the surface cuts the pixel's alpha by its mix weight; the path ends
+    where the holdout weight is 1 (kernel_path.h:285-296)."""
+    return Closure("holdout", (1.0, 1.0, 1.0))
+
+
 def background(color, strength=1.0):
     return Closure("background", _const_or_socket(color), strength=strength)
 
@@ -548,6 +557,11 @@ class SVMCompiler:
             else:
                 emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(v) for v in const)))
             emit((NODE_CLOSURE_EMISSION if c.kind == "emission" else NODE_CLOSURE_BACKGROUND, mix_weight, 0, 0))
+            return out
+        if c.kind == "holdout":
+            # nodes.cpp:3195-3201 HoldoutNode::compile
+            emit((NODE_CLOSURE_SET_WEIGHT, *(f32bits(1.0) for _ in range(3))))
+            emit((NODE_CLOSURE_HOLDOUT, mix_weight, 0, 0))
             return out
         if c.kind == "principled":
             return self.emit_principled(c, mix_weight)
@@ -844,6 +858,13 @@ class Mesh:
     object_color: tuple | None = None
     pass_index: int = 0
     object_random: float | None = None  # Object::random_id / 0xFFFFFFFF
+    # Object::use_holdout (SD_OBJECT_HOLDOUT_MASK, object.cpp:547-548)
+    holdout: bool = False
+    # the particle this object instances (Object::particle_system /
+    # particle_index, object.cpp:440-452; ParticleInfo node): a dict of
+    # KernelParticle fields index, age, lifetime, size, rotation (4),
+    # location, velocity, angular_velocity (3 each); None: particle 0
+    particle: dict | None = None
 
 
 @dataclass
@@ -858,6 +879,13 @@ class Hair:
     curve_first: np.ndarray
     curve_nkeys: np.ndarray
     shader: np.ndarray | int = 0  # per curve, or one material index
+    # curve attributes (Hair's AttributeSet, blender_curves.cpp ExportCurveSegments):
+    # key -> (element, data) with element "curve" (one value per curve) or
+    # "curve_key" (one per key), data (N,) float, (N, 2) float2 or (N, 3) float3;
+    # key an AttributeStandard id (ATTR_STD_CURVE_INTERCEPT, ATTR_STD_CURVE_RANDOM)
+    # or a name.  Absent attributes read 0, as on a host that exports none.
+    attributes: dict | None = None
+    holdout: bool = False
 
 
 @dataclass
@@ -873,6 +901,8 @@ class Instance:
     object_color: tuple | None = None  # None: the mesh's
     pass_index: int | None = None
     object_random: float | None = None
+    holdout: bool | None = None  # None: the mesh's
+    particle: dict | None = None  # None: the mesh's
 
 
 @dataclass
@@ -979,6 +1009,10 @@ class Scene:
     world_volume: "Closure | None" = None
     # Film exposure (film.cpp:363; applied by film convert)
     exposure: float = 1.0
+    # Film "Transparent" (Background::transparent, background.cpp:112): camera
+    # rays that leave the scene, and holdouts, make the pixel transparent
+    # (alpha = 1 - L_transparent) instead of showing the world
+    film_transparent: bool = False
 
 
 def _has_displacement(m) -> bool:
@@ -1362,7 +1396,17 @@ def compile_scene(scene: Scene) -> DeviceScene:
         kobjects[i].numkeys = ob.get("numkeys", 0)
         if ob["applied"]:
             object_flag[i] = SD_OBJECT_TRANSFORM_APPLIED
+        if ob.get("holdout"):
+            object_flag[i] |= SD_OBJECT_HOLDOUT_MASK
         object_node[i] = np.uint32(ob["node"] & 0xFFFFFFFF)
+    # particles (object.cpp:440-452, particles.cpp:57-103 device_update_particles):
+    # entry 0 is the dummy every object without a particle reads; the
+    # instancing objects' particles follow in object order
+    kparticles = [None]
+    for i, ob in enumerate(objects):
+        if ob.get("particle") is not None:
+            kobjects[i].particle_index = len(kparticles)
+            kparticles.append(ob["particle"])
 
     # --- volume objects (object.cpp:678-736 device_update_flags,
     # object.cpp:270-349 compute_volume_step_size, :378-389 volume density)
@@ -1538,7 +1582,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
         # scene; it is read only through a world volume, so scenes without
         # volumes keep 0 and their golden digests)
         kb.volume_step_size = float(np.float32(0.1) * np.float32(1.0))
-    kb.transparent = 0
+    kb.transparent = 1 if scene.film_transparent else 0
     kb.transparent_roughness_squared_threshold = -1.0
     kb.ao_factor = 0.0
     kb.ao_bounces_factor = 0.0
@@ -1664,6 +1708,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
         arrays["__attributes_map"] = np.zeros((2, 4), dtype=np.uint32)
     if attr_arrays is not None:
         arrays.update(attr_arrays)
+    if len(kparticles) > 1:
+        arrays["__particles"] = _pack_particles(kparticles)
     if g["ncurves"]:
         # Hair::pack_curves (render/hair.cpp): keys with radius, per curve the
         # first key, key count and shader id (get_shader_id(shader, false))
@@ -1712,7 +1758,8 @@ def _volume_attribute_dependency(v) -> bool:
 
 
 _ATTR_TYPES = {"float": 0, "float2": 1, "float3": 2, "rgba": 3}  # NodeAttributeType
-_ATTR_ELEMENTS = {"object": 1, "mesh": 2, "face": 3, "vertex": 4, "corner": 6, "corner_byte": 7}
+_ATTR_ELEMENTS = {"object": 1, "mesh": 2, "face": 3, "vertex": 4, "corner": 6, "corner_byte": 7, "curve": 8,
+                  "curve_key": 9}
 
 
 def _generated_coordinates(m: Mesh) -> np.ndarray:
@@ -1851,10 +1898,49 @@ def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobje
                 rows.append((aid, _ATTR_ELEMENTS[element], offset & 0xFFFFFFFF, _ATTR_TYPES[kind]))
             rows.append((0, 0, 0, 0))  # no subdivision surface
         rows.extend([(0, 0, 0, 0)] * 2)
+    # curves objects (Hair attributes): per-curve values indexed by the global
+    # curve number (prim), per-key values by the global key number
+    hair_offset = {}
+    for i, ob in enumerate(objects):
+        hr = ob.get("hair")
+        if hr is None or not hr.attributes:
+            continue
+        used = sorted(set(int(k) for k in np.unique(np.asarray(hr.shader).reshape(-1))))
+        reqs = []
+        for k in used:
+            for key in svm_compiler.requests[k]:
+                if key not in reqs:
+                    reqs.append(key)
+        hair_offset[i] = len(rows)
+        for key in reqs:
+            aid = svm_compiler.attribute_ids[key] if isinstance(key, str) else int(key)
+            if key not in hr.attributes:
+                rows.append((aid, 0, 0, 0))
+            else:
+                element, a = hr.attributes[key]
+                if element not in ("curve", "curve_key"):
+                    raise ValueError(f"hair attribute {key!r}: element must be curve or curve_key")
+                a = np.asarray(a, dtype=np.float32)
+                kind = "float" if a.ndim == 1 else {2: "float2", 3: "float3"}[a.shape[1]]
+                if kind == "float3":
+                    a4 = np.zeros((a.shape[0], 4), dtype=np.float32)
+                    a4[:, :3] = a
+                    a = a4
+                store = kind
+                offset = size[store]
+                data[store].append(a)
+                size[store] += a.shape[0]
+                offset -= ob["curve_offset"] if element == "curve" else ob["key_offset"]
+                rows.append((aid, _ATTR_ELEMENTS[element], offset & 0xFFFFFFFF, _ATTR_TYPES[kind]))
+            rows.append((0, 0, 0, 0))
+        rows.extend([(0, 0, 0, 0)] * 2)
     empty = len(rows)
     rows.extend([(0, 0, 0, 0)] * 2)
     for i, ob in enumerate(objects):
-        kobjects[i].attribute_map_offset = geom_offset[ob["geom"]] if ob.get("geom") is not None else empty
+        if i in hair_offset:
+            kobjects[i].attribute_map_offset = hair_offset[i]
+        else:
+            kobjects[i].attribute_map_offset = geom_offset[ob["geom"]] if ob.get("geom") is not None else empty
 
     def cat(store, shape, dtype):
         if not data[store]:
@@ -1929,7 +2015,9 @@ def _instance_props(inst) -> dict:
 
     return dict(color=pick(inst.object_color, inst.mesh.object_color),
                 pass_index=pick(inst.pass_index, inst.mesh.pass_index),
-                random=pick(inst.object_random, inst.mesh.object_random))
+                random=pick(inst.object_random, inst.mesh.object_random),
+                holdout=pick(inst.holdout, inst.mesh.holdout),
+                particle=pick(inst.particle, inst.mesh.particle))
 
 
 def _pack_geometry(scene: Scene) -> dict:
@@ -1947,7 +2035,8 @@ def _pack_geometry(scene: Scene) -> dict:
         v, t, sh, nrm = _mesh_arrays(m)
         geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(m.smooth), applied=True, mesh=m))
         objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True, color=m.object_color,
-                            pass_index=m.pass_index, random=m.object_random))
+                            pass_index=m.pass_index, random=m.object_random, holdout=m.holdout,
+                            particle=m.particle))
     for inst in scene.instances:
         tfm = np.asarray(inst.tfm, dtype=np.float64).reshape(3, 4)
         if users[id(inst.mesh)] == 1:
@@ -1963,7 +2052,7 @@ def _pack_geometry(scene: Scene) -> dict:
         objects.append(dict(geom=geom_of[id(inst.mesh)], tfm=tfm, applied=False, **_instance_props(inst)))
     # hair objects: transforms applied, after the meshes (object order)
     for hr in scene.hairs:
-        objects.append(dict(geom=None, hair=hr, tfm=ident, applied=True))
+        objects.append(dict(geom=None, hair=hr, tfm=ident, applied=True, holdout=hr.holdout))
 
     # global triangle / vertex arrays, geometry order (prim_offset, vert_offset)
     toff = voff = 0
@@ -2122,6 +2211,7 @@ def _pack_hair(objects: list, shape: str) -> dict:
         seg_index.append(np.concatenate([np.arange(n) for n in nseg]) if len(nseg) else np.zeros(0, np.int64))
         seg_obj.append(np.full(int(nseg.sum()), oi))
         ob["numkeys"] = len(k)
+        ob["key_offset"], ob["curve_offset"] = koff, coff
         koff += len(k)
         coff += len(first)
     if not coff:
@@ -2372,5 +2462,24 @@ ELEMENT_BYTES = {
     "__curves": 16, "__curve_keys": 16,
     "__object_volume_step": 4, "__attributes_map": 16,
     "__attributes_float": 4, "__attributes_float2": 8, "__attributes_float3": 16, "__attributes_uchar4": 4,
-    "__tri_patch": 4, "__ies": 4,
+    "__tri_patch": 4, "__ies": 4, "__particles": 80,
 }
+
+
+def _pack_particles(parts: list) -> np.ndarray:
+    """KernelParticle records (kernel_types.h:1551-1562, 80 bytes: index, age,
+    lifetime, size, float4 rotation, location, velocity, angular_velocity) of
+    ParticleSystemManager::device_update_particles (render/particles.cpp:57-103);
+    entry 0 the all-zero dummy."""
+    rec = np.zeros((len(parts), 20), dtype=np.float32)
+    for i, p in enumerate(parts):
+        if p is None:
+            continue
+        rec[i, 0] = np.array([int(p.get("index", 0))], dtype=np.int32).view(np.float32)[0]
+        rec[i, 1] = p.get("age", 0.0)
+        rec[i, 2] = p.get("lifetime", 0.0)
+        rec[i, 3] = p.get("size", 0.0)
+        rec[i, 4:8] = p.get("rotation", (0.0, 0.0, 0.0, 0.0))
+        for k, name in enumerate(("location", "velocity", "angular_velocity")):
+            rec[i, 8 + 4 * k:11 + 4 * k] = p.get(name, (0.0, 0.0, 0.0))
+    return rec.view(np.uint8).reshape(-1).copy()

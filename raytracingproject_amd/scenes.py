@@ -914,6 +914,120 @@ def bump_displace(width=40, height=40, samples=8) -> sc.Scene:
     return s
 
 
+def shading_holdout(width=48, height=48, samples=8) -> sc.Scene:
+    """Holdouts with a transparent film (kernel_path.h:285-296 with
+    shader_holdout_apply, kernel_shader.h:1020-1050): a Holdout closure mixed
+    at 0.5 into a diffuse sphere (the path goes on at half the alpha), a pure
+    Holdout quad (weight 1: the path ends), an object holdout (use_holdout)
+    and an object holdout whose material is part transparent (only the
+    transparent closures stay, weight 1 - transparency), a glass sphere in
+    front of a holdout (refracted camera rays have lost
+    PATH_RAY_TRANSPARENT_BACKGROUND: no holdout there), all over a floor that
+    catches their shadows; the world seen directly is transparent too."""
+    white = sc.diffuse((0.7, 0.7, 0.7))
+    half = sc.mix(0.5, sc.diffuse((0.8, 0.3, 0.2)), sc.holdout())
+    pure = sc.holdout()
+    blue = sc.diffuse((0.2, 0.3, 0.8))
+    seethrough = sc.mix(0.4, sc.diffuse((0.3, 0.8, 0.3)), sc.transparent((0.9, 0.9, 0.9)))
+    glass = sc.Closure("glass", (1.0, 1.0, 1.0), roughness=0.0, ior=1.45)
+    light = sc.emission((1.0, 0.95, 0.9), 8.0)
+    materials = [white, half, pure, blue, seethrough, glass, light]
+    meshes = [
+        sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0),
+        sc.Mesh(*_ellipsoid((-0.9, -0.45, 0.3), (0.5, 0.5, 0.5), 20, 12), shader=1, smooth=True),
+        sc.Mesh(*_quad((0.2, -1.0, 0.9), (1.2, -1.0, 0.9), (1.2, 0.2, 0.9), (0.2, 0.2, 0.9)), shader=2),
+        sc.Mesh(*_box((0.9, -0.6, -0.2), (0.6, 0.8, 0.6), 0.4), shader=3, holdout=True),
+        sc.Mesh(*_box((-0.2, -0.7, -0.9), (0.5, 0.6, 0.5), -0.3), shader=4, holdout=True),
+        sc.Mesh(*_ellipsoid((0.3, -0.6, -1.6), (0.35, 0.35, 0.35), 20, 12), shader=5, smooth=True),
+        sc.Mesh(*_quad((-1.5, 2.5, -1.0), (-0.5, 2.5, -1.0), (-0.5, 2.5, 0.0), (-1.5, 2.5, 0.0)), shader=6),
+    ]
+    lamps = [sc.Lamp("point", co=(1.5, 2.0, -1.5), size=0.2, color=(1.0, 0.9, 0.8), strength=60.0)]
+    cam = sc.Camera(eye=(0.0, 0.8, -3.6), target=(0.0, -0.3, 0.0), fov=math.radians(45.0), nearclip=0.01,
+                    farclip=100.0)
+    s = sc.Scene(width, height, cam, meshes, materials, world_color=(0.3, 0.35, 0.45), world_strength=1.0,
+                 samples=samples, lamps=lamps, name="shading_holdout")
+    s.film_transparent = True
+    s.transparent_max_bounce = 8
+    return s
+
+
+def shading_info(width=48, height=48, samples=8) -> sc.Scene:
+    """Particle Info and texture mapping: boxes instanced with a particle each
+    (index, age, lifetime, size, location, velocity, angular velocity driving
+    colours; Random hashes the index) beside quads whose colours run through a
+    TextureMapping matrix (svm_node_texture_mapping) with and without the
+    min/max clamp (svm_node_min_max) and the normalize of type NORMAL."""
+    from . import nodes as nd
+
+    pi = nd.particle_info()
+    col_a = nd.combine_xyz(nd.math("multiply", pi["Index"], 0.15), nd.math("divide", pi["Age"], pi["Lifetime"]),
+                           nd.math("multiply", pi["Size"], 2.0))
+    col_b = nd.mix_rgb("mix", pi["Random"], nd.vector_math("absolute", pi["Velocity"])["Vector"],
+                       nd.mapping(pi["Location"], scale=(0.3, 0.3, 0.3), location=(0.5, 0.5, 0.5)))
+    col_c = nd.vector_math("fraction", pi["Angular Velocity"])["Vector"]
+    P = nd.tex_coord()["Object"]
+    rot = [[0.8, -0.3, 0.1, 0.2], [0.25, 0.9, -0.2, -0.1], [0.0, 0.35, 1.1, 0.3]]
+    tm = nd.texture_mapping(P, rot)
+    tm_clamped = nd.texture_mapping(P, rot, (-0.2, 0.1, -0.3), (0.6, 0.7, 0.4))
+    tm_normal = nd.texture_mapping(nd.geometry()["Normal"], [[1.0, 0.2, 0.0, 0.0], [-0.3, 1.0, 0.1, 0.0],
+                                                             [0.0, 0.4, 0.7, 0.0]], normalize=True)
+    materials = [sc.diffuse((0.6, 0.6, 0.6)), sc.diffuse(col_a), sc.mix(0.3, sc.diffuse(col_b), sc.glossy(col_b, 0.3)),
+                 sc.diffuse(col_c),
+                 sc.diffuse(nd.checker(tm, (0.9, 0.3, 0.1), (0.1, 0.3, 0.9), 2.0)["Color"]),
+                 sc.diffuse(nd.mapping(tm_clamped, location=(0.4, 0.4, 0.4))),
+                 sc.diffuse(nd.mapping(tm_normal, scale=(0.5, 0.5, 0.5), location=(0.5, 0.5, 0.5))),
+                 sc.emission((1.0, 0.95, 0.9), 6.0)]
+    box = sc.Mesh(*_box((0.0, 0.0, 0.0), (1.0, 1.0, 1.0)), shader=1)
+    box2 = sc.Mesh(*_box((0.0, 0.0, 0.0), (1.0, 1.0, 1.0)), shader=2)
+    box3 = sc.Mesh(*_box((0.0, 0.0, 0.0), (1.0, 1.0, 1.0)), shader=3)
+    rng = np.random.default_rng(0x5EED + 77)
+    instances = []
+    for k in range(9):
+        part = {"index": 3 + 5 * k, "age": float(rng.uniform(0, 40)), "lifetime": float(rng.uniform(40, 90)),
+                "size": float(rng.uniform(0.05, 0.4)), "rotation": tuple(float(x) for x in rng.normal(size=4)),
+                "location": tuple(float(x) for x in rng.uniform(-2, 2, 3)),
+                "velocity": tuple(float(x) for x in rng.normal(0, 0.8, 3)),
+                "angular_velocity": tuple(float(x) for x in rng.normal(0, 2.0, 3))}
+        x, z = -1.6 + 0.8 * (k % 3), -0.6 + 0.8 * (k // 3)
+        mesh = (box, box2, box3)[k % 3]
+        instances.append(sc.Instance(mesh, _tfm((x, -0.75, z), 0.3 * k, (0.45, 0.45, 0.45)), particle=part))
+    meshes = [sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0)]
+    for i in range(3):
+        x0 = 0.5 + 0.75 * i
+        meshes.append(sc.Mesh(*_quad((x0, -1.0, -0.5), (x0 + 0.65, -1.0, -0.5), (x0 + 0.65, 0.4, -0.5),
+                                     (x0, 0.4, -0.5)), shader=4 + i))
+    meshes.append(sc.Mesh(*_quad((-1.5, 2.5, -1.0), (-0.5, 2.5, -1.0), (-0.5, 2.5, 0.0), (-1.5, 2.5, 0.0)), shader=7))
+    lamps = [sc.Lamp("point", co=(1.5, 2.0, -1.5), size=0.2, color=(1.0, 0.9, 0.8), strength=60.0)]
+    cam = sc.Camera(eye=(0.0, 1.2, -4.0), target=(0.0, -0.4, 0.2), fov=math.radians(45.0), nearclip=0.01,
+                    farclip=100.0)
+    return sc.Scene(width, height, cam, meshes, materials, world_color=(0.2, 0.22, 0.25), world_strength=1.0,
+                    samples=samples, lamps=lamps, instances=instances, name="shading_info")
+
+
+def hair_info(width=48, height=48, samples=8, shape="ribbon") -> sc.Scene:
+    """Hair Info on curves (svm_node_hair_info, curve_thickness,
+    curve_tangent_normal; Intercept / Random through the curves'
+    ATTR_STD_CURVE_INTERCEPT key and ATTR_STD_CURVE_RANDOM curve attributes,
+    curve_attribute_float): the fur of hair_ball coloured by them, Is Strand
+    on the mesh core (0) and on the strands (1)."""
+    from . import nodes as nd
+
+    s = hair_ball(width, height, samples, shape=shape, name=f"hair_info_{shape}")
+    hi = nd.hair_info()
+    fur_a = sc.diffuse(nd.combine_xyz(hi["Intercept"], hi["Random"], nd.math("multiply", hi["Thickness"], 20.0)))
+    fur_b = sc.mix(0.3, sc.diffuse(nd.mapping(hi["Tangent Normal"], scale=(0.5, 0.5, 0.5), location=(0.5, 0.5, 0.5))),
+                   sc.glossy(nd.combine_xyz(hi["Is Strand"], 0.4, hi["Intercept"]), 0.3))
+    core = sc.diffuse(nd.combine_xyz(hi["Is Strand"], 0.3, nd.math("add", hi["Thickness"], 0.5)))
+    s.materials[1], s.materials[2], s.materials[3] = core, fur_a, fur_b
+    hr = s.hairs[0]
+    nk = np.asarray(hr.curve_nkeys)
+    intercept = np.concatenate([np.linspace(0.0, 1.0, int(n)) for n in nk]).astype(np.float32)
+    rng = np.random.default_rng(0x5EED + 78)
+    hr.attributes = {sc.ATTR_STD_CURVE_INTERCEPT: ("curve_key", intercept),
+                     sc.ATTR_STD_CURVE_RANDOM: ("curve", rng.uniform(0.0, 1.0, len(nk)).astype(np.float32))}
+    return s
+
+
 def shading_raytrace(width=40, height=40, samples=8) -> sc.Scene:
     """Shader ray tracing (golden parity case, svm_ao.h / svm_bevel.h): Bevel
     normals on a glossy box (host-applied transform) and an instanced rotated

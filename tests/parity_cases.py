@@ -97,6 +97,13 @@ CASES = {
     "shading_bump_displace": lambda: scenes.bump_displace(40, 40, 8),
     # shader ray tracing: Ambient Occlusion and Bevel nodes (svm_ao.h, svm_bevel.h)
     "shading_raytrace": lambda: scenes.shading_raytrace(40, 40, 8),
+    # holdouts with a transparent film: Holdout closure, object holdout (also
+    # over a part-transparent material), glass in front of a holdout
+    "shading_holdout": lambda: scenes.shading_holdout(48, 48, 8),
+    # Particle Info on instanced objects, TextureMapping with min/max and normalize
+    "shading_info": lambda: scenes.shading_info(48, 48, 8),
+    # Hair Info: strand flag, thickness, tangent normal, intercept / random curve attributes
+    "hair_info_ribbon": lambda: scenes.hair_info(48, 48, 8, shape="ribbon"),
     "sss_disk": lambda: scenes.sss_disk_cornell(48, 48, 8),
     "sss_disk_instanced": lambda: scenes.sss_disk_cornell(48, 48, 8, instanced=True),
     "sss_disk_transparent": lambda: scenes.sss_disk_cornell(40, 40, 8, transparent=True),
@@ -145,7 +152,8 @@ JOE_KUO_CASES = {"cornell_joe_kuo"}
 HOST_LOOP_CASES = {"cornell_adaptive"}
 # Scenes with curves: the device traverses the bound BVH2 (unaligned nodes,
 # curve leaves) at every requested width; the wide layout holds triangles only.
-CURVE_CASES = {"hair_ribbon", "hair_thick", "hair_principled", "hair_principled_thick", "hair_reflection_transmission"}
+CURVE_CASES = {"hair_ribbon", "hair_thick", "hair_principled", "hair_principled_thick", "hair_reflection_transmission",
+               "hair_info_ribbon"}
 EMU_CASES = [n for n in CASES if n not in HOST_LOOP_CASES]
 
 # SHADER_EVAL_DISPLACE (tests/golden/displace.npz)

@@ -84,4 +84,12 @@ if [[ $MODE == micro ]]; then
   step build_micro 120 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -o gpurun_out/bin/node_fetch_bench tools/node_fetch_bench.hip
   step micro 300 gpurun_out/bin/node_fetch_bench
 fi
+if [[ $MODE == modes ]]; then
+  # rocprofv3 kernel traces of the render modes (tools/render_modes.py, tools/trace_gaps.py)
+  for m in ${MODES:-frame stream shard8}; do
+    step "trace_$m" 300 rocprofv3 --kernel-trace -d $OUT/trace_modes_$m -o run --output-format csv -- python3 tools/render_modes.py $m "$@"
+    python3 tools/trace_gaps.py $(ls $OUT/trace_modes_$m/*/run_kernel_trace.csv $OUT/trace_modes_$m/run_kernel_trace.csv 2>/dev/null | head -1) > $OUT/gaps_$m.txt 2>&1 || true
+    head -14 $OUT/gaps_$m.txt
+  done
+fi
 echo done
