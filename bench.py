@@ -84,6 +84,8 @@ def parse(argv=None):
     p.add_argument("--other-configs", default="bmw27_production,barbershop_standin,classroom_standin,junkshop_standin@1664x832+512x256",
                    help="BASELINE.json's other configs, one frame each after the headline measurement (rank 0, "
                         "N=1): name or name@XxY+WxH for a full-spp crop; empty disables")
+    p.add_argument("--other-profile", action="store_true",
+                   help="per-stage (closest / shade / shadow) times of each --other-configs frame")
     p.add_argument("--shard", default="auto", choices=("auto", "rows", "tiles"),
                    help="multi-GPU split: interleaved rows, or whole tiles per rank (auto: tiles for "
                         "adaptive-sampling scenes, whose filters run per RenderTile)")
@@ -642,6 +644,16 @@ def other_config(spec, device_index, args):
         res.update({"frame": f"{W}x{H} {S} spp", "region": [x, y, w, h],
                     "value": round(w * h * S / dt / 1e6, 3), "unit": "Msamples/s", "ms": round(1e3 * dt, 1),
                     "film_checksum": float(buf[..., :4].double().sum().item())})
+        if args.other_profile:
+            # one more frame with per-stage HIP events (lanes serialised, so
+            # the stage times add up to more than the timed frame)
+            dev.set_profiling(1)
+            buf.zero_()
+            dev.render_tile(_Buf, (x, y, w, h), 0, S, -(x + y * w), w)
+            torch.cuda.synchronize()
+            st = dev.stats()
+            res["stages_ms"] = {k: round(float(st[k]), 1) for k in ("closest_ms", "shade_ms", "shadow_ms", "total_ms")}
+            dev.set_profiling(0)
         del buf
     except Exception as e:  # reported beside the headline, never fatal
         res["error"] = f"{type(e).__name__}: {e}"[:300]
