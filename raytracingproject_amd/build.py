@@ -74,12 +74,14 @@ SHADE_VARIANTS = (1, 2, 4, 8)  # closure-array sizes of the shade kernel (csrc/d
 LARGE_SHADE_VARIANTS = (16, 64)  # texture / volume builds only (extended closure set)
 
 
-def build_device(force=False, variant=None, defines=(), traversal_only=False):
+def build_device(force=False, variant=None, defines=(), traversal_only=False, only=None):
     """The HIP device library: hipcycles.hip plus k_shade.hip compiled once per
     closure-array size.  A named variant (tuning builds with extra -D defines)
     goes to libhipcycles-<variant>.so next to the default one; with
     traversal_only the variant recompiles hipcycles.hip alone and links the
-    default build's shading objects."""
+    default build's shading objects; `only` (object names such as "mc2_tex" or
+    "hipcycles") recompiles just those and links the rest from the default
+    build (debugging builds, tools/dbg_trace.py)."""
     dev_dir = os.path.join(HERE, "csrc", "device")
     src = os.path.join(dev_dir, "hipcycles.hip")
     out = os.path.join(HERE, f"libhipcycles-{variant}.so" if variant else "libhipcycles.so")
@@ -94,16 +96,20 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False):
     from concurrent.futures import ThreadPoolExecutor
 
     cflags = [f for f in HIP_FLAGS if f != "-shared"]
-    jobs = [([HIPCC, *cflags, *dflags, inc, "-c", "-o", os.path.join(objdir, "hipcycles.o"), src],
-             os.path.join(objdir, "hipcycles.o"))]
-    shade_objs = []
+    default_dir = os.path.join(REPO, "build", "device", "default")
+    jobs, shade_objs = [], []
+    if only is not None and "hipcycles" not in only:
+        shade_objs.append(os.path.join(default_dir, "hipcycles.o"))
+    else:
+        jobs.append(([HIPCC, *cflags, *dflags, inc, "-c", "-o", os.path.join(objdir, "hipcycles.o"), src],
+                     os.path.join(objdir, "hipcycles.o")))
     for mc in SHADE_VARIANTS + LARGE_SHADE_VARIANTS:
         # plain (closure nodes only), _tex (texture nodes, extended closures),
         # _vol (_tex with volumes)
         for kind in ("", "_tex", "_vol") if mc in SHADE_VARIANTS else ("_tex", "_vol"):
             name = f"mc{mc}{kind}"
-            if traversal_only:
-                shade_objs.append(os.path.join(REPO, "build", "device", "default", f"k_shade_{name}.o"))
+            if traversal_only or (only is not None and name not in only):
+                shade_objs.append(os.path.join(default_dir, f"k_shade_{name}.o"))
                 continue
             obj = os.path.join(objdir, f"k_shade_{name}.o")
             jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
@@ -154,7 +160,8 @@ def build_all(ref=True, force=False):
 if __name__ == "__main__":
     if "--variant" in sys.argv:
         name = sys.argv[sys.argv.index("--variant") + 1]
+        only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
         build_device(variant=name, defines=[a[2:] for a in sys.argv if a.startswith("-D")],
-                     traversal_only="--traversal-only" in sys.argv)
+                     traversal_only="--traversal-only" in sys.argv, only=only)
     else:
         build_all(ref="--no-ref" not in sys.argv, force="--force" in sys.argv)

@@ -61,8 +61,9 @@ template<int W, bool INST> __device__ __forceinline__ CY_LDS CyStackEntry *lds_r
   }
 }
 
-/* HAIR (scenes with curves, W = 2 only): unaligned nodes and curve leaves of
- * the shapes HAIR selects (1 ribbons, 2 thick curves, 3 both). */
+/* HAIR (scenes with curves): unaligned nodes and curve leaves of the shapes
+ * HAIR selects (1 ribbons, 2 thick curves, 3 both).  Ribbon-only scenes also
+ * traverse the wide BVH (W = 4 / 8, cy_bvhw.h); thick curves keep the BVH2. */
 template<int W, bool any_hit, bool INST = true, int HAIR = 0>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
@@ -76,14 +77,14 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
   }
   else if constexpr (INST) {
     /* instanced scene: reference-order top level, wide BVH inside instances */
-    return bvh2_intersect<any_hit, true, W, CY_LDS_STACK_TOP>(kg, ray, visibility, isect, err, n_nodes, n_leaves,
-                                                               n_tris, (CY_LDS int *)(lds->top + t),
-                                                               (CY_LDS CyStackEntry *)(lds->ring + t), tie);
+    return bvh2_intersect<any_hit, true, W, CY_LDS_STACK_TOP, CY_BLOCK, HAIR>(
+        kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, (CY_LDS int *)(lds->top + t),
+        (CY_LDS CyStackEntry *)(lds->ring + t), tie);
   }
   else {
-    return bvhw_intersect<W, any_hit>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
-                                      (CY_LDS CyStackEntry *)(lds->ring + t), tie,
-                                      (CY_LDS const hc_float4 *)lds->top_nodes, kg->bvhw_top);
+    return bvhw_intersect<W, any_hit, HAIR>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
+                                            (CY_LDS CyStackEntry *)(lds->ring + t), tie,
+                                            (CY_LDS const hc_float4 *)lds->top_nodes, kg->bvhw_top);
   }
 }
 
@@ -397,7 +398,20 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_close
       hit = scene_traverse<W, false, INST, HAIR>(&kg, &ray, visibility, &isect, err,
                                                  STATS ? &n_nodes : nullptr, &n_leaves, &n_tris, &lds_stack, &tie);
     }
-    if constexpr (W > 2) {
+    if constexpr (W > 2 && HAIR != 0) {
+      if (tie) {
+        /* hair scenes: the near-tie (or twice-crossed ribbon) ray is re-traced
+         * here with the BVH2 in the reference's order (the shading kernels
+         * carry no curve intersection) */
+        hit = bvh2_intersect<false, INST, 2, 0, CY_BLOCK, HAIR>(&kg, &ray, visibility, &isect, err, nullptr, nullptr,
+                                                                 nullptr);
+        tie = false;
+        if (STATS) {
+          n_ties++;
+        }
+      }
+    }
+    if constexpr (W > 2 && HAIR == 0) {
       if (tie) {
         /* near-tie (cy_bvhw.h bvhw_traverse): flagged in the stored primitive;
          * the shading stage re-traces the ray with the bound BVH2 in the
@@ -1242,7 +1256,8 @@ __global__ void __launch_bounds__(CY_BLOCK) k_test_intersect(CyGlobals kg, const
       hit = scene_traverse<W, false, true, HAIR>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr,
                                                  &lds_stack, &tie);
       if (tie) {
-        hit = bvh2_intersect<false>(&kg, &ray, visibility, &isect, err, nullptr, nullptr, nullptr);
+        hit = bvh2_intersect<false, true, 2, CY_LDS_STACK, CY_BLOCK, HAIR>(&kg, &ray, visibility, &isect, err,
+                                                                           nullptr, nullptr, nullptr);
       }
     }
   }
@@ -1450,8 +1465,11 @@ struct ShadowK {
 };
 template<class K, bool S, bool I> static auto pick_width(int W, int hair)
 {
-  /* scenes with curves traverse the BVH2 (W = 2) with the hair node tests */
-  return hair == 1 ? K::template fn<S, 2, I, 1>() :
+  /* scenes with curves: the hair node tests; ribbons only on the wide BVH
+   * too, thick curves on the BVH2 (their intersection's starting points
+   * depend on the bound, cy_bvhw.h) */
+  return hair == 1 ? (W == 8 ? K::template fn<S, 8, I, 1>() : W == 4 ? K::template fn<S, 4, I, 1>() :
+                                                                     K::template fn<S, 2, I, 1>()) :
          hair == 2 ? K::template fn<S, 2, I, 2>() :
          hair == 3 ? K::template fn<S, 2, I, 3>() :
          W == 8 ? K::template fn<S, 8, I>() :
@@ -1611,6 +1629,13 @@ static int set_error(hipcy_device *dev, const std::string &msg)
 
 static int ensure_bvhw(hipcy_device *dev);
 
+/* The W-wide layout serves the scene: triangles, and ribbon curves (thick
+ * curves keep the bound BVH2: pick_width) */
+static bool wide_layout(const hipcy_device *dev)
+{
+  return dev->bvh_width > 2 && (!dev->data_host.bvh.have_curves || dev->curve_shapes == 1);
+}
+
 static bool build_globals(hipcy_device *dev, CyGlobals *kg)
 {
   memset(kg, 0, sizeof(*kg));
@@ -1622,9 +1647,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
   }
   CY_GLOBAL_ARRAYS(CY_BIND)
 #undef CY_BIND
-  /* scenes with curves keep the bound BVH2 (its unaligned nodes and curve
-   * leaves; the wide layout holds triangles only) */
-  const bool wide = dev->bvh_width > 2 && !dev->data_host.bvh.have_curves;
+  const bool wide = wide_layout(dev);
   kg->bvhw_nodes = wide ? dev->bvhw : nullptr;
   kg->bvhw_object_root = wide ? dev->bvhw_object_root : nullptr;
   kg->tri_index_identity = wide ? dev->tri_index_identity : 0;
@@ -1635,6 +1658,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
    * traverse their top level as the reference's BVH2) */
   const size_t wide_nodes = dev->bvh_width > 2 ? dev->bvhw_bytes / (32 * (size_t)dev->bvh_width) : 0;
   kg->bvhw_top = (wide && !dev->have_instancing) ? (int)std::min<size_t>(CY_LDS_TOP, wide_nodes) : 0;
+  kg->bvhw_width = wide ? dev->bvh_width : 0;
   return true;
 }
 
@@ -1642,7 +1666,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
  * the arrays are a few tens of MB even for BMW27-class scenes). */
 static int ensure_bvhw(hipcy_device *dev)
 {
-  if (dev->bvh_width == 2 || !dev->bvhw_dirty || dev->data_host.bvh.have_curves) {
+  if (!wide_layout(dev) || !dev->bvhw_dirty) {
     return 0;
   }
   auto nodes = dev->globals.find("__bvh_nodes");
@@ -1662,6 +1686,7 @@ static int ensure_bvhw(hipcy_device *dev)
   cybvhw::Collapser col;
   col.width = dev->bvh_width;
   col.merge_prims = dev->bvh_merge_prims;
+  col.allow_curves = dev->data_host.bvh.have_curves != 0;
   col.nodes2 = n2.data();
   col.n_nodes2 = n2.size() / 4;
   col.leaves2 = l2.data();
@@ -4127,7 +4152,7 @@ int hipcy_intersect(hipcy_device *dev, uint64_t rays, uint64_t out_f, uint64_t o
   build_globals(dev, &kg);
   HIP_CHECK(dev, hipMemsetAsync(dev->counters, 0, 64, dev->stream));
   const int W = kg.bvhw_nodes ? dev->bvh_width : 2;
-  auto ktest = kg.have_curves ? k_test_intersect<2, 3> :
+  auto ktest = kg.have_curves ? (W == 8 ? k_test_intersect<8, 1> : W == 4 ? k_test_intersect<4, 1> : k_test_intersect<2, 3>) :
                W == 8 ? k_test_intersect<8> : W == 4 ? k_test_intersect<4> : k_test_intersect<2>;
   hipLaunchKernelGGL(ktest,
                      dim3((n + CY_BLOCK - 1) / CY_BLOCK), dim3(CY_BLOCK), 0, dev->stream, kg,

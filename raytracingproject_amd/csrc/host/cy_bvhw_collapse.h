@@ -30,6 +30,18 @@
  * Instanced geometry (two-level BVH, bvh/bvh.cpp:323-520): each object BVH
  * root __object_node[object] is collapsed once into its own wide subtree;
  * object_root[object] is its wide root.
+ *
+ * Curves (allow_curves): the hair BVH2 stores the children of an *unaligned*
+ * node as oriented boxes (bvh2.cpp:133-163 pack_unaligned_node: visibility |
+ * PATH_RAY_NODE_UNALIGNED, the two children, per child the transform taking
+ * its box to the unit cube; 7 float4).  Such a node is not widened: it is
+ * copied as an oriented two-child node (OBB node, code CY_BVHW_OBB | index)
+ * in the same node array, its child addresses replaced by wide codes, so the
+ * traversal applies the reference's oriented slab test to the reference's own
+ * transforms.  Wide nodes open only aligned BVH2 nodes; an unaligned child
+ * stays a wide child (its parent's exact axis-aligned box) and becomes an OBB
+ * node below it.  Curve leaves keep their primitive ranges (merging is off: a
+ * merged leaf could mix types); the traversal reads the primitive type.
  */
 #ifndef CY_BVHW_COLLAPSE_H
 #define CY_BVHW_COLLAPSE_H
@@ -42,6 +54,11 @@
 #include <vector>
 
 namespace cybvhw {
+
+/* child code of an OBB node: its node index with this bit set (codes of wide
+ * inner nodes stay below it, leaf codes are negative) */
+static constexpr uint32_t OBB_CODE = 1u << 30;
+static constexpr uint32_t NODE_UNALIGNED = 1u << 13; /* PATH_RAY_NODE_UNALIGNED */
 
 struct Ref {
   int addr; /* BVH2 address: >= 0 inner node (float4 units), < 0 leaf ~index */
@@ -71,6 +88,18 @@ struct Collapser {
   std::string error;
   int max_depth = 0;
   std::vector<int> sub_start, sub_count; /* per BVH2 inner node (index addr/4): contiguous range or -1 */
+  bool allow_curves = false; /* hair BVH2: unaligned nodes become OBB nodes, curve leaves, no merging */
+  size_t n_obb = 0;          /* OBB nodes emitted */
+
+  bool unaligned(int addr) const
+  {
+    if (!allow_curves || addr < 0 || (size_t)addr >= n_nodes2) {
+      return false;
+    }
+    uint32_t w0;
+    memcpy(&w0, nodes2 + 4 * (size_t)addr, 4);
+    return (w0 & NODE_UNALIGNED) != 0;
+  }
 
   size_t words() const
   {
@@ -122,8 +151,9 @@ struct Collapser {
       *count = 0;
       return true;
     }
-    if ((w[3] & 1u) == 0u) { /* PRIMITIVE_TRIANGLE = 1 */
-      error = "only triangle leaves are supported";
+    /* PRIMITIVE_TRIANGLE = 1; curves: PRIMITIVE_ALL_CURVE = bits 2..5 */
+    if ((w[3] & 1u) == 0u && !(allow_curves && (w[3] & 0x3Cu))) {
+      error = allow_curves ? "leaf of an unsupported primitive type" : "only triangle leaves are supported";
       return false;
     }
     if (e - s < 1 || e - s > 15) {
@@ -179,7 +209,7 @@ struct Collapser {
     if (r.addr < 0) {
       return leaf_range(r.addr, start, count);
     }
-    if (merge_prims <= 0) {
+    if (merge_prims <= 0 || allow_curves) {
       return false;
     }
     int s, n;
@@ -203,8 +233,8 @@ struct Collapser {
       float ba = -1.0f;
       for (int i = 0; i < *n; i++) {
         int s, c;
-        if (ch[i].addr < 0 || (ch[i].vis & 0x0FFFFFFFu) == 0u) {
-          continue;
+        if (ch[i].addr < 0 || (ch[i].vis & 0x0FFFFFFFu) == 0u || unaligned(ch[i].addr)) {
+          continue; /* leaves, invisible children and oriented-box nodes stay */
         }
         if (mergeable(ch[i], &s, &c)) {
           continue;
@@ -267,7 +297,7 @@ struct Collapser {
       else {
         const size_t child = out.size() / words();
         out.resize(out.size() + words(), 0u);
-        w[6 * W + s] = (uint32_t)child;
+        w[6 * W + s] = (uint32_t)child | (unaligned(ch[i].addr) ? OBB_CODE : 0u);
         w[7 * W + s] = vis;
         pending->push_back(std::make_pair(child, ch[i]));
       }
@@ -275,6 +305,68 @@ struct Collapser {
     }
     memcpy(&out[idx * words()], w.data(), words() * 4);
     return true;
+  }
+
+  /* The unaligned BVH2 node at r.addr copied as an OBB node at idx: word 0..3
+   * the stored visibility of both children and their wide codes, words 4..27
+   * the two children's transforms as stored (bvh_unaligned_node_intersect). */
+  bool emit_obb(size_t idx, const Ref &r, std::vector<std::pair<size_t, Ref>> *pending)
+  {
+    if ((size_t)r.addr + 7 > n_nodes2) {
+      error = "unaligned node past __bvh_nodes";
+      return false;
+    }
+    if (idx >= OBB_CODE) {
+      error = "wide node index beyond the OBB code range";
+      return false;
+    }
+    const float *n = nodes2 + 4 * (size_t)r.addr;
+    uint32_t w0[4];
+    memcpy(w0, n, 16);
+    std::vector<uint32_t> w(words(), 0u);
+    w[0] = w0[0];
+    w[1] = w0[1];
+    for (int k = 0; k < 2; k++) {
+      const int a = (int)w0[2 + k];
+      if (a < 0) {
+        int start, count;
+        if (!leaf_range(a, &start, &count)) {
+          return false;
+        }
+        if (start >= (1 << 27)) {
+          error = "primitive index beyond the 2^27 leaf-code range";
+          return false;
+        }
+        w[2 + k] = ~(((uint32_t)start << 4) | (uint32_t)count);
+      }
+      else {
+        const size_t child = out.size() / words();
+        out.resize(out.size() + words(), 0u);
+        w[2 + k] = (uint32_t)child | (unaligned(a) ? OBB_CODE : 0u);
+        Ref c;
+        c.addr = a;
+        c.vis = w0[k];
+        for (int x = 0; x < 3; x++) {
+          c.lo[x] = -FLT_MAX;
+          c.hi[x] = FLT_MAX;
+        }
+        pending->push_back(std::make_pair(child, c));
+      }
+    }
+    memcpy(&w[4], n + 4, 24 * 4);
+    memcpy(&out[idx * words()], w.data(), words() * 4);
+    n_obb++;
+    return true;
+  }
+
+  /* one pending node: an OBB node for an unaligned BVH2 node, else a wide one */
+  bool process(size_t idx, const Ref &r, std::vector<Ref> &ch, std::vector<std::pair<size_t, Ref>> *next)
+  {
+    if (unaligned(r.addr)) {
+      return emit_obb(idx, r, next);
+    }
+    int n = 0;
+    return open(r, ch.data(), &n) && emit(idx, ch.data(), n, next);
   }
 
   std::vector<int> instances; /* objects referenced by instance leaves (may repeat) */
@@ -303,14 +395,25 @@ struct Collapser {
     Ref r;
     r.addr = root;
     r.vis = 0xFFFFFFFFu;
-    if (!open(r, ch.data(), &n) || !emit(base, ch.data(), n, &pending)) {
+    if (unaligned(root)) {
+      /* an oriented-box root: a wide root with that node as its only child */
+      for (int a = 0; a < 3; a++) {
+        r.lo[a] = -FLT_MAX;
+        r.hi[a] = FLT_MAX;
+      }
+      r.vis = 0x0FFFFFFFu;
+      if (!emit(base, &r, 1, &pending)) {
+        return -1;
+      }
+    }
+    else if (!open(r, ch.data(), &n) || !emit(base, ch.data(), n, &pending)) {
       return -1;
     }
     int depth = 1;
     while (!pending.empty()) {
       next.clear();
       for (auto &p : pending) {
-        if (!open(p.second, ch.data(), &n) || !emit(p.first, ch.data(), n, &next)) {
+        if (!process(p.first, p.second, ch, &next)) {
           return -1;
         }
       }
@@ -331,6 +434,7 @@ struct Collapser {
       return false;
     }
     out.clear();
+    n_obb = 0;
     sub_start.assign(n_nodes2 / 4 + 1, -1);
     sub_count.assign(n_nodes2 / 4 + 1, -2);
     instances.clear();

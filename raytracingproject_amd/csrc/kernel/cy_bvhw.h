@@ -33,6 +33,8 @@
 #ifndef CY_LDS_STACKW
 #  define CY_LDS_STACKW 8
 #endif
+/* child code bit of an oriented-box node (hair scenes; cy_bvhw_collapse.h) */
+#define CY_BVHW_OBB (1u << 30)
 #define CY_BVHW_STACK 96
 /* request the next triangle's vertices before testing the current one */
 #ifndef CY_TRI_PREFETCH
@@ -242,7 +244,7 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
  * matter: that ray is re-traced with the reference-order BVH2 traversal
  * (cy_integrator.h shade_path; about 1 ray in 3000 on the bench scene).  Hits
  * beyond the window lose in either order. */
-template<int W, bool any_hit>
+template<int W, bool any_hit, int HAIR>
 CY_FN bool bvhw_traverse(const CyGlobals *kg,
                          int root,
                          cfloat3 P,
@@ -307,6 +309,54 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
   }
 
   while (true) {
+    if constexpr (HAIR != 0) {
+      if (code >= 0 && (code & (int)CY_BVHW_OBB)) {
+        /* oriented-box node (cy_bvhw_collapse.h emit_obb): the reference's
+         * unaligned two-child test on its own transforms */
+        n_nodes++;
+        const int idx = code & ~(int)CY_BVHW_OBB;
+        hc_float4 nd[7];
+#if defined(__HIP_DEVICE_COMPILE__) && CY_LDS_TOP > 0 && !CY_LDS_TOP_SOA
+        if (idx < n_top) {
+          CY_LDS const hc_float4 *lp = top_nodes + (size_t)idx * (8 * Q);
+#  pragma unroll
+          for (int k = 0; k < 7; k++) {
+            nd[k] = lp[k];
+          }
+        }
+        else
+#endif
+        {
+          const hc_float4 *np = nodes + (size_t)idx * (8 * Q);
+#pragma unroll
+          for (int k = 0; k < 7; k++) {
+            nd[k] = np[k];
+          }
+        }
+        const hc_uint4 h = as_uint4(nd[0]);
+        const float t = CY_T_BOX;
+        float d0, d1;
+        const bool hit0 = bvh_obb_intersect(nd[1], nd[2], nd[3], P, dir, t, &d0) && (h.x & visibility);
+        const bool hit1 = bvh_obb_intersect(nd[4], nd[5], nd[6], P, dir, t, &d1) && (h.y & visibility);
+        if (hit0 && hit1) {
+          /* nearer child next, the other pushed (bvh_traversal.h:104-125) */
+          const bool first1 = d1 < d0;
+          if (!CY_STACK_PUSH(first1 ? (int)h.z : (int)h.w, first1 ? d0 : d1)) {
+            cy_set_error(err, CY_ERR_BVH_STACK, W);
+            return found_hit;
+          }
+          code = first1 ? (int)h.w : (int)h.z;
+          code_t = first1 ? d1 : d0;
+          continue;
+        }
+        if (hit0 || hit1) {
+          code = hit0 ? (int)h.z : (int)h.w;
+          code_t = hit0 ? d0 : d1;
+          continue;
+        }
+        goto pop;
+      }
+    }
     if (cur && budget > 0) {
       /* out of iterations: stop before processing `code` (never with entries
        * in the private overflow arrays, which do not outlive this call) */
@@ -473,6 +523,74 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         return found_hit;
       }
       const int prim_end = prim_addr + (packed & 15);
+      if constexpr (HAIR != 0) {
+        /* hair scenes: a leaf holds one primitive type (the BVH2's leaves,
+         * unmerged); ribbon segments here (HAIR = 1: thick curves keep the
+         * BVH2, see hipcycles.hip pick_width) */
+        if (kg->__prim_type[prim_addr] & PRIMITIVE_ALL_CURVE) {
+          for (; prim_addr < prim_end; prim_addr++) {
+            n_tris++;
+            const uint ctype = kg->__prim_type[prim_addr];
+            if (!(ctype & (CY_PRIMITIVE_CURVE_RIBBON | CY_PRIMITIVE_MOTION_CURVE_RIBBON))) {
+              cy_set_error(err, CY_ERR_PRIMITIVE, ctype);
+              return found_hit;
+            }
+            if (!(kg->__prim_visibility[prim_addr] & visibility)) {
+              continue;
+            }
+            cy_c4 curve[4];
+            curve_segment_keys(kg, (int)kg->__prim_index[prim_addr], (int)CY_PRIMITIVE_UNPACK_SEGMENT(ctype), curve);
+            float tt, uu, vv, tmin;
+            if (any_hit) {
+              /* the reference's ribbon test at the ray's own bound */
+              if (ribbon_intersect_steps<false>(P, dir, KD->bvh.curve_subdivisions, curve, isect->t, &tt, &uu, &vv,
+                                                &tmin)) {
+                isect->prim = prim_addr;
+                isect->object = object;
+                isect->type = (int)ctype;
+                isect->u = uu;
+                isect->v = vv;
+                isect->t = tt;
+                found_hit = true;
+                goto ray_done;
+              }
+              continue;
+            }
+            /* every step of the ribbon: with one step hit the result is that
+             * hit whatever bound it is tested against, like a triangle's; a
+             * ribbon crossed twice returns its first step's hit below the
+             * bound, which depends on the bound the reference's visiting
+             * order gives it -- such a ray is re-traced in that order unless
+             * all of its crossings lie beyond the tie window (sticky) */
+            const int steps = ribbon_intersect_steps<true>(P, dir, KD->bvh.curve_subdivisions, curve, CY_FLT_MAX, &tt,
+                                                           &uu, &vv, &tmin);
+            if (steps == 0 || !(tmin <= CY_T_CULL)) {
+              continue;
+            }
+            if (steps > 1) {
+              bad |= CY_EXACT_TIES != 0;
+              if (!(tt <= isect->t)) {
+                continue;
+              }
+            }
+            else {
+              tie = CY_EXACT_TIES && !(tt < isect->t * (1.0f - CY_TIE_EPS)) && isect->prim != PRIM_NONE;
+              bad |= CY_EXACT_TIES && tt <= isect->t && tt * (1.0f + CY_TIE_EPS) < code_t;
+              if (!(tt <= isect->t)) {
+                continue; /* inside the window only: the reference's bound rejects it */
+              }
+            }
+            isect->prim = prim_addr;
+            isect->object = object;
+            isect->type = (int)ctype;
+            isect->u = uu;
+            isect->v = vv;
+            isect->t = tt;
+            found_hit = true;
+          }
+          goto pop;
+        }
+      }
       const bool ident = kg->tri_index_identity != 0;
       uint vi = ident ? 3u * (uint)prim_addr : kg->__prim_tri_index[prim_addr];
       hc_float4 v0 = kg->__prim_tri_verts[vi], v1 = kg->__prim_tri_verts[vi + 1], v2 = kg->__prim_tri_verts[vi + 2];
@@ -805,7 +923,7 @@ out:
 
 /* Closest hit (any_hit == false) or opaque-shadow any hit over a scene without
  * instances with the wide BVH: scene_intersect (bvh/bvh.h:154-237). */
-template<int W, bool any_hit>
+template<int W, bool any_hit, int HAIR = 0>
 CY_FN bool bvhw_intersect(const CyGlobals *kg,
                           const CyRay *ray,
                           uint visibility,
@@ -830,8 +948,8 @@ CY_FN bool bvhw_intersect(const CyGlobals *kg,
   bvhw_traverse_ww<W, any_hit>(kg, ray->P, dir, rcp3(dir), visibility, isect, err, cnt_nodes, cnt_leaves, cnt_tris,
                                lds_ring, tie);
 #else
-  bvhw_traverse<W, any_hit>(kg, 0, ray->P, dir, rcp3(dir), OBJECT_NONE, visibility, isect, err, cnt_nodes,
-                            cnt_leaves, cnt_tris, lds_ring, tie, 0, nullptr, top_nodes, n_top);
+  bvhw_traverse<W, any_hit, HAIR>(kg, 0, ray->P, dir, rcp3(dir), OBJECT_NONE, visibility, isect, err, cnt_nodes,
+                                  cnt_leaves, cnt_tris, lds_ring, tie, 0, nullptr, top_nodes, n_top);
 #endif
   return isect->prim != PRIM_NONE;
 }

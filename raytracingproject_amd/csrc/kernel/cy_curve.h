@@ -496,7 +496,18 @@ CY_FN cy_c4 ribbon_to_ray_space(const cfloat3 ray_space[3], cfloat3 ray_org, cy_
   return c4(dot3(ray_space[0], P), dot3(ray_space[1], P), dot3(ray_space[2], P), P4.w);
 }
 
-CY_FN bool ribbon_intersect(cfloat3 ray_org, cfloat3 ray_dir, int N, cy_c4 curve[4], CyIsect *isect)
+/* ribbon_intersect (geom_curve_intersect.h:568-642) returns the hit of the
+ * first subdivision step (in curve parameter order) whose quad the ray hits
+ * within tfar -- not the nearest one -- so a ribbon crossed twice gives a
+ * result that depends on the tfar it is tested with.  SCAN = false is the
+ * reference's form (stops at that first hit).  SCAN = true (the wide BVH,
+ * cy_bvhw.h) tests every step: returns the number of steps hit (capped at 2),
+ * the first one's hit and the nearest distance of all of them, so the traversal can tell a
+ * ribbon whose result is the same for every tfar (at most one step hit) from
+ * one that needs the reference's visiting order. */
+template<bool SCAN>
+CY_FN int ribbon_intersect_steps(cfloat3 ray_org, cfloat3 ray_dir, int N, cy_c4 curve[4], float tfar, float *t_o,
+                                 float *u_o, float *v_o, float *t_min)
 {
   /* Transform control points into ray space. */
   cfloat3 ray_space[3];
@@ -525,6 +536,7 @@ CY_FN bool ribbon_intersect(cfloat3 ray_org, cfloat3 ray_dir, int N, cy_c4 curve
   }
   cfloat3 wn0 = mul3f(normalize3(mk3(dp0dt.y, -dp0dt.x, 0.0f)), p0.w);
 
+  int count = 0;
   /* Evaluate the bezier curve. */
   for (int i = 0; i < N; i++) {
     const float u = i * step_size;
@@ -548,7 +560,7 @@ CY_FN bool ribbon_intersect(cfloat3 ray_org, cfloat3 ray_dir, int N, cy_c4 curve
 
     /* Intersect quad. */
     float vu, vv, vt;
-    bool valid0 = ribbon_intersect_quad(isect->t, lp0, lp1, up1, up0, &vu, &vv, &vt);
+    bool valid0 = ribbon_intersect_quad(tfar, lp0, lp1, up1, up0, &vu, &vv, &vt);
 
     if (valid0) {
       /* ignore self intersections */
@@ -557,16 +569,37 @@ CY_FN bool ribbon_intersect(cfloat3 ray_org, cfloat3 ray_dir, int N, cy_c4 curve
       valid0 = vt > avoidance_factor * r;
 
       if (valid0) {
-        vv = 2.0f * vv - 1.0f;
-        isect->t = vt;
-        isect->u = u + vu * step_size;
-        isect->v = vv;
-        return true;
+        if (count == 0) {
+          vv = 2.0f * vv - 1.0f;
+          *t_o = vt;
+          *u_o = u + vu * step_size;
+          *v_o = vv;
+          *t_min = vt;
+        }
+        else {
+          *t_min = cmin(*t_min, vt);
+        }
+        count = count < 2 ? count + 1 : 2;
+        if (!SCAN) {
+          return count;
+        }
       }
     }
 
     p0 = p1;
     wn0 = wn1;
+  }
+  return count;
+}
+
+CY_FN bool ribbon_intersect(cfloat3 ray_org, cfloat3 ray_dir, int N, cy_c4 curve[4], CyIsect *isect)
+{
+  float t, u, v, tmin;
+  if (ribbon_intersect_steps<false>(ray_org, ray_dir, N, curve, isect->t, &t, &u, &v, &tmin)) {
+    isect->t = t;
+    isect->u = u;
+    isect->v = v;
+    return true;
   }
   return false;
 }

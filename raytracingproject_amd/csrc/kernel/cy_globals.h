@@ -76,6 +76,8 @@ typedef struct CyGlobals {
   /* wide nodes 0 .. bvhw_top-1 (the top levels, breadth first) are read from
    * the traversal kernels' LDS copy (cy_bvhw.h CY_LDS_TOP); 0 = none */
   int bvhw_top;
+  /* W of the wide layout (4 or 8) when bvhw_nodes is set, else 0 */
+  int bvhw_width;
 } CyGlobals;
 
 #endif /* CY_GLOBALS_H */

@@ -811,9 +811,18 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
   const uint max_hits = (uint)(transparent_max_bounce - state->transparent_bounce - 1);
   CyIsect hits[CY_SHADOW_MAX_HITS];
   uint num_hits = 0;
-  const bool blocked = kg->have_curves ?
-                           bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
-                           bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+  bool blocked;
+  bool wide = kg->bvhw_nodes != nullptr && !kg->have_instancing;
+  if (wide) {
+    /* the wide layout's record-all (same hits, another recording order) */
+    blocked = kg->have_curves ? bvhw_shadow_all<1>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
+                                bvhw_shadow_all<0>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+  }
+  else {
+    blocked = kg->have_curves ?
+                  bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
+                  bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+  }
   if (blocked || num_hits == 0) {
 #if CY_CLOSURE_EXT
     if (VOL && !blocked && vstack->e[0].shader != SHADER_NONE) {
@@ -824,14 +833,31 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
     return blocked;
   }
   /* sort_intersections (bvh/bvh.h:606-626): stable, by distance */
-  for (uint i = 1; i < num_hits; i++) {
-    const CyIsect h = hits[i];
-    int j = (int)i - 1;
-    while (j >= 0 && hits[j].t > h.t) {
-      hits[j + 1] = hits[j];
-      j--;
+  for (int pass = 0; pass < 2; pass++) {
+    for (uint i = 1; i < num_hits; i++) {
+      const CyIsect h = hits[i];
+      int j = (int)i - 1;
+      while (j >= 0 && hits[j].t > h.t) {
+        hits[j + 1] = hits[j];
+        j--;
+      }
+      hits[j + 1] = h;
     }
-    hits[j + 1] = h;
+    bool shared = false;
+    for (uint i = 1; wide && i < num_hits; i++) {
+      shared |= hits[i].t == hits[i - 1].t;
+    }
+    if (!shared) {
+      break;
+    }
+    /* two hits at one distance: the first one recorded is shaded and the
+     * other skipped, so the reference's recording order decides -- the BVH2
+     * query gives it (the set of hits, and so blocked, stays the same) */
+    wide = false;
+    num_hits = 0;
+    blocked = kg->have_curves ?
+                  bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
+                  bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
   }
   cfloat3 throughput = mk3(1.0f, 1.0f, 1.0f);
   const cfloat3 Pend = add3(ray.P, mul3f(ray.D, ray.t));
@@ -1254,7 +1280,12 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
                         path_state_rng_1D(kg, state, PRNG_LIGHT_TERMINATE) :
                         0.0f;
   CyLightSample ls;
+  CY_DBG3(state, "light uv", mk3(light_u, light_v, terminate));
   if (light_sample(kg, light_u, light_v, sd->P, state->bounce, &ls, err) && ls.pdf != 0.0f) {
+    CY_DBG3(state, "ls.P", ls.P);
+    CY_DBG3(state, "ls.D", ls.D);
+    CY_DBG3(state, "ls.Ng", ls.Ng);
+    CY_DBG3(state, "ls.t pdf fac", mk3(ls.t, ls.pdf, ls.eval_fac));
     cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
     cfloat3 I = neg3(ls.D);
     if (shader_constant_emission_eval(kg, ls.shader, &light_eval)) {
@@ -1308,6 +1339,9 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
           eval = mul3f(eval, weight);
         }
       }
+      CY_DBG3(state, "light_eval", light_eval);
+      CY_DBG3(state, "bsdf eval(light)", eval);
+      CY_DBG1(state, "bsdf pdf(light)", bpdf);
       eval = mul3(eval, div3f(light_eval, ls.pdf));
       if (((uint)ls.shader & SHADER_EXCLUDE_ANY) &&
           ((uint)ls.shader & SHADER_EXCLUDE_DIFFUSE)) {
@@ -1662,6 +1696,21 @@ CY_FN bool shade_path(const CyGlobals *kg,
     const hc_float4 L4 = cy_ld(&b->L[slot]);
     L = mk3(L4.x, L4.y, L4.z);
   }
+#ifdef CY_DBG_X
+  {
+    int dx, dy, ds;
+    item_pixel(tile, cam_item != CY_NO_ITEM ? cam_item : cy_ld(&b->item[slot]), &dx, &dy, &ds);
+    state.dbg = dx == CY_DBG_X && dy == CY_DBG_Y && ds == CY_DBG_S;
+  }
+  CY_DBGF(&state, "bounce %d flag %08x\n", state.bounce, state.flag);
+  CY_DBG3(&state, "ray.P", ray.P);
+  CY_DBG3(&state, "ray.D", ray.D);
+  CY_DBG1(&state, "ray.t", ray.t);
+  CY_DBG3(&state, "isect", mk3(is4.x, is4.y, is4.z));
+  CY_DBGF(&state, "prim %d\n", as_int(is4.w));
+  CY_DBG3(&state, "throughput", throughput);
+  CY_DBG3(&state, "L", L);
+#endif
 
 #if CY_CLOSURE_EXT
   /* the path's volume stack, with the update its last surface left pending */
@@ -1876,6 +1925,19 @@ CY_FN bool shade_path(const CyGlobals *kg,
 #else
     shader_setup_from_ray(kg, &sd, &isect, &ray);
 #endif
+    CY_DBG3(&state, "sd.P", sd.P);
+    CY_DBG3(&state, "sd.N", sd.N);
+    CY_DBG3(&state, "sd.Ng", sd.Ng);
+    CY_DBG3(&state, "sd.I", sd.I);
+    CY_DBG3(&state, "sd.uv", mk3(sd.u, sd.v, sd.ray_length));
+#if CY_CLOSURE_EXT
+    CY_DBG3(&state, "sd.dP.dx", sd.dP.dx);
+    CY_DBG3(&state, "sd.dP.dy", sd.dP.dy);
+    CY_DBG3(&state, "sd.dI.dx", sd.dI.dx);
+    CY_DBG3(&state, "sd.dI.dy", sd.dI.dy);
+    CY_DBG3(&state, "sd.du", mk3(sd.du.dx, sd.du.dy, sd.dv.dx));
+    CY_DBG1(&state, "sd.dv.dy", sd.dv.dy);
+#endif
 #if CY_CLOSURE_EXT
     if (VOL && (sd.flag & SD_HAS_ONLY_VOLUME)) {
       /* volume bounding surface: pass through without a bounce
@@ -1917,6 +1979,17 @@ CY_FN bool shade_path(const CyGlobals *kg,
     shader_eval_surface(kg, &sd, &state, state.flag, err);
 #endif
     shader_prepare_closures(&sd, &state);
+#ifdef CY_DBG_X
+    CY_DBGF(&state, "closures %d flag %08x\n", sd.num_closure, sd.flag);
+    CY_DBG3(&state, "sd.N'", sd.N);
+    for (int i = 0; i < sd.num_closure; i++) {
+      CY_DBGF(&state, "closure %d type %d sw %08x\n", i, sd.closure[i].type,
+              __builtin_bit_cast(unsigned, sd.closure[i].sample_weight));
+      CY_DBG3(&state, "  weight", sd.closure[i].weight);
+      CY_DBG3(&state, "  N", sd.closure[i].N);
+      CY_DBG3(&state, "  a", mk3(sd.closure[i].alpha_x, sd.closure[i].alpha_y, sd.closure[i].ior));
+    }
+#endif
 
     /* kernel_path_shader_apply (kernel_path.h:254-321); shadow catchers are
      * refused by hipcy_load_kernels */
@@ -2098,6 +2171,10 @@ CY_FN bool shade_path(const CyGlobals *kg,
 #else
         int label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err);
 #endif
+        CY_DBGF(&state, "bsdf label %d\n", label);
+        CY_DBG3(&state, "bsdf eval", bsdf_eval_v);
+        CY_DBG3(&state, "omega_in", omega_in);
+        CY_DBG1(&state, "bsdf pdf", bsdf_pdf);
         if (!(bsdf_pdf == 0.0f || is_zero3(bsdf_eval_v))) {
           float inverse_pdf = 1.0f / bsdf_pdf;
           throughput = mul3(throughput, mul3f(bsdf_eval_v, inverse_pdf));

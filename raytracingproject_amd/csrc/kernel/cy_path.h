@@ -532,11 +532,8 @@ CY_FN float bvh_instance_pop(
  * (bvh_unaligned_node_intersect :79-135: each child's box is the unit cube in
  * the affine space stored for it, 7 float4 per node).  Returns the traverse
  * mask; dist = entry distances. */
-CY_FN bool bvh_unaligned_node_intersect_child(const hc_float4 *nodes, int node_addr, int child, cfloat3 P,
-                                              cfloat3 dir, float t, float *dist)
+CY_FN bool bvh_obb_intersect(hc_float4 sx, hc_float4 sy, hc_float4 sz, cfloat3 P, cfloat3 dir, float t, float *dist)
 {
-  const int child_addr = node_addr + child * 3;
-  const hc_float4 sx = nodes[child_addr + 1], sy = nodes[child_addr + 2], sz = nodes[child_addr + 3];
   struct cy_tfm space;
   space.x.x = sx.x, space.x.y = sx.y, space.x.z = sx.z, space.x.w = sx.w;
   space.y.x = sy.x, space.y.y = sy.y, space.y.z = sy.z, space.y.w = sy.w;
@@ -556,6 +553,13 @@ CY_FN bool bvh_unaligned_node_intersect_child(const hc_float4 *nodes, int node_a
   const float tfar = min4(t, far_x, far_y, far_z);
   *dist = tnear;
   return tnear <= tfar;
+}
+
+CY_FN bool bvh_unaligned_node_intersect_child(const hc_float4 *nodes, int node_addr, int child, cfloat3 P,
+                                              cfloat3 dir, float t, float *dist)
+{
+  const int child_addr = node_addr + child * 3;
+  return bvh_obb_intersect(nodes[child_addr + 1], nodes[child_addr + 2], nodes[child_addr + 3], P, dir, t, dist);
 }
 
 template<int HAIR>
@@ -618,7 +622,7 @@ struct CyTravCursor {
 };
 
 /* Forward declaration: the wide traversal of one instance's BVH (cy_bvhw.h). */
-template<int W, bool any_hit>
+template<int W, bool any_hit, int HAIR = 0>
 CY_FN bool bvhw_traverse(const CyGlobals *kg, int root, cfloat3 P, cfloat3 dir, cfloat3 idir, int object,
                          uint visibility, CyIsect *isect, uint *err, uint *cnt_nodes, uint *cnt_leaves,
                          uint *cnt_tris, CY_LDS CyStackEntry *lds_ring, bool *tie_out, int budget = 0,
@@ -782,7 +786,7 @@ CY_FN bool bvh2_intersect(const CyGlobals *kg,
           if constexpr (WI > 2) {
             /* the instance's own BVH, wide; then the instance pop and the
              * top-level continuation, as the reference does at the sentinel */
-            const bool h = bvhw_traverse<WI, any_hit>(kg, kg->bvhw_object_root[object], P, dir, idir, object,
+            const bool h = bvhw_traverse<WI, any_hit, HAIR>(kg, kg->bvhw_object_root[object], P, dir, idir, object,
                                                        visibility, isect, err, cnt_nodes, cnt_leaves, cnt_tris,
                                                        lds_ring, tie);
             if (any_hit && h) {
@@ -974,6 +978,153 @@ CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
       --stack_ptr;
     }
   } while (node_addr != ENTRYPOINT_SENTINEL);
+  return false;
+}
+
+/* Record-all shadow traversal of the W-wide layout (non-instanced scenes;
+ * kg->bvhw_width 4 or 8, oriented-box nodes in ribbon scenes): the query of
+ * bvh2_shadow_all above with the same bound (the ray's own t, which no
+ * recorded hit shortens), the same slab arithmetic on the same boxes and the
+ * same primitive tests, so it records the same set of hits and blocks on the
+ * same conditions (an occluder without transparent shadow, or more than
+ * max_hits hits) -- only the recording order differs, which the caller's
+ * sort by distance removes unless two hits share a distance
+ * (shadow_blocked_transparent then repeats the query in the BVH2's order). */
+#ifndef CY_SHADOW_WIDE_STACK
+#  define CY_SHADOW_WIDE_STACK 96
+#endif
+template<int HAIR>
+CY_FN bool bvhw_shadow_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits, uint visibility, uint max_hits,
+                           uint *num_hits, uint *err)
+{
+  const int Q = kg->bvhw_width >> 2;
+  const hc_float4 *nodes = (const hc_float4 *)kg->bvhw_nodes;
+  const float tmax = ray->t;
+  const cfloat3 P = ray->P;
+  const cfloat3 dir = bvh_clamp_direction(ray->D);
+  const cfloat3 idir = rcp3(dir);
+  int stack[CY_SHADOW_WIDE_STACK];
+  int sp = 0;
+  int code = 0;
+  *num_hits = 0;
+  while (true) {
+    if (code >= 0) {
+      const bool obb = HAIR != 0 && (code & (1 << 30));
+      const hc_float4 *np = nodes + (size_t)(code & ~(1 << 30)) * (size_t)(8 * Q);
+      int next = 0, n_hit = 0;
+      if (obb) {
+        /* oriented-box node (cy_bvhw_collapse.h emit_obb) */
+        const hc_float4 h = np[0];
+        float d0, d1;
+        if (bvh_obb_intersect(np[1], np[2], np[3], P, dir, tmax, &d0) && (as_uint(h.x) & visibility)) {
+          next = as_int(h.z);
+          n_hit = 1;
+        }
+        if (bvh_obb_intersect(np[4], np[5], np[6], P, dir, tmax, &d1) && (as_uint(h.y) & visibility)) {
+          if (n_hit) {
+            if (sp == CY_SHADOW_WIDE_STACK) {
+              cy_set_error(err, CY_ERR_BVH_STACK, 3);
+              return true;
+            }
+            stack[sp++] = as_int(h.w);
+          }
+          else {
+            next = as_int(h.w);
+            n_hit = 1;
+          }
+        }
+      }
+      else {
+        for (int q = 0; q < Q; q++) {
+          const hc_float4 lx = np[0 * Q + q], hx = np[1 * Q + q];
+          const hc_float4 ly = np[2 * Q + q], hy = np[3 * Q + q];
+          const hc_float4 lz = np[4 * Q + q], hz = np[5 * Q + q];
+          const hc_float4 ch = np[6 * Q + q], mt = np[7 * Q + q];
+          const float alx[4] = {lx.x, lx.y, lx.z, lx.w}, ahx[4] = {hx.x, hx.y, hx.z, hx.w};
+          const float aly[4] = {ly.x, ly.y, ly.z, ly.w}, ahy[4] = {hy.x, hy.y, hy.z, hy.w};
+          const float alz[4] = {lz.x, lz.y, lz.z, lz.w}, ahz[4] = {hz.x, hz.y, hz.z, hz.w};
+          const int ach[4] = {as_int(ch.x), as_int(ch.y), as_int(ch.z), as_int(ch.w)};
+          const uint amt[4] = {as_uint(mt.x), as_uint(mt.y), as_uint(mt.z), as_uint(mt.w)};
+          for (int j = 0; j < 4; j++) {
+            const float clox = (alx[j] - P.x) * idir.x;
+            const float chix = (ahx[j] - P.x) * idir.x;
+            const float cloy = (aly[j] - P.y) * idir.y;
+            const float chiy = (ahy[j] - P.y) * idir.y;
+            const float cloz = (alz[j] - P.z) * idir.z;
+            const float chiz = (ahz[j] - P.z) * idir.z;
+            const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz));
+            const float cmx = min4(tmax, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
+            if ((cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility)) {
+              if (n_hit) {
+                if (sp == CY_SHADOW_WIDE_STACK) {
+                  cy_set_error(err, CY_ERR_BVH_STACK, 3);
+                  return true;
+                }
+                stack[sp++] = ach[j];
+              }
+              else {
+                next = ach[j];
+                n_hit = 1;
+              }
+            }
+          }
+        }
+      }
+      if (n_hit) {
+        code = next;
+        continue;
+      }
+    }
+    else {
+      const int packed = ~code;
+      int prim_addr = packed >> 4;
+      const int prim_end = prim_addr + (packed & 15);
+      if ((packed & 15) == 0) {
+        cy_set_error(err, CY_ERR_FEATURE, 1); /* instanced scenes keep bvh2_shadow_all */
+        return true;
+      }
+      const bool curves = HAIR != 0 && (kg->__prim_type[prim_addr] & PRIMITIVE_ALL_CURVE);
+      for (; prim_addr < prim_end; prim_addr++) {
+        CyIsect *h = &hits[*num_hits];
+        bool hit;
+        int shader;
+        if (curves) {
+          h->t = tmax;
+          hit = curve_intersect<HAIR>(kg, h, P, dir, visibility, OBJECT_NONE, prim_addr, kg->__prim_type[prim_addr]);
+          shader = hit ? as_int(kg->__curves[kg->__prim_index[prim_addr]].z) : 0;
+        }
+        else {
+          const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+          const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+          float tt, uu, vv;
+          hit = ray_triangle_intersect(P, dir, tmax, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv, &tt) &&
+                (kg->__prim_visibility[prim_addr] & visibility);
+          if (hit) {
+            h->prim = prim_addr;
+            h->object = OBJECT_NONE;
+            h->type = PRIMITIVE_TRIANGLE;
+            h->u = uu;
+            h->v = vv;
+            h->t = tt;
+          }
+          shader = hit ? (int)kg->__tri_shader[kg->__prim_index[prim_addr]] : 0;
+        }
+        if (hit) {
+          if (!(kg->__shaders[shader & SHADER_MASK].flags & SD_HAS_TRANSPARENT_SHADOW)) {
+            return true;
+          }
+          if (*num_hits == max_hits) {
+            return true;
+          }
+          (*num_hits)++;
+        }
+      }
+    }
+    if (sp == 0) {
+      break;
+    }
+    code = stack[--sp];
+  }
   return false;
 }
 

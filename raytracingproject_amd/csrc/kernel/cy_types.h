@@ -417,6 +417,32 @@ typedef struct CyPathState {
   float ray_t;
   int volume_bounce;        /* volume scenes only (cy_volume.h) */
   int volume_bounds_bounce;
+#ifdef CY_DBG_X
+  bool dbg; /* debugging builds: this path is the traced one (CY_DBG_*) */
+#endif
 } CyPathState;
+
+/* Debugging builds (-DCY_DBG_X=x -DCY_DBG_Y=y -DCY_DBG_S=sample): the shading
+ * stage prints the bit patterns of its intermediate values for one path, on
+ * the device (printf) and in the host emulation alike, so that the first
+ * differing line names the operation (tools/dbg_trace.py). */
+#ifdef CY_DBG_X
+#  define CY_DBGF(st, ...) \
+    do { \
+      if ((st)->dbg) { \
+        printf(__VA_ARGS__); \
+      } \
+    } while (0)
+#  define CY_DBG3(st, tag, v) \
+    CY_DBGF(st, "%s %08x %08x %08x\n", tag, __builtin_bit_cast(unsigned, (v).x), \
+            __builtin_bit_cast(unsigned, (v).y), __builtin_bit_cast(unsigned, (v).z))
+#  define CY_DBG1(st, tag, f) CY_DBGF(st, "%s %08x\n", tag, __builtin_bit_cast(unsigned, (float)(f)))
+#else
+#  define CY_DBGF(st, ...) \
+    do { \
+    } while (0)
+#  define CY_DBG3(st, tag, v) CY_DBGF(st)
+#  define CY_DBG1(st, tag, f) CY_DBGF(st)
+#endif
 
 #endif /* CY_TYPES_H */

@@ -75,11 +75,13 @@ class EmuScene:
         self.data = (ctypes.c_char * ctypes.sizeof(ds.data)).from_buffer_copy(bytes(ds.data))
         self.width = bvh_width
         self.wide, self.object_root = None, None
+        self.curve_shapes = curve_shapes(ds)
         if bvh_width > 2:
             self.wide, _, self.object_root = bvhw_build(lib, ds, bvh_width, merge_prims, with_roots=True)
 
     def args(self):
         self.lib.emu_set_width(self.width)
+        self.lib.emu_set_curve_shapes(self.curve_shapes)
         self.lib.emu_set_instancing(int(self.ds.info.get("instanced_objects", 0) > 0))
 
         self.lib.emu_set_object_root(None if self.object_root is None else self.object_root.ctypes.data)
@@ -113,11 +115,24 @@ class EmuScene:
         return buf
 
 
+def curve_shapes(ds):
+    """Curve primitive shapes of the scene as hipcycles.hip load_kernels
+    derives them from __prim_type: 0 none, 1 ribbons, 2 thick, 3 both."""
+    import numpy as np
+
+    if not ds.data.bvh.have_curves or "__prim_type" not in ds.arrays:
+        return 0
+    t = np.asarray(ds.arrays["__prim_type"]).astype(np.uint32)
+    shapes = (1 if np.any(t & ((1 << 4) | (1 << 5))) else 0) | (2 if np.any(t & ((1 << 2) | (1 << 3))) else 0)
+    return shapes or 3
+
+
 def bvhw_build(lib, ds, width=4, merge_prims=0, with_roots=False):
     """Widen the scene's BVH2 exactly like the device library; returns
     (uint32 array of 8*width words per node, depth[, per-object wide roots])."""
     import numpy as np
 
+    lib.emu_set_curve_shapes(curve_shapes(ds))
     nodes = np.ascontiguousarray(ds.arrays["__bvh_nodes"], dtype=np.float32).reshape(-1)
     leaves = np.ascontiguousarray(ds.arrays["__bvh_leaf_nodes"], dtype=np.float32).reshape(-1)
     pobj = np.ascontiguousarray(ds.arrays["__prim_object"], dtype=np.uint32)

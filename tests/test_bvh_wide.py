@@ -11,6 +11,13 @@ candidates' distances tie, the reference's visiting order decides
 util/util_math_intersect.h:178 accepts T <= ray_t*den); the wide traversal
 flags such rays and they are re-traced in the reference's order, so closest
 hits and renders are bit-identical to the reference.
+
+Ribbon hair scenes use the wide layout too: the BVH2's unaligned nodes are
+kept as oriented two-child nodes inside it (the reference's test on its own
+transforms), and a ribbon the ray crosses in two subdivision steps (whose
+result depends on the bound it is tested with) is re-traced in the
+reference's order like a near-tie.  Thick
+curves keep the BVH2 (cy_bvhw.h, hipcycles.hip pick_width).
 """
 import numpy as np
 import pytest
@@ -27,7 +34,12 @@ def emu():
     return nb.host_emu(libm_sincos=True)
 
 
-@pytest.fixture(scope="module", params=[(n, w, m) for n in EMU_CASES if n not in CURVE_CASES for w, m in VARIANTS],
+# hair scenes whose curves are all ribbons (the wide layout serves them)
+RIBBON_CASES = ["hair_ribbon", "hair_principled", "hair_info_ribbon"]
+WIDE_CASES = [n for n in EMU_CASES if n not in CURVE_CASES or n in RIBBON_CASES]
+
+
+@pytest.fixture(scope="module", params=[(n, w, m) for n in WIDE_CASES for w, m in VARIANTS],
                 ids=lambda p: f"{p[0]}-w{p[1]}-m{p[2]}")
 def case(request, emu):
     name, width, merge = request.param
@@ -36,61 +48,88 @@ def case(request, emu):
     return name, ds, g, nb.EmuScene(emu, ds, width, merge), merge
 
 
-def _decode(es):
-    W = es.width
-    w = es.wide.reshape(-1, 8, W)
-    f = w.view(np.float32)
-    lo = np.stack([f[:, 0], f[:, 2], f[:, 4]], axis=1)
-    hi = np.stack([f[:, 1], f[:, 3], f[:, 5]], axis=1)
-    return w[:, 6].view(np.int32), w[:, 7], lo, hi
-
-
 def _bvh2_leaves(ds):
     leaves = ds.arrays["__bvh_leaf_nodes"].reshape(-1, 4).view(np.int32)
     return {int(l[0]): int(l[1] - l[0]) for l in leaves}
 
 
+OBB = 1 << 30  # child code bit of an oriented-box node (hair scenes)
+
+
+def _walk(es, roots):
+    """Every node reachable from the roots: per node its kind and child codes
+    (wide node: (code, meta, lo, hi) per valid slot; OBB node: two codes)."""
+    W = es.width
+    words = es.wide.reshape(-1, 8 * W)
+    out, todo = {}, [(r, False) for r in roots]
+    while todo:
+        idx, obb = todo.pop()
+        if idx in out:
+            continue
+        w = words[idx]
+        if obb:
+            kids = [(int(np.int32(np.uint32(w[2 + k]))), None, None, None) for k in range(2)]
+        else:
+            f = w.view(np.float32).reshape(8, W)
+            m = w.reshape(8, W)
+            kids = [(int(np.int32(m[6, j])), int(m[7, j]), f[0:6:2, j], f[1:6:2, j])
+                    for j in range(W) if (m[7, j] & 0x0FFFFFFF) != 0]
+        out[idx] = (obb, kids)
+        for code, *_ in kids:
+            if code >= 0:
+                todo.append((code & ~OBB, bool(code & OBB)))
+    return out
+
+
 def test_collapse_structure(case):
     name, ds, g, es, merge = case
-    child, meta, lo, hi = _decode(es)
-    n = len(child)
-    valid = (meta & 0x0FFFFFFF) != 0
-    inner = valid & (child >= 0)
-    leaf = valid & (child < 0)
-    # every wide node except the roots (top level, each instanced geometry's
-    # own BVH) is referenced exactly once
-    refs = np.bincount(child[inner], minlength=n)
     onode = ds.arrays["__object_node"].view(np.int32)
     inst_objects = np.nonzero(ds.arrays["__object_flag"] & 4 == 0)[0]  # not SD_OBJECT_TRANSFORM_APPLIED
     roots = {0} | {int(es.object_root[o]) for o in inst_objects}
     assert all(es.object_root[o] >= 0 for o in inst_objects)
     assert len(roots) == 1 + len({int(onode[o]) for o in inst_objects})
+    nodes = _walk(es, sorted(roots))
+    # every node of the array is reached, each non-root node from exactly one
+    # parent slot
+    n = len(es.wide) // (8 * es.width)
+    assert set(nodes) == set(range(n))
+    refs = np.zeros(n, dtype=np.int64)
+    for obb, kids in nodes.values():
+        for code, *_ in kids:
+            if code >= 0:
+                refs[code & ~OBB] += 1
     is_root = np.zeros(n, dtype=bool)
     is_root[list(roots)] = True
     assert np.all(refs[is_root] == 0) and np.all(refs[~is_root] == 1)
+    if name not in CURVE_CASES:
+        assert not any(obb for obb, _ in nodes.values())
     # the leaf ranges tile the primitive array exactly once (instance slots,
     # prim_type 0, are entered through count-0 instance leaves instead)
-    starts, counts = (~child[leaf]) >> 4, meta[leaf] >> 28
-    assert np.array_equal((~child[leaf]) & 15, counts)
-    tri_leaf = counts > 0
-    assert set(((~child[leaf]) >> 4)[~tri_leaf].tolist()) == set(inst_objects.tolist())
-    starts, counts = starts[tri_leaf], counts[tri_leaf]
+    leaves = [(~code >> 4, ~code & 15, lo, hi) for obb, kids in nodes.values() for code, meta, lo, hi in kids
+              if code < 0]
+    counts = np.array([c for _, c, _, _ in leaves])
+    starts = np.array([s for s, _, _, _ in leaves])
+    assert set(starts[counts == 0].tolist()) == set(inst_objects.tolist())
     cover = np.zeros(len(ds.arrays["__prim_index"]), dtype=np.int32)
-    for s, c in zip(starts.tolist(), counts.tolist()):
-        cover[s:s + c] += 1
+    for st, c in zip(starts[counts > 0].tolist(), counts[counts > 0].tolist()):
+        cover[st:st + c] += 1
     assert np.all(cover == (ds.arrays["__prim_type"] != 0))
-    if merge == 0:
+    if merge == 0 or name in CURVE_CASES:
+        # hair scenes never merge (a merged leaf could mix primitive types)
         bvh2 = {k: v for k, v in _bvh2_leaves(ds).items() if k >= 0}
-        assert dict(zip(starts.tolist(), counts.tolist())) == bvh2
+        got = {int(st): int(c) for st, c in zip(starts.tolist(), counts.tolist()) if c > 0}
+        assert got == bvh2
     else:
         assert np.all(counts <= max(merge, 8))
-    leaf = leaf & ((meta >> 28) > 0)
-    # leaf boxes contain their triangles
+    # wide-node leaf boxes (exact BVH2 boxes) contain their triangles
+    ptype = ds.arrays["__prim_type"].astype(np.uint32)
     verts = ds.arrays["__prim_tri_verts"].reshape(-1, 4)[:, :3]
     tri_index = ds.arrays["__prim_tri_index"].astype(np.int64)
-    for (node, slot), s, c in zip(zip(*np.nonzero(leaf)), starts.tolist(), counts.tolist()):
-        v = np.concatenate([verts[tri_index[k]:tri_index[k] + 3] for k in range(s, s + c)])
-        assert np.all(v >= lo[node, :, slot]) and np.all(v <= hi[node, :, slot])
+    for st, c, lo, hi in leaves:
+        if c == 0 or lo is None or ptype[st] & 0x3C:
+            continue
+        v = np.concatenate([verts[tri_index[k]:tri_index[k] + 3] for k in range(st, st + c)])
+        assert np.all(v >= lo) and np.all(v <= hi)
 
 
 def test_wide_closest_hit_vs_reference(case):

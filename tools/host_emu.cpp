@@ -24,6 +24,14 @@
 /* Widen a packed BVH2 like the device library does (hipcycles.hip ensure_bvhw).
  * Returns the number of uint32 written (32 per node), or -1 with the reason
  * copied to err_out. */
+/* curve shapes of the scene (1 ribbons, 2 thick, 3 both; hipcycles.hip
+ * curve_shapes): ribbon-only scenes widen their hair BVH2 too */
+static int g_curve_shapes = 0;
+extern "C" void emu_set_curve_shapes(int shapes)
+{
+  g_curve_shapes = shapes;
+}
+
 extern "C" long emu_bvhw_build(int width,
                                int merge_prims,
                                const float *nodes2,
@@ -45,6 +53,7 @@ extern "C" long emu_bvhw_build(int width,
   cybvhw::Collapser col;
   col.width = width;
   col.merge_prims = merge_prims;
+  col.allow_curves = g_curve_shapes != 0;
   col.nodes2 = nodes2;
   col.n_nodes2 = (size_t)n_nodes2;
   col.leaves2 = leaves2;
@@ -68,6 +77,7 @@ extern "C" long emu_bvhw_build(int width,
 }
 
 static int g_width = 2;
+static int g_instancing = 0; /* emu_set_instancing */
 
 static const int *g_object_root = nullptr;
 
@@ -90,12 +100,16 @@ static void emu_bind(CyGlobals *kg, const void *data, int n_arrays, const char *
   }
   kg->bvhw_nodes = bvhw;
   kg->bvhw_object_root = g_object_root;
-  kg->have_instancing = 1; /* generic: the instance paths are always enabled on the host */
+  /* generic: the instance paths are always enabled on the host, except that
+   * a wide layout over a scene without instances takes the device's
+   * non-instanced paths (hipcycles.hip build_globals) */
+  kg->have_instancing = (bvhw && !g_instancing) ? 0 : 1;
   kg->tri_index_identity = 0;
   kg->have_curves = kg->data->bvh.have_curves ? 1 : 0;
-  if (kg->have_curves) {
-    kg->bvhw_nodes = nullptr; /* scenes with curves keep the BVH2 (hipcycles.hip build_globals) */
+  if (kg->have_curves && g_curve_shapes != 1) {
+    kg->bvhw_nodes = nullptr; /* thick curves keep the BVH2 (hipcycles.hip wide_layout) */
   }
+  kg->bvhw_width = kg->bvhw_nodes ? g_width : 0;
 }
 
 extern "C" void emu_set_width(int w)
@@ -105,7 +119,6 @@ extern "C" void emu_set_width(int w)
 
 /* instanced scene: the device's wide kernels then traverse the top level in
  * the reference's order and the instances wide (hipcycles.hip scene_traverse) */
-static int g_instancing = 0;
 extern "C" void emu_set_instancing(int on)
 {
   g_instancing = on;
@@ -115,6 +128,29 @@ template<bool any_hit>
 static bool emu_traverse_impl(const CyGlobals *kg, const CyRay *ray, uint vis, CyIsect *isect, uint *err,
                               uint *nn, uint *nl, uint *nt)
 {
+  if (kg->bvhw_nodes && kg->have_curves) {
+    /* ribbon scene on the wide BVH; near-ties and twice-crossed ribbons are
+     * re-traced in the reference's order (hipcycles.hip k_intersect_closest) */
+    bool tie = false, hit;
+    if (g_instancing) {
+      hit = g_width == 8 ?
+                bvh2_intersect<any_hit, true, 8, CY_LDS_STACK, CY_BLOCK, 1>(kg, ray, vis, isect, err, nn, nl, nt,
+                                                                           nullptr, nullptr, &tie) :
+                bvh2_intersect<any_hit, true, 4, CY_LDS_STACK, CY_BLOCK, 1>(kg, ray, vis, isect, err, nn, nl, nt,
+                                                                           nullptr, nullptr, &tie);
+    }
+    else {
+      hit = g_width == 8 ? bvhw_intersect<8, any_hit, 1>(kg, ray, vis, isect, err, nn, nl, nt, nullptr, &tie) :
+                           bvhw_intersect<4, any_hit, 1>(kg, ray, vis, isect, err, nn, nl, nt, nullptr, &tie);
+    }
+    if (!tie) {
+      return hit;
+    }
+    CyGlobals k2 = *kg;
+    k2.bvhw_nodes = nullptr;
+    return bvh2_intersect<any_hit, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(&k2, ray, vis, isect, err, nullptr, nullptr,
+                                                                        nullptr, nullptr);
+  }
   if (kg->bvhw_nodes) {
     bool tie = false, hit;
     if (g_instancing) {
@@ -173,7 +209,10 @@ static bool emu_traverse(const CyGlobals *kg, const CyRay *ray, uint vis, CyIsec
     CyGlobals k2 = *kg;
     k2.bvhw_nodes = nullptr;
     CyIsect i2;
-    const bool h2 = bvh2_intersect<false>(&k2, ray, vis, &i2, err, nullptr, nullptr, nullptr, nullptr);
+    const bool h2 = kg->have_curves ?
+                        bvh2_intersect<false, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(&k2, ray, vis, &i2, err, nullptr,
+                                                                                   nullptr, nullptr, nullptr) :
+                        bvh2_intersect<false>(&k2, ray, vis, &i2, err, nullptr, nullptr, nullptr, nullptr);
     if (h2 != hit || (hit && (i2.prim != isect->prim || as_uint(i2.t) != as_uint(isect->t)))) {
       const float rec[16] = {ray->P.x, ray->D.x, ray->P.y, ray->D.y, ray->P.z, ray->D.z, ray->t, as_float(vis),
                              (float)isect->prim, isect->t, (float)i2.prim, i2.t, (float)isect->object,
