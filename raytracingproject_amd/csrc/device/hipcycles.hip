@@ -26,6 +26,12 @@
  * the wide BVHs CY_LDS_STACKW (node, entry distance) pairs. */
 /* Minimum waves per SIMD the traversal kernels are register-allocated for
  * (amdgpu_waves_per_eu); with the LDS stack it sets their occupancy. */
+/* hair kernels (the ribbon and thick-curve intersectors) need more registers:
+ * at the 96 of five waves they spill */
+#ifndef CY_TRAV_HAIR_WAVES
+#  define CY_TRAV_HAIR_WAVES 3
+#endif
+#define CY_TRAV_WAVES(hair) ((hair) != 0 ? CY_TRAV_HAIR_WAVES : CY_TRAV_MIN_WAVES)
 #ifndef CY_TRAV_MIN_WAVES
 #  define CY_TRAV_MIN_WAVES 5
 #endif
@@ -370,7 +376,7 @@ __device__ __forceinline__ void cont_suspend(const CyGlobals *kg, const CyCont &
  * with camera-ray generation inside the traversal loop spills at the 80-VGPR
  * budget, and replacement rays break the camera rays' fetch coherence). */
 template<bool STATS, int W, bool INST, int HAIR = 0>
-__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_closest(CyGlobals kg,
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_WAVES(HAIR)) k_intersect_closest(CyGlobals kg,
                                                                  CyPathBuffers b,
                                                                  CyTile tile,
                                                                  int cam_n,
@@ -810,7 +816,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_shadow_finish(CyGlobals kg, CyPath
 
 /* Stage 3: occlusion of the light sample, deferred light add, finish + refill. */
 template<bool STATS, int W, bool INST, int HAIR = 0>
-__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_intersect_shadow(CyGlobals kg,
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_WAVES(HAIR)) k_intersect_shadow(CyGlobals kg,
                                                                 CyPathBuffers b,
                                                                 CyTile tile,
                                                                 const int *shadow_queue,

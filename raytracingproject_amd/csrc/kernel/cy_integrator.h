@@ -1400,7 +1400,11 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
             }
             else {
               bool blocked = false;
+#ifdef CY_EXP_SSS_NO_SHADOW /* profiling experiment only: exit points never occluded */
+              if (false) {
+#else
               if (scene_intersect_valid(&sray)) {
+#endif
                 CyIsect si;
                 blocked = kg->have_curves ?
                               bvh2_intersect<true, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(
@@ -1509,7 +1513,12 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
   uint lcg_state = lcg_init(state->rng_hash + (uint)state->rng_offset + (uint)state->sample * 0x68bc21ebu);
   CyLocalHits li;
   CyRay ss_ray;
+#ifdef CY_EXP_SSS_OFF /* profiling experiment only: no exit points */
+  const int num_hits = 0;
+  (void)lcg_state;
+#else
   const int num_hits = subsurface_scatter_disk(kg, &li, sd, sc, &lcg_state, bssrdf_u, bssrdf_v, &ss_ray, err);
+#endif
   int pushed = 0;
   CyPathState top_state;
   CyRay top_ray;

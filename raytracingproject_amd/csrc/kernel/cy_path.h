@@ -1013,24 +1013,25 @@ CY_FN bool bvhw_shadow_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits,
       const hc_float4 *np = nodes + (size_t)(code & ~(1 << 30)) * (size_t)(8 * Q);
       int next = 0, n_hit = 0;
       if (obb) {
-        /* oriented-box node (cy_bvhw_collapse.h emit_obb) */
-        const hc_float4 h = np[0];
-        float d0, d1;
-        if (bvh_obb_intersect(np[1], np[2], np[3], P, dir, tmax, &d0) && (as_uint(h.x) & visibility)) {
-          next = as_int(h.z);
-          n_hit = 1;
-        }
-        if (bvh_obb_intersect(np[4], np[5], np[6], P, dir, tmax, &d1) && (as_uint(h.y) & visibility)) {
-          if (n_hit) {
-            if (sp == CY_SHADOW_WIDE_STACK) {
-              cy_set_error(err, CY_ERR_BVH_STACK, 3);
-              return true;
+        /* oriented-box node (cy_bvhw_collapse.h emit_obb): up to four children */
+        const hc_float4 hc = np[0], hv = np[1];
+        const int acode[4] = {as_int(hc.x), as_int(hc.y), as_int(hc.z), as_int(hc.w)};
+        const uint avis[4] = {as_uint(hv.x), as_uint(hv.y), as_uint(hv.z), as_uint(hv.w)};
+        for (int k = 0; k < 4; k++) {
+          float d;
+          if ((avis[k] & visibility) && bvh_obb_intersect(np[2 + 3 * k], np[3 + 3 * k], np[4 + 3 * k], P, dir, tmax,
+                                                          &d)) {
+            if (n_hit) {
+              if (sp == CY_SHADOW_WIDE_STACK) {
+                cy_set_error(err, CY_ERR_BVH_STACK, 3);
+                return true;
+              }
+              stack[sp++] = acode[k];
             }
-            stack[sp++] = as_int(h.w);
-          }
-          else {
-            next = as_int(h.w);
-            n_hit = 1;
+            else {
+              next = acode[k];
+              n_hit = 1;
+            }
           }
         }
       }

@@ -13,7 +13,7 @@ flags such rays and they are re-traced in the reference's order, so closest
 hits and renders are bit-identical to the reference.
 
 Ribbon hair scenes use the wide layout too: the BVH2's unaligned nodes are
-kept as oriented two-child nodes inside it (the reference's test on its own
+widened into oriented four-child nodes (the reference's test on its own
 transforms), and a ribbon the ray crosses in two subdivision steps (whose
 result depends on the bound it is tested with) is re-traced in the
 reference's order like a near-tie.  Thick
@@ -68,7 +68,9 @@ def _walk(es, roots):
             continue
         w = words[idx]
         if obb:
-            kids = [(int(np.int32(np.uint32(w[2 + k]))), None, None, None) for k in range(2)]
+            # OBB node: four codes, four stored visibilities (0 = empty slot)
+            w = es.wide[idx * 8 * W: idx * 8 * W + 64]
+            kids = [(int(np.int32(np.uint32(w[k]))), None, None, None) for k in range(4) if w[4 + k] != 0]
         else:
             f = w.view(np.float32).reshape(8, W)
             m = w.reshape(8, W)
@@ -92,7 +94,9 @@ def test_collapse_structure(case):
     # every node of the array is reached, each non-root node from exactly one
     # parent slot
     n = len(es.wide) // (8 * es.width)
-    assert set(nodes) == set(range(n))
+    # (an OBB node takes 256 B: two slots at W = 4)
+    second = {i + 1 for i, (obb, _) in nodes.items() if obb and es.width == 4}
+    assert set(nodes) | second == set(range(n)) and not set(nodes) & second
     refs = np.zeros(n, dtype=np.int64)
     for obb, kids in nodes.values():
         for code, *_ in kids:
@@ -100,7 +104,10 @@ def test_collapse_structure(case):
                 refs[code & ~OBB] += 1
     is_root = np.zeros(n, dtype=bool)
     is_root[list(roots)] = True
-    assert np.all(refs[is_root] == 0) and np.all(refs[~is_root] == 1)
+    nodes_mask = np.zeros(n, dtype=bool)
+    nodes_mask[list(nodes)] = True
+    assert np.all(refs[is_root] == 0) and np.all(refs[~is_root & nodes_mask] == 1)
+    assert np.all(refs[~nodes_mask] == 0)
     if name not in CURVE_CASES:
         assert not any(obb for obb, _ in nodes.values())
     # the leaf ranges tile the primitive array exactly once (instance slots,

@@ -62,15 +62,19 @@ def main():
         ctypes.CDLL(None).fflush(None)
         return
     os.environ.setdefault("HIPCY_DEVICE_LIB", os.path.join(ROOT, "raytracingproject_amd", "libhipcycles-dbg.so"))
+    import torch
+
+    torch.zeros(1, device="cuda")  # the HIP runtime comes up through torch first, as in bench.py
     from raytracingproject_amd.device import HIPDevice
 
     dev = HIPDevice(0)
     dev.set_bvh_width(width)
     dev.upload_scene(ds)
     print(f"# device {name} pixel ({x},{y}) sample {s} W={width}", flush=True)
-    dev.render(samples=1, start_sample=s, tile=(x, y, 1, 1))
-    import torch
-
+    if os.environ.get("DBG_FULL_FRAME"):
+        dev.render()  # the whole frame: the traced path is one of them
+    else:
+        dev.render(samples=1, start_sample=s, tile=(x, y, 1, 1))
     torch.cuda.synchronize()
     dev.close()
     ctypes.CDLL(None).fflush(None)
