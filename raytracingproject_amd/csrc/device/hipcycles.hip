@@ -970,6 +970,29 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_MIN_WAVES) k_shadow_continue
   }
 }
 
+/* Transparent shadows, traversal half (non-instanced scenes): the record-all
+ * query of each pending shadow ray (bvh_shadow_all.h; the wide layout's
+ * bvhw_shadow_all or the BVH2's) at the traversal kernels' occupancy, leaving
+ * the shading kernel below only the occluders' shaders to evaluate.  The
+ * outcome goes to the slot's record (CyPathBuffers.shadow_nrec / _hits):
+ * blocked, or up to CY_SHADOW_REC_HITS hits sorted by distance; more hits, two
+ * at one distance, or a ray the shading kernel ends before its traversal
+ * (t = 0, transparent bounces spent) leave CY_SREC_NONE and the shading kernel
+ * traverses itself, as before. */
+template<int HAIR>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_WAVES(HAIR)) k_shadow_record(CyGlobals kg, CyPathBuffers b,
+                                                                                const int *shadow_queue,
+                                                                                const uint *shadow_count, uint *err)
+{
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int)*shadow_count) {
+    return;
+  }
+  const int slot = shadow_queue[i];
+  const uint rec = shadow_record<HAIR>(&kg, &b, slot, err);
+  cy_st(&b.shadow_nrec[slot], rec);
+}
+
 /* Stage 3 with transparent shadows (KernelIntegrator.transparent_shadows): the
  * record-all occlusion of the light sample with the occluders' shaders
  * evaluated (cy_integrator.h shadow_finish_transparent), then the same finish
@@ -1594,6 +1617,7 @@ struct hipcy_device {
   char *sss_pool = nullptr;           /* those records and their depths */
   bool use_ray_diff = false;          /* a shader reads ray differentials (Bump / *_BUMP_DX / _DY nodes) */
   char *diff_pool = nullptr;          /* the slots' ray and shadow-ray differentials */
+  char *srec_pool = nullptr;          /* the slots' transparent-shadow records (k_shadow_record) */
   int shade_closures = 1;             /* closure array of the shading kernel (variant by size) */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int curve_shapes = 0;               /* curve primitive shapes in __prim_type: 1 ribbon, 2 thick, 3 both */
@@ -1808,6 +1832,12 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   }
   dev->bufs.ray_diff = nullptr;
   dev->bufs.shadow_dP = nullptr;
+  if (dev->srec_pool) {
+    hipFree(dev->srec_pool);
+    dev->srec_pool = nullptr;
+  }
+  dev->bufs.shadow_hits = nullptr;
+  dev->bufs.shadow_nrec = nullptr;
   /* queues live in their own allocation (3 x slots ints) */
   for (int q = 0; q < 3; q++) {
     if (dev->queue[q]) {
@@ -1862,6 +1892,21 @@ static int ensure_diff_capacity(hipcy_device *dev)
   }
   dev->bufs.ray_diff = dev->use_ray_diff ? (hc_float4 *)dev->diff_pool : nullptr;
   dev->bufs.shadow_dP = dev->use_ray_diff ? (hc_float4 *)(dev->diff_pool + rays) : nullptr;
+  return 0;
+}
+
+/* The transparent-shadow records of k_shadow_record (CY_SHADOW_REC_HITS
+ * float4 and a count per slot, 68 B), for non-instanced scenes with
+ * transparent shadows only. */
+static int ensure_srec_capacity(hipcy_device *dev)
+{
+  const bool use = dev->data_host.integrator.transparent_shadows && !dev->have_instancing;
+  const size_t hits = (size_t)16 * CY_SHADOW_REC_HITS * dev->capacity;
+  if (use && !dev->srec_pool) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->srec_pool, hits + (size_t)4 * dev->capacity));
+  }
+  dev->bufs.shadow_hits = use ? (hc_float4 *)dev->srec_pool : nullptr;
+  dev->bufs.shadow_nrec = use ? (uint *)(dev->srec_pool + hits) : nullptr;
   return 0;
 }
 
@@ -1961,6 +2006,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->vol_pool) hipFree(dev->vol_pool);
   if (dev->sss_pool) hipFree(dev->sss_pool);
   if (dev->diff_pool) hipFree(dev->diff_pool);
+  if (dev->srec_pool) hipFree(dev->srec_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
   if (dev->records) hipFree(dev->records);
   if (dev->tile_descs) hipFree(dev->tile_descs);
@@ -3090,6 +3136,12 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     HIP_CHECK(dev, hipEventRecord(p.c, s));
   }
   if (dev->data_host.integrator.transparent_shadows) {
+    if (dev->bufs.shadow_nrec) {
+      const int hair = kg.have_curves ? dev->curve_shapes : 0;
+      auto krec = hair == 0 ? k_shadow_record<0> : hair == 1 ? k_shadow_record<1> :
+                  hair == 2 ? k_shadow_record<2> : k_shadow_record<3>;
+      hipLaunchKernelGGL(krec, grid, block, 0, s, kg, dev->bufs, ln.q[qs], ln.cnt + qs, err);
+    }
     auto kfn = dev->use_volumes ? k_intersect_shadow_transparent<true> : k_intersect_shadow_transparent<false>;
     hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb], ln.cnt + qb,
                        err);
@@ -3373,7 +3425,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
   }
   const size_t items = npix * per_pass;
   if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 ||
       ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }
@@ -3826,7 +3878,7 @@ static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
 static int stream_pool(hipcy_device *dev, size_t slots)
 {
   if (ensure_capacity(dev, slots) != 0 || ensure_volume_capacity(dev) != 0 || ensure_sss_capacity(dev) != 0 ||
-      ensure_diff_capacity(dev) != 0 || ensure_sort(dev) != 0) {
+      ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
     return -1;
   }
   return 0;

@@ -64,7 +64,18 @@ typedef struct CyPathBuffers {
    * point's dP the pending transparent shadow ray carries, 2 float4 per slot */
   hc_float4 *ray_diff;
   hc_float4 *shadow_dP;
+  /* transparent shadows in non-instanced scenes: the record-all traversal of
+   * each pending shadow ray, done by the traversal stage (hipcycles.hip
+   * k_shadow_record) before the shading stage evaluates the occluders --
+   * per slot CY_SHADOW_REC_HITS hits (t, u, v, prim bits) sorted by distance
+   * and their count, or CY_SREC_BLOCKED / CY_SREC_NONE (traverse here) */
+  hc_float4 *shadow_hits;
+  uint *shadow_nrec;
 } CyPathBuffers;
+
+#define CY_SHADOW_REC_HITS 4
+#define CY_SREC_BLOCKED 0x100u
+#define CY_SREC_NONE 0x200u
 
 #define CY_SSS_RECS (BSSRDF_MAX_HITS - 1)
 #define CY_SSS_REC_F4 9 /* state (3), ray (2), throughput, ray differentials (3) */
@@ -792,7 +803,8 @@ CY_FN bool shadow_finish(const CyPathBuffers *b, const CyTile *tile, int slot, b
 template<bool VOL = false>
 CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPathState *state, CyShadeMem mem,
                                       cfloat3 *shadow, uint *err, void *volume_stack = nullptr,
-                                      const CyDiff3 *ray_dP = nullptr)
+                                      const CyDiff3 *ray_dP = nullptr, uint rec = CY_SREC_NONE,
+                                      const hc_float4 *rec_hits = nullptr)
 {
 #if CY_CLOSURE_EXT
   /* volume scenes: the shadow ray's copy of the path's volume stack, crossed
@@ -813,7 +825,25 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
   uint num_hits = 0;
   bool blocked;
   bool wide = kg->bvhw_nodes != nullptr && !kg->have_instancing;
-  if (wide) {
+  if (rec == CY_SREC_BLOCKED) {
+    return true; /* the traversal stage's record-all met an occluder (blocked: no volume work) */
+  }
+  if (rec <= CY_SHADOW_REC_HITS) {
+    /* the traversal stage's hits: sorted, distinct distances */
+    for (uint k = 0; k < rec; k++) {
+      const hc_float4 h = cy_ld(&rec_hits[k]);
+      hits[k].t = h.x;
+      hits[k].u = h.y;
+      hits[k].v = h.z;
+      hits[k].prim = as_int(h.w);
+      hits[k].object = OBJECT_NONE;
+      hits[k].type = kg->have_curves ? (int)kg->__prim_type[hits[k].prim] : PRIMITIVE_TRIANGLE;
+    }
+    num_hits = rec;
+    blocked = false;
+    wide = false;
+  }
+  else if (wide) {
     /* the wide layout's record-all (same hits, another recording order) */
     blocked = kg->have_curves ? bvhw_shadow_all<1>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
                                 bvhw_shadow_all<0>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
@@ -924,6 +954,60 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
   return is_zero3(throughput);
 }
 
+/* The traversal half of a pending transparent shadow ray (hipcycles.hip
+ * k_shadow_record; non-instanced scenes): the record-all query, its hits
+ * sorted and stored in the slot's record when they fit and their distances
+ * are distinct.  Returns the record word (hit count, CY_SREC_BLOCKED or
+ * CY_SREC_NONE); shadow_finish_transparent takes it from there. */
+template<int HAIR>
+CY_FN uint shadow_record(const CyGlobals *kg, const CyPathBuffers *b, int slot, uint *err)
+{
+  CyRay ray;
+  shadow_load(b, slot, &ray);
+  const uint transparent_bounce = (as_uint(cy_ld(&b->shadow_T[slot]).w) >> 8) & 0xFFu;
+  const int transparent_max_bounce = KD->integrator.transparent_max_bounce;
+  if (ray.t == 0.0f || (int)transparent_bounce >= transparent_max_bounce) {
+    return CY_SREC_NONE; /* shadow_blocked_transparent ends these before traversing */
+  }
+  const uint max_hits = (uint)(transparent_max_bounce - (int)transparent_bounce - 1);
+  CyIsect hits[CY_SHADOW_MAX_HITS];
+  uint n = 0;
+  bool blocked;
+  if constexpr (HAIR <= 1) {
+    blocked = kg->bvhw_nodes ? bvhw_shadow_all<HAIR>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &n, err) :
+                               bvh2_shadow_all<false, HAIR>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &n, err);
+  }
+  else {
+    blocked = bvh2_shadow_all<false, HAIR>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &n, err);
+  }
+  if (blocked) {
+    return CY_SREC_BLOCKED;
+  }
+  if (n > CY_SHADOW_REC_HITS) {
+    return CY_SREC_NONE;
+  }
+  /* sort_intersections (bvh/bvh.h:606-626): stable, by distance */
+  for (uint k = 1; k < n; k++) {
+    const CyIsect h = hits[k];
+    int j = (int)k - 1;
+    while (j >= 0 && hits[j].t > h.t) {
+      hits[j + 1] = hits[j];
+      j--;
+    }
+    hits[j + 1] = h;
+  }
+  for (uint k = 1; k < n; k++) {
+    if (hits[k].t == hits[k - 1].t) {
+      return CY_SREC_NONE; /* the recording order decides: the shading kernel traverses in the BVH2's */
+    }
+  }
+  hc_float4 *out = b->shadow_hits + (size_t)slot * CY_SHADOW_REC_HITS;
+  for (uint k = 0; k < n; k++) {
+    cy_st(&out[k], mkf4(hits[k].t, hits[k].u, hits[k].v, int_as_float(hits[k].prim)));
+  }
+  return n;
+}
+
 /* The transparent-shadow counterpart of shadow_finish: occlusion and
  * attenuation of the pending light sample, then its contribution
  * (path_radiance_accum_light: throughput * shadow, times the eval, clamped). */
@@ -943,6 +1027,8 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
   state.diffuse_bounce = (int)((packed >> 16) & 0xFF);
   state.glossy_bounce = (int)(packed >> 24);
   state.transmission_bounce = as_int(cy_ld(&b->shadow_D[slot]).w);
+  const uint rec = b->shadow_nrec ? cy_ld(&b->shadow_nrec[slot]) : CY_SREC_NONE;
+  const hc_float4 *rec_hits = b->shadow_hits ? b->shadow_hits + (size_t)slot * CY_SHADOW_REC_HITS : nullptr;
   cfloat3 shadow;
   bool blocked;
 #if CY_CLOSURE_EXT
@@ -967,14 +1053,15 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
                               (int)r0.y, &vstack);
     }
     state.rng_offset = (int)r1.y;
-    blocked = shadow_blocked_transparent<true>(kg, ray, &state, mem, &shadow, err, &vstack, sdP_ptr);
+    blocked = shadow_blocked_transparent<true>(kg, ray, &state, mem, &shadow, err, &vstack, sdP_ptr, rec, rec_hits);
   }
   else
   {
-    blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err, nullptr, sdP_ptr);
+    blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err, nullptr, sdP_ptr, rec,
+                                                rec_hits);
   }
 #else
-  blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err);
+  blocked = shadow_blocked_transparent<false>(kg, ray, &state, mem, &shadow, err, nullptr, nullptr, rec, rec_hits);
 #endif
   hc_float4 L4 = cy_ld(&b->L[slot]);
   if (!blocked) {

@@ -22,6 +22,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+if len(sys.argv) > 1 and sys.argv[1] == "gpu":
+    # before any import of raytracingproject_amd.native reads it
+    os.environ.setdefault("HIPCY_DEVICE_LIB", os.path.join(ROOT, "raytracingproject_amd", "libhipcycles-dbg.so"))
 
 
 def main():
@@ -61,7 +64,6 @@ def main():
         es.render(tile=(x, y, 1, 1), start_sample=s, samples=1)
         ctypes.CDLL(None).fflush(None)
         return
-    os.environ.setdefault("HIPCY_DEVICE_LIB", os.path.join(ROOT, "raytracingproject_amd", "libhipcycles-dbg.so"))
     import torch
 
     torch.zeros(1, device="cuda")  # the HIP runtime comes up through torch first, as in bench.py

@@ -305,6 +305,9 @@ extern "C" int emu_render(const void *data,
   hc_uint4 s0, s1;
   uint item_slot = 0;
   CyPathBuffers b;
+  memset(&b, 0, sizeof(b)); /* buffers a feature does not use stay null */
+  hc_float4 srec_hits[CY_SHADOW_REC_HITS];
+  uint srec_n = CY_SREC_NONE;
   b.ray_P = &rec[0];
   b.ray_D = &rec[1];
   b.isect = &rec[2];
@@ -391,6 +394,14 @@ extern "C" int emu_render(const void *data,
                         shade_path<false>(&kg, &b, &tile, 0, cam_item, mem, &shadow, &finished, &err);
       cam_item = CY_NO_ITEM;
       if (shadow && kg.data->integrator.transparent_shadows) {
+        if (!kg.have_instancing) {
+          /* k_shadow_record: the traversal stage's record of the shadow ray */
+          b.shadow_hits = srec_hits;
+          b.shadow_nrec = &srec_n;
+          const int hair = kg.have_curves ? g_curve_shapes : 0;
+          srec_n = hair == 0 ? shadow_record<0>(&kg, &b, 0, &err) : hair == 1 ? shadow_record<1>(&kg, &b, 0, &err) :
+                   hair == 2 ? shadow_record<2>(&kg, &b, 0, &err) : shadow_record<3>(&kg, &b, 0, &err);
+        }
         /* k_intersect_shadow_transparent */
         if (vol) {
           shadow_finish_transparent<true>(&kg, &b, &tile, 0, mem, &err);
