@@ -89,6 +89,22 @@ CY_FN float int_as_float(int i)
   return as_float((uint)i);
 }
 
+/* float_to_int (util_math.h: (int)f) as the reference's x86 CPU kernel
+ * computes it: truncation toward zero, and for NaN or a value outside the int
+ * range cvttss2si's "integer indefinite" 0x80000000, where C leaves the
+ * conversion undefined and the GPU's v_cvt_i32_f32 saturates instead.  Texture
+ * nodes meet such values at the huge offsets of a Bump node's differentials
+ * (a checker at 1e11: x86 gives INT_MIN, the saturating conversion INT_MAX, and
+ * the parity of the cell flips). */
+CY_FN int cy_ftoi(float f)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : (int)0x80000000u;
+#else
+  return (int)f; /* cvttss2si */
+#endif
+}
+
 /* util_math.h:112-130 (ternary forms: NaN handling matches the reference). */
 CY_FN float cmin(float a, float b)
 {

@@ -1009,9 +1009,13 @@ CY_FN bool bvhw_shadow_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits,
   *num_hits = 0;
   while (true) {
     if (code >= 0) {
+      /* the node's hit children, visited nearest first (an occluder that
+       * blocks the light then ends the query early, as in the BVH2's order) */
       const bool obb = HAIR != 0 && (code & (1 << 30));
       const hc_float4 *np = nodes + (size_t)(code & ~(1 << 30)) * (size_t)(8 * Q);
-      int next = 0, n_hit = 0;
+      float tn[8];
+      int cc[8];
+      int n_hit = 0;
       if (obb) {
         /* oriented-box node (cy_bvhw_collapse.h emit_obb): up to four children */
         const hc_float4 hc = np[0], hv = np[1];
@@ -1021,17 +1025,9 @@ CY_FN bool bvhw_shadow_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits,
           float d;
           if ((avis[k] & visibility) && bvh_obb_intersect(np[2 + 3 * k], np[3 + 3 * k], np[4 + 3 * k], P, dir, tmax,
                                                           &d)) {
-            if (n_hit) {
-              if (sp == CY_SHADOW_WIDE_STACK) {
-                cy_set_error(err, CY_ERR_BVH_STACK, 3);
-                return true;
-              }
-              stack[sp++] = acode[k];
-            }
-            else {
-              next = acode[k];
-              n_hit = 1;
-            }
+            tn[n_hit] = d;
+            cc[n_hit] = acode[k];
+            n_hit++;
           }
         }
       }
@@ -1056,23 +1052,35 @@ CY_FN bool bvhw_shadow_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits,
             const float cmn = max4(0.0f, cmin(clox, chix), cmin(cloy, chiy), cmin(cloz, chiz));
             const float cmx = min4(tmax, cmax(clox, chix), cmax(cloy, chiy), cmax(cloz, chiz));
             if ((cmx >= cmn) && (amt[j] & 0x0FFFFFFFu & visibility)) {
-              if (n_hit) {
-                if (sp == CY_SHADOW_WIDE_STACK) {
-                  cy_set_error(err, CY_ERR_BVH_STACK, 3);
-                  return true;
-                }
-                stack[sp++] = ach[j];
-              }
-              else {
-                next = ach[j];
-                n_hit = 1;
-              }
+              tn[n_hit] = cmn;
+              cc[n_hit] = ach[j];
+              n_hit++;
             }
           }
         }
       }
-      if (n_hit) {
-        code = next;
+      if (n_hit > 0) {
+        /* insertion sort by entry distance; push far to near */
+        for (int a = 1; a < n_hit; a++) {
+          const float t0 = tn[a];
+          const int c0 = cc[a];
+          int b = a - 1;
+          while (b >= 0 && tn[b] > t0) {
+            tn[b + 1] = tn[b];
+            cc[b + 1] = cc[b];
+            b--;
+          }
+          tn[b + 1] = t0;
+          cc[b + 1] = c0;
+        }
+        if (sp + n_hit - 1 > CY_SHADOW_WIDE_STACK) {
+          cy_set_error(err, CY_ERR_BVH_STACK, 3);
+          return true;
+        }
+        for (int a = n_hit - 1; a >= 1; a--) {
+          stack[sp++] = cc[a];
+        }
+        code = cc[0];
         continue;
       }
     }

@@ -198,7 +198,7 @@ CY_FN int cy_wrap_clamp(int x, int width)
 }
 CY_FN float cy_tex_frac(float x, int *ix)
 {
-  int i = (int)x - ((x < 0.0f) ? 1 : 0);
+  int i = cy_ftoi(x) - ((x < 0.0f) ? 1 : 0);
   *ix = i;
   return x - (float)i;
 }
@@ -429,8 +429,8 @@ CY_FN void svm_node_tex_image(const CyGlobals *kg,
   const int num_nodes = (int)node.y;
   if (num_nodes > 0) {
     const int next_offset = (*offset) + num_nodes;
-    const int tx = (int)tu;
-    const int ty = (int)tv;
+    const int tx = cy_ftoi(tu);
+    const int ty = cy_ftoi(tv);
     if (tx >= 0 && ty >= 0 && tx < 10) {
       const int tile = 1001 + 10 * ty + tx;
       for (int i = 0; i < num_nodes; i++) {

@@ -116,7 +116,7 @@ CY_FN float compatible_signf(float f)
 }
 CY_FN float safe_powf(float a, float b)
 {
-  if (a < 0.0f && b != (float)(int)b) {
+  if (a < 0.0f && b != (float)cy_ftoi(b)) {
     return 0.0f;
   }
   return cy_powf(a, b);
@@ -791,9 +791,9 @@ CY_FN float svm_checker(cfloat3 p)
   p.x = (p.x + 0.000001f) * 0.999999f;
   p.y = (p.y + 0.000001f) * 0.999999f;
   p.z = (p.z + 0.000001f) * 0.999999f;
-  const int xi = abs((int)floorf(p.x));
-  const int yi = abs((int)floorf(p.y));
-  const int zi = abs((int)floorf(p.z));
+  const int xi = abs(cy_ftoi(floorf(p.x)));
+  const int yi = abs(cy_ftoi(floorf(p.y)));
+  const int zi = abs(cy_ftoi(floorf(p.z)));
   return ((xi % 2 == yi % 2) == (zi % 2)) ? 1.0f : 0.0f;
 }
 CY_FN void svm_node_tex_checker(CySvmStack stack, hc_uint4 node, uint *err)
@@ -953,19 +953,19 @@ CY_FN void svm_node_convert(const CyGlobals *kg, CySvmStack stack, uint type, ui
       break;
     }
     case 1: /* FI */
-      svm_store(stack, to, int_as_float((int)svm_load(stack, from, err)), err);
+      svm_store(stack, to, int_as_float(cy_ftoi(svm_load(stack, from, err))), err);
       break;
     case 2: /* CF */
       svm_store(stack, to, dot3(svm_load3(stack, from, err), rgb_to_y), err);
       break;
     case 3: /* CI */
-      svm_store(stack, to, int_as_float((int)dot3(svm_load3(stack, from, err), rgb_to_y)), err);
+      svm_store(stack, to, int_as_float(cy_ftoi(dot3(svm_load3(stack, from, err), rgb_to_y))), err);
       break;
     case 4: /* VF */
       svm_store(stack, to, average3(svm_load3(stack, from, err)), err);
       break;
     case 5: /* VI */
-      svm_store(stack, to, int_as_float((int)average3(svm_load3(stack, from, err))), err);
+      svm_store(stack, to, int_as_float(cy_ftoi(average3(svm_load3(stack, from, err)))), err);
       break;
     case 6: /* IF */
       svm_store(stack, to, (float)as_int(svm_load(stack, from, err)), err);

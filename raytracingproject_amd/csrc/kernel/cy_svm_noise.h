@@ -209,7 +209,7 @@ CY_FN float negate_if(float val, int condition)
 /* scalar branch, 1D */
 CY_NOINLINE float perlin_1d(float x)
 {
-  const int X = (int)x - ((x < 0.0f) ? 1 : 0); /* quick_floor_to_int */
+  const int X = cy_ftoi(x) - ((x < 0.0f) ? 1 : 0); /* quick_floor_to_int */
   const float fx = x - (float)X;
   const float u = fx * fx * fx * (fx * (fx * 6.0f - 15.0f) + 10.0f);
   const int h0 = (int)hash_uint((uint)X) & 15;
@@ -222,7 +222,7 @@ CY_NOINLINE float perlin_1d(float x)
 /* SSE2 branch helpers: ssef floorfrac (truncate + (x < 0 ? -1 : 0)), fade and mix */
 CY_FN float sse_floorfrac(float x, int *i)
 {
-  *i = (int)x + ((x < 0.0f) ? -1 : 0);
+  *i = cy_ftoi(x) + ((x < 0.0f) ? -1 : 0);
   return x - (float)(*i);
 }
 CY_FN float sse_fade(float t)
@@ -655,12 +655,12 @@ CY_NOINLINE void svm_brick(cfloat3 p, float mortar_size, float mortar_smooth, fl
                      int squash_frequency, float *tint_out, float *mortar_out)
 {
   float offset = 0.0f;
-  const int rownum = (int)floorf(p.y / row_height);
+  const int rownum = cy_ftoi(floorf(p.y / row_height));
   if (offset_frequency && squash_frequency) {
     brick_width *= (rownum % squash_frequency) ? 1.0f : squash_amount;
     offset = (rownum % offset_frequency) ? 0.0f : (brick_width * offset_amount);
   }
-  const int bricknum = (int)floorf((p.x + offset) / brick_width);
+  const int bricknum = cy_ftoi(floorf((p.x + offset) / brick_width));
   const float x = (p.x + offset) - brick_width * bricknum;
   const float y = p.y - row_height * rownum;
   const float tint = saturate((brick_noise((uint)((rownum << 16) + (bricknum & 0xFFFF))) + bias));
