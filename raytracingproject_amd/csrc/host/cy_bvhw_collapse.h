@@ -35,13 +35,15 @@
  * node as oriented boxes (bvh2.cpp:133-163 pack_unaligned_node: visibility |
  * PATH_RAY_NODE_UNALIGNED, the two children, per child the transform taking
  * its box to the unit cube; 7 float4).  Each child's transform is absolute
- * (world space to its unit cube), so unaligned nodes widen like aligned ones:
- * up to four oriented children per *OBB node* (code CY_BVHW_OBB | index, 256
- * B), whose transforms are the reference's own, so the traversal applies the
- * reference's oriented slab test to them.  Wide nodes open only aligned BVH2
- * nodes and OBB nodes only unaligned ones; a child of the other kind stays a
- * child (with the box its parent stores for it) and starts a node of its own
- * kind below.  Curve leaves keep their primitive ranges (merging is off: a
+ * (world space to its unit cube), but a child's oriented box need not lie
+ * inside its parent's, so unaligned nodes are not widened: each is copied as
+ * an oriented two-child *OBB node* (code CY_BVHW_OBB | index) whose
+ * transforms are the reference's own, and the traversal applies the
+ * reference's oriented slab test to them on every unaligned node of a path.
+ * Wide nodes open only aligned BVH2 nodes (an aligned child's box lies inside
+ * its parent's, so skipping it culls nothing the reference keeps); an
+ * unaligned child stays a wide child (the box its aligned parent stores) and
+ * becomes an OBB node below it.  Curve leaves keep their primitive ranges (merging is off: a
  * merged leaf could mix types); the traversal reads the primitive type.
  */
 #ifndef CY_BVHW_COLLAPSE_H
@@ -307,87 +309,38 @@ struct Collapser {
     return true;
   }
 
-  /* Node slots an OBB node takes: 256 B (two 128-B slots at W = 4, one at W = 8). */
+  /* Node slots an OBB node takes (112 B: one slot at every W). */
   size_t obb_slots() const
   {
-    return width == 4 ? 2 : 1;
+    return 1;
   }
 
-  /* A child of an unaligned BVH2 node: its address, stored visibility and
-   * transform (3 float4 rows, world -> unit cube). */
-  struct ObbChild {
-    int addr;
-    uint32_t vis;
-    float t[12];
-  };
-
-  void obb_children(int addr, ObbChild c[2]) const
-  {
-    const float *n = nodes2 + 4 * (size_t)addr;
-    uint32_t w0[4];
-    memcpy(w0, n, 16);
-    for (int k = 0; k < 2; k++) {
-      c[k].addr = (int)w0[2 + k];
-      c[k].vis = w0[k];
-      memcpy(c[k].t, n + 4 + 12 * k, 48);
-    }
-  }
-
-  /* The unaligned BVH2 node at r.addr and, breadth-first, its unaligned inner
-   * children (largest oriented box first: smallest |det| of the transform),
-   * up to four oriented children, written as one OBB node at idx (16 float4):
-   * float4 0 the children's wide codes, float4 1 their stored visibility
-   * (PATH_RAY_NODE_UNALIGNED included; 0 = empty slot), float4 2 + 3k .. 4 + 3k
-   * child k's transform as stored (bvh_unaligned_node_intersect's operands). */
+  /* The unaligned BVH2 node at r.addr copied as an OBB node at idx: words 0..3
+   * the stored visibility of both children (PATH_RAY_NODE_UNALIGNED included)
+   * and their wide codes, words 4..27 the two children's transforms as stored
+   * (bvh_unaligned_node_intersect's operands).  Not widened: a child's
+   * oriented box need not lie inside its parent's, so the reference's test of
+   * every unaligned node on a path is kept (a ribbon hit outside an
+   * ancestor's box is culled there; skipping that test found such hits --
+   * measured on the JNK crop: 9 film values off at 1024 spp). */
   bool emit_obb(size_t idx, const Ref &r, std::vector<std::pair<size_t, Ref>> *pending)
   {
+    if ((size_t)r.addr + 7 > n_nodes2) {
+      error = "unaligned node past __bvh_nodes";
+      return false;
+    }
     if (idx >= OBB_CODE) {
       error = "wide node index beyond the OBB code range";
       return false;
     }
-    auto valid = [&](int a) {
-      if ((size_t)a + 7 > n_nodes2) {
-        error = "unaligned node past __bvh_nodes";
-        return false;
-      }
-      return true;
-    };
-    if (!valid(r.addr)) {
-      return false;
-    }
-    ObbChild ch[4];
-    obb_children(r.addr, ch);
-    int n = 2;
-    while (n < 4) {
-      int best = -1;
-      double best_det = 0.0;
-      for (int i = 0; i < n; i++) {
-        if (ch[i].addr < 0 || (ch[i].vis & 0x0FFFFFFFu & ~NODE_UNALIGNED) == 0u || !unaligned(ch[i].addr)) {
-          continue;
-        }
-        const float *t = ch[i].t;
-        const double det = std::fabs((double)t[0] * ((double)t[5] * t[10] - (double)t[6] * t[9]) -
-                                     (double)t[1] * ((double)t[4] * t[10] - (double)t[6] * t[8]) +
-                                     (double)t[2] * ((double)t[4] * t[9] - (double)t[5] * t[8]));
-        if (best < 0 || det < best_det) {
-          best = i;
-          best_det = det;
-        }
-      }
-      if (best < 0) {
-        break;
-      }
-      if (!valid(ch[best].addr)) {
-        return false;
-      }
-      ObbChild two[2];
-      obb_children(ch[best].addr, two);
-      ch[best] = two[0];
-      ch[n++] = two[1];
-    }
-    std::vector<uint32_t> w(obb_slots() * words(), 0u);
-    for (int k = 0; k < n; k++) {
-      const int a = ch[k].addr;
+    const float *n = nodes2 + 4 * (size_t)r.addr;
+    uint32_t w0[4];
+    memcpy(w0, n, 16);
+    std::vector<uint32_t> w(words(), 0u);
+    w[0] = w0[0];
+    w[1] = w0[1];
+    for (int k = 0; k < 2; k++) {
+      const int a = (int)w0[2 + k];
       if (a < 0) {
         int start, count;
         if (!leaf_range(a, &start, &count)) {
@@ -397,24 +350,23 @@ struct Collapser {
           error = "primitive index beyond the 2^27 leaf-code range";
           return false;
         }
-        w[k] = ~(((uint32_t)start << 4) | (uint32_t)count);
+        w[2 + k] = ~(((uint32_t)start << 4) | (uint32_t)count);
       }
       else {
         const size_t child = alloc_node(a);
-        w[k] = (uint32_t)child | (unaligned(a) ? OBB_CODE : 0u);
+        w[2 + k] = (uint32_t)child | (unaligned(a) ? OBB_CODE : 0u);
         Ref c;
         c.addr = a;
-        c.vis = ch[k].vis;
+        c.vis = w0[k];
         for (int x = 0; x < 3; x++) {
           c.lo[x] = -FLT_MAX;
           c.hi[x] = FLT_MAX;
         }
         pending->push_back(std::make_pair(child, c));
       }
-      w[4 + k] = ch[k].vis;
-      memcpy(&w[8 + 12 * k], ch[k].t, 48);
     }
-    memcpy(&out[idx * words()], w.data(), w.size() * 4);
+    memcpy(&w[4], n + 4, 24 * 4);
+    memcpy(&out[idx * words()], w.data(), words() * 4);
     n_obb++;
     return true;
   }

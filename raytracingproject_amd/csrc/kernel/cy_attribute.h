@@ -343,6 +343,9 @@ typedef struct CyAttrIn {
   float bump_du, bump_dv;
   int bump;
 #endif
+#ifdef CY_DBG_X
+  bool dbg = false;
+#endif
 } CyAttrIn;
 
 /* primitive_surface_attribute_float / float2 / float3 (geom_primitive.h:57-241):
@@ -720,6 +723,12 @@ CY_FN void svm_node_set_bump(const CyGlobals *kg, const CyAttrIn &in, CySvmStack
     normal_out = attr_object_normal_transform(kg, in.object, normal_out);
   }
   normal_out = ensure_valid_reflection(in.Ng, in.I, normal_out);
+  CY_DBG3(&in, "bump h", mk3(h_c, h_x, h_y));
+  CY_DBG3(&in, "bump dPdx", dPdx);
+  CY_DBG3(&in, "bump dPdy", dPdy);
+  CY_DBG3(&in, "bump N in", normal_in);
+  CY_DBG3(&in, "bump det str scale", mk3(det, strength, scale));
+  CY_DBG3(&in, "bump N out", normal_out);
   svm_store3(stack, node.w, normal_out, err);
 }
 #endif

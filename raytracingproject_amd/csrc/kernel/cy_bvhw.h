@@ -312,16 +312,15 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
     if constexpr (HAIR != 0) {
       if (code >= 0 && (code & (int)CY_BVHW_OBB)) {
         /* oriented-box node (cy_bvhw_collapse.h emit_obb): the reference's
-         * unaligned-node test (bvh_nodes.h:79-135) on up to four children's
-         * own transforms, hit children sorted and pushed as in a wide node */
+         * unaligned two-child test (bvh_nodes.h:79-135) on its own transforms */
         n_nodes++;
         const int idx = code & ~(int)CY_BVHW_OBB;
-        hc_float4 nd[14];
+        hc_float4 nd[7];
 #if defined(__HIP_DEVICE_COMPILE__) && CY_LDS_TOP > 0 && !CY_LDS_TOP_SOA
-        if (idx + (W == 4 ? 2 : 1) <= n_top) {
+        if (idx < n_top) {
           CY_LDS const hc_float4 *lp = top_nodes + (size_t)idx * (8 * Q);
 #  pragma unroll
-          for (int k = 0; k < 14; k++) {
+          for (int k = 0; k < 7; k++) {
             nd[k] = lp[k];
           }
         }
@@ -330,59 +329,32 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         {
           const hc_float4 *np = nodes + (size_t)idx * (8 * Q);
 #pragma unroll
-          for (int k = 0; k < 14; k++) {
+          for (int k = 0; k < 7; k++) {
             nd[k] = np[k];
           }
         }
-        const hc_uint4 hc = as_uint4(nd[0]), hv = as_uint4(nd[1]);
-        const uint acode[4] = {hc.x, hc.y, hc.z, hc.w}, avis[4] = {hv.x, hv.y, hv.z, hv.w};
+        const hc_uint4 h = as_uint4(nd[0]);
         const float t = CY_T_BOX;
-        float tn[4];
-        int cc[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          float d;
-          const bool hit = (avis[k] & visibility) && bvh_obb_intersect(nd[2 + 3 * k], nd[3 + 3 * k], nd[4 + 3 * k], P,
-                                                                         dir, t, &d);
-          cc[k] = (int)acode[k];
-          tn[k] = hit ? d : CY_INF;
-        }
-        bvhw_sort<4>(tn, cc);
-        if (tn[0] == CY_INF) {
-          goto pop;
-        }
-        {
-          int npush = 0;
-#pragma unroll
-          for (int k = 1; k < 4; k++) {
-            npush += tn[k] != CY_INF ? 1 : 0;
+        float d0, d1;
+        const bool hit0 = (h.x & visibility) && bvh_obb_intersect(nd[1], nd[2], nd[3], P, dir, t, &d0);
+        const bool hit1 = (h.y & visibility) && bvh_obb_intersect(nd[4], nd[5], nd[6], P, dir, t, &d1);
+        if (hit0 && hit1) {
+          /* nearer child next, the other pushed (bvh_traversal.h:104-125) */
+          const bool first1 = d1 < d0;
+          if (!CY_STACK_PUSH(first1 ? (int)h.z : (int)h.w, first1 ? d0 : d1)) {
+            cy_set_error(err, CY_ERR_BVH_STACK, W);
+            return found_hit;
           }
-          while (n_ring + npush > CY_LDS_STACKW) {
-            if (n_over == CY_OVER_STACK) {
-              cy_set_error(err, CY_ERR_BVH_STACK, W);
-              return found_hit;
-            }
-            const CyStackEntry old = ring[((top - n_ring) & (CY_LDS_STACKW - 1)) * CY_RING_STRIDE];
-            over_node[n_over] = old.node;
-            over_t[n_over] = old.t;
-            n_over++;
-            n_ring--;
-          }
-#pragma unroll
-          for (int k = 3; k >= 1; k--) {
-            if (tn[k] != CY_INF) {
-              CyStackEntry e_;
-              e_.node = cc[k];
-              e_.t = tn[k];
-              ring[top * CY_RING_STRIDE] = e_;
-              top = (top + 1) & (CY_LDS_STACKW - 1);
-            }
-          }
-          n_ring += npush;
+          code = first1 ? (int)h.w : (int)h.z;
+          code_t = first1 ? d1 : d0;
+          continue;
         }
-        code = cc[0];
-        code_t = tn[0];
-        continue;
+        if (hit0 || hit1) {
+          code = hit0 ? (int)h.z : (int)h.w;
+          code_t = hit0 ? d0 : d1;
+          continue;
+        }
+        goto pop;
       }
     }
     if (cur && budget > 0) {

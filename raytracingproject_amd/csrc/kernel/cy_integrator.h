@@ -2021,6 +2021,9 @@ CY_FN bool shade_path(const CyGlobals *kg,
 #else
     shader_setup_from_ray(kg, &sd, &isect, &ray);
 #endif
+#ifdef CY_DBG_X
+    sd.dbg = state.dbg;
+#endif
     CY_DBG3(&state, "sd.P", sd.P);
     CY_DBG3(&state, "sd.N", sd.N);
     CY_DBG3(&state, "sd.Ng", sd.Ng);

@@ -1017,18 +1017,18 @@ CY_FN bool bvhw_shadow_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits,
       int cc[8];
       int n_hit = 0;
       if (obb) {
-        /* oriented-box node (cy_bvhw_collapse.h emit_obb): up to four children */
-        const hc_float4 hc = np[0], hv = np[1];
-        const int acode[4] = {as_int(hc.x), as_int(hc.y), as_int(hc.z), as_int(hc.w)};
-        const uint avis[4] = {as_uint(hv.x), as_uint(hv.y), as_uint(hv.z), as_uint(hv.w)};
-        for (int k = 0; k < 4; k++) {
-          float d;
-          if ((avis[k] & visibility) && bvh_obb_intersect(np[2 + 3 * k], np[3 + 3 * k], np[4 + 3 * k], P, dir, tmax,
-                                                          &d)) {
-            tn[n_hit] = d;
-            cc[n_hit] = acode[k];
-            n_hit++;
-          }
+        /* oriented-box node (cy_bvhw_collapse.h emit_obb): two children */
+        const hc_float4 h = np[0];
+        float d;
+        if ((as_uint(h.x) & visibility) && bvh_obb_intersect(np[1], np[2], np[3], P, dir, tmax, &d)) {
+          tn[n_hit] = d;
+          cc[n_hit] = as_int(h.z);
+          n_hit++;
+        }
+        if ((as_uint(h.y) & visibility) && bvh_obb_intersect(np[4], np[5], np[6], P, dir, tmax, &d)) {
+          tn[n_hit] = d;
+          cc[n_hit] = as_int(h.w);
+          n_hit++;
         }
       }
       else {
@@ -2819,8 +2819,10 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
           if (blend != 0.5f) {
             blend = cclamp(blend, 0.0f, 1.0f - 1e-5f);
             blend = (blend < 0.5f) ? 2.0f * blend : 0.5f / (1.0f - blend);
+            CY_DBG3(sd, "lw dot blend", mk3(f, blend, 0.0f));
             f = cy_powf(f, blend); /* glibc powf, restated (cy_math.h) */
           }
+          CY_DBG3(sd, "lw pow N", mk3(f, normal_in.x, normal_in.z));
           f = 1.0f - f;
         }
         svm_store(stack, out_offset, f, err);
@@ -2994,6 +2996,9 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
           ain.dPdx = sd->dP.dx;
           ain.dPdy = sd->dP.dy;
           ain.bump = bump;
+#ifdef CY_DBG_X
+          ain.dbg = sd->dbg;
+#endif
           ain.bump_du = (bump == 2) ? sd->du.dy : sd->du.dx;
           ain.bump_dv = (bump == 2) ? sd->dv.dy : sd->dv.dx;
 #endif

@@ -791,10 +791,13 @@ CY_FN float svm_checker(cfloat3 p)
   p.x = (p.x + 0.000001f) * 0.999999f;
   p.y = (p.y + 0.000001f) * 0.999999f;
   p.z = (p.z + 0.000001f) * 0.999999f;
-  const int xi = abs(cy_ftoi(floorf(p.x)));
-  const int yi = abs(cy_ftoi(floorf(p.y)));
-  const int zi = abs(cy_ftoi(floorf(p.z)));
-  return ((xi % 2 == yi % 2) == (zi % 2)) ? 1.0f : 0.0f;
+  /* abs(xi) % 2 as the parity bit xi & 1: the same for every int, and defined
+   * for INT_MIN (the x86 conversion of an out-of-range coordinate), where
+   * abs() is undefined and the device compiler may fold it to anything */
+  const int xi = cy_ftoi(floorf(p.x)) & 1;
+  const int yi = cy_ftoi(floorf(p.y)) & 1;
+  const int zi = cy_ftoi(floorf(p.z)) & 1;
+  return ((xi == yi) == zi) ? 1.0f : 0.0f;
 }
 CY_FN void svm_node_tex_checker(CySvmStack stack, hc_uint4 node, uint *err)
 {

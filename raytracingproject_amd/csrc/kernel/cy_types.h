@@ -368,6 +368,9 @@ typedef struct CySD {
   cfloat3 svm_closure_weight;
   cfloat3 closure_emission_background;
   cfloat3 closure_transparent_extinction;
+#ifdef CY_DBG_X
+  bool dbg = false; /* debugging builds: the traced path's shading point */
+#endif
   /* working memory of the shade stage (CyShadeMem): CY_MAX_CLOSURE closures
    * and the SVM stack, element i at svm_stack[i * svm_stride] */
   CyClosure *closure;

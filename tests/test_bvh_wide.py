@@ -13,8 +13,8 @@ flags such rays and they are re-traced in the reference's order, so closest
 hits and renders are bit-identical to the reference.
 
 Ribbon hair scenes use the wide layout too: the BVH2's unaligned nodes are
-widened into oriented four-child nodes (the reference's test on its own
-transforms), and a ribbon the ray crosses in two subdivision steps (whose
+kept as oriented two-child nodes (the reference's test on its own
+transforms, on every unaligned node of a path), and a ribbon the ray crosses in two subdivision steps (whose
 result depends on the bound it is tested with) is re-traced in the
 reference's order like a near-tie.  Thick
 curves keep the BVH2 (cy_bvhw.h, hipcycles.hip pick_width).
@@ -68,9 +68,8 @@ def _walk(es, roots):
             continue
         w = words[idx]
         if obb:
-            # OBB node: four codes, four stored visibilities (0 = empty slot)
-            w = es.wide[idx * 8 * W: idx * 8 * W + 64]
-            kids = [(int(np.int32(np.uint32(w[k]))), None, None, None) for k in range(4) if w[4 + k] != 0]
+            # OBB node: two stored visibilities, two codes, two transforms
+            kids = [(int(np.int32(np.uint32(w[2 + k]))), None, None, None) for k in range(2)]
         else:
             f = w.view(np.float32).reshape(8, W)
             m = w.reshape(8, W)
@@ -94,9 +93,7 @@ def test_collapse_structure(case):
     # every node of the array is reached, each non-root node from exactly one
     # parent slot
     n = len(es.wide) // (8 * es.width)
-    # (an OBB node takes 256 B: two slots at W = 4)
-    second = {i + 1 for i, (obb, _) in nodes.items() if obb and es.width == 4}
-    assert set(nodes) | second == set(range(n)) and not set(nodes) & second
+    assert set(nodes) == set(range(n))
     refs = np.zeros(n, dtype=np.int64)
     for obb, kids in nodes.values():
         for code, *_ in kids:

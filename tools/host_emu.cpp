@@ -456,3 +456,30 @@ extern "C" int emu_background(const void *data, int n_arrays, const char **names
   }
   return (int)err;
 }
+
+/* Debug aid: one curve primitive's ribbon test against a ray (P, D, bound):
+ * out = (hit, t, u, v) of the reference's form, then (steps hit, first t, min t)
+ * of the scanning form. */
+extern "C" void emu_ribbon_test(const void *data, int n_arrays, const char **names, const void **ptrs, int prim,
+                                const float *ray, float tfar, float *out)
+{
+  CyGlobals kg;
+  emu_bind(&kg, data, n_arrays, names, ptrs, nullptr);
+  const cfloat3 P = mk3(ray[0], ray[1], ray[2]);
+  const cfloat3 dir = bvh_clamp_direction(mk3(ray[3], ray[4], ray[5]));
+  const uint type = kg.__prim_type[prim];
+  cy_c4 curve[4];
+  curve_segment_keys(&kg, (int)kg.__prim_index[prim], (int)CY_PRIMITIVE_UNPACK_SEGMENT(type), curve);
+  cy_c4 c2[4] = {curve[0], curve[1], curve[2], curve[3]};
+  float t, u, v, tmin;
+  const int hit = ribbon_intersect_steps<false>(P, dir, kg.data->bvh.curve_subdivisions, curve, tfar, &t, &u, &v, &tmin);
+  out[0] = (float)hit;
+  out[1] = hit ? t : -1.0f;
+  out[2] = hit ? u : -1.0f;
+  out[3] = hit ? v : -1.0f;
+  float t2 = -1.0f, u2, v2, tmin2 = -1.0f;
+  const int steps = ribbon_intersect_steps<true>(P, dir, kg.data->bvh.curve_subdivisions, c2, CY_FLT_MAX, &t2, &u2, &v2, &tmin2);
+  out[4] = (float)steps;
+  out[5] = t2;
+  out[6] = tmin2;
+}
