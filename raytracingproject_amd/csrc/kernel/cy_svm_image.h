@@ -198,7 +198,7 @@ CY_FN int cy_wrap_clamp(int x, int width)
 }
 CY_FN float cy_tex_frac(float x, int *ix)
 {
-  int i = cy_ftoi(x) - ((x < 0.0f) ? 1 : 0);
+  int i = (int)((uint)cy_ftoi(x) - ((x < 0.0f) ? 1u : 0u)); /* wrapping, as x86 */
   *ix = i;
   return x - (float)i;
 }

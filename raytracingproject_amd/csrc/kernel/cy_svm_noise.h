@@ -209,11 +209,11 @@ CY_FN float negate_if(float val, int condition)
 /* scalar branch, 1D */
 CY_NOINLINE float perlin_1d(float x)
 {
-  const int X = cy_ftoi(x) - ((x < 0.0f) ? 1 : 0); /* quick_floor_to_int */
+  const int X = (int)((uint)cy_ftoi(x) - ((x < 0.0f) ? 1u : 0u)); /* quick_floor_to_int (wrapping, as x86) */
   const float fx = x - (float)X;
   const float u = fx * fx * fx * (fx * (fx * 6.0f - 15.0f) + 10.0f);
   const int h0 = (int)hash_uint((uint)X) & 15;
-  const int h1 = (int)hash_uint((uint)(X + 1)) & 15;
+  const int h1 = (int)hash_uint(((uint)X + (uint)1)) & 15;
   const float a = negate_if((float)(1 + (h0 & 7)), h0 & 8) * fx;
   const float b = negate_if((float)(1 + (h1 & 7)), h1 & 8) * (fx - 1.0f);
   return a + u * (b - a);
@@ -222,7 +222,7 @@ CY_NOINLINE float perlin_1d(float x)
 /* SSE2 branch helpers: ssef floorfrac (truncate + (x < 0 ? -1 : 0)), fade and mix */
 CY_FN float sse_floorfrac(float x, int *i)
 {
-  *i = cy_ftoi(x) + ((x < 0.0f) ? -1 : 0);
+  *i = (int)((uint)cy_ftoi(x) - ((x < 0.0f) ? 1u : 0u)); /* wrapping, as x86 */
   return x - (float)(*i);
 }
 CY_FN float sse_fade(float t)
@@ -267,9 +267,9 @@ CY_NOINLINE float perlin_2d(float x, float y)
   const float u = sse_fade(fx), v = sse_fade(fy);
   /* lanes (X, Y), (X, Y+1), (X+1, Y), (X+1, Y+1) */
   const float g0 = grad2(hash_uint2((uint)X, (uint)Y), fx, fy);
-  const float g1 = grad2(hash_uint2((uint)X, (uint)(Y + 1)), fx, fy - 1.0f);
-  const float g2 = grad2(hash_uint2((uint)(X + 1), (uint)Y), fx - 1.0f, fy);
-  const float g3 = grad2(hash_uint2((uint)(X + 1), (uint)(Y + 1)), fx - 1.0f, fy - 1.0f);
+  const float g1 = grad2(hash_uint2((uint)X, ((uint)Y + (uint)1)), fx, fy - 1.0f);
+  const float g2 = grad2(hash_uint2(((uint)X + (uint)1), (uint)Y), fx - 1.0f, fy);
+  const float g3 = grad2(hash_uint2(((uint)X + (uint)1), ((uint)Y + (uint)1)), fx - 1.0f, fy - 1.0f);
   return sse_mix(sse_mix(g0, g2, u), sse_mix(g1, g3, u), v);
 }
 
@@ -292,8 +292,8 @@ CY_NOINLINE float perlin_3d(float x, float y, float z)
   for (int k = 0; k < 4; k++) {
     const int dy = k >> 1, dz = k & 1;
     const float gy = dy ? fy - 1.0f : fy, gz = dz ? fz - 1.0f : fz;
-    g1[k] = grad3(hash_uint3((uint)X, (uint)(Y + dy), (uint)(Z + dz)), fx, gy, gz);
-    g2[k] = grad3(hash_uint3((uint)(X + 1), (uint)(Y + dy), (uint)(Z + dz)), fx - 1.0f, gy, gz);
+    g1[k] = grad3(hash_uint3((uint)X, ((uint)Y + (uint)dy), ((uint)Z + (uint)dz)), fx, gy, gz);
+    g2[k] = grad3(hash_uint3(((uint)X + (uint)1), ((uint)Y + (uint)dy), ((uint)Z + (uint)dz)), fx - 1.0f, gy, gz);
   }
   return sse_tri_mix(g1, g2, u, v, w);
 }
@@ -310,11 +310,11 @@ CY_NOINLINE float perlin_4d(float x, float y, float z, float w)
   for (int k = 0; k < 4; k++) {
     const int dy = k >> 1, dz = k & 1;
     const float gy = dy ? fy - 1.0f : fy, gz = dz ? fz - 1.0f : fz;
-    const uint yy = (uint)(Y + dy), zz = (uint)(Z + dz);
+    const uint yy = ((uint)Y + (uint)dy), zz = ((uint)Z + (uint)dz);
     g1[k] = grad4(hash_uint4((uint)X, yy, zz, (uint)W), fx, gy, gz, fw);
-    g2[k] = grad4(hash_uint4((uint)(X + 1), yy, zz, (uint)W), fx - 1.0f, gy, gz, fw);
-    g3[k] = grad4(hash_uint4((uint)X, yy, zz, (uint)(W + 1)), fx, gy, gz, fw - 1.0f);
-    g4[k] = grad4(hash_uint4((uint)(X + 1), yy, zz, (uint)(W + 1)), fx - 1.0f, gy, gz, fw - 1.0f);
+    g2[k] = grad4(hash_uint4(((uint)X + (uint)1), yy, zz, (uint)W), fx - 1.0f, gy, gz, fw);
+    g3[k] = grad4(hash_uint4((uint)X, yy, zz, ((uint)W + (uint)1)), fx, gy, gz, fw - 1.0f);
+    g4[k] = grad4(hash_uint4(((uint)X + (uint)1), yy, zz, ((uint)W + (uint)1)), fx - 1.0f, gy, gz, fw - 1.0f);
   }
   return sse_mix(sse_tri_mix(g1, g2, u, v, t), sse_tri_mix(g3, g4, u, v, t), s);
 }
@@ -663,7 +663,7 @@ CY_NOINLINE void svm_brick(cfloat3 p, float mortar_size, float mortar_smooth, fl
   const int bricknum = cy_ftoi(floorf((p.x + offset) / brick_width));
   const float x = (p.x + offset) - brick_width * bricknum;
   const float y = p.y - row_height * rownum;
-  const float tint = saturate((brick_noise((uint)((rownum << 16) + (bricknum & 0xFFFF))) + bias));
+  const float tint = saturate((brick_noise(((uint)rownum << 16) + (uint)(bricknum & 0xFFFF)) + bias));
   float min_dist = cy_min(cy_min(x, y), cy_min(brick_width - x, row_height - y));
   float mortar;
   if (min_dist >= mortar_size) {
