@@ -144,6 +144,12 @@ uint32_t hipcy_get_bvh_layout_mask(const hipcy_device *dev); /* BVH_LAYOUT_BVH2 
  * device's 4- or 8-wide BVH before the next path_trace/intersect; 2 traverses
  * the BVH2 exactly as bound (bit-identical visiting order to the reference). */
 int hipcy_set_bvh_width(hipcy_device *dev, int width);
+/* Scenes with curves: 0 (default) traverses the bound BVH2 at every width
+ * (measured faster on hair-heavy scenes: the JNK stand-in's crop 16.6 against
+ * 15.2 Msamples/s); 1 lets ribbon-only scenes use the W-wide layout too, with
+ * the BVH2's unaligned nodes kept as oriented two-child nodes (bit-exact to the
+ * reference like every width; thick curves keep the BVH2 either way). */
+int hipcy_set_curve_layout(hipcy_device *dev, int wide);
 /* Wide BVH only: BVH2 subtrees holding at most max_prims (0..15) primitives in
  * one contiguous range become a single leaf child (0 = keep BVH2 leaves). */
 int hipcy_set_bvh_leaf_merge(hipcy_device *dev, int max_prims);

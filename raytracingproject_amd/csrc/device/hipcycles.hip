@@ -1621,6 +1621,7 @@ struct hipcy_device {
   int shade_closures = 1;             /* closure array of the shading kernel (variant by size) */
   bool features_dirty = true;         /* KernelData or a bound array changed since load_kernels */
   int curve_shapes = 0;               /* curve primitive shapes in __prim_type: 1 ribbon, 2 thick, 3 both */
+  bool curve_wide = false;            /* hipcy_set_curve_layout */
   int tri_index_identity = 0;
   hipcy_stats stats;
   std::vector<hipEvent_t> events;
@@ -1659,11 +1660,13 @@ static int set_error(hipcy_device *dev, const std::string &msg)
 
 static int ensure_bvhw(hipcy_device *dev);
 
-/* The W-wide layout serves the scene: triangles, and ribbon curves (thick
- * curves keep the bound BVH2: pick_width) */
+/* The W-wide layout serves the scene: triangles, and ribbon curves when
+ * hipcy_set_curve_layout asked for it (thick curves keep the bound BVH2:
+ * pick_width) */
 static bool wide_layout(const hipcy_device *dev)
 {
-  return dev->bvh_width > 2 && (!dev->data_host.bvh.have_curves || dev->curve_shapes == 1);
+  return dev->bvh_width > 2 &&
+         (!dev->data_host.bvh.have_curves || (dev->curve_wide && dev->curve_shapes == 1));
 }
 
 static bool build_globals(hipcy_device *dev, CyGlobals *kg)
@@ -2278,6 +2281,18 @@ int hipcy_set_bvh_width(hipcy_device *dev, int width)
     dev->bvhw_dirty = true;
   }
   dev->bvh_width = width;
+  return 0;
+}
+
+int hipcy_set_curve_layout(hipcy_device *dev, int wide)
+{
+  if (wide != 0 && wide != 1) {
+    return set_error(dev, "set_curve_layout: 0 (BVH2) or 1 (wide layout for ribbon scenes)");
+  }
+  if ((wide != 0) != dev->curve_wide) {
+    dev->bvhw_dirty = true;
+  }
+  dev->curve_wide = wide != 0;
   return 0;
 }
 

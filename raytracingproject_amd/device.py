@@ -123,6 +123,11 @@ class HIPDevice:
         """4 (default) / 8: traverse the device-widened wide BVH; 2: the bound BVH2."""
         self._check(self.lib.hipcy_set_bvh_width(self.h, int(width)))
 
+    def set_curve_layout(self, wide: bool) -> None:
+        """Scenes with curves: False (default) traverse the bound BVH2; True
+        lets ribbon-only scenes use the wide layout (oriented-box nodes)."""
+        self._check(self.lib.hipcy_set_curve_layout(self.h, int(bool(wide))))
+
     def set_ray_sort(self, mode: int) -> None:
         """Bin the closest-hit queue by ray direction before every bounce
         iteration: 0 off, 3 octant, 5 octant x major axis; 8 sorts the shading

@@ -122,6 +122,7 @@ DEVICE_SYMBOLS = {
     "hipcy_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Stats)]),
     "hipcy_set_profiling": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_bvh_width": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hipcy_set_curve_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_ray_sort": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_traversal_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "hipcy_set_traversal_refill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),

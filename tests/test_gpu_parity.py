@@ -56,6 +56,9 @@ def case(request, device):
     assert str(g["digest"]) == scene_digest(ds), "scene generator drifted from the golden inputs"
     device.upload_scene(ds)
     device.set_bvh_width(width)
+    # ribbon scenes on the wide layout at W = 4 / 8 (hipcy_set_curve_layout;
+    # the device default, the BVH2, is the W = 2 traversal)
+    device.set_curve_layout(width > 2)
     device.bvh_width_under_test = width
     return name, ds, g
 
@@ -290,3 +293,20 @@ def test_traversal_budget_with_full_continuation_buffer(name, capacity, device, 
         monkeypatch.delenv("HIPCY_CONT_CAPACITY")
         device.render(samples=1)  # back to the default continuation buffers
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), (name, capacity)
+
+
+def test_curve_scene_default_layout_is_the_bvh2(device):
+    """Scenes with curves traverse the bound BVH2 unless hipcy_set_curve_layout
+    asks for the wide layout: at W = 4 the default render equals the reference
+    and the wide-layout render alike."""
+    ds = compile_case("hair_ribbon")
+    g = load_golden("hair_ribbon")
+    device.upload_scene(ds)
+    device.set_bvh_width(4)
+    device.set_curve_layout(False)
+    default = device.render()
+    device.set_curve_layout(True)
+    wide = device.render()
+    device.set_curve_layout(False)
+    assert_film_exact("hair_ribbon", default, g["buffer"], "default layout")
+    assert_film_exact("hair_ribbon", wide, g["buffer"], "wide layout")

@@ -55,6 +55,7 @@ def scale_case(request, device):
 def test_crop_matches_reference(scale_case, device, width):
     name, ds, g = scale_case
     device.set_bvh_width(width)
+    device.set_curve_layout(width > 2)  # JNK's ribbons on the wide layout at W = 4
     x, y, w, h = (int(v) for v in g["tile"])
     buf = device.render(tile=(x, y, w, h))
     ref = g["buffer"]
