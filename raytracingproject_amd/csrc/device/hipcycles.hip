@@ -27,9 +27,10 @@
 /* Minimum waves per SIMD the traversal kernels are register-allocated for
  * (amdgpu_waves_per_eu); with the LDS stack it sets their occupancy. */
 /* hair kernels (the ribbon and thick-curve intersectors) need more registers:
- * at the 96 of five waves they spill */
+ * at the 96 of five waves they spill; measured on the JNK crop (BVH2 hair):
+ * 4 waves (128 VGPRs) 18.6 Msamples/s, 3 waves 16.7 */
 #ifndef CY_TRAV_HAIR_WAVES
-#  define CY_TRAV_HAIR_WAVES 3
+#  define CY_TRAV_HAIR_WAVES 4
 #endif
 #define CY_TRAV_WAVES(hair) ((hair) != 0 ? CY_TRAV_HAIR_WAVES : CY_TRAV_MIN_WAVES)
 #ifndef CY_TRAV_MIN_WAVES
