@@ -274,18 +274,41 @@ class HIPCyclesDevice : public Device {
    * MultiDevice (device_multi.cpp:47-105 creates them all before any task) */
   static std::atomic<int> live_devices_;
 
-  /* The only device of the session holds as much as its slot pool keeps in
-   * flight (0: the device default, the whole pool plus as much in reserve), so
-   * a frame renders in as few wavefront iterations as a whole-frame pass.
-   * Devices sharing one TileManager queue each hold 2^25 pixel-samples (a
-   * 64x64 tile at 128 spp is 2^19), a small share of any frame they split:
-   * each takes tiles as fast as it finishes them. */
-  uint64_t stream_hold() const
+  /* How much of the session's tile queue one RENDER task may hold, in
+   * pixel-samples (0: the device default, its whole slot pool in flight plus as
+   * much in reserve).  The only device of the session takes the default, so a
+   * frame renders in as few wavefront iterations as a whole-frame pass.
+   * Devices sharing one TileManager queue (MultiDevice, device_multi.cpp:689-737)
+   * hold a fair part of the frame: the first tile's RenderBuffers tell the frame
+   * (BufferParams full_width x full_height at the tile's resolution divider,
+   * times the tile's sample count; buffers.h:38-50), and each of the
+   * live_devices_ devices holds CYCLES_HIPCY_HOLD_SHARE (default 1/2) of its
+   * 1/N of it: half the frame is dealt out by the first fills, the other half
+   * goes to whichever device runs low first, so devices that start late or
+   * draw expensive tiles still finish together.  Without RenderBuffers on the
+   * tile the hold is 2^25 pixel-samples (64 tiles of 64x64 at 128 spp). */
+  uint64_t stream_hold(const RenderTile *first) const
   {
     if (hold_) {
       return hold_;
     }
-    return live_devices_.load() > 1 ? (uint64_t)1 << 25 : 0;
+    const int live = live_devices_.load();
+    if (live <= 1) {
+      return 0;
+    }
+    if (first == nullptr || first->buffers == nullptr) {
+      return (uint64_t)1 << 25;
+    }
+    const BufferParams &p = first->buffers->params;
+    const uint64_t res = (uint64_t)std::max(first->resolution, 1);
+    const uint64_t frame = (uint64_t)std::max(p.full_width, p.width) * (uint64_t)std::max(p.full_height, p.height) /
+                           (res * res) * (uint64_t)std::max(first->num_samples, 1);
+    double share = 0.5;
+    if (const char *env = getenv("CYCLES_HIPCY_HOLD_SHARE")) {
+      share = std::min(std::max(atof(env), 0.05), 1.0);
+    }
+    const uint64_t tile = (uint64_t)first->w * first->h * (uint64_t)std::max(first->num_samples, 1);
+    return std::max<uint64_t>((uint64_t)(share * (double)frame / live), tile);
   }
 
   bool check(int rc)
@@ -308,32 +331,47 @@ class HIPCyclesDevice : public Device {
     HIPCyclesDevice *self;
     DeviceTask *task;
     std::deque<RenderTile> tiles; /* acquired, indexed by the feed tag */
+    bool have_first = false;      /* the tile render() acquired to size the hold */
+    RenderTile first;
   };
+
+  /* the next PATH_TRACE tile of the queue (others are released unrendered) */
+  static bool next_tile(Feed *f, RenderTile &tile)
+  {
+    if (f->have_first) {
+      f->have_first = false;
+      tile = f->first;
+      return true;
+    }
+    DeviceTask &task = *f->task;
+    while (task.acquire_tile(f->self, tile, task.tile_types)) {
+      if (tile.task == RenderTile::PATH_TRACE) {
+        return true;
+      }
+      task.release_tile(tile);
+    }
+    return false;
+  }
 
   static int feed_acquire(void *user, hipcy_work_tile *wt, uint64_t *tag)
   {
     Feed *f = (Feed *)user;
-    DeviceTask &task = *f->task;
     RenderTile tile;
-    while (task.acquire_tile(f->self, tile, task.tile_types)) {
-      if (tile.task != RenderTile::PATH_TRACE) {
-        task.release_tile(tile);
-        continue;
-      }
-      wt->x = tile.x;
-      wt->y = tile.y;
-      wt->w = tile.w;
-      wt->h = tile.h;
-      wt->start_sample = tile.start_sample;
-      wt->num_samples = tile.num_samples;
-      wt->offset = tile.offset;
-      wt->stride = tile.stride;
-      wt->buffer = (uint64_t)tile.buffer;
-      *tag = f->tiles.size();
-      f->tiles.push_back(tile);
-      return 1;
+    if (!next_tile(f, tile)) {
+      return 0;
     }
-    return 0;
+    wt->x = tile.x;
+    wt->y = tile.y;
+    wt->w = tile.w;
+    wt->h = tile.h;
+    wt->start_sample = tile.start_sample;
+    wt->num_samples = tile.num_samples;
+    wt->offset = tile.offset;
+    wt->stride = tile.stride;
+    wt->buffer = (uint64_t)tile.buffer;
+    *tag = f->tiles.size();
+    f->tiles.push_back(tile);
+    return 1;
   }
 
   /* every acquired tile comes back here once: finished, or (after a device
@@ -364,13 +402,24 @@ class HIPCyclesDevice : public Device {
     Feed f;
     f.self = this;
     f.task = &task;
+    /* the first tile sizes the hold; it is the first one the feed renders */
+    f.have_first = next_tile(&f, f.first);
+    if (!f.have_first) {
+      return;
+    }
+    f.have_first = true;
     hipcy_tile_feed feed;
     feed.user = &f;
     feed.acquire = feed_acquire;
     feed.release = feed_release;
     feed.cancelled = feed_cancelled;
-    feed.hold = stream_hold();
+    feed.hold = stream_hold(&f.first);
     check(hipcy_render_feed(dev_, &feed));
+    if (f.have_first) {
+      /* the feed failed before it took the first tile: hand it back unrendered */
+      f.have_first = false;
+      task.release_tile(f.first);
+    }
   }
 };
 

@@ -47,18 +47,21 @@
 #ifndef CY_LDS_STACK_TOP
 #  define CY_LDS_STACK_TOP 8
 #endif
-template<int W, bool INST> struct LdsStack {
+/* TOP: the kernel serves the wide BVH's top CY_LDS_TOP nodes (2 W float4
+ * each) from LDS (non-instanced scenes; k_intersect_closest and
+ * k_intersect_shadow, which fill them with lds_fill_top).  Other kernels
+ * reserve no LDS for them and traverse with n_top = 0. */
+template<int W, bool INST, bool TOP = false> struct LdsStack {
   CyStackEntry ring[CY_LDS_STACKW * CY_BLOCK];
   int top[(INST ? CY_LDS_STACK_TOP : 1) * CY_BLOCK];
-  /* the wide BVH's top CY_LDS_TOP nodes (2 W float4 each), non-instanced scenes */
-  hc_float4 top_nodes[(!INST && CY_LDS_TOP > 0) ? CY_LDS_TOP * 2 * W : 1];
+  hc_float4 top_nodes[(!INST && TOP && CY_LDS_TOP > 0) ? CY_LDS_TOP * 2 * W : 1];
 };
-template<bool INST> struct LdsStack<2, INST> {
+template<bool INST, bool TOP> struct LdsStack<2, INST, TOP> {
   int top[CY_LDS_STACK * CY_BLOCK];
 };
 
 /* This thread's ring column of the wide kernels' LDS stack (nullptr for BVH2). */
-template<int W, bool INST> __device__ __forceinline__ CY_LDS CyStackEntry *lds_ring_of(LdsStack<W, INST> *lds)
+template<int W, bool INST, bool TOP> __device__ __forceinline__ CY_LDS CyStackEntry *lds_ring_of(LdsStack<W, INST, TOP> *lds)
 {
   if constexpr (W > 2) {
     return (CY_LDS CyStackEntry *)(lds->ring + threadIdx.x);
@@ -71,10 +74,10 @@ template<int W, bool INST> __device__ __forceinline__ CY_LDS CyStackEntry *lds_r
 /* HAIR (scenes with curves): unaligned nodes and curve leaves of the shapes
  * HAIR selects (1 ribbons, 2 thick curves, 3 both).  Ribbon-only scenes also
  * traverse the wide BVH (W = 4 / 8, cy_bvhw.h); thick curves keep the BVH2. */
-template<int W, bool any_hit, bool INST = true, int HAIR = 0>
+template<int W, bool any_hit, bool INST = true, int HAIR = 0, bool TOP = false>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
-                                               uint *n_tris, LdsStack<W, INST> *lds, bool *tie = nullptr)
+                                               uint *n_tris, LdsStack<W, INST, TOP> *lds, bool *tie = nullptr)
 {
   const int t = threadIdx.x;
   if constexpr (W == 2) {
@@ -91,15 +94,16 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
   else {
     return bvhw_intersect<W, any_hit, HAIR>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
                                             (CY_LDS CyStackEntry *)(lds->ring + t), tie,
-                                            (CY_LDS const hc_float4 *)lds->top_nodes, kg->bvhw_top);
+                                            (CY_LDS const hc_float4 *)lds->top_nodes, TOP ? kg->bvhw_top : 0);
   }
 }
 
 /* Copy the wide BVH's top nodes into the workgroup's LDS (CY_LDS_TOP; every
  * thread of the block calls this before its traversal). */
-template<int W, bool INST> __device__ __forceinline__ void lds_fill_top(const CyGlobals *kg, LdsStack<W, INST> *lds)
+template<int W, bool INST, bool TOP>
+__device__ __forceinline__ void lds_fill_top(const CyGlobals *kg, LdsStack<W, INST, TOP> *lds)
 {
-  if constexpr (W > 2 && !INST && CY_LDS_TOP > 0) {
+  if constexpr (W > 2 && !INST && TOP && CY_LDS_TOP > 0) {
     const int n = kg->bvhw_top * 2 * W;
     const hc_float4 *src = (const hc_float4 *)kg->bvhw_nodes;
     for (int i = threadIdx.x; i < n; i += CY_BLOCK) {
@@ -389,8 +393,8 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_WAVES(HAIR)) k_intersect_clo
 {
   const int n_active = cam_n > 0 ? cam_n : (int)*counter;
   const int i = cy_queue_index(n_active);
-  __shared__ LdsStack<W, INST> lds_stack;
-  lds_fill_top<W, INST>(&kg, &lds_stack);
+  __shared__ LdsStack<W, INST, true> lds_stack;
+  lds_fill_top(&kg, &lds_stack);
   uint n_nodes = 0, n_leaves = 0, n_tris = 0, n_ties = 0;
   const bool active = i < n_active;
   if (active) {
@@ -829,8 +833,8 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_WAVES(HAIR)) k_intersect_sha
 {
   const int n_active = (int)*shadow_count;
   const int i = cy_queue_index(n_active);
-  __shared__ LdsStack<W, INST> lds_stack;
-  lds_fill_top<W, INST>(&kg, &lds_stack);
+  __shared__ LdsStack<W, INST, true> lds_stack;
+  lds_fill_top(&kg, &lds_stack);
   bool finished = false;
   int slot = 0;
   uint n_nodes = 0, n_leaves = 0, n_tris = 0;
@@ -1663,11 +1667,13 @@ static int ensure_bvhw(hipcy_device *dev);
 
 /* The W-wide layout serves the scene: triangles, and ribbon curves when
  * hipcy_set_curve_layout asked for it (thick curves keep the bound BVH2:
- * pick_width) */
+ * pick_width).  Instanced scenes with curves keep the BVH2 too: no golden case
+ * pins ribbons inside instances on the wide layout. */
 static bool wide_layout(const hipcy_device *dev)
 {
   return dev->bvh_width > 2 &&
-         (!dev->data_host.bvh.have_curves || (dev->curve_wide && dev->curve_shapes == 1));
+         (!dev->data_host.bvh.have_curves ||
+          (dev->curve_wide && dev->curve_shapes == 1 && !dev->have_instancing));
 }
 
 static bool build_globals(hipcy_device *dev, CyGlobals *kg)

@@ -94,7 +94,14 @@
  * comparison (hit = tmax >= tmin, the child sort, the stack's cull against the
  * current hit, the leaf-box entry check) or a copy into one, for which -0 and
  * +0 are equal, so the traversal decides exactly as the reference's arithmetic
- * does.  0 selects the reference's form (measurement switch). */
+ * does.  0 selects the reference's form (measurement switch).
+ * Exception: scene_intersect_valid, like the reference's (bvh/bvh.h), tests
+ * only P.x and D.x for finiteness, so a ray whose P.y, P.z, D.y or D.z is NaN
+ * or infinite is still traversed.  Its slab operands can be NaN, where
+ * fminf / fmaxf drop the NaN and the reference's ternaries keep it, so the wide
+ * traversal may open other boxes than the reference and the hit it reports is
+ * outside the bit-exactness claim.  Such a ray comes only from a path state
+ * that is already non-finite; no golden case produces one. */
 #ifndef CY_FAST_MINMAX
 #  define CY_FAST_MINMAX 1
 #endif

@@ -888,6 +888,11 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
     blocked = kg->have_curves ?
                   bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
                   bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+    if (blocked) {
+      /* the two queries record the same set of hits, so this does not happen;
+       * should it, the reference's own query decides, as in the first exit */
+      return true;
+    }
   }
   cfloat3 throughput = mk3(1.0f, 1.0f, 1.0f);
   const cfloat3 Pend = add3(ray.P, mul3f(ray.D, ray.t));

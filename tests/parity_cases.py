@@ -150,8 +150,10 @@ JOE_KUO_CASES = {"cornell_joe_kuo"}
 # path_trace); the host emulation renders single passes, so these are checked
 # on the GPU only (test_gpu_parity).
 HOST_LOOP_CASES = {"cornell_adaptive"}
-# Scenes with curves: the device traverses the bound BVH2 (unaligned nodes,
-# curve leaves) at every requested width; the wide layout holds triangles only.
+# Scenes with curves.  By default the device traverses the bound BVH2
+# (unaligned nodes, curve leaves) for them at every requested width; with
+# hipcy_set_curve_layout(1) ribbon-only, non-instanced scenes traverse the wide
+# layout (oriented two-child nodes, RIBBON_CASES in the GPU tests).
 CURVE_CASES = {"hair_ribbon", "hair_thick", "hair_principled", "hair_principled_thick", "hair_reflection_transmission",
                "hair_info_ribbon"}
 EMU_CASES = [n for n in CASES if n not in HOST_LOOP_CASES]

@@ -276,6 +276,12 @@ int main(int argc, char **argv)
   /* the TileManager's role: tiles in row order, each rendered with all
    * samples, handed out from one queue to whichever device asks */
   std::vector<RenderTile> tiles;
+  /* Session::acquire_tile hands out tiles with the RenderBuffers whose
+   * BufferParams describe the frame (full_width x full_height); the plugin sizes
+   * its share of the queue from them */
+  RenderBuffers *frame_buffers = new RenderBuffers(subs[0].dev);
+  frame_buffers->params.width = frame_buffers->params.full_width = W;
+  frame_buffers->params.height = frame_buffers->params.full_height = H;
   for (int y = 0; y < H; y += T) {
     for (int x = 0; x < W; x += T) {
       RenderTile t;
@@ -291,6 +297,7 @@ int main(int argc, char **argv)
       t.offset = 0;
       t.stride = W;
       t.tile_index = (int)tiles.size();
+      t.buffers = frame_buffers;
       tiles.push_back(t);
     }
   }
@@ -389,6 +396,7 @@ int main(int argc, char **argv)
   fwrite(film.data(), sizeof(float), film.size(), out);
   fclose(out);
 
+  delete frame_buffers;
   for (SubDevice &sd : subs) {
     for (auto *v : sd.arrays) {
       v->free();
