@@ -60,6 +60,8 @@ def parse(argv=None):
                    help="iteration budget of the wide traversal kernels (continuation launches); 0 0 disables")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
     p.add_argument("--slots", type=int, default=0, help="path slots in flight (0: device default)")
+    p.add_argument("--tail", type=int, default=-1,
+                   help="fused tail threshold in live paths per lane (hipcy_set_tail; -1: device default, 0: off)")
     p.add_argument("--tile", type=int, default=64,
                    help="tile-mode leg: render one extra frame as TxT RenderTiles through the plugin path "
                         "(0 disables)")
@@ -152,6 +154,8 @@ def main():
     dev.set_traversal_budget(*args.trav_budget)
     dev.set_traversal_refill(*args.refill)
     dev.set_slots(args.slots)
+    if args.tail >= 0:
+        dev.set_tail(args.tail)
     t0 = time.time()
     dev.upload_scene(ds)
     dev.load_kernels()  # validates the scene and widens the BVH (scene preparation)
@@ -626,6 +630,8 @@ def other_config(spec, device_index, args):
         dev = HIPDevice(device_index)
         dev.set_bvh_width(args.bvh_width)
         dev.set_ray_sort(args.ray_sort)
+        if args.tail >= 0:
+            dev.set_tail(args.tail)
         dev.upload_scene(ds)
         dev.load_kernels()
         buf = torch.zeros((h, w, PS), dtype=torch.float32, device=torch.device("cuda", device_index))

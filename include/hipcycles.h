@@ -133,6 +133,12 @@ int hipcy_bind_global(hipcy_device *dev, const char *name, uint64_t device_point
  * replaces it; hipcy_tex_free releases it. */
 int hipcy_tex_alloc(hipcy_device *dev, int slot, int data_type, int interpolation, int extension, int width,
                     int height, const void *pixels, size_t bytes);
+/* 3D textures (TextureInfo depth > 1; the Point Density node's voxel grid,
+ * kernel_tex_image_interp_3d): texels x-fastest, then y, then z;
+ * transform_3d (12 floats, rows x, y, z) or NULL sets
+ * TextureInfo::use_transform_3d / transform_3d (ImageManager, image.cpp). */
+int hipcy_tex_alloc_3d(hipcy_device *dev, int slot, int data_type, int interpolation, int extension, int width,
+                       int height, int depth, const float *transform_3d, const void *pixels, size_t bytes);
 int hipcy_tex_free(hipcy_device *dev, int slot);
 
 /* Validate that the scene uploaded so far only uses features the HIP kernels
@@ -181,6 +187,12 @@ int hipcy_set_traversal_budget(hipcy_device *dev, int first, int second);
  * and, once `min_idle` lanes of a wave have finished their rays, take the next
  * rays of the queue.  Results are bit-identical; rounds 0 disables. */
 int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle);
+/* Fused tail: once every work item of a lane is claimed and at most `paths` of
+ * its paths are live (default 2^17), one launch runs each of them to its end
+ * (closest hit, shading and shadow per bounce in one kernel) instead of one
+ * closest -> shade -> shadow iteration per bounce.  Plain shading variants,
+ * triangle scenes with opaque shadows; results are bit-identical; 0 disables. */
+int hipcy_set_tail(hipcy_device *dev, uint64_t paths);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

@@ -124,13 +124,13 @@ class HIPCyclesDevice : public Device {
    * keeps TextureInfo[slot] in its own __texture_info table */
   void tex_alloc(device_texture &mem)
   {
-    if (mem.data_depth > 1) {
-      set_error(string_printf("HIP device: 3D texture %s is not supported", mem.name));
-      return;
-    }
-    if (check(hipcy_tex_alloc(dev_, (int)mem.slot, (int)mem.info.data_type, (int)mem.info.interpolation,
-                              (int)mem.info.extension, (int)mem.data_width, (int)std::max<size_t>(mem.data_height, 1),
-                              mem.host_pointer, mem.memory_size()))) {
+    /* 3D textures (data_depth > 1: volume grids, Point Density voxels) keep
+     * their TextureInfo 3D transform (util_texture.h:93-107) */
+    const float *tfm3d = mem.info.use_transform_3d ? (const float *)&mem.info.transform_3d : nullptr;
+    if (check(hipcy_tex_alloc_3d(dev_, (int)mem.slot, (int)mem.info.data_type, (int)mem.info.interpolation,
+                                 (int)mem.info.extension, (int)mem.data_width,
+                                 (int)std::max<size_t>(mem.data_height, 1), (int)std::max<size_t>(mem.data_depth, 1),
+                                 tfm3d, mem.host_pointer, mem.memory_size()))) {
       mem.device_pointer = (device_ptr)(mem.slot + 1); /* a token: the device owns the texels */
       mem.device_size = mem.memory_size();
       stats.mem_alloc(mem.device_size);

@@ -19,104 +19,8 @@
 #include "hipcycles.h"
 #include "cy_device_common.h"
 #include "k_shade.h"
-#include "../kernel/cy_bvhw.h"
+#include "k_trav.h"
 #include "../host/cy_bvhw_collapse.h"
-
-/* Traversal stack in LDS: BVH2 keeps CY_LDS_STACK node addresses per thread,
- * the wide BVHs CY_LDS_STACKW (node, entry distance) pairs. */
-/* Minimum waves per SIMD the traversal kernels are register-allocated for
- * (amdgpu_waves_per_eu); with the LDS stack it sets their occupancy. */
-/* hair kernels (the ribbon and thick-curve intersectors) need more registers:
- * at the 96 of five waves they spill; measured on the JNK crop (BVH2 hair):
- * 4 waves (128 VGPRs) 18.6 Msamples/s, 3 waves 16.7 */
-#ifndef CY_TRAV_HAIR_WAVES
-#  define CY_TRAV_HAIR_WAVES 4
-#endif
-#define CY_TRAV_WAVES(hair) ((hair) != 0 ? CY_TRAV_HAIR_WAVES : CY_TRAV_MIN_WAVES)
-#ifndef CY_TRAV_MIN_WAVES
-#  define CY_TRAV_MIN_WAVES 5
-#endif
-
-#define CY_STATS_SHARDS 64
-
-/* LDS traversal stacks of one workgroup (one column per thread):
- *   W = 2          BVH2 node addresses, CY_LDS_STACK deep;
- *   W > 2          the wide traversal's ring of CY_LDS_STACKW entries, plus for
- *                  instanced scenes the reference-order top level's BVH2 stack
- *                  (CY_LDS_STACK_TOP deep; cy_path.h bvh2_intersect WI > 2). */
-#ifndef CY_LDS_STACK_TOP
-#  define CY_LDS_STACK_TOP 8
-#endif
-/* TOP: the kernel serves the wide BVH's top CY_LDS_TOP nodes (2 W float4
- * each) from LDS (non-instanced scenes; k_intersect_closest and
- * k_intersect_shadow, which fill them with lds_fill_top).  Other kernels
- * reserve no LDS for them and traverse with n_top = 0. */
-template<int W, bool INST, bool TOP = false> struct LdsStack {
-  CyStackEntry ring[CY_LDS_STACKW * CY_BLOCK];
-  int top[(INST ? CY_LDS_STACK_TOP : 1) * CY_BLOCK];
-  hc_float4 top_nodes[(!INST && TOP && CY_LDS_TOP > 0) ? CY_LDS_TOP * 2 * W : 1];
-};
-template<bool INST, bool TOP> struct LdsStack<2, INST, TOP> {
-  int top[CY_LDS_STACK * CY_BLOCK];
-};
-
-/* This thread's ring column of the wide kernels' LDS stack (nullptr for BVH2). */
-template<int W, bool INST, bool TOP> __device__ __forceinline__ CY_LDS CyStackEntry *lds_ring_of(LdsStack<W, INST, TOP> *lds)
-{
-  if constexpr (W > 2) {
-    return (CY_LDS CyStackEntry *)(lds->ring + threadIdx.x);
-  }
-  else {
-    return nullptr;
-  }
-}
-
-/* HAIR (scenes with curves): unaligned nodes and curve leaves of the shapes
- * HAIR selects (1 ribbons, 2 thick curves, 3 both).  Ribbon-only scenes also
- * traverse the wide BVH (W = 4 / 8, cy_bvhw.h); thick curves keep the BVH2. */
-template<int W, bool any_hit, bool INST = true, int HAIR = 0, bool TOP = false>
-__device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
-                                               CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
-                                               uint *n_tris, LdsStack<W, INST, TOP> *lds, bool *tie = nullptr)
-{
-  const int t = threadIdx.x;
-  if constexpr (W == 2) {
-    return bvh2_intersect<any_hit, INST, 2, CY_LDS_STACK, CY_BLOCK, HAIR>(kg, ray, visibility, isect, err, n_nodes,
-                                                                         n_leaves, n_tris,
-                                                                         (CY_LDS int *)(lds->top + t));
-  }
-  else if constexpr (INST) {
-    /* instanced scene: reference-order top level, wide BVH inside instances */
-    return bvh2_intersect<any_hit, true, W, CY_LDS_STACK_TOP, CY_BLOCK, HAIR>(
-        kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris, (CY_LDS int *)(lds->top + t),
-        (CY_LDS CyStackEntry *)(lds->ring + t), tie);
-  }
-  else {
-    return bvhw_intersect<W, any_hit, HAIR>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
-                                            (CY_LDS CyStackEntry *)(lds->ring + t), tie,
-                                            (CY_LDS const hc_float4 *)lds->top_nodes, TOP ? kg->bvhw_top : 0);
-  }
-}
-
-/* Copy the wide BVH's top nodes into the workgroup's LDS (CY_LDS_TOP; every
- * thread of the block calls this before its traversal). */
-template<int W, bool INST, bool TOP>
-__device__ __forceinline__ void lds_fill_top(const CyGlobals *kg, LdsStack<W, INST, TOP> *lds)
-{
-  if constexpr (W > 2 && !INST && TOP && CY_LDS_TOP > 0) {
-    const int n = kg->bvhw_top * 2 * W;
-    const hc_float4 *src = (const hc_float4 *)kg->bvhw_nodes;
-    for (int i = threadIdx.x; i < n; i += CY_BLOCK) {
-#  if CY_LDS_TOP_SOA
-      /* node i / 2W, float4 i % 2W */
-      lds->top_nodes[(i % (2 * W)) * CY_LDS_TOP + i / (2 * W)] = src[i];
-#  else
-      lds->top_nodes[i] = src[i];
-#  endif
-    }
-    __syncthreads();
-  }
-}
 
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
@@ -1580,6 +1484,10 @@ struct hipcy_device {
    * record buffers of cont_capacity entries. */
   int trav_budget[2] = {0, 0};
   int trav_refill[2] = {0, 0};     /* lane refill: iterations per round, idle lanes that trigger a refill */
+  /* fused tail (hipcy_set_tail): a lane whose items are all claimed runs its
+   * live paths to their ends in one k_tail launch once at most this many are
+   * live; 0 disables */
+  size_t tail_paths = (size_t)1 << 17;
   uint *refill_claim = nullptr;    /* CY_LANES x 8 per-part chunk counters */
   hc_float4 *cont_rec = nullptr;
   size_t cont_capacity = 0; /* records per buffer */
@@ -2176,12 +2084,18 @@ static int upload_texture_info(hipcy_device *dev)
 int hipcy_tex_alloc(hipcy_device *dev, int slot, int data_type, int interpolation, int extension, int width,
                     int height, const void *pixels, size_t bytes)
 {
-  if (!dev || slot < 0 || width <= 0 || height <= 0 || data_type < 0 || data_type > 7 || interpolation < 0 ||
-      interpolation > 3 || extension < 0 || extension > 2) {
+  return hipcy_tex_alloc_3d(dev, slot, data_type, interpolation, extension, width, height, 1, nullptr, pixels, bytes);
+}
+
+int hipcy_tex_alloc_3d(hipcy_device *dev, int slot, int data_type, int interpolation, int extension, int width,
+                       int height, int depth, const float *transform_3d, const void *pixels, size_t bytes)
+{
+  if (!dev || slot < 0 || width <= 0 || height <= 0 || depth <= 0 || data_type < 0 || data_type > 7 ||
+      interpolation < 0 || interpolation > 3 || extension < 0 || extension > 2) {
     return set_error(dev, "tex_alloc: invalid texture description");
   }
   static const size_t texel_bytes[8] = {16, 4, 8, 4, 1, 2, 8, 2}; /* ImageDataType order */
-  if (bytes != texel_bytes[data_type] * (size_t)width * (size_t)height) {
+  if (bytes != texel_bytes[data_type] * (size_t)width * (size_t)height * (size_t)depth) {
     return set_error(dev, "tex_alloc: pixel buffer size does not match the texture description");
   }
   if (hipcy_tex_free(dev, slot) != 0) {
@@ -2205,7 +2119,12 @@ int hipcy_tex_alloc(hipcy_device *dev, int slot, int data_type, int interpolatio
   info.extension = (uint32_t)extension;
   info.width = (uint32_t)width;
   info.height = (uint32_t)height;
-  info.depth = 1;
+  info.depth = (uint32_t)depth;
+  if (transform_3d) {
+    /* TextureInfo::transform_3d (util_texture.h:105), rows x, y, z */
+    info.use_transform_3d = 1;
+    memcpy(&info.transform_3d, transform_3d, 12 * sizeof(float));
+  }
   return upload_texture_info(dev);
 }
 
@@ -2320,6 +2239,12 @@ int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle)
   }
   dev->trav_refill[0] = rounds;
   dev->trav_refill[1] = min_idle;
+  return 0;
+}
+
+int hipcy_set_tail(hipcy_device *dev, uint64_t paths)
+{
+  dev->tail_paths = (size_t)paths;
   return 0;
 }
 
@@ -2558,6 +2483,31 @@ static std::string svm_scan(const std::vector<hc_uint4> &prog, size_t num_shader
           *uses_ray_diff = true;
           tex = true;
           break;
+        case NODE_ENTER_BUMP_EVAL: /* displacement method "both": the undisplaced position */
+          *uses_ray_diff = true;
+          *uses_attr = true;
+          tex = true;
+          break;
+        case NODE_LEAVE_BUMP_EVAL:
+          tex = true;
+          break;
+        case NODE_AOV_START: /* svm_aov.h: AOV outputs of the camera path's hits */
+        case NODE_AOV_COLOR:
+        case NODE_AOV_VALUE:
+          tex = true;
+          break;
+        case NODE_TEX_VOXEL: /* Point Density: a 3D texture; world space carries a transform */
+          len = ((node.z >> 24) & 0xFF) == 1u ? 4 : 1;
+          if (off + len > n) {
+            return "voxel texture: transform nodes past __svm_nodes";
+          }
+          if (!slot_ok((int)node.y) || (int)node.y == -1) {
+            return "shader " + std::to_string(sh) + ": voxel texture slot " + std::to_string((int)node.y) +
+                   " was never allocated (tex_alloc_3d)";
+          }
+          *uses_attr |= ((node.z >> 24) & 0xFF) == 0u;
+          tex = true;
+          break;
         case NODE_VECTOR_DISPLACEMENT: /* height / vector displacement inside a bump program */
           len = 2;
           tex = true;
@@ -2760,9 +2710,9 @@ int hipcy_load_kernels(hipcy_device *dev)
     why = "curve_subdivisions outside 1..16";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
   else if (d.film.use_light_pass) why = "light passes";
-  else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | (1 << 13) | (1 << 14))) != 0 ||
+  else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | (1 << 11) | (1 << 12) | (1 << 13) | (1 << 14))) != 0 ||
            d.film.pass_combined != 0)
-    why = "only the combined pass (+ adaptive aux buffer / sample count)";
+    why = "only the combined pass (+ AOV color / value, adaptive aux buffer / sample count)";
   else if (d.film.pass_denoising_data || d.film.cryptomatte_passes)
     why = "denoising / cryptomatte passes";
   else if (d.film.pass_adaptive_aux_buffer && (d.integrator.adaptive_step <= 0 ||
@@ -3008,6 +2958,7 @@ struct PassLane {
   hipEvent_t done;
   bool stream = false;  /* tile stream lane */
   bool min_live = false; /* tile stream: also reduce the live paths' smallest item */
+  bool tail = false;     /* the lane's fused tail (k_tail) is enqueued: its last launch */
 };
 
 /* The queue sort in effect: the requested mode, or (automatic, -1) the
@@ -3212,10 +3163,42 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
                                   hipMemcpyDeviceToHost, s));
   }
   HIP_CHECK(dev, hipGetLastError());
-  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, ln.stream ? 20 : 16, hipMemcpyDeviceToHost, s));
+  /* the queue counts and the next unclaimed item (cnt[4]) */
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, 20, hipMemcpyDeviceToHost, s));
   /* the kernels' error word, read with the lane's counts */
   HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt + 6, err, 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(dev, hipEventRecord(ln.done, s));
+  return 0;
+}
+
+/* Whether the pass may end its lanes with the fused tail kernel (k_shade.hip
+ * k_tail_*): the plain shading variants, triangle scenes with opaque shadows,
+ * no traversal budget / lane refill, no per-kernel timing. */
+static bool tail_allowed(const hipcy_device *dev, const CyGlobals &kg)
+{
+  return dev->tail_paths > 0 && dev->profiling == 0 && !kg.have_curves &&
+         !dev->data_host.integrator.transparent_shadows && dev->trav_budget[0] == 0 && dev->trav_refill[0] == 0 &&
+         !dev->shade_tex && !dev->use_volumes && dev->shade_closures <= 8;
+}
+
+/* The lane's last launch: its live paths (queue qa) run to their ends in one
+ * k_tail launch; the rays it traced come back in cnt[13] / cnt[14]. */
+static int lane_tail(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, int W)
+{
+  hipStream_t s = ln.s;
+  uint *err = dev->counters + 3;
+  dev->stats.iterations++;
+  HIP_CHECK(dev, hipMemsetAsync(ln.cnt + 13, 0, 8, s));
+  const dim3 grid((ln.n_active + CY_BLOCK - 1) / CY_BLOCK), block(CY_BLOCK);
+  if (!cy_launch_tail(dev->shade_closures, dev->shade_tex, dev->use_volumes, W, kg.have_instancing != 0, grid, block,
+                      s, kg, dev->bufs, ln.tile, ln.q[ln.qa], ln.cnt + ln.qa, ln.cnt + 13, err)) {
+    return set_error(dev, "path_trace: no tail kernel for this shading variant");
+  }
+  HIP_CHECK(dev, hipGetLastError());
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt, ln.cnt, 16 * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipMemcpyAsync(ln.hcnt + 6, err, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(dev, hipEventRecord(ln.done, s));
+  ln.tail = true;
   return 0;
 }
 
@@ -3322,11 +3305,22 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
     }
   }
   dev->host_counters[3] = 0;
+  const bool tail_ok = tail_allowed(dev, kg);
   while (n_fifo > 0) {
     PassLane &L = ln[fifo[head]];
     head = (head + 1) % CY_LANES;
     n_fifo--;
     HIP_CHECK(dev, hipEventSynchronize(L.done));
+    if (L.tail) {
+      /* the fused tail ran every remaining path of the lane to its end */
+      dev->stats.closest_rays += L.hcnt[13];
+      dev->stats.shadow_rays += L.hcnt[14];
+      if (L.hcnt[6]) {
+        dev->host_counters[3] = L.hcnt[6];
+        break;
+      }
+      continue;
+    }
     dev->stats.shadow_rays += L.hcnt[2];
     L.n_active = L.hcnt[L.qb];
     std::swap(L.qa, L.qb);
@@ -3335,7 +3329,9 @@ static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, 
       break;
     }
     if (L.n_active > 0) {
-      if (lane_iterate(dev, kg, L, W, ev, quads) != 0) {
+      /* every item of the lane claimed and few paths left: the fused tail */
+      const bool tail = tail_ok && L.n_active <= dev->tail_paths && L.hcnt[4] >= L.tile.n_items;
+      if ((tail ? lane_tail(dev, kg, L, W) : lane_iterate(dev, kg, L, W, ev, quads)) != 0) {
         return -1;
       }
       fifo[(head + n_fifo++) % CY_LANES] = L.index;

@@ -44,6 +44,30 @@ void cy_launch_shade_mc16_vol(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc64_vol(CY_SHADE_LAUNCHER_ARGS);
 #define CY_DEVICE_MAX_CLOSURE 64
 
+/* the fused tail kernel (k_shade.hip k_tail_*), plain variants only */
+#define CY_TAIL_LAUNCHER_ARGS \
+  int W, bool inst, dim3 grid, dim3 block, hipStream_t stream, const CyGlobals &kg, const CyPathBuffers &b, \
+      const CyTile &tile, const int *queue_in, const uint *count_in, uint *counts, uint *err
+void cy_launch_tail_mc1(CY_TAIL_LAUNCHER_ARGS);
+void cy_launch_tail_mc2(CY_TAIL_LAUNCHER_ARGS);
+void cy_launch_tail_mc4(CY_TAIL_LAUNCHER_ARGS);
+void cy_launch_tail_mc8(CY_TAIL_LAUNCHER_ARGS);
+
+/* false when the scene's shading variant has no tail kernel (texture nodes,
+ * volumes, more than 8 closures) */
+static inline bool cy_launch_tail(int max_closures, bool tex_nodes, bool volumes, CY_TAIL_LAUNCHER_ARGS)
+{
+  if (tex_nodes || volumes || max_closures > 8) {
+    return false;
+  }
+  auto fn = max_closures <= 1 ? cy_launch_tail_mc1 :
+            max_closures <= 2 ? cy_launch_tail_mc2 :
+            max_closures <= 4 ? cy_launch_tail_mc4 :
+                                cy_launch_tail_mc8;
+  fn(W, inst, grid, block, stream, kg, b, tile, queue_in, count_in, counts, err);
+  return true;
+}
+
 static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, CY_SHADE_LAUNCHER_ARGS)
 {
   auto fn = volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :

@@ -14,6 +14,9 @@
 #endif
 #include "cy_device_common.h"
 #include "k_shade.h"
+#if !CY_SVM_TEX
+#  include "k_trav.h"
+#endif
 
 #ifndef CY_SHADE_VARIANT
 #  error "CY_SHADE_VARIANT must be defined (mc1, mc2, mc4, mc8, mc16, mc64)"
@@ -96,3 +99,110 @@ void CY_CAT(cy_launch_shade_, CY_SHADE_VARIANT)(CY_SHADE_LAUNCHER_ARGS)
                      queue_in, count_in,
                      queue_out, count_out, shadow_queue, shadow_count, err);
 }
+
+#if !CY_SVM_TEX
+/* ---------------------------------------------------------------------------
+ * The fused tail (plain variants: basic closures, no texture nodes, no
+ * curves; opaque shadows).  Once every work item of a lane is claimed, its
+ * remaining live paths would need one closest -> shade -> shadow iteration per
+ * bounce, each three launches whose duration is set by the slowest ray of the
+ * launch (on the bench frame's N = 8 row shard the last six iterations hold
+ * 84K down to 768 paths per lane and take 4 of the frame's 14 ms:
+ * tools/trace_iters.py).  Here each remaining path runs to its end in one
+ * launch, through the very functions the three stage kernels call per slot
+ * (closest_load / scene_traverse / closest_store, shade_path, shadow_load /
+ * any-hit scene_traverse / shadow_finish) in the same order, so every path
+ * computes exactly what the wavefront would; only the scheduling differs.
+ * Paths never interact, and no work item is left to claim (the host launches
+ * this only when the lane's item counter is past its end), so nothing is
+ * refilled.  counts[0] / [1] add the closest / shadow rays traced. */
+#ifndef CY_TAIL_WAVES
+#  define CY_TAIL_WAVES 2
+#endif
+template<int W, bool INST>
+__global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SHADE_VARIANT)(CyGlobals kg,
+                                                                                             CyPathBuffers b,
+                                                                                             CyTile tile,
+                                                                                             const int *queue_in,
+                                                                                             const uint *count_in,
+                                                                                             uint *counts,
+                                                                                             uint *err)
+{
+#if CY_SHADE_LDS
+  __shared__ float lds[CY_BLOCK * (CY_CLOSURE_DWORDS + CY_SVM_LDS)];
+  float svm_spill[CY_SVM_STACK - CY_SVM_LDS];
+  CyShadeMem mem;
+  mem.closure = (CyClosure *)(lds + threadIdx.x * CY_CLOSURE_DWORDS);
+  mem.svm_stack = lds + CY_BLOCK * CY_CLOSURE_DWORDS + threadIdx.x;
+  mem.svm_stride = CY_BLOCK;
+  mem.svm_fast = CY_SVM_LDS;
+  mem.svm_spill = svm_spill;
+#else
+  CyClosure closure[CY_MAX_CLOSURE];
+  float svm[CY_SVM_STACK];
+  CyShadeMem mem;
+  mem.closure = closure;
+  mem.svm_stack = svm;
+  mem.svm_stride = 1;
+  mem.svm_fast = CY_SVM_STACK;
+  mem.svm_spill = nullptr;
+#endif
+  __shared__ LdsStack<W, INST, true> lds_stack;
+  lds_fill_top(&kg, &lds_stack); /* a barrier: before any thread leaves */
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int)*count_in) {
+    return;
+  }
+  const int slot = queue_in[i];
+  uint n_closest = 0, n_shadow = 0, n_leaves = 0, n_tris = 0;
+  for (;;) {
+    /* stage 1 (k_intersect_closest) */
+    CyRay ray;
+    uint visibility;
+    const bool has_ray = closest_load(&kg, &b, &tile, slot, CY_NO_ITEM, &ray, &visibility);
+    CyIsect isect;
+    bool hit = false, tie = false;
+    if (has_ray && scene_intersect_valid(&ray)) {
+      hit = scene_traverse<W, false, INST, 0>(&kg, &ray, visibility, &isect, err, nullptr, &n_leaves, &n_tris,
+                                              &lds_stack, &tie);
+    }
+    if constexpr (W > 2) {
+      if (tie) {
+        /* near-tie: re-traced by shade_path with the BVH2 in the reference's order */
+        isect.prim |= CY_PRIM_TIE;
+      }
+    }
+    closest_store<INST>(&b, slot, has_ray, hit, &isect);
+    n_closest++;
+    /* stage 2 (k_shade) */
+    bool shadow = false, finished = false;
+    const bool cont = shade_path<false>(&kg, &b, &tile, slot, CY_NO_ITEM, mem, &shadow, &finished, err);
+    /* stage 3 (k_intersect_shadow) */
+    if (shadow) {
+      CyRay sray;
+      shadow_load(&b, slot, &sray);
+      bool blocked = false;
+      if (scene_intersect_valid(&sray)) {
+        CyIsect sisect;
+        blocked = scene_traverse<W, true, INST, 0>(&kg, &sray, PATH_RAY_SHADOW_OPAQUE, &sisect, err, nullptr,
+                                                   &n_leaves, &n_tris, &lds_stack);
+      }
+      shadow_finish(&b, &tile, slot, blocked);
+      n_shadow++;
+    }
+    if (!cont) {
+      break;
+    }
+  }
+  atomicAdd(&counts[0], n_closest);
+  atomicAdd(&counts[1], n_shadow);
+}
+
+void CY_CAT(cy_launch_tail_, CY_SHADE_VARIANT)(CY_TAIL_LAUNCHER_ARGS)
+{
+  auto fn = W == 8 ? (inst ? CY_CAT(k_tail_, CY_SHADE_VARIANT)<8, true> : CY_CAT(k_tail_, CY_SHADE_VARIANT)<8, false>) :
+            W == 4 ? (inst ? CY_CAT(k_tail_, CY_SHADE_VARIANT)<4, true> : CY_CAT(k_tail_, CY_SHADE_VARIANT)<4, false>) :
+                     (inst ? CY_CAT(k_tail_, CY_SHADE_VARIANT)<2, true> : CY_CAT(k_tail_, CY_SHADE_VARIANT)<2, false>);
+  hipLaunchKernelGGL(fn, grid, block, 0, stream, kg, b, tile, queue_in, count_in, counts, err);
+}
+#endif

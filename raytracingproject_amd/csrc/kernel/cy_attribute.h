@@ -733,6 +733,78 @@ CY_FN void svm_node_set_bump(const CyGlobals *kg, const CyAttrIn &in, CySvmStack
 }
 #endif
 
+#if CY_CLOSURE_EXT
+/* svm_bump.h:21-46 svm_node_enter_bump_eval, the part after the saved state:
+ * the shading point as if undisplaced -- ATTR_STD_POSITION_UNDISPLACED
+ * (primitive_surface_attribute_float3 with its derivatives along the ray
+ * differentials, geom_triangle.h:241-298) moved to world space by the object's
+ * transform (object_position_transform / object_dir_transform; the CPU
+ * kernel's sd->ob_tfm is the object transform for objects without motion).
+ * found = 0 when the object has no such attribute (the state stays). */
+typedef struct CyBumpEval {
+  cfloat3 P, dPdx, dPdy;
+  int found;
+} CyBumpEval;
+
+CY_NOINLINE CyBumpEval svm_bump_undisplaced(const hc_KernelObject *objects, const hc_uint4 *attributes_map,
+                                            const hc_float4 *attributes_float3, const hc_uint4 *tri_vindex,
+                                            CyAttrIn in, float du_dx, float du_dy, float dv_dx, float dv_dy)
+{
+  CyGlobals kgv;
+  kgv.__objects = objects;
+  kgv.__attributes_map = attributes_map;
+  kgv.__attributes_float3 = attributes_float3;
+  kgv.__tri_vindex = tri_vindex;
+  const CyGlobals *kg = &kgv;
+  CyBumpEval r;
+  r.found = 0;
+  r.P = r.dPdx = r.dPdy = mk3(0.0f, 0.0f, 0.0f);
+  const CyAttr desc = (in.object != OBJECT_NONE) ? find_attribute(kg, in.object, in.prim, 10u /* UNDISPLACED */) :
+                                                   attribute_not_found();
+  if (desc.offset == (int)ATTR_STD_NOT_FOUND) {
+    return r;
+  }
+  r.found = 1;
+  if (in.type & PRIMITIVE_ALL_TRIANGLE) {
+    const int e = desc.element;
+    cfloat3 f[3] = {mk3(0.0f, 0.0f, 0.0f), mk3(0.0f, 0.0f, 0.0f), mk3(0.0f, 0.0f, 0.0f)};
+    bool interp = false;
+    if (e == ATTR_ELEMENT_VERTEX || e == ATTR_ELEMENT_VERTEX_MOTION) {
+      const hc_uint4 t = kg->__tri_vindex[in.prim];
+      const int idx[3] = {desc.offset + (int)t.x, desc.offset + (int)t.y, desc.offset + (int)t.z};
+      for (int k = 0; k < 3; k++) {
+        const hc_float4 a = kg->__attributes_float3[idx[k]];
+        f[k] = mk3(a.x, a.y, a.z);
+      }
+      interp = true;
+    }
+    else if (e == ATTR_ELEMENT_CORNER) {
+      const int tri = desc.offset + in.prim * 3;
+      for (int k = 0; k < 3; k++) {
+        const hc_float4 a = kg->__attributes_float3[tri + k];
+        f[k] = mk3(a.x, a.y, a.z);
+      }
+      interp = true;
+    }
+    else if (e == ATTR_ELEMENT_FACE || e == ATTR_ELEMENT_OBJECT || e == ATTR_ELEMENT_MESH) {
+      const hc_float4 a = kg->__attributes_float3[desc.offset + (e == ATTR_ELEMENT_FACE ? in.prim : 0)];
+      r.P = mk3(a.x, a.y, a.z);
+    }
+    if (interp) {
+      r.dPdx = sub3(add3(mul3f(f[0], du_dx), mul3f(f[1], dv_dx)), mul3f(f[2], du_dx + dv_dx));
+      r.dPdy = sub3(add3(mul3f(f[0], du_dy), mul3f(f[1], dv_dy)), mul3f(f[2], du_dy + dv_dy));
+      r.P = add3(add3(mul3f(f[0], in.u), mul3f(f[1], in.v)), mul3f(f[2], 1.0f - in.u - in.v));
+    }
+  }
+  /* curves carry no undisplaced positions (Mesh::add_undisplaced only) */
+  const struct cy_tfm *tfm = object_tfm(kg, in.object);
+  r.P = transform_point(tfm, r.P);
+  r.dPdx = transform_direction(tfm, r.dPdx);
+  r.dPdy = transform_direction(tfm, r.dPdy);
+  return r;
+}
+#endif
+
 /* NODE_ATTR / NODE_VERTEX_COLOR / NODE_NORMAL_MAP / NODE_TANGENT /
  * NODE_OBJECT_INFO / NODE_SET_BUMP out of line: the arrays they read in a local CyGlobals, so
  * the shading kernels' register allocation does not carry them */

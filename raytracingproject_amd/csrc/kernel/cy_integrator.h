@@ -639,6 +639,32 @@ CY_FN float *pixel_buffer(const CyTile *tile, uint p)
   return tile->buffer + (size_t)(tile->offset + x + ybuf * tile->stride) * tile->pass_stride;
 }
 
+/* Render-buffer pixel of work item `item` (its RenderTile's buffer at the
+ * tile's offset / stride): where the camera path's AOV outputs are added. */
+CY_FN float *item_buffer(const CyTile *tile, uint item)
+{
+  if (tile->stream) {
+    int k = tile_of_item(tile, item);
+    const CyTileDesc &g = tile->descs[k];
+    const uint q = (item - g.item_begin) % g.group_npix;
+    int lo = (int)g.group_first;
+    while (lo < k) {
+      const int mid = (lo + k + 1) >> 1;
+      if (tile->descs[mid].px_begin <= q) {
+        lo = mid;
+      }
+      else {
+        k = mid - 1;
+      }
+    }
+    const CyTileDesc &d = tile->descs[lo];
+    const uint p = q - d.px_begin;
+    const int x = d.x + (int)(p % (uint)d.w), y = d.y + (int)(p / (uint)d.w);
+    return d.buffer + (size_t)(d.offset + x + y * d.stride) * tile->pass_stride;
+  }
+  return pixel_buffer(tile, item % tile->npix);
+}
+
 /* kernel_path_trace_setup (kernel_path_common.h:21-46) for a work item.  With
  * adaptive sampling a pixel whose aux buffer marks it converged takes no
  * sample (kernel_path.h:654-659): reported as no camera ray (t = 0). */
@@ -2080,7 +2106,15 @@ CY_FN bool shade_path(const CyGlobals *kg,
     sd.closure[0].N = sd.N;
     sd.flag |= SD_BSDF | SD_BSDF_HAS_EVAL;
 #else
-    shader_eval_surface(kg, &sd, &state, state.flag, err);
+    {
+      /* the camera path's pixel for the AOV outputs (svm_aov.h), when the
+       * film has AOV passes */
+      float *aov_buffer = nullptr;
+      if ((KD->film.pass_aov_color_num > 0 || KD->film.pass_aov_value_num > 0) && (state.flag & PATH_RAY_CAMERA)) {
+        aov_buffer = item_buffer(tile, cam_item != CY_NO_ITEM ? cam_item : cy_ld(&b->item[slot]));
+      }
+      shader_eval_surface(kg, &sd, &state, state.flag, err, aov_buffer);
+    }
 #endif
     shader_prepare_closures(&sd, &state);
 #ifdef CY_DBG_X
@@ -2115,9 +2149,22 @@ CY_FN bool shade_path(const CyGlobals *kg,
     }
     if (!terminated) {
     if ((state.flag & PATH_RAY_CAMERA) && !(state.flag & PATH_RAY_SINGLE_PASS_DONE)) {
-      /* kernel_write_data_passes: no data passes, only the single-pass flag */
+      /* kernel_write_data_passes (kernel_passes.h:173-225): no data passes,
+       * only the single-pass flag, set at the first hit that is not
+       * transparent enough to show what is behind it (the AOV outputs of
+       * later hits are skipped) */
       if (!(sd.flag & SD_TRANSPARENT) || KD->film.pass_alpha_threshold == 0.0f) {
         state.flag |= PATH_RAY_SINGLE_PASS_DONE;
+      }
+      else {
+        /* shader_bsdf_alpha (kernel_shader.h:860-868) */
+        const cfloat3 tr = shader_bsdf_transparency(&sd);
+        cfloat3 alpha = mk3(1.0f - tr.x, 1.0f - tr.y, 1.0f - tr.z);
+        alpha = mk3(cmax(alpha.x, 0.0f), cmax(alpha.y, 0.0f), cmax(alpha.z, 0.0f));
+        alpha = mk3(cmin(alpha.x, 1.0f), cmin(alpha.y, 1.0f), cmin(alpha.z, 1.0f));
+        if (average3(alpha) >= KD->film.pass_alpha_threshold) {
+          state.flag |= PATH_RAY_SINGLE_PASS_DONE;
+        }
       }
     }
     if (KD->integrator.filter_glossy != CY_FLT_MAX) {

@@ -105,6 +105,17 @@ CY_FN int cy_ftoi(float f)
 #endif
 }
 
+/* kernel_write_pass_float (kernel_write_passes.h:21-30): an atomic add on GPU
+ * devices; the host emulation renders one path at a time */
+CY_FN void cy_pass_add(float *p, float v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicAdd(p, v);
+#else
+  *p += v;
+#endif
+}
+
 /* util_math.h:112-130 (ternary forms: NaN handling matches the reference). */
 CY_FN float cmin(float a, float b)
 {

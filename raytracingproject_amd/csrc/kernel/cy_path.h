@@ -2364,6 +2364,66 @@ typedef struct CySvmTexIn {
   int bounce, diffuse_bounce, glossy_bounce, transparent_bounce, transmission_bounce;
 } CySvmTexIn;
 
+#if CY_SVM_TEX
+/* svm_voxel.h:22-55 svm_node_tex_voxel (the Point Density node's dense grid):
+ * the input point in object space (volume_normalized_position,
+ * geom_volume.h:32-48: the object's inverse transform, then the mesh's
+ * ATTR_STD_GENERATED_TRANSFORM when it has one) or through the node's own
+ * world-space transform (three data nodes), then the 3D texture at its own
+ * interpolation; density = alpha, colour = rgb.  Returns the next node. */
+CY_NOINLINE int svm_node_tex_voxel(const hc_uint4 *svm_nodes, const hc_KernelObject *objects,
+                                   const hc_uint4 *attributes_map, const hc_float4 *attributes_float3,
+                                   const hc_TextureInfo *texture_info, int object, int prim, CySvmStack stack,
+                                   hc_uint4 node, int offset, uint *err)
+{
+  CyGlobals kgv;
+  kgv.__objects = objects;
+  kgv.__attributes_map = attributes_map;
+  kgv.__attributes_float3 = attributes_float3;
+  const CyGlobals *kg = &kgv;
+  uint co_offset, density_out_offset, color_out_offset, space;
+  svm_unpack4(node.z, &co_offset, &density_out_offset, &color_out_offset, &space);
+  cfloat3 co = svm_load3(stack, co_offset, err);
+  if (space == 0u) { /* NODE_TEX_VOXEL_SPACE_OBJECT */
+    if (object == OBJECT_NONE) {
+      /* the reference reads an unset object transform here (world volume) */
+      cy_set_error(err, CY_ERR_FEATURE, 12);
+    }
+    else {
+      const CyAttr desc = find_attribute(kg, object, prim, 8u /* ATTR_STD_GENERATED_TRANSFORM */);
+      co = transform_point(object_itfm(kg, object), co);
+      if (desc.offset != (int)ATTR_STD_NOT_FOUND) {
+        /* primitive_attribute_matrix (geom_attribute.h:93-103) */
+        struct cy_tfm t;
+        const hc_float4 r0 = kg->__attributes_float3[desc.offset + 0];
+        const hc_float4 r1 = kg->__attributes_float3[desc.offset + 1];
+        const hc_float4 r2 = kg->__attributes_float3[desc.offset + 2];
+        t.x = {r0.x, r0.y, r0.z, r0.w};
+        t.y = {r1.x, r1.y, r1.z, r1.w};
+        t.z = {r2.x, r2.y, r2.z, r2.w};
+        co = transform_point(&t, co);
+      }
+    }
+  }
+  else { /* NODE_TEX_VOXEL_SPACE_WORLD: read_node_float x 3 */
+    struct cy_tfm t;
+    const hc_uint4 a = svm_nodes[offset++], b = svm_nodes[offset++], c = svm_nodes[offset++];
+    t.x = {as_float(a.x), as_float(a.y), as_float(a.z), as_float(a.w)};
+    t.y = {as_float(b.x), as_float(b.y), as_float(b.z), as_float(b.w)};
+    t.z = {as_float(c.x), as_float(c.y), as_float(c.z), as_float(c.w)};
+    co = transform_point(&t, co);
+  }
+  const hc_float4 r = kernel_tex_image_interp_3d(texture_info, (int)node.y, co);
+  if (density_out_offset != SVM_STACK_INVALID) {
+    svm_store(stack, density_out_offset, r.w, err);
+  }
+  if (color_out_offset != SVM_STACK_INVALID) {
+    svm_store3(stack, color_out_offset, mk3(r.x, r.y, r.z), err);
+  }
+  return offset;
+}
+#endif
+
 CY_NOINLINE int svm_eval_texture_node(const hc_KernelData *data,
                                       const hc_uint4 *svm_nodes,
                                       const hc_KernelObject *objects,
@@ -2701,8 +2761,11 @@ CY_FN void svm_node_bevel(const CyGlobals *kg, CySD *sd, const CyPathState *stat
                           uint *err);
 #endif
 
+/* buffer: the camera path's render-buffer pixel (kernel_path_integrate passes
+ * it to every surface evaluation of the path, kernel_path.h:569), written by
+ * the AOV output nodes; nullptr elsewhere */
 CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err,
-                          int type = 0)
+                          int type = 0, float *buffer = nullptr)
 {
   CySvmStack stack;
   stack.p = sd->svm_stack;
@@ -2943,7 +3006,82 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
         return;
 #else
       {
+        if (node.x == NODE_AOV_START) {
+          /* svm_aov.h:21-27 svm_node_aov_check: only the camera path's first
+           * (non-transparent) hit writes AOVs; otherwise the nodes after this
+           * one, which only feed the AOV outputs, are skipped */
+          if (!(buffer != nullptr && (path_flag & PATH_RAY_CAMERA) && !(path_flag & PATH_RAY_SINGLE_PASS_DONE))) {
+            return;
+          }
+          break;
+        }
+        if (node.x == NODE_AOV_COLOR) {
+          /* svm_aov.h:29-39: kernel_write_pass_float4, an atomic add on GPU
+           * devices (kernel_write_passes.h:49-65) */
+          const cfloat3 val = svm_load3(stack, node.y, err);
+          if (buffer) {
+            float *p = buffer + KD->film.pass_aov_color + 4 * (int)node.z;
+            cy_pass_add(p + 0, val.x);
+            cy_pass_add(p + 1, val.y);
+            cy_pass_add(p + 2, val.z);
+            cy_pass_add(p + 3, 1.0f);
+          }
+          break;
+        }
+        if (node.x == NODE_AOV_VALUE) {
+          /* svm_aov.h:41-50 */
+          const float val = svm_load(stack, node.y, err);
+          if (buffer) {
+            cy_pass_add(buffer + KD->film.pass_aov_value + (int)node.z, val);
+          }
+          break;
+        }
+        if (node.x == NODE_TEX_VOXEL) {
+          offset = svm_node_tex_voxel(kg->__svm_nodes, kg->__objects, kg->__attributes_map, kg->__attributes_float3,
+                                      kg->__texture_info, sd->object, sd->prim, stack, node, offset, err);
+          break;
+        }
 #if CY_CLOSURE_EXT
+        if (node.x == NODE_ENTER_BUMP_EVAL) {
+          /* svm_bump.h:21-46: save P, dP.dx, dP.dy, then evaluate the bump
+           * program at the undisplaced position */
+          svm_store3(stack, node.y + 0, sd->P, err);
+          svm_store3(stack, node.y + 3, sd->dP.dx, err);
+          svm_store3(stack, node.y + 6, sd->dP.dy, err);
+          CyAttrIn bin;
+          bin.P = sd->P;
+          bin.N = sd->N;
+          bin.Ng = sd->Ng;
+          bin.I = sd->I;
+          bin.u = sd->u;
+          bin.v = sd->v;
+          bin.object = sd->object;
+          bin.prim = sd->prim;
+          bin.type = sd->type;
+          bin.flag = sd->flag;
+          bin.shader = sd->shader;
+          bin.dPdu = sd->dPdu;
+          bin.dPdx = sd->dP.dx;
+          bin.dPdy = sd->dP.dy;
+          bin.bump = 0;
+          bin.bump_du = bin.bump_dv = 0.0f;
+          const CyBumpEval be = svm_bump_undisplaced(kg->__objects, kg->__attributes_map, kg->__attributes_float3,
+                                                     kg->__tri_vindex, bin, sd->du.dx, sd->du.dy, sd->dv.dx,
+                                                     sd->dv.dy);
+          if (be.found) {
+            sd->P = be.P;
+            sd->dP.dx = be.dPdx;
+            sd->dP.dy = be.dPdy;
+          }
+          break;
+        }
+        if (node.x == NODE_LEAVE_BUMP_EVAL) {
+          /* svm_bump.h:48-60: restore the state */
+          sd->P = svm_load3(stack, node.y + 0, err);
+          sd->dP.dx = svm_load3(stack, node.y + 3, err);
+          sd->dP.dy = svm_load3(stack, node.y + 6, err);
+          break;
+        }
         /* the bump forms (svm.h:298-345) read their centre node at
          * P + dP.dx (.dy), u + du.dx, v + dv.dx (svm_geometry.h:54-100,
          * svm_tex_coord.h:97-255), attributes plus their derivative
@@ -3047,7 +3185,7 @@ CY_FN void svm_eval_nodes(const CyGlobals *kg, CySD *sd, const CyPathState *stat
 
 /* kernel_shader.h:1057-1112 */
 CY_FN void shader_eval_surface(
-    const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err)
+    const CyGlobals *kg, CySD *sd, const CyPathState *state, int path_flag, uint *err, float *buffer = nullptr)
 {
   int max_closures;
   if (path_flag & (PATH_RAY_TERMINATE | PATH_RAY_SHADOW | PATH_RAY_EMISSION)) {
@@ -3061,7 +3199,7 @@ CY_FN void shader_eval_surface(
    * holds every closure the shaders allocate, so allocations succeed exactly
    * as with the reference's budget; the clamp keeps extras in the array) */
   sd->num_closure_left = (max_closures < CY_MAX_CLOSURE) ? max_closures : CY_MAX_CLOSURE;
-  svm_eval_nodes(kg, sd, state, path_flag, err);
+  svm_eval_nodes(kg, sd, state, path_flag, err, 0, buffer);
 #if CY_CLOSURE_EXT
   if ((sd->flag & SD_BSDF_NEEDS_LCG) && state) {
     /* kernel_shader.h:1109-1111: lcg_state_init_addrspace(state, 0xb4bc3953) */

@@ -351,6 +351,192 @@ CY_FN hc_float4 kernel_tex_image_interp(const hc_TextureInfo *texture_info, int 
   }
 }
 
+/* ---- 3D textures (kernel_cpu_image.h:254-469 TextureInterpolator::interp_3d):
+ * dense voxel grids, e.g. the Point Density node's.  Unlike the 2D reader the
+ * clip extension returns zero only outside [0, 1]^3 and otherwise clamps like
+ * extend (ATTR_FALLTHROUGH); the voxel reads themselves are unchecked. */
+CY_FN int cy_tex3_index(const hc_TextureInfo *info, int x, int y, int z)
+{
+  return x + y * (int)info->width + z * (int)info->width * (int)info->height;
+}
+
+CY_FN bool cy_tex3_outside(float x, float y, float z)
+{
+  return x < 0.0f || y < 0.0f || z < 0.0f || x > 1.0f || y > 1.0f || z > 1.0f;
+}
+
+/* kernel_cpu_image.h:256-293 */
+CY_FN hc_float4 cy_interp_3d_closest(const hc_TextureInfo *info, float x, float y, float z)
+{
+  const int width = (int)info->width, height = (int)info->height, depth = (int)info->depth;
+  int ix, iy, iz;
+  cy_tex_frac(x * (float)width, &ix);
+  cy_tex_frac(y * (float)height, &iy);
+  cy_tex_frac(z * (float)depth, &iz);
+  switch (info->extension) {
+    case CY_EXTENSION_REPEAT:
+      ix = cy_wrap_periodic(ix, width);
+      iy = cy_wrap_periodic(iy, height);
+      iz = cy_wrap_periodic(iz, depth);
+      break;
+    case CY_EXTENSION_CLIP:
+      if (cy_tex3_outside(x, y, z)) {
+        return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+      /* fall through */
+    case CY_EXTENSION_EXTEND:
+      ix = cy_wrap_clamp(ix, width);
+      iy = cy_wrap_clamp(iy, height);
+      iz = cy_wrap_clamp(iz, depth);
+      break;
+    default:
+      return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  return cy_tex_read(info, cy_tex3_index(info, ix, iy, iz));
+}
+
+/* kernel_cpu_image.h:295-358: eight weighted voxels summed in order, each
+ * weight the product of its three factors left to right */
+CY_FN hc_float4 cy_interp_3d_linear(const hc_TextureInfo *info, float x, float y, float z)
+{
+  const int width = (int)info->width, height = (int)info->height, depth = (int)info->depth;
+  int ix, iy, iz, nix, niy, niz;
+  const float tx = cy_tex_frac(x * (float)width - 0.5f, &ix);
+  const float ty = cy_tex_frac(y * (float)height - 0.5f, &iy);
+  const float tz = cy_tex_frac(z * (float)depth - 0.5f, &iz);
+  switch (info->extension) {
+    case CY_EXTENSION_REPEAT:
+      ix = cy_wrap_periodic(ix, width);
+      iy = cy_wrap_periodic(iy, height);
+      iz = cy_wrap_periodic(iz, depth);
+      nix = cy_wrap_periodic(ix + 1, width);
+      niy = cy_wrap_periodic(iy + 1, height);
+      niz = cy_wrap_periodic(iz + 1, depth);
+      break;
+    case CY_EXTENSION_CLIP:
+      if (cy_tex3_outside(x, y, z)) {
+        return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+      /* fall through */
+    case CY_EXTENSION_EXTEND:
+      nix = cy_wrap_clamp(ix + 1, width);
+      niy = cy_wrap_clamp(iy + 1, height);
+      niz = cy_wrap_clamp(iz + 1, depth);
+      ix = cy_wrap_clamp(ix, width);
+      iy = cy_wrap_clamp(iy, height);
+      iz = cy_wrap_clamp(iz, depth);
+      break;
+    default:
+      return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  hc_float4 r = cy_f4_scale((1.0f - tz) * (1.0f - ty) * (1.0f - tx), cy_tex_read(info, cy_tex3_index(info, ix, iy, iz)));
+  r = cy_f4_add(r, cy_f4_scale((1.0f - tz) * (1.0f - ty) * tx, cy_tex_read(info, cy_tex3_index(info, nix, iy, iz))));
+  r = cy_f4_add(r, cy_f4_scale((1.0f - tz) * ty * (1.0f - tx), cy_tex_read(info, cy_tex3_index(info, ix, niy, iz))));
+  r = cy_f4_add(r, cy_f4_scale((1.0f - tz) * ty * tx, cy_tex_read(info, cy_tex3_index(info, nix, niy, iz))));
+  r = cy_f4_add(r, cy_f4_scale(tz * (1.0f - ty) * (1.0f - tx), cy_tex_read(info, cy_tex3_index(info, ix, iy, niz))));
+  r = cy_f4_add(r, cy_f4_scale(tz * (1.0f - ty) * tx, cy_tex_read(info, cy_tex3_index(info, nix, iy, niz))));
+  r = cy_f4_add(r, cy_f4_scale(tz * ty * (1.0f - tx), cy_tex_read(info, cy_tex3_index(info, ix, niy, niz))));
+  r = cy_f4_add(r, cy_f4_scale(tz * ty * tx, cy_tex_read(info, cy_tex3_index(info, nix, niy, niz))));
+  return r;
+}
+
+/* kernel_cpu_image.h:368-453 (tricubic B-spline):
+ * ROW_TERM(row) = w[row] * (COL_TERM(0, row) + ... + COL_TERM(3, row)),
+ * COL_TERM(col, row) = v[col] * (u0 D(0, col, row) + ... + u3 D(3, col, row)),
+ * the four row terms summed left to right */
+CY_FN hc_float4 cy_interp_3d_tricubic(const hc_TextureInfo *info, float x, float y, float z)
+{
+  const int width = (int)info->width, height = (int)info->height, depth = (int)info->depth;
+  int ix, iy, iz, nix, niy, niz, pix, piy, piz, nnix, nniy, nniz;
+  const float tx = cy_tex_frac(x * (float)width - 0.5f, &ix);
+  const float ty = cy_tex_frac(y * (float)height - 0.5f, &iy);
+  const float tz = cy_tex_frac(z * (float)depth - 0.5f, &iz);
+  switch (info->extension) {
+    case CY_EXTENSION_REPEAT:
+      ix = cy_wrap_periodic(ix, width);
+      iy = cy_wrap_periodic(iy, height);
+      iz = cy_wrap_periodic(iz, depth);
+      pix = cy_wrap_periodic(ix - 1, width);
+      piy = cy_wrap_periodic(iy - 1, height);
+      piz = cy_wrap_periodic(iz - 1, depth);
+      nix = cy_wrap_periodic(ix + 1, width);
+      niy = cy_wrap_periodic(iy + 1, height);
+      niz = cy_wrap_periodic(iz + 1, depth);
+      nnix = cy_wrap_periodic(ix + 2, width);
+      nniy = cy_wrap_periodic(iy + 2, height);
+      nniz = cy_wrap_periodic(iz + 2, depth);
+      break;
+    case CY_EXTENSION_CLIP:
+      if (cy_tex3_outside(x, y, z)) {
+        return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+      /* fall through */
+    case CY_EXTENSION_EXTEND:
+      pix = cy_wrap_clamp(ix - 1, width);
+      piy = cy_wrap_clamp(iy - 1, height);
+      piz = cy_wrap_clamp(iz - 1, depth);
+      nix = cy_wrap_clamp(ix + 1, width);
+      niy = cy_wrap_clamp(iy + 1, height);
+      niz = cy_wrap_clamp(iz + 1, depth);
+      nnix = cy_wrap_clamp(ix + 2, width);
+      nniy = cy_wrap_clamp(iy + 2, height);
+      nniz = cy_wrap_clamp(iz + 2, depth);
+      ix = cy_wrap_clamp(ix, width);
+      iy = cy_wrap_clamp(iy, height);
+      iz = cy_wrap_clamp(iz, depth);
+      break;
+    default:
+      return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  const int xc[4] = {pix, ix, nix, nnix};
+  const int yc[4] = {width * piy, width * iy, width * niy, width * nniy};
+  const int zc[4] = {width * height * piz, width * height * iz, width * height * niz, width * height * nniz};
+  float u[4], v[4], w[4];
+  cy_cubic_weights(u, tx);
+  cy_cubic_weights(v, ty);
+  cy_cubic_weights(w, tz);
+  hc_float4 r;
+  for (int row = 0; row < 4; row++) {
+    hc_float4 rt;
+    for (int col = 0; col < 4; col++) {
+      const int yz = yc[col] + zc[row];
+      hc_float4 c = cy_f4_scale(u[0], cy_tex_read(info, xc[0] + yz));
+      c = cy_f4_add(c, cy_f4_scale(u[1], cy_tex_read(info, xc[1] + yz)));
+      c = cy_f4_add(c, cy_f4_scale(u[2], cy_tex_read(info, xc[2] + yz)));
+      c = cy_f4_add(c, cy_f4_scale(u[3], cy_tex_read(info, xc[3] + yz)));
+      c = cy_f4_scale(v[col], c);
+      rt = (col == 0) ? c : cy_f4_add(rt, c);
+    }
+    rt = cy_f4_scale(w[row], rt);
+    r = (row == 0) ? rt : cy_f4_add(r, rt);
+  }
+  return r;
+}
+
+/* kernel_cpu_image.h:501-531 kernel_tex_image_interp_3d with
+ * INTERPOLATION_NONE: the texture's own interpolation; the optional 3D
+ * transform first (TextureInfo::use_transform_3d) */
+CY_FN hc_float4 kernel_tex_image_interp_3d(const hc_TextureInfo *texture_info, int id, cfloat3 P)
+{
+  const hc_TextureInfo *info = &texture_info[id];
+  if (info->use_transform_3d) {
+    const hc_Transform &t = info->transform_3d;
+    P = mk3(t.x.x * P.x + t.x.y * P.y + t.x.z * P.z + t.x.w, t.y.x * P.x + t.y.y * P.y + t.y.z * P.z + t.y.w,
+            t.z.x * P.x + t.z.y * P.y + t.z.z * P.z + t.z.w);
+  }
+  if (info->data == 0) {
+    return cy_f4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  switch (info->interpolation) {
+    case CY_INTERPOLATION_CLOSEST:
+      return cy_interp_3d_closest(info, P.x, P.y, P.z);
+    case CY_INTERPOLATION_LINEAR:
+      return cy_interp_3d_linear(info, P.x, P.y, P.z);
+    default:
+      return cy_interp_3d_tricubic(info, P.x, P.y, P.z);
+  }
+}
+
 /* util_color.h:185-242: the reference CPU kernel is built with __KERNEL_SSE2__,
  * so color_srgb_to_linear_v4 takes the SSE path: powf(x, 2.4) by fastpow24
  * (a float-bits initial guess refined by three Newton steps on the fifth

@@ -24,6 +24,12 @@ enum {
   NODE_TEX_COORD_BUMP_DX = 31,
   NODE_TEX_COORD_BUMP_DY = 32,
   NODE_CLOSURE_SET_NORMAL = 33,
+  NODE_ENTER_BUMP_EVAL = 34,
+  NODE_LEAVE_BUMP_EVAL = 35,
+  NODE_TEX_VOXEL = 87,
+  NODE_AOV_START = 88,
+  NODE_AOV_COLOR = 89,
+  NODE_AOV_VALUE = 90,
   NODE_HSV = 36,
   NODE_MATH = 42,
   NODE_VECTOR_MATH = 43,

@@ -148,6 +148,11 @@ class HIPDevice:
         new rays once `min_idle` lanes are idle.  0 disables."""
         self._check(self.lib.hipcy_set_traversal_refill(self.h, int(rounds), int(min_idle)))
 
+    def set_tail(self, paths: int) -> None:
+        """Fused tail (hipcy_set_tail): lanes with all items claimed and at most
+        `paths` live paths finish them in one launch.  0 disables."""
+        self._check(self.lib.hipcy_set_tail(self.h, int(paths)))
+
     def set_slots(self, slots: int = 0, record_bytes: int = 0) -> None:
         """Path slots in flight and the per-pass sample-record budget (0 keeps a value)."""
         self._check(self.lib.hipcy_set_slots(self.h, int(slots), int(record_bytes)))
@@ -182,10 +187,15 @@ class HIPDevice:
         from . import nodes
 
         a = image.texel_array()
-        self._check(self.lib.hipcy_tex_alloc(self.h, slot, nodes.IMAGE_DATA_TYPES.index(image.data_type),
-                                             nodes.INTERPOLATIONS.index(image.interpolation),
-                                             nodes.EXTENSIONS.index(image.extension), a.shape[1], a.shape[0],
-                                             a.ctypes.data, a.nbytes))
+        w, h, d = image.dims()
+        tfm = None
+        if image.transform_3d is not None:
+            t = np.ascontiguousarray(np.asarray(image.transform_3d, dtype=np.float32).reshape(12))
+            tfm = t.ctypes.data
+        self._check(self.lib.hipcy_tex_alloc_3d(self.h, slot, nodes.IMAGE_DATA_TYPES.index(image.data_type),
+                                                nodes.INTERPOLATIONS.index(image.interpolation),
+                                                nodes.EXTENSIONS.index(image.extension), w, h, d, tfm,
+                                                a.ctypes.data, a.nbytes))
 
     def update_background_map(self, ds: DeviceScene) -> None:
         """LightManager::device_update_background (light.cpp:568-716): the world

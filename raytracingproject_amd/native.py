@@ -110,6 +110,9 @@ DEVICE_SYMBOLS = {
     "hipcy_bind_global": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_size_t]),
     "hipcy_tex_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]),
+    "hipcy_tex_alloc_3d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_size_t]),
     "hipcy_tex_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_load_kernels": (ctypes.c_int, [ctypes.c_void_p]),
     "hipcy_get_bvh_layout_mask": (ctypes.c_uint32, [ctypes.c_void_p]),
@@ -126,6 +129,7 @@ DEVICE_SYMBOLS = {
     "hipcy_set_ray_sort": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_traversal_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "hipcy_set_traversal_refill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "hipcy_set_tail": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "hipcy_set_bvh_leaf_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_slots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "hipcy_intersect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),

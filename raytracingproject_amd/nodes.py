@@ -382,6 +382,8 @@ EXTENSIONS = ("repeat", "extend", "clip")
 IMAGE_PROJECTIONS = {"flat": 0, "sphere": 2, "tube": 3}
 ENVIRONMENT_PROJECTIONS = {"equirectangular": 0, "mirror_ball": 1}
 NODE_TEX_IMAGE, NODE_TEX_ENVIRONMENT = 23, 55
+NODE_TEX_VOXEL = 87  # svm_types.h
+ATTR_STD_GENERATED_TRANSFORM = 8  # kernel_types.h AttributeStandard
 NODE_IMAGE_COMPRESS_AS_SRGB, NODE_IMAGE_ALPHA_UNASSOCIATE = 1, 2
 
 
@@ -392,24 +394,35 @@ class Image:
     the device's tex_alloc.  `pixels` is (H, W, C) with C = 4 for the
     *4 types and 1 (or 2-D) for the single-channel ones; row 0 is v = 0.
     `tiles` maps UDIM tile numbers (1001, 1002, ...) to Images for a tiled
-    image; then `pixels` is unused."""
+    image; then `pixels` is unused.  A 3D image (volume grids, the Point
+    Density node's voxels) has `depth` > 1 and pixels (D, H, W, C);
+    `transform_3d` (3, 4) sets TextureInfo::use_transform_3d / transform_3d."""
     pixels: object = None
     data_type: str = "byte4"
     interpolation: str = "linear"
     extension: str = "repeat"
     compress_as_srgb: bool = False  # byte images stored in sRGB (ImageMetaData)
     tiles: dict | None = None
+    depth: int = 1
+    transform_3d: object = None
 
     def texel_array(self) -> np.ndarray:
         dt = {"float4": np.float32, "float": np.float32, "byte4": np.uint8, "byte": np.uint8,
               "half4": np.uint16, "half": np.uint16, "ushort4": np.uint16, "ushort": np.uint16}[self.data_type]
         a = np.ascontiguousarray(self.pixels, dtype=dt)
         ch = 4 if self.data_type.endswith("4") else 1
-        if a.ndim == 2 and ch == 1:
-            a = a[:, :, None]
-        if a.ndim != 3 or a.shape[2] != ch:
-            raise ValueError(f"{self.data_type} image needs shape (H, W, {ch}), got {a.shape}")
+        nd = 4 if self.depth > 1 else 3
+        if a.ndim == nd - 1 and ch == 1:
+            a = a[..., None]
+        if a.ndim != nd or a.shape[-1] != ch or (nd == 4 and a.shape[0] != self.depth):
+            want = f"(D={self.depth}, H, W, {ch})" if nd == 4 else f"(H, W, {ch})"
+            raise ValueError(f"{self.data_type} image needs shape {want}, got {a.shape}")
         return a
+
+    def dims(self) -> tuple:
+        """(width, height, depth) of the texel array"""
+        a = self.texel_array()
+        return (a.shape[2], a.shape[1], a.shape[0]) if self.depth > 1 else (a.shape[1], a.shape[0], 1)
 
 
 def image_texture(image: Image, vector=None, projection: str = "flat", alpha_unassociate: bool = False) -> Node:
@@ -420,6 +433,21 @@ def image_texture(image: Image, vector=None, projection: str = "flat", alpha_una
     return Node("image_texture", {"Vector": _default_vector(vector, "uv")},
                 params={"image": image, "projection": IMAGE_PROJECTIONS[projection],
                         "alpha_unassociate": alpha_unassociate})
+
+
+def point_density(image: Image, vector=None, space: str = "object", tfm=None) -> Node:
+    """Point Density texture node (nodes.cpp:1810-1852 PointDensityTextureNode::
+    compile, svm_voxel.h): the host-built voxel grid `image` (3D, float4:
+    colour in rgb, density in alpha) looked up at the input point, in object
+    space (volume_normalized_position) or through `tfm` (3x4, world space).
+    The vector defaults to the shading position."""
+    if space not in ("object", "world"):
+        raise ValueError(f"point density space {space!r}: object or world")
+    if image.depth <= 1:
+        raise ValueError("point density needs a 3D image (depth > 1)")
+    t = np.eye(4)[:3] if tfm is None else np.asarray(tfm, dtype=np.float64).reshape(3, 4)
+    return Node("point_density", {"Vector": vector if vector is not None else geometry()["Position"]},
+                params={"image": image, "space": space, "tfm": t})
 
 
 def environment_texture(image: Image, vector, projection: str = "equirectangular") -> Node:
@@ -836,6 +864,8 @@ def _outputs(node: Node) -> dict:
         return {"Result": "float"}
     if k in ("rgb_ramp", "image_texture", "environment_texture"):
         return {"Color": "color", "Alpha": "float"}
+    if k == "point_density":
+        return {"Color": "color", "Density": "float"}
     if k == "sky_texture":
         return {"Color": "color"}
     if k == "ies_texture":
@@ -889,6 +919,7 @@ _INPUT_TYPES = {
     "rgb_ramp": {"Fac": "float"},
     "image_texture": {"Vector": "vector"},
     "environment_texture": {"Vector": "vector"},
+    "point_density": {"Vector": "vector"},
     "sky_texture": {"Vector": "vector"},
     "ies_texture": {"Vector": "vector", "Strength": "float"},
     "wavelength": {"Wavelength": "float"},
@@ -920,6 +951,7 @@ def _width(t: str) -> int:
 # ShaderNode::has_spatial_varying (render/nodes.h): nodes whose value depends on
 # the shading point or direction (texture coordinate, geometry, textures)
 SPATIAL_KINDS = ("tex_coord", "geometry", "checker", "gradient", "image_texture", "environment_texture", "sky_texture", "ies_texture",
+                 "point_density",
                  "attribute", "vertex_color", "normal_map", "tangent", "object_info", "camera_data")
 
 
@@ -1386,6 +1418,22 @@ class NodeCompiler:
         else:
             slot = self.image_slot(image)
             self.emit((NODE_TEX_IMAGE, (-slot) & 0xFFFFFFFF, uchar4(vec, col, alpha, flags), n.params["projection"]))
+
+    def _n_point_density(self, n):  # nodes.cpp:1810-1852 PointDensityTextureNode::compile
+        p = n.params
+        dens, col = self.out(n, "Density"), self.out(n, "Color")
+        if dens == SVM_STACK_INVALID and col == SVM_STACK_INVALID:
+            return
+        vec = self.inp(n, "Vector")
+        space = 0 if p["space"] == "object" else 1
+        self.emit((NODE_TEX_VOXEL, self.image_slot(p["image"]), uchar4(vec, dens, col, space), 0))
+        if space == 1:
+            t = np.asarray(p["tfm"], dtype=np.float32)
+            for r in range(3):
+                self.emit(tuple(int(x) for x in t[r].view(np.uint32)))
+        if space == 0:
+            # PointDensityTextureNode::attributes: the mesh's generated transform
+            self.attribute(ATTR_STD_GENERATED_TRANSFORM)
 
     def _n_environment_texture(self, n):  # nodes.cpp EnvironmentTextureNode::compile
         image = n.params["image"]

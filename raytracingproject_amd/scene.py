@@ -52,6 +52,10 @@ PRNG_BOUNCE_NUM = 8
 
 NODE_END, NODE_SHADER_JUMP, NODE_CLOSURE_BSDF, NODE_CLOSURE_EMISSION = 0, 1, 2, 3
 NODE_SET_DISPLACEMENT = 20
+NODE_ENTER_BUMP_EVAL, NODE_LEAVE_BUMP_EVAL = 34, 35  # svm_types.h ShaderNodeType
+NODE_AOV_START, NODE_AOV_COLOR, NODE_AOV_VALUE = 88, 89, 90
+SVM_BUMP_EVAL_STATE_SIZE = 9  # svm_types.h
+ATTR_STD_POSITION_UNDISPLACED = 10  # kernel_types.h AttributeStandard
 NODE_CLOSURE_BACKGROUND, NODE_CLOSURE_SET_WEIGHT = 4, 5
 NODE_CLOSURE_HOLDOUT = 37  # svm_types.h ShaderNodeType
 NODE_CLOSURE_WEIGHT, NODE_EMISSION_WEIGHT = 6, 7
@@ -182,7 +186,8 @@ class Closure:
     # own SVM program, run by SHADER_EVAL_DISPLACE) or "bump" (a bump program
     # from the displacement graph ahead of the surface program, through ray
     # differentials; Blender's default).  "both" needs the mesh displaced with
-    # its undisplaced positions kept (ATTR_STD_POSITION_UNDISPLACED): refused.
+    # its undisplaced positions kept (ATTR_STD_POSITION_UNDISPLACED, Mesh.undisplaced)
+    # and adds a bump program evaluated at them (NODE_ENTER / LEAVE_BUMP_EVAL).
     displacement: object = None
     displacement_method: str = "true"
     # material output "Volume": a tree of volume closures (volume_absorption,
@@ -190,6 +195,11 @@ class Closure:
     volume: "Closure | None" = None
     pass_index: int = 0  # Material pass index (KernelShader.pass_id, Object Info "Material Index")
     density: object = 1.0  # volume closures
+    # AOV Output nodes of the material (OutputAOVNode, nodes.cpp): AOV name ->
+    # a colour or value (constant or socket) written to the film's AOV pass of
+    # that name at the camera path's first hit (svm_aov.h); names without a
+    # pass in Scene.aovs are dropped, as OutputAOVNode::simplify drops them
+    aovs: dict | None = None
 
     def closure_type(self) -> int:
         """The ClosureType the node compiles to, after simplify_settings
@@ -491,6 +501,9 @@ class SVMCompiler:
         # as standard ids or names, in first-use order
         self.requests: list[list] = []
         self._shader = 0
+        # Film::get_aov_offset (film.cpp:691-712): AOV name -> (is_color, index
+        # among the film's colour / value AOV passes)
+        self.aov_slots: dict[str, tuple[bool, int]] = {}
 
     def attribute(self, key) -> int:
         """SVMCompiler::attribute: the kernel's id for a standard attribute
@@ -790,17 +803,40 @@ class SVMCompiler:
             if _has_bump(sh):
                 # the bump program (svm.cpp:864-868, compile_type SHADER_TYPE_BUMP:
                 # the graph feeding the output's Normal, no NODE_END) falls
-                # through into the surface program
-                setn = nodes.bump_from_displacement(sh.displacement)
+                # through into the surface program.  Method "both" (svm.cpp:744-750,
+                # 811-813): the graph is finalized with the bump in object space
+                # (graph.cpp bump_from_displacement(use_object_space)) and wrapped
+                # in NODE_ENTER_BUMP_EVAL / NODE_LEAVE_BUMP_EVAL, which evaluate it
+                # at the undisplaced position (SVM_BUMP_EVAL_STATE_SIZE = 9 floats
+                # of saved P, dP.dx, dP.dy, reserved first)
+                both = _displacement_method(sh) == "both"
+                state = self.alloc(SVM_BUMP_EVAL_STATE_SIZE) if both else SVM_STACK_INVALID
+                if both:
+                    self.nodes.append((NODE_ENTER_BUMP_EVAL, state, 0, 0))
+                setn = nodes.bump_from_displacement(sh.displacement, object_space=both)
                 self.nc = self._node_compiler([setn], background=False)
                 self.nc.link(setn, "vector")
+                if both:
+                    self.nodes.append((NODE_LEAVE_BUMP_EVAL, state, 0, 0))
                 self.stack_top = 0
                 self.stack_used = [False] * SVM_STACK_SIZE
             socks = sh.sockets()
-            self.nc = self._node_compiler([v for v, _ in socks], background=sh is world)
+            # AOV outputs with a pass (OutputAOVNode::simplify: slot >= 0)
+            aovs = [(name, v) for name, v in (getattr(sh, "aovs", None) or {}).items() if name in self.aov_slots]
+            self.nc = self._node_compiler([v for v, _ in socks] + [v for _, v in aovs if nodes.is_linked(v)],
+                                          background=sh is world)
             for v, t in socks:
                 self.nc.link(v, t)
             self.nodes.extend(self.emit_closure(sh, SVM_STACK_INVALID))
+            if aovs and sh is not world:
+                # svm.cpp:782-806: NODE_AOV_START (the kernel stops here unless
+                # the camera path's first hit), then each AOV output's
+                # dependencies and its OutputAOVNode::compile
+                self.nodes.append((NODE_AOV_START, 0, 0, 0))
+                for name, v in aovs:
+                    is_color, slot = self.aov_slots[name]
+                    off = self.nc.assign(v, "color" if is_color else "float")
+                    self.nodes.append((NODE_AOV_COLOR if is_color else NODE_AOV_VALUE, off, slot, 0))
             self.nodes.append((NODE_END, 0, 0, 0))
             vol = getattr(sh, "volume", None)
             vol_start = 0
@@ -829,6 +865,9 @@ class SVMCompiler:
                 off = self.nc.link(disp, "vector")
                 self.nodes.append((NODE_SET_DISPLACEMENT, off, 0, 0))
                 self.nodes.append((NODE_END, 0, 0, 0))
+            if nodes.is_linked(disp) and _displacement_method(sh) == "both":
+                # Shader::attributes (shader.cpp:349-350): after the nodes' requests
+                self.attribute(ATTR_STD_POSITION_UNDISPLACED)
         self.nc = None
         return np.array(self.nodes, dtype=np.uint32).reshape(-1, 4)
 
@@ -865,6 +904,16 @@ class Mesh:
     # KernelParticle fields index, age, lifetime, size, rotation (4),
     # location, velocity, angular_velocity (3 each); None: particle 0
     particle: dict | None = None
+    # (V, 3) vertex positions before true displacement moved them
+    # (Mesh::add_undisplaced, mesh.cpp:535-560, copies the verts before
+    # MeshManager::displace runs): ATTR_STD_POSITION_UNDISPLACED, requested by
+    # shaders with displacement method "both" (shader.cpp:349-350); None: the
+    # verts themselves (nothing displaced them)
+    undisplaced: np.ndarray | None = None
+    # (3, 4) ATTR_STD_GENERATED_TRANSFORM (element MESH, three float4 rows; the
+    # texture space of volume meshes, read by volume_normalized_position for
+    # an object-space Point Density node); None: no such attribute
+    generated_transform: np.ndarray | None = None
 
 
 @dataclass
@@ -1009,6 +1058,9 @@ class Scene:
     world_volume: "Closure | None" = None
     # Film exposure (film.cpp:363; applied by film convert)
     exposure: float = 1.0
+    # AOV passes of the view layer (BlenderSync::sync_render_passes,
+    # Pass::add(PASS_AOV_COLOR / PASS_AOV_VALUE, name)): (name, "color" | "value")
+    aovs: list = field(default_factory=list)
     # Film "Transparent" (Background::transparent, background.cpp:112): camera
     # rays that leave the scene, and holdouts, make the pixel transparent
     # (alpha = 1 - L_transparent) instead of showing the world
@@ -1021,15 +1073,15 @@ def _has_displacement(m) -> bool:
 
 def _displacement_method(m) -> str:
     method = getattr(m, "displacement_method", "true")
-    if method not in ("true", "bump"):
-        raise ValueError(f"displacement_method {method!r}: true or bump ('both' needs displaced meshes)")
+    if method not in ("true", "bump", "both"):
+        raise ValueError(f"displacement_method {method!r}: true, bump or both")
     return method
 
 
 def _has_bump(m) -> bool:
-    """svm.cpp:836-837 has_bump: bump displacement with both the surface and
-    the displacement outputs linked."""
-    return (m is not None and _has_displacement(m) and _displacement_method(m) == "bump"
+    """svm.cpp:836-837 has_bump: displacement method "bump" or "both" with both
+    the surface and the displacement outputs linked."""
+    return (m is not None and _has_displacement(m) and _displacement_method(m) != "true"
             and m.kind not in ("none", "background"))
 
 
@@ -1087,7 +1139,10 @@ class DeviceScene:
             info[i, 2] = _nodes.IMAGE_DATA_TYPES.index(im.data_type)
             info[i, 4] = _nodes.INTERPOLATIONS.index(im.interpolation)
             info[i, 5] = _nodes.EXTENSIONS.index(im.extension)
-            info[i, 6], info[i, 7], info[i, 8] = a.shape[1], a.shape[0], 1
+            info[i, 6], info[i, 7], info[i, 8] = im.dims()
+            if im.transform_3d is not None:
+                info[i, 9] = 1  # use_transform_3d; transform_3d at byte 48
+                info[i, 12:24] = np.asarray(im.transform_3d, dtype=np.float32).reshape(12).view(np.uint32)
         return info.view(np.uint8).reshape(-1), keep
 
 
@@ -1339,6 +1394,15 @@ def compile_scene(scene: Scene) -> DeviceScene:
     world = background(scene.world_color, scene.world_strength)
     world.volume = scene.world_volume
     svm_compiler = SVMCompiler()
+    n_color = n_value = 0
+    for name, kind in scene.aovs:
+        if kind not in ("color", "value"):
+            raise ValueError(f"AOV {name!r}: kind must be color or value")
+        if name in svm_compiler.aov_slots:
+            continue  # Pass::add: one pass per name and type
+        svm_compiler.aov_slots[name] = (kind == "color", n_color if kind == "color" else n_value)
+        n_color += kind == "color"
+        n_value += kind == "value"
     svm = svm_compiler.compile(mats, world)
     n_shaders = len(mats) + 1
     kshaders = (abi.KernelShader * n_shaders)()
@@ -1629,14 +1693,43 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.display_divide_pass_stride = -1
     kf.use_display_exposure = 1 if kf.exposure != 1.0 else 0
     kf.use_display_pass_alpha = 1
+    # Film::device_update (film.cpp:425-625): the passes in the order
+    # BlenderSync::sync_render_passes adds them (combined, the AOVs, the
+    # adaptive sampling passes), stable-sorted by component count (Pass::add,
+    # film.cpp:263-266: 4-float passes first), offsets in that order, the
+    # stride aligned to 4 floats; pass_flag |= 1 << type.  PassType numbers
+    # (kernel_types.h:354-376 without __KERNEL_DEBUG__): AOV_COLOR 11,
+    # AOV_VALUE 12, ADAPTIVE_AUX_BUFFER 13, SAMPLE_COUNT 14.
+    passes = [("combined", 1, 4)]
+    seen = set()
+    for name, kind in scene.aovs:
+        if name not in seen:
+            seen.add(name)
+            passes.append(("aov_color", 11, 4) if kind == "color" else ("aov_value", 12, 1))
     if scene.adaptive_sampling:
-        # film.cpp:568-573 pass offsets, :621 stride aligned to 4 floats
-        kf.pass_adaptive_aux_buffer = 4
-        kf.pass_sample_count = 8
-        kf.pass_stride = 12
-        # film.cpp:447-450: 1 << type for PASS_ADAPTIVE_AUX_BUFFER (13) and
-        # PASS_SAMPLE_COUNT (14), kernel_types.h:354-376 without __KERNEL_DEBUG__
-        kf.pass_flag = PASSMASK_COMBINED | (1 << 13) | (1 << 14)
+        passes += [("adaptive_aux_buffer", 13, 4), ("sample_count", 14, 1)]
+    passes.sort(key=lambda p: -p[2])  # stable
+    stride = 0
+    kf.pass_flag = 0
+    kf.pass_aov_color_num = kf.pass_aov_value_num = 0
+    for kind, ptype, comps in passes:
+        kf.pass_flag |= 1 << ptype
+        if kind == "combined":
+            kf.pass_combined = stride
+        elif kind == "aov_color":
+            if kf.pass_aov_color_num == 0:
+                kf.pass_aov_color = stride
+            kf.pass_aov_color_num += 1
+        elif kind == "aov_value":
+            if kf.pass_aov_value_num == 0:
+                kf.pass_aov_value = stride
+            kf.pass_aov_value_num += 1
+        elif kind == "adaptive_aux_buffer":
+            kf.pass_adaptive_aux_buffer = stride
+        else:
+            kf.pass_sample_count = stride
+        stride += comps
+    kf.pass_stride = -(-stride // 4) * 4
     lookup = filter_table(scene.filter_type, scene.filter_width)
     kd.tables.beckmann_offset = 0
     if any(t in BECKMANN_CLOSURES for m in mats for t in m.closure_types()):
@@ -1757,7 +1850,7 @@ def _volume_attribute_dependency(v) -> bool:
                for s, _ in v.sockets() for n in _nodes.upstream(s))
 
 
-_ATTR_TYPES = {"float": 0, "float2": 1, "float3": 2, "rgba": 3}  # NodeAttributeType
+_ATTR_TYPES = {"float": 0, "float2": 1, "float3": 2, "rgba": 3, "matrix": 4}  # NodeAttributeType
 _ATTR_ELEMENTS = {"object": 1, "mesh": 2, "face": 3, "vertex": 4, "corner": 6, "corner_byte": 7, "curve": 8,
                   "curve_key": 9}
 
@@ -1793,6 +1886,19 @@ def _mesh_attribute(gm: dict, key):
         return "corner", "float2", np.asarray(m.uv, dtype=np.float32).reshape(3 * T, 2)
     if key == _nodes_mod.ATTR_STD_GENERATED:
         return "vertex", "float3", _generated_coordinates(m)
+    if key == _nodes_mod.ATTR_STD_GENERATED_TRANSFORM:
+        if m.generated_transform is None:
+            return None
+        return "mesh", "matrix", np.asarray(m.generated_transform, dtype=np.float32).reshape(3, 4)
+    if key == ATTR_STD_POSITION_UNDISPLACED:
+        # Mesh::add_undisplaced: the verts before displacement, in the space the
+        # geometry's verts are stored in (transform applied or not)
+        if m.undisplaced is None:
+            return "vertex", "float3", np.asarray(gm["v"], dtype=np.float32)
+        u = np.asarray(m.undisplaced, dtype=np.float32).reshape(-1, 3)
+        if gm.get("tfm") is not None and len(u):
+            u = np.stack([transform_point_f32(gm["tfm"], p) for p in u]).astype(np.float32)
+        return "vertex", "float3", u
     if key == _nodes_mod.ATTR_STD_VERTEX_NORMAL or key == "N":
         # Mesh::add_vertex_normals: the normals __tri_vnormal holds
         return "vertex", "float3", np.asarray(gm["nrm"], dtype=np.float32)
@@ -1881,7 +1987,7 @@ def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobje
                 rows.append((aid, 0, 0, 0))
             else:
                 element, kind, a = found
-                store = "uchar4" if kind == "rgba" else "float3" if kind == "float3" else kind
+                store = "uchar4" if kind == "rgba" else "float3" if kind in ("float3", "matrix") else kind
                 if kind == "float3":
                     a4 = np.zeros((a.shape[0], 4), dtype=np.float32)
                     a4[:, :3] = a
@@ -2041,7 +2147,8 @@ def _pack_geometry(scene: Scene) -> dict:
         tfm = np.asarray(inst.tfm, dtype=np.float64).reshape(3, 4)
         if users[id(inst.mesh)] == 1:
             v, t, sh, nrm = _mesh_arrays(inst.mesh, tfm.astype(np.float32))
-            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True, mesh=inst.mesh))
+            geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True, mesh=inst.mesh,
+                              tfm=tfm.astype(np.float32)))
             objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True,  # tfm reset on apply
                                 **_instance_props(inst)))
             continue

@@ -914,6 +914,62 @@ def bump_displace(width=40, height=40, samples=8) -> sc.Scene:
     return s
 
 
+def bump_both(width=40, height=40, samples=8) -> sc.Scene:
+    """Displacement method "both" (golden parity case): true displacement moved
+    the meshes' vertices (stand-in for MeshManager::displace: each vertex pushed
+    along its direction from the body's centre by a wave of its position) and
+    kept their undisplaced positions (Mesh::add_undisplaced,
+    ATTR_STD_POSITION_UNDISPLACED); the bump program from the same Displacement
+    output then runs at the undisplaced position (svm.cpp:744-750,
+    NODE_ENTER_BUMP_EVAL / NODE_LEAVE_BUMP_EVAL, the Bump node in object space).
+    Two world-space meshes (one smooth), a geometry instanced twice (undisplaced
+    positions in object space, moved to world space by the instance transform)
+    and a mesh whose material has method "both" but was not displaced (its
+    undisplaced positions are its verts)."""
+    import dataclasses
+
+    from . import nodes as nd
+
+    s = cornell_instanced(width, height, samples)
+    pos = nd.separate_xyz(nd.geometry()["Position"])
+    noise = nd.noise_texture(None, scale=0.05, detail=2.0)["Fac"]
+    wave = nd.math("sine", nd.math("multiply", pos["Y"], 0.11))
+    base = len(s.materials)
+    s.materials = list(s.materials) + [
+        dataclasses.replace(sc.diffuse((0.7, 0.6, 0.5)), displacement=nd.displacement(noise, 0.5, 10.0, space="object"),
+                            displacement_method="both"),
+        dataclasses.replace(sc.glossy((0.8, 0.8, 0.9), 0.25), displacement=nd.displacement(wave, 0.5, 6.0,
+                                                                                            space="world"),
+                            displacement_method="both"),
+        dataclasses.replace(sc.mix(0.3, sc.glass((0.95, 0.95, 1.0), 0.1, ior=1.4), sc.diffuse((0.3, 0.5, 0.8))),
+                            displacement=nd.vector_displacement(nd.combine_xyz(wave, noise, 0.0), 0.0, 4.0,
+                                                                space="world"),
+                            displacement_method="both"),
+    ]
+
+    def displaced(center, radii, nu, nv, shader, amp, smooth, tfm_space=False):
+        v, t = _ellipsoid(center, radii, nu, nv)
+        v = np.asarray(v, dtype=np.float32)
+        d = v - np.asarray(center, dtype=np.float32)
+        d = d / np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-6)
+        h = (amp * np.sin(v[:, 0] * (0.35 if tfm_space else 0.08)) * np.cos(v[:, 2] * (0.3 if tfm_space else 0.07)))
+        dv = (v + d * h[:, None].astype(np.float32)).astype(np.float32)
+        return sc.Mesh(dv, t, shader=shader, smooth=smooth, undisplaced=v)
+
+    s.meshes = list(s.meshes) + [
+        displaced((120.0, 80.0, 300.0), (60.0, 58.0, 60.0), 20, 12, base, 6.0, False),
+        displaced((440.0, 380.0, 400.0), (62.0, 60.0, 62.0), 22, 12, base + 1, 5.0, True),
+        sc.Mesh(*_ellipsoid((300.0, 120.0, 160.0), (55.0, 50.0, 55.0), 18, 10), shader=base + 2, smooth=True),
+    ]
+    inst = displaced((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), 16, 10, base, 0.12, True, tfm_space=True)
+    s.instances = list(s.instances) + [
+        sc.Instance(inst, _tfm((260.0, 300.0, 420.0), 0.4, (50.0, 40.0, 50.0))),
+        sc.Instance(inst, _tfm((470.0, 120.0, 330.0), -0.7, (40.0, 55.0, 40.0))),
+    ]
+    s.name = "bump_both"
+    return s
+
+
 def shading_holdout(width=48, height=48, samples=8) -> sc.Scene:
     """Holdouts with a transparent film (kernel_path.h:285-296 with
     shader_holdout_apply, kernel_shader.h:1020-1050): a Holdout closure mixed
@@ -1158,6 +1214,53 @@ def volume_cornell(width=48, height=48, samples=8, heterogeneous=False) -> sc.Sc
     s.world_volume = fog
     s.lamps = [sc.Lamp("point", co=(100.0, 450.0, 100.0), size=25.0, color=(1.0, 0.9, 0.8), strength=2.0e6)]
     s.name = "volume_hetero" if heterogeneous else "volume_cornell"
+    return s
+
+
+def voxel_cornell(width=40, height=40, samples=8) -> sc.Scene:
+    """Point Density textures (golden parity case; NODE_TEX_VOXEL, svm_voxel.h,
+    3D textures through kernel_tex_image_interp_3d): a volume box whose
+    scattering density and colour come from a 12x10x8 float4 voxel grid in
+    world space (the node's transform maps the box to the unit cube; linear,
+    clip extension), a diffuse ellipsoid coloured by another grid in object
+    space (instanced twice, its mesh with a generated-texture transform:
+    volume_normalized_position; tricubic, repeat), and a glossy box coloured
+    by a closest-interpolated grid (extend) whose TextureInfo carries a 3D
+    transform (use_transform_3d)."""
+    from . import nodes as nd
+
+    rng = np.random.default_rng(0x5EED + 87)
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+
+    def grid(d, h, w):
+        g = rng.random((d, h, w, 4), dtype=np.float64).astype(np.float32)
+        g[..., 3] *= 0.02  # density (alpha)
+        return g
+
+    g1 = nd.Image(pixels=grid(8, 10, 12), data_type="float4", interpolation="linear", extension="clip", depth=8)
+    lo, size = np.array([80.0, 180.0, 220.0]), np.array([200.0, 220.0, 180.0])
+    tfm = np.zeros((3, 4))
+    tfm[:, :3] = np.diag(1.0 / size)
+    tfm[:, 3] = -lo / size
+    pd1 = nd.point_density(g1, space="world", tfm=tfm)
+    smoke = sc.material(volume=sc.volume_scatter(pd1["Color"], density=pd1["Density"], anisotropy=0.3))
+    g2 = nd.Image(pixels=grid(6, 7, 9), data_type="float4", interpolation="cubic", extension="repeat", depth=6)
+    pd2 = nd.point_density(g2, space="object")
+    tinted = sc.diffuse(pd2["Color"])
+    g3 = nd.Image(pixels=grid(5, 4, 6), data_type="float4", interpolation="closest", extension="extend", depth=5,
+                  transform_3d=np.array([[0.004, 0.0, 0.0, -0.8], [0.0, 0.005, 0.0, -0.2], [0.0, 0.0, 0.003, -0.6]]))
+    pd3 = nd.point_density(g3, space="world")
+    shiny = sc.glossy(pd3["Color"], 0.3)
+    s.materials.extend([smoke, tinted, shiny])
+    s.meshes.append(sc.Mesh(*_box(tuple(lo + size / 2), tuple(size), 0.0), shader=base))
+    s.meshes.append(sc.Mesh(*_box((410.0, 100.0, 150.0), (110, 200, 110), 0.4), shader=base + 2))
+    ev, et = _ellipsoid((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), 20, 12)
+    ell = sc.Mesh(ev, et, shader=base + 1, smooth=True,
+                  generated_transform=np.array([[0.5, 0.0, 0.0, 0.5], [0.0, 0.5, 0.0, 0.5], [0.0, 0.0, 0.5, 0.5]]))
+    s.instances = [sc.Instance(ell, _tfm((380.0, 380.0, 420.0), 0.3, (70.0, 55.0, 70.0))),
+                   sc.Instance(ell, _tfm((170.0, 90.0, 420.0), -0.5, (60.0, 60.0, 45.0)))]
+    s.name = "voxel_cornell"
     return s
 
 
@@ -1621,6 +1724,47 @@ def transparent_shadows(width=48, height=48, samples=8) -> sc.Scene:
     s.meshes.append(sc.Mesh(*_quad((80, 20, 80), (250, 20, 80), (250, 250, 160), (80, 250, 160)), shader=base + 2))
     s.lamps = [sc.Lamp(kind="point", co=(400.0, 500.0, 250.0), color=(1.0, 0.95, 0.9), strength=2.0e5, size=10.0)]
     s.name = "transparent_shadows"
+    return s
+
+
+def shading_aov(width=40, height=40, samples=8) -> sc.Scene:
+    """AOV outputs (golden parity case; NODE_AOV_START / _COLOR / _VALUE,
+    svm_aov.h, film AOV passes after the combined pass): colour and value AOVs
+    from constants, a noise texture and a Fresnel node on the Cornell box's
+    materials; a pane 30 % transparent (alpha 0.7 >= the film's alpha
+    threshold: the first hit ends the AOV writes) and one 80 % transparent
+    (alpha 0.2: the surface behind writes its AOVs too, PATH_RAY_SINGLE_PASS_DONE
+    unset); a glass sphere (refracted rays are no camera rays); an AOV output
+    without a pass (dropped) and a pass no material writes (zero)."""
+    import dataclasses
+
+    from . import nodes as nd
+
+    s = cornell_box(width, height, samples)
+    noise = nd.noise_texture(None, scale=0.03, detail=2.0)
+    fres = nd.fresnel(1.5)
+    mats = list(s.materials)
+    for i, m in enumerate(mats):
+        col = m.color if isinstance(m.color, tuple) else (0.5, 0.5, 0.5)
+        mats[i] = dataclasses.replace(m, aovs={"albedo": col, "mask": float(i) * 0.25, "unused": (1.0, 0.0, 0.0)})
+    base = len(mats)
+    mats.append(dataclasses.replace(sc.diffuse(noise["Color"]),
+                                    aovs={"albedo": noise["Color"], "mask": fres, "fac": noise["Fac"]}))
+    mats.append(dataclasses.replace(sc.mix(0.3, sc.diffuse((0.2, 0.6, 0.3)), sc.transparent((0.9, 0.9, 0.9))),
+                                    aovs={"albedo": (0.2, 0.6, 0.3), "mask": 2.0}))
+    mats.append(dataclasses.replace(sc.mix(0.8, sc.diffuse((0.7, 0.2, 0.2)), sc.transparent((0.9, 0.9, 0.9))),
+                                    aovs={"albedo": (0.7, 0.2, 0.2), "mask": 3.0, "fac": fres}))
+    mats.append(dataclasses.replace(sc.glass((1.0, 1.0, 1.0), 0.0, ior=1.45), aovs={"mask": 4.0}))
+    s.materials = mats
+    s.meshes.append(sc.Mesh(*_ellipsoid((150.0, 100.0, 300.0), (80.0, 80.0, 80.0), 20, 12), shader=base,
+                            smooth=True))
+    s.meshes.append(sc.Mesh(*_quad((300, 60, 200), (480, 60, 200), (480, 260, 240), (300, 260, 240)), shader=base + 1))
+    s.meshes.append(sc.Mesh(*_quad((120, 280, 180), (320, 280, 180), (320, 470, 220), (120, 470, 220)),
+                            shader=base + 2))
+    s.meshes.append(sc.Mesh(*_ellipsoid((420.0, 380.0, 380.0), (70.0, 70.0, 70.0), 20, 12), shader=base + 3,
+                            smooth=True))
+    s.aovs = [("albedo", "color"), ("mask", "value"), ("fac", "value"), ("spare", "color")]
+    s.name = "shading_aov"
     return s
 
 

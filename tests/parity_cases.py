@@ -95,6 +95,11 @@ CASES = {
     "shading_bump_paths": lambda: scenes.bump_paths(40, 40, 8),
     # displacement method "bump": the bump program from the Displacement output
     "shading_bump_displace": lambda: scenes.bump_displace(40, 40, 8),
+    # displacement method "both": bump program at the undisplaced positions
+    # (NODE_ENTER_BUMP_EVAL / NODE_LEAVE_BUMP_EVAL, ATTR_STD_POSITION_UNDISPLACED)
+    "shading_bump_both": lambda: scenes.bump_both(40, 40, 8),
+    # AOV outputs into the film's AOV passes (svm_aov.h, film.cpp pass layout)
+    "shading_aov": lambda: scenes.shading_aov(40, 40, 8),
     # shader ray tracing: Ambient Occlusion and Bevel nodes (svm_ao.h, svm_bevel.h)
     "shading_raytrace": lambda: scenes.shading_raytrace(40, 40, 8),
     # holdouts with a transparent film: Holdout closure, object holdout (also
@@ -112,6 +117,9 @@ CASES = {
     # heterogeneous: texture-driven densities, ray marching
     "volume_cornell": lambda: scenes.volume_cornell(48, 48, 8),
     "volume_hetero": lambda: scenes.volume_cornell(32, 32, 4, heterogeneous=True),
+    # Point Density textures (svm_voxel.h): 3D textures in a volume density and
+    # on surfaces, object / world space, closest / linear / tricubic
+    "shading_voxel": lambda: scenes.voxel_cornell(40, 40, 8),
     # emitters with node-driven emission (direct_emissive_eval non-constant
     # branch): textured mesh light, Light Falloff / Light Path lamp shaders
     "emission_nodes": lambda: scenes.emission_nodes(48, 48, 8),
@@ -140,6 +148,36 @@ def sky_model(kind):
         return {"configs": g["hosek_configs"], "radiances": g["hosek_radiances"]}
     image = nd.Image(pixels=g["nishita_texture"], data_type="float4", interpolation="linear", extension="extend")
     return {"pixel_bottom": g["nishita_bottom"], "pixel_top": g["nishita_top"], "image": image}
+
+
+def atomic_pass_channels(ds) -> np.ndarray:
+    """Render-buffer channels the GPU adds with float atomics: the AOV passes
+    (svm_aov.h -> kernel_write_pass_float*, an atomic add on the reference's
+    GPU devices too, kernel_write_passes.h:21-65).  Their per-pixel sum order
+    follows the GPU's scheduling, so they match the reference's sequential
+    sums to rounding (tolerance below); every other channel is bit-exact."""
+    f = ds.data.film
+    mask = np.zeros(ds.pass_stride, dtype=bool)
+    mask[f.pass_aov_color:f.pass_aov_color + 4 * f.pass_aov_color_num] = f.pass_aov_color_num > 0
+    mask[f.pass_aov_value:f.pass_aov_value + f.pass_aov_value_num] = f.pass_aov_value_num > 0
+    return mask
+
+
+# relative tolerance of the atomically added channels (float32 sums of the
+# same per-sample values in another order; 8-64 samples per pixel)
+ATOMIC_RTOL = 1e-5
+
+
+def buffers_match(ds, a: np.ndarray, b: np.ndarray) -> bool:
+    """Bit-exact on every channel but the atomically added ones, which agree
+    to ATOMIC_RTOL (relative to the pixel's channel magnitude)."""
+    m = atomic_pass_channels(ds)
+    if not np.array_equal(a[..., ~m].view(np.uint32), b[..., ~m].view(np.uint32)):
+        return False
+    if m.any():
+        x, y = a[..., m].astype(np.float64), b[..., m].astype(np.float64)
+        return bool(np.all(np.abs(x - y) <= ATOMIC_RTOL * np.maximum(np.abs(y), 1.0)))
+    return True
 
 
 # Cases whose __sample_pattern_lut is the reference host's table (fixture)

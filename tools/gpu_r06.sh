@@ -45,4 +45,15 @@ if [[ $MODE == itrace ]]; then
     head -n 12 $OUT/itrace_$m.txt
   done
 fi
+if [[ $MODE == tailsweep ]]; then
+  # fused-tail thresholds: whole frame and the N = 8 / N = 2 row shards
+  for t in ${TAILS:-0 32768 131072 524288 4194304}; do
+    for m in frame shard8 shard2; do
+      step "tail_${m}_$t" 300 python3 tools/render_modes.py $m --frames 5 --tail $t
+    done
+  done
+fi
+if [[ $MODE == harness ]]; then
+  step pytest_harness 900 python -u -m pytest -v -m gpu --timeout 600 --timeout-method thread tests/test_plugin_harness.py "$@"
+fi
 echo done
