@@ -1527,6 +1527,9 @@ struct hipcy_device {
   bool shade_tex = false;             /* some shader uses texture / converter / input nodes */
   bool use_volumes = false;           /* KernelIntegrator.use_volumes: the volume shading / shadow kernels */
   bool use_disk_bssrdf = false;       /* disk BSSRDFs: the slots' subsurface indirect-ray records */
+  bool sss_pool_vol = false;          /* ... sized with their volume stacks */
+  bool use_catcher = false;           /* shadow-catcher objects: the slots' catcher records */
+  char *catcher_pool = nullptr;       /* those records (CY_CATCHER_F4 float4 per slot) */
   char *sss_pool = nullptr;           /* those records and their depths */
   bool use_ray_diff = false;          /* a shader reads ray differentials (Bump / *_BUMP_DX / _DY nodes) */
   char *diff_pool = nullptr;          /* the slots' ray and shadow-ray differentials */
@@ -1742,8 +1745,15 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     hipFree(dev->sss_pool);
     dev->sss_pool = nullptr;
   }
+  if (dev->catcher_pool) {
+    hipFree(dev->catcher_pool);
+    dev->catcher_pool = nullptr;
+  }
+  dev->bufs.catcher = nullptr;
   dev->bufs.sss_rec = nullptr;
+  dev->bufs.sss_vol = nullptr;
   dev->bufs.sss_count = nullptr;
+  dev->sss_pool_vol = false;
   if (dev->diff_pool) {
     hipFree(dev->diff_pool);
     dev->diff_pool = nullptr;
@@ -1781,6 +1791,17 @@ static int ensure_volume_capacity(hipcy_device *dev)
   return 0;
 }
 
+/* The slots' shadow-catcher records (cy_integrator.h CyCatcher, 48 B per
+ * slot), for scenes with shadow-catcher objects only. */
+static int ensure_catcher_capacity(hipcy_device *dev)
+{
+  if (dev->use_catcher && !dev->catcher_pool) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->catcher_pool, (size_t)16 * CY_CATCHER_F4 * dev->capacity));
+  }
+  dev->bufs.catcher = dev->use_catcher ? (hc_float4 *)dev->catcher_pool : nullptr;
+  return 0;
+}
+
 /* The slots' subsurface indirect-ray records (cy_integrator.h CY_SSS_RECS x
  * CY_SSS_REC_F4 float4 and a depth per slot, 292 B), for scenes with disk
  * BSSRDFs only.  Every path leaves its slot with depth 0, so the depths are
@@ -1789,13 +1810,24 @@ static int ensure_sss_capacity(hipcy_device *dev)
 {
   const size_t recs = (size_t)16 * CY_SSS_RECS * CY_SSS_REC_F4 * dev->capacity;
   const size_t counts = 4 * dev->capacity;
+  /* volume scenes: each record's volume stack and the pending shadow's
+   * (CY_SSS_RECS + 1 stacks of CY_VOLUME_STACK / 2 records, 512 B per slot) */
+  const bool vol = dev->use_disk_bssrdf && dev->use_volumes;
+  const size_t stacks = vol ? (size_t)16 * (CY_SSS_RECS + 1) * (CY_VOLUME_STACK / 2) * dev->capacity : 0;
+  if (dev->sss_pool && vol && !dev->sss_pool_vol) {
+    /* sized for a scene without volumes (no path is in flight between renders) */
+    HIP_CHECK(dev, hipFree(dev->sss_pool));
+    dev->sss_pool = nullptr;
+  }
   if (dev->use_disk_bssrdf && !dev->sss_pool) {
-    HIP_CHECK(dev, hipMalloc((void **)&dev->sss_pool, recs + counts));
-    HIP_CHECK(dev, hipMemset(dev->sss_pool + recs, 0, counts));
+    HIP_CHECK(dev, hipMalloc((void **)&dev->sss_pool, recs + stacks + counts));
+    HIP_CHECK(dev, hipMemset(dev->sss_pool + recs + stacks, 0, counts));
+    dev->sss_pool_vol = vol;
   }
   /* other scenes' shading never looks at the records */
   dev->bufs.sss_rec = dev->use_disk_bssrdf ? (hc_float4 *)dev->sss_pool : nullptr;
-  dev->bufs.sss_count = dev->use_disk_bssrdf ? (uint *)(dev->sss_pool + recs) : nullptr;
+  dev->bufs.sss_vol = vol ? (hc_uint4 *)(dev->sss_pool + recs) : nullptr;
+  dev->bufs.sss_count = dev->use_disk_bssrdf ? (uint *)(dev->sss_pool + recs + stacks) : nullptr;
   return 0;
 }
 
@@ -1923,6 +1955,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->pool) hipFree(dev->pool);
   if (dev->vol_pool) hipFree(dev->vol_pool);
   if (dev->sss_pool) hipFree(dev->sss_pool);
+  if (dev->catcher_pool) hipFree(dev->catcher_pool);
   if (dev->diff_pool) hipFree(dev->diff_pool);
   if (dev->srec_pool) hipFree(dev->srec_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
@@ -2688,9 +2721,6 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.cam.interocular_offset != 0.0f) why = "stereo";
   else if (d.integrator.sampling_pattern != 0) why = "only the Sobol pattern";
   else if (d.integrator.branched) why = "branched path tracing";
-  else if (d.integrator.use_volumes && d.integrator.volume_decoupled)
-    why = "decoupled volume ray marching (a CPU-device setting: GPU devices set volume_decoupled 0)";
-  else if (d.integrator.use_volumes && d.cam.is_inside_volume) why = "camera inside a volume object";
   else if (d.integrator.use_volumes && !d.integrator.transparent_shadows)
     why = "volumes without transparent shadows (shader.cpp:529-536 sets them for every volume shader)";
   else if (d.integrator.transparent_shadows && d.integrator.transparent_max_bounce > CY_SHADOW_MAX_HITS)
@@ -2798,12 +2828,21 @@ int hipcy_load_kernels(hipcy_device *dev)
     return set_error(dev, "load_kernels: unsupported shader: " + why);
   }
   /* kernel_path_shader_apply (kernel_path.h:254-283): shadow-catcher objects
-   * need the shadow-catcher radiance terms, refused before the first launch
-   * rather than mid-frame */
+   * take the extended shading kernels (the catcher's part of PathRadiance per
+   * slot, the all-lights connection behind a catcher) */
+  dev->use_catcher = false;
   for (uint32_t f : dev->object_flags) {
-    if (f & SD_OBJECT_SHADOW_CATCHER) {
-      return set_error(dev, "load_kernels: unsupported scene feature: shadow catcher objects");
+    dev->use_catcher |= (f & SD_OBJECT_SHADOW_CATCHER) != 0;
+  }
+  if (dev->use_catcher) {
+    if (d.integrator.use_volumes) {
+      return set_error(dev, "load_kernels: unsupported scene feature: shadow catcher objects in a scene with volumes");
     }
+    if (uses_bssrdf) {
+      return set_error(dev, "load_kernels: unsupported scene feature: shadow catcher objects with subsurface "
+                            "scattering");
+    }
+    dev->shade_tex = true;
   }
   dev->use_volumes = d.integrator.use_volumes != 0;
   dev->use_disk_bssrdf = uses_disk_bssrdf;
@@ -2813,10 +2852,9 @@ int hipcy_load_kernels(hipcy_device *dev)
     /* the volume stack of a path holds the world and every volume object it
      * is inside of (plus the terminator) */
     size_t volume_objects = 0;
-    bool intersects_volume = false, volume_attributes = false;
+    bool volume_attributes = false;
     for (uint32_t f : dev->object_flags) {
       volume_objects += (f & SD_OBJECT_HAS_VOLUME) ? 1 : 0;
-      intersects_volume |= (f & SD_OBJECT_INTERSECTS_VOLUME) != 0;
       volume_attributes |= (f & SD_OBJECT_HAS_VOLUME_ATTRIBUTES) != 0;
     }
     /* the volume stack's shaders evaluate into one closure array (merged
@@ -2834,12 +2872,6 @@ int hipcy_load_kernels(hipcy_device *dev)
     }
     else if (volume_attributes) {
       why = "volume attributes (voxel grids)";
-    }
-    else if (uses_disk_bssrdf) {
-      why = "disk BSSRDFs (cubic / gaussian / burley, principled burley) in a scene with volumes";
-    }
-    else if (uses_bssrdf && intersects_volume) {
-      why = "subsurface scattering on objects that intersect volume objects (volume stack update of the walk)";
     }
     else if (volume_objects && dev->globals.find("__object_volume_step") == dev->globals.end()) {
       why = "volume objects without __object_volume_step";
@@ -3443,7 +3475,8 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
   }
   const size_t items = npix * per_pass;
   if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 || ensure_catcher_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
+      ensure_srec_capacity(dev) != 0 ||
       ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
   }
@@ -3896,7 +3929,7 @@ static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
 static int stream_pool(hipcy_device *dev, size_t slots)
 {
   if (ensure_capacity(dev, slots) != 0 || ensure_volume_capacity(dev) != 0 || ensure_sss_capacity(dev) != 0 ||
-      ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
+      ensure_catcher_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
     return -1;
   }
   return 0;

@@ -58,6 +58,10 @@ typedef struct CyPathBuffers {
    * CY_SSS_RECS records of CY_SSS_REC_F4 float4 per slot, and its depth */
   hc_float4 *sss_rec;
   uint *sss_count;
+  /* ... in scenes with volumes too: each record's volume stack
+   * (CY_VOLUME_STACK / 2 records), and one more per slot for the stack the
+   * pending shadow ray of a path that handed its slot to a record sees */
+  hc_uint4 *sss_vol;
   /* scenes whose shaders read ray differentials (CyGlobals.use_ray_diff): the
    * path ray's dP / dD, CY_RAY_DIFF_F4 float4 per slot (written when the ray
    * is made; a camera launch's first shade recomputes them), and the shading
@@ -71,7 +75,25 @@ typedef struct CyPathBuffers {
    * and their count, or CY_SREC_BLOCKED / CY_SREC_NONE (traverse here) */
   hc_float4 *shadow_hits;
   uint *shadow_nrec;
+  /* scenes with shadow catcher objects: the path's shadow-catcher record of
+   * PathRadiance (kernel_types.h:540-556), CY_CATCHER_F4 float4 per slot */
+  hc_float4 *catcher;
 } CyPathBuffers;
+
+/* The shadow-catcher part of PathRadiance (kernel_accumulate.h:203-233,
+ * 526-620): the light a path behind a catcher would have received, shadowed
+ * and unshadowed, the background seen through the catcher and the catcher's
+ * throughput. */
+typedef struct CyCatcher {
+  cfloat3 path_total, path_total_shaded, background;
+  float throughput, transparency;
+  int has;
+  int film_transparent; /* KernelBackground.transparent (not stored) */
+} CyCatcher;
+#define CY_CATCHER_F4 3
+/* the kernels that render shadow catchers (hipcy_load_kernels picks them) */
+#define CY_CATCHER (CY_CLOSURE_EXT && CY_SVM_TEX)
+
 
 #define CY_SHADOW_REC_HITS 4
 #define CY_SREC_BLOCKED 0x100u
@@ -89,6 +111,8 @@ typedef struct CyPathBuffers {
 #define CY_VOP_PATH 1u       /* apply to the path's stack at its next shade */
 #define CY_VOP_SHADOW 2u     /* apply to the shadow ray's copy (kernel_shadow.h:22-45) */
 #define CY_VOP_BACKFACING 4u /* the surface was hit from behind (SD_BACKFACING) */
+#define CY_VOP_OWN_STACK 8u  /* the shadow ray's stack is the slot's sss_vol[CY_SSS_RECS] */
+#define CY_VOP_INIT_CAMERA 16u /* a new path's camera ray sets up the stack (camera inside a volume) */
 
 /* One RenderTile of a multi-tile pass (hipcy_path_trace_tiles), or of a lane's
  * tile stream (hipcy_render_feed). */
@@ -280,8 +304,8 @@ CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathSt
                       int_as_float(s->transmission_bounce)));
   cy_st(&dst[2], mkf4(int_as_float(s->transparent_bounce), s->min_ray_pdf, s->ray_pdf, s->ray_t));
   cy_st(&dst[3], mkf4(ray->P.x, ray->P.y, ray->P.z, ray->t));
-  cy_st(&dst[4], mkf4(ray->D.x, ray->D.y, ray->D.z, 0.0f));
-  cy_st(&dst[5], mkf4(throughput.x, throughput.y, throughput.z, 0.0f));
+  cy_st(&dst[4], mkf4(ray->D.x, ray->D.y, ray->D.z, int_as_float(s->volume_bounce)));
+  cy_st(&dst[5], mkf4(throughput.x, throughput.y, throughput.z, int_as_float(s->volume_bounds_bounce)));
   if (dP) {
     diff_store(&dst[6], *dP, *dD);
   }
@@ -310,8 +334,8 @@ CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals
   s->min_ray_pdf = r2.y;
   s->ray_pdf = r2.z;
   s->ray_t = r2.w;
-  s->volume_bounce = 0;
-  s->volume_bounds_bounce = 0;
+  s->volume_bounce = as_int(r4.w);
+  s->volume_bounds_bounce = as_int(r5.w);
   ray->P = mk3(r3.x, r3.y, r3.z);
   ray->t = r3.w;
   ray->D = mk3(r4.x, r4.y, r4.z);
@@ -321,10 +345,10 @@ CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals
   }
 }
 
-/* The slot's volume stack and pending update records (CyPathBuffers.vol_*). */
-CY_FN void vol_stack_load(const CyPathBuffers *b, int slot, CyVolumeStack *st)
+/* The slot's volume stack and pending update records (CyPathBuffers.vol_*);
+ * a volume stack kept at src / dst (CY_VOLUME_STACK / 2 records). */
+CY_FN void vol_stack_read(const hc_uint4 *src, CyVolumeStack *st)
 {
-  const hc_uint4 *src = b->vol_stack + (size_t)slot * (CY_VOLUME_STACK / 2);
   for (int k = 0; k < CY_VOLUME_STACK / 2; k++) {
     const hc_uint4 r = cy_ld(&src[k]);
     st->e[2 * k].object = (int)r.x;
@@ -337,9 +361,8 @@ CY_FN void vol_stack_load(const CyPathBuffers *b, int slot, CyVolumeStack *st)
   }
 }
 
-CY_FN void vol_stack_store(const CyPathBuffers *b, int slot, const CyVolumeStack *st)
+CY_FN void vol_stack_write(hc_uint4 *dst, const CyVolumeStack *st)
 {
-  hc_uint4 *dst = b->vol_stack + (size_t)slot * (CY_VOLUME_STACK / 2);
   for (int k = 0; k < CY_VOLUME_STACK / 2; k++) {
     hc_uint4 r;
     r.x = (uint)st->e[2 * k].object;
@@ -351,6 +374,22 @@ CY_FN void vol_stack_store(const CyPathBuffers *b, int slot, const CyVolumeStack
       break;
     }
   }
+}
+
+CY_FN void vol_stack_load(const CyPathBuffers *b, int slot, CyVolumeStack *st)
+{
+  vol_stack_read(b->vol_stack + (size_t)slot * (CY_VOLUME_STACK / 2), st);
+}
+
+CY_FN void vol_stack_store(const CyPathBuffers *b, int slot, const CyVolumeStack *st)
+{
+  vol_stack_write(b->vol_stack + (size_t)slot * (CY_VOLUME_STACK / 2), st);
+}
+
+/* record r's volume stack (r == CY_SSS_RECS: the pending shadow ray's) */
+CY_FN hc_uint4 *sss_vol_at(const CyPathBuffers *b, int slot, int r)
+{
+  return b->sss_vol + ((size_t)slot * (CY_SSS_RECS + 1) + (size_t)r) * (CY_VOLUME_STACK / 2);
 }
 
 CY_FN void vol_rec_store(const CyPathBuffers *b, int slot, uint object, uint shader, uint flags,
@@ -378,7 +417,7 @@ CY_FN void vol_slot_init(const CyGlobals *kg, const CyPathBuffers *b, int slot)
   CyPathState s;
   s.volume_bounce = 0;
   s.volume_bounds_bounce = 0;
-  vol_rec_store(b, slot, 0u, 0u, 0u, &s, 0);
+  vol_rec_store(b, slot, 0u, 0u, KD->cam.is_inside_volume ? CY_VOP_INIT_CAMERA : 0u, &s, 0);
 }
 
 #endif
@@ -496,10 +535,16 @@ CY_FN float path_state_continuation_probability(const CyGlobals *kg,
     if (s->transparent_bounce <= KD->integrator.transparent_min_bounce) {
       return 1.0f;
     }
+    else if ((s->flag & PATH_RAY_SHADOW_CATCHER) && s->transparent_bounce <= 8) {
+      return 1.0f; /* kernel_path_state.h:218-222: no RR behind a shadow catcher */
+    }
   }
   else {
     if (s->bounce <= KD->integrator.min_bounce) {
       return 1.0f;
+    }
+    else if ((s->flag & PATH_RAY_SHADOW_CATCHER) && s->bounce <= 3) {
+      return 1.0f; /* kernel_path_state.h:230-234 */
     }
   }
   /* branch_factor is 1.0 outside branched path tracing */
@@ -527,10 +572,44 @@ CY_FN cfloat3 path_radiance_clamp(const CyGlobals *kg, cfloat3 L, int bounce)
   return L;
 }
 
+/* the slot's catcher record (CyPathBuffers.catcher) */
+CY_FN void catcher_init(const CyGlobals *kg, CyCatcher *c)
+{
+  c->film_transparent = KD->background.transparent;
+  c->path_total = c->path_total_shaded = c->background = mk3(0.0f, 0.0f, 0.0f);
+  c->throughput = 0.0f;
+  c->transparency = 1.0f;
+  c->has = 0;
+}
+
+CY_FN void catcher_load(const CyGlobals *kg, const CyPathBuffers *b, int slot, CyCatcher *c)
+{
+  c->film_transparent = KD->background.transparent;
+  const hc_float4 *src = b->catcher + (size_t)slot * CY_CATCHER_F4;
+  const hc_float4 r0 = cy_ld(&src[0]);
+  const hc_float4 r1 = cy_ld(&src[1]);
+  const hc_float4 r2 = cy_ld(&src[2]);
+  c->path_total = mk3(r0.x, r0.y, r0.z);
+  c->throughput = r0.w;
+  c->path_total_shaded = mk3(r1.x, r1.y, r1.z);
+  c->transparency = r1.w;
+  c->background = mk3(r2.x, r2.y, r2.z);
+  c->has = as_int(r2.w);
+}
+
+CY_FN void catcher_store(const CyPathBuffers *b, int slot, const CyCatcher *c)
+{
+  hc_float4 *dst = b->catcher + (size_t)slot * CY_CATCHER_F4;
+  cy_st(&dst[0], mkf4(c->path_total.x, c->path_total.y, c->path_total.z, c->throughput));
+  cy_st(&dst[1], mkf4(c->path_total_shaded.x, c->path_total_shaded.y, c->path_total_shaded.z, c->transparency));
+  cy_st(&dst[2], mkf4(c->background.x, c->background.y, c->background.z, int_as_float(c->has)));
+}
+
 /* Record the finished sample: kernel_passes.h:338-433 with only the combined
  * pass (kernel_accumulate.h:622-688, use_light_pass == 0, no shadow catcher);
  * the buffer addition itself happens in accumulate_pixel. */
-CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float L_transparent)
+CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float L_transparent,
+                        const CyCatcher *catcher = nullptr)
 {
   cfloat3 L_sum = L_emission;
   float sum = fabsf(L_sum.x) + fabsf(L_sum.y) + fabsf(L_sum.z);
@@ -538,6 +617,26 @@ CY_FN void write_sample(const CyTile *tile, uint item, cfloat3 L_emission, float
     L_sum = mk3(0.0f, 0.0f, 0.0f);
   }
   float alpha = 1.0f - L_transparent;
+  if (catcher && catcher->has) {
+    /* path_radiance_sum_shadowcatcher (kernel_accumulate.h:590-620) */
+    const float path_total = average3(catcher->path_total);
+    float shadow;
+    if (!isfinite_safe(path_total)) {
+      shadow = 0.0f;
+    }
+    else if (path_total == 0.0f) {
+      shadow = catcher->transparency;
+    }
+    else {
+      shadow = average3(catcher->path_total_shaded) / path_total;
+    }
+    if (catcher->film_transparent) {
+      alpha -= catcher->throughput * shadow;
+    }
+    else {
+      L_sum = add3(L_sum, mul3f(catcher->background, shadow));
+    }
+  }
   cy_st(&tile->samples_out[item & tile->ring_mask], mkf4(L_sum.x, L_sum.y, L_sum.z, alpha));
 }
 
@@ -738,14 +837,19 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
   cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(path_state_ray_visibility(&s))));
   cy_st(&b->throughput[slot], mkf4(1.0f, 1.0f, 1.0f, 0.0f));
   cy_st(&b->L[slot], mkf4(0.0f, 0.0f, 0.0f, 0.0f));
+  if (b->catcher) {
+    CyCatcher c;
+    catcher_init(kg, &c);
+    catcher_store(b, slot, &c);
+  }
   return true;
 }
 
 /* Finish the path in a slot: record its sample; the slot then needs new work. */
 CY_FN void slot_finish(const CyPathBuffers *b, const CyTile *tile, int slot, uint item, cfloat3 L_emission,
-                       float L_transparent)
+                       float L_transparent, const CyCatcher *catcher = nullptr)
 {
-  write_sample(tile, item != CY_NO_ITEM ? item : cy_ld(&b->item[slot]), L_emission, L_transparent);
+  write_sample(tile, item != CY_NO_ITEM ? item : cy_ld(&b->item[slot]), L_emission, L_transparent, catcher);
 }
 
 /* ---------------------------------------------------------------------------
@@ -811,6 +915,8 @@ CY_FN bool shadow_finish(const CyPathBuffers *b, const CyTile *tile, int slot, b
     L4.z = L4.z + sl.z;
   }
   if (sl.w != 0.0f) {
+    /* (a path behind a shadow catcher traces its light samples itself: it
+     * never ends here) */
     slot_finish(b, tile, slot, CY_NO_ITEM, mk3(L4.x, L4.y, L4.z), cy_ld(&b->throughput[slot]).w);
     return true;
   }
@@ -830,7 +936,7 @@ template<bool VOL = false>
 CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPathState *state, CyShadeMem mem,
                                       cfloat3 *shadow, uint *err, void *volume_stack = nullptr,
                                       const CyDiff3 *ray_dP = nullptr, uint rec = CY_SREC_NONE,
-                                      const hc_float4 *rec_hits = nullptr)
+                                      const hc_float4 *rec_hits = nullptr, uint visibility = PATH_RAY_SHADOW)
 {
 #if CY_CLOSURE_EXT
   /* volume scenes: the shadow ray's copy of the path's volume stack, crossed
@@ -871,13 +977,13 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
   }
   else if (wide) {
     /* the wide layout's record-all (same hits, another recording order) */
-    blocked = kg->have_curves ? bvhw_shadow_all<1>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
-                                bvhw_shadow_all<0>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+    blocked = kg->have_curves ? bvhw_shadow_all<1>(kg, &ray, hits, visibility, max_hits, &num_hits, err) :
+                                bvhw_shadow_all<0>(kg, &ray, hits, visibility, max_hits, &num_hits, err);
   }
   else {
     blocked = kg->have_curves ?
-                  bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
-                  bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+                  bvh2_shadow_all<true, 3>(kg, &ray, hits, visibility, max_hits, &num_hits, err) :
+                  bvh2_shadow_all<true>(kg, &ray, hits, visibility, max_hits, &num_hits, err);
   }
   if (blocked || num_hits == 0) {
 #if CY_CLOSURE_EXT
@@ -912,8 +1018,8 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
     wide = false;
     num_hits = 0;
     blocked = kg->have_curves ?
-                  bvh2_shadow_all<true, 3>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err) :
-                  bvh2_shadow_all<true>(kg, &ray, hits, PATH_RAY_SHADOW, max_hits, &num_hits, err);
+                  bvh2_shadow_all<true, 3>(kg, &ray, hits, visibility, max_hits, &num_hits, err) :
+                  bvh2_shadow_all<true>(kg, &ray, hits, visibility, max_hits, &num_hits, err);
     if (blocked) {
       /* the two queries record the same set of hits, so this does not happen;
        * should it, the reference's own query decides, as in the first exit */
@@ -984,6 +1090,18 @@ CY_FN bool shadow_blocked_transparent(const CyGlobals *kg, CyRay ray, const CyPa
   *shadow = throughput;
   return is_zero3(throughput);
 }
+
+#if CY_CLOSURE_EXT
+/* shadow_blocked_transparent<true> for the light samples the shading stage
+ * traces itself (subsurface exit points, decoupled volume segments): one
+ * out-of-line copy instead of one inlined per call site. */
+CY_NOINLINE bool shadow_blocked_volume_inline(const CyGlobals *kg, const CyRay *ray, const CyPathState *state,
+                                              CyShadeMem mem, cfloat3 *shadow, uint *err, CyVolumeStack *stack,
+                                              const CyDiff3 *ray_dP)
+{
+  return shadow_blocked_transparent<true>(kg, *ray, state, mem, shadow, err, stack, ray_dP);
+}
+#endif
 
 /* The traversal half of a pending transparent shadow ray (hipcycles.hip
  * k_shadow_record; non-instanced scenes): the record-all query, its hits
@@ -1079,6 +1197,9 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
     vol_stack_load(b, slot, &vstack);
     const hc_uint4 r0 = cy_ld(&b->vol_rec[2 * (size_t)slot]);
     const hc_uint4 r1 = cy_ld(&b->vol_rec[2 * (size_t)slot + 1]);
+    if (r0.z & CY_VOP_OWN_STACK) {
+      vol_stack_read(sss_vol_at(b, slot, CY_SSS_RECS), &vstack);
+    }
     if (r0.z & CY_VOP_SHADOW) {
       volume_stack_enter_exit(SD_HAS_VOLUME | ((r0.z & CY_VOP_BACKFACING) ? SD_BACKFACING : 0), (int)r0.x,
                               (int)r0.y, &vstack);
@@ -1104,7 +1225,12 @@ CY_FN bool shadow_finish_transparent(const CyGlobals *kg, const CyPathBuffers *b
     L4.z = L4.z + contribution.z;
   }
   if (sl.w != 0.0f) {
-    slot_finish(b, tile, slot, CY_NO_ITEM, mk3(L4.x, L4.y, L4.z), cy_ld(&b->throughput[slot]).w);
+    CyCatcher catcher;
+    if (b->catcher) {
+      catcher_load(kg, b, slot, &catcher);
+    }
+    slot_finish(b, tile, slot, CY_NO_ITEM, mk3(L4.x, L4.y, L4.z), cy_ld(&b->throughput[slot]).w,
+                b->catcher ? &catcher : nullptr);
     return true;
   }
   cy_st(&b->L[slot], L4);
@@ -1380,6 +1506,22 @@ cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I,
 }
 #endif
 
+#if CY_CLOSURE_EXT
+/* light_sample (kernel_light.h:628-661) with a chosen lamp: lamp < 0 picks a
+ * light from the distribution as light_sample does. */
+CY_FN bool light_sample_lamp(const CyGlobals *kg, int lamp, float randu, float randv, cfloat3 P, int bounce,
+                             CyLightSample *ls, uint *err)
+{
+  if (lamp < 0) {
+    return light_sample(kg, randu, randv, P, bounce, ls, err);
+  }
+  if ((float)bounce > kg->__lights[lamp].max_bounces) {
+    return false;
+  }
+  return lamp_light_sample(kg, lamp, randu, randv, P, ls, err);
+}
+#endif
+
 /* Direct light at a shading point, one light sample (kernel_path_surface.h:23-140
  * kernel_branched_path_surface_connect_light with one sample, or
  * kernel_path_volume_connect_light, kernel_path_volume.h:21-61, when PHASE: a
@@ -1390,7 +1532,7 @@ cfloat3 emissive_eval_svm(const CyGlobals *kg, cfloat3 P, cfloat3 Ng, cfloat3 I,
 template<bool PHASE, bool INLINE = false>
 CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, const CySD *sd,
                          const CyPathState *state, cfloat3 throughput, cfloat3 *L, bool *shadow, cfloat3 *shadow_D,
-                         CyShadeMem mem, uint *err)
+                         CyShadeMem mem, uint *err, const void *inline_vstack = nullptr)
 {
   float light_u, light_v;
   path_state_rng_2D(kg, state, PRNG_LIGHT_U, &light_u, &light_v);
@@ -1508,8 +1650,21 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
             sray.t = st;
             if (KD->integrator.transparent_shadows) {
               cfloat3 attenuation;
-              const bool blocked = shadow_blocked_transparent<false>(kg, sray, state, mem, &attenuation, err,
-                                                                      nullptr, kg->use_ray_diff ? &sd->dP : nullptr);
+              bool blocked;
+              if (inline_vstack) {
+                /* volume scenes: the path's stack as the shadow ray sees it
+                 * (shadow_blocked_volume_path_state, kernel_shadow.h:23-45) */
+                CyVolumeStack sstack = *(const CyVolumeStack *)inline_vstack;
+                if (dot3(sd->Ng, sD) < 0.0f) {
+                  volume_stack_enter_exit(sd->flag, sd->object, sd->shader, &sstack);
+                }
+                blocked = shadow_blocked_volume_inline(kg, &sray, state, mem, &attenuation, err, &sstack,
+                                                       kg->use_ray_diff ? &sd->dP : nullptr);
+              }
+              else {
+                blocked = shadow_blocked_transparent<false>(kg, sray, state, mem, &attenuation, err, nullptr,
+                                                            kg->use_ray_diff ? &sd->dP : nullptr);
+              }
               *shadow = true;
               if (!blocked) {
                 const cfloat3 shaded = mul3(mul3f(throughput, 1.0f), attenuation);
@@ -1571,12 +1726,428 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
   }
 }
 
+#if CY_CLOSURE_EXT && CY_SVM_TEX
+/* direct_emission (kernel_emission.h:101-205) at a surface point on a path
+ * behind a shadow catcher: the BSDF-weighted light (*eval, the MIS weight
+ * applied) and the same without the MIS weight (*eval_no_mis,
+ * BsdfEval.sum_no_mis, kernel_accumulate.h:62-70), no light termination
+ * (kernel_emission.h:162-165); *light_ray the shadow ray (t = 0: the light
+ * casts no shadow).  False: no contribution. */
+CY_FN bool catcher_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightSample *ls, const CyPathState *state,
+                                   cfloat3 *eval, cfloat3 *eval_no_mis, CyRay *light_ray, CyShadeMem mem, uint *err)
+{
+  if (ls->pdf == 0.0f) {
+    return false;
+  }
+  cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
+  const cfloat3 I = neg3(ls->D);
+  if (shader_constant_emission_eval(kg, ls->shader, &light_eval)) {
+    if ((ls->prim != PRIM_NONE) && dot3(ls->Ng, I) < 0.0f) {
+      ls->Ng = neg3(ls->Ng);
+    }
+  }
+  else if (ls->type == LIGHT_BACKGROUND) {
+    light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info,
+                                     ls->D, mem, *state, PATH_RAY_EMISSION, err);
+  }
+  else {
+    light_eval = emissive_eval_svm(kg, ls->P, ls->Ng, I, ls->shader, ls->object, ls->prim, ls->lamp, ls->u, ls->v,
+                                   ls->t, mem, *state, err);
+    if ((ls->prim != PRIM_NONE) && dot3(ls->Ng, I) < 0.0f) {
+      ls->Ng = neg3(ls->Ng);
+    }
+  }
+  light_eval = mul3f(light_eval, ls->eval_fac);
+  if (ls->lamp != LAMP_NONE) {
+    light_eval = mul3(light_eval, klight_vec(kg->__lights[ls->lamp].strength));
+  }
+  if (is_zero3(light_eval)) {
+    return false;
+  }
+  float bpdf;
+  cfloat3 e = mk3(0.0f, 0.0f, 0.0f); /* shader_bsdf_multi_eval accumulates */
+  shader_bsdf_multi_eval(sd, ls->D, &bpdf, -1, &e, 0.0f, 0.0f);
+  cfloat3 no_mis = e;
+  if ((uint)ls->shader & SHADER_USE_MIS) {
+    e = mul3f(e, power_heuristic(ls->pdf, bpdf));
+  }
+  const cfloat3 scale = div3f(light_eval, ls->pdf);
+  e = mul3(e, scale);
+  no_mis = mul3(no_mis, scale);
+  if (((uint)ls->shader & SHADER_EXCLUDE_ANY) && ((uint)ls->shader & SHADER_EXCLUDE_DIFFUSE)) {
+    e = mk3(0.0f, 0.0f, 0.0f);
+  }
+  if (is_zero3(e)) {
+    return false;
+  }
+  if ((uint)ls->shader & SHADER_CAST_SHADOW) {
+    const bool transmit = (dot3(sd->Ng, ls->D) < 0.0f);
+    light_ray->P = ray_offset(sd->P, transmit ? neg3(sd->Ng) : sd->Ng);
+    if (ls->t == CY_FLT_MAX) {
+      light_ray->D = ls->D;
+      light_ray->t = ls->t;
+    }
+    else {
+      light_ray->D = normalize_len3(sub3(ray_offset(ls->P, ls->Ng), light_ray->P), &light_ray->t);
+    }
+  }
+  else {
+    light_ray->t = 0.0f;
+  }
+  *eval = e;
+  *eval_no_mis = no_mis;
+  return true;
+}
+
+/* kernel_branched_path_surface_connect_light (kernel_path_surface.h:22-140)
+ * with sample_all_lights, which kernel_path_surface_connect_light runs for a
+ * path behind a shadow catcher (kernel_path_surface.h:224-226): every lamp's
+ * samples and the mesh lights', each shadow ray traced here with the
+ * non-catcher shadow visibility (kernel_shadow.h:402-404), each sample's light
+ * added to the catcher's totals (path_radiance_accum_light /
+ * _accum_total_light with PATH_RAY_STORE_SHADOW_INFO, kernel_accumulate.h:
+ * 402-476; a catcher path adds nothing to the radiance itself).  The occluders'
+ * shaders are evaluated into shadow_mem, so sd's closures stay intact. */
+CY_NOINLINE void catcher_connect_all_lights(const CyGlobals *kg, const CySD *sd, const CyPathState *state,
+                                            cfloat3 throughput, CyCatcher *catcher, CyShadeMem mem, uint *err)
+{
+  if (!KD->integrator.use_direct_light) {
+    return;
+  }
+  CyClosure shadow_closures[CY_MAX_CLOSURE];
+  CyShadeMem shadow_mem = mem;
+  shadow_mem.closure = shadow_closures;
+  int num_lights = KD->integrator.num_all_lights;
+  if (KD->integrator.pdf_triangles != 0.0f) {
+    num_lights += 1;
+  }
+  for (int i = 0; i < num_lights; ++i) {
+    int num_samples = 1;
+    int num_all_lights = 1;
+    uint lamp_rng_hash = state->rng_hash;
+    bool double_pdf = false;
+    bool is_mesh_light = false;
+    const bool is_lamp = i < KD->integrator.num_all_lights;
+    if (is_lamp) {
+      if ((float)state->bounce > kg->__lights[i].max_bounces) {
+        continue;
+      }
+      num_samples = kg->__lights[i].samples;
+      num_all_lights = KD->integrator.num_all_lights;
+      lamp_rng_hash = cmj_hash(state->rng_hash, (uint)i);
+      double_pdf = KD->integrator.pdf_triangles != 0.0f;
+    }
+    else {
+      num_samples = KD->integrator.mesh_light_samples;
+      double_pdf = KD->integrator.num_all_lights != 0;
+      is_mesh_light = true;
+    }
+    const float num_samples_inv = 1.0f / (float)(num_samples * num_all_lights);
+    for (int j = 0; j < num_samples; j++) {
+      CyRay light_ray;
+      light_ray.t = 0.0f;
+      bool has_emission = false;
+      cfloat3 eval = mk3(0.0f, 0.0f, 0.0f), eval_no_mis = mk3(0.0f, 0.0f, 0.0f);
+      if (sd->flag & SD_BSDF_HAS_EVAL) {
+        float light_u, light_v;
+        path_branched_rng_2D(kg, lamp_rng_hash, state, j, num_samples, PRNG_LIGHT_U, &light_u, &light_v);
+        if (is_mesh_light && double_pdf) {
+          light_u = 0.5f * light_u;
+        }
+        CyLightSample ls;
+        if (light_sample_lamp(kg, is_lamp ? i : -1, light_u, light_v, sd->P, state->bounce, &ls, err)) {
+          if (double_pdf) {
+            ls.pdf *= 2.0f;
+          }
+          has_emission = catcher_direct_emission(kg, sd, &ls, state, &eval, &eval_no_mis, &light_ray, mem, err);
+        }
+      }
+      /* shadow_blocked (kernel_shadow.h:386-460) */
+      cfloat3 shadow = mk3(1.0f, 1.0f, 1.0f);
+      bool blocked = false;
+      if (light_ray.t != 0.0f) {
+        if (KD->integrator.transparent_shadows) {
+          blocked = shadow_blocked_transparent<false>(kg, light_ray, state, shadow_mem, &shadow, err, nullptr,
+                                                      kg->use_ray_diff ? &sd->dP : nullptr, CY_SREC_NONE, nullptr,
+                                                      PATH_RAY_SHADOW_NON_CATCHER);
+        }
+        else if (scene_intersect_valid(&light_ray)) {
+          CyIsect si;
+          blocked = kg->have_curves ?
+                        bvh2_intersect<true, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(
+                            kg, &light_ray, PATH_RAY_SHADOW_OPAQUE_NON_CATCHER, &si, err, nullptr, nullptr, nullptr) :
+                        bvh2_intersect<true>(kg, &light_ray, PATH_RAY_SHADOW_OPAQUE_NON_CATCHER, &si, err, nullptr,
+                                             nullptr, nullptr);
+        }
+      }
+      CY_DBGF(state, "catcher light %d sample %d emission %d blocked %d\n", i, j, (int)has_emission, (int)blocked);
+      CY_DBG3(state, "catcher eval_no_mis", eval_no_mis);
+      CY_DBG3(state, "catcher light_ray.D", light_ray.D);
+      CY_DBG1(state, "catcher light_ray.t", light_ray.t);
+      if (has_emission) {
+        const cfloat3 light = mul3(mul3f(throughput, num_samples_inv), eval_no_mis);
+        catcher->path_total = add3(catcher->path_total, light);
+        if (!blocked) {
+          catcher->path_total_shaded = add3(catcher->path_total_shaded, mul3(shadow, light));
+        }
+      }
+    }
+  }
+}
+#endif
+
+#if CY_CLOSURE_EXT && CY_SVM_TEX
+
+/* direct_emission (kernel_emission.h:101-205) at a volume scatter point (sd->prim
+ * == PRIM_NONE: the phase functions, MIS on the light's eval): *eval is the
+ * light's contribution per unit throughput; *light_ray the shadow ray (t = 0:
+ * the light casts no shadow).  False: no contribution. */
+CY_FN bool volume_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightSample *ls, const CyPathState *state,
+                                  float rand_terminate, cfloat3 *eval, CyRay *light_ray, CyShadeMem mem, uint *err)
+{
+  if (ls->pdf == 0.0f) {
+    return false;
+  }
+  cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
+  const cfloat3 I = neg3(ls->D);
+  /* direct_emissive_eval (kernel_emission.h:20-99) */
+  if (shader_constant_emission_eval(kg, ls->shader, &light_eval)) {
+    if ((ls->prim != PRIM_NONE) && dot3(ls->Ng, I) < 0.0f) {
+      ls->Ng = neg3(ls->Ng);
+    }
+  }
+  else if (ls->type == LIGHT_BACKGROUND) {
+    light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info,
+                                     ls->D, mem, *state, PATH_RAY_EMISSION, err);
+  }
+  else {
+    light_eval = emissive_eval_svm(kg, ls->P, ls->Ng, I, ls->shader, ls->object, ls->prim, ls->lamp, ls->u, ls->v,
+                                   ls->t, mem, *state, err);
+    if ((ls->prim != PRIM_NONE) && dot3(ls->Ng, I) < 0.0f) {
+      ls->Ng = neg3(ls->Ng);
+    }
+  }
+  light_eval = mul3f(light_eval, ls->eval_fac);
+  if (ls->lamp != LAMP_NONE) {
+    light_eval = mul3(light_eval, klight_vec(kg->__lights[ls->lamp].strength));
+  }
+  if (is_zero3(light_eval)) {
+    return false;
+  }
+  float bpdf;
+  cfloat3 e = shader_volume_phase_eval(sd, ls->D, &bpdf);
+  if ((uint)ls->shader & SHADER_USE_MIS) {
+    light_eval = mul3f(light_eval, power_heuristic(ls->pdf, bpdf));
+  }
+  e = mul3(e, div3f(light_eval, ls->pdf));
+  if (((uint)ls->shader & SHADER_EXCLUDE_ANY) && ((uint)ls->shader & SHADER_EXCLUDE_DIFFUSE)) {
+    e = mk3(0.0f, 0.0f, 0.0f);
+  }
+  if (is_zero3(e)) {
+    return false;
+  }
+  if (KD->integrator.light_inv_rr_threshold > 0.0f) {
+    const float probability = max3f(fabs3(e)) * KD->integrator.light_inv_rr_threshold;
+    if (probability < 1.0f) {
+      if (rand_terminate >= probability) {
+        return false;
+      }
+      e = mul3f(e, 1.0f / probability);
+    }
+  }
+  if ((uint)ls->shader & SHADER_CAST_SHADOW) {
+    const bool transmit = (dot3(sd->Ng, ls->D) < 0.0f);
+    light_ray->P = ray_offset(sd->P, transmit ? neg3(sd->Ng) : sd->Ng);
+    if (ls->t == CY_FLT_MAX) {
+      light_ray->D = ls->D;
+      light_ray->t = ls->t;
+    }
+    else {
+      light_ray->D = normalize_len3(sub3(ray_offset(ls->P, ls->Ng), light_ray->P), &light_ray->t);
+    }
+  }
+  else {
+    light_ray->t = 0.0f;
+  }
+  *eval = e;
+  return true;
+}
+
+/* kernel_branched_path_volume_connect_light (kernel_path_volume.h:131-257):
+ * direct light at points of the recorded segment, one light sample per lamp
+ * (or all lamps' samples and the mesh lights' with sample_all_lights), each
+ * at its own scatter distance (decoupled scatter toward the light sample,
+ * equiangular / MIS by the volumes' sampling method), occluded inline
+ * through transparent surfaces and volumes (the shadow ray's own copy of the
+ * volume stack, shadow_blocked_volume_path_state), added to *L in the
+ * reference's order.  The closure memory is shared with the shadow's surface
+ * evaluations: decoupled_scatter evaluates the segment's closures again
+ * before each light's phase evaluation. */
+CY_FN void volume_connect_all_lights(const CyGlobals *kg, CySD *sd, cfloat3 throughput, const CyPathState *state,
+                                     cfloat3 *L, bool sample_all_lights, const CyRay *ray,
+                                     const CyVolumeSegment *segment, const CyVolumeStack *stack, CyShadeMem mem,
+                                     uint *err)
+{
+  /* One LightSample for the whole loop: a light_sample that fails early (a
+   * triangle light facing away: pdf 0 before P and t are set) leaves the
+   * previous sample's P and t in place, and the equiangular sampling below
+   * then aims at that point.  In the reference the sample is a loop-local
+   * left uninitialised, which the CPU build keeps in one stack slot across
+   * the iterations: the same stale values (found on volume_mis_decoupled,
+   * one path whose mesh-light sample failed after a lamp sample). */
+  CyLightSample ls;
+  ls.P = mk3(0.0f, 0.0f, 0.0f);
+  ls.t = CY_FLT_MAX;
+  int num_lights = 1;
+  if (sample_all_lights) {
+    num_lights = KD->integrator.num_all_lights;
+    if (KD->integrator.pdf_triangles != 0.0f) {
+      num_lights += 1;
+    }
+  }
+  for (int i = 0; i < num_lights; ++i) {
+    int num_samples = 1;
+    int num_all_lights = 1;
+    uint lamp_rng_hash = state->rng_hash;
+    bool double_pdf = false;
+    bool is_mesh_light = false;
+    bool is_lamp = false;
+    if (sample_all_lights) {
+      is_lamp = i < KD->integrator.num_all_lights;
+      if (is_lamp) {
+        if ((float)state->bounce > kg->__lights[i].max_bounces) {
+          continue;
+        }
+        num_samples = kg->__lights[i].samples;
+        num_all_lights = KD->integrator.num_all_lights;
+        lamp_rng_hash = cmj_hash(state->rng_hash, (uint)i);
+        double_pdf = KD->integrator.pdf_triangles != 0.0f;
+      }
+      else {
+        num_samples = KD->integrator.mesh_light_samples;
+        double_pdf = KD->integrator.num_all_lights != 0;
+        is_mesh_light = true;
+      }
+    }
+    const float num_samples_inv = 1.0f / (float)(num_samples * num_all_lights);
+    for (int j = 0; j < num_samples; j++) {
+      CyRay light_ray;
+      light_ray.t = 0.0f;
+      bool has_emission = false;
+      cfloat3 tp = throughput;
+      cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
+      if (KD->integrator.use_direct_light) {
+        float light_u, light_v;
+        path_branched_rng_2D(kg, lamp_rng_hash, state, j, num_samples, PRNG_LIGHT_U, &light_u, &light_v);
+        if (is_mesh_light && double_pdf) {
+          light_u = 0.5f * light_u;
+        }
+        const int lamp = is_lamp ? i : -1;
+        const bool ls_ok = light_sample_lamp(kg, lamp, light_u, light_v, ray->P, state->bounce, &ls, err);
+        CY_DBGF(state, "ls_ok %d pdf %08x lamp %d\n", (int)ls_ok, __builtin_bit_cast(unsigned, ls.pdf), ls.lamp);
+        const float rphase = path_rng_1D(kg, state->rng_hash, state->sample * num_samples + j,
+                                         state->rng_offset + PRNG_PHASE_CHANNEL);
+        const float rscatter = path_rng_1D(kg, state->rng_hash, state->sample * num_samples + j,
+                                           state->rng_offset + PRNG_SCATTER_DISTANCE);
+        const cfloat3 light_P = ls.P;
+        CY_DBGF(state, "light %d sample %d\n", i, j);
+        CY_DBG3(state, "light uv rphase", mk3(light_u, light_v, rphase));
+        CY_DBG3(state, "ls.P", ls.P);
+        CY_DBG1(state, "ls.t", ls.t);
+        const int result = volume_decoupled_scatter(kg, state, ray, sd, stack, &tp, rphase, rscatter, segment,
+                                                    (ls.t != CY_FLT_MAX) ? &light_P : nullptr, false, err);
+        if (result == VOLUME_PATH_SCATTERED) {
+          if (light_sample_lamp(kg, lamp, light_u, light_v, sd->P, state->bounce, &ls, err)) {
+            if (double_pdf) {
+              ls.pdf *= 2.0f;
+            }
+            const float terminate = (KD->integrator.light_inv_rr_threshold > 0.0f) ?
+                                        path_rng_1D(kg, state->rng_hash, state->sample * num_samples + j,
+                                                    state->rng_offset + PRNG_LIGHT_TERMINATE) :
+                                        0.0f;
+            has_emission = volume_direct_emission(kg, sd, &ls, state, terminate, &eval, &light_ray, mem, err);
+          }
+        }
+      }
+      /* shadow_blocked: the path's volume stack as the shadow ray sees it
+       * (shadow_blocked_volume_path_state, kernel_shadow.h:23-45) */
+      bool blocked = false;
+      cfloat3 shadow = mk3(1.0f, 1.0f, 1.0f);
+      if (light_ray.t != 0.0f) {
+        CyVolumeStack sstack = *stack;
+        if (dot3(sd->Ng, light_ray.D) < 0.0f) {
+          volume_stack_enter_exit(sd->flag, sd->object, sd->shader, &sstack);
+        }
+        blocked = shadow_blocked_volume_inline(kg, &light_ray, state, mem, &shadow, err, &sstack,
+                                               kg->use_ray_diff ? &sd->dP : nullptr);
+      }
+      CY_DBGF(state, "has_emission %d blocked %d\n", (int)has_emission, (int)blocked);
+      CY_DBG3(state, "eval", eval);
+      CY_DBG3(state, "shadow", shadow);
+      CY_DBG3(state, "tp", tp);
+      if (has_emission && !blocked) {
+        /* path_radiance_accum_light (kernel_accumulate.h:402-459) */
+        const cfloat3 shaded_throughput = mul3(mul3f(tp, num_samples_inv), shadow);
+        *L = add3(*L, path_radiance_clamp(kg, mul3(shaded_throughput, eval), state->bounce));
+      }
+    }
+  }
+}
+
+/* kernel_path_volume (kernel_path.h:186-215), decoupled branch: the segment
+ * recorded once, its emission, direct light over all lights, then the
+ * indirect scatter decision.  Returns VOLUME_PATH_SCATTERED (vsd at the
+ * scatter point, throughput weighted) or VOLUME_PATH_ATTENUATED (throughput
+ * times the segment's transmittance). */
+CY_NOINLINE int volume_decoupled_path(const CyGlobals *kg, CySD *vsd, CyPathState *state,
+                                      const CyVolumeStack *stack, const CyRay *volume_ray, cfloat3 *L,
+                                      cfloat3 *throughput, float step_size, int sampling_method, CyShadeMem mem,
+                                      uint *err)
+{
+  CyVolumeStep steps[CY_DECOUPLED_STEPS];
+  CyVolumeSegment segment;
+  shader_setup_from_volume(vsd, volume_ray, mem);
+  volume_decoupled_record(kg, state, volume_ray, vsd, stack, &segment, step_size, steps, err);
+  segment.sampling_method = sampling_method;
+  if (segment.closure_flag & SD_EMISSION) {
+    volume_accum_emission(kg, state, L, *throughput, segment.accum_emission);
+  }
+  int result = VOLUME_PATH_ATTENUATED;
+  if (segment.closure_flag & SD_SCATTER) {
+    const bool all = KD->integrator.sample_all_lights_indirect != 0;
+    volume_connect_all_lights(kg, vsd, *throughput, state, L, all, volume_ray, &segment, stack, mem, err);
+    const float rphase = path_state_rng_1D(kg, state, PRNG_PHASE_CHANNEL);
+    const float rscatter = path_state_rng_1D(kg, state, PRNG_SCATTER_DISTANCE);
+    result = volume_decoupled_scatter(kg, state, volume_ray, vsd, stack, throughput, rphase, rscatter, &segment,
+                                      nullptr, true, err);
+  }
+  if (result != VOLUME_PATH_SCATTERED) {
+    *throughput = mul3(*throughput, segment.accum_transmittance);
+    return VOLUME_PATH_ATTENUATED;
+  }
+  return VOLUME_PATH_SCATTERED;
+}
+#endif
+
 #if CY_CLOSURE_EXT
+/* connect_light<false, true> for a subsurface exit point in a volume scene
+ * (the light sample traced through the fog with the path's stack): one
+ * out-of-line copy for the disk and random-walk exit points of the volume
+ * kernels. */
+CY_NOINLINE void connect_light_exit_vol(const CyGlobals *kg, const CyPathBuffers *b, int slot, const CySD *sd,
+                                        const CyPathState *state, cfloat3 throughput, cfloat3 *L, bool *reused,
+                                        CyShadeMem mem, uint *err, const CyVolumeStack *vstack)
+{
+  cfloat3 shadow_D;
+  connect_light<false, true>(kg, b, slot, sd, state, throughput, L, reused, &shadow_D, mem, err, vstack);
+}
+
 /* kernel_path_surface_bounce (kernel_path_surface.h:270-358) for the diffuse
- * closure at a subsurface exit point (no volumes: disk BSSRDFs are refused in
- * volume scenes). */
+ * closure at a subsurface exit point; with vstack (volume scenes) the ray's
+ * stack enters / leaves the surface's volume on a transmission bounce
+ * (kernel_path_surface.h:325-329). */
 CY_FN bool subsurface_exit_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *throughput, CyPathState *state,
-                                  CyRay *ray, uint *err, CyDiff3 *domega_in = nullptr)
+                                  CyRay *ray, uint *err, CyDiff3 *domega_in = nullptr, CyVolumeStack *vstack = nullptr)
 {
   if (!(sd->flag & SD_BSDF)) {
     return false;
@@ -1606,6 +2177,9 @@ CY_FN bool subsurface_exit_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *
   else {
     ray->t = CY_FLT_MAX;
   }
+  if (vstack && (label & LABEL_TRANSMIT)) {
+    volume_stack_enter_exit(sd->flag, sd->object, sd->shader, vstack);
+  }
   return true;
 }
 
@@ -1618,9 +2192,11 @@ CY_FN bool subsurface_exit_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *
  * replaces the path's state, ray and throughput here, the others wait in the
  * slot's SSS records until the path before them ends (shade_path).  Returns
  * the number of indirect rays. */
+template<bool VOL = false>
 CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int slot, uint cam_item, CySD *sd,
                                 const CyClosure *sc, float bssrdf_u, float bssrdf_v, CyPathState *state,
-                                CyRay *ray, cfloat3 *throughput, cfloat3 *L, CyShadeMem mem, uint *err)
+                                CyRay *ray, cfloat3 *throughput, cfloat3 *L, CyShadeMem mem, uint *err,
+                                CyVolumeStack *vstack = nullptr, CySD *stack_sd = nullptr)
 {
   if (!b->sss_rec || (cam_item == CY_NO_ITEM && cy_ld(&b->sss_count[slot]) != 0u)) {
     cy_set_error(err, CY_ERR_FEATURE, 12); /* no indirect-ray records, or a second scatter on one path */
@@ -1645,6 +2221,11 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
    * (shader_setup_from_subsurface keeps sd->dP, dI) and its sampled dD */
   const bool diff = kg->use_ray_diff != 0;
   CyDiff3 top_dD, hit_dD;
+  /* volume scenes: each indirect ray's own stack, from the path's, crossed by
+   * the ray from the path's previous point to the exit point when the object
+   * intersects a volume (kernel_path_subsurface.h:56-57, 92-99) */
+  const bool update_stack = vstack && (sd->object_flag & SD_OBJECT_INTERSECTS_VOLUME);
+  CyVolumeStack top_stack, hit_stack;
   for (int hit = 0; hit < num_hits; hit++) {
     /* subsurface_scatter_multi_setup (kernel_subsurface.h:284-313) */
     shader_setup_from_subsurface(kg, sd, &li.hits[hit], &ss_ray);
@@ -1655,7 +2236,12 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
     if (KD->integrator.use_direct_light && (sd->flag & SD_BSDF_HAS_EVAL)) {
       bool reused = false;
       cfloat3 shadow_D;
-      connect_light<false, true>(kg, b, slot, sd, state, *throughput, L, &reused, &shadow_D, mem, err);
+      if (VOL) {
+        connect_light_exit_vol(kg, b, slot, sd, state, *throughput, L, &reused, mem, err, vstack);
+      }
+      else {
+        connect_light<false, true>(kg, b, slot, sd, state, *throughput, L, &reused, &shadow_D, mem, err);
+      }
       if (reused) {
         shader_setup_from_subsurface(kg, sd, &li.hits[hit], &ss_ray);
         subsurface_scatter_setup_diffuse_bsdf(kg, sd, bssrdf_type, bssrdf_rough, weight, N);
@@ -1665,16 +2251,31 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
     CyRay hit_ray = *ray;
     cfloat3 hit_tp = *throughput;
     hit_state.rng_offset += PRNG_BOUNCE_NUM;
-    if (subsurface_exit_bounce(kg, sd, &hit_tp, &hit_state, &hit_ray, err, diff ? &hit_dD : nullptr)) {
+    if (vstack) {
+      hit_stack = *vstack;
+    }
+    if (subsurface_exit_bounce(kg, sd, &hit_tp, &hit_state, &hit_ray, err, diff ? &hit_dD : nullptr,
+                               vstack ? &hit_stack : nullptr)) {
       hit_state.ray_t = 0.0f;
+      if (update_stack) {
+        CyRay volume_ray = *ray;
+        volume_ray.D = normalize_len3(sub3(hit_ray.P, volume_ray.P), &volume_ray.t);
+        volume_stack_update_for_subsurface(kg, stack_sd, &volume_ray, &hit_stack, err);
+      }
       if (pushed > 0) {
         top_state.rng_offset += (pushed - 1) * PRNG_BOUNCE_NUM;
         sss_rec_store(b, slot, pushed - 1, &top_state, &top_ray, top_tp, diff ? &sd->dP : nullptr, &top_dD);
+        if (vstack) {
+          vol_stack_write(sss_vol_at(b, slot, pushed - 1), &top_stack);
+        }
       }
       top_state = hit_state;
       top_ray = hit_ray;
       top_tp = hit_tp;
       top_dD = hit_dD;
+      if (vstack) {
+        top_stack = hit_stack;
+      }
       pushed++;
     }
   }
@@ -1683,6 +2284,9 @@ CY_FN int subsurface_disk_paths(const CyGlobals *kg, const CyPathBuffers *b, int
     *state = top_state;
     *ray = top_ray;
     *throughput = top_tp;
+    if (vstack) {
+      *vstack = top_stack;
+    }
     if (diff) {
       diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, sd->dP, top_dD);
     }
@@ -1738,6 +2342,58 @@ CY_FN bool volume_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *throughpu
   return true;
 }
 #endif
+
+/* indirect_background (kernel_emission.h:288-345): the world seen along the
+ * ray (its light-path exclusions, the world shader evaluated with the bounce
+ * raised, the background MIS weight). */
+CY_FN cfloat3 indirect_background(const CyGlobals *kg, const CyPathBuffers *b, const CyTile *tile, int slot,
+                                  uint cam_item, const CyPathState *state, const CyRay *ray, CyShadeMem mem,
+                                  uint *err)
+{
+  uint shader = (uint)KD->background.surface_shader;
+  bool excluded = false;
+  if (shader & SHADER_EXCLUDE_ANY) {
+    if (((shader & SHADER_EXCLUDE_DIFFUSE) && (state->flag & PATH_RAY_DIFFUSE)) ||
+        ((shader & SHADER_EXCLUDE_GLOSSY) &&
+         ((state->flag & (PATH_RAY_GLOSSY | PATH_RAY_REFLECT)) ==
+          (PATH_RAY_GLOSSY | PATH_RAY_REFLECT))) ||
+        ((shader & SHADER_EXCLUDE_TRANSMIT) && (state->flag & PATH_RAY_TRANSMIT)) ||
+        ((shader & SHADER_EXCLUDE_CAMERA) && (state->flag & PATH_RAY_CAMERA)) ||
+        ((shader & SHADER_EXCLUDE_SCATTER) && (state->flag & PATH_RAY_VOLUME_SCATTER))) {
+      excluded = true;
+    }
+  }
+  cfloat3 L_background = mk3(0.0f, 0.0f, 0.0f);
+  if (!excluded) {
+    if (!shader_constant_emission_eval(kg, (int)shader, &L_background)) {
+      /* world shader evaluated along the ray, bounce raised for the
+       * light-path node (path_state_modify_bounce) */
+#if CY_SVM_TEX
+#if CY_CLOSURE_EXT
+      CyDiff3 rdP, rdD;
+      if (kg->use_ray_diff) {
+        ray_diff_load(kg, b, tile, slot, cam_item, &rdP, &rdD);
+      }
+      L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray->D,
+                                         mem, *state, state->flag | PATH_RAY_EMISSION, err,
+                                         kg->use_ray_diff ? &rdD : nullptr);
+#else
+      L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray->D,
+                                         mem, *state, state->flag | PATH_RAY_EMISSION, err);
+#endif
+#else
+      cy_set_error(err, CY_ERR_FEATURE, 3); /* node world in the kernel without texture nodes */
+#endif
+    }
+    /* background MIS weight (kernel_emission.h:325-335) */
+    if (!(state->flag & PATH_RAY_MIS_SKIP) && KD->background.use_mis) {
+      const float pdf = background_light_pdf(kg, ray->D);
+      const float mis_weight = power_heuristic(state->ray_pdf, pdf);
+      L_background = mul3f(L_background, mis_weight);
+    }
+  }
+  return L_background;
+}
 
 template<bool VOL = false>
 CY_FN bool shade_path(const CyGlobals *kg,
@@ -1823,6 +2479,17 @@ CY_FN bool shade_path(const CyGlobals *kg,
     const hc_float4 L4 = cy_ld(&b->L[slot]);
     L = mk3(L4.x, L4.y, L4.z);
   }
+#if CY_CATCHER
+  CyCatcher catcher;
+  if (b->catcher) {
+    if (cam_item != CY_NO_ITEM) {
+      catcher_init(kg, &catcher);
+    }
+    else {
+      catcher_load(kg, b, slot, &catcher);
+    }
+  }
+#endif
 #ifdef CY_DBG_X
   {
     int dx, dy, ds;
@@ -1846,7 +2513,13 @@ CY_FN bool shade_path(const CyGlobals *kg,
   int shadow_rng_offset = 0;
   if (VOL) {
     if (cam_item != CY_NO_ITEM) {
-      volume_stack_init(kg, &vstack);
+      if (KD->cam.is_inside_volume) {
+        CySD stack_sd;
+        volume_stack_init_camera(kg, &stack_sd, &ray, (uint)state.flag, &vstack, err);
+      }
+      else {
+        volume_stack_init(kg, &vstack);
+      }
     }
     else {
       vol_stack_load(b, slot, &vstack);
@@ -1854,6 +2527,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
       const hc_uint4 r1 = cy_ld(&b->vol_rec[2 * (size_t)slot + 1]);
       state.volume_bounce = (int)r0.w;
       state.volume_bounds_bounce = (int)r1.x;
+      if (r0.z & CY_VOP_INIT_CAMERA) {
+        /* path_state_init's kernel_volume_stack_init (kernel_path_state.h:62-68) */
+        CySD stack_sd;
+        volume_stack_init_camera(kg, &stack_sd, &ray, (uint)state.flag, &vstack, err);
+      }
       if (r0.z & CY_VOP_PATH) {
         volume_stack_enter_exit(SD_HAS_VOLUME | ((r0.z & CY_VOP_BACKFACING) ? SD_BACKFACING : 0), (int)r0.x,
                                 (int)r0.y, &vstack);
@@ -1916,10 +2594,16 @@ CY_FN bool shade_path(const CyGlobals *kg,
       if (!(state.flag & PATH_RAY_MIS_SKIP)) {
         lamp_L = mul3f(lamp_L, power_heuristic(state.ray_pdf, ls.pdf));
       }
-      /* path_radiance_accum_emission (kernel_accumulate.h:304-335) */
+      /* path_radiance_accum_emission (kernel_accumulate.h:304-335; nothing
+       * behind a shadow catcher) */
       cfloat3 contribution = mul3(throughput, lamp_L);
       contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
-      L = add3(L, contribution);
+#if CY_CATCHER
+      if (!(state.flag & PATH_RAY_SHADOW_CATCHER))
+#endif
+      {
+        L = add3(L, contribution);
+      }
     }
   }
 
@@ -1939,11 +2623,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
       volume_ray.t = hit ? is4.x : CY_FLT_MAX;
       const float step_size = volume_stack_step_size(kg, &vstack);
       CySD vsd;
-      const int result = volume_integrate(kg, &state, &vsd, &vstack, &volume_ray, &L, &throughput, step_size, mem,
-                                          err);
+      /* kernel_path.h:180-215: the CPU device's decoupled ray marching (direct
+       * light from all lights inline, cy_volume_decoupled.h), or distance
+       * sampling with one deferred light sample */
+      const int sampling_method = volume_stack_sampling_method(kg, &vstack);
+      const bool decoupled = volume_use_decoupled(kg, (state.flag & PATH_RAY_CAMERA) != 0, sampling_method);
+      const int result = decoupled ? volume_decoupled_path(kg, &vsd, &state, &vstack, &volume_ray, &L, &throughput,
+                                                           step_size, sampling_method, mem, err) :
+                                     volume_integrate(kg, &state, &vsd, &vstack, &volume_ray, &L, &throughput,
+                                                      step_size, mem, err);
       if (result == VOLUME_PATH_SCATTERED) {
         vol_scattered = true;
-        connect_light<true>(kg, b, slot, &vsd, &state, throughput, &L, shadow, &shadow_D, mem, err);
+        if (!decoupled) {
+          connect_light<true>(kg, b, slot, &vsd, &state, throughput, &L, shadow, &shadow_D, mem, err);
+        }
         shadow_rng_offset = state.rng_offset;
         if (volume_bounce(kg, &vsd, &throughput, &state, &ray)) {
           cont = true;
@@ -1979,53 +2672,22 @@ CY_FN bool shade_path(const CyGlobals *kg,
       if (path_state_ao_bounce(kg, &state)) {
         throughput = mul3f(throughput, KD->background.ao_bounces_factor);
       }
-      /* indirect_background (kernel_emission.h:288-345) */
-      uint shader = (uint)KD->background.surface_shader;
-      bool excluded = false;
-      if (shader & SHADER_EXCLUDE_ANY) {
-        if (((shader & SHADER_EXCLUDE_DIFFUSE) && (state.flag & PATH_RAY_DIFFUSE)) ||
-            ((shader & SHADER_EXCLUDE_GLOSSY) &&
-             ((state.flag & (PATH_RAY_GLOSSY | PATH_RAY_REFLECT)) ==
-              (PATH_RAY_GLOSSY | PATH_RAY_REFLECT))) ||
-            ((shader & SHADER_EXCLUDE_TRANSMIT) && (state.flag & PATH_RAY_TRANSMIT)) ||
-            ((shader & SHADER_EXCLUDE_CAMERA) && (state.flag & PATH_RAY_CAMERA)) ||
-            ((shader & SHADER_EXCLUDE_SCATTER) && (state.flag & PATH_RAY_VOLUME_SCATTER))) {
-          excluded = true;
-        }
-      }
-      cfloat3 L_background = mk3(0.0f, 0.0f, 0.0f);
-      if (!excluded) {
-        if (!shader_constant_emission_eval(kg, (int)shader, &L_background)) {
-          /* world shader evaluated along the ray, bounce raised for the
-           * light-path node (path_state_modify_bounce) */
-#if CY_SVM_TEX
-#if CY_CLOSURE_EXT
-          CyDiff3 rdP, rdD;
-          if (kg->use_ray_diff) {
-            ray_diff_load(kg, b, tile, slot, cam_item, &rdP, &rdD);
-          }
-          L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray.D,
-                                             mem, state, state.flag | PATH_RAY_EMISSION, err,
-                                             kg->use_ray_diff ? &rdD : nullptr);
-#else
-          L_background = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info, ray.D,
-                                             mem, state, state.flag | PATH_RAY_EMISSION, err);
-#endif
-#else
-          cy_set_error(err, CY_ERR_FEATURE, 3); /* node world in the kernel without texture nodes */
-#endif
-        }
-        /* background MIS weight (kernel_emission.h:325-335) */
-        if (!(state.flag & PATH_RAY_MIS_SKIP) && KD->background.use_mis) {
-          const float pdf = background_light_pdf(kg, ray.D);
-          const float mis_weight = power_heuristic(state.ray_pdf, pdf);
-          L_background = mul3f(L_background, mis_weight);
-        }
-      }
+      const cfloat3 L_background = indirect_background(kg, b, tile, slot, cam_item, &state, &ray, mem, err);
       /* path_radiance_accum_background (kernel_accumulate.h:478-520) */
-      cfloat3 contribution = mul3(throughput, L_background);
-      contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
-      L = add3(L, contribution);
+      bool catcher_path = false;
+#if CY_CATCHER
+      if (b->catcher && (state.flag & PATH_RAY_STORE_SHADOW_INFO)) {
+        catcher.path_total = add3(catcher.path_total, mul3(throughput, L_background));
+        catcher.path_total_shaded = add3(catcher.path_total_shaded,
+                                         mul3f(mul3(throughput, L_background), catcher.transparency));
+        catcher_path = (state.flag & PATH_RAY_SHADOW_CATCHER) != 0;
+      }
+#endif
+      if (!catcher_path) {
+        cfloat3 contribution = mul3(throughput, L_background);
+        contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
+        L = add3(L, contribution);
+      }
     }
   }
   else if (!path_state_ao_bounce(kg, &state)) {
@@ -2129,12 +2791,33 @@ CY_FN bool shade_path(const CyGlobals *kg,
     }
 #endif
 
-    /* kernel_path_shader_apply (kernel_path.h:254-321); shadow catchers are
-     * refused by hipcy_load_kernels */
+    /* kernel_path_shader_apply (kernel_path.h:254-321) */
     bool terminated = false;
+#if CY_CATCHER
     if (sd.object_flag & SD_OBJECT_SHADOW_CATCHER) {
-      cy_set_error(err, CY_ERR_FEATURE, 5);
+      if (state.flag & PATH_RAY_TRANSPARENT_BACKGROUND) {
+        /* a camera (or transparent) ray reaches the catcher: the path goes on
+         * behind it, recording the light it would have received
+         * (path_radiance_accum_shadowcatcher, kernel_accumulate.h:529-537) */
+        state.flag |= PATH_RAY_SHADOW_CATCHER | PATH_RAY_STORE_SHADOW_INFO;
+        cfloat3 bg = mk3(0.0f, 0.0f, 0.0f);
+        if (!KD->background.transparent) {
+          bg = indirect_background(kg, b, tile, slot, cam_item, &state, &ray, mem, err);
+        }
+        catcher.throughput += average3(throughput);
+        catcher.background = add3(catcher.background, mul3(throughput, bg));
+        catcher.has = 1;
+      }
     }
+    else if (state.flag & PATH_RAY_SHADOW_CATCHER) {
+      /* only update transparency after the catcher bounce */
+      catcher.transparency *= average3(shader_bsdf_transparency(&sd));
+    }
+#else
+    if (sd.object_flag & SD_OBJECT_SHADOW_CATCHER) {
+      cy_set_error(err, CY_ERR_FEATURE, 5); /* the _tex kernels render shadow catchers */
+    }
+#endif
     if (((sd.flag & SD_HOLDOUT) || (sd.object_flag & SD_OBJECT_HOLDOUT_MASK)) &&
         (state.flag & PATH_RAY_TRANSPARENT_BACKGROUND)) {
       /* holdout (kernel_path.h:285-296): the holdout weight makes the pixel
@@ -2209,7 +2892,12 @@ CY_FN bool shade_path(const CyGlobals *kg,
       /* path_radiance_accum_emission (kernel_accumulate.h:304-335) */
       cfloat3 contribution = mul3(throughput, emission);
       contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
-      L = add3(L, contribution);
+#if CY_CATCHER
+      if (!(state.flag & PATH_RAY_SHADOW_CATCHER))
+#endif
+      {
+        L = add3(L, contribution);
+      }
     }
 
     /* Russian roulette (kernel_path.h:587-599) */
@@ -2235,6 +2923,15 @@ CY_FN bool shade_path(const CyGlobals *kg,
      * PRNG_BOUNCE_NUM (the indirect ray's state), and a walk that never leaves
      * ends the path */
     bool sss_bounce = false;
+#if CY_CLOSURE_EXT
+    bool sss_update = false; /* random walk: the exit ray's volume stack is updated */
+    CyIsect ss_hit;
+    cfloat3 ss_weight, ss_N;
+    CyRay ss_ray;
+    int ss_type = 0;
+    float ss_rough = 0.0f;
+    const cfloat3 in_P = ray.P;
+#endif
     if (!terminated) {
       if (KD->integrator.use_ambient_occlusion) {
         cy_set_error(err, CY_ERR_FEATURE, 6);
@@ -2247,13 +2944,13 @@ CY_FN bool shade_path(const CyGlobals *kg,
         if (sc) {
           const int bssrdf_type = sc->type;
           const float bssrdf_rough = bssrdf_roughness(sc);
-          CyIsect ss_hit;
-          cfloat3 ss_weight;
-          CyRay ss_ray;
           if (CLOSURE_IS_DISK_BSSRDF(bssrdf_type)) {
             /* the exit points' light and bounces replace the path's own */
             if (VOL) {
-              cy_set_error(err, CY_ERR_CLOSURE, (uint)bssrdf_type); /* refused with volumes at load */
+              CySD stack_sd;
+              sss_disk_rays = subsurface_disk_paths<true>(kg, b, slot, cam_item, &sd, sc, bssrdf_u, bssrdf_v,
+                                                          &state, &ray, &throughput, &L, mem, err, &vstack,
+                                                          &stack_sd);
             }
             else {
               sss_disk_rays = subsurface_disk_paths(kg, b, slot, cam_item, &sd, sc, bssrdf_u, bssrdf_v, &state,
@@ -2265,10 +2962,17 @@ CY_FN bool shade_path(const CyGlobals *kg,
                                           err)) {
             /* subsurface_scatter_multi_setup (kernel_subsurface.h:284-313) */
             shader_setup_from_subsurface(kg, &sd, &ss_hit, &ss_ray);
-            cfloat3 ss_N = sd.N;
+            ss_N = sd.N;
             subsurface_color_bump_blur(kg, &sd, &state, &ss_weight, &ss_N, err);
             subsurface_scatter_setup_diffuse_bsdf(kg, &sd, bssrdf_type, bssrdf_rough, ss_weight, ss_N);
             sss_bounce = true;
+            if (VOL && (sd.object_flag & SD_OBJECT_INTERSECTS_VOLUME)) {
+              /* the exit ray's stack is updated after its bounce, so the exit
+               * point's light sample is traced here with the path's stack */
+              sss_update = true;
+              ss_type = bssrdf_type;
+              ss_rough = bssrdf_rough;
+            }
           }
           else {
             terminated = true;
@@ -2290,7 +2994,26 @@ CY_FN bool shade_path(const CyGlobals *kg,
 #else
       if (KD->integrator.use_direct_light && (sd.flag & SD_BSDF_HAS_EVAL)) {
 #endif
-        connect_light<false>(kg, b, slot, &sd, &state, throughput, &L, shadow, &shadow_D, mem, err);
+#if CY_CLOSURE_EXT
+        if (VOL && sss_update) {
+          bool reused = false;
+          connect_light_exit_vol(kg, b, slot, &sd, &state, throughput, &L, &reused, mem, err, &vstack);
+          if (reused) {
+            shader_setup_from_subsurface(kg, &sd, &ss_hit, &ss_ray);
+            subsurface_scatter_setup_diffuse_bsdf(kg, &sd, ss_type, ss_rough, ss_weight, ss_N);
+          }
+        }
+        else
+#endif
+#if CY_CATCHER
+        if (state.flag & PATH_RAY_SHADOW_CATCHER) {
+          catcher_connect_all_lights(kg, &sd, &state, throughput, &catcher, mem, err);
+        }
+        else
+#endif
+        {
+          connect_light<false>(kg, b, slot, &sd, &state, throughput, &L, shadow, &shadow_D, mem, err);
+        }
       }
 #if CY_CLOSURE_EXT
       if (VOL && *shadow) {
@@ -2355,6 +3078,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
             vop_shader = (uint)sd.shader;
             vop_flags |= CY_VOP_PATH | ((sd.flag & SD_BACKFACING) ? CY_VOP_BACKFACING : 0u);
           }
+          if (VOL && sss_update) {
+            /* kernel_path_subsurface.h:92-99: the surface's own update, then
+             * the volume surfaces from the path's previous point to the exit
+             * point (no shadow is pending: it was traced above) */
+            if (vop_flags & CY_VOP_PATH) {
+              volume_stack_enter_exit(sd.flag, sd.object, sd.shader, &vstack);
+              vop_flags &= ~(CY_VOP_PATH | CY_VOP_BACKFACING);
+            }
+            CyRay volume_ray;
+            volume_ray.P = in_P;
+            volume_ray.D = normalize_len3(sub3(ray.P, in_P), &volume_ray.t);
+            CySD stack_sd;
+            volume_stack_update_for_subsurface(kg, &stack_sd, &volume_ray, &vstack, err);
+          }
 #endif
         }
       }
@@ -2371,6 +3108,16 @@ CY_FN bool shade_path(const CyGlobals *kg,
      * (kernel_path_subsurface_setup_indirect), if any */
     const int pending = (sss_disk_rays == 0 || cam_item != CY_NO_ITEM) ? 0 : (int)cy_ld(&b->sss_count[slot]);
     if (pending > 0) {
+      if (VOL) {
+        /* the record's own stack; a shadow ray still pending keeps the ended
+         * path's (and its own crossing of the surface) */
+        if (*shadow) {
+          vol_stack_write(sss_vol_at(b, slot, CY_SSS_RECS), &vstack);
+          vop_flags |= CY_VOP_OWN_STACK;
+        }
+        vop_flags &= ~CY_VOP_PATH;
+        vol_stack_read(sss_vol_at(b, slot, pending - 1), &vstack);
+      }
       if (kg->use_ray_diff) {
         CyDiff3 pdP, pdD;
         sss_rec_load(b, slot, pending - 1, kg, &state, &ray, &throughput, &pdP, &pdD);
@@ -2389,6 +3136,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
   }
 #endif
 
+#if CY_CATCHER
+  if (b->catcher && (cont || *shadow)) {
+    catcher_store(b, slot, &catcher);
+  }
+#endif
   if (cont) {
     store_state(b, slot, &state);
     if (cam_item != CY_NO_ITEM) {
@@ -2413,7 +3165,17 @@ CY_FN bool shade_path(const CyGlobals *kg,
     cy_st(&b->shadow_L[slot], sl);
     return false;
   }
+#if CY_CATCHER
+  if (b->catcher) {
+    CY_DBG3(&state, "catcher total", catcher.path_total);
+    CY_DBG3(&state, "catcher shaded", catcher.path_total_shaded);
+    CY_DBG3(&state, "catcher background", catcher.background);
+    CY_DBG3(&state, "catcher tp transp has", mk3(catcher.throughput, catcher.transparency, (float)catcher.has));
+  }
+  slot_finish(b, tile, slot, cam_item, L, L_transparent, b->catcher ? &catcher : nullptr);
+#else
   slot_finish(b, tile, slot, cam_item, L, L_transparent);
+#endif
   *finished = true;
   return false;
 }

@@ -981,6 +981,155 @@ CY_FN bool bvh2_shadow_all(const CyGlobals *kg,
   return false;
 }
 
+#if CY_CLOSURE_EXT
+/* scene_intersect_volume_all (bvh/bvh.h:500-531, bvh/bvh_volume_all.h:38-327)
+ * on the BVH2: every triangle of an object with a volume (SD_OBJECT_HAS_VOLUME)
+ * the ray crosses within its own t, recorded in traversal order up to max_hits;
+ * instances without a volume are not entered, curves are never recorded.  Hits
+ * inside an instance get their t scaled to world space at the pop (or when
+ * max_hits ends the query inside it).  Returns the number of hits. */
+template<bool INST, int HAIR = 0>
+CY_FN uint bvh2_volume_all(const CyGlobals *kg, const CyRay *ray, CyIsect *hits, uint max_hits, uint visibility,
+                           uint *err)
+{
+  int stack[BVH_STACK_SIZE];
+  stack[0] = ENTRYPOINT_SENTINEL;
+  int stack_ptr = 0;
+  int node_addr = KD->bvh.root;
+  const float tmax = ray->t;
+  cfloat3 P = ray->P;
+  cfloat3 dir = bvh_clamp_direction(ray->D);
+  cfloat3 idir = rcp3(dir);
+  int object = OBJECT_NONE;
+  float isect_t = tmax;
+  uint num_hits_in_instance = 0;
+  uint num_hits = 0;
+  const hc_float4 *nodes = kg->__bvh_nodes;
+  do {
+    do {
+      while (node_addr >= 0 && node_addr != ENTRYPOINT_SENTINEL) {
+        const hc_float4 cnodes = nodes[node_addr + 0];
+        float c0min, c1min;
+        const int traverse_mask = bvh2_node_intersect<HAIR>(nodes, node_addr, cnodes, P, dir, idir, isect_t,
+                                                            visibility, &c0min, &c1min);
+        node_addr = as_int(cnodes.z);
+        int node_addr_child1 = as_int(cnodes.w);
+        if (traverse_mask == 3) {
+          if (c1min < c0min) {
+            const int tmp = node_addr;
+            node_addr = node_addr_child1;
+            node_addr_child1 = tmp;
+          }
+          if (++stack_ptr >= BVH_STACK_SIZE) {
+            cy_set_error(err, CY_ERR_BVH_STACK, 0);
+            return num_hits;
+          }
+          stack[stack_ptr] = node_addr_child1;
+        }
+        else if (traverse_mask == 2) {
+          node_addr = node_addr_child1;
+        }
+        else if (traverse_mask == 0) {
+          node_addr = stack[stack_ptr];
+          --stack_ptr;
+        }
+      }
+      if (node_addr < 0) {
+        const hc_float4 leaf = kg->__bvh_leaf_nodes[-node_addr - 1];
+        int prim_addr = as_int(leaf.x);
+        if (prim_addr >= 0) {
+          const int prim_addr2 = as_int(leaf.y);
+          const uint type = as_uint(leaf.w);
+          node_addr = stack[stack_ptr];
+          --stack_ptr;
+          if ((type & PRIMITIVE_ALL) == PRIMITIVE_TRIANGLE) {
+            for (; prim_addr < prim_addr2; prim_addr++) {
+              const int tri_object = (object == OBJECT_NONE) ? (int)kg->__prim_object[prim_addr] : object;
+              if (!(kg->__object_flag[tri_object] & SD_OBJECT_HAS_VOLUME)) {
+                continue;
+              }
+              const uint tri_vindex = kg->__prim_tri_index[prim_addr];
+              const hc_float4 *tv = kg->__prim_tri_verts + tri_vindex;
+              float tt, uu, vv;
+              if (ray_triangle_intersect(P, dir, isect_t, f4to3(tv[0]), f4to3(tv[1]), f4to3(tv[2]), &uu, &vv,
+                                         &tt) &&
+                  (kg->__prim_visibility[prim_addr] & visibility)) {
+                CyIsect *h = &hits[num_hits];
+                h->prim = prim_addr;
+                h->object = object;
+                h->type = PRIMITIVE_TRIANGLE;
+                h->u = uu;
+                h->v = vv;
+                h->t = tt;
+                num_hits++;
+                num_hits_in_instance++;
+                if (num_hits == max_hits) {
+                  if (INST && object != OBJECT_NONE) {
+                    /* bvh_volume_all.h:180-186 scales by the instance-space direction here */
+                    const float t_fac = 1.0f / len3(transform_direction(object_itfm(kg, object), dir));
+                    for (uint i = 0; i < num_hits_in_instance; i++) {
+                      hits[num_hits - 1 - i].t *= t_fac;
+                    }
+                  }
+                  return num_hits;
+                }
+              }
+            }
+          }
+          else if (!(HAIR != 0 && (type & PRIMITIVE_ALL_CURVE))) {
+            cy_set_error(err, CY_ERR_PRIMITIVE, type);
+            return num_hits;
+          }
+        }
+        else if (!INST) {
+          cy_set_error(err, CY_ERR_FEATURE, 1);
+          return num_hits;
+        }
+        else {
+          object = (int)kg->__prim_object[-prim_addr - 1];
+          if (kg->__object_flag[object] & SD_OBJECT_HAS_VOLUME) {
+            /* instance push */
+            isect_t = bvh_instance_push(kg, object, ray, &P, &dir, &idir, isect_t);
+            num_hits_in_instance = 0;
+            if (++stack_ptr >= BVH_STACK_SIZE) {
+              cy_set_error(err, CY_ERR_BVH_STACK, 0);
+              return num_hits;
+            }
+            stack[stack_ptr] = ENTRYPOINT_SENTINEL;
+            node_addr = (int)kg->__object_node[object];
+          }
+          else {
+            object = OBJECT_NONE;
+            node_addr = stack[stack_ptr];
+            --stack_ptr;
+          }
+        }
+      }
+    } while (node_addr != ENTRYPOINT_SENTINEL);
+    if (INST && stack_ptr >= 0) {
+      /* instance pop */
+      if (num_hits_in_instance) {
+        const float t_fac = 1.0f / len3(transform_direction(object_itfm(kg, object), ray->D));
+        for (uint i = 0; i < num_hits_in_instance; i++) {
+          hits[num_hits - 1 - i].t *= t_fac;
+        }
+        P = ray->P;
+        dir = bvh_clamp_direction(ray->D);
+        idir = rcp3(dir);
+      }
+      else {
+        bvh_instance_pop(kg, object, ray, &P, &dir, &idir, CY_FLT_MAX);
+      }
+      isect_t = tmax;
+      object = OBJECT_NONE;
+      node_addr = stack[stack_ptr];
+      --stack_ptr;
+    }
+  } while (node_addr != ENTRYPOINT_SENTINEL);
+  return num_hits;
+}
+#endif
+
 /* Record-all shadow traversal of the W-wide layout (non-instanced scenes;
  * kg->bvhw_width 4 or 8, oriented-box nodes in ribbon scenes): the query of
  * bvh2_shadow_all above with the same bound (the ray's own t, which no

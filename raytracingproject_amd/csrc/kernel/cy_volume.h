@@ -111,6 +111,110 @@ CY_FN void volume_stack_enter_exit(int sd_flag, int sd_object, int sd_shader, Cy
   }
 }
 
+/* The volume objects' surfaces along a ray: scene_intersect_volume_all with
+ * 2 * VOLUME_STACK_SIZE records (kernel_volume.h:1198-1199, 1366-1367),
+ * sorted by distance as qsort with intersections_compare does it
+ * (kernel_volume.h:1206, 1371; glibc's merge sort keeps equal distances in
+ * recording order). */
+#define CY_VOLUME_ALL_HITS 64
+#define CY_REF_VOLUME_STACK 32 /* kernel_types.h VOLUME_STACK_SIZE */
+CY_FN uint volume_all_sorted(const CyGlobals *kg, const CyRay *ray, CyIsect *hits, uint visibility, uint *err)
+{
+  if (!scene_intersect_valid(ray)) {
+    return 0;
+  }
+  const uint n = kg->have_curves ?
+                     bvh2_volume_all<true, 3>(kg, ray, hits, CY_VOLUME_ALL_HITS, visibility, err) :
+                     bvh2_volume_all<true>(kg, ray, hits, CY_VOLUME_ALL_HITS, visibility, err);
+  for (uint i = 1; i < n; i++) {
+    const CyIsect h = hits[i];
+    int j = (int)i - 1;
+    while (j >= 0 && hits[j].t > h.t) {
+      hits[j + 1] = hits[j];
+      j--;
+    }
+    hits[j + 1] = h;
+  }
+  return n;
+}
+
+/* kernel_volume_stack_init (kernel_volume.h:1165-1306), __VOLUME_RECORD_ALL__
+ * branch: with kernel_data.cam.is_inside_volume the camera ray, made infinite,
+ * collects the volumes it leaves without having entered them; stack_sd is
+ * scratch.  A stack beyond CY_VOLUME_STACK entries, or more entered volumes
+ * than the reference's array holds, sets an error instead. */
+CY_NOINLINE void volume_stack_init_camera(const CyGlobals *kg, CySD *stack_sd, const CyRay *ray, uint path_flag,
+                                          CyVolumeStack *stack, uint *err)
+{
+  if (!KD->cam.is_inside_volume) {
+    volume_stack_init(kg, stack);
+    return;
+  }
+  CyRay volume_ray = *ray;
+  volume_ray.t = CY_FLT_MAX;
+  CyIsect hits[CY_VOLUME_ALL_HITS];
+  const uint num_hits = volume_all_sorted(kg, &volume_ray, hits, path_flag & PATH_RAY_ALL_VISIBILITY, err);
+  int stack_index = 0, enclosed_index = 0;
+  int enclosed_volumes[CY_REF_VOLUME_STACK];
+  for (uint hit = 0; hit < num_hits; hit++) {
+    shader_setup_from_ray(kg, stack_sd, &hits[hit], &volume_ray);
+    if (stack_sd->flag & SD_BACKFACING) {
+      bool need_add = true;
+      for (int i = 0; i < enclosed_index && need_add; i++) {
+        if (enclosed_volumes[i] == stack_sd->object) {
+          need_add = false;
+        }
+      }
+      for (int i = 0; i < stack_index && need_add; i++) {
+        if (stack->e[i].object == stack_sd->object) {
+          need_add = false;
+          break;
+        }
+      }
+      if (need_add && stack_index < CY_REF_VOLUME_STACK - 1) {
+        if (stack_index >= CY_VOLUME_STACK - 1) {
+          cy_set_error(err, CY_ERR_FEATURE, 14); /* more nested volumes than the device's stack */
+          break;
+        }
+        stack->e[stack_index].object = stack_sd->object;
+        stack->e[stack_index].shader = stack_sd->shader;
+        ++stack_index;
+      }
+    }
+    else {
+      if (enclosed_index >= CY_REF_VOLUME_STACK) {
+        cy_set_error(err, CY_ERR_FEATURE, 14); /* beyond the reference's enclosed_volumes */
+        break;
+      }
+      enclosed_volumes[enclosed_index++] = stack_sd->object;
+    }
+  }
+  /* kernel_volume.h:1293-1305: no volume found and no world volume (a world
+   * volume is not put back when the camera is found in the air) */
+  if (stack_index == 0 && KD->background.volume_shader == SHADER_NONE) {
+    stack->e[0].shader = KD->background.volume_shader;
+    stack->e[0].object = OBJECT_NONE;
+    stack->e[1].shader = SHADER_NONE;
+  }
+  else {
+    stack->e[stack_index].shader = SHADER_NONE;
+  }
+}
+
+/* kernel_volume_stack_update_for_subsurface (kernel_volume.h:1354-1375): the
+ * volume surfaces between the path's previous surface point and a subsurface
+ * exit point enter or leave their volumes on the exit ray's stack. */
+CY_NOINLINE void volume_stack_update_for_subsurface(const CyGlobals *kg, CySD *stack_sd, const CyRay *ray,
+                                                    CyVolumeStack *stack, uint *err)
+{
+  CyIsect hits[CY_VOLUME_ALL_HITS];
+  const uint num_hits = volume_all_sorted(kg, ray, hits, PATH_RAY_ALL_VISIBILITY, err);
+  for (uint hit = 0; hit < num_hits; hit++) {
+    shader_setup_from_ray(kg, stack_sd, &hits[hit], ray);
+    volume_stack_enter_exit(stack_sd->flag, stack_sd->object, stack_sd->shader, stack);
+  }
+}
+
 /* kernel_volume_clean_stack: after a miss only the world's volume stays. */
 CY_FN void volume_stack_clean(const CyGlobals *kg, CyVolumeStack *stack)
 {
@@ -659,5 +763,7 @@ CY_FN int shader_volume_phase_sample(const CySD *sd, float randu, float randv, c
 }
 
 #endif /* CY_CLOSURE_EXT */
+
+#include "cy_volume_decoupled.h"
 
 #endif /* CY_VOLUME_H */

@@ -24,7 +24,9 @@ from . import nodes as _nodes  # compile_scene has a local "nodes" (BVH nodes)
 # ---------------------------------------------------------------------------
 # constants of the device ABI (kernel_types.h / svm_types.h)
 PATH_RAY_ALL_VISIBILITY = (1 << 14) - 1
+PATH_RAY_SHADOW_OPAQUE_NON_CATCHER = 1 << 7
 PATH_RAY_SHADOW_OPAQUE_CATCHER = 1 << 8
+PATH_RAY_SHADOW_TRANSPARENT_NON_CATCHER = 1 << 9
 PATH_RAY_SHADOW_TRANSPARENT_CATCHER = 1 << 10
 PATH_RAY_NODE_UNALIGNED = 1 << 13
 SHADER_SMOOTH_NORMAL = 1 << 31
@@ -133,10 +135,12 @@ SD_HAS_BUMP = 1 << 25
 SD_HAS_VOLUME = 1 << 18
 SD_HAS_ONLY_VOLUME = 1 << 19
 SD_HETEROGENEOUS_VOLUME = 1 << 20
+SD_VOLUME_EQUIANGULAR, SD_VOLUME_MIS = 1 << 22, 1 << 23  # kernel_types.h:887-889 ShaderDataFlag
 SD_NEED_VOLUME_ATTRIBUTES = 1 << 28
 SD_OBJECT_HAS_VOLUME = 1 << 4
 SD_OBJECT_INTERSECTS_VOLUME = 1 << 5
 SD_OBJECT_HOLDOUT_MASK = 1 << 0  # kernel_types.h ShaderDataObjectFlag; object.cpp:547-548 use_holdout
+SD_OBJECT_SHADOW_CATCHER = 1 << 7  # object.cpp:714-719 is_shadow_catcher
 CLOSURE_VOLUME_ABSORPTION_ID = 43
 CLOSURE_VOLUME_HENYEY_GREENSTEIN_ID = 44
 NODE_CLOSURE_VOLUME, NODE_PRINCIPLED_VOLUME = 40, 41
@@ -200,6 +204,9 @@ class Closure:
     # that name at the camera path's first hit (svm_aov.h); names without a
     # pass in Scene.aovs are dropped, as OutputAOVNode::simplify drops them
     aovs: dict | None = None
+    # Shader::volume_sampling_method of the material's volume: "distance",
+    # "equiangular" or "multiple_importance" (SD_VOLUME_EQUIANGULAR / _MIS)
+    volume_sampling: str = "distance"
 
     def closure_type(self) -> int:
         """The ClosureType the node compiles to, after simplify_settings
@@ -899,6 +906,10 @@ class Mesh:
     object_random: float | None = None  # Object::random_id / 0xFFFFFFFF
     # Object::use_holdout (SD_OBJECT_HOLDOUT_MASK, object.cpp:547-548)
     holdout: bool = False
+    # Object::is_shadow_catcher (SD_OBJECT_SHADOW_CATCHER, object.cpp:714-719;
+    # hidden from the shadow rays of paths behind a catcher,
+    # Object::visibility_for_tracing, object.cpp:260-270); meshes drawn once
+    shadow_catcher: bool = False
     # the particle this object instances (Object::particle_system /
     # particle_index, object.cpp:440-452; ParticleInfo node): a dict of
     # KernelParticle fields index, age, lifetime, size, rotation (4),
@@ -975,6 +986,9 @@ class Lamp:
     use_mis: bool = True
     cast_shadow: bool = True
     max_bounces: int = 1024
+    # Light::samples (KernelLight.samples, light_select_num_samples): light
+    # samples per shading point when all lights are sampled (decoupled volumes)
+    samples: int = 1
     # the light's shader (Light::shader; None: the shared default emission
     # shader of strength 1, color and strength then go to KernelLight.strength)
     shader: "Closure | None" = None
@@ -1058,6 +1072,9 @@ class Scene:
     world_volume: "Closure | None" = None
     # Film exposure (film.cpp:363; applied by film convert)
     exposure: float = 1.0
+    # decoupled volume ray marching (the CPU device's KernelIntegrator, see
+    # compile_scene); False: distance sampling as GPU devices integrate
+    volume_decoupled: bool = False
     # AOV passes of the view layer (BlenderSync::sync_render_passes,
     # Pass::add(PASS_AOV_COLOR / PASS_AOV_VALUE, name)): (name, "color" | "value")
     aovs: list = field(default_factory=list)
@@ -1435,6 +1452,15 @@ def compile_scene(scene: Scene) -> DeviceScene:
                 flag |= SD_HETEROGENEOUS_VOLUME
             if _volume_attribute_dependency(m.volume):
                 flag |= SD_NEED_VOLUME_ATTRIBUTES
+            # shader.cpp:541-544 Shader::volume_sampling_method (Blender's
+            # default is multiple importance; "distance" here unless asked)
+            vs = getattr(m, "volume_sampling", "distance")
+            if vs == "equiangular":
+                flag |= SD_VOLUME_EQUIANGULAR
+            elif vs == "multiple_importance":
+                flag |= SD_VOLUME_MIS
+            elif vs != "distance":
+                raise ValueError(f"volume_sampling {vs!r}: distance, equiangular or multiple_importance")
         kshaders[i].flags = flag
         kshaders[i].pass_id = int(getattr(m, "pass_index", 0))
     tri_shader = tri_shader_idx.astype(np.uint32) | np.uint32(SHADER_CAST_SHADOW | SHADER_AREA_LIGHT)
@@ -1462,6 +1488,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
             object_flag[i] = SD_OBJECT_TRANSFORM_APPLIED
         if ob.get("holdout"):
             object_flag[i] |= SD_OBJECT_HOLDOUT_MASK
+        if ob.get("shadow_catcher"):
+            object_flag[i] |= SD_OBJECT_SHADOW_CATCHER
         object_node[i] = np.uint32(ob["node"] & 0xFFFFFFFF)
     # particles (object.cpp:440-452, particles.cpp:57-103 device_update_particles):
     # entry 0 is the dummy every object without a particle reads; the
@@ -1607,12 +1635,16 @@ def compile_scene(scene: Scene) -> DeviceScene:
     ki.sample_clamp_direct = FLT_MAX
     ki.sample_clamp_indirect = FLT_MAX
     ki.branched = 0
-    ki.volume_decoupled = 0
+    # DeviceInfo::has_volume_decoupled (integrator.cpp:165): the CPU device's
+    # decoupled ray marching, with the Integrator's "sample all lights"
+    # defaults (true) that choose it for every volume segment
+    # (kernel_volume_use_decoupled); GPU devices upload 0
+    ki.volume_decoupled = int(scene.volume_decoupled)
     ki.diffuse_samples = ki.glossy_samples = ki.transmission_samples = 1
     ki.ao_samples = ki.mesh_light_samples = ki.subsurface_samples = ki.volume_samples = 1
     ki.start_sample = 0
-    ki.sample_all_lights_direct = 0
-    ki.sample_all_lights_indirect = 0
+    ki.sample_all_lights_direct = int(scene.volume_decoupled)
+    ki.sample_all_lights_indirect = int(scene.volume_decoupled)
     ki.sampling_pattern = 0
     ki.aa_samples = scene.samples
     if scene.adaptive_min_samples == 0:
@@ -2142,9 +2174,11 @@ def _pack_geometry(scene: Scene) -> dict:
         geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(m.smooth), applied=True, mesh=m))
         objects.append(dict(geom=len(geoms) - 1, tfm=ident, applied=True, color=m.object_color,
                             pass_index=m.pass_index, random=m.object_random, holdout=m.holdout,
-                            particle=m.particle))
+                            particle=m.particle, shadow_catcher=m.shadow_catcher))
     for inst in scene.instances:
         tfm = np.asarray(inst.tfm, dtype=np.float64).reshape(3, 4)
+        if inst.mesh.shadow_catcher:
+            raise ValueError("shadow catchers are supported on meshes drawn once, not on instances")
         if users[id(inst.mesh)] == 1:
             v, t, sh, nrm = _mesh_arrays(inst.mesh, tfm.astype(np.float32))
             geoms.append(dict(v=v, t=t, sh=sh, nrm=nrm, smooth=bool(inst.mesh.smooth), applied=True, mesh=inst.mesh,
@@ -2184,6 +2218,11 @@ def _pack_geometry(scene: Scene) -> dict:
     hair = _pack_hair(objects, scene.hair_shape)
 
     vis_obj = PATH_RAY_ALL_VISIBILITY & ~(PATH_RAY_SHADOW_OPAQUE_CATCHER | PATH_RAY_SHADOW_TRANSPARENT_CATCHER)
+    # a shadow catcher is seen by every shadow ray but those of paths behind a
+    # catcher (PATH_RAY_SHADOW_NON_CATCHER, kernel_shadow.h:402-404)
+    vis_catcher = PATH_RAY_ALL_VISIBILITY & ~(PATH_RAY_SHADOW_OPAQUE_NON_CATCHER |
+                                              PATH_RAY_SHADOW_TRANSPARENT_NON_CATCHER)
+    catchers = [oi for oi, ob in enumerate(objects) if ob.get("shadow_catcher")]
 
     # top level: triangles of objects with applied transforms + one reference per instance
     ref_tri, ref_obj = [], []
@@ -2197,11 +2236,15 @@ def _pack_geometry(scene: Scene) -> dict:
     ref_tri = np.concatenate(ref_tri) if ref_tri else np.zeros(0, np.int64)
     ref_obj = np.concatenate(ref_obj) if ref_obj else np.zeros(0, np.int64)
     if hair["nseg"]:
+        if catchers:
+            raise ValueError("shadow catchers in a scene with curves are not supported")
         return _pack_geometry_with_curves(objects, geoms, ref_tri, ref_obj, tri_pos, ntri, nvert, tri_shader_idx,
                                           tri_smooth, tri_vindex, tri_vnormal, vis_obj, hair)
     nref = len(ref_tri)
     is_inst = ref_tri < 0
     vis = np.full(nref, vis_obj, dtype=np.uint32)
+    if catchers:
+        vis[np.isin(ref_obj, catchers)] = vis_catcher
     if is_inst.any():
         boxes = np.zeros((nref, 6), dtype=np.float32)
         tp = tri_pos[np.where(is_inst, 0, ref_tri)]
@@ -2463,7 +2506,7 @@ def _pack_lamp(kl, lamp: Lamp, shader_index: int) -> bool:
     if not lamp.cast_shadow:
         shader_id &= ~SHADER_CAST_SHADOW
     kl.type = LIGHT_TYPES[lamp.kind]
-    kl.samples = 1
+    kl.samples = int(lamp.samples)
     strength = _f3(lamp.color) * f32(lamp.strength)
     kl.strength[:] = [float(c) for c in strength]
     uni = [0.0] * 12

@@ -1007,6 +1007,44 @@ def shading_holdout(width=48, height=48, samples=8) -> sc.Scene:
     return s
 
 
+def shadow_catcher(width=48, height=48, samples=8, transparent_film=False) -> sc.Scene:
+    """Shadow catcher (golden parity case; kernel_path.h:265-281,
+    kernel_accumulate.h:526-620): a floor that is a shadow catcher under a
+    diffuse sphere, a glossy box, a half-transparent pane (its shadow through
+    the transparent-shadow evaluation, seen by the catcher) and a second,
+    smaller catcher quad lifted off the floor (catchers are hidden from the
+    shadow rays of paths behind a catcher); a point lamp with two samples, an
+    area lamp and a mesh light (the all-lights connection behind a catcher,
+    lamps' and mesh lights' sample streams), a coloured world.
+    transparent_film=True: the catcher's shadow lowers the alpha instead of
+    darkening the background seen through it."""
+    white = sc.diffuse((0.7, 0.7, 0.7))
+    red = sc.diffuse((0.8, 0.25, 0.2))
+    gloss = sc.glossy((0.8, 0.8, 0.9), 0.25)
+    pane = sc.mix(0.5, sc.transparent((0.9, 0.9, 0.9)), sc.diffuse((0.2, 0.6, 0.3)))
+    light = sc.emission((1.0, 0.9, 0.8), 6.0)
+    materials = [white, red, gloss, pane, light]
+    meshes = [
+        sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0, shadow_catcher=True),
+        sc.Mesh(*_ellipsoid((-0.8, -0.45, 0.2), (0.5, 0.5, 0.5), 20, 12), shader=1, smooth=True),
+        sc.Mesh(*_box((0.8, -0.55, -0.1), (0.6, 0.9, 0.6), 0.4), shader=2),
+        sc.Mesh(*_quad((-0.4, -0.2, -1.2), (0.6, -0.2, -1.2), (0.6, 0.7, -1.2), (-0.4, 0.7, -1.2)), shader=3),
+        sc.Mesh(*_quad((0.9, -0.7, -1.8), (1.7, -0.7, -1.8), (1.7, -0.7, -1.0), (0.9, -0.7, -1.0)), shader=0,
+                shadow_catcher=True),
+        sc.Mesh(*_quad((-1.6, 2.2, -1.2), (-0.8, 2.2, -1.2), (-0.8, 2.2, -0.4), (-1.6, 2.2, -0.4)), shader=4),
+    ]
+    lamps = [sc.Lamp("point", co=(1.5, 2.0, -1.5), size=0.2, color=(1.0, 0.9, 0.8), strength=60.0, samples=2),
+             sc.Lamp("area", co=(-1.8, 1.8, 1.0), direction=(0.0, -1.0, 0.0), axisv=(0.0, 0.0, 1.0), size=0.8,
+                     color=(0.7, 0.8, 1.0), strength=40.0)]
+    cam = sc.Camera(eye=(0.0, 0.8, -3.6), target=(0.0, -0.3, 0.0), fov=math.radians(45.0), nearclip=0.01,
+                    farclip=100.0)
+    s = sc.Scene(width, height, cam, meshes, materials, world_color=(0.3, 0.35, 0.45), world_strength=1.0,
+                 samples=samples, lamps=lamps, name="shadow_catcher" + ("_film" if transparent_film else ""))
+    s.film_transparent = transparent_film
+    s.transparent_max_bounce = 8
+    return s
+
+
 def shading_info(width=48, height=48, samples=8) -> sc.Scene:
     """Particle Info and texture mapping: boxes instanced with a particle each
     (index, age, lifetime, size, location, velocity, angular velocity driving
@@ -1214,6 +1252,65 @@ def volume_cornell(width=48, height=48, samples=8, heterogeneous=False) -> sc.Sc
     s.world_volume = fog
     s.lamps = [sc.Lamp("point", co=(100.0, 450.0, 100.0), size=25.0, color=(1.0, 0.9, 0.8), strength=2.0e6)]
     s.name = "volume_hetero" if heterogeneous else "volume_cornell"
+    return s
+
+
+def sss_fog(width=48, height=48, samples=8, method="disk", box=False) -> sc.Scene:
+    """Subsurface scattering in a volume scene (golden parity cases): the
+    disk-BSSRDF (method="disk", sss_disk_cornell) or random-walk (sss_cornell)
+    spheres in world fog, so the exit points' light samples are attenuated by
+    the fog and every indirect ray carries its own volume stack
+    (kernel_path_subsurface.h:26-110).  box=True adds a smoke box overlapping
+    two of the spheres: their objects intersect a volume
+    (SD_OBJECT_INTERSECTS_VOLUME), so each exit ray's stack is updated by the
+    volume surfaces between the path's previous point and the exit point
+    (kernel_volume_stack_update_for_subsurface)."""
+    s = sss_disk_cornell(width, height, samples) if method == "disk" else sss_cornell(width, height, samples)
+    s.world_volume = sc.volume_scatter((0.9, 0.9, 0.95), density=0.0008, anisotropy=0.3)
+    if box:
+        s.materials.append(sc.material(volume=sc.principled_volume((0.7, 0.6, 0.5), density=0.01, anisotropy=0.2)))
+        s.meshes.append(sc.Mesh(*_box((250.0, 120.0, 240.0), (200, 160, 180), 0.3), shader=len(s.materials) - 1))
+    s.name = "sss_%s_fog%s" % ("disk" if method == "disk" else "walk", "_box" if box else "")
+    return s
+
+
+def volume_camera_inside(width=48, height=48, samples=8) -> sc.Scene:
+    """volume_cornell with the camera inside a volume object (golden parity
+    case): a thin smoke box around the eye reaching into the room, so
+    KernelCamera.is_inside_volume is set and every camera ray's volume stack is
+    found by the record-all volume query (kernel_volume_stack_init,
+    kernel_volume.h:1165-1306) -- the box the ray leaves without having
+    entered it."""
+    s = volume_cornell(width, height, samples)
+    s.materials.append(sc.material(volume=sc.volume_scatter((0.8, 0.85, 0.9), density=0.0015, anisotropy=0.1)))
+    s.meshes.append(sc.Mesh(*_box((278.0, 273.0, -350.0), (700, 700, 1100), 0.0), shader=len(s.materials) - 1))
+    s.name = "volume_camera_inside"
+    return s
+
+
+def volume_decoupled(width=48, height=48, samples=8, heterogeneous=False, sampling="distance") -> sc.Scene:
+    """volume_cornell as the reference's CPU device integrates it: decoupled
+    ray marching (KernelIntegrator.volume_decoupled, kernel_volume.h:754-1128)
+    with direct light from every lamp at each scatter segment
+    (kernel_branched_path_volume_connect_light).  sampling: the smoke box's
+    and the tinted glass's volume sampling method ("multiple_importance" also
+    gives the point lamp two samples and adds a second, area lamp, so
+    equiangular / distance MIS and the per-lamp branched sample streams are
+    exercised)."""
+    import dataclasses
+
+    s = volume_cornell(width, height, samples, heterogeneous=heterogeneous)
+    s.volume_decoupled = True
+    if sampling != "distance":
+        mats = list(s.materials)
+        base = len(mats) - (4 if heterogeneous else 3)
+        mats[base] = dataclasses.replace(mats[base], volume_sampling=sampling)
+        mats[base + 1] = dataclasses.replace(mats[base + 1], volume_sampling="equiangular")
+        s.materials = mats
+        s.lamps = [dataclasses.replace(s.lamps[0], samples=2),
+                   sc.Lamp("area", co=(420.0, 300.0, 80.0), direction=(0.0, 0.0, 1.0), size=60.0,
+                           color=(0.6, 0.8, 1.0), strength=4.0e4)]
+    s.name = "volume_decoupled" + ("_hetero" if heterogeneous else "") + ("" if sampling == "distance" else "_mis")
     return s
 
 

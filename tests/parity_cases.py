@@ -105,6 +105,11 @@ CASES = {
     # holdouts with a transparent film: Holdout closure, object holdout (also
     # over a part-transparent material), glass in front of a holdout
     "shading_holdout": lambda: scenes.shading_holdout(48, 48, 8),
+    # shadow catchers (kernel_path.h:265-281, kernel_accumulate.h:526-620): the
+    # catcher's background darkened by its shadows, or its alpha lowered with a
+    # transparent film; all-lights connection behind the catcher
+    "shadow_catcher": lambda: scenes.shadow_catcher(40, 40, 8),
+    "shadow_catcher_film": lambda: scenes.shadow_catcher(40, 40, 8, transparent_film=True),
     # Particle Info on instanced objects, TextureMapping with min/max and normalize
     "shading_info": lambda: scenes.shading_info(48, 48, 8),
     # Hair Info: strand flag, thickness, tangent normal, intercept / random curve attributes
@@ -117,6 +122,24 @@ CASES = {
     # heterogeneous: texture-driven densities, ray marching
     "volume_cornell": lambda: scenes.volume_cornell(48, 48, 8),
     "volume_hetero": lambda: scenes.volume_cornell(32, 32, 4, heterogeneous=True),
+    # decoupled volume ray marching with all-lights sampling, the CPU device's
+    # volume integrator (volume_decoupled = 1): homogeneous, heterogeneous
+    # (ray-marched records up to volume_max_steps), and equiangular / MIS
+    # distance sampling with two lamps and two samples per lamp
+    "volume_cornell_decoupled": lambda: scenes.volume_decoupled(48, 48, 8),
+    "volume_hetero_decoupled": lambda: scenes.volume_decoupled(32, 32, 4, heterogeneous=True),
+    "volume_mis_decoupled": lambda: scenes.volume_decoupled(40, 40, 8, sampling="multiple_importance"),
+    # subsurface scattering in volume scenes (kernel_path_subsurface.h): disk
+    # BSSRDF exit points in world fog (their shadows through the fog, a volume
+    # stack per indirect ray), and with a smoke box overlapping the spheres the
+    # exit rays' stack update (kernel_volume_stack_update_for_subsurface) for
+    # the disk and the random-walk BSSRDFs
+    "sss_disk_fog": lambda: scenes.sss_fog(40, 40, 8),
+    "sss_disk_fog_box": lambda: scenes.sss_fog(40, 40, 8, box=True),
+    "sss_walk_fog_box": lambda: scenes.sss_fog(40, 40, 8, method="random_walk", box=True),
+    # camera inside a volume object: each camera ray's stack from the
+    # record-all volume query (kernel_volume_stack_init)
+    "volume_camera_inside": lambda: scenes.volume_camera_inside(40, 40, 8),
     # Point Density textures (svm_voxel.h): 3D textures in a volume density and
     # on surfaces, object / world space, closest / linear / tricubic
     "shading_voxel": lambda: scenes.voxel_cornell(40, 40, 8),

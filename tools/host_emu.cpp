@@ -331,6 +331,10 @@ extern "C" int emu_render(const void *data,
   uint sss_count = 0;
   b.sss_rec = sss_rec;
   b.sss_count = &sss_count;
+  hc_uint4 sss_vol[(CY_SSS_RECS + 1) * (CY_VOLUME_STACK / 2)];
+  b.sss_vol = sss_vol;
+  hc_float4 catcher[CY_CATCHER_F4];
+  b.catcher = catcher; /* every scene: a path without a catcher leaves it unused */
   hc_float4 ray_diff[CY_RAY_DIFF_F4];
   hc_float4 shadow_dP[2];
   b.ray_diff = ray_diff;
