@@ -22,6 +22,9 @@
 #include "k_trav.h"
 #include "../host/cy_bvhw_collapse.h"
 
+/* PassType bits of the data passes (kernel_types.h:353-364: DEPTH .. MATERIAL_ID) */
+#define CY_HOST_DATA_PASSES ((1 << 2) | (1 << 3) | (1 << 4) | (1 << 5) | (1 << 6))
+
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
 
@@ -39,6 +42,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_accumulate(CyTile tile)
 
 /* chunk b carries on chunk a: the next sample range of the same RenderTile,
  * its items right after a's (stream_fill appends a tile's chunks in a row) */
+
 static __device__ bool stream_chunk_continues(const CyTileDesc &a, const CyTileDesc &b)
 {
   /* groups of one tile only (a tile split in sample ranges is never grouped) */
@@ -2740,9 +2744,11 @@ int hipcy_load_kernels(hipcy_device *dev)
     why = "curve_subdivisions outside 1..16";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
   else if (d.film.use_light_pass) why = "light passes";
-  else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | (1 << 11) | (1 << 12) | (1 << 13) | (1 << 14))) != 0 ||
+  else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | CY_HOST_DATA_PASSES | (1 << 11) | (1 << 12) |
+                                                                  (1 << 13) | (1 << 14))) != 0 ||
            d.film.pass_combined != 0)
-    why = "only the combined pass (+ AOV color / value, adaptive aux buffer / sample count)";
+    why = "only the combined pass (+ depth, normal, UV, object / material index, AOV color / value, adaptive aux "
+          "buffer / sample count)";
   else if (d.film.pass_denoising_data || d.film.cryptomatte_passes)
     why = "denoising / cryptomatte passes";
   else if (d.film.pass_adaptive_aux_buffer && (d.integrator.adaptive_step <= 0 ||
@@ -2826,6 +2832,11 @@ int hipcy_load_kernels(hipcy_device *dev)
   }
   if (!why.empty()) {
     return set_error(dev, "load_kernels: unsupported shader: " + why);
+  }
+  /* the data passes (depth, normal, UV, object / material index) are written
+   * by the extended shading kernels */
+  if (d.film.pass_flag & CY_HOST_DATA_PASSES) {
+    dev->shade_tex = true;
   }
   /* kernel_path_shader_apply (kernel_path.h:254-283): shadow-catcher objects
    * take the extended shading kernels (the catcher's part of PathRadiance per

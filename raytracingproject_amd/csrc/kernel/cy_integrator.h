@@ -2343,6 +2343,85 @@ CY_FN bool volume_bounce(const CyGlobals *kg, const CySD *sd, cfloat3 *throughpu
 }
 #endif
 
+#if CY_CLOSURE_EXT
+/* PassType bits of KernelFilm.pass_flag (kernel_types.h:353-364) */
+#define CY_PASS_DEPTH (1 << 2)
+#define CY_PASS_NORMAL (1 << 3)
+#define CY_PASS_UV (1 << 4)
+#define CY_PASS_OBJECT_ID (1 << 5)
+#define CY_PASS_MATERIAL_ID (1 << 6)
+#define CY_DATA_PASSES (CY_PASS_DEPTH | CY_PASS_NORMAL | CY_PASS_UV | CY_PASS_OBJECT_ID | CY_PASS_MATERIAL_ID)
+#define ATTR_STD_UV_ID 3u /* AttributeStandard ATTR_STD_UV */
+
+/* kernel_write_data_passes (kernel_passes.h:173-225), the writes at the
+ * camera path's first opaque-enough hit: depth, object and material index on
+ * the pixel's sample 0, the average BSDF normal and the UV map every sample
+ * (kernel_write_pass_float: added; atomically on the device, as the
+ * reference's GPU devices do). */
+CY_FN void write_data_passes(const CyGlobals *kg, float *buffer, const CySD *sd, const CyPathState *state)
+{
+  const int flag = KD->film.pass_flag;
+  if (state->sample == 0) {
+    if (flag & CY_PASS_DEPTH) {
+      /* camera_z_depth (kernel_camera.h:449-460) */
+      float depth;
+      if (KD->cam.type != 2 /* CAMERA_PANORAMA */) {
+        depth = transform_point((const struct cy_tfm *)&KD->cam.worldtocamera, sd->P).z;
+      }
+      else {
+        const hc_Transform &c = KD->cam.cameratoworld;
+        depth = len3(sub3(sd->P, mk3(c.x.w, c.y.w, c.z.w)));
+      }
+      cy_pass_add(buffer + KD->film.pass_depth, depth);
+    }
+    if (flag & CY_PASS_OBJECT_ID) {
+      /* object_pass_id (geom_object.h:237-243) */
+      cy_pass_add(buffer + KD->film.pass_object_id,
+                  (sd->object == OBJECT_NONE) ? 0.0f : kg->__objects[sd->object].pass_id);
+    }
+    if (flag & CY_PASS_MATERIAL_ID) {
+      /* shader_pass_id (geom_object.h:345-348) */
+      cy_pass_add(buffer + KD->film.pass_material_id,
+                  (float)kg->__shaders[(uint)sd->shader & SHADER_MASK].pass_id);
+    }
+  }
+  if (flag & CY_PASS_NORMAL) {
+    /* shader_bsdf_average_normal (kernel_shader.h:913-924) */
+    cfloat3 N = mk3(0.0f, 0.0f, 0.0f);
+    for (int i = 0; i < sd->num_closure; i++) {
+      const CyClosure *sc = &sd->closure[i];
+      if (CLOSURE_IS_BSDF_OR_BSSRDF(sc->type)) {
+        N = add3(N, mul3f(sc->N, fabsf(average3(sc->weight))));
+      }
+    }
+    N = is_zero3(N) ? sd->N : normalize3(N);
+    float *p = buffer + KD->film.pass_normal;
+    cy_pass_add(p + 0, N.x);
+    cy_pass_add(p + 1, N.y);
+    cy_pass_add(p + 2, N.z);
+  }
+  if (flag & CY_PASS_UV) {
+    /* primitive_uv (geom_primitive.h:259-268) */
+    cfloat3 uv = mk3(0.0f, 0.0f, 0.0f);
+    const CyAttr desc = find_attribute(kg, sd->object, sd->prim, ATTR_STD_UV_ID);
+    if (desc.offset != (int)ATTR_STD_NOT_FOUND) {
+      float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (sd->type & PRIMITIVE_ALL_TRIANGLE) {
+        triangle_attribute(kg, desc, sd->prim, sd->u, sd->v, 2, f);
+      }
+      else if (sd->type & PRIMITIVE_ALL_CURVE) {
+        curve_attribute(kg, desc, sd->prim, sd->type, sd->u, 2, f);
+      }
+      uv = mk3(f[0], f[1], 1.0f);
+    }
+    float *p = buffer + KD->film.pass_uv;
+    cy_pass_add(p + 0, uv.x);
+    cy_pass_add(p + 1, uv.y);
+    cy_pass_add(p + 2, uv.z);
+  }
+}
+#endif
+
 /* indirect_background (kernel_emission.h:288-345): the world seen along the
  * ray (its light-path exclusions, the world shader evaluated with the bounce
  * raised, the background MIS weight). */
@@ -2836,18 +2915,23 @@ CY_FN bool shade_path(const CyGlobals *kg,
        * only the single-pass flag, set at the first hit that is not
        * transparent enough to show what is behind it (the AOV outputs of
        * later hits are skipped) */
-      if (!(sd.flag & SD_TRANSPARENT) || KD->film.pass_alpha_threshold == 0.0f) {
-        state.flag |= PATH_RAY_SINGLE_PASS_DONE;
-      }
-      else {
+      bool single_pass = true;
+      if (!(!(sd.flag & SD_TRANSPARENT) || KD->film.pass_alpha_threshold == 0.0f)) {
         /* shader_bsdf_alpha (kernel_shader.h:860-868) */
         const cfloat3 tr = shader_bsdf_transparency(&sd);
         cfloat3 alpha = mk3(1.0f - tr.x, 1.0f - tr.y, 1.0f - tr.z);
         alpha = mk3(cmax(alpha.x, 0.0f), cmax(alpha.y, 0.0f), cmax(alpha.z, 0.0f));
         alpha = mk3(cmin(alpha.x, 1.0f), cmin(alpha.y, 1.0f), cmin(alpha.z, 1.0f));
-        if (average3(alpha) >= KD->film.pass_alpha_threshold) {
-          state.flag |= PATH_RAY_SINGLE_PASS_DONE;
+        single_pass = average3(alpha) >= KD->film.pass_alpha_threshold;
+      }
+      if (single_pass) {
+#if CY_CLOSURE_EXT
+        if (KD->film.pass_flag & CY_DATA_PASSES) {
+          write_data_passes(kg, item_buffer(tile, cam_item != CY_NO_ITEM ? cam_item : cy_ld(&b->item[slot])), &sd,
+                            &state);
         }
+#endif
+        state.flag |= PATH_RAY_SINGLE_PASS_DONE;
       }
     }
     if (KD->integrator.filter_glossy != CY_FLT_MAX) {

@@ -1078,6 +1078,9 @@ class Scene:
     # AOV passes of the view layer (BlenderSync::sync_render_passes,
     # Pass::add(PASS_AOV_COLOR / PASS_AOV_VALUE, name)): (name, "color" | "value")
     aovs: list = field(default_factory=list)
+    # data passes of the view layer (film.cpp pass_type_enum names): any of
+    # "depth", "normal", "uv", "object_id", "material_id"
+    passes: list = field(default_factory=list)
     # Film "Transparent" (Background::transparent, background.cpp:112): camera
     # rays that leave the scene, and holdouts, make the pixel transparent
     # (alpha = 1 - L_transparent) instead of showing the world
@@ -1533,8 +1536,11 @@ def compile_scene(scene: Scene) -> DeviceScene:
     # --- geometry attributes (geometry.cpp:379-474 device_update_attributes
     # + :508-620 update_attribute_element_offset)
     attr_arrays = None
-    if any(svm_compiler.requests):
-        attr_arrays = _pack_attributes(g, objects, tri_shader_idx, svm_compiler, kobjects)
+    # Scene::need_global_attribute (scene.cpp:341-351): a UV pass requests the
+    # UV map of every geometry, after its shaders' requests
+    global_reqs = [_nodes.ATTR_STD_UV] if "uv" in scene.passes else []
+    if any(svm_compiler.requests) or global_reqs:
+        attr_arrays = _pack_attributes(g, objects, tri_shader_idx, svm_compiler, kobjects, global_reqs)
 
     # --- lights (render/light.cpp:277-480, mesh lights only)
     # light.cpp:330-400: per object using emissive triangles, in object order,
@@ -1733,6 +1739,11 @@ def compile_scene(scene: Scene) -> DeviceScene:
     # (kernel_types.h:354-376 without __KERNEL_DEBUG__): AOV_COLOR 11,
     # AOV_VALUE 12, ADAPTIVE_AUX_BUFFER 13, SAMPLE_COUNT 14.
     passes = [("combined", 1, 4)]
+    # data passes (PassType DEPTH 2 .. MATERIAL_ID 6; components film.cpp:148-170:
+    # normal and UV take 4 floats, the kernel adds 3)
+    data_pass_types = {"depth": (2, 1), "normal": (3, 4), "uv": (4, 4), "object_id": (5, 1), "material_id": (6, 1)}
+    for name in sorted(set(scene.passes), key=lambda n: data_pass_types[n][0]):
+        passes.append((name, *data_pass_types[name]))
     seen = set()
     for name, kind in scene.aovs:
         if name not in seen:
@@ -1756,6 +1767,8 @@ def compile_scene(scene: Scene) -> DeviceScene:
             if kf.pass_aov_value_num == 0:
                 kf.pass_aov_value = stride
             kf.pass_aov_value_num += 1
+        elif kind in data_pass_types:
+            setattr(kf, "pass_" + kind, stride)
         elif kind == "adaptive_aux_buffer":
             kf.pass_adaptive_aux_buffer = stride
         else:
@@ -1990,7 +2003,7 @@ def _uv_tangents(gm: dict, uv: np.ndarray):
     return tc.reshape(-1, 3).astype(f32), sign.reshape(-1).astype(f32)
 
 
-def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobjects) -> dict:
+def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobjects, global_reqs=()) -> dict:
     """GeometryManager::device_update_attributes (render/geometry.cpp:379-474)
     and update_attribute_element_offset (:508-620): per geometry one map row
     pair (geometry, subdivision) per attribute its shaders request, closed by
@@ -2010,6 +2023,9 @@ def _pack_attributes(g: dict, objects: list, tri_shader_idx, svm_compiler, kobje
             for key in svm_compiler.requests[k]:
                 if key not in reqs:
                     reqs.append(key)
+        for key in global_reqs:
+            if key not in reqs:
+                reqs.append(key)
         geom_offset[gi] = len(rows)
         for key in reqs:
             aid = svm_compiler.attribute_ids[key] if isinstance(key, str) else int(key)

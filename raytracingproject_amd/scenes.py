@@ -1045,6 +1045,46 @@ def shadow_catcher(width=48, height=48, samples=8, transparent_film=False) -> sc
     return s
 
 
+def data_passes(width=40, height=40, samples=8) -> sc.Scene:
+    """Data passes (golden parity case; kernel_passes.h:173-225
+    kernel_write_data_passes): depth, normal, UV, object and material index
+    written at each camera path's first hit that is opaque enough (a
+    half-transparent pane in front is passed through below the alpha
+    threshold), next to the combined pass.  Objects and materials carry pass
+    indices; the floor and the sphere have UV maps, the box has none (its UV
+    pass reads 0); a glossy-diffuse mix gives the normal pass a weighted
+    average."""
+    import dataclasses
+
+    rng = np.random.default_rng(3)
+    white = dataclasses.replace(sc.diffuse((0.7, 0.7, 0.7)), pass_index=3)
+    red = dataclasses.replace(sc.diffuse((0.8, 0.25, 0.2)), pass_index=7)
+    mixed = dataclasses.replace(sc.mix(0.4, sc.glossy((0.8, 0.8, 0.9), 0.3), sc.diffuse((0.2, 0.4, 0.8))),
+                                pass_index=11)
+    pane = dataclasses.replace(sc.mix(0.7, sc.transparent((0.9, 0.9, 0.9)), sc.diffuse((0.2, 0.6, 0.3))),
+                               pass_index=5)
+    light = sc.emission((1.0, 0.9, 0.8), 6.0)
+    materials = [white, red, mixed, pane, light]
+    floor = sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0, pass_index=1)
+    floor.uv = rng.uniform(0.0, 1.0, (len(floor.tris), 3, 2)).astype(np.float32)
+    ball = sc.Mesh(*_ellipsoid((-0.8, -0.45, 0.2), (0.5, 0.5, 0.5), 20, 12), shader=1, smooth=True, pass_index=2)
+    ball.uv = rng.uniform(0.0, 1.0, (len(ball.tris), 3, 2)).astype(np.float32)
+    meshes = [
+        floor, ball,
+        sc.Mesh(*_box((0.8, -0.55, -0.1), (0.6, 0.9, 0.6), 0.4), shader=2, pass_index=4),
+        sc.Mesh(*_quad((-0.4, -0.2, -1.2), (0.6, -0.2, -1.2), (0.6, 0.7, -1.2), (-0.4, 0.7, -1.2)), shader=3,
+                pass_index=6),
+        sc.Mesh(*_quad((-1.6, 2.2, -1.2), (-0.8, 2.2, -1.2), (-0.8, 2.2, -0.4), (-1.6, 2.2, -0.4)), shader=4),
+    ]
+    lamps = [sc.Lamp("point", co=(1.5, 2.0, -1.5), size=0.2, color=(1.0, 0.9, 0.8), strength=60.0)]
+    cam = sc.Camera(eye=(0.0, 0.8, -3.6), target=(0.0, -0.3, 0.0), fov=math.radians(45.0), nearclip=0.01,
+                    farclip=100.0)
+    s = sc.Scene(width, height, cam, meshes, materials, world_color=(0.3, 0.35, 0.45), world_strength=1.0,
+                 samples=samples, lamps=lamps, name="data_passes")
+    s.passes = ["depth", "normal", "uv", "object_id", "material_id"]
+    return s
+
+
 def shading_info(width=48, height=48, samples=8) -> sc.Scene:
     """Particle Info and texture mapping: boxes instanced with a particle each
     (index, age, lifetime, size, location, velocity, angular velocity driving

@@ -110,6 +110,9 @@ CASES = {
     # transparent film; all-lights connection behind the catcher
     "shadow_catcher": lambda: scenes.shadow_catcher(40, 40, 8),
     "shadow_catcher_film": lambda: scenes.shadow_catcher(40, 40, 8, transparent_film=True),
+    # data passes (kernel_write_data_passes): depth, normal, UV, object and
+    # material index at the camera path's first opaque-enough hit
+    "data_passes": lambda: scenes.data_passes(40, 40, 8),
     # Particle Info on instanced objects, TextureMapping with min/max and normalize
     "shading_info": lambda: scenes.shading_info(48, 48, 8),
     # Hair Info: strand flag, thickness, tangent normal, intercept / random curve attributes
@@ -175,7 +178,8 @@ def sky_model(kind):
 
 def atomic_pass_channels(ds) -> np.ndarray:
     """Render-buffer channels the GPU adds with float atomics: the AOV passes
-    (svm_aov.h -> kernel_write_pass_float*, an atomic add on the reference's
+    and the normal / UV data passes (kernel_write_pass_float*, an atomic add
+    on the reference's
     GPU devices too, kernel_write_passes.h:21-65).  Their per-pixel sum order
     follows the GPU's scheduling, so they match the reference's sequential
     sums to rounding (tolerance below); every other channel is bit-exact."""
@@ -183,6 +187,12 @@ def atomic_pass_channels(ds) -> np.ndarray:
     mask = np.zeros(ds.pass_stride, dtype=bool)
     mask[f.pass_aov_color:f.pass_aov_color + 4 * f.pass_aov_color_num] = f.pass_aov_color_num > 0
     mask[f.pass_aov_value:f.pass_aov_value + f.pass_aov_value_num] = f.pass_aov_value_num > 0
+    # the data passes summed over samples (normal, UV: kernel_passes.h:208-214);
+    # depth and the indices are written once, at sample 0, so they stay exact
+    if f.pass_flag & (1 << 3):
+        mask[f.pass_normal:f.pass_normal + 3] = True
+    if f.pass_flag & (1 << 4):
+        mask[f.pass_uv:f.pass_uv + 3] = True
     return mask
 
 
