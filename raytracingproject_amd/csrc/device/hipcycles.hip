@@ -1533,6 +1533,8 @@ struct hipcy_device {
   bool use_disk_bssrdf = false;       /* disk BSSRDFs: the slots' subsurface indirect-ray records */
   bool sss_pool_vol = false;          /* ... sized with their volume stacks */
   bool use_catcher = false;           /* shadow-catcher objects: the slots' catcher records */
+  bool use_branched = false;          /* branched path tracing: the slots' branch records */
+  char *br_pool = nullptr;            /* those records and their counters */
   char *catcher_pool = nullptr;       /* those records (CY_CATCHER_F4 float4 per slot) */
   char *sss_pool = nullptr;           /* those records and their depths */
   bool use_ray_diff = false;          /* a shader reads ray differentials (Bump / *_BUMP_DX / _DY nodes) */
@@ -1754,6 +1756,12 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
     dev->catcher_pool = nullptr;
   }
   dev->bufs.catcher = nullptr;
+  if (dev->br_pool) {
+    hipFree(dev->br_pool);
+    dev->br_pool = nullptr;
+  }
+  dev->bufs.br_rec = nullptr;
+  dev->bufs.br_count = nullptr;
   dev->bufs.sss_rec = nullptr;
   dev->bufs.sss_vol = nullptr;
   dev->bufs.sss_count = nullptr;
@@ -1803,6 +1811,21 @@ static int ensure_catcher_capacity(hipcy_device *dev)
     HIP_CHECK(dev, hipMalloc((void **)&dev->catcher_pool, (size_t)16 * CY_CATCHER_F4 * dev->capacity));
   }
   dev->bufs.catcher = dev->use_catcher ? (hc_float4 *)dev->catcher_pool : nullptr;
+  return 0;
+}
+
+/* The slots' branch records (cy_integrator.h CY_BR_RECS x CY_BR_REC_F4 float4
+ * and two counters per slot, 2.6 KB), for branched path tracing only. */
+static int ensure_branch_capacity(hipcy_device *dev)
+{
+  const size_t recs = (size_t)16 * CY_BR_RECS * CY_BR_REC_F4 * dev->capacity;
+  const size_t counts = (size_t)8 * dev->capacity;
+  if (dev->use_branched && !dev->br_pool) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->br_pool, recs + counts));
+    HIP_CHECK(dev, hipMemset(dev->br_pool + recs, 0, counts));
+  }
+  dev->bufs.br_rec = dev->use_branched ? (hc_float4 *)dev->br_pool : nullptr;
+  dev->bufs.br_count = dev->use_branched ? (uint *)(dev->br_pool + recs) : nullptr;
   return 0;
 }
 
@@ -1960,6 +1983,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->vol_pool) hipFree(dev->vol_pool);
   if (dev->sss_pool) hipFree(dev->sss_pool);
   if (dev->catcher_pool) hipFree(dev->catcher_pool);
+  if (dev->br_pool) hipFree(dev->br_pool);
   if (dev->diff_pool) hipFree(dev->diff_pool);
   if (dev->srec_pool) hipFree(dev->srec_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
@@ -2855,6 +2879,32 @@ int hipcy_load_kernels(hipcy_device *dev)
     }
     dev->shade_tex = true;
   }
+  /* kernel_branched_path_integrate (kernel_path_branched.h): the extended
+   * shading kernels, each camera hit's indirect samples (and the camera ray
+   * through transparency) waiting in CY_BR_RECS records per slot; not with
+   * volumes, BSSRDFs or shadow catchers */
+  dev->use_branched = d.integrator.branched != 0;
+  if (dev->use_branched) {
+    const int samples = std::max(d.integrator.diffuse_samples,
+                                 std::max(d.integrator.glossy_samples, d.integrator.transmission_samples));
+    if (d.integrator.use_volumes) {
+      return set_error(dev, "load_kernels: unsupported scene feature: branched path tracing with volumes");
+    }
+    if (uses_bssrdf) {
+      return set_error(dev, "load_kernels: unsupported scene feature: branched path tracing with subsurface "
+                            "scattering");
+    }
+    if (dev->use_catcher) {
+      return set_error(dev, "load_kernels: unsupported scene feature: branched path tracing with shadow catchers");
+    }
+    if ((size_t)d.integrator.max_closures * (size_t)std::max(samples, 1) + 1 > (size_t)CY_BR_RECS + 1) {
+      return set_error(dev, "load_kernels: branched path tracing with up to " +
+                                std::to_string(d.integrator.max_closures) + " closures x " + std::to_string(samples) +
+                                " samples: more waiting paths than the device's " + std::to_string(CY_BR_RECS) +
+                                " per slot");
+    }
+    dev->shade_tex = true;
+  }
   dev->use_volumes = d.integrator.use_volumes != 0;
   dev->use_disk_bssrdf = uses_disk_bssrdf;
   dev->use_ray_diff = uses_ray_diff;
@@ -3486,7 +3536,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
   }
   const size_t items = npix * per_pass;
   if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 || ensure_catcher_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 || ensure_catcher_capacity(dev) != 0 || ensure_branch_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
       ensure_srec_capacity(dev) != 0 ||
       ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
@@ -3940,7 +3990,7 @@ static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
 static int stream_pool(hipcy_device *dev, size_t slots)
 {
   if (ensure_capacity(dev, slots) != 0 || ensure_volume_capacity(dev) != 0 || ensure_sss_capacity(dev) != 0 ||
-      ensure_catcher_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
+      ensure_catcher_capacity(dev) != 0 || ensure_branch_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
     return -1;
   }
   return 0;

@@ -78,6 +78,12 @@ typedef struct CyPathBuffers {
   /* scenes with shadow catcher objects: the path's shadow-catcher record of
    * PathRadiance (kernel_types.h:540-556), CY_CATCHER_F4 float4 per slot */
   hc_float4 *catcher;
+  /* branched path tracing (KernelIntegrator.branched): the paths a camera hit
+   * spawned that wait for the slot, CY_BR_RECS records of CY_BR_REC_F4 float4
+   * per slot, and per slot the next record to start and the end (first in,
+   * first out; cy_branched.h) */
+  hc_float4 *br_rec;
+  uint *br_count;
 } CyPathBuffers;
 
 /* The shadow-catcher part of PathRadiance (kernel_accumulate.h:203-233,
@@ -100,6 +106,8 @@ typedef struct CyCatcher {
 #define CY_SREC_NONE 0x200u
 
 #define CY_SSS_RECS (BSSRDF_MAX_HITS - 1)
+#define CY_BR_RECS 16
+#define CY_BR_REC_F4 10 /* a path record (CY_SSS_REC_F4) and its branch factor */
 #define CY_SSS_REC_F4 9 /* state (3), ray (2), throughput, ray differentials (3) */
 #define CY_RAY_DIFF_F4 3
 
@@ -294,10 +302,9 @@ CY_FN void diff_load(const hc_float4 *src, CyDiff3 *dP, CyDiff3 *dD)
 
 /* A subsurface indirect ray of the slot (state, ray, throughput; with ray
  * differentials their dP, dD). */
-CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathState *s, const CyRay *ray,
-                         cfloat3 throughput, const CyDiff3 *dP = nullptr, const CyDiff3 *dD = nullptr)
+CY_FN void path_rec_store(hc_float4 *dst, const CyPathState *s, const CyRay *ray, cfloat3 throughput,
+                          const CyDiff3 *dP, const CyDiff3 *dD)
 {
-  hc_float4 *dst = b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4;
   cy_st(&dst[0], mkf4(int_as_float(s->flag), as_float(s->rng_hash), int_as_float(s->rng_offset),
                       int_as_float(s->sample)));
   cy_st(&dst[1], mkf4(int_as_float(s->bounce), int_as_float(s->diffuse_bounce), int_as_float(s->glossy_bounce),
@@ -311,10 +318,15 @@ CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathSt
   }
 }
 
-CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals *kg, CyPathState *s, CyRay *ray,
-                        cfloat3 *throughput, CyDiff3 *dP = nullptr, CyDiff3 *dD = nullptr)
+CY_FN void sss_rec_store(const CyPathBuffers *b, int slot, int r, const CyPathState *s, const CyRay *ray,
+                         cfloat3 throughput, const CyDiff3 *dP = nullptr, const CyDiff3 *dD = nullptr)
 {
-  const hc_float4 *src = b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4;
+  path_rec_store(b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4, s, ray, throughput, dP, dD);
+}
+
+CY_FN void path_rec_load(const hc_float4 *src, const CyGlobals *kg, CyPathState *s, CyRay *ray, cfloat3 *throughput,
+                         CyDiff3 *dP, CyDiff3 *dD)
+{
   const hc_float4 r0 = cy_ld(&src[0]);
   const hc_float4 r1 = cy_ld(&src[1]);
   const hc_float4 r2 = cy_ld(&src[2]);
@@ -343,6 +355,19 @@ CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals
   if (dP) {
     diff_load(&src[6], dP, dD);
   }
+}
+
+CY_FN void sss_rec_load(const CyPathBuffers *b, int slot, int r, const CyGlobals *kg, CyPathState *s, CyRay *ray,
+                        cfloat3 *throughput, CyDiff3 *dP = nullptr, CyDiff3 *dD = nullptr)
+{
+  path_rec_load(b->sss_rec + ((size_t)slot * CY_SSS_RECS + (size_t)r) * CY_SSS_REC_F4, kg, s, ray, throughput, dP,
+                dD);
+}
+
+/* branch record r of the slot (the branch factor in its last float4) */
+CY_FN hc_float4 *br_rec_at(const CyPathBuffers *b, int slot, int r)
+{
+  return b->br_rec + ((size_t)slot * CY_BR_RECS + (size_t)r) * CY_BR_REC_F4;
 }
 
 /* The slot's volume stack and pending update records (CyPathBuffers.vol_*);
@@ -526,7 +551,8 @@ CY_FN uint path_state_ray_visibility(const CyPathState *s)
 /* kernel_path_state.h:208-244 */
 CY_FN float path_state_continuation_probability(const CyGlobals *kg,
                                                 const CyPathState *s,
-                                                cfloat3 throughput)
+                                                cfloat3 throughput,
+                                                float branch_factor = 1.0f)
 {
   if (s->flag & PATH_RAY_TERMINATE_IMMEDIATE) {
     return 0.0f;
@@ -548,7 +574,7 @@ CY_FN float path_state_continuation_probability(const CyGlobals *kg,
     }
   }
   /* branch_factor is 1.0 outside branched path tracing */
-  return cmin(sqrtf(max3f(fabs3(throughput)) * 1.0f), 1.0f);
+  return cmin(sqrtf(max3f(fabs3(throughput)) * branch_factor), 1.0f);
 }
 
 CY_FN bool path_state_ao_bounce(const CyGlobals *kg, const CyPathState *s)
@@ -836,7 +862,11 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
   cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
   cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(path_state_ray_visibility(&s))));
   cy_st(&b->throughput[slot], mkf4(1.0f, 1.0f, 1.0f, 0.0f));
-  cy_st(&b->L[slot], mkf4(0.0f, 0.0f, 0.0f, 0.0f));
+  cy_st(&b->L[slot], mkf4(0.0f, 0.0f, 0.0f, 1.0f)); /* w: the branch factor */
+  if (b->br_rec) {
+    cy_st(&b->br_count[2 * (size_t)slot], 0u); /* no waiting branched paths */
+    cy_st(&b->br_count[2 * (size_t)slot + 1], 0u);
+  }
   if (b->catcher) {
     CyCatcher c;
     catcher_init(kg, &c);
@@ -1591,6 +1621,14 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
       }
       else
 #endif
+#if CY_CLOSURE_EXT && CY_SVM_TEX
+      if (KD->integrator.branched) {
+        /* shader_bsdf_eval of branched path tracing (kernel_shader.h:626-628) */
+        cfloat3 no_mis;
+        shader_bsdf_eval_branched(sd, ls.D, ls.pdf, ((uint)ls.shader & SHADER_USE_MIS) != 0, &eval, &no_mis);
+      }
+      else
+#endif
       {
         /* shader_bsdf_eval (kernel_shader.h:606-636) */
         shader_bsdf_multi_eval(sd, ls.D, &bpdf, -1, &eval, 0.0f, 0.0f);
@@ -1726,175 +1764,7 @@ CY_FN void connect_light(const CyGlobals *kg, const CyPathBuffers *b, int slot, 
   }
 }
 
-#if CY_CLOSURE_EXT && CY_SVM_TEX
-/* direct_emission (kernel_emission.h:101-205) at a surface point on a path
- * behind a shadow catcher: the BSDF-weighted light (*eval, the MIS weight
- * applied) and the same without the MIS weight (*eval_no_mis,
- * BsdfEval.sum_no_mis, kernel_accumulate.h:62-70), no light termination
- * (kernel_emission.h:162-165); *light_ray the shadow ray (t = 0: the light
- * casts no shadow).  False: no contribution. */
-CY_FN bool catcher_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightSample *ls, const CyPathState *state,
-                                   cfloat3 *eval, cfloat3 *eval_no_mis, CyRay *light_ray, CyShadeMem mem, uint *err)
-{
-  if (ls->pdf == 0.0f) {
-    return false;
-  }
-  cfloat3 light_eval = mk3(0.0f, 0.0f, 0.0f);
-  const cfloat3 I = neg3(ls->D);
-  if (shader_constant_emission_eval(kg, ls->shader, &light_eval)) {
-    if ((ls->prim != PRIM_NONE) && dot3(ls->Ng, I) < 0.0f) {
-      ls->Ng = neg3(ls->Ng);
-    }
-  }
-  else if (ls->type == LIGHT_BACKGROUND) {
-    light_eval = background_eval_svm(kg->data, kg->__svm_nodes, kg->__shaders, kg->__objects, kg->__texture_info,
-                                     ls->D, mem, *state, PATH_RAY_EMISSION, err);
-  }
-  else {
-    light_eval = emissive_eval_svm(kg, ls->P, ls->Ng, I, ls->shader, ls->object, ls->prim, ls->lamp, ls->u, ls->v,
-                                   ls->t, mem, *state, err);
-    if ((ls->prim != PRIM_NONE) && dot3(ls->Ng, I) < 0.0f) {
-      ls->Ng = neg3(ls->Ng);
-    }
-  }
-  light_eval = mul3f(light_eval, ls->eval_fac);
-  if (ls->lamp != LAMP_NONE) {
-    light_eval = mul3(light_eval, klight_vec(kg->__lights[ls->lamp].strength));
-  }
-  if (is_zero3(light_eval)) {
-    return false;
-  }
-  float bpdf;
-  cfloat3 e = mk3(0.0f, 0.0f, 0.0f); /* shader_bsdf_multi_eval accumulates */
-  shader_bsdf_multi_eval(sd, ls->D, &bpdf, -1, &e, 0.0f, 0.0f);
-  cfloat3 no_mis = e;
-  if ((uint)ls->shader & SHADER_USE_MIS) {
-    e = mul3f(e, power_heuristic(ls->pdf, bpdf));
-  }
-  const cfloat3 scale = div3f(light_eval, ls->pdf);
-  e = mul3(e, scale);
-  no_mis = mul3(no_mis, scale);
-  if (((uint)ls->shader & SHADER_EXCLUDE_ANY) && ((uint)ls->shader & SHADER_EXCLUDE_DIFFUSE)) {
-    e = mk3(0.0f, 0.0f, 0.0f);
-  }
-  if (is_zero3(e)) {
-    return false;
-  }
-  if ((uint)ls->shader & SHADER_CAST_SHADOW) {
-    const bool transmit = (dot3(sd->Ng, ls->D) < 0.0f);
-    light_ray->P = ray_offset(sd->P, transmit ? neg3(sd->Ng) : sd->Ng);
-    if (ls->t == CY_FLT_MAX) {
-      light_ray->D = ls->D;
-      light_ray->t = ls->t;
-    }
-    else {
-      light_ray->D = normalize_len3(sub3(ray_offset(ls->P, ls->Ng), light_ray->P), &light_ray->t);
-    }
-  }
-  else {
-    light_ray->t = 0.0f;
-  }
-  *eval = e;
-  *eval_no_mis = no_mis;
-  return true;
-}
-
-/* kernel_branched_path_surface_connect_light (kernel_path_surface.h:22-140)
- * with sample_all_lights, which kernel_path_surface_connect_light runs for a
- * path behind a shadow catcher (kernel_path_surface.h:224-226): every lamp's
- * samples and the mesh lights', each shadow ray traced here with the
- * non-catcher shadow visibility (kernel_shadow.h:402-404), each sample's light
- * added to the catcher's totals (path_radiance_accum_light /
- * _accum_total_light with PATH_RAY_STORE_SHADOW_INFO, kernel_accumulate.h:
- * 402-476; a catcher path adds nothing to the radiance itself).  The occluders'
- * shaders are evaluated into shadow_mem, so sd's closures stay intact. */
-CY_NOINLINE void catcher_connect_all_lights(const CyGlobals *kg, const CySD *sd, const CyPathState *state,
-                                            cfloat3 throughput, CyCatcher *catcher, CyShadeMem mem, uint *err)
-{
-  if (!KD->integrator.use_direct_light) {
-    return;
-  }
-  CyClosure shadow_closures[CY_MAX_CLOSURE];
-  CyShadeMem shadow_mem = mem;
-  shadow_mem.closure = shadow_closures;
-  int num_lights = KD->integrator.num_all_lights;
-  if (KD->integrator.pdf_triangles != 0.0f) {
-    num_lights += 1;
-  }
-  for (int i = 0; i < num_lights; ++i) {
-    int num_samples = 1;
-    int num_all_lights = 1;
-    uint lamp_rng_hash = state->rng_hash;
-    bool double_pdf = false;
-    bool is_mesh_light = false;
-    const bool is_lamp = i < KD->integrator.num_all_lights;
-    if (is_lamp) {
-      if ((float)state->bounce > kg->__lights[i].max_bounces) {
-        continue;
-      }
-      num_samples = kg->__lights[i].samples;
-      num_all_lights = KD->integrator.num_all_lights;
-      lamp_rng_hash = cmj_hash(state->rng_hash, (uint)i);
-      double_pdf = KD->integrator.pdf_triangles != 0.0f;
-    }
-    else {
-      num_samples = KD->integrator.mesh_light_samples;
-      double_pdf = KD->integrator.num_all_lights != 0;
-      is_mesh_light = true;
-    }
-    const float num_samples_inv = 1.0f / (float)(num_samples * num_all_lights);
-    for (int j = 0; j < num_samples; j++) {
-      CyRay light_ray;
-      light_ray.t = 0.0f;
-      bool has_emission = false;
-      cfloat3 eval = mk3(0.0f, 0.0f, 0.0f), eval_no_mis = mk3(0.0f, 0.0f, 0.0f);
-      if (sd->flag & SD_BSDF_HAS_EVAL) {
-        float light_u, light_v;
-        path_branched_rng_2D(kg, lamp_rng_hash, state, j, num_samples, PRNG_LIGHT_U, &light_u, &light_v);
-        if (is_mesh_light && double_pdf) {
-          light_u = 0.5f * light_u;
-        }
-        CyLightSample ls;
-        if (light_sample_lamp(kg, is_lamp ? i : -1, light_u, light_v, sd->P, state->bounce, &ls, err)) {
-          if (double_pdf) {
-            ls.pdf *= 2.0f;
-          }
-          has_emission = catcher_direct_emission(kg, sd, &ls, state, &eval, &eval_no_mis, &light_ray, mem, err);
-        }
-      }
-      /* shadow_blocked (kernel_shadow.h:386-460) */
-      cfloat3 shadow = mk3(1.0f, 1.0f, 1.0f);
-      bool blocked = false;
-      if (light_ray.t != 0.0f) {
-        if (KD->integrator.transparent_shadows) {
-          blocked = shadow_blocked_transparent<false>(kg, light_ray, state, shadow_mem, &shadow, err, nullptr,
-                                                      kg->use_ray_diff ? &sd->dP : nullptr, CY_SREC_NONE, nullptr,
-                                                      PATH_RAY_SHADOW_NON_CATCHER);
-        }
-        else if (scene_intersect_valid(&light_ray)) {
-          CyIsect si;
-          blocked = kg->have_curves ?
-                        bvh2_intersect<true, true, 2, CY_LDS_STACK, CY_BLOCK, 3>(
-                            kg, &light_ray, PATH_RAY_SHADOW_OPAQUE_NON_CATCHER, &si, err, nullptr, nullptr, nullptr) :
-                        bvh2_intersect<true>(kg, &light_ray, PATH_RAY_SHADOW_OPAQUE_NON_CATCHER, &si, err, nullptr,
-                                             nullptr, nullptr);
-        }
-      }
-      CY_DBGF(state, "catcher light %d sample %d emission %d blocked %d\n", i, j, (int)has_emission, (int)blocked);
-      CY_DBG3(state, "catcher eval_no_mis", eval_no_mis);
-      CY_DBG3(state, "catcher light_ray.D", light_ray.D);
-      CY_DBG1(state, "catcher light_ray.t", light_ray.t);
-      if (has_emission) {
-        const cfloat3 light = mul3(mul3f(throughput, num_samples_inv), eval_no_mis);
-        catcher->path_total = add3(catcher->path_total, light);
-        if (!blocked) {
-          catcher->path_total_shaded = add3(catcher->path_total_shaded, mul3(shadow, light));
-        }
-      }
-    }
-  }
-}
-#endif
+#include "cy_branched.h"
 
 #if CY_CLOSURE_EXT && CY_SVM_TEX
 
@@ -2422,6 +2292,125 @@ CY_FN void write_data_passes(const CyGlobals *kg, float *buffer, const CySD *sd,
 }
 #endif
 
+#if CY_CLOSURE_EXT && CY_SVM_TEX
+/* kernel_branched_path_integrate's work at a camera hit (kernel_path_branched.h:
+ * 470-500) after the shader is applied: the direct light of all lights (or one),
+ * then per BSDF closure its diffuse / glossy / transmission samples' indirect
+ * paths (kernel_branched_path_surface_indirect_light, :201-280), and the camera
+ * ray carried on through the surface's transparency.  The first of these paths
+ * replaces the slot's (true returned, *state .. *branch_factor set), the others
+ * wait in the slot's branch records in the reference's order. */
+CY_FN bool branched_camera_hit(const CyGlobals *kg, const CyPathBuffers *b, int slot, const CySD *sd,
+                               CyPathState *state, cfloat3 *throughput, CyRay *ray, cfloat3 *L, float *branch_factor,
+                               CyCatcher *catcher, CyShadeMem mem, uint *err)
+{
+  const bool all = KD->integrator.sample_all_lights_direct || (state->flag & PATH_RAY_SHADOW_CATCHER);
+  connect_light_branched(kg, sd, state, *throughput, 1.0f, all, L, catcher, mem, err);
+  const bool diff = kg->use_ray_diff != 0;
+  bool have_first = false;
+  CyPathState first_state;
+  CyRay first_ray;
+  cfloat3 first_tp = mk3(0.0f, 0.0f, 0.0f);
+  float first_bf = 1.0f;
+  CyDiff3 first_dP, first_dD, dD;
+  int n = 0;
+  for (int i = 0; i < sd->num_closure; i++) {
+    const CyClosure *sc = &sd->closure[i];
+    /* transparency is not handled here, but in the camera loop */
+    if (!CLOSURE_IS_BSDF(sc->type) || sc->type == CLOSURE_BSDF_TRANSPARENT_ID) {
+      continue;
+    }
+    int num_samples;
+    if (CLOSURE_IS_BSDF_DIFFUSE(sc->type)) {
+      num_samples = KD->integrator.diffuse_samples;
+    }
+    else if (sc->type == CLOSURE_BSDF_BSSRDF_ID || sc->type == CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID) {
+      num_samples = 1;
+    }
+    else if ((sc->type >= CLOSURE_BSDF_REFLECTION_ID && sc->type <= CLOSURE_BSDF_HAIR_REFLECTION_ID) ||
+             sc->type == CLOSURE_BSDF_HAIR_PRINCIPLED_ID) {
+      num_samples = KD->integrator.glossy_samples;
+    }
+    else {
+      num_samples = KD->integrator.transmission_samples;
+    }
+    const float num_samples_inv = 1.0f / (float)num_samples;
+    for (int j = 0; j < num_samples; j++) {
+      CyPathState ps = *state;
+      cfloat3 tp = *throughput;
+      CyRay bray;
+      float bf = *branch_factor;
+      ps.rng_hash = cmj_hash(state->rng_hash, (uint)i);
+      if (!branched_surface_bounce(kg, sd, sc, j, num_samples, &tp, &ps, &bray, &bf, diff ? &dD : nullptr, err)) {
+        continue;
+      }
+      ps.rng_hash = state->rng_hash;
+      tp = mul3f(tp, num_samples_inv);
+      if (!have_first) {
+        have_first = true;
+        first_state = ps;
+        first_ray = bray;
+        first_tp = tp;
+        first_bf = bf;
+        first_dP = sd->dP;
+        first_dD = dD;
+      }
+      else if (n >= CY_BR_RECS) {
+        cy_set_error(err, CY_ERR_FEATURE, 15); /* more branched samples than the slot's records */
+      }
+      else {
+        hc_float4 *rec = br_rec_at(b, slot, n++);
+        path_rec_store(rec, &ps, &bray, tp, diff ? &sd->dP : nullptr, &dD);
+        cy_st(&rec[CY_BR_REC_F4 - 1], mkf4(bf, 0.0f, 0.0f, 0.0f));
+      }
+    }
+  }
+  /* continue in case of transparency (kernel_path_branched.h:487-516) */
+  const cfloat3 tpc = mul3(*throughput, shader_bsdf_transparency(sd));
+  if (!is_zero3(tpc)) {
+    CyPathState cs = *state;
+    path_state_next(kg, &cs, LABEL_TRANSPARENT);
+    CyRay cr;
+    cr.P = ray_offset(sd->P, neg3(sd->Ng));
+    cr.D = ray->D;
+    cr.t = ray->t - sd->ray_length;
+    CyDiff3 cdD;
+    cdD.dx = neg3(sd->dI.dx);
+    cdD.dy = neg3(sd->dI.dy);
+    if (!have_first) {
+      have_first = true;
+      first_state = cs;
+      first_ray = cr;
+      first_tp = tpc;
+      first_bf = *branch_factor;
+      first_dP = sd->dP;
+      first_dD = cdD;
+    }
+    else if (n >= CY_BR_RECS) {
+      cy_set_error(err, CY_ERR_FEATURE, 15);
+    }
+    else {
+      hc_float4 *rec = br_rec_at(b, slot, n++);
+      path_rec_store(rec, &cs, &cr, tpc, diff ? &sd->dP : nullptr, &cdD);
+      cy_st(&rec[CY_BR_REC_F4 - 1], mkf4(*branch_factor, 0.0f, 0.0f, 0.0f));
+    }
+  }
+  cy_st(&b->br_count[2 * (size_t)slot], 0u);
+  cy_st(&b->br_count[2 * (size_t)slot + 1], (uint)n);
+  if (!have_first) {
+    return false;
+  }
+  *state = first_state;
+  *ray = first_ray;
+  *throughput = first_tp;
+  *branch_factor = first_bf;
+  if (diff) {
+    diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, first_dP, first_dD);
+  }
+  return true;
+}
+#endif
+
 /* indirect_background (kernel_emission.h:288-345): the world seen along the
  * ray (its light-path exclusions, the world shader evaluated with the bounce
  * raised, the background MIS weight). */
@@ -2492,6 +2481,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
   CyRay ray;
   cfloat3 throughput, L;
   float L_transparent;
+  float branch_factor = 1.0f; /* PathState.branch_factor (path_state_branch) */
   uint rng_hash = 0, ray_visibility = 0;
   int sample = 0;
   if (cam_item != CY_NO_ITEM) {
@@ -2557,6 +2547,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
     L_transparent = tp4.w;
     const hc_float4 L4 = cy_ld(&b->L[slot]);
     L = mk3(L4.x, L4.y, L4.z);
+#if CY_CATCHER
+    if (KD->integrator.branched) {
+      branch_factor = L4.w; /* an indirect path of branched path tracing */
+    }
+#endif
   }
 #if CY_CATCHER
   CyCatcher catcher;
@@ -2857,7 +2852,20 @@ CY_FN bool shade_path(const CyGlobals *kg,
       shader_eval_surface(kg, &sd, &state, state.flag, err, aov_buffer);
     }
 #endif
-    shader_prepare_closures(&sd, &state);
+#if CY_CATCHER
+    /* kernel_branched_path_integrate: the camera segment of branched path
+     * tracing merges identical closures instead (kernel_path_branched.h:440) */
+    const bool branched_cam = KD->integrator.branched && (state.flag & PATH_RAY_CAMERA);
+    if (branched_cam) {
+      shader_merge_closures(&sd);
+    }
+    else
+#else
+    const bool branched_cam = false;
+#endif
+    {
+      shader_prepare_closures(&sd, &state);
+    }
 #ifdef CY_DBG_X
     CY_DBGF(&state, "closures %d flag %08x\n", sd.num_closure, sd.flag);
     CY_DBG3(&state, "sd.N'", sd.N);
@@ -2984,8 +2992,12 @@ CY_FN bool shade_path(const CyGlobals *kg,
       }
     }
 
-    /* Russian roulette (kernel_path.h:587-599) */
-    float probability = path_state_continuation_probability(kg, &state, throughput);
+    /* Russian roulette (kernel_path.h:587-599; on the camera segment of
+     * branched path tracing only behind transparency, kernel_path_branched.h:
+     * 449-466) */
+    const float probability = (branched_cam && !(state.flag & PATH_RAY_TRANSPARENT)) ?
+                                  1.0f :
+                                  path_state_continuation_probability(kg, &state, throughput, branch_factor);
     if (probability == 0.0f) {
       terminated = true;
     }
@@ -3069,6 +3081,13 @@ CY_FN bool shade_path(const CyGlobals *kg,
       }
 #endif
     }
+#if CY_CATCHER
+    if (!terminated && branched_cam) {
+      cont = branched_camera_hit(kg, b, slot, &sd, &state, &throughput, &ray, &L, &branch_factor, &catcher, mem,
+                                 err);
+      terminated = true;
+    }
+#endif
     if (!terminated) {
       /* Direct light: kernel_branched_path_surface_connect_light with one sample
        * (kernel_path_surface.h:23-140), light_sample + direct_emission
@@ -3090,8 +3109,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
         else
 #endif
 #if CY_CATCHER
-        if (state.flag & PATH_RAY_SHADOW_CATCHER) {
-          catcher_connect_all_lights(kg, &sd, &state, throughput, &catcher, mem, err);
+        if ((state.flag & PATH_RAY_SHADOW_CATCHER) ||
+            (KD->integrator.branched && KD->integrator.sample_all_lights_indirect)) {
+          /* kernel_path_indirect (kernel_path.h:470-476) / a path behind a
+           * shadow catcher: all lights */
+          connect_light_branched(kg, &sd, &state, throughput, 1.0f, true, &L, &catcher, mem, err);
         }
         else
 #endif
@@ -3214,6 +3236,27 @@ CY_FN bool shade_path(const CyGlobals *kg,
       cont = true;
     }
   }
+#if CY_CATCHER
+  if (!cont && b->br_rec && cam_item == CY_NO_ITEM) {
+    /* the path ended: the next path its camera hit spawned, if any */
+    const uint next = cy_ld(&b->br_count[2 * (size_t)slot]);
+    const uint end = cy_ld(&b->br_count[2 * (size_t)slot + 1]);
+    if (next < end) {
+      const hc_float4 *rec = br_rec_at(b, slot, (int)next);
+      if (kg->use_ray_diff) {
+        CyDiff3 pdP, pdD;
+        path_rec_load(rec, kg, &state, &ray, &throughput, &pdP, &pdD);
+        diff_store(b->ray_diff + (size_t)slot * CY_RAY_DIFF_F4, pdP, pdD);
+      }
+      else {
+        path_rec_load(rec, kg, &state, &ray, &throughput, nullptr, nullptr);
+      }
+      branch_factor = cy_ld(&rec[CY_BR_REC_F4 - 1]).x;
+      cy_st(&b->br_count[2 * (size_t)slot], next + 1);
+      cont = true;
+    }
+  }
+#endif
   if (VOL && (cont || *shadow)) {
     vol_stack_store(b, slot, &vstack);
     vol_rec_store(b, slot, vop_object, vop_shader, vop_flags, &state, shadow_rng_offset);
@@ -3233,7 +3276,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     cy_st(&b->ray_P[slot], mkf4(ray.P.x, ray.P.y, ray.P.z, ray.t));
     cy_st(&b->ray_D[slot], mkf4(ray.D.x, ray.D.y, ray.D.z, as_float(path_state_ray_visibility(&state))));
     cy_st(&b->throughput[slot], mkf4(throughput.x, throughput.y, throughput.z, L_transparent));
-    cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, 0.0f));
+    cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, branch_factor));
     return true;
   }
   if (*shadow) {
@@ -3243,7 +3286,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
       cy_st(&b->item[slot], cam_item);
     }
     cy_st(&b->throughput[slot], mkf4(throughput.x, throughput.y, throughput.z, L_transparent));
-    cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, 0.0f));
+    cy_st(&b->L[slot], mkf4(L.x, L.y, L.z, branch_factor));
     hc_float4 sl = cy_ld(&b->shadow_L[slot]);
     sl.w = 1.0f;
     cy_st(&b->shadow_L[slot], sl);

@@ -3467,6 +3467,30 @@ CY_FN void shader_bsdf_multi_eval(const CySD *sd,
   *pdf = (sum_sample_weight > 0.0f) ? sum_pdf / sum_sample_weight : 0.0f;
 }
 
+/* _shader_bsdf_multi_eval_branched (kernel_shader.h:583-601), which
+ * shader_bsdf_eval runs whenever KernelIntegrator.branched is set: every BSDF
+ * closure MIS-weighted against the light on its own pdf; *eval_no_mis the
+ * unweighted sum (BsdfEval.sum_no_mis) */
+CY_FN void shader_bsdf_eval_branched(const CySD *sd, cfloat3 omega_in, float light_pdf, bool use_mis, cfloat3 *eval,
+                                     cfloat3 *eval_no_mis)
+{
+  *eval = mk3(0.0f, 0.0f, 0.0f);
+  *eval_no_mis = mk3(0.0f, 0.0f, 0.0f);
+  for (int i = 0; i < sd->num_closure; i++) {
+    const CyClosure *sc = &sd->closure[i];
+    if (CLOSURE_IS_BSDF(sc->type)) {
+      float bsdf_pdf = 0.0f;
+      const cfloat3 e = bsdf_eval(sd, sc, omega_in, &bsdf_pdf);
+      if (bsdf_pdf != 0.0f) {
+        const float mis_weight = use_mis ? power_heuristic(light_pdf, bsdf_pdf) : 1.0f;
+        const cfloat3 value = mul3(e, sc->weight);
+        *eval_no_mis = add3(*eval_no_mis, value);
+        *eval = add3(*eval, mul3f(value, mis_weight));
+      }
+    }
+  }
+}
+
 /* kernel_shader.h:638-680 */
 CY_FN int shader_bsdf_pick(const CySD *sd, float *randu)
 {

@@ -1075,6 +1075,17 @@ class Scene:
     # decoupled volume ray marching (the CPU device's KernelIntegrator, see
     # compile_scene); False: distance sampling as GPU devices integrate
     volume_decoupled: bool = False
+    # Integrator "Sampling" method (integrator.cpp:83, KernelIntegrator.branched):
+    # "path" or "branched_path", with the branched sample counts per closure
+    # kind and the all-lights switches (integrator.cpp:164-181; Blender's
+    # defaults)
+    integrator: str = "path"
+    diffuse_samples: int = 1
+    glossy_samples: int = 1
+    transmission_samples: int = 1
+    mesh_light_samples: int = 1
+    sample_all_lights_direct: bool = True
+    sample_all_lights_indirect: bool = True
     # AOV passes of the view layer (BlenderSync::sync_render_passes,
     # Pass::add(PASS_AOV_COLOR / PASS_AOV_VALUE, name)): (name, "color" | "value")
     aovs: list = field(default_factory=list)
@@ -1640,17 +1651,27 @@ def compile_scene(scene: Scene) -> DeviceScene:
     ki.use_ambient_occlusion = 0
     ki.sample_clamp_direct = FLT_MAX
     ki.sample_clamp_indirect = FLT_MAX
-    ki.branched = 0
+    branched = scene.integrator == "branched_path"
+    ki.branched = int(branched)
     # DeviceInfo::has_volume_decoupled (integrator.cpp:165): the CPU device's
     # decoupled ray marching, with the Integrator's "sample all lights"
     # defaults (true) that choose it for every volume segment
     # (kernel_volume_use_decoupled); GPU devices upload 0
     ki.volume_decoupled = int(scene.volume_decoupled)
-    ki.diffuse_samples = ki.glossy_samples = ki.transmission_samples = 1
-    ki.ao_samples = ki.mesh_light_samples = ki.subsurface_samples = ki.volume_samples = 1
+    ki.diffuse_samples = scene.diffuse_samples
+    ki.glossy_samples = scene.glossy_samples
+    ki.transmission_samples = scene.transmission_samples
+    ki.ao_samples = ki.subsurface_samples = ki.volume_samples = 1
+    ki.mesh_light_samples = scene.mesh_light_samples
     ki.start_sample = 0
-    ki.sample_all_lights_direct = int(scene.volume_decoupled)
-    ki.sample_all_lights_indirect = int(scene.volume_decoupled)
+    if branched:
+        ki.sample_all_lights_direct = int(scene.sample_all_lights_direct)
+        ki.sample_all_lights_indirect = int(scene.sample_all_lights_indirect)
+    else:
+        # the decoupled volume cases keep the switches on, the setting under
+        # which kernel_volume_use_decoupled takes every segment
+        ki.sample_all_lights_direct = int(scene.volume_decoupled)
+        ki.sample_all_lights_indirect = int(scene.volume_decoupled)
     ki.sampling_pattern = 0
     ki.aa_samples = scene.samples
     if scene.adaptive_min_samples == 0:
@@ -1668,8 +1689,16 @@ def compile_scene(scene: Scene) -> DeviceScene:
     ki.light_inv_rr_threshold = (1.0 / scene.light_sampling_threshold) if scene.light_sampling_threshold > 0 else 0.0
     ki.use_volumes = int(use_volumes)  # shader.cpp:601
     ki.max_closures = max([m.material_closures() for m in mats + [world]] + [1])
+    # integrator.cpp:218-234: branched path tracing sizes the table for its
+    # largest sample count
+    max_samples = 1
+    if branched:
+        max_samples = max([max_samples] + [lamp.samples for lamp in scene.lamps])
+        max_samples = max(max_samples, scene.diffuse_samples, scene.glossy_samples, scene.transmission_samples)
+        max_samples = max(max_samples, ki.ao_samples, scene.mesh_light_samples, ki.subsurface_samples,
+                          ki.volume_samples)
     total_bounces = scene.max_bounce + scene.transparent_max_bounce + 3 + VOLUME_BOUNDS_MAX + BSSRDF_MAX_BOUNCES
-    dims = min(PRNG_BASE_NUM + total_bounces * PRNG_BOUNCE_NUM, sobol.SOBOL_MAX_DIMENSIONS)
+    dims = min(PRNG_BASE_NUM + max_samples * total_bounces * PRNG_BOUNCE_NUM, sobol.SOBOL_MAX_DIMENSIONS)
     lut = sobol.sample_pattern_lut(dims)
 
     # --- background (render/background.cpp:63-118)

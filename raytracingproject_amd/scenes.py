@@ -1045,6 +1045,39 @@ def shadow_catcher(width=48, height=48, samples=8, transparent_film=False) -> sc
     return s
 
 
+def branched_cornell(width=40, height=40, samples=4, sample_all=True) -> sc.Scene:
+    """Branched path tracing (golden parity case; kernel_path_branched.h):
+    at each camera hit (and through the transparent pane in front) every BSDF
+    closure spawns its own indirect paths (2 diffuse, 2 glossy, 1 transmission
+    samples), with direct light from every lamp's samples (a point lamp with
+    two samples, an area lamp) and the mesh light; indirect paths sample all
+    lights too.  Closures: diffuse walls, a diffuse + glossy mix (two closures
+    sampled separately), a glass sphere (reflection and refraction closures)
+    and a half-transparent pane (the camera segment carries on through it).
+    sample_all=False: one light sample per hit, direct and indirect."""
+    s = cornell_box(width, height, samples)
+    base = len(s.materials)
+    s.materials.extend([
+        sc.mix(0.5, sc.glossy((0.9, 0.85, 0.8), 0.2), sc.diffuse((0.3, 0.5, 0.8))),
+        sc.Closure("glass", (1.0, 1.0, 1.0), roughness=0.0, ior=1.45),
+        sc.mix(0.5, sc.transparent((0.9, 0.9, 0.9)), sc.diffuse((0.8, 0.7, 0.3))),
+    ])
+    s.meshes.append(sc.Mesh(*_ellipsoid((140.0, 90.0, 200.0), (80.0, 80.0, 80.0), 20, 12), shader=base, smooth=True))
+    s.meshes.append(sc.Mesh(*_ellipsoid((400.0, 90.0, 150.0), (80.0, 80.0, 80.0), 20, 12), shader=base + 1,
+                            smooth=True))
+    s.meshes.append(sc.Mesh(*_quad((180.0, 150.0, -60.0), (380.0, 150.0, -60.0), (380.0, 350.0, -60.0),
+                                   (180.0, 350.0, -60.0)), shader=base + 2))
+    s.lamps = [sc.Lamp("point", co=(140.0, 480.0, 40.0), size=20.0, color=(1.0, 0.8, 0.6), strength=2.0e6, samples=2),
+               sc.Lamp("area", co=(420.0, 540.0, 380.0), direction=(0.0, -1.0, 0.0), axisv=(0.0, 0.0, 1.0),
+                       size=60.0, color=(0.6, 0.8, 1.0), strength=4.0e4)]
+    s.integrator = "branched_path"
+    s.diffuse_samples, s.glossy_samples, s.transmission_samples = 2, 2, 1
+    s.sample_all_lights_direct = s.sample_all_lights_indirect = sample_all
+    s.max_bounce = 4
+    s.name = "branched_cornell" + ("" if sample_all else "_one_light")
+    return s
+
+
 def data_passes(width=40, height=40, samples=8) -> sc.Scene:
     """Data passes (golden parity case; kernel_passes.h:173-225
     kernel_write_data_passes): depth, normal, UV, object and material index

@@ -110,6 +110,11 @@ CASES = {
     # transparent film; all-lights connection behind the catcher
     "shadow_catcher": lambda: scenes.shadow_catcher(40, 40, 8),
     "shadow_catcher_film": lambda: scenes.shadow_catcher(40, 40, 8, transparent_film=True),
+    # branched path tracing (kernel_path_branched.h): per-closure indirect
+    # samples, all-lights direct and indirect, camera segment through a
+    # transparent pane; and with one light sample per hit
+    "branched_cornell": lambda: scenes.branched_cornell(32, 32, 4),
+    "branched_one_light": lambda: scenes.branched_cornell(32, 32, 4, sample_all=False),
     # data passes (kernel_write_data_passes): depth, normal, UV, object and
     # material index at the camera path's first opaque-enough hit
     "data_passes": lambda: scenes.data_passes(40, 40, 8),

@@ -335,6 +335,12 @@ extern "C" int emu_render(const void *data,
   b.sss_vol = sss_vol;
   hc_float4 catcher[CY_CATCHER_F4];
   b.catcher = catcher; /* every scene: a path without a catcher leaves it unused */
+  hc_float4 br_rec[CY_BR_RECS * CY_BR_REC_F4];
+  uint br_count[2] = {0u, 0u};
+  if (((const hc_KernelData *)data)->integrator.branched) {
+    b.br_rec = br_rec;
+    b.br_count = br_count;
+  }
   hc_float4 ray_diff[CY_RAY_DIFF_F4];
   hc_float4 shadow_dP[2];
   b.ray_diff = ray_diff;
