@@ -84,14 +84,13 @@ class HIPCyclesDevice : public Device {
    * once more against the uploaded KernelData and SVM programs before the first
    * render (hair curves, subsurface scattering, volumes and the shader
    * ray-tracing nodes are implemented; hipcy_load_kernels checks their
-   * variants: curve shapes, BSSRDF falloffs, volume_decoupled, camera in
-   * volume, shadow catchers).  use_shader_raytrace is what
+   * variants: curve shapes, BSSRDF falloffs, branched path tracing with
+   * volumes / BSSRDFs / shadow catchers).  use_shader_raytrace is what
    * ShaderManager::get_requested_features sets for any Ambient Occlusion or
    * Bevel node (render/shader.cpp:724-725): those nodes run on the device. */
   bool load_kernels(const DeviceRequestedFeatures &f) override
   {
-    if (f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_integrator_branched ||
-        f.use_patch_evaluation || f.use_denoising) {
+    if (f.use_object_motion || f.use_camera_motion || f.use_baking || f.use_patch_evaluation || f.use_denoising) {
       set_error("HIP device: requested features are not implemented (" + f.get_build_options() + ")");
       return false;
     }

@@ -24,6 +24,10 @@
 
 /* PassType bits of the data passes (kernel_types.h:353-364: DEPTH .. MATERIAL_ID) */
 #define CY_HOST_DATA_PASSES ((1 << 2) | (1 << 3) | (1 << 4) | (1 << 5) | (1 << 6))
+/* the light passes this device writes (PASSMASK(type) = 1 << (type % 32):
+ * MIST 0, EMISSION 1, BACKGROUND 2, SHADOW 4, LIGHT 5 (no pass), DIFFUSE_*
+ * 6-8, GLOSSY_* 9-11, TRANSMISSION_* 12-14, VOLUME_* 18-19; not AO 3) */
+#define CY_HOST_LIGHT_PASSES ((0x7fff & ~(1 << 3)) | (1 << 18) | (1 << 19))
 
 /* ------------------------------------------------------------------------- */
 /* Kernels                                                                     */
@@ -1448,7 +1452,6 @@ struct GlobalBinding {
 
 }  // namespace
 
-#define CY_LANES 4
 
 struct hipcy_device {
   int ordinal = 0;
@@ -1535,6 +1538,8 @@ struct hipcy_device {
   bool use_catcher = false;           /* shadow-catcher objects: the slots' catcher records */
   bool use_branched = false;          /* branched path tracing: the slots' branch records */
   char *br_pool = nullptr;            /* those records and their counters */
+  bool use_lightpass = false;         /* light passes: the slots' PathRadiance components */
+  char *lp_pool = nullptr;            /* those records (CY_LP_F4 float4 per slot) */
   char *catcher_pool = nullptr;       /* those records (CY_CATCHER_F4 float4 per slot) */
   char *sss_pool = nullptr;           /* those records and their depths */
   bool use_ray_diff = false;          /* a shader reads ray differentials (Bump / *_BUMP_DX / _DY nodes) */
@@ -1762,6 +1767,11 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   }
   dev->bufs.br_rec = nullptr;
   dev->bufs.br_count = nullptr;
+  if (dev->lp_pool) {
+    hipFree(dev->lp_pool);
+    dev->lp_pool = nullptr;
+  }
+  dev->bufs.lp = nullptr;
   dev->bufs.sss_rec = nullptr;
   dev->bufs.sss_vol = nullptr;
   dev->bufs.sss_count = nullptr;
@@ -1826,6 +1836,17 @@ static int ensure_branch_capacity(hipcy_device *dev)
   }
   dev->bufs.br_rec = dev->use_branched ? (hc_float4 *)dev->br_pool : nullptr;
   dev->bufs.br_count = dev->use_branched ? (uint *)(dev->br_pool + recs) : nullptr;
+  return 0;
+}
+
+/* The slots' light-pass records (cy_integrator.h CyLightPass, 256 B per
+ * slot), for films with light passes only. */
+static int ensure_lightpass_capacity(hipcy_device *dev)
+{
+  if (dev->use_lightpass && !dev->lp_pool) {
+    HIP_CHECK(dev, hipMalloc((void **)&dev->lp_pool, (size_t)16 * CY_LP_F4 * dev->capacity));
+  }
+  dev->bufs.lp = dev->use_lightpass ? (hc_float4 *)dev->lp_pool : nullptr;
   return 0;
 }
 
@@ -1984,6 +2005,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->sss_pool) hipFree(dev->sss_pool);
   if (dev->catcher_pool) hipFree(dev->catcher_pool);
   if (dev->br_pool) hipFree(dev->br_pool);
+  if (dev->lp_pool) hipFree(dev->lp_pool);
   if (dev->diff_pool) hipFree(dev->diff_pool);
   if (dev->srec_pool) hipFree(dev->srec_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
@@ -2748,7 +2770,6 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.cam.shuttertime != -1.0f || d.cam.num_motion_steps) why = "motion blur";
   else if (d.cam.interocular_offset != 0.0f) why = "stereo";
   else if (d.integrator.sampling_pattern != 0) why = "only the Sobol pattern";
-  else if (d.integrator.branched) why = "branched path tracing";
   else if (d.integrator.use_volumes && !d.integrator.transparent_shadows)
     why = "volumes without transparent shadows (shader.cpp:529-536 sets them for every volume shader)";
   else if (d.integrator.transparent_shadows && d.integrator.transparent_max_bounce > CY_SHADOW_MAX_HITS)
@@ -2767,7 +2788,9 @@ int hipcy_load_kernels(hipcy_device *dev)
   else if (d.bvh.have_curves && (d.bvh.curve_subdivisions < 1 || d.bvh.curve_subdivisions > 16))
     why = "curve_subdivisions outside 1..16";
   else if (d.bvh.bvh_layout != 1) why = "bvh_layout must be BVH2";
-  else if (d.film.use_light_pass) why = "light passes";
+  else if (d.film.use_light_pass && (d.film.light_pass_flag & ~CY_HOST_LIGHT_PASSES) != 0)
+    why = "light passes other than mist, emission, background, shadow and the diffuse / glossy / transmission / "
+          "volume direct, indirect and colour passes (no AO pass)";
   else if ((d.film.pass_flag & 2) == 0 || (d.film.pass_flag & ~(2 | CY_HOST_DATA_PASSES | (1 << 11) | (1 << 12) |
                                                                   (1 << 13) | (1 << 14))) != 0 ||
            d.film.pass_combined != 0)
@@ -2902,6 +2925,21 @@ int hipcy_load_kernels(hipcy_device *dev)
                                 std::to_string(d.integrator.max_closures) + " closures x " + std::to_string(samples) +
                                 " samples: more waiting paths than the device's " + std::to_string(CY_BR_RECS) +
                                 " per slot");
+    }
+    dev->shade_tex = true;
+  }
+  /* kernel_write_light_passes (kernel_passes.h:285-337): the extended shading
+   * kernels keep the path's PathRadiance components in a record per slot;
+   * not with volumes, BSSRDFs, shadow catchers or branched path tracing */
+  dev->use_lightpass = d.film.use_light_pass != 0;
+  if (dev->use_lightpass) {
+    const char *with = d.integrator.use_volumes ? "volumes"
+                       : uses_bssrdf            ? "subsurface scattering"
+                       : dev->use_catcher       ? "shadow catchers"
+                       : dev->use_branched      ? "branched path tracing"
+                                                : nullptr;
+    if (with) {
+      return set_error(dev, std::string("load_kernels: unsupported scene feature: light passes with ") + with);
     }
     dev->shade_tex = true;
   }
@@ -3281,7 +3319,7 @@ static int lane_tail(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, int W
   hipStream_t s = ln.s;
   uint *err = dev->counters + 3;
   dev->stats.iterations++;
-  HIP_CHECK(dev, hipMemsetAsync(ln.cnt + 13, 0, 8, s));
+  HIP_CHECK(dev, hipMemsetAsync(ln.cnt + 13, 0, 12, s)); /* ray counts and the take-next counter */
   const dim3 grid((ln.n_active + CY_BLOCK - 1) / CY_BLOCK), block(CY_BLOCK);
   if (!cy_launch_tail(dev->shade_closures, dev->shade_tex, dev->use_volumes, W, kg.have_instancing != 0, grid, block,
                       s, kg, dev->bufs, ln.tile, ln.q[ln.qa], ln.cnt + ln.qa, ln.cnt + 13, err)) {
@@ -3536,7 +3574,7 @@ static int path_trace(hipcy_device *dev, const hipcy_work_tile *tiles, int n_til
   }
   const size_t items = npix * per_pass;
   if (ensure_capacity(dev, std::min(items, dev->slots_wanted)) != 0 || ensure_volume_capacity(dev) != 0 ||
-      ensure_sss_capacity(dev) != 0 || ensure_catcher_capacity(dev) != 0 || ensure_branch_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
+      ensure_sss_capacity(dev) != 0 || ensure_catcher_capacity(dev) != 0 || ensure_branch_capacity(dev) != 0 || ensure_lightpass_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 ||
       ensure_srec_capacity(dev) != 0 ||
       ensure_records(dev, items) != 0 || ensure_bvhw(dev) != 0) {
     return -1;
@@ -3990,7 +4028,7 @@ static int stream_restart(StreamState &st, StreamLane &S, uint n_live)
 static int stream_pool(hipcy_device *dev, size_t slots)
 {
   if (ensure_capacity(dev, slots) != 0 || ensure_volume_capacity(dev) != 0 || ensure_sss_capacity(dev) != 0 ||
-      ensure_catcher_capacity(dev) != 0 || ensure_branch_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
+      ensure_catcher_capacity(dev) != 0 || ensure_branch_capacity(dev) != 0 || ensure_lightpass_capacity(dev) != 0 || ensure_diff_capacity(dev) != 0 || ensure_srec_capacity(dev) != 0 || ensure_sort(dev) != 0) {
     return -1;
   }
   return 0;

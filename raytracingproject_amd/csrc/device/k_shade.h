@@ -45,6 +45,12 @@ void cy_launch_shade_mc64_vol(CY_SHADE_LAUNCHER_ARGS);
 #define CY_DEVICE_MAX_CLOSURE 64
 
 /* the fused tail kernel (k_shade.hip k_tail_*), plain variants only */
+/* lanes of a pass (slot-pool quarters on their own streams, hipcycles.hip) */
+#define CY_LANES 4
+
+/* grid.x = blocks for every waiting path; the launcher clamps it to the lane's
+ * share of the resident blocks (the tail kernel is persistent), and counts[2]
+ * is the kernel's take-next counter (zeroed with counts[0..1]) */
 #define CY_TAIL_LAUNCHER_ARGS \
   int W, bool inst, dim3 grid, dim3 block, hipStream_t stream, const CyGlobals &kg, const CyPathBuffers &b, \
       const CyTile &tile, const int *queue_in, const uint *count_in, uint *counts, uint *err

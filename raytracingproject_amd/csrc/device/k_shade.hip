@@ -12,6 +12,8 @@
 #ifndef CY_CLOSURE_EXT
 #  define CY_CLOSURE_EXT CY_SVM_TEX
 #endif
+#include <algorithm>
+
 #include "cy_device_common.h"
 #include "k_shade.h"
 #if !CY_SVM_TEX
@@ -149,11 +151,16 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SH
 #endif
   __shared__ LdsStack<W, INST, true> lds_stack;
   lds_fill_top(&kg, &lds_stack); /* a barrier: before any thread leaves */
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int)*count_in) {
+  /* persistent: the grid holds what the chip keeps resident for the lane
+   * (cy_launch_tail_*), and a thread whose path ends takes the next waiting
+   * one (counts[2]), so no block waits on its slowest path while paths are
+   * left; one wave-combined atomic per wave and grab */
+  const uint n = *count_in;
+  uint next = atomicAdd(&counts[2], 1u);
+  if (next >= n) {
     return;
   }
-  const int slot = queue_in[i];
+  int slot = queue_in[next];
   uint n_closest = 0, n_shadow = 0, n_leaves = 0, n_tris = 0;
   for (;;) {
     /* stage 1 (k_intersect_closest) */
@@ -191,7 +198,11 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SH
       n_shadow++;
     }
     if (!cont) {
-      break;
+      next = atomicAdd(&counts[2], 1u);
+      if (next >= n) {
+        break;
+      }
+      slot = queue_in[next];
     }
   }
   atomicAdd(&counts[0], n_closest);
@@ -203,6 +214,23 @@ void CY_CAT(cy_launch_tail_, CY_SHADE_VARIANT)(CY_TAIL_LAUNCHER_ARGS)
   auto fn = W == 8 ? (inst ? CY_CAT(k_tail_, CY_SHADE_VARIANT)<8, true> : CY_CAT(k_tail_, CY_SHADE_VARIANT)<8, false>) :
             W == 4 ? (inst ? CY_CAT(k_tail_, CY_SHADE_VARIANT)<4, true> : CY_CAT(k_tail_, CY_SHADE_VARIANT)<4, false>) :
                      (inst ? CY_CAT(k_tail_, CY_SHADE_VARIANT)<2, true> : CY_CAT(k_tail_, CY_SHADE_VARIANT)<2, false>);
-  hipLaunchKernelGGL(fn, grid, block, 0, stream, kg, b, tile, queue_in, count_in, counts, err);
+  /* the lane's share of the resident blocks (the CY_LANES lanes' tails run
+   * side by side); at least one block */
+  static int occupancy[3][2] = {};
+  int &occ = occupancy[W == 8 ? 2 : W == 4 ? 1 : 0][inst ? 1 : 0];
+  if (occ == 0) {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, (int)block.x, 0) != hipSuccess || o < 1) {
+      o = 1;
+    }
+    occ = o;
+  }
+  int device = 0, cus = 0;
+  if (hipGetDevice(&device) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) {
+    cus = 1;
+  }
+  const dim3 g(std::max(1u, std::min(grid.x, (unsigned)(occ * cus / CY_LANES))));
+  hipLaunchKernelGGL(fn, g, block, 0, stream, kg, b, tile, queue_in, count_in, counts, err);
 }
 #endif

@@ -127,7 +127,7 @@ CY_FN float path_branched_rng_1D(const CyGlobals *kg, uint rng_hash, const CyPat
  * contribution. */
 CY_FN bool surface_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightSample *ls, const CyPathState *state,
                                    float rand_terminate, cfloat3 *eval, cfloat3 *eval_no_mis, CyRay *light_ray,
-                                   CyShadeMem mem, uint *err)
+                                   CyShadeMem mem, uint *err, CyBsdfEvalLP *ev_lp = nullptr)
 {
   if (ls->pdf == 0.0f) {
     return false;
@@ -159,7 +159,49 @@ CY_FN bool surface_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightS
   }
   cfloat3 e = mk3(0.0f, 0.0f, 0.0f); /* shader_bsdf_multi_eval accumulates */
   cfloat3 no_mis;
-  if (KD->integrator.branched) {
+  if (ev_lp) {
+    /* light passes: shader_bsdf_eval per component (kernel_shader.h:606-636),
+     * the light's eval, the pass exclusions per component
+     * (kernel_emission.h:141-153), the termination on the components' sum */
+    bsdf_eval_lp_zero(ev_lp);
+    float bpdf;
+    shader_bsdf_multi_eval_lp(sd, ls->D, &bpdf, -1, ev_lp, 0.0f, 0.0f);
+    if ((uint)ls->shader & SHADER_USE_MIS) {
+      bsdf_eval_lp_mul(ev_lp, power_heuristic(ls->pdf, bpdf));
+    }
+    bsdf_eval_lp_mul3(ev_lp, div3f(light_eval, ls->pdf));
+    const uint sh = (uint)ls->shader;
+    if (sh & SHADER_EXCLUDE_ANY) {
+      const cfloat3 z = mk3(0.0f, 0.0f, 0.0f);
+      if (sh & SHADER_EXCLUDE_DIFFUSE) {
+        ev_lp->diffuse = z;
+      }
+      if (sh & SHADER_EXCLUDE_GLOSSY) {
+        ev_lp->glossy = z;
+      }
+      if (sh & SHADER_EXCLUDE_TRANSMIT) {
+        ev_lp->transmission = z;
+      }
+      if (sh & SHADER_EXCLUDE_SCATTER) {
+        ev_lp->volume = z;
+      }
+    }
+    if (bsdf_eval_lp_is_zero(ev_lp)) {
+      return false;
+    }
+    if (KD->integrator.light_inv_rr_threshold > 0.0f && !(state->flag & PATH_RAY_SHADOW_CATCHER)) {
+      const float probability = max3f(fabs3(bsdf_eval_lp_sum(ev_lp))) * KD->integrator.light_inv_rr_threshold;
+      if (probability < 1.0f) {
+        if (rand_terminate >= probability) {
+          return false;
+        }
+        bsdf_eval_lp_mul(ev_lp, 1.0f / probability);
+      }
+    }
+    e = bsdf_eval_lp_sum(ev_lp);
+    no_mis = e;
+  }
+  else if (KD->integrator.branched) {
     shader_bsdf_eval_branched(sd, ls->D, ls->pdf, ((uint)ls->shader & SHADER_USE_MIS) != 0, &e, &no_mis);
   }
   else {
@@ -176,10 +218,10 @@ CY_FN bool surface_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightS
   if (((uint)ls->shader & SHADER_EXCLUDE_ANY) && ((uint)ls->shader & SHADER_EXCLUDE_DIFFUSE)) {
     e = mk3(0.0f, 0.0f, 0.0f);
   }
-  if (is_zero3(e)) {
+  if (!ev_lp && is_zero3(e)) {
     return false;
   }
-  if (KD->integrator.light_inv_rr_threshold > 0.0f && !(state->flag & PATH_RAY_SHADOW_CATCHER)) {
+  if (!ev_lp && KD->integrator.light_inv_rr_threshold > 0.0f && !(state->flag & PATH_RAY_SHADOW_CATCHER)) {
     const float probability = max3f(fabs3(e)) * KD->integrator.light_inv_rr_threshold;
     if (probability < 1.0f) {
       if (rand_terminate >= probability) {
@@ -218,7 +260,8 @@ CY_FN bool surface_direct_emission(const CyGlobals *kg, const CySD *sd, CyLightS
  * are evaluated into shadow_mem, so sd's closures stay intact. */
 CY_NOINLINE void connect_light_branched(const CyGlobals *kg, const CySD *sd, const CyPathState *state,
                                         cfloat3 throughput, float num_samples_adjust, bool sample_all_lights,
-                                        cfloat3 *L, CyCatcher *catcher, CyShadeMem mem, uint *err)
+                                        cfloat3 *L, CyCatcher *catcher, CyShadeMem mem, uint *err,
+                                        CyLightPass *lp = nullptr)
 {
   if (!KD->integrator.use_direct_light) {
     return;
@@ -265,6 +308,7 @@ CY_NOINLINE void connect_light_branched(const CyGlobals *kg, const CySD *sd, con
       light_ray.t = 0.0f;
       bool has_emission = false;
       cfloat3 eval = mk3(0.0f, 0.0f, 0.0f), eval_no_mis = mk3(0.0f, 0.0f, 0.0f);
+      CyBsdfEvalLP ev_lp;
       if (sd->flag & SD_BSDF_HAS_EVAL) {
         float light_u, light_v;
         path_branched_rng_2D(kg, lamp_rng_hash, state, j, num_samples, PRNG_LIGHT_U, &light_u, &light_v);
@@ -281,7 +325,12 @@ CY_NOINLINE void connect_light_branched(const CyGlobals *kg, const CySD *sd, con
             ls.pdf *= 2.0f;
           }
           has_emission = surface_direct_emission(kg, sd, &ls, state, terminate, &eval, &eval_no_mis, &light_ray,
-                                                 mem, err);
+                                                 mem, err, lp ? &ev_lp : nullptr);
+          if (has_emission) {
+            /* direct_emission writes is_lamp, the variable the next sample's
+             * lamp choice reads (kernel_path_surface.h:98-112) */
+            is_lamp = (ls.prim == PRIM_NONE && ls.type != LIGHT_BACKGROUND);
+          }
         }
       }
       /* shadow_blocked (kernel_shadow.h:386-460) */
@@ -316,7 +365,32 @@ CY_NOINLINE void connect_light_branched(const CyGlobals *kg, const CySD *sd, con
             continue;
           }
         }
-        if (!blocked) {
+        if (!blocked && lp) {
+          /* path_radiance_accum_light with light passes (kernel_accumulate.h:425-452) */
+          cfloat3 shaded_throughput = mul3(tp, shadow);
+          cfloat3 full_contribution = mul3(shaded_throughput, bsdf_eval_lp_sum(&ev_lp));
+          const float limit = (state->bounce > 0) ? KD->integrator.sample_clamp_indirect :
+                                                    KD->integrator.sample_clamp_direct;
+          const float sum = reduce_add3(fabs3(full_contribution));
+          if (sum > limit) {
+            const float clamp_factor = limit / sum;
+            full_contribution = mul3f(full_contribution, clamp_factor);
+            shaded_throughput = mul3f(shaded_throughput, clamp_factor);
+          }
+          if (state->bounce == 0) {
+            lp->direct_diffuse = add3(lp->direct_diffuse, mul3(shaded_throughput, ev_lp.diffuse));
+            lp->direct_glossy = add3(lp->direct_glossy, mul3(shaded_throughput, ev_lp.glossy));
+            lp->direct_transmission = add3(lp->direct_transmission, mul3(shaded_throughput, ev_lp.transmission));
+            lp->direct_volume = add3(lp->direct_volume, mul3(shaded_throughput, ev_lp.volume));
+            if (is_lamp) {
+              lp->shadow = add3(lp->shadow, mul3f(shadow, num_samples_inv));
+            }
+          }
+          else {
+            lp->indirect = add3(lp->indirect, full_contribution);
+          }
+        }
+        else if (!blocked) {
           const cfloat3 contribution = mul3(mul3(tp, shadow), eval);
           *L = add3(*L, path_radiance_clamp(kg, contribution, state->bounce));
         }

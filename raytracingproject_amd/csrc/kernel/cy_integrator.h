@@ -84,6 +84,9 @@ typedef struct CyPathBuffers {
    * first out; cy_branched.h) */
   hc_float4 *br_rec;
   uint *br_count;
+  /* light passes (KernelFilm.use_light_pass): the path's PathRadiance
+   * components, CY_LP_F4 float4 per slot (CyLightPass) */
+  hc_float4 *lp;
 } CyPathBuffers;
 
 /* The shadow-catcher part of PathRadiance (kernel_accumulate.h:203-233,
@@ -598,6 +601,73 @@ CY_FN cfloat3 path_radiance_clamp(const CyGlobals *kg, cfloat3 L, int bounce)
   return L;
 }
 
+/* PathRadiance with light passes (kernel_types.h:523-578): the components a
+ * path adds to (emission stays the radiance L itself) and PathRadianceState,
+ * the first bounce's BSDF weights per component */
+typedef struct CyLightPass {
+  cfloat3 background, direct_emission, indirect;
+  cfloat3 direct_diffuse, direct_glossy, direct_transmission, direct_volume;
+  cfloat3 color_diffuse, color_glossy, color_transmission;
+  cfloat3 state_diffuse, state_glossy, state_transmission, state_volume, state_direct;
+  cfloat3 shadow;
+  float mist;
+} CyLightPass;
+#define CY_LP_F4 16
+
+CY_FN void lightpass_init(CyLightPass *p)
+{
+  const cfloat3 z = mk3(0.0f, 0.0f, 0.0f);
+  p->background = p->direct_emission = p->indirect = z;
+  p->direct_diffuse = p->direct_glossy = p->direct_transmission = p->direct_volume = z;
+  p->color_diffuse = p->color_glossy = p->color_transmission = z;
+  p->state_diffuse = p->state_glossy = p->state_transmission = p->state_volume = p->state_direct = z;
+  p->shadow = z;
+  p->mist = 0.0f;
+}
+
+CY_FN void lightpass_load(const CyPathBuffers *b, int slot, CyLightPass *p)
+{
+  const hc_float4 *src = b->lp + (size_t)slot * CY_LP_F4;
+  cfloat3 *f[15] = {&p->background, &p->direct_emission, &p->indirect, &p->direct_diffuse, &p->direct_glossy,
+                    &p->direct_transmission, &p->direct_volume, &p->color_diffuse, &p->color_glossy,
+                    &p->color_transmission, &p->state_diffuse, &p->state_glossy, &p->state_transmission,
+                    &p->state_volume, &p->state_direct};
+  for (int k = 0; k < 15; k++) {
+    const hc_float4 r = cy_ld(&src[k]);
+    *f[k] = mk3(r.x, r.y, r.z);
+  }
+  const hc_float4 r = cy_ld(&src[15]);
+  p->shadow = mk3(r.x, r.y, r.z);
+  p->mist = r.w;
+}
+
+CY_FN void lightpass_store(const CyPathBuffers *b, int slot, const CyLightPass *p)
+{
+  hc_float4 *dst = b->lp + (size_t)slot * CY_LP_F4;
+  const cfloat3 *f[15] = {&p->background, &p->direct_emission, &p->indirect, &p->direct_diffuse, &p->direct_glossy,
+                          &p->direct_transmission, &p->direct_volume, &p->color_diffuse, &p->color_glossy,
+                          &p->color_transmission, &p->state_diffuse, &p->state_glossy, &p->state_transmission,
+                          &p->state_volume, &p->state_direct};
+  for (int k = 0; k < 15; k++) {
+    cy_st(&dst[k], mkf4(f[k]->x, f[k]->y, f[k]->z, 0.0f));
+  }
+  cy_st(&dst[15], mkf4(p->shadow.x, p->shadow.y, p->shadow.z, p->mist));
+}
+
+/* path_radiance_accum_emission with light passes (kernel_accumulate.h:320-330) */
+CY_FN void lightpass_accum_emission(CyLightPass *p, cfloat3 *L, int bounce, cfloat3 contribution)
+{
+  if (bounce == 0) {
+    *L = add3(*L, contribution);
+  }
+  else if (bounce == 1) {
+    p->direct_emission = add3(p->direct_emission, contribution);
+  }
+  else {
+    p->indirect = add3(p->indirect, contribution);
+  }
+}
+
 /* the slot's catcher record (CyPathBuffers.catcher) */
 CY_FN void catcher_init(const CyGlobals *kg, CyCatcher *c)
 {
@@ -766,6 +836,76 @@ CY_FN float *pixel_buffer(const CyTile *tile, uint p)
 
 /* Render-buffer pixel of work item `item` (its RenderTile's buffer at the
  * tile's offset / stride): where the camera path's AOV outputs are added. */
+CY_FN float *item_buffer(const CyTile *tile, uint item);
+
+/* path_radiance_clamp_and_sum with light passes (kernel_accumulate.h:622-676)
+ * and kernel_write_light_passes (kernel_passes.h:292-337): the combined value
+ * summed from the components (returned), the light passes added to the pixel */
+CY_FN cfloat3 lightpass_finish(const CyGlobals *kg, float *buffer, cfloat3 emission, CyLightPass *p)
+{
+  /* path_radiance_sum_indirect (kernel_accumulate.h:536-556) */
+  const cfloat3 dE = safe_divide_color(p->direct_emission, p->state_direct);
+  p->direct_diffuse = add3(p->direct_diffuse, mul3(p->state_diffuse, dE));
+  p->direct_glossy = add3(p->direct_glossy, mul3(p->state_glossy, dE));
+  p->direct_transmission = add3(p->direct_transmission, mul3(p->state_transmission, dE));
+  p->direct_volume = add3(p->direct_volume, mul3(p->state_volume, dE));
+  const cfloat3 ind = safe_divide_color(p->indirect, p->state_direct);
+  const cfloat3 z = mk3(0.0f, 0.0f, 0.0f);
+  cfloat3 indirect_diffuse = add3(z, mul3(p->state_diffuse, ind));
+  cfloat3 indirect_glossy = add3(z, mul3(p->state_glossy, ind));
+  cfloat3 indirect_transmission = add3(z, mul3(p->state_transmission, ind));
+  cfloat3 indirect_volume = add3(z, mul3(p->state_volume, ind));
+  cfloat3 L_direct = add3(add3(add3(add3(p->direct_diffuse, p->direct_glossy), p->direct_transmission),
+                               p->direct_volume),
+                          emission);
+  const cfloat3 L_indirect = add3(add3(add3(indirect_diffuse, indirect_glossy), indirect_transmission),
+                                  indirect_volume);
+  if (!KD->background.transparent) {
+    L_direct = add3(L_direct, p->background);
+  }
+  cfloat3 L_sum = add3(L_direct, L_indirect);
+  const float sum = fabsf(L_sum.x) + fabsf(L_sum.y) + fabsf(L_sum.z);
+  if (!isfinite_safe(sum)) {
+    L_sum = z;
+    p->direct_diffuse = p->direct_glossy = p->direct_transmission = p->direct_volume = z;
+    indirect_diffuse = indirect_glossy = indirect_transmission = indirect_volume = z;
+    emission = z;
+  }
+  const int flag = KD->film.light_pass_flag;
+  auto add = [&](int bit, int offset, cfloat3 v) {
+    if (flag & (1 << bit)) {
+      cy_pass_add(buffer + offset + 0, v.x);
+      cy_pass_add(buffer + offset + 1, v.y);
+      cy_pass_add(buffer + offset + 2, v.z);
+    }
+  };
+  /* PASSMASK(type) = 1 << (type % 32), PassType MIST 32 .. VOLUME_INDIRECT 51 */
+  add(7, KD->film.pass_diffuse_indirect, indirect_diffuse);
+  add(10, KD->film.pass_glossy_indirect, indirect_glossy);
+  add(13, KD->film.pass_transmission_indirect, indirect_transmission);
+  add(19, KD->film.pass_volume_indirect, indirect_volume);
+  add(6, KD->film.pass_diffuse_direct, p->direct_diffuse);
+  add(9, KD->film.pass_glossy_direct, p->direct_glossy);
+  add(12, KD->film.pass_transmission_direct, p->direct_transmission);
+  add(18, KD->film.pass_volume_direct, p->direct_volume);
+  add(1, KD->film.pass_emission, emission);
+  add(2, KD->film.pass_background, p->background);
+  add(8, KD->film.pass_diffuse_color, p->color_diffuse);
+  add(11, KD->film.pass_glossy_color, p->color_glossy);
+  add(14, KD->film.pass_transmission_color, p->color_transmission);
+  if (flag & (1 << 4)) {
+    float *q = buffer + KD->film.pass_shadow;
+    cy_pass_add(q + 0, p->shadow.x);
+    cy_pass_add(q + 1, p->shadow.y);
+    cy_pass_add(q + 2, p->shadow.z);
+    cy_pass_add(q + 3, KD->film.pass_shadow_scale);
+  }
+  if (flag & (1 << 0)) {
+    cy_pass_add(buffer + KD->film.pass_mist, 1.0f - p->mist);
+  }
+  return L_sum;
+}
+
 CY_FN float *item_buffer(const CyTile *tile, uint item)
 {
   if (tile->stream) {
@@ -872,6 +1012,13 @@ CY_FN bool slot_start(const CyGlobals *kg, const CyPathBuffers *b, const CyTile 
     catcher_init(kg, &c);
     catcher_store(b, slot, &c);
   }
+#if CY_CLOSURE_EXT
+  if (b->lp) {
+    CyLightPass p;
+    lightpass_init(&p);
+    lightpass_store(b, slot, &p);
+  }
+#endif
   return true;
 }
 
@@ -2563,6 +2710,16 @@ CY_FN bool shade_path(const CyGlobals *kg,
       catcher_load(kg, b, slot, &catcher);
     }
   }
+  /* light passes: the path's PathRadiance components */
+  CyLightPass lp;
+  if (b->lp) {
+    if (cam_item != CY_NO_ITEM) {
+      lightpass_init(&lp);
+    }
+    else {
+      lightpass_load(b, slot, &lp);
+    }
+  }
 #endif
 #ifdef CY_DBG_X
   {
@@ -2673,7 +2830,10 @@ CY_FN bool shade_path(const CyGlobals *kg,
       cfloat3 contribution = mul3(throughput, lamp_L);
       contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
 #if CY_CATCHER
-      if (!(state.flag & PATH_RAY_SHADOW_CATCHER))
+      if (b->lp) {
+        lightpass_accum_emission(&lp, &L, state.bounce, contribution);
+      }
+      else if (!(state.flag & PATH_RAY_SHADOW_CATCHER))
 #endif
       {
         L = add3(L, contribution);
@@ -2760,7 +2920,24 @@ CY_FN bool shade_path(const CyGlobals *kg,
       if (!catcher_path) {
         cfloat3 contribution = mul3(throughput, L_background);
         contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
-        L = add3(L, contribution);
+#if CY_CATCHER
+        if (b->lp) {
+          /* path_radiance_accum_background with light passes (kernel_accumulate.h:500-510) */
+          if (state.flag & PATH_RAY_TRANSPARENT_BACKGROUND) {
+            lp.background = add3(lp.background, contribution);
+          }
+          else if (state.bounce == 1) {
+            lp.direct_emission = add3(lp.direct_emission, contribution);
+          }
+          else {
+            lp.indirect = add3(lp.indirect, contribution);
+          }
+        }
+        else
+#endif
+        {
+          L = add3(L, contribution);
+        }
       }
     }
   }
@@ -2942,6 +3119,65 @@ CY_FN bool shade_path(const CyGlobals *kg,
         state.flag |= PATH_RAY_SINGLE_PASS_DONE;
       }
     }
+#if CY_CATCHER
+    if (b->lp && (state.flag & PATH_RAY_CAMERA)) {
+      /* kernel_passes.h:251-281: colour passes and mist at camera hits */
+      const int lflag = KD->film.light_pass_flag;
+      cfloat3 cd = mk3(0.0f, 0.0f, 0.0f), cg = cd, ct = cd;
+      for (int i = 0; i < sd.num_closure; i++) {
+        const CyClosure *sc = &sd.closure[i];
+        if (CLOSURE_IS_BSDF_DIFFUSE(sc->type) || CLOSURE_IS_BSSRDF(sc->type) || CLOSURE_IS_BSDF_BSSRDF(sc->type)) {
+          cd = add3(cd, sc->weight);
+        }
+        if (CLOSURE_IS_BSDF_GLOSSY(sc->type)) {
+          cg = add3(cg, sc->weight);
+        }
+        if (CLOSURE_IS_BSDF_TRANSMISSION(sc->type)) {
+          ct = add3(ct, sc->weight);
+        }
+      }
+      if (lflag & ((1 << 6) | (1 << 7) | (1 << 8))) {
+        lp.color_diffuse = add3(lp.color_diffuse, mul3(cd, throughput));
+      }
+      if (lflag & ((1 << 9) | (1 << 10) | (1 << 11))) {
+        lp.color_glossy = add3(lp.color_glossy, mul3(cg, throughput));
+      }
+      if (lflag & ((1 << 12) | (1 << 13) | (1 << 14))) {
+        lp.color_transmission = add3(lp.color_transmission, mul3(ct, throughput));
+      }
+      if (lflag & 1) {
+        /* camera_distance (kernel_camera.h:472-482) */
+        const hc_Transform &c = KD->cam.cameratoworld;
+        const cfloat3 camP = mk3(c.x.w, c.y.w, c.z.w);
+        float depth;
+        if (KD->cam.type == 1 /* CAMERA_ORTHOGRAPHIC */) {
+          const cfloat3 camD = mk3(c.x.z, c.y.z, c.z.z);
+          depth = fabsf(dot3(sub3(sd.P, camP), camD));
+        }
+        else {
+          depth = len3(sub3(sd.P, camP));
+        }
+        float mist = saturate((depth - KD->film.mist_start) * KD->film.mist_inv_depth);
+        const float falloff = KD->film.mist_falloff;
+        if (falloff == 1.0f) {
+        }
+        else if (falloff == 2.0f) {
+          mist = mist * mist;
+        }
+        else if (falloff == 0.5f) {
+          mist = sqrtf(mist);
+        }
+        else {
+          mist = cy_powf(mist, falloff);
+        }
+        const cfloat3 tr = shader_bsdf_transparency(&sd);
+        cfloat3 alpha = mk3(1.0f - tr.x, 1.0f - tr.y, 1.0f - tr.z);
+        alpha = mk3(cmax(alpha.x, 0.0f), cmax(alpha.y, 0.0f), cmax(alpha.z, 0.0f));
+        alpha = mk3(cmin(alpha.x, 1.0f), cmin(alpha.y, 1.0f), cmin(alpha.z, 1.0f));
+        lp.mist += (1.0f - mist) * average3(mul3(throughput, alpha));
+      }
+    }
+#endif
     if (KD->integrator.filter_glossy != CY_FLT_MAX) {
       float blur_pdf = KD->integrator.filter_glossy * state.min_ray_pdf;
       if (blur_pdf < 1.0f) {
@@ -2985,7 +3221,10 @@ CY_FN bool shade_path(const CyGlobals *kg,
       cfloat3 contribution = mul3(throughput, emission);
       contribution = path_radiance_clamp(kg, contribution, state.bounce - 1);
 #if CY_CATCHER
-      if (!(state.flag & PATH_RAY_SHADOW_CATCHER))
+      if (b->lp) {
+        lightpass_accum_emission(&lp, &L, state.bounce, contribution);
+      }
+      else if (!(state.flag & PATH_RAY_SHADOW_CATCHER))
 #endif
       {
         L = add3(L, contribution);
@@ -3109,8 +3348,13 @@ CY_FN bool shade_path(const CyGlobals *kg,
         else
 #endif
 #if CY_CATCHER
-        if ((state.flag & PATH_RAY_SHADOW_CATCHER) ||
-            (KD->integrator.branched && KD->integrator.sample_all_lights_indirect)) {
+        if (b->lp) {
+          /* light passes: the light sample traced here, added per component */
+          connect_light_branched(kg, &sd, &state, throughput, 1.0f, (state.flag & PATH_RAY_SHADOW_CATCHER) != 0, &L,
+                                 &catcher, mem, err, &lp);
+        }
+        else if ((state.flag & PATH_RAY_SHADOW_CATCHER) ||
+                 (KD->integrator.branched && KD->integrator.sample_all_lights_indirect)) {
           /* kernel_path_indirect (kernel_path.h:470-476) / a path behind a
            * shadow catcher: all lights */
           connect_light_branched(kg, &sd, &state, throughput, 1.0f, true, &L, &catcher, mem, err);
@@ -3146,8 +3390,18 @@ CY_FN bool shade_path(const CyGlobals *kg,
         float bsdf_pdf = 0.0f;
 #if CY_CLOSURE_EXT
         CyDiff3 domega;
-        int label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err,
-                                       kg->use_ray_diff ? &domega : nullptr);
+        CyBsdfEvalLP ev_lp;
+        int label;
+        if (CY_CATCHER && b->lp) {
+          label = shader_bsdf_sample_lp(kg, &sd, bsdf_u, bsdf_v, &ev_lp, &omega_in, &bsdf_pdf, err,
+                                        kg->use_ray_diff ? &domega : nullptr);
+          /* bsdf_eval_is_zero over every component (the transparent one too) */
+          bsdf_eval_v = bsdf_eval_lp_is_zero(&ev_lp) ? mk3(0.0f, 0.0f, 0.0f) : mk3(1.0f, 1.0f, 1.0f);
+        }
+        else {
+          label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err,
+                                     kg->use_ray_diff ? &domega : nullptr);
+        }
 #else
         int label = shader_bsdf_sample(kg, &sd, bsdf_u, bsdf_v, &bsdf_eval_v, &omega_in, &bsdf_pdf, err);
 #endif
@@ -3157,7 +3411,29 @@ CY_FN bool shade_path(const CyGlobals *kg,
         CY_DBG1(&state, "bsdf pdf", bsdf_pdf);
         if (!(bsdf_pdf == 0.0f || is_zero3(bsdf_eval_v))) {
           float inverse_pdf = 1.0f / bsdf_pdf;
-          throughput = mul3(throughput, mul3f(bsdf_eval_v, inverse_pdf));
+#if CY_CATCHER
+          if (b->lp) {
+            /* path_radiance_bsdf_bounce with light passes (kernel_accumulate.h:247-265) */
+            if (state.bounce == 0 && !(label & LABEL_TRANSPARENT)) {
+              const cfloat3 value = mul3f(throughput, inverse_pdf);
+              lp.state_diffuse = mul3(ev_lp.diffuse, value);
+              lp.state_glossy = mul3(ev_lp.glossy, value);
+              lp.state_transmission = mul3(ev_lp.transmission, value);
+              lp.state_volume = mul3(ev_lp.volume, value);
+              throughput = add3(add3(add3(lp.state_diffuse, lp.state_glossy), lp.state_transmission),
+                                lp.state_volume);
+              lp.state_direct = throughput;
+            }
+            else {
+              const cfloat3 sum = mul3f(add3(bsdf_eval_lp_sum(&ev_lp), ev_lp.transparent), inverse_pdf);
+              throughput = mul3(throughput, sum);
+            }
+          }
+          else
+#endif
+          {
+            throughput = mul3(throughput, mul3f(bsdf_eval_v, inverse_pdf));
+          }
           if (!(label & LABEL_TRANSPARENT)) {
             state.ray_pdf = bsdf_pdf;
             state.ray_t = 0.0f;
@@ -3267,6 +3543,9 @@ CY_FN bool shade_path(const CyGlobals *kg,
   if (b->catcher && (cont || *shadow)) {
     catcher_store(b, slot, &catcher);
   }
+  if (b->lp && (cont || *shadow)) {
+    lightpass_store(b, slot, &lp);
+  }
 #endif
   if (cont) {
     store_state(b, slot, &state);
@@ -3298,6 +3577,11 @@ CY_FN bool shade_path(const CyGlobals *kg,
     CY_DBG3(&state, "catcher shaded", catcher.path_total_shaded);
     CY_DBG3(&state, "catcher background", catcher.background);
     CY_DBG3(&state, "catcher tp transp has", mk3(catcher.throughput, catcher.transparency, (float)catcher.has));
+  }
+  if (b->lp) {
+    /* light passes: the combined value summed from the components */
+    const uint fitem = cam_item != CY_NO_ITEM ? cam_item : cy_ld(&b->item[slot]);
+    L = lightpass_finish(kg, item_buffer(tile, fitem), L, &lp);
   }
   slot_finish(b, tile, slot, cam_item, L, L_transparent, b->catcher ? &catcher : nullptr);
 #else

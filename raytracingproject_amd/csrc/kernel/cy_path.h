@@ -3491,6 +3491,92 @@ CY_FN void shader_bsdf_eval_branched(const CySD *sd, cfloat3 omega_in, float lig
   }
 }
 
+/* BsdfEval with light passes (kernel_types.h:565-581, kernel_accumulate.h:
+ * 24-98): the BSDF value per closure component */
+#define CLOSURE_IS_BSDF_GLOSSY(type) \
+  (((type) >= CLOSURE_BSDF_REFLECTION_ID && (type) <= CLOSURE_BSDF_HAIR_REFLECTION_ID) || \
+   (type) == CLOSURE_BSDF_HAIR_PRINCIPLED_ID)
+#define CLOSURE_IS_BSDF_TRANSMISSION(type) \
+  ((type) >= CLOSURE_BSDF_REFRACTION_ID && (type) <= CLOSURE_BSDF_HAIR_TRANSMISSION_ID)
+#define CLOSURE_IS_BSDF_BSSRDF(type) \
+  ((type) == CLOSURE_BSDF_BSSRDF_ID || (type) == CLOSURE_BSDF_BSSRDF_PRINCIPLED_ID)
+typedef struct CyBsdfEvalLP {
+  cfloat3 diffuse, glossy, transmission, transparent, volume;
+} CyBsdfEvalLP;
+
+CY_FN void bsdf_eval_lp_zero(CyBsdfEvalLP *e)
+{
+  e->diffuse = e->glossy = e->transmission = e->transparent = e->volume = mk3(0.0f, 0.0f, 0.0f);
+}
+
+/* bsdf_eval_accum's component (transparent closures add nothing there) */
+CY_FN cfloat3 *bsdf_eval_lp_component(CyBsdfEvalLP *e, int type)
+{
+  if (CLOSURE_IS_BSDF_DIFFUSE(type) || CLOSURE_IS_BSDF_BSSRDF(type)) {
+    return &e->diffuse;
+  }
+  if (CLOSURE_IS_BSDF_GLOSSY(type)) {
+    return &e->glossy;
+  }
+  if (CLOSURE_IS_BSDF_TRANSMISSION(type)) {
+    return &e->transmission;
+  }
+  if (CLOSURE_IS_PHASE(type)) {
+    return &e->volume;
+  }
+  return nullptr;
+}
+
+CY_FN cfloat3 bsdf_eval_lp_sum(const CyBsdfEvalLP *e)
+{
+  return add3(add3(add3(e->diffuse, e->glossy), e->transmission), e->volume);
+}
+
+CY_FN bool bsdf_eval_lp_is_zero(const CyBsdfEvalLP *e)
+{
+  return is_zero3(e->diffuse) && is_zero3(e->glossy) && is_zero3(e->transmission) && is_zero3(e->transparent) &&
+         is_zero3(e->volume);
+}
+
+/* bsdf_eval_mis / bsdf_eval_mul3: every component but the transparent one */
+CY_FN void bsdf_eval_lp_mul3(CyBsdfEvalLP *e, cfloat3 v)
+{
+  e->diffuse = mul3(e->diffuse, v);
+  e->glossy = mul3(e->glossy, v);
+  e->transmission = mul3(e->transmission, v);
+  e->volume = mul3(e->volume, v);
+}
+
+CY_FN void bsdf_eval_lp_mul(CyBsdfEvalLP *e, float v)
+{
+  e->diffuse = mul3f(e->diffuse, v);
+  e->glossy = mul3f(e->glossy, v);
+  e->transmission = mul3f(e->transmission, v);
+  e->volume = mul3f(e->volume, v);
+}
+
+/* _shader_bsdf_multi_eval with light passes (kernel_shader.h:553-581) */
+CY_FN void shader_bsdf_multi_eval_lp(const CySD *sd, const cfloat3 omega_in, float *pdf, int skip_sc,
+                                     CyBsdfEvalLP *result_eval, float sum_pdf, float sum_sample_weight)
+{
+  for (int i = 0; i < sd->num_closure; i++) {
+    const CyClosure *sc = &sd->closure[i];
+    if (i != skip_sc && CLOSURE_IS_BSDF(sc->type)) {
+      float bsdf_pdf = 0.0f;
+      cfloat3 eval = bsdf_eval(sd, sc, omega_in, &bsdf_pdf);
+      if (bsdf_pdf != 0.0f) {
+        cfloat3 *c = bsdf_eval_lp_component(result_eval, sc->type);
+        if (c) {
+          *c = add3(*c, mul3f(mul3(eval, sc->weight), 1.0f));
+        }
+        sum_pdf += bsdf_pdf * sc->sample_weight;
+      }
+      sum_sample_weight += sc->sample_weight;
+    }
+  }
+  *pdf = (sum_sample_weight > 0.0f) ? sum_pdf / sum_sample_weight : 0.0f;
+}
+
 /* kernel_shader.h:638-680 */
 CY_FN int shader_bsdf_pick(const CySD *sd, float *randu)
 {
@@ -3563,6 +3649,54 @@ CY_FN int shader_bsdf_sample(const CyGlobals *kg,
   }
   return label;
 }
+
+#if CY_CLOSURE_EXT
+/* shader_bsdf_sample (kernel_shader.h:683-720) with light passes: the sampled
+ * closure's value in its component (bsdf_eval_init), the others' added by
+ * theirs */
+CY_FN int shader_bsdf_sample_lp(const CyGlobals *kg, const CySD *sd, float randu, float randv, CyBsdfEvalLP *ev,
+                                cfloat3 *omega_in, float *pdf, uint *err, CyDiff3 *domega_in)
+{
+  bsdf_eval_lp_zero(ev);
+  int sci = shader_bsdf_pick(sd, &randu);
+  if (sci < 0) {
+    *pdf = 0.0f;
+    return LABEL_NONE;
+  }
+  const CyClosure *sc = &sd->closure[sci];
+  int label;
+  cfloat3 eval = mk3(0.0f, 0.0f, 0.0f);
+  *pdf = 0.0f;
+  if (domega_in) {
+    CyDiffRule rule;
+    rule.kind = CY_DIFF_ZERO;
+    label = bsdf_sample(kg, sd, sc, randu, randv, &eval, omega_in, pdf, err, &rule);
+    domega_in->dx = diff_rule_apply(rule, sd->dI.dx);
+    domega_in->dy = diff_rule_apply(rule, sd->dI.dy);
+  }
+  else {
+    label = bsdf_sample(kg, sd, sc, randu, randv, &eval, omega_in, pdf, err);
+  }
+  if (*pdf != 0.0f) {
+    /* bsdf_eval_init (kernel_accumulate.h:26-61) */
+    const cfloat3 value = mul3(eval, sc->weight);
+    if (sc->type == CLOSURE_BSDF_TRANSPARENT_ID) {
+      ev->transparent = value;
+    }
+    else {
+      cfloat3 *c = bsdf_eval_lp_component(ev, sc->type);
+      if (c) {
+        *c = value;
+      }
+    }
+    if (sd->num_closure > 1) {
+      float sweight = sc->sample_weight;
+      shader_bsdf_multi_eval_lp(sd, *omega_in, pdf, sci, ev, *pdf * sweight, sweight);
+    }
+  }
+  return label;
+}
+#endif
 
 /* ---------------------------------------------------------------------------
  * Lights: kernel_light.h:331-617 (mesh lights with constant emission).

@@ -1089,9 +1089,16 @@ class Scene:
     # AOV passes of the view layer (BlenderSync::sync_render_passes,
     # Pass::add(PASS_AOV_COLOR / PASS_AOV_VALUE, name)): (name, "color" | "value")
     aovs: list = field(default_factory=list)
-    # data passes of the view layer (film.cpp pass_type_enum names): any of
-    # "depth", "normal", "uv", "object_id", "material_id"
+    # data and light passes of the view layer (film.cpp pass_type_enum names):
+    # any of "depth", "normal", "uv", "object_id", "material_id" and the light
+    # passes "mist", "emission", "background", "shadow", "diffuse_direct",
+    # "diffuse_indirect", "diffuse_color" (and glossy_*, transmission_*),
+    # "volume_direct", "volume_indirect"
     passes: list = field(default_factory=list)
+    # mist pass (Film mist_start / mist_depth / mist_falloff, film.cpp:374-376)
+    mist_start: float = 0.0
+    mist_depth: float = 100.0
+    mist_falloff: float = 1.0
     # Film "Transparent" (Background::transparent, background.cpp:112): camera
     # rays that leave the scene, and holdouts, make the pixel transparent
     # (alpha = 1 - L_transparent) instead of showing the world
@@ -1771,8 +1778,18 @@ def compile_scene(scene: Scene) -> DeviceScene:
     # data passes (PassType DEPTH 2 .. MATERIAL_ID 6; components film.cpp:148-170:
     # normal and UV take 4 floats, the kernel adds 3)
     data_pass_types = {"depth": (2, 1), "normal": (3, 4), "uv": (4, 4), "object_id": (5, 1), "material_id": (6, 1)}
-    for name in sorted(set(scene.passes), key=lambda n: data_pass_types[n][0]):
-        passes.append((name, *data_pass_types[name]))
+    # light passes (PassType MIST 32 .. VOLUME_INDIRECT 51, film.cpp:152-236)
+    light_pass_types = {"mist": (32, 1), "emission": (33, 4), "background": (34, 4), "shadow": (36, 4),
+                        "diffuse_direct": (38, 4), "diffuse_indirect": (39, 4), "diffuse_color": (40, 4),
+                        "glossy_direct": (41, 4), "glossy_indirect": (42, 4), "glossy_color": (43, 4),
+                        "transmission_direct": (44, 4), "transmission_indirect": (45, 4),
+                        "transmission_color": (46, 4), "volume_direct": (50, 4), "volume_indirect": (51, 4)}
+    all_types = {**data_pass_types, **light_pass_types}
+    for name in set(scene.passes):
+        if name not in all_types:
+            raise ValueError(f"pass {name!r}: one of {sorted(all_types)}")
+    for name in sorted(set(scene.passes), key=lambda n: all_types[n][0]):
+        passes.append((name, *all_types[name]))
     seen = set()
     for name, kind in scene.aovs:
         if name not in seen:
@@ -1785,7 +1802,15 @@ def compile_scene(scene: Scene) -> DeviceScene:
     kf.pass_flag = 0
     kf.pass_aov_color_num = kf.pass_aov_value_num = 0
     for kind, ptype, comps in passes:
-        kf.pass_flag |= 1 << ptype
+        # film.cpp:448-455: main passes in pass_flag, light passes in
+        # light_pass_flag (and use_light_pass)
+        if ptype <= 31:
+            kf.pass_flag |= 1 << ptype
+        else:
+            kf.use_light_pass = 1
+            kf.light_pass_flag |= 1 << (ptype % 32)
+        if kind in ("diffuse_color", "glossy_color", "transmission_color"):
+            kf.display_divide_pass_stride = stride  # film.cpp:596-599
         if kind == "combined":
             kf.pass_combined = stride
         elif kind == "aov_color":
@@ -1796,7 +1821,7 @@ def compile_scene(scene: Scene) -> DeviceScene:
             if kf.pass_aov_value_num == 0:
                 kf.pass_aov_value = stride
             kf.pass_aov_value_num += 1
-        elif kind in data_pass_types:
+        elif kind in all_types:
             setattr(kf, "pass_" + kind, stride)
         elif kind == "adaptive_aux_buffer":
             kf.pass_adaptive_aux_buffer = stride
@@ -1804,6 +1829,22 @@ def compile_scene(scene: Scene) -> DeviceScene:
             kf.pass_sample_count = stride
         stride += comps
     kf.pass_stride = -(-stride // 4) * 4
+    if kf.use_light_pass:
+        # film.cpp:641-644 mist parameters
+        kf.mist_start = float(f32(scene.mist_start))
+        kf.mist_inv_depth = float(f32(1.0) / f32(scene.mist_depth)) if scene.mist_depth > 0 else 0.0
+        kf.mist_falloff = float(f32(scene.mist_falloff))
+        # light.cpp:483-491: the shadow pass scale compensates for emitting
+        # triangles and background lights taking light samples
+        kf.pass_shadow_scale = 0.0
+        if ki.use_direct_light:
+            scale = f32(1.0)
+            if ki.pdf_triangles != 0.0:
+                scale = f32(scale * f32(0.5))
+            n_bg = int(bg_light)
+            if n_bg < num_lights:
+                scale = f32(scale * f32(f32(num_lights - n_bg) / f32(num_lights)))
+            kf.pass_shadow_scale = float(scale)
     lookup = filter_table(scene.filter_type, scene.filter_width)
     kd.tables.beckmann_offset = 0
     if any(t in BECKMANN_CLOSURES for m in mats for t in m.closure_types()):

@@ -1118,6 +1118,41 @@ def data_passes(width=40, height=40, samples=8) -> sc.Scene:
     return s
 
 
+def light_passes(width=40, height=40, samples=8, mist_falloff=2.0, film_transparent=False) -> sc.Scene:
+    """Light passes (golden parity case; kernel_passes.h:251-337, the
+    PathRadiance components of kernel_accumulate.h): mist, emission,
+    background, shadow and the diffuse / glossy / transmission direct,
+    indirect and colour passes beside the combined pass, which is then the
+    sum of the components (path_radiance_clamp_and_sum).  A diffuse floor, a
+    glossy-diffuse box, a glass ball, a half-transparent pane (mist and colour
+    passes see through it), an emitting quad and a lamp with MIS; the world
+    is seen by camera rays (the background pass)."""
+    white = sc.diffuse((0.7, 0.7, 0.7))
+    mixed = sc.mix(0.4, sc.glossy((0.8, 0.8, 0.9), 0.3), sc.diffuse((0.2, 0.4, 0.8)))
+    glass = sc.glass((0.95, 0.9, 0.85), 0.1, ior=1.45)
+    pane = sc.mix(0.6, sc.transparent((0.9, 0.9, 0.9)), sc.diffuse((0.2, 0.6, 0.3)))
+    light = sc.emission((1.0, 0.9, 0.8), 6.0)
+    materials = [white, mixed, glass, pane, light]
+    meshes = [
+        sc.Mesh(*_quad((-3, -1, -3), (3, -1, -3), (3, -1, 3), (-3, -1, 3)), shader=0),
+        sc.Mesh(*_box((0.8, -0.55, -0.1), (0.6, 0.9, 0.6), 0.4), shader=1),
+        sc.Mesh(*_ellipsoid((-0.8, -0.45, 0.2), (0.5, 0.5, 0.5), 20, 12), shader=2, smooth=True),
+        sc.Mesh(*_quad((-0.4, -0.2, -1.2), (0.6, -0.2, -1.2), (0.6, 0.7, -1.2), (-0.4, 0.7, -1.2)), shader=3),
+        sc.Mesh(*_quad((-1.6, 2.2, -1.2), (-0.8, 2.2, -1.2), (-0.8, 2.2, -0.4), (-1.6, 2.2, -0.4)), shader=4),
+    ]
+    lamps = [sc.Lamp("point", co=(1.5, 2.0, -1.5), size=0.2, color=(1.0, 0.9, 0.8), strength=60.0)]
+    cam = sc.Camera(eye=(0.0, 0.8, -3.6), target=(0.0, -0.3, 0.0), fov=math.radians(45.0), nearclip=0.01,
+                    farclip=100.0)
+    s = sc.Scene(width, height, cam, meshes, materials, world_color=(0.3, 0.35, 0.45), world_strength=1.0,
+                 samples=samples, lamps=lamps, name="light_passes")
+    s.passes = ["mist", "emission", "background", "shadow", "diffuse_direct", "diffuse_indirect", "diffuse_color",
+                "glossy_direct", "glossy_indirect", "glossy_color", "transmission_direct", "transmission_indirect",
+                "transmission_color", "volume_direct", "volume_indirect"]
+    s.mist_start, s.mist_depth, s.mist_falloff = 1.0, 6.0, mist_falloff
+    s.film_transparent = film_transparent
+    return s
+
+
 def shading_info(width=48, height=48, samples=8) -> sc.Scene:
     """Particle Info and texture mapping: boxes instanced with a particle each
     (index, age, lifetime, size, location, velocity, angular velocity driving

@@ -118,6 +118,10 @@ CASES = {
     # data passes (kernel_write_data_passes): depth, normal, UV, object and
     # material index at the camera path's first opaque-enough hit
     "data_passes": lambda: scenes.data_passes(40, 40, 8),
+    # light passes (kernel_write_light_passes): the PathRadiance components,
+    # mist (falloff 2; 0.7 through powf with a transparent film)
+    "light_passes": lambda: scenes.light_passes(40, 40, 8),
+    "light_passes_film": lambda: scenes.light_passes(40, 40, 8, mist_falloff=0.7, film_transparent=True),
     # Particle Info on instanced objects, TextureMapping with min/max and normalize
     "shading_info": lambda: scenes.shading_info(48, 48, 8),
     # Hair Info: strand flag, thickness, tangent normal, intercept / random curve attributes
@@ -198,6 +202,19 @@ def atomic_pass_channels(ds) -> np.ndarray:
         mask[f.pass_normal:f.pass_normal + 3] = True
     if f.pass_flag & (1 << 4):
         mask[f.pass_uv:f.pass_uv + 3] = True
+    # the light passes (kernel_write_light_passes, kernel_passes.h:285-337)
+    if f.use_light_pass:
+        lf = f.light_pass_flag
+        for bit, name in ((1, "emission"), (2, "background"), (4, "shadow"), (6, "diffuse_direct"),
+                          (7, "diffuse_indirect"), (8, "diffuse_color"), (9, "glossy_direct"),
+                          (10, "glossy_indirect"), (11, "glossy_color"), (12, "transmission_direct"),
+                          (13, "transmission_indirect"), (14, "transmission_color"), (18, "volume_direct"),
+                          (19, "volume_indirect")):
+            if lf & (1 << bit):
+                off = getattr(f, "pass_" + name)
+                mask[off:off + (4 if name == "shadow" else 3)] = True
+        if lf & 1:
+            mask[f.pass_mist] = True
     return mask
 
 
