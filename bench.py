@@ -60,6 +60,8 @@ def parse(argv=None):
                    help="iteration budget of the wide traversal kernels (continuation launches); 0 0 disables")
     p.add_argument("--leaf-merge", type=int, default=0, help="wide BVH: merge subtrees of <= N prims")
     p.add_argument("--slots", type=int, default=0, help="path slots in flight (0: device default)")
+    p.add_argument("--shadow-sort", type=int, default=0, choices=(0, 3, 5),
+                   help="opaque-shadow queue sort by direction (hipcy_set_shadow_sort)")
     p.add_argument("--tail", type=int, default=-1,
                    help="fused tail threshold in live paths per lane (hipcy_set_tail; -1: device default, 0: off)")
     p.add_argument("--tile", type=int, default=64,
@@ -151,6 +153,7 @@ def main():
     dev.set_bvh_width(args.bvh_width)
     dev.set_bvh_leaf_merge(args.leaf_merge)
     dev.set_ray_sort(args.ray_sort)
+    dev.set_shadow_sort(args.shadow_sort)
     dev.set_traversal_budget(*args.trav_budget)
     dev.set_traversal_refill(*args.refill)
     dev.set_slots(args.slots)
@@ -347,6 +350,7 @@ def main():
                                 else f"rows interleaved over {world} GPU(s)"),
                 "wavefront_iterations_per_frame": int(timing["iterations"]),
                 "ray_sort": args.ray_sort,
+                "shadow_sort": args.shadow_sort,
                 "traversal_budget": list(args.trav_budget),
                 "traversal_refill": list(args.refill),
                 "scene_compile_s": round(t_compile, 2),
@@ -630,6 +634,7 @@ def other_config(spec, device_index, args):
         dev = HIPDevice(device_index)
         dev.set_bvh_width(args.bvh_width)
         dev.set_ray_sort(args.ray_sort)
+        dev.set_shadow_sort(args.shadow_sort)
         if args.tail >= 0:
             dev.set_tail(args.tail)
         dev.upload_scene(ds)

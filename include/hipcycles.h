@@ -193,6 +193,12 @@ int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle);
  * closest -> shade -> shadow iteration per bounce.  Plain shading variants,
  * triangle scenes with opaque shadows; results are bit-identical; 0 disables. */
 int hipcy_set_tail(hipcy_device *dev, uint64_t paths);
+/* Shadow-queue sort: the opaque-shadow queue binned before its traversal
+ * launch by the shadow ray's direction, as hipcy_set_ray_sort mode 3 (octant)
+ * or 5 (octant x major axis), so a wave's rays head for one light and share
+ * the BVH nodes they open; 0 (the default) keeps the shading order.  Results
+ * are bit-identical. */
+int hipcy_set_shadow_sort(hipcy_device *dev, int mode);
 
 int hipcy_path_trace(hipcy_device *dev, const hipcy_work_tile *tile);
 /* Same, with the tile's rows taken every y_step image rows (y, y+y_step, ...)

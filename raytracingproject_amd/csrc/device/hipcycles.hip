@@ -8,6 +8,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
@@ -1059,7 +1060,7 @@ template<int MODE> __device__ __forceinline__ uint ray_sort_key(const hc_float4 
   return oct * 4u + major;
 }
 
-template<int MODE>
+template<int MODE, bool SHADOW = false>
 __global__ void __launch_bounds__(CY_BLOCK) k_sort_count(CyPathBuffers b, const int *queue, const uint *count,
                                                          unsigned char *keys, uint *hist, int nblocks)
 {
@@ -1071,7 +1072,7 @@ __global__ void __launch_bounds__(CY_BLOCK) k_sort_count(CyPathBuffers b, const 
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < (int)*count) {
-    const uint key = ray_sort_key<MODE>(b.ray_D[queue[i]]);
+    const uint key = ray_sort_key<MODE>(SHADOW ? b.shadow_D[queue[i]] : b.ray_D[queue[i]]);
     keys[i] = (unsigned char)key;
     atomicAdd(&h[key], 1u);
   }
@@ -1479,6 +1480,7 @@ struct hipcy_device {
   /* closest-queue sorting (hipcy_set_ray_sort): sorted queue, per-ray bin and
    * the per-lane bin x block histogram / scanned offsets */
   int ray_sort = -1; /* -1: automatic (shading-queue sort for the extended shading kernel) */
+  int shadow_sort = 0; /* hipcy_set_shadow_sort: 0, 3 or 5 */
   int *sort_queue = nullptr;
   unsigned char *sort_key = nullptr;
   uint *sort_hist = nullptr;
@@ -1539,6 +1541,9 @@ struct hipcy_device {
   bool use_branched = false;          /* branched path tracing: the slots' branch records */
   char *br_pool = nullptr;            /* those records and their counters */
   bool use_lightpass = false;         /* light passes: the slots' PathRadiance components */
+  bool use_decoupled = false;         /* decoupled volume ray marching: the slots' segment steps */
+  char *dec_pool = nullptr;           /* those steps (CY_DECOUPLED_STEPS x CY_DECOUPLED_STEP_BYTES per slot) */
+  size_t dec_slots = 0;               /* slots the steps are allocated for */
   char *lp_pool = nullptr;            /* those records (CY_LP_F4 float4 per slot) */
   char *catcher_pool = nullptr;       /* those records (CY_CATCHER_F4 float4 per slot) */
   char *sss_pool = nullptr;           /* those records and their depths */
@@ -1746,6 +1751,12 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
   dev->bufs.shadow_T = (hc_float4 *)take(rec);
   dev->bufs.item = (uint *)take(ints);
   dev->capacity = slots;
+  if (dev->dec_pool) {
+    hipFree(dev->dec_pool);
+    dev->dec_pool = nullptr;
+    dev->dec_slots = 0;
+  }
+  dev->bufs.dec_steps = nullptr;
   if (dev->vol_pool) {
     hipFree(dev->vol_pool);
     dev->vol_pool = nullptr;
@@ -1801,8 +1812,23 @@ static int ensure_capacity(hipcy_device *dev, size_t slots)
 /* The per-slot volume stack (CY_VOLUME_STACK / 2 records) and 2 volume
  * records (cy_integrator.h CyPathBuffers.vol_*), for scenes with volumes:
  * 160 B per slot that other scenes do not pay for. */
+/* Slots in flight of decoupled volume scenes: each holds its segment's steps
+ * (64 KB), 2^18 slots = 16 GB of the 288 GB. */
+#define CY_DEC_SLOTS ((size_t)1 << 18)
+
+static size_t slot_limit(const hipcy_device *dev)
+{
+  return dev->use_decoupled ? CY_DEC_SLOTS : SIZE_MAX;
+}
+
 static int ensure_volume_capacity(hipcy_device *dev)
 {
+  if (dev->use_decoupled && !dev->dec_pool) {
+    dev->dec_slots = std::min(dev->capacity, CY_DEC_SLOTS);
+    HIP_CHECK(dev, hipMalloc((void **)&dev->dec_pool,
+                             dev->dec_slots * (size_t)CY_DECOUPLED_STEPS * CY_DECOUPLED_STEP_BYTES));
+  }
+  dev->bufs.dec_steps = dev->use_decoupled ? dev->dec_pool : nullptr;
   if (!dev->use_volumes || dev->vol_pool) {
     return 0;
   }
@@ -1872,10 +1898,14 @@ static int ensure_sss_capacity(hipcy_device *dev)
     HIP_CHECK(dev, hipMemset(dev->sss_pool + recs + stacks, 0, counts));
     dev->sss_pool_vol = vol;
   }
-  /* other scenes' shading never looks at the records */
+  /* other scenes' shading never looks at the records; the depths sit where
+   * the pool's own layout put them (a pool sized for a volume scene keeps
+   * its stacks when a scene without volumes follows) */
+  const size_t pool_stacks = dev->sss_pool_vol ? (size_t)16 * (CY_SSS_RECS + 1) * (CY_VOLUME_STACK / 2) * dev->capacity
+                                               : 0;
   dev->bufs.sss_rec = dev->use_disk_bssrdf ? (hc_float4 *)dev->sss_pool : nullptr;
   dev->bufs.sss_vol = vol ? (hc_uint4 *)(dev->sss_pool + recs) : nullptr;
-  dev->bufs.sss_count = dev->use_disk_bssrdf ? (uint *)(dev->sss_pool + recs + stacks) : nullptr;
+  dev->bufs.sss_count = dev->use_disk_bssrdf ? (uint *)(dev->sss_pool + recs + pool_stacks) : nullptr;
   return 0;
 }
 
@@ -2006,6 +2036,7 @@ void hipcy_destroy(hipcy_device *dev)
   if (dev->catcher_pool) hipFree(dev->catcher_pool);
   if (dev->br_pool) hipFree(dev->br_pool);
   if (dev->lp_pool) hipFree(dev->lp_pool);
+  if (dev->dec_pool) hipFree(dev->dec_pool);
   if (dev->diff_pool) hipFree(dev->diff_pool);
   if (dev->srec_pool) hipFree(dev->srec_pool);
   if (dev->bvhw) hipFree(dev->bvhw);
@@ -2328,6 +2359,15 @@ int hipcy_set_traversal_refill(hipcy_device *dev, int rounds, int min_idle)
 int hipcy_set_tail(hipcy_device *dev, uint64_t paths)
 {
   dev->tail_paths = (size_t)paths;
+  return 0;
+}
+
+int hipcy_set_shadow_sort(hipcy_device *dev, int mode)
+{
+  if (mode != 0 && mode != 3 && mode != 5) {
+    return set_error(dev, "set_shadow_sort: mode must be 0, 3 or 5");
+  }
+  dev->shadow_sort = mode;
   return 0;
 }
 
@@ -2944,6 +2984,7 @@ int hipcy_load_kernels(hipcy_device *dev)
     dev->shade_tex = true;
   }
   dev->use_volumes = d.integrator.use_volumes != 0;
+  dev->use_decoupled = dev->use_volumes && d.integrator.volume_decoupled != 0;
   dev->use_disk_bssrdf = uses_disk_bssrdf;
   dev->use_ray_diff = uses_ray_diff;
   dev->shade_closures = d.integrator.max_closures;
@@ -3274,8 +3315,25 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
                          ln.q[qb], ln.cnt + qb);
     }
     else {
+      const int *shadow_queue = ln.q[qs];
+      if (dev->shadow_sort && dev->sort_queue && dev->sort_capacity >= dev->capacity &&
+          ln.n_active >= 4 * CY_BLOCK) {
+        /* shadow-queue sort (hipcy_set_shadow_sort): the sort buffers are free
+         * again once shading has read the closest queue (same stream) */
+        const int nblocks = (int)grid.x;
+        const int K = dev->shadow_sort == 3 ? 8 : CY_SORT_BINS;
+        uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
+        unsigned char *keys = dev->sort_key + ln.slot_base;
+        int *sorted = dev->sort_queue + ln.slot_base;
+        hipLaunchKernelGGL(dev->shadow_sort == 3 ? k_sort_count<3, true> : k_sort_count<5, true>, grid, block, 0, s,
+                           dev->bufs, ln.q[qs], ln.cnt + qs, keys, hist, nblocks);
+        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, K * nblocks);
+        hipLaunchKernelGGL(dev->shadow_sort == 3 ? k_sort_scatter<3> : k_sort_scatter<5>, grid, block, 0, s, ln.q[qs],
+                           ln.cnt + qs, keys, hist, nblocks, sorted);
+        shadow_queue = sorted;
+      }
       auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0, dev->curve_shapes);
-      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, ln.q[qs], ln.cnt + qs, ln.q[qb],
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, shadow_queue, ln.cnt + qs, ln.q[qb],
                          ln.cnt + qb, err, dev->stats_dev);
     }
   }
@@ -3338,7 +3396,7 @@ static int lane_tail(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, int W
  * tile stream), so the automatic shading-queue sort runs on both. */
 static int ensure_sort(hipcy_device *dev)
 {
-  if (effective_sort(dev) && dev->sort_capacity < dev->capacity) {
+  if ((effective_sort(dev) || dev->shadow_sort) && dev->sort_capacity < dev->capacity) {
     const size_t cap = dev->capacity;
     if (dev->sort_queue) HIP_CHECK(dev, hipFree(dev->sort_queue));
     if (dev->sort_key) HIP_CHECK(dev, hipFree(dev->sort_key));
@@ -3364,7 +3422,7 @@ static int ensure_sort(hipcy_device *dev)
 static int path_trace_pass(hipcy_device *dev, const CyGlobals &kg, CyTile tile, int W, size_t *ev,
                            std::vector<EvQuad> *quads)
 {
-  const size_t n_slots = std::min<size_t>(tile.n_items, dev->capacity);
+  const size_t n_slots = std::min<size_t>(std::min<size_t>(tile.n_items, dev->capacity), slot_limit(dev));
   /* per-kernel event timing (profiling bit 0) needs kernels that do not
    * overlap: one lane then */
   const int max_lanes = (dev->profiling & 1) ? 1 : CY_LANES;
@@ -4284,6 +4342,7 @@ int hipcy_render_feed(hipcy_device *dev, const hipcy_tile_feed *feed)
                                   : dev->stream_hold ? dev->stream_hold : 2 * dev->slots_wanted;
   /* half of a lane's share in flight, half in reserve */
   size_t lane_slots = std::min(dev->slots_wanted / lanes, std::max<size_t>(hold / (2 * lanes), 4 * CY_BLOCK));
+  lane_slots = std::min(lane_slots, slot_limit(dev) / lanes);
   lane_slots = (lane_slots + CY_BLOCK - 1) / CY_BLOCK * CY_BLOCK;
   /* per-lane record ring: the largest power of two the record budget holds */
   uint ring_cap = 1u << 12;

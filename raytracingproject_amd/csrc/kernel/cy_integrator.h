@@ -87,6 +87,11 @@ typedef struct CyPathBuffers {
   /* light passes (KernelFilm.use_light_pass): the path's PathRadiance
    * components, CY_LP_F4 float4 per slot (CyLightPass) */
   hc_float4 *lp;
+  /* decoupled volume ray marching (KernelIntegrator.volume_decoupled): the
+   * slot's segment steps, CY_DECOUPLED_STEPS CyVolumeStep of at most
+   * CY_DECOUPLED_STEP_BYTES each per slot (the device bounds the slots in
+   * flight of such scenes so the 64 KB per slot fit) */
+  void *dec_steps;
 } CyPathBuffers;
 
 /* The shadow-catcher part of PathRadiance (kernel_accumulate.h:203-233,
@@ -2119,9 +2124,8 @@ CY_FN void volume_connect_all_lights(const CyGlobals *kg, CySD *sd, cfloat3 thro
 CY_NOINLINE int volume_decoupled_path(const CyGlobals *kg, CySD *vsd, CyPathState *state,
                                       const CyVolumeStack *stack, const CyRay *volume_ray, cfloat3 *L,
                                       cfloat3 *throughput, float step_size, int sampling_method, CyShadeMem mem,
-                                      uint *err)
+                                      CyVolumeStep *steps, uint *err)
 {
-  CyVolumeStep steps[CY_DECOUPLED_STEPS];
   CyVolumeSegment segment;
   shader_setup_from_volume(vsd, volume_ray, mem);
   volume_decoupled_record(kg, state, volume_ray, vsd, stack, &segment, step_size, steps, err);
@@ -2863,7 +2867,10 @@ CY_FN bool shade_path(const CyGlobals *kg,
       const int sampling_method = volume_stack_sampling_method(kg, &vstack);
       const bool decoupled = volume_use_decoupled(kg, (state.flag & PATH_RAY_CAMERA) != 0, sampling_method);
       const int result = decoupled ? volume_decoupled_path(kg, &vsd, &state, &vstack, &volume_ray, &L, &throughput,
-                                                           step_size, sampling_method, mem, err) :
+                                                           step_size, sampling_method, mem,
+                                                           (CyVolumeStep *)b->dec_steps +
+                                                               (size_t)slot * CY_DECOUPLED_STEPS,
+                                                           err) :
                                      volume_integrate(kg, &state, &vsd, &vstack, &volume_ray, &L, &throughput,
                                                       step_size, mem, err);
       if (result == VOLUME_PATH_SCATTERED) {

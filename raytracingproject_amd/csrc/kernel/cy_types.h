@@ -293,6 +293,12 @@ enum {
 /* threads per workgroup of every wavefront kernel, and LDS-resident traversal
  * stack depth (CY_LDS_STACK * CY_BLOCK * 4 B = 32 KiB per workgroup) */
 #define CY_BLOCK 256
+/* decoupled volume segments (cy_volume_decoupled.h): at most this many steps,
+ * each CyVolumeStep in CY_DECOUPLED_STEP_BYTES of the slot's record */
+#ifndef CY_DECOUPLED_STEPS
+#  define CY_DECOUPLED_STEPS 1024
+#endif
+#define CY_DECOUPLED_STEP_BYTES 64
 #define CY_LDS_STACK 32
 
 /* LDS-qualified pointers: per-thread stacks and closure arrays carved out of a

@@ -8,7 +8,9 @@
  *                                      kernel/kernel_volume.h:297-372
  *   volume_stack_sampling_method       kernel/kernel_volume.h:145-173
  *   kernel_volume_use_decoupled        kernel/kernel_volume.h:1133-1158
- * The segment's steps live in the calling thread's private memory, at most
+ * The segment's steps live in the slot's record in device memory
+ * (CyPathBuffers.dec_steps; private memory for 1024 steps would be 60 KB of
+ * scratch per lane, more than the runtime allocates for a full chip), at most
  * CY_DECOUPLED_STEPS of them (the reference mallocs volume_max_steps); a
  * segment that needs more raises CY_ERR_FEATURE 13 instead of being cut.
  * The light connection over all lights and the shade-stage driver are in
@@ -35,6 +37,7 @@ typedef struct CyVolumeStep {
   float shade_t;               /* jittered distance where shading was done in step */
   int closure_flag;            /* shader evaluation closure flags */
 } CyVolumeStep;
+static_assert(sizeof(CyVolumeStep) <= CY_DECOUPLED_STEP_BYTES, "CyPathBuffers.dec_steps stride");
 
 typedef struct CyVolumeSegment {
   CyVolumeStep *steps;

@@ -148,6 +148,11 @@ class HIPDevice:
         new rays once `min_idle` lanes are idle.  0 disables."""
         self._check(self.lib.hipcy_set_traversal_refill(self.h, int(rounds), int(min_idle)))
 
+    def set_shadow_sort(self, mode: int) -> None:
+        """Shadow-queue sort by shadow ray direction (hipcy_set_shadow_sort):
+        0 off (default), 3 octant, 5 octant x major axis."""
+        self._check(self.lib.hipcy_set_shadow_sort(self.h, int(mode)))
+
     def set_tail(self, paths: int) -> None:
         """Fused tail (hipcy_set_tail): lanes with all items claimed and at most
         `paths` live paths finish them in one launch.  0 disables."""

@@ -130,6 +130,7 @@ DEVICE_SYMBOLS = {
     "hipcy_set_traversal_budget": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "hipcy_set_traversal_refill": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "hipcy_set_tail": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "hipcy_set_shadow_sort": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_bvh_leaf_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hipcy_set_slots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "hipcy_intersect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),

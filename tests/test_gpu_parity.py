@@ -225,6 +225,27 @@ def test_render_with_ray_sort_matches_reference(name, mode, device):
     assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), name
 
 
+@pytest.mark.parametrize("mode", [3, 5])
+@pytest.mark.parametrize("name", ["cornell_64", "bmw_small", "cornell_lamps", "cornell_instanced", "world_mis"])
+def test_render_with_shadow_sort_matches_reference(name, mode, device):
+    """Shadow-queue sort (hipcy_set_shadow_sort): the opaque-shadow queue of
+    every iteration binned by shadow ray direction before its traversal; the
+    light each path adds depends on its own shadow ray alone, so the film stays
+    bit-identical to the reference."""
+    if name not in CASES:
+        pytest.skip(f"{name} not a parity case")
+    ds = compile_case(name)
+    g = load_golden(name)
+    device.upload_scene(ds)
+    device.set_bvh_width(4)
+    device.set_shadow_sort(mode)
+    try:
+        buf = device.render()
+    finally:
+        device.set_shadow_sort(0)
+    assert np.array_equal(buf.view(np.uint32), g["buffer"].view(np.uint32)), name
+
+
 @pytest.mark.parametrize("tail", [0, 1 << 40])
 @pytest.mark.parametrize("width", [2, 4, 8])
 @pytest.mark.parametrize("name", ["cornell_64", "bmw_small", "cornell_lamps", "cornell_instanced", "camera_dof",

@@ -48,8 +48,16 @@ fi
 if [[ $MODE == tailsweep ]]; then
   # fused-tail thresholds: whole frame and the N = 8 / N = 2 row shards
   for t in ${TAILS:-0 32768 131072 524288 4194304}; do
-    for m in frame shard8 shard2; do
+    for m in ${TAIL_MODES:-frame shard8 shard2}; do
       step "tail_${m}_$t" 300 python3 tools/render_modes.py $m --frames 5 --tail $t
+    done
+  done
+fi
+if [[ $MODE == ssort ]]; then
+  # opaque-shadow queue sort (hipcy_set_shadow_sort): whole frame and the N = 8 row shard
+  for m in ${SSORTS:-0 3 5}; do
+    for f in frame shard8; do
+      step "ssort_${f}_$m" 300 python3 tools/render_modes.py $f --frames 5 --shadow-sort $m
     done
   done
 fi

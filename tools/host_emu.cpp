@@ -337,6 +337,8 @@ extern "C" int emu_render(const void *data,
   b.catcher = catcher; /* every scene: a path without a catcher leaves it unused */
   hc_float4 br_rec[CY_BR_RECS * CY_BR_REC_F4];
   uint br_count[2] = {0u, 0u};
+  static CyVolumeStep dec_steps[CY_DECOUPLED_STEPS]; /* slot 0's decoupled segment */
+  b.dec_steps = dec_steps;
   hc_float4 lp[CY_LP_F4];
   if (((const hc_KernelData *)data)->film.use_light_pass) {
     b.lp = lp;
