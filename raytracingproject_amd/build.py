@@ -72,6 +72,7 @@ def kernel_source_digest():
 
 SHADE_VARIANTS = (1, 2, 4, 8)  # closure-array sizes of the shade kernel (csrc/device/k_shade.h)
 LARGE_SHADE_VARIANTS = (16, 64)  # texture / volume builds only (extended closure set)
+EXT_SHADE_VARIANTS = (8, 64)  # integrator-extras builds (catchers, branched, light passes)
 
 
 def build_device(force=False, variant=None, defines=(), traversal_only=False, only=None):
@@ -106,14 +107,20 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False, on
     for mc in SHADE_VARIANTS + LARGE_SHADE_VARIANTS:
         # plain (closure nodes only), _tex (texture nodes, extended closures),
         # _vol (_tex with volumes)
-        for kind in ("", "_tex", "_vol") if mc in SHADE_VARIANTS else ("_tex", "_vol"):
+        # _ext (_tex with the integrator extras: shadow catchers, branched path
+        # tracing, light passes; 8 and 64 closures only)
+        kinds = ("", "_tex", "_vol") if mc in SHADE_VARIANTS else ("_tex", "_vol")
+        if mc in EXT_SHADE_VARIANTS:
+            kinds += ("_ext",)
+        for kind in kinds:
             name = f"mc{mc}{kind}"
             if traversal_only or (only is not None and name not in only):
                 shade_objs.append(os.path.join(default_dir, f"k_shade_{name}.o"))
                 continue
             obj = os.path.join(objdir, f"k_shade_{name}.o")
             jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
-                          f"-DCY_SVM_TEX={0 if kind == '' else 1}", f"-DCY_VOLUME={1 if kind == '_vol' else 0}", inc,
+                          f"-DCY_SVM_TEX={0 if kind == '' else 1}", f"-DCY_VOLUME={1 if kind == '_vol' else 0}",
+                          f"-DCY_INTEGRATOR_EXT={1 if kind == '_ext' else 0}", inc,
                           "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
     # per-object staleness: the traversal file and the shading kernels share
     # the kernel headers but not each other's source

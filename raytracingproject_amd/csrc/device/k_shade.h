@@ -42,6 +42,10 @@ void cy_launch_shade_mc16_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc64_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc16_vol(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc64_vol(CY_SHADE_LAUNCHER_ARGS);
+/* the integrator extras (shadow catchers, branched path tracing, light passes;
+ * cy_integrator.h CY_CATCHER) on the extended closure set */
+void cy_launch_shade_mc8_ext(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc64_ext(CY_SHADE_LAUNCHER_ARGS);
 #define CY_DEVICE_MAX_CLOSURE 64
 
 /* the fused tail kernel (k_shade.hip k_tail_*), plain variants only */
@@ -74,9 +78,10 @@ static inline bool cy_launch_tail(int max_closures, bool tex_nodes, bool volumes
   return true;
 }
 
-static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, CY_SHADE_LAUNCHER_ARGS)
+static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, bool ext, CY_SHADE_LAUNCHER_ARGS)
 {
-  auto fn = volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :
+  auto fn = ext ? (max_closures <= 8 ? cy_launch_shade_mc8_ext : cy_launch_shade_mc64_ext) :
+            volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :
                        max_closures <= 2 ? cy_launch_shade_mc2_vol :
                        max_closures <= 4 ? cy_launch_shade_mc4_vol :
                        max_closures <= 8 ? cy_launch_shade_mc8_vol :

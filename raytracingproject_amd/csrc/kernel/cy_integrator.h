@@ -105,8 +105,14 @@ typedef struct CyCatcher {
   int film_transparent; /* KernelBackground.transparent (not stored) */
 } CyCatcher;
 #define CY_CATCHER_F4 3
-/* the kernels that render shadow catchers (hipcy_load_kernels picks them) */
-#define CY_CATCHER (CY_CLOSURE_EXT && CY_SVM_TEX)
+/* the kernels with the integrator extras -- shadow catchers, branched path
+ * tracing, light passes (the _ext shading variants, which hipcy_load_kernels
+ * picks for such scenes; kept out of the _tex variants, whose private memory
+ * they would double) */
+#ifndef CY_INTEGRATOR_EXT
+#  define CY_INTEGRATOR_EXT 0
+#endif
+#define CY_CATCHER (CY_CLOSURE_EXT && CY_SVM_TEX && CY_INTEGRATOR_EXT)
 
 
 #define CY_SHADOW_REC_HITS 4
@@ -3086,7 +3092,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
     }
 #else
     if (sd.object_flag & SD_OBJECT_SHADOW_CATCHER) {
-      cy_set_error(err, CY_ERR_FEATURE, 5); /* the _tex kernels render shadow catchers */
+      cy_set_error(err, CY_ERR_FEATURE, 5); /* the _ext kernels render shadow catchers */
     }
 #endif
     if (((sd.flag & SD_HOLDOUT) || (sd.object_flag & SD_OBJECT_HOLDOUT_MASK)) &&
