@@ -3327,8 +3327,8 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
         uint *hist = dev->sort_hist + (size_t)CY_SORT_BINS * (ln.slot_base / CY_BLOCK + ln.index);
         unsigned char *keys = dev->sort_key + ln.slot_base;
         int *sorted = dev->sort_queue + ln.slot_base;
-        hipLaunchKernelGGL(dev->shadow_sort == 3 ? k_sort_count<3, true> : k_sort_count<5, true>, grid, block, 0, s,
-                           dev->bufs, ln.q[qs], ln.cnt + qs, keys, hist, nblocks);
+        auto kcount = dev->shadow_sort == 3 ? k_sort_count<3, true> : k_sort_count<5, true>;
+        hipLaunchKernelGGL(kcount, grid, block, 0, s, dev->bufs, ln.q[qs], ln.cnt + qs, keys, hist, nblocks);
         hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(1024), 0, s, hist, K * nblocks);
         hipLaunchKernelGGL(dev->shadow_sort == 3 ? k_sort_scatter<3> : k_sort_scatter<5>, grid, block, 0, s, ln.q[qs],
                            ln.cnt + qs, keys, hist, nblocks, sorted);
