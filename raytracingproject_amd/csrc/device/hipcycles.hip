@@ -23,6 +23,12 @@
 #include "k_trav.h"
 #include "../host/cy_bvhw_collapse.h"
 
+/* wide nodes the opaque-shadow kernel serves from LDS (the closest-hit kernel
+ * and the fused tail keep CY_LDS_TOP, cy_bvhw.h) */
+#ifndef CY_LDS_TOP_SHADOW
+#  define CY_LDS_TOP_SHADOW CY_LDS_TOP
+#endif
+
 /* PassType bits of the data passes (kernel_types.h:353-364: DEPTH .. MATERIAL_ID) */
 #define CY_HOST_DATA_PASSES ((1 << 2) | (1 << 3) | (1 << 4) | (1 << 5) | (1 << 6))
 /* the light passes this device writes (PASSMASK(type) = 1 << (type % 32):
@@ -746,7 +752,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TRAV_WAVES(HAIR)) k_intersect_sha
 {
   const int n_active = (int)*shadow_count;
   const int i = cy_queue_index(n_active);
-  __shared__ LdsStack<W, INST, true> lds_stack;
+  __shared__ LdsStack<W, INST, true, CY_LDS_TOP_SHADOW> lds_stack;
   lds_fill_top(&kg, &lds_stack);
   bool finished = false;
   int slot = 0;
@@ -1542,6 +1548,7 @@ struct hipcy_device {
   char *br_pool = nullptr;            /* those records and their counters */
   bool use_lightpass = false;         /* light passes: the slots' PathRadiance components */
   bool use_decoupled = false;         /* decoupled volume ray marching: the slots' segment steps */
+  int bvhw_top_shadow = 0;            /* wide nodes the opaque-shadow kernel keeps in LDS */
   bool shade_ext = false;             /* the _ext shading variants (catchers, branched, light passes) */
   char *dec_pool = nullptr;           /* those steps (CY_DECOUPLED_STEPS x CY_DECOUPLED_STEP_BYTES per slot) */
   size_t dec_slots = 0;               /* slots the steps are allocated for */
@@ -1626,6 +1633,7 @@ static bool build_globals(hipcy_device *dev, CyGlobals *kg)
    * traverse their top level as the reference's BVH2) */
   const size_t wide_nodes = dev->bvh_width > 2 ? dev->bvhw_bytes / (32 * (size_t)dev->bvh_width) : 0;
   kg->bvhw_top = (wide && !dev->have_instancing) ? (int)std::min<size_t>(CY_LDS_TOP, wide_nodes) : 0;
+  dev->bvhw_top_shadow = (wide && !dev->have_instancing) ? (int)std::min<size_t>(CY_LDS_TOP_SHADOW, wide_nodes) : 0;
   kg->bvhw_width = wide ? dev->bvh_width : 0;
   return true;
 }
@@ -3335,7 +3343,9 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
         shadow_queue = sorted;
       }
       auto kfn = pick_kernel<ShadowK>(counters, W, kg.have_instancing != 0, dev->curve_shapes);
-      hipLaunchKernelGGL(kfn, grid, block, 0, s, kg, dev->bufs, ln.tile, shadow_queue, ln.cnt + qs, ln.q[qb],
+      CyGlobals kgs = kg; /* its own count of LDS-resident top nodes (CY_LDS_TOP_SHADOW) */
+      kgs.bvhw_top = std::min(kg.bvhw_top > 0 ? dev->bvhw_top_shadow : 0, dev->bvhw_top_shadow);
+      hipLaunchKernelGGL(kfn, grid, block, 0, s, kgs, dev->bufs, ln.tile, shadow_queue, ln.cnt + qs, ln.q[qb],
                          ln.cnt + qb, err, dev->stats_dev);
     }
   }

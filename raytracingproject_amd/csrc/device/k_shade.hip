@@ -121,6 +121,11 @@ void CY_CAT(cy_launch_shade_, CY_SHADE_VARIANT)(CY_SHADE_LAUNCHER_ARGS)
 #ifndef CY_TAIL_WAVES
 #  define CY_TAIL_WAVES 2
 #endif
+/* the tail's closures and SVM stack in LDS as the shading kernel's (1), or in
+ * private memory (0: less LDS per block, so more blocks per CU) */
+#ifndef CY_TAIL_SHADE_LDS
+#  define CY_TAIL_SHADE_LDS CY_SHADE_LDS
+#endif
 template<int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SHADE_VARIANT)(CyGlobals kg,
                                                                                              CyPathBuffers b,
@@ -130,7 +135,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SH
                                                                                              uint *counts,
                                                                                              uint *err)
 {
-#if CY_SHADE_LDS
+#if CY_TAIL_SHADE_LDS
   __shared__ float lds[CY_BLOCK * (CY_CLOSURE_DWORDS + CY_SVM_LDS)];
   float svm_spill[CY_SVM_STACK - CY_SVM_LDS];
   CyShadeMem mem;

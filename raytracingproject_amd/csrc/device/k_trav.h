@@ -36,21 +36,23 @@
 #ifndef CY_LDS_STACK_TOP
 #  define CY_LDS_STACK_TOP 8
 #endif
-/* TOP: the kernel serves the wide BVH's top CY_LDS_TOP nodes (2 W float4
- * each) from LDS (non-instanced scenes; k_intersect_closest and
- * k_intersect_shadow, which fill them with lds_fill_top).  Other kernels
- * reserve no LDS for them and traverse with n_top = 0. */
-template<int W, bool INST, bool TOP = false> struct LdsStack {
+/* TOP: the kernel serves the wide BVH's top nodes (2 W float4 each) from
+ * LDS, at most NTOP of them (non-instanced scenes; k_intersect_closest,
+ * k_intersect_shadow and k_tail, which fill them with lds_fill_top; the host
+ * passes the count in kg->bvhw_top).  Other kernels reserve no LDS for them
+ * and traverse with n_top = 0. */
+template<int W, bool INST, bool TOP = false, int NTOP = CY_LDS_TOP> struct LdsStack {
   CyStackEntry ring[CY_LDS_STACKW * CY_BLOCK];
   int top[(INST ? CY_LDS_STACK_TOP : 1) * CY_BLOCK];
-  hc_float4 top_nodes[(!INST && TOP && CY_LDS_TOP > 0) ? CY_LDS_TOP * 2 * W : 1];
+  hc_float4 top_nodes[(!INST && TOP && NTOP > 0) ? NTOP * 2 * W : 1];
 };
-template<bool INST, bool TOP> struct LdsStack<2, INST, TOP> {
+template<bool INST, bool TOP, int NTOP> struct LdsStack<2, INST, TOP, NTOP> {
   int top[CY_LDS_STACK * CY_BLOCK];
 };
 
 /* This thread's ring column of the wide kernels' LDS stack (nullptr for BVH2). */
-template<int W, bool INST, bool TOP> __device__ __forceinline__ CY_LDS CyStackEntry *lds_ring_of(LdsStack<W, INST, TOP> *lds)
+template<int W, bool INST, bool TOP, int NTOP>
+__device__ __forceinline__ CY_LDS CyStackEntry *lds_ring_of(LdsStack<W, INST, TOP, NTOP> *lds)
 {
   if constexpr (W > 2) {
     return (CY_LDS CyStackEntry *)(lds->ring + threadIdx.x);
@@ -63,10 +65,10 @@ template<int W, bool INST, bool TOP> __device__ __forceinline__ CY_LDS CyStackEn
 /* HAIR (scenes with curves): unaligned nodes and curve leaves of the shapes
  * HAIR selects (1 ribbons, 2 thick curves, 3 both).  Ribbon-only scenes also
  * traverse the wide BVH (W = 4 / 8, cy_bvhw.h); thick curves keep the BVH2. */
-template<int W, bool any_hit, bool INST = true, int HAIR = 0, bool TOP = false>
+template<int W, bool any_hit, bool INST = true, int HAIR = 0, bool TOP = false, int NTOP = CY_LDS_TOP>
 __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay *ray, uint visibility,
                                                CyIsect *isect, uint *err, uint *n_nodes, uint *n_leaves,
-                                               uint *n_tris, LdsStack<W, INST, TOP> *lds, bool *tie = nullptr)
+                                               uint *n_tris, LdsStack<W, INST, TOP, NTOP> *lds, bool *tie = nullptr)
 {
   const int t = threadIdx.x;
   if constexpr (W == 2) {
@@ -83,22 +85,23 @@ __device__ __forceinline__ bool scene_traverse(const CyGlobals *kg, const CyRay 
   else {
     return bvhw_intersect<W, any_hit, HAIR>(kg, ray, visibility, isect, err, n_nodes, n_leaves, n_tris,
                                             (CY_LDS CyStackEntry *)(lds->ring + t), tie,
-                                            (CY_LDS const hc_float4 *)lds->top_nodes, TOP ? kg->bvhw_top : 0);
+                                            (CY_LDS const hc_float4 *)lds->top_nodes,
+                                            TOP ? (kg->bvhw_top < NTOP ? kg->bvhw_top : NTOP) : 0);
   }
 }
 
 /* Copy the wide BVH's top nodes into the workgroup's LDS (CY_LDS_TOP; every
  * thread of the block calls this before its traversal). */
-template<int W, bool INST, bool TOP>
-__device__ __forceinline__ void lds_fill_top(const CyGlobals *kg, LdsStack<W, INST, TOP> *lds)
+template<int W, bool INST, bool TOP, int NTOP>
+__device__ __forceinline__ void lds_fill_top(const CyGlobals *kg, LdsStack<W, INST, TOP, NTOP> *lds)
 {
-  if constexpr (W > 2 && !INST && TOP && CY_LDS_TOP > 0) {
-    const int n = kg->bvhw_top * 2 * W;
+  if constexpr (W > 2 && !INST && TOP && NTOP > 0) {
+    const int n = (kg->bvhw_top < NTOP ? kg->bvhw_top : NTOP) * 2 * W;
     const hc_float4 *src = (const hc_float4 *)kg->bvhw_nodes;
     for (int i = threadIdx.x; i < n; i += CY_BLOCK) {
 #  if CY_LDS_TOP_SOA
       /* node i / 2W, float4 i % 2W */
-      lds->top_nodes[(i % (2 * W)) * CY_LDS_TOP + i / (2 * W)] = src[i];
+      lds->top_nodes[(i % (2 * W)) * NTOP + i / (2 * W)] = src[i];
 #  else
       lds->top_nodes[i] = src[i];
 #  endif

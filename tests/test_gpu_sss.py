@@ -1,6 +1,7 @@
 """Disk BSSRDFs on the device beyond the golden renders (test_gpu_parity.py
-covers sss_disk*, sss_blur at BVH widths 2/4/8): the load-time refusal of
-the one combination the device does not take."""
+covers sss_disk*, sss_blur at BVH widths 2/4/8): the load and render of a
+disk BSSRDF in a volume scene."""
+import numpy as np
 import pytest
 
 from raytracingproject_amd import scene as sc
@@ -9,11 +10,12 @@ from raytracingproject_amd import scenes
 pytestmark = pytest.mark.gpu
 
 
-def test_disk_bssrdf_in_a_volume_scene_is_refused_at_load():
-    """Disk BSSRDFs with volumes would need the exit points' volume stack
-    updates (kernel_path_subsurface.h:84-95): load_kernels names the feature
-    instead of rendering something else."""
-    from raytracingproject_amd.device import DeviceError, HIPDevice
+def test_disk_bssrdf_in_a_volume_scene_loads_and_renders():
+    """Disk BSSRDFs with volumes (round 6): the exit points' volume stack
+    updates (kernel_path_subsurface.h:84-97, kernel_volume.h:1355) are carried,
+    so load_kernels accepts the scene and it renders; bit-exact parity is the
+    sss_disk_fog / sss_disk_fog_box goldens' (test_gpu_parity.py)."""
+    from raytracingproject_amd.device import HIPDevice
 
     s = scenes.sss_disk_cornell(16, 16, 1)
     s.world_volume = sc.volume_scatter((0.8, 0.8, 0.8), density=0.001)
@@ -21,7 +23,8 @@ def test_disk_bssrdf_in_a_volume_scene_is_refused_at_load():
     assert ds.data.integrator.use_volumes
     dev = HIPDevice(0)
     try:
-        with pytest.raises(DeviceError, match="disk BSSRDFs"):
-            dev.upload_scene(ds)
+        dev.upload_scene(ds)
+        buf = dev.render()
+        assert np.isfinite(buf).all() and buf[..., 0].sum() > 0
     finally:
         dev.close()

@@ -123,9 +123,11 @@ def test_constant_emission_detection():
 
 @pytest.mark.gpu
 def test_unimplemented_node_rejected_at_load_kernels():
-    """A node the device does not run (here NODE_TEX_VOXEL, svm_types.h, patched over a
-    Math node of a compiled program) is rejected by the program scan before
-    any render, naming the node."""
+    """A node the device does not run is rejected by the program scan before
+    any render, naming the node.  Every node of svm_types.h runs since round 6
+    (the last ones were NODE_TEX_VOXEL and the AOV / bump-eval nodes), so the
+    program gets a node number past the reference's enum, patched over a Math
+    node (a program from a newer or corrupt compiler)."""
     from raytracingproject_amd.device import DeviceError, HIPDevice
 
     s = scenes.shading_math(8, 8, 1)
@@ -133,10 +135,10 @@ def test_unimplemented_node_rejected_at_load_kernels():
     ds = sc.compile_scene(s)
     prog = ds.arrays["__svm_nodes"]
     k = int(np.flatnonzero(prog[:, 0] == 42)[0])  # NODE_MATH
-    prog[k, 0] = 87  # NODE_TEX_VOXEL
+    prog[k, 0] = 150  # past the last node number of svm_types.h
     dev = HIPDevice(0)
     try:
-        with pytest.raises(DeviceError, match="SVM node 87 is not implemented"):
+        with pytest.raises(DeviceError, match="SVM node 150 is not implemented"):
             dev.upload_scene(ds)
     finally:
         dev.close()

@@ -37,6 +37,7 @@ def main():
     p.add_argument("--slots", type=int, default=0)
     p.add_argument("--tail", type=int, default=-1, help="hipcy_set_tail (-1: device default)")
     p.add_argument("--shadow-sort", type=int, default=0, help="hipcy_set_shadow_sort (0, 3, 5)")
+    p.add_argument("--ray-sort", type=int, default=-1, help="hipcy_set_ray_sort (-1 automatic, 0, 3, 5, 8)")
     a = p.parse_args()
     ds = sc.compile_scene(scenes.CONFIGS[a.config]())
     dev = HIPDevice(0)
@@ -44,6 +45,7 @@ def main():
     if a.tail >= 0:
         dev.set_tail(a.tail)
     dev.set_shadow_sort(a.shadow_sort)
+    dev.set_ray_sort(a.ray_sort)
     dev.upload_scene(ds)
     dev.load_kernels()
     W, H, S, PS = ds.width, ds.height, ds.samples, ds.pass_stride
@@ -77,7 +79,7 @@ def main():
 
     times = [frame() for _ in range(a.frames)]
     st = dev.stats()
-    print(json.dumps({"mode": a.mode, "tail": a.tail, "shadow_sort": a.shadow_sort, "frame_ms": [round(1e3 * t, 3) for t in times],
+    print(json.dumps({"mode": a.mode, "tail": a.tail, "shadow_sort": a.shadow_sort, "ray_sort": a.ray_sort, "frame_ms": [round(1e3 * t, 3) for t in times],
                       "samples": shard.rows * W * S, "iterations": int(st["iterations"])}), flush=True)
     dev.close()
 
