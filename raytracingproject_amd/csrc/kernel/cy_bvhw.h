@@ -214,6 +214,12 @@ template<int W> CY_FN void bvhw_sort(float (&t)[W], int (&c)[W])
 #ifndef CY_ANYHIT_NOSORT
 #  define CY_ANYHIT_NOSORT 0
 #endif
+/* opaque any-hit with the hit leaf children first (measurement switch): a
+ * shadow ray ends at any occluder, so the order of the children only decides
+ * how soon one is found, never the result */
+#ifndef CY_ANYHIT_LEAF_FIRST
+#  define CY_ANYHIT_LEAF_FIRST 0
+#endif
 
 /* Near-tie window of the exact closest hit: hits within 2^-20 (about 8 ulps)
  * of the best distance are kept as candidates and resolved in the reference's
@@ -476,6 +482,12 @@ CY_FN bool bvhw_traverse(const CyGlobals *kg,
         }
         code = next;
         continue;
+      }
+      if (any_hit && CY_ANYHIT_LEAF_FIRST) {
+#pragma unroll
+        for (int s = 0; s < W; s++) {
+          tn[s] = (tn[s] != CY_INF && cc[s] < 0) ? -1.0f : tn[s];
+        }
       }
       bvhw_sort<W>(tn, cc);
       if (tn[0] == CY_INF) {
