@@ -108,10 +108,12 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False, on
         # plain (closure nodes only), _tex (texture nodes, extended closures),
         # _vol (_tex with volumes)
         # _ext (_tex with the integrator extras: shadow catchers, branched path
-        # tracing, light passes; 8 and 64 closures only)
+        # tracing, light passes) and _vext (_vol with the volume extras:
+        # decoupled ray marching, camera inside a volume, SSS in volume
+        # scenes); 8 and 64 closures only
         kinds = ("", "_tex", "_vol") if mc in SHADE_VARIANTS else ("_tex", "_vol")
         if mc in EXT_SHADE_VARIANTS:
-            kinds += ("_ext",)
+            kinds += ("_ext", "_vext")
         for kind in kinds:
             name = f"mc{mc}{kind}"
             if traversal_only or (only is not None and name not in only):
@@ -119,7 +121,9 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False, on
                 continue
             obj = os.path.join(objdir, f"k_shade_{name}.o")
             jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
-                          f"-DCY_SVM_TEX={0 if kind == '' else 1}", f"-DCY_VOLUME={1 if kind == '_vol' else 0}",
+                          f"-DCY_SVM_TEX={0 if kind == '' else 1}",
+                          f"-DCY_VOLUME={1 if kind in ('_vol', '_vext') else 0}",
+                          f"-DCY_VOLUME_EXT={1 if kind == '_vext' else 0}",
                           f"-DCY_INTEGRATOR_EXT={1 if kind == '_ext' else 0}", inc,
                           "-c", "-o", obj, os.path.join(dev_dir, "k_shade.hip")], obj))
     # per-object staleness: the traversal file and the shading kernels share

@@ -1550,6 +1550,7 @@ struct hipcy_device {
   bool use_decoupled = false;         /* decoupled volume ray marching: the slots' segment steps */
   int bvhw_top_shadow = 0;            /* wide nodes the opaque-shadow kernel keeps in LDS */
   bool shade_ext = false;             /* the _ext shading variants (catchers, branched, light passes) */
+  bool shade_vext = false;            /* the _vext variants (decoupled, camera in a volume, SSS with volumes) */
   char *dec_pool = nullptr;           /* those steps (CY_DECOUPLED_STEPS x CY_DECOUPLED_STEP_BYTES per slot) */
   size_t dec_slots = 0;               /* slots the steps are allocated for */
   char *lp_pool = nullptr;            /* those records (CY_LP_F4 float4 per slot) */
@@ -2995,6 +2996,7 @@ int hipcy_load_kernels(hipcy_device *dev)
   dev->shade_ext = dev->use_catcher || dev->use_branched || dev->use_lightpass;
   dev->use_volumes = d.integrator.use_volumes != 0;
   dev->use_decoupled = dev->use_volumes && d.integrator.volume_decoupled != 0;
+  dev->shade_vext = dev->use_volumes && (dev->use_decoupled || d.cam.is_inside_volume || uses_bssrdf);
   dev->use_disk_bssrdf = uses_disk_bssrdf;
   dev->use_ray_diff = uses_ray_diff;
   dev->shade_closures = d.integrator.max_closures;
@@ -3284,7 +3286,8 @@ static int lane_iterate(hipcy_device *dev, const CyGlobals &kg, PassLane &ln, in
     hipLaunchKernelGGL(k_sort_scatter<5>, grid, block, 0, s, queue_in, ln.cnt + qa, keys, hist, nblocks, sorted);
     shade_queue = sorted;
   }
-  cy_launch_shade(dev->shade_closures, dev->shade_tex, dev->use_volumes, dev->shade_ext, grid, block, s, kg,
+  cy_launch_shade(dev->shade_closures, dev->shade_tex, dev->use_volumes, dev->shade_ext, dev->shade_vext, grid,
+                  block, s, kg,
                   dev->bufs, ln.tile, cam_n,
                   ln.slot_base, shade_queue, ln.cnt + qa, ln.q[qb], ln.cnt + qb, ln.q[qs], ln.cnt + qs, err);
   if (prof) {

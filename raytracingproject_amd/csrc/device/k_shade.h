@@ -46,6 +46,10 @@ void cy_launch_shade_mc64_vol(CY_SHADE_LAUNCHER_ARGS);
  * cy_integrator.h CY_CATCHER) on the extended closure set */
 void cy_launch_shade_mc8_ext(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc64_ext(CY_SHADE_LAUNCHER_ARGS);
+/* the volume extras (decoupled ray marching, camera inside a volume, SSS in
+ * volume scenes; cy_integrator.h CY_VOLUME_EXT) */
+void cy_launch_shade_mc8_vext(CY_SHADE_LAUNCHER_ARGS);
+void cy_launch_shade_mc64_vext(CY_SHADE_LAUNCHER_ARGS);
 #define CY_DEVICE_MAX_CLOSURE 64
 
 /* the fused tail kernel (k_shade.hip k_tail_*), plain variants only */
@@ -78,9 +82,11 @@ static inline bool cy_launch_tail(int max_closures, bool tex_nodes, bool volumes
   return true;
 }
 
-static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, bool ext, CY_SHADE_LAUNCHER_ARGS)
+static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, bool ext, bool vext,
+                                   CY_SHADE_LAUNCHER_ARGS)
 {
   auto fn = ext ? (max_closures <= 8 ? cy_launch_shade_mc8_ext : cy_launch_shade_mc64_ext) :
+            vext ? (max_closures <= 8 ? cy_launch_shade_mc8_vext : cy_launch_shade_mc64_vext) :
             volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :
                        max_closures <= 2 ? cy_launch_shade_mc2_vol :
                        max_closures <= 4 ? cy_launch_shade_mc4_vol :

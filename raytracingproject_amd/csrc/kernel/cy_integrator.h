@@ -113,6 +113,13 @@ typedef struct CyCatcher {
 #  define CY_INTEGRATOR_EXT 0
 #endif
 #define CY_CATCHER (CY_CLOSURE_EXT && CY_SVM_TEX && CY_INTEGRATOR_EXT)
+/* the volume extras -- decoupled ray marching, a camera inside a volume
+ * object, subsurface scattering in volume scenes (their stacks per exit ray):
+ * the _vext shading variants (hipcy_load_kernels picks them); the _vol
+ * variants keep the distance-sampled volume path alone */
+#ifndef CY_VOLUME_EXT
+#  define CY_VOLUME_EXT 1
+#endif
 
 
 #define CY_SHADOW_REC_HITS 4
@@ -2754,7 +2761,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
   int shadow_rng_offset = 0;
   if (VOL) {
     if (cam_item != CY_NO_ITEM) {
-      if (KD->cam.is_inside_volume) {
+      if (CY_VOLUME_EXT && KD->cam.is_inside_volume) {
         CySD stack_sd;
         volume_stack_init_camera(kg, &stack_sd, &ray, (uint)state.flag, &vstack, err);
       }
@@ -2768,7 +2775,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
       const hc_uint4 r1 = cy_ld(&b->vol_rec[2 * (size_t)slot + 1]);
       state.volume_bounce = (int)r0.w;
       state.volume_bounds_bounce = (int)r1.x;
-      if (r0.z & CY_VOP_INIT_CAMERA) {
+      if (CY_VOLUME_EXT && (r0.z & CY_VOP_INIT_CAMERA)) {
         /* path_state_init's kernel_volume_stack_init (kernel_path_state.h:62-68) */
         CySD stack_sd;
         volume_stack_init_camera(kg, &stack_sd, &ray, (uint)state.flag, &vstack, err);
@@ -2871,7 +2878,8 @@ CY_FN bool shade_path(const CyGlobals *kg,
        * light from all lights inline, cy_volume_decoupled.h), or distance
        * sampling with one deferred light sample */
       const int sampling_method = volume_stack_sampling_method(kg, &vstack);
-      const bool decoupled = volume_use_decoupled(kg, (state.flag & PATH_RAY_CAMERA) != 0, sampling_method);
+      const bool decoupled = CY_VOLUME_EXT && volume_use_decoupled(kg, (state.flag & PATH_RAY_CAMERA) != 0,
+                                                                   sampling_method);
       const int result = decoupled ? volume_decoupled_path(kg, &vsd, &state, &vstack, &volume_ray, &L, &throughput,
                                                            step_size, sampling_method, mem,
                                                            (CyVolumeStep *)b->dec_steps +
@@ -3294,7 +3302,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
           const float bssrdf_rough = bssrdf_roughness(sc);
           if (CLOSURE_IS_DISK_BSSRDF(bssrdf_type)) {
             /* the exit points' light and bounces replace the path's own */
-            if (VOL) {
+            if constexpr (VOL && CY_VOLUME_EXT) {
               CySD stack_sd;
               sss_disk_rays = subsurface_disk_paths<true>(kg, b, slot, cam_item, &sd, sc, bssrdf_u, bssrdf_v,
                                                           &state, &ray, &throughput, &L, mem, err, &vstack,
@@ -3314,7 +3322,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
             subsurface_color_bump_blur(kg, &sd, &state, &ss_weight, &ss_N, err);
             subsurface_scatter_setup_diffuse_bsdf(kg, &sd, bssrdf_type, bssrdf_rough, ss_weight, ss_N);
             sss_bounce = true;
-            if (VOL && (sd.object_flag & SD_OBJECT_INTERSECTS_VOLUME)) {
+            if (VOL && CY_VOLUME_EXT && (sd.object_flag & SD_OBJECT_INTERSECTS_VOLUME)) {
               /* the exit ray's stack is updated after its bounce, so the exit
                * point's light sample is traced here with the path's stack */
               sss_update = true;
@@ -3350,7 +3358,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
       if (KD->integrator.use_direct_light && (sd.flag & SD_BSDF_HAS_EVAL)) {
 #endif
 #if CY_CLOSURE_EXT
-        if (VOL && sss_update) {
+        if (VOL && CY_VOLUME_EXT && sss_update) {
           bool reused = false;
           connect_light_exit_vol(kg, b, slot, &sd, &state, throughput, &L, &reused, mem, err, &vstack);
           if (reused) {
@@ -3473,7 +3481,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
             vop_shader = (uint)sd.shader;
             vop_flags |= CY_VOP_PATH | ((sd.flag & SD_BACKFACING) ? CY_VOP_BACKFACING : 0u);
           }
-          if (VOL && sss_update) {
+          if (VOL && CY_VOLUME_EXT && sss_update) {
             /* kernel_path_subsurface.h:92-99: the surface's own update, then
              * the volume surfaces from the path's previous point to the exit
              * point (no shadow is pending: it was traced above) */
@@ -3503,7 +3511,7 @@ CY_FN bool shade_path(const CyGlobals *kg,
      * (kernel_path_subsurface_setup_indirect), if any */
     const int pending = (sss_disk_rays == 0 || cam_item != CY_NO_ITEM) ? 0 : (int)cy_ld(&b->sss_count[slot]);
     if (pending > 0) {
-      if (VOL) {
+      if (VOL && CY_VOLUME_EXT) {
         /* the record's own stack; a shadow ray still pending keeps the ended
          * path's (and its own crossing of the surface) */
         if (*shadow) {
