@@ -126,6 +126,11 @@ void CY_CAT(cy_launch_shade_, CY_SHADE_VARIANT)(CY_SHADE_LAUNCHER_ARGS)
 #ifndef CY_TAIL_SHADE_LDS
 #  define CY_TAIL_SHADE_LDS CY_SHADE_LDS
 #endif
+/* 1: lane pairs (the path's next ray and its light sample's shadow ray traced
+ * side by side, below) */
+#ifndef CY_TAIL_PAIRS
+#  define CY_TAIL_PAIRS 0
+#endif
 template<int W, bool INST>
 __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SHADE_VARIANT)(CyGlobals kg,
                                                                                              CyPathBuffers b,
@@ -156,6 +161,97 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SH
 #endif
   __shared__ LdsStack<W, INST, true> lds_stack;
   lds_fill_top(&kg, &lds_stack); /* a barrier: before any thread leaves */
+#if CY_TAIL_PAIRS
+  /* lane pairs: the even lane runs the path (closest hit, shading, the light
+   * sample's bookkeeping), its odd partner traces the light sample's shadow
+   * ray while the even lane traces the path's next ray.  The two rays are
+   * independent and shadow_finish still adds the light before the next
+   * shading (the sequential order of every write), so a bounce costs
+   * max(closest, shadow) + shading on the path's chain instead of the sum.
+   * The shadow ray runs the closest-hit traversal with the opaque-shadow
+   * visibility (blocked iff it has a hit, the any-hit answer), so both lanes
+   * run one code path.  The pair takes paths as one (counts[2]). */
+  const bool odd = (threadIdx.x & 1) != 0;
+  const uint n = *count_in;
+  uint mine = 0u;
+  if (!odd) {
+    mine = atomicAdd(&counts[2], 1u);
+  }
+  /* shuffles run with both lanes of the pair active (a disabled source lane
+   * gives no defined value) */
+  const uint theirs = (uint)__shfl_xor((int)mine, 1);
+  uint next = odd ? theirs : mine;
+  if (next >= n) {
+    return;
+  }
+  int slot = queue_in[next];
+  bool alive = true, pending = false;
+  uint n_closest = 0, n_shadow = 0, n_leaves = 0, n_tris = 0;
+  for (;;) {
+    CyRay ray;
+    uint visibility = PATH_RAY_SHADOW_OPAQUE;
+    bool has_ray = false;
+    if (!odd) {
+      if (alive) {
+        has_ray = closest_load(&kg, &b, &tile, slot, CY_NO_ITEM, &ray, &visibility);
+      }
+    }
+    else if (pending) {
+      shadow_load(&b, slot, &ray);
+      has_ray = true;
+    }
+    CyIsect isect;
+    bool hit = false, tie = false;
+    if (has_ray && scene_intersect_valid(&ray)) {
+      hit = scene_traverse<W, false, INST, 0>(&kg, &ray, visibility, &isect, err, nullptr, &n_leaves, &n_tris,
+                                              &lds_stack, &tie);
+    }
+    const bool partner_hit = __shfl_xor((int)hit, 1) != 0;
+    int state = 0; /* bit 0 alive, bit 1 pending, bit 2 done */
+    if (!odd) {
+      if (pending) {
+        shadow_finish(&b, &tile, slot, partner_hit);
+        n_shadow++;
+      }
+      bool shadow = false, cont = false;
+      if (alive) {
+        if constexpr (W > 2) {
+          if (tie) {
+            isect.prim |= CY_PRIM_TIE; /* re-traced by shade_path in the reference's order */
+          }
+        }
+        closest_store<INST>(&b, slot, has_ray, hit, &isect);
+        n_closest++;
+        bool finished = false;
+        cont = shade_path<false>(&kg, &b, &tile, slot, CY_NO_ITEM, mem, &shadow, &finished, err);
+      }
+      if (!cont && !shadow) {
+        next = atomicAdd(&counts[2], 1u);
+        if (next >= n) {
+          state = 4;
+        }
+        else {
+          slot = queue_in[next];
+          state = 1;
+        }
+      }
+      else {
+        state = (cont ? 1 : 0) | (shadow ? 2 : 0);
+      }
+    }
+    const int partner_state = __shfl_xor(state, 1);
+    const int slot_b = __shfl_xor(slot, 1);
+    if (odd) {
+      state = partner_state;
+      slot = slot_b;
+    }
+    if (state & 4) {
+      break;
+    }
+    alive = (state & 1) != 0;
+    pending = (state & 2) != 0;
+  }
+#else
   /* persistent: the grid holds what the chip keeps resident for the lane
    * (cy_launch_tail_*), and a thread whose path ends takes the next waiting
    * one (counts[2]), so no block waits on its slowest path while paths are
@@ -210,6 +306,7 @@ __global__ void __launch_bounds__(CY_BLOCK, CY_TAIL_WAVES) CY_CAT(k_tail_, CY_SH
       slot = queue_in[next];
     }
   }
+#endif
   atomicAdd(&counts[0], n_closest);
   atomicAdd(&counts[1], n_shadow);
 }
@@ -235,7 +332,8 @@ void CY_CAT(cy_launch_tail_, CY_SHADE_VARIANT)(CY_TAIL_LAUNCHER_ARGS)
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) {
     cus = 1;
   }
-  const dim3 g(std::max(1u, std::min(grid.x, (unsigned)(occ * cus / CY_LANES))));
+  const unsigned want = grid.x * (CY_TAIL_PAIRS ? 2u : 1u); /* a thread (pair) per path */
+  const dim3 g(std::max(1u, std::min(want, (unsigned)(occ * cus / CY_LANES))));
   hipLaunchKernelGGL(fn, g, block, 0, stream, kg, b, tile, queue_in, count_in, counts, err);
 }
 #endif
