@@ -111,7 +111,10 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False, on
         # tracing, light passes) and _vext (_vol with the volume extras:
         # decoupled ray marching, camera inside a volume, SSS in volume
         # scenes); 8 and 64 closures only
-        kinds = ("", "_tex", "_vol") if mc in SHADE_VARIANTS else ("_tex", "_vol")
+        # (the _vol variants -- volumes without the extras -- are not built: on
+        # the GPU they rendered volume scenes wrong; every
+        # volume scene takes _vext)
+        kinds = ("", "_tex") if mc in SHADE_VARIANTS else ("_tex",)
         if mc in EXT_SHADE_VARIANTS:
             kinds += ("_ext", "_vext")
         for kind in kinds:
@@ -120,7 +123,10 @@ def build_device(force=False, variant=None, defines=(), traversal_only=False, on
                 shade_objs.append(os.path.join(default_dir, f"k_shade_{name}.o"))
                 continue
             obj = os.path.join(objdir, f"k_shade_{name}.o")
-            jobs.append(([HIPCC, *cflags, *dflags, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
+            # plain variants: the fused tail with lane pairs (CY_TAIL_PAIRS,
+            # k_shade.hip; N = 8 shard 12.95 -> 12.55 ms, profiles/r06/tail/)
+            pairs = ["-DCY_TAIL_PAIRS=1"] if kind == "" else []
+            jobs.append(([HIPCC, *cflags, *dflags, *pairs, f"-DCY_MAX_CLOSURE={mc}", f"-DCY_SHADE_VARIANT={name}",
                           f"-DCY_SVM_TEX={0 if kind == '' else 1}",
                           f"-DCY_VOLUME={1 if kind in ('_vol', '_vext') else 0}",
                           f"-DCY_VOLUME_EXT={1 if kind == '_vext' else 0}",

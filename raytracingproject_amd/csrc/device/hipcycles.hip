@@ -2996,7 +2996,11 @@ int hipcy_load_kernels(hipcy_device *dev)
   dev->shade_ext = dev->use_catcher || dev->use_branched || dev->use_lightpass;
   dev->use_volumes = d.integrator.use_volumes != 0;
   dev->use_decoupled = dev->use_volumes && d.integrator.volume_decoupled != 0;
-  dev->shade_vext = dev->use_volumes && (dev->use_decoupled || d.cam.is_inside_volume || uses_bssrdf);
+  /* every volume scene takes the _vext variants: the _vol build (the volume
+   * extras compiled out, CY_VOLUME_EXT = 0) rendered volume_cornell,
+   * volume_hetero, shading_voxel and the JNK crop wrong on the GPU while its
+   * host emulation matched, so it is not built */
+  dev->shade_vext = dev->use_volumes;
   dev->use_disk_bssrdf = uses_disk_bssrdf;
   dev->use_ray_diff = uses_ray_diff;
   dev->shade_closures = d.integrator.max_closures;

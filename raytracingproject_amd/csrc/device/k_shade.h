@@ -31,17 +31,11 @@ void cy_launch_shade_mc1_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc2_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc4_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc8_tex(CY_SHADE_LAUNCHER_ARGS);
-void cy_launch_shade_mc1_vol(CY_SHADE_LAUNCHER_ARGS);
-void cy_launch_shade_mc2_vol(CY_SHADE_LAUNCHER_ARGS);
-void cy_launch_shade_mc4_vol(CY_SHADE_LAUNCHER_ARGS);
-void cy_launch_shade_mc8_vol(CY_SHADE_LAUNCHER_ARGS);
 /* large closure arrays (mixed Principled BSDFs and the like; the reference
  * CPU kernel's MAX_CLOSURE is 64): extended closure set only, in private
  * memory */
 void cy_launch_shade_mc16_tex(CY_SHADE_LAUNCHER_ARGS);
 void cy_launch_shade_mc64_tex(CY_SHADE_LAUNCHER_ARGS);
-void cy_launch_shade_mc16_vol(CY_SHADE_LAUNCHER_ARGS);
-void cy_launch_shade_mc64_vol(CY_SHADE_LAUNCHER_ARGS);
 /* the integrator extras (shadow catchers, branched path tracing, light passes;
  * cy_integrator.h CY_CATCHER) on the extended closure set */
 void cy_launch_shade_mc8_ext(CY_SHADE_LAUNCHER_ARGS);
@@ -85,14 +79,10 @@ static inline bool cy_launch_tail(int max_closures, bool tex_nodes, bool volumes
 static inline void cy_launch_shade(int max_closures, bool tex_nodes, bool volumes, bool ext, bool vext,
                                    CY_SHADE_LAUNCHER_ARGS)
 {
+  /* volume scenes always run _vext (the host sets vext with volumes) */
+  (void)volumes;
   auto fn = ext ? (max_closures <= 8 ? cy_launch_shade_mc8_ext : cy_launch_shade_mc64_ext) :
             vext ? (max_closures <= 8 ? cy_launch_shade_mc8_vext : cy_launch_shade_mc64_vext) :
-            volumes ? (max_closures <= 1 ? cy_launch_shade_mc1_vol :
-                       max_closures <= 2 ? cy_launch_shade_mc2_vol :
-                       max_closures <= 4 ? cy_launch_shade_mc4_vol :
-                       max_closures <= 8 ? cy_launch_shade_mc8_vol :
-                       max_closures <= 16 ? cy_launch_shade_mc16_vol :
-                                            cy_launch_shade_mc64_vol) :
             max_closures > 8 ? (max_closures <= 16 ? cy_launch_shade_mc16_tex : cy_launch_shade_mc64_tex) :
             tex_nodes ? (max_closures <= 1 ? cy_launch_shade_mc1_tex :
                          max_closures <= 2 ? cy_launch_shade_mc2_tex :
